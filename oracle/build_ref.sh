@@ -1,0 +1,78 @@
+#!/usr/bin/env bash
+# TEST INFRASTRUCTURE: compile the reference Fortran 77 programs from their
+# own sources under /root/reference into oracle/_ref/ (git-ignored).
+#
+# Recipe: ROCm flang -O2.  ROCm flang's runtime has no
+# rand_/srand_, so a 2-line C forwarder maps them onto the GNU Fortran
+# runtime's own _gfortran_rand/_gfortran_srand (libgfortran.so.4, present in
+# this image under /opt/conda/lib).  Nothing is re-implemented: the RNG the
+# reference uses is the real libgfortran one.
+#
+# Parameters are hard-coded in each reference program (e.g.
+# Fortran/Square/bondc.f:67-92), so each variant is a sed-edited copy made in
+# a scratch directory OUTSIDE the repository; only binaries land in
+# oracle/_ref/.  Reference sources are never copied into the repo.
+set -euo pipefail
+REF=${REF:-/root/reference}
+HERE=$(cd "$(dirname "$0")" && pwd)
+OUT="$HERE/_ref"
+FLANG=${FLANG:-/opt/rocm/lib/llvm/bin/flang}
+GF=${GF:-/opt/conda/lib}
+if [ ! -d "$REF/Fortran" ]; then
+  echo "build_ref.sh: $REF not present; skipping reference build" >&2
+  exit 0
+fi
+if [ ! -e "$GF/libgfortran.so.4" ]; then
+  echo "build_ref.sh: $GF/libgfortran.so.4 missing; reference unbuildable" >&2
+  exit 0
+fi
+mkdir -p "$OUT"
+TMP=$(mktemp -d /tmp/percref.XXXXXX)
+trap 'rm -rf "$TMP"' EXIT
+
+cat > "$TMP/gfrand.c" <<'EOF'
+/* forwarders: ROCm flang external rand_/srand_ -> libgfortran */
+float _gfortran_rand(int *);
+void _gfortran_srand(int *);
+float rand_(int *i) { return _gfortran_rand(i); }
+void srand_(int *i) { _gfortran_srand(i); }
+EOF
+gcc -O2 -c "$TMP/gfrand.c" -o "$TMP/gfrand.o"
+
+# build NAME SRC [sed-expr ...]
+build() {
+  local name=$1 src=$2
+  shift 2
+  local f="$TMP/$name.f"
+  cp "$REF/Fortran/$src" "$f"
+  for e in "$@"; do sed -i "$e" "$f"; done
+  "$FLANG" -O2 "$f" "$TMP/gfrand.o" -L"$GF" -lgfortran -Wl,-rpath,"$GF" \
+    -o "$OUT/$name"
+}
+
+UNCOMMENT_VINT='/write(6,\*) (Vint(i), i = 1,(t-2\*m))/s/^C /  /'
+TIGHT='s/1.00d-08,2500,iter,err/1.00d-14,200000,iter,err/'
+
+# square bond + conductance (bondc), SURVEY.md §4.2
+build sq_bondc_p50            Square/bondc.f
+build sq_bondc_p60            Square/bondc.f 's/pb = 0.50d+00/pb = 0.60d+00/' "$UNCOMMENT_VINT"
+build sq_bondc_p60_tight      Square/bondc.f 's/pb = 0.50d+00/pb = 0.60d+00/' "$TIGHT"
+build sq_bondc_p60_pbc        Square/bondc.f 's/pb = 0.50d+00/pb = 0.60d+00/' 's/pbc = 0 /pbc = 1 /'
+build sq_bondc_20x30_p55      Square/bondc.f 's/m = 50 /m = 20 /' 's/n = 50 /n = 30 /' 's/pb = 0.50d+00/pb = 0.55d+00/' 's/seed = 626504/seed = 777/'
+build tri_bondc_p35           Triangular/bondc.f "$UNCOMMENT_VINT"
+build tri_bondc_p35_tight     Triangular/bondc.f "$TIGHT"
+build tri_bondc_p40_pbc       Triangular/bondc.f 's/pb = 0.35d+00/pb = 0.40d+00/' 's/pbc = 0 /pbc = 1 /'
+# site labeling (config 1 = 64x64 ps .60)
+build sq_site                 Square/site.f
+build sq_site_64              Square/site.f 's/m = 50 /m = 64 /' 's/n = 50 /n = 64 /'
+build sq_site_pbc             Square/site.f 's/pbc = 0 /pbc = 1 /'
+build tri_site                Triangular/site.f
+# mixed site-then-bond
+build sq_sitebond             Square/sitebond.f
+build sq_sitebond_p9          Square/sitebond.f 's/ps = 0.50d+00/ps = 0.90d+00/' 's/pb = 0.50d+00/pb = 0.60d+00/'
+build tri_sitebond            Triangular/sitebond.f
+# ensemble driver (trial seeds, pb sweep, per-step spanning)
+build sq_bond_cond            Square/bond_cond.f
+build sq_bond_cond_3t         Square/bond_cond.f 's/numtrials = 1 /numtrials = 3 /' 's/m = 10 /m = 12 /' 's/n = 10 /n = 12 /'
+build tri_bond_cond           Triangular/bond_cond.f
+echo "reference binaries in $OUT"
