@@ -1,0 +1,237 @@
+#!/usr/bin/env python3
+"""Benchmark: conductance solves/s + CG SpMV GB/s on the BASELINE.json metric
+workload (square L=4096 bond percolation at p=0.60, bondc semantics).
+
+One "step" = one realisation through the whole hot path: occupancy from a
+device-resident occupation order, GPU labeling + spanning, Kirchhoff
+assembly, fused Jacobi-PCG to tol 1e-8 (linbcg stopping rule, itmax 1e6),
+terminal currents.  Realisations shard across ranks (ii = step*world+rank,
+seeds tseed(ii) from master 58302, bond_cond.f:65-70); the only collective
+is the RCCL all-reduce of the ensemble statistics.  Weak scaling.
+
+  python bench.py [--gpus N --steps K --warmup W --L 4096 --p 0.6]
+  torchrun --nproc-per-node N bench.py --gpus N ...
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+sys.path.insert(0, os.path.join(REPO, "tests"))
+
+PEAK_HBM_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def cg_spmv_bytes(N, nnz):
+    """Algorithmic bytes of one fused CG SpMV launch (k_cg_spmv): rowptr,
+    col+val of the off-diagonals, diag, p_old and r (read once), p_new and
+    q (written once)."""
+    return 4 * (N + 1) + 12 * nnz + 8 * N + 8 * N + 8 * N + 16 * N
+
+
+def spmv_bytes(N, nnz):
+    """B = 8(N+nnz) + 4 nnz + 4(N+1) + 16N (plain SpMV)."""
+    return 8 * (N + nnz) + 4 * nnz + 4 * (N + 1) + 16 * N
+
+
+def cpu_baseline(L_, p, seed, gpu_iters, cpu_iters):
+    """The oracle (oracle/perc_oracle.c, a serial C restatement of the
+    reference path, bit-exact against it) on one host core, on a bounded
+    sample of the same workload: union-find labeling + assembly + `cpu_iters`
+    linbcg iterations + currents of one L x L realisation; the solve is
+    extrapolated to the GPU's iteration count for that realisation."""
+    import ctypes as C
+
+    import oracle_lib as O
+    Or = O.lib()
+    lat, m, n = 0, L_, L_
+    t, N = m * n, m * n - 2 * m
+    b1, b2, o1, o2 = O.bond_order(lat, m, n, 0, seed)
+    nb = len(b1)
+    tb = int(p * nb)
+    label, cs = O.i32(nb), O.i32(nb + 2)
+    mx, ms = C.c_int(), C.c_int()
+    t0 = time.perf_counter()
+    cln = Or.or_label_bonds_replay(lat, m, n, 0, nb, b1, b2, o1, o2, tb, label, cs, C.byref(mx),
+                                   C.byref(ms))
+    perc = Or.or_span_bonds(m, n, nb, b1, b2, label, cs, cln)
+    t1 = time.perf_counter()
+    del o1, o2
+    gval = O.f64(nb)
+    Or.or_bond_values(0, nb, b1, b2, label, O.i32(1), perc, 1.0, 1e-12, gval)
+    nmax = N + 1 + 2 * nb + 8
+    sa, ija = O.f64(nmax), O.i32(nmax)
+    itemp, diag = O.f64(N), O.f64(t)
+    Or.or_assemble(lat, m, n, 0, nb, b1, b2, gval, 1.0, 1e-16, 0, nmax, sa, ija, itemp, diag)
+    t2 = time.perf_counter()
+    vint = O.f64(N)
+    it, err = C.c_int(), C.c_double()
+    Or.or_linbcg(sa, ija, N, itemp, vint, 2, -1.0, cpu_iters - 1, C.byref(it), C.byref(err),
+                 None)
+    t3 = time.perf_counter()
+    gt, gb = C.c_double(), C.c_double()
+    Or.or_currents(lat, m, n, 0, nb, b1, b2, gval, diag, vint, 1.0, 1e-10, 0, C.byref(gt),
+                   C.byref(gb))
+    t4 = time.perf_counter()
+    per_iter = (t3 - t2) / it.value
+    total = (t1 - t0) + (t2 - t1) + per_iter * gpu_iters + (t4 - t3)
+    return dict(value=1.0 / total, unit="solves/s", cores=1, kind="port",
+                sample=("oracle C restatement (perc_oracle.c) on 1 core: union-find labeling "
+                        "%.2fs + assembly %.2fs + %d linbcg iterations (%.3fs/it, extrapolated "
+                        "to the GPU's %d) + currents %.2fs, one L=%d p=%.2f realisation"
+                        % (t1 - t0, t2 - t1, it.value, per_iter, gpu_iters, t4 - t3, L_, p)),
+                sample_seconds=round(t4 - t0, 2), s_per_solve=round(total, 2))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=2)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--L", type=int, default=4096)
+    ap.add_argument("--p", type=float, default=0.60)
+    ap.add_argument("--master", type=int, default=58302)
+    ap.add_argument("--tol", type=float, default=1e-8)
+    ap.add_argument("--itmax", type=int, default=10 ** 6)
+    ap.add_argument("--cpu-iters", type=int, default=20)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    import percolation_amd as P
+    from percolation_amd import api
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    L_, p = args.L, args.p
+    nb = api.nbonds(0, L_, L_, 0)
+    tb = int(p * nb)  # bondc.f:191
+    seeds = api.trial_seeds(args.master, 1000)
+    nreal = args.warmup + args.steps
+    # inputs: occupation orders generated on the host (REAL*4 Fisher-Yates,
+    # bondc.f:162-174) and made resident in HBM before the timed region
+    t0 = time.perf_counter()
+    orders, ii_list = [], []
+    for k in range(nreal):
+        ii = (k * world + rank) % 1000
+        o = api.shuffled_ids(nb, int(seeds[ii]))
+        orders.append(torch.from_numpy(o[:tb].copy()).to(dev))
+        ii_list.append(ii)
+    torch.cuda.synchronize()
+    log("rank %d: %d orders (nb=%d, tbonds=%d) in %.1fs" % (rank, nreal, nb, tb,
+                                                            time.perf_counter() - t0))
+    ctx = api.Context(0, L_, L_, 0, device=local)
+    N, nnz = ctx.system_size()
+
+    def run(k):
+        return ctx.bondc_realisation(None, tb, tol=args.tol, itmax=args.itmax,
+                                     device_ptr=orders[k].data_ptr())
+
+    for k in range(args.warmup):
+        r = run(k)
+        log("warmup %d: iter=%d Gtop=%.12g %.0f ms" % (k, r["iter"], r["gtop"], r["t_total_ms"]))
+    ctx.set_kernel_timing(True)
+    ctx.kernel_stats(reset=True)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    results = []
+    for k in range(args.warmup, nreal):
+        r = run(k)
+        results.append(r)
+        log("step %d (ii=%d): nspan=%d iter=%d Gtop=%.12g Gbot=%.12g label %.0f ms solve %.0f ms "
+            "total %.0f ms" % (k - args.warmup, ii_list[k] + 1, r["nspan"], r["iter"], r["gtop"],
+                               r["gbot"], r["t_label_ms"], r["t_solve_ms"], r["t_total_ms"]))
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    ks = ctx.kernel_stats(reset=True)
+    # ensemble statistics: the only collective (RCCL all-reduce over xGMI)
+    g = np.array([r["gtop"] for r in results])
+    stats = torch.tensor([len(results), g.sum(), (g * g).sum(),
+                          sum(r["nspan"] > 0 for r in results), sum(r["iter"] for r in results),
+                          elapsed], dtype=torch.float64, device=dev)
+    tmax = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(stats[:5], op=dist.ReduceOp.SUM)
+        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+    tmax = float(tmax.item())
+    stats = stats.cpu().numpy()
+    nsolves = int(stats[0])
+    value = nsolves / tmax
+
+    spmv_avg_ms = ks["spmv_ms"] / max(ks["spmv_n"], 1)
+    upd_avg_ms = ks["update_ms"] / max(ks["update_n"], 1)
+    bA = cg_spmv_bytes(N, nnz)
+    achieved = bA / (spmv_avg_ms * 1e-3) / 1e9
+    # plain SpMV (SURVEY formula) on the last assembled system, after the timed region
+    plain_ms = ctx.bench_kernel(0, 50)
+    plain_gbs = spmv_bytes(N, nnz) / (plain_ms * 1e-3) / 1e9
+    upd_gbs = 56 * N / (upd_avg_ms * 1e-3) / 1e9
+
+    out = {
+        "metric": "CG SpMV GB/s + conductance solves/sec, L=4096 square lattice at p=0.60",
+        "value": round(value, 5),
+        "unit": "solves/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(tmax / max(args.steps, 1) * 1e3, 2),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic (reference RNG: gfortran rand, tseed(ii) from master %d)"
+                % args.master,
+        "config": {"workload": "square L=%d bond percolation p=%.2f, bondc semantics "
+                               "(labeling+assembly+Jacobi-PCG tol %g itol 2+currents)"
+                               % (L_, p, args.tol),
+                   "L": L_, "p": p, "rows": N, "nnz_offdiag": nnz, "parallelism":
+                   "realisations sharded over %d GPU(s), RCCL stats all-reduce" % world},
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS,
+                     "unit": "GB/s", "frac": round(achieved / PEAK_HBM_GBS, 4), "traffic": None,
+                     "kernel": "k_cg_spmv (fused p-update + CSR SpMV + dot)",
+                     "bytes_per_launch": bA, "avg_launch_ms": round(spmv_avg_ms, 5),
+                     "launches": ks["spmv_n"]},
+        "cg_iterations_mean": round(float(stats[4]) / max(nsolves, 1), 1),
+        "spanning_fraction": round(float(stats[3]) / max(nsolves, 1), 3),
+        "gtop_mean": float(stats[1]) / max(nsolves, 1),
+        "cg_update": {"avg_launch_ms": round(upd_avg_ms, 5), "gbs": round(upd_gbs, 1)},
+        "spmv_plain": {"avg_launch_ms": round(plain_ms, 5), "gbs": round(plain_gbs, 1),
+                       "bytes_per_launch": spmv_bytes(N, nnz)},
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        log("cpu baseline: oracle on a bounded sample ...")
+        try:
+            out["cpu_baseline"] = cpu_baseline(L_, p, int(seeds[ii_list[args.warmup]]),
+                                               results[0]["iter"], args.cpu_iters)
+        except Exception as e:  # keep the GPU line even if the host is short of memory
+            out["cpu_baseline"] = {"value": None, "error": repr(e)}
+    ctx.close()
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,204 @@
+/*
+ * perc.h -- libperc C-ABI: MI355X-native cluster labeling + Kirchhoff
+ * conductance for the IsaiahSteinke/Percolation Fortran drivers.
+ *
+ * Plain C types only (int32 indices, fp64 values, caller-owned host arrays).
+ * Every entry returns an int status (PERC_OK == 0) where the reference would
+ * `pause` (Fortran/Square/bondc.f:737,777,891,906).  One context per device
+ * and host thread; no hidden globals except the gfortran-compatible RNG
+ * stream (perc_srand/perc_rand), which is process-global exactly like
+ * libgfortran's rand/srand.
+ *
+ * Reference interfaces replaced (paths relative to the reference root):
+ *   nearestn          Fortran/Square/bondc.f:617-715, Triangular/bondc.f:619-804
+ *   bond list         Fortran/Square/bondc.f:137-154
+ *   rand / srand      GNU Fortran runtime; call sites Square/bondc.f:162,167
+ *   labeling loops    Square/bondc.f:194-393, Square/site.f:167-289,
+ *                     Square/sitebond.f:187-400
+ *   spanning test     Square/bondc.f:413-456, Square/site.f:309-344,
+ *                     Square/sitebond.f:423-458
+ *   assembly + solve  Square/bondc.f:465-595 (bond); MATLAB/ConductCalc.m:
+ *                     88-196 (site / mixed weight rules)
+ *   NR sparse layer   sprsin/linbcg/atimes/asolve/snrm/dsprsax/dsprstx,
+ *                     Square/bondc.f:723-917 (symbols below, F77 ABI)
+ */
+#ifndef PERC_H
+#define PERC_H
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- status codes ---------------------------------------------------- */
+#define PERC_OK 0
+#define PERC_EINVAL (-1)     /* bad argument                                  */
+#define PERC_ENOMEM (-2)     /* device or host allocation failed              */
+#define PERC_EHIP (-3)       /* HIP runtime error                             */
+#define PERC_ENMAX (-4)      /* 'nmax too small in sprsin'  (bondc.f:737)     */
+#define PERC_EITOL (-5)      /* 'illegal itol in linbcg'    (bondc.f:777)     */
+#define PERC_EMISMATCH (-6)  /* 'mismatched vector and matrix' (bondc.f:891)  */
+#define PERC_EREPLAY (-7)    /* label replay impossible (H7: odd-m triangular) */
+#define PERC_ENODEV (-8)     /* no HIP device                                  */
+#define PERC_ESTATE (-9)     /* call order violated (e.g. solve before label)  */
+
+/* lattice kinds */
+#define PERC_SQUARE 0
+#define PERC_TRIANGULAR 1
+/* occupancy kinds */
+#define PERC_BOND 0
+#define PERC_SITE 1
+#define PERC_SITEBOND 2
+/* conductance weight rules (which bonds get g0; all others get `leak`) */
+#define PERC_RULE_BOND 0     /* bond label == perccln         (bondc.f:483) */
+#define PERC_RULE_SITE 1     /* both end sites in perccln     (ConductCalc.m:90) */
+#define PERC_RULE_MIXED 2    /* bond and both sites in perccln (ConductCalc.m:136) */
+/* terminal-current rules */
+#define PERC_CUR_FORTRAN 0   /* sprsin(G,1e-10) + dsprsax, ascending sums (bondc.f:576-592) */
+#define PERC_CUR_MATLAB 1    /* full G*V, Itop summed from site t down (ConductCalc.m:188-196) */
+
+typedef struct perc_ctx perc_ctx;
+
+/* ---- RNG: GNU Fortran rand/srand (Park-Miller 16807, 2^31-1) ----------- */
+void perc_srand(int seed);
+float perc_rand(int i);
+/* tseed(1..k) = int(rand(0)*1e7)+1 after srand(master) (bond_cond.f:65-70) */
+void perc_trial_seeds(int master, int k, int *tseed);
+
+/* ---- host-side lattice helpers --------------------------------------- */
+int perc_nbonds(int lattice, int m, int n, int pbc);
+/* nn[0..5] of site rn (1-based), 0 = none; returns scn */
+int perc_nearestn(int lattice, int m, int n, int pbc, int rn, int *nn);
+/* bond list b1[k] < b2[k], k = 0..nb-1 in reference order; returns nb */
+int perc_bond_list(int lattice, int m, int n, int pbc, int *b1, int *b2);
+/* REAL*4 Fisher-Yates of a 1-based id permutation, H2-exact: order has N+1
+   slots; on entry order[k] = k+1 (k<N) and order[N] = 0; uses the global
+   RNG stream from the current seed (Square/bondc.f:166-174). */
+void perc_shuffle(int N, int *order);
+
+/* ---- context --------------------------------------------------------- */
+int perc_ctx_create(int device, int lattice, int m, int n, int pbc, perc_ctx **out);
+int perc_ctx_destroy(perc_ctx *h);
+/* last HIP error string for diagnostics (never NULL) */
+const char *perc_last_error(void);
+
+/* ---- occupancy + labeling -------------------------------------------- */
+/* Occupy the first `count` entries of `order` (1-based bond ids for
+   PERC_BOND, site ids for PERC_SITE; 0 = H2 sentinel, skipped).  For
+   PERC_SITEBOND both lists are given.  Host arrays, copied to the device. */
+int perc_occupy(perc_ctx *h, int kind, int nsites, const int *site_order,
+                int nbonds, const int *bond_order);
+
+/* Same, with the order lists already resident in device memory (device
+   pointers on the context's device); used when inputs live in HBM. */
+int perc_occupy_device(perc_ctx *h, int kind, int nsites, const int *d_site_order,
+                       int nbonds, const int *d_bond_order);
+
+typedef struct {
+  int nclusters;      /* connected components with >= 1 occupied element     */
+  int nspan;          /* spanning components                                  */
+  int span_root;      /* canonical id (min site) of the chosen spanning one, 0 */
+  int span_sites;     /* sites in the chosen spanning component               */
+  int replayed;       /* 1 if the host label replay decided the lowest label  */
+  int perccln;        /* reference label of the chosen component if known     */
+} perc_label_info;
+
+/* GPU connected components of the occupancy + spanning detection.  When
+   more than one component spans, the reference's lowest-label rule is
+   resolved by the host replay (hazard H4).  canon_out (optional, host,
+   t ints) receives the canonical component id (min site id, 0 = empty site)
+   per site. */
+int perc_label(perc_ctx *h, perc_label_info *info, int *canon_out);
+
+/* Reference label numbers (history-dependent, Square/bondc.f:275-364) by
+   O(N alpha) host replay of the last occupancy.  Any output may be NULL.
+   bond_label[nb], site_label[t], csize[cap] (cap >= nb+2 bond, t+2 site,
+   t+nb+2 mixed), stats[4] = {cln, maxcn, maxcs, perccln}. */
+int perc_label_numbers(perc_ctx *h, int *bond_label, int *site_label,
+                       int *csize, int cap, int *stats);
+
+/* Same numbering without a context or device: host-only O(N alpha) replay
+   of an explicit occupancy (used by the drivers' text output and tests). */
+int perc_replay_labels(int lattice, int m, int n, int pbc, int kind, int nsites,
+                       const int *site_order, int nbonds, const int *bond_order,
+                       int *bond_label, int *site_label, int *csize, int cap,
+                       int *stats);
+
+/* ---- conductance ----------------------------------------------------- */
+typedef struct {
+  double gtop, gbot;  /* Itop/Va, |Ibot|/Va                                  */
+  double err;         /* final linbcg err                                    */
+  int iter;           /* linbcg iterations                                   */
+  int status;         /* 0 ok, 1 = no spanning cluster (G = 0)               */
+  double t_assemble_ms, t_solve_ms, t_currents_ms;
+} perc_cond_result;
+
+/* Assemble the interior Kirchhoff system of the chosen spanning component
+   (CSR, diagonal first), solve it with the fused Jacobi-PCG that follows
+   linbcg's operation order and stopping rule (itol 1 or 2), and compute
+   the terminal currents.  vint_out (optional, host, t-2m doubles). */
+int perc_conductance(perc_ctx *h, int rule, int cur_rule, double Va, double g0,
+                     double leak, int itol, double tol, int itmax,
+                     perc_cond_result *res, double *vint_out);
+
+/* Matrix access for parity tests / roofline runs: copy the assembled
+   interior CSR (0-based: rowptr[N+1], col[nnz], val[nnz], diag[N], rhs[N]).
+   Pass NULL to skip an array; *nnz_out receives nnz. */
+int perc_get_system(perc_ctx *h, int *rowptr, int *col, double *val,
+                    double *diag, double *rhs, int *n_out, int *nnz_out);
+/* y = A x on the assembled system (dsprsax order), host in / host out */
+int perc_spmv_host(perc_ctx *h, const double *x, double *y);
+/* Roofline probe: `reps` back-to-back SpMVs (dsprsax) / fused CG SpMV
+   kernels on the assembled system; returns mean kernel ms (HIP events on
+   the context stream).  which: 0 = plain SpMV, 1 = fused CG SpMV, 2 = CG
+   update kernel. */
+int perc_bench_kernel(perc_ctx *h, int which, int reps, double *ms);
+
+/* Live kernel timing: when enabled, every CG SpMV / update launch inside
+   perc_conductance is bracketed by HIP events on the context stream; the
+   accumulated device time of launches that did work is returned (ms) with
+   their count.  stats[0..3] = {spmv_ms, spmv_launches, update_ms,
+   update_launches}; reset clears the accumulators. */
+int perc_set_kernel_timing(perc_ctx *h, int enable);
+int perc_kernel_stats(perc_ctx *h, double *stats, int reset);
+/* Sizes of the assembled system: out[0] = N (rows), out[1] = nnz (off-diagonal) */
+int perc_system_size(perc_ctx *h, long long *out);
+
+/* ---- one hot-path realisation (bench / ensemble) ---------------------- */
+typedef struct {
+  perc_label_info label;
+  perc_cond_result cond;
+  double t_upload_ms, t_label_ms, t_total_ms;
+} perc_realisation;
+/* occupy + label + conductance for PERC_BOND with the bondc rules;
+   bond_order is a host array, or a device array when on_device != 0 */
+int perc_bondc_realisation(perc_ctx *h, int tbonds, const int *bond_order,
+                           int on_device, double Va, double g0, double tol,
+                           int itmax, perc_realisation *out);
+
+/* ---- ensemble statistics (bond_cond, config 4) ----------------------- */
+/* Accumulate stats for one pb point: {count, sum G, sum G^2, count spanning,
+   sum iter} into acc[5*point..]. */
+void perc_stats_accumulate(double *acc, int point, double g, int spanning, int iter);
+
+/* ---- Numerical-Recipes-compatible layer (F77 ABI, by reference) ------- *
+ * Same names and argument meaning as the routines embedded in the
+ * reference (Square/bondc.f:723-917).  linbcg_/atimes_/asolve_ read the
+ * matrix from COMMON /mat/ sa(NMAX), ija(NMAX) (symbol mat_, NMAX=20000 as
+ * in the reference) unless perc_nr_bind() points them at other storage.
+ * linbcg_ runs the HIP PCG on device 0.  Errors that `pause` in the
+ * reference are reported through perc_nr_status(). */
+void sprsin_(double *a, int *n, int *np, double *thresh, int *nmax, double *sa, int *ija);
+void dsprsax_(double *sa, int *ija, double *x, double *b, int *n);
+void dsprstx_(double *sa, int *ija, double *x, double *b, int *n);
+void atimes_(int *n, double *x, double *r, int *itrnsp);
+void asolve_(int *n, double *b, double *x, int *itrnsp);
+double snrm_(int *n, double *sx, int *itol);
+void linbcg_(int *n, double *b, double *x, int *itol, double *tol, int *itmax,
+             int *iter, double *err);
+void perc_nr_bind(double *sa, int *ija, int nmax);
+int perc_nr_status(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PERC_H */

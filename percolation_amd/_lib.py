@@ -1,0 +1,120 @@
+"""ctypes binding of libperc.so (include/perc.h).
+
+The library is built in-tree (percolation_amd/libperc.so, by
+percolation_amd/build.py or `make -C percolation_amd/csrc`).  Loading fails
+loudly when it is missing: there is no Python or CPU fallback for any
+compute entry point.
+"""
+import ctypes as C
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIBPERC = os.path.join(HERE, "libperc.so")
+
+PERC_OK = 0
+ERRORS = {
+    -1: "PERC_EINVAL", -2: "PERC_ENOMEM", -3: "PERC_EHIP", -4: "PERC_ENMAX",
+    -5: "PERC_EITOL", -6: "PERC_EMISMATCH", -7: "PERC_EREPLAY", -8: "PERC_ENODEV",
+    -9: "PERC_ESTATE",
+}
+SQUARE, TRIANGULAR = 0, 1
+BOND, SITE, SITEBOND = 0, 1, 2
+RULE_BOND, RULE_SITE, RULE_MIXED = 0, 1, 2
+CUR_FORTRAN, CUR_MATLAB = 0, 1
+
+
+class LabelInfo(C.Structure):
+    _fields_ = [("nclusters", C.c_int), ("nspan", C.c_int), ("span_root", C.c_int),
+                ("span_sites", C.c_int), ("replayed", C.c_int), ("perccln", C.c_int)]
+
+
+class CondResult(C.Structure):
+    _fields_ = [("gtop", C.c_double), ("gbot", C.c_double), ("err", C.c_double),
+                ("iter", C.c_int), ("status", C.c_int), ("t_assemble_ms", C.c_double),
+                ("t_solve_ms", C.c_double), ("t_currents_ms", C.c_double)]
+
+
+class Realisation(C.Structure):
+    _fields_ = [("label", LabelInfo), ("cond", CondResult), ("t_upload_ms", C.c_double),
+                ("t_label_ms", C.c_double), ("t_total_ms", C.c_double)]
+
+
+class PercError(RuntimeError):
+    pass
+
+
+_I = np.ctypeslib.ndpointer(dtype=np.int32, flags="C_CONTIGUOUS")
+_D = np.ctypeslib.ndpointer(dtype=np.float64, flags="C_CONTIGUOUS")
+_VP = C.c_void_p
+_lib = None
+
+# name -> (restype, argtypes); every symbol declared in include/perc.h
+SIGNATURES = {
+    "perc_srand": (None, [C.c_int]),
+    "perc_rand": (C.c_float, [C.c_int]),
+    "perc_trial_seeds": (None, [C.c_int, C.c_int, _I]),
+    "perc_nbonds": (C.c_int, [C.c_int] * 4),
+    "perc_nearestn": (C.c_int, [C.c_int] * 5 + [_I]),
+    "perc_bond_list": (C.c_int, [C.c_int] * 4 + [_I, _I]),
+    "perc_shuffle": (None, [C.c_int, _I]),
+    "perc_ctx_create": (C.c_int, [C.c_int] * 5 + [C.POINTER(C.c_void_p)]),
+    "perc_ctx_destroy": (C.c_int, [_VP]),
+    "perc_last_error": (C.c_char_p, []),
+    "perc_occupy": (C.c_int, [_VP, C.c_int, C.c_int, _VP, C.c_int, _VP]),
+    "perc_label": (C.c_int, [_VP, C.POINTER(LabelInfo), _VP]),
+    "perc_label_numbers": (C.c_int, [_VP, _VP, _VP, _VP, C.c_int, _VP]),
+    "perc_replay_labels": (C.c_int, [C.c_int] * 6 + [_VP, C.c_int, _VP, _VP, _VP, _VP, C.c_int,
+                                                      _VP]),
+    "perc_conductance": (C.c_int, [_VP, C.c_int, C.c_int, C.c_double, C.c_double, C.c_double,
+                                   C.c_int, C.c_double, C.c_int, C.POINTER(CondResult), _VP]),
+    "perc_get_system": (C.c_int, [_VP, _VP, _VP, _VP, _VP, _VP, C.POINTER(C.c_int),
+                                  C.POINTER(C.c_int)]),
+    "perc_spmv_host": (C.c_int, [_VP, _D, _D]),
+    "perc_bench_kernel": (C.c_int, [_VP, C.c_int, C.c_int, C.POINTER(C.c_double)]),
+    "perc_bondc_realisation": (C.c_int, [_VP, C.c_int, _VP, C.c_int, C.c_double, C.c_double,
+                                         C.c_double, C.c_int, C.POINTER(Realisation)]),
+    "perc_occupy_device": (C.c_int, [_VP, C.c_int, C.c_int, _VP, C.c_int, _VP]),
+    "perc_set_kernel_timing": (C.c_int, [_VP, C.c_int]),
+    "perc_kernel_stats": (C.c_int, [_VP, _D, C.c_int]),
+    "perc_system_size": (C.c_int, [_VP, np.ctypeslib.ndpointer(dtype=np.int64)]),
+    "perc_stats_accumulate": (None, [_D, C.c_int, C.c_double, C.c_int, C.c_int]),
+    "sprsin_": (None, [_VP] * 7),
+    "dsprsax_": (None, [_VP] * 5),
+    "dsprstx_": (None, [_VP] * 5),
+    "atimes_": (None, [_VP] * 4),
+    "asolve_": (None, [_VP] * 4),
+    "snrm_": (C.c_double, [_VP] * 3),
+    "linbcg_": (None, [_VP] * 8),
+    "perc_nr_bind": (None, [_VP, _VP, C.c_int]),
+    "perc_nr_status": (C.c_int, []),
+}
+
+
+def lib():
+    """Load libperc.so (raises if it has not been built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIBPERC):
+        raise PercError("libperc.so not built: run `python -c 'import __graft_entry__ as g; "
+                        "g.build()'` or `make -C percolation_amd/csrc` (%s missing)" % LIBPERC)
+    L = C.CDLL(LIBPERC, mode=C.RTLD_GLOBAL)
+    for name, (res, args) in SIGNATURES.items():
+        f = getattr(L, name)
+        f.restype = res
+        f.argtypes = args
+    _lib = L
+    return L
+
+
+def check(rc, what=""):
+    if rc != PERC_OK:
+        msg = lib().perc_last_error().decode(errors="replace")
+        raise PercError("%s failed: %s (%s)" % (what, ERRORS.get(rc, rc), msg))
+    return rc
+
+
+def ptr(a):
+    return None if a is None else a.ctypes.data_as(C.c_void_p)

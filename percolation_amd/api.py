@@ -1,0 +1,367 @@
+"""Host-side mirror of the reference drivers over the libperc C-ABI.
+
+The drop-in host is Fortran (percolation_amd/fortran/); this module mirrors
+the same programs for tests and the benchmark, with the reference's
+parameter names and semantics:
+
+  bondc      Fortran/Square/bondc.f, Fortran/Triangular/bondc.f
+  site       Fortran/*/site.f (+ MATLAB/ConductCalc.m site rule)
+  sitebond   Fortran/*/sitebond.f (+ ConductCalc.m mixed rule)
+  bond_cond  Fortran/*/bond_cond.f grid-point conductances
+
+Every compute step runs in libperc on the GPU; there is no fallback.
+"""
+import ctypes as C
+
+import numpy as np
+
+from . import _lib as L
+
+LEAK = 1.0e-12  # bondc.f:487
+
+
+def _i32(n):
+    return np.zeros(n, dtype=np.int32)
+
+
+def nbonds(lattice, m, n, pbc=0):
+    return L.lib().perc_nbonds(lattice, m, n, pbc)
+
+
+def bond_list(lattice, m, n, pbc=0):
+    """(b1, b2) in reference order (bondc.f:137-154)."""
+    nb = nbonds(lattice, m, n, pbc)
+    b1, b2 = _i32(nb), _i32(nb)
+    got = L.lib().perc_bond_list(lattice, m, n, pbc, b1, b2)
+    assert got == nb
+    return b1, b2
+
+
+def nearestn(lattice, m, n, pbc, rn):
+    nn = _i32(6)
+    scn = L.lib().perc_nearestn(lattice, m, n, pbc, rn, nn)
+    return nn[:scn]
+
+
+def shuffled_ids(N, seed):
+    """1-based id permutation after srand(seed) + REAL*4 Fisher-Yates;
+    N+1 slots, slot N is the H2 spill slot (bondc.f:162-174)."""
+    order = _i32(N + 1)
+    order[:N] = np.arange(1, N + 1, dtype=np.int32)
+    lib = L.lib()
+    lib.perc_srand(seed)
+    lib.perc_shuffle(N, order)
+    return order
+
+
+def trial_seeds(master, k=1000):
+    ts = _i32(k)
+    L.lib().perc_trial_seeds(master, k, ts)
+    return ts
+
+
+def replay_labels(lattice, m, n, pbc, kind, site_order=None, nsites=0, bond_order=None,
+                  nbond=0):
+    """Reference label numbering of an explicit occupancy (host replay, no
+    device): dict(bond_label, site_label, csize, cln, maxcn, maxcs, perccln)."""
+    t = m * n
+    nb = nbonds(lattice, m, n, pbc)
+    cap = {L.BOND: nb + 2, L.SITE: t + 2}.get(kind, t + nb + 2)
+    bl = _i32(nb) if kind != L.SITE else None
+    sl = _i32(t) if kind != L.BOND else None
+    cs, st = _i32(cap), _i32(4)
+    so = None if site_order is None else np.ascontiguousarray(site_order, dtype=np.int32)
+    bo = None if bond_order is None else np.ascontiguousarray(bond_order, dtype=np.int32)
+    L.check(L.lib().perc_replay_labels(lattice, m, n, pbc, kind, nsites, L.ptr(so), nbond,
+                                       L.ptr(bo), L.ptr(bl), L.ptr(sl), L.ptr(cs), cap,
+                                       L.ptr(st)), "perc_replay_labels")
+    return dict(bond_label=bl, site_label=sl, csize=cs, cln=int(st[0]), maxcn=int(st[1]),
+                maxcs=int(st[2]), perccln=int(st[3]))
+
+
+class Context:
+    """One libperc context (one lattice on one device)."""
+
+    def __init__(self, lattice, m, n, pbc=0, device=0):
+        self.lattice, self.m, self.n, self.pbc = lattice, m, n, pbc
+        self.t = m * n
+        self.nb = nbonds(lattice, m, n, pbc)
+        self.N = self.t - 2 * m
+        h = C.c_void_p()
+        L.check(L.lib().perc_ctx_create(device, lattice, m, n, pbc, C.byref(h)),
+                "perc_ctx_create")
+        self.h = h
+
+    def close(self):
+        if self.h:
+            L.lib().perc_ctx_destroy(self.h)
+            self.h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # -- occupancy ---------------------------------------------------------
+    def occupy(self, kind, site_order=None, nsites=0, bond_order=None, nbonds_=0):
+        so = None if site_order is None else np.ascontiguousarray(site_order, dtype=np.int32)
+        bo = None if bond_order is None else np.ascontiguousarray(bond_order, dtype=np.int32)
+        L.check(L.lib().perc_occupy(self.h, kind, nsites, L.ptr(so), nbonds_, L.ptr(bo)),
+                "perc_occupy")
+
+    def label(self, canon=False):
+        info = L.LabelInfo()
+        out = _i32(self.t) if canon else None
+        L.check(L.lib().perc_label(self.h, C.byref(info), L.ptr(out)), "perc_label")
+        res = {k: getattr(info, k) for k, _ in L.LabelInfo._fields_}
+        if canon:
+            res["canon"] = out
+        return res
+
+    def label_numbers(self, kind):
+        if kind == L.BOND:
+            cap = self.nb + 2
+        elif kind == L.SITE:
+            cap = self.t + 2
+        else:
+            cap = self.t + self.nb + 2
+        bl = _i32(self.nb) if kind != L.SITE else None
+        sl = _i32(self.t) if kind != L.BOND else None
+        cs, st = _i32(cap), _i32(4)
+        L.check(L.lib().perc_label_numbers(self.h, L.ptr(bl), L.ptr(sl), L.ptr(cs), cap,
+                                           L.ptr(st)), "perc_label_numbers")
+        return dict(bond_label=bl, site_label=sl, csize=cs, cln=int(st[0]), maxcn=int(st[1]),
+                    maxcs=int(st[2]), perccln=int(st[3]))
+
+    # -- conductance -------------------------------------------------------
+    def conductance(self, rule=L.RULE_BOND, cur_rule=L.CUR_FORTRAN, Va=1.0, g0=1.0, leak=LEAK,
+                    itol=2, tol=1e-8, itmax=2500, vint=False):
+        res = L.CondResult()
+        v = np.zeros(self.N, dtype=np.float64) if vint else None
+        L.check(L.lib().perc_conductance(self.h, rule, cur_rule, Va, g0, leak, itol, tol, itmax,
+                                         C.byref(res), L.ptr(v)), "perc_conductance")
+        out = {k: getattr(res, k) for k, _ in L.CondResult._fields_}
+        if vint:
+            out["vint"] = v
+        return out
+
+    def system(self):
+        n, nnz = C.c_int(), C.c_int()
+        L.check(L.lib().perc_get_system(self.h, None, None, None, None, None, C.byref(n),
+                                        C.byref(nnz)), "perc_get_system")
+        rp, col = _i32(n.value + 1), _i32(nnz.value)
+        val, diag, rhs = (np.zeros(k, np.float64) for k in (nnz.value, n.value, n.value))
+        L.check(L.lib().perc_get_system(self.h, L.ptr(rp), L.ptr(col), L.ptr(val), L.ptr(diag),
+                                        L.ptr(rhs), C.byref(n), C.byref(nnz)),
+                "perc_get_system")
+        return dict(rowptr=rp, col=col, val=val, diag=diag, rhs=rhs)
+
+    def spmv(self, x):
+        x = np.ascontiguousarray(x, dtype=np.float64)
+        y = np.zeros_like(x)
+        L.check(L.lib().perc_spmv_host(self.h, x, y), "perc_spmv_host")
+        return y
+
+    def bench_kernel(self, which, reps):
+        ms = C.c_double()
+        L.check(L.lib().perc_bench_kernel(self.h, which, reps, C.byref(ms)), "perc_bench_kernel")
+        return ms.value
+
+    def set_kernel_timing(self, enable=True):
+        L.check(L.lib().perc_set_kernel_timing(self.h, int(enable)), "perc_set_kernel_timing")
+
+    def kernel_stats(self, reset=True):
+        st = np.zeros(4)
+        L.check(L.lib().perc_kernel_stats(self.h, st, int(reset)), "perc_kernel_stats")
+        return dict(spmv_ms=st[0], spmv_n=int(st[1]), update_ms=st[2], update_n=int(st[3]))
+
+    def system_size(self):
+        out = np.zeros(2, dtype=np.int64)
+        L.check(L.lib().perc_system_size(self.h, out), "perc_system_size")
+        return int(out[0]), int(out[1])
+
+    def bondc_realisation(self, order, tbonds, Va=1.0, g0=1.0, tol=1e-8, itmax=2500,
+                          device_ptr=None):
+        """occupy + label + conductance.  `order` is a host int32 array, or
+        pass device_ptr (int address of a device int32 array) instead."""
+        r = L.Realisation()
+        if device_ptr is not None:
+            src, on_dev = C.c_void_p(device_ptr), 1
+        else:
+            order = np.ascontiguousarray(order, dtype=np.int32)
+            src, on_dev = L.ptr(order), 0
+        L.check(L.lib().perc_bondc_realisation(self.h, tbonds, src, on_dev, Va, g0, tol, itmax,
+                                               C.byref(r)), "perc_bondc_realisation")
+        out = {k: getattr(r.label, k) for k, _ in L.LabelInfo._fields_}
+        out.update({k: getattr(r.cond, k) for k, _ in L.CondResult._fields_})
+        out.update(t_upload_ms=r.t_upload_ms, t_label_ms=r.t_label_ms,
+                   t_total_ms=r.t_total_ms)
+        return out
+
+
+# ---------------------------------------------------------------- programs
+def bondc(lattice=0, m=50, n=50, pbc=0, pb=0.50, seed=626504, Va=1.0, g0=1.0, tol=1e-8,
+          itmax=2500, labels=True, ctx=None, device=0):
+    """One bond realisation filled to pb, spanning test, conductance
+    (Fortran/Square/bondc.f; triangular defaults pb=.35, seed=62703)."""
+    own = ctx is None
+    ctx = ctx or Context(lattice, m, n, pbc, device)
+    try:
+        nb = ctx.nb
+        order = shuffled_ids(nb, seed)
+        tbonds = int(pb * nb)  # bondc.f:191
+        ctx.occupy(L.BOND, bond_order=order, nbonds_=tbonds)
+        li = ctx.label()
+        out = dict(nb=nb, tbonds=tbonds, order=order, nspan=li["nspan"],
+                   span_root=li["span_root"], span_sites=li["span_sites"])
+        if labels:
+            ln = ctx.label_numbers(L.BOND)
+            out.update(label=ln["bond_label"], csize=ln["csize"], cln=ln["cln"],
+                       maxcn=ln["maxcn"], maxcs=ln["maxcs"], perccln=ln["perccln"],
+                       perccls=int(ln["csize"][ln["perccln"]]) if ln["perccln"] else 0)
+        c = ctx.conductance(L.RULE_BOND, L.CUR_FORTRAN, Va, g0, LEAK, 2, tol, itmax)
+        out.update(gtop=c["gtop"], gbot=c["gbot"], iter=c["iter"], err=c["err"],
+                   cond_status=c["status"])
+        return out
+    finally:
+        if own:
+            ctx.close()
+
+
+def site(lattice=0, m=50, n=50, pbc=0, ps=0.60, seed=1080115, conductance=False, Va=1.0,
+         g0=1.0, tol=1e-8, itmax=100000, cur_rule=L.CUR_MATLAB, ctx=None, device=0):
+    """Site realisation (Fortran/Square/site.f) and, optionally, the
+    ConductCalc.m site-rule conductance of its spanning cluster."""
+    own = ctx is None
+    ctx = ctx or Context(lattice, m, n, pbc, device)
+    try:
+        t = ctx.t
+        order = shuffled_ids(t, seed)
+        tsites = int(ps * t)
+        ctx.occupy(L.SITE, site_order=order, nsites=tsites)
+        li = ctx.label()
+        ln = ctx.label_numbers(L.SITE)
+        out = dict(order=order, tsites=tsites, site_label=ln["site_label"], csize=ln["csize"],
+                   cln=ln["cln"], maxcn=ln["maxcn"], maxcs=ln["maxcs"], perccln=ln["perccln"],
+                   nspan=li["nspan"], span_root=li["span_root"])
+        if conductance:
+            c = ctx.conductance(L.RULE_SITE, cur_rule, Va, g0, LEAK, 2, tol, itmax)
+            out.update(gtop=c["gtop"], gbot=c["gbot"], iter=c["iter"], err=c["err"])
+        return out
+    finally:
+        if own:
+            ctx.close()
+
+
+def sitebond(lattice=0, m=50, n=50, pbc=0, ps=0.50, pb=0.50, sseed=143285, bseed=43716,
+             conductance=False, Va=1.0, g0=1.0, tol=1e-8, itmax=100000, cur_rule=L.CUR_MATLAB,
+             ctx=None, device=0):
+    """Mixed site-then-bond realisation (Fortran/Square/sitebond.f) and,
+    optionally, the ConductCalc.m mixed-rule conductance."""
+    own = ctx is None
+    ctx = ctx or Context(lattice, m, n, pbc, device)
+    try:
+        t, nb = ctx.t, ctx.nb
+        sorder = shuffled_ids(t, sseed)   # sitebond.f:129-143
+        border = shuffled_ids(nb, bseed)  # sitebond.f:177-189
+        ts, tb = int(ps * t), int(pb * nb)
+        ctx.occupy(L.SITEBOND, site_order=sorder, nsites=ts, bond_order=border, nbonds_=tb)
+        li = ctx.label()
+        ln = ctx.label_numbers(L.SITEBOND)
+        out = dict(sorder=sorder, border=border, site_label=ln["site_label"],
+                   bond_label=ln["bond_label"], csize=ln["csize"], cln=ln["cln"],
+                   maxcn=ln["maxcn"], maxcs=ln["maxcs"], perccln=ln["perccln"],
+                   nspan=li["nspan"], span_root=li["span_root"])
+        if conductance:
+            c = ctx.conductance(L.RULE_MIXED, cur_rule, Va, g0, LEAK, 2, tol, itmax)
+            out.update(gtop=c["gtop"], gbot=c["gbot"], iter=c["iter"], err=c["err"])
+        return out
+    finally:
+        if own:
+            ctx.close()
+
+
+def pb_grid(lattice, nb):
+    """nbarr of bond_cond.f:84-97 (square 0.49.., triangular 0.35.., +5e-3)."""
+    pbarr = np.zeros(250)
+    pbarr[0] = 0.35 if lattice else 0.49
+    npts = 131 if lattice else 103
+    for i in range(1, npts):
+        pbarr[i] = pbarr[i - 1] + 5.00e-03
+    return (pbarr * nb).astype(np.int64).astype(np.int32)  # truncation (H3 repeats kept)
+
+
+def first_spanning(ctx, order, lo=0, hi=None):
+    """Smallest bf at which a spanning cluster exists (the pc step of
+    bond_cond.f:381), by bisection over occupation counts with the GPU
+    labeling (spanning is monotone in bf)."""
+    hi = ctx.nb if hi is None else hi
+    ctx.occupy(L.BOND, bond_order=order, nbonds_=hi)
+    if ctx.label()["nspan"] == 0:
+        return 0
+    while hi - lo > 1:
+        mid = (lo + hi) // 2
+        ctx.occupy(L.BOND, bond_order=order, nbonds_=mid)
+        if ctx.label()["nspan"]:
+            hi = mid
+        else:
+            lo = mid
+    return hi
+
+
+def bond_cond_grid(lattice=0, m=10, n=10, pbc=0, master=58302, numtrials=1, Va=1.0, g0=1.0,
+                   tol=1e-8, itmax=2500, trials=None, with_labels=True, ctx=None, device=0):
+    """bond_cond (Fortran/Square/bond_cond.f:123-498): per trial ii, seed
+    tseed(ii), conductance of the lowest-label spanning cluster at each
+    grid point nbarr(jj) until the sweep ends (or stalls on a repeated
+    nbarr value, hazard H3), pc = first spanning fraction, and the final
+    lowest spanning label."""
+    own = ctx is None
+    ctx = ctx or Context(lattice, m, n, pbc, device)
+    try:
+        nb = ctx.nb
+        seeds = trial_seeds(master, 1000)
+        nbarr = pb_grid(lattice, nb)
+        out = []
+        for ii in (trials if trials is not None else range(numtrials)):
+            order = shuffled_ids(nb, int(seeds[ii]))
+            rows = []
+            jj = 0
+            for bf in nbarr:
+                if bf <= 0 or jj >= len(nbarr) or bf != nbarr[jj]:
+                    break
+                if rows and bf <= rows[-1]["bf"]:
+                    break  # H3: repeated nbarr value stalls the sweep
+                ctx.occupy(L.BOND, bond_order=order, nbonds_=int(bf))
+                li = ctx.label()
+                c = ctx.conductance(L.RULE_BOND, L.CUR_FORTRAN, Va, g0, LEAK, 2, tol, itmax)
+                pbv = float(np.float32(np.float32(bf) / np.float32(nb)))
+                rows.append(dict(bf=int(bf), pb=pbv, gbot=c["gbot"], gtop=c["gtop"],
+                                 iter=c["iter"], spanning=li["nspan"] > 0))
+                jj += 1
+            bfc = first_spanning(ctx, order)
+            pc = float(np.float32(np.float32(bfc) / np.float32(nb))) if bfc else 0.0
+            tr = dict(ii=ii + 1, seed=int(seeds[ii]), rows=rows, pc=pc, bf_c=bfc)
+            if with_labels:
+                ctx.occupy(L.BOND, bond_order=order, nbonds_=nb)
+                tr["perccln"] = ctx.label_numbers(L.BOND)["perccln"] if bfc else 0
+            out.append(tr)
+        return out
+    finally:
+        if own:
+            ctx.close()
+
+
+# ---------------------------------------------------------------- file output
+def fmt_i10(*cols):
+    """Records of (i10,",",i10,...) -- the reference's formatted writes."""
+    n = len(cols[0])
+    f = ",".join(["%10d"] * len(cols)) + "\n"
+    return "".join(f % tuple(int(c[i]) for c in cols) for i in range(n))

@@ -1,0 +1,167 @@
+// lattice.h -- lattice topology for libperc, usable on host and gfx950.
+//
+// Neighbour order is part of the reference's semantics (it fixes label
+// tie-breaks, bond-list order and the RHS summation order), so nearestn()
+// reproduces Fortran/Square/bondc.f:617-715 and Fortran/Triangular/
+// bondc.f:619-804 branch for branch.  Sites are 1-based, row-major from the
+// bottom row; nn[k] == 0 means "no neighbour".
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+namespace perc {
+
+enum Lattice : int { kSquare = 0, kTriangular = 1 };
+
+struct Geom {
+  int lattice;  // kSquare / kTriangular
+  int m, n;     // width, height (sites)
+  int pbc;      // left/right periodic
+  int t;        // m*n
+  int scn;      // site coordination number (4 / 6)
+  int bcn;      // bond coordination number (6 / 10)
+};
+
+__host__ __device__ inline Geom make_geom(int lattice, int m, int n, int pbc) {
+  Geom g;
+  g.lattice = lattice;
+  g.m = m;
+  g.n = n;
+  g.pbc = pbc;
+  g.t = m * n;
+  g.scn = lattice == kSquare ? 4 : 6;
+  g.bcn = lattice == kSquare ? 6 : 10;
+  return g;
+}
+
+// Square/bondc.f:119-123, Triangular/bondc.f:121-125
+__host__ __device__ inline long long nbonds(const Geom& g) {
+  long long m = g.m, n = g.n;
+  if (g.lattice == kSquare) return g.pbc ? m * (2 * n - 1) : 2 * m * n - m - n;
+  return g.pbc ? m * (3 * n - 2) : 3 * m * n - 2 * m - 2 * n + 1;
+}
+
+__host__ __device__ inline void nearestn_square(const Geom& g, int rn, int* nn) {
+  const int m = g.m, t = g.t;
+  nn[0] = nn[1] = nn[2] = nn[3] = 0;
+  if (rn == 1) { nn[0] = rn + 1; nn[1] = rn + m; if (g.pbc) nn[2] = m; return; }
+  if (rn == m) { nn[0] = rn - 1; nn[1] = rn + m; if (g.pbc) nn[2] = 1; return; }
+  if (rn == t - (m - 1)) { nn[0] = rn - m; nn[1] = rn + 1; if (g.pbc) nn[2] = t; return; }
+  if (rn == t) { nn[0] = rn - m; nn[1] = rn - 1; if (g.pbc) nn[2] = rn - (m - 1); return; }
+  if (rn < m) { nn[0] = rn - 1; nn[1] = rn + 1; nn[2] = rn + m; return; }
+  if (rn > t - m) { nn[0] = rn - m; nn[1] = rn - 1; nn[2] = rn + 1; return; }
+  if ((rn - 1) % m == 0) {
+    nn[0] = rn - m; nn[1] = rn + 1; nn[2] = rn + m;
+    if (g.pbc) nn[3] = rn + (m - 1);
+    return;
+  }
+  if (rn % m == 0) {
+    nn[0] = rn - m; nn[1] = rn - 1; nn[2] = rn + m;
+    if (g.pbc) nn[3] = rn - (m - 1);
+    return;
+  }
+  nn[0] = rn - m; nn[1] = rn - 1; nn[2] = rn + 1; nn[3] = rn + m;
+}
+
+__host__ __device__ inline void nearestn_tri(const Geom& g, int rn, int* nn) {
+  const int m = g.m, t = g.t;
+  const bool odd_m = (m % 2) == 1;
+  for (int z = 0; z < 6; ++z) nn[z] = 0;
+  if (rn == 1) {
+    nn[0] = rn + 1; nn[1] = rn + m; nn[2] = rn + (m + 1);
+    if (g.pbc) { nn[3] = rn + (m - 1); nn[4] = rn + (2 * m - 1); }
+    return;
+  }
+  if (rn == m) {
+    nn[0] = rn - 1; nn[1] = rn + m;
+    if (odd_m) { nn[2] = rn + (m - 1); return; }
+    if (g.pbc) nn[2] = 1;
+    return;
+  }
+  if (rn == t - (m - 1)) {
+    nn[0] = rn - m; nn[1] = rn + 1;
+    if (g.pbc) nn[2] = t;
+    return;
+  }
+  if (rn == t) {
+    if (odd_m) { nn[0] = rn - m; nn[1] = rn - 1; return; }
+    nn[0] = rn - (m + 1); nn[1] = rn - m; nn[2] = rn - 1;
+    if (g.pbc) { nn[3] = rn - (2 * m - 1); nn[4] = rn - (m - 1); }
+    return;
+  }
+  if (rn < m) {  // bottom row
+    if (rn % 2 == 0) {
+      nn[0] = rn - 1; nn[1] = rn + 1; nn[2] = rn + m;
+    } else {
+      nn[0] = rn - 1; nn[1] = rn + 1; nn[2] = rn + (m - 1); nn[3] = rn + m; nn[4] = rn + (m + 1);
+    }
+    return;
+  }
+  if (rn > t - m) {  // top row
+    if (rn % 2 == 0) {
+      nn[0] = rn - (m + 1); nn[1] = rn - m; nn[2] = rn - (m - 1); nn[3] = rn - 1; nn[4] = rn + 1;
+    } else {
+      nn[0] = rn - m; nn[1] = rn - 1; nn[2] = rn + 1;
+    }
+    return;
+  }
+  if ((rn - 1) % m == 0) {  // left edge
+    nn[0] = rn - m; nn[1] = rn + 1; nn[2] = rn + m; nn[3] = rn + (m + 1);
+    if (g.pbc) { nn[4] = rn + (m - 1); nn[5] = rn + (2 * m - 1); }
+    return;
+  }
+  if (rn % m == 0) {  // right edge
+    if (odd_m) {
+      nn[0] = rn - m; nn[1] = rn - 1; nn[2] = rn + (m - 1); nn[3] = rn + m;
+      return;
+    }
+    nn[0] = rn - (m + 1); nn[1] = rn - m; nn[2] = rn - 1; nn[3] = rn + m;
+    if (g.pbc) { nn[4] = rn - (2 * m - 1); nn[5] = rn - (m - 1); }
+    return;
+  }
+  bool up;  // "up" form: rn-(m+1), rn-m, rn-(m-1), rn-1, rn+1, rn+m
+  if (odd_m) {
+    up = ((rn / m) % 2 == 0) ? (rn % 2 == 0) : (rn % 2 != 0);
+  } else {
+    up = (rn % 2 == 0);
+  }
+  if (up) {
+    nn[0] = rn - (m + 1); nn[1] = rn - m; nn[2] = rn - (m - 1);
+    nn[3] = rn - 1; nn[4] = rn + 1; nn[5] = rn + m;
+  } else {
+    nn[0] = rn - m; nn[1] = rn - 1; nn[2] = rn + 1;
+    nn[3] = rn + (m - 1); nn[4] = rn + m; nn[5] = rn + (m + 1);
+  }
+}
+
+__host__ __device__ inline void nearestn(const Geom& g, int rn, int* nn) {
+  if (g.lattice == kSquare) nearestn_square(g, rn, nn);
+  else nearestn_tri(g, rn, nn);
+}
+
+// Neighbours of rn sorted ascending (the dense-row scan order of G, used for
+// the diagonal row sum, Square/bondc.f:499-505, and by sprsin's column scan).
+// Returns the count; out[] holds up to 6 sites.
+__host__ __device__ inline int sorted_neighbours(const Geom& g, int rn, int* out) {
+  int nn[6];
+  nearestn(g, rn, nn);
+  int c = 0;
+  for (int k = 0; k < g.scn; ++k)
+    if (nn[k] != 0) {
+      int v = nn[k], j = c;
+      while (j > 0 && out[j - 1] > v) { out[j] = out[j - 1]; --j; }
+      out[j] = v;
+      ++c;
+    }
+  return c;
+}
+
+// Number of bonds whose smaller end is rn (bond list, Square/bondc.f:139-154)
+__host__ __device__ inline int forward_count(const Geom& g, int rn) {
+  int nn[6], c = 0;
+  nearestn(g, rn, nn);
+  for (int k = 0; k < g.scn; ++k) c += nn[k] > rn;
+  return c;
+}
+
+}  // namespace perc

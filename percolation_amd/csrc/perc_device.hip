@@ -1,0 +1,979 @@
+// perc_device.hip -- gfx950 kernels of libperc.
+//
+// Hot path (BASELINE.json north_star): cluster labeling of the occupancy
+// grid + Kirchhoff assembly + fused Jacobi-PCG whose SpMV is the roofline
+// kernel.  All floating-point elementwise work is written out in the
+// reference's operation order and compiled with -ffp-contract=off, so every
+// per-row value (SpMV rows, p, x, r, z updates, diagonal sums, currents) is
+// bitwise what Fortran/Square/bondc.f computes for the same inputs; only the
+// global dot products (reductions) are re-associated, deterministically
+// (fixed grid, fixed tree, last-arriving workgroup sums the partials in
+// index order).
+#include <hipcub/hipcub.hpp>
+
+#include "perc_internal.h"
+
+namespace perc {
+namespace {
+
+#define HIP_TRY(x)                          \
+  do {                                      \
+    hipError_t e_ = (x);                    \
+    if (e_ != hipSuccess) return e_;        \
+  } while (0)
+
+__host__ __device__ inline int cdiv(long long a, long long b) { return (int)((a + b - 1) / b); }
+
+// ---------------------------------------------------------------------------
+// XCD-aware logical block id: blocks b and b+8 share an XCD (round-robin
+// dispatch), so give each XCD a contiguous range of logical ids (bijective
+// for any grid, cdna_hip_programming.md T1).  Speed only, never correctness.
+__device__ __forceinline__ int xcd_logical_block(int b, int nwg) {
+  const int xcd = b % 8, q = nwg / 8, r = nwg % 8;
+  const int base = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
+  return base + b / 8;
+}
+
+// ---------------------------------------------------------------------------
+// Deterministic reductions.  Wave64 butterfly, then 4 waves through LDS in
+// wave order.  Partial of each workgroup stored write-through (sc1), drained,
+// then one agent-scope ticket add; the workgroup drawing the last ticket sums
+// all partials in index order (cdna_hip_programming.md §6 Guideline 16, the
+// counter form with sc1 payload).
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v = v + __shfl_xor(v, off, 64);
+  return v;
+}
+
+template <int NV>
+__device__ __forceinline__ void block_sum(double (&v)[NV], double* s_red /*4*NV*/) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+#pragma unroll
+  for (int j = 0; j < NV; ++j) {
+    double w = wave_sum(v[j]);
+    if (lane == 0) s_red[wid * NV + j] = w;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+#pragma unroll
+    for (int j = 0; j < NV; ++j)
+      v[j] = ((s_red[0 * NV + j] + s_red[1 * NV + j]) + s_red[2 * NV + j]) + s_red[3 * NV + j];
+  }
+}
+
+__device__ __forceinline__ void store_sc1(double* p, double v) {
+  __hip_atomic_store(reinterpret_cast<unsigned long long*>(p), __double_as_longlong(v),
+                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double load_sc1(const double* p) {
+  return __longlong_as_double(__hip_atomic_load(
+      reinterpret_cast<unsigned long long*>(const_cast<double*>(p)), __ATOMIC_RELAXED,
+      __HIP_MEMORY_SCOPE_AGENT));
+}
+
+// Publish this workgroup's NV partials at partials[j*nwg + lb]; returns true
+// in every thread of the last-arriving workgroup, which then holds the totals
+// in tot[] (all threads).  Must be called by all threads of the workgroup.
+template <int NV>
+__device__ bool publish_and_reduce(double (&v)[NV], double* partials, unsigned* ticket, int lb,
+                                   int nwg, double (&tot)[NV], double* s_red, int* s_flag) {
+  block_sum<NV>(v, s_red);
+  if (threadIdx.x == 0) {
+#pragma unroll
+    for (int j = 0; j < NV; ++j) store_sc1(&partials[j * nwg + lb], v[j]);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    unsigned tk = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    *s_flag = (tk == (unsigned)(nwg - 1));
+  }
+  __syncthreads();
+  if (!*s_flag) return false;
+  // last arriver: every thread sums a fixed strided subset in index order
+  double acc[NV];
+#pragma unroll
+  for (int j = 0; j < NV; ++j) acc[j] = 0.0;
+  for (int i = threadIdx.x; i < nwg; i += blockDim.x) {
+#pragma unroll
+    for (int j = 0; j < NV; ++j) acc[j] = acc[j] + load_sc1(&partials[j * nwg + i]);
+  }
+  __syncthreads();  // s_red reuse
+  block_sum<NV>(acc, s_red);
+  if (threadIdx.x == 0) {
+#pragma unroll
+    for (int j = 0; j < NV; ++j) s_red[16 + j] = acc[j];
+    __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < NV; ++j) tot[j] = s_red[16 + j];
+  return true;
+}
+
+// ---------------------------------------------------------------------------
+// Lattice build
+__global__ void k_forward_count(Geom g, int* fc /* t+2 */) {
+  const long long s = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (s > g.t + 1) return;
+  fc[s] = (s >= 1 && s <= g.t - 1) ? forward_count(g, (int)s) : 0;
+}
+
+__device__ __forceinline__ int bond_id(const Geom& g, const int* bond_first, int p, int q) {
+  // p < q; bond-list index of (p,q) or -1
+  int nn[6];
+  nearestn(g, p, nn);
+  int r = 0;
+  for (int k = 0; k < g.scn; ++k)
+    if (nn[k] > p) {
+      if (nn[k] == q) return bond_first[p] + r;
+      ++r;
+    }
+  return -1;
+}
+
+__global__ void k_row_count(Geom g, int N, int* rc /* N+1 */) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i > N) return;
+  if (i == N) { rc[N] = 0; return; }
+  const int s = i + g.m + 1;
+  int nbr[6];
+  const int c = sorted_neighbours(g, s, nbr);
+  int cnt = 0;
+  for (int j = 0; j < c; ++j) cnt += (nbr[j] > g.m && nbr[j] <= g.t - g.m);
+  rc[i] = cnt;
+}
+
+__global__ void k_fill_col(Geom g, int N, const int* rowptr, int* col) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= N) return;
+  const int s = i + g.m + 1;
+  int nbr[6];
+  const int c = sorted_neighbours(g, s, nbr);
+  int k = rowptr[i];
+  for (int j = 0; j < c; ++j)
+    if (nbr[j] > g.m && nbr[j] <= g.t - g.m) col[k++] = nbr[j] - g.m - 1;
+}
+
+// ---------------------------------------------------------------------------
+// Occupancy
+__global__ void k_occupy(const int* order, int count, long long limit, uint8_t* occ) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= count) return;
+  const int id = order[k];
+  if (id > 0 && id <= limit) occ[id - 1] = 1;
+}
+__global__ void k_occupy_sites(const int* order, int count, int t, uint8_t* socc) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= count) return;
+  const int id = order[k];
+  if (id > 0 && id <= t) socc[id] = 1;
+}
+
+// ---------------------------------------------------------------------------
+// Connected components: lock-free union-find, roots always linked larger ->
+// smaller, so the final root of a component is its minimum site id (a
+// canonical, schedule-independent partition).  Path halving; stale L1 reads
+// only cost retries (parents only move to smaller ancestors).
+__device__ __forceinline__ int find_root(int* parent, int x) {
+  int p = parent[x];
+  while (p != x) {
+    const int gp = parent[p];
+    if (gp != p) parent[x] = gp;
+    x = gp;
+    p = parent[x];
+  }
+  return x;
+}
+
+__device__ __forceinline__ void unite(int* parent, int a, int b) {
+  while (true) {
+    a = find_root(parent, a);
+    b = find_root(parent, b);
+    if (a == b) return;
+    if (a < b) { const int tmp = a; a = b; b = tmp; }
+    const int old = atomicCAS(&parent[a], a, b);
+    if (old == a) return;
+    a = old;
+  }
+}
+
+__global__ void k_cc_init(int t, int* parent, uint8_t* member, uint8_t* bot, uint8_t* top) {
+  const long long s = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (s > t) return;
+  parent[s] = (int)s;
+  member[s] = 0;
+  bot[s] = 0;
+  top[s] = 0;
+}
+
+__global__ void k_cc_hook(Geom g, int kind, const int* bond_first, const uint8_t* bocc,
+                          const uint8_t* socc, int* parent, uint8_t* member) {
+  const int s = blockIdx.x * blockDim.x + threadIdx.x + 1;
+  if (s > g.t) return;
+  if (kind != PERC_BOND && socc[s]) member[s] = 1;
+  if (s > g.t - 1) return;
+  int nn[6];
+  nearestn(g, s, nn);
+  const int fb = bond_first[s];
+  int r = 0;
+  for (int k = 0; k < g.scn; ++k) {
+    const int q = nn[k];
+    if (q <= s) continue;
+    bool link;
+    if (kind == PERC_BOND) link = bocc[fb + r];
+    else if (kind == PERC_SITE) link = socc[s] && socc[q];
+    else link = bocc[fb + r] && socc[s] && socc[q];
+    ++r;
+    if (link) {
+      if (kind == PERC_BOND) { member[s] = 1; member[q] = 1; }
+      unite(parent, s, q);
+    }
+  }
+}
+
+__global__ void k_cc_compress(int t, int* parent) {
+  const int s = blockIdx.x * blockDim.x + threadIdx.x + 1;
+  if (s > t) return;
+  parent[s] = find_root(parent, s);
+}
+
+// spanning flags at roots: bottom row (sites 1..m) / top row (t-m+1..t)
+__global__ void k_span_flags(Geom g, int kind, const int* bond_first, const uint8_t* bocc,
+                             const uint8_t* socc, const int* parent, uint8_t* bot, uint8_t* top) {
+  const int s = blockIdx.x * blockDim.x + threadIdx.x + 1;
+  if (s > g.t) return;
+  if (kind == PERC_BOND) {
+    // bondc.f:419-441: a bond with b1 <= m, and one with b2 > t-m
+    if (s > g.t - 1) return;
+    int nn[6];
+    nearestn(g, s, nn);
+    const int fb = bond_first[s];
+    int r = 0;
+    for (int k = 0; k < g.scn; ++k) {
+      const int q = nn[k];
+      if (q <= s) continue;
+      if (bocc[fb + r]) {
+        if (s <= g.m) bot[parent[s]] = 1;
+        if (q > g.t - g.m) top[parent[q]] = 1;
+      }
+      ++r;
+    }
+  } else {
+    // site.f:319-333: an occupied site in the bottom and in the top row
+    if (!socc[s]) return;
+    if (s <= g.m) bot[parent[s]] = 1;
+    if (s > g.t - g.m) top[parent[s]] = 1;
+  }
+}
+
+__global__ void k_span_collect(int t, const int* parent, const uint8_t* member,
+                               const uint8_t* bot, const uint8_t* top, int* counters) {
+  const int s = blockIdx.x * blockDim.x + threadIdx.x + 1;
+  if (s > t) return;
+  if (!member[s] || parent[s] != s) return;
+  atomicAdd(&counters[1], 1);
+  if (bot[s] && top[s]) {
+    const int idx = atomicAdd(&counters[0], 1);
+    if (idx < kMaxSpanList) counters[8 + idx] = s;
+  }
+}
+
+__global__ void k_count_root(int t, const int* parent, const uint8_t* member, int root,
+                             int* counter) {
+  const int s = blockIdx.x * blockDim.x + threadIdx.x + 1;
+  if (s > t) return;
+  const bool in = member[s] && parent[s] == root;
+  const unsigned long long b = __ballot(in);
+  if ((threadIdx.x & 63) == 0 && b) atomicAdd(counter, __popcll(b));
+}
+
+__global__ void k_canon(int t, const int* parent, const uint8_t* member, int* canon) {
+  const int s = blockIdx.x * blockDim.x + threadIdx.x + 1;
+  if (s > t) return;
+  canon[s - 1] = member[s] ? parent[s] : 0;
+}
+
+// ---------------------------------------------------------------------------
+// Kirchhoff assembly (bondc.f:482-538, ConductCalc.m:88-165)
+__device__ __forceinline__ double bond_value(int rule, int id, int s, int c, int ps,
+                                             const uint8_t* bocc, const uint8_t* socc,
+                                             int span_root, double g0, double leak) {
+  bool in;
+  if (rule == PERC_RULE_BOND) in = bocc[id] && ps == span_root;
+  else if (rule == PERC_RULE_SITE) in = socc[s] && socc[c] && ps == span_root;
+  else in = bocc[id] && socc[s] && socc[c] && ps == span_root;
+  return in ? -g0 : -leak;
+}
+
+__global__ void k_assemble(Geom g, int N, const int* bond_first, const uint8_t* bocc,
+                           const uint8_t* socc, const int* parent, const int* rowptr,
+                           double* val, double* diag, double* rhs, int rule, double g0,
+                           double leak, double Va, int span_root) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= N) return;
+  const int m = g.m, t = g.t, s = i + m + 1;
+  const int ps = parent[s];
+  int nbr[6];
+  const int cnt = sorted_neighbours(g, s, nbr);
+  double rowsum = 0.0;  // bondc.f:500-504: ascending-column dense row sum
+  int k = rowptr[i];
+  for (int j = 0; j < cnt; ++j) {
+    const int c = nbr[j];
+    const int id = s < c ? bond_id(g, bond_first, s, c) : bond_id(g, bond_first, c, s);
+    if (id < 0) continue;
+    const double gv = bond_value(rule, id, s, c, ps, bocc, socc, span_root, g0, leak);
+    rowsum = rowsum + gv;
+    if (c > m && c <= t - m) val[k++] = gv;
+  }
+  diag[i] = -rowsum;
+  // RHS in bond-list order (bondc.f:490-497)
+  double acc = 0.0;
+  if (s > t - 2 * m && s <= t - m) {
+    int nn[6];
+    nearestn(g, s, nn);
+    const int fb = bond_first[s];
+    int r = 0;
+    for (int kk = 0; kk < g.scn; ++kk) {
+      const int q = nn[kk];
+      if (q <= s) continue;
+      if (q > t - m) {
+        const double gv = bond_value(rule, fb + r, s, q, ps, bocc, socc, span_root, g0, leak);
+        acc = acc - (gv * Va);
+      }
+      ++r;
+    }
+  }
+  rhs[i] = acc;
+}
+
+// Terminal currents of the 2m boundary rows (bondc.f:554-592; ConductCalc.m:188)
+__global__ void k_currents(Geom g, const int* bond_first, const uint8_t* bocc,
+                           const uint8_t* socc, const int* parent, const double* x, int rule,
+                           int cur_rule, double g0, double leak, double Va, int span_root,
+                           double thresh, double* iout) {
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  const int m = g.m, t = g.t;
+  if (idx >= 2 * m) return;
+  const int s = idx < m ? idx + 1 : t - m + 1 + (idx - m);
+  const int ps = parent[s];
+  int nbr[6];
+  const int cnt = sorted_neighbours(g, s, nbr);
+  double gv[6];
+  double rowsum = 0.0;
+  for (int j = 0; j < cnt; ++j) {
+    const int c = nbr[j];
+    const int id = s < c ? bond_id(g, bond_first, s, c) : bond_id(g, bond_first, c, s);
+    gv[j] = id < 0 ? 0.0 : bond_value(rule, id, s, c, ps, bocc, socc, span_root, g0, leak);
+    rowsum = rowsum + gv[j];
+  }
+  const double d = -rowsum;
+  auto V = [&](int c) -> double { return c <= m ? 0.0 : (c > t - m ? Va : x[c - m - 1]); };
+  double acc;
+  if (cur_rule == PERC_CUR_FORTRAN) {
+    acc = d * V(s);
+    for (int j = 0; j < cnt; ++j)
+      if (fabs(gv[j]) >= thresh) acc = acc + gv[j] * V(nbr[j]);
+  } else {
+    acc = 0.0;
+    bool done = false;
+    for (int j = 0; j < cnt; ++j) {
+      if (!done && nbr[j] > s) { acc = acc + d * V(s); done = true; }
+      acc = acc + gv[j] * V(nbr[j]);
+    }
+    if (!done) acc = acc + d * V(s);
+  }
+  iout[idx] = acc;
+}
+
+// ---------------------------------------------------------------------------
+// CSR SpMV, rows staged through LDS.  y(i) = d(i)*x(i) + sum_k val*x(col) in
+// ascending column order (dsprsax, bondc.f:887-899).
+struct CsrView {
+  int N;
+  const int* rowptr;
+  const int* col;
+  const double* val;
+  const double* diag;
+};
+
+constexpr int kMaxNnzRow = 6;
+
+__global__ __launch_bounds__(kBlock) void k_spmv(CsrView A, const double* __restrict__ x,
+                                                 double* __restrict__ y) {
+  __shared__ int s_ptr[kRowsPerTile + 1];
+  __shared__ int s_col[kRowsPerTile * kMaxNnzRow];
+  __shared__ double s_val[kRowsPerTile * kMaxNnzRow];
+  const int tid = threadIdx.x;
+  const int nrb = cdiv(A.N, kRowsPerTile);
+  const int lb = xcd_logical_block(blockIdx.x, gridDim.x);
+  const int chunk = cdiv(nrb, gridDim.x);
+  const int rb0 = lb * chunk, rb1 = min(rb0 + chunk, nrb);
+  for (int rb = rb0; rb < rb1; ++rb) {
+    const int r0 = rb * kRowsPerTile, nr = min(kRowsPerTile, A.N - r0);
+    if (tid <= nr) s_ptr[tid] = A.rowptr[r0 + tid];
+    __syncthreads();
+    const int e0 = s_ptr[0], ne = s_ptr[nr] - e0;
+    // tiles wider than the LDS stage (rows with > kMaxNnzRow entries, e.g. a
+    // general NR matrix) are read straight from global memory
+    const bool staged = ne <= kRowsPerTile * kMaxNnzRow;
+    if (staged)
+      for (int j = tid; j < ne; j += kBlock) {
+        s_col[j] = A.col[e0 + j];
+        s_val[j] = A.val[e0 + j];
+      }
+    __syncthreads();
+    const int* cc = staged ? s_col : A.col + e0;
+    const double* vv = staged ? s_val : A.val + e0;
+    if (tid < nr) {
+      const int i = r0 + tid;
+      double acc = A.diag[i] * x[i];
+      const int a = s_ptr[tid] - e0, b = s_ptr[tid + 1] - e0;
+      for (int j = a; j < b; ++j) acc = acc + vv[j] * x[cc[j]];
+      y[i] = acc;
+    }
+    __syncthreads();
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Fused PCG kernels.  One linbcg iteration (bondc.f:780-835, symmetric A so
+// rr==r, pp==p, zz==z, dsprstx==dsprsax bitwise) is two launches:
+//   A: p = bk*p + r/d (p = r/d on iteration 1); q = A p; akden = q.p
+//   B: x += ak p; r -= ak q; z = r/d; bknum' = z.r; err = ||r||/bnrm
+// Scalars and the stop flag live on the device, so a fixed sequence of
+// launches (or a captured graph) runs any number of iterations; launches
+// after convergence return immediately.
+struct CGArgs {
+  CsrView A;
+  const double* rhs;
+  double* x;
+  double* r;
+  double* p0;
+  double* p1;
+  double* q;
+  double* partials;
+  unsigned* tickets;
+  CGScalars* S;
+  double* err_hist;
+  int err_hist_cap;
+};
+
+__global__ __launch_bounds__(kBlock) void k_cg_spmv(CGArgs a) {
+  __shared__ int s_ptr[kRowsPerTile + 1];
+  __shared__ int s_col[kRowsPerTile * kMaxNnzRow];
+  __shared__ double s_val[kRowsPerTile * kMaxNnzRow];
+  __shared__ double s_red[32];
+  __shared__ int s_flag;
+  CGScalars* S = a.S;
+  if (S->done) return;
+  const int k = S->iter + 1;
+  const bool first = k == 1;
+  const double bk = first ? 0.0 : S->bknum / S->bkden;
+  const double* __restrict__ pold = (k & 1) ? a.p1 : a.p0;
+  double* __restrict__ pnew = (k & 1) ? a.p0 : a.p1;
+  const double* __restrict__ r = a.r;
+  const double* __restrict__ d = a.A.diag;
+  const int N = a.A.N, tid = threadIdx.x;
+  const int nrb = cdiv(N, kRowsPerTile);
+  const int lb = xcd_logical_block(blockIdx.x, gridDim.x);
+  const int chunk = cdiv(nrb, gridDim.x);
+  const int rb0 = lb * chunk, rb1 = min(rb0 + chunk, nrb);
+  double dot[1] = {0.0};
+  for (int rb = rb0; rb < rb1; ++rb) {
+    const int r0 = rb * kRowsPerTile, nr = min(kRowsPerTile, N - r0);
+    if (tid <= nr) s_ptr[tid] = a.A.rowptr[r0 + tid];
+    __syncthreads();
+    const int e0 = s_ptr[0], ne = s_ptr[nr] - e0;
+    const bool staged = ne <= kRowsPerTile * kMaxNnzRow;
+    if (staged)
+      for (int j = tid; j < ne; j += kBlock) {
+        s_col[j] = a.A.col[e0 + j];
+        s_val[j] = a.A.val[e0 + j];
+      }
+    __syncthreads();
+    const int* cc = staged ? s_col : a.A.col + e0;
+    const double* vv = staged ? s_val : a.A.val + e0;
+    if (tid < nr) {
+      const int i = r0 + tid;
+      const double di = d[i];
+      const double zi = r[i] / di;
+      const double pi = first ? zi : bk * pold[i] + zi;
+      pnew[i] = pi;
+      double acc = di * pi;
+      const int e = s_ptr[tid + 1] - e0;
+      for (int j = s_ptr[tid] - e0; j < e; ++j) {
+        const int c = cc[j];
+        const double zc = r[c] / d[c];
+        const double pc = first ? zc : bk * pold[c] + zc;
+        acc = acc + vv[j] * pc;
+      }
+      a.q[i] = acc;
+      dot[0] = dot[0] + acc * pi;
+    }
+    __syncthreads();
+  }
+  double tot[1];
+  if (publish_and_reduce<1>(dot, a.partials, &a.tickets[0], lb, gridDim.x, tot, s_red, &s_flag)) {
+    if (tid == 0) {
+      const double bknum = S->bknum;
+      S->akden = tot[0];
+      S->ak = bknum / tot[0];
+      S->bkden = bknum;
+    }
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void k_cg_update(CGArgs a) {
+  __shared__ double s_red[32];
+  __shared__ int s_flag;
+  CGScalars* S = a.S;
+  if (S->done) return;
+  const int k = S->iter + 1;
+  const double* __restrict__ p = (k & 1) ? a.p0 : a.p1;
+  const double* __restrict__ q = a.q;
+  const double* __restrict__ d = a.A.diag;
+  double* __restrict__ x = a.x;
+  double* __restrict__ r = a.r;
+  const double ak = S->ak;
+  const int N = a.A.N;
+  const int lb = xcd_logical_block(blockIdx.x, gridDim.x);
+  // contiguous, even-aligned chunk per logical block; pairs via 16 B loads
+  const int npair = (N + 1) / 2;
+  const int chunk = cdiv(npair, gridDim.x);
+  const int q0 = lb * chunk, q1 = min(q0 + chunk, npair);
+  double acc[2] = {0.0, 0.0};  // z.r, r.r
+  for (int j = q0 + threadIdx.x; j < q1; j += kBlock) {
+    const int i = 2 * j;
+    if (i + 1 < N) {
+      const double2 xv = *reinterpret_cast<const double2*>(x + i);
+      const double2 pv = *reinterpret_cast<const double2*>(p + i);
+      const double2 qv = *reinterpret_cast<const double2*>(q + i);
+      const double2 rv = *reinterpret_cast<const double2*>(r + i);
+      const double2 dv = *reinterpret_cast<const double2*>(d + i);
+      double2 xn, rn;
+      xn.x = xv.x + ak * pv.x;
+      xn.y = xv.y + ak * pv.y;
+      rn.x = rv.x - ak * qv.x;
+      rn.y = rv.y - ak * qv.y;
+      *reinterpret_cast<double2*>(x + i) = xn;
+      *reinterpret_cast<double2*>(r + i) = rn;
+      const double z0 = rn.x / dv.x, z1 = rn.y / dv.y;
+      acc[0] = acc[0] + z0 * rn.x;
+      acc[0] = acc[0] + z1 * rn.y;
+      acc[1] = acc[1] + rn.x * rn.x;
+      acc[1] = acc[1] + rn.y * rn.y;
+    } else {
+      const double xn = x[i] + ak * p[i];
+      const double rn = r[i] - ak * q[i];
+      x[i] = xn;
+      r[i] = rn;
+      const double z0 = rn / d[i];
+      acc[0] = acc[0] + z0 * rn;
+      acc[1] = acc[1] + rn * rn;
+    }
+  }
+  double tot[2];
+  if (publish_and_reduce<2>(acc, a.partials + 2 * (size_t)gridDim.x, &a.tickets[1], lb, gridDim.x,
+                            tot, s_red, &s_flag)) {
+    if (threadIdx.x == 0) {
+      const double err = sqrt(tot[1]) / S->bnrm;
+      S->bknum = tot[0];
+      S->err = err;
+      if (k - 1 < a.err_hist_cap) a.err_hist[k - 1] = err;
+      S->iter = k;
+      if (!(err > S->tol) || k >= S->itmax + 1) S->done = 1;
+    }
+  }
+}
+
+// r = b - A x (or r = b when x = 0), then bnrm and the first bknum
+// (linbcg prologue, bondc.f:758-779)
+__global__ __launch_bounds__(kBlock) void k_cg_init(CGArgs a, int itol, int x0_zero) {
+  __shared__ double s_red[32];
+  __shared__ int s_flag;
+  const double* __restrict__ b = a.rhs;
+  const double* __restrict__ d = a.A.diag;
+  const int N = a.A.N;
+  const int lb = xcd_logical_block(blockIdx.x, gridDim.x);
+  const int chunk = cdiv(N, gridDim.x);
+  const int i0 = lb * chunk, i1 = min(i0 + chunk, N);
+  double acc[2] = {0.0, 0.0};  // bnrm^2, z.r
+  for (int i = i0 + threadIdx.x; i < i1; i += kBlock) {
+    double ax = 0.0;
+    if (!x0_zero) {
+      const double* x = a.x;
+      ax = d[i] * x[i];
+      for (int j = a.A.rowptr[i]; j < a.A.rowptr[i + 1]; ++j) ax = ax + a.A.val[j] * x[a.A.col[j]];
+    }
+    const double ri = b[i] - ax;
+    a.r[i] = ri;
+    const double zb = itol == 1 ? b[i] : b[i] / d[i];
+    acc[0] = acc[0] + zb * zb;
+    const double zr = ri / d[i];
+    acc[1] = acc[1] + zr * ri;
+  }
+  double tot[2];
+  if (publish_and_reduce<2>(acc, a.partials, &a.tickets[2], lb, gridDim.x, tot, s_red, &s_flag)) {
+    if (threadIdx.x == 0) {
+      a.S->bnrm = sqrt(tot[0]);
+      a.S->bknum = tot[1];
+      a.S->bkden = 1.0;
+      a.S->iter = 0;
+      a.S->done = 0;
+    }
+  }
+}
+
+__global__ void k_zero(double* v, long long n) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) v[i] = 0.0;
+}
+
+CGArgs make_cg_args(perc_ctx* h) {
+  CGArgs a;
+  a.A = CsrView{h->N, h->d.rowptr, h->d.col, h->d.val, h->d.diag};
+  a.rhs = h->d.rhs;
+  a.x = h->d.x;
+  a.r = h->d.r;
+  a.p0 = h->d.p0;
+  a.p1 = h->d.p1;
+  a.q = h->d.q;
+  a.partials = h->d.partials;
+  a.tickets = h->d.tickets;
+  a.S = h->d.scal;
+  a.err_hist = h->d.err_hist;
+  a.err_hist_cap = h->d.err_hist_cap;
+  return a;
+}
+
+inline dim3 blocks_for(long long n) { return dim3((unsigned)((n + kBlock - 1) / kBlock)); }
+
+template <typename T>
+hipError_t dmalloc(T** p, size_t n) {
+  return hipMalloc(reinterpret_cast<void**>(p), sizeof(T) * (n ? n : 1));
+}
+
+hipError_t exclusive_scan(const int* in, int* out, int n, hipStream_t st) {
+  size_t bytes = 0;
+  HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, bytes, in, out, n, st));
+  void* tmp = nullptr;
+  HIP_TRY(hipMalloc(&tmp, bytes ? bytes : 1));
+  hipError_t e = hipcub::DeviceScan::ExclusiveSum(tmp, bytes, in, out, n, st);
+  hipError_t e2 = hipStreamSynchronize(st);
+  hipFree(tmp);
+  return e != hipSuccess ? e : e2;
+}
+
+}  // namespace
+
+// ===========================================================================
+hipError_t dev_build_lattice(perc_ctx* h) {
+  const Geom& g = h->g;
+  const int t = g.t, N = h->N;
+  hipStream_t st = h->stream;
+  DeviceBuffers& d = h->d;
+  // bond_first
+  int* fc = nullptr;
+  HIP_TRY(dmalloc(&fc, t + 2));
+  HIP_TRY(dmalloc(&d.bond_first, t + 2));
+  k_forward_count<<<blocks_for(t + 2), kBlock, 0, st>>>(g, fc);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(exclusive_scan(fc, d.bond_first, t + 2, st));
+  HIP_TRY(hipFree(fc));
+  h->h_bond_first.resize(t + 2);
+  HIP_TRY(hipMemcpy(h->h_bond_first.data(), d.bond_first, sizeof(int) * (t + 2),
+                    hipMemcpyDeviceToHost));
+  // CSR pattern of the interior block
+  int* rc = nullptr;
+  HIP_TRY(dmalloc(&rc, N + 1));
+  HIP_TRY(dmalloc(&d.rowptr, N + 1));
+  k_row_count<<<blocks_for(N + 1), kBlock, 0, st>>>(g, N, rc);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(exclusive_scan(rc, d.rowptr, N + 1, st));
+  HIP_TRY(hipFree(rc));
+  int nnz = 0;
+  HIP_TRY(hipMemcpy(&nnz, d.rowptr + N, sizeof(int), hipMemcpyDeviceToHost));
+  h->nnz = nnz;
+  HIP_TRY(dmalloc(&d.col, (size_t)nnz + 8));
+  HIP_TRY(dmalloc(&d.val, (size_t)nnz + 8));
+  k_fill_col<<<blocks_for(N), kBlock, 0, st>>>(g, N, d.rowptr, d.col);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(dmalloc(&d.diag, N + 2));
+  HIP_TRY(dmalloc(&d.rhs, N + 2));
+  // occupancy + labeling
+  HIP_TRY(dmalloc(&d.bocc, (size_t)h->nb + 8));
+  HIP_TRY(dmalloc(&d.socc, t + 8));
+  HIP_TRY(dmalloc(&d.order, (size_t)std::max<long long>(h->nb, t) + 8));
+  HIP_TRY(dmalloc(&d.parent, t + 8));
+  HIP_TRY(dmalloc(&d.member, t + 8));
+  HIP_TRY(dmalloc(&d.bot, t + 8));
+  HIP_TRY(dmalloc(&d.top, t + 8));
+  HIP_TRY(dmalloc(&d.counters, 8 + kMaxSpanList));
+  // CG (vectors padded to even length for the 16 B paths)
+  const size_t nv = (size_t)N + 2;
+  HIP_TRY(dmalloc(&d.x, nv));
+  HIP_TRY(dmalloc(&d.r, nv));
+  HIP_TRY(dmalloc(&d.p0, nv));
+  HIP_TRY(dmalloc(&d.p1, nv));
+  HIP_TRY(dmalloc(&d.q, nv));
+  const int nrb = cdiv(N, kRowsPerTile);
+  h->grid = std::max(1, std::min(nrb, 2048));
+  HIP_TRY(dmalloc(&d.partials, 4 * (size_t)h->grid));
+  HIP_TRY(dmalloc(&d.tickets, 8));
+  HIP_TRY(hipMemset(d.tickets, 0, 8 * sizeof(unsigned)));
+  HIP_TRY(dmalloc(&d.scal, 1));
+  HIP_TRY(dmalloc(&d.iout, 2 * (size_t)g.m));
+  HIP_TRY(hipMemset(d.bocc, 0, (size_t)h->nb + 8));
+  HIP_TRY(hipMemset(d.socc, 0, t + 8));
+  return hipStreamSynchronize(st);
+}
+
+hipError_t dev_alloc_matrix(perc_ctx* h, int N, long long nnz) {
+  DeviceBuffers& d = h->d;
+  h->N = N;
+  h->nnz = nnz;
+  HIP_TRY(dmalloc(&d.rowptr, N + 1));
+  HIP_TRY(dmalloc(&d.col, (size_t)nnz + 8));
+  HIP_TRY(dmalloc(&d.val, (size_t)nnz + 8));
+  HIP_TRY(dmalloc(&d.diag, N + 2));
+  HIP_TRY(dmalloc(&d.rhs, N + 2));
+  const size_t nv = (size_t)N + 2;
+  HIP_TRY(dmalloc(&d.x, nv));
+  HIP_TRY(dmalloc(&d.r, nv));
+  HIP_TRY(dmalloc(&d.p0, nv));
+  HIP_TRY(dmalloc(&d.p1, nv));
+  HIP_TRY(dmalloc(&d.q, nv));
+  h->grid = std::max(1, std::min(cdiv(N, kRowsPerTile), 2048));
+  HIP_TRY(dmalloc(&d.partials, 4 * (size_t)h->grid));
+  HIP_TRY(dmalloc(&d.tickets, 8));
+  HIP_TRY(hipMemset(d.tickets, 0, 8 * sizeof(unsigned)));
+  HIP_TRY(dmalloc(&d.scal, 1));
+  return hipSuccess;
+}
+
+void dev_free_all(perc_ctx* h) {
+  DeviceBuffers& d = h->d;
+  void* ptrs[] = {d.bond_first, d.rowptr, d.col, d.val, d.diag, d.rhs, d.bocc, d.socc,
+                  d.order, d.parent, d.member, d.bot, d.top, d.counters, d.x, d.r,
+                  d.p0, d.p1, d.q, d.partials, d.tickets, d.scal, d.err_hist, d.iout};
+  for (void* p : ptrs)
+    if (p) hipFree(p);
+  d = DeviceBuffers{};
+  h->N = 0;
+  h->nnz = 0;
+}
+
+hipError_t dev_occupy(perc_ctx* h, int kind, int nsites, const int* site_order, int nbonds,
+                      const int* bond_order, bool device_src) {
+  hipStream_t st = h->stream;
+  DeviceBuffers& d = h->d;
+  HIP_TRY(hipMemsetAsync(d.bocc, 0, (size_t)h->nb + 8, st));
+  HIP_TRY(hipMemsetAsync(d.socc, 0, h->g.t + 8, st));
+  if (kind != PERC_BOND && nsites > 0) {
+    const int* src = site_order;
+    if (!device_src) {
+      HIP_TRY(hipMemcpyAsync(d.order, site_order, sizeof(int) * nsites, hipMemcpyHostToDevice, st));
+      src = d.order;
+    }
+    k_occupy_sites<<<blocks_for(nsites), kBlock, 0, st>>>(src, nsites, h->g.t, d.socc);
+    HIP_TRY(hipGetLastError());
+  }
+  if (kind != PERC_SITE && nbonds > 0) {
+    const int* src = bond_order;
+    if (!device_src) {
+      HIP_TRY(hipMemcpyAsync(d.order, bond_order, sizeof(int) * nbonds, hipMemcpyHostToDevice, st));
+      src = d.order;
+    }
+    k_occupy<<<blocks_for(nbonds), kBlock, 0, st>>>(src, nbonds, h->nb, d.bocc);
+    HIP_TRY(hipGetLastError());
+  }
+  return hipSuccess;
+}
+
+hipError_t dev_label(perc_ctx* h, int* nspan, int* span_list, int* nclusters) {
+  const Geom& g = h->g;
+  hipStream_t st = h->stream;
+  DeviceBuffers& d = h->d;
+  const int kind = h->last.kind;
+  k_cc_init<<<blocks_for(g.t + 1), kBlock, 0, st>>>(g.t, d.parent, d.member, d.bot, d.top);
+  k_cc_hook<<<blocks_for(g.t), kBlock, 0, st>>>(g, kind, d.bond_first, d.bocc, d.socc, d.parent,
+                                                 d.member);
+  k_cc_compress<<<blocks_for(g.t), kBlock, 0, st>>>(g.t, d.parent);
+  k_span_flags<<<blocks_for(g.t), kBlock, 0, st>>>(g, kind, d.bond_first, d.bocc, d.socc,
+                                                    d.parent, d.bot, d.top);
+  HIP_TRY(hipMemsetAsync(d.counters, 0, sizeof(int) * (8 + kMaxSpanList), st));
+  k_span_collect<<<blocks_for(g.t), kBlock, 0, st>>>(g.t, d.parent, d.member, d.bot, d.top,
+                                                      d.counters);
+  HIP_TRY(hipGetLastError());
+  int hc[8 + kMaxSpanList];
+  HIP_TRY(hipMemcpyAsync(hc, d.counters, sizeof(hc), hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipStreamSynchronize(st));
+  *nspan = hc[0];
+  *nclusters = hc[1];
+  for (int i = 0; i < std::min(hc[0], kMaxSpanList); ++i) span_list[i] = hc[8 + i];
+  return hipSuccess;
+}
+
+hipError_t dev_span_sites(perc_ctx* h, int root, int* count) {
+  hipStream_t st = h->stream;
+  HIP_TRY(hipMemsetAsync(h->d.counters + 2, 0, sizeof(int), st));
+  k_count_root<<<blocks_for(h->g.t), kBlock, 0, st>>>(h->g.t, h->d.parent, h->d.member, root,
+                                                       h->d.counters + 2);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipMemcpyAsync(count, h->d.counters + 2, sizeof(int), hipMemcpyDeviceToHost, st));
+  return hipStreamSynchronize(st);
+}
+
+hipError_t dev_canon(perc_ctx* h, int* canon_out) {
+  hipStream_t st = h->stream;
+  int* tmp = nullptr;
+  HIP_TRY(dmalloc(&tmp, h->g.t));
+  k_canon<<<blocks_for(h->g.t), kBlock, 0, st>>>(h->g.t, h->d.parent, h->d.member, tmp);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipMemcpyAsync(canon_out, tmp, sizeof(int) * h->g.t, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipStreamSynchronize(st));
+  return hipFree(tmp);
+}
+
+hipError_t dev_assemble(perc_ctx* h, int rule, double g0, double leak, double Va, int span_root) {
+  DeviceBuffers& d = h->d;
+  k_assemble<<<blocks_for(h->N), kBlock, 0, h->stream>>>(h->g, h->N, d.bond_first, d.bocc, d.socc,
+                                                          d.parent, d.rowptr, d.val, d.diag, d.rhs,
+                                                          rule, g0, leak, Va, span_root);
+  return hipGetLastError();
+}
+
+hipError_t dev_solve(perc_ctx* h, int itol, double tol, int itmax, bool x0_zero, int* iter,
+                     double* err) {
+  DeviceBuffers& d = h->d;
+  hipStream_t st = h->stream;
+  if (d.err_hist_cap < itmax + 2) {
+    if (d.err_hist) HIP_TRY(hipFree(d.err_hist));
+    d.err_hist_cap = itmax + 2;
+    HIP_TRY(dmalloc(&d.err_hist, d.err_hist_cap));
+  }
+  CGScalars hs{};
+  hs.tol = tol;
+  hs.itmax = itmax;
+  hs.bkden = 1.0;
+  HIP_TRY(hipMemcpyAsync(d.scal, &hs, sizeof(hs), hipMemcpyHostToDevice, st));
+  HIP_TRY(hipMemsetAsync(d.tickets, 0, 8 * sizeof(unsigned), st));
+  if (x0_zero) {
+    k_zero<<<blocks_for(h->N + 2), kBlock, 0, st>>>(d.x, h->N + 2);
+  }
+  CGArgs a = make_cg_args(h);
+  const int G = h->grid;
+  k_cg_init<<<G, kBlock, 0, st>>>(a, itol, x0_zero ? 1 : 0);
+  HIP_TRY(hipGetLastError());
+  // iterate in chunks; the device flag makes surplus launches no-ops
+  int chunk = 8;
+  CGScalars* hsp = nullptr;
+  HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&hsp), sizeof(CGScalars)));
+  hipError_t e = hipSuccess;
+  long long launched = 0;
+  KernelTiming& T = h->timing;
+  const int kMaxChunk = 256;
+  if (T.enabled && T.ev.size() < 3 * (size_t)kMaxChunk) {
+    const size_t have = T.ev.size();
+    T.ev.resize(3 * (size_t)kMaxChunk);
+    for (size_t i = have; i < T.ev.size(); ++i) HIP_TRY(hipEventCreate(&T.ev[i]));
+  }
+  int done_iters = 0;
+  while (true) {
+    for (int j = 0; j < chunk; ++j) {
+      if (T.enabled) hipEventRecord(T.ev[3 * j], st);
+      k_cg_spmv<<<G, kBlock, 0, st>>>(a);
+      if (T.enabled) hipEventRecord(T.ev[3 * j + 1], st);
+      k_cg_update<<<G, kBlock, 0, st>>>(a);
+      if (T.enabled) hipEventRecord(T.ev[3 * j + 2], st);
+    }
+    launched += chunk;
+    e = hipGetLastError();
+    if (e != hipSuccess) break;
+    e = hipMemcpyAsync(hsp, d.scal, sizeof(CGScalars), hipMemcpyDeviceToHost, st);
+    if (e != hipSuccess) break;
+    e = hipStreamSynchronize(st);
+    if (e != hipSuccess) break;
+    if (T.enabled) {  // launches of this chunk that did work
+      const int real = std::min(chunk, hsp->iter - done_iters);
+      for (int j = 0; j < real; ++j) {
+        float ta = 0.f, tb = 0.f;
+        hipEventElapsedTime(&ta, T.ev[3 * j], T.ev[3 * j + 1]);
+        hipEventElapsedTime(&tb, T.ev[3 * j + 1], T.ev[3 * j + 2]);
+        T.spmv_ms += ta;
+        T.update_ms += tb;
+      }
+      T.spmv_n += real;
+      T.update_n += real;
+    }
+    done_iters = hsp->iter;
+    if (hsp->done) break;
+    if (launched > (long long)itmax + 2) break;  // cannot happen: device stops at itmax+1
+    chunk = std::min(chunk * 2, kMaxChunk);
+  }
+  *iter = hsp->iter;
+  *err = hsp->err;
+  hipHostFree(hsp);
+  return e;
+}
+
+hipError_t dev_currents(perc_ctx* h, int rule, int cur_rule, double g0, double leak, double Va,
+                        int span_root, double thresh, double* iout_host) {
+  DeviceBuffers& d = h->d;
+  hipStream_t st = h->stream;
+  const int m = h->g.m;
+  k_currents<<<blocks_for(2 * m), kBlock, 0, st>>>(h->g, d.bond_first, d.bocc, d.socc, d.parent,
+                                                    d.x, rule, cur_rule, g0, leak, Va, span_root,
+                                                    thresh, d.iout);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipMemcpyAsync(iout_host, d.iout, sizeof(double) * 2 * m, hipMemcpyDeviceToHost, st));
+  return hipStreamSynchronize(st);
+}
+
+hipError_t dev_spmv(perc_ctx* h, const double* x, double* y) {
+  DeviceBuffers& d = h->d;
+  hipStream_t st = h->stream;
+  const size_t bytes = sizeof(double) * h->N;
+  HIP_TRY(hipMemcpyAsync(d.p0, x, bytes, hipMemcpyHostToDevice, st));
+  CsrView A{h->N, d.rowptr, d.col, d.val, d.diag};
+  k_spmv<<<h->grid, kBlock, 0, st>>>(A, d.p0, d.q);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipMemcpyAsync(y, d.q, bytes, hipMemcpyDeviceToHost, st));
+  return hipStreamSynchronize(st);
+}
+
+hipError_t dev_bench(perc_ctx* h, int which, int reps, double* ms) {
+  DeviceBuffers& d = h->d;
+  hipStream_t st = h->stream;
+  CGArgs a = make_cg_args(h);
+  CsrView A{h->N, d.rowptr, d.col, d.val, d.diag};
+  // scalars for a steady-state iteration (iter = 1 -> general p update)
+  CGScalars hs{};
+  hs.bknum = 1.0;
+  hs.bkden = 2.0;
+  hs.ak = 0.5;
+  hs.bnrm = 1.0;
+  hs.tol = -1.0;
+  hs.itmax = 1 << 30;
+  hs.iter = 1;
+  HIP_TRY(hipMemcpyAsync(d.scal, &hs, sizeof(hs), hipMemcpyHostToDevice, st));
+  HIP_TRY(hipMemsetAsync(d.tickets, 0, 8 * sizeof(unsigned), st));
+  auto launch = [&]() {
+    if (which == 0) k_spmv<<<h->grid, kBlock, 0, st>>>(A, d.p0, d.q);
+    else if (which == 1) k_cg_spmv<<<h->grid, kBlock, 0, st>>>(a);
+    else k_cg_update<<<h->grid, kBlock, 0, st>>>(a);
+  };
+  // the update kernel advances iter; keep the kernel under test on the same
+  // parity by re-seeding the scalars is unnecessary for timing
+  for (int i = 0; i < 3; ++i) launch();
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipEventRecord(h->ev[0], st));
+  for (int i = 0; i < reps; ++i) launch();
+  HIP_TRY(hipEventRecord(h->ev[1], st));
+  HIP_TRY(hipEventSynchronize(h->ev[1]));
+  float t = 0.f;
+  HIP_TRY(hipEventElapsedTime(&t, h->ev[0], h->ev[1]));
+  *ms = (double)t / reps;
+  return hipSuccess;
+}
+
+}  // namespace perc

@@ -1,0 +1,142 @@
+// perc_internal.h -- libperc internals shared by the host and device units.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "../../include/perc.h"
+#include "lattice.h"
+
+namespace perc {
+
+constexpr int kBlock = 256;       // threads per workgroup (4 wave64)
+constexpr int kRowsPerTile = 256; // CSR rows staged per LDS tile
+constexpr int kMaxSpanList = 64;  // spanning roots recorded per labeling
+
+// Device-resident CG scalars (one cache line each group; written only by the
+// last-arriving workgroup of a kernel, read by the next kernel).
+struct CGScalars {
+  double bknum;  // z.r for the coming iteration (linbcg bknum)
+  double bkden;  // previous bknum
+  double akden;  // q.p of the current iteration
+  double ak;     // bknum / akden
+  double bnrm;   // ||D^-1 b|| (itol 2) or ||b|| (itol 1)
+  double err;    // last err
+  double tol;
+  int iter;      // completed iterations
+  int itmax;
+  int done;      // set once err <= tol or iter > itmax
+  int pad[3];
+};
+
+struct DeviceBuffers {
+  // lattice (1-based sites): bonds whose smaller end is s are
+  // [bond_first[s], bond_first[s+1]) in bond-list order
+  int* bond_first = nullptr;  // t+2
+  // interior CSR, 0-based: off-diagonals only, ascending column
+  int* rowptr = nullptr;  // N+1
+  int* col = nullptr;     // nnz (+pad)
+  double* val = nullptr;  // nnz (+pad)
+  double* diag = nullptr; // N
+  double* rhs = nullptr;  // N
+  // occupancy
+  uint8_t* bocc = nullptr;  // nb
+  uint8_t* socc = nullptr;  // t+1
+  int* order = nullptr;     // upload buffer (max(nb,t)+1)
+  // labeling
+  int* parent = nullptr;     // t+1
+  uint8_t* member = nullptr; // t+1 (site belongs to some cluster)
+  uint8_t* bot = nullptr;    // t+1
+  uint8_t* top = nullptr;    // t+1
+  int* counters = nullptr;   // [0]=nspan [1]=nclusters [2]=span_sites, then list
+  // CG
+  double* x = nullptr;
+  double* r = nullptr;
+  double* p0 = nullptr;
+  double* p1 = nullptr;
+  double* q = nullptr;
+  double* partials = nullptr;   // 4 * grid
+  unsigned* tickets = nullptr;  // 8
+  CGScalars* scal = nullptr;
+  double* err_hist = nullptr;   // itmax+2
+  int err_hist_cap = 0;
+  double* iout = nullptr;       // 2m (boundary-row currents)
+};
+
+struct ReplayOrder {
+  int kind = PERC_BOND;
+  std::vector<int> sites;  // occupied prefix of the site order (ids, 0 = sentinel)
+  std::vector<int> bonds;  // occupied prefix of the bond order (1-based ids)
+  // device-resident source (perc_occupy_device): copied to the host vectors
+  // only if a host replay needs them
+  const int* d_sites = nullptr;
+  const int* d_bonds = nullptr;
+  int n_sites = 0, n_bonds = 0;
+  bool host_valid = true;
+};
+
+struct KernelTiming {
+  bool enabled = false;
+  std::vector<hipEvent_t> ev;  // 3 per iteration slot of a launch chunk
+  double spmv_ms = 0.0, update_ms = 0.0;
+  long long spmv_n = 0, update_n = 0;
+};
+
+}  // namespace perc
+
+struct perc_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  perc::Geom g{};
+  long long nb = 0;
+  int N = 0;       // interior rows t-2m
+  long long nnz = 0;
+  int grid = 0;    // fixed grid of the CG kernels (reduction order depends on it)
+  perc::DeviceBuffers d;
+  std::vector<int> h_bond_first;  // host copy, t+2
+  perc::ReplayOrder last;          // last occupancy (for the host replay)
+  bool occupied = false;
+  bool labeled = false;
+  bool assembled = false;
+  int span_root = 0;
+  int perccln = 0;
+  int rule = -1;
+  hipEvent_t ev[8];
+  perc::KernelTiming timing;
+};
+
+namespace perc {
+
+// device entry points (perc_device.hip)
+hipError_t dev_build_lattice(perc_ctx* h);
+hipError_t dev_alloc_matrix(perc_ctx* h, int N, long long nnz);
+void dev_free_all(perc_ctx* h);
+hipError_t dev_occupy(perc_ctx* h, int kind, int nsites, const int* site_order, int nbonds,
+                      const int* bond_order, bool device_src);
+hipError_t dev_label(perc_ctx* h, int* nspan, int* span_list, int* nclusters);
+hipError_t dev_span_sites(perc_ctx* h, int root, int* count);
+hipError_t dev_canon(perc_ctx* h, int* canon_out);
+hipError_t dev_assemble(perc_ctx* h, int rule, double g0, double leak, double Va, int span_root);
+hipError_t dev_solve(perc_ctx* h, int itol, double tol, int itmax, bool x0_zero, int* iter,
+                     double* err);
+hipError_t dev_currents(perc_ctx* h, int rule, int cur_rule, double g0, double leak, double Va,
+                        int span_root, double thresh, double* iout_host);
+hipError_t dev_spmv(perc_ctx* h, const double* x, double* y);
+hipError_t dev_bench(perc_ctx* h, int which, int reps, double* ms);
+
+// host replay (perc_replay.cpp): reference label numbering
+int replay_bonds(const Geom& g, const std::vector<int>& bond_first, const int* order,
+                 int count, int* label, int* csize, int cap, int* stats);
+int replay_sites(const Geom& g, const int* order, int count, int* label, int* csize, int cap,
+                 int* stats);
+int replay_sitebond(const Geom& g, const std::vector<int>& bond_first, const int* sorder,
+                    int nsites, const int* border, int nbonds, int* site_label,
+                    int* bond_label, int* csize, int cap, int* stats);
+
+void set_error(const std::string& msg);
+int hip_status(hipError_t e, const char* where);
+
+}  // namespace perc

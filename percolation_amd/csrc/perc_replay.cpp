@@ -1,0 +1,288 @@
+// perc_replay.cpp -- reference label numbering by O(N alpha) host replay.
+//
+// Cluster label numbers in the reference are history-dependent: a new
+// cluster takes the counter `cln`, a merge keeps the label of the largest
+// neighbouring cluster (ties: first in nearestn/nnb order) and zeroes the
+// absorbed sizes (Fortran/Square/bondc.f:275-364, Square/site.f:184-254,
+// Square/sitebond.f:230-389).  The GPU labeling produces the partition; these
+// replays reproduce the numbers with a union-find over sites, in
+// O(N alpha) instead of the reference's O(N^2) relabel scans.
+#include <algorithm>
+#include <cstring>
+#include <numeric>
+#include <vector>
+
+#include "perc_internal.h"
+
+namespace perc {
+namespace {
+
+struct DSU {
+  std::vector<int> par, sz;
+  explicit DSU(int n) : par(n), sz(n, 1) { std::iota(par.begin(), par.end(), 0); }
+  int find(int x) {
+    int r = x;
+    while (par[r] != r) r = par[r];
+    while (par[x] != r) {
+      const int nx = par[x];
+      par[x] = r;
+      x = nx;
+    }
+    return r;
+  }
+  int unite(int a, int b) {
+    a = find(a);
+    b = find(b);
+    if (a == b) return a;
+    if (sz[a] < sz[b]) std::swap(a, b);
+    par[b] = a;
+    sz[a] += sz[b];
+    return a;
+  }
+};
+
+// bond-list index of (p<q) using the per-site forward neighbour rank
+inline int bond_index(const Geom& g, const std::vector<int>& bond_first, int p, int q) {
+  if (p < 1 || p > g.t) return -1;
+  int nn[6];
+  nearestn(g, p, nn);
+  int r = 0;
+  for (int k = 0; k < g.scn; ++k)
+    if (nn[k] > p) {
+      if (nn[k] == q) return bond_first[p] + r;
+      ++r;
+    }
+  return -1;
+}
+
+// bond id (0-based) -> endpoints
+inline void bond_ends(const Geom& g, const std::vector<int>& bond_first, int id, int* p, int* q) {
+  const int s = int(std::upper_bound(bond_first.begin() + 1, bond_first.begin() + g.t + 1, id) -
+                    bond_first.begin()) - 1;
+  int nn[6];
+  nearestn(g, s, nn);
+  int r = bond_first[s];
+  for (int k = 0; k < g.scn; ++k)
+    if (nn[k] > s) {
+      if (r == id) { *p = s; *q = nn[k]; return; }
+      ++r;
+    }
+  *p = *q = 0;
+}
+
+inline void track_max(const std::vector<int>& c, int lcn, int lcs, int* maxcn, int* maxcs) {
+  // bondc.f:382-391 / site.f:263-272
+  if (c[lcn] > *maxcs) {
+    *maxcs = c[lcn];
+    *maxcn = lcn;
+  } else if (lcs == 0 && *maxcs == 0) {
+    *maxcs = 1;
+    *maxcn = 1;
+  }
+}
+
+}  // namespace
+
+int replay_bonds(const Geom& g, const std::vector<int>& bond_first, const int* order, int count,
+                 int* label, int* csize, int cap, int* stats) {
+  const long long nb = nbonds(g);
+  if (cap < nb + 2) return PERC_EINVAL;
+  std::vector<int> c(cap, 0);  // c(0) stays 0 (hazard H1)
+  std::vector<int> clab(g.t + 1, 0);
+  std::vector<uint8_t> occ(nb, 0);
+  DSU dsu(g.t + 1);
+  int cln = 1, maxcn = 0, maxcs = 0;
+  for (int i = 0; i < count; ++i) {
+    const int id = order[i];
+    if (id <= 0 || id > nb) {
+      // H2 sentinel (0,0): no nnb row or b row matches; the reference opens
+      // a cluster number that no bond carries.
+      c[cln] = 1;
+      ++cln;
+      if (maxcs == 0) { maxcs = 1; maxcn = 1; }
+      continue;
+    }
+    int a, b;
+    bond_ends(g, bond_first, id - 1, &a, &b);
+    // nnb rows: neighbours of a (except b), then of b (except a)
+    int rs[10], rlab[10], rsz[10], rc = 0;
+    int nn[6];
+    nearestn(g, a, nn);
+    for (int k = 0; k < g.scn; ++k)
+      if (nn[k] != 0 && nn[k] != b) {
+        const int lo = std::min(a, nn[k]), hi = std::max(a, nn[k]);
+        const int q = bond_index(g, bond_first, lo, hi);
+        rs[rc] = lo;
+        rlab[rc] = (q >= 0 && occ[q]) ? clab[dsu.find(lo)] : 0;
+        ++rc;
+      }
+    nearestn(g, b, nn);
+    for (int k = 0; k < g.scn; ++k)
+      if (nn[k] != 0 && nn[k] != a) {
+        const int lo = std::min(b, nn[k]), hi = std::max(b, nn[k]);
+        const int q = bond_index(g, bond_first, lo, hi);
+        rs[rc] = lo;
+        rlab[rc] = (q >= 0 && occ[q]) ? clab[dsu.find(lo)] : 0;
+        ++rc;
+      }
+    for (int k = 0; k < rc; ++k) rsz[k] = c[rlab[k]];
+    int lcn = rc ? rlab[0] : 0, lcs = rc ? rsz[0] : 0;
+    for (int k = 1; k < rc; ++k)
+      if (rlab[k] != 0 && rsz[k] > lcs) { lcn = rlab[k]; lcs = rsz[k]; }
+    occ[id - 1] = 1;
+    if (lcs == 0) {
+      if (clab[dsu.find(a)] != 0 || clab[dsu.find(b)] != 0) return PERC_EREPLAY;  // H7
+      const int r = dsu.unite(a, b);
+      clab[r] = cln;
+      c[cln] = 1;
+      ++cln;
+    } else {
+      int clsum = lcs;
+      for (int k = 0; k < rc; ++k) {
+        if (rlab[k] == 0) continue;
+        if (rlab[k] != lcn) {
+          bool dup = false;
+          for (int l = 0; l < k; ++l) dup |= rlab[l] == rlab[k];
+          if (!dup) clsum += rsz[k];
+          c[rlab[k]] = 0;
+        }
+        dsu.unite(a, rs[k]);
+      }
+      const int r = dsu.unite(a, b);
+      clab[r] = lcn;
+      c[lcn] = clsum + 1;
+    }
+    track_max(c, lcn, lcs, &maxcn, &maxcs);
+  }
+  if (label) {
+    for (int s = 1; s < g.t; ++s)
+      for (int k = bond_first[s]; k < bond_first[s + 1]; ++k)
+        label[k] = occ[k] ? clab[dsu.find(s)] : 0;
+  }
+  if (csize) std::memcpy(csize, c.data(), sizeof(int) * cap);
+  if (stats) { stats[0] = cln; stats[1] = maxcn; stats[2] = maxcs; }
+  return PERC_OK;
+}
+
+int replay_sites(const Geom& g, const int* order, int count, int* label, int* csize, int cap,
+                 int* stats) {
+  if (cap < g.t + 2) return PERC_EINVAL;
+  std::vector<int> c(cap, 0);
+  std::vector<int> clab(g.t + 1, 0);
+  std::vector<uint8_t> occ(g.t + 1, 0);
+  DSU dsu(g.t + 1);
+  int cln = 1, maxcn = 0, maxcs = 0;
+  for (int i = 0; i < count; ++i) {
+    const int sn = order[i];
+    if (sn <= 0 || sn > g.t) continue;  // H2 sentinel: reference reads s(-1); skipped
+    int nn[6], lab[6], siz[6];
+    nearestn(g, sn, nn);
+    for (int k = 0; k < g.scn; ++k) {
+      lab[k] = (nn[k] > 0 && occ[nn[k]]) ? clab[dsu.find(nn[k])] : 0;
+      siz[k] = c[lab[k]];
+    }
+    int lcn = lab[0], lcs = siz[0];
+    for (int k = 1; k < g.scn; ++k)
+      if (nn[k] != 0 && lab[k] != 0 && siz[k] > lcs) { lcn = lab[k]; lcs = siz[k]; }
+    occ[sn] = 1;
+    if (lcs == 0) {
+      clab[sn] = cln;
+      c[cln] = 1;
+      ++cln;
+    } else {
+      int clsum = lcs;
+      for (int k = 0; k < g.scn; ++k) {
+        if (nn[k] == 0 || lab[k] == 0) continue;
+        if (lab[k] != lcn) {
+          bool dup = false;
+          for (int l = 0; l < k; ++l) dup |= lab[l] == lab[k];
+          if (!dup) {
+            clsum += siz[k];
+            c[lab[k]] = 0;
+          }
+        }
+        dsu.unite(sn, nn[k]);
+      }
+      clab[dsu.find(sn)] = lcn;
+      c[lcn] = clsum + 1;
+    }
+    track_max(c, lcn, lcs, &maxcn, &maxcs);
+  }
+  if (label)
+    for (int s = 1; s <= g.t; ++s) label[s - 1] = occ[s] ? clab[dsu.find(s)] : 0;
+  if (csize) std::memcpy(csize, c.data(), sizeof(int) * cap);
+  if (stats) { stats[0] = cln; stats[1] = maxcn; stats[2] = maxcs; }
+  return PERC_OK;
+}
+
+int replay_sitebond(const Geom& g, const std::vector<int>& bond_first, const int* sorder,
+                    int nsites, const int* border, int nbond, int* site_label, int* bond_label,
+                    int* csize, int cap, int* stats) {
+  const long long nb = nbonds(g);
+  if (cap < g.t + nb + 2) return PERC_EINVAL;
+  std::vector<int> c(cap, 0);
+  std::vector<int> clab(g.t + 1, 0);
+  std::vector<uint8_t> socc(g.t + 1, 0);
+  std::vector<int> battach(nb, 0);  // >0: site whose cluster the bond follows; <0: own label
+  DSU dsu(g.t + 1);
+  int cln = 1;
+  for (int i = 0; i < nsites; ++i) {  // sitebond.f:187-196
+    const int sn = sorder[i];
+    if (sn > 0 && sn <= g.t) {
+      socc[sn] = 1;
+      clab[sn] = cln;
+    }
+    c[cln] = 1;
+    ++cln;
+  }
+  int maxcn = 1, maxcs = 1, lcn = 0;
+  for (int i = 0; i < nbond; ++i) {  // sitebond.f:223-400
+    const int id = border[i];
+    if (id > 0 && id <= nb) {
+      int a, b;
+      bond_ends(g, bond_first, id - 1, &a, &b);
+      const int la = socc[a] ? clab[dsu.find(a)] : 0;
+      const int lb = socc[b] ? clab[dsu.find(b)] : 0;
+      if (la == 0 && lb == 0) {
+        battach[id - 1] = -cln;
+        c[cln] = 1;
+        ++cln;
+      } else if (la > 0 && lb == 0) {
+        lcn = la;
+        battach[id - 1] = a;
+        c[la] += 1;
+      } else if (la == 0 && lb > 0) {
+        lcn = lb;
+        battach[id - 1] = b;
+        c[lb] += 1;
+      } else if (la == lb) {
+        lcn = la;
+        battach[id - 1] = a;
+        c[la] += 1;
+      } else {
+        int oldcn;
+        if (c[la] > c[lb]) { lcn = la; oldcn = lb; }
+        else { lcn = lb; oldcn = la; }
+        const int clsum = c[lcn] + c[oldcn] + 1;
+        const int r = dsu.unite(a, b);
+        clab[r] = lcn;
+        battach[id - 1] = a;
+        c[oldcn] = 0;
+        c[lcn] = clsum;
+      }
+    }
+    if (c[lcn] > maxcs) { maxcs = c[lcn]; maxcn = lcn; }  // sitebond.f:387-390
+  }
+  if (site_label)
+    for (int s = 1; s <= g.t; ++s) site_label[s - 1] = socc[s] ? clab[dsu.find(s)] : 0;
+  if (bond_label)
+    for (long long k = 0; k < nb; ++k) {
+      const int at = battach[k];
+      bond_label[k] = at > 0 ? clab[dsu.find(at)] : (at < 0 ? -at : 0);
+    }
+  if (csize) std::memcpy(csize, c.data(), sizeof(int) * cap);
+  if (stats) { stats[0] = cln; stats[1] = maxcn; stats[2] = maxcs; }
+  return PERC_OK;
+}
+
+}  // namespace perc

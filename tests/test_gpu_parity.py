@@ -1,0 +1,342 @@
+"""GPU parity: libperc's HIP path against the oracle and the reference goldens.
+
+Bars: partitions bit-exact (canonical ids), assembled
+system and SpMV bitwise, CG iteration count within +-1 of the reference's,
+Gtop within 1e-10 relative at the reference settings (tol 1e-8), Gtop and
+Gbot within 1e-10 relative when both sides solve to tol 1e-14.
+"""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+import golden_io as G
+import oracle_lib as O
+import percolation_amd as P
+from percolation_amd import _lib as PL
+from percolation_amd import api
+
+pytestmark = pytest.mark.gpu
+REL = 1e-10
+
+
+def rel(a, b):
+    return abs(a - b) / max(abs(b), 1e-300)
+
+
+# ------------------------------------------------------------ helpers
+def oracle_canon_bonds(b1, b2, label, t):
+    """per-site canonical id (min site of the component) from bond labels"""
+    canon = np.zeros(t, np.int64)
+    lab = label.astype(np.int64)
+    occ = lab > 0
+    if not occ.any():
+        return canon
+    big = np.iinfo(np.int64).max
+    mins = np.full(lab.max() + 1, big)
+    np.minimum.at(mins, lab[occ], b1[occ])
+    for arr in (b1, b2):
+        np.maximum.at(canon, arr[occ] - 1, mins[lab[occ]])
+    return canon
+
+
+def oracle_canon_sites(s):
+    t = len(s)
+    canon = np.zeros(t, np.int64)
+    occ = s > 0
+    big = np.iinfo(np.int64).max
+    mins = np.full(s.max() + 1 if occ.any() else 1, big)
+    sites = np.arange(1, t + 1)
+    np.minimum.at(mins, s[occ], sites[occ])
+    canon[occ] = mins[s[occ]]
+    return canon
+
+
+# ------------------------------------------------------------ labeling
+BOND_CASES = [(0, 64, 64, 0, 0.5, 1), (0, 128, 96, 1, 0.52, 2), (1, 64, 64, 0, 0.35, 3),
+              (1, 100, 80, 1, 0.33, 4), (0, 256, 256, 0, 0.5, 5), (0, 256, 256, 0, 0.7, 6)]
+
+
+@pytest.mark.parametrize("lat,m,n,pbc,p,seed", BOND_CASES)
+def test_bond_partition_bitexact(lat, m, n, pbc, p, seed):
+    b1, b2 = api.bond_list(lat, m, n, pbc)
+    nb = len(b1)
+    order = api.shuffled_ids(nb, seed)
+    tb = int(p * nb)
+    with api.Context(lat, m, n, pbc) as ctx:
+        ctx.occupy(PL.BOND, bond_order=order, nbonds_=tb)
+        li = ctx.label(canon=True)
+        ref = api.replay_labels(lat, m, n, pbc, PL.BOND, bond_order=order, nbond=tb)
+        want = oracle_canon_bonds(b1, b2, ref["bond_label"], m * n)
+        assert np.array_equal(li["canon"].astype(np.int64), want)
+        # spanning agrees with the reference rule
+        assert (li["nspan"] > 0) == (ref["perccln"] > 0)
+        if li["nspan"] == 1:
+            k = np.nonzero(ref["bond_label"] == ref["perccln"])[0][0]
+            assert li["span_root"] == want[b1[k] - 1]
+
+
+@pytest.mark.parametrize("lat,m,n,pbc,p,seed", [(0, 64, 64, 0, 0.6, 7), (1, 64, 64, 0, 0.5, 8),
+                                                 (0, 200, 150, 1, 0.59, 9),
+                                                 (1, 128, 128, 1, 0.5, 10)])
+def test_site_partition_bitexact(lat, m, n, pbc, p, seed):
+    t = m * n
+    order = api.shuffled_ids(t, seed)
+    ts = int(p * t)
+    with api.Context(lat, m, n, pbc) as ctx:
+        ctx.occupy(PL.SITE, site_order=order, nsites=ts)
+        li = ctx.label(canon=True)
+    ref = api.replay_labels(lat, m, n, pbc, PL.SITE, site_order=order, nsites=ts)
+    assert np.array_equal(li["canon"].astype(np.int64), oracle_canon_sites(ref["site_label"]))
+    assert (li["nspan"] > 0) == (ref["perccln"] > 0)
+
+
+@pytest.mark.parametrize("lat,m,n,pbc,ps,pb,seed", [(0, 64, 64, 0, 0.9, 0.6, 11),
+                                                     (1, 64, 64, 0, 0.8, 0.5, 12),
+                                                     (0, 128, 128, 0, 0.593, 1.0, 13)])
+def test_sitebond_partition_bitexact(lat, m, n, pbc, ps, pb, seed):
+    t, nb = m * n, api.nbonds(lat, m, n, pbc)
+    so, bo = api.shuffled_ids(t, seed), api.shuffled_ids(nb, seed + 1)
+    ts, tb = int(ps * t), int(pb * nb)
+    with api.Context(lat, m, n, pbc) as ctx:
+        ctx.occupy(PL.SITEBOND, site_order=so, nsites=ts, bond_order=bo, nbonds_=tb)
+        li = ctx.label(canon=True)
+    ref = api.replay_labels(lat, m, n, pbc, PL.SITEBOND, site_order=so, nsites=ts, bond_order=bo,
+                            nbond=tb)
+    assert np.array_equal(li["canon"].astype(np.int64), oracle_canon_sites(ref["site_label"]))
+    assert (li["nspan"] > 0) == (ref["perccln"] > 0)
+
+
+# ------------------------------------------------------------ assembly + SpMV
+def oracle_system(lat, m, n, pbc, b1, b2, gval):
+    t, N = m * n, m * n - 2 * m
+    nmax = N + 1 + 2 * len(b1) + 8
+    sa, ija = O.f64(nmax), O.i32(nmax)
+    itemp, diag = O.f64(N), O.f64(t)
+    k = O.lib().or_assemble(lat, m, n, pbc, len(b1), b1, b2, gval, 1.0, 1e-16, 0, nmax, sa, ija,
+                            itemp, diag)
+    return sa, ija, itemp, diag, k
+
+
+@pytest.mark.parametrize("lat,m,n,pbc,p,seed", BOND_CASES[:4])
+def test_assembly_and_spmv_bitwise(lat, m, n, pbc, p, seed):
+    b1, b2 = api.bond_list(lat, m, n, pbc)
+    nb = len(b1)
+    order = api.shuffled_ids(nb, seed)
+    tb = int(max(p, 0.6 if lat == 0 else 0.4) * nb)
+    with api.Context(lat, m, n, pbc) as ctx:
+        ctx.occupy(PL.BOND, bond_order=order, nbonds_=tb)
+        li = ctx.label()
+        assert li["nspan"] >= 1
+        ctx.conductance(itmax=3)
+        sysm = ctx.system()
+        ref = api.replay_labels(lat, m, n, pbc, PL.BOND, bond_order=order, nbond=tb)
+        gval = O.f64(nb)
+        O.lib().or_bond_values(0, nb, b1, b2, ref["bond_label"], O.i32(1), ref["perccln"], 1.0,
+                               1e-12, gval)
+        sa, ija, itemp, diag, k = oracle_system(lat, m, n, pbc, b1, b2, gval)
+        N = m * n - 2 * m
+        # NR layout -> CSR
+        rp = ija[:N + 1] - (N + 2)
+        assert np.array_equal(sysm["rowptr"], rp)
+        assert np.array_equal(sysm["col"], ija[N + 1:k] - 1)
+        assert np.array_equal(sysm["val"].view(np.uint64), sa[N + 1:k].view(np.uint64))
+        assert np.array_equal(sysm["diag"].view(np.uint64), sa[:N].view(np.uint64))
+        assert np.array_equal(sysm["rhs"].view(np.uint64), itemp.view(np.uint64))
+        x = np.random.default_rng(seed).standard_normal(N)
+        y = ctx.spmv(x)
+        yo = O.f64(N)
+        O.lib().or_dsprsax(sa, ija, x, yo, N)
+        assert np.array_equal(y.view(np.uint64), yo.view(np.uint64))
+
+
+# ------------------------------------------------------------ conductance
+BONDC = [v for v in G.variants() if G.meta(v)["kind"] == "bondc" and G.meta(v)["perccln"]]
+
+
+@pytest.mark.parametrize("v", BONDC)
+def test_bondc_against_reference(v):
+    md = G.meta(v)
+    p = md["params"]
+    tol, itmax = p.get("tol", 1e-8), p.get("itmax", 2500)
+    r = api.bondc(p["lattice"], p["m"], p["n"], p["pbc"], p["pb"], p["seed"], tol=tol,
+                  itmax=itmax)
+    assert r["perccln"] == md["perccln"] and r["perccls"] == md["perccls"]
+    assert abs(r["iter"] - md["iter"]) <= 1, (r["iter"], md["iter"])
+    assert rel(r["gtop"], md["gtop"]) < REL, (r["gtop"], md["gtop"])
+    if tol <= 1e-13:
+        assert rel(r["gbot"], md["gbot"]) < REL, (r["gbot"], md["gbot"])
+    else:
+        # the reference's own Gbot at tol 1e-8 is off the converged value by
+        # up to ~3e-7 (SURVEY.md §7 hard part 2): compare at that scale
+        assert rel(r["gbot"], md["gbot"]) < 1e-6
+
+
+@pytest.mark.parametrize("lat,m,n,p,seed", [(0, 128, 128, 0.6, 21), (1, 96, 96, 0.4, 22),
+                                            (0, 200, 160, 0.55, 23)])
+def test_conductance_vs_oracle_linbcg(lat, m, n, p, seed):
+    """Larger lattices: oracle literal linbcg (CPU) vs fused GPU PCG."""
+    b1, b2 = api.bond_list(lat, m, n, 0)
+    nb = len(b1)
+    order = api.shuffled_ids(nb, seed)
+    tb = int(p * nb)
+    ref = api.replay_labels(lat, m, n, 0, PL.BOND, bond_order=order, nbond=tb)
+    assert ref["perccln"] > 0
+    gval = O.f64(nb)
+    O.lib().or_bond_values(0, nb, b1, b2, ref["bond_label"], O.i32(1), ref["perccln"], 1.0, 1e-12,
+                           gval)
+    oc = O.conductance(lat, m, n, 0, b1, b2, gval, itmax=100000)
+    with api.Context(lat, m, n, 0) as ctx:
+        ctx.occupy(PL.BOND, bond_order=order, nbonds_=tb)
+        ctx.label()
+        c = ctx.conductance(itmax=100000, vint=True)
+    assert abs(c["iter"] - oc["iter"]) <= 1
+    assert rel(c["gtop"], oc["gtop"]) < REL
+    assert np.max(np.abs(c["vint"] - oc["vint"])) < 1e-6
+
+
+def test_site_and_mixed_rules_vs_direct_solve():
+    """ConductCalc.m site / mixed rules (parity unpinned vs MATLAB: checked
+    against an independent direct sparse solve of the oracle's system)."""
+    import scipy.sparse as sp
+    import scipy.sparse.linalg as spla
+    for kind, rule, lat, m, n in [(PL.SITE, PL.RULE_SITE, 0, 64, 64),
+                                  (PL.SITE, PL.RULE_SITE, 1, 64, 64),
+                                  (PL.SITEBOND, PL.RULE_MIXED, 0, 64, 64)]:
+        t = m * n
+        b1, b2 = api.bond_list(lat, m, n, 0)
+        nb = len(b1)
+        if kind == PL.SITE:
+            r = api.site(lat, m, n, 0, ps=0.65 if lat == 0 else 0.55, seed=1080115,
+                         conductance=True, tol=1e-14, itmax=200000)
+            s, bl = r["site_label"], O.i32(nb)
+        else:
+            r = api.sitebond(lat, m, n, 0, ps=0.95, pb=0.75, conductance=True, tol=1e-14,
+                             itmax=200000)
+            s, bl = r["site_label"], r["bond_label"]
+        assert r["perccln"] > 0
+        gval = O.f64(nb)
+        O.lib().or_bond_values(rule, nb, b1, b2, bl, s, r["perccln"], 1.0, 1e-12, gval)
+        sa, ija, itemp, diag, k = oracle_system(lat, m, n, 0, b1, b2, gval)
+        N = t - 2 * m
+        rows = np.repeat(np.arange(N), np.diff(ija[:N + 1]))
+        A = sp.csr_matrix((sa[N + 1:k], (rows, ija[N + 1:k] - 1)), shape=(N, N)) + \
+            sp.diags(sa[:N])
+        v = spla.spsolve(A.tocsc(), itemp)
+        gt, gb = C.c_double(), C.c_double()
+        O.lib().or_currents(lat, m, n, 0, nb, b1, b2, gval, diag, v, 1.0, 0.0, 1, C.byref(gt),
+                            C.byref(gb))
+        assert rel(r["gtop"], gt.value) < 1e-9, (kind, r["gtop"], gt.value)
+        assert rel(r["gbot"], gb.value) < 1e-9, (kind, r["gbot"], gb.value)
+
+
+def test_multiple_spanning_clusters_use_lowest_label():
+    """Hazard H4: with >1 spanning cluster only the lowest reference label
+    gets g0; the GPU path resolves it with the host replay."""
+    lat, m, n = 0, 24, 6  # wide and short: several spanning clusters are common
+    nb = api.nbonds(lat, m, n, 0)
+    found = 0
+    for seed in range(1, 400):
+        order = api.shuffled_ids(nb, seed)
+        tb = int(0.5 * nb)
+        with api.Context(lat, m, n, 0) as ctx:
+            ctx.occupy(PL.BOND, bond_order=order, nbonds_=tb)
+            li = ctx.label()
+            if li["nspan"] < 2:
+                continue
+            found += 1
+            ref = api.replay_labels(lat, m, n, 0, PL.BOND, bond_order=order, nbond=tb)
+            assert li["replayed"] == 1 and li["perccln"] == ref["perccln"]
+            c = ctx.conductance(tol=1e-14, itmax=100000)
+        b1, b2 = api.bond_list(lat, m, n, 0)
+        gval = O.f64(nb)
+        O.lib().or_bond_values(0, nb, b1, b2, ref["bond_label"], O.i32(1), ref["perccln"], 1.0,
+                               1e-12, gval)
+        oc = O.conductance(lat, m, n, 0, b1, b2, gval, tol=1e-14, itmax=100000)
+        assert rel(c["gtop"], oc["gtop"]) < REL
+        if found >= 3:
+            break
+    assert found >= 1
+
+
+def test_nr_linbcg_symbol():
+    """linbcg_ (F77 ABI, COMMON /mat/ via perc_nr_bind) vs the oracle's
+    literal linbcg on the reference 50x50 system."""
+    lat, m, n = 0, 50, 50
+    b1, b2 = api.bond_list(lat, m, n, 0)
+    nb = len(b1)
+    order = api.shuffled_ids(nb, 626504)
+    ref = api.replay_labels(lat, m, n, 0, PL.BOND, bond_order=order, nbond=int(0.6 * nb))
+    gval = O.f64(nb)
+    O.lib().or_bond_values(0, nb, b1, b2, ref["bond_label"], O.i32(1), ref["perccln"], 1.0, 1e-12,
+                           gval)
+    sa, ija, itemp, diag, k = oracle_system(lat, m, n, 0, b1, b2, gval)
+    N = m * n - 2 * m
+    oc = O.conductance(lat, m, n, 0, b1, b2, gval)
+    L = P.lib()
+    L.perc_nr_bind(sa.ctypes.data, ija.ctypes.data, len(sa))
+    x = np.zeros(N)
+    nn, itol, itmax, it = C.c_int(N), C.c_int(2), C.c_int(2500), C.c_int()
+    tol, err = C.c_double(1e-8), C.c_double()
+    b = itemp.copy()
+    L.linbcg_(C.byref(nn), b.ctypes.data, x.ctypes.data, C.byref(itol), C.byref(tol),
+              C.byref(itmax), C.byref(it), C.byref(err))
+    assert L.perc_nr_status() == 0
+    assert abs(it.value - oc["iter"]) <= 1
+    assert np.max(np.abs(x - oc["vint"])) < 1e-6
+    # dsprsax_ bitwise
+    y, yo = np.zeros(N), O.f64(N)
+    L.dsprsax_(sa.ctypes.data, ija.ctypes.data, x.ctypes.data, y.ctypes.data, C.byref(nn))
+    O.lib().or_dsprsax(sa, ija, x, yo, N)
+    assert np.array_equal(y.view(np.uint64), yo.view(np.uint64))
+    L.perc_nr_bind(None, None, 0)
+
+
+def test_bond_cond_rows_against_reference():
+    for v in [v for v in G.variants() if G.meta(v)["kind"] == "bond_cond"]:
+        p = G.meta(v)["params"]
+        txt = G.text(v, "bondcond.txt").decode().splitlines()
+        res = api.bond_cond_grid(p["lattice"], p["m"], p["n"], p["pbc"], p["seed"],
+                                 p["numtrials"])
+        want, cur = [], None
+        for line in txt:
+            if "Trial #" in line:
+                cur = dict(rows=[])
+                want.append(cur)
+            elif cur is not None and line.count(",") == 3:
+                cur["rows"].append([float(x) for x in line.split(",")])
+            elif "lattice-spanning cluster:" in line:
+                cur["perccln"] = int(line.split(":")[1])
+            elif "pc =" in line:
+                cur["pc"] = float(line.split("=")[1])
+        for tr, w in zip(res, want):
+            assert len(tr["rows"]) == len(w["rows"])
+            for r, wr in zip(tr["rows"], w["rows"]):
+                assert "%12.9f" % r["pb"] == "%12.9f" % wr[0]
+                # f12.9 text: agree to the printed precision
+                assert abs(r["gbot"] - wr[1]) <= 2e-9 and abs(r["gtop"] - wr[2]) <= 2e-9
+            assert tr["pc"] == w["pc"]
+            assert tr["perccln"] == w["perccln"]
+
+
+@pytest.mark.parametrize("L_,p", [(1024, 0.6), (1024, 0.5)])
+def test_full_size_properties(L_, p):
+    """1024^2 (config 2 size): the reported err equals the recomputed
+    residual, current is conserved at tight tolerance, labels partition."""
+    nb = api.nbonds(0, L_, L_, 0)
+    order = api.shuffled_ids(nb, 4562929)
+    with api.Context(0, L_, L_, 0) as ctx:
+        ctx.occupy(PL.BOND, bond_order=order, nbonds_=int(p * nb))
+        li = ctx.label()
+        if li["nspan"] == 0:
+            pytest.skip("no spanning cluster for this seed")
+        c = ctx.conductance(tol=1e-12, itmax=10 ** 6, vint=True)
+        s = ctx.system()
+        N = L_ * L_ - 2 * L_
+        rows = np.repeat(np.arange(N), np.diff(s["rowptr"]))
+        ax = s["diag"] * c["vint"] + np.bincount(rows, weights=s["val"] * c["vint"][s["col"]],
+                                                 minlength=N)
+        res = np.sqrt(np.sum((s["rhs"] - ax) ** 2)) / np.sqrt(np.sum((s["rhs"] / s["diag"]) ** 2))
+        assert res < 1e-11
+        assert abs(res - c["err"]) < 1e-3 * c["err"] + 1e-14
+        assert rel(c["gtop"], c["gbot"]) < 1e-6
