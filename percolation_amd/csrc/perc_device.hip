@@ -207,25 +207,26 @@ __global__ void k_cc_init(int t, int* parent, uint8_t* member, uint8_t* bot, uin
 
 __global__ void k_cc_hook(Geom g, int kind, const int* bond_first, const uint8_t* bocc,
                           const uint8_t* socc, int* parent, uint8_t* member) {
-  const int s = blockIdx.x * blockDim.x + threadIdx.x + 1;
-  if (s > g.t) return;
-  if (kind != PERC_BOND && socc[s]) member[s] = 1;
-  if (s > g.t - 1) return;
-  int nn[6];
-  nearestn(g, s, nn);
-  const int fb = bond_first[s];
-  int r = 0;
-  for (int k = 0; k < g.scn; ++k) {
-    const int q = nn[k];
-    if (q <= s) continue;
-    bool link;
-    if (kind == PERC_BOND) link = bocc[fb + r];
-    else if (kind == PERC_SITE) link = socc[s] && socc[q];
-    else link = bocc[fb + r] && socc[s] && socc[q];
-    ++r;
-    if (link) {
-      if (kind == PERC_BOND) { member[s] = 1; member[q] = 1; }
-      unite(parent, s, q);
+  for (int s = blockIdx.x * blockDim.x + threadIdx.x + 1; s <= g.t;
+       s += gridDim.x * blockDim.x) {
+    if (kind != PERC_BOND && socc[s]) member[s] = 1;
+    if (s > g.t - 1) continue;
+    int nn[6];
+    nearestn(g, s, nn);
+    const int fb = bond_first[s];
+    int r = 0;
+    for (int k = 0; k < g.scn; ++k) {
+      const int q = nn[k];
+      if (q <= s) continue;
+      bool link;
+      if (kind == PERC_BOND) link = bocc[fb + r];
+      else if (kind == PERC_SITE) link = socc[s] && socc[q];
+      else link = bocc[fb + r] && socc[s] && socc[q];
+      ++r;
+      if (link) {
+        if (kind == PERC_BOND) { member[s] = 1; member[q] = 1; }
+        unite(parent, s, q);
+      }
     }
   }
 }
@@ -794,10 +795,19 @@ hipError_t dev_label(perc_ctx* h, int* nspan, int* span_list, int* nclusters) {
   hipStream_t st = h->stream;
   DeviceBuffers& d = h->d;
   const int kind = h->last.kind;
+  static const int variant = getenv("PERC_CC_VARIANT") ? atoi(getenv("PERC_CC_VARIANT")) : 0;
   k_cc_init<<<blocks_for(g.t + 1), kBlock, 0, st>>>(g.t, d.parent, d.member, d.bot, d.top);
-  k_cc_hook<<<blocks_for(g.t), kBlock, 0, st>>>(g, kind, d.bond_first, d.bocc, d.socc, d.parent,
-                                                 d.member);
+  if (variant == 4) {
+    k_cc_hook<<<1, 1, 0, st>>>(g, kind, d.bond_first, d.bocc, d.socc, d.parent, d.member);
+  } else {
+    k_cc_hook<<<blocks_for(g.t), kBlock, 0, st>>>(g, kind, d.bond_first, d.bocc, d.socc,
+                                                   d.parent, d.member);
+  }
+  if (variant == 2)
+    k_cc_hook<<<blocks_for(g.t), kBlock, 0, st>>>(g, kind, d.bond_first, d.bocc, d.socc,
+                                                   d.parent, d.member);
   k_cc_compress<<<blocks_for(g.t), kBlock, 0, st>>>(g.t, d.parent);
+  if (variant == 3) k_cc_compress<<<blocks_for(g.t), kBlock, 0, st>>>(g.t, d.parent);
   k_span_flags<<<blocks_for(g.t), kBlock, 0, st>>>(g, kind, d.bond_first, d.bocc, d.socc,
                                                     d.parent, d.bot, d.top);
   HIP_TRY(hipMemsetAsync(d.counters, 0, sizeof(int) * (8 + kMaxSpanList), st));
