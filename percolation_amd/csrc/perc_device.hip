@@ -231,10 +231,18 @@ __global__ void k_cc_hook(Geom g, int kind, const int* bond_first, const uint8_t
   }
 }
 
+// Final flattening: a read-only walk, then each thread writes only its own
+// entry.  (Path halving here would let one thread overwrite another
+// thread's freshly written root with an intermediate ancestor.)
 __global__ void k_cc_compress(int t, int* parent) {
   const int s = blockIdx.x * blockDim.x + threadIdx.x + 1;
   if (s > t) return;
-  parent[s] = find_root(parent, s);
+  int x = s, p = parent[x];
+  while (p != x) {
+    x = p;
+    p = parent[x];
+  }
+  parent[s] = x;
 }
 
 // spanning flags at roots: bottom row (sites 1..m) / top row (t-m+1..t)
@@ -646,6 +654,16 @@ CGArgs make_cg_args(perc_ctx* h) {
   return a;
 }
 
+// PERC_SYNC_DEBUG=1: synchronise after each launch and name the failing one
+hipError_t dbg_sync(hipStream_t st, const char* name) {
+  static const bool on = getenv("PERC_SYNC_DEBUG") != nullptr;
+  if (!on) return hipGetLastError();
+  hipError_t e = hipStreamSynchronize(st);
+  if (e == hipSuccess) e = hipGetLastError();
+  if (e != hipSuccess) fprintf(stderr, "[perc] kernel %s failed: %s\n", name, hipGetErrorString(e));
+  return e;
+}
+
 inline dim3 blocks_for(long long n) { return dim3((unsigned)((n + kBlock - 1) / kBlock)); }
 
 template <typename T>
@@ -849,7 +867,7 @@ hipError_t dev_assemble(perc_ctx* h, int rule, double g0, double leak, double Va
   k_assemble<<<blocks_for(h->N), kBlock, 0, h->stream>>>(h->g, h->N, d.bond_first, d.bocc, d.socc,
                                                           d.parent, d.rowptr, d.val, d.diag, d.rhs,
                                                           rule, g0, leak, Va, span_root);
-  return hipGetLastError();
+  return dbg_sync(h->stream, "k_assemble");
 }
 
 hipError_t dev_solve(perc_ctx* h, int itol, double tol, int itmax, bool x0_zero, int* iter,
@@ -873,7 +891,7 @@ hipError_t dev_solve(perc_ctx* h, int itol, double tol, int itmax, bool x0_zero,
   CGArgs a = make_cg_args(h);
   const int G = h->grid;
   k_cg_init<<<G, kBlock, 0, st>>>(a, itol, x0_zero ? 1 : 0);
-  HIP_TRY(hipGetLastError());
+  HIP_TRY(dbg_sync(st, "k_cg_init"));
   // iterate in chunks; the device flag makes surplus launches no-ops
   int chunk = 8;
   CGScalars* hsp = nullptr;
@@ -892,8 +910,10 @@ hipError_t dev_solve(perc_ctx* h, int itol, double tol, int itmax, bool x0_zero,
     for (int j = 0; j < chunk; ++j) {
       if (T.enabled) hipEventRecord(T.ev[3 * j], st);
       k_cg_spmv<<<G, kBlock, 0, st>>>(a);
+      HIP_TRY(dbg_sync(st, "k_cg_spmv"));
       if (T.enabled) hipEventRecord(T.ev[3 * j + 1], st);
       k_cg_update<<<G, kBlock, 0, st>>>(a);
+      HIP_TRY(dbg_sync(st, "k_cg_update"));
       if (T.enabled) hipEventRecord(T.ev[3 * j + 2], st);
     }
     launched += chunk;
@@ -934,7 +954,7 @@ hipError_t dev_currents(perc_ctx* h, int rule, int cur_rule, double g0, double l
   k_currents<<<blocks_for(2 * m), kBlock, 0, st>>>(h->g, d.bond_first, d.bocc, d.socc, d.parent,
                                                     d.x, rule, cur_rule, g0, leak, Va, span_root,
                                                     thresh, d.iout);
-  HIP_TRY(hipGetLastError());
+  HIP_TRY(dbg_sync(st, "k_currents"));
   HIP_TRY(hipMemcpyAsync(iout_host, d.iout, sizeof(double) * 2 * m, hipMemcpyDeviceToHost, st));
   return hipStreamSynchronize(st);
 }

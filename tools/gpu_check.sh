@@ -1,23 +1,34 @@
 #!/usr/bin/env bash
-# One GPU session: parity tests, smoke, benches.  Stops at the first step
-# that faults / aborts / times out (exit codes other than 0 and 1).
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+# One GPU session: parity tests, smoke, benches, profiles.  Stops at the
+# first step that faults / aborts / times out (exit codes other than 0/1, or
+# a GPU memory fault reported in the step's log).
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
 mkdir -p gpurun_out
-STEP_OK() { local rc=$1; [ "$rc" -eq 0 ] || [ "$rc" -eq 1 ]; }
 run() {  # run NAME TIMEOUT CMD...
-  local name=$1 to=$2; shift 2
+  local name=$1 to=$2
+  shift 2
   echo "== $name: $*" | tee -a gpurun_out/summary.log
   timeout -k 10 "$to" "$@" > "gpurun_out/$name.log" 2>&1
   local rc=$?
   echo "== $name rc=$rc" | tee -a gpurun_out/summary.log
   tail -5 "gpurun_out/$name.log" | tee -a gpurun_out/summary.log
-  STEP_OK $rc || { echo "stopping after $name (rc=$rc)" | tee -a gpurun_out/summary.log; exit $rc; }
+  if grep -q -i -E "illegal memory access|memory access fault|HSA_STATUS_ERROR|core dumped" \
+      "gpurun_out/$name.log"; then
+    echo "stopping: GPU fault in $name" | tee -a gpurun_out/summary.log
+    exit 3
+  fi
+  if [ "$rc" -ne 0 ] && [ "$rc" -ne 1 ]; then
+    echo "stopping after $name (rc=$rc)" | tee -a gpurun_out/summary.log
+    exit "$rc"
+  fi
 }
 for step in "$@"; do
   case "$step" in
-    tests) run pytest_gpu 900 python -m pytest tests -m gpu -x -q -rs ;;
+    tests) run pytest_gpu 900 python -m pytest tests -m gpu -q -rs -x ;;
+    testsall) run pytest_gpu 900 python -m pytest tests -m gpu -q -rs ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench1024) run bench1024 600 python bench.py --L 1024 --p 0.6 --steps 3 --warmup 1 --no-cpu-baseline ;;
+    bench1024dbg) PERC_SYNC_DEBUG=1 run bench1024dbg 600 python bench.py --L 1024 --p 0.6 --steps 1 --warmup 0 --no-cpu-baseline ;;
     bench) run bench 1100 python bench.py ;;
     bench_quick) run bench_quick 900 python bench.py --steps 1 --warmup 1 --no-cpu-baseline ;;
     *) echo "unknown step $step"; exit 2 ;;
