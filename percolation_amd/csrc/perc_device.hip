@@ -418,7 +418,7 @@ __global__ __launch_bounds__(kBlock) void k_spmv(CsrView A, const double* __rest
   const int rb0 = lb * chunk, rb1 = min(rb0 + chunk, nrb);
   for (int rb = rb0; rb < rb1; ++rb) {
     const int r0 = rb * kRowsPerTile, nr = min(kRowsPerTile, A.N - r0);
-    if (tid <= nr) s_ptr[tid] = A.rowptr[r0 + tid];
+    for (int j = tid; j <= nr; j += kBlock) s_ptr[j] = A.rowptr[r0 + j];  // nr+1 offsets
     __syncthreads();
     const int e0 = s_ptr[0], ne = s_ptr[nr] - e0;
     // tiles wider than the LDS stage (rows with > kMaxNnzRow entries, e.g. a
@@ -489,7 +489,7 @@ __global__ __launch_bounds__(kBlock) void k_cg_spmv(CGArgs a) {
   double dot[1] = {0.0};
   for (int rb = rb0; rb < rb1; ++rb) {
     const int r0 = rb * kRowsPerTile, nr = min(kRowsPerTile, N - r0);
-    if (tid <= nr) s_ptr[tid] = a.A.rowptr[r0 + tid];
+    for (int j = tid; j <= nr; j += kBlock) s_ptr[j] = a.A.rowptr[r0 + j];  // nr+1 offsets
     __syncthreads();
     const int e0 = s_ptr[0], ne = s_ptr[nr] - e0;
     const bool staged = ne <= kRowsPerTile * kMaxNnzRow;
@@ -813,19 +813,13 @@ hipError_t dev_label(perc_ctx* h, int* nspan, int* span_list, int* nclusters) {
   hipStream_t st = h->stream;
   DeviceBuffers& d = h->d;
   const int kind = h->last.kind;
-  static const int variant = getenv("PERC_CC_VARIANT") ? atoi(getenv("PERC_CC_VARIANT")) : 0;
   k_cc_init<<<blocks_for(g.t + 1), kBlock, 0, st>>>(g.t, d.parent, d.member, d.bot, d.top);
-  if (variant == 4) {
-    k_cc_hook<<<1, 1, 0, st>>>(g, kind, d.bond_first, d.bocc, d.socc, d.parent, d.member);
-  } else {
-    k_cc_hook<<<blocks_for(g.t), kBlock, 0, st>>>(g, kind, d.bond_first, d.bocc, d.socc,
-                                                   d.parent, d.member);
-  }
-  if (variant == 2)
-    k_cc_hook<<<blocks_for(g.t), kBlock, 0, st>>>(g, kind, d.bond_first, d.bocc, d.socc,
-                                                   d.parent, d.member);
+  HIP_TRY(dbg_sync(st, "k_cc_init"));
+  k_cc_hook<<<blocks_for(g.t), kBlock, 0, st>>>(g, kind, d.bond_first, d.bocc, d.socc, d.parent,
+                                                 d.member);
+  HIP_TRY(dbg_sync(st, "k_cc_hook"));
   k_cc_compress<<<blocks_for(g.t), kBlock, 0, st>>>(g.t, d.parent);
-  if (variant == 3) k_cc_compress<<<blocks_for(g.t), kBlock, 0, st>>>(g.t, d.parent);
+  HIP_TRY(dbg_sync(st, "k_cc_compress"));
   k_span_flags<<<blocks_for(g.t), kBlock, 0, st>>>(g, kind, d.bond_first, d.bocc, d.socc,
                                                     d.parent, d.bot, d.top);
   HIP_TRY(hipMemsetAsync(d.counters, 0, sizeof(int) * (8 + kMaxSpanList), st));
