@@ -147,10 +147,10 @@ int perc_get_system(perc_ctx *h, int *rowptr, int *col, double *val,
                     double *diag, double *rhs, int *n_out, int *nnz_out);
 /* y = A x on the assembled system (dsprsax order), host in / host out */
 int perc_spmv_host(perc_ctx *h, const double *x, double *y);
-/* Roofline probe: `reps` back-to-back SpMVs (dsprsax) / fused CG SpMV
-   kernels on the assembled system; returns mean kernel ms (HIP events on
-   the context stream).  which: 0 = plain SpMV, 1 = fused CG SpMV, 2 = CG
-   update kernel. */
+/* Roofline probe: `reps` back-to-back launches of one solver kernel on the
+   assembled system; returns mean kernel ms (HIP events on the context
+   stream).  which: 0 = SpMV (dsprsax), 1 = CG SpMV + q.p dot, 2 = CG
+   residual update (B), 3 = CG x/p update (P).  Clobbers solver vectors. */
 int perc_bench_kernel(perc_ctx *h, int which, int reps, double *ms);
 
 /* Live kernel timing: when enabled, every CG SpMV / update launch inside

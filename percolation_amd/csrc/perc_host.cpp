@@ -569,7 +569,7 @@ int perc_spmv_host(perc_ctx* h, const double* x, double* y) {
 }
 
 int perc_bench_kernel(perc_ctx* h, int which, int reps, double* ms) {
-  if (!h || !ms || reps <= 0 || which < 0 || which > 2) return PERC_EINVAL;
+  if (!h || !ms || reps <= 0 || which < 0 || which > 3) return PERC_EINVAL;
   if (!h->assembled) return PERC_ESTATE;
   hipSetDevice(h->device);
   h->assembled = which == 0;  // the CG kernels clobber the solver vectors
