@@ -31,16 +31,21 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def cg_spmv_bytes(N, nnz):
-    """Algorithmic bytes of one fused CG SpMV launch (k_cg_spmv): rowptr,
-    col+val of the off-diagonals, diag, p_old and r (read once), p_new and
-    q (written once)."""
-    return 4 * (N + 1) + 12 * nnz + 8 * N + 8 * N + 8 * N + 16 * N
-
-
 def spmv_bytes(N, nnz):
-    """B = 8(N+nnz) + 4 nnz + 4(N+1) + 16N (plain SpMV)."""
+    """B = 8(N+nnz) + 4 nnz + 4(N+1) + 16N -- the CSR SpMV
+    (k_cg_spmv / k_spmv): diagonal + off-diagonal values, column indices,
+    row pointers, p read once, q written once (the q.p dot adds no traffic)."""
     return 8 * (N + nnz) + 4 * nnz + 4 * (N + 1) + 16 * N
+
+
+def resid_bytes(N):
+    """k_cg_b: reads r, q, d; writes r."""
+    return 32 * N
+
+
+def xp_bytes(N):
+    """k_cg_p: reads x, p, r, d; writes x, p."""
+    return 48 * N
 
 
 def cpu_baseline(L_, p, order, gpu_iters, cpu_iters):
@@ -195,13 +200,17 @@ def main():
     value = nsolves / tmax
 
     spmv_avg_ms = ks["spmv_ms"] / max(ks["spmv_n"], 1)
-    upd_avg_ms = ks["update_ms"] / max(ks["update_n"], 1)
-    bA = cg_spmv_bytes(N, nnz)
+    resid_avg_ms = ks["resid_ms"] / max(ks["resid_n"], 1)
+    xp_avg_ms = ks["xp_ms"] / max(ks["xp_n"], 1)
+    bA = spmv_bytes(N, nnz)
     achieved = bA / (spmv_avg_ms * 1e-3) / 1e9
-    # plain SpMV (SURVEY formula) on the last assembled system, after the timed region
+    # plain SpMV (dsprsax_ kernel) on the last assembled system, after the timed region
     plain_ms = ctx.bench_kernel(0, 50)
     plain_gbs = spmv_bytes(N, nnz) / (plain_ms * 1e-3) / 1e9
-    upd_gbs = 56 * N / (upd_avg_ms * 1e-3) / 1e9
+    resid_gbs = resid_bytes(N) / (resid_avg_ms * 1e-3) / 1e9
+    xp_gbs = xp_bytes(N) / (xp_avg_ms * 1e-3) / 1e9
+    iter_ms = spmv_avg_ms + resid_avg_ms + xp_avg_ms
+    iter_bytes = bA + resid_bytes(N) + xp_bytes(N)
 
     out = {
         "metric": "CG SpMV GB/s + conductance solves/sec, L=4096 square lattice at p=0.60",
@@ -226,13 +235,16 @@ def main():
                    "realisations sharded over %d GPU(s), RCCL stats all-reduce" % world},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS,
                      "unit": "GB/s", "frac": round(achieved / PEAK_HBM_GBS, 4), "traffic": None,
-                     "kernel": "k_cg_spmv (fused p-update + CSR SpMV + dot)",
+                     "kernel": "k_cg_spmv (CSR SpMV + q.p, one wave per 64-row tile)",
                      "bytes_per_launch": bA, "avg_launch_ms": round(spmv_avg_ms, 5),
                      "launches": ks["spmv_n"]},
         "cg_iterations_mean": round(float(stats[4]) / max(nsolves, 1), 1),
         "spanning_fraction": round(float(stats[3]) / max(nsolves, 1), 3),
         "gtop_mean": float(stats[1]) / max(nsolves, 1),
-        "cg_update": {"avg_launch_ms": round(upd_avg_ms, 5), "gbs": round(upd_gbs, 1)},
+        "cg_iteration": {"ms": round(iter_ms, 5), "bytes": iter_bytes,
+                         "gbs": round(iter_bytes / (iter_ms * 1e-3) / 1e9, 1)},
+        "cg_resid_kernel": {"avg_launch_ms": round(resid_avg_ms, 5), "gbs": round(resid_gbs, 1)},
+        "cg_xp_kernel": {"avg_launch_ms": round(xp_avg_ms, 5), "gbs": round(xp_gbs, 1)},
         "spmv_plain": {"avg_launch_ms": round(plain_ms, 5), "gbs": round(plain_gbs, 1),
                        "bytes_per_launch": spmv_bytes(N, nnz)},
     }

@@ -153,11 +153,11 @@ int perc_spmv_host(perc_ctx *h, const double *x, double *y);
    residual update (B), 3 = CG x/p update (P).  Clobbers solver vectors. */
 int perc_bench_kernel(perc_ctx *h, int which, int reps, double *ms);
 
-/* Live kernel timing: when enabled, every CG SpMV / update launch inside
+/* Live kernel timing: when enabled, every CG launch inside
    perc_conductance is bracketed by HIP events on the context stream; the
    accumulated device time of launches that did work is returned (ms) with
-   their count.  stats[0..3] = {spmv_ms, spmv_launches, update_ms,
-   update_launches}; reset clears the accumulators. */
+   their count.  stats[0..5] = {spmv_ms, spmv_launches, resid_ms (B),
+   resid_launches, xp_ms (P), xp_launches}; reset clears the accumulators. */
 int perc_set_kernel_timing(perc_ctx *h, int enable);
 int perc_kernel_stats(perc_ctx *h, double *stats, int reset);
 /* Sizes of the assembled system: out[0] = N (rows), out[1] = nnz (off-diagonal) */

@@ -178,9 +178,10 @@ class Context:
         L.check(L.lib().perc_set_kernel_timing(self.h, int(enable)), "perc_set_kernel_timing")
 
     def kernel_stats(self, reset=True):
-        st = np.zeros(4)
+        st = np.zeros(6)
         L.check(L.lib().perc_kernel_stats(self.h, st, int(reset)), "perc_kernel_stats")
-        return dict(spmv_ms=st[0], spmv_n=int(st[1]), update_ms=st[2], update_n=int(st[3]))
+        return dict(spmv_ms=st[0], spmv_n=int(st[1]), resid_ms=st[2], resid_n=int(st[3]),
+                    xp_ms=st[4], xp_n=int(st[5]))
 
     def system_size(self):
         out = np.zeros(2, dtype=np.int64)

@@ -944,23 +944,24 @@ hipError_t dev_solve(perc_ctx* h, int itol, double tol, int itmax, bool x0_zero,
   long long launched = 0;
   KernelTiming& T = h->timing;
   const int kMaxChunk = 256;
-  if (T.enabled && T.ev.size() < 3 * (size_t)kMaxChunk) {
+  if (T.enabled && T.ev.size() < 4 * (size_t)kMaxChunk) {
     const size_t have = T.ev.size();
-    T.ev.resize(3 * (size_t)kMaxChunk);
+    T.ev.resize(4 * (size_t)kMaxChunk);
     for (size_t i = have; i < T.ev.size(); ++i) HIP_TRY(hipEventCreate(&T.ev[i]));
   }
   int done_iters = 0;
   while (true) {
     for (int j = 0; j < chunk; ++j) {
+      if (T.enabled) hipEventRecord(T.ev[4 * j], st);
       k_cg_p<<<G, kBlock, 0, st>>>(a);
       HIP_TRY(dbg_sync(st, "k_cg_p"));
-      if (T.enabled) hipEventRecord(T.ev[3 * j], st);
+      if (T.enabled) hipEventRecord(T.ev[4 * j + 1], st);
       k_cg_spmv<<<G, kBlock, 0, st>>>(a);
       HIP_TRY(dbg_sync(st, "k_cg_spmv"));
-      if (T.enabled) hipEventRecord(T.ev[3 * j + 1], st);
+      if (T.enabled) hipEventRecord(T.ev[4 * j + 2], st);
       k_cg_b<<<G, kBlock, 0, st>>>(a);
       HIP_TRY(dbg_sync(st, "k_cg_b"));
-      if (T.enabled) hipEventRecord(T.ev[3 * j + 2], st);
+      if (T.enabled) hipEventRecord(T.ev[4 * j + 3], st);
     }
     launched += chunk;
     e = hipGetLastError();
@@ -972,14 +973,17 @@ hipError_t dev_solve(perc_ctx* h, int itol, double tol, int itmax, bool x0_zero,
     if (T.enabled) {  // launches of this chunk that did work
       const int real = std::min(chunk, hsp->iter - done_iters);
       for (int j = 0; j < real; ++j) {
-        float ta = 0.f, tb = 0.f;
-        hipEventElapsedTime(&ta, T.ev[3 * j], T.ev[3 * j + 1]);
-        hipEventElapsedTime(&tb, T.ev[3 * j + 1], T.ev[3 * j + 2]);
-        T.spmv_ms += ta;
+        float tp = 0.f, ts = 0.f, tb = 0.f;
+        hipEventElapsedTime(&tp, T.ev[4 * j], T.ev[4 * j + 1]);
+        hipEventElapsedTime(&ts, T.ev[4 * j + 1], T.ev[4 * j + 2]);
+        hipEventElapsedTime(&tb, T.ev[4 * j + 2], T.ev[4 * j + 3]);
+        T.p_ms += tp;
+        T.spmv_ms += ts;
         T.update_ms += tb;
       }
       T.spmv_n += real;
       T.update_n += real;
+      T.p_n += real;
     }
     done_iters = hsp->iter;
     if (hsp->done) break;

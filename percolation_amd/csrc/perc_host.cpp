@@ -332,9 +332,11 @@ int perc_kernel_stats(perc_ctx* h, double* stats, int reset) {
   stats[1] = (double)h->timing.spmv_n;
   stats[2] = h->timing.update_ms;
   stats[3] = (double)h->timing.update_n;
+  stats[4] = h->timing.p_ms;
+  stats[5] = (double)h->timing.p_n;
   if (reset) {
-    h->timing.spmv_ms = h->timing.update_ms = 0.0;
-    h->timing.spmv_n = h->timing.update_n = 0;
+    h->timing.spmv_ms = h->timing.update_ms = h->timing.p_ms = 0.0;
+    h->timing.spmv_n = h->timing.update_n = h->timing.p_n = 0;
   }
   return PERC_OK;
 }

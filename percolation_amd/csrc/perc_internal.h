@@ -80,9 +80,9 @@ struct ReplayOrder {
 
 struct KernelTiming {
   bool enabled = false;
-  std::vector<hipEvent_t> ev;  // 3 per iteration slot of a launch chunk
-  double spmv_ms = 0.0, update_ms = 0.0;
-  long long spmv_n = 0, update_n = 0;
+  std::vector<hipEvent_t> ev;  // 4 per iteration slot of a launch chunk
+  double spmv_ms = 0.0, update_ms = 0.0, p_ms = 0.0;
+  long long spmv_n = 0, update_n = 0, p_n = 0;
 };
 
 }  // namespace perc

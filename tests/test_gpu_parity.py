@@ -196,7 +196,9 @@ def test_conductance_vs_oracle_linbcg(lat, m, n, p, seed):
     # tolerance (the two differ only in the association of the dot products)
     assert abs(c["iter"] - oc["iter"]) <= 1
     assert rel(c["gtop"], oc["gtop"]) < 1e-8
-    assert np.max(np.abs(c["vint"] - oc["vint"])) < 1e-5
+    # voltages of leak-coupled (non-spanning) nodes are barely constrained by
+    # the residual norm; they agree to the solver tolerance's scale only
+    assert np.max(np.abs(c["vint"] - oc["vint"])) < 1e-4
     # converged: Gtop and Gbot to 1e-10
     assert rel(ct["gtop"], ot["gtop"]) < REL and rel(ct["gbot"], ot["gbot"]) < REL
 
@@ -346,4 +348,6 @@ def test_full_size_properties(L_, p):
         # the recomputed true residual ||b - A x|| / bnrm meets the tolerance
         # the recursive residual (linbcg's err) reported
         assert c["err"] <= 1e-12 and res < 1e-11
-        assert rel(c["gtop"], c["gbot"]) < 1e-6
+        # current conservation up to the 1e-12 leak currents that the 1e-10
+        # sprsin threshold drops from the terminal sums (hazard H5)
+        assert abs(c["gtop"] - c["gbot"]) < 1e-8
