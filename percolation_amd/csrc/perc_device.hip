@@ -422,38 +422,77 @@ __device__ __forceinline__ void wave_lds_sync() {
 
 // One 64-row tile: returns q(i) for this lane's row (0 if r >= N) and adds
 // q(i)*x(i) to *dot when DOT.
+// Memory-level parallelism: the tile's row pointers arrive with the previous
+// tile (prefetch), and all kMaxNnzRow (col, val) slots of a lane are loaded
+// back to back with clamped indices (no per-slot branch, so hipcc issues them
+// together and waits once), then all x gathers, then the products.  Slots
+// past the tile's entries recompute the last entry into LDS slots no row
+// reads (col/val are padded by 8 entries for the empty-tile case).
 template <bool DOT>
 __device__ __forceinline__ void spmv_tile(const CsrView& A, const double* __restrict__ x,
-                                          double* __restrict__ y, int r0, double* s_prod,
-                                          double* dot) {
+                                          double* __restrict__ y, int r0, int a, int b,
+                                          double* s_prod, double* dot) {
   const int lane = threadIdx.x & 63;
   const int r = r0 + lane;
   const bool valid = r < A.N;
   const int last = min(63, A.N - 1 - r0);
-  const int a = valid ? A.rowptr[r] : 0;
-  const int b = valid ? A.rowptr[r + 1] : 0;
   const int e0 = __shfl(a, 0, 64);
   const int ne = __shfl(b, last, 64) - e0;
-  const bool staged = ne <= 64 * kMaxNnzRow;
-  if (staged) {
-    for (int j = lane; j < ne; j += 64) {
-      const int c = A.col[e0 + j];
-      s_prod[j] = A.val[e0 + j] * x[c];
+  const double xi = valid ? x[r] : 0.0;
+  const double di = valid ? A.diag[r] : 0.0;
+  if (ne <= 64 * kMaxNnzRow) {
+    const int jmax = max(ne - 1, 0);
+    int c[kMaxNnzRow];
+    double v[kMaxNnzRow], xv[kMaxNnzRow];
+#pragma unroll
+    for (int s = 0; s < kMaxNnzRow; ++s) {
+      const int j = min(lane + 64 * s, jmax);
+      c[s] = A.col[e0 + j];
+      v[s] = A.val[e0 + j];
     }
+#pragma unroll
+    for (int s = 0; s < kMaxNnzRow; ++s) xv[s] = x[c[s]];
+#pragma unroll
+    for (int s = 0; s < kMaxNnzRow; ++s) s_prod[lane + 64 * s] = v[s] * xv[s];
     wave_lds_sync();
-  }
-  if (valid) {
-    const double xi = x[r];
-    double acc = A.diag[r] * xi;
-    if (staged) {
+    if (valid) {
+      double acc = di * xi;
       for (int k = a - e0; k < b - e0; ++k) acc = acc + s_prod[k];
-    } else {
-      for (int k = a; k < b; ++k) acc = acc + A.val[k] * x[A.col[k]];
+      y[r] = acc;
+      if (DOT) *dot = *dot + acc * xi;
     }
+    wave_lds_sync();  // s_prod reused by the next tile
+  } else if (valid) {  // rows longer than the LDS stage (general NR matrices)
+    double acc = di * xi;
+    for (int k = a; k < b; ++k) acc = acc + A.val[k] * x[A.col[k]];
     y[r] = acc;
     if (DOT) *dot = *dot + acc * xi;
   }
-  if (staged) wave_lds_sync();  // s_prod reused by the next tile
+}
+
+// a wave's tiles tile0, tile0+stride, ... < t1, row pointers prefetched one
+// tile ahead
+template <bool DOT>
+__device__ __forceinline__ void spmv_tiles(const CsrView& A, const double* __restrict__ x,
+                                           double* __restrict__ y, int tile0, int t1, int stride,
+                                           double* s_prod, double* dot) {
+  const int lane = threadIdx.x & 63;
+  int a = 0, b = 0;
+  if (tile0 < t1) {
+    const int r = tile0 * 64 + lane;
+    if (r < A.N) { a = A.rowptr[r]; b = A.rowptr[r + 1]; }
+  }
+  for (int tile = tile0; tile < t1; tile += stride) {
+    int an = 0, bn = 0;
+    const int nt = tile + stride;
+    if (nt < t1) {
+      const int r = nt * 64 + lane;
+      if (r < A.N) { an = A.rowptr[r]; bn = A.rowptr[r + 1]; }
+    }
+    spmv_tile<DOT>(A, x, y, tile * 64, a, b, s_prod, dot);
+    a = an;
+    b = bn;
+  }
 }
 
 // wave tiles [t0, t1) of a logical block, strided over its 4 waves
@@ -472,8 +511,7 @@ __global__ __launch_bounds__(kBlock) void k_spmv(CsrView A, const double* __rest
   int t0, t1;
   block_tiles(A.N, &t0, &t1);
   double dummy = 0.0;
-  for (int tile = t0 + wid; tile < t1; tile += kWaves)
-    spmv_tile<false>(A, x, y, tile * 64, s_prod[wid], &dummy);
+  spmv_tiles<false>(A, x, y, t0 + wid, t1, kWaves, s_prod[wid], &dummy);
 }
 
 // ---------------------------------------------------------------------------
@@ -525,33 +563,43 @@ __global__ __launch_bounds__(kBlock) void k_cg_p(CGArgs a) {
   const int N = a.A.N;
   int q0, q1;
   block_pairs(N, &q0, &q1);
-  for (int j = q0 + threadIdx.x; j < q1; j += kBlock) {
-    const int i = 2 * j;
-    if (i + 1 < N) {
+  const int qf = min(q1, N / 2);  // full pairs; an odd tail row is done below
+  if (first) {
+#pragma unroll 4
+    for (int j = q0 + threadIdx.x; j < qf; j += kBlock) {
+      const int i = 2 * j;
       const double2 rv = *reinterpret_cast<const double2*>(r + i);
       const double2 dv = *reinterpret_cast<const double2*>(d + i);
       double2 pn;
-      if (first) {
-        pn.x = rv.x / dv.x;
-        pn.y = rv.y / dv.y;
-      } else {
-        const double2 pv = *reinterpret_cast<const double2*>(p + i);
-        double2 xv = *reinterpret_cast<const double2*>(x + i);
-        xv.x = xv.x + ak * pv.x;
-        xv.y = xv.y + ak * pv.y;
-        *reinterpret_cast<double2*>(x + i) = xv;
-        pn.x = bk * pv.x + rv.x / dv.x;
-        pn.y = bk * pv.y + rv.y / dv.y;
-      }
+      pn.x = rv.x / dv.x;
+      pn.y = rv.y / dv.y;
       *reinterpret_cast<double2*>(p + i) = pn;
+    }
+  } else {
+#pragma unroll 4
+    for (int j = q0 + threadIdx.x; j < qf; j += kBlock) {
+      const int i = 2 * j;
+      const double2 rv = *reinterpret_cast<const double2*>(r + i);
+      const double2 dv = *reinterpret_cast<const double2*>(d + i);
+      const double2 pv = *reinterpret_cast<const double2*>(p + i);
+      double2 xv = *reinterpret_cast<const double2*>(x + i);
+      xv.x = xv.x + ak * pv.x;
+      xv.y = xv.y + ak * pv.y;
+      *reinterpret_cast<double2*>(x + i) = xv;
+      double2 pn;
+      pn.x = bk * pv.x + rv.x / dv.x;
+      pn.y = bk * pv.y + rv.y / dv.y;
+      *reinterpret_cast<double2*>(p + i) = pn;
+    }
+  }
+  if ((N & 1) && q1 > N / 2 && threadIdx.x == 0) {
+    const int i = N - 1;
+    const double z = r[i] / d[i];
+    if (first) {
+      p[i] = z;
     } else {
-      const double z = r[i] / d[i];
-      if (first) {
-        p[i] = z;
-      } else {
-        x[i] = x[i] + ak * p[i];
-        p[i] = bk * p[i] + z;
-      }
+      x[i] = x[i] + ak * p[i];
+      p[i] = bk * p[i] + z;
     }
   }
   // bkden = bknum once every workgroup has read it (linbcg :800)
@@ -573,8 +621,7 @@ __global__ __launch_bounds__(kBlock) void k_cg_spmv(CGArgs a) {
   int t0, t1;
   block_tiles(a.A.N, &t0, &t1);
   double dot[1] = {0.0};
-  for (int tile = t0 + wid; tile < t1; tile += kWaves)
-    spmv_tile<true>(a.A, a.p, a.q, tile * 64, s_prod[wid], &dot[0]);
+  spmv_tiles<true>(a.A, a.p, a.q, t0 + wid, t1, kWaves, s_prod[wid], &dot[0]);
   double tot[1];
   if (publish_and_reduce<1>(dot, a.partials, &a.tickets[0], xcd_logical_block(blockIdx.x, gridDim.x),
                             gridDim.x, tot, s_red, &s_flag)) {
@@ -599,27 +646,29 @@ __global__ __launch_bounds__(kBlock) void k_cg_b(CGArgs a) {
   int q0, q1;
   block_pairs(N, &q0, &q1);
   double acc[2] = {0.0, 0.0};  // z.r, r.r
-  for (int j = q0 + threadIdx.x; j < q1; j += kBlock) {
+  const int qf = min(q1, N / 2);
+#pragma unroll 4
+  for (int j = q0 + threadIdx.x; j < qf; j += kBlock) {
     const int i = 2 * j;
-    if (i + 1 < N) {
-      const double2 qv = *reinterpret_cast<const double2*>(q + i);
-      const double2 dv = *reinterpret_cast<const double2*>(d + i);
-      double2 rv = *reinterpret_cast<const double2*>(r + i);
-      rv.x = rv.x - ak * qv.x;
-      rv.y = rv.y - ak * qv.y;
-      *reinterpret_cast<double2*>(r + i) = rv;
-      const double z0 = rv.x / dv.x, z1 = rv.y / dv.y;
-      acc[0] = acc[0] + z0 * rv.x;
-      acc[0] = acc[0] + z1 * rv.y;
-      acc[1] = acc[1] + rv.x * rv.x;
-      acc[1] = acc[1] + rv.y * rv.y;
-    } else {
-      const double rn = r[i] - ak * q[i];
-      r[i] = rn;
-      const double z0 = rn / d[i];
-      acc[0] = acc[0] + z0 * rn;
-      acc[1] = acc[1] + rn * rn;
-    }
+    const double2 qv = *reinterpret_cast<const double2*>(q + i);
+    const double2 dv = *reinterpret_cast<const double2*>(d + i);
+    double2 rv = *reinterpret_cast<const double2*>(r + i);
+    rv.x = rv.x - ak * qv.x;
+    rv.y = rv.y - ak * qv.y;
+    *reinterpret_cast<double2*>(r + i) = rv;
+    const double z0 = rv.x / dv.x, z1 = rv.y / dv.y;
+    acc[0] = acc[0] + z0 * rv.x;
+    acc[0] = acc[0] + z1 * rv.y;
+    acc[1] = acc[1] + rv.x * rv.x;
+    acc[1] = acc[1] + rv.y * rv.y;
+  }
+  if ((N & 1) && q1 > N / 2 && threadIdx.x == 0) {
+    const int i = N - 1;
+    const double rn = r[i] - ak * q[i];
+    r[i] = rn;
+    const double z0 = rn / d[i];
+    acc[0] = acc[0] + z0 * rn;
+    acc[1] = acc[1] + rn * rn;
   }
   double tot[2];
   if (publish_and_reduce<2>(acc, a.partials + (size_t)gridDim.x, &a.tickets[1],
