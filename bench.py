@@ -31,21 +31,31 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def spmv_bytes(N, nnz):
-    """B = 8(N+nnz) + 4 nnz + 4(N+1) + 16N -- the CSR SpMV
-    (k_cg_spmv / k_spmv): diagonal + off-diagonal values, column indices,
-    row pointers, p read once, q written once (the q.p dot adds no traffic)."""
-    return 8 * (N + nnz) + 4 * nnz + 4 * (N + 1) + 16 * N
+def spmv_bytes(N, nnz, fmt):
+    """Algorithmic bytes of one SpMV (k_cg_spmv / k_spmv), p read once and q
+    written once (the q.p dot adds no traffic).
+    csr: SURVEY.md §8(d) B = 8(N+nnz) + 4 nnz + 4(N+1) + 16N -- diagonal and
+         off-diagonal values, column indices, row pointers, p, q;
+    stencil: a 2-byte code per row + p + q = 18N (columns, values and the
+         diagonal are rebuilt from the code and the row-form table)."""
+    if fmt == "csr":
+        return 8 * (N + nnz) + 4 * nnz + 4 * (N + 1) + 16 * N
+    return 18 * N
 
 
-def resid_bytes(N):
-    """k_cg_b: reads r, q, d; writes r."""
-    return 32 * N
+def resid_bytes(N, fmt):
+    """k_cg_b: reads r, q and d (csr: 8 B diag, stencil: 2 B code); writes r."""
+    return 32 * N if fmt == "csr" else 26 * N
 
 
-def xp_bytes(N):
-    """k_cg_p: reads x, p, r, d; writes x, p."""
-    return 48 * N
+def xp_bytes(N, fmt):
+    """k_cg_p: reads x, p, r and d (csr: 8 B, stencil: 2 B); writes x, p."""
+    return 48 * N if fmt == "csr" else 42 * N
+
+
+KERNELS = {"spmv": "k_cg_spmv (SpMV q = A p + q.p dot)",
+           "resid": "k_cg_b (r -= ak q, z = r/d, z.r and r.r dots)",
+           "xp": "k_cg_p (x += ak p, p = bk p + r/d)"}
 
 
 def cpu_baseline(L_, p, order, gpu_iters, cpu_iters):
@@ -114,6 +124,8 @@ def main():
     ap.add_argument("--cpu-iters", type=int, default=20)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--occupancy", choices=("uniform", "reference"), default="uniform")
+    ap.add_argument("--format", choices=("auto", "stencil", "csr"), default="auto",
+                    help="solver operator format (perc_set_matrix_format)")
     args = ap.parse_args()
 
     import torch
@@ -158,6 +170,8 @@ def main():
     log("rank %d: %d orders (nb=%d, tbonds=%d) in %.1fs" % (rank, nreal, nb, tb,
                                                             time.perf_counter() - t0))
     ctx = api.Context(0, L_, L_, 0, device=local)
+    ctx.set_matrix_format({"auto": P.FMT_AUTO, "stencil": P.FMT_STENCIL,
+                           "csr": P.FMT_CSR}[args.format])
     N, nnz = ctx.system_size()
 
     def run(k):
@@ -199,18 +213,39 @@ def main():
     nsolves = int(stats[0])
     value = nsolves / tmax
 
-    spmv_avg_ms = ks["spmv_ms"] / max(ks["spmv_n"], 1)
-    resid_avg_ms = ks["resid_ms"] / max(ks["resid_n"], 1)
-    xp_avg_ms = ks["xp_ms"] / max(ks["xp_n"], 1)
-    bA = spmv_bytes(N, nnz)
-    achieved = bA / (spmv_avg_ms * 1e-3) / 1e9
-    # plain SpMV (dsprsax_ kernel) on the last assembled system, after the timed region
-    plain_ms = ctx.bench_kernel(0, 50)
-    plain_gbs = spmv_bytes(N, nnz) / (plain_ms * 1e-3) / 1e9
-    resid_gbs = resid_bytes(N) / (resid_avg_ms * 1e-3) / 1e9
-    xp_gbs = xp_bytes(N) / (xp_avg_ms * 1e-3) / 1e9
-    iter_ms = spmv_avg_ms + resid_avg_ms + xp_avg_ms
-    iter_bytes = bA + resid_bytes(N) + xp_bytes(N)
+    fmt = "stencil" if ctx.matrix_format() == P.FMT_STENCIL else "csr"
+    # per-kernel live timing (HIP events on the context stream around every
+    # launch that did work, over the timed realisations)
+    kern = {}
+    for key, nbytes in (("spmv", spmv_bytes(N, nnz, fmt)), ("resid", resid_bytes(N, fmt)),
+                        ("xp", xp_bytes(N, fmt))):
+        n_ = max(ks[key + "_n"], 1)
+        avg = ks[key + "_ms"] / n_
+        kern[key] = {"kernel": KERNELS[key], "avg_launch_ms": round(avg, 5),
+                     "launches": ks[key + "_n"], "total_ms": round(ks[key + "_ms"], 1),
+                     "bytes_per_launch": nbytes,
+                     "gbs": round(nbytes / (avg * 1e-3) / 1e9, 1)}
+    # the roofline line is the kernel with the most device time
+    dom = max(kern, key=lambda k_: kern[k_]["total_ms"])
+    achieved = kern[dom]["bytes_per_launch"] / (kern[dom]["avg_launch_ms"] * 1e-3) / 1e9
+    iter_ms = sum(v["avg_launch_ms"] for v in kern.values())
+    iter_bytes = sum(v["bytes_per_launch"] for v in kern.values())
+    # after the timed region, on the last assembled system: each kernel in
+    # both operator formats, back to back (perc_bench_kernel; clobbers x)
+    probe = {}
+    for fname, fcode in (("stencil", P.FMT_STENCIL), ("csr", P.FMT_CSR)):
+        try:
+            ctx.set_matrix_format(fcode)
+        except Exception:
+            continue
+        row = {}
+        for key, which, nbytes in (("spmv_plain", 0, spmv_bytes(N, nnz, fname)),
+                                   ("spmv", 1, spmv_bytes(N, nnz, fname)),
+                                   ("resid", 2, resid_bytes(N, fname)),
+                                   ("xp", 3, xp_bytes(N, fname))):
+            ms = ctx.bench_kernel(which, 50)
+            row[key] = {"ms": round(ms, 5), "gbs": round(nbytes / (ms * 1e-3) / 1e9, 1)}
+        probe[fname] = row
 
     out = {
         "metric": "CG SpMV GB/s + conductance solves/sec, L=4096 square lattice at p=0.60",
@@ -235,18 +270,17 @@ def main():
                    "realisations sharded over %d GPU(s), RCCL stats all-reduce" % world},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS,
                      "unit": "GB/s", "frac": round(achieved / PEAK_HBM_GBS, 4), "traffic": None,
-                     "kernel": "k_cg_spmv (CSR SpMV + q.p, one wave per 64-row tile)",
-                     "bytes_per_launch": bA, "avg_launch_ms": round(spmv_avg_ms, 5),
-                     "launches": ks["spmv_n"]},
+                     "kernel": kern[dom]["kernel"], "format": fmt,
+                     "bytes_per_launch": kern[dom]["bytes_per_launch"],
+                     "avg_launch_ms": kern[dom]["avg_launch_ms"],
+                     "launches": kern[dom]["launches"]},
         "cg_iterations_mean": round(float(stats[4]) / max(nsolves, 1), 1),
         "spanning_fraction": round(float(stats[3]) / max(nsolves, 1), 3),
         "gtop_mean": float(stats[1]) / max(nsolves, 1),
         "cg_iteration": {"ms": round(iter_ms, 5), "bytes": iter_bytes,
                          "gbs": round(iter_bytes / (iter_ms * 1e-3) / 1e9, 1)},
-        "cg_resid_kernel": {"avg_launch_ms": round(resid_avg_ms, 5), "gbs": round(resid_gbs, 1)},
-        "cg_xp_kernel": {"avg_launch_ms": round(xp_avg_ms, 5), "gbs": round(xp_gbs, 1)},
-        "spmv_plain": {"avg_launch_ms": round(plain_ms, 5), "gbs": round(plain_gbs, 1),
-                       "bytes_per_launch": spmv_bytes(N, nnz)},
+        "cg_kernels": kern,
+        "kernel_probe": probe,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         log("cpu baseline: oracle on a bounded sample ...")

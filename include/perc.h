@@ -163,6 +163,23 @@ int perc_kernel_stats(perc_ctx *h, double *stats, int reset);
 /* Sizes of the assembled system: out[0] = N (rows), out[1] = nnz (off-diagonal) */
 int perc_system_size(perc_ctx *h, long long *out);
 
+/* Operator format of the solver.  The Kirchhoff matrix of a lattice has two
+   distinct off-diagonal values (-g0 inside the spanning component, -leak
+   elsewhere, bondc.f:482-538) on a fixed stencil, so besides the CSR copy
+   the assembly writes one byte per row (bit j = "in" for the j-th sorted
+   neighbour slot) and the SpMV/CG kernels rebuild each row -- values,
+   diagonal and summation order -- from that byte: bitwise the same numbers
+   as the CSR path from ~1/4 of its bytes.  PERC_FMT_AUTO (default) uses the
+   stencil operator whenever every stencil bond exists; the NR symbols
+   (sprsin_/linbcg_) always use CSR. */
+#define PERC_FMT_AUTO 0
+#define PERC_FMT_CSR 1
+#define PERC_FMT_STENCIL 2
+int perc_set_matrix_format(perc_ctx *h, int fmt);
+/* format the solver kernels use on the assembled system (PERC_FMT_CSR or
+   PERC_FMT_STENCIL) */
+int perc_matrix_format(perc_ctx *h);
+
 /* ---- one hot-path realisation (bench / ensemble) ---------------------- */
 typedef struct {
   perc_label_info label;

@@ -23,6 +23,7 @@ SQUARE, TRIANGULAR = 0, 1
 BOND, SITE, SITEBOND = 0, 1, 2
 RULE_BOND, RULE_SITE, RULE_MIXED = 0, 1, 2
 CUR_FORTRAN, CUR_MATLAB = 0, 1
+FMT_AUTO, FMT_CSR, FMT_STENCIL = 0, 1, 2
 
 
 class LabelInfo(C.Structure):
@@ -79,6 +80,8 @@ SIGNATURES = {
     "perc_set_kernel_timing": (C.c_int, [_VP, C.c_int]),
     "perc_kernel_stats": (C.c_int, [_VP, _D, C.c_int]),
     "perc_system_size": (C.c_int, [_VP, np.ctypeslib.ndpointer(dtype=np.int64)]),
+    "perc_set_matrix_format": (C.c_int, [_VP, C.c_int]),
+    "perc_matrix_format": (C.c_int, [_VP]),
     "perc_stats_accumulate": (None, [_D, C.c_int, C.c_double, C.c_int, C.c_int]),
     "sprsin_": (None, [_VP] * 7),
     "dsprsax_": (None, [_VP] * 5),

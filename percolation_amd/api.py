@@ -183,6 +183,16 @@ class Context:
         return dict(spmv_ms=st[0], spmv_n=int(st[1]), resid_ms=st[2], resid_n=int(st[3]),
                     xp_ms=st[4], xp_n=int(st[5]))
 
+    def set_matrix_format(self, fmt):
+        """PERC_FMT_AUTO / PERC_FMT_CSR / PERC_FMT_STENCIL (perc.h)."""
+        L.check(L.lib().perc_set_matrix_format(self.h, int(fmt)), "perc_set_matrix_format")
+
+    def matrix_format(self):
+        rc = L.lib().perc_matrix_format(self.h)
+        if rc < 0:
+            L.check(rc, "perc_matrix_format")
+        return rc
+
     def system_size(self):
         out = np.zeros(2, dtype=np.int64)
         L.check(L.lib().perc_system_size(self.h, out), "perc_system_size")

@@ -72,36 +72,85 @@ __device__ __forceinline__ double load_sc1(const double* p) {
       __HIP_MEMORY_SCOPE_AGENT));
 }
 
-// Publish this workgroup's NV partials at partials[j*nwg + lb]; returns true
-// in every thread of the last-arriving workgroup, which then holds the totals
-// in tot[] (all threads).  Must be called by all threads of the workgroup.
+// Two-level ticket reduction.  Workgroups form groups of kGroup consecutive
+// logical ids, each group counting arrivals on its own 128-B counter line
+// (one device-scope counter per 64 arrivals instead of one for the whole
+// grid: same-address device-scope atomics serialise at ~12 ns each,
+// MI355X_MICROARCH.md 'fanin').  The last arriver of a group sums that
+// group's partials (wave 0, lanes in index order, butterfly) and publishes
+// the group partial; the last group sums the group partials.  Every sum has
+// a fixed order, whichever workgroup happens to arrive last.
+constexpr int kGroup = 64;
+constexpr int kTicketStride = 32;  // unsigned per counter (128 B)
+constexpr int kRedSlots = 3;       // 0: S (q.p), 1: B (z.r, r.r), 2: prologue
+
+__host__ __device__ inline int red_groups(int nwg) { return (nwg + kGroup - 1) / kGroup; }
+// per slot: NV<=2 values for nwg partials and for the group partials
+__host__ __device__ inline size_t red_partials_size(int nwg) {
+  return 2 * ((size_t)nwg + red_groups(nwg));
+}
+__host__ __device__ inline size_t red_tickets_size(int nwg) {
+  return ((size_t)red_groups(nwg) + 1) * kTicketStride;
+}
+
+// Publish this workgroup's NV partials; returns true in every thread of the
+// one workgroup that finishes the reduction, which then holds the totals in
+// tot[] (all threads).  Must be called by all threads of the workgroup.
 template <int NV>
-__device__ bool publish_and_reduce(double (&v)[NV], double* partials, unsigned* ticket, int lb,
+__device__ bool publish_and_reduce(double (&v)[NV], double* partials, unsigned* tickets, int lb,
                                    int nwg, double (&tot)[NV], double* s_red, int* s_flag) {
   block_sum<NV>(v, s_red);
+  const int ngroups = red_groups(nwg);
+  const int grp = lb / kGroup, g0 = grp * kGroup, gn = min(kGroup, nwg - g0);
+  double* gpart = partials + (size_t)NV * nwg;
   if (threadIdx.x == 0) {
 #pragma unroll
-    for (int j = 0; j < NV; ++j) store_sc1(&partials[j * nwg + lb], v[j]);
+    for (int j = 0; j < NV; ++j) store_sc1(&partials[(size_t)j * nwg + lb], v[j]);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    unsigned tk = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    *s_flag = (tk == (unsigned)(nwg - 1));
+    const unsigned tk = __hip_atomic_fetch_add(&tickets[grp * kTicketStride], 1u,
+                                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_flag[0] = tk == (unsigned)(gn - 1);
   }
   __syncthreads();
-  if (!*s_flag) return false;
-  // last arriver: every thread sums a fixed strided subset in index order
+  if (!s_flag[0]) return false;
+  // last of its group: wave 0 sums the group's partials
+  if (threadIdx.x < 64) {
+    const int lane = threadIdx.x;
+    double w[NV];
+#pragma unroll
+    for (int j = 0; j < NV; ++j) {
+      w[j] = lane < gn ? load_sc1(&partials[(size_t)j * nwg + g0 + lane]) : 0.0;
+      w[j] = wave_sum(w[j]);
+    }
+    if (lane == 0) {
+#pragma unroll
+      for (int j = 0; j < NV; ++j) store_sc1(&gpart[(size_t)j * ngroups + grp], w[j]);
+      __hip_atomic_store(&tickets[grp * kTicketStride], 0u, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const unsigned tk = __hip_atomic_fetch_add(&tickets[ngroups * kTicketStride], 1u,
+                                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      s_flag[1] = tk == (unsigned)(ngroups - 1);
+    }
+  }
+  __syncthreads();
+  if (!s_flag[1]) return false;
+  // last group: every thread sums a strided subset of the group partials in
+  // index order, then the block tree
   double acc[NV];
 #pragma unroll
   for (int j = 0; j < NV; ++j) acc[j] = 0.0;
-  for (int i = threadIdx.x; i < nwg; i += blockDim.x) {
+  for (int i = threadIdx.x; i < ngroups; i += blockDim.x) {
 #pragma unroll
-    for (int j = 0; j < NV; ++j) acc[j] = acc[j] + load_sc1(&partials[j * nwg + i]);
+    for (int j = 0; j < NV; ++j) acc[j] = acc[j] + load_sc1(&gpart[(size_t)j * ngroups + i]);
   }
   __syncthreads();  // s_red reuse
   block_sum<NV>(acc, s_red);
   if (threadIdx.x == 0) {
 #pragma unroll
     for (int j = 0; j < NV; ++j) s_red[16 + j] = acc[j];
-    __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&tickets[ngroups * kTicketStride], 0u, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
   }
   __syncthreads();
 #pragma unroll
@@ -315,8 +364,9 @@ __device__ __forceinline__ double bond_value(int rule, int id, int s, int c, int
 
 __global__ void k_assemble(Geom g, int N, const int* bond_first, const uint8_t* bocc,
                            const uint8_t* socc, const int* parent, const int* rowptr,
-                           double* val, double* diag, double* rhs, int rule, double g0,
-                           double leak, double Va, int span_root) {
+                           double* val, double* diag, double* rhs, uint16_t* code, int* sflag,
+                           StencilForms F, int rule, double g0, double leak, double Va,
+                           int span_root) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= N) return;
   const int m = g.m, t = g.t, s = i + m + 1;
@@ -325,14 +375,30 @@ __global__ void k_assemble(Geom g, int N, const int* bond_first, const uint8_t* 
   const int cnt = sorted_neighbours(g, s, nbr);
   double rowsum = 0.0;  // bondc.f:500-504: ascending-column dense row sum
   int k = rowptr[i];
+  unsigned bits = 0;
   for (int j = 0; j < cnt; ++j) {
     const int c = nbr[j];
     const int id = s < c ? bond_id(g, bond_first, s, c) : bond_id(g, bond_first, c, s);
-    if (id < 0) continue;
+    if (id < 0) {  // no bond in this slot: the stencil operator cannot be used
+      atomicOr(sflag, 1);
+      continue;
+    }
     const double gv = bond_value(rule, id, s, c, ps, bocc, socc, span_root, g0, leak);
+    if (gv == -g0) bits |= 1u << j;
     rowsum = rowsum + gv;
     if (c > m && c <= t - m) val[k++] = gv;
   }
+  int form = -1;  // the row's form: same count and offsets
+  for (int f = 0; f < F.nforms && form < 0; ++f) {
+    bool same = F.cnt[f] == cnt;
+    for (int j = 0; j < cnt && same; ++j) same = F.off[f][j] == nbr[j] - s;
+    if (same) form = f;
+  }
+  if (form < 0) {
+    atomicOr(sflag, 2);
+    form = 0;
+  }
+  code[i] = (uint16_t)(bits | (unsigned)cnt << 8 | (unsigned)form << 11);
   diag[i] = -rowsum;
   // RHS in bond-list order (bondc.f:490-497)
   double acc = 0.0;
@@ -515,6 +581,149 @@ __global__ __launch_bounds__(kBlock) void k_spmv(CsrView A, const double* __rest
 }
 
 // ---------------------------------------------------------------------------
+// Stencil-coded operator (PERC_FMT_STENCIL).  Row i of the interior system is
+// lattice site s = i+m+1; its off-diagonals are the sorted neighbours of s
+// that are interior sites (sprsin's column scan), each -g0 or -leak, and
+// diag(i) = -(sum of all slots' values in sorted order) (bondc.f:499-505).
+// A row's sorted neighbour offsets (c - s) take one of a few "forms" per
+// lattice (interior / edge columns, up / down triangles); the assembly stores
+//   code[i] = slot "in" bits (0..5) | slot count << 8 | form id << 11
+// and the kernels rebuild the row -- column i+off, value, diagonal, and the
+// summation order -- from the code and the form table (staged in LDS), so
+// y(i), z(i) = r(i)/d(i) etc. are bitwise the CSR path's, with no lattice
+// arithmetic in the loop.
+struct StencilView {
+  int N;
+  const uint16_t* code;
+  double ng0, nleak;  // -g0, -leak
+  StencilForms F;
+};
+
+__device__ __forceinline__ double code_diag(unsigned c, double ng0, double nleak) {
+  const int cnt = (c >> 8) & 7;
+  double rs = 0.0;
+#pragma unroll
+  for (int j = 0; j < kMaxSlots; ++j)
+    if (j < cnt) rs = rs + (((c >> j) & 1u) ? ng0 : nleak);
+  return -rs;
+}
+
+// stage the form offsets in LDS (all threads call; ends with a barrier)
+__device__ __forceinline__ void load_forms(const StencilForms& F, int* s_off) {
+  if (threadIdx.x < kMaxForms * kMaxSlots)
+    s_off[threadIdx.x] = F.off[threadIdx.x / kMaxSlots][threadIdx.x % kMaxSlots];
+  __syncthreads();
+}
+
+// y(i) for rows base + k*kBlock (k < R) of [.., i1): codes first, then all
+// gathers, then the row sums in the reference order.  S = slots per row
+// (4 square, 6 triangular).  Adds y(i)*x(i) to *dot in k order when DOT.
+// d(i)*x(i) + sum over used slots of value*x(col), in slot order
+template <int S>
+__device__ __forceinline__ double st_combine(unsigned c, const double (&xv)[S],
+                                             const bool (&use)[S], double xi, double ng0,
+                                             double nleak) {
+  const int cnt = (c >> 8) & 7;
+  double gv[S];
+  double rs = 0.0;
+#pragma unroll
+  for (int j = 0; j < S; ++j) {
+    gv[j] = ((c >> j) & 1u) ? ng0 : nleak;
+    if (j < cnt) rs = rs + gv[j];
+  }
+  double acc = (-rs) * xi;
+#pragma unroll
+  for (int j = 0; j < S; ++j) {
+    const double pr = gv[j] * xv[j];
+    acc = use[j] ? acc + pr : acc;
+  }
+  return acc;
+}
+
+template <int S, int R, bool DOT>
+__device__ __forceinline__ void st_rows(const StencilView& A, const int* s_off,
+                                        const double* __restrict__ x, double* __restrict__ y,
+                                        int base, int i1, double* dot) {
+  const int N = A.N;
+  unsigned c[R];
+#pragma unroll
+  for (int k = 0; k < R; ++k) {
+    const int i = base + k * kBlock;
+    c[k] = i < i1 ? A.code[i] : 0u;
+  }
+  double xv[R][S], xi[R];
+  bool use[R][S];
+#pragma unroll
+  for (int k = 0; k < R; ++k) {
+    const int i = base + k * kBlock;
+    const int ii = i < i1 ? i : base;  // rows past the end: cnt 0, harmless loads
+    const int f = c[k] >> 11, cnt = (c[k] >> 8) & 7;
+#pragma unroll
+    for (int j = 0; j < S; ++j) {
+      const int col = ii + s_off[f * kMaxSlots + j];
+      use[k][j] = j < cnt && (unsigned)col < (unsigned)N;
+      xv[k][j] = x[use[k][j] ? col : ii];
+    }
+    xi[k] = x[ii];
+  }
+#pragma unroll
+  for (int k = 0; k < R; ++k) {
+    const int i = base + k * kBlock;
+    if (i < i1) {
+      const double acc = st_combine<S>(c[k], xv[k], use[k], xi[k], A.ng0, A.nleak);
+      y[i] = acc;
+      if (DOT) *dot = *dot + acc * xi[k];
+    }
+  }
+}
+
+// one row, for the non-hot callers (CG prologue with x0 != 0)
+__device__ __forceinline__ double st_rowval(const StencilView& A, const int* s_off,
+                                            const double* __restrict__ x, int i) {
+  const unsigned c = A.code[i];
+  const int f = c >> 11, cnt = (c >> 8) & 7;
+  double xv[kMaxSlots];
+  bool use[kMaxSlots];
+#pragma unroll
+  for (int j = 0; j < kMaxSlots; ++j) {
+    const int col = i + s_off[f * kMaxSlots + j];
+    use[j] = j < cnt && (unsigned)col < (unsigned)A.N;
+    xv[j] = x[use[j] ? col : i];
+  }
+  return st_combine<kMaxSlots>(c, xv, use, x[i], A.ng0, A.nleak);
+}
+
+constexpr int kStRowsPerThread = 8;  // rows of a thread per CG workgroup
+constexpr int kStBatch = 4;          // rows in flight per thread
+
+// contiguous row range of the logical block
+__device__ __forceinline__ void block_rows(int N, int* i0, int* i1) {
+  const int lb = xcd_logical_block(blockIdx.x, gridDim.x);
+  const int chunk = cdiv(N, gridDim.x);
+  *i0 = lb * chunk;
+  *i1 = min(*i0 + chunk, N);
+}
+
+template <int S, bool DOT>
+__device__ __forceinline__ void st_block(const StencilView& A, const int* s_off,
+                                         const double* __restrict__ x, double* __restrict__ y,
+                                         double* dot) {
+  int i0, i1;
+  block_rows(A.N, &i0, &i1);
+  for (int base = i0 + threadIdx.x; base < i1; base += kBlock * kStBatch)
+    st_rows<S, kStBatch, DOT>(A, s_off, x, y, base, i1, dot);
+}
+
+template <int S>
+__global__ __launch_bounds__(kBlock) void k_spmv_st(StencilView A, const double* __restrict__ x,
+                                                    double* __restrict__ y) {
+  __shared__ int s_off[kMaxForms * kMaxSlots];
+  load_forms(A.F, s_off);
+  double dummy = 0.0;
+  st_block<S, false>(A, s_off, x, y, &dummy);
+}
+
+// ---------------------------------------------------------------------------
 // Jacobi-PCG in linbcg's order (bondc.f:780-835; A symmetric, so rr==r,
 // pp==p, zz==z and dsprstx==dsprsax bitwise).  Iteration k is three launches
 //   P(k): x += ak(k-1) p(k-1)  [deferred from iteration k-1]
@@ -526,6 +735,7 @@ __global__ __launch_bounds__(kBlock) void k_spmv(CsrView A, const double* __rest
 // any number of iterations; launches after the stop are no-ops.
 struct CGArgs {
   CsrView A;
+  StencilView St;
   const double* rhs;
   double* x;
   double* r;
@@ -538,6 +748,23 @@ struct CGArgs {
   int err_hist_cap;
 };
 
+// diagonal of rows i, i+1 (i even) from the CSR diag array or the stencil code
+template <bool ST>
+__device__ __forceinline__ double2 diag2(const CGArgs& a, int i) {
+  if (ST) {
+    const unsigned cc = *reinterpret_cast<const unsigned*>(a.St.code + i);
+    double2 d;
+    d.x = code_diag(cc & 0xffffu, a.St.ng0, a.St.nleak);
+    d.y = code_diag(cc >> 16, a.St.ng0, a.St.nleak);
+    return d;
+  }
+  return *reinterpret_cast<const double2*>(a.A.diag + i);
+}
+template <bool ST>
+__device__ __forceinline__ double diag1(const CGArgs& a, int i) {
+  return ST ? code_diag(a.St.code[i], a.St.ng0, a.St.nleak) : a.A.diag[i];
+}
+
 // contiguous, even-aligned pair range of the logical block (16 B accesses)
 __device__ __forceinline__ void block_pairs(int N, int* q0, int* q1) {
   const int npair = (N + 1) / 2;
@@ -547,19 +774,16 @@ __device__ __forceinline__ void block_pairs(int N, int* q0, int* q1) {
   *q1 = min(*q0 + chunk, npair);
 }
 
+template <bool ST>
 __global__ __launch_bounds__(kBlock) void k_cg_p(CGArgs a) {
   CGScalars* S = a.S;
   if (S->done) return;
-  __shared__ double s_red[32];
-  __shared__ int s_flag;
-  const int k = S->iter + 1;
-  const bool first = k == 1;
-  const double bk = first ? 0.0 : S->bknum / S->bkden;
+  const bool first = S->iter == 0;
+  const double bk = S->bk;  // bknum/bkden, formed by the previous B
   const double ak = S->ak;
   double* __restrict__ x = a.x;
   double* __restrict__ p = a.p;
   const double* __restrict__ r = a.r;
-  const double* __restrict__ d = a.A.diag;
   const int N = a.A.N;
   int q0, q1;
   block_pairs(N, &q0, &q1);
@@ -569,7 +793,7 @@ __global__ __launch_bounds__(kBlock) void k_cg_p(CGArgs a) {
     for (int j = q0 + threadIdx.x; j < qf; j += kBlock) {
       const int i = 2 * j;
       const double2 rv = *reinterpret_cast<const double2*>(r + i);
-      const double2 dv = *reinterpret_cast<const double2*>(d + i);
+      const double2 dv = diag2<ST>(a, i);
       double2 pn;
       pn.x = rv.x / dv.x;
       pn.y = rv.y / dv.y;
@@ -580,7 +804,7 @@ __global__ __launch_bounds__(kBlock) void k_cg_p(CGArgs a) {
     for (int j = q0 + threadIdx.x; j < qf; j += kBlock) {
       const int i = 2 * j;
       const double2 rv = *reinterpret_cast<const double2*>(r + i);
-      const double2 dv = *reinterpret_cast<const double2*>(d + i);
+      const double2 dv = diag2<ST>(a, i);
       const double2 pv = *reinterpret_cast<const double2*>(p + i);
       double2 xv = *reinterpret_cast<const double2*>(x + i);
       xv.x = xv.x + ak * pv.x;
@@ -594,7 +818,7 @@ __global__ __launch_bounds__(kBlock) void k_cg_p(CGArgs a) {
   }
   if ((N & 1) && q1 > N / 2 && threadIdx.x == 0) {
     const int i = N - 1;
-    const double z = r[i] / d[i];
+    const double z = r[i] / diag1<ST>(a, i);
     if (first) {
       p[i] = z;
     } else {
@@ -602,29 +826,31 @@ __global__ __launch_bounds__(kBlock) void k_cg_p(CGArgs a) {
       p[i] = bk * p[i] + z;
     }
   }
-  // bkden = bknum once every workgroup has read it (linbcg :800)
-  double none[1] = {0.0}, tot[1];
-  if (publish_and_reduce<1>(none, a.partials + 3 * (size_t)gridDim.x, &a.tickets[3],
-                            xcd_logical_block(blockIdx.x, gridDim.x), gridDim.x, tot, s_red,
-                            &s_flag)) {
-    if (threadIdx.x == 0) S->bkden = S->bknum;
-  }
 }
 
+// S(k): q = A p and akden = q.p, then ak = bknum/akden.  SL = 0: CSR,
+// SL = 4 / 6: stencil operator with that many slots per row.
+template <int SL>
 __global__ __launch_bounds__(kBlock) void k_cg_spmv(CGArgs a) {
   CGScalars* S = a.S;
   if (S->done) return;
-  __shared__ double s_prod[kWaves][64 * kMaxNnzRow];
+  __shared__ double s_prod[SL ? 1 : kWaves][SL ? 1 : 64 * kMaxNnzRow];
+  __shared__ int s_off[kMaxForms * kMaxSlots];
   __shared__ double s_red[32];
-  __shared__ int s_flag;
-  const int wid = threadIdx.x >> 6;
-  int t0, t1;
-  block_tiles(a.A.N, &t0, &t1);
+  __shared__ int s_flag[2];
   double dot[1] = {0.0};
-  spmv_tiles<true>(a.A, a.p, a.q, t0 + wid, t1, kWaves, s_prod[wid], &dot[0]);
+  if (SL) {
+    load_forms(a.St.F, s_off);
+    st_block<SL ? SL : 4, true>(a.St, s_off, a.p, a.q, &dot[0]);
+  } else {
+    const int wid = threadIdx.x >> 6;
+    int t0, t1;
+    block_tiles(a.A.N, &t0, &t1);
+    spmv_tiles<true>(a.A, a.p, a.q, t0 + wid, t1, kWaves, s_prod[SL ? 0 : wid], &dot[0]);
+  }
   double tot[1];
-  if (publish_and_reduce<1>(dot, a.partials, &a.tickets[0], xcd_logical_block(blockIdx.x, gridDim.x),
-                            gridDim.x, tot, s_red, &s_flag)) {
+  if (publish_and_reduce<1>(dot, a.partials, a.tickets, xcd_logical_block(blockIdx.x, gridDim.x),
+                            gridDim.x, tot, s_red, s_flag)) {
     if (threadIdx.x == 0) {
       S->akden = tot[0];
       S->ak = S->bknum / tot[0];
@@ -632,15 +858,15 @@ __global__ __launch_bounds__(kBlock) void k_cg_spmv(CGArgs a) {
   }
 }
 
+template <bool ST>
 __global__ __launch_bounds__(kBlock) void k_cg_b(CGArgs a) {
   CGScalars* S = a.S;
   if (S->done) return;
   __shared__ double s_red[32];
-  __shared__ int s_flag;
+  __shared__ int s_flag[2];
   const int k = S->iter + 1;
   const double ak = S->ak;
   const double* __restrict__ q = a.q;
-  const double* __restrict__ d = a.A.diag;
   double* __restrict__ r = a.r;
   const int N = a.A.N;
   int q0, q1;
@@ -651,7 +877,7 @@ __global__ __launch_bounds__(kBlock) void k_cg_b(CGArgs a) {
   for (int j = q0 + threadIdx.x; j < qf; j += kBlock) {
     const int i = 2 * j;
     const double2 qv = *reinterpret_cast<const double2*>(q + i);
-    const double2 dv = *reinterpret_cast<const double2*>(d + i);
+    const double2 dv = diag2<ST>(a, i);
     double2 rv = *reinterpret_cast<const double2*>(r + i);
     rv.x = rv.x - ak * qv.x;
     rv.y = rv.y - ak * qv.y;
@@ -666,16 +892,18 @@ __global__ __launch_bounds__(kBlock) void k_cg_b(CGArgs a) {
     const int i = N - 1;
     const double rn = r[i] - ak * q[i];
     r[i] = rn;
-    const double z0 = rn / d[i];
+    const double z0 = rn / diag1<ST>(a, i);
     acc[0] = acc[0] + z0 * rn;
     acc[1] = acc[1] + rn * rn;
   }
   double tot[2];
-  if (publish_and_reduce<2>(acc, a.partials + (size_t)gridDim.x, &a.tickets[1],
+  if (publish_and_reduce<2>(acc, a.partials + red_partials_size(gridDim.x),
+                            a.tickets + red_tickets_size(gridDim.x),
                             xcd_logical_block(blockIdx.x, gridDim.x), gridDim.x, tot, s_red,
-                            &s_flag)) {
+                            s_flag)) {
     if (threadIdx.x == 0) {
       const double err = sqrt(tot[1]) / S->bnrm;
+      S->bk = tot[0] / S->bknum;  // next iteration's bknum/bkden (linbcg :799)
       S->bknum = tot[0];
       S->err = err;
       if (k - 1 < a.err_hist_cap) a.err_hist[k - 1] = err;
@@ -695,36 +923,46 @@ __global__ __launch_bounds__(kBlock) void k_cg_xfinal(CGArgs a) {
 
 // r = b - A x (or r = b when x = 0), then bnrm and the first bknum
 // (linbcg prologue, bondc.f:758-779)
+template <bool ST>
 __global__ __launch_bounds__(kBlock) void k_cg_init(CGArgs a, int itol, int x0_zero) {
   __shared__ double s_red[32];
-  __shared__ int s_flag;
+  __shared__ int s_flag[2];
+  __shared__ int s_off[kMaxForms * kMaxSlots];
+  if (ST) load_forms(a.St.F, s_off);
   const double* __restrict__ b = a.rhs;
-  const double* __restrict__ d = a.A.diag;
   const int N = a.A.N;
   const int lb = xcd_logical_block(blockIdx.x, gridDim.x);
-  const int chunk = cdiv(N, gridDim.x);
-  const int i0 = lb * chunk, i1 = min(i0 + chunk, N);
+  int i0, i1;
+  block_rows(N, &i0, &i1);
   double acc[2] = {0.0, 0.0};  // bnrm^2, z.r
   for (int i = i0 + threadIdx.x; i < i1; i += kBlock) {
+    const double di = diag1<ST>(a, i);
     double ax = 0.0;
     if (!x0_zero) {
       const double* x = a.x;
-      ax = d[i] * x[i];
-      for (int j = a.A.rowptr[i]; j < a.A.rowptr[i + 1]; ++j) ax = ax + a.A.val[j] * x[a.A.col[j]];
+      if (ST) {
+        ax = st_rowval(a.St, s_off, x, i);
+      } else {
+        ax = di * x[i];
+        for (int j = a.A.rowptr[i]; j < a.A.rowptr[i + 1]; ++j) ax = ax + a.A.val[j] * x[a.A.col[j]];
+      }
     }
     const double ri = b[i] - ax;
     a.r[i] = ri;
-    const double zb = itol == 1 ? b[i] : b[i] / d[i];
+    const double zb = itol == 1 ? b[i] : b[i] / di;
     acc[0] = acc[0] + zb * zb;
-    const double zr = ri / d[i];
+    const double zr = ri / di;
     acc[1] = acc[1] + zr * ri;
   }
   double tot[2];
-  if (publish_and_reduce<2>(acc, a.partials, &a.tickets[2], lb, gridDim.x, tot, s_red, &s_flag)) {
+  if (publish_and_reduce<2>(acc, a.partials + 2 * red_partials_size(gridDim.x),
+                            a.tickets + 2 * red_tickets_size(gridDim.x), lb, gridDim.x, tot, s_red,
+                            s_flag)) {
     if (threadIdx.x == 0) {
       a.S->bnrm = sqrt(tot[0]);
       a.S->bknum = tot[1];
       a.S->bkden = 1.0;
+      a.S->bk = 0.0;
       a.S->ak = 0.0;
       a.S->iter = 0;
       a.S->done = 0;
@@ -740,6 +978,7 @@ __global__ void k_zero(double* v, long long n) {
 CGArgs make_cg_args(perc_ctx* h) {
   CGArgs a;
   a.A = CsrView{h->N, h->d.rowptr, h->d.col, h->d.val, h->d.diag};
+  a.St = StencilView{h->N, h->d.code, h->st_ng0, h->st_nleak, h->forms};
   a.rhs = h->d.rhs;
   a.x = h->d.x;
   a.r = h->d.r;
@@ -753,6 +992,45 @@ CGArgs make_cg_args(perc_ctx* h) {
   return a;
 }
 
+void launch_cg_spmv(perc_ctx* h, const CGArgs& a, int G) {
+  if (!h->stencil) k_cg_spmv<0><<<G, kBlock, 0, h->stream>>>(a);
+  else if (h->g.scn == 4) k_cg_spmv<4><<<G, kBlock, 0, h->stream>>>(a);
+  else k_cg_spmv<6><<<G, kBlock, 0, h->stream>>>(a);
+}
+
+void launch_spmv(perc_ctx* h, const CGArgs& a, const double* x, double* y) {
+  if (!h->stencil) k_spmv<<<h->grid, kBlock, 0, h->stream>>>(a.A, x, y);
+  else if (h->g.scn == 4) k_spmv_st<4><<<h->grid, kBlock, 0, h->stream>>>(a.St, x, y);
+  else k_spmv_st<6><<<h->grid, kBlock, 0, h->stream>>>(a.St, x, y);
+}
+
+// Row forms of the interior system (sorted neighbour offsets c - s).  A
+// row's form depends only on its column and the parity of its lattice row,
+// so the first two interior rows hold every form; the assembly checks each
+// row against the table anyway (sflag bit 2).
+StencilForms stencil_forms(const Geom& g) {
+  StencilForms F{};
+  const int rows = std::min(2, g.n - 2);
+  for (int r = 1; r <= rows; ++r)
+    for (int cx = 0; cx < g.m; ++cx) {
+      const int s = r * g.m + cx + 1;
+      int nb[6];
+      const int cnt = sorted_neighbours(g, s, nb);
+      int f = 0;
+      for (; f < F.nforms; ++f) {
+        bool same = F.cnt[f] == cnt;
+        for (int j = 0; j < cnt && same; ++j) same = F.off[f][j] == nb[j] - s;
+        if (same) break;
+      }
+      if (f < F.nforms) continue;
+      if (F.nforms == kMaxForms) return StencilForms{};  // no stencil operator
+      F.cnt[f] = cnt;
+      for (int j = 0; j < kMaxSlots; ++j) F.off[f][j] = j < cnt ? nb[j] - s : 0;
+      ++F.nforms;
+    }
+  return F;
+}
+
 // PERC_SYNC_DEBUG=1: synchronise after each launch and name the failing one
 hipError_t dbg_sync(hipStream_t st, const char* name) {
   static const bool on = getenv("PERC_SYNC_DEBUG") != nullptr;
@@ -764,6 +1042,13 @@ hipError_t dbg_sync(hipStream_t st, const char* name) {
 }
 
 inline dim3 blocks_for(long long n) { return dim3((unsigned)((n + kBlock - 1) / kBlock)); }
+
+// fixed CG grid (the dot-product reduction order depends on it): about
+// kStRowsPerThread rows per thread, at most kMaxCgGrid workgroups
+constexpr int kMaxCgGrid = 8192;
+inline int cg_grid(int N) {
+  return std::max(1, std::min(cdiv(N, (long long)kBlock * kStRowsPerThread), kMaxCgGrid));
+}
 
 template <typename T>
 hipError_t dmalloc(T** p, size_t n) {
@@ -817,6 +1102,9 @@ hipError_t dev_build_lattice(perc_ctx* h) {
   HIP_TRY(hipGetLastError());
   HIP_TRY(dmalloc(&d.diag, N + 2));
   HIP_TRY(dmalloc(&d.rhs, N + 2));
+  HIP_TRY(dmalloc(&d.code, (size_t)N + 8));
+  h->forms = stencil_forms(g);
+  HIP_TRY(dmalloc(&d.sflag, 4));
   // occupancy + labeling
   HIP_TRY(dmalloc(&d.bocc, (size_t)h->nb + 8));
   HIP_TRY(dmalloc(&d.socc, t + 8));
@@ -833,11 +1121,10 @@ hipError_t dev_build_lattice(perc_ctx* h) {
   HIP_TRY(dmalloc(&d.p0, nv));
   HIP_TRY(dmalloc(&d.p1, nv));
   HIP_TRY(dmalloc(&d.q, nv));
-  const int nrb = cdiv(N, kRowsPerTile);
-  h->grid = std::max(1, std::min(nrb, 2048));
-  HIP_TRY(dmalloc(&d.partials, 4 * (size_t)h->grid));
-  HIP_TRY(dmalloc(&d.tickets, 8));
-  HIP_TRY(hipMemset(d.tickets, 0, 8 * sizeof(unsigned)));
+  h->grid = cg_grid(N);
+  HIP_TRY(dmalloc(&d.partials, kRedSlots * red_partials_size(h->grid)));
+  HIP_TRY(dmalloc(&d.tickets, kRedSlots * red_tickets_size(h->grid)));
+  HIP_TRY(hipMemset(d.tickets, 0, kRedSlots * red_tickets_size(h->grid) * sizeof(unsigned)));
   HIP_TRY(dmalloc(&d.scal, 1));
   HIP_TRY(dmalloc(&d.iout, 2 * (size_t)g.m));
   HIP_TRY(hipMemset(d.bocc, 0, (size_t)h->nb + 8));
@@ -860,17 +1147,17 @@ hipError_t dev_alloc_matrix(perc_ctx* h, int N, long long nnz) {
   HIP_TRY(dmalloc(&d.p0, nv));
   HIP_TRY(dmalloc(&d.p1, nv));
   HIP_TRY(dmalloc(&d.q, nv));
-  h->grid = std::max(1, std::min(cdiv(N, kRowsPerTile), 2048));
-  HIP_TRY(dmalloc(&d.partials, 4 * (size_t)h->grid));
-  HIP_TRY(dmalloc(&d.tickets, 8));
-  HIP_TRY(hipMemset(d.tickets, 0, 8 * sizeof(unsigned)));
+  h->grid = cg_grid(N);
+  HIP_TRY(dmalloc(&d.partials, kRedSlots * red_partials_size(h->grid)));
+  HIP_TRY(dmalloc(&d.tickets, kRedSlots * red_tickets_size(h->grid)));
+  HIP_TRY(hipMemset(d.tickets, 0, kRedSlots * red_tickets_size(h->grid) * sizeof(unsigned)));
   HIP_TRY(dmalloc(&d.scal, 1));
   return hipSuccess;
 }
 
 void dev_free_all(perc_ctx* h) {
   DeviceBuffers& d = h->d;
-  void* ptrs[] = {d.bond_first, d.rowptr, d.col, d.val, d.diag, d.rhs, d.bocc, d.socc,
+  void* ptrs[] = {d.bond_first, d.rowptr, d.col, d.val, d.diag, d.rhs, d.code, d.sflag, d.bocc, d.socc,
                   d.order, d.parent, d.member, d.bot, d.top, d.counters, d.x, d.r,
                   d.p0, d.p1, d.q, d.partials, d.tickets, d.scal, d.err_hist, d.iout};
   for (void* p : ptrs)
@@ -957,10 +1244,20 @@ hipError_t dev_canon(perc_ctx* h, int* canon_out) {
 
 hipError_t dev_assemble(perc_ctx* h, int rule, double g0, double leak, double Va, int span_root) {
   DeviceBuffers& d = h->d;
-  k_assemble<<<blocks_for(h->N), kBlock, 0, h->stream>>>(h->g, h->N, d.bond_first, d.bocc, d.socc,
-                                                          d.parent, d.rowptr, d.val, d.diag, d.rhs,
-                                                          rule, g0, leak, Va, span_root);
-  return dbg_sync(h->stream, "k_assemble");
+  hipStream_t st = h->stream;
+  HIP_TRY(hipMemsetAsync(d.sflag, 0, 4 * sizeof(int), st));
+  k_assemble<<<blocks_for(h->N), kBlock, 0, st>>>(h->g, h->N, d.bond_first, d.bocc, d.socc,
+                                                   d.parent, d.rowptr, d.val, d.diag, d.rhs, d.code,
+                                                   d.sflag, h->forms, rule, g0, leak, Va, span_root);
+  HIP_TRY(dbg_sync(st, "k_assemble"));
+  int flag = 0;
+  HIP_TRY(hipMemcpyAsync(&flag, d.sflag, sizeof(int), hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipStreamSynchronize(st));
+  h->st_ng0 = -g0;
+  h->st_nleak = -leak;
+  h->stencil_ok = flag == 0 && h->forms.nforms > 0;
+  h->stencil = h->fmt_req != PERC_FMT_CSR && h->stencil_ok;
+  return hipSuccess;
 }
 
 hipError_t dev_solve(perc_ctx* h, int itol, double tol, int itmax, bool x0_zero, int* iter,
@@ -977,13 +1274,15 @@ hipError_t dev_solve(perc_ctx* h, int itol, double tol, int itmax, bool x0_zero,
   hs.itmax = itmax;
   hs.bkden = 1.0;
   HIP_TRY(hipMemcpyAsync(d.scal, &hs, sizeof(hs), hipMemcpyHostToDevice, st));
-  HIP_TRY(hipMemsetAsync(d.tickets, 0, 8 * sizeof(unsigned), st));
+  HIP_TRY(hipMemsetAsync(d.tickets, 0, kRedSlots * red_tickets_size(h->grid) * sizeof(unsigned), st));
   if (x0_zero) {
     k_zero<<<blocks_for(h->N + 2), kBlock, 0, st>>>(d.x, h->N + 2);
   }
   CGArgs a = make_cg_args(h);
   const int G = h->grid;
-  k_cg_init<<<G, kBlock, 0, st>>>(a, itol, x0_zero ? 1 : 0);
+  const bool ST = h->stencil;
+  if (ST) k_cg_init<true><<<G, kBlock, 0, st>>>(a, itol, x0_zero ? 1 : 0);
+  else k_cg_init<false><<<G, kBlock, 0, st>>>(a, itol, x0_zero ? 1 : 0);
   HIP_TRY(dbg_sync(st, "k_cg_init"));
   // iterate in chunks; the device flag makes surplus launches no-ops
   int chunk = 8;
@@ -1002,13 +1301,15 @@ hipError_t dev_solve(perc_ctx* h, int itol, double tol, int itmax, bool x0_zero,
   while (true) {
     for (int j = 0; j < chunk; ++j) {
       if (T.enabled) hipEventRecord(T.ev[4 * j], st);
-      k_cg_p<<<G, kBlock, 0, st>>>(a);
+      if (ST) k_cg_p<true><<<G, kBlock, 0, st>>>(a);
+      else k_cg_p<false><<<G, kBlock, 0, st>>>(a);
       HIP_TRY(dbg_sync(st, "k_cg_p"));
       if (T.enabled) hipEventRecord(T.ev[4 * j + 1], st);
-      k_cg_spmv<<<G, kBlock, 0, st>>>(a);
+      launch_cg_spmv(h, a, G);
       HIP_TRY(dbg_sync(st, "k_cg_spmv"));
       if (T.enabled) hipEventRecord(T.ev[4 * j + 2], st);
-      k_cg_b<<<G, kBlock, 0, st>>>(a);
+      if (ST) k_cg_b<true><<<G, kBlock, 0, st>>>(a);
+      else k_cg_b<false><<<G, kBlock, 0, st>>>(a);
       HIP_TRY(dbg_sync(st, "k_cg_b"));
       if (T.enabled) hipEventRecord(T.ev[4 * j + 3], st);
     }
@@ -1068,8 +1369,8 @@ hipError_t dev_spmv(perc_ctx* h, const double* x, double* y) {
   hipStream_t st = h->stream;
   const size_t bytes = sizeof(double) * h->N;
   HIP_TRY(hipMemcpyAsync(d.p0, x, bytes, hipMemcpyHostToDevice, st));
-  CsrView A{h->N, d.rowptr, d.col, d.val, d.diag};
-  k_spmv<<<h->grid, kBlock, 0, st>>>(A, d.p0, d.q);
+  CGArgs a = make_cg_args(h);
+  launch_spmv(h, a, d.p0, d.q);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipMemcpyAsync(y, d.q, bytes, hipMemcpyDeviceToHost, st));
   return hipStreamSynchronize(st);
@@ -1079,23 +1380,32 @@ hipError_t dev_bench(perc_ctx* h, int which, int reps, double* ms) {
   DeviceBuffers& d = h->d;
   hipStream_t st = h->stream;
   CGArgs a = make_cg_args(h);
-  CsrView A{h->N, d.rowptr, d.col, d.val, d.diag};
+  const bool ST = h->stencil;
   // scalars for a steady-state iteration (iter = 1 -> general p update)
   CGScalars hs{};
   hs.bknum = 1.0;
   hs.bkden = 2.0;
+  hs.bk = 0.5;
   hs.ak = 0.5;
   hs.bnrm = 1.0;
   hs.tol = -1.0;
   hs.itmax = 1 << 30;
   hs.iter = 1;
   HIP_TRY(hipMemcpyAsync(d.scal, &hs, sizeof(hs), hipMemcpyHostToDevice, st));
-  HIP_TRY(hipMemsetAsync(d.tickets, 0, 8 * sizeof(unsigned), st));
+  HIP_TRY(hipMemsetAsync(d.tickets, 0, kRedSlots * red_tickets_size(h->grid) * sizeof(unsigned), st));
   auto launch = [&]() {
-    if (which == 0) k_spmv<<<h->grid, kBlock, 0, st>>>(A, d.p0, d.q);
-    else if (which == 1) k_cg_spmv<<<h->grid, kBlock, 0, st>>>(a);
-    else if (which == 2) k_cg_b<<<h->grid, kBlock, 0, st>>>(a);
-    else k_cg_p<<<h->grid, kBlock, 0, st>>>(a);
+    const int G = h->grid;
+    if (which == 0) {
+      launch_spmv(h, a, d.p0, d.q);
+    } else if (which == 1) {
+      launch_cg_spmv(h, a, G);
+    } else if (which == 2) {
+      if (ST) k_cg_b<true><<<G, kBlock, 0, st>>>(a);
+      else k_cg_b<false><<<G, kBlock, 0, st>>>(a);
+    } else {
+      if (ST) k_cg_p<true><<<G, kBlock, 0, st>>>(a);
+      else k_cg_p<false><<<G, kBlock, 0, st>>>(a);
+    }
   };
   // the B kernel advances iter (tol < 0 keeps it running); values are
   // irrelevant for timing

@@ -505,6 +505,10 @@ int perc_conductance(perc_ctx* h, int rule, int cur_rule, double Va, double g0, 
   hipEventRecord(h->ev[0], st);
   hipError_t e = dev_assemble(h, rule, g0, leak, Va, h->span_root);
   if (e != hipSuccess) return hip_status(e, "perc_conductance/assemble");
+  if (h->fmt_req == PERC_FMT_STENCIL && !h->stencil_ok) {
+    set_error("perc_conductance: stencil operator requested but a stencil slot has no bond");
+    return PERC_EINVAL;
+  }
   hipEventRecord(h->ev[1], st);
   h->assembled = true;
   h->rule = rule;
@@ -570,11 +574,25 @@ int perc_spmv_host(perc_ctx* h, const double* x, double* y) {
   return hip_status(dev_spmv(h, x, y), "perc_spmv_host");
 }
 
+int perc_set_matrix_format(perc_ctx* h, int fmt) {
+  if (!h || fmt < PERC_FMT_AUTO || fmt > PERC_FMT_STENCIL) return PERC_EINVAL;
+  if (h->assembled && fmt == PERC_FMT_STENCIL && !h->stencil_ok) return PERC_EINVAL;
+  h->fmt_req = fmt;
+  if (h->assembled) h->stencil = fmt != PERC_FMT_CSR && h->stencil_ok;
+  return PERC_OK;
+}
+
+int perc_matrix_format(perc_ctx* h) {
+  if (!h) return PERC_EINVAL;
+  if (!h->assembled) return PERC_ESTATE;
+  return h->stencil ? PERC_FMT_STENCIL : PERC_FMT_CSR;
+}
+
 int perc_bench_kernel(perc_ctx* h, int which, int reps, double* ms) {
   if (!h || !ms || reps <= 0 || which < 0 || which > 3) return PERC_EINVAL;
   if (!h->assembled) return PERC_ESTATE;
   hipSetDevice(h->device);
-  h->assembled = which == 0;  // the CG kernels clobber the solver vectors
+  // the CG kernels clobber the solver vectors (x, r, p, q), not the system
   return hip_status(dev_bench(h, which, reps, ms), "perc_bench_kernel");
 }
 

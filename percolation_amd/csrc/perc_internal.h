@@ -15,6 +15,17 @@ namespace perc {
 constexpr int kBlock = 256;       // threads per workgroup (4 wave64)
 constexpr int kRowsPerTile = 256; // CSR rows staged per LDS tile
 constexpr int kMaxSpanList = 64;  // spanning roots recorded per labeling
+constexpr int kMaxForms = 8;      // stencil row forms per lattice
+constexpr int kMaxSlots = 6;      // neighbour slots per row
+
+// Sorted neighbour offsets (c - s) of each row form of the stencil operator
+// (interior / edge columns, up / down triangles): row i's columns are
+// i + off[f][j] for its form f (perc_device.hip, "Stencil-coded operator").
+struct StencilForms {
+  int nforms;
+  int cnt[kMaxForms];
+  int off[kMaxForms][kMaxSlots];
+};
 
 // Device-resident CG scalars (one cache line each group; written only by the
 // last-arriving workgroup of a kernel, read by the next kernel).
@@ -26,6 +37,7 @@ struct CGScalars {
   double bnrm;   // ||D^-1 b|| (itol 2) or ||b|| (itol 1)
   double err;    // last err
   double tol;
+  double bk;     // bknum / bkden for the coming p update (linbcg :799)
   int iter;      // completed iterations
   int itmax;
   int done;      // set once err <= tol or iter > itmax
@@ -42,6 +54,11 @@ struct DeviceBuffers {
   double* val = nullptr;  // nnz (+pad)
   double* diag = nullptr; // N
   double* rhs = nullptr;  // N
+  // stencil-coded operator: code[i] = slot bits (bit j: sorted neighbour
+  // slot j carries -g0, else -leak) | count << 8 | form << 11; sflag[0] != 0
+  // if some slot has no bond (1) or a row matches no form (2)
+  uint16_t* code = nullptr;  // N (+pad)
+  int* sflag = nullptr;      // 4
   // occupancy
   uint8_t* bocc = nullptr;  // nb
   uint8_t* socc = nullptr;  // t+1
@@ -104,6 +121,11 @@ struct perc_ctx {
   int span_root = 0;
   int perccln = 0;
   int rule = -1;
+  int fmt_req = PERC_FMT_AUTO;  // perc_set_matrix_format
+  bool stencil_ok = false;      // every stencil slot of the assembled system has a bond
+  bool stencil = false;         // solver kernels use the stencil operator
+  double st_ng0 = 0.0, st_nleak = 0.0;  // its two off-diagonal values
+  perc::StencilForms forms{};            // row forms of this lattice
   hipEvent_t ev[8];
   perc::KernelTiming timing;
 };

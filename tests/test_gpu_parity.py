@@ -118,8 +118,12 @@ def oracle_system(lat, m, n, pbc, b1, b2, gval):
     return sa, ija, itemp, diag, k
 
 
+FORMATS = [PL.FMT_STENCIL, PL.FMT_CSR]
+
+
+@pytest.mark.parametrize("fmt", FORMATS)
 @pytest.mark.parametrize("lat,m,n,pbc,p,seed", BOND_CASES[:4])
-def test_assembly_and_spmv_bitwise(lat, m, n, pbc, p, seed):
+def test_assembly_and_spmv_bitwise(lat, m, n, pbc, p, seed, fmt):
     b1, b2 = api.bond_list(lat, m, n, pbc)
     nb = len(b1)
     order = api.shuffled_ids(nb, seed)
@@ -128,7 +132,9 @@ def test_assembly_and_spmv_bitwise(lat, m, n, pbc, p, seed):
         ctx.occupy(PL.BOND, bond_order=order, nbonds_=tb)
         li = ctx.label()
         assert li["nspan"] >= 1
+        ctx.set_matrix_format(fmt)
         ctx.conductance(itmax=3)
+        assert ctx.matrix_format() == fmt
         sysm = ctx.system()
         ref = api.replay_labels(lat, m, n, pbc, PL.BOND, bond_order=order, nbond=tb)
         gval = O.f64(nb)
@@ -172,9 +178,10 @@ def test_bondc_against_reference(v):
         assert rel(r["gbot"], md["gbot"]) < 1e-6
 
 
+@pytest.mark.parametrize("fmt", FORMATS)
 @pytest.mark.parametrize("lat,m,n,p,seed", [(0, 128, 128, 0.6, 21), (1, 96, 96, 0.4, 22),
                                             (0, 200, 160, 0.55, 23)])
-def test_conductance_vs_oracle_linbcg(lat, m, n, p, seed):
+def test_conductance_vs_oracle_linbcg(lat, m, n, p, seed, fmt):
     """Larger lattices: oracle literal linbcg (CPU) vs fused GPU PCG."""
     b1, b2 = api.bond_list(lat, m, n, 0)
     nb = len(b1)
@@ -188,19 +195,58 @@ def test_conductance_vs_oracle_linbcg(lat, m, n, p, seed):
     oc = O.conductance(lat, m, n, 0, b1, b2, gval, itmax=100000)
     ot = O.conductance(lat, m, n, 0, b1, b2, gval, tol=1e-13, itmax=100000)
     with api.Context(lat, m, n, 0) as ctx:
+        ctx.set_matrix_format(fmt)
         ctx.occupy(PL.BOND, bond_order=order, nbonds_=tb)
         ctx.label()
         c = ctx.conductance(itmax=100000, vint=True)
+        assert ctx.matrix_format() == fmt
         ct = ctx.conductance(tol=1e-13, itmax=100000)
     # reference settings: same iteration count, answers agree to the solver
     # tolerance (the two differ only in the association of the dot products)
     assert abs(c["iter"] - oc["iter"]) <= 1
     assert rel(c["gtop"], oc["gtop"]) < 1e-8
-    # voltages of leak-coupled (non-spanning) nodes are barely constrained by
-    # the residual norm; they agree to the solver tolerance's scale only
-    assert np.max(np.abs(c["vint"] - oc["vint"])) < 1e-4
+    # voltages: tight on the spanning cluster's sites; nodes coupled only by
+    # the 1e-12 leak are barely constrained by the residual norm at tol 1e-8
+    # and agree to that scale only (their drift depends on the dot-product
+    # association)
+    t = m * n
+    on = np.zeros(t + 1, bool)
+    sel = ref["bond_label"] == ref["perccln"]
+    on[b1[sel]] = True
+    on[b2[sel]] = True
+    span = on[m + 1:t - m + 1]
+    dv = np.abs(c["vint"] - oc["vint"])
+    assert np.max(dv[span]) < 1e-6, np.max(dv[span])
+    assert np.max(dv) < 1e-3
     # converged: Gtop and Gbot to 1e-10
     assert rel(ct["gtop"], ot["gtop"]) < REL and rel(ct["gbot"], ot["gbot"]) < REL
+
+
+@pytest.mark.parametrize("lat,m,n,pbc,p", [(0, 300, 200, 0, 0.6), (0, 128, 96, 1, 0.55),
+                                           (1, 160, 120, 0, 0.4), (1, 128, 100, 1, 0.42)])
+def test_stencil_matches_csr_solver(lat, m, n, pbc, p):
+    """The stencil operator rebuilds the CSR numbers bitwise, so both formats
+    give the same iterates up to the association of the q.p dot (its
+    per-thread row order differs): same iteration count within 1, Gtop and
+    the voltages to the solver's precision, and bitwise-equal SpMVs."""
+    nb = api.nbonds(lat, m, n, pbc)
+    order = api.shuffled_ids(nb, 777)
+    out = {}
+    x = np.random.default_rng(5).standard_normal(m * n - 2 * m)
+    for fmt in FORMATS:
+        with api.Context(lat, m, n, pbc) as ctx:
+            ctx.set_matrix_format(fmt)
+            ctx.occupy(PL.BOND, bond_order=order, nbonds_=int(p * nb))
+            if ctx.label()["nspan"] == 0:
+                pytest.skip("no spanning cluster")
+            c = ctx.conductance(tol=1e-12, itmax=100000, vint=True)
+            assert ctx.matrix_format() == fmt
+            out[fmt] = (c, ctx.spmv(x))
+    (cs, ys), (cc, yc) = out[PL.FMT_STENCIL], out[PL.FMT_CSR]
+    assert np.array_equal(ys.view(np.uint64), yc.view(np.uint64))
+    assert abs(cs["iter"] - cc["iter"]) <= 1
+    assert rel(cs["gtop"], cc["gtop"]) < REL and rel(cs["gbot"], cc["gbot"]) < REL
+    assert np.max(np.abs(cs["vint"] - cc["vint"])) < 1e-6
 
 
 def test_site_and_mixed_rules_vs_direct_solve():

@@ -31,6 +31,14 @@ for step in "$@"; do
     bench1024dbg) PERC_SYNC_DEBUG=1 run bench1024dbg 600 python bench.py --L 1024 --p 0.6 --steps 1 --warmup 0 --no-cpu-baseline ;;
     bench) run bench 1100 python bench.py ;;
     bench_quick) run bench_quick 900 python bench.py --steps 1 --warmup 1 --no-cpu-baseline ;;
+    prof) run prof 900 rocprofv3 --kernel-trace --stats -f csv -d gpurun_out/prof -o run -- \
+            python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline ;;
+    pmc_fetch) run pmc_fetch 900 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "k_cg|k_spmv" \
+            -f csv -d gpurun_out/pmc_fetch -o run -- \
+            python3 bench.py --steps 1 --warmup 0 --itmax 300 --no-cpu-baseline ;;
+    pmc_write) run pmc_write 900 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "k_cg|k_spmv" \
+            -f csv -d gpurun_out/pmc_write -o run -- \
+            python3 bench.py --steps 1 --warmup 0 --itmax 300 --no-cpu-baseline ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
