@@ -111,6 +111,39 @@ def cpu_baseline(L_, p, order, gpu_iters, cpu_iters):
                 sample_seconds=round(t4 - t0, 2), s_per_solve=round(total, 2))
 
 
+# rocprof kernel names of the CG kernels, per operator format
+ROCPROF_NAMES = {("spmv", "stencil"): ("k_cg_spmv<4>", "k_cg_spmv<6>"),
+                 ("spmv", "csr"): ("k_cg_spmv<0>",),
+                 ("resid", "stencil"): ("k_cg_b<true>",), ("resid", "csr"): ("k_cg_b<false>",),
+                 ("xp", "stencil"): ("k_cg_p<true>",), ("xp", "csr"): ("k_cg_p<false>",)}
+
+
+def pmc_traffic(key, fmt, L_):
+    """HBM bytes per launch of a CG kernel from the committed rocprofv3 PMC
+    summaries of this bench (profiles/*_pmc_{fetch,write}_L<L>.csv, made by
+    tools/prof_csv.py from separate --pmc FETCH_SIZE / WRITE_SIZE passes;
+    FETCH_SIZE doubled per the gfx950 correction).  None if absent."""
+    import csv
+    import glob
+    names = ROCPROF_NAMES.get((key, fmt), ())
+    tot, src = 0.0, []
+    for kind, ctr in (("fetch", "FETCH_SIZE"), ("write", "WRITE_SIZE")):
+        files = sorted(glob.glob(os.path.join(REPO, "profiles", "*_pmc_%s_L%d.csv" % (kind, L_))))
+        got = None
+        for f in reversed(files):  # newest round first
+            with open(f) as fh:
+                for r in csv.DictReader(fh):
+                    if r["kernel"] in names and r["counter"] == ctr:
+                        got = float(r["bytes_per_dispatch"])
+            if got is not None:
+                src.append(os.path.relpath(f, REPO))
+                break
+        if got is None:
+            return None, None
+        tot += got
+    return tot, src
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -227,6 +260,7 @@ def main():
                      "gbs": round(nbytes / (avg * 1e-3) / 1e9, 1)}
     # the roofline line is the kernel with the most device time
     dom = max(kern, key=lambda k_: kern[k_]["total_ms"])
+    traffic, traffic_src = pmc_traffic(dom, fmt, L_)
     achieved = kern[dom]["bytes_per_launch"] / (kern[dom]["avg_launch_ms"] * 1e-3) / 1e9
     iter_ms = sum(v["avg_launch_ms"] for v in kern.values())
     iter_bytes = sum(v["bytes_per_launch"] for v in kern.values())
@@ -269,7 +303,8 @@ def main():
                    "L": L_, "p": p, "rows": N, "nnz_offdiag": nnz, "parallelism":
                    "realisations sharded over %d GPU(s), RCCL stats all-reduce" % world},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS,
-                     "unit": "GB/s", "frac": round(achieved / PEAK_HBM_GBS, 4), "traffic": None,
+                     "unit": "GB/s", "frac": round(achieved / PEAK_HBM_GBS, 4),
+                     "traffic": traffic, "traffic_source": traffic_src,
                      "kernel": kern[dom]["kernel"], "format": fmt,
                      "bytes_per_launch": kern[dom]["bytes_per_launch"],
                      "avg_launch_ms": kern[dom]["avg_launch_ms"],
