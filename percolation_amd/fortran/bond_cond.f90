@@ -1,0 +1,152 @@
+! bond_cond.f90 -- drop-in for Fortran/Square/bond_cond.f and Fortran/
+! Triangular/bond_cond.f: for each trial ii (seed tseed(ii) from the master
+! seed, bond_cond.f:62-70) the bond order is shuffled and the conductance
+! of the lowest-label spanning cluster is computed at each grid point
+! nbarr(jj) = pbarr(jj)*nb (square .49 + 5e-3 steps, 103 points;
+! triangular .35, 131 points), then pc = first spanning fraction and the
+! final spanning label are reported (bond_cond.f:123-498).
+!
+! The reference re-labels bond by bond and checks spanning after every
+! bond; here each grid point is one GPU occupancy + labeling, pc is the
+! smallest spanning occupation found by bisection (spanning is monotone in
+! bf), and the conductance is the HIP Jacobi-PCG in linbcg order.  A grid
+! value equal to the previous one stalls the sweep exactly as the
+! reference's `bf == nbarr(jj)` test does (hazard H3).
+!
+! Parameters: the reference's block (10x10, numtrials 1, master seed 58302),
+! overridable by bond_cond.nml (&bond_cond_nml lattice, m, n, pbc,
+! numtrials, seed, Va, g0, tol, itmax, device /).  Output: bondcond.txt as
+! the reference writes it (bond_cond.f:107-117, 481-496).
+program bond_cond
+  use perc_api
+  implicit none
+#ifndef PERC_LATTICE
+#define PERC_LATTICE 0
+#endif
+  integer(c_int) :: lattice, m, n, pbc, numtrials, seed, itmax, device
+  double precision :: Va, g0, tol
+  namelist /bond_cond_nml/ lattice, m, n, pbc, numtrials, seed, Va, g0, tol, itmax, device
+  integer(c_int) :: t, nb, i, ii, jj, bf, lastbf, npts, lo, hi, mid, bfc, perccln, stats(4)
+  integer(c_int) :: tseed(1000), nbarr(250)
+  double precision :: pbarr(250), pb, pc, Gtop, Gbot
+  integer(c_int), allocatable, target :: order(:)
+  type(c_ptr) :: h
+  type(perc_label_info) :: info
+  type(perc_cond_result) :: res
+  integer :: u
+
+  lattice = PERC_LATTICE
+  m = 10
+  n = 10
+  pbc = 0
+  Va = 1.00d+00
+  g0 = 1.00d+00
+  numtrials = 1
+  seed = 58302
+  tol = 1.00d-08
+  itmax = 2500
+  device = 0
+  if (perc_have_file('bond_cond.nml')) then
+    open(newunit=u, file='bond_cond.nml', status='old')
+    read(u, nml=bond_cond_nml)
+    close(u)
+  end if
+  if (numtrials < 1 .or. numtrials > 1000) error stop 'numtrials must be 1..1000'
+
+  call perc_trial_seeds(seed, 1000, tseed)
+  t = m * n
+  nb = perc_nbonds(lattice, m, n, pbc)
+  pbarr = 0.00d+00
+  nbarr = 0
+  if (lattice == PERC_SQUARE) then
+    pbarr(1) = 0.49d+00
+    npts = 103
+  else
+    pbarr(1) = 0.35d+00
+    npts = 131
+  end if
+  do i = 2, npts
+    pbarr(i) = pbarr(i - 1) + 5.00d-03
+  end do
+  do i = 1, 250
+    nbarr(i) = pbarr(i) * nb
+  end do
+
+  open(unit=10, file='bondcond.txt')
+  write(10, *) "m =", m
+  write(10, *) "n =", n
+  write(10, *) "t =", t
+  write(10, *) "pbc =", pbc
+  write(10, *) "total number of bonds in the lattice:", nb
+  write(10, *) "Va =", Va
+  write(10, *) "g0 =", g0
+  write(10, *) "total number of iterations:", numtrials
+  write(10, *) "random number for generating the trial seeds:", seed
+  write(10, *) "------------------------------"
+
+  allocate(order(nb + 1))
+  call perc_check(perc_ctx_create(device, lattice, m, n, pbc, h), 'perc_ctx_create')
+  do ii = 1, numtrials
+    write(6, *) "Trial #", ii
+    write(10, *) "Trial #", ii
+    write(6, *) "Random number seed:", tseed(ii)
+    write(10, *) "Random number seed:", tseed(ii)
+    call perc_shuffled_ids(nb, tseed(ii), order)
+
+    jj = 1
+    lastbf = -1
+    do while (jj <= 250)
+      bf = nbarr(jj)
+      if (bf <= 0 .or. bf <= lastbf) exit
+      call perc_check(perc_occupy(h, PERC_BOND, 0, c_null_ptr, bf, c_loc(order)), 'perc_occupy')
+      call perc_check(perc_label(h, info, c_null_ptr), 'perc_label')
+      call perc_check(perc_conductance(h, PERC_RULE_BOND, PERC_CUR_FORTRAN, Va, g0, PERC_LEAK, &
+                                       2, tol, itmax, res, c_null_ptr), 'perc_conductance')
+      Gtop = res%gtop
+      Gbot = res%gbot
+      pb = real(bf) / real(nb)               ! REAL*4 quotient (bond_cond.f:351)
+      write(6, 111) pb, Gbot, Gtop, ((Gbot + Gtop) / 2)
+      write(10, 111) pb, Gbot, Gtop, ((Gbot + Gtop) / 2)
+      lastbf = bf
+      jj = jj + 1
+    end do
+
+    ! pc: first occupation with a spanning cluster (bond_cond.f:381)
+    call perc_check(perc_occupy(h, PERC_BOND, 0, c_null_ptr, nb, c_loc(order)), 'perc_occupy')
+    call perc_check(perc_label(h, info, c_null_ptr), 'perc_label')
+    bfc = 0
+    perccln = 0
+    if (info%nspan > 0) then
+      ! final lowest spanning label (all bonds filled)
+      call perc_check(perc_label_numbers(h, c_null_ptr, c_null_ptr, c_null_ptr, 0, stats), &
+                      'perc_label_numbers')
+      perccln = stats(4)
+      lo = 0
+      hi = nb
+      do while (hi - lo > 1)
+        mid = (lo + hi) / 2
+        call perc_check(perc_occupy(h, PERC_BOND, 0, c_null_ptr, mid, c_loc(order)), &
+                        'perc_occupy')
+        call perc_check(perc_label(h, info, c_null_ptr), 'perc_label')
+        if (info%nspan > 0) then
+          hi = mid
+        else
+          lo = mid
+        end if
+      end do
+      bfc = hi
+    end if
+    pc = 0.00d+00
+    if (bfc > 0) pc = real(bfc) / real(nb)
+    write(6, *) "lattice-spanning cluster:", perccln
+    write(10, *) "lattice-spanning cluster:", perccln
+    write(6, *) "pc =", pc
+    write(10, *) "pc =", pc
+    write(6, *) "------------------------------"
+    write(10, *) "------------------------------"
+  end do
+  close(10)
+  call perc_check(perc_ctx_destroy(h), 'perc_ctx_destroy')
+
+111 format(f12.9, ",", f12.9, ",", f12.9, ",", f12.9)
+end program bond_cond

@@ -1,0 +1,111 @@
+! bondc.f90 -- drop-in for Fortran/Square/bondc.f and Fortran/Triangular/
+! bondc.f: one bond-percolation realisation filled to pb, the spanning test
+! and the conductance of the spanning cluster, on libperc.
+!
+! Parameters: the reference's block (Square/bondc.f:67-92; Triangular:
+! pb = .35, seed = 62703), overridable by an optional namelist file
+! bondc.nml (&bondc lattice, m, n, pbc, pb, seed, Va, g0, tol, itmax,
+! device /).  Outputs as the reference: bondorder.txt (i10,",",i10) in
+! shuffled order (bondc.f:177-180), bond.txt (b1, b2, label, j, c(j);
+! bondc.f:600-604) and the run summary on stdout.  The per-bond trace
+! bondocc.txt is not written (SURVEY.md §8(b): optional).
+program bondc
+  use perc_api
+  implicit none
+#ifndef PERC_LATTICE
+#define PERC_LATTICE 0
+#endif
+  integer(c_int) :: lattice, m, n, pbc, seed, itmax, device
+  double precision :: pb, Va, g0, tol
+  namelist /bondc_nml/ lattice, m, n, pbc, pb, seed, Va, g0, tol, itmax, device
+  integer(c_int) :: nb, tbonds, i, j, id, rc, stats(4), perccln, perccls
+  integer(c_int), allocatable, target :: b1(:), b2(:), order(:), label(:), csize(:)
+  type(c_ptr) :: h
+  type(perc_label_info) :: info
+  type(perc_cond_result) :: res
+  integer :: u
+
+  ! reference parameter block
+  lattice = PERC_LATTICE
+  m = 50
+  n = 50
+  pbc = 0
+  if (lattice == PERC_SQUARE) then
+    pb = 0.50d+00
+    seed = 626504
+  else
+    pb = 0.35d+00
+    seed = 62703
+  end if
+  Va = 1.00d+00
+  g0 = 1.00d+00
+  tol = 1.00d-08            ! linbcg call, bondc.f:545
+  itmax = 2500              ! linbcg call, bondc.f:545
+  device = 0
+  if (perc_have_file('bondc.nml')) then
+    open(newunit=u, file='bondc.nml', status='old')
+    read(u, nml=bondc_nml)
+    close(u)
+  end if
+
+  ! bond list in reference order and the shuffled bond order
+  nb = perc_nbonds(lattice, m, n, pbc)
+  allocate(b1(nb), b2(nb), order(nb + 1), label(nb), csize(nb + 2))
+  rc = perc_bond_list(lattice, m, n, pbc, b1, b2)
+  call perc_shuffled_ids(nb, seed, order)
+  open(unit=12, file='bondorder.txt')
+  do i = 1, nb
+    id = order(i)
+    if (id > 0) then
+      write(12, 121) b1(id), b2(id)
+    else
+      write(12, 121) 0, 0
+    end if
+  end do
+  close(12)
+
+  ! occupy the first tbonds of the order, label on the GPU
+  tbonds = pb * nb          ! bondc.f:191 (truncation)
+  call perc_check(perc_ctx_create(device, lattice, m, n, pbc, h), 'perc_ctx_create')
+  call perc_check(perc_occupy(h, PERC_BOND, 0, c_null_ptr, tbonds, c_loc(order)), 'perc_occupy')
+  call perc_check(perc_label(h, info, c_null_ptr), 'perc_label')
+  ! reference label numbers and cluster sizes (bond.txt) by host replay
+  call perc_check(perc_label_numbers(h, c_loc(label), c_null_ptr, c_loc(csize), nb + 2, stats), &
+                  'perc_label_numbers')
+  perccln = stats(4)
+  perccls = 0
+  if (perccln > 0) perccls = csize(perccln + 1)
+
+  write(6, *)
+  write(6, *) "******************************"
+  write(6, *) "largest overall cluster number:", stats(2)
+  write(6, *) "largest overall cluster size:", stats(3)
+  if (perccln > 0) then
+    write(6, *) "infinite cluster present"
+    write(6, *) "infinite cluster number:", perccln
+    write(6, *) "infinite cluster size:", perccls
+  else
+    write(6, *) "no infinite cluster present"
+  end if
+  write(6, *) "******************************"
+
+  if (perccln > 0) then
+    write(6, *) "Calculating internal node voltages"
+    call perc_check(perc_conductance(h, PERC_RULE_BOND, PERC_CUR_FORTRAN, Va, g0, PERC_LEAK, &
+                                     2, tol, itmax, res, c_null_ptr), 'perc_conductance')
+    write(6, *) "Calculating currents"
+    write(6, *) "--------------------"
+    write(6, *) "Conductance:", res%gtop, res%gbot
+    write(6, *) "linbcg iterations:", res%iter, " err:", res%err
+  end if
+
+  open(unit=10, file='bond.txt')
+  do j = 1, nb
+    write(10, 111) b1(j), b2(j), label(j), j, csize(j + 1)
+  end do
+  close(10)
+  call perc_check(perc_ctx_destroy(h), 'perc_ctx_destroy')
+
+111 format(i10, ",", i10, ",", i10, ",", i10, ",", i10)
+121 format(i10, ",", i10)
+end program bondc

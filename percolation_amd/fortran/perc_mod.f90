@@ -1,0 +1,152 @@
+! perc_mod.f90 -- ISO_C_BINDING interface of libperc (include/perc.h) for
+! the Fortran drivers.  The drivers keep the reference programs' parameter
+! blocks, RNG stream and output files (Fortran/Square/bondc.f,
+! bond_cond.f, site.f, sitebond.f and their Triangular twins); the O(N^2)
+! labeling loops, the dense Kirchhoff matrix, sprsin and linbcg are replaced
+! by the libperc calls below (GPU labeling + host label replay + HIP
+! Jacobi-PCG).
+module perc_api
+  use, intrinsic :: iso_c_binding
+  implicit none
+
+  integer(c_int), parameter :: PERC_OK = 0
+  integer(c_int), parameter :: PERC_SQUARE = 0, PERC_TRIANGULAR = 1
+  integer(c_int), parameter :: PERC_BOND = 0, PERC_SITE = 1, PERC_SITEBOND = 2
+  integer(c_int), parameter :: PERC_RULE_BOND = 0, PERC_RULE_SITE = 1, PERC_RULE_MIXED = 2
+  integer(c_int), parameter :: PERC_CUR_FORTRAN = 0, PERC_CUR_MATLAB = 1
+  ! off-diagonal value of bonds outside the spanning cluster (bondc.f:487)
+  real(c_double), parameter :: PERC_LEAK = 1.0d-12
+
+  type, bind(C) :: perc_label_info
+    integer(c_int) :: nclusters, nspan, span_root, span_sites, replayed, perccln
+  end type perc_label_info
+
+  type, bind(C) :: perc_cond_result
+    real(c_double) :: gtop, gbot, err
+    integer(c_int) :: iter, status
+    real(c_double) :: t_assemble_ms, t_solve_ms, t_currents_ms
+  end type perc_cond_result
+
+  interface
+    subroutine perc_srand(seed) bind(C, name='perc_srand')
+      import :: c_int
+      integer(c_int), value :: seed
+    end subroutine perc_srand
+
+    real(c_float) function perc_rand(i) bind(C, name='perc_rand')
+      import :: c_int, c_float
+      integer(c_int), value :: i
+    end function perc_rand
+
+    subroutine perc_trial_seeds(master, k, tseed) bind(C, name='perc_trial_seeds')
+      import :: c_int
+      integer(c_int), value :: master, k
+      integer(c_int) :: tseed(*)
+    end subroutine perc_trial_seeds
+
+    integer(c_int) function perc_nbonds(lattice, m, n, pbc) bind(C, name='perc_nbonds')
+      import :: c_int
+      integer(c_int), value :: lattice, m, n, pbc
+    end function perc_nbonds
+
+    integer(c_int) function perc_bond_list(lattice, m, n, pbc, b1, b2) &
+        bind(C, name='perc_bond_list')
+      import :: c_int
+      integer(c_int), value :: lattice, m, n, pbc
+      integer(c_int) :: b1(*), b2(*)
+    end function perc_bond_list
+
+    subroutine perc_shuffle(nn, order) bind(C, name='perc_shuffle')
+      import :: c_int
+      integer(c_int), value :: nn
+      integer(c_int) :: order(*)
+    end subroutine perc_shuffle
+
+    integer(c_int) function perc_ctx_create(device, lattice, m, n, pbc, h) &
+        bind(C, name='perc_ctx_create')
+      import :: c_int, c_ptr
+      integer(c_int), value :: device, lattice, m, n, pbc
+      type(c_ptr) :: h
+    end function perc_ctx_create
+
+    integer(c_int) function perc_ctx_destroy(h) bind(C, name='perc_ctx_destroy')
+      import :: c_int, c_ptr
+      type(c_ptr), value :: h
+    end function perc_ctx_destroy
+
+    type(c_ptr) function perc_last_error() bind(C, name='perc_last_error')
+      import :: c_ptr
+    end function perc_last_error
+
+    ! array arguments are pointers so that unused ones can be c_null_ptr
+    integer(c_int) function perc_occupy(h, kind, nsites, site_order, nbond, bond_order) &
+        bind(C, name='perc_occupy')
+      import :: c_int, c_ptr
+      type(c_ptr), value :: h, site_order, bond_order
+      integer(c_int), value :: kind, nsites, nbond
+    end function perc_occupy
+
+    integer(c_int) function perc_label(h, info, canon_out) bind(C, name='perc_label')
+      import :: c_int, c_ptr, perc_label_info
+      type(c_ptr), value :: h, canon_out
+      type(perc_label_info) :: info
+    end function perc_label
+
+    integer(c_int) function perc_label_numbers(h, bond_label, site_label, csize, cap, stats) &
+        bind(C, name='perc_label_numbers')
+      import :: c_int, c_ptr
+      type(c_ptr), value :: h, bond_label, site_label, csize
+      integer(c_int), value :: cap
+      integer(c_int) :: stats(4)
+    end function perc_label_numbers
+
+    integer(c_int) function perc_conductance(h, rule, cur_rule, Va, g0, leak, itol, tol, &
+        itmax, res, vint_out) bind(C, name='perc_conductance')
+      import :: c_int, c_ptr, c_double, perc_cond_result
+      type(c_ptr), value :: h, vint_out
+      integer(c_int), value :: rule, cur_rule, itol, itmax
+      real(c_double), value :: Va, g0, leak, tol
+      type(perc_cond_result) :: res
+    end function perc_conductance
+  end interface
+
+contains
+
+  ! The reference `pause`s on errors; libperc returns a status instead.
+  subroutine perc_check(rc, what)
+    integer(c_int), intent(in) :: rc
+    character(*), intent(in) :: what
+    character(kind=c_char), pointer :: msg(:)
+    integer :: k
+    if (rc == PERC_OK) return
+    call c_f_pointer(perc_last_error(), msg, [4096])
+    k = 0
+    do while (msg(k + 1) /= c_null_char .and. k < 4096)
+      k = k + 1
+    end do
+    write(0, '(a,a,i0,a)') what, ' failed: status ', rc, ' ('
+    write(0, *) msg(1:k), ')'
+    error stop 1
+  end subroutine perc_check
+
+  ! 1-based id permutation of 1..nn after srand(seed): the reference's
+  ! REAL*4 Fisher-Yates (bondc.f:162-174, site.f:131-147) with its spill
+  ! slot nn+1 (hazard H2: a draw of j = nn+1 swaps in a 0 sentinel).
+  subroutine perc_shuffled_ids(nn, seed, order)
+    integer(c_int), intent(in) :: nn, seed
+    integer(c_int), intent(out) :: order(nn + 1)
+    integer(c_int) :: i
+    do i = 1, nn
+      order(i) = i
+    end do
+    order(nn + 1) = 0
+    call perc_srand(seed)
+    call perc_shuffle(nn, order)
+  end subroutine perc_shuffled_ids
+
+  ! an optional NAMELIST file overrides the reference parameter block
+  logical function perc_have_file(name)
+    character(*), intent(in) :: name
+    inquire(file=name, exist=perc_have_file)
+  end function perc_have_file
+end module perc_api
