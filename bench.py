@@ -165,7 +165,7 @@ def main():
     import torch.distributed as dist
 
     import percolation_amd as P
-    from percolation_amd import api
+    from percolation_amd import api, ensemble
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -190,8 +190,7 @@ def main():
     # reference RNG.
     t0 = time.perf_counter()
     orders, ii_list, host_orders = [], [], []
-    for k in range(nreal):
-        ii = (k * world + rank) % 1000
+    for k, ii in enumerate(ensemble.trial_indices(nreal, world, rank)):
         if args.occupancy == "reference":
             o = api.shuffled_ids(nb, int(seeds[ii]))[:tb]
         else:
@@ -233,16 +232,7 @@ def main():
     elapsed = time.perf_counter() - t0
     ks = ctx.kernel_stats(reset=True)
     # ensemble statistics: the only collective (RCCL all-reduce over xGMI)
-    g = np.array([r["gtop"] for r in results])
-    stats = torch.tensor([len(results), g.sum(), (g * g).sum(),
-                          sum(r["nspan"] > 0 for r in results), sum(r["iter"] for r in results),
-                          elapsed], dtype=torch.float64, device=dev)
-    tmax = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(stats[:5], op=dist.ReduceOp.SUM)
-        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
-    tmax = float(tmax.item())
-    stats = stats.cpu().numpy()
+    stats, tmax = ensemble.allreduce(ensemble.local_stats(results), elapsed, device=dev)
     nsolves = int(stats[0])
     value = nsolves / tmax
 
@@ -280,6 +270,9 @@ def main():
             ms = ctx.bench_kernel(which, 50)
             row[key] = {"ms": round(ms, 5), "gbs": round(nbytes / (ms * 1e-3) / 1e9, 1)}
         probe[fname] = row
+    copy_ms = ctx.bench_kernel(4, 50)
+    stream_copy = {"ms": round(copy_ms, 5), "bytes": 16 * N,
+                   "gbs": round(16 * N / (copy_ms * 1e-3) / 1e9, 1)}
 
     out = {
         "metric": "CG SpMV GB/s + conductance solves/sec, L=4096 square lattice at p=0.60",
@@ -316,6 +309,7 @@ def main():
                          "gbs": round(iter_bytes / (iter_ms * 1e-3) / 1e9, 1)},
         "cg_kernels": kern,
         "kernel_probe": probe,
+        "stream_copy": stream_copy,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         log("cpu baseline: oracle on a bounded sample ...")

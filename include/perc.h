@@ -150,7 +150,8 @@ int perc_spmv_host(perc_ctx *h, const double *x, double *y);
 /* Roofline probe: `reps` back-to-back launches of one solver kernel on the
    assembled system; returns mean kernel ms (HIP events on the context
    stream).  which: 0 = SpMV (dsprsax), 1 = CG SpMV + q.p dot, 2 = CG
-   residual update (B), 3 = CG x/p update (P).  Clobbers solver vectors. */
+   residual update (B), 3 = CG x/p update (P), 4 = STREAM copy of N doubles
+   (16-B accesses; the achievable-HBM reference).  Clobbers solver vectors. */
 int perc_bench_kernel(perc_ctx *h, int which, int reps, double *ms);
 
 /* Live kernel timing: when enabled, every CG launch inside

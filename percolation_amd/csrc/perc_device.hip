@@ -970,6 +970,20 @@ __global__ __launch_bounds__(kBlock) void k_cg_init(CGArgs a, int itol, int x0_z
   }
 }
 
+// STREAM-style copy of N doubles (16-B accesses, contiguous 256-aligned
+// chunk per workgroup): the achievable-HBM reference for the roofline
+__global__ __launch_bounds__(kBlock) void k_copy(const double* __restrict__ a,
+                                                 double* __restrict__ b, int n) {
+  const int n2 = n / 2;
+  const int chunk = (cdiv(n2, gridDim.x) + kBlock - 1) / kBlock * kBlock;
+  const int i0 = blockIdx.x * chunk, i1 = min(i0 + chunk, n2);
+  const double2* __restrict__ a2 = reinterpret_cast<const double2*>(a);
+  double2* __restrict__ b2 = reinterpret_cast<double2*>(b);
+#pragma unroll 4
+  for (int i = i0 + threadIdx.x; i < i1; i += kBlock) b2[i] = a2[i];
+  if (blockIdx.x == 0 && threadIdx.x == 0 && (n & 1)) b[n - 1] = a[n - 1];
+}
+
 __global__ void k_zero(double* v, long long n) {
   const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) v[i] = 0.0;
@@ -1402,9 +1416,11 @@ hipError_t dev_bench(perc_ctx* h, int which, int reps, double* ms) {
     } else if (which == 2) {
       if (ST) k_cg_b<true><<<G, kBlock, 0, st>>>(a);
       else k_cg_b<false><<<G, kBlock, 0, st>>>(a);
-    } else {
+    } else if (which == 3) {
       if (ST) k_cg_p<true><<<G, kBlock, 0, st>>>(a);
       else k_cg_p<false><<<G, kBlock, 0, st>>>(a);
+    } else {
+      k_copy<<<2 * G, kBlock, 0, st>>>(d.p0, d.q, h->N);
     }
   };
   // the B kernel advances iter (tol < 0 keeps it running); values are

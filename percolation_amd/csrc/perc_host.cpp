@@ -589,7 +589,7 @@ int perc_matrix_format(perc_ctx* h) {
 }
 
 int perc_bench_kernel(perc_ctx* h, int which, int reps, double* ms) {
-  if (!h || !ms || reps <= 0 || which < 0 || which > 3) return PERC_EINVAL;
+  if (!h || !ms || reps <= 0 || which < 0 || which > 4) return PERC_EINVAL;
   if (!h->assembled) return PERC_ESTATE;
   hipSetDevice(h->device);
   // the CG kernels clobber the solver vectors (x, r, p, q), not the system
