@@ -43,6 +43,13 @@ def spmv_bytes(N, nnz, fmt):
     return 18 * N
 
 
+def ps_bytes(N):
+    """k_cg_ps (fused p update + SpMV + q.p, LDS-tiled): reads x, p(k-1), r,
+    code; writes x, p(k), q -- 50N (the tile halo's re-reads are not
+    algorithmic; they show in the PMC traffic)."""
+    return 50 * N
+
+
 def resid_bytes(N, fmt):
     """k_cg_b: reads r, q and d (csr: 8 B diag, stencil: 2 B code); writes r."""
     return 32 * N if fmt == "csr" else 26 * N
@@ -53,7 +60,8 @@ def xp_bytes(N, fmt):
     return 48 * N if fmt == "csr" else 42 * N
 
 
-KERNELS = {"spmv": "k_cg_spmv (SpMV q = A p + q.p dot)",
+KERNELS = {"ps": "k_cg_ps (fused p = bk p + r/d, x += ak p, q = A p, q.p; LDS tiles)",
+           "spmv": "k_cg_spmv (SpMV q = A p + q.p dot)",
            "resid": "k_cg_b (r -= ak q, z = r/d, z.r and r.r dots)",
            "xp": "k_cg_p (x += ak p, p = bk p + r/d)"}
 
@@ -112,10 +120,19 @@ def cpu_baseline(L_, p, order, gpu_iters, cpu_iters):
 
 
 # rocprof kernel names of the CG kernels, per operator format
-ROCPROF_NAMES = {("spmv", "stencil"): ("k_cg_spmv<4>", "k_cg_spmv<6>"),
+ROCPROF_NAMES = {("ps", "stencil"): ("k_cg_ps<4>", "k_cg_ps<6>"),
+                 ("spmv", "stencil_split"): ("k_cg_spmv<4>", "k_cg_spmv<6>"),
+                 ("resid", "stencil_split"): ("k_cg_b<true>",),
+                 ("xp", "stencil_split"): ("k_cg_p<true>",),
+                 ("spmv", "stencil"): ("k_cg_spmv<4>", "k_cg_spmv<6>"),
                  ("spmv", "csr"): ("k_cg_spmv<0>",),
                  ("resid", "stencil"): ("k_cg_b<true>",), ("resid", "csr"): ("k_cg_b<false>",),
                  ("xp", "stencil"): ("k_cg_p<true>",), ("xp", "csr"): ("k_cg_p<false>",)}
+
+
+def base_name(k):
+    """'k_cg_ps<4, false, 1, 1024, 32>' -> 'k_cg_ps<4' (first template argument)"""
+    return k.split(",")[0].rstrip(">")
 
 
 def pmc_traffic(key, fmt, L_):
@@ -128,12 +145,13 @@ def pmc_traffic(key, fmt, L_):
     names = ROCPROF_NAMES.get((key, fmt), ())
     tot, src = 0.0, []
     for kind, ctr in (("fetch", "FETCH_SIZE"), ("write", "WRITE_SIZE")):
-        files = sorted(glob.glob(os.path.join(REPO, "profiles", "*_pmc_%s_L%d.csv" % (kind, L_))))
+        files = sorted(glob.glob(os.path.join(REPO, "profiles", "*_pmc_%s_L%d.csv" % (kind, L_))),
+                       key=lambda f: (os.path.getmtime(f), f))
         got = None
-        for f in reversed(files):  # newest round first
+        for f in reversed(files):  # newest first
             with open(f) as fh:
                 for r in csv.DictReader(fh):
-                    if r["kernel"] in names and r["counter"] == ctr:
+                    if base_name(r["kernel"]) in map(base_name, names) and r["counter"] == ctr:
                         got = float(r["bytes_per_dispatch"])
             if got is not None:
                 src.append(os.path.relpath(f, REPO))
@@ -157,7 +175,8 @@ def main():
     ap.add_argument("--cpu-iters", type=int, default=20)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--occupancy", choices=("uniform", "reference"), default="uniform")
-    ap.add_argument("--format", choices=("auto", "stencil", "csr"), default="auto",
+    ap.add_argument("--format", choices=("auto", "stencil", "stencil_split", "csr"),
+                    default="auto",
                     help="solver operator format (perc_set_matrix_format)")
     args = ap.parse_args()
 
@@ -203,7 +222,7 @@ def main():
                                                             time.perf_counter() - t0))
     ctx = api.Context(0, L_, L_, 0, device=local)
     ctx.set_matrix_format({"auto": P.FMT_AUTO, "stencil": P.FMT_STENCIL,
-                           "csr": P.FMT_CSR}[args.format])
+                           "stencil_split": P.FMT_STENCIL_SPLIT, "csr": P.FMT_CSR}[args.format])
     N, nnz = ctx.system_size()
 
     def run(k):
@@ -236,16 +255,25 @@ def main():
     nsolves = int(stats[0])
     value = nsolves / tmax
 
-    fmt = "stencil" if ctx.matrix_format() == P.FMT_STENCIL else "csr"
+    fmt = {P.FMT_STENCIL: "stencil", P.FMT_STENCIL_SPLIT: "stencil_split",
+           P.FMT_CSR: "csr"}[ctx.matrix_format()]
+
+    def kernel_set(f):
+        """(key, stats key, perc_bench_kernel id, bytes) of the CG kernels of
+        operator format f"""
+        if f == "stencil":
+            return [("ps", "spmv", 1, ps_bytes(N)), ("resid", "resid", 2, resid_bytes(N, f))]
+        return [("spmv", "spmv", 1, spmv_bytes(N, nnz, f)), ("resid", "resid", 2, resid_bytes(N, f)),
+                ("xp", "xp", 3, xp_bytes(N, f))]
+
     # per-kernel live timing (HIP events on the context stream around every
     # launch that did work, over the timed realisations)
     kern = {}
-    for key, nbytes in (("spmv", spmv_bytes(N, nnz, fmt)), ("resid", resid_bytes(N, fmt)),
-                        ("xp", xp_bytes(N, fmt))):
-        n_ = max(ks[key + "_n"], 1)
-        avg = ks[key + "_ms"] / n_
+    for key, skey, _, nbytes in kernel_set(fmt):
+        n_ = max(ks[skey + "_n"], 1)
+        avg = ks[skey + "_ms"] / n_
         kern[key] = {"kernel": KERNELS[key], "avg_launch_ms": round(avg, 5),
-                     "launches": ks[key + "_n"], "total_ms": round(ks[key + "_ms"], 1),
+                     "launches": ks[skey + "_n"], "total_ms": round(ks[skey + "_ms"], 1),
                      "bytes_per_launch": nbytes,
                      "gbs": round(nbytes / (avg * 1e-3) / 1e9, 1)}
     # the roofline line is the kernel with the most device time
@@ -257,22 +285,22 @@ def main():
     # after the timed region, on the last assembled system: each kernel in
     # both operator formats, back to back (perc_bench_kernel; clobbers x)
     probe = {}
-    for fname, fcode in (("stencil", P.FMT_STENCIL), ("csr", P.FMT_CSR)):
+    for fname, fcode in (("stencil", P.FMT_STENCIL), ("stencil_split", P.FMT_STENCIL_SPLIT),
+                         ("csr", P.FMT_CSR)):
         try:
             ctx.set_matrix_format(fcode)
         except Exception:
             continue
         row = {}
-        for key, which, nbytes in (("spmv_plain", 0, spmv_bytes(N, nnz, fname)),
-                                   ("spmv", 1, spmv_bytes(N, nnz, fname)),
-                                   ("resid", 2, resid_bytes(N, fname)),
-                                   ("xp", 3, xp_bytes(N, fname))):
+        plain = [] if fname == "stencil" else [("spmv_plain", "", 0, spmv_bytes(N, nnz, fname))]
+        for key, _, which, nbytes in plain + kernel_set(fname):
             ms = ctx.bench_kernel(which, 50)
             row[key] = {"ms": round(ms, 5), "gbs": round(nbytes / (ms * 1e-3) / 1e9, 1)}
         probe[fname] = row
-    copy_ms = ctx.bench_kernel(4, 50)
-    stream_copy = {"ms": round(copy_ms, 5), "bytes": 16 * N,
-                   "gbs": round(16 * N / (copy_ms * 1e-3) / 1e9, 1)}
+    copy_ms = ctx.bench_kernel(4, 20)
+    copy_bytes = 2 * 8 * (64 << 20)  # 512 MB read + 512 MB written (perc_bench_kernel 4)
+    stream_copy = {"ms": round(copy_ms, 5), "bytes": copy_bytes,
+                   "gbs": round(copy_bytes / (copy_ms * 1e-3) / 1e9, 1)}
 
     out = {
         "metric": "CG SpMV GB/s + conductance solves/sec, L=4096 square lattice at p=0.60",

@@ -150,8 +150,9 @@ int perc_spmv_host(perc_ctx *h, const double *x, double *y);
 /* Roofline probe: `reps` back-to-back launches of one solver kernel on the
    assembled system; returns mean kernel ms (HIP events on the context
    stream).  which: 0 = SpMV (dsprsax), 1 = CG SpMV + q.p dot, 2 = CG
-   residual update (B), 3 = CG x/p update (P), 4 = STREAM copy of N doubles
-   (16-B accesses; the achievable-HBM reference).  Clobbers solver vectors. */
+   residual update (B), 3 = CG x/p update (P), 4 = STREAM copy 512 MB ->
+   512 MB (16-B accesses, past the 256 MB Infinity Cache; the achievable-HBM
+   reference).  Clobbers solver vectors. */
 int perc_bench_kernel(perc_ctx *h, int which, int reps, double *ms);
 
 /* Live kernel timing: when enabled, every CG launch inside
@@ -175,10 +176,11 @@ int perc_system_size(perc_ctx *h, long long *out);
    (sprsin_/linbcg_) always use CSR. */
 #define PERC_FMT_AUTO 0
 #define PERC_FMT_CSR 1
-#define PERC_FMT_STENCIL 2
+#define PERC_FMT_STENCIL 2        /* stencil, p update fused into the SpMV  */
+#define PERC_FMT_STENCIL_SPLIT 3  /* stencil, separate p-update and SpMV kernels */
 int perc_set_matrix_format(perc_ctx *h, int fmt);
-/* format the solver kernels use on the assembled system (PERC_FMT_CSR or
-   PERC_FMT_STENCIL) */
+/* format the solver kernels use on the assembled system (PERC_FMT_CSR,
+   PERC_FMT_STENCIL or PERC_FMT_STENCIL_SPLIT) */
 int perc_matrix_format(perc_ctx *h);
 
 /* ---- one hot-path realisation (bench / ensemble) ---------------------- */

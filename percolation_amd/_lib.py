@@ -23,7 +23,7 @@ SQUARE, TRIANGULAR = 0, 1
 BOND, SITE, SITEBOND = 0, 1, 2
 RULE_BOND, RULE_SITE, RULE_MIXED = 0, 1, 2
 CUR_FORTRAN, CUR_MATLAB = 0, 1
-FMT_AUTO, FMT_CSR, FMT_STENCIL = 0, 1, 2
+FMT_AUTO, FMT_CSR, FMT_STENCIL, FMT_STENCIL_SPLIT = 0, 1, 2, 3
 
 
 class LabelInfo(C.Structure):

@@ -184,7 +184,7 @@ class Context:
                     xp_ms=st[4], xp_n=int(st[5]))
 
     def set_matrix_format(self, fmt):
-        """PERC_FMT_AUTO / PERC_FMT_CSR / PERC_FMT_STENCIL (perc.h)."""
+        """PERC_FMT_AUTO / _CSR / _STENCIL (fused) / _STENCIL_SPLIT (perc.h)."""
         L.check(L.lib().perc_set_matrix_format(self.h, int(fmt)), "perc_set_matrix_format")
 
     def matrix_format(self):

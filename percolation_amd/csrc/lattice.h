@@ -156,6 +156,18 @@ __host__ __device__ inline int sorted_neighbours(const Geom& g, int rn, int* out
   return c;
 }
 
+// Neighbour c of site s in lattice steps: row difference and column
+// difference, the column wrapped into {-1, 0, 1} for left/right pbc.
+__host__ __device__ inline void lattice_delta(const Geom& g, int s, int c, int* dr, int* dc) {
+  const int sr = (s - 1) / g.m, sc = (s - 1) % g.m;
+  const int cr = (c - 1) / g.m, cc = (c - 1) % g.m;
+  int d = cc - sc;
+  if (d > 1) d -= g.m;
+  else if (d < -1) d += g.m;
+  *dr = cr - sr;
+  *dc = d;
+}
+
 // Number of bonds whose smaller end is rn (bond list, Square/bondc.f:139-154)
 __host__ __device__ inline int forward_count(const Geom& g, int rn) {
   int nn[6], c = 0;

@@ -505,8 +505,9 @@ int perc_conductance(perc_ctx* h, int rule, int cur_rule, double Va, double g0, 
   hipEventRecord(h->ev[0], st);
   hipError_t e = dev_assemble(h, rule, g0, leak, Va, h->span_root);
   if (e != hipSuccess) return hip_status(e, "perc_conductance/assemble");
-  if (h->fmt_req == PERC_FMT_STENCIL && !h->stencil_ok) {
-    set_error("perc_conductance: stencil operator requested but a stencil slot has no bond");
+  if ((h->fmt_req == PERC_FMT_STENCIL && !h->tiled_ok) ||
+      (h->fmt_req == PERC_FMT_STENCIL_SPLIT && !h->stencil_ok)) {
+    set_error("perc_conductance: requested stencil operator not available for this system");
     return PERC_EINVAL;
   }
   hipEventRecord(h->ev[1], st);
@@ -575,17 +576,19 @@ int perc_spmv_host(perc_ctx* h, const double* x, double* y) {
 }
 
 int perc_set_matrix_format(perc_ctx* h, int fmt) {
-  if (!h || fmt < PERC_FMT_AUTO || fmt > PERC_FMT_STENCIL) return PERC_EINVAL;
-  if (h->assembled && fmt == PERC_FMT_STENCIL && !h->stencil_ok) return PERC_EINVAL;
+  if (!h || fmt < PERC_FMT_AUTO || fmt > PERC_FMT_STENCIL_SPLIT) return PERC_EINVAL;
+  if (h->assembled && fmt == PERC_FMT_STENCIL && !h->tiled_ok) return PERC_EINVAL;
+  if (h->assembled && fmt == PERC_FMT_STENCIL_SPLIT && !h->stencil_ok) return PERC_EINVAL;
   h->fmt_req = fmt;
-  if (h->assembled) h->stencil = fmt != PERC_FMT_CSR && h->stencil_ok;
+  if (h->assembled) select_format(h);
   return PERC_OK;
 }
 
 int perc_matrix_format(perc_ctx* h) {
   if (!h) return PERC_EINVAL;
   if (!h->assembled) return PERC_ESTATE;
-  return h->stencil ? PERC_FMT_STENCIL : PERC_FMT_CSR;
+  if (!h->stencil) return PERC_FMT_CSR;
+  return h->fused ? PERC_FMT_STENCIL : PERC_FMT_STENCIL_SPLIT;
 }
 
 int perc_bench_kernel(perc_ctx* h, int which, int reps, double* ms) {

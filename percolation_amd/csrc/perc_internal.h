@@ -21,10 +21,14 @@ constexpr int kMaxSlots = 6;      // neighbour slots per row
 // Sorted neighbour offsets (c - s) of each row form of the stencil operator
 // (interior / edge columns, up / down triangles): row i's columns are
 // i + off[f][j] for its form f (perc_device.hip, "Stencil-coded operator").
+// dr/dc: the slot's neighbour in lattice (row, column) steps, column
+// wrapped for pbc; always in {-1, 0, 1} (the LDS-tiled kernel's halo).
 struct StencilForms {
   int nforms;
   int cnt[kMaxForms];
   int off[kMaxForms][kMaxSlots];
+  int dr[kMaxForms][kMaxSlots];
+  int dc[kMaxForms][kMaxSlots];
 };
 
 // Device-resident CG scalars (one cache line each group; written only by the
@@ -124,6 +128,9 @@ struct perc_ctx {
   int fmt_req = PERC_FMT_AUTO;  // perc_set_matrix_format
   bool stencil_ok = false;      // every stencil slot of the assembled system has a bond
   bool stencil = false;         // solver kernels use the stencil operator
+  bool tiled_ok = false;        // every row's slots are (row, col) +-1 steps of its form
+  bool fused = false;           // stencil P+S fused into the LDS-tiled kernel
+  int tile_grid = 0;            // workgroups of the tiled kernel
   double st_ng0 = 0.0, st_nleak = 0.0;  // its two off-diagonal values
   perc::StencilForms forms{};            // row forms of this lattice
   hipEvent_t ev[8];
@@ -142,6 +149,7 @@ hipError_t dev_label(perc_ctx* h, int* nspan, int* span_list, int* nclusters);
 hipError_t dev_span_sites(perc_ctx* h, int root, int* count);
 hipError_t dev_canon(perc_ctx* h, int* canon_out);
 hipError_t dev_assemble(perc_ctx* h, int rule, double g0, double leak, double Va, int span_root);
+void select_format(perc_ctx* h);  // stencil / fused flags from fmt_req + assembly checks
 hipError_t dev_solve(perc_ctx* h, int itol, double tol, int itmax, bool x0_zero, int* iter,
                      double* err);
 hipError_t dev_currents(perc_ctx* h, int rule, int cur_rule, double g0, double leak, double Va,

@@ -118,7 +118,7 @@ def oracle_system(lat, m, n, pbc, b1, b2, gval):
     return sa, ija, itemp, diag, k
 
 
-FORMATS = [PL.FMT_STENCIL, PL.FMT_CSR]
+FORMATS = [PL.FMT_STENCIL, PL.FMT_STENCIL_SPLIT, PL.FMT_CSR]
 
 
 @pytest.mark.parametrize("fmt", FORMATS)
@@ -223,12 +223,17 @@ def test_conductance_vs_oracle_linbcg(lat, m, n, p, seed, fmt):
 
 
 @pytest.mark.parametrize("lat,m,n,pbc,p", [(0, 300, 200, 0, 0.6), (0, 128, 96, 1, 0.55),
-                                           (1, 160, 120, 0, 0.4), (1, 128, 100, 1, 0.42)])
+                                           (1, 160, 120, 0, 0.4), (1, 128, 100, 1, 0.42),
+                                           # tile edges: m past one 256-column tile, rows
+                                           # not a multiple of 16, tiny pbc widths
+                                           (0, 520, 37, 1, 0.55), (1, 514, 30, 1, 0.42),
+                                           (0, 24, 50, 1, 0.55), (1, 20, 18, 0, 0.45)])
 def test_stencil_matches_csr_solver(lat, m, n, pbc, p):
-    """The stencil operator rebuilds the CSR numbers bitwise, so both formats
-    give the same iterates up to the association of the q.p dot (its
-    per-thread row order differs): same iteration count within 1, Gtop and
-    the voltages to the solver's precision, and bitwise-equal SpMVs."""
+    """The stencil operator (fused LDS-tiled and split kernels) rebuilds the
+    CSR numbers bitwise, so all formats give the same iterates up to the
+    association of the q.p dot (its per-thread row order differs): same
+    iteration count within 1, Gtop and the voltages to the solver's
+    precision, and bitwise-equal SpMVs."""
     nb = api.nbonds(lat, m, n, pbc)
     order = api.shuffled_ids(nb, 777)
     out = {}
@@ -242,11 +247,13 @@ def test_stencil_matches_csr_solver(lat, m, n, pbc, p):
             c = ctx.conductance(tol=1e-12, itmax=100000, vint=True)
             assert ctx.matrix_format() == fmt
             out[fmt] = (c, ctx.spmv(x))
-    (cs, ys), (cc, yc) = out[PL.FMT_STENCIL], out[PL.FMT_CSR]
-    assert np.array_equal(ys.view(np.uint64), yc.view(np.uint64))
-    assert abs(cs["iter"] - cc["iter"]) <= 1
-    assert rel(cs["gtop"], cc["gtop"]) < REL and rel(cs["gbot"], cc["gbot"]) < REL
-    assert np.max(np.abs(cs["vint"] - cc["vint"])) < 1e-6
+    cc, yc = out[PL.FMT_CSR]
+    for fmt in (PL.FMT_STENCIL, PL.FMT_STENCIL_SPLIT):
+        cs, ys = out[fmt]
+        assert np.array_equal(ys.view(np.uint64), yc.view(np.uint64))
+        assert abs(cs["iter"] - cc["iter"]) <= 1
+        assert rel(cs["gtop"], cc["gtop"]) < REL and rel(cs["gbot"], cc["gbot"]) < REL
+        assert np.max(np.abs(cs["vint"] - cc["vint"])) < 1e-6
 
 
 def test_site_and_mixed_rules_vs_direct_solve():
