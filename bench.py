@@ -43,11 +43,18 @@ def spmv_bytes(N, nnz, fmt):
     return 18 * N
 
 
-def ps_bytes(N):
-    """k_cg_ps (fused p update + SpMV + q.p, LDS-tiled): reads x, p(k-1), r,
-    code; writes x, p(k), q -- 50N (the tile halo's re-reads are not
+def x_bytes(N, m, full):
+    """x += ak p: read + write of x on every row (full voltages), or on the
+    two interior rows next to the electrodes only (perc_set_full_voltages
+    off: the currents read no other voltage, bondc.f:554-592)."""
+    return 16 * N if full else 16 * 2 * m
+
+
+def ps_bytes(N, m, full):
+    """k_cg_ps (fused p update + SpMV + q.p, LDS-tiled): reads p(k-1), r,
+    code; writes p(k), q -- 34N, plus x (the tile halo's re-reads are not
     algorithmic; they show in the PMC traffic)."""
-    return 50 * N
+    return 34 * N + x_bytes(N, m, full)
 
 
 def resid_bytes(N, fmt):
@@ -55,9 +62,9 @@ def resid_bytes(N, fmt):
     return 32 * N if fmt == "csr" else 26 * N
 
 
-def xp_bytes(N, fmt):
-    """k_cg_p: reads x, p, r and d (csr: 8 B, stencil: 2 B); writes x, p."""
-    return 48 * N if fmt == "csr" else 42 * N
+def xp_bytes(N, fmt, m, full):
+    """k_cg_p: reads p, r and d (csr: 8 B, stencil: 2 B); writes p; plus x."""
+    return (32 * N if fmt == "csr" else 26 * N) + x_bytes(N, m, full)
 
 
 KERNELS = {"ps": "k_cg_ps (fused p = bk p + r/d, x += ak p, q = A p, q.p; LDS tiles)",
@@ -175,6 +182,8 @@ def main():
     ap.add_argument("--cpu-iters", type=int, default=20)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--occupancy", choices=("uniform", "reference"), default="uniform")
+    ap.add_argument("--full-voltages", action="store_true",
+                    help="update x on every row every iteration (perc_set_full_voltages)")
     ap.add_argument("--format", choices=("auto", "stencil", "stencil_split", "csr"),
                     default="auto",
                     help="solver operator format (perc_set_matrix_format)")
@@ -223,6 +232,7 @@ def main():
     ctx = api.Context(0, L_, L_, 0, device=local)
     ctx.set_matrix_format({"auto": P.FMT_AUTO, "stencil": P.FMT_STENCIL,
                            "stencil_split": P.FMT_STENCIL_SPLIT, "csr": P.FMT_CSR}[args.format])
+    ctx.set_full_voltages(args.full_voltages)
     N, nnz = ctx.system_size()
 
     def run(k):
@@ -261,10 +271,12 @@ def main():
     def kernel_set(f):
         """(key, stats key, perc_bench_kernel id, bytes) of the CG kernels of
         operator format f"""
+        full = args.full_voltages
         if f == "stencil":
-            return [("ps", "spmv", 1, ps_bytes(N)), ("resid", "resid", 2, resid_bytes(N, f))]
+            return [("ps", "spmv", 1, ps_bytes(N, L_, full)),
+                    ("resid", "resid", 2, resid_bytes(N, f))]
         return [("spmv", "spmv", 1, spmv_bytes(N, nnz, f)), ("resid", "resid", 2, resid_bytes(N, f)),
-                ("xp", "xp", 3, xp_bytes(N, f))]
+                ("xp", "xp", 3, xp_bytes(N, f, L_, full))]
 
     # per-kernel live timing (HIP events on the context stream around every
     # launch that did work, over the timed realisations)
@@ -321,7 +333,8 @@ def main():
         "config": {"workload": "square L=%d bond percolation p=%.2f, bondc semantics "
                                "(labeling+assembly+Jacobi-PCG tol %g itol 2+currents)"
                                % (L_, p, args.tol),
-                   "L": L_, "p": p, "rows": N, "nnz_offdiag": nnz, "parallelism":
+                   "L": L_, "p": p, "rows": N, "nnz_offdiag": nnz,
+                   "full_voltages": bool(args.full_voltages), "parallelism":
                    "realisations sharded over %d GPU(s), RCCL stats all-reduce" % world},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS,
                      "unit": "GB/s", "frac": round(achieved / PEAK_HBM_GBS, 4),

@@ -179,6 +179,14 @@ int perc_system_size(perc_ctx *h, long long *out);
 #define PERC_FMT_STENCIL 2        /* stencil, p update fused into the SpMV  */
 #define PERC_FMT_STENCIL_SPLIT 3  /* stencil, separate p-update and SpMV kernels */
 int perc_set_matrix_format(perc_ctx *h, int fmt);
+/* Interior voltages.  linbcg never reads x inside its iteration and the
+   terminal currents read it only on the interior rows next to the
+   electrodes (Square/bondc.f:554-592), so perc_conductance keeps x on those
+   2m rows only (bitwise the same values there) unless vint_out is given or
+   this option is on -- then every row is updated every iteration, as
+   linbcg does.  Default off. */
+int perc_set_full_voltages(perc_ctx *h, int enable);
+
 /* format the solver kernels use on the assembled system (PERC_FMT_CSR,
    PERC_FMT_STENCIL or PERC_FMT_STENCIL_SPLIT) */
 int perc_matrix_format(perc_ctx *h);

@@ -82,6 +82,7 @@ SIGNATURES = {
     "perc_system_size": (C.c_int, [_VP, np.ctypeslib.ndpointer(dtype=np.int64)]),
     "perc_set_matrix_format": (C.c_int, [_VP, C.c_int]),
     "perc_matrix_format": (C.c_int, [_VP]),
+    "perc_set_full_voltages": (C.c_int, [_VP, C.c_int]),
     "perc_stats_accumulate": (None, [_D, C.c_int, C.c_double, C.c_int, C.c_int]),
     "sprsin_": (None, [_VP] * 7),
     "dsprsax_": (None, [_VP] * 5),

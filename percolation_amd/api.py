@@ -187,6 +187,10 @@ class Context:
         """PERC_FMT_AUTO / _CSR / _STENCIL (fused) / _STENCIL_SPLIT (perc.h)."""
         L.check(L.lib().perc_set_matrix_format(self.h, int(fmt)), "perc_set_matrix_format")
 
+    def set_full_voltages(self, enable=True):
+        """Keep every interior voltage up to date during the solve (perc.h)."""
+        L.check(L.lib().perc_set_full_voltages(self.h, int(enable)), "perc_set_full_voltages")
+
     def matrix_format(self):
         rc = L.lib().perc_matrix_format(self.h)
         if rc < 0:

@@ -759,6 +759,7 @@ struct CGArgs {
   double* pb[2];  // fused kernel: p(k) lives in pb[k & 1]
   int fused;
   int b_reverse;  // B walks the row chunks in reverse logical order (fused mode)
+  int xrows;      // 0: x kept on all rows; else only rows i < xrows or i >= N - xrows
   double* q;
   double* partials;  // kRedSlots slots of pstride doubles
   unsigned* tickets; // kRedSlots slots of tstride counters
@@ -828,10 +829,12 @@ __global__ __launch_bounds__(kBlock) void k_cg_p(CGArgs a) {
       const double2 rv = *reinterpret_cast<const double2*>(r + i);
       const double2 dv = diag2<ST>(a, i);
       const double2 pv = *reinterpret_cast<const double2*>(p + i);
-      double2 xv = *reinterpret_cast<const double2*>(x + i);
-      xv.x = xv.x + ak * pv.x;
-      xv.y = xv.y + ak * pv.y;
-      *reinterpret_cast<double2*>(x + i) = xv;
+      if (a.xrows == 0 || i < a.xrows || i >= N - a.xrows) {
+        double2 xv = *reinterpret_cast<const double2*>(x + i);
+        xv.x = xv.x + ak * pv.x;
+        xv.y = xv.y + ak * pv.y;
+        *reinterpret_cast<double2*>(x + i) = xv;
+      }
       double2 pn;
       pn.x = bk * pv.x + rv.x / dv.x;
       pn.y = bk * pv.y + rv.y / dv.y;
@@ -844,7 +847,7 @@ __global__ __launch_bounds__(kBlock) void k_cg_p(CGArgs a) {
     if (first) {
       p[i] = z;
     } else {
-      x[i] = x[i] + ak * p[i];
+      if (a.xrows == 0 || i < a.xrows || i >= N - a.xrows) x[i] = x[i] + ak * p[i];
       p[i] = bk * p[i] + z;
     }
   }
@@ -942,7 +945,7 @@ __global__ __launch_bounds__(kBlock) void k_cg_xfinal(CGArgs a) {
   const int N = a.A.N;
   const double* __restrict__ p = a.fused ? a.pb[a.S->iter & 1] : a.p;
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < N; i += gridDim.x * blockDim.x)
-    a.x[i] = a.x[i] + ak * p[i];
+    if (a.xrows == 0 || i < a.xrows || i >= N - a.xrows) a.x[i] = a.x[i] + ak * p[i];
 }
 
 // ---------------------------------------------------------------------------
@@ -998,7 +1001,7 @@ __global__ __launch_bounds__(NT) void k_cg_ps(CGArgs a) {
   constexpr int kPairs = kTH * (kTW / 2);
   for (int e0 = threadIdx.x; e0 < kPairs; e0 += NT * kPairBatch) {
     int idx[kPairBatch], tr[kPairBatch], tc[kPairBatch];
-    bool ok[kPairBatch], own[kPairBatch];
+    bool ok[kPairBatch], own[kPairBatch], xw[kPairBatch];
     unsigned cc[kPairBatch];
     double2 rv[kPairBatch], pv[kPairBatch], xv[kPairBatch];
 #pragma unroll
@@ -1015,11 +1018,12 @@ __global__ __launch_bounds__(NT) void k_cg_ps(CGArgs a) {
       }
       own[u] = ok[u] && tr[u] >= 1 && tr[u] <= heff && tc[u] >= 2 && tc[u] < 2 + weff;
       idx[u] = ok[u] ? gr * T.m + gc : 0;
+      xw[u] = own[u] && (a.xrows == 0 || idx[u] < a.xrows || idx[u] >= a.St.N - a.xrows);
       if (ok[u]) {
         cc[u] = *reinterpret_cast<const unsigned*>(a.St.code + idx[u]);
         rv[u] = *reinterpret_cast<const double2*>(r + idx[u]);
         if (!first) pv[u] = *reinterpret_cast<const double2*>(pold + idx[u]);
-        if (!first && own[u]) xv[u] = *reinterpret_cast<const double2*>(x + idx[u]);
+        if (!first && xw[u]) xv[u] = *reinterpret_cast<const double2*>(x + idx[u]);
       }
     }
 #pragma unroll
@@ -1036,7 +1040,7 @@ __global__ __launch_bounds__(NT) void k_cg_ps(CGArgs a) {
         } else {
           pn.x = bk * pv[u].x + z0;
           pn.y = bk * pv[u].y + z1;
-          if (own[u]) {
+          if (xw[u]) {
             double2 xn;
             xn.x = xv[u].x + ak * pv[u].x;
             xn.y = xv[u].y + ak * pv[u].y;
@@ -1173,6 +1177,7 @@ CGArgs make_cg_args(perc_ctx* h) {
   // kernel starts on the r that B wrote last (measured: B 0.112 -> 0.097 ms
   // at L = 4096)
   a.b_reverse = h->fused ? 1 : 0;
+  a.xrows = h->full_voltages || h->g.m <= 0 ? 0 : h->g.m;  // see dev_solve
   a.pstride = red_partials_size(red_grid(h));
   a.tstride = red_tickets_size(red_grid(h));
   a.rhs = h->d.rhs;
@@ -1473,8 +1478,8 @@ hipError_t dev_assemble(perc_ctx* h, int rule, double g0, double leak, double Va
   return hipSuccess;
 }
 
-hipError_t dev_solve(perc_ctx* h, int itol, double tol, int itmax, bool x0_zero, int* iter,
-                     double* err) {
+hipError_t dev_solve(perc_ctx* h, int itol, double tol, int itmax, bool x0_zero, bool full_x,
+                     int* iter, double* err) {
   DeviceBuffers& d = h->d;
   hipStream_t st = h->stream;
   if (d.err_hist_cap < itmax + 2) {
@@ -1493,6 +1498,12 @@ hipError_t dev_solve(perc_ctx* h, int itol, double tol, int itmax, bool x0_zero,
     k_zero<<<blocks_for(h->N + 2), kBlock, 0, st>>>(d.x, h->N + 2);
   }
   CGArgs a = make_cg_args(h);
+  // linbcg never reads x inside the iteration (r is recursive), and the
+  // terminal currents read it only on the interior rows next to the
+  // electrodes (bondc.f:554-592): unless the caller wants every voltage, x
+  // is carried on the first and last lattice rows only -- bitwise the same
+  // values there, 16 B/row/iteration less traffic
+  a.xrows = full_x || h->g.m <= 0 ? 0 : h->g.m;
   const int G = h->grid;
   const bool ST = h->stencil;
   if (ST) k_cg_init<true><<<G, kBlock, 0, st>>>(a, itol, x0_zero ? 1 : 0);

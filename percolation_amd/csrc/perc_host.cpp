@@ -515,7 +515,7 @@ int perc_conductance(perc_ctx* h, int rule, int cur_rule, double Va, double g0, 
   h->rule = rule;
   int iter = 0;
   double err = 0.0;
-  e = dev_solve(h, itol, tol, itmax, true, &iter, &err);
+  e = dev_solve(h, itol, tol, itmax, true, h->full_voltages || vint_out != nullptr, &iter, &err);
   if (e != hipSuccess) return hip_status(e, "perc_conductance/solve");
   hipEventRecord(h->ev[2], st);
   std::vector<double> iout(2 * (size_t)h->g.m);
@@ -581,6 +581,12 @@ int perc_set_matrix_format(perc_ctx* h, int fmt) {
   if (h->assembled && fmt == PERC_FMT_STENCIL_SPLIT && !h->stencil_ok) return PERC_EINVAL;
   h->fmt_req = fmt;
   if (h->assembled) select_format(h);
+  return PERC_OK;
+}
+
+int perc_set_full_voltages(perc_ctx* h, int enable) {
+  if (!h) return PERC_EINVAL;
+  h->full_voltages = enable != 0;
   return PERC_OK;
 }
 

@@ -131,6 +131,7 @@ struct perc_ctx {
   bool tiled_ok = false;        // every row's slots are (row, col) +-1 steps of its form
   bool fused = false;           // stencil P+S fused into the LDS-tiled kernel
   int tile_grid = 0;            // workgroups of the tiled kernel
+  bool full_voltages = false;   // perc_set_full_voltages: keep x on every row
   double st_ng0 = 0.0, st_nleak = 0.0;  // its two off-diagonal values
   perc::StencilForms forms{};            // row forms of this lattice
   hipEvent_t ev[8];
@@ -150,8 +151,8 @@ hipError_t dev_span_sites(perc_ctx* h, int root, int* count);
 hipError_t dev_canon(perc_ctx* h, int* canon_out);
 hipError_t dev_assemble(perc_ctx* h, int rule, double g0, double leak, double Va, int span_root);
 void select_format(perc_ctx* h);  // stencil / fused flags from fmt_req + assembly checks
-hipError_t dev_solve(perc_ctx* h, int itol, double tol, int itmax, bool x0_zero, int* iter,
-                     double* err);
+hipError_t dev_solve(perc_ctx* h, int itol, double tol, int itmax, bool x0_zero, bool full_x,
+                     int* iter, double* err);
 hipError_t dev_currents(perc_ctx* h, int rule, int cur_rule, double g0, double leak, double Va,
                         int span_root, double thresh, double* iout_host);
 hipError_t dev_spmv(perc_ctx* h, const double* x, double* y);

@@ -275,7 +275,7 @@ void linbcg_(int* n_, double* b, double* x, int* itol, double* tol, int* itmax, 
   double er = 0.0;
   bool x0_zero = true;
   for (int i = 0; i < n && x0_zero; ++i) x0_zero = x[i] == 0.0 && !std::signbit(x[i]);
-  if (e == hipSuccess) e = dev_solve(g_nr, *itol, *tol, *itmax, x0_zero, &it, &er);
+  if (e == hipSuccess) e = dev_solve(g_nr, *itol, *tol, *itmax, x0_zero, true, &it, &er);
   if (e == hipSuccess) e = hipMemcpy(x, g_nr->d.x, sizeof(double) * n, hipMemcpyDeviceToHost);
   g_status = hip_status(e, "linbcg_");
   *iter = it;

@@ -256,6 +256,30 @@ def test_stencil_matches_csr_solver(lat, m, n, pbc, p):
         assert np.max(np.abs(cs["vint"] - cc["vint"])) < 1e-6
 
 
+@pytest.mark.parametrize("fmt", FORMATS)
+@pytest.mark.parametrize("lat,m,n,pbc,p", [(0, 260, 140, 0, 0.6), (1, 130, 90, 1, 0.42)])
+def test_boundary_row_voltages_bitwise(lat, m, n, pbc, p, fmt):
+    """Without vint_out the solver keeps x on the two interior rows next to
+    the electrodes only; Gtop/Gbot/iter/err are bitwise those of the
+    full-voltage solve, and those rows' voltages too."""
+    nb = api.nbonds(lat, m, n, pbc)
+    order = api.shuffled_ids(nb, 4242)
+    with api.Context(lat, m, n, pbc) as ctx:
+        ctx.set_matrix_format(fmt)
+        ctx.occupy(PL.BOND, bond_order=order, nbonds_=int(p * nb))
+        if ctx.label()["nspan"] == 0:
+            pytest.skip("no spanning cluster")
+        part = ctx.conductance(tol=1e-10, itmax=100000)
+        ctx.set_full_voltages(True)
+        full = ctx.conductance(tol=1e-10, itmax=100000)
+        vfull = ctx.conductance(tol=1e-10, itmax=100000, vint=True)["vint"]
+        ctx.set_full_voltages(False)
+        vpart = ctx.conductance(tol=1e-10, itmax=100000, vint=True)["vint"]
+    for k in ("gtop", "gbot", "err", "iter"):
+        assert part[k] == full[k], k
+    assert np.array_equal(vfull.view(np.uint64), vpart.view(np.uint64))  # vint forces all rows
+
+
 def test_site_and_mixed_rules_vs_direct_solve():
     """ConductCalc.m site / mixed rules (parity unpinned vs MATLAB: checked
     against an independent direct sparse solve of the oracle's system)."""
