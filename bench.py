@@ -130,10 +130,11 @@ def cpu_baseline(L_, p, order, gpu_iters, cpu_iters):
 ROCPROF_NAMES = {("ps", "stencil"): ("k_cg_ps<4>", "k_cg_ps<6>"),
                  ("spmv", "stencil_split"): ("k_cg_spmv<4>", "k_cg_spmv<6>"),
                  ("resid", "stencil_split"): ("k_cg_b<true>",),
+                 ("resid", "stencil"): ("k_cg_b<true>",),
                  ("xp", "stencil_split"): ("k_cg_p<true>",),
                  ("spmv", "stencil"): ("k_cg_spmv<4>", "k_cg_spmv<6>"),
                  ("spmv", "csr"): ("k_cg_spmv<0>",),
-                 ("resid", "stencil"): ("k_cg_b<true>",), ("resid", "csr"): ("k_cg_b<false>",),
+                 ("resid", "csr"): ("k_cg_b<false>",),
                  ("xp", "stencil"): ("k_cg_p<true>",), ("xp", "csr"): ("k_cg_p<false>",)}
 
 

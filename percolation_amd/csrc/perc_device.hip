@@ -949,41 +949,106 @@ __global__ __launch_bounds__(kBlock) void k_cg_xfinal(CGArgs a) {
 }
 
 // ---------------------------------------------------------------------------
-// Fused P(k) + S(k) on LDS-tiled lattice blocks (stencil operator only).
-// A workgroup owns kTileH lattice rows x kTileW columns of the interior
-// system.  Phase 1 forms p(k) = bk p(k-1) + r/d (p = r/d at k = 1) for the
-// tile and a one-site halo into LDS -- every stencil neighbour is a (row,
-// col) +-1 step (columns wrapped for pbc; checked per row at assembly) --
-// writes p(k) of its own sites to pb[k & 1] (p(k-1) stays readable in the
-// other buffer for the neighbours' halos) and applies the deferred
-// x += ak(k-1) p(k-1).  Phase 2 forms q = A p(k) from LDS and the q.p dot.
-// Every number is the unfused kernels' (same expressions, same order).
-// Phase 1 works on column pairs with 16-B loads: an LDS row holds columns
+// LDS-tiled stencil kernels (stencil operator, m even).  A workgroup owns a
+// tile of kTileH lattice rows x kTileW columns of the interior system and
+// stages one vector of the tile plus a one-site halo in LDS -- every stencil
+// neighbour is a (row, col) +-1 step (columns wrapped for pbc; checked per
+// row at assembly) -- so the SpMV reads its neighbours from LDS.  The halo
+// is loaded in column pairs with 16-B accesses: an LDS row holds columns
 // c0-2 .. c0+kTileW+1, so with m even every pair is 16-B aligned and a pbc
-// wrap maps a pair onto a contiguous pair (odd m: the split kernels run).
-// Tile 32 x 256 sites (halo re-reads 6 %), 1024 threads, 70 KB LDS: two
-// workgroups = 32 waves per CU.  Measured at L = 4096 (tools/exp_ps.sh):
-// 16-row tiles, 256/512 threads and 1-5 pairs in flight per thread all ran
-// 0.171-0.200 ms; this one 0.171 ms.
+// wrap maps a pair onto a contiguous pair.  Tile 32 x 256 sites (halo
+// re-reads 6 %), 1024 threads, 70 KB LDS: two workgroups = 32 waves per CU
+// (16-row tiles, 256/512 threads and 1-5 pairs in flight per thread all
+// measured 0.171-0.200 ms for the fused kernel at L = 4096; this 0.171).
+//
+// One CG iteration is two launches:
+//   k_cg_ps(k): p(k) = bk p(k-1) + r/d (p = r/d at k = 1) on tile + halo
+//               into LDS, p(k) of its own sites to pb[k & 1] (p(k-1) stays
+//               readable in the other buffer for the neighbours' halos),
+//               x += ak(k-1) p(k-1), then q = A p(k) from LDS and q.p
+//               (ak = bknum / q.p)
+//   k_cg_b(k):  the streaming B, walking its row chunks in reverse (see
+//               make_cg_args)
+// Every number is the split kernels' (same expressions, same order).
+// (Not storing q and rebuilding it in a tiled B from p(k) moves ~12 % fewer
+// bytes, but the tiled B ran 0.154 ms against the streaming B's 0.084 at
+// L = 4096: its r/code loads wait for the barrier, and hoisting them costs
+// occupancy.)
 constexpr int kTileW = 256, kTileH = 32, kPSThreads = 1024;
-constexpr int kTW = kTileW + 4;
-template <int SL, bool CODE_LDS = false, int kPairBatch = 1, int NT = kPSThreads,
-          int TILEH = kTileH>
-__global__ __launch_bounds__(NT) void k_cg_ps(CGArgs a) {
-  constexpr int kTH = TILEH + 2;
+constexpr int kTW = kTileW + 4, kTH = kTileH + 2;
+constexpr int kTilePairs = kTH * (kTW / 2);
+constexpr int kRowsPerThread = kTileH * kTileW / kPSThreads;  // phase 2: 8 rows, loads batched
+
+struct Tile {
+  int r0, c0, heff, weff;
+};
+
+__device__ __forceinline__ Tile tile_of(const TileGeom& T, int lb) {
+  const int trow = lb / T.tpr, tcol = lb - trow * T.tpr;
+  Tile t;
+  t.r0 = trow * kTileH;
+  t.c0 = tcol * kTileW;
+  t.heff = min(kTileH, T.nrows - t.r0);
+  t.weff = min(kTileW, T.m - t.c0);
+  return t;
+}
+
+// LDS pair e of the tile: LDS row tr, column tc (even), global index idx of
+// its first site; false if the pair is outside the lattice / not needed.
+// *own: both sites belong to this tile.
+__device__ __forceinline__ bool tile_pair(const TileGeom& T, const Tile& t, int e, int* tr,
+                                          int* tc, int* idx, bool* own) {
+  *tr = e / (kTW / 2);
+  *tc = 2 * (e - *tr * (kTW / 2));
+  const int gr = t.r0 - 1 + *tr;
+  int gc = t.c0 - 2 + *tc;
+  bool ok = *tc <= t.weff + 3 && gr >= 0 && gr < T.nrows;
+  if (gc < 0 || gc >= T.m) {
+    if (T.pbc) gc += gc < 0 ? T.m : -T.m;
+    else ok = false;
+  }
+  *own = ok && *tr >= 1 && *tr <= t.heff && *tc >= 2 && *tc < 2 + t.weff;
+  *idx = ok ? gr * T.m + gc : 0;
+  return ok;
+}
+
+// row-form offsets (global) and LDS deltas of every slot
+__device__ __forceinline__ void load_form_lds(const StencilView& St, int* s_off, int* s_dd) {
+  if (threadIdx.x < kMaxForms * kMaxSlots) {
+    const int f = threadIdx.x / kMaxSlots, j = threadIdx.x % kMaxSlots;
+    s_off[threadIdx.x] = St.F.off[f][j];
+    s_dd[threadIdx.x] = St.F.dr[f][j] * kTW + St.F.dc[f][j];
+  }
+}
+
+// y(i) of row i (code c) from the LDS tile; e0 = LDS index of site i
+template <int SL>
+__device__ __forceinline__ double tile_row(const StencilView& St, const int* s_off,
+                                           const int* s_dd, const double* s_p, int i, int e0,
+                                           unsigned c, double* xi) {
+  const int f = c >> 11, cnt = (c >> 8) & 7;
+  double xv[SL];
+  bool use[SL];
+#pragma unroll
+  for (int j = 0; j < SL; ++j) {
+    const int col = i + s_off[f * kMaxSlots + j];
+    use[j] = j < cnt && (unsigned)col < (unsigned)St.N;
+    xv[j] = s_p[use[j] ? e0 + s_dd[f * kMaxSlots + j] : e0];
+  }
+  *xi = s_p[e0];
+  return st_combine<SL>(c, xv, use, *xi, St.ng0, St.nleak);
+}
+
+template <int SL, bool STORE_Q>
+__global__ __launch_bounds__(kPSThreads) void k_cg_ps(CGArgs a) {
   CGScalars* S = a.S;
   if (S->done) return;
   __shared__ __attribute__((aligned(16))) double s_p[kTH * kTW];
-  __shared__ uint16_t s_code[CODE_LDS ? TILEH * kTileW : 1];
   __shared__ int s_off[kMaxForms * kMaxSlots];
   __shared__ int s_dd[kMaxForms * kMaxSlots];
   __shared__ double s_red[32];
   __shared__ int s_flag[2];
-  if (threadIdx.x < kMaxForms * kMaxSlots) {
-    const int f = threadIdx.x / kMaxSlots, j = threadIdx.x % kMaxSlots;
-    s_off[threadIdx.x] = a.St.F.off[f][j];
-    s_dd[threadIdx.x] = a.St.F.dr[f][j] * kTW + a.St.F.dc[f][j];
-  }
+  load_form_lds(a.St, s_off, s_dd);
   const int k = S->iter + 1;
   const bool first = k == 1;
   const double bk = S->bk, ak = S->ak;
@@ -992,95 +1057,65 @@ __global__ __launch_bounds__(NT) void k_cg_ps(CGArgs a) {
   double* __restrict__ pnew = a.pb[k & 1];
   const double* __restrict__ r = a.r;
   double* __restrict__ x = a.x;
-  const TileGeom T = a.T;
+  const int N = a.St.N;
   const int lb = xcd_logical_block(blockIdx.x, gridDim.x);
-  const int trow = lb / T.tpr, tcol = lb - trow * T.tpr;
-  const int r0 = trow * TILEH, c0 = tcol * kTileW;
-  const int heff = min(TILEH, T.nrows - r0), weff = min(kTileW, T.m - c0);
+  const Tile t = tile_of(a.T, lb);
   // phase 1: p(k) on the tile and its halo, two columns per step
-  constexpr int kPairs = kTH * (kTW / 2);
-  for (int e0 = threadIdx.x; e0 < kPairs; e0 += NT * kPairBatch) {
-    int idx[kPairBatch], tr[kPairBatch], tc[kPairBatch];
-    bool ok[kPairBatch], own[kPairBatch], xw[kPairBatch];
-    unsigned cc[kPairBatch];
-    double2 rv[kPairBatch], pv[kPairBatch], xv[kPairBatch];
-#pragma unroll
-    for (int u = 0; u < kPairBatch; ++u) {
-      const int e = e0 + u * NT;
-      tr[u] = e / (kTW / 2);
-      tc[u] = 2 * (e - tr[u] * (kTW / 2));
-      const int gr = r0 - 1 + tr[u];
-      int gc = c0 - 2 + tc[u];
-      ok[u] = e < kPairs && tc[u] <= weff + 3 && gr >= 0 && gr < T.nrows;
-      if (gc < 0 || gc >= T.m) {
-        if (T.pbc) gc += gc < 0 ? T.m : -T.m;
-        else ok[u] = false;
-      }
-      own[u] = ok[u] && tr[u] >= 1 && tr[u] <= heff && tc[u] >= 2 && tc[u] < 2 + weff;
-      idx[u] = ok[u] ? gr * T.m + gc : 0;
-      xw[u] = own[u] && (a.xrows == 0 || idx[u] < a.xrows || idx[u] >= a.St.N - a.xrows);
-      if (ok[u]) {
-        cc[u] = *reinterpret_cast<const unsigned*>(a.St.code + idx[u]);
-        rv[u] = *reinterpret_cast<const double2*>(r + idx[u]);
-        if (!first) pv[u] = *reinterpret_cast<const double2*>(pold + idx[u]);
-        if (!first && xw[u]) xv[u] = *reinterpret_cast<const double2*>(x + idx[u]);
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < kPairBatch; ++u) {
-      const int e = e0 + u * NT;
-      if (e >= kPairs) continue;
-      double2 pn = make_double2(0.0, 0.0);
-      if (ok[u]) {
-        const double z0 = rv[u].x / code_diag(cc[u] & 0xffffu, ng0, nleak);
-        const double z1 = rv[u].y / code_diag(cc[u] >> 16, ng0, nleak);
-        if (first) {
-          pn.x = z0;
-          pn.y = z1;
-        } else {
-          pn.x = bk * pv[u].x + z0;
-          pn.y = bk * pv[u].y + z1;
-          if (xw[u]) {
-            double2 xn;
-            xn.x = xv[u].x + ak * pv[u].x;
-            xn.y = xv[u].y + ak * pv[u].y;
-            *reinterpret_cast<double2*>(x + idx[u]) = xn;
-          }
-        }
-        if (own[u]) {
-          *reinterpret_cast<double2*>(pnew + idx[u]) = pn;
-          if (CODE_LDS) {
-            const int o = (tr[u] - 1) * kTileW + (tc[u] - 2);
-            s_code[o] = (uint16_t)(cc[u] & 0xffffu);
-            s_code[o + 1] = (uint16_t)(cc[u] >> 16);
-          }
+  for (int e = threadIdx.x; e < kTilePairs; e += kPSThreads) {
+    int tr, tc, idx;
+    bool own;
+    double2 pn = make_double2(0.0, 0.0);
+    if (tile_pair(a.T, t, e, &tr, &tc, &idx, &own)) {
+      const bool xw = own && !first && (a.xrows == 0 || idx < a.xrows || idx >= N - a.xrows);
+      // every load issued before any arithmetic (one memory round trip)
+      const unsigned cc = *reinterpret_cast<const unsigned*>(a.St.code + idx);
+      const double2 rv = *reinterpret_cast<const double2*>(r + idx);
+      const double2 pv = first ? make_double2(0.0, 0.0)
+                               : *reinterpret_cast<const double2*>(pold + idx);
+      double2 xv = xw ? *reinterpret_cast<const double2*>(x + idx) : make_double2(0.0, 0.0);
+      const double z0 = rv.x / code_diag(cc & 0xffffu, ng0, nleak);
+      const double z1 = rv.y / code_diag(cc >> 16, ng0, nleak);
+      if (first) {
+        pn.x = z0;
+        pn.y = z1;
+      } else {
+        pn.x = bk * pv.x + z0;
+        pn.y = bk * pv.y + z1;
+        if (xw) {
+          xv.x = xv.x + ak * pv.x;
+          xv.y = xv.y + ak * pv.y;
+          *reinterpret_cast<double2*>(x + idx) = xv;
         }
       }
-      *reinterpret_cast<double2*>(&s_p[tr[u] * kTW + tc[u]]) = pn;
+      if (own) *reinterpret_cast<double2*>(pnew + idx) = pn;
+    } else {
+      tr = e / (kTW / 2);
+      tc = 2 * (e - tr * (kTW / 2));
     }
+    *reinterpret_cast<double2*>(&s_p[tr * kTW + tc]) = pn;
   }
   __syncthreads();
-  // phase 2: q = A p(k) from LDS, q.p
+  // phase 2: q = A p(k) from LDS, q.p; the thread's 8 row codes loaded
+  // first (issuing them before phase 1 instead holds 8 more VGPRs across
+  // it, and above 64 VGPRs only one 1024-thread workgroup fits per CU)
   double dot[1] = {0.0};
-  const int N = a.St.N;
-  for (int o = threadIdx.x; o < TILEH * kTileW; o += NT) {
-    const int lr = o / kTileW, lc = o - lr * kTileW;
-    if (lr < heff && lc < weff) {
-      const int i = (r0 + lr) * T.m + c0 + lc;
-      const unsigned c = CODE_LDS ? s_code[o] : a.St.code[i];
-      const int f = c >> 11, cnt = (c >> 8) & 7;
-      const int e0 = (lr + 1) * kTW + lc + 2;
-      double xv[SL];
-      bool use[SL];
+  const int lc = threadIdx.x % kTileW, lr0 = threadIdx.x / kTileW;
+  constexpr int kLrStep = kPSThreads / kTileW;
+  unsigned cr[kRowsPerThread];
 #pragma unroll
-      for (int j = 0; j < SL; ++j) {
-        const int col = i + s_off[f * kMaxSlots + j];
-        use[j] = j < cnt && (unsigned)col < (unsigned)N;
-        xv[j] = s_p[use[j] ? e0 + s_dd[f * kMaxSlots + j] : e0];
-      }
-      const double xi = s_p[e0];
-      const double qv = st_combine<SL>(c, xv, use, xi, ng0, nleak);
-      a.q[i] = qv;
+  for (int u = 0; u < kRowsPerThread; ++u) {
+    const int lr = lr0 + u * kLrStep;
+    cr[u] = lr < t.heff && lc < t.weff ? a.St.code[(t.r0 + lr) * a.T.m + t.c0 + lc] : 0u;
+  }
+#pragma unroll
+  for (int u = 0; u < kRowsPerThread; ++u) {
+    const int lr = lr0 + u * kLrStep;
+    if (lr < t.heff && lc < t.weff) {
+      const int i = (t.r0 + lr) * a.T.m + t.c0 + lc;
+      double xi;
+      const double qv =
+          tile_row<SL>(a.St, s_off, s_dd, s_p, i, (lr + 1) * kTW + lc + 2, cr[u], &xi);
+      if (STORE_Q) a.q[i] = qv;
       dot[0] = dot[0] + qv * xi;
     }
   }
@@ -1172,10 +1207,10 @@ CGArgs make_cg_args(perc_ctx* h) {
   a.pb[0] = h->d.p0;
   a.pb[1] = h->d.p1;
   a.fused = h->fused ? 1 : 0;
-  // B walks its row chunks in reverse: it starts on the q the tiled kernel
-  // wrote last (still in the 256 MB Infinity Cache), and the next tiled
-  // kernel starts on the r that B wrote last (measured: B 0.112 -> 0.097 ms
-  // at L = 4096)
+  // fused format: B walks its row chunks in reverse, so it starts on the q
+  // the tiled kernel wrote last (still in the 256 MB Infinity Cache), and
+  // the next tiled kernel starts on the r that B wrote last (measured: B
+  // 0.112 -> 0.097 ms at L = 4096)
   a.b_reverse = h->fused ? 1 : 0;
   a.xrows = h->full_voltages || h->g.m <= 0 ? 0 : h->g.m;  // see dev_solve
   a.pstride = red_partials_size(red_grid(h));
@@ -1196,11 +1231,20 @@ CGArgs make_cg_args(perc_ctx* h) {
 // S(k), or the fused P(k)+S(k) of the tiled stencil kernel
 void launch_cg_spmv(perc_ctx* h, const CGArgs& a, int G) {
   if (h->fused) {
-    if (h->g.scn == 4) k_cg_ps<4><<<h->tile_grid, kPSThreads, 0, h->stream>>>(a);
-    else k_cg_ps<6><<<h->tile_grid, kPSThreads, 0, h->stream>>>(a);
+    if (h->g.scn == 4) k_cg_ps<4, true><<<h->tile_grid, kPSThreads, 0, h->stream>>>(a);
+    else k_cg_ps<6, true><<<h->tile_grid, kPSThreads, 0, h->stream>>>(a);
   } else if (!h->stencil) k_cg_spmv<0><<<G, kBlock, 0, h->stream>>>(a);
   else if (h->g.scn == 4) k_cg_spmv<4><<<G, kBlock, 0, h->stream>>>(a);
   else k_cg_spmv<6><<<G, kBlock, 0, h->stream>>>(a);
+}
+
+// B(k) (streaming; the fused format walks its chunks in reverse)
+void launch_cg_b(perc_ctx* h, const CGArgs& a, int G) {
+  if (h->stencil) {
+    k_cg_b<true><<<G, kBlock, 0, h->stream>>>(a);
+  } else {
+    k_cg_b<false><<<G, kBlock, 0, h->stream>>>(a);
+  }
 }
 
 void launch_spmv(perc_ctx* h, const CGArgs& a, const double* x, double* y) {
@@ -1535,8 +1579,7 @@ hipError_t dev_solve(perc_ctx* h, int itol, double tol, int itmax, bool x0_zero,
       launch_cg_spmv(h, a, G);
       HIP_TRY(dbg_sync(st, "k_cg_spmv"));
       if (T.enabled) hipEventRecord(T.ev[4 * j + 2], st);
-      if (ST) k_cg_b<true><<<G, kBlock, 0, st>>>(a);
-      else k_cg_b<false><<<G, kBlock, 0, st>>>(a);
+      launch_cg_b(h, a, G);
       HIP_TRY(dbg_sync(st, "k_cg_b"));
       if (T.enabled) hipEventRecord(T.ev[4 * j + 3], st);
     }
@@ -1636,8 +1679,7 @@ hipError_t dev_bench(perc_ctx* h, int which, int reps, double* ms) {
     } else if (which == 1) {
       launch_cg_spmv(h, a, G);
     } else if (which == 2) {
-      if (ST) k_cg_b<true><<<G, kBlock, 0, st>>>(a);
-      else k_cg_b<false><<<G, kBlock, 0, st>>>(a);
+      launch_cg_b(h, a, G);
     } else if (which == 3) {
       if (ST) k_cg_p<true><<<G, kBlock, 0, st>>>(a);
       else k_cg_p<false><<<G, kBlock, 0, st>>>(a);
