@@ -703,7 +703,6 @@ __device__ __forceinline__ double st_rowval(const StencilView& A, const int* s_o
   return st_combine<kMaxSlots>(c, xv, use, x[i], A.ng0, A.nleak);
 }
 
-constexpr int kStRowsPerThread = 8;  // rows of a thread per CG workgroup
 constexpr int kStBatch = 4;          // rows in flight per thread
 
 // contiguous row range of the logical block
@@ -743,7 +742,7 @@ __global__ __launch_bounds__(kBlock) void k_spmv_st(StencilView A, const double*
 // and a final X pass applies the last x += ak p.  Scalars and the stop flag
 // live on the device, so a fixed launch sequence (or a captured graph) runs
 // any number of iterations; launches after the stop are no-ops.
-// interior system as a lattice of nrows x m sites, in tiles of kTileH x kTileW
+// interior system as a lattice of nrows x m sites, in tiles of TILEH x kTileW
 struct TileGeom {
   int m, nrows, pbc, tpr;  // tpr: tiles per lattice row
 };
@@ -950,7 +949,7 @@ __global__ __launch_bounds__(kBlock) void k_cg_xfinal(CGArgs a) {
 
 // ---------------------------------------------------------------------------
 // LDS-tiled stencil kernels (stencil operator, m even).  A workgroup owns a
-// tile of kTileH lattice rows x kTileW columns of the interior system and
+// tile of TILEH lattice rows x kTileW columns of the interior system and
 // stages one vector of the tile plus a one-site halo in LDS -- every stencil
 // neighbour is a (row, col) +-1 step (columns wrapped for pbc; checked per
 // row at assembly) -- so the SpMV reads its neighbours from LDS.  The halo
@@ -974,21 +973,25 @@ __global__ __launch_bounds__(kBlock) void k_cg_xfinal(CGArgs a) {
 // bytes, but the tiled B ran 0.154 ms against the streaming B's 0.084 at
 // L = 4096: its r/code loads wait for the barrier, and hoisting them costs
 // occupancy.)
-constexpr int kTileW = 256, kTileH = 32, kPSThreads = 1024;
-constexpr int kTW = kTileW + 4, kTH = kTileH + 2;
-constexpr int kTilePairs = kTH * (kTW / 2);
-constexpr int kRowsPerThread = kTileH * kTileW / kPSThreads;  // phase 2: 8 rows, loads batched
+// Tile height TILEH in {32, 16, 8} with 32*TILEH threads (8 phase-2 rows per
+// thread); the tallest one that still gives >= kMinTiles workgroups is used
+// (L = 4096: 32; L = 1024: 8 -- 32-row tiles would leave half the CUs idle).
+constexpr int kTileW = 256, kTileHMax = 32, kMinTiles = 512;
+constexpr int kTW = kTileW + 4;
+constexpr int kRowsPerThread = 8;
+__host__ __device__ constexpr int tile_threads(int tileh) { return tileh * kTileW / kRowsPerThread; }
 
 struct Tile {
   int r0, c0, heff, weff;
 };
 
+template <int TILEH>
 __device__ __forceinline__ Tile tile_of(const TileGeom& T, int lb) {
   const int trow = lb / T.tpr, tcol = lb - trow * T.tpr;
   Tile t;
-  t.r0 = trow * kTileH;
+  t.r0 = trow * TILEH;
   t.c0 = tcol * kTileW;
-  t.heff = min(kTileH, T.nrows - t.r0);
+  t.heff = min(TILEH, T.nrows - t.r0);
   t.weff = min(kTileW, T.m - t.c0);
   return t;
 }
@@ -1039,8 +1042,11 @@ __device__ __forceinline__ double tile_row(const StencilView& St, const int* s_o
   return st_combine<SL>(c, xv, use, *xi, St.ng0, St.nleak);
 }
 
-template <int SL, bool STORE_Q>
-__global__ __launch_bounds__(kPSThreads) void k_cg_ps(CGArgs a) {
+template <int SL, bool STORE_Q, int TILEH>
+__global__ __launch_bounds__(tile_threads(TILEH)) void k_cg_ps(CGArgs a) {
+  constexpr int kPSThreads = tile_threads(TILEH);
+  constexpr int kTH = TILEH + 2;
+  constexpr int kTilePairs = kTH * (kTW / 2);
   CGScalars* S = a.S;
   if (S->done) return;
   __shared__ __attribute__((aligned(16))) double s_p[kTH * kTW];
@@ -1059,7 +1065,7 @@ __global__ __launch_bounds__(kPSThreads) void k_cg_ps(CGArgs a) {
   double* __restrict__ x = a.x;
   const int N = a.St.N;
   const int lb = xcd_logical_block(blockIdx.x, gridDim.x);
-  const Tile t = tile_of(a.T, lb);
+  const Tile t = tile_of<TILEH>(a.T, lb);
   // phase 1: p(k) on the tile and its halo, two columns per step
   for (int e = threadIdx.x; e < kTilePairs; e += kPSThreads) {
     int tr, tc, idx;
@@ -1231,8 +1237,18 @@ CGArgs make_cg_args(perc_ctx* h) {
 // S(k), or the fused P(k)+S(k) of the tiled stencil kernel
 void launch_cg_spmv(perc_ctx* h, const CGArgs& a, int G) {
   if (h->fused) {
-    if (h->g.scn == 4) k_cg_ps<4, true><<<h->tile_grid, kPSThreads, 0, h->stream>>>(a);
-    else k_cg_ps<6, true><<<h->tile_grid, kPSThreads, 0, h->stream>>>(a);
+    const int th = h->tile_h;
+    const dim3 G2(h->tile_grid), B2(tile_threads(th));
+    hipStream_t st = h->stream;
+    if (h->g.scn == 4) {
+      if (th == 32) k_cg_ps<4, true, 32><<<G2, B2, 0, st>>>(a);
+      else if (th == 16) k_cg_ps<4, true, 16><<<G2, B2, 0, st>>>(a);
+      else k_cg_ps<4, true, 8><<<G2, B2, 0, st>>>(a);
+    } else {
+      if (th == 32) k_cg_ps<6, true, 32><<<G2, B2, 0, st>>>(a);
+      else if (th == 16) k_cg_ps<6, true, 16><<<G2, B2, 0, st>>>(a);
+      else k_cg_ps<6, true, 8><<<G2, B2, 0, st>>>(a);
+    }
   } else if (!h->stencil) k_cg_spmv<0><<<G, kBlock, 0, h->stream>>>(a);
   else if (h->g.scn == 4) k_cg_spmv<4><<<G, kBlock, 0, h->stream>>>(a);
   else k_cg_spmv<6><<<G, kBlock, 0, h->stream>>>(a);
@@ -1296,11 +1312,12 @@ hipError_t dbg_sync(hipStream_t st, const char* name) {
 
 inline dim3 blocks_for(long long n) { return dim3((unsigned)((n + kBlock - 1) / kBlock)); }
 
-// fixed CG grid (the dot-product reduction order depends on it): about
-// kStRowsPerThread rows per thread, at most kMaxCgGrid workgroups
+// fixed CG grid (the dot-product reduction order depends on it): 2 rows per
+// thread while that stays under kMaxCgGrid workgroups (small lattices keep
+// every CU busy), else more rows per thread
 constexpr int kMaxCgGrid = 8192;
 inline int cg_grid(int N) {
-  return std::max(1, std::min(cdiv(N, (long long)kBlock * kStRowsPerThread), kMaxCgGrid));
+  return std::max(1, std::min(cdiv(N, (long long)kBlock * 2), kMaxCgGrid));
 }
 
 template <typename T>
@@ -1375,7 +1392,10 @@ hipError_t dev_build_lattice(perc_ctx* h) {
   HIP_TRY(dmalloc(&d.p1, nv));
   HIP_TRY(dmalloc(&d.q, nv));
   h->grid = cg_grid(N);
-  h->tile_grid = cdiv(std::max(g.n - 2, 0), kTileH) * cdiv(g.m, kTileW);
+  h->tile_h = kTileHMax;
+  while (h->tile_h > 8 && cdiv(std::max(g.n - 2, 0), h->tile_h) * cdiv(g.m, kTileW) < kMinTiles)
+    h->tile_h /= 2;
+  h->tile_grid = cdiv(std::max(g.n - 2, 0), h->tile_h) * cdiv(g.m, kTileW);
   HIP_TRY(dmalloc(&d.partials, kRedSlots * red_partials_size(red_grid(h))));
   HIP_TRY(dmalloc(&d.tickets, kRedSlots * red_tickets_size(red_grid(h))));
   HIP_TRY(hipMemset(d.tickets, 0, kRedSlots * red_tickets_size(red_grid(h)) * sizeof(unsigned)));

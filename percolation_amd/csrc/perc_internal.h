@@ -131,6 +131,7 @@ struct perc_ctx {
   bool tiled_ok = false;        // every row's slots are (row, col) +-1 steps of its form
   bool fused = false;           // stencil P+S fused into the LDS-tiled kernel
   int tile_grid = 0;            // workgroups of the tiled kernel
+  int tile_h = 32;              // its tile height (rows)
   bool full_voltages = false;   // perc_set_full_voltages: keep x on every row
   double st_ng0 = 0.0, st_nleak = 0.0;  // its two off-diagonal values
   perc::StencilForms forms{};            // row forms of this lattice

@@ -280,6 +280,26 @@ def test_boundary_row_voltages_bitwise(lat, m, n, pbc, p, fmt):
     assert np.array_equal(vfull.view(np.uint64), vpart.view(np.uint64))  # vint forces all rows
 
 
+@pytest.mark.parametrize("lat,m,n,pbc,p", [(0, 2048, 2048, 0, 0.6), (1, 1024, 2050, 1, 0.42)])
+def test_tall_tiles_match_split_kernels(lat, m, n, pbc, p):
+    """Lattices large enough for the 32-row (2048^2) and 16-row (1024 x 2050)
+    tiles of the fused kernel: same solve as the split stencil kernels."""
+    nb = api.nbonds(lat, m, n, pbc)
+    order = api.shuffled_ids(nb, 99)
+    out = {}
+    for fmt in (PL.FMT_STENCIL, PL.FMT_STENCIL_SPLIT):
+        with api.Context(lat, m, n, pbc) as ctx:
+            ctx.set_matrix_format(fmt)
+            ctx.occupy(PL.BOND, bond_order=order, nbonds_=int(p * nb))
+            if ctx.label()["nspan"] == 0:
+                pytest.skip("no spanning cluster")
+            out[fmt] = ctx.conductance(tol=1e-10, itmax=10 ** 6)
+            assert ctx.matrix_format() == fmt
+    a, b = out[PL.FMT_STENCIL], out[PL.FMT_STENCIL_SPLIT]
+    assert abs(a["iter"] - b["iter"]) <= 2
+    assert rel(a["gtop"], b["gtop"]) < REL and rel(a["gbot"], b["gbot"]) < REL
+
+
 def test_site_and_mixed_rules_vs_direct_solve():
     """ConductCalc.m site / mixed rules (parity unpinned vs MATLAB: checked
     against an independent direct sparse solve of the oracle's system)."""
