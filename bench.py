@@ -183,6 +183,10 @@ def main():
     ap.add_argument("--cpu-iters", type=int, default=20)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--occupancy", choices=("uniform", "reference"), default="uniform")
+    ap.add_argument("--lattice", choices=("square", "tri"), default="square")
+    ap.add_argument("--kind", choices=("bond", "site", "sitebond"), default="bond",
+                    help="site / sitebond use the ConductCalc.m site / mixed rules")
+    ap.add_argument("--ps", type=float, default=0.593, help="site fraction for --kind sitebond")
     ap.add_argument("--full-voltages", action="store_true",
                     help="update x on every row every iteration (perc_set_full_voltages)")
     ap.add_argument("--format", choices=("auto", "stencil", "stencil_split", "csr"),
@@ -205,8 +209,16 @@ def main():
         dist.init_process_group("nccl", device_id=dev)
 
     L_, p = args.L, args.p
-    nb = api.nbonds(0, L_, L_, 0)
+    lat = 0 if args.lattice == "square" else 1
+    nb = api.nbonds(lat, L_, L_, 0)
+    t_sites = L_ * L_
     tb = int(p * nb)  # bondc.f:191
+    if args.kind == "site":
+        tb = 0
+    elif args.kind == "sitebond":
+        ts = int(args.ps * t_sites)
+    if args.kind == "site":
+        ts = int(p * t_sites)
     seeds = api.trial_seeds(args.master, 1000)
     nreal = args.warmup + args.steps
     # inputs: occupation orders generated on the host and made resident in
@@ -218,27 +230,48 @@ def main():
     # (numpy PCG64 seeded by tseed(ii)); the drop-in drivers keep the
     # reference RNG.
     t0 = time.perf_counter()
-    orders, ii_list, host_orders = [], [], []
-    for k, ii in enumerate(ensemble.trial_indices(nreal, world, rank)):
+    orders, site_orders, ii_list, host_orders = [], [], [], []
+
+    def draw(n, cnt, seed, salt=0):
         if args.occupancy == "reference":
-            o = api.shuffled_ids(nb, int(seeds[ii]))[:tb]
-        else:
-            o = (np.random.default_rng(int(seeds[ii])).permutation(nb)[:tb] + 1).astype(np.int32)
+            return api.shuffled_ids(n, seed)[:cnt]
+        rng = np.random.default_rng([seed, salt] if salt else seed)
+        return (rng.permutation(n)[:cnt] + 1).astype(np.int32)
+
+    for k, ii in enumerate(ensemble.trial_indices(nreal, world, rank)):
+        o = draw(nb, tb, int(seeds[ii])) if args.kind != "site" else np.zeros(1, np.int32)
         orders.append(torch.from_numpy(np.ascontiguousarray(o)).to(dev))
+        if args.kind != "bond":
+            so = draw(t_sites, ts, int(seeds[ii]), salt=1)
+            site_orders.append(torch.from_numpy(np.ascontiguousarray(so)).to(dev))
         host_orders.append(o if k == args.warmup else None)
         ii_list.append(ii)
     torch.cuda.synchronize()
     log("rank %d: %d orders (nb=%d, tbonds=%d) in %.1fs" % (rank, nreal, nb, tb,
                                                             time.perf_counter() - t0))
-    ctx = api.Context(0, L_, L_, 0, device=local)
+    ctx = api.Context(lat, L_, L_, 0, device=local)
     ctx.set_matrix_format({"auto": P.FMT_AUTO, "stencil": P.FMT_STENCIL,
                            "stencil_split": P.FMT_STENCIL_SPLIT, "csr": P.FMT_CSR}[args.format])
     ctx.set_full_voltages(args.full_voltages)
     N, nnz = ctx.system_size()
 
     def run(k):
-        return ctx.bondc_realisation(None, tb, tol=args.tol, itmax=args.itmax,
-                                     device_ptr=orders[k].data_ptr())
+        if args.kind == "bond":
+            return ctx.bondc_realisation(None, tb, tol=args.tol, itmax=args.itmax,
+                                         device_ptr=orders[k].data_ptr())
+        # ConductCalc.m site / mixed rules (MATLAB/ConductCalc.m:88-165)
+        kind = P._lib.SITE if args.kind == "site" else P._lib.SITEBOND
+        t_0 = time.perf_counter()
+        ctx.occupy_device(kind, site_orders[k].data_ptr(), ts,
+                          orders[k].data_ptr() if kind == P._lib.SITEBOND else None, tb)
+        li = ctx.label()
+        t_1 = time.perf_counter()
+        c = ctx.conductance(P._lib.RULE_SITE if args.kind == "site" else P._lib.RULE_MIXED,
+                            P._lib.CUR_MATLAB, tol=args.tol, itmax=args.itmax)
+        t_2 = time.perf_counter()
+        return dict(gtop=c["gtop"], gbot=c["gbot"], iter=c["iter"], nspan=li["nspan"],
+                    t_label_ms=(t_1 - t_0) * 1e3, t_solve_ms=c["t_solve_ms"],
+                    t_total_ms=(t_2 - t_0) * 1e3)
 
     for k in range(args.warmup):
         r = run(k)
@@ -331,9 +364,14 @@ def main():
                  "tseed(ii) from master %d (bond_cond.f:65-70)"
                  % ("uniform PCG64" if args.occupancy == "uniform"
                     else "reference REAL*4 gfortran-rand Fisher-Yates", args.master)),
-        "config": {"workload": "square L=%d bond percolation p=%.2f, bondc semantics "
-                               "(labeling+assembly+Jacobi-PCG tol %g itol 2+currents)"
-                               % (L_, p, args.tol),
+        "config": {"workload": (
+            "%s L=%d bond percolation p=%.2f, bondc semantics" % (args.lattice, L_, p)
+            if args.kind == "bond" else
+            "%s L=%d site percolation p=%.3f, ConductCalc site rule" % (args.lattice, L_, p)
+            if args.kind == "site" else
+            "%s L=%d mixed ps=%.3f pb=%.3f, ConductCalc mixed rule" % (args.lattice, L_, args.ps, p))
+            + " (labeling+assembly+Jacobi-PCG tol %g itol 2+currents)" % args.tol,
+                   "lattice": args.lattice, "kind": args.kind,
                    "L": L_, "p": p, "rows": N, "nnz_offdiag": nnz,
                    "full_voltages": bool(args.full_voltages), "parallelism":
                    "realisations sharded over %d GPU(s), RCCL stats all-reduce" % world},
@@ -353,7 +391,7 @@ def main():
         "kernel_probe": probe,
         "stream_copy": stream_copy,
     }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.kind == "bond" and lat == 0:
         log("cpu baseline: oracle on a bounded sample ...")
         try:
             out["cpu_baseline"] = cpu_baseline(L_, p, host_orders[args.warmup],

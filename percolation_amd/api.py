@@ -116,6 +116,14 @@ class Context:
         L.check(L.lib().perc_occupy(self.h, kind, nsites, L.ptr(so), nbonds_, L.ptr(bo)),
                 "perc_occupy")
 
+    def occupy_device(self, kind, site_ptr=None, nsites=0, bond_ptr=None, nbonds_=0):
+        """perc_occupy_device: order lists already in device memory (int
+        addresses of device int32 arrays on this context's device)."""
+        sp = C.c_void_p(site_ptr) if site_ptr else None
+        bp = C.c_void_p(bond_ptr) if bond_ptr else None
+        L.check(L.lib().perc_occupy_device(self.h, kind, nsites, sp, nbonds_, bp),
+                "perc_occupy_device")
+
     def label(self, canon=False):
         info = L.LabelInfo()
         out = _i32(self.t) if canon else None
