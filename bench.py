@@ -299,8 +299,13 @@ def main():
     nsolves = int(stats[0])
     value = nsolves / tmax
 
-    fmt = {P.FMT_STENCIL: "stencil", P.FMT_STENCIL_SPLIT: "stencil_split",
-           P.FMT_CSR: "csr"}[ctx.matrix_format()]
+    try:  # the format the solves used (the last realisation may not span: no system)
+        fmt = {P.FMT_STENCIL: "stencil", P.FMT_STENCIL_SPLIT: "stencil_split",
+               P.FMT_CSR: "csr"}[ctx.matrix_format()]
+        assembled = True
+    except P.PercError:
+        fmt = {"auto": "stencil"}.get(args.format, args.format)
+        assembled = False
 
     def kernel_set(f):
         """(key, stats key, perc_bench_kernel id, bytes) of the CG kernels of
@@ -321,18 +326,18 @@ def main():
         kern[key] = {"kernel": KERNELS[key], "avg_launch_ms": round(avg, 5),
                      "launches": ks[skey + "_n"], "total_ms": round(ks[skey + "_ms"], 1),
                      "bytes_per_launch": nbytes,
-                     "gbs": round(nbytes / (avg * 1e-3) / 1e9, 1)}
+                     "gbs": round(nbytes / (avg * 1e-3) / 1e9, 1) if avg > 0 else None}
     # the roofline line is the kernel with the most device time
     dom = max(kern, key=lambda k_: kern[k_]["total_ms"])
     traffic, traffic_src = pmc_traffic(dom, fmt, L_)
-    achieved = kern[dom]["bytes_per_launch"] / (kern[dom]["avg_launch_ms"] * 1e-3) / 1e9
+    achieved = kern[dom]["gbs"] or 0.0  # 0: no realisation spanned, nothing solved
     iter_ms = sum(v["avg_launch_ms"] for v in kern.values())
     iter_bytes = sum(v["bytes_per_launch"] for v in kern.values())
     # after the timed region, on the last assembled system: each kernel in
     # both operator formats, back to back (perc_bench_kernel; clobbers x)
     probe = {}
     for fname, fcode in (("stencil", P.FMT_STENCIL), ("stencil_split", P.FMT_STENCIL_SPLIT),
-                         ("csr", P.FMT_CSR)):
+                         ("csr", P.FMT_CSR)) if assembled else ():
         try:
             ctx.set_matrix_format(fcode)
         except Exception:
@@ -386,7 +391,8 @@ def main():
         "spanning_fraction": round(float(stats[3]) / max(nsolves, 1), 3),
         "gtop_mean": float(stats[1]) / max(nsolves, 1),
         "cg_iteration": {"ms": round(iter_ms, 5), "bytes": iter_bytes,
-                         "gbs": round(iter_bytes / (iter_ms * 1e-3) / 1e9, 1)},
+                         "gbs": round(iter_bytes / (iter_ms * 1e-3) / 1e9, 1) if iter_ms > 0
+                         else None},
         "cg_kernels": kern,
         "kernel_probe": probe,
         "stream_copy": stream_copy,

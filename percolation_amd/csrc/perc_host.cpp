@@ -599,7 +599,7 @@ int perc_matrix_format(perc_ctx* h) {
 
 int perc_bench_kernel(perc_ctx* h, int which, int reps, double* ms) {
   if (!h || !ms || reps <= 0 || which < 0 || which > 4) return PERC_EINVAL;
-  if (!h->assembled) return PERC_ESTATE;
+  if (!h->assembled && which != 4) return PERC_ESTATE;  // the copy needs no system
   hipSetDevice(h->device);
   // the CG kernels clobber the solver vectors (x, r, p, q), not the system
   return hip_status(dev_bench(h, which, reps, ms), "perc_bench_kernel");
