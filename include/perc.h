@@ -63,6 +63,9 @@ void perc_srand(int seed);
 float perc_rand(int i);
 /* tseed(1..k) = int(rand(0)*1e7)+1 after srand(master) (bond_cond.f:65-70) */
 void perc_trial_seeds(int master, int k, int *tseed);
+/* same with int(rand(0)*scale)+1: the threshold scans use scale 1e6
+   (Square/bond_perc.f:70-74, Square/site_perc.f:71-75) */
+void perc_trial_seeds_scaled(int master, int k, int scale, int *tseed);
 
 /* ---- host-side lattice helpers --------------------------------------- */
 int perc_nbonds(int lattice, int m, int n, int pbc);
@@ -115,6 +118,17 @@ int perc_label(perc_ctx *h, perc_label_info *info, int *canon_out);
    t+nb+2 mixed), stats[4] = {cln, maxcn, maxcs, perccln}. */
 int perc_label_numbers(perc_ctx *h, int *bond_label, int *site_label,
                        int *csize, int cap, int *stats);
+
+/* Percolation threshold of one order (Square/bond_perc.f:204-366,
+   Square/site_perc.f:150-256, Square/bond_cond.f:381 pc): *first = the
+   smallest count c such that occupying order[0..c) (bond ids for PERC_BOND,
+   site ids for PERC_SITE) has a spanning cluster, 0 if even all n do not.
+   Bisection over c with the GPU labeling (spanning is monotone in c); the
+   order is uploaded once (or is a device array when on_device != 0).  The
+   context is left occupied at c (or n) and labeled, so perc_label_numbers
+   gives the reference's maxcs / spanning-cluster size at that step. */
+int perc_first_spanning(perc_ctx *h, int kind, const int *order, int n, int on_device,
+                        int *first);
 
 /* Same numbering without a context or device: host-only O(N alpha) replay
    of an explicit occupancy (used by the drivers' text output and tests). */

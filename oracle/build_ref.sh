@@ -75,6 +75,13 @@ build tri_sitebond            Triangular/sitebond.f
 build sq_bond_cond            Square/bond_cond.f
 build sq_bond_cond_3t         Square/bond_cond.f 's/numtrials = 1 /numtrials = 3 /' 's/m = 10 /m = 12 /' 's/n = 10 /n = 12 /'
 build tri_bond_cond           Triangular/bond_cond.f
+
+build sq_bond_perc            Square/bond_perc.f
+build sq_bond_perc_pbc        Square/bond_perc.f 's/pbc = 0 /pbc = 1 /' 's/m = 50 /m = 40 /' 's/n = 50 /n = 30 /'
+build tri_bond_perc           Triangular/bond_perc.f
+build sq_site_perc            Square/site_perc.f 's/numtrials = 1000 /numtrials = 40 /'
+build tri_site_perc           Triangular/site_perc.f 's/numtrials = 1000 /numtrials = 40 /'
+build sq_site_perc_pbc        Square/site_perc.f 's/numtrials = 1000 /numtrials = 40 /' 's/pbc = 0 /pbc = 1 /' 's/m = 50 /m = 36 /' 's/n = 50 /n = 44 /'
 # NR-level drop-in (route 1): the reference program with its
 # embedded Numerical Recipes routines (sprsin ... dsprstx, from the line
 # "SUBROUTINE sprsin" to the end of the file) deleted and libperc.so linked

@@ -82,6 +82,8 @@ SIGNATURES = {
     "perc_system_size": (C.c_int, [_VP, np.ctypeslib.ndpointer(dtype=np.int64)]),
     "perc_set_matrix_format": (C.c_int, [_VP, C.c_int]),
     "perc_matrix_format": (C.c_int, [_VP]),
+    "perc_first_spanning": (C.c_int, [_VP, C.c_int, _VP, C.c_int, C.c_int, _VP]),
+    "perc_trial_seeds_scaled": (None, [C.c_int, C.c_int, C.c_int, _I]),
     "perc_set_full_voltages": (C.c_int, [_VP, C.c_int]),
     "perc_stats_accumulate": (None, [_D, C.c_int, C.c_double, C.c_int, C.c_int]),
     "sprsin_": (None, [_VP] * 7),

@@ -54,9 +54,14 @@ def shuffled_ids(N, seed):
     return order
 
 
-def trial_seeds(master, k=1000):
+def trial_seeds(master, k=1000, scale=10000000):
+    """tseed(1..k) = int(rand(0)*scale)+1 after srand(master): scale 1e7 in
+    bond_cond.f:65-70, 1e6 in bond_perc.f / site_perc.f:70-74."""
     ts = _i32(k)
-    L.lib().perc_trial_seeds(master, k, ts)
+    if scale == 10000000:
+        L.lib().perc_trial_seeds(master, k, ts)
+    else:
+        L.lib().perc_trial_seeds_scaled(master, k, scale, ts)
     return ts
 
 
@@ -321,22 +326,51 @@ def pb_grid(lattice, nb):
     return (pbarr * nb).astype(np.int64).astype(np.int32)  # truncation (H3 repeats kept)
 
 
-def first_spanning(ctx, order, lo=0, hi=None):
-    """Smallest bf at which a spanning cluster exists (the pc step of
-    bond_cond.f:381), by bisection over occupation counts with the GPU
-    labeling (spanning is monotone in bf)."""
-    hi = ctx.nb if hi is None else hi
-    ctx.occupy(L.BOND, bond_order=order, nbonds_=hi)
-    if ctx.label()["nspan"] == 0:
-        return 0
-    while hi - lo > 1:
-        mid = (lo + hi) // 2
-        ctx.occupy(L.BOND, bond_order=order, nbonds_=mid)
-        if ctx.label()["nspan"]:
-            hi = mid
-        else:
-            lo = mid
-    return hi
+def first_spanning(ctx, order, kind=L.BOND, n=None):
+    """Smallest count c such that occupying order[:c] spans (the pc step of
+    bond_cond.f:381; bond_perc.f / site_perc.f), 0 if none: perc_first_spanning,
+    a bisection with the GPU labeling.  The context is left occupied at c."""
+    n = (ctx.nb if kind == L.BOND else ctx.t) if n is None else n
+    o = np.ascontiguousarray(order[:n], dtype=np.int32)
+    first = C.c_int()
+    L.check(L.lib().perc_first_spanning(ctx.h, kind, L.ptr(o), n, 0, C.byref(first)),
+            "perc_first_spanning")
+    return first.value
+
+
+def threshold_scan(lattice=0, m=50, n=50, pbc=0, kind=L.BOND, master=58302, numtrials=10,
+                   ctx=None, device=0):
+    """bond_perc / site_perc (Fortran/Square/bond_perc.f, site_perc.f): per
+    trial ii, seed tseed(ii) = int(rand(0)*1e6)+1, the reference shuffle,
+    then the first occupation count that spans; the record is (tseed,
+    fraction = REAL*4 count/N, largest cluster size, spanning cluster size)
+    at that step (the whole order if nothing spans), sizes by the host
+    label replay."""
+    own = ctx is None
+    ctx = ctx or Context(lattice, m, n, pbc, device)
+    try:
+        N = ctx.nb if kind == L.BOND else ctx.t
+        seeds = trial_seeds(master, max(numtrials, 1), scale=1000000)
+        out = []
+        for ii in range(numtrials):
+            order = shuffled_ids(N, int(seeds[ii]))
+            first = first_spanning(ctx, order, kind, N)
+            c = first if first else N
+            r = ctx.label_numbers(kind)
+            perccls = int(r["csize"][r["perccln"]]) if first and r["perccln"] else 0
+            out.append(dict(tseed=int(seeds[ii]), count=c,
+                            f=float(np.float32(np.float32(c) / np.float32(N))),
+                            maxcs=r["maxcs"], perccls=perccls, perccln=r["perccln"]))
+        return out
+    finally:
+        if own:
+            ctx.close()
+
+
+def fmt_perc_rows(rows):
+    """bond_perc.txt / site_perc.txt records: (i10,",",f12.9,",",i10,",",i10)."""
+    return "".join("%10d,%12.9f,%10d,%10d\n" % (r["tseed"], r["f"], r["maxcs"], r["perccls"])
+                   for r in rows)
 
 
 def bond_cond_grid(lattice=0, m=10, n=10, pbc=0, master=58302, numtrials=1, Va=1.0, g0=1.0,

@@ -160,13 +160,17 @@ float perc_rand(int i) {
   return rand_locked(i);
 }
 
-void perc_trial_seeds(int master, int k, int* tseed) {
+void perc_trial_seeds_scaled(int master, int k, int scale, int* tseed) {
   std::lock_guard<std::mutex> lk(g_rand_mu);
   srand_locked(master);
   for (int i = 0; i < k; ++i) {
-    const float v = rand_locked(0) * (float)10000000;
+    const float v = rand_locked(0) * (float)scale;  // REAL*4 product, then int()
     tseed[i] = (int)v + 1;
   }
+}
+
+void perc_trial_seeds(int master, int k, int* tseed) {
+  perc_trial_seeds_scaled(master, k, 10000000, tseed);
 }
 
 int perc_nbonds(int lattice, int m, int n, int pbc) {
@@ -454,6 +458,49 @@ static int label_numbers_impl(const Geom& g, const std::vector<int>& bond_first,
   }
   if (stats) std::memcpy(stats, st, sizeof(st));
   return PERC_OK;
+}
+
+int perc_first_spanning(perc_ctx* h, int kind, const int* order, int n, int on_device,
+                        int* first) {
+  if (!h || !first || (kind != PERC_BOND && kind != PERC_SITE)) return PERC_EINVAL;
+  const long long cap = kind == PERC_BOND ? h->nb : h->g.t;
+  if (n < 0 || n > cap || (n && !order)) return PERC_EINVAL;
+  hipSetDevice(h->device);
+  const int* d = order;
+  if (!on_device && n) {  // one upload; every probe occupies a prefix of it
+    hipError_t e = hipMemcpy(h->d.order, order, sizeof(int) * n, hipMemcpyHostToDevice);
+    if (e != hipSuccess) return hip_status(e, "perc_first_spanning");
+    d = h->d.order;
+  }
+  auto occupy = [&](int c) {
+    return occupy_impl(h, kind, kind == PERC_SITE ? c : 0, d, kind == PERC_BOND ? c : 0, d, true);
+  };
+  auto spans = [&](int c, bool* out) -> int {
+    int rc = occupy(c);
+    if (rc) return rc;
+    int nspan = 0, nclus = 0, list[kMaxSpanList];
+    hipError_t e = dev_label(h, &nspan, list, &nclus);
+    if (e != hipSuccess) return hip_status(e, "perc_first_spanning");
+    *out = nspan > 0;
+    return PERC_OK;
+  };
+  // spanning only appears as elements are added (monotone in the count)
+  bool s = false;
+  int rc = spans(n, &s);
+  if (rc) return rc;
+  int lo = 0, hi = s ? n : 0;
+  while (s && hi - lo > 1) {
+    const int mid = lo + (hi - lo) / 2;
+    bool sm = false;
+    rc = spans(mid, &sm);
+    if (rc) return rc;
+    if (sm) hi = mid;
+    else lo = mid;
+  }
+  *first = hi;
+  rc = occupy(hi ? hi : n);  // leave the context at the first spanning count (or n)
+  if (rc) return rc;
+  return perc_label(h, nullptr, nullptr);
 }
 
 int perc_label_numbers(perc_ctx* h, int* bond_label, int* site_label, int* csize, int cap,

@@ -44,6 +44,21 @@ module perc_api
       integer(c_int) :: tseed(*)
     end subroutine perc_trial_seeds
 
+    subroutine perc_trial_seeds_scaled(master, k, scale, tseed) &
+        bind(C, name='perc_trial_seeds_scaled')
+      import :: c_int
+      integer(c_int), value :: master, k, scale
+      integer(c_int) :: tseed(*)
+    end subroutine perc_trial_seeds_scaled
+
+    integer(c_int) function perc_first_spanning(h, kind, order, nn, on_device, first) &
+        bind(C, name='perc_first_spanning')
+      import :: c_int, c_ptr
+      type(c_ptr), value :: h, order
+      integer(c_int), value :: kind, nn, on_device
+      integer(c_int) :: first
+    end function perc_first_spanning
+
     integer(c_int) function perc_nbonds(lattice, m, n, pbc) bind(C, name='perc_nbonds')
       import :: c_int
       integer(c_int), value :: lattice, m, n, pbc

@@ -54,10 +54,20 @@ VARIANTS = {
     "sq_bond_cond_3t": ("bond_cond", dict(lattice=0, m=12, n=12, pbc=0, numtrials=3,
                                           seed=58302)),
     "tri_bond_cond": ("bond_cond", dict(lattice=1, m=10, n=10, pbc=0, numtrials=1, seed=58302)),
+    # threshold scans (Square/bond_perc.f, site_perc.f): per trial tseed, first
+    # spanning fraction, largest and spanning cluster sizes
+    "sq_bond_perc": ("bond_perc", dict(lattice=0, m=50, n=50, pbc=0, numtrials=10, seed=58302)),
+    "sq_bond_perc_pbc": ("bond_perc", dict(lattice=0, m=40, n=30, pbc=1, numtrials=10,
+                                           seed=58302)),
+    "tri_bond_perc": ("bond_perc", dict(lattice=1, m=50, n=50, pbc=0, numtrials=10, seed=58302)),
+    "sq_site_perc": ("site_perc", dict(lattice=0, m=50, n=50, pbc=0, numtrials=40, seed=58302)),
+    "tri_site_perc": ("site_perc", dict(lattice=1, m=50, n=50, pbc=0, numtrials=40, seed=58302)),
+    "sq_site_perc_pbc": ("site_perc", dict(lattice=0, m=36, n=44, pbc=1, numtrials=40,
+                                           seed=58302)),
 }
 
 KEEP = {"bond.txt", "bondorder.txt", "site.txt", "siteorder.txt", "bondlist.txt",
-        "sbsite.txt", "sbbond.txt", "bondcond.txt"}
+        "sbsite.txt", "sbbond.txt", "bondcond.txt", "bond_perc.txt", "site_perc.txt"}
 MD5_ONLY = {"bondocc.txt", "siteocc.txt", "sbdebug.txt"}
 NUM = r"[-+]?(?:\d+\.?\d*|\.\d+)(?:[EeDd][-+]?\d+)?"
 

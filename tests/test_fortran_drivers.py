@@ -24,10 +24,14 @@ import golden_io as G
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 BIN = os.path.join(REPO, "percolation_amd", "fortran", "bin")
 TRACES = {"bondocc.txt", "siteocc.txt", "sbdebug.txt"}  # per-step logs, not produced
-NML = {"bondc": ("bondc", ("lattice", "m", "n", "pbc", "pb", "seed", "tol", "itmax")),
-       "site": ("site", ("lattice", "m", "n", "pbc", "ps", "seed")),
-       "sitebond": ("sitebond", ("lattice", "m", "n", "pbc", "ps", "pb", "sseed", "bseed")),
-       "bond_cond": ("bond_cond", ("lattice", "m", "n", "pbc", "numtrials", "seed"))}
+# golden kind -> (program, namelist group, parameters)
+NML = {"bondc": ("bondc", "bondc", ("lattice", "m", "n", "pbc", "pb", "seed", "tol", "itmax")),
+       "site": ("site", "site", ("lattice", "m", "n", "pbc", "ps", "seed")),
+       "sitebond": ("sitebond", "sitebond",
+                    ("lattice", "m", "n", "pbc", "ps", "pb", "sseed", "bseed")),
+       "bond_cond": ("bond_cond", "bond_cond", ("lattice", "m", "n", "pbc", "numtrials", "seed")),
+       "bond_perc": ("bond_perc", "perc_scan", ("lattice", "m", "n", "pbc", "numtrials", "seed")),
+       "site_perc": ("site_perc", "perc_scan", ("lattice", "m", "n", "pbc", "numtrials", "seed"))}
 
 
 def exe(prog, lattice):
@@ -39,14 +43,14 @@ def exe(prog, lattice):
 
 def run_variant(v, tmp_path, expect_ok=True):
     md = G.meta(v)
-    prog, keys = NML[md["kind"]]
+    prog, group, keys = NML[md["kind"]]
     p = md["params"]
     items = []
     for k in keys:
         if k in p:
             val = p[k]
             items.append("%s=%s" % (k, repr(float(val)) if isinstance(val, float) else int(val)))
-    (tmp_path / ("%s.nml" % prog)).write_text("&%s_nml %s /\n" % (prog, ", ".join(items)))
+    (tmp_path / ("%s.nml" % prog)).write_text("&%s_nml %s /\n" % (group, ", ".join(items)))
     r = subprocess.run([exe(prog, p["lattice"])], cwd=tmp_path, capture_output=True, text=True,
                        timeout=600)
     if expect_ok:
@@ -81,7 +85,8 @@ def test_driver_without_device_fails_loudly(tmp_path):
     assert not (tmp_path / "bond.txt").exists()
 
 
-FILE_VARIANTS = [v for v in G.variants() if G.meta(v)["kind"] in ("bondc", "site", "sitebond")]
+FILE_VARIANTS = [v for v in G.variants()
+                 if G.meta(v)["kind"] in ("bondc", "site", "sitebond", "bond_perc", "site_perc")]
 
 
 @pytest.mark.gpu
