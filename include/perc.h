@@ -130,6 +130,27 @@ int perc_label_numbers(perc_ctx *h, int *bond_label, int *site_label,
 int perc_first_spanning(perc_ctx *h, int kind, const int *order, int n, int on_device,
                         int *first);
 
+/* Mixed threshold scans (Square/sb_perc.f:104-372, Square/bs_perc.f:104-
+   395): one kind fixed, the other scanned.  scan = PERC_BOND: sites
+   site_order[0..nsites) occupied, *first = smallest c <= nbonds such that
+   bonds bond_order[0..c) make a spanning mixed cluster (bonds connect sites
+   whose ends are both occupied; spanning on bottom/top-row sites);
+   scan = PERC_SITE: bonds bond_order[0..nbonds) fixed, sites scanned.  0 if
+   nothing spans.  GPU labeling in a bisection; the context is left
+   unoccupied. */
+int perc_first_spanning_mixed(perc_ctx *h, int scan, const int *site_order, int nsites,
+                              const int *bond_order, int nbonds, int on_device, int *first);
+
+/* bs_perc's scan (Square/bs_perc.f:236-395) by O(N alpha) host replay:
+   bonds bond_order[0..nbond) fixed, sites added in site_order; *first = the
+   site count at which a cluster spans (0 if none).  c0_overflow != 0
+   reproduces the flang-built reference, whose out-of-bounds read of c(0)
+   exceeds every cluster size (hazard H11: a site whose first neighbour
+   bond is unoccupied leaves the lattice together with every cluster it
+   touches); c0_overflow == 0 is the intended site+bond connectivity. */
+int perc_bs_perc_replay(int lattice, int m, int n, int pbc, const int *site_order, int nsites,
+                        const int *bond_order, int nbond, int c0_overflow, int *first);
+
 /* Same numbering without a context or device: host-only O(N alpha) replay
    of an explicit occupancy (used by the drivers' text output and tests). */
 int perc_replay_labels(int lattice, int m, int n, int pbc, int kind, int nsites,

@@ -82,6 +82,10 @@ build tri_bond_perc           Triangular/bond_perc.f
 build sq_site_perc            Square/site_perc.f 's/numtrials = 1000 /numtrials = 40 /'
 build tri_site_perc           Triangular/site_perc.f 's/numtrials = 1000 /numtrials = 40 /'
 build sq_site_perc_pbc        Square/site_perc.f 's/numtrials = 1000 /numtrials = 40 /' 's/pbc = 0 /pbc = 1 /' 's/m = 50 /m = 36 /' 's/n = 50 /n = 44 /'
+build sq_sb_perc              Square/sb_perc.f 's/pscount = 42 /pscount = 4 /' 's/iter = 100/iter = 5/' 's/0.59d+00+(0.01d+00\*(i-1))/0.65d+00+(0.10d+00*(i-1))/'
+build tri_sb_perc             Triangular/sb_perc.f 's/pscount = 51 /pscount = 4 /' 's/iter = 100/iter = 5/' 's/0.50d+00+(0.01d+00\*(i-1))/0.60d+00+(0.10d+00*(i-1))/'
+build sq_bs_perc              Square/bs_perc.f 's/pbcount = 71 /pbcount = 5 /' 's/iter = 1000/iter = 8/' 's/0.30d+00+(0.01d+00\*(i-1))/0.55d+00+(0.10d+00*(i-1))/'
+build tri_bs_perc             Triangular/bs_perc.f 's/pbcount = 71 /pbcount = 5 /' 's/iter = 1000/iter = 8/' 's/0.30d+00+(0.01d+00\*(i-1))/0.55d+00+(0.10d+00*(i-1))/'
 # NR-level drop-in (route 1): the reference program with its
 # embedded Numerical Recipes routines (sprsin ... dsprstx, from the line
 # "SUBROUTINE sprsin" to the end of the file) deleted and libperc.so linked

@@ -83,6 +83,9 @@ SIGNATURES = {
     "perc_set_matrix_format": (C.c_int, [_VP, C.c_int]),
     "perc_matrix_format": (C.c_int, [_VP]),
     "perc_first_spanning": (C.c_int, [_VP, C.c_int, _VP, C.c_int, C.c_int, _VP]),
+    "perc_bs_perc_replay": (C.c_int, [C.c_int] * 4 + [_VP, C.c_int, _VP, C.c_int, C.c_int, _VP]),
+    "perc_first_spanning_mixed": (C.c_int, [_VP, C.c_int, _VP, C.c_int, _VP, C.c_int, C.c_int,
+                                            _VP]),
     "perc_trial_seeds_scaled": (None, [C.c_int, C.c_int, C.c_int, _I]),
     "perc_set_full_voltages": (C.c_int, [_VP, C.c_int]),
     "perc_stats_accumulate": (None, [_D, C.c_int, C.c_double, C.c_int, C.c_int]),

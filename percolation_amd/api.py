@@ -367,6 +367,95 @@ def threshold_scan(lattice=0, m=50, n=50, pbc=0, kind=L.BOND, master=58302, numt
             ctx.close()
 
 
+def first_spanning_mixed(ctx, scan, site_order, nsites, bond_order, nbonds):
+    """perc_first_spanning_mixed: sites fixed and bonds scanned (scan=BOND,
+    sb_perc) or bonds fixed and sites scanned (scan=SITE, bs_perc)."""
+    so = np.ascontiguousarray(site_order[:max(nsites, 1)], dtype=np.int32)
+    bo = np.ascontiguousarray(bond_order[:max(nbonds, 1)], dtype=np.int32)
+    first = C.c_int()
+    L.check(L.lib().perc_first_spanning_mixed(ctx.h, scan, L.ptr(so), nsites, L.ptr(bo), nbonds,
+                                              0, C.byref(first)), "perc_first_spanning_mixed")
+    return first.value
+
+
+def bs_perc_replay(lattice, m, n, pbc, site_order, nsites, bond_order, nbond, c0_overflow=True):
+    """perc_bs_perc_replay: bs_perc's site scan by host replay (first
+    spanning site count); c0_overflow reproduces the reference build
+    (hazard H11), False gives the intended site+bond connectivity."""
+    so = np.ascontiguousarray(site_order[:max(nsites, 1)], dtype=np.int32)
+    bo = np.ascontiguousarray(bond_order[:max(nbond, 1)], dtype=np.int32)
+    first = C.c_int()
+    L.check(L.lib().perc_bs_perc_replay(lattice, m, n, pbc, L.ptr(so), nsites, L.ptr(bo), nbond,
+                                        int(c0_overflow), C.byref(first)), "perc_bs_perc_replay")
+    return first.value
+
+
+def paired_seeds(pseed, k=1000):
+    """sseed(jj), bseed(jj) = int(rand(0)*1e7)+1 drawn alternately after
+    srand(pseed) (sb_perc.f / bs_perc.f:106-111)."""
+    lib = L.lib()
+    lib.perc_srand(int(pseed))
+    ss, bs = _i32(k), _i32(k)
+    for j in range(k):
+        ss[j] = int(np.float32(lib.perc_rand(0)) * np.float32(10000000)) + 1
+        bs[j] = int(np.float32(lib.perc_rand(0)) * np.float32(10000000)) + 1
+    return ss, bs
+
+
+def mixed_scan(lattice=0, m=50, n=50, pbc=0, scan=L.BOND, master=8811064, points=None,
+               iters=100, as_built=True, ctx=None, device=0):
+    """sb_perc (scan=BOND: sites fixed at ps, bonds added until a mixed
+    cluster spans; Square/sb_perc.f) / bs_perc (scan=SITE: bonds fixed at
+    pb, sites added; Square/bs_perc.f).  points: the ps (sb) / pb (bs)
+    values, default the reference's (square 0.59 + 0.01 i x 42, triangular
+    0.50 + 0.01 i x 51) / 0.30 + 0.01 i x 71.  Records (sseed, bseed, ps,
+    pb); the scanned fraction is 0 when nothing spans.  sb_perc's first
+    spanning bond count is the GPU bisection (perc_first_spanning_mixed);
+    bs_perc's is the host replay of the reference as built (as_built, hazard
+    H11) or, with as_built=False, the GPU bisection of the intended rule."""
+    own = ctx is None
+    ctx = ctx or Context(lattice, m, n, pbc, device)
+    try:
+        t, nb = ctx.t, ctx.nb
+        if points is None:
+            if scan == L.BOND:
+                points = ([0.59 + 0.01 * i for i in range(42)] if lattice == 0
+                          else [0.50 + 0.01 * i for i in range(51)])
+            else:
+                points = [0.30 + 0.01 * i for i in range(71)]
+        pseed = trial_seeds(master, 100)
+        out = []
+        for ii, pt in enumerate(points):
+            ss, bs = paired_seeds(pseed[ii])
+            for jj in range(iters):
+                so = shuffled_ids(t, int(ss[jj]))
+                bo = shuffled_ids(nb, int(bs[jj]))
+                if scan == L.BOND:
+                    ts = int(pt * t)  # sb_perc.f:210 (truncation)
+                    first = first_spanning_mixed(ctx, L.BOND, so, ts, bo, nb)
+                    ps = float(np.float32(ts) / np.float32(t))
+                    pb = float(np.float32(first) / np.float32(nb)) if first else 0.0
+                else:
+                    tb = int(pt * nb)  # bs_perc.f:209
+                    if as_built:
+                        first = bs_perc_replay(lattice, m, n, pbc, so, t, bo, tb, True)
+                    else:
+                        first = first_spanning_mixed(ctx, L.SITE, so, t, bo, tb)
+                    pb = float(np.float32(tb) / np.float32(nb))
+                    ps = float(np.float32(first) / np.float32(t)) if first else 0.0
+                out.append(dict(sseed=int(ss[jj]), bseed=int(bs[jj]), ps=ps, pb=pb, first=first))
+        return out
+    finally:
+        if own:
+            ctx.close()
+
+
+def fmt_mixed_rows(rows):
+    """sb_perc.txt / bs_perc.txt records: (i10,",",i10,",",f12.9,",",f12.9)."""
+    return "".join("%10d,%10d,%12.9f,%12.9f\n" % (r["sseed"], r["bseed"], r["ps"], r["pb"])
+                   for r in rows)
+
+
 def fmt_perc_rows(rows):
     """bond_perc.txt / site_perc.txt records: (i10,",",f12.9,",",i10,",",i10)."""
     return "".join("%10d,%12.9f,%10d,%10d\n" % (r["tseed"], r["f"], r["maxcs"], r["perccls"])

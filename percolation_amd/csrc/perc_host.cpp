@@ -503,6 +503,79 @@ int perc_first_spanning(perc_ctx* h, int kind, const int* order, int n, int on_d
   return perc_label(h, nullptr, nullptr);
 }
 
+int perc_bs_perc_replay(int lattice, int m, int n, int pbc, const int* site_order, int nsites,
+                        const int* bond_order, int nbond, int c0_overflow, int* first) {
+  if ((lattice != PERC_SQUARE && lattice != PERC_TRIANGULAR) || m < 2 || n < 2 || !first)
+    return PERC_EINVAL;
+  const Geom g = make_geom(lattice, m, n, pbc);
+  std::vector<int> bf(g.t + 2, 0);
+  for (int s = 1; s <= g.t + 1; ++s)
+    bf[s] = bf[s - 1] + ((s - 1 >= 1 && s - 1 <= g.t - 1) ? forward_count(g, s - 1) : 0);
+  if (nsites < 0 || nsites > g.t || nbond < 0 || nbond > bf[g.t + 1] || (nsites && !site_order) ||
+      (nbond && !bond_order))
+    return PERC_EINVAL;
+  *first = replay_bs_scan(g, bf, site_order, nsites, bond_order, nbond, c0_overflow != 0);
+  return PERC_OK;
+}
+
+int perc_first_spanning_mixed(perc_ctx* h, int scan, const int* site_order, int nsites,
+                              const int* bond_order, int nbonds, int on_device, int* first) {
+  if (!h || !first || (scan != PERC_BOND && scan != PERC_SITE)) return PERC_EINVAL;
+  if (nsites < 0 || nsites > h->g.t || nbonds < 0 || nbonds > h->nb) return PERC_EINVAL;
+  if ((nsites && !site_order) || (nbonds && !bond_order)) return PERC_EINVAL;
+  hipSetDevice(h->device);
+  // both lists on the device: the bond list in the context's upload buffer,
+  // the site list in a scratch buffer (host inputs are copied once)
+  const int* ds = site_order;
+  const int* db = bond_order;
+  int* tmp = nullptr;
+  hipError_t e = hipSuccess;
+  if (!on_device) {
+    e = hipMalloc(reinterpret_cast<void**>(&tmp), sizeof(int) * (nsites + 1));
+    if (e == hipSuccess && nsites)
+      e = hipMemcpy(tmp, site_order, sizeof(int) * nsites, hipMemcpyHostToDevice);
+    if (e == hipSuccess && nbonds)
+      e = hipMemcpy(h->d.order, bond_order, sizeof(int) * nbonds, hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+      if (tmp) hipFree(tmp);
+      return hip_status(e, "perc_first_spanning_mixed");
+    }
+    ds = tmp;
+    db = h->d.order;
+  }
+  auto occupy = [&](int c) {
+    return scan == PERC_BOND ? occupy_impl(h, PERC_SITEBOND, nsites, ds, c, db, true)
+                             : occupy_impl(h, PERC_SITEBOND, c, ds, nbonds, db, true);
+  };
+  auto spans = [&](int c, bool* out) -> int {
+    int rc = occupy(c);
+    if (rc) return rc;
+    int nspan = 0, nclus = 0, list[kMaxSpanList];
+    hipError_t err = dev_label(h, &nspan, list, &nclus);
+    if (err != hipSuccess) return hip_status(err, "perc_first_spanning_mixed");
+    *out = nspan > 0;
+    return PERC_OK;
+  };
+  const int n = scan == PERC_BOND ? nbonds : nsites;
+  bool s = false;
+  int rc = spans(n, &s);
+  int lo = 0, hi = s ? n : 0;
+  while (!rc && s && hi - lo > 1) {  // monotone in the scanned count
+    const int mid = lo + (hi - lo) / 2;
+    bool sm = false;
+    rc = spans(mid, &sm);
+    if (sm) hi = mid;
+    else lo = mid;
+  }
+  if (!rc) *first = hi;
+  // the device lists are not kept: the context is left unoccupied
+  h->occupied = h->labeled = h->assembled = false;
+  hipError_t e2 = hipDeviceSynchronize();
+  if (tmp) hipFree(tmp);
+  if (rc) return rc;
+  return hip_status(e2, "perc_first_spanning_mixed");
+}
+
 int perc_label_numbers(perc_ctx* h, int* bond_label, int* site_label, int* csize, int cap,
                        int* stats) {
   if (!h) return PERC_EINVAL;

@@ -168,6 +168,9 @@ int replay_sitebond(const Geom& g, const std::vector<int>& bond_first, const int
                     int nsites, const int* border, int nbonds, int* site_label,
                     int* bond_label, int* csize, int cap, int* stats);
 
+int replay_bs_scan(const Geom& g, const std::vector<int>& bond_first, const int* sorder,
+                   int nsites, const int* border, int nbond, bool c0_overflow);
+
 void set_error(const std::string& msg);
 int hip_status(hipError_t e, const char* where);
 

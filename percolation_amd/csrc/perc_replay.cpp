@@ -285,4 +285,96 @@ int replay_sitebond(const Geom& g, const std::vector<int>& bond_first, const int
   return PERC_OK;
 }
 
+// bs_perc's site loop (Square/bs_perc.f:236-350): bonds border[0..nbonds)
+// occupied first, each its own cluster of size 1; then sites are added in
+// order, each joining the clusters of its occupied neighbour bonds (the
+// largest one keeps its number, the others merge into it); returns the
+// first site count at which a cluster of >= 2n-1 elements holds a bottom-
+// and a top-row site, 0 if none.
+//
+// c0_overflow reproduces the reference as built (hazard H11): for an
+// unoccupied neighbour bond the reference reads c(b(j,3)) = c(0), out of
+// bounds, and in the flang build that word exceeds every cluster size. So
+// when a site's FIRST neighbour bond (nearestn order) is unoccupied, cluster
+// 0 wins the largest-cluster choice (bs_perc.f:271-285): the site and every
+// cluster reached through its other occupied bonds are renumbered to 0 --
+// they leave the lattice.  Without it (c(0) = 0, the intended rule) this is
+// plain site+bond connectivity, what perc_first_spanning_mixed computes.
+int replay_bs_scan(const Geom& g, const std::vector<int>& bond_first, const int* sorder,
+                   int nsites, const int* border, int nbond, bool c0_overflow) {
+  const int nbt = (int)nbonds(g), t = g.t;
+  const long long kHuge = 1ll << 60;  // c(0) as read by the reference build
+  DSU u(nbt + t + 1);                 // bonds 0..nbt-1, site s -> nbt + s
+  std::vector<char> occ(nbt, 0), dead(nbt + t + 1, 0), bot(nbt + t + 1, 0), top(nbt + t + 1, 0);
+  std::vector<long long> size(nbt + t + 1, 1);
+  for (int i = 0; i < nbond; ++i) {
+    const int id = border[i];
+    if (id > 0 && id <= nbt) occ[id - 1] = 1;
+  }
+  struct Row {
+    int root;        // -1: cluster 0 (unoccupied or removed bond)
+    long long size;  // nnb(k,4)
+  };
+  for (int i = 1; i <= nsites; ++i) {
+    const int s = sorder[i - 1];
+    if (s < 1 || s > t) continue;  // H2 spill sentinel: a phantom one-site cluster
+    int nn[6];
+    nearestn(g, s, nn);
+    Row rows[6];
+    int nr = 0;
+    for (int k = 0; k < g.scn; ++k) {
+      if (nn[k] == 0) continue;
+      const int lo = std::min(s, nn[k]), hi = std::max(s, nn[k]);
+      const int id = bond_index(g, bond_first, lo, hi);
+      Row r{-1, 0};
+      if (id >= 0) {
+        if (occ[id] && !dead[u.find(id)]) {
+          r.root = u.find(id);
+          r.size = size[r.root];
+        } else {
+          r.size = c0_overflow ? kHuge : 0;  // c(0)
+        }
+      }
+      rows[nr++] = r;
+    }
+    int lcn = nr ? rows[0].root : -1;
+    long long lcs = nr ? rows[0].size : 0;
+    for (int k = 1; k < nr; ++k)
+      if (rows[k].root >= 0 && rows[k].size > lcs) {
+        lcn = rows[k].root;
+        lcs = rows[k].size;
+      }
+    const int node = nbt + s;
+    if (lcs == 0) {  // no occupied neighbour bond: a new one-site cluster
+      bot[node] = s <= g.m;
+      top[node] = s > t - g.m;
+      continue;      // size 1 never spans (n >= 2)
+    }
+    if (lcn < 0) {  // merged into cluster 0: the site and those clusters leave
+      dead[node] = 1;
+      for (int k = 0; k < nr; ++k)
+        if (rows[k].root >= 0) dead[u.find(rows[k].root)] = 1;
+      continue;
+    }
+    long long tot = size[lcn];
+    char b = bot[lcn], tp = top[lcn];
+    int root = lcn;
+    for (int k = 0; k < nr; ++k) {
+      if (rows[k].root < 0) continue;
+      const int r = u.find(rows[k].root);
+      if (r == u.find(root)) continue;  // lcn itself, or a cluster already merged
+      tot += size[r];
+      b |= bot[r];
+      tp |= top[r];
+      root = u.unite(root, r);
+    }
+    root = u.unite(root, node);
+    size[root] = tot + 1;
+    bot[root] = b | (s <= g.m);
+    top[root] = tp | (s > t - g.m);
+    if (size[root] >= 2ll * g.n - 1 && bot[root] && top[root]) return i;
+  }
+  return 0;
+}
+
 }  // namespace perc

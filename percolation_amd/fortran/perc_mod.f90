@@ -59,6 +59,22 @@ module perc_api
       integer(c_int) :: first
     end function perc_first_spanning
 
+    integer(c_int) function perc_first_spanning_mixed(h, scan, site_order, nsites, &
+        bond_order, nbond, on_device, first) bind(C, name='perc_first_spanning_mixed')
+      import :: c_int, c_ptr
+      type(c_ptr), value :: h, site_order, bond_order
+      integer(c_int), value :: scan, nsites, nbond, on_device
+      integer(c_int) :: first
+    end function perc_first_spanning_mixed
+
+    integer(c_int) function perc_bs_perc_replay(lattice, m, n, pbc, site_order, nsites, &
+        bond_order, nbond, c0_overflow, first) bind(C, name='perc_bs_perc_replay')
+      import :: c_int
+      integer(c_int), value :: lattice, m, n, pbc, nsites, nbond, c0_overflow
+      integer(c_int) :: site_order(*), bond_order(*)
+      integer(c_int) :: first
+    end function perc_bs_perc_replay
+
     integer(c_int) function perc_nbonds(lattice, m, n, pbc) bind(C, name='perc_nbonds')
       import :: c_int
       integer(c_int), value :: lattice, m, n, pbc

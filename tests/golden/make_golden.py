@@ -64,10 +64,21 @@ VARIANTS = {
     "tri_site_perc": ("site_perc", dict(lattice=1, m=50, n=50, pbc=0, numtrials=40, seed=58302)),
     "sq_site_perc_pbc": ("site_perc", dict(lattice=0, m=36, n=44, pbc=1, numtrials=40,
                                            seed=58302)),
+    # mixed threshold scans (Square/sb_perc.f, bs_perc.f): points = the ps
+    # (sb) / pb (bs) values as edited in oracle/build_ref.sh, iters per point
+    "sq_sb_perc": ("sb_perc", dict(lattice=0, m=50, n=50, pbc=0, seed=8811064, iters=5,
+                                   points=[0.65 + 0.10 * i for i in range(4)])),
+    "tri_sb_perc": ("sb_perc", dict(lattice=1, m=50, n=50, pbc=0, seed=8811064, iters=5,
+                                    points=[0.60 + 0.10 * i for i in range(4)])),
+    "sq_bs_perc": ("bs_perc", dict(lattice=0, m=10, n=10, pbc=0, seed=229102, iters=8,
+                                   points=[0.55 + 0.10 * i for i in range(5)])),
+    "tri_bs_perc": ("bs_perc", dict(lattice=1, m=10, n=10, pbc=0, seed=229102, iters=8,
+                                    points=[0.55 + 0.10 * i for i in range(5)])),
 }
 
 KEEP = {"bond.txt", "bondorder.txt", "site.txt", "siteorder.txt", "bondlist.txt",
-        "sbsite.txt", "sbbond.txt", "bondcond.txt", "bond_perc.txt", "site_perc.txt"}
+        "sbsite.txt", "sbbond.txt", "bondcond.txt", "bond_perc.txt", "site_perc.txt",
+        "sb_perc.txt", "bs_perc.txt"}
 MD5_ONLY = {"bondocc.txt", "siteocc.txt", "sbdebug.txt"}
 NUM = r"[-+]?(?:\d+\.?\d*|\.\d+)(?:[EeDd][-+]?\d+)?"
 

@@ -31,7 +31,9 @@ NML = {"bondc": ("bondc", "bondc", ("lattice", "m", "n", "pbc", "pb", "seed", "t
                     ("lattice", "m", "n", "pbc", "ps", "pb", "sseed", "bseed")),
        "bond_cond": ("bond_cond", "bond_cond", ("lattice", "m", "n", "pbc", "numtrials", "seed")),
        "bond_perc": ("bond_perc", "perc_scan", ("lattice", "m", "n", "pbc", "numtrials", "seed")),
-       "site_perc": ("site_perc", "perc_scan", ("lattice", "m", "n", "pbc", "numtrials", "seed"))}
+       "site_perc": ("site_perc", "perc_scan", ("lattice", "m", "n", "pbc", "numtrials", "seed")),
+       "sb_perc": ("sb_perc", "mixed_scan", ("lattice", "m", "n", "pbc", "seed", "iters")),
+       "bs_perc": ("bs_perc", "mixed_scan", ("lattice", "m", "n", "pbc", "seed", "iters"))}
 
 
 def exe(prog, lattice):
@@ -50,6 +52,10 @@ def run_variant(v, tmp_path, expect_ok=True):
         if k in p:
             val = p[k]
             items.append("%s=%s" % (k, repr(float(val)) if isinstance(val, float) else int(val)))
+    if "points" in p:  # psarray(i) = pstart + pstep*(i-1), as edited in oracle/build_ref.sh
+        pts = p["points"]
+        items += ["pstart=%r" % round(pts[0], 6), "pstep=%r" % round(pts[1] - pts[0], 6),
+                  "npoints=%d" % len(pts)]
     (tmp_path / ("%s.nml" % prog)).write_text("&%s_nml %s /\n" % (group, ", ".join(items)))
     r = subprocess.run([exe(prog, p["lattice"])], cwd=tmp_path, capture_output=True, text=True,
                        timeout=600)
@@ -86,7 +92,8 @@ def test_driver_without_device_fails_loudly(tmp_path):
 
 
 FILE_VARIANTS = [v for v in G.variants()
-                 if G.meta(v)["kind"] in ("bondc", "site", "sitebond", "bond_perc", "site_perc")]
+                 if G.meta(v)["kind"] in ("bondc", "site", "sitebond", "bond_perc", "site_perc",
+                                          "sb_perc", "bs_perc")]
 
 
 @pytest.mark.gpu

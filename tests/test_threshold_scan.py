@@ -67,3 +67,98 @@ def test_threshold_scan_gpu(v):
     rows = api.threshold_scan(p["lattice"], p["m"], p["n"], p["pbc"], kind_of(v), p["seed"],
                               p["numtrials"])
     assert api.fmt_perc_rows(rows).encode() == G.text(v, fname(v))
+
+
+# ---------------------------------------------------------------- mixed scans
+MIXED = [v for v in G.variants() if G.meta(v)["kind"] in ("sb_perc", "bs_perc")]
+
+
+def mixed_rows(v, first_of):
+    """sb_perc / bs_perc records with the first spanning count from first_of(
+    scan, so, fixed-count, bo, N)."""
+    md = G.meta(v)
+    p = md["params"]
+    lat, m, n, pbc = p["lattice"], p["m"], p["n"], p["pbc"]
+    t, nb = m * n, api.nbonds(lat, m, n, pbc)
+    scan_b = md["kind"] == "sb_perc"
+    pseed = api.trial_seeds(p["seed"], 100)
+    rows = []
+    for ii, pt in enumerate(p["points"]):
+        ss, bs = api.paired_seeds(pseed[ii])
+        for jj in range(p["iters"]):
+            so, bo = api.shuffled_ids(t, int(ss[jj])), api.shuffled_ids(nb, int(bs[jj]))
+            fixed = int(pt * (t if scan_b else nb))
+            first = first_of(scan_b, so, fixed, bo)
+            N, F = (nb, t) if scan_b else (t, nb)
+            f = float(np.float32(first) / np.float32(N)) if first else 0.0
+            fx = float(np.float32(fixed) / np.float32(F))
+            rows.append(dict(sseed=int(ss[jj]), bseed=int(bs[jj]), ps=fx if scan_b else f,
+                             pb=f if scan_b else fx))
+    return rows
+
+
+@pytest.mark.parametrize("v", MIXED)
+def test_mixed_scan_host(v):
+    """sb_perc: bisection with the host sitebond replay as the spanning test;
+    bs_perc: the as-built replay (hazard H11)."""
+    p = G.meta(v)["params"]
+    lat, m, n, pbc = p["lattice"], p["m"], p["n"], p["pbc"]
+    t, nb = m * n, api.nbonds(lat, m, n, pbc)
+
+    def first_of(scan_b, so, fixed, bo):
+        if not scan_b:
+            return api.bs_perc_replay(lat, m, n, pbc, so, t, bo, fixed, True)
+
+        def spans(c):
+            return api.replay_labels(lat, m, n, pbc, PL.SITEBOND, site_order=so, nsites=fixed,
+                                     bond_order=bo, nbond=c)["perccln"] > 0
+        lo, hi = 0, nb
+        if not spans(nb):
+            return 0
+        while hi - lo > 1:
+            mid = (lo + hi) // 2
+            if spans(mid):
+                hi = mid
+            else:
+                lo = mid
+        return hi
+    assert api.fmt_mixed_rows(mixed_rows(v, first_of)).encode() == \
+        G.text(v, G.meta(v)["kind"] + ".txt")
+
+
+def test_bs_perc_intended_rule_is_connectivity():
+    """Without the c(0) overflow the bs_perc replay is plain site+bond
+    connectivity: its first spanning count equals the sitebond replay's."""
+    lat, m, n, pbc = 0, 12, 12, 0
+    t, nb = m * n, api.nbonds(lat, m, n, pbc)
+    for seed in range(1, 25):
+        so, bo = api.shuffled_ids(t, seed), api.shuffled_ids(nb, seed + 1000)
+        tb = int(0.7 * nb)
+        first = api.bs_perc_replay(lat, m, n, pbc, so, t, bo, tb, False)
+        c = next((c for c in range(1, t + 1)
+                  if api.replay_labels(lat, m, n, pbc, PL.SITEBOND, site_order=so, nsites=c,
+                                       bond_order=bo, nbond=tb)["perccln"] > 0), 0)
+        assert first == c, seed
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("v", MIXED)
+def test_mixed_scan_gpu(v):
+    md = G.meta(v)
+    p = md["params"]
+    rows = api.mixed_scan(p["lattice"], p["m"], p["n"], p["pbc"],
+                          PL.BOND if md["kind"] == "sb_perc" else PL.SITE, p["seed"],
+                          p["points"], p["iters"])
+    assert api.fmt_mixed_rows(rows).encode() == G.text(v, md["kind"] + ".txt")
+
+
+@pytest.mark.gpu
+def test_bs_scan_gpu_intended_equals_replay():
+    lat, m, n, pbc = 1, 20, 16, 1
+    t, nb = m * n, api.nbonds(lat, m, n, pbc)
+    with api.Context(lat, m, n, pbc) as ctx:
+        for seed in range(1, 12):
+            so, bo = api.shuffled_ids(t, seed), api.shuffled_ids(nb, seed + 77)
+            tb = int(0.6 * nb)
+            assert api.first_spanning_mixed(ctx, PL.SITE, so, t, bo, tb) == \
+                api.bs_perc_replay(lat, m, n, pbc, so, t, bo, tb, False)
