@@ -183,6 +183,9 @@ def main():
     ap.add_argument("--cpu-iters", type=int, default=20)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--occupancy", choices=("uniform", "reference"), default="uniform")
+    ap.add_argument("--force-dist", action="store_true",
+                    help="initialise the RCCL process group even at world size 1 (checks the "
+                         "multi-GPU path on one GPU)")
     ap.add_argument("--lattice", choices=("square", "tri"), default="square")
     ap.add_argument("--kind", choices=("bond", "site", "sitebond"), default="bond",
                     help="site / sitebond use the ConductCalc.m site / mixed rules")
@@ -205,7 +208,8 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    if world > 1:
+    use_dist = world > 1 or args.force_dist
+    if use_dist:
         dist.init_process_group("nccl", device_id=dev)
 
     L_, p = args.L, args.p
@@ -278,7 +282,7 @@ def main():
         log("warmup %d: iter=%d Gtop=%.12g %.0f ms" % (k, r["iter"], r["gtop"], r["t_total_ms"]))
     ctx.set_kernel_timing(True)
     ctx.kernel_stats(reset=True)
-    if world > 1:
+    if use_dist:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -290,7 +294,7 @@ def main():
             "total %.0f ms" % (k - args.warmup, ii_list[k] + 1, r["nspan"], r["iter"], r["gtop"],
                                r["gbot"], r["t_label_ms"], r["t_solve_ms"], r["t_total_ms"]))
     torch.cuda.synchronize()
-    if world > 1:
+    if use_dist:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     ks = ctx.kernel_stats(reset=True)
@@ -407,7 +411,7 @@ def main():
     ctx.close()
     if rank == 0:
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if use_dist:
         dist.destroy_process_group()
 
 

@@ -47,7 +47,7 @@ def allreduce(stats, elapsed, device="cpu"):
     import torch.distributed as dist
     s = torch.as_tensor(np.asarray(stats, dtype=np.float64), device=device).clone()
     t = torch.tensor([float(elapsed)], dtype=torch.float64, device=device)
-    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+    if dist.is_available() and dist.is_initialized():
         dist.all_reduce(s, op=dist.ReduceOp.SUM)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return s.cpu().numpy(), float(t.item())
