@@ -67,7 +67,8 @@ def xp_bytes(N, fmt, m, full):
     return (32 * N if fmt == "csr" else 26 * N) + x_bytes(N, m, full)
 
 
-KERNELS = {"ps": "k_cg_ps (fused p = bk p + r/d, x += ak p, q = A p, q.p; LDS tiles)",
+KERNELS = {"pm": "k_cg_pm (fused p = bk p + r/d, x += ak p, q = A p, q.p; register march)",
+           "ps": "k_cg_ps (fused p = bk p + r/d, x += ak p, q = A p, q.p; LDS tiles)",
            "spmv": "k_cg_spmv (SpMV q = A p + q.p dot)",
            "resid": "k_cg_b (r -= ak q, z = r/d, z.r and r.r dots)",
            "xp": "k_cg_p (x += ak p, p = bk p + r/d)"}
@@ -127,7 +128,9 @@ def cpu_baseline(L_, p, order, gpu_iters, cpu_iters):
 
 
 # rocprof kernel names of the CG kernels, per operator format
-ROCPROF_NAMES = {("ps", "stencil"): ("k_cg_ps<4>", "k_cg_ps<6>"),
+ROCPROF_NAMES = {("pm", "stencil"): ("k_cg_pm",),
+                 ("ps", "stencil_tiled"): ("k_cg_ps<4>", "k_cg_ps<6>"),
+                 ("resid", "stencil_tiled"): ("k_cg_b<true>",),
                  ("spmv", "stencil_split"): ("k_cg_spmv<4>", "k_cg_spmv<6>"),
                  ("resid", "stencil_split"): ("k_cg_b<true>",),
                  ("resid", "stencil"): ("k_cg_b<true>",),
@@ -192,7 +195,7 @@ def main():
     ap.add_argument("--ps", type=float, default=0.593, help="site fraction for --kind sitebond")
     ap.add_argument("--full-voltages", action="store_true",
                     help="update x on every row every iteration (perc_set_full_voltages)")
-    ap.add_argument("--format", choices=("auto", "stencil", "stencil_split", "csr"),
+    ap.add_argument("--format", choices=("auto", "stencil", "stencil_tiled", "stencil_split", "csr"),
                     default="auto",
                     help="solver operator format (perc_set_matrix_format)")
     args = ap.parse_args()
@@ -255,6 +258,7 @@ def main():
                                                             time.perf_counter() - t0))
     ctx = api.Context(lat, L_, L_, 0, device=local)
     ctx.set_matrix_format({"auto": P.FMT_AUTO, "stencil": P.FMT_STENCIL,
+                           "stencil_tiled": P.FMT_STENCIL_TILED,
                            "stencil_split": P.FMT_STENCIL_SPLIT, "csr": P.FMT_CSR}[args.format])
     ctx.set_full_voltages(args.full_voltages)
     N, nnz = ctx.system_size()
@@ -304,8 +308,8 @@ def main():
     value = nsolves / tmax
 
     try:  # the format the solves used (the last realisation may not span: no system)
-        fmt = {P.FMT_STENCIL: "stencil", P.FMT_STENCIL_SPLIT: "stencil_split",
-               P.FMT_CSR: "csr"}[ctx.matrix_format()]
+        fmt = {P.FMT_STENCIL: "stencil", P.FMT_STENCIL_TILED: "stencil_tiled",
+               P.FMT_STENCIL_SPLIT: "stencil_split", P.FMT_CSR: "csr"}[ctx.matrix_format()]
         assembled = True
     except P.PercError:
         fmt = {"auto": "stencil"}.get(args.format, args.format)
@@ -315,8 +319,8 @@ def main():
         """(key, stats key, perc_bench_kernel id, bytes) of the CG kernels of
         operator format f"""
         full = args.full_voltages
-        if f == "stencil":
-            return [("ps", "spmv", 1, ps_bytes(N, L_, full)),
+        if f in ("stencil", "stencil_tiled"):
+            return [("pm" if f == "stencil" else "ps", "spmv", 1, ps_bytes(N, L_, full)),
                     ("resid", "resid", 2, resid_bytes(N, f))]
         return [("spmv", "spmv", 1, spmv_bytes(N, nnz, f)), ("resid", "resid", 2, resid_bytes(N, f)),
                 ("xp", "xp", 3, xp_bytes(N, f, L_, full))]
@@ -340,14 +344,15 @@ def main():
     # after the timed region, on the last assembled system: each kernel in
     # both operator formats, back to back (perc_bench_kernel; clobbers x)
     probe = {}
-    for fname, fcode in (("stencil", P.FMT_STENCIL), ("stencil_split", P.FMT_STENCIL_SPLIT),
+    for fname, fcode in (("stencil", P.FMT_STENCIL), ("stencil_tiled", P.FMT_STENCIL_TILED),
+                         ("stencil_split", P.FMT_STENCIL_SPLIT),
                          ("csr", P.FMT_CSR)) if assembled else ():
         try:
             ctx.set_matrix_format(fcode)
         except Exception:
             continue
         row = {}
-        plain = [] if fname == "stencil" else [("spmv_plain", "", 0, spmv_bytes(N, nnz, fname))]
+        plain = [] if fname in ("stencil", "stencil_tiled") else [("spmv_plain", "", 0, spmv_bytes(N, nnz, fname))]
         for key, _, which, nbytes in plain + kernel_set(fname):
             ms = ctx.bench_kernel(which, 50)
             row[key] = {"ms": round(ms, 5), "gbs": round(nbytes / (ms * 1e-3) / 1e9, 1)}

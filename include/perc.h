@@ -203,16 +203,19 @@ int perc_system_size(perc_ctx *h, long long *out);
 /* Operator format of the solver.  The Kirchhoff matrix of a lattice has two
    distinct off-diagonal values (-g0 inside the spanning component, -leak
    elsewhere, bondc.f:482-538) on a fixed stencil, so besides the CSR copy
-   the assembly writes one byte per row (bit j = "in" for the j-th sorted
-   neighbour slot) and the SpMV/CG kernels rebuild each row -- values,
-   diagonal and summation order -- from that byte: bitwise the same numbers
-   as the CSR path from ~1/4 of its bytes.  PERC_FMT_AUTO (default) uses the
-   stencil operator whenever every stencil bond exists; the NR symbols
-   (sprsin_/linbcg_) always use CSR. */
+   the assembly writes a 16-bit code per row (bit j = "in" for the j-th
+   sorted neighbour slot, slot count, row form) and the SpMV/CG kernels
+   rebuild each row -- values, diagonal and summation order -- from that
+   code: bitwise the same numbers as the CSR path from 2 of its 76 bytes.
+   PERC_FMT_AUTO (default) uses the stencil operator whenever every stencil
+   bond exists; the NR symbols (sprsin_/linbcg_) always use CSR.
+   PERC_FMT_STENCIL fuses the p update into the SpMV: the register-march
+   kernel when m is a multiple of 128, else the LDS-tiled one (m even). */
 #define PERC_FMT_AUTO 0
 #define PERC_FMT_CSR 1
 #define PERC_FMT_STENCIL 2        /* stencil, p update fused into the SpMV  */
 #define PERC_FMT_STENCIL_SPLIT 3  /* stencil, separate p-update and SpMV kernels */
+#define PERC_FMT_STENCIL_TILED 4  /* stencil, fused, always the LDS-tiled kernel */
 int perc_set_matrix_format(perc_ctx *h, int fmt);
 /* Interior voltages.  linbcg never reads x inside its iteration and the
    terminal currents read it only on the interior rows next to the
@@ -222,8 +225,15 @@ int perc_set_matrix_format(perc_ctx *h, int fmt);
    linbcg does.  Default off. */
 int perc_set_full_voltages(perc_ctx *h, int enable);
 
-/* format the solver kernels use on the assembled system (PERC_FMT_CSR,
-   PERC_FMT_STENCIL or PERC_FMT_STENCIL_SPLIT) */
+/* Band height (lattice rows per wave) of the register-march kernel; 0 (default)
+   picks the tallest of 32, 16, .. 2 rows that still gives >= 4096 waves.
+   A tuning / test knob: results are the same up to the association of the
+   q.p dot. */
+int perc_set_march_rows(perc_ctx *h, int rows);
+
+/* format the solver kernels use on the assembled system: PERC_FMT_CSR,
+   PERC_FMT_STENCIL (register-march fused kernel), PERC_FMT_STENCIL_TILED
+   (LDS-tiled fused kernel) or PERC_FMT_STENCIL_SPLIT */
 int perc_matrix_format(perc_ctx *h);
 
 /* ---- one hot-path realisation (bench / ensemble) ---------------------- */

@@ -23,7 +23,7 @@ SQUARE, TRIANGULAR = 0, 1
 BOND, SITE, SITEBOND = 0, 1, 2
 RULE_BOND, RULE_SITE, RULE_MIXED = 0, 1, 2
 CUR_FORTRAN, CUR_MATLAB = 0, 1
-FMT_AUTO, FMT_CSR, FMT_STENCIL, FMT_STENCIL_SPLIT = 0, 1, 2, 3
+FMT_AUTO, FMT_CSR, FMT_STENCIL, FMT_STENCIL_SPLIT, FMT_STENCIL_TILED = 0, 1, 2, 3, 4
 
 
 class LabelInfo(C.Structure):
@@ -88,6 +88,7 @@ SIGNATURES = {
                                             _VP]),
     "perc_trial_seeds_scaled": (None, [C.c_int, C.c_int, C.c_int, _I]),
     "perc_set_full_voltages": (C.c_int, [_VP, C.c_int]),
+    "perc_set_march_rows": (C.c_int, [_VP, C.c_int]),
     "perc_stats_accumulate": (None, [_D, C.c_int, C.c_double, C.c_int, C.c_int]),
     "sprsin_": (None, [_VP] * 7),
     "dsprsax_": (None, [_VP] * 5),

@@ -197,12 +197,16 @@ class Context:
                     xp_ms=st[4], xp_n=int(st[5]))
 
     def set_matrix_format(self, fmt):
-        """PERC_FMT_AUTO / _CSR / _STENCIL (fused) / _STENCIL_SPLIT (perc.h)."""
+        """PERC_FMT_AUTO / _CSR / _STENCIL (fused) / _STENCIL_SPLIT / _STENCIL_TILED (perc.h)."""
         L.check(L.lib().perc_set_matrix_format(self.h, int(fmt)), "perc_set_matrix_format")
 
     def set_full_voltages(self, enable=True):
         """Keep every interior voltage up to date during the solve (perc.h)."""
         L.check(L.lib().perc_set_full_voltages(self.h, int(enable)), "perc_set_full_voltages")
+
+    def set_march_rows(self, rows=0):
+        """Band height of the register-march kernel (0: auto; perc.h)."""
+        L.check(L.lib().perc_set_march_rows(self.h, int(rows)), "perc_set_march_rows")
 
     def matrix_format(self):
         rc = L.lib().perc_matrix_format(self.h)

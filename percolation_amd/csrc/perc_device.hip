@@ -66,6 +66,24 @@ __device__ __forceinline__ void block_sum(double (&v)[NV], double* s_red /*8*NV*
   }
 }
 
+// Nontemporal stores for the CG vectors each kernel writes and the next one
+// reads (p, q, r): they stream past L2 / the Infinity Cache instead of
+// evicting what the next kernel reads.  Measured on the real PS/B sequence
+// with pure streams (tools/mix_bench.hip): 0.177 -> 0.130 ms / iteration.
+typedef double nt_double2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void st2(double* p, double2 v, bool nt) {
+  if (nt) {
+    nt_double2 t = {v.x, v.y};
+    __builtin_nontemporal_store(t, reinterpret_cast<nt_double2*>(p));
+  } else {
+    *reinterpret_cast<double2*>(p) = v;
+  }
+}
+__device__ __forceinline__ void st1(double* p, double v, bool nt) {
+  if (nt) __builtin_nontemporal_store(v, p);
+  else *p = v;
+}
+
 __device__ __forceinline__ void store_sc1(double* p, double v) {
   __hip_atomic_store(reinterpret_cast<unsigned long long*>(p), __double_as_longlong(v),
                      __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -607,6 +625,7 @@ struct StencilView {
   const uint16_t* code;
   double ng0, nleak;  // -g0, -leak
   StencilForms F;
+  const double* dtab;  // code_diag of every code, by diag_idx (filled per assembly)
 };
 
 __device__ __forceinline__ double code_diag(unsigned c, double ng0, double nleak) {
@@ -616,6 +635,22 @@ __device__ __forceinline__ double code_diag(unsigned c, double ng0, double nleak
   for (int j = 0; j < kMaxSlots; ++j)
     if (j < cnt) rs = rs + (((c >> j) & 1u) ? ng0 : nleak);
   return -rs;
+}
+
+// The diagonal of a row depends on 9 bits of its code (slot in-bits, count):
+// the hot kernels read it from a 512-entry table (filled by code_diag itself,
+// so bitwise the same) staged in LDS instead of re-summing the slots.
+constexpr int kDiagTab = 512;
+__device__ __forceinline__ unsigned diag_idx(unsigned c) { return (c & 0x3fu) | ((c >> 2) & 0x1c0u); }
+
+__global__ void k_fill_dtab(double* dtab, double ng0, double nleak) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e < kDiagTab) dtab[e] = code_diag((e & 0x3fu) | ((e & 0x1c0u) << 2), ng0, nleak);
+}
+
+// copy the table to LDS (all threads call; the caller's barrier publishes it)
+__device__ __forceinline__ void load_dtab(const StencilView& St, double* s_dt) {
+  for (int e = threadIdx.x; e < kDiagTab; e += blockDim.x) s_dt[e] = St.dtab[e];
 }
 
 // stage the form offsets in LDS (all threads call; ends with a barrier)
@@ -645,6 +680,21 @@ __device__ __forceinline__ double st_combine(unsigned c, const double (&xv)[S],
 #pragma unroll
   for (int j = 0; j < S; ++j) {
     const double pr = gv[j] * xv[j];
+    acc = use[j] ? acc + pr : acc;
+  }
+  return acc;
+}
+
+// st_combine with the row's diagonal d (= code_diag(c)) supplied
+template <int S>
+__device__ __forceinline__ double st_combine_d(unsigned c, double d, const double (&xv)[S],
+                                               const bool (&use)[S], double xi, double ng0,
+                                               double nleak) {
+  double acc = d * xi;
+#pragma unroll
+  for (int j = 0; j < S; ++j) {
+    const double gv = ((c >> j) & 1u) ? ng0 : nleak;
+    const double pr = gv * xv[j];
     acc = use[j] ? acc + pr : acc;
   }
   return acc;
@@ -745,6 +795,7 @@ __global__ __launch_bounds__(kBlock) void k_spmv_st(StencilView A, const double*
 // interior system as a lattice of nrows x m sites, in tiles of TILEH x kTileW
 struct TileGeom {
   int m, nrows, pbc, tpr;  // tpr: tiles per lattice row
+  int bh;                  // band height of the register-march kernel
 };
 
 struct CGArgs {
@@ -759,6 +810,7 @@ struct CGArgs {
   int fused;
   int b_reverse;  // B walks the row chunks in reverse logical order (fused mode)
   int xrows;      // 0: x kept on all rows; else only rows i < xrows or i >= N - xrows
+  int nt;         // nontemporal stores of p, q, r (stencil kernels)
   double* q;
   double* partials;  // kRedSlots slots of pstride doubles
   unsigned* tickets; // kRedSlots slots of tstride counters
@@ -888,6 +940,11 @@ __global__ __launch_bounds__(kBlock) void k_cg_b(CGArgs a) {
   if (S->done) return;
   __shared__ double s_red[32];
   __shared__ int s_flag[2];
+  __shared__ double s_dt[ST ? kDiagTab : 1];
+  if (ST) {
+    load_dtab(a.St, s_dt);
+    __syncthreads();
+  }
   const int k = S->iter + 1;
   const double ak = S->ak;
   const double* __restrict__ q = a.q;
@@ -899,20 +956,40 @@ __global__ __launch_bounds__(kBlock) void k_cg_b(CGArgs a) {
   block_pairs_lb(N, lbq, &q0, &q1);
   double acc[2] = {0.0, 0.0};  // z.r, r.r
   const int qf = min(q1, N / 2);
-#pragma unroll 4
-  for (int j = q0 + threadIdx.x; j < qf; j += kBlock) {
-    const int i = 2 * j;
-    const double2 qv = *reinterpret_cast<const double2*>(q + i);
-    const double2 dv = diag2<ST>(a, i);
-    double2 rv = *reinterpret_cast<const double2*>(r + i);
-    rv.x = rv.x - ak * qv.x;
-    rv.y = rv.y - ak * qv.y;
-    *reinterpret_cast<double2*>(r + i) = rv;
-    const double z0 = rv.x / dv.x, z1 = rv.y / dv.y;
-    acc[0] = acc[0] + z0 * rv.x;
-    acc[0] = acc[0] + z1 * rv.y;
-    acc[1] = acc[1] + rv.x * rv.x;
-    acc[1] = acc[1] + rv.y * rv.y;
+  const bool nt = ST && a.nt;
+  // kBU pairs per thread in flight: every load of a batch is issued before
+  // the first store (the compiler will not move loads of r above a store
+  // to r, so a plain loop waits out one memory round trip per pair)
+  constexpr int kBU = 4;
+  for (int j0 = q0 + threadIdx.x; j0 < qf; j0 += kBlock * kBU) {
+    double2 qv[kBU], rv[kBU], dv[kBU];
+    unsigned cc[kBU];
+#pragma unroll
+    for (int u = 0; u < kBU; ++u) {
+      const int j = j0 + u * kBlock;
+      if (j < qf) {
+        qv[u] = *reinterpret_cast<const double2*>(q + 2 * j);
+        rv[u] = *reinterpret_cast<const double2*>(r + 2 * j);
+        if (ST) cc[u] = *reinterpret_cast<const unsigned*>(a.St.code + 2 * j);
+        else dv[u] = *reinterpret_cast<const double2*>(a.A.diag + 2 * j);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < kBU; ++u) {
+      const int j = j0 + u * kBlock;
+      if (j < qf) {
+        if (ST) dv[u] = make_double2(s_dt[diag_idx(cc[u] & 0xffffu)], s_dt[diag_idx(cc[u] >> 16)]);
+        double2 rn;
+        rn.x = rv[u].x - ak * qv[u].x;
+        rn.y = rv[u].y - ak * qv[u].y;
+        st2(r + 2 * j, rn, nt);
+        const double z0 = rn.x / dv[u].x, z1 = rn.y / dv[u].y;
+        acc[0] = acc[0] + z0 * rn.x;
+        acc[0] = acc[0] + z1 * rn.y;
+        acc[1] = acc[1] + rn.x * rn.x;
+        acc[1] = acc[1] + rn.y * rn.y;
+      }
+    }
   }
   if ((N & 1) && q1 > N / 2 && threadIdx.x == 0) {
     const int i = N - 1;
@@ -1027,8 +1104,8 @@ __device__ __forceinline__ void load_form_lds(const StencilView& St, int* s_off,
 // y(i) of row i (code c) from the LDS tile; e0 = LDS index of site i
 template <int SL>
 __device__ __forceinline__ double tile_row(const StencilView& St, const int* s_off,
-                                           const int* s_dd, const double* s_p, int i, int e0,
-                                           unsigned c, double* xi) {
+                                           const int* s_dd, const double* s_dt, const double* s_p,
+                                           int i, int e0, unsigned c, double* xi) {
   const int f = c >> 11, cnt = (c >> 8) & 7;
   double xv[SL];
   bool use[SL];
@@ -1039,7 +1116,7 @@ __device__ __forceinline__ double tile_row(const StencilView& St, const int* s_o
     xv[j] = s_p[use[j] ? e0 + s_dd[f * kMaxSlots + j] : e0];
   }
   *xi = s_p[e0];
-  return st_combine<SL>(c, xv, use, *xi, St.ng0, St.nleak);
+  return st_combine_d<SL>(c, s_dt[diag_idx(c)], xv, use, *xi, St.ng0, St.nleak);
 }
 
 template <int SL, bool STORE_Q, int TILEH>
@@ -1052,13 +1129,15 @@ __global__ __launch_bounds__(tile_threads(TILEH)) void k_cg_ps(CGArgs a) {
   __shared__ __attribute__((aligned(16))) double s_p[kTH * kTW];
   __shared__ int s_off[kMaxForms * kMaxSlots];
   __shared__ int s_dd[kMaxForms * kMaxSlots];
+  __shared__ double s_dt[kDiagTab];
   __shared__ double s_red[32];
   __shared__ int s_flag[2];
   load_form_lds(a.St, s_off, s_dd);
+  load_dtab(a.St, s_dt);
+  __syncthreads();
   const int k = S->iter + 1;
   const bool first = k == 1;
   const double bk = S->bk, ak = S->ak;
-  const double ng0 = a.St.ng0, nleak = a.St.nleak;
   const double* __restrict__ pold = a.pb[(k - 1) & 1];
   double* __restrict__ pnew = a.pb[k & 1];
   const double* __restrict__ r = a.r;
@@ -1079,8 +1158,8 @@ __global__ __launch_bounds__(tile_threads(TILEH)) void k_cg_ps(CGArgs a) {
       const double2 pv = first ? make_double2(0.0, 0.0)
                                : *reinterpret_cast<const double2*>(pold + idx);
       double2 xv = xw ? *reinterpret_cast<const double2*>(x + idx) : make_double2(0.0, 0.0);
-      const double z0 = rv.x / code_diag(cc & 0xffffu, ng0, nleak);
-      const double z1 = rv.y / code_diag(cc >> 16, ng0, nleak);
+      const double z0 = rv.x / s_dt[diag_idx(cc & 0xffffu)];
+      const double z1 = rv.y / s_dt[diag_idx(cc >> 16)];
       if (first) {
         pn.x = z0;
         pn.y = z1;
@@ -1093,7 +1172,7 @@ __global__ __launch_bounds__(tile_threads(TILEH)) void k_cg_ps(CGArgs a) {
           *reinterpret_cast<double2*>(x + idx) = xv;
         }
       }
-      if (own) *reinterpret_cast<double2*>(pnew + idx) = pn;
+      if (own) st2(pnew + idx, pn, a.nt);
     } else {
       tr = e / (kTW / 2);
       tc = 2 * (e - tr * (kTW / 2));
@@ -1120,13 +1199,254 @@ __global__ __launch_bounds__(tile_threads(TILEH)) void k_cg_ps(CGArgs a) {
       const int i = (t.r0 + lr) * a.T.m + t.c0 + lc;
       double xi;
       const double qv =
-          tile_row<SL>(a.St, s_off, s_dd, s_p, i, (lr + 1) * kTW + lc + 2, cr[u], &xi);
-      if (STORE_Q) a.q[i] = qv;
+          tile_row<SL>(a.St, s_off, s_dd, s_dt, s_p, i, (lr + 1) * kTW + lc + 2, cr[u], &xi);
+      if (STORE_Q) st1(a.q + i, qv, a.nt);
       dot[0] = dot[0] + qv * xi;
     }
   }
   double tot[1];
   if (publish_and_reduce<1>(dot, a.partials, a.tickets, lb, gridDim.x, tot, s_red, s_flag)) {
+    if (threadIdx.x == 0) {
+      S->akden = tot[0];
+      S->ak = S->bknum / tot[0];
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Register-march fused P(k)+S(k) (stencil operator, m a multiple of 128).
+// A wave owns a strip of 128 columns (a column pair per lane, 16-B
+// accesses) and walks down a band of H rows.  Rows are prefetched D steps
+// ahead into registers; p(k) of the rows above, at and below the current
+// row live in a three-row register window, the column neighbours come from
+// the adjacent lanes (lanes 0 / 63 also form p(k) of the halo column left
+// / right of the strip).  No LDS tile, no barrier between loading and the
+// SpMV: every wave streams like the B kernel.  Per row and element the
+// arithmetic is k_cg_ps's (z = r/d, p = bk p + z, x += ak p, q in slot
+// order), so every value is bitwise the other kernels'; only the q.p
+// association differs (rows summed per lane).
+constexpr int kMarchW = 128;     // columns per wave strip
+constexpr int kMarchWaves = 4;   // waves (strips) per workgroup
+constexpr int kMarchMinWaves = 4096;
+
+struct MRow {       // one prefetched row of the lane's pair (+ halo column)
+  double2 p, r;     // p(k-1), r
+  unsigned c;       // the pair's codes
+  double hp, hr;    // halo column (lanes 0 and 63)
+  unsigned hc;
+};
+struct MWin {       // p(k) at columns col-1, col, col+1, col+2 of one row
+  double l, e0, e1, rr;
+};
+
+// neighbour value at raster position kp (0..7: (-1,-1) (-1,0) (-1,1) (0,-1)
+// (0,1) (1,-1) (1,0) (1,1)) of element E (0: column col, 1: col+1)
+template <int E>
+__device__ __forceinline__ double mwin_at(int kp, const MWin& U, const MWin& C, const MWin& D) {
+  const MWin& W = kp < 3 ? U : (kp < 5 ? C : D);
+  const int dc = kp < 3 ? kp - 1 : (kp == 3 ? -1 : (kp == 4 ? 1 : kp - 6));
+  const int s = E + 1 + dc;  // 0: l, 1: e0, 2: e1, 3: rr
+  return s == 0 ? W.l : (s == 1 ? W.e0 : (s == 2 ? W.e1 : W.rr));
+}
+
+// q of element E: d x + sum over the form's slots (slot order) of g x_nb,
+// when the wave's rows all share one regular form (slot order = raster
+// order) with used-position bits `mask` (wave-uniform: scalar branches)
+template <int E>
+__device__ __forceinline__ double march_q(unsigned c, double d, double xi, unsigned mask,
+                                          const MWin& U, const MWin& C, const MWin& D,
+                                          double ng0, double nleak) {
+  double acc = d * xi;
+  int j = 0;
+#pragma unroll
+  for (int kp = 0; kp < 8; ++kp) {
+    if (mask & (1u << kp)) {
+      const double gv = ((c >> j) & 1u) ? ng0 : nleak;
+      acc = acc + gv * mwin_at<E>(kp, U, C, D);
+      ++j;
+    }
+  }
+  return acc;
+}
+
+// general path (rows whose wave mixes forms, or wrapped-column forms): the
+// lane's 12 window values are in the wave's LDS scratch s_w[v * 64 + lane]
+// (v = row * 4 + {l, e0, e1, rr}); slot j reads value kvi(kp_j) + E
+template <int E>
+__device__ __forceinline__ double march_q_gen(unsigned c, double d, double xi, unsigned pos,
+                                              const double* s_w, int lane, double ng0,
+                                              double nleak) {
+  // raster position -> window value index (row * 4 + 1 + dc), 4 bits each
+  constexpr unsigned kVi = 0xA9864210u;
+  double acc = d * xi;
+  const int cnt = (c >> 8) & 7;
+#pragma unroll
+  for (int j = 0; j < kMaxSlots; ++j) {
+    if (j < cnt) {
+      const int kp = (pos >> (3 * j)) & 7;
+      const int v = ((kVi >> (4 * kp)) & 15u) + E;
+      const double gv = ((c >> j) & 1u) ? ng0 : nleak;
+      acc = acc + gv * s_w[v * 64 + lane];
+    }
+  }
+  return acc;
+}
+
+constexpr int kMarchDepth = 2;  // rows prefetched ahead (3: +22 VGPRs, no faster)
+
+__global__ __launch_bounds__(64 * kMarchWaves) void k_cg_pm(CGArgs a) {
+  constexpr int D = kMarchDepth;
+  CGScalars* S = a.S;
+  if (S->done) return;
+  __shared__ double s_red[32];
+  __shared__ int s_flag[2];
+  __shared__ unsigned s_rpos[kMaxForms];
+  __shared__ double s_dt[kDiagTab];
+  __shared__ double s_win[kMarchWaves][12 * 64];  // general-path window scratch
+  if (threadIdx.x < kMaxForms) s_rpos[threadIdx.x] = a.St.F.rpos[threadIdx.x];
+  load_dtab(a.St, s_dt);
+  __syncthreads();
+  const int k = S->iter + 1;
+  const bool first = k == 1;
+  const double bk = S->bk, ak = S->ak;
+  const double ng0 = a.St.ng0, nleak = a.St.nleak;
+  const double* __restrict__ pold = a.pb[(k - 1) & 1];
+  double* __restrict__ pnew = a.pb[k & 1];
+  const double* __restrict__ r = a.r;
+  const uint16_t* __restrict__ code = a.St.code;
+  double* __restrict__ x = a.x;
+  const int N = a.St.N, m = a.T.m, nrows = a.T.nrows, H = a.T.bh;
+  const int lb = xcd_logical_block(blockIdx.x, gridDim.x);
+  const int lane = threadIdx.x & 63;
+  const int w = lb * kMarchWaves + (threadIdx.x >> 6);
+  const int spr = m / kMarchW;
+  const int band = w / spr, strip = w - band * spr;
+  const int r0 = band * H;
+  double dot = 0.0;
+  if (r0 < nrows) {  // wave-uniform
+    const int c0 = strip * kMarchW, col = c0 + 2 * lane;
+    int hcol = lane == 0 ? c0 - 1 : c0 + kMarchW;
+    bool hok = lane == 0 || lane == 63;
+    if (hcol < 0 || hcol >= m) {
+      if (a.T.pbc) hcol += hcol < 0 ? m : -m;
+      else hok = false;
+    }
+    const int rend = min(r0 + H, nrows);
+    const int nsteps = rend - r0 + 2;  // rows r0-1 .. rend
+    auto load = [&](int gr, MRow& R) {
+      R.p = R.r = make_double2(0.0, 0.0);
+      R.c = R.hc = 0u;
+      R.hp = R.hr = 0.0;
+      if (gr >= 0 && gr < nrows) {
+        const int i = gr * m + col;
+        R.c = *reinterpret_cast<const unsigned*>(code + i);
+        R.r = *reinterpret_cast<const double2*>(r + i);
+        if (!first) R.p = *reinterpret_cast<const double2*>(pold + i);
+        if (hok) {
+          const int hi = gr * m + hcol;
+          R.hc = code[hi];
+          R.hr = r[hi];
+          if (!first) R.hp = pold[hi];
+        }
+      }
+    };
+    MWin U{0.0, 0.0, 0.0, 0.0}, C = U, Dn = U;
+    unsigned cC = 0u, cD = 0u;
+    double dC0 = 1.0, dC1 = 1.0, dD0 = 1.0, dD1 = 1.0;
+    // p(k) of row gr (the new bottom row of the window), then q of row gr - 1
+    auto step = [&](const MRow& R, int gr) {
+      double2 pn = make_double2(0.0, 0.0);
+      double hpn = 0.0, d0 = 1.0, d1 = 1.0;
+      if (gr >= 0 && gr < nrows) {
+        d0 = s_dt[diag_idx(R.c & 0xffffu)];
+        d1 = s_dt[diag_idx(R.c >> 16)];
+        const double z0 = R.r.x / d0, z1 = R.r.y / d1;
+        if (first) {
+          pn.x = z0;
+          pn.y = z1;
+        } else {
+          pn.x = bk * R.p.x + z0;
+          pn.y = bk * R.p.y + z1;
+        }
+        if (hok) {
+          const double zh = R.hr / s_dt[diag_idx(R.hc)];
+          hpn = first ? zh : bk * R.hp + zh;
+        }
+        if (gr >= r0 && gr < rend) {  // own row (rend: the next band's first row)
+          const int i = gr * m + col;
+          st2(pnew + i, pn, a.nt);
+          if (!first && (a.xrows == 0 || i < a.xrows || i >= N - a.xrows)) {
+            double2 xv = *reinterpret_cast<const double2*>(x + i);
+            xv.x = xv.x + ak * R.p.x;
+            xv.y = xv.y + ak * R.p.y;
+            *reinterpret_cast<double2*>(x + i) = xv;
+          }
+        }
+      }
+      MWin W;
+      W.e0 = pn.x;
+      W.e1 = pn.y;
+      const double up = __shfl_up(pn.y, 1);
+      const double dn = __shfl_down(pn.x, 1);
+      W.l = lane == 0 ? hpn : up;
+      W.rr = lane == 63 ? hpn : dn;
+      U = C;
+      C = Dn;
+      Dn = W;
+      cC = cD;
+      dC0 = dD0;
+      dC1 = dD1;
+      cD = R.c;
+      dD0 = d0;
+      dD1 = d1;
+      if (gr - 1 >= r0) {  // the middle row is complete: q, q.p
+        const unsigned c0w = cC & 0xffffu, c1w = cC >> 16;
+        const unsigned f0 = c0w >> 11, f1 = c1w >> 11;
+        const unsigned ff = __builtin_amdgcn_readfirstlane(f0);
+        const bool uni = !__any(f0 != ff || f1 != ff) && a.St.F.regular[ff];
+        double q0, q1;
+        if (uni) {
+          const unsigned mask = a.St.F.rmask[ff];
+          q0 = march_q<0>(c0w, dC0, C.e0, mask, U, C, Dn, ng0, nleak);
+          q1 = march_q<1>(c1w, dC1, C.e1, mask, U, C, Dn, ng0, nleak);
+        } else {
+          double* s_w = s_win[threadIdx.x >> 6];
+          const MWin* rows[3] = {&U, &C, &Dn};
+#pragma unroll
+          for (int rr = 0; rr < 3; ++rr) {
+            s_w[(4 * rr + 0) * 64 + lane] = rows[rr]->l;
+            s_w[(4 * rr + 1) * 64 + lane] = rows[rr]->e0;
+            s_w[(4 * rr + 2) * 64 + lane] = rows[rr]->e1;
+            s_w[(4 * rr + 3) * 64 + lane] = rows[rr]->rr;
+          }
+          // lane-private slots: no cross-lane hazard, only the wave's own
+          // LDS write -> read order (lgkmcnt, inserted by the compiler)
+          q0 = march_q_gen<0>(c0w, dC0, C.e0, s_rpos[f0], s_w, lane, ng0, nleak);
+          q1 = march_q_gen<1>(c1w, dC1, C.e1, s_rpos[f1], s_w, lane, ng0, nleak);
+        }
+        const int i = (gr - 1) * m + col;
+        st2(a.q + i, make_double2(q0, q1), a.nt);
+        dot = dot + q0 * C.e0;
+        dot = dot + q1 * C.e1;
+      }
+    };
+    MRow ring[D];
+#pragma unroll
+    for (int u = 0; u < D; ++u) load(r0 - 1 + u, ring[u]);
+    for (int j0 = 0; j0 < nsteps; j0 += D) {
+#pragma unroll
+      for (int u = 0; u < D; ++u) {
+        const int j = j0 + u;
+        if (j < nsteps) {
+          const MRow R = ring[u];
+          if (j + D < nsteps) load(r0 - 1 + j + D, ring[u]);
+          step(R, r0 - 1 + j);
+        }
+      }
+    }
+  }
+  double v[1] = {dot}, tot[1];
+  if (publish_and_reduce<1>(v, a.partials, a.tickets, lb, gridDim.x, tot, s_red, s_flag)) {
     if (threadIdx.x == 0) {
       S->akden = tot[0];
       S->ak = S->bknum / tot[0];
@@ -1203,13 +1523,14 @@ __global__ void k_zero(double* v, long long n) {
 }
 
 // workgroups of the largest reduction (CG kernels or the tiled kernel)
-int red_grid(const perc_ctx* h) { return std::max(h->grid, h->tile_grid); }
+int red_grid(const perc_ctx* h) { return std::max({h->grid, h->tile_grid, h->march_grid_max}); }
+
 
 CGArgs make_cg_args(perc_ctx* h) {
   CGArgs a;
   a.A = CsrView{h->N, h->d.rowptr, h->d.col, h->d.val, h->d.diag};
-  a.St = StencilView{h->N, h->d.code, h->st_ng0, h->st_nleak, h->forms};
-  a.T = TileGeom{h->g.m, h->g.n - 2, h->g.pbc, (h->g.m + kTileW - 1) / kTileW};
+  a.St = StencilView{h->N, h->d.code, h->st_ng0, h->st_nleak, h->forms, h->d.dtab};
+  a.T = TileGeom{h->g.m, h->g.n - 2, h->g.pbc, (h->g.m + kTileW - 1) / kTileW, h->march_h};
   a.pb[0] = h->d.p0;
   a.pb[1] = h->d.p1;
   a.fused = h->fused ? 1 : 0;
@@ -1218,6 +1539,8 @@ CGArgs make_cg_args(perc_ctx* h) {
   // the next tiled kernel starts on the r that B wrote last (measured: B
   // 0.112 -> 0.097 ms at L = 4096)
   a.b_reverse = h->fused ? 1 : 0;
+  static const int nt_env = getenv("PERC_NT") ? atoi(getenv("PERC_NT")) : 1;
+  a.nt = nt_env;
   a.xrows = h->full_voltages || h->g.m <= 0 ? 0 : h->g.m;  // see dev_solve
   a.pstride = red_partials_size(red_grid(h));
   a.tstride = red_tickets_size(red_grid(h));
@@ -1240,6 +1563,10 @@ void launch_cg_spmv(perc_ctx* h, const CGArgs& a, int G) {
     const int th = h->tile_h;
     const dim3 G2(h->tile_grid), B2(tile_threads(th));
     hipStream_t st = h->stream;
+    if (h->march) {
+      k_cg_pm<<<h->march_grid, 64 * kMarchWaves, 0, st>>>(a);
+      return;
+    }
     if (h->g.scn == 4) {
       if (th == 32) k_cg_ps<4, true, 32><<<G2, B2, 0, st>>>(a);
       else if (th == 16) k_cg_ps<4, true, 16><<<G2, B2, 0, st>>>(a);
@@ -1297,6 +1624,22 @@ StencilForms stencil_forms(const Geom& g) {
       }
       ++F.nforms;
     }
+  for (int f = 0; f < F.nforms; ++f) {
+    F.regular[f] = 1;
+    int last = -1;
+    for (int j = 0; j < F.cnt[f]; ++j) {
+      const int dr = F.dr[f][j], dc = F.dc[f][j];
+      if (dr < -1 || dr > 1 || dc < -1 || dc > 1 || (dr == 0 && dc == 0)) {
+        F.regular[f] = 0;  // not a 3x3 stencil: the tiled kernels are not used
+        continue;
+      }
+      const int k9 = (dr + 1) * 3 + (dc + 1), kp = k9 < 4 ? k9 : k9 - 1;
+      F.rpos[f] |= (unsigned)kp << (3 * j);
+      F.rmask[f] |= 1u << kp;
+      if (kp <= last) F.regular[f] = 0;
+      last = kp;
+    }
+  }
   return F;
 }
 
@@ -1373,6 +1716,7 @@ hipError_t dev_build_lattice(perc_ctx* h) {
   HIP_TRY(dmalloc(&d.diag, N + 2));
   HIP_TRY(dmalloc(&d.rhs, N + 2));
   HIP_TRY(dmalloc(&d.code, (size_t)N + 8));
+  HIP_TRY(dmalloc(&d.dtab, kDiagTab));
   h->forms = stencil_forms(g);
   HIP_TRY(dmalloc(&d.sflag, 4));
   // occupancy + labeling
@@ -1396,6 +1740,11 @@ hipError_t dev_build_lattice(perc_ctx* h) {
   while (h->tile_h > 8 && cdiv(std::max(g.n - 2, 0), h->tile_h) * cdiv(g.m, kTileW) < kMinTiles)
     h->tile_h /= 2;
   h->tile_grid = cdiv(std::max(g.n - 2, 0), h->tile_h) * cdiv(g.m, kTileW);
+  // register-march kernel (full 128-column strips): reduction buffers for
+  // its largest grid (band height 1)
+  h->march_grid_max =
+      g.m % kMarchW == 0 && g.n > 2 ? cdiv((g.m / kMarchW) * (g.n - 2), kMarchWaves) : 0;
+  march_geometry(h);
   HIP_TRY(dmalloc(&d.partials, kRedSlots * red_partials_size(red_grid(h))));
   HIP_TRY(dmalloc(&d.tickets, kRedSlots * red_tickets_size(red_grid(h))));
   HIP_TRY(hipMemset(d.tickets, 0, kRedSlots * red_tickets_size(red_grid(h)) * sizeof(unsigned)));
@@ -1423,6 +1772,7 @@ hipError_t dev_alloc_matrix(perc_ctx* h, int N, long long nnz) {
   HIP_TRY(dmalloc(&d.q, nv));
   h->grid = cg_grid(N);
   h->tile_grid = 0;
+  h->march_grid = h->march_grid_max = 0;
   HIP_TRY(dmalloc(&d.partials, kRedSlots * red_partials_size(red_grid(h))));
   HIP_TRY(dmalloc(&d.tickets, kRedSlots * red_tickets_size(red_grid(h))));
   HIP_TRY(hipMemset(d.tickets, 0, kRedSlots * red_tickets_size(red_grid(h)) * sizeof(unsigned)));
@@ -1432,7 +1782,7 @@ hipError_t dev_alloc_matrix(perc_ctx* h, int N, long long nnz) {
 
 void dev_free_all(perc_ctx* h) {
   DeviceBuffers& d = h->d;
-  void* ptrs[] = {d.bond_first, d.rowptr, d.col, d.val, d.diag, d.rhs, d.code, d.sflag, d.bocc, d.socc,
+  void* ptrs[] = {d.bond_first, d.rowptr, d.col, d.val, d.diag, d.rhs, d.code, d.dtab, d.sflag, d.bocc, d.socc,
                   d.order, d.parent, d.member, d.bot, d.top, d.counters, d.x, d.r,
                   d.p0, d.p1, d.q, d.partials, d.tickets, d.scal, d.err_hist, d.iout};
   for (void* p : ptrs)
@@ -1517,10 +1867,28 @@ hipError_t dev_canon(perc_ctx* h, int* canon_out) {
   return hipFree(tmp);
 }
 
+// band height and grid of the register-march kernel: the requested height,
+// or the tallest (32 .. 2 rows) that still gives kMarchMinWaves waves
+void march_geometry(perc_ctx* h) {
+  const Geom& g = h->g;
+  h->march_grid = 0;
+  if (g.m % kMarchW != 0 || g.n <= 2) return;
+  const int spr = g.m / kMarchW, nrows = g.n - 2;
+  if (h->march_rows_req > 0) {
+    h->march_h = h->march_rows_req;
+  } else {
+    h->march_h = 32;
+    while (h->march_h > 2 && (long long)spr * cdiv(nrows, h->march_h) < kMarchMinWaves)
+      h->march_h /= 2;
+  }
+  h->march_grid = cdiv(spr * cdiv(nrows, h->march_h), kMarchWaves);
+}
+
 // solver kernels for the requested format and what the assembly allows
 void select_format(perc_ctx* h) {
   h->stencil = h->fmt_req != PERC_FMT_CSR && h->stencil_ok;
   h->fused = h->stencil && h->tiled_ok && h->fmt_req != PERC_FMT_STENCIL_SPLIT;
+  h->march = h->fused && h->march_ok && h->fmt_req != PERC_FMT_STENCIL_TILED;
 }
 
 hipError_t dev_assemble(perc_ctx* h, int rule, double g0, double leak, double Va, int span_root) {
@@ -1536,8 +1904,13 @@ hipError_t dev_assemble(perc_ctx* h, int rule, double g0, double leak, double Va
   HIP_TRY(hipStreamSynchronize(st));
   h->st_ng0 = -g0;
   h->st_nleak = -leak;
+  if (d.dtab) {
+    k_fill_dtab<<<cdiv(kDiagTab, kBlock), kBlock, 0, st>>>(d.dtab, -g0, -leak);
+    HIP_TRY(hipGetLastError());
+  }
   h->stencil_ok = (flag & 3) == 0 && h->forms.nforms > 0;
   h->tiled_ok = h->stencil_ok && (flag & 4) == 0 && h->tile_grid > 0 && h->g.m % 2 == 0;
+  h->march_ok = h->tiled_ok && h->march_grid > 0;
   select_format(h);
   return hipSuccess;
 }

@@ -625,7 +625,7 @@ int perc_conductance(perc_ctx* h, int rule, int cur_rule, double Va, double g0, 
   hipEventRecord(h->ev[0], st);
   hipError_t e = dev_assemble(h, rule, g0, leak, Va, h->span_root);
   if (e != hipSuccess) return hip_status(e, "perc_conductance/assemble");
-  if ((h->fmt_req == PERC_FMT_STENCIL && !h->tiled_ok) ||
+  if (((h->fmt_req == PERC_FMT_STENCIL || h->fmt_req == PERC_FMT_STENCIL_TILED) && !h->tiled_ok) ||
       (h->fmt_req == PERC_FMT_STENCIL_SPLIT && !h->stencil_ok)) {
     set_error("perc_conductance: requested stencil operator not available for this system");
     return PERC_EINVAL;
@@ -696,8 +696,9 @@ int perc_spmv_host(perc_ctx* h, const double* x, double* y) {
 }
 
 int perc_set_matrix_format(perc_ctx* h, int fmt) {
-  if (!h || fmt < PERC_FMT_AUTO || fmt > PERC_FMT_STENCIL_SPLIT) return PERC_EINVAL;
-  if (h->assembled && fmt == PERC_FMT_STENCIL && !h->tiled_ok) return PERC_EINVAL;
+  if (!h || fmt < PERC_FMT_AUTO || fmt > PERC_FMT_STENCIL_TILED) return PERC_EINVAL;
+  if (h->assembled && (fmt == PERC_FMT_STENCIL || fmt == PERC_FMT_STENCIL_TILED) && !h->tiled_ok)
+    return PERC_EINVAL;
   if (h->assembled && fmt == PERC_FMT_STENCIL_SPLIT && !h->stencil_ok) return PERC_EINVAL;
   h->fmt_req = fmt;
   if (h->assembled) select_format(h);
@@ -710,11 +711,19 @@ int perc_set_full_voltages(perc_ctx* h, int enable) {
   return PERC_OK;
 }
 
+int perc_set_march_rows(perc_ctx* h, int rows) {
+  if (!h || rows < 0 || rows > 1024) return PERC_EINVAL;
+  h->march_rows_req = rows;
+  march_geometry(h);
+  return PERC_OK;
+}
+
 int perc_matrix_format(perc_ctx* h) {
   if (!h) return PERC_EINVAL;
   if (!h->assembled) return PERC_ESTATE;
   if (!h->stencil) return PERC_FMT_CSR;
-  return h->fused ? PERC_FMT_STENCIL : PERC_FMT_STENCIL_SPLIT;
+  if (!h->fused) return PERC_FMT_STENCIL_SPLIT;
+  return h->march ? PERC_FMT_STENCIL : PERC_FMT_STENCIL_TILED;
 }
 
 int perc_bench_kernel(perc_ctx* h, int which, int reps, double* ms) {

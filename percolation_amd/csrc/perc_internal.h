@@ -29,6 +29,13 @@ struct StencilForms {
   int off[kMaxForms][kMaxSlots];
   int dr[kMaxForms][kMaxSlots];
   int dc[kMaxForms][kMaxSlots];
+  // register-march kernel: slot j's raster position in the 3x3 block
+  // around the row (0..7 row-major, centre skipped) as 3-bit fields of
+  // rpos; rmask has a bit per used position; regular: slot order is
+  // raster order (every non-wrapped form)
+  unsigned rpos[kMaxForms];
+  unsigned rmask[kMaxForms];
+  int regular[kMaxForms];
 };
 
 // Device-resident CG scalars (one cache line each group; written only by the
@@ -62,6 +69,7 @@ struct DeviceBuffers {
   // slot j carries -g0, else -leak) | count << 8 | form << 11; sflag[0] != 0
   // if some slot has no bond (1) or a row matches no form (2)
   uint16_t* code = nullptr;  // N (+pad)
+  double* dtab = nullptr;    // 512: the diagonal of every code (see diag_idx)
   int* sflag = nullptr;      // 4
   // occupancy
   uint8_t* bocc = nullptr;  // nb
@@ -132,6 +140,12 @@ struct perc_ctx {
   bool fused = false;           // stencil P+S fused into the LDS-tiled kernel
   int tile_grid = 0;            // workgroups of the tiled kernel
   int tile_h = 32;              // its tile height (rows)
+  bool march_ok = false;        // register-march kernel usable (m % 128 == 0, tileable)
+  bool march = false;           // fused format runs the register-march kernel
+  int march_h = 32;             // its band height (rows per wave)
+  int march_grid = 0;           // its workgroups
+  int march_grid_max = 0;       // workgroups at band height 1 (reduction buffers)
+  int march_rows_req = 0;       // perc_set_march_rows (0: auto)
   bool full_voltages = false;   // perc_set_full_voltages: keep x on every row
   double st_ng0 = 0.0, st_nleak = 0.0;  // its two off-diagonal values
   perc::StencilForms forms{};            // row forms of this lattice
@@ -152,6 +166,7 @@ hipError_t dev_span_sites(perc_ctx* h, int root, int* count);
 hipError_t dev_canon(perc_ctx* h, int* canon_out);
 hipError_t dev_assemble(perc_ctx* h, int rule, double g0, double leak, double Va, int span_root);
 void select_format(perc_ctx* h);  // stencil / fused flags from fmt_req + assembly checks
+void march_geometry(perc_ctx* h); // band height + grid of the register-march kernel
 hipError_t dev_solve(perc_ctx* h, int itol, double tol, int itmax, bool x0_zero, bool full_x,
                      int* iter, double* err);
 hipError_t dev_currents(perc_ctx* h, int rule, int cur_rule, double g0, double leak, double Va,

@@ -118,7 +118,14 @@ def oracle_system(lat, m, n, pbc, b1, b2, gval):
     return sa, ija, itemp, diag, k
 
 
-FORMATS = [PL.FMT_STENCIL, PL.FMT_STENCIL_SPLIT, PL.FMT_CSR]
+FORMATS = [PL.FMT_STENCIL, PL.FMT_STENCIL_TILED, PL.FMT_STENCIL_SPLIT, PL.FMT_CSR]
+
+
+def used_fmt(fmt, m):
+    """The format perc_matrix_format reports for a request: PERC_FMT_STENCIL
+    runs the register-march kernel when m is a multiple of 128, else the
+    LDS-tiled one."""
+    return PL.FMT_STENCIL_TILED if fmt == PL.FMT_STENCIL and m % 128 else fmt
 
 
 @pytest.mark.parametrize("fmt", FORMATS)
@@ -134,7 +141,7 @@ def test_assembly_and_spmv_bitwise(lat, m, n, pbc, p, seed, fmt):
         assert li["nspan"] >= 1
         ctx.set_matrix_format(fmt)
         ctx.conductance(itmax=3)
-        assert ctx.matrix_format() == fmt
+        assert ctx.matrix_format() == used_fmt(fmt, m)
         sysm = ctx.system()
         ref = api.replay_labels(lat, m, n, pbc, PL.BOND, bond_order=order, nbond=tb)
         gval = O.f64(nb)
@@ -199,7 +206,7 @@ def test_conductance_vs_oracle_linbcg(lat, m, n, p, seed, fmt):
         ctx.occupy(PL.BOND, bond_order=order, nbonds_=tb)
         ctx.label()
         c = ctx.conductance(itmax=100000, vint=True)
-        assert ctx.matrix_format() == fmt
+        assert ctx.matrix_format() == used_fmt(fmt, m)
         ct = ctx.conductance(tol=1e-13, itmax=100000)
     # reference settings: same iteration count, answers agree to the solver
     # tolerance (the two differ only in the association of the dot products)
@@ -227,7 +234,11 @@ def test_conductance_vs_oracle_linbcg(lat, m, n, p, seed, fmt):
                                            # tile edges: m past one 256-column tile, rows
                                            # not a multiple of 16, tiny pbc widths
                                            (0, 520, 37, 1, 0.55), (1, 514, 30, 1, 0.42),
-                                           (0, 24, 50, 1, 0.55), (1, 20, 18, 0, 0.45)])
+                                           (0, 24, 50, 1, 0.55), (1, 20, 18, 0, 0.45),
+                                           # register-march kernel: several strips,
+                                           # pbc wrap columns, triangular forms
+                                           (0, 256, 77, 0, 0.6), (1, 384, 50, 1, 0.42),
+                                           (0, 128, 300, 1, 0.55)])
 def test_stencil_matches_csr_solver(lat, m, n, pbc, p):
     """The stencil operator (fused LDS-tiled and split kernels) rebuilds the
     CSR numbers bitwise, so all formats give the same iterates up to the
@@ -245,10 +256,10 @@ def test_stencil_matches_csr_solver(lat, m, n, pbc, p):
             if ctx.label()["nspan"] == 0:
                 pytest.skip("no spanning cluster")
             c = ctx.conductance(tol=1e-12, itmax=100000, vint=True)
-            assert ctx.matrix_format() == fmt
+            assert ctx.matrix_format() == used_fmt(fmt, m)
             out[fmt] = (c, ctx.spmv(x))
     cc, yc = out[PL.FMT_CSR]
-    for fmt in (PL.FMT_STENCIL, PL.FMT_STENCIL_SPLIT):
+    for fmt in (PL.FMT_STENCIL, PL.FMT_STENCIL_TILED, PL.FMT_STENCIL_SPLIT):
         cs, ys = out[fmt]
         assert np.array_equal(ys.view(np.uint64), yc.view(np.uint64))
         assert abs(cs["iter"] - cc["iter"]) <= 1
@@ -257,7 +268,8 @@ def test_stencil_matches_csr_solver(lat, m, n, pbc, p):
 
 
 @pytest.mark.parametrize("fmt", FORMATS)
-@pytest.mark.parametrize("lat,m,n,pbc,p", [(0, 260, 140, 0, 0.6), (1, 130, 90, 1, 0.42)])
+@pytest.mark.parametrize("lat,m,n,pbc,p", [(0, 260, 140, 0, 0.6), (1, 130, 90, 1, 0.42),
+                                           (0, 256, 140, 0, 0.6), (1, 128, 90, 1, 0.42)])
 def test_boundary_row_voltages_bitwise(lat, m, n, pbc, p, fmt):
     """Without vint_out the solver keeps x on the two interior rows next to
     the electrodes only; Gtop/Gbot/iter/err are bitwise those of the
@@ -294,7 +306,7 @@ def test_tall_tiles_match_split_kernels(lat, m, n, pbc, p):
             if ctx.label()["nspan"] == 0:
                 pytest.skip("no spanning cluster")
             out[fmt] = ctx.conductance(tol=1e-10, itmax=10 ** 6)
-            assert ctx.matrix_format() == fmt
+            assert ctx.matrix_format() == used_fmt(fmt, m)
     a, b = out[PL.FMT_STENCIL], out[PL.FMT_STENCIL_SPLIT]
     assert abs(a["iter"] - b["iter"]) <= 2
     assert rel(a["gtop"], b["gtop"]) < REL and rel(a["gbot"], b["gbot"]) < REL
@@ -448,3 +460,30 @@ def test_full_size_properties(L_, p):
         # current conservation up to the 1e-12 leak currents that the 1e-10
         # sprsin threshold drops from the terminal sums (hazard H5)
         assert abs(c["gtop"] - c["gbot"]) < 1e-8
+
+
+@pytest.mark.parametrize("lat,m,n,pbc,p", [(0, 256, 150, 0, 0.6), (1, 128, 99, 1, 0.42),
+                                           (0, 384, 40, 1, 0.55)])
+def test_march_band_heights(lat, m, n, pbc, p):
+    """Register-march kernel at band heights from 1 row to more than the
+    lattice (partial last band, single band), against the LDS-tiled kernel:
+    same solve up to the q.p association; the x rows next to the electrodes
+    and the currents come from the same per-row arithmetic."""
+    nb = api.nbonds(lat, m, n, pbc)
+    order = api.shuffled_ids(nb, 1234)
+    with api.Context(lat, m, n, pbc) as ctx:
+        ctx.occupy(PL.BOND, bond_order=order, nbonds_=int(p * nb))
+        if ctx.label()["nspan"] == 0:
+            pytest.skip("no spanning cluster")
+        ctx.set_matrix_format(PL.FMT_STENCIL_TILED)
+        ref = ctx.conductance(tol=1e-12, itmax=100000, vint=True)
+        assert ctx.matrix_format() == PL.FMT_STENCIL_TILED
+        ctx.set_matrix_format(PL.FMT_STENCIL)
+        for rows in (1, 2, 3, 7, 32, 64):
+            ctx.set_march_rows(rows)
+            c = ctx.conductance(tol=1e-12, itmax=100000, vint=True)
+            assert ctx.matrix_format() == PL.FMT_STENCIL
+            assert abs(c["iter"] - ref["iter"]) <= 2, rows
+            assert rel(c["gtop"], ref["gtop"]) < REL and rel(c["gbot"], ref["gbot"]) < REL, rows
+            assert np.max(np.abs(c["vint"] - ref["vint"])) < 1e-6, rows
+        ctx.set_march_rows(0)

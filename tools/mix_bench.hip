@@ -1,0 +1,255 @@
+// mix_bench.hip -- streaming HBM throughput for the read/write mixes of the
+// CG kernels at L = 4096 (N = 4094 * 4096 rows, fp64 vectors + u16 codes):
+//   ps:  read p, r, code; write p', q      (34 B / row, 47 % writes)
+//   b:   read q, r, code; write r in place (26 B / row, 31 % writes)
+//   r2w2, r2w1, r3w0, copy: plain mixes for reference
+// Pure streams, no stencil: the ceiling the fused kernels could reach with
+// their byte counts.  Also nontemporal variants of the stores.
+//   hipcc --offload-arch=gfx950 -O3 tools/mix_bench.hip -o tools/mix_bench
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+#define CHK(x)                                                                  \
+  do {                                                                          \
+    hipError_t e_ = (x);                                                        \
+    if (e_ != hipSuccess) {                                                     \
+      fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e_)); \
+      exit(1);                                                                  \
+    }                                                                           \
+  } while (0)
+
+typedef double dvec2 __attribute__((ext_vector_type(2)));
+
+struct Bufs {
+  dvec2 *a, *b, *c, *d;
+  const unsigned* code;
+  long long n;  // pairs
+};
+
+template <int NR, int NW, bool CODE, bool INPLACE, bool NT, int U>
+__global__ void k_mix(Bufs B) {
+  const long long n = B.n;
+  const long long chunk = ((n + gridDim.x - 1) / gridDim.x + blockDim.x * U - 1) /
+                          (blockDim.x * U) * (blockDim.x * U);
+  const long long i0 = blockIdx.x * chunk, i1 = std::min(i0 + chunk, n);
+  for (long long base = i0 + threadIdx.x; base < i1; base += (long long)blockDim.x * U) {
+    dvec2 va[U], vb[U];
+    unsigned vc[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const long long i = base + (long long)u * blockDim.x;
+      if (i < i1) {
+        va[u] = B.a[i];
+        if (NR > 1) vb[u] = B.b[i];
+        if (NR > 2) va[u] += B.d[i];
+        if (CODE) vc[u] = B.code[i];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const long long i = base + (long long)u * blockDim.x;
+      if (i < i1) {
+        dvec2 o1 = va[u] * 0.5;
+        if (NR > 1) o1 += vb[u];
+        if (CODE) o1 += (double)(vc[u] & 7);
+        if (NW >= 1) {
+          dvec2* dst = INPLACE ? B.b : B.c;
+          if (NT) __builtin_nontemporal_store(o1, dst + i);
+          else dst[i] = o1;
+        }
+        if (NW >= 2) {
+          dvec2 o2 = va[u] - 1.0;
+          if (NT) __builtin_nontemporal_store(o2, B.d + i);
+          else B.d[i] = o2;
+        }
+        if (NW == 0 && o1.x == 12345.0) B.c[i] = o1;
+      }
+    }
+  }
+}
+
+// the CG iteration's real sequence on the solver's buffers: PS-like
+// (read pold, r, code; write pnew, q) then B-like (read q, r, code; write r),
+// p ping-pong; B optionally walks its chunks in reverse (as k_cg_b does)
+template <bool NT, bool REV>
+__global__ void k_b_seq(const dvec2* __restrict__ q, dvec2* __restrict__ r,
+                        const unsigned* __restrict__ code, long long n) {
+  const int lb = REV ? (int)gridDim.x - 1 - (int)blockIdx.x : (int)blockIdx.x;
+  const long long chunk = ((n + gridDim.x - 1) / gridDim.x + blockDim.x * 4 - 1) /
+                          (blockDim.x * 4) * (blockDim.x * 4);
+  const long long i0 = lb * chunk, i1 = std::min(i0 + chunk, n);
+  for (long long base = i0 + threadIdx.x; base < i1; base += (long long)blockDim.x * 4) {
+    dvec2 vq[4], vr[4];
+    unsigned vc[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const long long i = base + (long long)u * blockDim.x;
+      if (i < i1) {
+        vq[u] = q[i];
+        vr[u] = r[i];
+        vc[u] = code[i];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const long long i = base + (long long)u * blockDim.x;
+      if (i < i1) {
+        const dvec2 o = vr[u] - 0.5 * vq[u] + (double)(vc[u] & 1);
+        if (NT) __builtin_nontemporal_store(o, r + i);
+        else r[i] = o;
+      }
+    }
+  }
+}
+template <bool NT>
+__global__ void k_ps_seq(const dvec2* __restrict__ pold, const dvec2* __restrict__ r,
+                         const unsigned* __restrict__ code, dvec2* __restrict__ pnew,
+                         dvec2* __restrict__ q, long long n) {
+  const long long chunk = ((n + gridDim.x - 1) / gridDim.x + blockDim.x * 4 - 1) /
+                          (blockDim.x * 4) * (blockDim.x * 4);
+  const long long i0 = blockIdx.x * chunk, i1 = std::min(i0 + chunk, n);
+  for (long long base = i0 + threadIdx.x; base < i1; base += (long long)blockDim.x * 4) {
+    dvec2 vp[4], vr[4];
+    unsigned vc[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const long long i = base + (long long)u * blockDim.x;
+      if (i < i1) {
+        vp[u] = pold[i];
+        vr[u] = r[i];
+        vc[u] = code[i];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const long long i = base + (long long)u * blockDim.x;
+      if (i < i1) {
+        const dvec2 pn = 0.5 * vp[u] + vr[u];
+        const dvec2 qq = pn * (double)(vc[u] & 3);
+        if (NT) {
+          __builtin_nontemporal_store(pn, pnew + i);
+          __builtin_nontemporal_store(qq, q + i);
+        } else {
+          pnew[i] = pn;
+          q[i] = qq;
+        }
+      }
+    }
+  }
+}
+
+struct V {
+  const char* name;
+  void (*k)(Bufs);
+  double bytes_per_pair;
+};
+
+int main(int argc, char** argv) {
+  const int reps = argc > 1 ? atoi(argv[1]) : 20;
+  const long long rows = 4094ll * 4096, n = rows / 2;
+  Bufs B;
+  CHK(hipMalloc(&B.a, n * 16));
+  CHK(hipMalloc(&B.b, n * 16));
+  CHK(hipMalloc(&B.c, n * 16));
+  CHK(hipMalloc(&B.d, n * 16));
+  unsigned* code;
+  CHK(hipMalloc(&code, n * 4));
+  B.code = code;
+  B.n = n;
+  CHK(hipMemset(B.a, 0, n * 16));
+  CHK(hipMemset(B.b, 0, n * 16));
+  CHK(hipMemset(B.d, 0, n * 16));
+  CHK(hipMemset(code, 0, n * 4));
+  std::vector<V> vs = {
+      {"ps   r2+code w2", k_mix<2, 2, true, false, false, 4>, 68},
+      {"ps   r2+code w2 nt", k_mix<2, 2, true, false, true, 4>, 68},
+      {"ps   r2+code w2 u2", k_mix<2, 2, true, false, false, 2>, 68},
+      {"b    r2+code w1 inpl", k_mix<2, 1, true, true, false, 4>, 52},
+      {"b    r2+code w1 inpl nt", k_mix<2, 1, true, true, true, 4>, 52},
+      {"r2w2", k_mix<2, 2, false, false, false, 4>, 64},
+      {"r2w1", k_mix<2, 1, false, false, false, 4>, 48},
+      {"r3w0", k_mix<3, 0, false, false, false, 4>, 48},
+      {"r1w1 copy", k_mix<1, 1, false, false, false, 4>, 32},
+      {"r1w1 copy nt", k_mix<1, 1, false, false, true, 4>, 32},
+  };
+  hipEvent_t e0, e1;
+  CHK(hipEventCreate(&e0));
+  CHK(hipEventCreate(&e1));
+  for (int g : {8192}) {
+    for (auto& v : vs) v.k<<<g, 256>>>(B);
+    CHK(hipDeviceSynchronize());
+    for (auto& v : vs) {
+      double best = 1e30;
+      for (int round = 0; round < 3; ++round) {
+        CHK(hipEventRecord(e0));
+        for (int r = 0; r < reps; ++r) v.k<<<g, 256>>>(B);
+        CHK(hipEventRecord(e1));
+        CHK(hipEventSynchronize(e1));
+        float t;
+        CHK(hipEventElapsedTime(&t, e0, e1));
+        best = std::min(best, (double)t / reps);
+      }
+      printf("g%-6d %-26s %8.4f ms %7.1f GB/s\n", g, v.name, best,
+             v.bytes_per_pair * n / (best * 1e-3) / 1e9);
+    }
+  }
+  // real sequence: PS(p0 -> p1), B, PS(p1 -> p0), B ...
+  for (int mode = 0; mode < 4; ++mode) {
+    const bool nt = mode & 1, rev = mode & 2;
+    const int g = 8192;
+    auto iter = [&](int k) {
+      dvec2* po = (k & 1) ? B.c : B.a;
+      dvec2* pn = (k & 1) ? B.a : B.c;
+      if (nt) k_ps_seq<true><<<g, 256>>>(po, B.b, code, pn, B.d, n);
+      else k_ps_seq<false><<<g, 256>>>(po, B.b, code, pn, B.d, n);
+      if (nt && rev) k_b_seq<true, true><<<g, 256>>>(B.d, B.b, code, n);
+      else if (nt) k_b_seq<true, false><<<g, 256>>>(B.d, B.b, code, n);
+      else if (rev) k_b_seq<false, true><<<g, 256>>>(B.d, B.b, code, n);
+      else k_b_seq<false, false><<<g, 256>>>(B.d, B.b, code, n);
+    };
+    for (int k = 0; k < 4; ++k) iter(k);
+    CHK(hipDeviceSynchronize());
+    // per-kernel split (events between the launches)
+    {
+      std::vector<hipEvent_t> ev(3);
+      for (auto& e : ev) CHK(hipEventCreate(&e));
+      double tps = 0, tb = 0;
+      for (int k = 0; k < 2 * reps; ++k) {
+        dvec2* po = (k & 1) ? B.c : B.a;
+        dvec2* pn = (k & 1) ? B.a : B.c;
+        CHK(hipEventRecord(ev[0]));
+        if (nt) k_ps_seq<true><<<g, 256>>>(po, B.b, code, pn, B.d, n);
+        else k_ps_seq<false><<<g, 256>>>(po, B.b, code, pn, B.d, n);
+        CHK(hipEventRecord(ev[1]));
+        if (nt) k_b_seq<true, false><<<g, 256>>>(B.d, B.b, code, n);
+        else k_b_seq<false, false><<<g, 256>>>(B.d, B.b, code, n);
+        CHK(hipEventRecord(ev[2]));
+        CHK(hipEventSynchronize(ev[2]));
+        float a1, a2;
+        CHK(hipEventElapsedTime(&a1, ev[0], ev[1]));
+        CHK(hipEventElapsedTime(&a2, ev[1], ev[2]));
+        tps += a1;
+        tb += a2;
+      }
+      printf("cg-iter split nt=%d: ps-like %.4f ms  b-like %.4f ms\n", nt, tps / (2 * reps),
+             tb / (2 * reps));
+    }
+    double best = 1e30;
+    for (int round = 0; round < 3; ++round) {
+      CHK(hipEventRecord(e0));
+      for (int k = 0; k < 2 * reps; ++k) iter(k);
+      CHK(hipEventRecord(e1));
+      CHK(hipEventSynchronize(e1));
+      float t;
+      CHK(hipEventElapsedTime(&t, e0, e1));
+      best = std::min(best, (double)t / (2 * reps));
+    }
+    printf("cg-iter seq nt=%d b_reverse=%d: %8.4f ms / iteration  %7.1f GB/s (60 B/row)\n", nt,
+           rev, best, 60.0 * rows / (best * 1e-3) / 1e9);
+  }
+  return 0;
+}
