@@ -325,8 +325,9 @@ def main():
         return [("spmv", "spmv", 1, spmv_bytes(N, nnz, f)), ("resid", "resid", 2, resid_bytes(N, f)),
                 ("xp", "xp", 3, xp_bytes(N, f, L_, full))]
 
-    # per-kernel live timing (HIP events on the context stream around every
-    # launch that did work, over the timed realisations)
+    # per-kernel live timing: HIP events on the context stream around the
+    # launches of every 8th CG iteration of the timed realisations (those
+    # that did work; perc_set_kernel_timing)
     kern = {}
     for key, skey, _, nbytes in kernel_set(fmt):
         n_ = max(ks[skey + "_n"], 1)

@@ -190,10 +190,11 @@ int perc_spmv_host(perc_ctx *h, const double *x, double *y);
    reference).  Clobbers solver vectors. */
 int perc_bench_kernel(perc_ctx *h, int which, int reps, double *ms);
 
-/* Live kernel timing: when enabled, every CG launch inside
-   perc_conductance is bracketed by HIP events on the context stream; the
-   accumulated device time of launches that did work is returned (ms) with
-   their count.  stats[0..5] = {spmv_ms, spmv_launches, resid_ms (B),
+/* Live kernel timing: when enabled, the CG launches of every 8th
+   iteration inside perc_conductance are bracketed by HIP events on the
+   context stream (events between every launch would cost ~10 % of an
+   L = 4096 iteration); the accumulated device time of the sampled launches
+   that did work is returned (ms) with their count.  stats[0..5] = {spmv_ms, spmv_launches, resid_ms (B),
    resid_launches, xp_ms (P), xp_launches}; reset clears the accumulators. */
 int perc_set_kernel_timing(perc_ctx *h, int enable);
 int perc_kernel_stats(perc_ctx *h, double *stats, int reset);
