@@ -811,6 +811,7 @@ struct CGArgs {
   int b_reverse;  // B walks the row chunks in reverse logical order (fused mode)
   int xrows;      // 0: x kept on all rows; else only rows i < xrows or i >= N - xrows
   int nt;         // nontemporal stores of p, q, r (stencil kernels)
+  int kiter;      // the launch's CG iteration (fused PS kernels; host-counted)
   double* q;
   double* partials;  // kRedSlots slots of pstride doubles
   unsigned* tickets; // kRedSlots slots of tstride counters
@@ -1292,23 +1293,23 @@ __device__ __forceinline__ double march_q_gen(unsigned c, double d, double xi, u
   return acc;
 }
 
-constexpr int kMarchDepth = 2;  // rows prefetched ahead (3: +22 VGPRs, no faster)
+// rows prefetched ahead: 3 (+22 VGPRs) is no faster, nor are taller bands
+// with fewer waves and 4-6 rows ahead (H = 64: 0.138 vs 0.111 ms at L = 4096)
+constexpr int kMarchDepth = 2;
 
+template <int D = kMarchDepth>
 __global__ __launch_bounds__(64 * kMarchWaves) void k_cg_pm(CGArgs a) {
-  constexpr int D = kMarchDepth;
   CGScalars* S = a.S;
-  if (S->done) return;
   __shared__ double s_red[32];
   __shared__ int s_flag[2];
   __shared__ unsigned s_rpos[kMaxForms];
   __shared__ double s_dt[kDiagTab];
   __shared__ double s_win[kMarchWaves][12 * 64];  // general-path window scratch
-  if (threadIdx.x < kMaxForms) s_rpos[threadIdx.x] = a.St.F.rpos[threadIdx.x];
-  load_dtab(a.St, s_dt);
-  __syncthreads();
-  const int k = S->iter + 1;
+  // the launch's iteration comes from the host (launch j of a solve is
+  // iteration j + 1 until the stop; later launches return below), so the
+  // first rows' loads go out before any device scalar is read
+  const int k = a.kiter;
   const bool first = k == 1;
-  const double bk = S->bk, ak = S->ak;
   const double ng0 = a.St.ng0, nleak = a.St.nleak;
   const double* __restrict__ pold = a.pb[(k - 1) & 1];
   double* __restrict__ pnew = a.pb[k & 1];
@@ -1322,34 +1323,45 @@ __global__ __launch_bounds__(64 * kMarchWaves) void k_cg_pm(CGArgs a) {
   const int spr = m / kMarchW;
   const int band = w / spr, strip = w - band * spr;
   const int r0 = band * H;
-  double dot = 0.0;
-  if (r0 < nrows) {  // wave-uniform
-    const int c0 = strip * kMarchW, col = c0 + 2 * lane;
-    int hcol = lane == 0 ? c0 - 1 : c0 + kMarchW;
-    bool hok = lane == 0 || lane == 63;
-    if (hcol < 0 || hcol >= m) {
-      if (a.T.pbc) hcol += hcol < 0 ? m : -m;
-      else hok = false;
-    }
-    const int rend = min(r0 + H, nrows);
-    const int nsteps = rend - r0 + 2;  // rows r0-1 .. rend
-    auto load = [&](int gr, MRow& R) {
-      R.p = R.r = make_double2(0.0, 0.0);
-      R.c = R.hc = 0u;
-      R.hp = R.hr = 0.0;
-      if (gr >= 0 && gr < nrows) {
-        const int i = gr * m + col;
-        R.c = *reinterpret_cast<const unsigned*>(code + i);
-        R.r = *reinterpret_cast<const double2*>(r + i);
-        if (!first) R.p = *reinterpret_cast<const double2*>(pold + i);
-        if (hok) {
-          const int hi = gr * m + hcol;
-          R.hc = code[hi];
-          R.hr = r[hi];
-          if (!first) R.hp = pold[hi];
-        }
+  const bool active = r0 < nrows;  // wave-uniform
+  const int c0 = strip * kMarchW, col = c0 + 2 * lane;
+  int hcol = lane == 0 ? c0 - 1 : c0 + kMarchW;
+  bool hok = lane == 0 || lane == 63;
+  if (hcol < 0 || hcol >= m) {
+    if (a.T.pbc) hcol += hcol < 0 ? m : -m;
+    else hok = false;
+  }
+  const int rend = min(r0 + H, nrows);
+  const int nsteps = rend - r0 + 2;  // rows r0-1 .. rend
+  auto load = [&](int gr, MRow& R) {
+    R.p = R.r = make_double2(0.0, 0.0);
+    R.c = R.hc = 0u;
+    R.hp = R.hr = 0.0;
+    if (gr >= 0 && gr < nrows) {
+      const int i = gr * m + col;
+      R.c = *reinterpret_cast<const unsigned*>(code + i);
+      R.r = *reinterpret_cast<const double2*>(r + i);
+      if (!first) R.p = *reinterpret_cast<const double2*>(pold + i);
+      if (hok) {
+        const int hi = gr * m + hcol;
+        R.hc = code[hi];
+        R.hr = r[hi];
+        if (!first) R.hp = pold[hi];
       }
-    };
+    }
+  };
+  MRow ring[D];
+  if (active) {
+#pragma unroll
+    for (int u = 0; u < D; ++u) load(r0 - 1 + u, ring[u]);
+  }
+  if (S->done) return;
+  if (threadIdx.x < kMaxForms) s_rpos[threadIdx.x] = a.St.F.rpos[threadIdx.x];
+  load_dtab(a.St, s_dt);
+  __syncthreads();
+  const double bk = S->bk, ak = S->ak;
+  double dot = 0.0;
+  if (active) {
     MWin U{0.0, 0.0, 0.0, 0.0}, C = U, Dn = U;
     unsigned cC = 0u, cD = 0u;
     double dC0 = 1.0, dC1 = 1.0, dD0 = 1.0, dD1 = 1.0;
@@ -1430,9 +1442,6 @@ __global__ __launch_bounds__(64 * kMarchWaves) void k_cg_pm(CGArgs a) {
         dot = dot + q1 * C.e1;
       }
     };
-    MRow ring[D];
-#pragma unroll
-    for (int u = 0; u < D; ++u) load(r0 - 1 + u, ring[u]);
     for (int j0 = 0; j0 < nsteps; j0 += D) {
 #pragma unroll
       for (int u = 0; u < D; ++u) {
@@ -1541,6 +1550,7 @@ CGArgs make_cg_args(perc_ctx* h) {
   a.b_reverse = h->fused ? 1 : 0;
   static const int nt_env = getenv("PERC_NT") ? atoi(getenv("PERC_NT")) : 1;
   a.nt = nt_env;
+  a.kiter = 1;
   a.xrows = h->full_voltages || h->g.m <= 0 ? 0 : h->g.m;  // see dev_solve
   a.pstride = red_partials_size(red_grid(h));
   a.tstride = red_tickets_size(red_grid(h));
@@ -1966,6 +1976,7 @@ hipError_t dev_solve(perc_ctx* h, int itol, double tol, int itmax, bool x0_zero,
   while (true) {
     for (int j = 0; j < chunk; ++j) {
       const bool tm = T.enabled && j % kTimeEvery == 0;
+      a.kiter = (int)(launched + j + 1);
       if (tm) hipEventRecord(T.ev[4 * j], st);
       if (!h->fused) {
         if (ST) k_cg_p<true><<<G, kBlock, 0, st>>>(a);
@@ -2059,6 +2070,7 @@ hipError_t dev_bench(perc_ctx* h, int which, int reps, double* ms) {
   hs.tol = -1.0;
   hs.itmax = 1 << 30;
   hs.iter = 1;
+  a.kiter = 2;
   HIP_TRY(hipMemcpyAsync(d.scal, &hs, sizeof(hs), hipMemcpyHostToDevice, st));
   HIP_TRY(hipMemsetAsync(d.tickets, 0, kRedSlots * red_tickets_size(red_grid(h)) * sizeof(unsigned),
                          st));

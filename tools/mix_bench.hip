@@ -142,6 +142,76 @@ __global__ void k_ps_seq(const dvec2* __restrict__ pold, const dvec2* __restrict
   }
 }
 
+// march-shaped pure stream: the register-march kernel's access pattern
+// (wave = 128-column strip x H-row band, rows r0-1 .. r0+H read, rows
+// r0 .. r0+H-1 written, D rows prefetched) with trivial arithmetic
+template <int D, int PPL>
+__global__ __launch_bounds__(256) void k_march_stream(const double* __restrict__ pold,
+                                                      const double* __restrict__ r,
+                                                      const unsigned short* __restrict__ code,
+                                                      double* __restrict__ pnew,
+                                                      double* __restrict__ q, int m, int pitch,
+                                                      int nrows, int H) {
+  const int lane = threadIdx.x & 63;
+  const int w = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int spr = m / (128 * PPL);
+  const int band = w / spr, strip = w - band * spr;
+  const int r0 = band * H;
+  if (r0 >= nrows) return;
+  const int col = strip * 128 * PPL + 2 * lane;
+  const int rend = min(r0 + H, nrows), nsteps = rend - r0 + 2;
+  struct Row {
+    dvec2 p[PPL], rr[PPL];
+    unsigned c[PPL];
+  };
+  auto load = [&](int gr, Row& R) {
+#pragma unroll
+    for (int k = 0; k < PPL; ++k) {
+      R.p[k] = R.rr[k] = dvec2{0.0, 0.0};
+      R.c[k] = 0;
+    }
+    if (gr >= 0 && gr < nrows) {
+#pragma unroll
+      for (int k = 0; k < PPL; ++k) {
+        const long long i = (long long)gr * pitch + col + 128 * k;
+        R.p[k] = *reinterpret_cast<const dvec2*>(pold + i);
+        R.rr[k] = *reinterpret_cast<const dvec2*>(r + i);
+        R.c[k] = *reinterpret_cast<const unsigned*>(code + i);
+      }
+    }
+  };
+  dvec2 prev[PPL];
+#pragma unroll
+  for (int k = 0; k < PPL; ++k) prev[k] = dvec2{0.0, 0.0};
+  Row ring[D];
+#pragma unroll
+  for (int u = 0; u < D; ++u) load(r0 - 1 + u, ring[u]);
+  for (int j0 = 0; j0 < nsteps; j0 += D) {
+#pragma unroll
+    for (int u = 0; u < D; ++u) {
+      const int j = j0 + u;
+      if (j < nsteps) {
+        const Row R = ring[u];
+        if (j + D < nsteps) load(r0 - 1 + j + D, ring[u]);
+        const int gr = r0 - 1 + j;
+#pragma unroll
+        for (int k = 0; k < PPL; ++k) {
+          const dvec2 pn = 0.5 * R.p[k] + R.rr[k] + (double)(R.c[k] & 3);
+          if (gr >= r0 && gr < rend) {
+            const long long i = (long long)gr * pitch + col + 128 * k;
+            __builtin_nontemporal_store(pn, reinterpret_cast<dvec2*>(pnew + i));
+          }
+          if (gr - 1 >= r0) {
+            const long long i = (long long)(gr - 1) * pitch + col + 128 * k;
+            __builtin_nontemporal_store(prev[k] + pn, reinterpret_cast<dvec2*>(q + i));
+          }
+          prev[k] = pn;
+        }
+      }
+    }
+  }
+}
+
 struct V {
   const char* name;
   void (*k)(Bufs);
@@ -151,19 +221,20 @@ struct V {
 int main(int argc, char** argv) {
   const int reps = argc > 1 ? atoi(argv[1]) : 20;
   const long long rows = 4094ll * 4096, n = rows / 2;
+  const long long nalloc = 4094ll * 4160 / 2;  // room for a padded row pitch
   Bufs B;
-  CHK(hipMalloc(&B.a, n * 16));
-  CHK(hipMalloc(&B.b, n * 16));
-  CHK(hipMalloc(&B.c, n * 16));
-  CHK(hipMalloc(&B.d, n * 16));
+  CHK(hipMalloc(&B.a, nalloc * 16));
+  CHK(hipMalloc(&B.b, nalloc * 16));
+  CHK(hipMalloc(&B.c, nalloc * 16));
+  CHK(hipMalloc(&B.d, nalloc * 16));
   unsigned* code;
-  CHK(hipMalloc(&code, n * 4));
+  CHK(hipMalloc(&code, nalloc * 4));
   B.code = code;
   B.n = n;
-  CHK(hipMemset(B.a, 0, n * 16));
-  CHK(hipMemset(B.b, 0, n * 16));
-  CHK(hipMemset(B.d, 0, n * 16));
-  CHK(hipMemset(code, 0, n * 4));
+  CHK(hipMemset(B.a, 0, nalloc * 16));
+  CHK(hipMemset(B.b, 0, nalloc * 16));
+  CHK(hipMemset(B.d, 0, nalloc * 16));
+  CHK(hipMemset(code, 0, nalloc * 4));
   std::vector<V> vs = {
       {"ps   r2+code w2", k_mix<2, 2, true, false, false, 4>, 68},
       {"ps   r2+code w2 nt", k_mix<2, 2, true, false, true, 4>, 68},
@@ -195,6 +266,51 @@ int main(int argc, char** argv) {
       }
       printf("g%-6d %-26s %8.4f ms %7.1f GB/s\n", g, v.name, best,
              v.bytes_per_pair * n / (best * 1e-3) / 1e9);
+    }
+  }
+  // march-shaped stream in the CG sequence with the b-like stream:
+  // strip width 128 * PPL columns, row pitch 4096 (or padded)
+  {
+    const int m = 4096, nrows = 4094;
+    const unsigned short* code16 = reinterpret_cast<const unsigned short*>(code);
+    struct MV {
+      const char* name;
+      void (*k)(const double*, const double*, const unsigned short*, double*, double*, int, int,
+                int, int);
+      int ppl, pitch, H;
+    };
+    std::vector<MV> mvs = {{"ppl1 pitch4096 H32", k_march_stream<2, 1>, 1, 4096, 32},
+                           {"ppl1 pitch4096 H16", k_march_stream<2, 1>, 1, 4096, 16},
+                           {"ppl1 pitch4160 H32", k_march_stream<2, 1>, 1, 4160, 32},
+                           {"ppl2 pitch4096 H32", k_march_stream<2, 2>, 2, 4096, 32},
+                           {"ppl2 pitch4096 H16", k_march_stream<2, 2>, 2, 4096, 16},
+                           {"ppl4 pitch4096 H16", k_march_stream<2, 4>, 4, 4096, 16},
+                           {"ppl4 pitch4096 H8", k_march_stream<2, 4>, 4, 4096, 8}};
+    for (auto& mv : mvs) {
+      const int waves = (m / (128 * mv.ppl)) * ((nrows + mv.H - 1) / mv.H), grid = (waves + 3) / 4;
+      std::vector<hipEvent_t> ev(3);
+      for (auto& e : ev) CHK(hipEventCreate(&e));
+      double tps = 0, tb = 0;
+      for (int k = 0; k < 2 * reps + 4; ++k) {
+        const double* po = (const double*)((k & 1) ? B.c : B.a);
+        double* pn = (double*)((k & 1) ? B.a : B.c);
+        CHK(hipEventRecord(ev[0]));
+        mv.k<<<grid, 256>>>(po, (const double*)B.b, code16, pn, (double*)B.d, m, mv.pitch, nrows,
+                             mv.H);
+        CHK(hipEventRecord(ev[1]));
+        k_b_seq<true, false><<<8192, 256>>>(B.d, B.b, code, n);
+        CHK(hipEventRecord(ev[2]));
+        CHK(hipEventSynchronize(ev[2]));
+        float a1, a2;
+        CHK(hipEventElapsedTime(&a1, ev[0], ev[1]));
+        CHK(hipEventElapsedTime(&a2, ev[1], ev[2]));
+        if (k >= 4) {
+          tps += a1;
+          tb += a2;
+        }
+      }
+      printf("march-stream %-20s in sequence: march %.4f ms  b-like %.4f ms\n", mv.name,
+             tps / (2 * reps), tb / (2 * reps));
     }
   }
   // real sequence: PS(p0 -> p1), B, PS(p1 -> p0), B ...

@@ -22,6 +22,8 @@ def main():
     ap.add_argument("--p", type=float, default=0.60)
     ap.add_argument("--reps", type=int, default=300)
     ap.add_argument("--tag", default=os.environ.get("PERC_PS_VARIANT", "0"))
+    ap.add_argument("--march-rows", type=int, default=int(os.environ.get("PERC_MARCH_ROWS", "0")),
+                    help="band height of the register-march kernel (0: auto)")
     ap.add_argument("--itmax", type=int, default=10**6,
                     help="small values: timing only (no fingerprint), for variants that "
                          "do not compute the real iteration")
@@ -33,6 +35,7 @@ def main():
         tb = int(a.p * nb)
         order = (np.random.default_rng(seed).permutation(nb)[:tb] + 1).astype(np.int32)
         with api.Context(0, L_, L_, 0) as ctx:
+            ctx.set_march_rows(a.march_rows)
             t0 = time.perf_counter()
             r = ctx.bondc_realisation(order, tb, tol=1e-8, itmax=a.itmax)
             t1 = time.perf_counter()
