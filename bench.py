@@ -50,15 +50,17 @@ def x_bytes(N, m, full):
     return 16 * N if full else 16 * 2 * m
 
 
-def ps_bytes(N, m, full):
-    """k_cg_ps (fused p update + SpMV + q.p, LDS-tiled): reads p(k-1), r,
-    code; writes p(k), q -- 34N, plus x (the tile halo's re-reads are not
+def ps_bytes(N, m, full, qfree=False):
+    """Fused P(k)+S(k) (p update + SpMV + q.p; march or LDS tiles): reads
+    p(k-1), r, code; writes p(k) and, unless the B kernel rebuilds q
+    (q-free march), q -- 34N (26N q-free), plus x (halo re-reads are not
     algorithmic; they show in the PMC traffic)."""
-    return 34 * N + x_bytes(N, m, full)
+    return (26 if qfree else 34) * N + x_bytes(N, m, full)
 
 
 def resid_bytes(N, fmt):
-    """k_cg_b: reads r, q and d (csr: 8 B diag, stencil: 2 B code); writes r."""
+    """B: reads r, q and d (csr: 8 B diag, stencil: 2 B code); writes r.  The
+    q-free march B reads p(k) instead of q: the same 26N."""
     return 32 * N if fmt == "csr" else 26 * N
 
 
@@ -67,7 +69,7 @@ def xp_bytes(N, fmt, m, full):
     return (32 * N if fmt == "csr" else 26 * N) + x_bytes(N, m, full)
 
 
-KERNELS = {"pm": "k_cg_pm (fused p = bk p + r/d, x += ak p, q = A p, q.p; register march)",
+KERNELS = {"pm": "march kernel (fused p = bk p + r/d, x += ak p, q = A p, q.p)",
            "ps": "k_cg_ps (fused p = bk p + r/d, x += ak p, q = A p, q.p; LDS tiles)",
            "spmv": "k_cg_spmv (SpMV q = A p + q.p dot)",
            "resid": "k_cg_b (r -= ak q, z = r/d, z.r and r.r dots)",
@@ -127,13 +129,27 @@ def cpu_baseline(L_, p, order, gpu_iters, cpu_iters):
                 sample_seconds=round(t4 - t0, 2), s_per_solve=round(total, 2))
 
 
+def kernel_label(key, minfo):
+    """Name + role of a CG kernel, for the march variant that ran."""
+    if key == "pm" and minfo.get("kernel") in ("wave", "rows"):
+        name = "k_cg_rm (workgroup row-march" if minfo["kernel"] == "rows" else \
+            "k_cg_march (per-wave register march"
+        return "%s %d cols x %d rows%s): fused p = bk p + r/d, x += ak p, q = A p, q.p%s" % (
+            name, minfo["strip_cols"], minfo["band_rows"], ", alternating" if minfo["alt"] else "",
+            "" if minfo["qfree"] else ", q stored")
+    if key == "resid" and minfo.get("qfree"):
+        return ("k_cg_rm" if minfo["kernel"] == "rows" else "k_cg_march") + \
+            " B (march: q = A p(k) rebuilt, r -= ak q, z = r/d, z.r and r.r dots)"
+    return KERNELS[key]
+
+
 # rocprof kernel names of the CG kernels, per operator format
-ROCPROF_NAMES = {("pm", "stencil"): ("k_cg_pm",),
+ROCPROF_NAMES = {("pm", "stencil"): ("k_cg_rm<0", "k_cg_rm<1", "k_cg_march<0", "k_cg_march<1"),
                  ("ps", "stencil_tiled"): ("k_cg_ps<4>", "k_cg_ps<6>"),
                  ("resid", "stencil_tiled"): ("k_cg_b<true>",),
                  ("spmv", "stencil_split"): ("k_cg_spmv<4>", "k_cg_spmv<6>"),
                  ("resid", "stencil_split"): ("k_cg_b<true>",),
-                 ("resid", "stencil"): ("k_cg_b<true>",),
+                 ("resid", "stencil"): ("k_cg_b<true>", "k_cg_rm<2", "k_cg_march<2"),
                  ("xp", "stencil_split"): ("k_cg_p<true>",),
                  ("spmv", "stencil"): ("k_cg_spmv<4>", "k_cg_spmv<6>"),
                  ("spmv", "csr"): ("k_cg_spmv<0>",),
@@ -195,6 +211,8 @@ def main():
     ap.add_argument("--ps", type=float, default=0.593, help="site fraction for --kind sitebond")
     ap.add_argument("--full-voltages", action="store_true",
                     help="update x on every row every iteration (perc_set_full_voltages)")
+    ap.add_argument("--march-mode", type=int, default=-1,
+                    help="perc_set_march_mode bits (QFREE 1, ALT 2, ROWS 4); -1: library default")
     ap.add_argument("--format", choices=("auto", "stencil", "stencil_tiled", "stencil_split", "csr"),
                     default="auto",
                     help="solver operator format (perc_set_matrix_format)")
@@ -261,6 +279,8 @@ def main():
                            "stencil_tiled": P.FMT_STENCIL_TILED,
                            "stencil_split": P.FMT_STENCIL_SPLIT, "csr": P.FMT_CSR}[args.format])
     ctx.set_full_voltages(args.full_voltages)
+    if args.march_mode >= 0:
+        ctx.set_march_mode(args.march_mode)
     N, nnz = ctx.system_size()
 
     def run(k):
@@ -311,7 +331,9 @@ def main():
         fmt = {P.FMT_STENCIL: "stencil", P.FMT_STENCIL_TILED: "stencil_tiled",
                P.FMT_STENCIL_SPLIT: "stencil_split", P.FMT_CSR: "csr"}[ctx.matrix_format()]
         assembled = True
+        minfo = ctx.march_info()
     except P.PercError:
+        minfo = dict(kernel="none", qfree=False)
         fmt = {"auto": "stencil"}.get(args.format, args.format)
         assembled = False
 
@@ -320,7 +342,8 @@ def main():
         operator format f"""
         full = args.full_voltages
         if f in ("stencil", "stencil_tiled"):
-            return [("pm" if f == "stencil" else "ps", "spmv", 1, ps_bytes(N, L_, full)),
+            qf = f == "stencil" and minfo["qfree"]
+            return [("pm" if f == "stencil" else "ps", "spmv", 1, ps_bytes(N, L_, full, qf)),
                     ("resid", "resid", 2, resid_bytes(N, f))]
         return [("spmv", "spmv", 1, spmv_bytes(N, nnz, f)), ("resid", "resid", 2, resid_bytes(N, f)),
                 ("xp", "xp", 3, xp_bytes(N, f, L_, full))]
@@ -332,7 +355,7 @@ def main():
     for key, skey, _, nbytes in kernel_set(fmt):
         n_ = max(ks[skey + "_n"], 1)
         avg = ks[skey + "_ms"] / n_
-        kern[key] = {"kernel": KERNELS[key], "avg_launch_ms": round(avg, 5),
+        kern[key] = {"kernel": kernel_label(key, minfo), "avg_launch_ms": round(avg, 5),
                      "launches": ks[skey + "_n"], "total_ms": round(ks[skey + "_ms"], 1),
                      "bytes_per_launch": nbytes,
                      "gbs": round(nbytes / (avg * 1e-3) / 1e9, 1) if avg > 0 else None}

@@ -187,8 +187,14 @@ int perc_spmv_host(perc_ctx *h, const double *x, double *y);
    stream).  which: 0 = SpMV (dsprsax), 1 = CG SpMV + q.p dot, 2 = CG
    residual update (B), 3 = CG x/p update (P), 4 = STREAM copy 512 MB ->
    512 MB (16-B accesses, past the 256 MB Infinity Cache; the achievable-HBM
-   reference).  Clobbers solver vectors. */
+   reference), 5 = one whole CG iteration (every kernel of it, in order).
+   Clobbers solver vectors. */
 int perc_bench_kernel(perc_ctx *h, int which, int reps, double *ms);
+/* Self-test of the solver's table division (z = r/d from y = RN(1/d) and
+   one Markstein correction, bitwise IEEE division when it holds) on the
+   default device: n random (a, d) pairs; out3[0] = mismatches against `/`,
+   out3[1..2] = bit patterns of the first mismatching a and d. */
+int perc_selftest_division(long long n, unsigned long long seed, unsigned long long *out3);
 
 /* Live kernel timing: when enabled, the CG launches of every 8th
    iteration inside perc_conductance are bracketed by HIP events on the
@@ -231,6 +237,26 @@ int perc_set_full_voltages(perc_ctx *h, int enable);
    A tuning / test knob: results are the same up to the association of the
    q.p dot. */
 int perc_set_march_rows(perc_ctx *h, int rows);
+
+/* Register-march loop structure (PERC_FMT_STENCIL with m a multiple of
+   128).  PERC_MARCH_QFREE: the P+S kernel does not store q; the B kernel
+   (r -= ak q, z.r, r.r) marches too and rebuilds q = A p(k) from p(k), so
+   an iteration moves 52 instead of 60 bytes per row.  PERC_MARCH_ALT:
+   neighbouring bands walk in opposite directions, so the halo rows they
+   share are read at the same moment (cache hits).  Per-row arithmetic is
+   unchanged in every mode (bitwise the same values); the dot products are
+   summed in a different association.  The mode is read when the system is
+   assembled; default PERC_MARCH_DEFAULT. */
+#define PERC_MARCH_QFREE 1
+#define PERC_MARCH_ALT 2
+#define PERC_MARCH_ROWS 4
+#define PERC_MARCH_DEFAULT PERC_MARCH_ALT
+int perc_set_march_mode(perc_ctx *h, int mode);
+/* Solver loop of the assembled system: out5[0] = 0 (no march kernel: LDS
+   tiles, split or CSR), 1 (per-wave march k_cg_march), 2 (workgroup
+   row-march k_cg_rm); out5[1] = q-free B, out5[2] = alternating
+   directions, out5[3] = band height, out5[4] = strip width (columns). */
+int perc_march_info(perc_ctx *h, int *out5);
 
 /* format the solver kernels use on the assembled system: PERC_FMT_CSR,
    PERC_FMT_STENCIL (register-march fused kernel), PERC_FMT_STENCIL_TILED

@@ -24,6 +24,8 @@ BOND, SITE, SITEBOND = 0, 1, 2
 RULE_BOND, RULE_SITE, RULE_MIXED = 0, 1, 2
 CUR_FORTRAN, CUR_MATLAB = 0, 1
 FMT_AUTO, FMT_CSR, FMT_STENCIL, FMT_STENCIL_SPLIT, FMT_STENCIL_TILED = 0, 1, 2, 3, 4
+MARCH_QFREE, MARCH_ALT, MARCH_ROWS = 1, 2, 4
+MARCH_DEFAULT = MARCH_ALT
 
 
 class LabelInfo(C.Structure):
@@ -89,6 +91,9 @@ SIGNATURES = {
     "perc_trial_seeds_scaled": (None, [C.c_int, C.c_int, C.c_int, _I]),
     "perc_set_full_voltages": (C.c_int, [_VP, C.c_int]),
     "perc_set_march_rows": (C.c_int, [_VP, C.c_int]),
+    "perc_set_march_mode": (C.c_int, [_VP, C.c_int]),
+    "perc_march_info": (C.c_int, [_VP, _VP]),
+    "perc_selftest_division": (C.c_int, [C.c_longlong, C.c_ulonglong, _VP]),
     "perc_stats_accumulate": (None, [_D, C.c_int, C.c_double, C.c_int, C.c_int]),
     "sprsin_": (None, [_VP] * 7),
     "dsprsax_": (None, [_VP] * 5),

@@ -208,6 +208,17 @@ class Context:
         """Band height of the register-march kernel (0: auto; perc.h)."""
         L.check(L.lib().perc_set_march_rows(self.h, int(rows)), "perc_set_march_rows")
 
+    def set_march_mode(self, mode):
+        """PERC_MARCH_QFREE | PERC_MARCH_ALT bits of the register-march loop (perc.h)."""
+        L.check(L.lib().perc_set_march_mode(self.h, int(mode)), "perc_set_march_mode")
+
+    def march_info(self):
+        """The solver loop of the assembled system (perc_march_info)."""
+        out = np.zeros(5, dtype=np.int32)
+        L.check(L.lib().perc_march_info(self.h, out.ctypes.data), "perc_march_info")
+        return dict(kernel=("none", "wave", "rows")[out[0]], qfree=bool(out[1]),
+                    alt=bool(out[2]), band_rows=int(out[3]), strip_cols=int(out[4]))
+
     def matrix_format(self):
         rc = L.lib().perc_matrix_format(self.h)
         if rc < 0:

@@ -625,7 +625,7 @@ struct StencilView {
   const uint16_t* code;
   double ng0, nleak;  // -g0, -leak
   StencilForms F;
-  const double* dtab;  // code_diag of every code, by diag_idx (filled per assembly)
+  const double2* dtab;  // {code_diag, RN(1/code_diag)} of every code, by diag_idx
 };
 
 __device__ __forceinline__ double code_diag(unsigned c, double ng0, double nleak) {
@@ -639,17 +639,82 @@ __device__ __forceinline__ double code_diag(unsigned c, double ng0, double nleak
 
 // The diagonal of a row depends on 9 bits of its code (slot in-bits, count):
 // the hot kernels read it from a 512-entry table (filled by code_diag itself,
-// so bitwise the same) staged in LDS instead of re-summing the slots.
+// so bitwise the same) staged in LDS instead of re-summing the slots.  Each
+// entry also holds y = RN(1/d), so z = r/d is formed without the IEEE
+// division sequence (div_tab).
 constexpr int kDiagTab = 512;
 __device__ __forceinline__ unsigned diag_idx(unsigned c) { return (c & 0x3fu) | ((c >> 2) & 0x1c0u); }
 
-__global__ void k_fill_dtab(double* dtab, double ng0, double nleak) {
+__global__ void k_fill_dtab(double2* dtab, double ng0, double nleak) {
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
-  if (e < kDiagTab) dtab[e] = code_diag((e & 0x3fu) | ((e & 0x1c0u) << 2), ng0, nleak);
+  if (e < kDiagTab) {
+    const double d = code_diag((e & 0x3fu) | ((e & 0x1c0u) << 2), ng0, nleak);
+    // slot count 0 is no row's code; {1, 1} keeps the zero rows the
+    // row-march forms outside the lattice finite
+    dtab[e] = (e & 0x1c0u) ? make_double2(d, 1.0 / d) : make_double2(1.0, 1.0);
+  }
+}
+
+// a / d correctly rounded from y = RN(1/d): q = RN(a y) is within an ulp of
+// a/d, the remainder a - q d is exact (one fma), and RN(q + rem y) is the
+// correctly rounded quotient (Markstein's theorem; no overflow or
+// underflow at the magnitudes of r and d here).  3 fp64 operations and a
+// select instead of the ~10 of the IEEE division sequence; bitwise the same
+// quotient
+// (checked against `/` by perc_selftest_division, tests/test_gpu_parity.py).
+__device__ __forceinline__ double div_tab(double a, double2 dy) {
+  const double q = a * dy.y;
+  const double rem = __builtin_fma(-q, dy.x, a);
+  // rem == 0: q is exact (and keeps the sign of a zero quotient, which
+  // q + rem y would turn into +0)
+  return rem == 0.0 ? q : __builtin_fma(rem, dy.y, q);
+}
+
+// div_tab against IEEE `/`: n random (a, d) pairs, a over 600 binades (and
+// signed zeros), d the diagonals of the Kirchhoff rows (sums of 1..6 slot
+// values g0 / leak) or random over 90 binades; counts bitwise mismatches
+__device__ __forceinline__ unsigned long long splitmix64(unsigned long long x) {
+  x += 0x9E3779B97F4A7C15ull;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+  return x ^ (x >> 31);
+}
+__device__ __forceinline__ double rand_double(unsigned long long h, int emin, int emax) {
+  const unsigned long long e = (unsigned long long)(1023 + emin + (int)((h >> 52) % (emax - emin + 1)));
+  return __longlong_as_double((long long)(((h >> 11) & 1ull) << 63 | e << 52 |
+                                          (splitmix64(h) & 0xFFFFFFFFFFFFFull)));
+}
+__global__ void k_selftest_div(long long n, unsigned long long seed, unsigned long long* out) {
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n;
+       i += (long long)gridDim.x * blockDim.x) {
+    const unsigned long long h1 = splitmix64(seed ^ (2 * i)), h2 = splitmix64(seed ^ (2 * i + 1));
+    double a = rand_double(h1, -300, 300);
+    if ((h1 & 63) == 0) a = (h1 & 64) ? -0.0 : 0.0;
+    double d;
+    if (h2 & 1) {
+      const int c = 1 + (int)((h2 >> 1) % 6), kin = (int)((h2 >> 4) % (c + 1));
+      const double g0 = (h2 & 128) ? 1.0 : fabs(rand_double(h2 >> 8, -3, 3));
+      const double leak = (h2 & 256) ? 1e-12 : fabs(rand_double(h2 >> 9, -45, -20));
+      double rs = 0.0;
+      for (int j = 0; j < c; ++j) rs = rs + (j < kin ? -g0 : -leak);
+      d = -rs;
+    } else {
+      d = rand_double(h2, -45, 45);
+    }
+    const double2 dy = make_double2(d, 1.0 / d);
+    const double q1 = a / d, q2 = div_tab(a, dy);
+    if (__double_as_longlong(q1) != __double_as_longlong(q2)) {
+      const unsigned long long k = atomicAdd(out, 1ull);
+      if (k == 0) {
+        out[1] = (unsigned long long)__double_as_longlong(a);
+        out[2] = (unsigned long long)__double_as_longlong(d);
+      }
+    }
+  }
 }
 
 // copy the table to LDS (all threads call; the caller's barrier publishes it)
-__device__ __forceinline__ void load_dtab(const StencilView& St, double* s_dt) {
+__device__ __forceinline__ void load_dtab(const StencilView& St, double2* s_dt) {
   for (int e = threadIdx.x; e < kDiagTab; e += blockDim.x) s_dt[e] = St.dtab[e];
 }
 
@@ -796,6 +861,7 @@ __global__ __launch_bounds__(kBlock) void k_spmv_st(StencilView A, const double*
 struct TileGeom {
   int m, nrows, pbc, tpr;  // tpr: tiles per lattice row
   int bh;                  // band height of the register-march kernel
+  int rm_h;                // band height of the workgroup row-march kernel
 };
 
 struct CGArgs {
@@ -810,8 +876,9 @@ struct CGArgs {
   int fused;
   int b_reverse;  // B walks the row chunks in reverse logical order (fused mode)
   int xrows;      // 0: x kept on all rows; else only rows i < xrows or i >= N - xrows
-  int nt;         // nontemporal stores of p, q, r (stencil kernels)
   int kiter;      // the launch's CG iteration (fused PS kernels; host-counted)
+  int march_alt;  // march kernels: odd bands walk up in P, even bands in B
+  int bx;         // the streaming B applies x += ak p(k) (P and k_cg_xfinal do not)
   double* q;
   double* partials;  // kRedSlots slots of pstride doubles
   unsigned* tickets; // kRedSlots slots of tstride counters
@@ -941,7 +1008,7 @@ __global__ __launch_bounds__(kBlock) void k_cg_b(CGArgs a) {
   if (S->done) return;
   __shared__ double s_red[32];
   __shared__ int s_flag[2];
-  __shared__ double s_dt[ST ? kDiagTab : 1];
+  __shared__ double2 s_dt[ST ? kDiagTab : 1];
   if (ST) {
     load_dtab(a.St, s_dt);
     __syncthreads();
@@ -957,7 +1024,18 @@ __global__ __launch_bounds__(kBlock) void k_cg_b(CGArgs a) {
   block_pairs_lb(N, lbq, &q0, &q1);
   double acc[2] = {0.0, 0.0};  // z.r, r.r
   const int qf = min(q1, N / 2);
-  const bool nt = ST && a.nt;
+  constexpr bool nt = ST;
+  if (a.bx) {
+    // x += ak(k) p(k) on the rows x is kept on (linbcg's update of
+    // iteration k, bondc.f:795), before the march P of the next iteration
+    // would have applied it: the march kernels then carry no x at all
+    const double* __restrict__ pk = a.pb[k & 1];
+    const int xr = a.xrows == 0 ? N : a.xrows;
+    const int i0 = 2 * q0, i1 = min(2 * q1, N);
+    for (int i = i0 + threadIdx.x; i < min(i1, xr); i += kBlock) a.x[i] = a.x[i] + ak * pk[i];
+    if (a.xrows != 0)
+      for (int i = max(i0, max(N - xr, xr)) + threadIdx.x; i < i1; i += kBlock) a.x[i] = a.x[i] + ak * pk[i];
+  }
   // kBU pairs per thread in flight: every load of a batch is issued before
   // the first store (the compiler will not move loads of r above a store
   // to r, so a plain loop waits out one memory round trip per pair)
@@ -979,12 +1057,18 @@ __global__ __launch_bounds__(kBlock) void k_cg_b(CGArgs a) {
     for (int u = 0; u < kBU; ++u) {
       const int j = j0 + u * kBlock;
       if (j < qf) {
-        if (ST) dv[u] = make_double2(s_dt[diag_idx(cc[u] & 0xffffu)], s_dt[diag_idx(cc[u] >> 16)]);
         double2 rn;
         rn.x = rv[u].x - ak * qv[u].x;
         rn.y = rv[u].y - ak * qv[u].y;
         st2(r + 2 * j, rn, nt);
-        const double z0 = rn.x / dv[u].x, z1 = rn.y / dv[u].y;
+        double z0, z1;
+        if (ST) {
+          z0 = div_tab(rn.x, s_dt[diag_idx(cc[u] & 0xffffu)]);
+          z1 = div_tab(rn.y, s_dt[diag_idx(cc[u] >> 16)]);
+        } else {
+          z0 = rn.x / dv[u].x;
+          z1 = rn.y / dv[u].y;
+        }
         acc[0] = acc[0] + z0 * rn.x;
         acc[0] = acc[0] + z1 * rn.y;
         acc[1] = acc[1] + rn.x * rn.x;
@@ -1105,7 +1189,7 @@ __device__ __forceinline__ void load_form_lds(const StencilView& St, int* s_off,
 // y(i) of row i (code c) from the LDS tile; e0 = LDS index of site i
 template <int SL>
 __device__ __forceinline__ double tile_row(const StencilView& St, const int* s_off,
-                                           const int* s_dd, const double* s_dt, const double* s_p,
+                                           const int* s_dd, const double2* s_dt, const double* s_p,
                                            int i, int e0, unsigned c, double* xi) {
   const int f = c >> 11, cnt = (c >> 8) & 7;
   double xv[SL];
@@ -1117,7 +1201,7 @@ __device__ __forceinline__ double tile_row(const StencilView& St, const int* s_o
     xv[j] = s_p[use[j] ? e0 + s_dd[f * kMaxSlots + j] : e0];
   }
   *xi = s_p[e0];
-  return st_combine_d<SL>(c, s_dt[diag_idx(c)], xv, use, *xi, St.ng0, St.nleak);
+  return st_combine_d<SL>(c, s_dt[diag_idx(c)].x, xv, use, *xi, St.ng0, St.nleak);
 }
 
 template <int SL, bool STORE_Q, int TILEH>
@@ -1130,7 +1214,7 @@ __global__ __launch_bounds__(tile_threads(TILEH)) void k_cg_ps(CGArgs a) {
   __shared__ __attribute__((aligned(16))) double s_p[kTH * kTW];
   __shared__ int s_off[kMaxForms * kMaxSlots];
   __shared__ int s_dd[kMaxForms * kMaxSlots];
-  __shared__ double s_dt[kDiagTab];
+  __shared__ double2 s_dt[kDiagTab];
   __shared__ double s_red[32];
   __shared__ int s_flag[2];
   load_form_lds(a.St, s_off, s_dd);
@@ -1159,8 +1243,8 @@ __global__ __launch_bounds__(tile_threads(TILEH)) void k_cg_ps(CGArgs a) {
       const double2 pv = first ? make_double2(0.0, 0.0)
                                : *reinterpret_cast<const double2*>(pold + idx);
       double2 xv = xw ? *reinterpret_cast<const double2*>(x + idx) : make_double2(0.0, 0.0);
-      const double z0 = rv.x / s_dt[diag_idx(cc & 0xffffu)];
-      const double z1 = rv.y / s_dt[diag_idx(cc >> 16)];
+      const double z0 = div_tab(rv.x, s_dt[diag_idx(cc & 0xffffu)]);
+      const double z1 = div_tab(rv.y, s_dt[diag_idx(cc >> 16)]);
       if (first) {
         pn.x = z0;
         pn.y = z1;
@@ -1173,7 +1257,7 @@ __global__ __launch_bounds__(tile_threads(TILEH)) void k_cg_ps(CGArgs a) {
           *reinterpret_cast<double2*>(x + idx) = xv;
         }
       }
-      if (own) st2(pnew + idx, pn, a.nt);
+      if (own) st2(pnew + idx, pn, true);
     } else {
       tr = e / (kTW / 2);
       tc = 2 * (e - tr * (kTW / 2));
@@ -1201,7 +1285,7 @@ __global__ __launch_bounds__(tile_threads(TILEH)) void k_cg_ps(CGArgs a) {
       double xi;
       const double qv =
           tile_row<SL>(a.St, s_off, s_dd, s_dt, s_p, i, (lr + 1) * kTW + lc + 2, cr[u], &xi);
-      if (STORE_Q) st1(a.q + i, qv, a.nt);
+      if (STORE_Q) st1(a.q + i, qv, true);
       dot[0] = dot[0] + qv * xi;
     }
   }
@@ -1293,172 +1377,680 @@ __device__ __forceinline__ double march_q_gen(unsigned c, double d, double xi, u
   return acc;
 }
 
+// q of element E for a wave whose rows are all regular (slot order = raster
+// order) but not one form: lane-private raster -> slot map (rmap), so edge
+// strips (columns 0 and m-1 lack a neighbour) take this register path too.
+// Positions a row lacks read an exact 0 from the window (outside the
+// lattice or the interior system) or are skipped by the select.
+template <int E>
+__device__ __forceinline__ double march_q_map(unsigned c, double d, double xi, unsigned map,
+                                              unsigned umask, const MWin& U, const MWin& C,
+                                              const MWin& D, double ng0, double nleak) {
+  double acc = d * xi;
+#pragma unroll
+  for (int kp = 0; kp < 8; ++kp) {
+    if (umask & (1u << kp)) {
+      const unsigned j = (map >> (4 * kp)) & 15u;
+      const double gv = ((c >> j) & 1u) ? ng0 : nleak;
+      const double pr = gv * mwin_at<E>(kp, U, C, D);
+      acc = j != 15u ? acc + pr : acc;
+    }
+  }
+  return acc;
+}
+
 // rows prefetched ahead: 3 (+22 VGPRs) is no faster, nor are taller bands
 // with fewer waves and 4-6 rows ahead (H = 64: 0.138 vs 0.111 ms at L = 4096)
 constexpr int kMarchDepth = 2;
 
-template <int D = kMarchDepth>
-__global__ __launch_bounds__(64 * kMarchWaves) void k_cg_pm(CGArgs a) {
+// Register march, three kernels of one loop (MODE):
+//   kMarchPQ: P(k)+S(k), stores q for the streaming B (k_cg_b)
+//   kMarchP:  P(k)+S(k) without the q store
+//   kMarchB:  B(k) rebuilding q = A p(k) from p(k) (+ halo) instead of
+//             reading it: r -= ak q, z = r/d, z.r, r.r, bk, err, stop
+// With kMarchP + kMarchB an iteration moves 52N bytes instead of 60N.
+// Direction: a wave walks its band down (increasing rows) or up.  With
+// a.march_alt, odd bands walk up in P and even bands walk up in B, so the
+// halo rows two neighbouring bands share are read by both waves at the
+// same moment (start or end of the walk: the second read hits L2 / the
+// Infinity Cache), and B starts each band on the rows P wrote last.
+constexpr int kMarchPQ = 0, kMarchP = 1, kMarchB = 2;
+
+struct MGeom {
+  int r0, rend, col, hcol;
+  bool hok;
+};
+
+template <int MODE>
+__device__ __forceinline__ void march_load(const CGArgs& a, const MGeom& g, int gr, bool first,
+                                           const double* __restrict__ psrc, MRow& R) {
+  R.p = R.r = make_double2(0.0, 0.0);
+  R.c = R.hc = 0u;
+  R.hp = R.hr = 0.0;
+  const int m = a.T.m;
+  if (gr >= 0 && gr < a.T.nrows) {
+    const int i = gr * m + g.col;
+    R.c = *reinterpret_cast<const unsigned*>(a.St.code + i);
+    if (MODE != kMarchB || (gr >= g.r0 && gr < g.rend))
+      R.r = *reinterpret_cast<const double2*>(a.r + i);
+    if (!first) R.p = *reinterpret_cast<const double2*>(psrc + i);
+    if (g.hok) {
+      const int hi = gr * m + g.hcol;
+      if (MODE != kMarchB) {
+        R.hc = a.St.code[hi];
+        R.hr = a.r[hi];
+      }
+      if (!first) R.hp = psrc[hi];
+    }
+  }
+}
+
+struct MState {
+  MWin U, C, Dn;
+  unsigned cN, cM;        // codes of the newest / middle window rows
+  double2 rN, rM;         // r of the newest / middle rows (kMarchB)
+};
+
+// one step: row gr enters the window, then the middle row (gr -+ 1) is
+// finished when it is one of the band's own rows
+template <int MODE, bool UP>
+__device__ __forceinline__ void march_step(const CGArgs& a, const MGeom& g, const MRow& R, int gr,
+                                           bool first, double bk, double ak,
+                                           double* __restrict__ pnew, const double2* s_dt,
+                                           const unsigned* s_rpos, const unsigned* s_rmap,
+                                           double* s_w, MState& W, double (&acc)[2]) {
+  const int lane = threadIdx.x & 63;
+  const int m = a.T.m, nrows = a.T.nrows, N = a.St.N;
+  const double ng0 = a.St.ng0, nleak = a.St.nleak;
+  double2 pn = make_double2(0.0, 0.0);
+  double hpn = 0.0;
+  double2 d0 = make_double2(1.0, 1.0), d1 = d0;  // {d, 1/d}
+  if (gr >= 0 && gr < nrows) {
+    d0 = s_dt[diag_idx(R.c & 0xffffu)];
+    d1 = s_dt[diag_idx(R.c >> 16)];
+    if (MODE == kMarchB) {
+      pn = R.p;
+      hpn = R.hp;
+    } else {
+      const double z0 = div_tab(R.r.x, d0), z1 = div_tab(R.r.y, d1);
+      if (first) {
+        pn.x = z0;
+        pn.y = z1;
+      } else {
+        pn.x = bk * R.p.x + z0;
+        pn.y = bk * R.p.y + z1;
+      }
+      if (g.hok) {
+        const double zh = div_tab(R.hr, s_dt[diag_idx(R.hc)]);
+        hpn = first ? zh : bk * R.hp + zh;
+      }
+      if (gr >= g.r0 && gr < g.rend) {  // own row
+        const int i = gr * m + g.col;
+        st2(pnew + i, pn, true);
+        if (!first && !a.bx && (a.xrows == 0 || i < a.xrows || i >= N - a.xrows)) {
+          double2 xv = *reinterpret_cast<const double2*>(a.x + i);
+          xv.x = xv.x + ak * R.p.x;
+          xv.y = xv.y + ak * R.p.y;
+          *reinterpret_cast<double2*>(a.x + i) = xv;
+        }
+      }
+    }
+  }
+  MWin Nw;
+  Nw.e0 = pn.x;
+  Nw.e1 = pn.y;
+  const double up = __shfl_up(pn.y, 1);
+  const double dn = __shfl_down(pn.x, 1);
+  Nw.l = lane == 0 ? hpn : up;
+  Nw.rr = lane == 63 ? hpn : dn;
+  if (UP) {
+    W.Dn = W.C;
+    W.C = W.U;
+    W.U = Nw;
+  } else {
+    W.U = W.C;
+    W.C = W.Dn;
+    W.Dn = Nw;
+  }
+  W.cM = W.cN;
+  W.cN = R.c;
+  if (MODE == kMarchB) {
+    W.rM = W.rN;
+    W.rN = R.r;
+  }
+  const int mid = UP ? gr + 1 : gr - 1;
+  if (mid >= g.r0 && mid < g.rend) {  // wave-uniform
+    const unsigned c0w = W.cM & 0xffffu, c1w = W.cM >> 16;
+    const unsigned f0 = c0w >> 11, f1 = c1w >> 11;
+    const double2 dM0 = s_dt[diag_idx(c0w)], dM1 = s_dt[diag_idx(c1w)];
+    const unsigned ff = __builtin_amdgcn_readfirstlane(f0);
+    const bool uni = !__any(f0 != ff || f1 != ff) && a.St.F.regular[ff];
+    double q0, q1;
+    if (uni) {
+      const unsigned mask = a.St.F.rmask[ff];
+      q0 = march_q<0>(c0w, dM0.x, W.C.e0, mask, W.U, W.C, W.Dn, ng0, nleak);
+      q1 = march_q<1>(c1w, dM1.x, W.C.e1, mask, W.U, W.C, W.Dn, ng0, nleak);
+    } else {
+      const unsigned mp0 = s_rmap[f0], mp1 = s_rmap[f1];
+      if (!__any(mp0 == kRmapIrregular || mp1 == kRmapIrregular)) {
+        const unsigned um = a.St.F.umask;
+        q0 = march_q_map<0>(c0w, dM0.x, W.C.e0, mp0, um, W.U, W.C, W.Dn, ng0, nleak);
+        q1 = march_q_map<1>(c1w, dM1.x, W.C.e1, mp1, um, W.U, W.C, W.Dn, ng0, nleak);
+      } else {
+        const MWin* rows[3] = {&W.U, &W.C, &W.Dn};
+#pragma unroll
+        for (int rr = 0; rr < 3; ++rr) {
+          s_w[(4 * rr + 0) * 64 + lane] = rows[rr]->l;
+          s_w[(4 * rr + 1) * 64 + lane] = rows[rr]->e0;
+          s_w[(4 * rr + 2) * 64 + lane] = rows[rr]->e1;
+          s_w[(4 * rr + 3) * 64 + lane] = rows[rr]->rr;
+        }
+        // lane-private slots: no cross-lane hazard, only the wave's own
+        // LDS write -> read order (lgkmcnt, inserted by the compiler)
+        q0 = march_q_gen<0>(c0w, dM0.x, W.C.e0, s_rpos[f0], s_w, lane, ng0, nleak);
+        q1 = march_q_gen<1>(c1w, dM1.x, W.C.e1, s_rpos[f1], s_w, lane, ng0, nleak);
+      }
+    }
+    const int i = mid * m + g.col;
+    if (MODE == kMarchB) {
+      // k_cg_b's per-pair arithmetic
+      double2 rn;
+      rn.x = W.rM.x - ak * q0;
+      rn.y = W.rM.y - ak * q1;
+      st2(a.r + i, rn, true);
+      const double z0 = div_tab(rn.x, dM0), z1 = div_tab(rn.y, dM1);
+      acc[0] = acc[0] + z0 * rn.x;
+      acc[0] = acc[0] + z1 * rn.y;
+      acc[1] = acc[1] + rn.x * rn.x;
+      acc[1] = acc[1] + rn.y * rn.y;
+    } else {
+      if (MODE == kMarchPQ) st2(a.q + i, make_double2(q0, q1), true);
+      acc[0] = acc[0] + q0 * W.C.e0;
+      acc[0] = acc[0] + q1 * W.C.e1;
+    }
+  }
+}
+
+template <int MODE, int D, bool UP>
+__device__ __forceinline__ void march_walk(const CGArgs& a, const MGeom& g, MRow (&ring)[D],
+                                           bool first, double bk, double ak,
+                                           const double* __restrict__ psrc,
+                                           double* __restrict__ pnew, const double2* s_dt,
+                                           const unsigned* s_rpos, const unsigned* s_rmap,
+                                           double* s_w, double (&acc)[2]) {
+  MState W;
+  W.U = MWin{0.0, 0.0, 0.0, 0.0};
+  W.C = W.U;
+  W.Dn = W.U;
+  W.cN = W.cM = 0u;
+  W.rN = W.rM = make_double2(0.0, 0.0);
+  const int nsteps = g.rend - g.r0 + 2;  // rows r0-1 .. rend
+  for (int j0 = 0; j0 < nsteps; j0 += D) {
+#pragma unroll
+    for (int u = 0; u < D; ++u) {
+      const int j = j0 + u;
+      if (j < nsteps) {
+        const MRow R = ring[u];
+        if (j + D < nsteps)
+          march_load<MODE>(a, g, UP ? g.rend - (j + D) : g.r0 - 1 + j + D, first, psrc, ring[u]);
+        march_step<MODE, UP>(a, g, R, UP ? g.rend - j : g.r0 - 1 + j, first, bk, ak, pnew, s_dt,
+                             s_rpos, s_rmap, s_w, W, acc);
+      }
+    }
+  }
+}
+
+template <int MODE, int D = kMarchDepth>
+__global__ __launch_bounds__(64 * kMarchWaves) void k_cg_march(CGArgs a) {
   CGScalars* S = a.S;
   __shared__ double s_red[32];
   __shared__ int s_flag[2];
-  __shared__ unsigned s_rpos[kMaxForms];
-  __shared__ double s_dt[kDiagTab];
+  __shared__ unsigned s_rpos[kMaxForms], s_rmap[kMaxForms];
+  __shared__ double2 s_dt[kDiagTab];
   __shared__ double s_win[kMarchWaves][12 * 64];  // general-path window scratch
   // the launch's iteration comes from the host (launch j of a solve is
   // iteration j + 1 until the stop; later launches return below), so the
   // first rows' loads go out before any device scalar is read
   const int k = a.kiter;
-  const bool first = k == 1;
-  const double ng0 = a.St.ng0, nleak = a.St.nleak;
-  const double* __restrict__ pold = a.pb[(k - 1) & 1];
+  const bool first = MODE != kMarchB && k == 1;
+  // P reads p(k-1) and writes p(k); B reads p(k)
+  const double* __restrict__ psrc = a.pb[(MODE == kMarchB ? k : k - 1) & 1];
   double* __restrict__ pnew = a.pb[k & 1];
-  const double* __restrict__ r = a.r;
-  const uint16_t* __restrict__ code = a.St.code;
-  double* __restrict__ x = a.x;
-  const int N = a.St.N, m = a.T.m, nrows = a.T.nrows, H = a.T.bh;
+  const int m = a.T.m, nrows = a.T.nrows, H = a.T.bh;
   const int lb = xcd_logical_block(blockIdx.x, gridDim.x);
   const int lane = threadIdx.x & 63;
   const int w = lb * kMarchWaves + (threadIdx.x >> 6);
   const int spr = m / kMarchW;
   const int band = w / spr, strip = w - band * spr;
-  const int r0 = band * H;
-  const bool active = r0 < nrows;  // wave-uniform
-  const int c0 = strip * kMarchW, col = c0 + 2 * lane;
-  int hcol = lane == 0 ? c0 - 1 : c0 + kMarchW;
-  bool hok = lane == 0 || lane == 63;
+  MGeom g;
+  g.r0 = band * H;
+  g.rend = min(g.r0 + H, nrows);
+  const bool active = g.r0 < nrows;  // wave-uniform
+  const int c0 = strip * kMarchW;
+  g.col = c0 + 2 * lane;
+  g.hcol = lane == 0 ? c0 - 1 : c0 + kMarchW;
+  g.hok = lane == 0 || lane == 63;
+  if (g.hcol < 0 || g.hcol >= m) {
+    if (a.T.pbc) g.hcol += g.hcol < 0 ? m : -m;
+    else g.hok = false;
+  }
+  const bool up = (a.march_alt && (band & 1)) != (MODE == kMarchB);
+  const int nsteps = g.rend - g.r0 + 2;
+  MRow ring[D];
+  if (active) {
+#pragma unroll
+    for (int u = 0; u < D; ++u)
+      if (u < nsteps) march_load<MODE>(a, g, up ? g.rend - u : g.r0 - 1 + u, first, psrc, ring[u]);
+  }
+  if (S->done) return;
+  if (threadIdx.x < kMaxForms) {
+    s_rpos[threadIdx.x] = a.St.F.rpos[threadIdx.x];
+    s_rmap[threadIdx.x] = a.St.F.rmap[threadIdx.x];
+  }
+  load_dtab(a.St, s_dt);
+  __syncthreads();
+  const double bk = S->bk, ak = S->ak;
+  double acc[2] = {0.0, 0.0};
+  if (active) {
+    double* s_w = s_win[threadIdx.x >> 6];
+    if (up) march_walk<MODE, D, true>(a, g, ring, first, bk, ak, psrc, pnew, s_dt, s_rpos, s_rmap, s_w, acc);
+    else march_walk<MODE, D, false>(a, g, ring, first, bk, ak, psrc, pnew, s_dt, s_rpos, s_rmap, s_w, acc);
+  }
+  if (MODE != kMarchB) {
+    double v[1] = {acc[0]}, tot[1];
+    if (publish_and_reduce<1>(v, a.partials, a.tickets, lb, gridDim.x, tot, s_red, s_flag)) {
+      if (threadIdx.x == 0) {
+        S->akden = tot[0];
+        S->ak = S->bknum / tot[0];
+      }
+    }
+  } else {
+    double tot[2];
+    if (publish_and_reduce<2>(acc, a.partials + a.pstride, a.tickets + a.tstride, lb, gridDim.x,
+                              tot, s_red, s_flag)) {
+      if (threadIdx.x == 0) {  // k_cg_b's epilogue
+        const int kk = S->iter + 1;
+        const double err = sqrt(tot[1]) / S->bnrm;
+        S->bk = tot[0] / S->bknum;
+        S->bknum = tot[0];
+        S->err = err;
+        if (kk - 1 < a.err_hist_cap) a.err_hist[kk - 1] = err;
+        S->iter = kk;
+        if (!(err > S->tol) || kk >= S->itmax + 1) S->done = 1;
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Workgroup row-march (stencil operator, m a multiple of W).  A workgroup of
+// W/4 threads owns a strip of W columns (thread t: column pairs 2t and
+// 2t + W/2, so each wave instruction moves 1 KB contiguous) and walks an
+// H-row band, one lattice row per step.  Each step forms the row's p(k)
+// into a 4-slot LDS ring (plus the strip's two halo columns), one barrier,
+// then sums q of the previous row from the ring in slot order.  Against
+// the per-wave march (k_cg_march) a step moves a whole 16 KB row segment
+// per stream for the workgroup, which streams ~14 % faster on the pure
+// access pattern (tools/mix_bench.hip: 0.0887 vs 0.1035 ms).  Modes,
+// directions and per-row arithmetic are k_cg_march's.
+constexpr int kRmSlots = 4;
+constexpr int kRmMinGroups = 512;
+
+struct RRow {       // one prefetched row of the thread's two pairs (+ halo)
+  double2 pa, pb, ra, rb;
+  unsigned ca, cb;
+  double hp, hr;
+  unsigned hc;
+};
+
+// Workgroup barrier for LDS traffic only: the workgroup's own ds_writes are
+// complete (lgkmcnt(0)), then s_barrier.  __syncthreads() is a release
+// fence for global memory too, i.e. s_waitcnt vmcnt(0) before the barrier:
+// in the row-march that drained every prefetched row and every store in
+// flight once per step.  The asm's "memory" clobber keeps the compiler from
+// moving memory accesses across it.
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+// q of one element from the ring in slot order (every form, wrapped ones too)
+__device__ __forceinline__ double rm_q(unsigned c, double d, double xi, unsigned rpos,
+                                       const double* sU, const double* sC, const double* sD,
+                                       int lc, double ng0, double nleak) {
+  double acc = d * xi;
+  const int cnt = (c >> 8) & 7;
+#pragma unroll
+  for (int j = 0; j < kMaxSlots; ++j) {
+    if (j < cnt) {
+      const int kp = (rpos >> (3 * j)) & 7;
+      const double* row = kp < 3 ? sU : (kp < 5 ? sC : sD);
+      const int dc = kp < 3 ? kp - 1 : (kp == 3 ? -1 : (kp == 4 ? 1 : kp - 6));
+      const double gv = ((c >> j) & 1u) ? ng0 : nleak;
+      acc = acc + gv * row[lc + dc];
+    }
+  }
+  return acc;
+}
+
+// rm_q for a wave whose elements all share one regular form (slot order =
+// raster order, used positions `mask`): wave-uniform branches, fixed offsets
+__device__ __forceinline__ double rm_q_uni(unsigned c, double d, double xi, unsigned mask,
+                                           const double* sU, const double* sC, const double* sD,
+                                           int lc, double ng0, double nleak) {
+  double acc = d * xi;
+  int j = 0;
+#pragma unroll
+  for (int kp = 0; kp < 8; ++kp) {
+    if (mask & (1u << kp)) {
+      const double* row = kp < 3 ? sU : (kp < 5 ? sC : sD);
+      const int dc = kp < 3 ? kp - 1 : (kp == 3 ? -1 : (kp == 4 ? 1 : kp - 6));
+      const double gv = ((c >> j) & 1u) ? ng0 : nleak;
+      acc = acc + gv * row[lc + dc];
+      ++j;
+    }
+  }
+  return acc;
+}
+
+// Buffer access with a hardware range check: a byte offset at or past the
+// buffer's size makes a load return 0 and drops a store.  The row-march
+// keeps every memory instruction of a step unconditional this way (rows
+// outside the lattice or the band, halo columns of non-halo threads, q of
+// the steps without a finished row, x off the electrode rows), so hipcc's
+// s_waitcnt bookkeeping stays exact across the loop: with loads and stores
+// under branches it waited for vmcnt(0) -- every prefetched row and every
+// store in flight -- once per step.
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+constexpr unsigned kOOB = 0x80000000u;  // buffers are kept below 2 GB (march_geometry)
+constexpr int kNT = 2;                  // aux bits: nontemporal
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* p, unsigned bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, (int)bytes, 0x00020000);
+}
+__device__ __forceinline__ double2 bld2(__amdgpu_buffer_rsrc_t r, unsigned off) {
+  return __builtin_bit_cast(double2, __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 0));
+}
+__device__ __forceinline__ double bld1(__amdgpu_buffer_rsrc_t r, unsigned off) {
+  return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, (int)off, 0, 0));
+}
+template <int AUX>
+__device__ __forceinline__ void bst2(__amdgpu_buffer_rsrc_t r, unsigned off, double2 v) {
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, (int)off, 0, AUX);
+}
+
+template <int MODE, int W, int D, bool XB>
+__device__ __forceinline__ void rm_walk(const CGArgs& a, RRow (&ring)[D], int t, int r0, int rend,
+                                        bool up, int cA, int hcol, bool hok, bool first,
+                                        double bk, double ak, const double2* s_dt,
+                                        const unsigned* s_rpos, double* s_ring,
+                                        double (&acc)[2]);
+
+template <int MODE, int W, int D = 2>
+__global__ __launch_bounds__(W / 4) void k_cg_rm(CGArgs a) {
+  constexpr int T = W / 4, SL = W + 4;  // slot: [1] left halo, [2 + c], [W + 2] right halo
+  CGScalars* S = a.S;
+  __shared__ __attribute__((aligned(16))) double s_ring[kRmSlots * SL];
+  __shared__ double2 s_dt[kDiagTab];
+  __shared__ unsigned s_rpos[kMaxForms];
+  __shared__ double s_red[32];
+  __shared__ int s_flag[2];
+  const int t = threadIdx.x;
+  const int k = a.kiter;
+  const bool first = MODE != kMarchB && k == 1;
+  const int m = a.T.m, nrows = a.T.nrows, H = a.T.rm_h, N = a.St.N;
+  const int lb = xcd_logical_block(blockIdx.x, gridDim.x);
+  const int spr = m / W;
+  const int band = lb / spr, strip = lb - band * spr;
+  const int r0 = band * H, rend = min(r0 + H, nrows);
+  const bool active = r0 < nrows;  // workgroup-uniform
+  const int cA = strip * W + 2 * t;
+  int hcol = t == 0 ? strip * W - 1 : strip * W + W;
+  bool hok = t == 0 || t == T - 1;
   if (hcol < 0 || hcol >= m) {
     if (a.T.pbc) hcol += hcol < 0 ? m : -m;
     else hok = false;
   }
-  const int rend = min(r0 + H, nrows);
-  const int nsteps = rend - r0 + 2;  // rows r0-1 .. rend
-  auto load = [&](int gr, MRow& R) {
-    R.p = R.r = make_double2(0.0, 0.0);
-    R.c = R.hc = 0u;
-    R.hp = R.hr = 0.0;
-    if (gr >= 0 && gr < nrows) {
-      const int i = gr * m + col;
-      R.c = *reinterpret_cast<const unsigned*>(code + i);
-      R.r = *reinterpret_cast<const double2*>(r + i);
-      if (!first) R.p = *reinterpret_cast<const double2*>(pold + i);
-      if (hok) {
-        const int hi = gr * m + hcol;
-        R.hc = code[hi];
-        R.hr = r[hi];
-        if (!first) R.hp = pold[hi];
-      }
-    }
-  };
-  MRow ring[D];
-  if (active) {
-#pragma unroll
-    for (int u = 0; u < D; ++u) load(r0 - 1 + u, ring[u]);
-  }
+  const bool up = (a.march_alt && (band & 1)) != (MODE == kMarchB);
+  // bands holding an electrode-adjacent row (or every band, with all
+  // voltages kept) also carry x in their ring
+  // (the q-storing mode always runs with the streaming B, which does x)
+  const bool xb = MODE == kMarchP && !a.bx && (a.xrows == 0 || r0 == 0 || rend == nrows);
+  RRow ring[D];
   if (S->done) return;
-  if (threadIdx.x < kMaxForms) s_rpos[threadIdx.x] = a.St.F.rpos[threadIdx.x];
+  if (t < kMaxForms) s_rpos[t] = a.St.F.rpos[t];
   load_dtab(a.St, s_dt);
   __syncthreads();
   const double bk = S->bk, ak = S->ak;
-  double dot = 0.0;
+  double acc[2] = {0.0, 0.0};
   if (active) {
-    MWin U{0.0, 0.0, 0.0, 0.0}, C = U, Dn = U;
-    unsigned cC = 0u, cD = 0u;
-    double dC0 = 1.0, dC1 = 1.0, dD0 = 1.0, dD1 = 1.0;
-    // p(k) of row gr (the new bottom row of the window), then q of row gr - 1
-    auto step = [&](const MRow& R, int gr) {
-      double2 pn = make_double2(0.0, 0.0);
-      double hpn = 0.0, d0 = 1.0, d1 = 1.0;
-      if (gr >= 0 && gr < nrows) {
-        d0 = s_dt[diag_idx(R.c & 0xffffu)];
-        d1 = s_dt[diag_idx(R.c >> 16)];
-        const double z0 = R.r.x / d0, z1 = R.r.y / d1;
-        if (first) {
-          pn.x = z0;
-          pn.y = z1;
-        } else {
-          pn.x = bk * R.p.x + z0;
-          pn.y = bk * R.p.y + z1;
-        }
-        if (hok) {
-          const double zh = R.hr / s_dt[diag_idx(R.hc)];
-          hpn = first ? zh : bk * R.hp + zh;
-        }
-        if (gr >= r0 && gr < rend) {  // own row (rend: the next band's first row)
-          const int i = gr * m + col;
-          st2(pnew + i, pn, a.nt);
-          if (!first && (a.xrows == 0 || i < a.xrows || i >= N - a.xrows)) {
-            double2 xv = *reinterpret_cast<const double2*>(x + i);
-            xv.x = xv.x + ak * R.p.x;
-            xv.y = xv.y + ak * R.p.y;
-            *reinterpret_cast<double2*>(x + i) = xv;
-          }
-        }
+    if (xb) rm_walk<MODE, W, D, true>(a, ring, t, r0, rend, up, cA, hcol, hok, first, bk, ak, s_dt,
+                                      s_rpos, s_ring, acc);
+    else rm_walk<MODE, W, D, false>(a, ring, t, r0, rend, up, cA, hcol, hok, first, bk, ak, s_dt,
+                                    s_rpos, s_ring, acc);
+  }
+  (void)N;
+  if (MODE != kMarchB) {
+    double v[1] = {acc[0]}, tot[1];
+    if (publish_and_reduce<1>(v, a.partials, a.tickets, lb, gridDim.x, tot, s_red, s_flag)) {
+      if (threadIdx.x == 0) {
+        S->akden = tot[0];
+        S->ak = S->bknum / tot[0];
       }
-      MWin W;
-      W.e0 = pn.x;
-      W.e1 = pn.y;
-      const double up = __shfl_up(pn.y, 1);
-      const double dn = __shfl_down(pn.x, 1);
-      W.l = lane == 0 ? hpn : up;
-      W.rr = lane == 63 ? hpn : dn;
-      U = C;
-      C = Dn;
-      Dn = W;
-      cC = cD;
-      dC0 = dD0;
-      dC1 = dD1;
-      cD = R.c;
-      dD0 = d0;
-      dD1 = d1;
-      if (gr - 1 >= r0) {  // the middle row is complete: q, q.p
-        const unsigned c0w = cC & 0xffffu, c1w = cC >> 16;
-        const unsigned f0 = c0w >> 11, f1 = c1w >> 11;
-        const unsigned ff = __builtin_amdgcn_readfirstlane(f0);
-        const bool uni = !__any(f0 != ff || f1 != ff) && a.St.F.regular[ff];
-        double q0, q1;
-        if (uni) {
-          const unsigned mask = a.St.F.rmask[ff];
-          q0 = march_q<0>(c0w, dC0, C.e0, mask, U, C, Dn, ng0, nleak);
-          q1 = march_q<1>(c1w, dC1, C.e1, mask, U, C, Dn, ng0, nleak);
-        } else {
-          double* s_w = s_win[threadIdx.x >> 6];
-          const MWin* rows[3] = {&U, &C, &Dn};
-#pragma unroll
-          for (int rr = 0; rr < 3; ++rr) {
-            s_w[(4 * rr + 0) * 64 + lane] = rows[rr]->l;
-            s_w[(4 * rr + 1) * 64 + lane] = rows[rr]->e0;
-            s_w[(4 * rr + 2) * 64 + lane] = rows[rr]->e1;
-            s_w[(4 * rr + 3) * 64 + lane] = rows[rr]->rr;
-          }
-          // lane-private slots: no cross-lane hazard, only the wave's own
-          // LDS write -> read order (lgkmcnt, inserted by the compiler)
-          q0 = march_q_gen<0>(c0w, dC0, C.e0, s_rpos[f0], s_w, lane, ng0, nleak);
-          q1 = march_q_gen<1>(c1w, dC1, C.e1, s_rpos[f1], s_w, lane, ng0, nleak);
-        }
-        const int i = (gr - 1) * m + col;
-        st2(a.q + i, make_double2(q0, q1), a.nt);
-        dot = dot + q0 * C.e0;
-        dot = dot + q1 * C.e1;
-      }
-    };
-    for (int j0 = 0; j0 < nsteps; j0 += D) {
-#pragma unroll
-      for (int u = 0; u < D; ++u) {
-        const int j = j0 + u;
-        if (j < nsteps) {
-          const MRow R = ring[u];
-          if (j + D < nsteps) load(r0 - 1 + j + D, ring[u]);
-          step(R, r0 - 1 + j);
-        }
+    }
+  } else {
+    double tot[2];
+    if (publish_and_reduce<2>(acc, a.partials + a.pstride, a.tickets + a.tstride, lb, gridDim.x,
+                              tot, s_red, s_flag)) {
+      if (threadIdx.x == 0) {  // k_cg_b's epilogue
+        const int kk = S->iter + 1;
+        const double err = sqrt(tot[1]) / S->bnrm;
+        S->bk = tot[0] / S->bknum;
+        S->bknum = tot[0];
+        S->err = err;
+        if (kk - 1 < a.err_hist_cap) a.err_hist[kk - 1] = err;
+        S->iter = kk;
+        if (!(err > S->tol) || kk >= S->itmax + 1) S->done = 1;
       }
     }
   }
-  double v[1] = {dot}, tot[1];
-  if (publish_and_reduce<1>(v, a.partials, a.tickets, lb, gridDim.x, tot, s_red, s_flag)) {
-    if (threadIdx.x == 0) {
-      S->akden = tot[0];
-      S->ak = S->bknum / tot[0];
+}
+
+template <int MODE, int W, int D, bool XB>
+__device__ __forceinline__ void rm_walk(const CGArgs& a, RRow (&ring)[D], int t, int r0, int rend,
+                                        bool up, int cA, int hcol, bool hok, bool first,
+                                        double bk, double ak, const double2* s_dt,
+                                        const unsigned* s_rpos, double* s_ring,
+                                        double (&acc)[2]) {
+  constexpr int T = W / 4, SL = W + 4;
+  const int m = a.T.m, nrows = a.T.nrows, N = a.St.N;
+  const int k = a.kiter;
+  const unsigned vbytes = (unsigned)(N + 2) * 8u;
+  const __amdgpu_buffer_rsrc_t rc = rsrc(a.St.code, (unsigned)N * 2u);
+  const __amdgpu_buffer_rsrc_t rr = rsrc(a.r, vbytes);
+  const __amdgpu_buffer_rsrc_t rp = rsrc(a.pb[(MODE == kMarchB ? k : k - 1) & 1], vbytes);
+  const __amdgpu_buffer_rsrc_t rpn = rsrc(a.pb[k & 1], vbytes);
+  const __amdgpu_buffer_rsrc_t rq = rsrc(a.q, vbytes);
+  const __amdgpu_buffer_rsrc_t rx = rsrc(a.x, vbytes);
+  const double ng0 = a.St.ng0, nleak = a.St.nleak;
+  const int nsteps = rend - r0 + 2;  // rows r0-1 .. rend
+  auto rowof = [&](int j) { return up ? rend - j : r0 - 1 + j; };
+  auto xrow = [&](int gr) {  // x kept on this row (XB bands only)
+    const int i = gr * m;
+    return a.xrows == 0 || i < a.xrows || i >= N - a.xrows;
+  };
+  // x of the thread's two pairs rides in the ring's p slots' neighbours:
+  // XB bands load it with the row (hp/hr halo slots are separate)
+  double2 ringx[XB ? D : 1][2];
+  auto load = [&](int j, RRow& R, double2 (&X)[2]) {
+    const int gr = rowof(j);
+    const bool ok = j < nsteps && gr >= 0 && gr < nrows;
+    const unsigned ia = (unsigned)(gr * m + cA), ih = (unsigned)(gr * m + hcol);
+    const unsigned o8a = ok ? ia * 8u : kOOB, o8b = ok ? (ia + W / 2) * 8u : kOOB;
+    R.ca = __builtin_amdgcn_raw_buffer_load_b32(rc, (int)(ok ? ia * 2u : kOOB), 0, 0);
+    R.cb = __builtin_amdgcn_raw_buffer_load_b32(rc, (int)(ok ? (ia + W / 2) * 2u : kOOB), 0, 0);
+    const bool rok = MODE != kMarchB || (gr >= r0 && gr < rend);
+    R.ra = bld2(rr, rok ? o8a : kOOB);
+    R.rb = bld2(rr, rok ? o8b : kOOB);
+    R.pa = bld2(rp, first ? kOOB : o8a);
+    R.pb = bld2(rp, first ? kOOB : o8b);
+    const bool hl = ok && hok;
+    R.hp = bld1(rp, hl && !first ? ih * 8u : kOOB);
+    if (MODE != kMarchB) {
+      R.hr = bld1(rr, hl ? ih * 8u : kOOB);
+      R.hc = __builtin_amdgcn_raw_buffer_load_b16(rc, (int)(hl ? ih * 2u : kOOB), 0, 0);
+    } else {
+      R.hr = 0.0;
+      R.hc = 0u;
+    }
+    if (XB) {
+      const bool xo = ok && !first && gr >= r0 && gr < rend && xrow(gr);
+      X[0] = bld2(rx, xo ? o8a : kOOB);
+      X[1] = bld2(rx, xo ? o8b : kOOB);
+    }
+  };
+#pragma unroll
+  for (int u = 0; u < D; ++u) load(u, ring[u], ringx[XB ? u : 0]);
+  // Step j forms row rowof(j) into slot j & 3 and sums q of the row formed
+  // two steps earlier from the rows of steps j-3 .. j-1, which every wave
+  // finished before the previous barrier: the two halves of a step do not
+  // wait for each other, and one barrier per step keeps the 4-slot ring
+  // safe (slot j & 3 was last read in step j-1).  One extra step sums the
+  // band's last row.
+  unsigned c1a = 0u, c1b = 0u, c2a = 0u, c2b = 0u;  // codes of steps j-1, j-2
+  double2 r1a = make_double2(0.0, 0.0), r1b = r1a, r2a = r1a, r2b = r1a;  // r (B)
+  const int nloop = nsteps + 1;
+  for (int j0 = 0; j0 < nloop; j0 += D) {
+#pragma unroll
+    for (int u = 0; u < D; ++u) {
+      const int j = j0 + u;
+      if (j >= nloop) break;  // workgroup-uniform
+      const RRow R = ring[u];
+      double2 X[2] = {make_double2(0.0, 0.0), make_double2(0.0, 0.0)};
+      if (XB) {
+        X[0] = ringx[XB ? u : 0][0];
+        X[1] = ringx[XB ? u : 0][1];
+      }
+      load(j + D, ring[u], ringx[XB ? u : 0]);
+      const int gr = rowof(j);
+      const bool ok = j < nsteps && gr >= 0 && gr < nrows;
+      const bool own = j < nsteps && gr >= r0 && gr < rend;
+      double* sl = s_ring + (j & 3) * SL;
+      double2 pa, pb;
+      double hpn;
+      if (MODE == kMarchB) {
+        pa = R.pa;
+        pb = R.pb;
+        hpn = R.hp;
+      } else {
+        const double za0 = div_tab(R.ra.x, s_dt[diag_idx(R.ca & 0xffffu)]);
+        const double za1 = div_tab(R.ra.y, s_dt[diag_idx(R.ca >> 16)]);
+        const double zb0 = div_tab(R.rb.x, s_dt[diag_idx(R.cb & 0xffffu)]);
+        const double zb1 = div_tab(R.rb.y, s_dt[diag_idx(R.cb >> 16)]);
+        const double zh = div_tab(R.hr, s_dt[diag_idx(R.hc)]);
+        if (first) {
+          pa = make_double2(za0, za1);
+          pb = make_double2(zb0, zb1);
+          hpn = zh;
+        } else {
+          pa.x = bk * R.pa.x + za0;
+          pa.y = bk * R.pa.y + za1;
+          pb.x = bk * R.pb.x + zb0;
+          pb.y = bk * R.pb.y + zb1;
+          hpn = bk * R.hp + zh;
+        }
+        if (!ok) pa = pb = make_double2(0.0, 0.0);
+        if (!(ok && hok)) hpn = 0.0;
+        const unsigned ia = (unsigned)(gr * m + cA);
+        bst2<kNT>(rpn, own ? ia * 8u : kOOB, pa);
+        bst2<kNT>(rpn, own ? (ia + W / 2) * 8u : kOOB, pb);
+        if (XB) {
+          const bool xo = own && !first && xrow(gr);
+          double2 xa = X[0], xb = X[1];
+          xa.x = xa.x + ak * R.pa.x;
+          xa.y = xa.y + ak * R.pa.y;
+          xb.x = xb.x + ak * R.pb.x;
+          xb.y = xb.y + ak * R.pb.y;
+          bst2<0>(rx, xo ? ia * 8u : kOOB, xa);
+          bst2<0>(rx, xo ? (ia + W / 2) * 8u : kOOB, xb);
+        }
+      }
+      *reinterpret_cast<double2*>(sl + 2 + 2 * t) = pa;
+      *reinterpret_cast<double2*>(sl + 2 + 2 * t + W / 2) = pb;
+      if (t == 0) sl[1] = hpn;
+      if (t == T - 1) sl[W + 2] = hpn;
+      const int mid = up ? rend - j + 2 : r0 - 3 + j;
+      const bool qok = j >= 3 && mid >= r0 && mid < rend;  // workgroup-uniform
+      {
+        const double* s1 = s_ring + ((j - 1) & 3) * SL + 2;  // row formed at step j-1
+        const double* sM = s_ring + ((j - 2) & 3) * SL + 2;  // row mid
+        const double* s3 = s_ring + ((j - 3) & 3) * SL + 2;  // row formed at step j-3
+        const double* sU = up ? s1 : s3;                      // row mid - 1
+        const double* sD = up ? s3 : s1;                      // row mid + 1
+        const unsigned cs[4] = {c2a & 0xffffu, c2a >> 16, c2b & 0xffffu, c2b >> 16};
+        double2 dM[4];  // {d, 1/d}
+#pragma unroll
+        for (int e = 0; e < 4; ++e) dM[e] = s_dt[diag_idx(cs[e])];
+        double qv[4], xv[4];
+        const unsigned ff = __builtin_amdgcn_readfirstlane(cs[0] >> 11);
+        const bool uni = !__any((cs[0] >> 11) != ff || (cs[1] >> 11) != ff ||
+                                (cs[2] >> 11) != ff || (cs[3] >> 11) != ff) &&
+                         a.St.F.regular[ff];
+        if (uni) {
+          const unsigned mask = a.St.F.rmask[ff];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int lc = 2 * t + (e & 1) + (e >> 1) * (W / 2);
+            xv[e] = sM[lc];
+            qv[e] = rm_q_uni(cs[e], dM[e].x, xv[e], mask, sU, sM, sD, lc, ng0, nleak);
+          }
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int lc = 2 * t + (e & 1) + (e >> 1) * (W / 2);
+            xv[e] = sM[lc];
+            qv[e] = rm_q(cs[e], dM[e].x, xv[e], s_rpos[cs[e] >> 11], sU, sM, sD, lc, ng0, nleak);
+          }
+        }
+        const unsigned im = (unsigned)(mid * m + cA);
+        const unsigned oqa = qok ? im * 8u : kOOB, oqb = qok ? (im + W / 2) * 8u : kOOB;
+        if (MODE == kMarchB) {
+          const double rv[4] = {r2a.x, r2a.y, r2b.x, r2b.y};
+          double rn[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) rn[e] = rv[e] - ak * qv[e];
+          bst2<kNT>(rr, oqa, make_double2(rn[0], rn[1]));
+          bst2<kNT>(rr, oqb, make_double2(rn[2], rn[3]));
+          if (qok) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const double z = div_tab(rn[e], dM[e]);
+              acc[0] = acc[0] + z * rn[e];
+            }
+#pragma unroll
+            for (int e = 0; e < 4; ++e) acc[1] = acc[1] + rn[e] * rn[e];
+          }
+        } else {
+          if (MODE == kMarchPQ) {
+            bst2<kNT>(rq, oqa, make_double2(qv[0], qv[1]));
+            bst2<kNT>(rq, oqb, make_double2(qv[2], qv[3]));
+          }
+          if (qok) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) acc[0] = acc[0] + qv[e] * xv[e];
+          }
+        }
+      }
+      c2a = c1a;
+      c2b = c1b;
+      c1a = R.ca;
+      c1b = R.cb;
+      if (MODE == kMarchB) {
+        r2a = r1a;
+        r2b = r1b;
+        r1a = R.ra;
+        r1b = R.rb;
+      }
+      lds_barrier();
     }
   }
 }
@@ -1539,7 +2131,8 @@ CGArgs make_cg_args(perc_ctx* h) {
   CGArgs a;
   a.A = CsrView{h->N, h->d.rowptr, h->d.col, h->d.val, h->d.diag};
   a.St = StencilView{h->N, h->d.code, h->st_ng0, h->st_nleak, h->forms, h->d.dtab};
-  a.T = TileGeom{h->g.m, h->g.n - 2, h->g.pbc, (h->g.m + kTileW - 1) / kTileW, h->march_h};
+  a.T = TileGeom{h->g.m, h->g.n - 2, h->g.pbc, (h->g.m + kTileW - 1) / kTileW, h->march_h,
+                 h->rm_h};
   a.pb[0] = h->d.p0;
   a.pb[1] = h->d.p1;
   a.fused = h->fused ? 1 : 0;
@@ -1548,9 +2141,9 @@ CGArgs make_cg_args(perc_ctx* h) {
   // the next tiled kernel starts on the r that B wrote last (measured: B
   // 0.112 -> 0.097 ms at L = 4096)
   a.b_reverse = h->fused ? 1 : 0;
-  static const int nt_env = getenv("PERC_NT") ? atoi(getenv("PERC_NT")) : 1;
-  a.nt = nt_env;
   a.kiter = 1;
+  a.march_alt = h->march_alt ? 1 : 0;
+  a.bx = (h->march || h->rowmarch) && !h->qfree ? 1 : 0;
   a.xrows = h->full_voltages || h->g.m <= 0 ? 0 : h->g.m;  // see dev_solve
   a.pstride = red_partials_size(red_grid(h));
   a.tstride = red_tickets_size(red_grid(h));
@@ -1573,8 +2166,24 @@ void launch_cg_spmv(perc_ctx* h, const CGArgs& a, int G) {
     const int th = h->tile_h;
     const dim3 G2(h->tile_grid), B2(tile_threads(th));
     hipStream_t st = h->stream;
+    if (h->rowmarch) {
+      const dim3 g(h->rm_grid), b(h->rm_w / 4);
+      const bool qf = h->qfree;
+      if (h->rm_w == 2048) {
+        if (qf) k_cg_rm<kMarchP, 2048><<<g, b, 0, st>>>(a);
+        else k_cg_rm<kMarchPQ, 2048><<<g, b, 0, st>>>(a);
+      } else if (h->rm_w == 1024) {
+        if (qf) k_cg_rm<kMarchP, 1024><<<g, b, 0, st>>>(a);
+        else k_cg_rm<kMarchPQ, 1024><<<g, b, 0, st>>>(a);
+      } else {
+        if (qf) k_cg_rm<kMarchP, 512><<<g, b, 0, st>>>(a);
+        else k_cg_rm<kMarchPQ, 512><<<g, b, 0, st>>>(a);
+      }
+      return;
+    }
     if (h->march) {
-      k_cg_pm<<<h->march_grid, 64 * kMarchWaves, 0, st>>>(a);
+      if (h->qfree) k_cg_march<kMarchP><<<h->march_grid, 64 * kMarchWaves, 0, st>>>(a);
+      else k_cg_march<kMarchPQ><<<h->march_grid, 64 * kMarchWaves, 0, st>>>(a);
       return;
     }
     if (h->g.scn == 4) {
@@ -1593,7 +2202,14 @@ void launch_cg_spmv(perc_ctx* h, const CGArgs& a, int G) {
 
 // B(k) (streaming; the fused format walks its chunks in reverse)
 void launch_cg_b(perc_ctx* h, const CGArgs& a, int G) {
-  if (h->stencil) {
+  if (h->rowmarch && h->qfree) {
+    const dim3 g(h->rm_grid), b(h->rm_w / 4);
+    if (h->rm_w == 2048) k_cg_rm<kMarchB, 2048><<<g, b, 0, h->stream>>>(a);
+    else if (h->rm_w == 1024) k_cg_rm<kMarchB, 1024><<<g, b, 0, h->stream>>>(a);
+    else k_cg_rm<kMarchB, 512><<<g, b, 0, h->stream>>>(a);
+  } else if (h->march && h->qfree) {
+    k_cg_march<kMarchB><<<h->march_grid, 64 * kMarchWaves, 0, h->stream>>>(a);
+  } else if (h->stencil) {
     k_cg_b<true><<<G, kBlock, 0, h->stream>>>(a);
   } else {
     k_cg_b<false><<<G, kBlock, 0, h->stream>>>(a);
@@ -1648,6 +2264,16 @@ StencilForms stencil_forms(const Geom& g) {
       F.rmask[f] |= 1u << kp;
       if (kp <= last) F.regular[f] = 0;
       last = kp;
+    }
+    F.rmap[f] = kRmapIrregular;
+    if (F.regular[f]) {
+      F.rmap[f] = 0xFFFFFFFFu;
+      for (int j = 0; j < F.cnt[f]; ++j) {
+        const unsigned kp = (F.rpos[f] >> (3 * j)) & 7u;
+        F.rmap[f] &= ~(0xFu << (4 * kp));
+        F.rmap[f] |= (unsigned)j << (4 * kp);
+      }
+      F.umask |= F.rmask[f];
     }
   }
   return F;
@@ -1726,7 +2352,7 @@ hipError_t dev_build_lattice(perc_ctx* h) {
   HIP_TRY(dmalloc(&d.diag, N + 2));
   HIP_TRY(dmalloc(&d.rhs, N + 2));
   HIP_TRY(dmalloc(&d.code, (size_t)N + 8));
-  HIP_TRY(dmalloc(&d.dtab, kDiagTab));
+  HIP_TRY(dmalloc(&d.dtab, kDiagTab));  // double2 entries
   h->forms = stencil_forms(g);
   HIP_TRY(dmalloc(&d.sflag, 4));
   // occupancy + labeling
@@ -1892,6 +2518,26 @@ void march_geometry(perc_ctx* h) {
       h->march_h /= 2;
   }
   h->march_grid = cdiv(spr * cdiv(nrows, h->march_h), kMarchWaves);
+  // workgroup row-march: the widest strip of 2048 / 1024 / 512 columns that
+  // divides m, the tallest band (32 .. 2 rows) that gives >= kRmMinGroups
+  // workgroups (two per CU), or the requested height
+  h->rm_grid = 0;
+  h->rm_w = g.m % 2048 == 0 ? 2048 : (g.m % 1024 == 0 ? 1024 : (g.m % 512 == 0 ? 512 : 0));
+  if (((long long)h->N + 2) * 8 >= (1ll << 31)) h->rm_w = 0;  // buffer offsets (kOOB)
+  if (h->rm_w == 0) return;
+  const int rspr = g.m / h->rm_w;
+  if (h->march_rows_req > 0) {
+    h->rm_h = h->march_rows_req;
+  } else {
+    h->rm_h = 32;
+    while (h->rm_h > 8 && (long long)rspr * cdiv(nrows, h->rm_h) < kRmMinGroups) h->rm_h /= 2;
+    // below 8-row bands the two halo rows per band cost more than the
+    // row segments gain: the per-wave march is used (L = 1024: 0.0285 vs
+    // 0.0294 ms per iteration)
+    if ((long long)rspr * cdiv(nrows, h->rm_h) < kRmMinGroups) h->rm_w = 0;
+  }
+  if (h->rm_w == 0) return;
+  h->rm_grid = rspr * cdiv(nrows, h->rm_h);
 }
 
 // solver kernels for the requested format and what the assembly allows
@@ -1899,6 +2545,11 @@ void select_format(perc_ctx* h) {
   h->stencil = h->fmt_req != PERC_FMT_CSR && h->stencil_ok;
   h->fused = h->stencil && h->tiled_ok && h->fmt_req != PERC_FMT_STENCIL_SPLIT;
   h->march = h->fused && h->march_ok && h->fmt_req != PERC_FMT_STENCIL_TILED;
+  h->rowmarch = h->fused && h->rm_grid > 0 && h->fmt_req != PERC_FMT_STENCIL_TILED &&
+                (h->march_mode & PERC_MARCH_ROWS);
+  h->march = h->march && !h->rowmarch;
+  h->qfree = (h->march || h->rowmarch) && (h->march_mode & PERC_MARCH_QFREE);
+  h->march_alt = (h->march || h->rowmarch) && (h->march_mode & PERC_MARCH_ALT);
 }
 
 hipError_t dev_assemble(perc_ctx* h, int rule, double g0, double leak, double Va, int span_root) {
@@ -2019,7 +2670,7 @@ hipError_t dev_solve(perc_ctx* h, int itol, double tol, int itmax, bool x0_zero,
     if (launched > (long long)itmax + 2) break;  // cannot happen: device stops at itmax+1
     chunk = std::min(chunk * 2, kMaxChunk);
   }
-  if (e == hipSuccess && hsp->iter > 0) {
+  if (e == hipSuccess && hsp->iter > 0 && !a.bx) {
     k_cg_xfinal<<<G, kBlock, 0, st>>>(a);
     e = dbg_sync(st, "k_cg_xfinal");
     if (e == hipSuccess) e = hipStreamSynchronize(st);
@@ -2053,6 +2704,16 @@ hipError_t dev_spmv(perc_ctx* h, const double* x, double* y) {
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipMemcpyAsync(y, d.q, bytes, hipMemcpyDeviceToHost, st));
   return hipStreamSynchronize(st);
+}
+
+hipError_t dev_selftest_division(long long n, unsigned long long seed, unsigned long long* out3) {
+  unsigned long long* d = nullptr;
+  HIP_TRY(dmalloc(&d, 3));
+  HIP_TRY(hipMemset(d, 0, 3 * sizeof(unsigned long long)));
+  k_selftest_div<<<4096, kBlock>>>(n, seed, d);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipMemcpy(out3, d, 3 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+  return hipFree(d);
 }
 
 hipError_t dev_bench(perc_ctx* h, int which, int reps, double* ms) {
@@ -2093,6 +2754,13 @@ hipError_t dev_bench(perc_ctx* h, int which, int reps, double* ms) {
     } else if (which == 3) {
       if (ST) k_cg_p<true><<<G, kBlock, 0, st>>>(a);
       else k_cg_p<false><<<G, kBlock, 0, st>>>(a);
+    } else if (which == 5) {  // one whole iteration
+      if (!h->fused) {
+        if (ST) k_cg_p<true><<<G, kBlock, 0, st>>>(a);
+        else k_cg_p<false><<<G, kBlock, 0, st>>>(a);
+      }
+      launch_cg_spmv(h, a, G);
+      launch_cg_b(h, a, G);
     } else {
       k_copy<<<8192, kBlock, 0, st>>>(cp_src, cp_dst, (int)cp_n);
     }

@@ -718,16 +718,39 @@ int perc_set_march_rows(perc_ctx* h, int rows) {
   return PERC_OK;
 }
 
+int perc_set_march_mode(perc_ctx* h, int mode) {
+  if (!h || mode < 0 || mode > (PERC_MARCH_QFREE | PERC_MARCH_ALT | PERC_MARCH_ROWS)) return PERC_EINVAL;
+  h->march_mode = mode;
+  if (h->assembled) select_format(h);
+  return PERC_OK;
+}
+
+int perc_march_info(perc_ctx* h, int* out5) {
+  if (!h || !out5) return PERC_EINVAL;
+  if (!h->assembled) return PERC_ESTATE;
+  out5[0] = h->rowmarch ? 2 : (h->march ? 1 : 0);
+  out5[1] = h->qfree ? 1 : 0;
+  out5[2] = h->march_alt ? 1 : 0;
+  out5[3] = h->rowmarch ? h->rm_h : (h->march ? h->march_h : 0);
+  out5[4] = h->rowmarch ? h->rm_w : (h->march ? 128 : 0);
+  return PERC_OK;
+}
+
 int perc_matrix_format(perc_ctx* h) {
   if (!h) return PERC_EINVAL;
   if (!h->assembled) return PERC_ESTATE;
   if (!h->stencil) return PERC_FMT_CSR;
   if (!h->fused) return PERC_FMT_STENCIL_SPLIT;
-  return h->march ? PERC_FMT_STENCIL : PERC_FMT_STENCIL_TILED;
+  return h->march || h->rowmarch ? PERC_FMT_STENCIL : PERC_FMT_STENCIL_TILED;
+}
+
+int perc_selftest_division(long long n, unsigned long long seed, unsigned long long* out3) {
+  if (n < 0 || !out3) return PERC_EINVAL;
+  return hip_status(dev_selftest_division(n, seed, out3), "perc_selftest_division");
 }
 
 int perc_bench_kernel(perc_ctx* h, int which, int reps, double* ms) {
-  if (!h || !ms || reps <= 0 || which < 0 || which > 4) return PERC_EINVAL;
+  if (!h || !ms || reps <= 0 || which < 0 || which > 5) return PERC_EINVAL;
   if (!h->assembled && which != 4) return PERC_ESTATE;  // the copy needs no system
   hipSetDevice(h->device);
   // the CG kernels clobber the solver vectors (x, r, p, q), not the system

@@ -36,7 +36,13 @@ struct StencilForms {
   unsigned rpos[kMaxForms];
   unsigned rmask[kMaxForms];
   int regular[kMaxForms];
+  // inverse of rpos for regular forms: 4-bit field kp = slot index of
+  // raster position kp, 0xF where the form has no neighbour there;
+  // kRmapIrregular for forms whose slot order is not raster order
+  unsigned rmap[kMaxForms];
+  unsigned umask;  // union of rmask over the regular forms
 };
+constexpr unsigned kRmapIrregular = 0xEEEEEEEEu;
 
 // Device-resident CG scalars (one cache line each group; written only by the
 // last-arriving workgroup of a kernel, read by the next kernel).
@@ -69,7 +75,7 @@ struct DeviceBuffers {
   // slot j carries -g0, else -leak) | count << 8 | form << 11; sflag[0] != 0
   // if some slot has no bond (1) or a row matches no form (2)
   uint16_t* code = nullptr;  // N (+pad)
-  double* dtab = nullptr;    // 512: the diagonal of every code (see diag_idx)
+  double2* dtab = nullptr;    // 512: the diagonal of every code (see diag_idx)
   int* sflag = nullptr;      // 4
   // occupancy
   uint8_t* bocc = nullptr;  // nb
@@ -146,6 +152,12 @@ struct perc_ctx {
   int march_grid = 0;           // its workgroups
   int march_grid_max = 0;       // workgroups at band height 1 (reduction buffers)
   int march_rows_req = 0;       // perc_set_march_rows (0: auto)
+  int march_mode = PERC_MARCH_DEFAULT;  // perc_set_march_mode
+  bool qfree = false;           // march B rebuilds q (52N / iteration)
+  bool march_alt = false;       // alternating walk directions
+  bool rowmarch = false;        // workgroup row-march kernels (k_cg_rm)
+  int rm_w = 0, rm_h = 16;      // their strip width (columns) and band height
+  int rm_grid = 0;              // their workgroups
   bool full_voltages = false;   // perc_set_full_voltages: keep x on every row
   double st_ng0 = 0.0, st_nleak = 0.0;  // its two off-diagonal values
   perc::StencilForms forms{};            // row forms of this lattice
@@ -172,6 +184,7 @@ hipError_t dev_solve(perc_ctx* h, int itol, double tol, int itmax, bool x0_zero,
 hipError_t dev_currents(perc_ctx* h, int rule, int cur_rule, double g0, double leak, double Va,
                         int span_root, double thresh, double* iout_host);
 hipError_t dev_spmv(perc_ctx* h, const double* x, double* y);
+hipError_t dev_selftest_division(long long n, unsigned long long seed, unsigned long long* out3);
 hipError_t dev_bench(perc_ctx* h, int which, int reps, double* ms);
 
 // host replay (perc_replay.cpp): reference label numbering

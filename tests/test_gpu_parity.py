@@ -462,8 +462,16 @@ def test_full_size_properties(L_, p):
         assert abs(c["gtop"] - c["gbot"]) < 1e-8
 
 
+MARCH_MODES = (PL.MARCH_DEFAULT, 0, PL.MARCH_QFREE, PL.MARCH_ALT, PL.MARCH_ROWS,
+               PL.MARCH_ROWS | PL.MARCH_QFREE, PL.MARCH_ROWS | PL.MARCH_ALT,
+               PL.MARCH_ROWS | PL.MARCH_QFREE | PL.MARCH_ALT)
+
+
 @pytest.mark.parametrize("lat,m,n,pbc,p", [(0, 256, 150, 0, 0.6), (1, 128, 99, 1, 0.42),
-                                           (0, 384, 40, 1, 0.55)])
+                                           (0, 384, 40, 1, 0.55),
+                                           # workgroup row-march strips of 512 / 1024 / 2048
+                                           (0, 1536, 40, 1, 0.55), (1, 1024, 45, 0, 0.42),
+                                           (0, 2048, 21, 0, 0.6), (1, 512, 70, 1, 0.42)])
 def test_march_band_heights(lat, m, n, pbc, p):
     """Register-march kernel at band heights from 1 row to more than the
     lattice (partial last band, single band), against the LDS-tiled kernel:
@@ -479,11 +487,50 @@ def test_march_band_heights(lat, m, n, pbc, p):
         ref = ctx.conductance(tol=1e-12, itmax=100000, vint=True)
         assert ctx.matrix_format() == PL.FMT_STENCIL_TILED
         ctx.set_matrix_format(PL.FMT_STENCIL)
-        for rows in (1, 2, 3, 7, 32, 64):
-            ctx.set_march_rows(rows)
-            c = ctx.conductance(tol=1e-12, itmax=100000, vint=True)
-            assert ctx.matrix_format() == PL.FMT_STENCIL
-            assert abs(c["iter"] - ref["iter"]) <= 2, rows
-            assert rel(c["gtop"], ref["gtop"]) < REL and rel(c["gbot"], ref["gbot"]) < REL, rows
-            assert np.max(np.abs(c["vint"] - ref["vint"])) < 1e-6, rows
+        for mode in MARCH_MODES:
+            ctx.set_march_mode(mode)
+            for rows in (1, 2, 3, 7, 32, 64):
+                ctx.set_march_rows(rows)
+                c = ctx.conductance(tol=1e-12, itmax=100000, vint=True)
+                assert ctx.matrix_format() == PL.FMT_STENCIL
+                assert abs(c["iter"] - ref["iter"]) <= 2, (mode, rows)
+                assert rel(c["gtop"], ref["gtop"]) < REL, (mode, rows)
+                assert rel(c["gbot"], ref["gbot"]) < REL, (mode, rows)
+                assert np.max(np.abs(c["vint"] - ref["vint"])) < 1e-6, (mode, rows)
         ctx.set_march_rows(0)
+        ctx.set_march_mode(PL.MARCH_DEFAULT)
+
+
+@pytest.mark.parametrize("lat,m,n,pbc,p", [(0, 256, 150, 0, 0.6), (1, 256, 99, 0, 0.42),
+                                           (0, 384, 40, 1, 0.55), (1, 128, 64, 1, 0.42),
+                                           (0, 1024, 50, 1, 0.55), (1, 2048, 30, 0, 0.42)])
+def test_march_modes_one_iteration_bitwise(lat, m, n, pbc, p):
+    """Every march mode computes the same per-row numbers: with itmax = 1
+    (one iteration: p = r/d, q = A p, r -= ak q, one stop test) the voltages
+    agree with the split kernels up to ak's association only -- and with
+    the same ak they would be bitwise; here: 1e-13 relative."""
+    nb = api.nbonds(lat, m, n, pbc)
+    order = api.shuffled_ids(nb, 4321)
+    with api.Context(lat, m, n, pbc) as ctx:
+        ctx.occupy(PL.BOND, bond_order=order, nbonds_=int(p * nb))
+        if ctx.label()["nspan"] == 0:
+            pytest.skip("no spanning cluster")
+        ctx.set_matrix_format(PL.FMT_STENCIL_SPLIT)
+        ref = ctx.conductance(tol=1e-30, itmax=3, vint=True)
+        ctx.set_matrix_format(PL.FMT_STENCIL)
+        for mode in MARCH_MODES:
+            ctx.set_march_mode(mode)
+            c = ctx.conductance(tol=1e-30, itmax=3, vint=True)
+            assert c["iter"] == ref["iter"]
+            assert np.max(np.abs(c["vint"] - ref["vint"])) <= 1e-13 * np.max(np.abs(ref["vint"]))
+            assert rel(c["err"], ref["err"]) < 1e-12
+
+
+def test_table_division_is_ieee_division():
+    """The solver forms z = r/d as div_tab(r, {d, RN(1/d)}) (one product and
+    two fmas); bitwise IEEE division over 2^30 random pairs (a over 600
+    binades and signed zeros, d = Kirchhoff diagonals and random values)."""
+    out = np.zeros(3, dtype=np.uint64)
+    for seed in (1, 0xC0FFEE):
+        assert P.lib().perc_selftest_division(1 << 29, seed, out.ctypes.data) == 0
+        assert out[0] == 0, (int(out[0]), np.array(out[1:]).view(np.float64))

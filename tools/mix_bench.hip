@@ -145,24 +145,32 @@ __global__ void k_ps_seq(const dvec2* __restrict__ pold, const dvec2* __restrict
 // march-shaped pure stream: the register-march kernel's access pattern
 // (wave = 128-column strip x H-row band, rows r0-1 .. r0+H read, rows
 // r0 .. r0+H-1 written, D rows prefetched) with trivial arithmetic
-template <int D, int PPL>
+// (row-major: strip stride 128*PPL, row pitch m; strip-major: strip stride
+// nrows*128*PPL, row pitch 128*PPL -- every wave then walks one contiguous
+// stream; HALO adds the halo-column scalar loads of lanes 0 and 63)
+template <int D, int PPL, bool HALO>
 __global__ __launch_bounds__(256) void k_march_stream(const double* __restrict__ pold,
                                                       const double* __restrict__ r,
                                                       const unsigned short* __restrict__ code,
                                                       double* __restrict__ pnew,
                                                       double* __restrict__ q, int m, int pitch,
-                                                      int nrows, int H) {
+                                                      long long spitch, int nrows, int H) {
   const int lane = threadIdx.x & 63;
   const int w = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int spr = m / (128 * PPL);
   const int band = w / spr, strip = w - band * spr;
   const int r0 = band * H;
   if (r0 >= nrows) return;
-  const int col = strip * 128 * PPL + 2 * lane;
+  const long long col = strip * spitch + 2 * lane;
   const int rend = min(r0 + H, nrows), nsteps = rend - r0 + 2;
+  const long long hcol = lane == 0 ? (strip > 0 ? col - 2 - spitch + 128 * PPL : col)
+                                   : (strip + 1 < spr ? col - 126 + spitch : col);
+  const bool hok = HALO && (lane == 0 || lane == 63);
   struct Row {
     dvec2 p[PPL], rr[PPL];
     unsigned c[PPL];
+    double hp, hr;
+    unsigned hc;
   };
   auto load = [&](int gr, Row& R) {
 #pragma unroll
@@ -177,6 +185,14 @@ __global__ __launch_bounds__(256) void k_march_stream(const double* __restrict__
         R.p[k] = *reinterpret_cast<const dvec2*>(pold + i);
         R.rr[k] = *reinterpret_cast<const dvec2*>(r + i);
         R.c[k] = *reinterpret_cast<const unsigned*>(code + i);
+      }
+      R.hp = R.hr = 0.0;
+      R.hc = 0;
+      if (hok) {
+        const long long hi = (long long)gr * pitch + hcol;
+        R.hp = pold[hi];
+        R.hr = r[hi];
+        R.hc = code[hi];
       }
     }
   };
@@ -196,7 +212,8 @@ __global__ __launch_bounds__(256) void k_march_stream(const double* __restrict__
         const int gr = r0 - 1 + j;
 #pragma unroll
         for (int k = 0; k < PPL; ++k) {
-          const dvec2 pn = 0.5 * R.p[k] + R.rr[k] + (double)(R.c[k] & 3);
+          dvec2 pn = 0.5 * R.p[k] + R.rr[k] + (double)(R.c[k] & 3);
+          if (HALO && k == 0) pn.x += R.hp * R.hr + (double)(R.hc & 1);
           if (gr >= r0 && gr < rend) {
             const long long i = (long long)gr * pitch + col + 128 * k;
             __builtin_nontemporal_store(pn, reinterpret_cast<dvec2*>(pnew + i));
@@ -206,6 +223,93 @@ __global__ __launch_bounds__(256) void k_march_stream(const double* __restrict__
             __builtin_nontemporal_store(prev[k] + pn, reinterpret_cast<dvec2*>(q + i));
           }
           prev[k] = pn;
+        }
+      }
+    }
+  }
+}
+
+
+// workgroup row-march: a workgroup owns a strip of W columns (W/4 threads,
+// column pairs 2t and 2t + W/2) and an H-row band; each step loads one row
+// of the strip (p, r, code; D rows ahead in registers), forms the new p row
+// into a 4-slot LDS ring, one barrier, then the previous row's neighbour sum
+// from LDS.  UPALT: odd bands walk up (shared halo rows read together).
+template <int D, int W, bool UPALT>
+__global__ __launch_bounds__(W / 4) void k_rowmarch(const double* __restrict__ pold,
+                                                     const double* __restrict__ r,
+                                                     const unsigned short* __restrict__ code,
+                                                     double* __restrict__ pnew,
+                                                     double* __restrict__ q, int m, int nrows,
+                                                     int H) {
+  extern __shared__ double s_ring[];  // 4 slots x (W + 2)
+  constexpr int T = W / 4, SL = W + 2;
+  const int t = threadIdx.x;
+  const int spr = m / W;
+  const int band = blockIdx.x / spr, strip = blockIdx.x - band * spr;
+  const int r0 = band * H;
+  if (r0 >= nrows) return;
+  const int rend = min(r0 + H, nrows), nsteps = rend - r0 + 2;
+  const bool up = UPALT && (band & 1);
+  const int cA = strip * W + 2 * t, cB = cA + W / 2;
+  struct Row {
+    dvec2 pa, pb, ra, rb;
+    unsigned ca, cb;
+  };
+  auto rowof = [&](int j) { return up ? rend - j : r0 - 1 + j; };
+  auto load = [&](int gr, Row& R) {
+    R.pa = R.pb = R.ra = R.rb = dvec2{0.0, 0.0};
+    R.ca = R.cb = 0;
+    if (gr >= 0 && gr < nrows) {
+      const long long i = (long long)gr * m;
+      R.pa = *reinterpret_cast<const dvec2*>(pold + i + cA);
+      R.pb = *reinterpret_cast<const dvec2*>(pold + i + cB);
+      R.ra = *reinterpret_cast<const dvec2*>(r + i + cA);
+      R.rb = *reinterpret_cast<const dvec2*>(r + i + cB);
+      R.ca = *reinterpret_cast<const unsigned*>(code + i + cA);
+      R.cb = *reinterpret_cast<const unsigned*>(code + i + cB);
+    }
+  };
+  Row ring[D];
+#pragma unroll
+  for (int u = 0; u < D; ++u) load(rowof(u), ring[u]);
+  if (t < 4) {  // zero halo columns of every slot
+    s_ring[t * SL] = 0.0;
+    s_ring[t * SL + W + 1] = 0.0;
+  }
+  for (int j0 = 0; j0 < nsteps; j0 += D) {
+#pragma unroll
+    for (int u = 0; u < D; ++u) {
+      const int j = j0 + u;
+      if (j < nsteps) {
+        const Row R = ring[u];
+        if (j + D < nsteps) load(rowof(j + D), ring[u]);
+        const int gr = rowof(j);
+        const dvec2 pa = 0.5 * R.pa + R.ra + (double)(R.ca & 3);
+        const dvec2 pb = 0.5 * R.pb + R.rb + (double)(R.cb & 3);
+        double* sl = s_ring + (j & 3) * SL + 1;
+        *reinterpret_cast<dvec2*>(sl + 2 * t) = pa;
+        *reinterpret_cast<dvec2*>(sl + 2 * t + W / 2) = pb;
+        if (gr >= r0 && gr < rend) {
+          const long long i = (long long)gr * m;
+          __builtin_nontemporal_store(pa, reinterpret_cast<dvec2*>(pnew + i + cA));
+          __builtin_nontemporal_store(pb, reinterpret_cast<dvec2*>(pnew + i + cB));
+        }
+        __syncthreads();
+        const int mid = up ? gr + 1 : gr - 1;
+        if (j >= 2 && mid >= r0 && mid < rend) {
+          const double* sm = s_ring + ((j - 1) & 3) * SL + 1;
+          const double* su = s_ring + ((j - 2) & 3) * SL + 1;
+          const double* sn = sl;
+          dvec2 qa, qb;
+          qa.x = sm[2 * t] * 4.0 - sm[2 * t - 1] - sm[2 * t + 1] - su[2 * t] - sn[2 * t];
+          qa.y = sm[2 * t + 1] * 4.0 - sm[2 * t] - sm[2 * t + 2] - su[2 * t + 1] - sn[2 * t + 1];
+          const int b = 2 * t + W / 2;
+          qb.x = sm[b] * 4.0 - sm[b - 1] - sm[b + 1] - su[b] - sn[b];
+          qb.y = sm[b + 1] * 4.0 - sm[b] - sm[b + 2] - su[b + 1] - sn[b + 1];
+          const long long i = (long long)mid * m;
+          __builtin_nontemporal_store(qa, reinterpret_cast<dvec2*>(q + i + cA));
+          __builtin_nontemporal_store(qb, reinterpret_cast<dvec2*>(q + i + cB));
         }
       }
     }
@@ -276,16 +380,25 @@ int main(int argc, char** argv) {
     struct MV {
       const char* name;
       void (*k)(const double*, const double*, const unsigned short*, double*, double*, int, int,
-                int, int);
-      int ppl, pitch, H;
+                long long, int, int);
+      int ppl, pitch;
+      long long spitch;
+      int H;
     };
-    std::vector<MV> mvs = {{"ppl1 pitch4096 H32", k_march_stream<2, 1>, 1, 4096, 32},
-                           {"ppl1 pitch4096 H16", k_march_stream<2, 1>, 1, 4096, 16},
-                           {"ppl1 pitch4160 H32", k_march_stream<2, 1>, 1, 4160, 32},
-                           {"ppl2 pitch4096 H32", k_march_stream<2, 2>, 2, 4096, 32},
-                           {"ppl2 pitch4096 H16", k_march_stream<2, 2>, 2, 4096, 16},
-                           {"ppl4 pitch4096 H16", k_march_stream<2, 4>, 4, 4096, 16},
-                           {"ppl4 pitch4096 H8", k_march_stream<2, 4>, 4, 4096, 8}};
+    const long long sm = (long long)nrows * 128;  // strip-major strip stride (PPL 1)
+    std::vector<MV> mvs = {
+        {"rowmaj D2 H32", k_march_stream<2, 1, false>, 1, 4096, 128, 32},
+        {"rowmaj D2 H32 halo", k_march_stream<2, 1, true>, 1, 4096, 128, 32},
+        {"rowmaj D3 H32 halo", k_march_stream<3, 1, true>, 1, 4096, 128, 32},
+        {"rowmaj D4 H32 halo", k_march_stream<4, 1, true>, 1, 4096, 128, 32},
+        {"stripmaj D2 H32", k_march_stream<2, 1, false>, 1, 128, sm, 32},
+        {"stripmaj D2 H32 halo", k_march_stream<2, 1, true>, 1, 128, sm, 32},
+        {"stripmaj D3 H32 halo", k_march_stream<3, 1, true>, 1, 128, sm, 32},
+        {"stripmaj D4 H32 halo", k_march_stream<4, 1, true>, 1, 128, sm, 32},
+        {"stripmaj D2 H64 halo", k_march_stream<2, 1, true>, 1, 128, sm, 64},
+        {"stripmaj D4 H64 halo", k_march_stream<4, 1, true>, 1, 128, sm, 64},
+        {"rowmaj ppl2 D2 H16 halo", k_march_stream<2, 2, true>, 2, 4096, 256, 16},
+        {"stripmaj ppl2 D2 H16 halo", k_march_stream<2, 2, true>, 2, 256, 2 * sm, 16}};
     for (auto& mv : mvs) {
       const int waves = (m / (128 * mv.ppl)) * ((nrows + mv.H - 1) / mv.H), grid = (waves + 3) / 4;
       std::vector<hipEvent_t> ev(3);
@@ -295,8 +408,8 @@ int main(int argc, char** argv) {
         const double* po = (const double*)((k & 1) ? B.c : B.a);
         double* pn = (double*)((k & 1) ? B.a : B.c);
         CHK(hipEventRecord(ev[0]));
-        mv.k<<<grid, 256>>>(po, (const double*)B.b, code16, pn, (double*)B.d, m, mv.pitch, nrows,
-                             mv.H);
+        mv.k<<<grid, 256>>>(po, (const double*)B.b, code16, pn, (double*)B.d, m, mv.pitch,
+                             mv.spitch, nrows, mv.H);
         CHK(hipEventRecord(ev[1]));
         k_b_seq<true, false><<<8192, 256>>>(B.d, B.b, code, n);
         CHK(hipEventRecord(ev[2]));
@@ -310,6 +423,54 @@ int main(int argc, char** argv) {
         }
       }
       printf("march-stream %-20s in sequence: march %.4f ms  b-like %.4f ms\n", mv.name,
+             tps / (2 * reps), tb / (2 * reps));
+    }
+  }
+  {
+    const int m = 4096, nrows = 4094;
+    const unsigned short* code16 = reinterpret_cast<const unsigned short*>(code);
+    struct RV {
+      const char* name;
+      void (*k)(const double*, const double*, const unsigned short*, double*, double*, int, int,
+                int);
+      int W, H;
+    };
+    std::vector<RV> rvs = {{"rowmarch W4096 D2 H16", k_rowmarch<2, 4096, false>, 4096, 16},
+                           {"rowmarch W4096 D2 H16 alt", k_rowmarch<2, 4096, true>, 4096, 16},
+                           {"rowmarch W4096 D3 H16 alt", k_rowmarch<3, 4096, true>, 4096, 16},
+                           {"rowmarch W2048 D2 H16 alt", k_rowmarch<2, 2048, true>, 2048, 16},
+                           {"rowmarch W2048 D3 H16 alt", k_rowmarch<3, 2048, true>, 2048, 16},
+                           {"rowmarch W2048 D2 H32 alt", k_rowmarch<2, 2048, true>, 2048, 32},
+                           {"rowmarch W1024 D3 H16 alt", k_rowmarch<3, 1024, true>, 1024, 16},
+                           {"rowmarch W1024 D3 H32 alt", k_rowmarch<3, 1024, true>, 1024, 32}};
+    for (auto& rv : rvs) {
+      const int grid = (m / rv.W) * ((nrows + rv.H - 1) / rv.H);
+      const size_t lds = 4 * (rv.W + 2) * sizeof(double);
+      CHK(hipFuncSetAttribute((const void*)rv.k, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)lds));
+      std::vector<hipEvent_t> ev(3);
+      for (auto& e : ev) CHK(hipEventCreate(&e));
+      double tps = 0, tb = 0;
+      for (int k = 0; k < 2 * reps + 4; ++k) {
+        const double* po = (const double*)((k & 1) ? B.c : B.a);
+        double* pn = (double*)((k & 1) ? B.a : B.c);
+        CHK(hipEventRecord(ev[0]));
+        rv.k<<<grid, rv.W / 4, lds>>>(po, (const double*)B.b, code16, pn, (double*)B.d, m, nrows,
+                                      rv.H);
+        CHK(hipEventRecord(ev[1]));
+        k_b_seq<true, false><<<8192, 256>>>(B.d, B.b, code, n);
+        CHK(hipEventRecord(ev[2]));
+        CHK(hipEventSynchronize(ev[2]));
+        float a1, a2;
+        CHK(hipEventElapsedTime(&a1, ev[0], ev[1]));
+        CHK(hipEventElapsedTime(&a2, ev[1], ev[2]));
+        if (k >= 4) {
+          tps += a1;
+          tb += a2;
+        }
+      }
+      CHK(hipGetLastError());
+      printf("%-28s grid %5d in sequence: march %.4f ms  b-like %.4f ms\n", rv.name, grid,
              tps / (2 * reps), tb / (2 * reps));
     }
   }
