@@ -137,6 +137,10 @@ def kernel_label(key, minfo):
         return "%s %d cols x %d rows%s): fused p = bk p + r/d, x += ak p, q = A p, q.p%s" % (
             name, minfo["strip_cols"], minfo["band_rows"], ", alternating" if minfo["alt"] else "",
             "" if minfo["qfree"] else ", q stored")
+    if key == "res":
+        return ("k_cg_res (resident persistent solve, %d-row bands: p in LDS, r/q in registers, "
+                "2 grid-wide reductions per iteration; HBM bytes = exchanged band-edge rows + x)"
+                % minfo["band_rows"])
     if key == "resid" and minfo.get("qfree"):
         return ("k_cg_rm" if minfo["kernel"] == "rows" else "k_cg_march") + \
             " B (march: q = A p(k) rebuilt, r -= ak q, z = r/d, z.r and r.r dots)"
@@ -144,7 +148,8 @@ def kernel_label(key, minfo):
 
 
 # rocprof kernel names of the CG kernels, per operator format
-ROCPROF_NAMES = {("pm", "stencil"): ("k_cg_rm<0", "k_cg_rm<1", "k_cg_march<0", "k_cg_march<1"),
+ROCPROF_NAMES = {("res", "stencil"): ("k_cg_res",),
+                 ("pm", "stencil"): ("k_cg_rm<0", "k_cg_rm<1", "k_cg_march<0", "k_cg_march<1"),
                  ("ps", "stencil_tiled"): ("k_cg_ps<4>", "k_cg_ps<6>"),
                  ("resid", "stencil_tiled"): ("k_cg_b<true>",),
                  ("spmv", "stencil_split"): ("k_cg_spmv<4>", "k_cg_spmv<6>"),
@@ -337,10 +342,16 @@ def main():
         fmt = {"auto": "stencil"}.get(args.format, args.format)
         assembled = False
 
-    def kernel_set(f):
+    def kernel_set(f, probe=False):
         """(key, stats key, perc_bench_kernel id, bytes) of the CG kernels of
         operator format f"""
         full = args.full_voltages
+        if f == "stencil" and minfo.get("kernel") == "resident" and not probe:
+            # whole iterations in one persistent launch; per iteration it
+            # moves only the exchanged band-edge rows (r, p: 4 rows of m per
+            # band, written and read) and the electrode-adjacent x rows
+            G = -(-(L_ - 2) // max(minfo["band_rows"], 1))
+            return [("res", "spmv", 5, G * 4 * L_ * 8 * 2 + x_bytes(N, L_, full))]
         if f in ("stencil", "stencil_tiled"):
             qf = f == "stencil" and minfo["qfree"]
             return [("pm" if f == "stencil" else "ps", "spmv", 1, ps_bytes(N, L_, full, qf)),
@@ -377,7 +388,7 @@ def main():
             continue
         row = {}
         plain = [] if fname in ("stencil", "stencil_tiled") else [("spmv_plain", "", 0, spmv_bytes(N, nnz, fname))]
-        for key, _, which, nbytes in plain + kernel_set(fname):
+        for key, _, which, nbytes in plain + kernel_set(fname, probe=True):
             ms = ctx.bench_kernel(which, 50)
             row[key] = {"ms": round(ms, 5), "gbs": round(nbytes / (ms * 1e-3) / 1e9, 1)}
         probe[fname] = row

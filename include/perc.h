@@ -250,11 +250,13 @@ int perc_set_march_rows(perc_ctx *h, int rows);
 #define PERC_MARCH_QFREE 1
 #define PERC_MARCH_ALT 2
 #define PERC_MARCH_ROWS 4
-#define PERC_MARCH_DEFAULT PERC_MARCH_ALT
+#define PERC_SOLVE_RESIDENT 8
+#define PERC_MARCH_DEFAULT (PERC_MARCH_ALT | PERC_SOLVE_RESIDENT)
 int perc_set_march_mode(perc_ctx *h, int mode);
 /* Solver loop of the assembled system: out5[0] = 0 (no march kernel: LDS
    tiles, split or CSR), 1 (per-wave march k_cg_march), 2 (workgroup
-   row-march k_cg_rm); out5[1] = q-free B, out5[2] = alternating
+   row-march k_cg_rm), 3 (resident persistent solve k_cg_res); out5[1] =
+   q-free B, out5[2] = alternating
    directions, out5[3] = band height, out5[4] = strip width (columns). */
 int perc_march_info(perc_ctx *h, int *out5);
 

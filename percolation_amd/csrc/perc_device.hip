@@ -1773,6 +1773,10 @@ __device__ __forceinline__ double2 bld2(__amdgpu_buffer_rsrc_t r, unsigned off) 
 __device__ __forceinline__ double bld1(__amdgpu_buffer_rsrc_t r, unsigned off) {
   return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, (int)off, 0, 0));
 }
+// sc1 (agent-coherent) load: data another workgroup stored with sc1
+__device__ __forceinline__ double bld1s(__amdgpu_buffer_rsrc_t r, unsigned off) {
+  return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, (int)off, 0, 16));
+}
 template <int AUX>
 __device__ __forceinline__ void bst2(__amdgpu_buffer_rsrc_t r, unsigned off, double2 v) {
   __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, (int)off, 0, AUX);
@@ -2052,6 +2056,340 @@ __device__ __forceinline__ void rm_walk(const CGArgs& a, RRow (&ring)[D], int t,
       }
       lds_barrier();
     }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Resident persistent solve for small lattices (every band's state fits on
+// chip).  One cooperative launch runs the whole linbcg loop: workgroup w
+// (NT threads, one per CU) owns lattice rows [w H, w H + H) at full width;
+// p of its rows lives in LDS, r, q and the row codes in registers (thread t
+// holds columns t + j NT, j < MT, of every own row).  Per iteration (the
+// order of linbcg, bondc.f:780-835, every per-row operation as in the other
+// kernels):
+//   1. p = bk p + r/d (z = r/d at k = 1) into LDS; the band's first and last
+//      rows also to a write-through exchange buffer;  grid barrier
+//   2. q = A p from LDS and the neighbours' exchanged rows; q.p;  barrier
+//   3. every workgroup sums the q.p partials in workgroup order (the same
+//      value everywhere): ak; r -= ak q, z = r/d, z.r, r.r, x += ak p on
+//      the rows x is kept on;  barrier;  bk, err, stop test (identical in
+//      every workgroup, so all leave the loop together)
+// Three grid barriers and no launches per iteration: at L = 1024 an
+// iteration of the launched kernels is ~28 us, almost all fixed costs.
+// The grid barrier counts arrivals per XCD group (blocks b, b+8, ..) and
+// then per group on one counter, after each workgroup's write-through
+// stores are complete (s_waitcnt vmcnt(0)); data crossing workgroups is
+// written and read with sc1 (agent-scope) accesses, as in
+// publish_and_reduce.  A wait that exceeds ~1 s sets an error flag and
+// leaves the kernel instead of hanging the device.
+constexpr int kResThreads = 1024;
+constexpr int kResLdsRows = 16384;  // own-row p elements per workgroup (128 KB)
+
+struct ResArgs {
+  StencilView St;
+  int m, nrows, pbc, G, H;
+  int xrows;
+  const double* r0;  // r after k_cg_init
+  double* x;
+  CGScalars* S;
+  double* err_hist;
+  int err_hist_cap;
+  double* xch;       // [2 parity][G][top, bottom][r, p][m]
+  double* part;      // [2 parity][3][G]
+  unsigned* bar;     // 9 counters, 128 B apart (zeroed before the launch)
+};
+
+__device__ __forceinline__ bool res_barrier(const ResArgs& a, unsigned& epoch, int* s_flag) {
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    ++epoch;
+    const int G = a.G, grp = blockIdx.x & 7, ngrp = G < 8 ? G : 8;
+    const unsigned ng = (unsigned)((G - grp + 7) / 8);
+    const unsigned old = __hip_atomic_fetch_add(&a.bar[grp * kTicketStride], 1u, __ATOMIC_RELAXED,
+                                                __HIP_MEMORY_SCOPE_AGENT);
+    if (old == epoch * ng - 1)
+      __hip_atomic_fetch_add(&a.bar[8 * kTicketStride], 1u, __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+    int ok = 1;
+    for (unsigned spin = 0;; ++spin) {
+      if (__hip_atomic_load(&a.bar[8 * kTicketStride], __ATOMIC_RELAXED,
+                            __HIP_MEMORY_SCOPE_AGENT) >= epoch * (unsigned)ngrp)
+        break;
+      if (spin > (1u << 25)) {  // ~1 s: give up, report, leave
+        a.S->pad[0] = 1;
+        ok = 0;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+    s_flag[0] = ok;
+  }
+  __syncthreads();
+  return s_flag[0] != 0;
+}
+
+// every workgroup sums the G partials of one slot in workgroup order
+template <int NV>
+__device__ __forceinline__ void res_total(const ResArgs& a, const double* part, double (&tot)[NV],
+                                          double* s_red) {
+  if (threadIdx.x < 64) {
+    const int lane = threadIdx.x;
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+      double acc = 0.0;
+      for (int i = lane; i < a.G; i += 64) acc = acc + load_sc1(&part[(size_t)v * a.G + i]);
+      acc = wave_sum(acc);
+      if (lane == 0) s_red[24 + v] = acc;
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int v = 0; v < NV; ++v) tot[v] = s_red[24 + v];
+  __syncthreads();
+}
+
+// one raster position KP of an element's q (compile-time row / column
+// offsets: the neighbours' rows next to the band come from named registers,
+// never from an indexed register array, which hipcc puts in scratch)
+struct ResHalo {
+  double l, c, r;  // columns c-1, c, c+1
+};
+template <int DC>
+__device__ __forceinline__ double halo_at(const ResHalo& h) {
+  return DC < 0 ? h.l : (DC == 0 ? h.c : h.r);
+}
+template <int KP>
+__device__ __forceinline__ void res_pos(double& acc, unsigned um, unsigned map, unsigned cc, int lr,
+                                        int Hw, int m, int c, const double* s_p, const ResHalo& hu,
+                                        const ResHalo& hd, double ng0, double nleak) {
+  constexpr int DR = KP < 3 ? -1 : (KP < 5 ? 0 : 1);
+  constexpr int DC = KP < 3 ? KP - 1 : (KP == 3 ? -1 : (KP == 4 ? 1 : KP - 6));
+  if (!(um & (1u << KP))) return;  // wave-uniform
+  const int col = c + DC;  // in range for every position a regular form uses
+  double v;
+  if (DR < 0) {
+    v = lr > 0 ? s_p[(lr > 0 ? lr - 1 : 0) * m + col] : halo_at<DC>(hu);
+  } else if (DR > 0) {
+    v = lr + 1 < Hw ? s_p[(lr + 1 < Hw ? lr + 1 : lr) * m + col] : halo_at<DC>(hd);
+  } else {
+    v = s_p[lr * m + col];
+  }
+  const unsigned sj = (map >> (4 * KP)) & 15u;
+  const double gv = ((cc >> sj) & 1u) ? ng0 : nleak;
+  const double pr = gv * v;
+  acc = sj != 15u ? acc + pr : acc;
+}
+
+template <int MT, int HMAX>
+__global__ __launch_bounds__(kResThreads) void k_cg_res(ResArgs a) {
+  __shared__ double s_p[kResLdsRows];
+  __shared__ double2 s_dt[kDiagTab];
+  __shared__ unsigned s_rmap[kMaxForms];
+  __shared__ double s_red[32];
+  __shared__ int s_flag[2];
+  const int t = threadIdx.x, w = blockIdx.x;
+  const int m = a.m, nrows = a.nrows, N = a.St.N, G = a.G;
+  const int R0 = w * a.H, Hw = min(a.H, nrows - R0);  // >= 1 (host sizes G)
+  const bool has_up = R0 > 0, has_dn = R0 + Hw < nrows;
+  const double ng0 = a.St.ng0, nleak = a.St.nleak;
+  CGScalars* S = a.S;
+  if (t < kMaxForms) s_rmap[t] = a.St.F.rmap[t];
+  load_dtab(a.St, s_dt);
+  // own state: r and the codes of (row lr, column t + j NT)
+  double rv[HMAX][MT], qv[HMAX][MT];
+  unsigned cv[HMAX][MT];
+#pragma unroll
+  for (int lr = 0; lr < HMAX; ++lr)
+#pragma unroll
+    for (int j = 0; j < MT; ++j) {
+      const int i = (R0 + lr) * m + t + j * kResThreads;
+      const bool own = lr < Hw;
+      rv[lr][j] = own ? a.r0[i] : 0.0;
+      cv[lr][j] = own ? a.St.code[i] : 0u;
+      qv[lr][j] = 0.0;
+    }
+  // the neighbours' rows next to the band, columns c-1 .. c+1: their codes
+  // (static) and whether the position exists
+  // (column c + d - 1 exists unless c + d - 1 is -1 or m; regular forms
+  // use no wrapped column)
+  auto hin = [&](int j, int d) { const int cc = t + j * kResThreads + d - 1; return cc >= 0 && cc < m; };
+  auto hcol = [&](int j, int d) { const int cc = t + j * kResThreads + d - 1; return cc < 0 ? 0 : (cc >= m ? m - 1 : cc); };
+  unsigned hcu[MT][3], hcd[MT][3];
+#pragma unroll
+  for (int j = 0; j < MT; ++j)
+#pragma unroll
+    for (int d = 0; d < 3; ++d) {
+      hcu[j][d] = has_up && hin(j, d) ? a.St.code[(R0 - 1) * m + hcol(j, d)] : 0u;
+      hcd[j][d] = has_dn && hin(j, d) ? a.St.code[(R0 + Hw) * m + hcol(j, d)] : 0u;
+    }
+  const __amdgpu_buffer_rsrc_t rx = rsrc(a.xch, (unsigned)((size_t)2 * G * 4 * m * 8));
+  // exchange rows: [parity][w][top, bottom][r, p][m]
+  auto xrow = [&](int par, int ww, int tb, int rp) {
+    return a.xch + ((((size_t)par * G + ww) * 2 + tb) * 2 + rp) * m;
+  };
+  // r(1) of the band's first and last rows, for the neighbours' p(1)
+#pragma unroll
+  for (int lr = 0; lr < HMAX; ++lr)
+#pragma unroll
+    for (int j = 0; j < MT; ++j) {
+      const int c = t + j * kResThreads;
+      if (lr == 0) store_sc1(&xrow(1, w, 0, 0)[c], rv[lr][j]);
+      if (lr == Hw - 1) store_sc1(&xrow(1, w, 1, 0)[c], rv[lr][j]);
+    }
+  unsigned epoch = 0;
+  bool ok = res_barrier(a, epoch, s_flag);
+  double bknum = S->bknum, bk = 0.0, ak = 0.0;
+  const double bnrm = S->bnrm, tol = S->tol;
+  const int itmax = S->itmax;
+  int k = 0;
+  double err = 0.0;
+  bool done = !ok;
+  while (!done) {
+    ++k;
+    const int par = k & 1;
+    double* part = a.part + (size_t)par * 3 * G;
+    // 1. halo loads first (their latency overlaps the own rows' p(k))
+    // (buffer loads with sc1, out-of-range offsets for absent positions: one
+    // per-lane offset register for all of them, no branches)
+    double hur[MT][3], hup[MT][3], hdr[MT][3], hdp[MT][3];
+    {
+      const unsigned um = a.St.F.umask;
+      const unsigned bu = (unsigned)((xrow(par, w - 1, 1, 0) - a.xch) * 8);
+      const unsigned bd = (unsigned)((xrow(par, w + 1, 0, 0) - a.xch) * 8);
+      const unsigned rs = (unsigned)m * 8u;  // r -> p row of one exchange slot
+#pragma unroll
+      for (int j = 0; j < MT; ++j)
+#pragma unroll
+        for (int d = 0; d < 3; ++d) {
+          const bool u = has_up && hin(j, d) && (um & (1u << d));
+          const bool dn = has_dn && hin(j, d) && (um & (1u << (5 + d)));
+          const unsigned co = (unsigned)hcol(j, d) * 8u;
+          hur[j][d] = bld1s(rx, u ? bu + co : kOOB);
+          hup[j][d] = bld1s(rx, u && k > 1 ? bu + rs + co : kOOB);
+          hdr[j][d] = bld1s(rx, dn ? bd + co : kOOB);
+          hdp[j][d] = bld1s(rx, dn && k > 1 ? bd + rs + co : kOOB);
+        }
+    }
+    // p(k) of the own rows into LDS
+#pragma unroll
+    for (int lr = 0; lr < HMAX; ++lr)
+#pragma unroll
+      for (int j = 0; j < MT; ++j) {
+        if (lr < Hw) {
+          const int e = lr * m + t + j * kResThreads;
+          const double z = div_tab(rv[lr][j], s_dt[diag_idx(cv[lr][j])]);
+          s_p[e] = k == 1 ? z : bk * s_p[e] + z;
+        }
+      }
+    // p(k) of the neighbours' rows, with the same arithmetic
+    ResHalo hu[MT], hd[MT];
+#pragma unroll
+    for (int j = 0; j < MT; ++j) {
+      double u3[3], d3[3];
+#pragma unroll
+      for (int d = 0; d < 3; ++d) {
+        const double zu = div_tab(hur[j][d], s_dt[diag_idx(hcu[j][d])]);
+        const double zd = div_tab(hdr[j][d], s_dt[diag_idx(hcd[j][d])]);
+        u3[d] = has_up && hin(j, d) ? (k == 1 ? zu : bk * hup[j][d] + zu) : 0.0;
+        d3[d] = has_dn && hin(j, d) ? (k == 1 ? zd : bk * hdp[j][d] + zd) : 0.0;
+      }
+      hu[j] = ResHalo{u3[0], u3[1], u3[2]};
+      hd[j] = ResHalo{d3[0], d3[1], d3[2]};
+    }
+    __syncthreads();
+    // 2. q = A p, q.p
+    double dot = 0.0;
+#pragma unroll
+    for (int lr = 0; lr < HMAX; ++lr)
+#pragma unroll
+      for (int j = 0; j < MT; ++j) {
+        if (lr < Hw) {
+          const int c = t + j * kResThreads;
+          const unsigned cc = cv[lr][j];
+          const double xi = s_p[lr * m + c];
+          // raster positions in order (compile-time row / column offsets):
+          // for the regular forms the resident path is limited to, raster
+          // order is slot order; the slot of position kp comes from rmap
+          const unsigned map = s_rmap[cc >> 11];
+          double acc = s_dt[diag_idx(cc)].x * xi;
+          const unsigned um = a.St.F.umask;
+          res_pos<0>(acc, um, map, cc, lr, Hw, m, c, s_p, hu[j], hd[j], ng0, nleak);
+          res_pos<1>(acc, um, map, cc, lr, Hw, m, c, s_p, hu[j], hd[j], ng0, nleak);
+          res_pos<2>(acc, um, map, cc, lr, Hw, m, c, s_p, hu[j], hd[j], ng0, nleak);
+          res_pos<3>(acc, um, map, cc, lr, Hw, m, c, s_p, hu[j], hd[j], ng0, nleak);
+          res_pos<4>(acc, um, map, cc, lr, Hw, m, c, s_p, hu[j], hd[j], ng0, nleak);
+          res_pos<5>(acc, um, map, cc, lr, Hw, m, c, s_p, hu[j], hd[j], ng0, nleak);
+          res_pos<6>(acc, um, map, cc, lr, Hw, m, c, s_p, hu[j], hd[j], ng0, nleak);
+          res_pos<7>(acc, um, map, cc, lr, Hw, m, c, s_p, hu[j], hd[j], ng0, nleak);
+          qv[lr][j] = acc;
+          dot = dot + acc * xi;
+        }
+        // one element at a time (hoisting every element's LDS reads spills)
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    {
+      double v1[1] = {dot};
+      block_sum<1>(v1, s_red);
+      if (t == 0) store_sc1(&part[w], v1[0]);
+    }
+    if (!(ok = res_barrier(a, epoch, s_flag))) break;
+    {
+      double tot[1];
+      res_total<1>(a, part, tot, s_red);
+      ak = bknum / tot[0];
+    }
+    // 3. r, z, dots, x; the band's first / last rows of r(k+1) and p(k)
+    //    to the exchange for the neighbours' p(k+1)
+    const int npar = (k + 1) & 1;
+    double acc2[2] = {0.0, 0.0};
+#pragma unroll
+    for (int lr = 0; lr < HMAX; ++lr)
+#pragma unroll
+      for (int j = 0; j < MT; ++j) {
+        if (lr < Hw) {
+          const int c = t + j * kResThreads;
+          const double rn = rv[lr][j] - ak * qv[lr][j];
+          rv[lr][j] = rn;
+          const double z = div_tab(rn, s_dt[diag_idx(cv[lr][j])]);
+          acc2[0] = acc2[0] + z * rn;
+          acc2[1] = acc2[1] + rn * rn;
+          const double pk = s_p[lr * m + c];
+          const int i = (R0 + lr) * m + c;
+          if (a.xrows == 0 || i < a.xrows || i >= N - a.xrows) a.x[i] = a.x[i] + ak * pk;
+          if (lr == 0) {
+            store_sc1(&xrow(npar, w, 0, 0)[c], rn);
+            store_sc1(&xrow(npar, w, 0, 1)[c], pk);
+          }
+          if (lr == Hw - 1) {
+            store_sc1(&xrow(npar, w, 1, 0)[c], rn);
+            store_sc1(&xrow(npar, w, 1, 1)[c], pk);
+          }
+        }
+      }
+    block_sum<2>(acc2, s_red);
+    if (t == 0) {
+      store_sc1(&part[G + w], acc2[0]);
+      store_sc1(&part[2 * G + w], acc2[1]);
+    }
+    if (!(ok = res_barrier(a, epoch, s_flag))) break;
+    {
+      double tot[2];
+      res_total<2>(a, part + G, tot, s_red);
+      err = sqrt(tot[1]) / bnrm;
+      bk = tot[0] / bknum;
+      bknum = tot[0];
+      if (w == 0 && t == 0 && k - 1 < a.err_hist_cap) a.err_hist[k - 1] = err;
+      done = !(err > tol) || k >= itmax + 1;
+    }
+  }
+  if (w == 0 && t == 0) {
+    S->iter = k;
+    S->err = err;
+    S->ak = ak;
+    S->bk = bk;
+    S->bknum = bknum;
+    S->done = ok ? 1 : 0;
   }
 }
 
@@ -2381,6 +2719,12 @@ hipError_t dev_build_lattice(perc_ctx* h) {
   h->march_grid_max =
       g.m % kMarchW == 0 && g.n > 2 ? cdiv((g.m / kMarchW) * (g.n - 2), kMarchWaves) : 0;
   march_geometry(h);
+  res_geometry(h);
+  if (h->res_G > 0) {
+    HIP_TRY(dmalloc(&d.res_xch, (size_t)2 * h->res_G * 2 * 2 * g.m));
+    HIP_TRY(dmalloc(&d.res_part, (size_t)2 * 3 * h->res_G));
+    HIP_TRY(dmalloc(&d.res_bar, 9 * kTicketStride));
+  }
   HIP_TRY(dmalloc(&d.partials, kRedSlots * red_partials_size(red_grid(h))));
   HIP_TRY(dmalloc(&d.tickets, kRedSlots * red_tickets_size(red_grid(h))));
   HIP_TRY(hipMemset(d.tickets, 0, kRedSlots * red_tickets_size(red_grid(h)) * sizeof(unsigned)));
@@ -2420,7 +2764,8 @@ void dev_free_all(perc_ctx* h) {
   DeviceBuffers& d = h->d;
   void* ptrs[] = {d.bond_first, d.rowptr, d.col, d.val, d.diag, d.rhs, d.code, d.dtab, d.sflag, d.bocc, d.socc,
                   d.order, d.parent, d.member, d.bot, d.top, d.counters, d.x, d.r,
-                  d.p0, d.p1, d.q, d.partials, d.tickets, d.scal, d.err_hist, d.iout};
+                  d.p0, d.p1, d.q, d.partials, d.tickets, d.scal, d.err_hist, d.iout,
+                  d.res_xch, d.res_part, d.res_bar};
   for (void* p : ptrs)
     if (p) hipFree(p);
   d = DeviceBuffers{};
@@ -2540,6 +2885,31 @@ void march_geometry(perc_ctx* h) {
   h->rm_grid = rspr * cdiv(nrows, h->rm_h);
 }
 
+// resident solve: m a multiple of 1024 (MT = m / 1024 columns per thread
+// and row), the band height H of ceil(nrows / CUs) rows within the LDS and
+// register budget, one workgroup per CU
+void res_geometry(perc_ctx* h) {
+  const Geom& g = h->g;
+  h->res_G = 0;
+  if (g.m % kResThreads != 0 || g.n <= 2) return;
+  int cus = 0, coop = 0;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, h->device) != hipSuccess ||
+      hipDeviceGetAttribute(&coop, hipDeviceAttributeCooperativeLaunch, h->device) != hipSuccess ||
+      !coop || cus <= 0)
+    return;
+  const int nrows = g.n - 2, MT = g.m / kResThreads;
+  const int H = cdiv(nrows, cus);
+  // 4 elements per thread (r, q, code of each in registers, 97 VGPRs); more
+  // spill at 1024 threads: m = 1024 and at most 4 rows per CU
+  if (MT != 1 || H > 4 || (long long)H * g.m > kResLdsRows) return;
+  for (int f = 0; f < h->forms.nforms; ++f)
+    if (!h->forms.regular[f]) return;  // wrapped columns (pbc): slot order is not raster order
+  h->res_MT = MT;
+  h->res_H = H;
+  h->res_HMAX = 4;
+  h->res_G = cdiv(nrows, H);
+}
+
 // solver kernels for the requested format and what the assembly allows
 void select_format(perc_ctx* h) {
   h->stencil = h->fmt_req != PERC_FMT_CSR && h->stencil_ok;
@@ -2548,6 +2918,9 @@ void select_format(perc_ctx* h) {
   h->rowmarch = h->fused && h->rm_grid > 0 && h->fmt_req != PERC_FMT_STENCIL_TILED &&
                 (h->march_mode & PERC_MARCH_ROWS);
   h->march = h->march && !h->rowmarch;
+  // (dev_solve only: the march kernels stay selected for the probes)
+  h->resident = h->fused && h->res_G > 0 && h->fmt_req != PERC_FMT_STENCIL_TILED &&
+                (h->march_mode & PERC_SOLVE_RESIDENT) && h->march_rows_req == 0;
   h->qfree = (h->march || h->rowmarch) && (h->march_mode & PERC_MARCH_QFREE);
   h->march_alt = (h->march || h->rowmarch) && (h->march_mode & PERC_MARCH_ALT);
 }
@@ -2573,6 +2946,58 @@ hipError_t dev_assemble(perc_ctx* h, int rule, double g0, double leak, double Va
   h->tiled_ok = h->stencil_ok && (flag & 4) == 0 && h->tile_grid > 0 && h->g.m % 2 == 0;
   h->march_ok = h->tiled_ok && h->march_grid > 0;
   select_format(h);
+  return hipSuccess;
+}
+
+// one cooperative launch runs the whole iteration loop (k_cg_res)
+hipError_t dev_solve_resident(perc_ctx* h, const CGArgs& ca, int* iter, double* err) {
+  DeviceBuffers& d = h->d;
+  hipStream_t st = h->stream;
+  ResArgs a;
+  a.St = ca.St;
+  a.m = h->g.m;
+  a.nrows = h->g.n - 2;
+  a.pbc = h->g.pbc;
+  a.G = h->res_G;
+  a.H = h->res_H;
+  a.xrows = ca.xrows;
+  a.r0 = d.r;
+  a.x = d.x;
+  a.S = d.scal;
+  a.err_hist = d.err_hist;
+  a.err_hist_cap = d.err_hist_cap;
+  a.xch = d.res_xch;
+  a.part = d.res_part;
+  a.bar = d.res_bar;
+  HIP_TRY(hipMemsetAsync(d.res_bar, 0, 9 * kTicketStride * sizeof(unsigned), st));
+  void* args[] = {&a};
+  const void* fn = nullptr;
+  fn = (const void*)k_cg_res<1, 4>;
+  KernelTiming& T = h->timing;
+  if (T.enabled) {
+    if (T.ev.size() < 2) T.ev.resize(2, nullptr);
+    for (int i = 0; i < 2; ++i)
+      if (!T.ev[i]) HIP_TRY(hipEventCreate(&T.ev[i]));
+    HIP_TRY(hipEventRecord(T.ev[0], st));
+  }
+  HIP_TRY(hipLaunchCooperativeKernel(fn, dim3(a.G), dim3(kResThreads), args, 0, st));
+  HIP_TRY(dbg_sync(st, "k_cg_res"));
+  if (T.enabled) HIP_TRY(hipEventRecord(T.ev[1], st));
+  CGScalars hs{};
+  HIP_TRY(hipMemcpyAsync(&hs, d.scal, sizeof(hs), hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipStreamSynchronize(st));
+  if (hs.pad[0] != 0) {
+    fprintf(stderr, "[perc] k_cg_res: grid barrier timed out\n");
+    return hipErrorLaunchTimeOut;
+  }
+  if (T.enabled && hs.iter > 0) {
+    float ms = 0.f;
+    HIP_TRY(hipEventElapsedTime(&ms, T.ev[0], T.ev[1]));
+    T.spmv_ms += ms;  // whole iterations: P+S and B together
+    T.spmv_n += hs.iter;
+  }
+  *iter = hs.iter;
+  *err = hs.err;
   return hipSuccess;
 }
 
@@ -2607,6 +3032,7 @@ hipError_t dev_solve(perc_ctx* h, int itol, double tol, int itmax, bool x0_zero,
   if (ST) k_cg_init<true><<<G, kBlock, 0, st>>>(a, itol, x0_zero ? 1 : 0);
   else k_cg_init<false><<<G, kBlock, 0, st>>>(a, itol, x0_zero ? 1 : 0);
   HIP_TRY(dbg_sync(st, "k_cg_init"));
+  if (h->resident) return dev_solve_resident(h, a, iter, err);
   // iterate in chunks; the device flag makes surplus launches no-ops
   int chunk = 8;
   CGScalars* hsp = nullptr;

@@ -99,6 +99,9 @@ struct DeviceBuffers {
   double* err_hist = nullptr;   // itmax+2
   int err_hist_cap = 0;
   double* iout = nullptr;       // 2m (boundary-row currents)
+  double* res_xch = nullptr;    // resident solve: exchange rows, partials
+  double* res_part = nullptr;
+  unsigned* res_bar = nullptr;
 };
 
 struct ReplayOrder {
@@ -156,6 +159,8 @@ struct perc_ctx {
   bool qfree = false;           // march B rebuilds q (52N / iteration)
   bool march_alt = false;       // alternating walk directions
   bool rowmarch = false;        // workgroup row-march kernels (k_cg_rm)
+  bool resident = false;        // persistent resident solve (k_cg_res)
+  int res_G = 0, res_H = 0, res_MT = 0, res_HMAX = 0;  // its grid, band height, template
   int rm_w = 0, rm_h = 16;      // their strip width (columns) and band height
   int rm_grid = 0;              // their workgroups
   bool full_voltages = false;   // perc_set_full_voltages: keep x on every row
@@ -179,6 +184,7 @@ hipError_t dev_canon(perc_ctx* h, int* canon_out);
 hipError_t dev_assemble(perc_ctx* h, int rule, double g0, double leak, double Va, int span_root);
 void select_format(perc_ctx* h);  // stencil / fused flags from fmt_req + assembly checks
 void march_geometry(perc_ctx* h); // band height + grid of the register-march kernel
+void res_geometry(perc_ctx* h);   // grid + band height of the resident solve
 hipError_t dev_solve(perc_ctx* h, int itol, double tol, int itmax, bool x0_zero, bool full_x,
                      int* iter, double* err);
 hipError_t dev_currents(perc_ctx* h, int rule, int cur_rule, double g0, double leak, double Va,

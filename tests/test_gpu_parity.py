@@ -534,3 +534,32 @@ def test_table_division_is_ieee_division():
     for seed in (1, 0xC0FFEE):
         assert P.lib().perc_selftest_division(1 << 29, seed, out.ctypes.data) == 0
         assert out[0] == 0, (int(out[0]), np.array(out[1:]).view(np.float64))
+
+
+@pytest.mark.parametrize("lat,m,n,pbc,p", [(0, 1024, 1024, 0, 0.6), (1, 1024, 1024, 0, 0.42),
+                                           (0, 1024, 40, 0, 0.6), (1, 1024, 300, 0, 0.42),
+                                           (0, 1024, 700, 0, 0.55)])
+def test_resident_solve_matches_march(lat, m, n, pbc, p):
+    """The persistent resident solve (one cooperative launch, p in LDS,
+    three grid barriers per iteration; bands of 1..4 rows per CU) against
+    the launched march kernels: same per-row arithmetic, so the same solve
+    up to the association of the dots."""
+    nb = api.nbonds(lat, m, n, pbc)
+    order = api.shuffled_ids(nb, 2024)
+    out = {}
+    with api.Context(lat, m, n, pbc) as ctx:
+        ctx.occupy(PL.BOND, bond_order=order, nbonds_=int(p * nb))
+        if ctx.label()["nspan"] == 0:
+            pytest.skip("no spanning cluster")
+        for mode in (PL.MARCH_ALT, PL.MARCH_DEFAULT):
+            ctx.set_march_mode(mode)
+            c = ctx.conductance(tol=1e-12, itmax=100000, vint=True)
+            out[mode] = (c, ctx.march_info()["kernel"])
+            # boundary rows only (the default): bitwise-identical to the full solve's
+            part = ctx.conductance(tol=1e-12, itmax=100000)
+            assert part["gtop"] == c["gtop"] and part["iter"] == c["iter"]
+    (cm, km), (cr, kr) = out[PL.MARCH_ALT], out[PL.MARCH_DEFAULT]
+    assert km == "wave" and kr == "resident"
+    assert abs(cr["iter"] - cm["iter"]) <= 2
+    assert rel(cr["gtop"], cm["gtop"]) < REL and rel(cr["gbot"], cm["gbot"]) < REL
+    assert np.max(np.abs(cr["vint"] - cm["vint"])) < 1e-6

@@ -26,7 +26,7 @@ for step in "$@"; do
   case "$step" in
     tests) run pytest_gpu 900 python -m pytest tests -m gpu -q -rs -x ;;
     testsall) run pytest_gpu 900 python -m pytest tests -m gpu -q -rs ;;
-    tests_march) run pytest_march 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread -k "march or division" ;;
+    tests_march) run pytest_march 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread -k "march or division or resident" ;;
     probe) run march_probe 600 python tools/march_probe.py ;;
     pmc_sq) run pmc_sq 600 bash tools/pmc_march.sh ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
