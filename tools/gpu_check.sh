@@ -29,6 +29,7 @@ for step in "$@"; do
     tests_march) run pytest_march 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread -k "march or division or resident" ;;
     probe) run march_probe 600 python tools/march_probe.py ;;
     pmc_sq) run pmc_sq 600 bash tools/pmc_march.sh ;;
+    configs) run configs 1100 bash tools/configs.sh ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench1024) run bench1024 600 python bench.py --L 1024 --p 0.6 --steps 3 --warmup 1 --no-cpu-baseline ;;
     bench1024dbg) PERC_SYNC_DEBUG=1 run bench1024dbg 600 python bench.py --L 1024 --p 0.6 --steps 1 --warmup 0 --no-cpu-baseline ;;
