@@ -48,6 +48,7 @@ extern "C" {
 #define PERC_BOND 0
 #define PERC_SITE 1
 #define PERC_SITEBOND 2
+#define PERC_BONDSITE 3  /* bonds first, then sites (Square/bondsite.f); perc_replay_labels only */
 /* conductance weight rules (which bonds get g0; all others get `leak`) */
 #define PERC_RULE_BOND 0     /* bond label == perccln         (bondc.f:483) */
 #define PERC_RULE_SITE 1     /* both end sites in perccln     (ConductCalc.m:90) */
@@ -152,7 +153,12 @@ int perc_bs_perc_replay(int lattice, int m, int n, int pbc, const int *site_orde
                         const int *bond_order, int nbond, int c0_overflow, int *first);
 
 /* Same numbering without a context or device: host-only O(N alpha) replay
-   of an explicit occupancy (used by the drivers' text output and tests). */
+   of an explicit occupancy (used by the drivers' text output and tests).
+   kind PERC_BONDSITE replays Square/bondsite.f:182-354 (bonds first, each a
+   size-1 cluster, then sites merging their neighbour bonds' clusters; sizes
+   count bonds and sites; spanning: lowest label of size >= 2n-1 holding a
+   bottom- and a top-row site, bondsite.f:364-415).  csize needs
+   cap >= t + nb + 2; stats = {cln, maxcn, maxcs, perccln}. */
 int perc_replay_labels(int lattice, int m, int n, int pbc, int kind, int nsites,
                        const int *site_order, int nbonds, const int *bond_order,
                        int *bond_label, int *site_label, int *csize, int cap,

@@ -71,6 +71,14 @@ build tri_site                Triangular/site.f
 build sq_sitebond             Square/sitebond.f
 build sq_sitebond_p9          Square/sitebond.f 's/ps = 0.50d+00/ps = 0.90d+00/' 's/pb = 0.50d+00/pb = 0.60d+00/'
 build tri_sitebond            Triangular/sitebond.f
+# mixed bonds-then-sites (bondsite, Square/bondsite.f:182-354)
+BS30='s/m = 10  /m = 30  /'
+BN30='s/n = 10  /n = 30  /'
+build sq_bondsite             Square/bondsite.f
+build sq_bondsite_30          Square/bondsite.f "$BS30" "$BN30" 's/ps = 0.50d+00/ps = 0.80d+00/' 's/pb = 0.50d+00/pb = 0.70d+00/'
+build sq_bondsite_30_pbc      Square/bondsite.f "$BS30" "$BN30" 's/ps = 0.50d+00/ps = 0.80d+00/' 's/pb = 0.50d+00/pb = 0.70d+00/' 's/pbc = 0 /pbc = 1 /'
+build tri_bondsite            Triangular/bondsite.f
+build tri_bondsite_30         Triangular/bondsite.f "$BS30" "$BN30" 's/ps = 0.50d+00/ps = 0.70d+00/' 's/pb = 0.50d+00/pb = 0.60d+00/'
 # ensemble driver (trial seeds, pb sweep, per-step spanning)
 build sq_bond_cond            Square/bond_cond.f
 build sq_bond_cond_3t         Square/bond_cond.f 's/numtrials = 1 /numtrials = 3 /' 's/m = 10 /m = 12 /' 's/n = 10 /n = 12 /'

@@ -658,6 +658,93 @@ int or_label_sitebond(int lattice, int m, int n, int pbc, int nb,
 }
 
 /* ======================================================================
+ * Mixed bonds-then-sites labeling, literal.  Square/bondsite.f:170-322
+ * (Triangular/bondsite.f: the same loops, scn 6).  border = shuffled bond
+ * ids (0 = the shuffle's spill slot), sorder = shuffled sites.  s[t],
+ * blabel[nb], csize[cap >= t + nb + 2] (c(0) = csize[0] stays 0: the
+ * reference reads c(0) for an unoccupied first neighbour bond, and in its
+ * build that word is 0).  Returns cln.
+ * ==================================================================== */
+int or_label_bondsite(int lattice, int m, int n, int pbc, int nb,
+                      const int *b1, const int *b2,
+                      const int *border, int tbonds,
+                      const int *sorder, int tsites,
+                      int *s, int *blabel, int *csize, int *maxcn_o,
+                      int *maxcs_o) {
+  int t = m * n, i, j, k, l, cln = 1, maxcn = 1, maxcs = 1;
+  int *sp = (int *)calloc((size_t)t + 1, sizeof(int));
+  memset(blabel, 0, sizeof(int) * (size_t)nb);
+  memset(csize, 0, sizeof(int) * (size_t)(t + nb + 2));
+  for (i = 1; i <= tbonds; i++) { /* bondsite.f:182-199 */
+    int id = border[i - 1];
+    if (id > 0) blabel[id - 1] = cln; /* b(j,3) = cln for the matching row */
+    csize[cln] = 1;
+    cln++;
+  }
+  for (i = 1; i <= tsites; i++) { /* bondsite.f:220-320 */
+    int sn = sorder[i - 1], nn[10], nnb[12][4], rc = 0, lcn, lcs, clsum;
+    memset(nnb, 0, sizeof(nnb));
+    if (sn <= 0) { /* spill slot: no neighbour bond matches -> case 1 */
+      csize[cln] = 1;
+      cln++;
+      lcn = 0;
+      goto track;
+    }
+    or_nearestn(lattice, m, n, pbc, sn, nn);
+    for (j = 0; j < (lattice ? 6 : 4); j++) {
+      if (nn[j] != 0) {
+        nnb[rc][0] = nn[j] > sn ? sn : nn[j];
+        nnb[rc][1] = nn[j] > sn ? nn[j] : sn;
+        rc++;
+      }
+    }
+    for (j = 0; j < nb; j++) /* bondsite.f:245-254 */
+      for (k = 0; k < (lattice ? 6 : 4); k++)
+        if (b1[j] == nnb[k][0] && b2[j] == nnb[k][1]) {
+          nnb[k][2] = blabel[j];
+          nnb[k][3] = csize[blabel[j]];
+        }
+    lcn = nnb[0][2];
+    lcs = nnb[0][3];
+    for (k = 1; k < (lattice ? 6 : 4); k++) /* bondsite.f:262-272 */
+      if (nnb[k][0] != 0 && nnb[k][2] != 0 && nnb[k][3] > lcs) {
+        lcn = nnb[k][2];
+        lcs = nnb[k][3];
+      }
+    if (lcs == 0) { /* case 1 */
+      sp[sn] = cln;
+      csize[cln] = 1;
+      cln++;
+      goto track;
+    }
+    clsum = lcs; /* case 2 */
+    for (k = 0; k < (lattice ? 6 : 4); k++) {
+      if (nnb[k][0] == 0 || nnb[k][2] == 0 || nnb[k][2] == lcn) continue;
+      {
+        int dup = 0;
+        for (l = 0; l < k; l++) if (nnb[l][2] == nnb[k][2]) dup = 1;
+        if (!dup) {
+          clsum += nnb[k][3];
+          for (j = 0; j < nb; j++) if (blabel[j] == nnb[k][2]) blabel[j] = lcn;
+          for (j = 1; j <= t; j++) if (sp[j] == nnb[k][2]) sp[j] = lcn;
+        }
+      }
+      csize[nnb[k][2]] = 0;
+    }
+    sp[sn] = lcn;
+    clsum = clsum + 1;
+    csize[lcn] = clsum;
+  track:
+    if (csize[lcn] > maxcs) { maxcs = csize[lcn]; maxcn = lcn; }
+  }
+  for (j = 1; j <= t; j++) s[j - 1] = sp[j];
+  free(sp);
+  if (maxcn_o) *maxcn_o = maxcn;
+  if (maxcs_o) *maxcs_o = maxcs;
+  return cln;
+}
+
+/* ======================================================================
  * Spanning detection.
  * ==================================================================== */
 int or_span_bonds(int m, int n, int nb, const int *b1, const int *b2,

@@ -74,6 +74,14 @@ int or_label_sitebond(int lattice, int m, int n, int pbc, int nb,
                       const int *o1, const int *o2, int tbonds,
                       int *s, int *blabel, int *csize, int *maxcn, int *maxcs);
 
+/* mixed bonds-then-sites: Square/bondsite.f:170-322 (literal); border =
+   bond ids (0: spill slot), s[t], blabel[nb], csize[t+nb+2]; returns cln */
+int or_label_bondsite(int lattice, int m, int n, int pbc, int nb,
+                      const int *b1, const int *b2,
+                      const int *border, int tbonds,
+                      const int *sorder, int tsites,
+                      int *s, int *blabel, int *csize, int *maxcn, int *maxcs);
+
 /* ---- spanning detection --------------------------------------------- */
 /* bond: lowest label l < cln with c(l) >= n-1 touching bottom (b1<=m) and
    top (b2>t-m) (Square/bondc.f:413-456).  0 if none. */

@@ -20,7 +20,7 @@ ERRORS = {
     -9: "PERC_ESTATE",
 }
 SQUARE, TRIANGULAR = 0, 1
-BOND, SITE, SITEBOND = 0, 1, 2
+BOND, SITE, SITEBOND, BONDSITE = 0, 1, 2, 3
 RULE_BOND, RULE_SITE, RULE_MIXED = 0, 1, 2
 CUR_FORTRAN, CUR_MATLAB = 0, 1
 FMT_AUTO, FMT_CSR, FMT_STENCIL, FMT_STENCIL_SPLIT, FMT_STENCIL_TILED = 0, 1, 2, 3, 4

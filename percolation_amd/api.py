@@ -331,6 +331,28 @@ def sitebond(lattice=0, m=50, n=50, pbc=0, ps=0.50, pb=0.50, sseed=143285, bseed
             ctx.close()
 
 
+def bondsite(lattice=0, m=10, n=10, pbc=0, ps=0.50, pb=0.50, sseed=143285, bseed=43716):
+    """Mixed bonds-then-sites realisation (Fortran/Square/bondsite.f): bonds
+    to pb (seed bseed), each a size-1 cluster, then sites to ps (seed sseed)
+    merging their neighbour bonds' clusters; reference numbering by host
+    replay (perc_replay_labels, PERC_BONDSITE).  Also the drop-in text of
+    bssite.txt / bsbond.txt (bondsite.f:420-430)."""
+    t, nb = m * n, nbonds(lattice, m, n, pbc)
+    sorder = shuffled_ids(t, sseed)   # bondsite.f:116-127
+    border = shuffled_ids(nb, bseed)  # bondsite.f:153-166
+    ts, tb = int(ps * t), int(pb * nb)
+    r = replay_labels(lattice, m, n, pbc, L.BONDSITE, site_order=sorder, nsites=ts,
+                      bond_order=border, nbond=tb)
+    b1, b2 = bond_list(lattice, m, n, pbc)
+    s_ext = np.zeros(nb + 1, dtype=np.int64)
+    s_ext[1:min(t, nb) + 1] = r["site_label"][:min(t, nb)]
+    c = r["csize"]
+    r["bssite"] = fmt_i10(np.arange(1, nb + 1), s_ext[1:], c[1:nb + 1])
+    r["bsbond"] = fmt_i10(b1, b2, r["bond_label"])
+    r.update(sorder=sorder, border=border)
+    return r
+
+
 def pb_grid(lattice, nb):
     """nbarr of bond_cond.f:84-97 (square 0.49.., triangular 0.35.., +5e-3)."""
     pbarr = np.zeros(250)

@@ -410,6 +410,12 @@ static int label_numbers_impl(const Geom& g, const std::vector<int>& bond_first,
     c.assign(g.t + 2, 0);
     sl.assign(g.t, 0);
     rc = replay_sites(g, sites, nsites, sl.data(), c.data(), (int)c.size(), st);
+  } else if (kind == PERC_BONDSITE) {
+    c.assign(g.t + nb + 2, 0);
+    sl.assign(g.t, 0);
+    bl.assign(nb, 0);
+    rc = replay_bondsite(g, bond_first, sites, nsites, bonds, nbond, sl.data(), bl.data(),
+                         c.data(), (int)c.size(), st);
   } else {
     c.assign(g.t + nb + 2, 0);
     sl.assign(g.t, 0);
@@ -591,7 +597,7 @@ int perc_replay_labels(int lattice, int m, int n, int pbc, int kind, int nsites,
                        const int* site_order, int nbond, const int* bond_order, int* bond_label,
                        int* site_label, int* csize, int cap, int* stats) {
   if ((lattice != PERC_SQUARE && lattice != PERC_TRIANGULAR) || m < 2 || n < 2 ||
-      kind < PERC_BOND || kind > PERC_SITEBOND)
+      kind < PERC_BOND || kind > PERC_BONDSITE)
     return PERC_EINVAL;
   const Geom g = make_geom(lattice, m, n, pbc);
   std::vector<int> bf(g.t + 2, 0);

@@ -198,6 +198,9 @@ int replay_bonds(const Geom& g, const std::vector<int>& bond_first, const int* o
                  int count, int* label, int* csize, int cap, int* stats);
 int replay_sites(const Geom& g, const int* order, int count, int* label, int* csize, int cap,
                  int* stats);
+int replay_bondsite(const Geom& g, const std::vector<int>& bond_first, const int* sorder,
+                    int nsites, const int* border, int nbond, int* site_label, int* bond_label,
+                    int* csize, int cap, int* stats);
 int replay_sitebond(const Geom& g, const std::vector<int>& bond_first, const int* sorder,
                     int nsites, const int* border, int nbonds, int* site_label,
                     int* bond_label, int* csize, int cap, int* stats);

@@ -285,6 +285,102 @@ int replay_sitebond(const Geom& g, const std::vector<int>& bond_first, const int
   return PERC_OK;
 }
 
+// bondsite (Square/bondsite.f:182-354, Triangular/bondsite.f the same with
+// scn 6): bonds border[0..nbond) occupied first, each a cluster of size 1
+// numbered in occupation order (an id of 0, the shuffle's spill slot H2,
+// still takes a number); then sites in sorder, each joining the clusters of
+// its occupied neighbour bonds: the largest (first in nearestn order on a
+// tie, the first row's cluster kept unless a later one is strictly larger)
+// keeps its number, the others merge into it and their sizes drop to 0, and
+// the site counts 1.  A site with no occupied neighbour bond starts its own
+// cluster.  Sizes count bonds and sites.  The reference reads c(0) for an
+// unoccupied first neighbour bond; in its build that word is 0 (all five
+// reference fixtures match with c(0) = 0), so the choice above is the
+// intended one.  Union-find over bonds 0..nb-1 and sites nb+s.
+int replay_bondsite(const Geom& g, const std::vector<int>& bond_first, const int* sorder,
+                    int nsites, const int* border, int nbond, int* site_label, int* bond_label,
+                    int* csize, int cap, int* stats) {
+  const int nb = (int)nbonds(g), t = g.t;
+  if (cap < t + nb + 2) return PERC_EINVAL;
+  std::vector<int> c(cap, 0);
+  std::vector<int> lab(nb + t + 1, 0);  // label of a root element
+  std::vector<char> bocc(nb, 0), socc(t + 1, 0);
+  DSU u(nb + t + 1);
+  int cln = 1;
+  for (int i = 0; i < nbond; ++i) {  // bondsite.f:182-199
+    const int id = border[i];
+    if (id > 0 && id <= nb) {
+      bocc[id - 1] = 1;
+      lab[id - 1] = cln;
+    }
+    c[cln] = 1;
+    ++cln;
+  }
+  int maxcn = 1, maxcs = 1;
+  for (int i = 0; i < nsites; ++i) {  // bondsite.f:220-320
+    const int sn = sorder[i];
+    int lcn = 0;
+    if (sn < 1 || sn > t) {  // spill slot: a one-site cluster with no site
+      c[cln] = 1;
+      ++cln;
+    } else {
+      int nn[6];
+      nearestn(g, sn, nn);
+      int rl[6], re[6], nr = 0;  // row label, an element of its cluster
+      for (int k = 0; k < g.scn; ++k) {
+        if (nn[k] == 0) continue;
+        const int id = bond_index(g, bond_first, std::min(sn, nn[k]), std::max(sn, nn[k]));
+        rl[nr] = id >= 0 && bocc[id] ? lab[u.find(id)] : 0;
+        re[nr] = id;
+        ++nr;
+      }
+      lcn = nr ? rl[0] : 0;
+      int lcs = nr ? c[lcn] : 0;
+      int le = nr ? re[0] : -1;
+      for (int k = 1; k < nr; ++k)
+        if (rl[k] != 0 && c[rl[k]] > lcs) {
+          lcn = rl[k];
+          lcs = c[rl[k]];
+          le = re[k];
+        }
+      const int node = nb + sn;
+      socc[sn] = 1;
+      if (lcs == 0) {  // bondsite.f:264-274
+        lab[node] = cln;
+        c[cln] = 1;
+        ++cln;
+      } else {         // bondsite.f:278-313
+        int clsum = lcs;
+        int root = u.find(le);
+        for (int k = 0; k < nr; ++k) {
+          if (rl[k] == 0 || rl[k] == lcn) continue;
+          bool dup = false;
+          for (int l = 0; l < k; ++l) dup = dup || rl[l] == rl[k];
+          if (!dup) {
+            clsum += c[rl[k]];
+            root = u.unite(root, re[k]);
+          }
+          c[rl[k]] = 0;
+        }
+        root = u.unite(root, node);
+        lab[root] = lcn;
+        c[lcn] = clsum + 1;
+      }
+    }
+    if (c[lcn] > maxcs) {  // bondsite.f:316-319
+      maxcs = c[lcn];
+      maxcn = lcn;
+    }
+  }
+  if (site_label)
+    for (int s = 1; s <= t; ++s) site_label[s - 1] = socc[s] ? lab[u.find(nb + s)] : 0;
+  if (bond_label)
+    for (int k = 0; k < nb; ++k) bond_label[k] = bocc[k] ? lab[u.find(k)] : 0;
+  if (csize) std::memcpy(csize, c.data(), sizeof(int) * cap);
+  if (stats) { stats[0] = cln; stats[1] = maxcn; stats[2] = maxcs; }
+  return PERC_OK;
+}
+
 // bs_perc's site loop (Square/bs_perc.f:236-350): bonds border[0..nbonds)
 // occupied first, each its own cluster of size 1; then sites are added in
 // order, each joining the clusters of its occupied neighbour bonds (the

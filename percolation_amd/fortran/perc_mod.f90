@@ -11,7 +11,8 @@ module perc_api
 
   integer(c_int), parameter :: PERC_OK = 0
   integer(c_int), parameter :: PERC_SQUARE = 0, PERC_TRIANGULAR = 1
-  integer(c_int), parameter :: PERC_BOND = 0, PERC_SITE = 1, PERC_SITEBOND = 2
+  integer(c_int), parameter :: PERC_BOND = 0, PERC_SITE = 1, PERC_SITEBOND = 2, &
+                                PERC_BONDSITE = 3
   integer(c_int), parameter :: PERC_RULE_BOND = 0, PERC_RULE_SITE = 1, PERC_RULE_MIXED = 2
   integer(c_int), parameter :: PERC_CUR_FORTRAN = 0, PERC_CUR_MATLAB = 1
   ! off-diagonal value of bonds outside the spanning cluster (bondc.f:487)
@@ -74,6 +75,15 @@ module perc_api
       integer(c_int) :: site_order(*), bond_order(*)
       integer(c_int) :: first
     end function perc_bs_perc_replay
+
+    integer(c_int) function perc_replay_labels(lattice, m, n, pbc, kind, nsites, site_order, &
+        nbond, bond_order, bond_label, site_label, csize, cap, stats) &
+        bind(C, name='perc_replay_labels')
+      import :: c_int, c_ptr
+      integer(c_int), value :: lattice, m, n, pbc, kind, nsites, nbond, cap
+      type(c_ptr), value :: site_order, bond_order, bond_label, site_label, csize
+      integer(c_int) :: stats(4)
+    end function perc_replay_labels
 
     integer(c_int) function perc_nbonds(lattice, m, n, pbc) bind(C, name='perc_nbonds')
       import :: c_int

@@ -50,6 +50,17 @@ VARIANTS = {
                                         sseed=143285, bseed=43716)),
     "tri_sitebond": ("sitebond", dict(lattice=1, m=10, n=10, pbc=0, ps=0.50, pb=0.50,
                                       sseed=143285, bseed=43716)),
+    # bonds first, then sites (Square/bondsite.f, Triangular/bondsite.f)
+    "sq_bondsite": ("bondsite", dict(lattice=0, m=10, n=10, pbc=0, ps=0.50, pb=0.50,
+                                     sseed=143285, bseed=43716)),
+    "sq_bondsite_30": ("bondsite", dict(lattice=0, m=30, n=30, pbc=0, ps=0.80, pb=0.70,
+                                        sseed=143285, bseed=43716)),
+    "sq_bondsite_30_pbc": ("bondsite", dict(lattice=0, m=30, n=30, pbc=1, ps=0.80, pb=0.70,
+                                            sseed=143285, bseed=43716)),
+    "tri_bondsite": ("bondsite", dict(lattice=1, m=10, n=10, pbc=0, ps=0.50, pb=0.50,
+                                      sseed=143285, bseed=43716)),
+    "tri_bondsite_30": ("bondsite", dict(lattice=1, m=30, n=30, pbc=0, ps=0.70, pb=0.60,
+                                         sseed=143285, bseed=43716)),
     "sq_bond_cond": ("bond_cond", dict(lattice=0, m=10, n=10, pbc=0, numtrials=1, seed=58302)),
     "sq_bond_cond_3t": ("bond_cond", dict(lattice=0, m=12, n=12, pbc=0, numtrials=3,
                                           seed=58302)),
@@ -78,8 +89,8 @@ VARIANTS = {
 
 KEEP = {"bond.txt", "bondorder.txt", "site.txt", "siteorder.txt", "bondlist.txt",
         "sbsite.txt", "sbbond.txt", "bondcond.txt", "bond_perc.txt", "site_perc.txt",
-        "sb_perc.txt", "bs_perc.txt"}
-MD5_ONLY = {"bondocc.txt", "siteocc.txt", "sbdebug.txt"}
+        "sb_perc.txt", "bs_perc.txt", "bssite.txt", "bsbond.txt"}
+MD5_ONLY = {"bondocc.txt", "siteocc.txt", "sbdebug.txt", "bsdebug.txt"}
 NUM = r"[-+]?(?:\d+\.?\d*|\.\d+)(?:[EeDd][-+]?\d+)?"
 
 

@@ -48,6 +48,7 @@ def lib():
         "or_label_sites_literal": (i, [i, i, i, i, _I, i, _I, _I, _IP, _IP]),
         "or_label_sites_replay": (i, [i, i, i, i, _I, i, _I, _I, _IP, _IP]),
         "or_label_sitebond": (i, [i, i, i, i, i, _I, _I, _I, i, _I, _I, i, _I, _I, _I, _IP, _IP]),
+        "or_label_bondsite": (i, [i, i, i, i, i, _I, _I, _I, i, _I, i, _I, _I, _I, _IP, _IP]),
         "or_span_bonds": (i, [i, i, i, _I, _I, _I, _I, i]),
         "or_span_sites": (i, [i, i, _I, _I, i, i]),
         "or_bond_values": (None, [i, i, _I, _I, _I, _I, i, d, d, _D]),

@@ -23,11 +23,13 @@ import golden_io as G
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 BIN = os.path.join(REPO, "percolation_amd", "fortran", "bin")
-TRACES = {"bondocc.txt", "siteocc.txt", "sbdebug.txt"}  # per-step logs, not produced
+TRACES = {"bondocc.txt", "siteocc.txt", "sbdebug.txt", "bsdebug.txt"}  # per-step logs, not produced
 # golden kind -> (program, namelist group, parameters)
 NML = {"bondc": ("bondc", "bondc", ("lattice", "m", "n", "pbc", "pb", "seed", "tol", "itmax")),
        "site": ("site", "site", ("lattice", "m", "n", "pbc", "ps", "seed")),
        "sitebond": ("sitebond", "sitebond",
+                    ("lattice", "m", "n", "pbc", "ps", "pb", "sseed", "bseed")),
+       "bondsite": ("bondsite", "bondsite",
                     ("lattice", "m", "n", "pbc", "ps", "pb", "sseed", "bseed")),
        "bond_cond": ("bond_cond", "bond_cond", ("lattice", "m", "n", "pbc", "numtrials", "seed")),
        "bond_perc": ("bond_perc", "perc_scan", ("lattice", "m", "n", "pbc", "numtrials", "seed")),
@@ -110,6 +112,19 @@ def test_driver_outputs_byte_identical(v, tmp_path):
         assert abs(gtop - md["gtop"]) <= 1e-10 * abs(md["gtop"])
         tight = md["params"].get("tol", 1e-8) <= 1e-13
         assert abs(gbot - md["gbot"]) <= (1e-10 if tight else 1e-6) * abs(md["gbot"])
+
+
+@pytest.mark.parametrize("v", [v for v in G.variants() if G.meta(v)["kind"] == "bondsite"])
+def test_bondsite_driver_byte_identical(v, tmp_path):
+    """bondsite (host replay through the Fortran binding; the reference
+    computes no conductance there, so no device): bssite.txt and bsbond.txt
+    byte-identical, largest / spanning cluster as printed."""
+    md, r = run_variant(v, tmp_path)
+    for f in golden_files(v):
+        assert (tmp_path / f).read_bytes() == G.text(v, f), f
+    assert "largest overall cluster size: %d" % md["maxcs"] in " ".join(r.stdout.split())
+    if md["perccln"]:
+        assert "infinite cluster number: %d" % md["perccln"] in " ".join(r.stdout.split())
 
 
 @pytest.mark.gpu

@@ -107,6 +107,25 @@ def test_sitebond_partition_bitexact(lat, m, n, pbc, ps, pb, seed):
     assert (li["nspan"] > 0) == (ref["perccln"] > 0)
 
 
+@pytest.mark.parametrize("lat,m,n,pbc,ps,pb,seed", [(0, 30, 30, 1, 0.8, 0.7, 21),
+                                                     (1, 64, 48, 0, 0.7, 0.6, 22),
+                                                     (0, 128, 96, 0, 0.85, 0.75, 23)])
+def test_bondsite_site_partition_matches_gpu(lat, m, n, pbc, ps, pb, seed):
+    """bondsite (bonds first, then sites) connects two sites exactly when an
+    occupied bond joins them, as the GPU mixed labeling does: the site
+    partition of the PERC_BONDSITE replay equals the GPU's (canonical
+    min-site ids), whatever the history-dependent numbering."""
+    t, nb = m * n, api.nbonds(lat, m, n, pbc)
+    so, bo = api.shuffled_ids(t, seed), api.shuffled_ids(nb, seed + 1)
+    ts, tb = int(ps * t), int(pb * nb)
+    with api.Context(lat, m, n, pbc) as ctx:
+        ctx.occupy(PL.SITEBOND, site_order=so, nsites=ts, bond_order=bo, nbonds_=tb)
+        li = ctx.label(canon=True)
+    ref = api.replay_labels(lat, m, n, pbc, PL.BONDSITE, site_order=so, nsites=ts,
+                            bond_order=bo, nbond=tb)
+    assert np.array_equal(li["canon"].astype(np.int64), oracle_canon_sites(ref["site_label"]))
+
+
 # ------------------------------------------------------------ assembly + SpMV
 def oracle_system(lat, m, n, pbc, b1, b2, gval):
     t, N = m * n, m * n - 2 * m

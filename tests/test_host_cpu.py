@@ -204,6 +204,30 @@ def test_replay_equals_literal_sitebond(lat, m, n, pbc, p, seed):
     assert (r["cln"], r["maxcn"], r["maxcs"]) == (cln, mx.value, ms.value)
 
 
+@pytest.mark.parametrize("lat,m,n,pbc,p,seed", CASES)
+@pytest.mark.parametrize("ps", [0.45, 0.8])
+def test_replay_equals_literal_bondsite(lat, m, n, pbc, p, seed, ps):
+    """PERC_BONDSITE replay (union-find) == the oracle's literal bondsite.f
+    loops: labels, sizes, cln, largest cluster, spanning label."""
+    t = m * n
+    Or = O.lib()
+    b1, b2 = O.bond_list(lat, m, n, pbc)
+    nb = len(b1)
+    so, bo = O.site_order(t, seed), O.site_order(nb, seed + 100)
+    ts, tb = int(ps * t), int(p * nb)
+    s, bl, cs = O.i32(t), O.i32(nb), O.i32(t + nb + 2)
+    mx, ms = C.c_int(), C.c_int()
+    cln = Or.or_label_bondsite(lat, m, n, pbc, nb, b1, b2, bo, tb, so, ts, s, bl, cs,
+                               C.byref(mx), C.byref(ms))
+    r = api.replay_labels(lat, m, n, pbc, PL.BONDSITE, site_order=api.shuffled_ids(t, seed),
+                          nsites=ts, bond_order=api.shuffled_ids(nb, seed + 100), nbond=tb)
+    assert np.array_equal(r["site_label"], s)
+    assert np.array_equal(r["bond_label"], bl)
+    assert np.array_equal(r["csize"], cs)
+    assert (r["cln"], r["maxcn"], r["maxcs"]) == (cln, mx.value, ms.value)
+    assert r["perccln"] == Or.or_span_sites(m, n, s, cs, cln, 2 * n - 1)
+
+
 def test_pb_grid_matches_reference_rows():
     """nbarr of bond_cond.f:84-97 gives the reference's row pb values."""
     for v in [v for v in G.variants() if G.meta(v)["kind"] == "bond_cond"]:

@@ -12,12 +12,14 @@ import numpy as np
 import pytest
 
 import golden_io as G
+from percolation_amd import api
 import oracle_lib as O
 
 BONDC = [v for v in G.variants() if G.meta(v)["kind"] == "bondc"]
 SITE = [v for v in G.variants() if G.meta(v)["kind"] == "site"]
 SITEBOND = [v for v in G.variants() if G.meta(v)["kind"] == "sitebond"]
 BONDCOND = [v for v in G.variants() if G.meta(v)["kind"] == "bond_cond"]
+BONDSITE = [v for v in G.variants() if G.meta(v)["kind"] == "bondsite"]
 
 LIBGFORTRAN = "/opt/conda/lib/libgfortran.so.4"
 
@@ -168,6 +170,36 @@ def test_sitebond_labels(v):
     assert G.fmt_i10(b1, b2, bl) == G.text(v, "sbbond.txt")
     assert (mx.value, ms.value) == (md["maxcn"], md["maxcs"])
     assert L.or_span_sites(m, n, s, cs, cln, 2 * n - 1) == md["perccln"]
+
+
+@pytest.mark.parametrize("v", BONDSITE)
+def test_bondsite_labels(v):
+    """bssite.txt / bsbond.txt byte-identical (Square/bondsite.f:170-430),
+    the oracle's literal loops and libperc's O(N alpha) replay alike."""
+    md = G.meta(v)
+    p = md["params"]
+    lat, m, n, pbc = p["lattice"], p["m"], p["n"], p["pbc"]
+    t = m * n
+    L = O.lib()
+    b1, b2 = O.bond_list(lat, m, n, pbc)
+    nb = len(b1)
+    sorder = O.site_order(t, p["sseed"])
+    border = O.site_order(nb, p["bseed"])  # shuffled bond ids (0: spill slot)
+    ts, tb = int(p["ps"] * t), int(p["pb"] * nb)
+    s, bl, cs = O.i32(t), O.i32(nb), O.i32(t + nb + 2)
+    mx, ms = C.c_int(), C.c_int()
+    cln = L.or_label_bondsite(lat, m, n, pbc, nb, b1, b2, border, tb, sorder, ts, s, bl, cs,
+                              C.byref(mx), C.byref(ms))
+    s_ext = np.zeros(nb, dtype=np.int64)
+    s_ext[:min(t, nb)] = s[:min(t, nb)]
+    assert G.fmt_i10(np.arange(1, nb + 1), s_ext, cs[1:nb + 1]) == G.text(v, "bssite.txt")
+    assert G.fmt_i10(b1, b2, bl) == G.text(v, "bsbond.txt")
+    assert (mx.value, ms.value) == (md["maxcn"], md["maxcs"])
+    assert L.or_span_sites(m, n, s, cs, cln, 2 * n - 1) == md["perccln"]
+    r = api.bondsite(lat, m, n, pbc, p["ps"], p["pb"], p["sseed"], p["bseed"])
+    assert r["bssite"].encode() == G.text(v, "bssite.txt")
+    assert r["bsbond"].encode() == G.text(v, "bsbond.txt")
+    assert (r["maxcn"], r["maxcs"], r["perccln"]) == (md["maxcn"], md["maxcs"], md["perccln"])
 
 
 @pytest.mark.parametrize("v", BONDCOND)
