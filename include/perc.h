@@ -259,6 +259,13 @@ int perc_set_march_rows(perc_ctx *h, int rows);
 #define PERC_SOLVE_RESIDENT 8
 #define PERC_MARCH_DEFAULT (PERC_MARCH_ALT | PERC_SOLVE_RESIDENT)
 int perc_set_march_mode(perc_ctx *h, int mode);
+/* Random bond conductances (MATLAB/ConductCalc.m condtype 2, :38-47 and
+   :94-97): the bonds of the spanning cluster get G = -g0 * w[id] instead of
+   -g0 (w[id] = the MATLAB rand drawn for that bond; the draw order is the
+   caller's, see api.conductcalc_weights).  w = NULL restores fixed
+   conductances.  n = the lattice's bond count.  With weights the solver
+   runs the CSR operator (the stencil code encodes two values only). */
+int perc_set_bond_weights(perc_ctx *h, const double *w, long long n);
 /* Solver loop of the assembled system: out5[0] = 0 (no march kernel: LDS
    tiles, split or CSR), 1 (per-wave march k_cg_march), 2 (workgroup
    row-march k_cg_rm), 3 (resident persistent solve k_cg_res); out5[1] =

@@ -93,6 +93,7 @@ SIGNATURES = {
     "perc_set_march_rows": (C.c_int, [_VP, C.c_int]),
     "perc_set_march_mode": (C.c_int, [_VP, C.c_int]),
     "perc_march_info": (C.c_int, [_VP, _VP]),
+    "perc_set_bond_weights": (C.c_int, [_VP, _VP, C.c_longlong]),
     "perc_selftest_division": (C.c_int, [C.c_longlong, C.c_ulonglong, _VP]),
     "perc_stats_accumulate": (None, [_D, C.c_int, C.c_double, C.c_int, C.c_int]),
     "sprsin_": (None, [_VP] * 7),

@@ -212,6 +212,16 @@ class Context:
         """PERC_MARCH_QFREE | PERC_MARCH_ALT bits of the register-march loop (perc.h)."""
         L.check(L.lib().perc_set_march_mode(self.h, int(mode)), "perc_set_march_mode")
 
+    def set_bond_weights(self, w=None):
+        """Per-bond conductance multipliers for the spanning cluster's bonds
+        (ConductCalc.m condtype 2; None: fixed g0).  perc_set_bond_weights."""
+        if w is None:
+            L.check(L.lib().perc_set_bond_weights(self.h, None, 0), "perc_set_bond_weights")
+            return
+        w = np.ascontiguousarray(w, dtype=np.float64)
+        L.check(L.lib().perc_set_bond_weights(self.h, w.ctypes.data, len(w)),
+                "perc_set_bond_weights")
+
     def march_info(self):
         """The solver loop of the assembled system (perc_march_info)."""
         out = np.zeros(5, dtype=np.int32)
@@ -351,6 +361,25 @@ def bondsite(lattice=0, m=10, n=10, pbc=0, ps=0.50, pb=0.50, sseed=143285, bseed
     r["bsbond"] = fmt_i10(b1, b2, r["bond_label"])
     r.update(sorder=sorder, border=border)
     return r
+
+
+def conductcalc_weights(rule, b1, b2, bond_label, site_label, perccln, seed=1838534):
+    """ConductCalc.m condtype 2 (MATLAB/ConductCalc.m:38-47, 94-97, 114-118,
+    136-146): the bonds that get -g0 under the rule get -g0*rand instead,
+    one rand per such bond in bond-list order from rand('twister', seed).
+    MATLAB's 'twister' is MT19937 seeded by init_genrand(seed) with 53-bit
+    doubles (genrand_res53) -- the generator numpy.random.RandomState(seed)
+    .random_sample implements.  Parity with MATLAB itself is unpinned (no
+    MATLAB here).  Returns w (1.0 for the other bonds)."""
+    nb = len(b1)
+    if rule == L.RULE_BOND:
+        mask = bond_label == perccln
+    else:
+        both = (site_label[b1 - 1] == perccln) & (site_label[b2 - 1] == perccln)
+        mask = both if rule == L.RULE_SITE else both & (bond_label == perccln)
+    w = np.ones(nb)
+    w[mask] = np.random.RandomState(seed).random_sample(int(mask.sum()))
+    return w
 
 
 def pb_grid(lattice, nb):

@@ -374,22 +374,26 @@ __global__ void k_canon(int t, const int* parent, const uint8_t* member, int* ca
 
 // ---------------------------------------------------------------------------
 // Kirchhoff assembly (bondc.f:482-538, ConductCalc.m:88-165)
+// w (optional): ConductCalc.m condtype 2, G = -g0*rand for the bonds of the
+// spanning cluster (ConductCalc.m:94-97): per-bond multipliers w[id]
 __device__ __forceinline__ double bond_value(int rule, int id, int s, int c, int ps,
                                              const uint8_t* bocc, const uint8_t* socc,
-                                             int span_root, double g0, double leak) {
+                                             int span_root, double g0, double leak,
+                                             const double* w) {
   bool in;
   if (rule == PERC_RULE_BOND) in = bocc[id] && ps == span_root;
   else if (rule == PERC_RULE_SITE) in = socc[s] && socc[c] && ps == span_root;
   else in = bocc[id] && socc[s] && socc[c] && ps == span_root;
-  return in ? -g0 : -leak;
+  return in ? (w ? -g0 * w[id] : -g0) : -leak;
 }
 
 __global__ void k_assemble(Geom g, int N, const int* bond_first, const uint8_t* bocc,
                            const uint8_t* socc, const int* parent, const int* rowptr,
                            double* val, double* diag, double* rhs, uint16_t* code, int* sflag,
                            StencilForms F, int rule, double g0, double leak, double Va,
-                           int span_root) {
+                           int span_root, const double* w) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i == 0 && w) atomicOr(sflag, 1);  // per-bond values: no two-value stencil code
   if (i >= N) return;
   const int m = g.m, t = g.t, s = i + m + 1;
   const int ps = parent[s];
@@ -405,7 +409,7 @@ __global__ void k_assemble(Geom g, int N, const int* bond_first, const uint8_t* 
       atomicOr(sflag, 1);
       continue;
     }
-    const double gv = bond_value(rule, id, s, c, ps, bocc, socc, span_root, g0, leak);
+    const double gv = bond_value(rule, id, s, c, ps, bocc, socc, span_root, g0, leak, w);
     if (gv == -g0) bits |= 1u << j;
     rowsum = rowsum + gv;
     if (c > m && c <= t - m) val[k++] = gv;
@@ -439,7 +443,8 @@ __global__ void k_assemble(Geom g, int N, const int* bond_first, const uint8_t* 
       const int q = nn[kk];
       if (q <= s) continue;
       if (q > t - m) {
-        const double gv = bond_value(rule, fb + r, s, q, ps, bocc, socc, span_root, g0, leak);
+        const double gv =
+            bond_value(rule, fb + r, s, q, ps, bocc, socc, span_root, g0, leak, w);
         acc = acc - (gv * Va);
       }
       ++r;
@@ -452,7 +457,7 @@ __global__ void k_assemble(Geom g, int N, const int* bond_first, const uint8_t* 
 __global__ void k_currents(Geom g, const int* bond_first, const uint8_t* bocc,
                            const uint8_t* socc, const int* parent, const double* x, int rule,
                            int cur_rule, double g0, double leak, double Va, int span_root,
-                           double thresh, double* iout) {
+                           double thresh, double* iout, const double* w) {
   const int idx = blockIdx.x * blockDim.x + threadIdx.x;
   const int m = g.m, t = g.t;
   if (idx >= 2 * m) return;
@@ -465,7 +470,7 @@ __global__ void k_currents(Geom g, const int* bond_first, const uint8_t* bocc,
   for (int j = 0; j < cnt; ++j) {
     const int c = nbr[j];
     const int id = s < c ? bond_id(g, bond_first, s, c) : bond_id(g, bond_first, c, s);
-    gv[j] = id < 0 ? 0.0 : bond_value(rule, id, s, c, ps, bocc, socc, span_root, g0, leak);
+    gv[j] = id < 0 ? 0.0 : bond_value(rule, id, s, c, ps, bocc, socc, span_root, g0, leak, w);
     rowsum = rowsum + gv[j];
   }
   const double d = -rowsum;
@@ -2765,7 +2770,7 @@ void dev_free_all(perc_ctx* h) {
   void* ptrs[] = {d.bond_first, d.rowptr, d.col, d.val, d.diag, d.rhs, d.code, d.dtab, d.sflag, d.bocc, d.socc,
                   d.order, d.parent, d.member, d.bot, d.top, d.counters, d.x, d.r,
                   d.p0, d.p1, d.q, d.partials, d.tickets, d.scal, d.err_hist, d.iout,
-                  d.res_xch, d.res_part, d.res_bar};
+                  d.res_xch, d.res_part, d.res_bar, d.bw};
   for (void* p : ptrs)
     if (p) hipFree(p);
   d = DeviceBuffers{};
@@ -2931,7 +2936,8 @@ hipError_t dev_assemble(perc_ctx* h, int rule, double g0, double leak, double Va
   HIP_TRY(hipMemsetAsync(d.sflag, 0, 4 * sizeof(int), st));
   k_assemble<<<blocks_for(h->N), kBlock, 0, st>>>(h->g, h->N, d.bond_first, d.bocc, d.socc,
                                                    d.parent, d.rowptr, d.val, d.diag, d.rhs, d.code,
-                                                   d.sflag, h->forms, rule, g0, leak, Va, span_root);
+                                                   d.sflag, h->forms, rule, g0, leak, Va, span_root,
+                                                   h->has_weights ? d.bw : nullptr);
   HIP_TRY(dbg_sync(st, "k_assemble"));
   int flag = 0;
   HIP_TRY(hipMemcpyAsync(&flag, d.sflag, sizeof(int), hipMemcpyDeviceToHost, st));
@@ -3114,7 +3120,7 @@ hipError_t dev_currents(perc_ctx* h, int rule, int cur_rule, double g0, double l
   const int m = h->g.m;
   k_currents<<<blocks_for(2 * m), kBlock, 0, st>>>(h->g, d.bond_first, d.bocc, d.socc, d.parent,
                                                     d.x, rule, cur_rule, g0, leak, Va, span_root,
-                                                    thresh, d.iout);
+                                                    thresh, d.iout, h->has_weights ? d.bw : nullptr);
   HIP_TRY(dbg_sync(st, "k_currents"));
   HIP_TRY(hipMemcpyAsync(iout_host, d.iout, sizeof(double) * 2 * m, hipMemcpyDeviceToHost, st));
   return hipStreamSynchronize(st);
@@ -3130,6 +3136,18 @@ hipError_t dev_spmv(perc_ctx* h, const double* x, double* y) {
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipMemcpyAsync(y, d.q, bytes, hipMemcpyDeviceToHost, st));
   return hipStreamSynchronize(st);
+}
+
+hipError_t dev_set_bond_weights(perc_ctx* h, const double* w) {
+  DeviceBuffers& d = h->d;
+  if (!w) {
+    h->has_weights = false;
+    return hipSuccess;
+  }
+  if (!d.bw) HIP_TRY(dmalloc(&d.bw, (size_t)h->nb + 8));
+  HIP_TRY(hipMemcpy(d.bw, w, sizeof(double) * h->nb, hipMemcpyHostToDevice));
+  h->has_weights = true;
+  return hipSuccess;
 }
 
 hipError_t dev_selftest_division(long long n, unsigned long long seed, unsigned long long* out3) {

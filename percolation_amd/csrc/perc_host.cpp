@@ -732,6 +732,12 @@ int perc_set_march_mode(perc_ctx* h, int mode) {
   return PERC_OK;
 }
 
+int perc_set_bond_weights(perc_ctx* h, const double* w, long long n) {
+  if (!h || (w && n != h->nb)) return PERC_EINVAL;
+  hipSetDevice(h->device);
+  return hip_status(dev_set_bond_weights(h, w), "perc_set_bond_weights");
+}
+
 int perc_march_info(perc_ctx* h, int* out5) {
   if (!h || !out5) return PERC_EINVAL;
   if (!h->assembled) return PERC_ESTATE;

@@ -99,6 +99,7 @@ struct DeviceBuffers {
   double* err_hist = nullptr;   // itmax+2
   int err_hist_cap = 0;
   double* iout = nullptr;       // 2m (boundary-row currents)
+  double* bw = nullptr;         // per-bond conductance multipliers (ConductCalc condtype 2)
   double* res_xch = nullptr;    // resident solve: exchange rows, partials
   double* res_part = nullptr;
   unsigned* res_bar = nullptr;
@@ -159,6 +160,7 @@ struct perc_ctx {
   bool qfree = false;           // march B rebuilds q (52N / iteration)
   bool march_alt = false;       // alternating walk directions
   bool rowmarch = false;        // workgroup row-march kernels (k_cg_rm)
+  bool has_weights = false;     // perc_set_bond_weights: G = -g0 w for the spanning bonds
   bool resident = false;        // persistent resident solve (k_cg_res)
   int res_G = 0, res_H = 0, res_MT = 0, res_HMAX = 0;  // its grid, band height, template
   int rm_w = 0, rm_h = 16;      // their strip width (columns) and band height
@@ -191,6 +193,7 @@ hipError_t dev_currents(perc_ctx* h, int rule, int cur_rule, double g0, double l
                         int span_root, double thresh, double* iout_host);
 hipError_t dev_spmv(perc_ctx* h, const double* x, double* y);
 hipError_t dev_selftest_division(long long n, unsigned long long seed, unsigned long long* out3);
+hipError_t dev_set_bond_weights(perc_ctx* h, const double* w);
 hipError_t dev_bench(perc_ctx* h, int which, int reps, double* ms);
 
 // host replay (perc_replay.cpp): reference label numbering

@@ -582,3 +582,49 @@ def test_resident_solve_matches_march(lat, m, n, pbc, p):
     assert abs(cr["iter"] - cm["iter"]) <= 2
     assert rel(cr["gtop"], cm["gtop"]) < REL and rel(cr["gbot"], cm["gbot"]) < REL
     assert np.max(np.abs(cr["vint"] - cm["vint"])) < 1e-6
+
+
+@pytest.mark.parametrize("kind,rule,lat,m,n,ps,pb", [(PL.BOND, PL.RULE_BOND, 0, 64, 64, 0, 0.6),
+                                                     (PL.SITE, PL.RULE_SITE, 1, 48, 48, 0.6, 0),
+                                                     (PL.SITEBOND, PL.RULE_MIXED, 0, 48, 40,
+                                                      0.9, 0.8)])
+def test_random_conductance_vs_direct_solve(kind, rule, lat, m, n, ps, pb):
+    """ConductCalc.m condtype 2: spanning bonds get -g0*rand (MATLAB twister
+    order: one draw per such bond in bond order).  Solved on the CSR
+    operator; Gtop/Gbot against a direct sparse solve of the oracle system
+    with the same values (parity with MATLAB's own draws unpinned)."""
+    import scipy.sparse as sp
+    import scipy.sparse.linalg as spla
+    t, nb = m * n, api.nbonds(lat, m, n, 0)
+    so, bo = api.shuffled_ids(t, 31), api.shuffled_ids(nb, 32)
+    ts, tb = int(ps * t), int(pb * nb)
+    b1, b2 = api.bond_list(lat, m, n, 0)
+    with api.Context(lat, m, n, 0) as ctx:
+        ctx.occupy(kind, site_order=so if ts else None, nsites=ts,
+                   bond_order=bo if tb else None, nbonds_=tb)
+        if ctx.label()["nspan"] == 0:
+            pytest.skip("no spanning cluster")
+        ln = ctx.label_numbers(kind)
+        bl = ln["bond_label"] if ln["bond_label"] is not None else O.i32(nb)
+        sl = ln["site_label"] if ln["site_label"] is not None else O.i32(t)
+        w = api.conductcalc_weights(rule, b1, b2, bl, sl, ln["perccln"])
+        ctx.set_bond_weights(w)
+        c = ctx.conductance(rule, PL.CUR_MATLAB, tol=1e-14, itmax=400000)
+        assert ctx.matrix_format() == PL.FMT_CSR
+        ctx.set_bond_weights(None)
+        c_fixed = ctx.conductance(rule, PL.CUR_MATLAB, tol=1e-14, itmax=400000)
+    gval = O.f64(nb)
+    O.lib().or_bond_values(rule, nb, b1, b2, np.ascontiguousarray(bl, np.int32),
+                           np.ascontiguousarray(sl, np.int32), ln["perccln"], 1.0, 1e-12, gval)
+    inc = gval == -1.0
+    gval[inc] = -1.0 * w[inc]
+    sa, ija, itemp, diag, k = oracle_system(lat, m, n, 0, b1, b2, gval)
+    N = t - 2 * m
+    rows = np.repeat(np.arange(N), np.diff(ija[:N + 1]))
+    A = sp.csr_matrix((sa[N + 1:k], (rows, ija[N + 1:k] - 1)), shape=(N, N)) + sp.diags(sa[:N])
+    v = spla.spsolve(A.tocsc(), itemp)
+    gt, gb = C.c_double(), C.c_double()
+    O.lib().or_currents(lat, m, n, 0, nb, b1, b2, gval, diag, v, 1.0, 0.0, 1, C.byref(gt),
+                        C.byref(gb))
+    assert rel(c["gtop"], gt.value) < 1e-9 and rel(c["gbot"], gb.value) < 1e-9
+    assert rel(c["gtop"], c_fixed["gtop"]) > 1e-3  # the weights did act
