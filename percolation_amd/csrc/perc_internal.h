@@ -160,6 +160,7 @@ struct perc_ctx {
   bool qfree = false;           // march B rebuilds q (52N / iteration)
   bool march_alt = false;       // alternating walk directions
   bool rowmarch = false;        // workgroup row-march kernels (k_cg_rm)
+  int b_grid = 0;               // streaming B workgroups in the fused formats (2 per CU)
   bool has_weights = false;     // perc_set_bond_weights: G = -g0 w for the spanning bonds
   bool resident = false;        // persistent resident solve (k_cg_res)
   int res_G = 0, res_H = 0, res_MT = 0, res_HMAX = 0;  // its grid, band height, template
