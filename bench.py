@@ -216,6 +216,9 @@ def main():
     ap.add_argument("--ps", type=float, default=0.593, help="site fraction for --kind sitebond")
     ap.add_argument("--full-voltages", action="store_true",
                     help="update x on every row every iteration (perc_set_full_voltages)")
+    ap.add_argument("--concurrent", type=int, default=1,
+                    help="realisations in flight per GPU (one context and stream each); the "
+                         "per-kernel roofline timings then overlap")
     ap.add_argument("--march-mode", type=int, default=-1,
                     help="perc_set_march_mode bits (QFREE 1, ALT 2, ROWS 4); -1: library default")
     ap.add_argument("--format", choices=("auto", "stencil", "stencil_tiled", "stencil_split", "csr"),
@@ -279,16 +282,26 @@ def main():
     torch.cuda.synchronize()
     log("rank %d: %d orders (nb=%d, tbonds=%d) in %.1fs" % (rank, nreal, nb, tb,
                                                             time.perf_counter() - t0))
-    ctx = api.Context(lat, L_, L_, 0, device=local)
-    ctx.set_matrix_format({"auto": P.FMT_AUTO, "stencil": P.FMT_STENCIL,
-                           "stencil_tiled": P.FMT_STENCIL_TILED,
-                           "stencil_split": P.FMT_STENCIL_SPLIT, "csr": P.FMT_CSR}[args.format])
-    ctx.set_full_voltages(args.full_voltages)
-    if args.march_mode >= 0:
-        ctx.set_march_mode(args.march_mode)
+    K = max(1, args.concurrent)
+
+    def make_ctx():
+        c = api.Context(lat, L_, L_, 0, device=local)
+        c.set_matrix_format({"auto": P.FMT_AUTO, "stencil": P.FMT_STENCIL,
+                             "stencil_tiled": P.FMT_STENCIL_TILED,
+                             "stencil_split": P.FMT_STENCIL_SPLIT, "csr": P.FMT_CSR}[args.format])
+        c.set_full_voltages(args.full_voltages)
+        mode = args.march_mode if args.march_mode >= 0 else P.MARCH_DEFAULT
+        if K > 1:  # no concurrent cooperative (resident) launches
+            mode &= ~P._lib.SOLVE_RESIDENT
+        c.set_march_mode(mode)
+        return c
+
+    # K contexts (each its own HIP stream): K realisations in flight per GPU
+    ctxs = [make_ctx() for _ in range(K)]
+    ctx = ctxs[0]
     N, nnz = ctx.system_size()
 
-    def run(k):
+    def run(k, ctx=ctx):
         if args.kind == "bond":
             return ctx.bondc_realisation(None, tb, tol=args.tol, itmax=args.itmax,
                                          device_ptr=orders[k].data_ptr())
@@ -307,18 +320,27 @@ def main():
                     t_total_ms=(t_2 - t_0) * 1e3)
 
     for k in range(args.warmup):
-        r = run(k)
+        r = run(k, ctxs[k % K])
         log("warmup %d: iter=%d Gtop=%.12g %.0f ms" % (k, r["iter"], r["gtop"], r["t_total_ms"]))
-    ctx.set_kernel_timing(True)
-    ctx.kernel_stats(reset=True)
+    for c in ctxs:
+        c.set_kernel_timing(True)
+        c.kernel_stats(reset=True)
     if use_dist:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    results = []
-    for k in range(args.warmup, nreal):
-        r = run(k)
-        results.append(r)
+    timed = list(range(args.warmup, nreal))
+    if K == 1:
+        results = [run(k) for k in timed]
+    else:  # one host thread per context (ctypes drops the GIL in libperc calls)
+        from concurrent.futures import ThreadPoolExecutor
+        lanes = [[k for k in timed if (k - args.warmup) % K == ci] for ci in range(K)]
+        with ThreadPoolExecutor(K) as pool:
+            futs = [pool.submit(lambda ks_, c_: [run(k_, c_) for k_ in ks_], lanes[ci], ctxs[ci])
+                    for ci in range(K)]
+            per = [f.result() for f in futs]
+        results = [per[(k - args.warmup) % K][(k - args.warmup) // K] for k in timed]
+    for k, r in zip(timed, results):
         log("step %d (ii=%d): nspan=%d iter=%d Gtop=%.12g Gbot=%.12g label %.0f ms solve %.0f ms "
             "total %.0f ms" % (k - args.warmup, ii_list[k] + 1, r["nspan"], r["iter"], r["gtop"],
                                r["gbot"], r["t_label_ms"], r["t_solve_ms"], r["t_total_ms"]))
@@ -327,6 +349,9 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     ks = ctx.kernel_stats(reset=True)
+    for c in ctxs[1:]:
+        for key_, v_ in c.kernel_stats(reset=True).items():
+            ks[key_] += v_
     # ensemble statistics: the only collective (RCCL all-reduce over xGMI)
     stats, tmax = ensemble.allreduce(ensemble.local_stats(results), elapsed, device=dev)
     nsolves = int(stats[0])
@@ -423,14 +448,17 @@ def main():
                    "lattice": args.lattice, "kind": args.kind,
                    "L": L_, "p": p, "rows": N, "nnz_offdiag": nnz,
                    "full_voltages": bool(args.full_voltages), "parallelism":
-                   "realisations sharded over %d GPU(s), RCCL stats all-reduce" % world},
+                   "realisations sharded over %d GPU(s), RCCL stats all-reduce" % world,
+                   "concurrent_per_gpu": K},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS,
                      "unit": "GB/s", "frac": round(achieved / PEAK_HBM_GBS, 4),
                      "traffic": traffic, "traffic_source": traffic_src,
                      "kernel": kern[dom]["kernel"], "format": fmt,
                      "bytes_per_launch": kern[dom]["bytes_per_launch"],
                      "avg_launch_ms": kern[dom]["avg_launch_ms"],
-                     "launches": kern[dom]["launches"]},
+                     "launches": kern[dom]["launches"],
+                     **({"note": "%d realisations in flight per GPU: kernel durations overlap"
+                                 % K} if K > 1 else {})},
         "cg_iterations_mean": round(float(stats[4]) / max(nsolves, 1), 1),
         "spanning_fraction": round(float(stats[3]) / max(nsolves, 1), 3),
         "gtop_mean": float(stats[1]) / max(nsolves, 1),
@@ -448,7 +476,8 @@ def main():
                                                results[0]["iter"], args.cpu_iters)
         except Exception as e:  # keep the GPU line even if the host is short of memory
             out["cpu_baseline"] = {"value": None, "error": repr(e)}
-    ctx.close()
+    for c in ctxs:
+        c.close()
     if rank == 0:
         print(json.dumps(out), flush=True)
     if use_dist:
