@@ -628,3 +628,52 @@ def test_random_conductance_vs_direct_solve(kind, rule, lat, m, n, ps, pb):
                         C.byref(gb))
     assert rel(c["gtop"], gt.value) < 1e-9 and rel(c["gbot"], gb.value) < 1e-9
     assert rel(c["gtop"], c_fixed["gtop"]) > 1e-3  # the weights did act
+
+
+# ------------------------------------------------------------ edge cases
+@pytest.mark.parametrize("kind,lat,pbc", [(PL.BOND, 0, 0), (PL.SITE, 1, 1), (PL.SITEBOND, 0, 1)])
+def test_empty_occupancy_is_not_spanning(kind, lat, pbc):
+    """Nothing occupied: no cluster spans, the conductance is G = 0 with
+    status 1 (bond_cond.f:484-487), no solve runs."""
+    m = n = 64
+    with api.Context(lat, m, n, pbc) as ctx:
+        ctx.occupy(kind, site_order=np.zeros(1, np.int32), nsites=0,
+                   bond_order=np.zeros(1, np.int32), nbonds_=0)
+        li = ctx.label()
+        assert li["nspan"] == 0
+        c = ctx.conductance(PL.RULE_BOND if kind == PL.BOND else PL.RULE_MIXED)
+        assert c["status"] == 1 and c["gtop"] == 0.0 and c["iter"] == 0
+
+
+@pytest.mark.parametrize("m,n,pbc", [(1024, 1024, 0), (1024, 1024, 1), (2048, 512, 0),
+                                     (256, 2000, 1)])
+def test_full_square_lattice_analytic(m, n, pbc):
+    """Every bond occupied (a maximum-size cluster): each row is an
+    equipotential, so G = m / (n - 1) exactly (horizontal bonds carry no
+    current); resident, march and pbc paths alike."""
+    nb = api.nbonds(0, m, n, pbc)
+    with api.Context(0, m, n, pbc) as ctx:
+        ctx.occupy(PL.BOND, bond_order=np.arange(1, nb + 1, dtype=np.int32), nbonds_=nb)
+        li = ctx.label()
+        assert li["nspan"] == 1
+        c = ctx.conductance(tol=1e-13, itmax=10 ** 6)
+    want = m / (n - 1)
+    assert rel(c["gtop"], want) < 1e-9 and rel(c["gbot"], want) < 1e-9
+
+
+@pytest.mark.parametrize("lat,m,n,pbc", [(1, 64, 64, 0), (1, 64, 64, 1), (0, 3, 3, 0),
+                                         (0, 3, 4, 0), (1, 4, 4, 0), (0, 4, 3, 1)])
+def test_full_and_tiny_lattices_vs_oracle(lat, m, n, pbc):
+    """Fully occupied triangular lattices and the smallest lattices libperc
+    takes (m, n >= 3, even m on the triangular lattice: one or two interior
+    rows, 3-4 columns): GPU solve vs
+    the oracle's literal linbcg on the same system."""
+    b1, b2 = api.bond_list(lat, m, n, pbc)
+    nb = len(b1)
+    with api.Context(lat, m, n, pbc) as ctx:
+        ctx.occupy(PL.BOND, bond_order=np.arange(1, nb + 1, dtype=np.int32), nbonds_=nb)
+        assert ctx.label()["nspan"] == 1
+        c = ctx.conductance(tol=1e-14, itmax=100000)
+    oc = O.conductance(lat, m, n, pbc, b1, b2, -np.ones(nb), tol=1e-14, itmax=100000)
+    assert rel(c["gtop"], oc["gtop"]) < REL and rel(c["gbot"], oc["gbot"]) < REL
+    assert abs(c["iter"] - oc["iter"]) <= 1

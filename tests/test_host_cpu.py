@@ -247,3 +247,11 @@ def test_pb_grid_matches_reference_rows():
                 break
             want.append((bf, float(np.float32(np.float32(bf) / np.float32(nb)))))
         assert ["%11.9f" % x for _, x in want] == ["%11.9f" % x for x in first_trial]
+
+
+def test_degenerate_lattice_is_rejected():
+    """m or n below 3 (no interior row or column to solve for) is refused
+    with PERC_EINVAL, before any device is touched."""
+    for m, n in [(2, 3), (3, 2), (1, 1)]:
+        with pytest.raises(P.PercError, match="PERC_EINVAL"):
+            api.Context(0, m, n, 0)
