@@ -252,11 +252,18 @@ int perc_set_march_rows(perc_ctx *h, int rows);
    share are read at the same moment (cache hits).  Per-row arithmetic is
    unchanged in every mode (bitwise the same values); the dot products are
    summed in a different association.  The mode is read when the system is
-   assembled; default PERC_MARCH_DEFAULT. */
+   assembled; default PERC_MARCH_DEFAULT.  PERC_MARCH_STRIPS: for the
+   solve, r, p, q and the row codes are kept strip-major (each 128-column
+   strip of the lattice contiguous, rows of a strip 1 KB apart), so every
+   wave of the per-wave march walks one contiguous stream; x stays
+   row-major.  Measured at L = 4096: march 0.118 vs 0.111 ms row-major
+   (although the pure access pattern streams 8 % faster strip-major,
+   tools/mix_bench.hip), so it is not in the default. */
 #define PERC_MARCH_QFREE 1
 #define PERC_MARCH_ALT 2
 #define PERC_MARCH_ROWS 4
 #define PERC_SOLVE_RESIDENT 8
+#define PERC_MARCH_STRIPS 16
 #define PERC_MARCH_DEFAULT (PERC_MARCH_ALT | PERC_SOLVE_RESIDENT)
 int perc_set_march_mode(perc_ctx *h, int mode);
 /* Random bond conductances (MATLAB/ConductCalc.m condtype 2, :38-47 and

@@ -884,6 +884,7 @@ struct CGArgs {
   int kiter;      // the launch's CG iteration (fused PS kernels; host-counted)
   int march_alt;  // march kernels: odd bands walk up in P, even bands in B
   int bx;         // the streaming B applies x += ak p(k) (P and k_cg_xfinal do not)
+  int sm;         // r, p, q, code strip-major (march solve, PERC_MARCH_STRIPS); x row-major
   double* q;
   double* partials;  // kRedSlots slots of pstride doubles
   unsigned* tickets; // kRedSlots slots of tstride counters
@@ -908,6 +909,18 @@ __device__ __forceinline__ double2 diag2(const CGArgs& a, int i) {
 template <bool ST>
 __device__ __forceinline__ double diag1(const CGArgs& a, int i) {
   return ST ? code_diag(a.St.code[i], a.St.ng0, a.St.nleak) : a.A.diag[i];
+}
+
+// Strip-major layout (PERC_MARCH_STRIPS): the interior lattice of nrows x m
+// in strips of kStripW columns, each strip contiguous (rows kStripW
+// elements apart), so a march wave's band is one contiguous stream.
+constexpr int kStripW = 128;  // = kMarchW
+__device__ __forceinline__ int sm_at(const TileGeom& T, int gr, int col) {
+  return ((col / kStripW) * T.nrows + gr) * kStripW + (col % kStripW);
+}
+__device__ __forceinline__ int sm_index(const TileGeom& T, int i) {  // from row-major i
+  const int gr = i / T.m;
+  return sm_at(T, gr, i - gr * T.m);
 }
 
 // contiguous, even-aligned pair range of the logical block (16 B accesses)
@@ -1037,9 +1050,12 @@ __global__ __launch_bounds__(kBlock) void k_cg_b(CGArgs a) {
     const double* __restrict__ pk = a.pb[k & 1];
     const int xr = a.xrows == 0 ? N : a.xrows;
     const int i0 = 2 * q0, i1 = min(2 * q1, N);
-    for (int i = i0 + threadIdx.x; i < min(i1, xr); i += kBlock) a.x[i] = a.x[i] + ak * pk[i];
+    // x is row-major; in the strip-major solve p(k) is read through the map
+    // (the x rows are logical ranges handed out like the pair chunks)
+    auto pat = [&](int i) { return a.sm ? pk[sm_index(a.T, i)] : pk[i]; };
+    for (int i = i0 + threadIdx.x; i < min(i1, xr); i += kBlock) a.x[i] = a.x[i] + ak * pat(i);
     if (a.xrows != 0)
-      for (int i = max(i0, max(N - xr, xr)) + threadIdx.x; i < i1; i += kBlock) a.x[i] = a.x[i] + ak * pk[i];
+      for (int i = max(i0, max(N - xr, xr)) + threadIdx.x; i < i1; i += kBlock) a.x[i] = a.x[i] + ak * pat(i);
   }
   // kBU pairs per thread in flight: every load of a batch is issued before
   // the first store (the compiler will not move loads of r above a store
@@ -1426,21 +1442,26 @@ struct MGeom {
   bool hok;
 };
 
-template <int MODE>
+// element (row gr, column col) in the solve's layout
+template <bool SM>
+__device__ __forceinline__ int midx(const CGArgs& a, int gr, int col) {
+  return SM ? sm_at(a.T, gr, col) : gr * a.T.m + col;
+}
+
+template <int MODE, bool SM>
 __device__ __forceinline__ void march_load(const CGArgs& a, const MGeom& g, int gr, bool first,
                                            const double* __restrict__ psrc, MRow& R) {
   R.p = R.r = make_double2(0.0, 0.0);
   R.c = R.hc = 0u;
   R.hp = R.hr = 0.0;
-  const int m = a.T.m;
   if (gr >= 0 && gr < a.T.nrows) {
-    const int i = gr * m + g.col;
+    const int i = midx<SM>(a, gr, g.col);
     R.c = *reinterpret_cast<const unsigned*>(a.St.code + i);
     if (MODE != kMarchB || (gr >= g.r0 && gr < g.rend))
       R.r = *reinterpret_cast<const double2*>(a.r + i);
     if (!first) R.p = *reinterpret_cast<const double2*>(psrc + i);
     if (g.hok) {
-      const int hi = gr * m + g.hcol;
+      const int hi = midx<SM>(a, gr, g.hcol);
       if (MODE != kMarchB) {
         R.hc = a.St.code[hi];
         R.hr = a.r[hi];
@@ -1458,14 +1479,14 @@ struct MState {
 
 // one step: row gr enters the window, then the middle row (gr -+ 1) is
 // finished when it is one of the band's own rows
-template <int MODE, bool UP>
+template <int MODE, bool UP, bool SM>
 __device__ __forceinline__ void march_step(const CGArgs& a, const MGeom& g, const MRow& R, int gr,
                                            bool first, double bk, double ak,
                                            double* __restrict__ pnew, const double2* s_dt,
                                            const unsigned* s_rpos, const unsigned* s_rmap,
                                            double* s_w, MState& W, double (&acc)[2]) {
   const int lane = threadIdx.x & 63;
-  const int m = a.T.m, nrows = a.T.nrows, N = a.St.N;
+  const int nrows = a.T.nrows, N = a.St.N;
   const double ng0 = a.St.ng0, nleak = a.St.nleak;
   double2 pn = make_double2(0.0, 0.0);
   double hpn = 0.0;
@@ -1490,9 +1511,9 @@ __device__ __forceinline__ void march_step(const CGArgs& a, const MGeom& g, cons
         hpn = first ? zh : bk * R.hp + zh;
       }
       if (gr >= g.r0 && gr < g.rend) {  // own row
-        const int i = gr * m + g.col;
+        const int i = midx<SM>(a, gr, g.col);
         st2(pnew + i, pn, true);
-        if (!first && !a.bx && (a.xrows == 0 || i < a.xrows || i >= N - a.xrows)) {
+        if (!SM && !first && !a.bx && (a.xrows == 0 || i < a.xrows || i >= N - a.xrows)) {
           double2 xv = *reinterpret_cast<const double2*>(a.x + i);
           xv.x = xv.x + ak * R.p.x;
           xv.y = xv.y + ak * R.p.y;
@@ -1556,7 +1577,7 @@ __device__ __forceinline__ void march_step(const CGArgs& a, const MGeom& g, cons
         q1 = march_q_gen<1>(c1w, dM1.x, W.C.e1, s_rpos[f1], s_w, lane, ng0, nleak);
       }
     }
-    const int i = mid * m + g.col;
+    const int i = midx<SM>(a, mid, g.col);
     if (MODE == kMarchB) {
       // k_cg_b's per-pair arithmetic
       double2 rn;
@@ -1576,7 +1597,7 @@ __device__ __forceinline__ void march_step(const CGArgs& a, const MGeom& g, cons
   }
 }
 
-template <int MODE, int D, bool UP>
+template <int MODE, int D, bool UP, bool SM>
 __device__ __forceinline__ void march_walk(const CGArgs& a, const MGeom& g, MRow (&ring)[D],
                                            bool first, double bk, double ak,
                                            const double* __restrict__ psrc,
@@ -1597,15 +1618,15 @@ __device__ __forceinline__ void march_walk(const CGArgs& a, const MGeom& g, MRow
       if (j < nsteps) {
         const MRow R = ring[u];
         if (j + D < nsteps)
-          march_load<MODE>(a, g, UP ? g.rend - (j + D) : g.r0 - 1 + j + D, first, psrc, ring[u]);
-        march_step<MODE, UP>(a, g, R, UP ? g.rend - j : g.r0 - 1 + j, first, bk, ak, pnew, s_dt,
+          march_load<MODE, SM>(a, g, UP ? g.rend - (j + D) : g.r0 - 1 + j + D, first, psrc, ring[u]);
+        march_step<MODE, UP, SM>(a, g, R, UP ? g.rend - j : g.r0 - 1 + j, first, bk, ak, pnew, s_dt,
                              s_rpos, s_rmap, s_w, W, acc);
       }
     }
   }
 }
 
-template <int MODE, int D = kMarchDepth>
+template <int MODE, bool SM = false, int D = kMarchDepth>
 __global__ __launch_bounds__(64 * kMarchWaves) void k_cg_march(CGArgs a) {
   CGScalars* S = a.S;
   __shared__ double s_red[32];
@@ -1645,7 +1666,7 @@ __global__ __launch_bounds__(64 * kMarchWaves) void k_cg_march(CGArgs a) {
   if (active) {
 #pragma unroll
     for (int u = 0; u < D; ++u)
-      if (u < nsteps) march_load<MODE>(a, g, up ? g.rend - u : g.r0 - 1 + u, first, psrc, ring[u]);
+      if (u < nsteps) march_load<MODE, SM>(a, g, up ? g.rend - u : g.r0 - 1 + u, first, psrc, ring[u]);
   }
   if (S->done) return;
   if (threadIdx.x < kMaxForms) {
@@ -1658,8 +1679,8 @@ __global__ __launch_bounds__(64 * kMarchWaves) void k_cg_march(CGArgs a) {
   double acc[2] = {0.0, 0.0};
   if (active) {
     double* s_w = s_win[threadIdx.x >> 6];
-    if (up) march_walk<MODE, D, true>(a, g, ring, first, bk, ak, psrc, pnew, s_dt, s_rpos, s_rmap, s_w, acc);
-    else march_walk<MODE, D, false>(a, g, ring, first, bk, ak, psrc, pnew, s_dt, s_rpos, s_rmap, s_w, acc);
+    if (up) march_walk<MODE, D, true, SM>(a, g, ring, first, bk, ak, psrc, pnew, s_dt, s_rpos, s_rmap, s_w, acc);
+    else march_walk<MODE, D, false, SM>(a, g, ring, first, bk, ak, psrc, pnew, s_dt, s_rpos, s_rmap, s_w, acc);
   }
   if (MODE != kMarchB) {
     double v[1] = {acc[0]}, tot[1];
@@ -2466,6 +2487,16 @@ __global__ void k_zero(double* v, long long n) {
   if (i < n) v[i] = 0.0;
 }
 
+// row-major -> strip-major copies of the solve's inputs (r after k_cg_init,
+// the row codes), once per solve: one row segment of a strip per wave
+template <typename E>
+__global__ __launch_bounds__(kBlock) void k_to_strips(TileGeom T, const E* __restrict__ src,
+                                                       E* __restrict__ dst) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (long long)T.nrows * T.m) return;
+  dst[sm_index(T, (int)i)] = src[i];
+}
+
 // workgroups of the largest reduction (CG kernels or the tiled kernel)
 int red_grid(const perc_ctx* h) { return std::max({h->grid, h->tile_grid, h->march_grid_max}); }
 
@@ -2487,6 +2518,7 @@ CGArgs make_cg_args(perc_ctx* h) {
   a.kiter = 1;
   a.march_alt = h->march_alt ? 1 : 0;
   a.bx = (h->march || h->rowmarch) && !h->qfree ? 1 : 0;
+  a.sm = 0;  // dev_solve / dev_bench switch to the strip-major copies
   a.xrows = h->full_voltages || h->g.m <= 0 ? 0 : h->g.m;  // see dev_solve
   a.pstride = red_partials_size(red_grid(h));
   a.tstride = red_tickets_size(red_grid(h));
@@ -2526,6 +2558,7 @@ void launch_cg_spmv(perc_ctx* h, const CGArgs& a, int G) {
     }
     if (h->march) {
       if (h->qfree) k_cg_march<kMarchP><<<h->march_grid, 64 * kMarchWaves, 0, st>>>(a);
+      else if (a.sm) k_cg_march<kMarchPQ, true><<<h->march_grid, 64 * kMarchWaves, 0, st>>>(a);
       else k_cg_march<kMarchPQ><<<h->march_grid, 64 * kMarchWaves, 0, st>>>(a);
       return;
     }
@@ -2779,7 +2812,7 @@ void dev_free_all(perc_ctx* h) {
   void* ptrs[] = {d.bond_first, d.rowptr, d.col, d.val, d.diag, d.rhs, d.code, d.dtab, d.sflag, d.bocc, d.socc,
                   d.order, d.parent, d.member, d.bot, d.top, d.counters, d.x, d.r,
                   d.p0, d.p1, d.q, d.partials, d.tickets, d.scal, d.err_hist, d.iout,
-                  d.res_xch, d.res_part, d.res_bar, d.bw};
+                  d.res_xch, d.res_part, d.res_bar, d.bw, d.code_sm};
   for (void* p : ptrs)
     if (p) hipFree(p);
   d = DeviceBuffers{};
@@ -2937,6 +2970,25 @@ void select_format(perc_ctx* h) {
                 (h->march_mode & PERC_SOLVE_RESIDENT) && h->march_rows_req == 0;
   h->qfree = (h->march || h->rowmarch) && (h->march_mode & PERC_MARCH_QFREE);
   h->march_alt = (h->march || h->rowmarch) && (h->march_mode & PERC_MARCH_ALT);
+  // strip-major solve: the per-wave march with the streaming B (x in B)
+  h->strips = h->march && !h->qfree && (h->march_mode & PERC_MARCH_STRIPS);
+}
+
+// strip-major copies of r (into the q buffer: r and q swap roles for the
+// solve) and of the row codes; a switches to them
+hipError_t to_strips(perc_ctx* h, CGArgs& a) {
+  DeviceBuffers& d = h->d;
+  hipStream_t st = h->stream;
+  if (!d.code_sm) HIP_TRY(dmalloc(&d.code_sm, (size_t)h->N + 8));
+  const long long n = (long long)a.T.nrows * a.T.m;
+  k_to_strips<uint16_t><<<blocks_for(n), kBlock, 0, st>>>(a.T, d.code, d.code_sm);
+  k_to_strips<double><<<blocks_for(n), kBlock, 0, st>>>(a.T, d.r, d.q);
+  HIP_TRY(dbg_sync(st, "k_to_strips"));
+  a.r = d.q;
+  a.q = d.r;
+  a.St.code = d.code_sm;
+  a.sm = 1;
+  return hipSuccess;
 }
 
 hipError_t dev_assemble(perc_ctx* h, int rule, double g0, double leak, double Va, int span_root) {
@@ -3048,6 +3100,7 @@ hipError_t dev_solve(perc_ctx* h, int itol, double tol, int itmax, bool x0_zero,
   else k_cg_init<false><<<G, kBlock, 0, st>>>(a, itol, x0_zero ? 1 : 0);
   HIP_TRY(dbg_sync(st, "k_cg_init"));
   if (h->resident) return dev_solve_resident(h, a, iter, err);
+  if (h->strips) HIP_TRY(to_strips(h, a));
   // iterate in chunks; the device flag makes surplus launches no-ops
   int chunk = 8;
   CGScalars* hsp = nullptr;
@@ -3185,6 +3238,8 @@ hipError_t dev_bench(perc_ctx* h, int which, int reps, double* ms) {
   hs.itmax = 1 << 30;
   hs.iter = 1;
   a.kiter = 2;
+  // the solve's layout for the CG kernels (the plain SpMV probe stays row-major)
+  if (h->strips && (which == 1 || which == 2 || which == 5)) HIP_TRY(to_strips(h, a));
   HIP_TRY(hipMemcpyAsync(d.scal, &hs, sizeof(hs), hipMemcpyHostToDevice, st));
   HIP_TRY(hipMemsetAsync(d.tickets, 0, kRedSlots * red_tickets_size(red_grid(h)) * sizeof(unsigned),
                          st));

@@ -725,7 +725,8 @@ int perc_set_march_rows(perc_ctx* h, int rows) {
 }
 
 int perc_set_march_mode(perc_ctx* h, int mode) {
-  if (!h || mode < 0 || mode > (PERC_MARCH_QFREE | PERC_MARCH_ALT | PERC_MARCH_ROWS | PERC_SOLVE_RESIDENT))
+  if (!h || mode < 0 || mode > (PERC_MARCH_QFREE | PERC_MARCH_ALT | PERC_MARCH_ROWS | PERC_SOLVE_RESIDENT |
+                                 PERC_MARCH_STRIPS))
     return PERC_EINVAL;
   h->march_mode = mode;
   if (h->assembled) select_format(h);

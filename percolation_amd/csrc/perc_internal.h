@@ -75,6 +75,7 @@ struct DeviceBuffers {
   // slot j carries -g0, else -leak) | count << 8 | form << 11; sflag[0] != 0
   // if some slot has no bond (1) or a row matches no form (2)
   uint16_t* code = nullptr;  // N (+pad)
+  uint16_t* code_sm = nullptr;  // strip-major copy of code (PERC_MARCH_STRIPS solves)
   double2* dtab = nullptr;    // 512: the diagonal of every code (see diag_idx)
   int* sflag = nullptr;      // 4
   // occupancy
@@ -159,6 +160,7 @@ struct perc_ctx {
   int march_mode = PERC_MARCH_DEFAULT;  // perc_set_march_mode
   bool qfree = false;           // march B rebuilds q (52N / iteration)
   bool march_alt = false;       // alternating walk directions
+  bool strips = false;          // march solve in the strip-major layout
   bool rowmarch = false;        // workgroup row-march kernels (k_cg_rm)
   int b_grid = 0;               // streaming B workgroups in the fused formats (2 per CU)
   bool has_weights = false;     // perc_set_bond_weights: G = -g0 w for the spanning bonds
