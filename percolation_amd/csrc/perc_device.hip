@@ -2497,6 +2497,10 @@ __global__ __launch_bounds__(kBlock) void k_to_strips(TileGeom T, const E* __res
   dst[sm_index(T, (int)i)] = src[i];
 }
 
+// a vector larger than this does not stay in the 256 MB Infinity Cache
+// between kernels (L = 8192: 537 MB; L = 4096: 134 MB)
+constexpr size_t kLargeVector = (size_t)256 << 20;
+
 // workgroups of the largest reduction (CG kernels or the tiled kernel)
 int red_grid(const perc_ctx* h) { return std::max({h->grid, h->tile_grid, h->march_grid_max}); }
 
@@ -2578,10 +2582,8 @@ void launch_cg_spmv(perc_ctx* h, const CGArgs& a, int G) {
 
 // B(k) (streaming; the fused format walks its chunks in reverse)
 void launch_cg_b(perc_ctx* h, const CGArgs& a, int G) {
-  // fused formats: two long-lived streaming workgroups per CU instead of
-  // one 8-pair batch per thread (L = 4096: 0.063 vs 0.069 ms; 256, 384,
-  // 768, 1024 and 2048 workgroups measured 0.069-0.079)
-  if (h->fused && h->b_grid > 0 && h->b_grid < G) G = h->b_grid;
+  // fused formats: b_grid (set with the lattice, see dev_build_lattice)
+  if (h->fused && h->b_grid > 0) G = h->b_grid;
   if (h->rowmarch && h->qfree) {
     const dim3 g(h->rm_grid), b(h->rm_w / 4);
     if (h->rm_w == 2048) k_cg_rm<kMarchB, 2048><<<g, b, 0, h->stream>>>(a);
@@ -2752,11 +2754,9 @@ hipError_t dev_build_lattice(perc_ctx* h) {
   HIP_TRY(dmalloc(&d.p1, nv));
   HIP_TRY(dmalloc(&d.q, nv));
   h->grid = cg_grid(N);
-  {
-    int cus = 0;
-    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, h->device) == hipSuccess)
-      h->b_grid = 2 * cus;
-  }
+  int cus = 0;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, h->device) != hipSuccess)
+    cus = 0;
   h->tile_h = kTileHMax;
   while (h->tile_h > 8 && cdiv(std::max(g.n - 2, 0), h->tile_h) * cdiv(g.m, kTileW) < kMinTiles)
     h->tile_h /= 2;
@@ -2767,6 +2767,17 @@ hipError_t dev_build_lattice(perc_ctx* h) {
       g.m % kMarchW == 0 && g.n > 2 ? cdiv((g.m / kMarchW) * (g.n - 2), kMarchWaves) : 0;
   march_geometry(h);
   res_geometry(h);
+  // grid of the streaming B in the fused formats.  Vectors that fit the
+  // 256 MB Infinity Cache (L <= 4096): two long-lived workgroups per CU
+  // (L = 4096: 0.063 vs 0.069 ms for 8192 short ones; 256 .. 2048 long
+  // ones 0.069-0.079).  Larger vectors: short workgroups of 2 pairs per
+  // thread, dispatched in address order, so the accesses in flight stay
+  // in a narrow window of the arrays (L = 8192: 0.312 ms vs 0.361 with
+  // 512, 0.334 with 16384); the partials buffer bounds the grid
+  if ((size_t)N * sizeof(double) > kLargeVector)
+    h->b_grid = std::min<long long>(cdiv((long long)N, 4ll * kBlock), red_grid(h));
+  else
+    h->b_grid = std::min(2 * cus, h->grid);
   if (h->res_G > 0) {
     HIP_TRY(dmalloc(&d.res_xch, (size_t)2 * h->res_G * 2 * 2 * g.m));
     HIP_TRY(dmalloc(&d.res_part, (size_t)2 * 3 * h->res_G));
@@ -2905,7 +2916,10 @@ void march_geometry(perc_ctx* h) {
   if (h->march_rows_req > 0) {
     h->march_h = h->march_rows_req;
   } else {
-    h->march_h = 32;
+    // vectors past the Infinity Cache: 16-row bands, i.e. several rounds
+    // of resident waves, each over a narrower window of the arrays (L =
+    // 8192: 0.423 vs 0.451 ms with 32 rows; at L = 4096 32 rows stay best)
+    h->march_h = (size_t)g.m * nrows * sizeof(double) > kLargeVector ? 16 : 32;
     while (h->march_h > 2 && (long long)spr * cdiv(nrows, h->march_h) < kMarchMinWaves)
       h->march_h /= 2;
   }

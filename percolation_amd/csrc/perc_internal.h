@@ -162,7 +162,7 @@ struct perc_ctx {
   bool march_alt = false;       // alternating walk directions
   bool strips = false;          // march solve in the strip-major layout
   bool rowmarch = false;        // workgroup row-march kernels (k_cg_rm)
-  int b_grid = 0;               // streaming B workgroups in the fused formats (2 per CU)
+  int b_grid = 0;               // streaming B workgroups in the fused formats (dev_build_lattice)
   bool has_weights = false;     // perc_set_bond_weights: G = -g0 w for the spanning bonds
   bool resident = false;        // persistent resident solve (k_cg_res)
   int res_G = 0, res_H = 0, res_MT = 0, res_HMAX = 0;  // its grid, band height, template
