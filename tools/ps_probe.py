@@ -36,6 +36,8 @@ def main():
         order = (np.random.default_rng(seed).permutation(nb)[:tb] + 1).astype(np.int32)
         with api.Context(0, L_, L_, 0) as ctx:
             ctx.set_march_rows(a.march_rows)
+            if os.environ.get("PERC_MODE"):
+                ctx.set_march_mode(int(os.environ["PERC_MODE"]))
             t0 = time.perf_counter()
             r = ctx.bondc_realisation(order, tb, tol=1e-8, itmax=a.itmax)
             t1 = time.perf_counter()
