@@ -481,6 +481,39 @@ def test_full_size_properties(L_, p):
         assert abs(c["gtop"] - c["gbot"]) < 1e-8
 
 
+def test_headline_size_properties():
+    """BASELINE metric size (4096^2 bond, p = 0.6, uniform order as bench.py,
+    reference settings tol 1e-8, itol 2): the default march solve and the
+    LDS-tiled kernels (another q.p association) agree on the iteration
+    count within 1 and on Gtop to the solver's tolerance; the recomputed
+    true residual of the returned voltages meets the tolerance; the two
+    terminal currents agree to the tolerance's precision."""
+    L_, p = 4096, 0.6
+    nb = api.nbonds(0, L_, L_, 0)
+    seed = int(api.trial_seeds(58302, 1)[0])
+    order = (np.random.default_rng(seed).permutation(nb)[:int(p * nb)] + 1).astype(np.int32)
+    out = {}
+    with api.Context(0, L_, L_, 0) as ctx:
+        ctx.occupy(PL.BOND, bond_order=order, nbonds_=len(order))
+        assert ctx.label()["nspan"] >= 1
+        for fmt in (PL.FMT_STENCIL, PL.FMT_STENCIL_TILED):
+            ctx.set_matrix_format(fmt)
+            out[fmt] = ctx.conductance(tol=1e-8, itmax=10 ** 6, vint=fmt == PL.FMT_STENCIL)
+            assert ctx.matrix_format() == fmt
+        s = ctx.system()
+    c, t = out[PL.FMT_STENCIL], out[PL.FMT_STENCIL_TILED]
+    assert c["err"] <= 1e-8 and t["err"] <= 1e-8
+    assert abs(c["iter"] - t["iter"]) <= 1
+    assert rel(c["gtop"], t["gtop"]) < 1e-6 and rel(c["gbot"], t["gbot"]) < 1e-6
+    assert rel(c["gtop"], c["gbot"]) < 1e-5
+    N = L_ * L_ - 2 * L_
+    rows = np.repeat(np.arange(N, dtype=np.int32), np.diff(s["rowptr"]))
+    ax = s["diag"] * c["vint"] + np.bincount(rows, weights=s["val"] * c["vint"][s["col"]],
+                                             minlength=N)
+    res = np.sqrt(np.sum((s["rhs"] - ax) ** 2)) / np.sqrt(np.sum((s["rhs"] / s["diag"]) ** 2))
+    assert res < 2e-8
+
+
 MARCH_MODES = (PL.MARCH_DEFAULT, 0, PL.MARCH_QFREE, PL.MARCH_ALT, PL.MARCH_ROWS,
                PL.MARCH_ROWS | PL.MARCH_QFREE, PL.MARCH_ROWS | PL.MARCH_ALT,
                PL.MARCH_ROWS | PL.MARCH_QFREE | PL.MARCH_ALT, PL.MARCH_STRIPS,
