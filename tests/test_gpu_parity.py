@@ -514,6 +514,32 @@ def test_headline_size_properties():
     assert res < 2e-8
 
 
+def test_large_vector_grids_8192():
+    """8192^2 (config 5 size; vectors past the Infinity Cache, so 16-row
+    march bands and the short in-order B grid): the fused march solve
+    against the split kernels (fixed 8192-workgroup grid, another dot
+    association): iteration count within 1, Gtop/Gbot to the tolerance,
+    current conserved."""
+    L_, p = 8192, 0.9
+    nb = api.nbonds(0, L_, L_, 0)
+    order = (np.random.default_rng(77).permutation(nb)[:int(p * nb)] + 1).astype(np.int32)
+    out = {}
+    with api.Context(0, L_, L_, 0) as ctx:
+        ctx.occupy(PL.BOND, bond_order=order, nbonds_=len(order))
+        assert ctx.label()["nspan"] >= 1
+        for fmt in (PL.FMT_STENCIL, PL.FMT_STENCIL_SPLIT):
+            ctx.set_matrix_format(fmt)
+            out[fmt] = ctx.conductance(tol=1e-8, itmax=10 ** 6)
+            assert ctx.matrix_format() == fmt
+            if fmt == PL.FMT_STENCIL:
+                assert ctx.march_info()["band_rows"] == 16
+    c, t = out[PL.FMT_STENCIL], out[PL.FMT_STENCIL_SPLIT]
+    assert c["err"] <= 1e-8 and t["err"] <= 1e-8
+    assert abs(c["iter"] - t["iter"]) <= 1
+    assert rel(c["gtop"], t["gtop"]) < 1e-6 and rel(c["gbot"], t["gbot"]) < 1e-6
+    assert rel(c["gtop"], c["gbot"]) < 1e-5
+
+
 MARCH_MODES = (PL.MARCH_DEFAULT, 0, PL.MARCH_QFREE, PL.MARCH_ALT, PL.MARCH_ROWS,
                PL.MARCH_ROWS | PL.MARCH_QFREE, PL.MARCH_ROWS | PL.MARCH_ALT,
                PL.MARCH_ROWS | PL.MARCH_QFREE | PL.MARCH_ALT, PL.MARCH_STRIPS,
