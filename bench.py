@@ -15,6 +15,7 @@ is the RCCL all-reduce of the ensemble statistics.  Weak scaling.
 import argparse
 import json
 import os
+import re
 import sys
 import time
 
@@ -177,8 +178,11 @@ def pmc_traffic(key, fmt, L_):
     names = ROCPROF_NAMES.get((key, fmt), ())
     tot, src = 0.0, []
     for kind, ctr in (("fetch", "FETCH_SIZE"), ("write", "WRITE_SIZE")):
+        # newest round last: r<round>_<n> prefixes compared as numbers
+        # (file times are not kept by every copy of the tree)
         files = sorted(glob.glob(os.path.join(REPO, "profiles", "*_pmc_%s_L%d.csv" % (kind, L_))),
-                       key=lambda f: (os.path.getmtime(f), f))
+                       key=lambda f: [int(t) if t.isdigit() else t
+                                      for t in re.split(r"(\d+)", os.path.basename(f))])
         got = None
         for f in reversed(files):  # newest first
             with open(f) as fh:
