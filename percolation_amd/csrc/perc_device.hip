@@ -2110,6 +2110,7 @@ __device__ __forceinline__ void rm_walk(const CGArgs& a, RRow (&ring)[D], int t,
 // leaves the kernel instead of hanging the device.
 constexpr int kResThreads = 1024;
 constexpr int kResLdsRows = 16384;  // own-row p elements per workgroup (128 KB)
+constexpr unsigned kResSquareMask = 0x5Au;  // raster positions (-1,0) (0,-1) (0,1) (1,0)
 
 struct ResArgs {
   StencilView St;
@@ -2185,13 +2186,14 @@ template <int DC>
 __device__ __forceinline__ double halo_at(const ResHalo& h) {
   return DC < 0 ? h.l : (DC == 0 ? h.c : h.r);
 }
-template <int KP>
+template <int KP, unsigned UMC>
 __device__ __forceinline__ void res_pos(double& acc, unsigned um, unsigned map, unsigned cc, int lr,
                                         int Hw, int m, int c, const double* s_p, const ResHalo& hu,
                                         const ResHalo& hd, double ng0, double nleak) {
   constexpr int DR = KP < 3 ? -1 : (KP < 5 ? 0 : 1);
   constexpr int DC = KP < 3 ? KP - 1 : (KP == 3 ? -1 : (KP == 4 ? 1 : KP - 6));
-  if (!(um & (1u << KP))) return;  // wave-uniform
+  if (!(UMC & (1u << KP))) return;  // position no form of the lattice uses
+  if (!(um & (1u << KP))) return;   // wave-uniform
   const int col = c + DC;  // in range for every position a regular form uses
   double v;
   if (DR < 0) {
@@ -2207,14 +2209,23 @@ __device__ __forceinline__ void res_pos(double& acc, unsigned um, unsigned map, 
   acc = sj != 15u ? acc + pr : acc;
 }
 
-template <int MT, int HMAX>
+// QREG: q of the own rows kept in registers between the q.p reduction and
+// the r update; else (wider / taller bands: L = 2048 has 16 elements per
+// thread) q is formed again from p(k) in LDS and the halo registers with
+// the same arithmetic (bitwise the same q), so the thread holds only r and
+// the codes
+// UMC: compile-time superset of the raster positions the forms use (0x5A:
+// the square lattice's four neighbours), so unused positions and their
+// halo columns take no registers
+template <int MT, int HMAX, bool QREG = true, unsigned UMC = 0xFFu>
 __global__ __launch_bounds__(kResThreads) void k_cg_res(ResArgs a) {
   __shared__ double s_p[kResLdsRows];
   __shared__ double2 s_dt[kDiagTab];
   __shared__ unsigned s_rmap[kMaxForms];
   __shared__ double s_red[32];
   __shared__ int s_flag[2];
-  const int t = threadIdx.x, w = blockIdx.x;
+  int t = threadIdx.x;  // re-made opaque each iteration when !QREG (below)
+  const int w = blockIdx.x;
   const int m = a.m, nrows = a.nrows, N = a.St.N, G = a.G;
   const int R0 = w * a.H, Hw = min(a.H, nrows - R0);  // >= 1 (host sizes G)
   const bool has_up = R0 > 0, has_dn = R0 + Hw < nrows;
@@ -2223,8 +2234,10 @@ __global__ __launch_bounds__(kResThreads) void k_cg_res(ResArgs a) {
   if (t < kMaxForms) s_rmap[t] = a.St.F.rmap[t];
   load_dtab(a.St, s_dt);
   // own state: r and the codes of (row lr, column t + j NT)
-  double rv[HMAX][MT], qv[HMAX][MT];
-  unsigned cv[HMAX][MT];
+  double rv[HMAX][MT], qv[QREG ? HMAX : 1][QREG ? MT : 1];
+  // the row codes (u16), two per register when MT = 2
+  unsigned cv[HMAX][(MT + 1) / 2];
+  auto code_at = [&](int lr, int j) { return (cv[lr][j / 2] >> (16 * (j & 1))) & 0xffffu; };
 #pragma unroll
   for (int lr = 0; lr < HMAX; ++lr)
 #pragma unroll
@@ -2232,8 +2245,10 @@ __global__ __launch_bounds__(kResThreads) void k_cg_res(ResArgs a) {
       const int i = (R0 + lr) * m + t + j * kResThreads;
       const bool own = lr < Hw;
       rv[lr][j] = own ? a.r0[i] : 0.0;
-      cv[lr][j] = own ? a.St.code[i] : 0u;
-      qv[lr][j] = 0.0;
+      const unsigned cj = own ? a.St.code[i] : 0u;
+      if (j & 1) cv[lr][j / 2] |= cj << 16;
+      else cv[lr][j / 2] = cj;
+      if constexpr (QREG) qv[lr][j] = 0.0;
     }
   // the neighbours' rows next to the band, columns c-1 .. c+1: their codes
   // (static) and whether the position exists
@@ -2246,6 +2261,10 @@ __global__ __launch_bounds__(kResThreads) void k_cg_res(ResArgs a) {
   for (int j = 0; j < MT; ++j)
 #pragma unroll
     for (int d = 0; d < 3; ++d) {
+      if (!(UMC & (1u << d)) && !(UMC & (1u << (5 + d)))) {
+        hcu[j][d] = hcd[j][d] = 0u;
+        continue;
+      }
       hcu[j][d] = has_up && hin(j, d) ? a.St.code[(R0 - 1) * m + hcol(j, d)] : 0u;
       hcd[j][d] = has_dn && hin(j, d) ? a.St.code[(R0 + Hw) * m + hcol(j, d)] : 0u;
     }
@@ -2272,6 +2291,10 @@ __global__ __launch_bounds__(kResThreads) void k_cg_res(ResArgs a) {
   double err = 0.0;
   bool done = !ok;
   while (!done) {
+    // 16 elements per thread: keep the compiler from hoisting every
+    // element's addresses out of the loop (they would stay live across it
+    // and spill); recomputing them is a few integer ops
+    if constexpr (!QREG) asm volatile("" : "+v"(t));
     ++k;
     const int par = k & 1;
     double* part = a.part + (size_t)par * 3 * G;
@@ -2288,6 +2311,10 @@ __global__ __launch_bounds__(kResThreads) void k_cg_res(ResArgs a) {
       for (int j = 0; j < MT; ++j)
 #pragma unroll
         for (int d = 0; d < 3; ++d) {
+          if (!(UMC & (1u << d)) && !(UMC & (1u << (5 + d)))) {
+            hur[j][d] = hup[j][d] = hdr[j][d] = hdp[j][d] = 0.0;
+            continue;
+          }
           const bool u = has_up && hin(j, d) && (um & (1u << d));
           const bool dn = has_dn && hin(j, d) && (um & (1u << (5 + d)));
           const unsigned co = (unsigned)hcol(j, d) * 8u;
@@ -2304,9 +2331,10 @@ __global__ __launch_bounds__(kResThreads) void k_cg_res(ResArgs a) {
       for (int j = 0; j < MT; ++j) {
         if (lr < Hw) {
           const int e = lr * m + t + j * kResThreads;
-          const double z = div_tab(rv[lr][j], s_dt[diag_idx(cv[lr][j])]);
+          const double z = div_tab(rv[lr][j], s_dt[diag_idx(code_at(lr, j))]);
           s_p[e] = k == 1 ? z : bk * s_p[e] + z;
         }
+        if constexpr (!QREG) __builtin_amdgcn_sched_barrier(0);
       }
     // p(k) of the neighbours' rows, with the same arithmetic
     ResHalo hu[MT], hd[MT];
@@ -2315,6 +2343,10 @@ __global__ __launch_bounds__(kResThreads) void k_cg_res(ResArgs a) {
       double u3[3], d3[3];
 #pragma unroll
       for (int d = 0; d < 3; ++d) {
+        if (!(UMC & (1u << d)) && !(UMC & (1u << (5 + d)))) {
+          u3[d] = d3[d] = 0.0;
+          continue;
+        }
         const double zu = div_tab(hur[j][d], s_dt[diag_idx(hcu[j][d])]);
         const double zd = div_tab(hdr[j][d], s_dt[diag_idx(hcd[j][d])]);
         u3[d] = has_up && hin(j, d) ? (k == 1 ? zu : bk * hup[j][d] + zu) : 0.0;
@@ -2324,6 +2356,26 @@ __global__ __launch_bounds__(kResThreads) void k_cg_res(ResArgs a) {
       hd[j] = ResHalo{d3[0], d3[1], d3[2]};
     }
     __syncthreads();
+    // q of own element (lr, j) from p(k) in LDS and the halo rows
+    auto qcalc = [&](int lr, int j, double xi) {
+      const int c = t + j * kResThreads;
+      const unsigned cc = code_at(lr, j);
+      // raster positions in order (compile-time row / column offsets):
+      // for the regular forms the resident path is limited to, raster
+      // order is slot order; the slot of position kp comes from rmap
+      const unsigned map = s_rmap[cc >> 11];
+      double acc = s_dt[diag_idx(cc)].x * xi;
+      const unsigned um = a.St.F.umask;
+      res_pos<0, UMC>(acc, um, map, cc, lr, Hw, m, c, s_p, hu[j], hd[j], ng0, nleak);
+      res_pos<1, UMC>(acc, um, map, cc, lr, Hw, m, c, s_p, hu[j], hd[j], ng0, nleak);
+      res_pos<2, UMC>(acc, um, map, cc, lr, Hw, m, c, s_p, hu[j], hd[j], ng0, nleak);
+      res_pos<3, UMC>(acc, um, map, cc, lr, Hw, m, c, s_p, hu[j], hd[j], ng0, nleak);
+      res_pos<4, UMC>(acc, um, map, cc, lr, Hw, m, c, s_p, hu[j], hd[j], ng0, nleak);
+      res_pos<5, UMC>(acc, um, map, cc, lr, Hw, m, c, s_p, hu[j], hd[j], ng0, nleak);
+      res_pos<6, UMC>(acc, um, map, cc, lr, Hw, m, c, s_p, hu[j], hd[j], ng0, nleak);
+      res_pos<7, UMC>(acc, um, map, cc, lr, Hw, m, c, s_p, hu[j], hd[j], ng0, nleak);
+      return acc;
+    };
     // 2. q = A p, q.p
     double dot = 0.0;
 #pragma unroll
@@ -2331,24 +2383,9 @@ __global__ __launch_bounds__(kResThreads) void k_cg_res(ResArgs a) {
 #pragma unroll
       for (int j = 0; j < MT; ++j) {
         if (lr < Hw) {
-          const int c = t + j * kResThreads;
-          const unsigned cc = cv[lr][j];
-          const double xi = s_p[lr * m + c];
-          // raster positions in order (compile-time row / column offsets):
-          // for the regular forms the resident path is limited to, raster
-          // order is slot order; the slot of position kp comes from rmap
-          const unsigned map = s_rmap[cc >> 11];
-          double acc = s_dt[diag_idx(cc)].x * xi;
-          const unsigned um = a.St.F.umask;
-          res_pos<0>(acc, um, map, cc, lr, Hw, m, c, s_p, hu[j], hd[j], ng0, nleak);
-          res_pos<1>(acc, um, map, cc, lr, Hw, m, c, s_p, hu[j], hd[j], ng0, nleak);
-          res_pos<2>(acc, um, map, cc, lr, Hw, m, c, s_p, hu[j], hd[j], ng0, nleak);
-          res_pos<3>(acc, um, map, cc, lr, Hw, m, c, s_p, hu[j], hd[j], ng0, nleak);
-          res_pos<4>(acc, um, map, cc, lr, Hw, m, c, s_p, hu[j], hd[j], ng0, nleak);
-          res_pos<5>(acc, um, map, cc, lr, Hw, m, c, s_p, hu[j], hd[j], ng0, nleak);
-          res_pos<6>(acc, um, map, cc, lr, Hw, m, c, s_p, hu[j], hd[j], ng0, nleak);
-          res_pos<7>(acc, um, map, cc, lr, Hw, m, c, s_p, hu[j], hd[j], ng0, nleak);
-          qv[lr][j] = acc;
+          const double xi = s_p[lr * m + t + j * kResThreads];
+          const double acc = qcalc(lr, j, xi);
+          if constexpr (QREG) qv[lr][j] = acc;
           dot = dot + acc * xi;
         }
         // one element at a time (hoisting every element's LDS reads spills)
@@ -2375,9 +2412,12 @@ __global__ __launch_bounds__(kResThreads) void k_cg_res(ResArgs a) {
       for (int j = 0; j < MT; ++j) {
         if (lr < Hw) {
           const int c = t + j * kResThreads;
-          const double rn = rv[lr][j] - ak * qv[lr][j];
+          double qq;
+          if constexpr (QREG) qq = qv[lr][j];
+          else qq = qcalc(lr, j, s_p[lr * m + c]);
+          const double rn = rv[lr][j] - ak * qq;
           rv[lr][j] = rn;
-          const double z = div_tab(rn, s_dt[diag_idx(cv[lr][j])]);
+          const double z = div_tab(rn, s_dt[diag_idx(code_at(lr, j))]);
           acc2[0] = acc2[0] + z * rn;
           acc2[1] = acc2[1] + rn * rn;
           const double pk = s_p[lr * m + c];
@@ -2392,6 +2432,7 @@ __global__ __launch_bounds__(kResThreads) void k_cg_res(ResArgs a) {
             store_sc1(&xrow(npar, w, 1, 1)[c], pk);
           }
         }
+        if constexpr (!QREG) __builtin_amdgcn_sched_barrier(0);
       }
     block_sum<2>(acc2, s_red);
     if (t == 0) {
@@ -2960,14 +3001,16 @@ void res_geometry(perc_ctx* h) {
     return;
   const int nrows = g.n - 2, MT = g.m / kResThreads;
   const int H = cdiv(nrows, cus);
-  // 4 elements per thread (r, q, code of each in registers, 97 VGPRs); more
-  // spill at 1024 threads: m = 1024 and at most 4 rows per CU
-  if (MT != 1 || H > 4 || (long long)H * g.m > kResLdsRows) return;
+  // m = 1024: at most 4 rows per CU (r, q, code of 4 elements per thread
+  // in registers, 97 VGPRs); m = 2048: at most 8 rows per CU, q formed
+  // twice instead of kept (16 elements per thread: r and code only)
+  if (!((MT == 1 && H <= 4) || (MT == 2 && H <= 8)) || (long long)H * g.m > kResLdsRows) return;
+  if (MT == 2 && (h->forms.umask & ~kResSquareMask) != 0) return;  // square lattice only
   for (int f = 0; f < h->forms.nforms; ++f)
     if (!h->forms.regular[f]) return;  // wrapped columns (pbc): slot order is not raster order
   h->res_MT = MT;
   h->res_H = H;
-  h->res_HMAX = 4;
+  h->res_HMAX = MT == 1 ? 4 : 8;
   h->res_G = cdiv(nrows, H);
 }
 
@@ -3053,7 +3096,8 @@ hipError_t dev_solve_resident(perc_ctx* h, const CGArgs& ca, int* iter, double* 
   HIP_TRY(hipMemsetAsync(d.res_bar, 0, 9 * kTicketStride * sizeof(unsigned), st));
   void* args[] = {&a};
   const void* fn = nullptr;
-  fn = (const void*)k_cg_res<1, 4>;
+  fn = h->res_MT == 1 ? (const void*)k_cg_res<1, 4>
+                      : (const void*)k_cg_res<2, 8, false, kResSquareMask>;
   KernelTiming& T = h->timing;
   if (T.enabled) {
     if (T.ev.size() < 2) T.ev.resize(2, nullptr);

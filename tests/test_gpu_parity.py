@@ -582,7 +582,9 @@ def test_march_band_heights(lat, m, n, pbc, p):
 
 @pytest.mark.parametrize("lat,m,n,pbc,p", [(0, 256, 150, 0, 0.6), (1, 256, 99, 0, 0.42),
                                            (0, 384, 40, 1, 0.55), (1, 128, 64, 1, 0.42),
-                                           (0, 1024, 50, 1, 0.55), (1, 2048, 30, 0, 0.42)])
+                                           (0, 1024, 50, 1, 0.55), (1, 2048, 30, 0, 0.42),
+                                           # resident solve with 2048 columns (default mode)
+                                           (0, 2048, 600, 0, 0.5)])
 def test_march_modes_one_iteration_bitwise(lat, m, n, pbc, p):
     """Every march mode computes the same per-row numbers: with itmax = 1
     (one iteration: p = r/d, q = A p, r -= ak q, one stop test) the voltages
@@ -617,7 +619,10 @@ def test_table_division_is_ieee_division():
 
 @pytest.mark.parametrize("lat,m,n,pbc,p", [(0, 1024, 1024, 0, 0.6), (1, 1024, 1024, 0, 0.42),
                                            (0, 1024, 40, 0, 0.6), (1, 1024, 300, 0, 0.42),
-                                           (0, 1024, 700, 0, 0.55)])
+                                           (0, 1024, 700, 0, 0.55),
+                                           # 2048 columns: two per thread, q formed twice
+                                           (0, 2048, 2048, 0, 0.6), (0, 2048, 300, 0, 0.55),
+                                           (0, 2048, 1500, 0, 0.58)])
 def test_resident_solve_matches_march(lat, m, n, pbc, p):
     """The persistent resident solve (one cooperative launch, p in LDS,
     three grid barriers per iteration; bands of 1..4 rows per CU) against
