@@ -2102,9 +2102,10 @@ __device__ __forceinline__ void rm_walk(const CGArgs& a, RRow (&ring)[D], int t,
 //      every workgroup, so all leave the loop together)
 // Three grid barriers and no launches per iteration: at L = 1024 an
 // iteration of the launched kernels is ~28 us, almost all fixed costs.
-// The grid barrier counts arrivals per XCD group (blocks b, b+8, ..) and
-// then per group on one counter, after each workgroup's write-through
-// stores are complete (s_waitcnt vmcnt(0)); data crossing workgroups is
+// The grid barrier counts arrivals per XCD group (blocks b, b+8, ..), after
+// each workgroup's write-through stores are complete (s_waitcnt
+// vmcnt(0)); m = 1024 polls the 8 group counters directly, m = 2048 has the
+// last arriver of a group bump one top counter (res_barrier); data crossing workgroups is
 // written and read with sc1 (agent-scope) accesses, as in
 // publish_and_reduce.  A wait that exceeds ~1 s sets an error flag and
 // leaves the kernel instead of hanging the device.
@@ -2126,7 +2127,45 @@ struct ResArgs {
   unsigned* bar;     // 9 counters, 128 B apart (zeroed before the launch)
 };
 
-__device__ __forceinline__ bool res_barrier(const ResArgs& a, unsigned& epoch, int* s_flag) {
+// single-level (m = 1024: 0.0166 vs 0.0178 ms per iteration)
+__device__ __forceinline__ bool res_barrier1(const ResArgs& a, unsigned& epoch, int* s_flag) {
+  __syncthreads();  // (a release fence: every wave's stores are complete)
+  ++epoch;
+  if (threadIdx.x < 64) {
+    // one arrival on the workgroup's XCD-group counter, then wave 0 polls
+    // the (up to) 8 group counters together, one per lane, until they sum
+    // to epoch * G: no second-level counter hop on the critical path
+    const int lane = threadIdx.x, G = a.G, ngrp = G < 8 ? G : 8;
+    if (lane == 0)
+      __hip_atomic_fetch_add(&a.bar[(blockIdx.x & 7) * kTicketStride], 1u, __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned want = epoch * (unsigned)G;
+    int ok = 1;
+    for (unsigned spin = 0;; ++spin) {
+      unsigned v = lane < ngrp ? __hip_atomic_load(&a.bar[lane * kTicketStride], __ATOMIC_RELAXED,
+                                                   __HIP_MEMORY_SCOPE_AGENT)
+                               : 0u;
+#pragma unroll
+      for (int o = 4; o > 0; o >>= 1) v += __shfl_xor(v, o);  // lanes 0..7
+      if (__builtin_amdgcn_readfirstlane(v) >= want) break;
+      if (spin > (1u << 25)) {  // ~1 s: give up, report, leave
+        if (lane == 0) a.S->pad[0] = 1;
+        ok = 0;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+    if (lane == 0) s_flag[0] = ok;
+  }
+  __syncthreads();
+  return s_flag[0] != 0;
+}
+
+// two-level: the last arriver of an XCD group bumps one top counter, which
+// thread 0 of every workgroup polls (m = 2048: arrivals are spread out over
+// the longer phases, and polling all 8 group counters slows them: 0.0373
+// vs 0.0352 ms per iteration)
+__device__ __forceinline__ bool res_barrier2(const ResArgs& a, unsigned& epoch, int* s_flag) {
   __syncthreads();
   if (threadIdx.x == 0) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -2154,6 +2193,11 @@ __device__ __forceinline__ bool res_barrier(const ResArgs& a, unsigned& epoch, i
   }
   __syncthreads();
   return s_flag[0] != 0;
+}
+
+template <bool POLL8>
+__device__ __forceinline__ bool res_barrier(const ResArgs& a, unsigned& epoch, int* s_flag) {
+  return POLL8 ? res_barrier1(a, epoch, s_flag) : res_barrier2(a, epoch, s_flag);
 }
 
 // every workgroup sums the G partials of one slot in workgroup order
@@ -2283,7 +2327,7 @@ __global__ __launch_bounds__(kResThreads) void k_cg_res(ResArgs a) {
       if (lr == Hw - 1) store_sc1(&xrow(1, w, 1, 0)[c], rv[lr][j]);
     }
   unsigned epoch = 0;
-  bool ok = res_barrier(a, epoch, s_flag);
+  bool ok = res_barrier<MT == 1>(a, epoch, s_flag);
   double bknum = S->bknum, bk = 0.0, ak = 0.0;
   const double bnrm = S->bnrm, tol = S->tol;
   const int itmax = S->itmax;
@@ -2396,7 +2440,7 @@ __global__ __launch_bounds__(kResThreads) void k_cg_res(ResArgs a) {
       block_sum<1>(v1, s_red);
       if (t == 0) store_sc1(&part[w], v1[0]);
     }
-    if (!(ok = res_barrier(a, epoch, s_flag))) break;
+    if (!(ok = res_barrier<MT == 1>(a, epoch, s_flag))) break;
     {
       double tot[1];
       res_total<1>(a, part, tot, s_red);
@@ -2439,7 +2483,7 @@ __global__ __launch_bounds__(kResThreads) void k_cg_res(ResArgs a) {
       store_sc1(&part[G + w], acc2[0]);
       store_sc1(&part[2 * G + w], acc2[1]);
     }
-    if (!(ok = res_barrier(a, epoch, s_flag))) break;
+    if (!(ok = res_barrier<MT == 1>(a, epoch, s_flag))) break;
     {
       double tot[2];
       res_total<2>(a, part + G, tot, s_red);
