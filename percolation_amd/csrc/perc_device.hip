@@ -3201,7 +3201,18 @@ hipError_t dev_solve(perc_ctx* h, int itol, double tol, int itmax, bool x0_zero,
   if (ST) k_cg_init<true><<<G, kBlock, 0, st>>>(a, itol, x0_zero ? 1 : 0);
   else k_cg_init<false><<<G, kBlock, 0, st>>>(a, itol, x0_zero ? 1 : 0);
   HIP_TRY(dbg_sync(st, "k_cg_init"));
-  if (h->resident) return dev_solve_resident(h, a, iter, err);
+  if (h->resident) {
+    const hipError_t e = dev_solve_resident(h, a, iter, err);
+    // the cooperative launch can be refused when the grid cannot be
+    // co-resident (e.g. CUs taken by another context): nothing ran, r and
+    // the scalars are as k_cg_init left them, so the launched kernels take
+    // over for this solve
+    if (e != hipErrorCooperativeLaunchTooLarge && e != hipErrorInvalidConfiguration) return e;
+    (void)hipGetLastError();
+    fprintf(stderr, "[perc] resident solve not launchable (%s): launched kernels\n",
+            hipGetErrorString(e));
+    h->resident = false;
+  }
   if (h->strips) HIP_TRY(to_strips(h, a));
   // iterate in chunks; the device flag makes surplus launches no-ops
   int chunk = 8;
