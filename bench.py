@@ -130,6 +130,45 @@ def cpu_baseline(L_, p, order, gpu_iters, cpu_iters):
                 sample_seconds=round(t4 - t0, 2), s_per_solve=round(total, 2))
 
 
+def cpu_worker(spec, cpu_iters):
+    """One process of the all-cores CPU ensemble baseline: the 1-core
+    sample of cpu_baseline on its own realisation (spec = L, p, seed,
+    iters, nb, tb; the order drawn as main() draws it)."""
+    L_, p, seed, iters, nb, tb = (int(spec[0]), float(spec[1]), int(spec[2]), int(spec[3]),
+                                  int(spec[4]), int(spec[5]))
+    order = (np.random.default_rng(seed).permutation(nb)[:tb] + 1).astype(np.int32)
+    print(json.dumps(cpu_baseline(L_, p, order, iters, cpu_iters)), flush=True)
+
+
+def cpu_ensemble(L_, p, seeds, iters, nb, tb, cpu_iters, cores):
+    """ensemble throughput of the CPU path with all host
+    cores, one independent realisation per core (child processes running
+    cpu_worker concurrently, so memory-bandwidth contention is included)."""
+    import subprocess
+    t0 = time.perf_counter()
+    procs = [subprocess.Popen([sys.executable, os.path.abspath(__file__), "--cpu-iters",
+                               str(cpu_iters), "--cpu-worker", str(L_), str(p), str(int(sd)),
+                               str(iters), str(nb), str(tb)],
+                              stdout=subprocess.PIPE, stderr=subprocess.DEVNULL, text=True)
+             for sd in seeds[:cores]]
+    res = []
+    for pr in procs:
+        out, _ = pr.communicate()
+        if pr.returncode == 0 and out.strip():
+            res.append(json.loads(out.strip().splitlines()[-1]))
+    if not res:
+        return {"value": None, "error": "no worker finished"}
+    per = [r["s_per_solve"] for r in res]
+    return {"value": round(sum(1.0 / x for x in per), 8), "unit": "solves/s", "cores": len(res),
+            "kind": "port",
+            "sample": "%d concurrent processes, each the 1-core sample of cpu_baseline on its own "
+                      "realisation (labeling + assembly + %d linbcg iterations + currents, solve "
+                      "extrapolated to %d iterations, the GPU mean); value = sum of per-process "
+                      "rates" % (len(res), cpu_iters, iters),
+            "s_per_solve_mean": round(float(np.mean(per)), 2),
+            "wall_seconds": round(time.perf_counter() - t0, 2)}
+
+
 def kernel_label(key, minfo):
     """Name + role of a CG kernel, for the march variant that ran."""
     if key == "pm" and minfo.get("kernel") in ("wave", "rows"):
@@ -228,7 +267,13 @@ def main():
     ap.add_argument("--format", choices=("auto", "stencil", "stencil_tiled", "stencil_split", "csr"),
                     default="auto",
                     help="solver operator format (perc_set_matrix_format)")
+    ap.add_argument("--cpu-worker", nargs=6, default=None, help=argparse.SUPPRESS)
+    ap.add_argument("--cpu-cores", type=int, default=0,
+                    help="processes of the all-cores CPU ensemble baseline (0: the host CPU "
+                         "share, at most 16; -1: skip)")
     args = ap.parse_args()
+    if args.cpu_worker:
+        return cpu_worker(args.cpu_worker, args.cpu_iters)
 
     import torch
     import torch.distributed as dist
@@ -505,6 +550,20 @@ def main():
                                                results[0]["iter"], args.cpu_iters)
         except Exception as e:  # keep the GPU line even if the host is short of memory
             out["cpu_baseline"] = {"value": None, "error": repr(e)}
+        if args.cpu_cores >= 0 and args.occupancy == "uniform":
+            try:
+                aff = len(os.sched_getaffinity(0))
+            except AttributeError:
+                aff = os.cpu_count() or 1
+            cores = args.cpu_cores or max(1, min(16, aff, int(os.environ.get("OMP_NUM_THREADS", "16"))))
+            log("cpu ensemble baseline: %d processes ..." % cores)
+            iters_mean = int(round(np.mean([r["iter"] for r in results])))
+            ens_seeds = [int(seeds[(ii_list[args.warmup] + j) % len(seeds)]) for j in range(cores)]
+            try:
+                out["cpu_baseline_ensemble"] = cpu_ensemble(L_, p, ens_seeds, iters_mean, nb, tb,
+                                                            args.cpu_iters, cores)
+            except Exception as e:
+                out["cpu_baseline_ensemble"] = {"value": None, "error": repr(e)}
     for c in ctxs:
         c.close()
     if rank == 0:
