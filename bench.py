@@ -350,7 +350,20 @@ def main():
     ctx = ctxs[0]
     N, nnz = ctx.system_size()
 
+    seen = {}  # solver of a realisation that spanned (the last one may not)
+
+    def note_solver(c, r):
+        if r.get("nspan", 0) > 0 and "fmt" not in seen:
+            try:
+                seen["fmt"], seen["minfo"] = c.matrix_format(), c.march_info()
+            except P.PercError:
+                pass
+        return r
+
     def run(k, ctx=ctx):
+        return note_solver(ctx, run_(k, ctx))
+
+    def run_(k, ctx):
         if args.kind == "bond":
             return ctx.bondc_realisation(None, tb, tol=args.tol, itmax=args.itmax,
                                          device_ptr=orders[k].data_ptr())
@@ -406,15 +419,18 @@ def main():
     nsolves = int(stats[0])
     value = nsolves / tmax
 
+    fmt_names = {P.FMT_STENCIL: "stencil", P.FMT_STENCIL_TILED: "stencil_tiled",
+                 P.FMT_STENCIL_SPLIT: "stencil_split", P.FMT_CSR: "csr"}
     try:  # the format the solves used (the last realisation may not span: no system)
-        fmt = {P.FMT_STENCIL: "stencil", P.FMT_STENCIL_TILED: "stencil_tiled",
-               P.FMT_STENCIL_SPLIT: "stencil_split", P.FMT_CSR: "csr"}[ctx.matrix_format()]
+        fmt = fmt_names[ctx.matrix_format()]
         assembled = True
         minfo = ctx.march_info()
     except P.PercError:
         minfo = dict(kernel="none", qfree=False)
         fmt = {"auto": "stencil"}.get(args.format, args.format)
         assembled = False
+    if "fmt" in seen:  # what the spanning realisations ran (labels + bytes below)
+        fmt, minfo = fmt_names[seen["fmt"]], seen["minfo"]
 
     def kernel_set(f, probe=False):
         """(key, stats key, perc_bench_kernel id, bytes) of the CG kernels of
