@@ -3049,7 +3049,6 @@ void res_geometry(perc_ctx* h) {
   // in registers, 97 VGPRs); m = 2048: at most 8 rows per CU, q formed
   // twice instead of kept (16 elements per thread: r and code only)
   if (!((MT == 1 && H <= 4) || (MT == 2 && H <= 8)) || (long long)H * g.m > kResLdsRows) return;
-  if (MT == 2 && (h->forms.umask & ~kResSquareMask) != 0) return;  // square lattice only
   for (int f = 0; f < h->forms.nforms; ++f)
     if (!h->forms.regular[f]) return;  // wrapped columns (pbc): slot order is not raster order
   h->res_MT = MT;
@@ -3141,7 +3140,9 @@ hipError_t dev_solve_resident(perc_ctx* h, const CGArgs& ca, int* iter, double* 
   void* args[] = {&a};
   const void* fn = nullptr;
   fn = h->res_MT == 1 ? (const void*)k_cg_res<1, 4>
-                      : (const void*)k_cg_res<2, 8, false, kResSquareMask>;
+                      : (h->forms.umask & ~kResSquareMask) == 0
+                            ? (const void*)k_cg_res<2, 8, false, kResSquareMask>
+                            : (const void*)k_cg_res<2, 8, false>;
   KernelTiming& T = h->timing;
   if (T.enabled) {
     if (T.ev.size() < 2) T.ev.resize(2, nullptr);
