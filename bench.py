@@ -301,8 +301,10 @@ def main():
         ts = int(args.ps * t_sites)
     if args.kind == "site":
         ts = int(p * t_sites)
-    seeds = api.trial_seeds(args.master, 1000)
     nreal = args.warmup + args.steps
+    # tseed(ii) as bond_cond.f:65-70 generates them; never reused (the
+    # reference's 1000 are extended with the same stream when needed)
+    seeds = api.trial_seeds(args.master, max(1000, nreal * world))
     # inputs: occupation orders generated on the host and made resident in
     # HBM before the timed region.  "reference": the REAL*4 Fisher-Yates with
     # gfortran rand (bondc.f:162-174) -- for nb > 2^22 bonds its 22-bit
@@ -320,7 +322,7 @@ def main():
         rng = np.random.default_rng([seed, salt] if salt else seed)
         return (rng.permutation(n)[:cnt] + 1).astype(np.int32)
 
-    for k, ii in enumerate(ensemble.trial_indices(nreal, world, rank)):
+    for k, ii in enumerate(ensemble.trial_indices(nreal, world, rank, nseeds=len(seeds))):
         o = draw(nb, tb, int(seeds[ii])) if args.kind != "site" else np.zeros(1, np.int32)
         orders.append(torch.from_numpy(np.ascontiguousarray(o)).to(dev))
         if args.kind != "bond":

@@ -302,6 +302,45 @@ int perc_bondc_realisation(perc_ctx *h, int tbonds, const int *bond_order,
    sum iter} into acc[5*point..]. */
 void perc_stats_accumulate(double *acc, int point, double g, int spanning, int iter);
 
+/* ---- multi-GPU ensemble (one process, one host thread per device) ----- *
+ * Replaces the reference's serial trial loop (Fortran/Square/bond_cond.f:
+ * 62-70 seeds, :123-498 trials, rows written at :481-482).  Trial ii
+ * (1-based) runs on device (ii-1) mod ndev; each device has its own
+ * perc_ctx and host thread; per-trial results land in the caller's arrays
+ * at index ii-1 (ii order whatever device ran them).  The only collective
+ * is one RCCL all-reduce (sum, fp64) over a communicator ncclCommInitAll
+ * builds across the devices. */
+typedef struct perc_ensemble perc_ensemble;
+/* devices == NULL: devices 0..ndev-1 */
+int perc_ensemble_create(int ndev, const int *devices, int lattice, int m, int n, int pbc,
+                         perc_ensemble **out);
+int perc_ensemble_destroy(perc_ensemble *e);
+int perc_ensemble_ndev(perc_ensemble *e);
+/* device dev's own context (e.g. for single-trial calls); NULL if out of range */
+perc_ctx *perc_ensemble_ctx(perc_ensemble *e, int dev);
+/* the trials device `dev` of `ndev` runs, 1-based, ascending (ii_out may be
+   NULL); returns their count.  Host-only. */
+int perc_ensemble_trials(int ntrials, int ndev, int dev, int *ii_out);
+/* stats holds ndev slices of k doubles (device d's at stats[d*k]); on return
+   every slice holds the element-wise sum over the devices (ncclAllReduce). */
+int perc_ensemble_allreduce(perc_ensemble *e, double *stats, int k);
+/* bond_cond over the devices: trial ii shuffles with tseed[ii-1] (REAL*4
+   Fisher-Yates, bondc.f:162-174), computes the lowest-label conductance at
+   grid points nbarr[0..) until a value <= 0, a repeat (hazard H3) or npts;
+   outputs, per trial t = ii-1: nrows[t] rows at [t*npts + j] of gbot, gtop,
+   iters; bf_c[t] = first spanning bond count (0: none), perccln[t] = lowest
+   spanning label with every bond occupied (bond_cond.f:381, 486-496).
+   stats (npts*5, may be NULL) = the all-reduced {count, sum Gtop,
+   sum Gtop^2, count spanning, sum iter} per grid point. */
+int perc_ensemble_bond_cond(perc_ensemble *e, int ntrials, const int *tseed, int npts,
+                            const int *nbarr, double Va, double g0, double tol, int itmax,
+                            int *nrows, double *gbot, double *gtop, int *iters, int *bf_c,
+                            int *perccln, double *stats);
+/* REAL*4 Fisher-Yates of ids 1..N after srand(seed) on a stream local to the
+   call (thread-safe; same sequence as perc_srand + perc_shuffle): order has
+   N+1 slots, order[N] = 0 (hazard H2). */
+void perc_shuffle_seeded(int seed, int N, int *order);
+
 /* ---- Numerical-Recipes-compatible layer (F77 ABI, by reference) ------- *
  * Same names and argument meaning as the routines embedded in the
  * reference (Square/bondc.f:723-917).  linbcg_/atimes_/asolve_ read the
@@ -319,6 +358,7 @@ void linbcg_(int *n, double *b, double *x, int *itol, double *tol, int *itmax,
              int *iter, double *err);
 void perc_nr_bind(double *sa, int *ija, int nmax);
 int perc_nr_status(void);
+int perc_nr_status_(void);  /* F77 spelling: `integer perc_nr_status` */
 
 #ifdef __cplusplus
 }

@@ -94,30 +94,4 @@ build sq_sb_perc              Square/sb_perc.f 's/pscount = 42 /pscount = 4 /' '
 build tri_sb_perc             Triangular/sb_perc.f 's/pscount = 51 /pscount = 4 /' 's/iter = 100/iter = 5/' 's/0.50d+00+(0.01d+00\*(i-1))/0.60d+00+(0.10d+00*(i-1))/'
 build sq_bs_perc              Square/bs_perc.f 's/pbcount = 71 /pbcount = 5 /' 's/iter = 1000/iter = 8/' 's/0.30d+00+(0.01d+00\*(i-1))/0.55d+00+(0.10d+00*(i-1))/'
 build tri_bs_perc             Triangular/bs_perc.f 's/pbcount = 71 /pbcount = 5 /' 's/iter = 1000/iter = 8/' 's/0.30d+00+(0.01d+00\*(i-1))/0.55d+00+(0.10d+00*(i-1))/'
-# NR-level drop-in (route 1): the reference program with its
-# embedded Numerical Recipes routines (sprsin ... dsprstx, from the line
-# "SUBROUTINE sprsin" to the end of the file) deleted and libperc.so linked
-# in their place -- its calls to sprsin/linbcg/dsprsax then run libperc's
-# F77 symbols (linbcg_ on the GPU) against the program's own COMMON /mat/.
-LIBPERC_DIR="$HERE/../percolation_amd"
-build_nr() {
-  local name=$1 src=$2
-  shift 2
-  if [ ! -e "$LIBPERC_DIR/libperc.so" ]; then
-    echo "build_ref.sh: libperc.so not built; skipping $name" >&2
-    return 0
-  fi
-  local f="$TMP/$name.f"
-  cp "$REF/Fortran/$src" "$f"
-  for e in "$@"; do sed -i "$e" "$f"; done
-  sed -i '/SUBROUTINE sprsin/,$d' "$f"
-  "$FLANG" -O2 "$f" "$TMP/gfrand.o" -L"$GF" -lgfortran -L"$LIBPERC_DIR" -lperc \
-    -Wl,-rpath,"$GF" -Wl,-rpath,'$ORIGIN/../../percolation_amd' -o "$OUT/$name"
-}
-build_nr nr_sq_bondc_p60        Square/bondc.f 's/pb = 0.50d+00/pb = 0.60d+00/'
-build_nr nr_sq_bondc_p60_pbc    Square/bondc.f 's/pb = 0.50d+00/pb = 0.60d+00/' 's/pbc = 0 /pbc = 1 /'
-build_nr nr_tri_bondc_p35       Triangular/bondc.f
-build_nr nr_sq_bond_cond_3t     Square/bond_cond.f 's/numtrials = 1 /numtrials = 3 /' 's/m = 10 /m = 12 /' 's/n = 10 /n = 12 /'
-build_nr nr_tri_bond_cond       Triangular/bond_cond.f
-
 echo "reference binaries in $OUT"

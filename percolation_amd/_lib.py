@@ -105,6 +105,17 @@ SIGNATURES = {
     "linbcg_": (None, [_VP] * 8),
     "perc_nr_bind": (None, [_VP, _VP, C.c_int]),
     "perc_nr_status": (C.c_int, []),
+    "perc_nr_status_": (C.c_int, []),
+    "perc_shuffle_seeded": (None, [C.c_int, C.c_int, _I]),
+    "perc_ensemble_create": (C.c_int, [C.c_int, _VP, C.c_int, C.c_int, C.c_int, C.c_int,
+                                       C.POINTER(C.c_void_p)]),
+    "perc_ensemble_destroy": (C.c_int, [_VP]),
+    "perc_ensemble_ndev": (C.c_int, [_VP]),
+    "perc_ensemble_ctx": (C.c_void_p, [_VP, C.c_int]),
+    "perc_ensemble_trials": (C.c_int, [C.c_int, C.c_int, C.c_int, _VP]),
+    "perc_ensemble_allreduce": (C.c_int, [_VP, _D, C.c_int]),
+    "perc_ensemble_bond_cond": (C.c_int, [_VP, C.c_int, _I, C.c_int, _I, C.c_double, C.c_double,
+                                          C.c_double, C.c_int, _I, _D, _D, _I, _I, _I, _VP]),
 }
 
 

@@ -577,3 +577,74 @@ def fmt_i10(*cols):
     n = len(cols[0])
     f = ",".join(["%10d"] * len(cols)) + "\n"
     return "".join(f % tuple(int(c[i]) for c in cols) for i in range(n))
+
+
+# ---------------------------------------------------------------- multi-GPU ensemble
+class Ensemble:
+    """perc_ensemble: one context + host thread per device of this node,
+    trials striped ii -> device (ii-1) mod ndev, one RCCL all-reduce of the
+    per-grid-point statistics (include/perc.h; Square/bond_cond.f:123-498)."""
+
+    def __init__(self, lattice, m, n, pbc=0, ndev=1, devices=None):
+        self.lattice, self.m, self.n, self.pbc = lattice, m, n, pbc
+        self.nb = nbonds(lattice, m, n, pbc)
+        h = C.c_void_p()
+        dv = None if devices is None else np.ascontiguousarray(devices, dtype=np.int32)
+        L.check(L.lib().perc_ensemble_create(ndev, L.ptr(dv), lattice, m, n, pbc, C.byref(h)),
+                "perc_ensemble_create")
+        self.h = h
+        self.ndev = L.lib().perc_ensemble_ndev(h)
+
+    def close(self):
+        if self.h:
+            L.lib().perc_ensemble_destroy(self.h)
+            self.h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def allreduce(self, per_device):
+        """per_device: (ndev, k) array; returns the sum over devices (RCCL)."""
+        a = np.ascontiguousarray(per_device, dtype=np.float64).copy()
+        k = a.shape[1]
+        L.check(L.lib().perc_ensemble_allreduce(self.h, a.reshape(-1), k),
+                "perc_ensemble_allreduce")
+        return a
+
+    def bond_cond(self, master=58302, numtrials=1, Va=1.0, g0=1.0, tol=1e-8, itmax=2500):
+        """The bond_cond trial loop over the devices; same records as
+        bond_cond_grid, plus the all-reduced statistics (npts, 5)."""
+        seeds = trial_seeds(master, 1000)
+        nbarr = pb_grid(self.lattice, self.nb)
+        npts = len(nbarr)
+        nrows, bfc, pl = _i32(numtrials), _i32(numtrials), _i32(numtrials)
+        gbot, gtop = np.zeros(numtrials * npts), np.zeros(numtrials * npts)
+        iters = _i32(numtrials * npts)
+        stats = np.zeros(npts * 5)
+        L.check(L.lib().perc_ensemble_bond_cond(self.h, numtrials, seeds, npts, nbarr, Va, g0,
+                                                tol, itmax, nrows, gbot, gtop, iters, bfc, pl,
+                                                stats.ctypes.data_as(C.c_void_p)),
+                "perc_ensemble_bond_cond")
+        out = []
+        for t in range(numtrials):
+            rows = []
+            for j in range(nrows[t]):
+                o = t * npts + j
+                bf = int(nbarr[j])
+                rows.append(dict(bf=bf, pb=float(np.float32(np.float32(bf) / np.float32(self.nb))),
+                                 gbot=float(gbot[o]), gtop=float(gtop[o]), iter=int(iters[o])))
+            b = int(bfc[t])
+            out.append(dict(ii=t + 1, seed=int(seeds[t]), rows=rows, bf_c=b, perccln=int(pl[t]),
+                            pc=float(np.float32(np.float32(b) / np.float32(self.nb))) if b else 0.0))
+        return out, stats.reshape(npts, 5)
+
+
+def ensemble_trials(ntrials, ndev, dev):
+    """1-based trials device `dev` of `ndev` runs (perc_ensemble_trials)."""
+    cnt = L.lib().perc_ensemble_trials(ntrials, ndev, dev, None)
+    out = _i32(max(cnt, 0))
+    L.lib().perc_ensemble_trials(ntrials, ndev, dev, L.ptr(out))
+    return out

@@ -138,6 +138,8 @@ void perc_nr_bind(double* sa, int* ija, int nmax) {
 }
 
 int perc_nr_status(void) { return g_status; }
+// the same for F77 callers (implicit interface: integer perc_nr_status)
+int perc_nr_status_(void) { return g_status; }
 
 // sprsin: dense (column-major np x np) -> NR row-indexed storage (bondc.f:723-746)
 void sprsin_(double* a, int* n_, int* np_, double* thresh_, int* nmax_, double* sa, int* ija) {

@@ -16,9 +16,15 @@ NSTAT = 5  # count, sum G, sum G^2, spanning, sum iter
 
 
 def trial_indices(nreal, world, rank, nseeds=1000):
-    """0-based trial ids of this rank's nreal realisations (wrapping over
-    the nseeds precomputed seeds, bond_cond.f:67)."""
-    return [(k * world + rank) % nseeds for k in range(nreal)]
+    """0-based trial ids of this rank's nreal realisations: trial ii (0-based)
+    runs on rank ii mod world, as perc_ensemble_trials stripes devices.  The
+    reference never reuses a seed (tseed(1..1000), bond_cond.f:67), so an
+    ensemble larger than the seeds generated is an error, not a wrap."""
+    if nreal * world > nseeds:
+        raise ValueError("ensemble of %d x %d realisations exceeds the %d trial seeds; "
+                         "generate more seeds (perc_trial_seeds with k >= %d)"
+                         % (nreal, world, nseeds, nreal * world))
+    return [k * world + rank for k in range(nreal)]
 
 
 def local_stats(results):

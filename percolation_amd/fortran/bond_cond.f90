@@ -15,22 +15,33 @@
 !
 ! Parameters: the reference's block (10x10, numtrials 1, master seed 58302),
 ! overridable by bond_cond.nml (&bond_cond_nml lattice, m, n, pbc,
-! numtrials, seed, Va, g0, tol, itmax, device /).  Output: bondcond.txt as
+! numtrials, seed, Va, g0, tol, itmax, device, ndev /).  Output: bondcond.txt as
 ! the reference writes it (bond_cond.f:107-117, 481-496).
+!
+! ndev >= 1 shards the trials over devices 0..ndev-1 of the node
+! (perc_ensemble_bond_cond: trial ii on device (ii-1) mod ndev, one host
+! thread each, rows gathered in ii order) and all-reduces the per-grid-point
+! statistics with RCCL; bondcond.txt is the same file, and the reduced
+! statistics go to bondcond_stats.txt.  ndev = 0 (default) runs every trial
+! on `device` in this thread.
 program bond_cond
   use perc_api
   implicit none
 #ifndef PERC_LATTICE
 #define PERC_LATTICE 0
 #endif
-  integer(c_int) :: lattice, m, n, pbc, numtrials, seed, itmax, device
+  integer(c_int) :: lattice, m, n, pbc, numtrials, seed, itmax, device, ndev
   double precision :: Va, g0, tol
-  namelist /bond_cond_nml/ lattice, m, n, pbc, numtrials, seed, Va, g0, tol, itmax, device
+  namelist /bond_cond_nml/ lattice, m, n, pbc, numtrials, seed, Va, g0, tol, itmax, device, &
+                           ndev
   integer(c_int) :: t, nb, i, ii, jj, bf, lastbf, npts, lo, hi, mid, bfc, perccln, stats(4)
   integer(c_int) :: tseed(1000), nbarr(250)
   double precision :: pbarr(250), pb, pc, Gtop, Gbot
   integer(c_int), allocatable, target :: order(:)
-  type(c_ptr) :: h
+  type(c_ptr) :: h, ens
+  integer(c_int), allocatable :: e_nrows(:), e_iters(:), e_bfc(:), e_pl(:)
+  double precision, allocatable :: e_gbot(:), e_gtop(:), e_stats(:)
+  double precision :: cnt, gm, gv
   type(perc_label_info) :: info
   type(perc_cond_result) :: res
   integer :: u
@@ -46,6 +57,7 @@ program bond_cond
   tol = 1.00d-08
   itmax = 2500
   device = 0
+  ndev = 0
   if (perc_have_file('bond_cond.nml')) then
     open(newunit=u, file='bond_cond.nml', status='old')
     read(u, nml=bond_cond_nml)
@@ -83,6 +95,54 @@ program bond_cond
   write(10, *) "total number of iterations:", numtrials
   write(10, *) "random number for generating the trial seeds:", seed
   write(10, *) "------------------------------"
+
+  if (ndev >= 1) then
+    allocate(e_nrows(numtrials), e_bfc(numtrials), e_pl(numtrials))
+    allocate(e_gbot(numtrials * 250), e_gtop(numtrials * 250), e_iters(numtrials * 250))
+    allocate(e_stats(250 * 5))
+    call perc_check(perc_ensemble_create(ndev, c_null_ptr, lattice, m, n, pbc, ens), &
+                    'perc_ensemble_create')
+    call perc_check(perc_ensemble_bond_cond(ens, numtrials, tseed, 250, nbarr, Va, g0, tol, &
+                    itmax, e_nrows, e_gbot, e_gtop, e_iters, e_bfc, e_pl, e_stats), &
+                    'perc_ensemble_bond_cond')
+    call perc_check(perc_ensemble_destroy(ens), 'perc_ensemble_destroy')
+    do ii = 1, numtrials   ! rows in trial order, as the serial loop writes them
+      write(6, *) "Trial #", ii
+      write(10, *) "Trial #", ii
+      write(6, *) "Random number seed:", tseed(ii)
+      write(10, *) "Random number seed:", tseed(ii)
+      do jj = 1, e_nrows(ii)
+        i = (ii - 1) * 250 + jj
+        pb = real(nbarr(jj)) / real(nb)     ! REAL*4 quotient (bond_cond.f:351)
+        write(6, 111) pb, e_gbot(i), e_gtop(i), ((e_gbot(i) + e_gtop(i)) / 2)
+        write(10, 111) pb, e_gbot(i), e_gtop(i), ((e_gbot(i) + e_gtop(i)) / 2)
+      end do
+      pc = 0.00d+00
+      if (e_bfc(ii) > 0) pc = real(e_bfc(ii)) / real(nb)
+      write(6, *) "lattice-spanning cluster:", e_pl(ii)
+      write(10, *) "lattice-spanning cluster:", e_pl(ii)
+      write(6, *) "pc =", pc
+      write(10, *) "pc =", pc
+      write(6, *) "------------------------------"
+      write(10, *) "------------------------------"
+    end do
+    close(10)
+    ! ensemble statistics (RCCL all-reduced): pb, count, <Gtop>, var Gtop,
+    ! spanning fraction, mean iterations
+    open(unit=11, file='bondcond_stats.txt')
+    write(11, '(a,i0)') 'devices: ', ndev
+    do jj = 1, 250
+      cnt = e_stats((jj - 1) * 5 + 1)
+      if (cnt <= 0.0d0) exit
+      gm = e_stats((jj - 1) * 5 + 2) / cnt
+      gv = max(e_stats((jj - 1) * 5 + 3) / cnt - gm * gm, 0.0d0)
+      pb = real(nbarr(jj)) / real(nb)
+      write(11, 112) pb, int(cnt), gm, gv, e_stats((jj - 1) * 5 + 4) / cnt, &
+                     e_stats((jj - 1) * 5 + 5) / cnt
+    end do
+    close(11)
+    stop
+  end if
 
   allocate(order(nb + 1))
   call perc_check(perc_ctx_create(device, lattice, m, n, pbc, h), 'perc_ctx_create')
@@ -149,4 +209,5 @@ program bond_cond
   call perc_check(perc_ctx_destroy(h), 'perc_ctx_destroy')
 
 111 format(f12.9, ",", f12.9, ",", f12.9, ",", f12.9)
+112 format(f12.9, ",", i8, ",", es24.16, ",", es24.16, ",", f10.6, ",", f14.2)
 end program bond_cond

@@ -149,6 +149,31 @@ module perc_api
       real(c_double), value :: Va, g0, leak, tol
       type(perc_cond_result) :: res
     end function perc_conductance
+
+    ! multi-GPU ensemble: one host thread + context per device, RCCL stats
+    integer(c_int) function perc_ensemble_create(ndev, devices, lattice, m, n, pbc, e) &
+        bind(C, name='perc_ensemble_create')
+      import :: c_int, c_ptr
+      integer(c_int), value :: ndev, lattice, m, n, pbc
+      type(c_ptr), value :: devices
+      type(c_ptr) :: e
+    end function perc_ensemble_create
+
+    integer(c_int) function perc_ensemble_destroy(e) bind(C, name='perc_ensemble_destroy')
+      import :: c_int, c_ptr
+      type(c_ptr), value :: e
+    end function perc_ensemble_destroy
+
+    integer(c_int) function perc_ensemble_bond_cond(e, ntrials, tseed, npts, nbarr, Va, g0, &
+        tol, itmax, nrows, gbot, gtop, iters, bf_c, perccln, stats) &
+        bind(C, name='perc_ensemble_bond_cond')
+      import :: c_int, c_ptr, c_double
+      type(c_ptr), value :: e
+      integer(c_int), value :: ntrials, npts, itmax
+      real(c_double), value :: Va, g0, tol
+      integer(c_int) :: tseed(*), nbarr(*), nrows(*), iters(*), bf_c(*), perccln(*)
+      real(c_double) :: gbot(*), gtop(*), stats(*)
+    end function perc_ensemble_bond_cond
   end interface
 
 contains

@@ -1,9 +1,13 @@
 """Multi-rank path of the ensemble (percolation_amd/ensemble.py, used by
 bench.py) with world size 2 over gloo on CPU: the trial shards are
 disjoint and cover the ensemble, and the all-reduced statistics equal the
-single-process statistics of all realisations.  The realisations here are
-produced by the host label replay (no GPU): trial ii -> tseed(ii) ->
-reference shuffle -> spanning label -> a deterministic stand-in "G"."""
+single-process statistics of all realisations.  With no GPU here, each
+rank's realisations are the oracle's (tests only: oracle/perc_oracle.c):
+trial ii -> tseed(ii) -> reference shuffle -> labels -> the spanning
+cluster's conductance by the literal linbcg (Square/bondc.f:189-595).
+Also the device striping of perc_ensemble (include/perc.h) for 2-8 virtual
+devices: ii -> device (ii-1) mod ndev, every trial exactly once, rows
+gathered in ii order."""
 import os
 import socket
 
@@ -12,19 +16,19 @@ import pytest
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from percolation_amd import _lib as PL
+import oracle_lib as O
 from percolation_amd import api, ensemble
 
 L_, P_, NREAL = 24, 0.55, 5
 
 
 def realisation(ii, seeds):
-    nb = api.nbonds(0, L_, L_, 0)
-    order = api.shuffled_ids(nb, int(seeds[ii]))
-    r = api.replay_labels(0, L_, L_, 0, PL.BOND, bond_order=order, nbond=int(P_ * nb))
+    """oracle bondc realisation (labels, spanning, Kirchhoff system, linbcg,
+    terminal currents) for trial ii's seed; G = 0 when nothing spans."""
+    r = O.bondc(0, L_, L_, 0, P_, int(seeds[ii]))
     span = r["perccln"] > 0
-    g = float(r["csize"][r["perccln"]]) / nb if span else 0.0
-    return dict(gtop=g, nspan=1 if span else 0, iter=int(r["maxcs"]))
+    return dict(gtop=r["gtop"] if span else 0.0, nspan=1 if span else 0,
+                iter=r["iter"] if span else 0)
 
 
 def _worker(rank, world, port, q):
@@ -53,6 +57,54 @@ def test_shards_disjoint_and_cover():
     ids = [ensemble.trial_indices(10, w, r) for r in range(w)]
     flat = sorted(i for s in ids for i in s)
     assert flat == list(range(40))
+
+
+def test_trial_indices_never_wrap():
+    with pytest.raises(ValueError):
+        ensemble.trial_indices(300, 4, 0, nseeds=1000)
+
+
+@pytest.mark.parametrize("ndev", [2, 3, 4, 5, 8])
+@pytest.mark.parametrize("ntrials", [1, 7, 512])
+def test_device_striping_and_gather_order(ndev, ntrials):
+    """perc_ensemble_trials (C) == ensemble.trial_indices (bench ranks), every
+    trial on exactly one device, and gathering each device's rows into slot
+    ii-1 reproduces the serial ii order."""
+    owner = np.full(ntrials + 1, -1)
+    slots = [None] * ntrials
+    for d in range(ndev):
+        ii = api.ensemble_trials(ntrials, ndev, d)
+        assert list(ii) == list(range(d + 1, ntrials + 1, ndev))
+        k = len(ii)
+        if ntrials >= ndev * k:  # whole rounds: the ranks' 0-based ids
+            assert [i - 1 for i in ii] == ensemble.trial_indices(k, ndev, d, nseeds=ntrials)
+        for i in ii:
+            assert owner[i] == -1
+            owner[i] = d
+            slots[i - 1] = ("row", i)  # what device d writes for trial i
+    assert (owner[1:] >= 0).all()
+    assert slots == [("row", i) for i in range(1, ntrials + 1)]
+
+
+def test_seeded_shuffle_equals_global_stream():
+    """the per-thread shuffle of perc_ensemble equals srand + the REAL*4
+    Fisher-Yates on the global stream (bondc.f:162-174)"""
+    for n, seed in [(40, 4562929), (2000, 123), (5, 0)]:
+        a = np.zeros(n + 1, np.int32)
+        from percolation_amd import _lib as PL
+        PL.lib().perc_shuffle_seeded(seed, n, a)
+        b = api.shuffled_ids(n, seed)
+        assert np.array_equal(a[:n], b[:n])
+
+
+def test_ensemble_without_device_fails_loudly():
+    import ctypes as C
+    import torch
+    from percolation_amd import _lib as PL
+    if torch.cuda.is_available():
+        pytest.skip("device present")
+    h = C.c_void_p()
+    assert PL.lib().perc_ensemble_create(2, None, 0, 16, 16, 0, C.byref(h)) == -8
 
 
 def test_world2_gloo_stats_equal_single_process():

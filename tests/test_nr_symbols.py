@@ -1,0 +1,164 @@
+"""libperc's Numerical-Recipes layer called from Fortran 77.
+
+`percolation_amd/fortran/nr_caller.f` is a builder-written F77 program that
+declares COMMON /mat/ sa(20000), ija(20000) and calls sprsin, dsprsax,
+dsprstx, atimes, asolve, snrm and linbcg by reference, exactly as the
+reference's conductance programs do (Fortran/Square/bondc.f:538-580,
+723-917); the symbols resolve to libperc.so.  Every result is compared with
+the oracle's literal restatement of the same routine, and linbcg's answer
+with the reference's own 50x50 golden (Vint, iter, Gtop).
+"""
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+import golden_io as G
+import oracle_lib as O
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+EXE = os.path.join(REPO, "percolation_amd", "fortran", "bin", "nr_caller")
+ENODEV = -8
+
+
+def oracle_system(lat, m, n, pbc, pb, seed, thresh=1e-16):
+    """interior NR storage + rhs + diag of one bondc realisation (oracle)."""
+    r = O.bondc(lat, m, n, pbc, pb, seed)
+    b1, b2 = O.bond_list(lat, m, n, pbc)
+    nb = len(b1)
+    gval = O.f64(nb)
+    O.lib().or_bond_values(0, nb, b1, b2, r["label"], O.i32(1), r["perccln"], 1.0, 1e-12, gval)
+    t, N = m * n, m * n - 2 * m
+    nmax = N + 1 + 2 * nb + 8
+    sa, ija = O.f64(nmax), O.i32(nmax)
+    itemp, diag = O.f64(N), O.f64(t)
+    k = O.lib().or_assemble(lat, m, n, pbc, nb, b1, b2, gval, 1.0, thresh, 0, nmax, sa, ija,
+                            itemp, diag)
+    return dict(sa=sa[:k], ija=ija[:k], rhs=itemp, N=N, k=k, b1=b1, b2=b2, gval=gval,
+                diag=diag)
+
+
+def dense(s):
+    """the dense interior matrix Gtemp that sprsin reads (bondc.f:520-538)."""
+    N, sa, ija = s["N"], s["sa"], s["ija"]
+    a = np.zeros((N, N))
+    a[np.arange(N), np.arange(N)] = sa[:N]
+    for i in range(N):
+        for kk in range(ija[i] - 1, ija[i + 1] - 1):
+            a[i, ija[kk] - 1] = sa[kk]
+    return a
+
+
+def write_inputs(d, small, x, big, itol=2, tol=1e-8, itmax=2500):
+    a = dense(small)
+    N = small["N"]
+    npd = 600
+    full = np.zeros((npd, npd))
+    full[:N, :N] = a
+    with open(d / "dense.bin", "wb") as f:
+        np.array([N, npd], np.int32).tofile(f)
+        np.array([1e-16]).tofile(f)
+        full.T.astype(np.float64).tofile(f)  # column-major
+    with open(d / "vec.bin", "wb") as f:
+        np.array([N], np.int32).tofile(f)
+        x.astype(np.float64).tofile(f)
+    with open(d / "system.bin", "wb") as f:
+        np.array([big["N"], big["k"]], np.int32).tofile(f)
+        big["sa"].tofile(f)
+        big["ija"].astype(np.int32).tofile(f)
+        big["rhs"].tofile(f)
+        np.array([itol], np.int32).tofile(f)
+        np.array([tol]).tofile(f)
+        np.array([itmax], np.int32).tofile(f)
+
+
+def run_caller(tmp_path):
+    if not os.path.exists(EXE):
+        pytest.skip("nr_caller not built (make -C percolation_amd/fortran)")
+    small = oracle_system(0, 20, 30, 0, 0.55, 777)
+    big = oracle_system(0, 50, 50, 0, 0.60, 626504)
+    x = np.random.default_rng(5).standard_normal(small["N"])
+    write_inputs(tmp_path, small, x, big)
+    r = subprocess.run([EXE], cwd=tmp_path, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    return small, big, x
+
+
+def read_sprsin(path):
+    raw = path.read_bytes()
+    st, k = np.frombuffer(raw[:8], np.int32)
+    sa = np.frombuffer(raw[8:8 + 8 * k], np.float64)
+    ija = np.frombuffer(raw[8 + 8 * k:8 + 12 * k], np.int32)
+    return st, sa, ija
+
+
+def serial_snrm(x, itol):
+    if itol <= 3:
+        s = 0.0
+        for v in x:
+            s = s + v * v
+        return np.sqrt(s)
+    return float(np.max(np.abs(x)))
+
+
+def check_host_parts(tmp_path, small, x):
+    st, sa, ija = read_sprsin(tmp_path / "sprsin.bin")
+    assert st == 0
+    assert np.array_equal(ija, small["ija"])
+    assert np.array_equal(sa.view(np.uint64), small["sa"].view(np.uint64))
+    raw = (tmp_path / "ops.bin").read_bytes()
+    N = small["N"]
+    st = np.frombuffer(raw[:4], np.int32)[0]
+    vals = np.frombuffer(raw[4:], np.float64)
+    ops = vals[:5 * N].reshape(5, N)
+    s1, s2, s4 = vals[5 * N:]
+    # snrm (bondc.f:867-884): serial sum of squares for itol <= 3, max |x| else
+    assert s1 == serial_snrm(x, 1) and s2 == serial_snrm(x, 2) and s4 == serial_snrm(x, 4)
+    return st, ops
+
+
+def test_nr_host_symbols_from_fortran_without_device(tmp_path):
+    """sprsin and snrm run on the host; with no device the products must
+    fail loudly (status PERC_ENODEV), never fall back to the CPU."""
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("device present: covered by the gpu variant")
+    small, big, x = run_caller(tmp_path)
+    st, ops = check_host_parts(tmp_path, small, x)
+    assert st == ENODEV
+    raw = (tmp_path / "linbcg.bin").read_bytes()
+    assert np.frombuffer(raw[:4], np.int32)[0] == ENODEV
+
+
+@pytest.mark.gpu
+def test_nr_symbols_from_fortran(tmp_path):
+    small, big, x = run_caller(tmp_path)
+    st, ops = check_host_parts(tmp_path, small, x)
+    assert st == 0
+    N = small["N"]
+    want_ax, want_atx = O.f64(N), O.f64(N)
+    O.lib().or_dsprsax(small["sa"], small["ija"], x, want_ax, N)
+    O.lib().or_dsprstx(small["sa"], small["ija"], x, want_atx, N)
+    bits = lambda a: np.ascontiguousarray(a).view(np.uint64)  # noqa: E731
+    assert np.array_equal(bits(ops[0]), bits(want_ax))       # dsprsax
+    assert np.array_equal(bits(ops[1]), bits(want_atx))      # dsprstx
+    assert np.array_equal(bits(ops[2]), bits(want_ax))       # atimes(itrnsp=0)
+    assert np.array_equal(bits(ops[3]), bits(want_atx))      # atimes(itrnsp=1)
+    assert np.array_equal(bits(ops[4]), bits(x / small["sa"][:N]))  # asolve (bondc.f:860)
+    # linbcg on COMMON /mat/: the reference's own 50x50 run (golden sq_bondc_p60)
+    raw = (tmp_path / "linbcg.bin").read_bytes()
+    st, it = np.frombuffer(raw[:8], np.int32)
+    err = np.frombuffer(raw[8:16], np.float64)[0]
+    v = np.frombuffer(raw[16:], np.float64)
+    assert st == 0
+    md = G.meta("sq_bondc_p60")
+    assert abs(int(it) - md["iter"]) <= 1 and err <= 1e-8
+    assert np.max(np.abs(v - np.array(md["vint"]))) < 1e-6
+    gt, gb = C.c_double(), C.c_double()
+    O.lib().or_currents(0, 50, 50, 0, len(big["b1"]), big["b1"], big["b2"], big["gval"],
+                        big["diag"], np.ascontiguousarray(v), 1.0, 1e-10, 0, C.byref(gt),
+                        C.byref(gb))
+    assert abs(gt.value - md["gtop"]) <= 1e-10 * md["gtop"]
+    assert abs(gb.value - md["gbot"]) <= 1e-6 * md["gbot"]
