@@ -172,8 +172,13 @@ def solve(args):
 
 def main(cases):
     os.makedirs(OUT, exist_ok=True)
-    jobs = [(c, tol) for c in cases for tol in TOLS]
-    with Pool(min(len(jobs), 6)) as pool:
+    def done(c, tol):
+        path = os.path.join(OUT, c + ".json")
+        return os.path.exists(path) and ("%g" % tol) in json.load(open(path)).get("solves", {})
+    jobs = [(c, tol) for c in cases for tol in TOLS if not done(c, tol)]
+    if not jobs:
+        return
+    with Pool(min(len(jobs), int(os.environ.get("GOLDEN_PROCS", 6)))) as pool:
         for case, tol, ii, seed, info, res in pool.imap_unordered(solve, jobs):
             path = os.path.join(OUT, case + ".json")
             doc = json.load(open(path)) if os.path.exists(path) else {}

@@ -24,7 +24,7 @@ run() {  # run NAME TIMEOUT CMD...
 }
 for step in "$@"; do
   case "$step" in
-    tests) run pytest_gpu 900 python -m pytest tests -m gpu -q -rs -x ;;
+    tests) run pytest_gpu 900 python -u -m pytest tests -m gpu -v -rs -x --timeout 300 --timeout-method thread ;;
     testsall) run pytest_gpu 900 python -m pytest tests -m gpu -q -rs ;;
     tests_march) run pytest_march 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread -k "march or division or resident" ;;
     probe) run march_probe 600 python tools/march_probe.py ;;
