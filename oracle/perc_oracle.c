@@ -657,6 +657,109 @@ int or_label_sitebond(int lattice, int m, int n, int pbc, int nb,
   return cln;
 }
 
+/* Mixed site-then-bond labeling, union-find replay of or_label_sitebond
+   (Square/sitebond.f:187-400): the same labels, sizes, cln and maxcn/maxcs,
+   in O(N alpha).  A merge relabels oldcn -> lcn everywhere
+   (sitebond.f:330-352); here label oldcn is linked to lcn in a union-find
+   over label ids and every stored label is resolved through it. */
+static int lab_find(int *lp, int x) {
+  int r = x;
+  while (lp[r] != r) r = lp[r];
+  while (lp[x] != r) { int nx = lp[x]; lp[x] = r; x = nx; }
+  return r;
+}
+int or_label_sitebond_replay(int lattice, int m, int n, int pbc, int nb,
+                             const int *b1, const int *b2,
+                             const int *sorder, int tsites,
+                             const int *o1, const int *o2, int tbonds,
+                             int *s, int *blabel, int *csize, int *maxcn_o,
+                             int *maxcs_o) {
+  int t = m * n, i, j, k, cln = 1, maxcn, maxcs, lcn = 0, lcs = 0;
+  size_t cap = (size_t)t + (size_t)nb + 2;
+  int *sp = (int *)calloc((size_t)t + 1, sizeof(int));
+  int *lp = (int *)malloc(sizeof(int) * cap);
+  bond_index bi;
+  (void)lattice; (void)pbc;
+  bi.first = (int *)calloc((size_t)t + 2, sizeof(int));
+  bi.b2 = b2;
+  bi.t = t;
+  for (k = 0; k < nb; k++) bi.first[b1[k] + 1]++;
+  for (i = 1; i <= t + 1; i++) bi.first[i] += bi.first[i - 1];
+  for (k = 0; k < (int)cap; k++) lp[k] = k;
+  memset(blabel, 0, sizeof(int) * (size_t)nb);
+  memset(csize, 0, sizeof(int) * cap);
+  for (i = 1; i <= tsites; i++) { /* sitebond.f:187-196 */
+    int sn = sorder[i - 1];
+    if (sn > 0) sp[sn] = cln;
+    csize[cln] = 1;
+    cln++;
+  }
+  maxcn = 1;
+  maxcs = 1;
+  for (i = 1; i <= tbonds; i++) { /* sitebond.f:223-400 */
+    int a = o1[i - 1], bb = o2[i - 1];
+    j = a > 0 ? bidx(&bi, a, bb) : -1; /* the (0,0) spill matches no bond */
+    if (j >= 0) {
+      int sa = sp[b1[j]] ? lab_find(lp, sp[b1[j]]) : 0;
+      int sb = sp[b2[j]] ? lab_find(lp, sp[b2[j]]) : 0, oldcn;
+      if (sa == 0 && sb == 0) {
+        blabel[j] = cln; csize[cln] = 1; cln++;
+      } else if (sa > 0 && sb == 0) {
+        lcn = sa; lcs = csize[sa]; blabel[j] = lcn; csize[sa] = lcs + 1;
+      } else if (sa == 0 && sb > 0) {
+        lcn = sb; lcs = csize[sb]; blabel[j] = lcn; csize[sb] = lcs + 1;
+      } else if (sa == sb) {
+        lcn = sa; lcs = csize[sa]; blabel[j] = lcn; csize[sa] = lcs + 1;
+      } else {
+        if (csize[sa] > csize[sb]) { lcn = sa; oldcn = sb; }
+        else { lcn = sb; oldcn = sa; }
+        lcs = csize[lcn];
+        blabel[j] = lcn;
+        lp[oldcn] = lcn;
+        csize[lcn] = lcs + csize[oldcn] + 1;
+        csize[oldcn] = 0;
+      }
+    }
+    if (csize[lcn] > maxcs) { maxcs = csize[lcn]; maxcn = lcn; }
+  }
+  for (j = 1; j <= t; j++) s[j - 1] = sp[j] ? lab_find(lp, sp[j]) : 0;
+  for (j = 0; j < nb; j++) blabel[j] = blabel[j] ? lab_find(lp, blabel[j]) : 0;
+  free(sp);
+  free(lp);
+  free(bi.first);
+  if (maxcn_o) *maxcn_o = maxcn;
+  if (maxcs_o) *maxcs_o = maxcs;
+  return cln;
+}
+
+/* Canonical partition ids (test helpers): canon[s-1] = the minimum site of
+   the cluster site s belongs to, 0 for a site in no cluster.  Sites: by the
+   site label s[]; bonds: a site is in the cluster of every occupied bond
+   (label > 0) it ends. */
+void or_canon_sites(int t, const int *s, int maxlab, int *canon) {
+  int *mins = (int *)malloc(sizeof(int) * ((size_t)maxlab + 1)), k;
+  for (k = 0; k <= maxlab; k++) mins[k] = 0;
+  for (k = 1; k <= t; k++) {
+    int l = s[k - 1];
+    if (l > 0 && mins[l] == 0) mins[l] = k; /* ascending k: first = min */
+  }
+  for (k = 1; k <= t; k++) canon[k - 1] = s[k - 1] > 0 ? mins[s[k - 1]] : 0;
+  free(mins);
+}
+void or_canon_bonds(int t, int nb, const int *b1, const int *b2, const int *label, int maxlab,
+                    int *canon) {
+  int *mins = (int *)malloc(sizeof(int) * ((size_t)maxlab + 1)), k;
+  for (k = 0; k <= maxlab; k++) mins[k] = 0;
+  for (k = 0; k < nb; k++) {
+    int l = label[k];
+    if (l > 0 && (mins[l] == 0 || b1[k] < mins[l])) mins[l] = b1[k];
+  }
+  for (k = 0; k < t; k++) canon[k] = 0;
+  for (k = 0; k < nb; k++)
+    if (label[k] > 0) canon[b1[k] - 1] = canon[b2[k] - 1] = mins[label[k]];
+  free(mins);
+}
+
 /* ======================================================================
  * Mixed bonds-then-sites labeling, literal.  Square/bondsite.f:170-322
  * (Triangular/bondsite.f: the same loops, scn 6).  border = shuffled bond

@@ -74,6 +74,17 @@ int or_label_sitebond(int lattice, int m, int n, int pbc, int nb,
                       const int *o1, const int *o2, int tbonds,
                       int *s, int *blabel, int *csize, int *maxcn, int *maxcs);
 
+/* same, union-find replay (O(N alpha)); csize cap >= t + nb + 2 */
+int or_label_sitebond_replay(int lattice, int m, int n, int pbc, int nb,
+                             const int *b1, const int *b2,
+                             const int *sorder, int tsites,
+                             const int *o1, const int *o2, int tbonds,
+                             int *s, int *blabel, int *csize, int *maxcn, int *maxcs);
+/* canonical partition ids (min site of the cluster; 0 = no cluster) */
+void or_canon_sites(int t, const int *s, int maxlab, int *canon);
+void or_canon_bonds(int t, int nb, const int *b1, const int *b2, const int *label, int maxlab,
+                    int *canon);
+
 /* mixed bonds-then-sites: Square/bondsite.f:170-322 (literal); border =
    bond ids (0: spill slot), s[t], blabel[nb], csize[t+nb+2]; returns cln */
 int or_label_bondsite(int lattice, int m, int n, int pbc, int nb,

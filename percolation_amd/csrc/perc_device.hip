@@ -9,8 +9,6 @@
 // global dot products (reductions) are re-associated, deterministically
 // (fixed grid, fixed tree, last-arriving workgroup sums the partials in
 // index order).
-#include <hipcub/hipcub.hpp>
-
 #include "perc_internal.h"
 
 namespace perc {
@@ -240,10 +238,28 @@ __global__ void k_occupy_sites(const int* order, int count, int t, uint8_t* socc
 }
 
 // ---------------------------------------------------------------------------
-// Connected components: lock-free union-find, roots always linked larger ->
-// smaller, so the final root of a component is its minimum site id (a
-// canonical, schedule-independent partition).  Path halving; stale L1 reads
-// only cost retries (parents only move to smaller ancestors).
+// Connected components (the partition of bondc.f:194-393, site.f:167-289,
+// sitebond.f:190-400).  Roots are always linked larger -> smaller, so the
+// final root of a component is its minimum site id: a canonical,
+// schedule-independent partition.  Three passes:
+//
+//  k_cc_tile      one workgroup per kCcW x kCcH block of sites.  The links
+//                 inside the block are united in an LDS union-find (local
+//                 index order = site order inside a block, so the local root
+//                 is the block-local minimum site); then every site's parent
+//                 (that root's global id) and member flag are written once,
+//                 coalesced.  No global atomics.
+//  k_cc_merge     only the links that cross a block edge (sites on the top
+//                 row or the edge columns of a block: ~1/32 + 2/128 of them)
+//                 are united in the global array (lock-free CAS, same rule).
+//  k_cc_compress  parent[s] = final root; cluster count reduced per
+//                 workgroup (one atomic per workgroup of a fixed grid).
+//
+// Path halving (LDS and global): stale reads only cost retries, parents only
+// ever move to smaller ancestors, and only roots are CASed.
+constexpr int kCcW = 128, kCcH = 32, kCcSites = kCcW * kCcH, kCcThreads = 256;
+constexpr int kReduceGrid = 1024;  // fixed grid of the counting passes
+
 __device__ __forceinline__ int find_root(int* parent, int x) {
   int p = parent[x];
   while (p != x) {
@@ -267,20 +283,39 @@ __device__ __forceinline__ void unite(int* parent, int a, int b) {
   }
 }
 
-__global__ void k_cc_init(int t, int* parent, uint8_t* member, uint8_t* bot, uint8_t* top) {
-  const long long s = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (s > t) return;
-  parent[s] = (int)s;
-  member[s] = 0;
-  bot[s] = 0;
-  top[s] = 0;
+// link predicate of the forward bond id = (s, q), s < q (bondc.f:194-393:
+// occupied bond; site.f: both sites occupied; sitebond.f / the mixed
+// conductance rule: bond and both sites)
+__device__ __forceinline__ bool cc_link(int kind, const uint8_t* bocc, const uint8_t* socc,
+                                        long long id, int s, int q) {
+  if (kind == PERC_BOND) return bocc[id];
+  if (kind == PERC_SITE) return socc[s] && socc[q];
+  return bocc[id] && socc[s] && socc[q];
 }
 
-__global__ void k_cc_hook(Geom g, int kind, const int* bond_first, const uint8_t* bocc,
-                          const uint8_t* socc, int* parent, uint8_t* member) {
-  for (int s = blockIdx.x * blockDim.x + threadIdx.x + 1; s <= g.t;
-       s += gridDim.x * blockDim.x) {
-    if (kind != PERC_BOND && socc[s]) member[s] = 1;
+__global__ __launch_bounds__(kCcThreads) void k_cc_tile(Geom g, int kind, const int* bond_first,
+                                                        const uint8_t* bocc,
+                                                        const uint8_t* socc, int* parent,
+                                                        uint8_t* member) {
+  __shared__ int lp[kCcSites];
+  __shared__ uint8_t lm[kCcSites];
+  const int ntx = cdiv(g.m, kCcW);
+  const int tx = blockIdx.x % ntx, ty = blockIdx.x / ntx;
+  const int c0 = tx * kCcW, r0 = ty * kCcH;
+  const int tw = min(kCcW, g.m - c0), th = min(kCcH, g.n - r0);
+  for (int li = threadIdx.x; li < kCcSites; li += kCcThreads) {
+    lp[li] = li;
+    lm[li] = 0;
+  }
+  __syncthreads();
+  for (int li = threadIdx.x; li < kCcSites; li += kCcThreads) {
+    const int lr = li / kCcW, lc = li % kCcW;
+    if (lr >= th || lc >= tw) continue;
+    const int s = (r0 + lr) * g.m + c0 + lc + 1;
+    if (kind != PERC_BOND) {
+      if (!socc[s]) continue;  // an empty site has no links
+      lm[li] = 1;
+    }
     if (s > g.t - 1) continue;
     int nn[6];
     nearestn(g, s, nn);
@@ -289,41 +324,61 @@ __global__ void k_cc_hook(Geom g, int kind, const int* bond_first, const uint8_t
     for (int k = 0; k < g.scn; ++k) {
       const int q = nn[k];
       if (q <= s) continue;
-      bool link;
-      if (kind == PERC_BOND) link = bocc[fb + r];
-      else if (kind == PERC_SITE) link = socc[s] && socc[q];
-      else link = bocc[fb + r] && socc[s] && socc[q];
+      const bool link = cc_link(kind, bocc, socc, fb + r, s, q);
       ++r;
-      if (link) {
-        if (kind == PERC_BOND) { member[s] = 1; member[q] = 1; }
-        unite(parent, s, q);
+      if (!link) continue;
+      if (kind == PERC_BOND) lm[li] = 1;
+      const int qr = (q - 1) / g.m - r0, qc = (q - 1) % g.m - c0;
+      if (qr < 0 || qr >= th || qc < 0 || qc >= tw) continue;  // crossing: k_cc_merge
+      const int lq = qr * kCcW + qc;
+      if (kind == PERC_BOND) lm[lq] = 1;
+      // LDS union (larger local root -> smaller)
+      int a = li, b = lq;
+      while (true) {
+        a = find_root(lp, a);
+        b = find_root(lp, b);
+        if (a == b) break;
+        if (a < b) { const int tmp = a; a = b; b = tmp; }
+        const int old = atomicCAS(&lp[a], a, b);
+        if (old == a) break;
+        a = old;
       }
     }
   }
-}
-
-// Final flattening: a read-only walk, then each thread writes only its own
-// entry.  (Path halving here would let one thread overwrite another
-// thread's freshly written root with an intermediate ancestor.)
-__global__ void k_cc_compress(int t, int* parent) {
-  const int s = blockIdx.x * blockDim.x + threadIdx.x + 1;
-  if (s > t) return;
-  int x = s, p = parent[x];
-  while (p != x) {
-    x = p;
-    p = parent[x];
+  __syncthreads();
+  for (int li = threadIdx.x; li < kCcSites; li += kCcThreads) {
+    const int lr = li / kCcW, lc = li % kCcW;
+    if (lr >= th || lc >= tw) continue;
+    int x = li, p = lp[x];
+    while (p != x) {
+      x = p;
+      p = lp[x];
+    }
+    const int s = (r0 + lr) * g.m + c0 + lc + 1;
+    parent[s] = (r0 + x / kCcW) * g.m + c0 + x % kCcW + 1;
+    member[s] = lm[li];
   }
-  parent[s] = x;
 }
 
-// spanning flags at roots: bottom row (sites 1..m) / top row (t-m+1..t)
-__global__ void k_span_flags(Geom g, int kind, const int* bond_first, const uint8_t* bocc,
-                             const uint8_t* socc, const int* parent, uint8_t* bot, uint8_t* top) {
-  const int s = blockIdx.x * blockDim.x + threadIdx.x + 1;
-  if (s > g.t) return;
-  if (kind == PERC_BOND) {
-    // bondc.f:419-441: a bond with b1 <= m, and one with b2 > t-m
-    if (s > g.t - 1) return;
+// one workgroup per lattice row: the sites whose forward links may leave
+// their block (block top row: every column; other rows: the block edge
+// columns and the last column), then only the links that do
+__global__ __launch_bounds__(kCcThreads) void k_cc_merge(Geom g, int kind, const int* bond_first,
+                                                         const uint8_t* bocc,
+                                                         const uint8_t* socc, int* parent,
+                                                         uint8_t* member) {
+  const int row = blockIdx.x;
+  const bool full = row % kCcH == kCcH - 1;
+  const int ntx = cdiv(g.m, kCcW);
+  const int cnt = full ? g.m : 2 * ntx + 1;
+  for (int j = threadIdx.x; j < cnt; j += kCcThreads) {
+    int c;
+    if (full) c = j;
+    else if (j == 2 * ntx) c = g.m - 1;
+    else c = min((j >> 1) * kCcW + (j & 1) * (kCcW - 1), g.m - 1);
+    const int s = row * g.m + c + 1;
+    if (s > g.t - 1) continue;
+    if (kind != PERC_BOND && !socc[s]) continue;
     int nn[6];
     nearestn(g, s, nn);
     const int fb = bond_first[s];
@@ -331,45 +386,189 @@ __global__ void k_span_flags(Geom g, int kind, const int* bond_first, const uint
     for (int k = 0; k < g.scn; ++k) {
       const int q = nn[k];
       if (q <= s) continue;
-      if (bocc[fb + r]) {
-        if (s <= g.m) bot[parent[s]] = 1;
-        if (q > g.t - g.m) top[parent[q]] = 1;
-      }
+      const bool link = cc_link(kind, bocc, socc, fb + r, s, q);
       ++r;
+      if (!link) continue;
+      const int qrow = (q - 1) / g.m, qcol = (q - 1) % g.m;
+      if (qrow / kCcH == row / kCcH && qcol / kCcW == c / kCcW) continue;  // inside: k_cc_tile
+      if (kind == PERC_BOND) member[q] = 1;
+      unite(parent, s, q);
     }
-  } else {
-    // site.f:319-333: an occupied site in the bottom and in the top row
-    if (!socc[s]) return;
-    if (s <= g.m) bot[parent[s]] = 1;
-    if (s > g.t - g.m) top[parent[s]] = 1;
   }
 }
 
-__global__ void k_span_collect(int t, const int* parent, const uint8_t* member,
-                               const uint8_t* bot, const uint8_t* top, int* counters) {
-  const int s = blockIdx.x * blockDim.x + threadIdx.x + 1;
-  if (s > t) return;
-  if (!member[s] || parent[s] != s) return;
-  atomicAdd(&counters[1], 1);
-  if (bot[s] && top[s]) {
-    const int idx = atomicAdd(&counters[0], 1);
-    if (idx < kMaxSpanList) counters[8 + idx] = s;
+__device__ __forceinline__ int wave_sum_int(int v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+
+// sum of v over the workgroup of kCcThreads, then one atomic add
+__device__ __forceinline__ void block_count_add(int v, int* counter) {
+  __shared__ int s_cnt[kCcThreads / 64];
+  v = wave_sum_int(v);
+  if ((threadIdx.x & 63) == 0) s_cnt[threadIdx.x >> 6] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int tot = 0;
+#pragma unroll
+    for (int w = 0; w < kCcThreads / 64; ++w) tot += s_cnt[w];
+    if (tot) atomicAdd(counter, tot);
   }
 }
 
-__global__ void k_count_root(int t, const int* parent, const uint8_t* member, int root,
-                             int* counter) {
-  const int s = blockIdx.x * blockDim.x + threadIdx.x + 1;
-  if (s > t) return;
-  const bool in = member[s] && parent[s] == root;
-  const unsigned long long b = __ballot(in);
-  if ((threadIdx.x & 63) == 0 && b) atomicAdd(counter, __popcll(b));
+// final flattening: a read-only walk, then each thread writes only its own
+// entry (path halving here would let one thread overwrite another's freshly
+// written root with an intermediate ancestor); counts the clusters (member
+// roots)
+__global__ __launch_bounds__(kCcThreads) void k_cc_compress(int t, int* parent,
+                                                            const uint8_t* member,
+                                                            int* nclusters) {
+  int cnt = 0;
+  for (int s = blockIdx.x * kCcThreads + threadIdx.x + 1; s <= t; s += gridDim.x * kCcThreads) {
+    int x = s, p = parent[x];
+    while (p != x) {
+      x = p;
+      p = parent[x];
+    }
+    parent[s] = x;
+    cnt += x == s && member[s];
+  }
+  block_count_add(cnt, nclusters);
+}
+
+// Spanning clusters (bondc.f:413-456, site.f:309-344, sitebond.f:423-458).
+// The root is the component's minimum site, so a component reaches the
+// bottom row (bond: a bond with b1 <= m; site / mixed: an occupied site
+// there) iff its root is <= m; it reaches the top row (bond: b2 > t-m; site:
+// an occupied site) iff one of the m top-row sites is a member of it.  One
+// workgroup: flag[root] for the top-row members whose root is <= m, then the
+// flagged roots in ascending order (ballot compaction) -> counters[0] =
+// count, counters[8..] = the first kMaxSpanList roots.
+__global__ __launch_bounds__(1024) void k_span_top(Geom g, const int* parent,
+                                                   const uint8_t* member, uint8_t* flag,
+                                                   int* counters) {
+  __shared__ int s_w[16];
+  __shared__ int s_base;
+  const int m = g.m;
+  for (int c = threadIdx.x; c <= m; c += 1024) flag[c] = 0;
+  if (threadIdx.x == 0) s_base = 0;
+  __syncthreads();
+  for (int c = threadIdx.x; c < m; c += 1024) {
+    const int s = g.t - m + 1 + c;
+    if (member[s]) {
+      const int root = parent[s];
+      if (root <= m) flag[root] = 1;
+    }
+  }
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  for (int base = 1; base <= m; base += 1024) {
+    const int c = base + threadIdx.x;
+    const bool f = c <= m && flag[c];
+    const unsigned long long b = __ballot(f);
+    if (lane == 0) s_w[wid] = __popcll(b);
+    __syncthreads();
+    int off = s_base;
+    for (int w = 0; w < wid; ++w) off += s_w[w];
+    off += __popcll(b & ((1ull << lane) - 1ull));
+    if (f && off < kMaxSpanList) counters[8 + off] = c;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      int tot = 0;
+      for (int w = 0; w < 16; ++w) tot += s_w[w];
+      s_base += tot;
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) counters[0] = s_base;
+}
+
+// member sites of the component rooted at root (fixed grid, one atomic per
+// workgroup)
+__global__ __launch_bounds__(kCcThreads) void k_count_root(int t, const int* parent,
+                                                           const uint8_t* member, int root,
+                                                           int* counter) {
+  int cnt = 0;
+  for (int s = blockIdx.x * kCcThreads + threadIdx.x + 1; s <= t; s += gridDim.x * kCcThreads)
+    cnt += member[s] && parent[s] == root;
+  block_count_add(cnt, counter);
 }
 
 __global__ void k_canon(int t, const int* parent, const uint8_t* member, int* canon) {
   const int s = blockIdx.x * blockDim.x + threadIdx.x + 1;
   if (s > t) return;
   canon[s - 1] = member[s] ? parent[s] : 0;
+}
+
+// ---------------------------------------------------------------------------
+// Exclusive scan of int32 (the lattice build's bond offsets and CSR row
+// pointers; once per context).  kScanItems per workgroup: per-workgroup
+// totals, one workgroup scans the totals, then each workgroup scans its
+// items plus its offset.
+constexpr int kScanPer = 4, kScanItems = kCcThreads * kScanPer;
+
+// exclusive prefix of v over the workgroup (thread order) + total
+__device__ __forceinline__ int block_exclusive_scan(int v, int* total) {
+  __shared__ int s_w[kCcThreads / 64];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  int inc = v;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const int y = __shfl_up(inc, off, 64);
+    if (lane >= off) inc += y;
+  }
+  if (lane == 63) s_w[wid] = inc;
+  __syncthreads();
+  int before = 0, tot = 0;
+#pragma unroll
+  for (int w = 0; w < kCcThreads / 64; ++w) {
+    before += w < wid ? s_w[w] : 0;
+    tot += s_w[w];
+  }
+  __syncthreads();
+  *total = tot;
+  return before + inc - v;
+}
+
+__global__ __launch_bounds__(kCcThreads) void k_scan_totals(const int* in, int n, int* totals) {
+  const long long i0 = (long long)blockIdx.x * kScanItems + threadIdx.x * kScanPer;
+  int v = 0;
+#pragma unroll
+  for (int k = 0; k < kScanPer; ++k) v += i0 + k < n ? in[i0 + k] : 0;
+  int tot;
+  block_exclusive_scan(v, &tot);
+  if (threadIdx.x == 0) totals[blockIdx.x] = tot;
+}
+
+__global__ __launch_bounds__(kCcThreads) void k_scan_top(int* totals, int nt) {
+  int carry = 0;
+  for (int base = 0; base < nt; base += kCcThreads) {
+    const int i = base + threadIdx.x;
+    const int v = i < nt ? totals[i] : 0;
+    int tot;
+    const int ex = block_exclusive_scan(v, &tot);
+    if (i < nt) totals[i] = carry + ex;
+    carry += tot;
+  }
+}
+
+__global__ __launch_bounds__(kCcThreads) void k_scan_apply(const int* in, int n,
+                                                           const int* totals, int* out) {
+  const long long i0 = (long long)blockIdx.x * kScanItems + threadIdx.x * kScanPer;
+  int v[kScanPer], sum = 0;
+#pragma unroll
+  for (int k = 0; k < kScanPer; ++k) {
+    v[k] = i0 + k < n ? in[i0 + k] : 0;
+    sum += v[k];
+  }
+  int tot;
+  int run = totals[blockIdx.x] + block_exclusive_scan(sum, &tot);
+#pragma unroll
+  for (int k = 0; k < kScanPer; ++k) {
+    if (i0 + k < n) out[i0 + k] = run;
+    run += v[k];
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -2772,13 +2971,15 @@ hipError_t dmalloc(T** p, size_t n) {
 }
 
 hipError_t exclusive_scan(const int* in, int* out, int n, hipStream_t st) {
-  size_t bytes = 0;
-  HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, bytes, in, out, n, st));
-  void* tmp = nullptr;
-  HIP_TRY(hipMalloc(&tmp, bytes ? bytes : 1));
-  hipError_t e = hipcub::DeviceScan::ExclusiveSum(tmp, bytes, in, out, n, st);
+  const int nt = cdiv(n, kScanItems);
+  int* totals = nullptr;
+  HIP_TRY(dmalloc(&totals, nt));
+  k_scan_totals<<<nt, kCcThreads, 0, st>>>(in, n, totals);
+  k_scan_top<<<1, kCcThreads, 0, st>>>(totals, nt);
+  k_scan_apply<<<nt, kCcThreads, 0, st>>>(in, n, totals, out);
+  hipError_t e = hipGetLastError();
   hipError_t e2 = hipStreamSynchronize(st);
-  hipFree(tmp);
+  hipFree(totals);
   return e != hipSuccess ? e : e2;
 }
 
@@ -2828,7 +3029,6 @@ hipError_t dev_build_lattice(perc_ctx* h) {
   HIP_TRY(dmalloc(&d.order, (size_t)std::max<long long>(h->nb, t) + 8));
   HIP_TRY(dmalloc(&d.parent, t + 8));
   HIP_TRY(dmalloc(&d.member, t + 8));
-  HIP_TRY(dmalloc(&d.bot, t + 8));
   HIP_TRY(dmalloc(&d.top, t + 8));
   HIP_TRY(dmalloc(&d.counters, 8 + kMaxSpanList));
   // CG (vectors padded to even length for the 16 B paths)
@@ -2906,7 +3106,7 @@ hipError_t dev_alloc_matrix(perc_ctx* h, int N, long long nnz) {
 void dev_free_all(perc_ctx* h) {
   DeviceBuffers& d = h->d;
   void* ptrs[] = {d.bond_first, d.rowptr, d.col, d.val, d.diag, d.rhs, d.code, d.dtab, d.sflag, d.bocc, d.socc,
-                  d.order, d.parent, d.member, d.bot, d.top, d.counters, d.x, d.r,
+                  d.order, d.parent, d.member, d.top, d.counters, d.x, d.r,
                   d.p0, d.p1, d.q, d.partials, d.tickets, d.scal, d.err_hist, d.iout,
                   d.res_xch, d.res_part, d.res_bar, d.bw, d.code_sm};
   for (void* p : ptrs)
@@ -2948,19 +3148,19 @@ hipError_t dev_label(perc_ctx* h, int* nspan, int* span_list, int* nclusters) {
   hipStream_t st = h->stream;
   DeviceBuffers& d = h->d;
   const int kind = h->last.kind;
-  k_cc_init<<<blocks_for(g.t + 1), kBlock, 0, st>>>(g.t, d.parent, d.member, d.bot, d.top);
-  HIP_TRY(dbg_sync(st, "k_cc_init"));
-  k_cc_hook<<<blocks_for(g.t), kBlock, 0, st>>>(g, kind, d.bond_first, d.bocc, d.socc, d.parent,
-                                                 d.member);
-  HIP_TRY(dbg_sync(st, "k_cc_hook"));
-  k_cc_compress<<<blocks_for(g.t), kBlock, 0, st>>>(g.t, d.parent);
-  HIP_TRY(dbg_sync(st, "k_cc_compress"));
-  k_span_flags<<<blocks_for(g.t), kBlock, 0, st>>>(g, kind, d.bond_first, d.bocc, d.socc,
-                                                    d.parent, d.bot, d.top);
   HIP_TRY(hipMemsetAsync(d.counters, 0, sizeof(int) * (8 + kMaxSpanList), st));
-  k_span_collect<<<blocks_for(g.t), kBlock, 0, st>>>(g.t, d.parent, d.member, d.bot, d.top,
-                                                      d.counters);
-  HIP_TRY(hipGetLastError());
+  const int tiles = cdiv(g.m, kCcW) * cdiv(g.n, kCcH);
+  k_cc_tile<<<tiles, kCcThreads, 0, st>>>(g, kind, d.bond_first, d.bocc, d.socc, d.parent,
+                                          d.member);
+  HIP_TRY(dbg_sync(st, "k_cc_tile"));
+  k_cc_merge<<<g.n, kCcThreads, 0, st>>>(g, kind, d.bond_first, d.bocc, d.socc, d.parent,
+                                         d.member);
+  HIP_TRY(dbg_sync(st, "k_cc_merge"));
+  k_cc_compress<<<std::min(cdiv(g.t, kCcThreads), kReduceGrid), kCcThreads, 0, st>>>(
+      g.t, d.parent, d.member, d.counters + 1);
+  HIP_TRY(dbg_sync(st, "k_cc_compress"));
+  k_span_top<<<1, 1024, 0, st>>>(g, d.parent, d.member, d.top, d.counters);
+  HIP_TRY(dbg_sync(st, "k_span_top"));
   int hc[8 + kMaxSpanList];
   HIP_TRY(hipMemcpyAsync(hc, d.counters, sizeof(hc), hipMemcpyDeviceToHost, st));
   HIP_TRY(hipStreamSynchronize(st));
@@ -2973,8 +3173,8 @@ hipError_t dev_label(perc_ctx* h, int* nspan, int* span_list, int* nclusters) {
 hipError_t dev_span_sites(perc_ctx* h, int root, int* count) {
   hipStream_t st = h->stream;
   HIP_TRY(hipMemsetAsync(h->d.counters + 2, 0, sizeof(int), st));
-  k_count_root<<<blocks_for(h->g.t), kBlock, 0, st>>>(h->g.t, h->d.parent, h->d.member, root,
-                                                       h->d.counters + 2);
+  k_count_root<<<std::min(cdiv(h->g.t, kCcThreads), kReduceGrid), kCcThreads, 0, st>>>(
+      h->g.t, h->d.parent, h->d.member, root, h->d.counters + 2);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipMemcpyAsync(count, h->d.counters + 2, sizeof(int), hipMemcpyDeviceToHost, st));
   return hipStreamSynchronize(st);

@@ -85,8 +85,7 @@ struct DeviceBuffers {
   // labeling
   int* parent = nullptr;     // t+1
   uint8_t* member = nullptr; // t+1 (site belongs to some cluster)
-  uint8_t* bot = nullptr;    // t+1
-  uint8_t* top = nullptr;    // t+1
+  uint8_t* top = nullptr;    // t+1 (spanning-root flags, m+1 used)
   int* counters = nullptr;   // [0]=nspan [1]=nclusters [2]=span_sites, then list
   // CG
   double* x = nullptr;

@@ -49,6 +49,10 @@ def lib():
         "or_label_sites_replay": (i, [i, i, i, i, _I, i, _I, _I, _IP, _IP]),
         "or_label_sitebond": (i, [i, i, i, i, i, _I, _I, _I, i, _I, _I, i, _I, _I, _I, _IP, _IP]),
         "or_label_bondsite": (i, [i, i, i, i, i, _I, _I, _I, i, _I, i, _I, _I, _I, _IP, _IP]),
+        "or_label_sitebond_replay": (i, [i, i, i, i, i, _I, _I, _I, i, _I, _I, i, _I, _I, _I, _IP,
+                                         _IP]),
+        "or_canon_sites": (None, [i, _I, i, _I]),
+        "or_canon_bonds": (None, [i, i, _I, _I, _I, i, _I]),
         "or_span_bonds": (i, [i, i, i, _I, _I, _I, _I, i]),
         "or_span_sites": (i, [i, i, _I, _I, i, i]),
         "or_bond_values": (None, [i, i, _I, _I, _I, _I, i, d, d, _D]),
@@ -128,6 +132,33 @@ def label_sites(lattice, m, n, pbc, order, tsites, literal=True):
     f = L.or_label_sites_literal if literal else L.or_label_sites_replay
     cln = f(lattice, m, n, pbc, order, tsites, s, csize, C.byref(mx), C.byref(ms))
     return s, csize, cln, mx.value, ms.value
+
+
+def label_sitebond(lattice, m, n, pbc, b1, b2, sorder, tsites, o1, o2, tbonds, literal=True):
+    """mixed site-then-bond labels (sitebond.f:187-400): literal or O(N alpha) replay"""
+    L = lib()
+    t, nb = m * n, len(b1)
+    s, bl, csize = i32(t), i32(nb), i32(t + nb + 2)
+    mx, ms = C.c_int(), C.c_int()
+    f = L.or_label_sitebond if literal else L.or_label_sitebond_replay
+    cln = f(lattice, m, n, pbc, nb, b1, b2, sorder, tsites, o1, o2, tbonds, s, bl, csize,
+            C.byref(mx), C.byref(ms))
+    return s, bl, csize, cln, mx.value, ms.value
+
+
+def canon_sites(s, maxlab):
+    """canonical partition ids from site labels (min site of the cluster)"""
+    out = i32(len(s))
+    lib().or_canon_sites(len(s), np.ascontiguousarray(s, dtype=np.int32), int(maxlab), out)
+    return out
+
+
+def canon_bonds(t, b1, b2, label, maxlab):
+    """canonical partition ids per site from bond labels"""
+    out = i32(t)
+    lib().or_canon_bonds(t, len(b1), b1, b2, np.ascontiguousarray(label, dtype=np.int32),
+                         int(maxlab), out)
+    return out
 
 
 def conductance(lattice, m, n, pbc, b1, b2, gval, Va=1.0, itol=2, tol=1e-8,

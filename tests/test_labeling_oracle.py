@@ -1,0 +1,208 @@
+"""GPU labeling against the oracle's own replays, directly (no libperc replay
+in between), over block-edge geometries and at the BASELINE config sizes.
+
+The GPU labels with an LDS-tiled union-find (k_cc_tile over 128 x 32 blocks
+of sites, k_cc_merge for the links that cross a block edge, k_cc_compress):
+the partition (canonical id = minimum site of the cluster) must equal the
+partition of the reference's sequential labeling (Square/bondc.f:194-393,
+site.f:167-289, sitebond.f:187-400) bit for bit, and a spanning cluster must
+be found exactly when the reference finds one (bondc.f:413-456,
+site.f:309-344, sitebond.f:423-458).  The oracle side is oracle/perc_oracle.c
+(O(N alpha) replays; the mixed replay is pinned to the literal loop here on
+CPU).
+"""
+import numpy as np
+import pytest
+
+import oracle_lib as O
+from percolation_amd import _lib as PL
+from percolation_amd import api
+
+
+def _perm_ids(N, seed):
+    """uniform 1-based id permutation (the bench's occupation orders)"""
+    return (np.random.default_rng(seed).permutation(N) + 1).astype(np.int32)
+
+
+def _pairs(b1, b2, ids, k):
+    o1, o2 = O.i32(len(b1) + 1), O.i32(len(b1) + 1)
+    sel = ids[:k].astype(np.int64) - 1
+    o1[:k], o2[:k] = b1[sel], b2[sel]
+    return o1, o2
+
+
+def oracle_bond(lat, m, n, pbc, ids, tb):
+    b1, b2 = O.bond_list(lat, m, n, pbc)
+    o1, o2 = _pairs(b1, b2, ids, tb)
+    label, csize, cln, _, _ = O.label_bonds(lat, m, n, pbc, b1, b2, o1, o2, tb, literal=False)
+    perccln = O.lib().or_span_bonds(m, n, len(b1), b1, b2, label, csize, cln)
+    canon = O.canon_bonds(m * n, b1, b2, label, cln)
+    span_root = 0
+    if perccln > 0:
+        k = int(np.nonzero(label == perccln)[0][0])
+        span_root = int(canon[b1[k] - 1])
+    return canon, perccln, span_root
+
+
+def oracle_site(lat, m, n, pbc, order, ts):
+    o = O.i32(m * n + 1)
+    o[:len(order)] = order
+    s, csize, cln, _, _ = O.label_sites(lat, m, n, pbc, o, ts, literal=False)
+    perccln = O.lib().or_span_sites(m, n, s, csize, cln, n)
+    canon = O.canon_sites(s, cln)
+    span_root = int(canon[np.nonzero(s == perccln)[0][0]]) if perccln > 0 else 0
+    return canon, perccln, span_root
+
+
+def oracle_mixed(lat, m, n, pbc, sids, ts, bids, tb):
+    b1, b2 = O.bond_list(lat, m, n, pbc)
+    so = O.i32(m * n + 1)
+    so[:len(sids)] = sids
+    o1, o2 = _pairs(b1, b2, bids, tb)
+    s, bl, csize, cln, _, _ = O.label_sitebond(lat, m, n, pbc, b1, b2, so, ts, o1, o2, tb,
+                                               literal=False)
+    perccln = O.lib().or_span_sites(m, n, s, csize, cln, 2 * n - 1)
+    # the site partition: only sites carry the spanning test and the
+    # ConductCalc mixed rule; bonds with both ends empty form clusters of
+    # their own that no site belongs to
+    canon = O.canon_sites(s, cln)
+    span_root = int(canon[np.nonzero(s == perccln)[0][0]]) if perccln > 0 else 0
+    return canon, perccln, span_root
+
+
+def gpu_label(lat, m, n, pbc, kind, sids=None, ts=0, bids=None, tb=0):
+    with api.Context(lat, m, n, pbc) as ctx:
+        ctx.occupy(kind, site_order=sids, nsites=ts, bond_order=bids, nbonds_=tb)
+        return ctx.label(canon=True)
+
+
+def check(li, canon, perccln, span_root):
+    got = li["canon"]
+    if not np.array_equal(got, canon):
+        bad = np.nonzero(got != canon)[0]
+        raise AssertionError("partition differs at %d sites, first site %d: gpu %d oracle %d"
+                             % (len(bad), bad[0] + 1, got[bad[0]], canon[bad[0]]))
+    assert (li["nspan"] > 0) == (perccln > 0), (li["nspan"], perccln)
+    if perccln > 0:
+        assert li["span_root"] == span_root
+
+
+# ------------------------------------------------------------ CPU: the oracle's mixed replay
+@pytest.mark.parametrize("lat,m,n,pbc,ps,pb,seed", [
+    (0, 20, 20, 0, 0.6, 0.5, 1), (0, 24, 18, 1, 0.8, 0.7, 2), (1, 20, 16, 0, 0.7, 0.6, 3),
+    (1, 22, 20, 1, 0.9, 0.4, 4), (0, 30, 30, 0, 0.593, 1.0, 5), (1, 18, 18, 0, 1.0, 0.5, 6)])
+def test_sitebond_replay_equals_literal(lat, m, n, pbc, ps, pb, seed):
+    t = m * n
+    b1, b2, o1, o2 = O.bond_order(lat, m, n, pbc, seed)
+    so = O.site_order(t, seed + 100)
+    ts, tb = int(ps * t), int(pb * len(b1))
+    lit = O.label_sitebond(lat, m, n, pbc, b1, b2, so, ts, o1, o2, tb, literal=True)
+    rep = O.label_sitebond(lat, m, n, pbc, b1, b2, so, ts, o1, o2, tb, literal=False)
+    for a, b in zip(lit[:3], rep[:3]):
+        assert np.array_equal(a, b)
+    assert lit[3:] == rep[3:]
+
+
+def test_canon_helpers_match_python():
+    lat, m, n, pbc = 0, 40, 30, 0
+    b1, b2, o1, o2 = O.bond_order(lat, m, n, pbc, 77)
+    tb = len(b1) // 2
+    label, _, cln, _, _ = O.label_bonds(lat, m, n, pbc, b1, b2, o1, o2, tb, literal=False)
+    want = np.zeros(m * n, np.int64)
+    for lab in np.unique(label[label > 0]):
+        ks = np.nonzero(label == lab)[0]
+        sites = np.concatenate([b1[ks], b2[ks]])
+        want[sites - 1] = sites.min()
+    assert np.array_equal(O.canon_bonds(m * n, b1, b2, label, cln), want)
+    so = O.site_order(m * n, 5)
+    s, _, cln, _, _ = O.label_sites(lat, m, n, pbc, so, 700, literal=False)
+    want = np.zeros(m * n, np.int64)
+    for lab in np.unique(s[s > 0]):
+        idx = np.nonzero(s == lab)[0]
+        want[idx] = idx.min() + 1
+    assert np.array_equal(O.canon_sites(s, cln), want)
+
+
+# ------------------------------------------------------------ GPU: block-edge geometries
+# widths / heights that are not multiples of the 128 x 32 block, pbc wraps,
+# triangular diagonals across block edges, single block rows
+GEOMS = [(0, 200, 70, 0), (0, 384, 65, 1), (0, 129, 31, 1), (1, 130, 33, 0), (1, 256, 96, 1),
+         (1, 64, 40, 1), (0, 1000, 33, 1), (0, 16, 300, 0)]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("geom", GEOMS)
+@pytest.mark.parametrize("p", [0.45, 0.6, 0.9])
+def test_bond_partition_vs_oracle(geom, p):
+    lat, m, n, pbc = geom
+    nb = api.nbonds(lat, m, n, pbc)
+    ids = api.shuffled_ids(nb, 1000 + m + n)
+    if lat == 1:
+        p -= 0.12
+    tb = int(p * nb)
+    li = gpu_label(lat, m, n, pbc, PL.BOND, bids=ids, tb=tb)
+    check(li, *oracle_bond(lat, m, n, pbc, ids, tb))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("geom", GEOMS)
+@pytest.mark.parametrize("p", [0.45, 0.6, 0.9])
+def test_site_partition_vs_oracle(geom, p):
+    lat, m, n, pbc = geom
+    t = m * n
+    ids = api.shuffled_ids(t, 2000 + m + n)
+    ts = int(p * t)
+    li = gpu_label(lat, m, n, pbc, PL.SITE, sids=ids, ts=ts)
+    check(li, *oracle_site(lat, m, n, pbc, ids, ts))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("geom", GEOMS)
+@pytest.mark.parametrize("ps,pb", [(0.6, 0.9), (0.85, 0.85), (1.0, 0.5)])
+def test_mixed_partition_vs_oracle(geom, ps, pb):
+    lat, m, n, pbc = geom
+    t, nb = m * n, api.nbonds(lat, m, n, pbc)
+    sids, bids = api.shuffled_ids(t, 3000 + m), api.shuffled_ids(nb, 4000 + n)
+    ts, tb = int(ps * t), int(pb * nb)
+    li = gpu_label(lat, m, n, pbc, PL.SITEBOND, sids=sids, ts=ts, bids=bids, tb=tb)
+    check(li, *oracle_mixed(lat, m, n, pbc, sids, ts, bids, tb))
+
+
+# ------------------------------------------------------------ GPU: BASELINE config sizes
+@pytest.mark.gpu
+def test_metric_bond_4096_partition_vs_oracle():
+    """the metric workload's partition (square 4096^2, bond p = 0.6, the
+    bench's uniform order of its first realisation)"""
+    lat, m, n, pbc = 0, 4096, 4096, 0
+    nb = api.nbonds(lat, m, n, pbc)
+    seed = int(api.trial_seeds(58302, 1)[0])
+    ids = _perm_ids(nb, seed)
+    tb = int(0.6 * nb)
+    li = gpu_label(lat, m, n, pbc, PL.BOND, bids=ids, tb=tb)
+    check(li, *oracle_bond(lat, m, n, pbc, ids, tb))
+    assert li["nspan"] == 1
+
+
+@pytest.mark.gpu
+def test_config3_tri_site_1024_partition_vs_oracle():
+    """config 3: triangular 1024^2 site p = 0.5, reference shuffle of tseed(1)"""
+    lat, m, n, pbc = 1, 1024, 1024, 0
+    t = m * n
+    ids = api.shuffled_ids(t, int(api.trial_seeds(58302, 1)[0]))
+    ts = t // 2
+    li = gpu_label(lat, m, n, pbc, PL.SITE, sids=ids, ts=ts)
+    check(li, *oracle_site(lat, m, n, pbc, ids, ts))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("ps,pb", [(0.593, 0.50), (0.85, 0.85)])
+def test_config5_mixed_8192_partition_vs_oracle(ps, pb):
+    """config 5: square 8192^2 mixed site-then-bond at ps = 0.593, pb = 0.5
+    (sub-critical under the reference rule) and its
+    near-critical companion; uniform orders"""
+    lat, m, n, pbc = 0, 8192, 8192, 0
+    t, nb = m * n, api.nbonds(lat, m, n, pbc)
+    sids, bids = _perm_ids(t, 8192), _perm_ids(nb, 8193)
+    ts, tb = int(ps * t), int(pb * nb)
+    li = gpu_label(lat, m, n, pbc, PL.SITEBOND, sids=sids, ts=ts, bids=bids, tb=tb)
+    check(li, *oracle_mixed(lat, m, n, pbc, sids, ts, bids, tb))
