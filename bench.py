@@ -188,8 +188,8 @@ def kernel_label(key, minfo):
 
 
 # rocprof kernel names of the CG kernels, per operator format
-ROCPROF_NAMES = {("res", "stencil"): ("k_cg_res",),
-                 ("pm", "stencil"): ("k_cg_rm<0", "k_cg_rm<1", "k_cg_march<0", "k_cg_march<1"),
+ROCPROF_NAMES = {("res", "stencil"): ("k_cg_res",),  # default kernel of each role first
+                 ("pm", "stencil"): ("k_cg_march<0", "k_cg_march<1", "k_cg_rm<0", "k_cg_rm<1"),
                  ("ps", "stencil_tiled"): ("k_cg_ps<4>", "k_cg_ps<6>"),
                  ("resid", "stencil_tiled"): ("k_cg_b<true>",),
                  ("spmv", "stencil_split"): ("k_cg_spmv<4>", "k_cg_spmv<6>"),
@@ -209,21 +209,37 @@ def base_name(k):
 
 def pmc_traffic(key, fmt, L_):
     """HBM bytes per launch of a CG kernel from the committed rocprofv3 PMC
-    summaries of this bench (profiles/*_pmc_{fetch,write}_L<L>.csv, made by
-    tools/prof_csv.py from separate --pmc FETCH_SIZE / WRITE_SIZE passes;
-    FETCH_SIZE doubled per the gfx950 correction).  None if absent."""
+    summaries.  Preferred: profiles/*_pmc_reconcile_L<L>.csv
+    (tools/pmc_r2.sh + tools/pmc_reconcile.py): one fixed dispatch set of
+    work launches in every pass, read bytes from the 32/64/128-B EA read
+    request counters (exact; gfx950's FETCH_SIZE tallies 128-B requests at
+    64 B), write bytes from WRITE_SIZE.  Else the older per-counter
+    summaries (*_pmc_{fetch,write}_L<L>.csv, FETCH_SIZE doubled).  None if
+    absent."""
     import csv
     import glob
+
+    def newest_first(pattern):
+        # r<round>_<n> prefixes compared as numbers (file times are not kept
+        # by every copy of the tree)
+        files = glob.glob(os.path.join(REPO, "profiles", pattern))
+        return sorted(files, key=lambda f: [int(t) if t.isdigit() else t
+                                            for t in re.split(r"(\d+)", os.path.basename(f))],
+                      reverse=True)
+
     names = ROCPROF_NAMES.get((key, fmt), ())
+    # the reconcile rows name kernels without template arguments: the role's
+    # default kernel (first name) only
+    base = base_name(names[0]).split("<")[0] if names else None
+    for f in newest_first("*_pmc_reconcile_L%d.csv" % L_):
+        with open(f) as fh:
+            for r in csv.DictReader(fh):
+                if r["kernel"] == base and r["read_bytes"] and r["write_bytes"]:
+                    return float(r["read_bytes"]) + float(r["write_bytes"]), [os.path.relpath(f, REPO)]
     tot, src = 0.0, []
     for kind, ctr in (("fetch", "FETCH_SIZE"), ("write", "WRITE_SIZE")):
-        # newest round last: r<round>_<n> prefixes compared as numbers
-        # (file times are not kept by every copy of the tree)
-        files = sorted(glob.glob(os.path.join(REPO, "profiles", "*_pmc_%s_L%d.csv" % (kind, L_))),
-                       key=lambda f: [int(t) if t.isdigit() else t
-                                      for t in re.split(r"(\d+)", os.path.basename(f))])
         got = None
-        for f in reversed(files):  # newest first
+        for f in newest_first("*_pmc_%s_L%d.csv" % (kind, L_)):
             with open(f) as fh:
                 for r in csv.DictReader(fh):
                     if base_name(r["kernel"]) in map(base_name, names) and r["counter"] == ctr:
@@ -322,11 +338,16 @@ def main():
         rng = np.random.default_rng([seed, salt] if salt else seed)
         return (rng.permutation(n)[:cnt] + 1).astype(np.int32)
 
+    t_draw = 0.0
     for k, ii in enumerate(ensemble.trial_indices(nreal, world, rank, nseeds=len(seeds))):
+        td = time.perf_counter()
         o = draw(nb, tb, int(seeds[ii])) if args.kind != "site" else np.zeros(1, np.int32)
+        t_draw += time.perf_counter() - td
         orders.append(torch.from_numpy(np.ascontiguousarray(o)).to(dev))
         if args.kind != "bond":
+            td = time.perf_counter()
             so = draw(t_sites, ts, int(seeds[ii]), salt=1)
+            t_draw += time.perf_counter() - td
             site_orders.append(torch.from_numpy(np.ascontiguousarray(so)).to(dev))
         host_orders.append(o if k == args.warmup else None)
         ii_list.append(ii)
@@ -418,7 +439,11 @@ def main():
             ks[key_] += v_
     # ensemble statistics: the only collective (RCCL all-reduce over xGMI)
     stats, tmax = ensemble.allreduce(ensemble.local_stats(results), elapsed, device=dev)
+    # solves/s = realisations completed per second end to
+    # end (labeling + spanning test, and assembly + CG + currents when a
+    # cluster spans); the CG solves among them are reported separately
     nsolves = int(stats[0])
+    nspan = int(stats[3])
     value = nsolves / tmax
 
     fmt_names = {P.FMT_STENCIL: "stencil", P.FMT_STENCIL_TILED: "stencil_tiled",
@@ -519,6 +544,8 @@ def main():
                    "concurrent_per_gpu": K},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS,
                      "unit": "GB/s", "frac": round(achieved / PEAK_HBM_GBS, 4),
+                     "achievable": stream_copy["gbs"],
+                     "frac_of_achievable": round(achieved / stream_copy["gbs"], 4),
                      "traffic": traffic, "traffic_source": traffic_src,
                      "kernel": kern[dom]["kernel"], "format": fmt,
                      "bytes_per_launch": kern[dom]["bytes_per_launch"],
@@ -526,8 +553,15 @@ def main():
                      "launches": kern[dom]["launches"],
                      **({"note": "%d realisations in flight per GPU: kernel durations overlap"
                                  % K} if K > 1 else {})},
-        "cg_iterations_mean": round(float(stats[4]) / max(nsolves, 1), 1),
+        "realisations_per_s": round(value, 5),
+        "cg_solves_per_s": round(nspan / tmax, 5),
+        "cg_solves": nspan,
+        "cg_iterations_mean": round(float(stats[4]) / max(nspan, 1), 1),
         "spanning_fraction": round(float(stats[3]) / max(nsolves, 1), 3),
+        "host_order_ms_per_realisation": round(t_draw * 1e3 / max(nreal, 1), 1),
+        "host_order_note": ("occupation orders are drawn on the host before the timed region "
+                            "and kept in HBM; an ensemble that draws them inline pays this per "
+                            "realisation on one host core unless it overlaps the GPU solve"),
         "gtop_mean": float(stats[1]) / max(nsolves, 1),
         "cg_iteration": {"ms": round(iter_ms, 5), "bytes": iter_bytes,
                          "gbs": round(iter_bytes / (iter_ms * 1e-3) / 1e9, 1) if iter_ms > 0

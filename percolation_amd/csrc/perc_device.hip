@@ -11,6 +11,8 @@
 // index order).
 #include "perc_internal.h"
 
+#include <hip/hip_ext.h>
+
 namespace perc {
 namespace {
 
@@ -2752,17 +2754,17 @@ __global__ __launch_bounds__(kBlock) void k_cg_init(CGArgs a, int itol, int x0_z
   }
 }
 
-// STREAM-style copy of N doubles (16-B accesses, contiguous 256-aligned
-// chunk per workgroup): the achievable-HBM reference for the roofline
+// STREAM-style copy of N doubles: one 16-B load per thread, nontemporal
+// 16-B store, one pass of n / (2 kBlock) workgroups -- the achievable-HBM
+// reference for the roofline.  Measured against a chunked loop (8192
+// workgroups, 16 pairs per thread: 5.24-5.47 TB/s) and 2 / 4 / 8 loads in
+// flight per thread (5.38-5.99): 6.37-6.42 TB/s with the nontemporal
+// store, 6.19-6.27 without (profiles/r2_2_copy_variants.log)
 __global__ __launch_bounds__(kBlock) void k_copy(const double* __restrict__ a,
                                                  double* __restrict__ b, int n) {
   const int n2 = n / 2;
-  const int chunk = (cdiv(n2, gridDim.x) + kBlock - 1) / kBlock * kBlock;
-  const int i0 = blockIdx.x * chunk, i1 = min(i0 + chunk, n2);
-  const double2* __restrict__ a2 = reinterpret_cast<const double2*>(a);
-  double2* __restrict__ b2 = reinterpret_cast<double2*>(b);
-#pragma unroll 4
-  for (int i = i0 + threadIdx.x; i < i1; i += kBlock) b2[i] = a2[i];
+  const int i = blockIdx.x * kBlock + threadIdx.x;
+  if (i < n2) st2(b + 2 * (size_t)i, reinterpret_cast<const double2*>(a)[i], true);
   if (blockIdx.x == 0 && threadIdx.x == 0 && (n & 1)) b[n - 1] = a[n - 1];
 }
 
@@ -2823,6 +2825,19 @@ CGArgs make_cg_args(perc_ctx* h) {
   return a;
 }
 
+// launch a CG kernel; when kernel timing armed h->ev_next, the launch
+// records them at the kernel's own start and end (hipExtLaunchKernel: the
+// dispatch packet's timestamps, no separate event packets around it)
+template <typename K>
+void klaunch(perc_ctx* h, K kern, dim3 g, dim3 b, hipStream_t st, const CGArgs& a) {
+  if (h->ev_next[0]) {
+    hipExtLaunchKernelGGL(kern, g, b, 0, st, h->ev_next[0], h->ev_next[1], 0, a);
+    h->ev_next[0] = h->ev_next[1] = nullptr;
+  } else {
+    kern<<<g, b, 0, st>>>(a);
+  }
+}
+
 // S(k), or the fused P(k)+S(k) of the tiled stencil kernel
 void launch_cg_spmv(perc_ctx* h, const CGArgs& a, int G) {
   if (h->fused) {
@@ -2833,35 +2848,35 @@ void launch_cg_spmv(perc_ctx* h, const CGArgs& a, int G) {
       const dim3 g(h->rm_grid), b(h->rm_w / 4);
       const bool qf = h->qfree;
       if (h->rm_w == 2048) {
-        if (qf) k_cg_rm<kMarchP, 2048><<<g, b, 0, st>>>(a);
-        else k_cg_rm<kMarchPQ, 2048><<<g, b, 0, st>>>(a);
+        if (qf) klaunch(h, k_cg_rm<kMarchP, 2048>, g, b, st, a);
+        else klaunch(h, k_cg_rm<kMarchPQ, 2048>, g, b, st, a);
       } else if (h->rm_w == 1024) {
-        if (qf) k_cg_rm<kMarchP, 1024><<<g, b, 0, st>>>(a);
-        else k_cg_rm<kMarchPQ, 1024><<<g, b, 0, st>>>(a);
+        if (qf) klaunch(h, k_cg_rm<kMarchP, 1024>, g, b, st, a);
+        else klaunch(h, k_cg_rm<kMarchPQ, 1024>, g, b, st, a);
       } else {
-        if (qf) k_cg_rm<kMarchP, 512><<<g, b, 0, st>>>(a);
-        else k_cg_rm<kMarchPQ, 512><<<g, b, 0, st>>>(a);
+        if (qf) klaunch(h, k_cg_rm<kMarchP, 512>, g, b, st, a);
+        else klaunch(h, k_cg_rm<kMarchPQ, 512>, g, b, st, a);
       }
       return;
     }
     if (h->march) {
-      if (h->qfree) k_cg_march<kMarchP><<<h->march_grid, 64 * kMarchWaves, 0, st>>>(a);
-      else if (a.sm) k_cg_march<kMarchPQ, true><<<h->march_grid, 64 * kMarchWaves, 0, st>>>(a);
-      else k_cg_march<kMarchPQ><<<h->march_grid, 64 * kMarchWaves, 0, st>>>(a);
+      if (h->qfree) klaunch(h, k_cg_march<kMarchP>, h->march_grid, 64 * kMarchWaves, st, a);
+      else if (a.sm) klaunch(h, k_cg_march<kMarchPQ, true>, h->march_grid, 64 * kMarchWaves, st, a);
+      else klaunch(h, k_cg_march<kMarchPQ>, h->march_grid, 64 * kMarchWaves, st, a);
       return;
     }
     if (h->g.scn == 4) {
-      if (th == 32) k_cg_ps<4, true, 32><<<G2, B2, 0, st>>>(a);
-      else if (th == 16) k_cg_ps<4, true, 16><<<G2, B2, 0, st>>>(a);
-      else k_cg_ps<4, true, 8><<<G2, B2, 0, st>>>(a);
+      if (th == 32) klaunch(h, k_cg_ps<4, true, 32>, G2, B2, st, a);
+      else if (th == 16) klaunch(h, k_cg_ps<4, true, 16>, G2, B2, st, a);
+      else klaunch(h, k_cg_ps<4, true, 8>, G2, B2, st, a);
     } else {
-      if (th == 32) k_cg_ps<6, true, 32><<<G2, B2, 0, st>>>(a);
-      else if (th == 16) k_cg_ps<6, true, 16><<<G2, B2, 0, st>>>(a);
-      else k_cg_ps<6, true, 8><<<G2, B2, 0, st>>>(a);
+      if (th == 32) klaunch(h, k_cg_ps<6, true, 32>, G2, B2, st, a);
+      else if (th == 16) klaunch(h, k_cg_ps<6, true, 16>, G2, B2, st, a);
+      else klaunch(h, k_cg_ps<6, true, 8>, G2, B2, st, a);
     }
-  } else if (!h->stencil) k_cg_spmv<0><<<G, kBlock, 0, h->stream>>>(a);
-  else if (h->g.scn == 4) k_cg_spmv<4><<<G, kBlock, 0, h->stream>>>(a);
-  else k_cg_spmv<6><<<G, kBlock, 0, h->stream>>>(a);
+  } else if (!h->stencil) klaunch(h, k_cg_spmv<0>, G, kBlock, h->stream, a);
+  else if (h->g.scn == 4) klaunch(h, k_cg_spmv<4>, G, kBlock, h->stream, a);
+  else klaunch(h, k_cg_spmv<6>, G, kBlock, h->stream, a);
 }
 
 // B(k) (streaming; the fused format walks its chunks in reverse)
@@ -2870,15 +2885,15 @@ void launch_cg_b(perc_ctx* h, const CGArgs& a, int G) {
   if (h->fused && h->b_grid > 0) G = h->b_grid;
   if (h->rowmarch && h->qfree) {
     const dim3 g(h->rm_grid), b(h->rm_w / 4);
-    if (h->rm_w == 2048) k_cg_rm<kMarchB, 2048><<<g, b, 0, h->stream>>>(a);
-    else if (h->rm_w == 1024) k_cg_rm<kMarchB, 1024><<<g, b, 0, h->stream>>>(a);
-    else k_cg_rm<kMarchB, 512><<<g, b, 0, h->stream>>>(a);
+    if (h->rm_w == 2048) klaunch(h, k_cg_rm<kMarchB, 2048>, g, b, h->stream, a);
+    else if (h->rm_w == 1024) klaunch(h, k_cg_rm<kMarchB, 1024>, g, b, h->stream, a);
+    else klaunch(h, k_cg_rm<kMarchB, 512>, g, b, h->stream, a);
   } else if (h->march && h->qfree) {
-    k_cg_march<kMarchB><<<h->march_grid, 64 * kMarchWaves, 0, h->stream>>>(a);
+    klaunch(h, k_cg_march<kMarchB>, h->march_grid, 64 * kMarchWaves, h->stream, a);
   } else if (h->stencil) {
-    k_cg_b<true><<<G, kBlock, 0, h->stream>>>(a);
+    klaunch(h, k_cg_b<true>, G, kBlock, h->stream, a);
   } else {
-    k_cg_b<false><<<G, kBlock, 0, h->stream>>>(a);
+    klaunch(h, k_cg_b<false>, G, kBlock, h->stream, a);
   }
 }
 
@@ -3423,32 +3438,35 @@ hipError_t dev_solve(perc_ctx* h, int itol, double tol, int itmax, bool x0_zero,
   long long launched = 0;
   KernelTiming& T = h->timing;
   const int kMaxChunk = 256;
-  if (T.enabled && T.ev.size() < 4 * (size_t)kMaxChunk) {
+  // per timed iteration: start/stop of P, S and B, recorded by the
+  // kernels' own dispatch packets (klaunch)
+  constexpr int kEv = 6;
+  if (T.enabled && T.ev.size() < kEv * (size_t)kMaxChunk) {
     const size_t have = T.ev.size();
-    T.ev.resize(4 * (size_t)kMaxChunk);
+    T.ev.resize(kEv * (size_t)kMaxChunk);
     for (size_t i = have; i < T.ev.size(); ++i) HIP_TRY(hipEventCreate(&T.ev[i]));
   }
   int done_iters = 0;
-  // kernel timing samples every kTimeEvery-th iteration of a chunk: events
-  // between back-to-back launches cost ~10 % of an L = 4096 iteration
+  // kernel timing samples every kTimeEvery-th iteration of a chunk
   constexpr int kTimeEvery = 8;
   while (true) {
     for (int j = 0; j < chunk; ++j) {
       const bool tm = T.enabled && j % kTimeEvery == 0;
+      hipEvent_t* ev = tm ? &T.ev[kEv * j] : nullptr;
       a.kiter = (int)(launched + j + 1);
-      if (tm) hipEventRecord(T.ev[4 * j], st);
       if (!h->fused) {
-        if (ST) k_cg_p<true><<<G, kBlock, 0, st>>>(a);
-        else k_cg_p<false><<<G, kBlock, 0, st>>>(a);
+        if (tm) h->ev_next[0] = ev[0], h->ev_next[1] = ev[1];
+        if (ST) klaunch(h, k_cg_p<true>, G, kBlock, st, a);
+        else klaunch(h, k_cg_p<false>, G, kBlock, st, a);
         HIP_TRY(dbg_sync(st, "k_cg_p"));
       }
-      if (tm) hipEventRecord(T.ev[4 * j + 1], st);
+      if (tm) h->ev_next[0] = ev[2], h->ev_next[1] = ev[3];
       launch_cg_spmv(h, a, G);
       HIP_TRY(dbg_sync(st, "k_cg_spmv"));
-      if (tm) hipEventRecord(T.ev[4 * j + 2], st);
+      if (tm) h->ev_next[0] = ev[4], h->ev_next[1] = ev[5];
       launch_cg_b(h, a, G);
       HIP_TRY(dbg_sync(st, "k_cg_b"));
-      if (tm) hipEventRecord(T.ev[4 * j + 3], st);
+      h->ev_next[0] = h->ev_next[1] = nullptr;
     }
     launched += chunk;
     e = hipGetLastError();
@@ -3462,9 +3480,9 @@ hipError_t dev_solve(perc_ctx* h, int itol, double tol, int itmax, bool x0_zero,
       int nt = 0;
       for (int j = 0; j < real; j += kTimeEvery, ++nt) {
         float tp = 0.f, ts = 0.f, tb = 0.f;
-        hipEventElapsedTime(&tp, T.ev[4 * j], T.ev[4 * j + 1]);
-        hipEventElapsedTime(&ts, T.ev[4 * j + 1], T.ev[4 * j + 2]);
-        hipEventElapsedTime(&tb, T.ev[4 * j + 2], T.ev[4 * j + 3]);
+        if (!h->fused) hipEventElapsedTime(&tp, T.ev[kEv * j], T.ev[kEv * j + 1]);
+        hipEventElapsedTime(&ts, T.ev[kEv * j + 2], T.ev[kEv * j + 3]);
+        hipEventElapsedTime(&tb, T.ev[kEv * j + 4], T.ev[kEv * j + 5]);
         T.p_ms += tp;
         T.spmv_ms += ts;
         T.update_ms += tb;
@@ -3584,7 +3602,7 @@ hipError_t dev_bench(perc_ctx* h, int which, int reps, double* ms) {
       launch_cg_spmv(h, a, G);
       launch_cg_b(h, a, G);
     } else {
-      k_copy<<<8192, kBlock, 0, st>>>(cp_src, cp_dst, (int)cp_n);
+      k_copy<<<cdiv(cp_n / 2, kBlock), kBlock, 0, st>>>(cp_src, cp_dst, (int)cp_n);
     }
   };
   // the B kernel advances iter (tol < 0 keeps it running); values are

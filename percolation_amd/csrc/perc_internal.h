@@ -119,7 +119,7 @@ struct ReplayOrder {
 
 struct KernelTiming {
   bool enabled = false;
-  std::vector<hipEvent_t> ev;  // 4 per iteration slot of a launch chunk
+  std::vector<hipEvent_t> ev;  // 6 per iteration slot of a launch chunk
   double spmv_ms = 0.0, update_ms = 0.0, p_ms = 0.0;
   long long spmv_n = 0, update_n = 0, p_n = 0;
 };
@@ -171,6 +171,7 @@ struct perc_ctx {
   double st_ng0 = 0.0, st_nleak = 0.0;  // its two off-diagonal values
   perc::StencilForms forms{};            // row forms of this lattice
   hipEvent_t ev[8];
+  hipEvent_t ev_next[2] = {nullptr, nullptr};  // klaunch: start/stop of the next CG launch
   perc::KernelTiming timing;
 };
 

@@ -38,12 +38,8 @@ for step in "$@"; do
     bench_quick) run bench_quick 900 python bench.py --steps 1 --warmup 1 --no-cpu-baseline ;;
     prof) run prof 900 rocprofv3 --kernel-trace --stats -f csv -d gpurun_out/prof -o run -- \
             python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline ;;
-    pmc_fetch) run pmc_fetch 900 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "k_cg|k_spmv" \
-            -f csv -d gpurun_out/pmc_fetch -o run -- \
-            python3 bench.py --steps 1 --warmup 0 --itmax 300 --no-cpu-baseline ;;
-    pmc_write) run pmc_write 900 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "k_cg|k_spmv" \
-            -f csv -d gpurun_out/pmc_write -o run -- \
-            python3 bench.py --steps 1 --warmup 0 --itmax 300 --no-cpu-baseline ;;
+    pmc) run pmc 900 bash tools/pmc_r2.sh ;;
+    full_voltages) run bench_fullv 900 python bench.py --full-voltages --steps 1 --warmup 1 --no-cpu-baseline ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
