@@ -283,6 +283,8 @@ def main():
     ap.add_argument("--format", choices=("auto", "stencil", "stencil_tiled", "stencil_split", "csr"),
                     default="auto",
                     help="solver operator format (perc_set_matrix_format)")
+    ap.add_argument("--slabs", type=int, default=1,
+                    help="row slabs of each CG solve on this GPU (perc_set_slabs; SURVEY §8(f) 2)")
     ap.add_argument("--cpu-worker", nargs=6, default=None, help=argparse.SUPPRESS)
     ap.add_argument("--cpu-cores", type=int, default=0,
                     help="processes of the all-cores CPU ensemble baseline (0: the host CPU "
@@ -366,6 +368,8 @@ def main():
         if K > 1:  # no concurrent cooperative (resident) launches
             mode &= ~P._lib.SOLVE_RESIDENT
         c.set_march_mode(mode)
+        if args.slabs > 1:
+            c.set_slabs(args.slabs)
         return c
 
     # K contexts (each its own HIP stream): K realisations in flight per GPU
@@ -541,7 +545,7 @@ def main():
                    "L": L_, "p": p, "rows": N, "nnz_offdiag": nnz,
                    "full_voltages": bool(args.full_voltages), "parallelism":
                    "realisations sharded over %d GPU(s), RCCL stats all-reduce" % world,
-                   "concurrent_per_gpu": K},
+                   "concurrent_per_gpu": K, "slabs": args.slabs},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS,
                      "unit": "GB/s", "frac": round(achieved / PEAK_HBM_GBS, 4),
                      "achievable": stream_copy["gbs"],

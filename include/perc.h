@@ -238,6 +238,18 @@ int perc_set_matrix_format(perc_ctx *h, int fmt);
    linbcg does.  Default off. */
 int perc_set_full_voltages(perc_ctx *h, int enable);
 
+/* Row-slab decomposition of the CG solve (replaces
+   one linbcg loop, Square/bondc.f:780-836): the interior rows split into
+   nslab contiguous slabs with private r, p, q, x and one ghost row of r and
+   p towards each neighbour; per iteration each slab runs the march P+S and
+   the streaming B kernels on its rows, the q.p and z.r / r.r partials are
+   combined in slab order, and the slabs' edge rows of r are copied into
+   the neighbours' ghost rows.  Per-row arithmetic is the single-slab
+   solve's; only the dot-product association differs.  Needs the register-
+   march format (m a multiple of 128, PERC_FMT_STENCIL); a solve with
+   nslab > 1 in another format fails with PERC_EHIP.  Default 1. */
+int perc_set_slabs(perc_ctx *h, int nslab);
+
 /* Band height (lattice rows per wave) of the register-march kernel; 0 (default)
    picks the tallest of 32, 16, .. 2 rows that still gives >= 4096 waves.
    A tuning / test knob: results are the same up to the association of the

@@ -91,6 +91,7 @@ SIGNATURES = {
     "perc_trial_seeds_scaled": (None, [C.c_int, C.c_int, C.c_int, _I]),
     "perc_set_full_voltages": (C.c_int, [_VP, C.c_int]),
     "perc_set_march_rows": (C.c_int, [_VP, C.c_int]),
+    "perc_set_slabs": (C.c_int, [_VP, C.c_int]),
     "perc_set_march_mode": (C.c_int, [_VP, C.c_int]),
     "perc_march_info": (C.c_int, [_VP, _VP]),
     "perc_set_bond_weights": (C.c_int, [_VP, _VP, C.c_longlong]),

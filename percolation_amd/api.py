@@ -204,6 +204,10 @@ class Context:
         """Keep every interior voltage up to date during the solve (perc.h)."""
         L.check(L.lib().perc_set_full_voltages(self.h, int(enable)), "perc_set_full_voltages")
 
+    def set_slabs(self, nslab=1):
+        """Row-slab decomposition of the CG solve (perc_set_slabs)."""
+        L.check(L.lib().perc_set_slabs(self.h, int(nslab)), "perc_set_slabs")
+
     def set_march_rows(self, rows=0):
         """Band height of the register-march kernel (0: auto; perc.h)."""
         L.check(L.lib().perc_set_march_rows(self.h, int(rows)), "perc_set_march_rows")

@@ -1086,6 +1086,13 @@ struct CGArgs {
   int march_alt;  // march kernels: odd bands walk up in P, even bands in B
   int bx;         // the streaming B applies x += ak p(k) (P and k_cg_xfinal do not)
   int sm;         // r, p, q, code strip-major (march solve, PERC_MARCH_STRIPS); x row-major
+  // row slabs (dev_solve_slabs): rows [glo, ghi) may be loaded (glo = -1 /
+  // ghi = nrows + 1 when a ghost row of the neighbouring slab is present);
+  // slab != 0: the march, B and init epilogues store their raw dot partials
+  // in S->part and leave the scalars to k_slab_combine
+  int glo, ghi;
+  int slab;
+  int xhi;        // x kept on rows i >= N - xhi too (< 0: xhi = xrows); xrows < 0: no low rows
   double* q;
   double* partials;  // kRedSlots slots of pstride doubles
   unsigned* tickets; // kRedSlots slots of tstride counters
@@ -1249,14 +1256,15 @@ __global__ __launch_bounds__(kBlock) void k_cg_b(CGArgs a) {
     // iteration k, bondc.f:795), before the march P of the next iteration
     // would have applied it: the march kernels then carry no x at all
     const double* __restrict__ pk = a.pb[k & 1];
-    const int xr = a.xrows == 0 ? N : a.xrows;
+    const int xr = a.xrows == 0 ? N : max(a.xrows, 0);
+    const int xh = a.xhi < 0 ? a.xrows : a.xhi;
     const int i0 = 2 * q0, i1 = min(2 * q1, N);
     // x is row-major; in the strip-major solve p(k) is read through the map
     // (the x rows are logical ranges handed out like the pair chunks)
     auto pat = [&](int i) { return a.sm ? pk[sm_index(a.T, i)] : pk[i]; };
     for (int i = i0 + threadIdx.x; i < min(i1, xr); i += kBlock) a.x[i] = a.x[i] + ak * pat(i);
     if (a.xrows != 0)
-      for (int i = max(i0, max(N - xr, xr)) + threadIdx.x; i < i1; i += kBlock) a.x[i] = a.x[i] + ak * pat(i);
+      for (int i = max(i0, max(N - xh, xr)) + threadIdx.x; i < i1; i += kBlock) a.x[i] = a.x[i] + ak * pat(i);
   }
   // kBU pairs per thread in flight: every load of a batch is issued before
   // the first store (the compiler will not move loads of r above a store
@@ -1310,7 +1318,10 @@ __global__ __launch_bounds__(kBlock) void k_cg_b(CGArgs a) {
   if (publish_and_reduce<2>(acc, a.partials + a.pstride, a.tickets + a.tstride,
                             lbq, gridDim.x, tot, s_red,
                             s_flag)) {
-    if (threadIdx.x == 0) {
+    if (threadIdx.x == 0 && a.slab) {
+      S->part[1] = tot[0];
+      S->part[2] = tot[1];
+    } else if (threadIdx.x == 0) {
       const double err = sqrt(tot[1]) / S->bnrm;
       S->bk = tot[0] / S->bknum;  // next iteration's bknum/bkden (linbcg :799)
       S->bknum = tot[0];
@@ -1655,7 +1666,7 @@ __device__ __forceinline__ void march_load(const CGArgs& a, const MGeom& g, int 
   R.p = R.r = make_double2(0.0, 0.0);
   R.c = R.hc = 0u;
   R.hp = R.hr = 0.0;
-  if (gr >= 0 && gr < a.T.nrows) {
+  if (gr >= a.glo && gr < a.ghi) {
     const int i = midx<SM>(a, gr, g.col);
     R.c = *reinterpret_cast<const unsigned*>(a.St.code + i);
     if (MODE != kMarchB || (gr >= g.r0 && gr < g.rend))
@@ -1692,7 +1703,7 @@ __device__ __forceinline__ void march_step(const CGArgs& a, const MGeom& g, cons
   double2 pn = make_double2(0.0, 0.0);
   double hpn = 0.0;
   double2 d0 = make_double2(1.0, 1.0), d1 = d0;  // {d, 1/d}
-  if (gr >= 0 && gr < nrows) {
+  if (gr >= a.glo && gr < a.ghi) {
     d0 = s_dt[diag_idx(R.c & 0xffffu)];
     d1 = s_dt[diag_idx(R.c >> 16)];
     if (MODE == kMarchB) {
@@ -1711,7 +1722,9 @@ __device__ __forceinline__ void march_step(const CGArgs& a, const MGeom& g, cons
         const double zh = div_tab(R.hr, s_dt[diag_idx(R.hc)]);
         hpn = first ? zh : bk * R.hp + zh;
       }
-      if (gr >= g.r0 && gr < g.rend) {  // own row
+      // own row; in a slab also the ghost rows, so the next iteration's
+      // halo p(k) is at hand (bitwise the neighbour slab's own value)
+      if ((gr >= g.r0 && gr < g.rend) || (a.slab && (gr < 0 || gr >= nrows))) {
         const int i = midx<SM>(a, gr, g.col);
         st2(pnew + i, pn, true);
         if (!SM && !first && !a.bx && (a.xrows == 0 || i < a.xrows || i >= N - a.xrows)) {
@@ -1887,8 +1900,12 @@ __global__ __launch_bounds__(64 * kMarchWaves) void k_cg_march(CGArgs a) {
     double v[1] = {acc[0]}, tot[1];
     if (publish_and_reduce<1>(v, a.partials, a.tickets, lb, gridDim.x, tot, s_red, s_flag)) {
       if (threadIdx.x == 0) {
-        S->akden = tot[0];
-        S->ak = S->bknum / tot[0];
+        if (a.slab) {
+          S->part[0] = tot[0];
+        } else {
+          S->akden = tot[0];
+          S->ak = S->bknum / tot[0];
+        }
       }
     }
   } else {
@@ -2742,7 +2759,10 @@ __global__ __launch_bounds__(kBlock) void k_cg_init(CGArgs a, int itol, int x0_z
   if (publish_and_reduce<2>(acc, a.partials + 2 * a.pstride, a.tickets + 2 * a.tstride, lb,
                             gridDim.x, tot, s_red,
                             s_flag)) {
-    if (threadIdx.x == 0) {
+    if (threadIdx.x == 0 && a.slab) {
+      a.S->part[3] = tot[0];
+      a.S->part[1] = tot[1];
+    } else if (threadIdx.x == 0) {
       a.S->bnrm = sqrt(tot[0]);
       a.S->bknum = tot[1];
       a.S->bkden = 1.0;
@@ -2809,6 +2829,10 @@ CGArgs make_cg_args(perc_ctx* h) {
   a.march_alt = h->march_alt ? 1 : 0;
   a.bx = (h->march || h->rowmarch) && !h->qfree ? 1 : 0;
   a.sm = 0;  // dev_solve / dev_bench switch to the strip-major copies
+  a.glo = 0;
+  a.ghi = h->g.n - 2;
+  a.slab = 0;
+  a.xhi = -1;
   a.xrows = h->full_voltages || h->g.m <= 0 ? 0 : h->g.m;  // see dev_solve
   a.pstride = red_partials_size(red_grid(h));
   a.tstride = red_tickets_size(red_grid(h));
@@ -3405,6 +3429,9 @@ hipError_t dev_solve(perc_ctx* h, int itol, double tol, int itmax, bool x0_zero,
   if (x0_zero) {
     k_zero<<<blocks_for(h->N + 2), kBlock, 0, st>>>(d.x, h->N + 2);
   }
+  // row slabs (perc_set_slabs; the prologue starts from x = 0, as linbcg's
+  // callers do)
+  if (h->nslab > 1 && x0_zero) return dev_solve_slabs(h, h->nslab, itol, tol, itmax, full_x, iter, err);
   CGArgs a = make_cg_args(h);
   // linbcg never reads x inside the iteration (r is recursive), and the
   // terminal currents read it only on the interior rows next to the
@@ -3505,6 +3532,231 @@ hipError_t dev_solve(perc_ctx* h, int itol, double tol, int itmax, bool x0_zero,
   *err = hsp->err;
   hipHostFree(hsp);
   return e;
+}
+
+// ---------------------------------------------------------------------------
+// Row-slab decomposition of one CG solve (the loop of
+// linbcg, Square/bondc.f:780-836).  The interior rows split into K
+// contiguous slabs; slab s owns rows [R_s, R_s+1) and keeps private r, p
+// (ping-pong), q and x with one ghost row of r and p on each side that
+// borders another slab.  Per iteration:
+//   march P+S on every slab (p(k) of the ghost rows formed and stored
+//     locally from the ghost r(k) and p(k-1): bitwise the owner's value)
+//   -> k_slab_combine<0>: q.p = sum of the slab partials in slab order,
+//      ak = bknum / q.p into every slab's scalars
+//   -> streaming B on every slab -> k_slab_combine<1>: z.r, r.r, bk, err,
+//      stop flag (linbcg :799-812), the same on every slab
+//   -> halo: each slab's edge rows of r(k+1) into the neighbours' ghost rows
+//      (2 (K-1) copies of m doubles).
+// Per-row arithmetic is the single-slab solve's; the dot products are
+// associated per slab, then across slabs.  Here the K slabs live on one
+// device (buffers private per slab, halo by device copies) so the exchange
+// pattern is tested on one GPU; across GPUs the halo copies become xGMI
+// peer copies and the combines an all-gather of 3 doubles.
+template <int STAGE>  // 0: q.p; 1: z.r, r.r (B epilogue); 2: the prologue
+__global__ void k_slab_combine(CGScalars* S, int K, double* err_hist, int cap) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  if (STAGE != 2 && S[0].done) return;
+  double t0 = 0.0, t1 = 0.0;
+  for (int s = 0; s < K; ++s) {
+    t0 = t0 + S[s].part[STAGE == 0 ? 0 : (STAGE == 1 ? 1 : 3)];
+    t1 = t1 + S[s].part[STAGE == 1 ? 2 : 1];
+  }
+  CGScalars v = S[0];
+  if (STAGE == 0) {
+    v.akden = t0;
+    v.ak = v.bknum / t0;
+  } else if (STAGE == 1) {
+    const int k = v.iter + 1;
+    const double err = sqrt(t1) / v.bnrm;
+    v.bk = t0 / v.bknum;
+    v.bknum = t0;
+    v.err = err;
+    if (k - 1 < cap) err_hist[k - 1] = err;
+    v.iter = k;
+    if (!(err > v.tol) || k >= v.itmax + 1) v.done = 1;
+  } else {
+    v.bnrm = sqrt(t0);
+    v.bknum = t1;
+    v.bkden = 1.0;
+    v.bk = 0.0;
+    v.ak = 0.0;
+    v.iter = 0;
+    v.done = 0;
+  }
+  for (int s = 0; s < K; ++s) S[s] = v;
+}
+
+namespace {
+struct Slab {
+  int r0 = 0, rows = 0, N = 0, glo = 0, ghi = 0;
+  int march_h = 0, march_grid = 0, b_grid = 0, init_grid = 0, red = 0;
+  double *r = nullptr, *p0 = nullptr, *p1 = nullptr, *q = nullptr, *x = nullptr;  // r/p: base row -1
+  double* partials = nullptr;
+  unsigned* tickets = nullptr;
+};
+}  // namespace
+
+hipError_t dev_solve_slabs(perc_ctx* h, int K, int itol, double tol, int itmax, bool full_x,
+                           int* iter, double* err) {
+  DeviceBuffers& d = h->d;
+  hipStream_t st = h->stream;
+  const int m = h->g.m, nrows = h->g.n - 2;
+  if (!h->march || h->qfree || h->strips || K < 1 || K > nrows) return hipErrorInvalidValue;
+  int cus = 0;
+  HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, h->device));
+  const int spr = m / kMarchW;
+  std::vector<Slab> sl(K);
+  hipError_t e = hipSuccess;
+  CGScalars* S = nullptr;
+  CGScalars* hsp = nullptr;
+  auto cleanup = [&]() {
+    for (Slab& b : sl) {
+      for (double* v : {b.r, b.p0, b.p1, b.q, b.x, b.partials}) if (v) (void)hipFree(v);
+      if (b.tickets) (void)hipFree(b.tickets);
+    }
+    if (S) (void)hipFree(S);
+    if (hsp) (void)hipHostFree(hsp);
+  };
+#define SLAB_TRY(x)               \
+  do {                            \
+    e = (x);                      \
+    if (e != hipSuccess) {        \
+      cleanup();                  \
+      return e;                   \
+    }                             \
+  } while (0)
+  const size_t gpad = 2 * (size_t)m + 8;  // ghost rows + tail pad of the paired loads
+  for (int s = 0, r0 = 0; s < K; ++s) {
+    Slab& b = sl[s];
+    b.rows = nrows / K + (s < nrows % K ? 1 : 0);
+    b.r0 = r0;
+    r0 += b.rows;
+    b.N = b.rows * m;
+    b.glo = s > 0 ? -1 : 0;
+    b.ghi = s < K - 1 ? b.rows + 1 : b.rows;
+    // march band height as march_geometry picks it for this slab's rows
+    b.march_h = h->march_rows_req > 0 ? h->march_rows_req : ((size_t)b.N * 8 > kLargeVector ? 16 : 32);
+    if (h->march_rows_req <= 0)
+      while (b.march_h > 2 && (long long)spr * cdiv(b.rows, b.march_h) < kMarchMinWaves) b.march_h /= 2;
+    b.march_grid = cdiv(spr * cdiv(b.rows, b.march_h), kMarchWaves);
+    b.b_grid = std::max(1, std::min(2 * cus, cg_grid(b.N)));
+    b.init_grid = cg_grid(b.N);
+    b.red = std::max({b.march_grid, b.b_grid, b.init_grid});
+    SLAB_TRY(dmalloc(&b.r, b.N + gpad));
+    SLAB_TRY(dmalloc(&b.p0, b.N + gpad));
+    SLAB_TRY(dmalloc(&b.p1, b.N + gpad));
+    SLAB_TRY(dmalloc(&b.q, (size_t)b.N + 8));
+    SLAB_TRY(dmalloc(&b.x, (size_t)b.N + 8));
+    SLAB_TRY(dmalloc(&b.partials, kRedSlots * red_partials_size(b.red)));
+    SLAB_TRY(dmalloc(&b.tickets, kRedSlots * red_tickets_size(b.red)));
+    SLAB_TRY(hipMemsetAsync(b.tickets, 0, kRedSlots * red_tickets_size(b.red) * sizeof(unsigned), st));
+    SLAB_TRY(hipMemsetAsync(b.x, 0, ((size_t)b.N + 8) * sizeof(double), st));
+    for (double* v : {b.r, b.p0, b.p1}) SLAB_TRY(hipMemsetAsync(v, 0, (b.N + gpad) * sizeof(double), st));
+  }
+  SLAB_TRY(dmalloc(&S, K));
+  SLAB_TRY(hipHostMalloc(reinterpret_cast<void**>(&hsp), sizeof(CGScalars)));
+  {
+    CGScalars s0{};
+    s0.tol = tol;
+    s0.itmax = itmax;
+    std::vector<CGScalars> hs(K, s0);
+    SLAB_TRY(hipMemcpyAsync(S, hs.data(), sizeof(CGScalars) * K, hipMemcpyHostToDevice, st));
+  }
+  const CGArgs base = make_cg_args(h);
+  auto args = [&](int s) {
+    const Slab& b = sl[s];
+    CGArgs a = base;
+    a.A.N = b.N;
+    a.St.N = b.N;
+    a.St.code = d.code + (size_t)b.r0 * m;  // the global code array: ghost rows are its neighbours
+    a.T.nrows = b.rows;
+    a.T.bh = b.march_h;
+    a.rhs = d.rhs + (size_t)b.r0 * m;
+    a.r = b.r + m;
+    a.pb[0] = b.p0 + m;
+    a.pb[1] = b.p1 + m;
+    a.p = a.pb[0];
+    a.q = b.q;
+    a.x = b.x;
+    a.fused = 1;
+    a.b_reverse = 1;
+    a.bx = 1;
+    a.glo = b.glo;
+    a.ghi = b.ghi;
+    a.slab = 1;
+    // x on the rows next to the electrodes only: global row 0 (slab 0) and
+    // global row nrows - 1 (slab K-1), unless every voltage is wanted
+    a.xrows = full_x ? 0 : (s == 0 ? m : -1);
+    a.xhi = full_x ? -1 : (s == K - 1 ? m : 0);
+    a.pstride = red_partials_size(b.red);
+    a.tstride = red_tickets_size(b.red);
+    a.partials = b.partials;
+    a.tickets = b.tickets;
+    a.S = S + s;
+    return a;
+  };
+  std::vector<CGArgs> A(K);
+  for (int s = 0; s < K; ++s) A[s] = args(s);
+  // halo: r rows of each slab edge into the neighbours' ghost rows
+  auto halo = [&]() -> hipError_t {
+    const size_t row = sizeof(double) * m;
+    for (int s = 0; s + 1 < K; ++s) {
+      HIP_TRY(hipMemcpyAsync(sl[s + 1].r, sl[s].r + (size_t)sl[s].rows * m, row,
+                             hipMemcpyDeviceToDevice, st));  // below ghost of s+1
+      HIP_TRY(hipMemcpyAsync(sl[s].r + (size_t)(sl[s].rows + 1) * m, sl[s + 1].r + m, row,
+                             hipMemcpyDeviceToDevice, st));  // above ghost of s
+    }
+    return hipSuccess;
+  };
+  // prologue (x0 = 0: r = b), bnrm and the first bknum over all slabs
+  for (int s = 0; s < K; ++s)
+    k_cg_init<true><<<sl[s].init_grid, kBlock, 0, st>>>(A[s], itol, 1);
+  SLAB_TRY(dbg_sync(st, "k_cg_init (slabs)"));
+  k_slab_combine<2><<<1, 64, 0, st>>>(S, K, d.err_hist, d.err_hist_cap);
+  SLAB_TRY(halo());
+  int chunk = 8;
+  long long launched = 0;
+  const int kMaxChunk = 256;
+  while (true) {
+    for (int j = 0; j < chunk; ++j) {
+      for (int s = 0; s < K; ++s) {
+        A[s].kiter = (int)(launched + j + 1);
+        k_cg_march<kMarchPQ><<<sl[s].march_grid, 64 * kMarchWaves, 0, st>>>(A[s]);
+      }
+      SLAB_TRY(dbg_sync(st, "k_cg_march (slabs)"));
+      k_slab_combine<0><<<1, 64, 0, st>>>(S, K, d.err_hist, d.err_hist_cap);
+      for (int s = 0; s < K; ++s) k_cg_b<true><<<sl[s].b_grid, kBlock, 0, st>>>(A[s]);
+      SLAB_TRY(dbg_sync(st, "k_cg_b (slabs)"));
+      k_slab_combine<1><<<1, 64, 0, st>>>(S, K, d.err_hist, d.err_hist_cap);
+      SLAB_TRY(halo());
+    }
+    launched += chunk;
+    SLAB_TRY(hipGetLastError());
+    SLAB_TRY(hipMemcpyAsync(hsp, S, sizeof(CGScalars), hipMemcpyDeviceToHost, st));
+    SLAB_TRY(hipStreamSynchronize(st));
+    if (hsp->done || launched > (long long)itmax + 2) break;
+    chunk = std::min(chunk * 2, kMaxChunk);
+  }
+  // voltages back into the context's x (the currents read rows 0 and N-1)
+  const size_t row = sizeof(double) * m;
+  if (full_x) {
+    for (int s = 0; s < K; ++s)
+      SLAB_TRY(hipMemcpyAsync(d.x + (size_t)sl[s].r0 * m, sl[s].x, row * sl[s].rows,
+                              hipMemcpyDeviceToDevice, st));
+  } else {
+    SLAB_TRY(hipMemcpyAsync(d.x, sl[0].x, row, hipMemcpyDeviceToDevice, st));
+    SLAB_TRY(hipMemcpyAsync(d.x + (size_t)(nrows - 1) * m, sl[K - 1].x + (size_t)(sl[K - 1].rows - 1) * m,
+                            row, hipMemcpyDeviceToDevice, st));
+  }
+  // the context's scalars as a single-slab solve leaves them
+  SLAB_TRY(hipMemcpyAsync(d.scal, S, sizeof(CGScalars), hipMemcpyDeviceToDevice, st));
+  SLAB_TRY(hipStreamSynchronize(st));
+  *iter = hsp->iter;
+  *err = hsp->err;
+  cleanup();
+#undef SLAB_TRY
+  return hipSuccess;
 }
 
 hipError_t dev_currents(perc_ctx* h, int rule, int cur_rule, double g0, double leak, double Va,

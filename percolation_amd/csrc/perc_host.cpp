@@ -717,6 +717,12 @@ int perc_set_full_voltages(perc_ctx* h, int enable) {
   return PERC_OK;
 }
 
+int perc_set_slabs(perc_ctx* h, int nslab) {
+  if (!h || nslab < 1 || (h->g.n > 2 && nslab > h->g.n - 2)) return PERC_EINVAL;
+  h->nslab = nslab;
+  return PERC_OK;
+}
+
 int perc_set_march_rows(perc_ctx* h, int rows) {
   if (!h || rows < 0 || rows > 1024) return PERC_EINVAL;
   h->march_rows_req = rows;

@@ -59,6 +59,7 @@ struct CGScalars {
   int itmax;
   int done;      // set once err <= tol or iter > itmax
   int pad[3];
+  double part[4];  // row slabs: this slab's raw partials (q.p, z.r, r.r, ||D^-1 b||^2)
 };
 
 struct DeviceBuffers {
@@ -168,6 +169,7 @@ struct perc_ctx {
   int rm_w = 0, rm_h = 16;      // their strip width (columns) and band height
   int rm_grid = 0;              // their workgroups
   bool full_voltages = false;   // perc_set_full_voltages: keep x on every row
+  int nslab = 1;                // perc_set_slabs: row slabs of the CG solve
   double st_ng0 = 0.0, st_nleak = 0.0;  // its two off-diagonal values
   perc::StencilForms forms{};            // row forms of this lattice
   hipEvent_t ev[8];
@@ -190,6 +192,8 @@ hipError_t dev_assemble(perc_ctx* h, int rule, double g0, double leak, double Va
 void select_format(perc_ctx* h);  // stencil / fused flags from fmt_req + assembly checks
 void march_geometry(perc_ctx* h); // band height + grid of the register-march kernel
 void res_geometry(perc_ctx* h);   // grid + band height of the resident solve
+hipError_t dev_solve_slabs(perc_ctx* h, int K, int itol, double tol, int itmax, bool full_x,
+                           int* iter, double* err);
 hipError_t dev_solve(perc_ctx* h, int itol, double tol, int itmax, bool x0_zero, bool full_x,
                      int* iter, double* err);
 hipError_t dev_currents(perc_ctx* h, int rule, int cur_rule, double g0, double leak, double Va,

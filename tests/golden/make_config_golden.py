@@ -50,7 +50,7 @@ CASES = {
     # the metric: 4096^2 square bond at 0.6 (bench.py's first realisation)
     "metric_sq4096_bond_p60": dict(lattice=0, L=4096, kind="bond", p=0.60, order="pcg64"),
 }
-TOLS = (1e-8, 1e-13)
+TOLS = (1e-8, 1e-13, 1e-14)
 HIST_EVERY = 256
 
 
