@@ -1543,9 +1543,38 @@ __global__ __launch_bounds__(tile_threads(TILEH)) void k_cg_ps(CGArgs a) {
 // arithmetic is k_cg_ps's (z = r/d, p = bk p + z, x += ak p, q in slot
 // order), so every value is bitwise the other kernels'; only the q.p
 // association differs (rows summed per lane).
+// Buffer access with a hardware range check: a byte offset at or past the
+// buffer's size makes a load return 0 and drops a store.  The row-march
+// keeps every memory instruction of a step unconditional this way (rows
+// outside the lattice or the band, halo columns of non-halo threads, q of
+// the steps without a finished row, x off the electrode rows), so hipcc's
+// s_waitcnt bookkeeping stays exact across the loop: with loads and stores
+// under branches it waited for vmcnt(0) -- every prefetched row and every
+// store in flight -- once per step.
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+constexpr unsigned kOOB = 0x80000000u;  // buffers are kept below 2 GB (march_geometry)
+constexpr int kNT = 2;                  // aux bits: nontemporal
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* p, unsigned bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, (int)bytes, 0x00020000);
+}
+__device__ __forceinline__ double2 bld2(__amdgpu_buffer_rsrc_t r, unsigned off) {
+  return __builtin_bit_cast(double2, __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 0));
+}
+__device__ __forceinline__ double bld1(__amdgpu_buffer_rsrc_t r, unsigned off) {
+  return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, (int)off, 0, 0));
+}
+// sc1 (agent-coherent) load: data another workgroup stored with sc1
+__device__ __forceinline__ double bld1s(__amdgpu_buffer_rsrc_t r, unsigned off) {
+  return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, (int)off, 0, 16));
+}
+template <int AUX>
+__device__ __forceinline__ void bst2(__amdgpu_buffer_rsrc_t r, unsigned off, double2 v) {
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, (int)off, 0, AUX);
+}
+
 constexpr int kMarchW = 128;     // columns per wave strip
 constexpr int kMarchWaves = 4;   // waves (strips) per workgroup
-constexpr int kMarchMinWaves = 4096;
 
 struct MRow {       // one prefetched row of the lane's pair (+ halo column)
   double2 p, r;     // p(k-1), r
@@ -1632,8 +1661,14 @@ __device__ __forceinline__ double march_q_map(unsigned c, double d, double xi, u
   return acc;
 }
 
-// rows prefetched ahead: 3 (+22 VGPRs) is no faster, nor are taller bands
-// with fewer waves and 4-6 rows ahead (H = 64: 0.138 vs 0.111 ms at L = 4096)
+// Rows prefetched ahead (template D).  The P+S kernel of the solve runs
+// D = 3 (march_geometry: 173 VGPRs, 2 waves per SIMD, one round of 64-row
+// bands at L = 4096): 0.104-0.107 vs 0.114-0.117 ms with D = 2 (136 VGPRs,
+// 3 waves per SIMD, 43-row bands) on the same box, D = 4 no better
+// (profiles/r2_4_march_depth.log).  Before the memory instructions were
+// made unconditional (MBuf) every step waited for vmcnt(0) and deeper
+// prefetch could not help.  The opt-in variants (q-free P and B, strip-
+// major) keep D = 2.
 constexpr int kMarchDepth = 2;
 
 // Register march, three kernels of one loop (MODE):
@@ -1660,9 +1695,66 @@ __device__ __forceinline__ int midx(const CGArgs& a, int gr, int col) {
   return SM ? sm_at(a.T, gr, col) : gr * a.T.m + col;
 }
 
+// Buffer views of the rows one march wave touches, [lo, hi) = its band plus
+// the halo rows, clipped to the loadable rows [glo, ghi): every load and
+// store of a step is issued unconditionally with a byte offset that is out
+// of range (kOOB, or a row outside the view) where the row-major kernel had
+// a branch -- a row outside the lattice, a halo column of a non-halo lane,
+// p(k-1) of the first iteration, q / p of a row the wave does not own.
+// With memory instructions under branches hipcc's waitcnt pass put
+// s_waitcnt vmcnt(0) at the top of every step (every prefetched row and
+// every store drained once per step: ~3.5 read requests in flight per wave,
+// TCC_EA0_RDREQ_LEVEL, profiles/r2_3_*); unconditional, the waits count
+// exactly and the prefetch ring keeps its rows in flight.
+struct MBuf {
+  __amdgpu_buffer_rsrc_t p, r, c, pn, q, x;  // p(k-1), r, codes, p(k): rows [lo, hi); q, x: own rows
+  int lo, hi;
+};
+
+template <int MODE>
+__device__ __forceinline__ MBuf march_bufs(const CGArgs& a, const MGeom& g, const double* psrc,
+                                           double* pnew) {
+  const int m = a.T.m;
+  MBuf B;
+  B.lo = max(g.r0 - 1, a.glo);
+  B.hi = max(min(g.rend + 1, a.ghi), B.lo);
+  const long long base = (long long)B.lo * m;
+  const unsigned n = (unsigned)(B.hi - B.lo) * (unsigned)m;
+  const unsigned nown = (unsigned)max(g.rend - g.r0, 0) * (unsigned)m;
+  B.p = rsrc(psrc + base, n * 8u);
+  B.r = rsrc(a.r + base, n * 8u);
+  B.c = rsrc(a.St.code + base, n * 2u);
+  B.pn = rsrc(pnew + base, n * 8u);
+  B.q = rsrc(MODE == kMarchPQ ? a.q + (long long)g.r0 * m : a.r, MODE == kMarchPQ ? nown * 8u : 0u);
+  B.x = rsrc(MODE == kMarchP ? a.x + (long long)g.r0 * m : a.r, MODE == kMarchP ? nown * 8u : 0u);
+  return B;
+}
+
 template <int MODE, bool SM>
-__device__ __forceinline__ void march_load(const CGArgs& a, const MGeom& g, int gr, bool first,
-                                           const double* __restrict__ psrc, MRow& R) {
+__device__ __forceinline__ void march_load(const CGArgs& a, const MGeom& g, const MBuf& B, int gr,
+                                           bool first, const double* __restrict__ psrc, MRow& R) {
+  if constexpr (!SM) {
+    const int m = a.T.m;
+    const bool rowok = (unsigned)(gr - B.lo) < (unsigned)(B.hi - B.lo);
+    const unsigned e = (unsigned)((gr - B.lo) * m + g.col);
+    const unsigned eh = (unsigned)((gr - B.lo) * m + g.hcol);
+    const unsigned o8 = rowok ? e * 8u : kOOB;
+    const bool rown = MODE != kMarchB || (gr >= g.r0 && gr < g.rend);
+    const bool hk = rowok && g.hok;
+    const unsigned h8 = hk ? eh * 8u : kOOB;
+    R.c = __builtin_amdgcn_raw_buffer_load_b32(B.c, (int)(rowok ? e * 2u : kOOB), 0, 0);
+    R.r = bld2(B.r, rown ? o8 : kOOB);
+    R.p = bld2(B.p, first ? kOOB : o8);
+    if (MODE != kMarchB) {
+      R.hc = __builtin_amdgcn_raw_buffer_load_b16(B.c, (int)(hk ? eh * 2u : kOOB), 0, 0);
+      R.hr = bld1(B.r, h8);
+    } else {
+      R.hc = 0u;
+      R.hr = 0.0;
+    }
+    R.hp = bld1(B.p, first ? kOOB : h8);
+    return;
+  }
   R.p = R.r = make_double2(0.0, 0.0);
   R.c = R.hc = 0u;
   R.hp = R.hr = 0.0;
@@ -1692,7 +1784,8 @@ struct MState {
 // one step: row gr enters the window, then the middle row (gr -+ 1) is
 // finished when it is one of the band's own rows
 template <int MODE, bool UP, bool SM>
-__device__ __forceinline__ void march_step(const CGArgs& a, const MGeom& g, const MRow& R, int gr,
+__device__ __forceinline__ void march_step(const CGArgs& a, const MGeom& g, const MBuf& B,
+                                           const MRow& R, int gr,
                                            bool first, double bk, double ak,
                                            double* __restrict__ pnew, const double2* s_dt,
                                            const unsigned* s_rpos, const unsigned* s_rmap,
@@ -1724,15 +1817,27 @@ __device__ __forceinline__ void march_step(const CGArgs& a, const MGeom& g, cons
       }
       // own row; in a slab also the ghost rows, so the next iteration's
       // halo p(k) is at hand (bitwise the neighbour slab's own value)
-      if ((gr >= g.r0 && gr < g.rend) || (a.slab && (gr < 0 || gr >= nrows))) {
+      if (SM && ((gr >= g.r0 && gr < g.rend) || (a.slab && (gr < 0 || gr >= nrows)))) {
         const int i = midx<SM>(a, gr, g.col);
         st2(pnew + i, pn, true);
-        if (!SM && !first && !a.bx && (a.xrows == 0 || i < a.xrows || i >= N - a.xrows)) {
-          double2 xv = *reinterpret_cast<const double2*>(a.x + i);
-          xv.x = xv.x + ak * R.p.x;
-          xv.y = xv.y + ak * R.p.y;
-          *reinterpret_cast<double2*>(a.x + i) = xv;
-        }
+      }
+    }
+  }
+  if constexpr (!SM) {
+    if (MODE != kMarchB) {
+      const int m = a.T.m;
+      const bool own = gr >= g.r0 && gr < g.rend;
+      const bool pst = (unsigned)(gr - B.lo) < (unsigned)(B.hi - B.lo) &&
+                       (own || (a.slab && (gr < 0 || gr >= nrows)));
+      bst2<kNT>(B.pn, pst ? (unsigned)((gr - B.lo) * m + g.col) * 8u : kOOB, pn);
+      if (MODE == kMarchP) {  // x += ak p(k-1) on the x rows (the P-only march keeps x)
+        const int i = gr * m + g.col;
+        const bool xw = own && !first && !a.bx && (a.xrows == 0 || i < a.xrows || i >= N - a.xrows);
+        const unsigned ox = xw ? (unsigned)((gr - g.r0) * m + g.col) * 8u : kOOB;
+        double2 xv = bld2(B.x, ox);
+        xv.x = xv.x + ak * R.p.x;
+        xv.y = xv.y + ak * R.p.y;
+        bst2<0>(B.x, ox, xv);
       }
     }
   }
@@ -1759,7 +1864,9 @@ __device__ __forceinline__ void march_step(const CGArgs& a, const MGeom& g, cons
     W.rN = R.r;
   }
   const int mid = UP ? gr + 1 : gr - 1;
-  if (mid >= g.r0 && mid < g.rend) {  // wave-uniform
+  const bool mown = mid >= g.r0 && mid < g.rend;  // wave-uniform
+  double2 mq = make_double2(0.0, 0.0), mr = mq;   // q / r(k+1) of the middle row
+  if (mown) {
     const unsigned c0w = W.cM & 0xffffu, c1w = W.cM >> 16;
     const unsigned f0 = c0w >> 11, f1 = c1w >> 11;
     const double2 dM0 = s_dt[diag_idx(c0w)], dM1 = s_dt[diag_idx(c1w)];
@@ -1797,22 +1904,32 @@ __device__ __forceinline__ void march_step(const CGArgs& a, const MGeom& g, cons
       double2 rn;
       rn.x = W.rM.x - ak * q0;
       rn.y = W.rM.y - ak * q1;
-      st2(a.r + i, rn, true);
+      if (SM) st2(a.r + i, rn, true);
+      mr = rn;
       const double z0 = div_tab(rn.x, dM0), z1 = div_tab(rn.y, dM1);
       acc[0] = acc[0] + z0 * rn.x;
       acc[0] = acc[0] + z1 * rn.y;
       acc[1] = acc[1] + rn.x * rn.x;
       acc[1] = acc[1] + rn.y * rn.y;
     } else {
-      if (MODE == kMarchPQ) st2(a.q + i, make_double2(q0, q1), true);
+      if (SM && MODE == kMarchPQ) st2(a.q + i, make_double2(q0, q1), true);
+      mq = make_double2(q0, q1);
       acc[0] = acc[0] + q0 * W.C.e0;
       acc[0] = acc[0] + q1 * W.C.e1;
     }
   }
+  if constexpr (!SM) {
+    const int m = a.T.m;
+    if (MODE == kMarchPQ)
+      bst2<kNT>(B.q, mown ? (unsigned)((mid - g.r0) * m + g.col) * 8u : kOOB, mq);
+    if (MODE == kMarchB)
+      bst2<kNT>(B.r, mown ? (unsigned)((mid - B.lo) * m + g.col) * 8u : kOOB, mr);
+  }
 }
 
 template <int MODE, int D, bool UP, bool SM>
-__device__ __forceinline__ void march_walk(const CGArgs& a, const MGeom& g, MRow (&ring)[D],
+__device__ __forceinline__ void march_walk(const CGArgs& a, const MGeom& g, const MBuf& B,
+                                           MRow (&ring)[D],
                                            bool first, double bk, double ak,
                                            const double* __restrict__ psrc,
                                            double* __restrict__ pnew, const double2* s_dt,
@@ -1829,12 +1946,21 @@ __device__ __forceinline__ void march_walk(const CGArgs& a, const MGeom& g, MRow
 #pragma unroll
     for (int u = 0; u < D; ++u) {
       const int j = j0 + u;
-      if (j < nsteps) {
+      if constexpr (!SM) {
+        // no branches around memory instructions: a step past the walk
+        // (odd step count) and the prefetch past its end address rows
+        // outside the view (loads return 0, stores are dropped) and finish
+        // no row
+        const MRow R = ring[u];
+        march_load<MODE, SM>(a, g, B, UP ? g.rend - (j + D) : g.r0 - 1 + j + D, first, psrc, ring[u]);
+        march_step<MODE, UP, SM>(a, g, B, R, UP ? g.rend - j : g.r0 - 1 + j, first, bk, ak, pnew, s_dt,
+                                 s_rpos, s_rmap, s_w, W, acc);
+      } else if (j < nsteps) {
         const MRow R = ring[u];
         if (j + D < nsteps)
-          march_load<MODE, SM>(a, g, UP ? g.rend - (j + D) : g.r0 - 1 + j + D, first, psrc, ring[u]);
-        march_step<MODE, UP, SM>(a, g, R, UP ? g.rend - j : g.r0 - 1 + j, first, bk, ak, pnew, s_dt,
-                             s_rpos, s_rmap, s_w, W, acc);
+          march_load<MODE, SM>(a, g, B, UP ? g.rend - (j + D) : g.r0 - 1 + j + D, first, psrc, ring[u]);
+        march_step<MODE, UP, SM>(a, g, B, R, UP ? g.rend - j : g.r0 - 1 + j, first, bk, ak, pnew, s_dt,
+                                 s_rpos, s_rmap, s_w, W, acc);
       }
     }
   }
@@ -1859,7 +1985,9 @@ __global__ __launch_bounds__(64 * kMarchWaves) void k_cg_march(CGArgs a) {
   const int m = a.T.m, nrows = a.T.nrows, H = a.T.bh;
   const int lb = xcd_logical_block(blockIdx.x, gridDim.x);
   const int lane = threadIdx.x & 63;
-  const int w = lb * kMarchWaves + (threadIdx.x >> 6);
+  // wave-uniform in SGPRs (the buffer views below must be: a resource
+  // the compiler cannot prove uniform gets a readfirstlane loop per access)
+  const int w = __builtin_amdgcn_readfirstlane(lb * kMarchWaves + (threadIdx.x >> 6));
   const int spr = m / kMarchW;
   const int band = w / spr, strip = w - band * spr;
   MGeom g;
@@ -1876,11 +2004,12 @@ __global__ __launch_bounds__(64 * kMarchWaves) void k_cg_march(CGArgs a) {
   }
   const bool up = (a.march_alt && (band & 1)) != (MODE == kMarchB);
   const int nsteps = g.rend - g.r0 + 2;
+  const MBuf B = march_bufs<MODE>(a, g, psrc, pnew);
   MRow ring[D];
   if (active) {
 #pragma unroll
     for (int u = 0; u < D; ++u)
-      if (u < nsteps) march_load<MODE, SM>(a, g, up ? g.rend - u : g.r0 - 1 + u, first, psrc, ring[u]);
+      if (u < nsteps) march_load<MODE, SM>(a, g, B, up ? g.rend - u : g.r0 - 1 + u, first, psrc, ring[u]);
   }
   if (S->done) return;
   if (threadIdx.x < kMaxForms) {
@@ -1893,8 +2022,8 @@ __global__ __launch_bounds__(64 * kMarchWaves) void k_cg_march(CGArgs a) {
   double acc[2] = {0.0, 0.0};
   if (active) {
     double* s_w = s_win[threadIdx.x >> 6];
-    if (up) march_walk<MODE, D, true, SM>(a, g, ring, first, bk, ak, psrc, pnew, s_dt, s_rpos, s_rmap, s_w, acc);
-    else march_walk<MODE, D, false, SM>(a, g, ring, first, bk, ak, psrc, pnew, s_dt, s_rpos, s_rmap, s_w, acc);
+    if (up) march_walk<MODE, D, true, SM>(a, g, B, ring, first, bk, ak, psrc, pnew, s_dt, s_rpos, s_rmap, s_w, acc);
+    else march_walk<MODE, D, false, SM>(a, g, B, ring, first, bk, ak, psrc, pnew, s_dt, s_rpos, s_rmap, s_w, acc);
   }
   if (MODE != kMarchB) {
     double v[1] = {acc[0]}, tot[1];
@@ -1994,36 +2123,6 @@ __device__ __forceinline__ double rm_q_uni(unsigned c, double d, double xi, unsi
     }
   }
   return acc;
-}
-
-// Buffer access with a hardware range check: a byte offset at or past the
-// buffer's size makes a load return 0 and drops a store.  The row-march
-// keeps every memory instruction of a step unconditional this way (rows
-// outside the lattice or the band, halo columns of non-halo threads, q of
-// the steps without a finished row, x off the electrode rows), so hipcc's
-// s_waitcnt bookkeeping stays exact across the loop: with loads and stores
-// under branches it waited for vmcnt(0) -- every prefetched row and every
-// store in flight -- once per step.
-typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
-constexpr unsigned kOOB = 0x80000000u;  // buffers are kept below 2 GB (march_geometry)
-constexpr int kNT = 2;                  // aux bits: nontemporal
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* p, unsigned bytes) {
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, (int)bytes, 0x00020000);
-}
-__device__ __forceinline__ double2 bld2(__amdgpu_buffer_rsrc_t r, unsigned off) {
-  return __builtin_bit_cast(double2, __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 0));
-}
-__device__ __forceinline__ double bld1(__amdgpu_buffer_rsrc_t r, unsigned off) {
-  return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, (int)off, 0, 0));
-}
-// sc1 (agent-coherent) load: data another workgroup stored with sc1
-__device__ __forceinline__ double bld1s(__amdgpu_buffer_rsrc_t r, unsigned off) {
-  return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, (int)off, 0, 16));
-}
-template <int AUX>
-__device__ __forceinline__ void bst2(__amdgpu_buffer_rsrc_t r, unsigned off, double2 v) {
-  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, (int)off, 0, AUX);
 }
 
 template <int MODE, int W, int D, bool XB>
@@ -2886,7 +2985,8 @@ void launch_cg_spmv(perc_ctx* h, const CGArgs& a, int G) {
     if (h->march) {
       if (h->qfree) klaunch(h, k_cg_march<kMarchP>, h->march_grid, 64 * kMarchWaves, st, a);
       else if (a.sm) klaunch(h, k_cg_march<kMarchPQ, true>, h->march_grid, 64 * kMarchWaves, st, a);
-      else klaunch(h, k_cg_march<kMarchPQ>, h->march_grid, 64 * kMarchWaves, st, a);
+      else if (h->march_depth == 2) klaunch(h, k_cg_march<kMarchPQ, false, 2>, h->march_grid, 64 * kMarchWaves, st, a);
+      else klaunch(h, k_cg_march<kMarchPQ, false, 3>, h->march_grid, 64 * kMarchWaves, st, a);
       return;
     }
     if (h->g.scn == 4) {
@@ -3058,7 +3158,6 @@ hipError_t dev_build_lattice(perc_ctx* h) {
   HIP_TRY(hipGetLastError());
   HIP_TRY(dmalloc(&d.diag, N + 2));
   HIP_TRY(dmalloc(&d.rhs, N + 2));
-  HIP_TRY(dmalloc(&d.code, (size_t)N + 8));
   HIP_TRY(dmalloc(&d.dtab, kDiagTab));  // double2 entries
   h->forms = stencil_forms(g);
   HIP_TRY(dmalloc(&d.sflag, 4));
@@ -3070,13 +3169,19 @@ hipError_t dev_build_lattice(perc_ctx* h) {
   HIP_TRY(dmalloc(&d.member, t + 8));
   HIP_TRY(dmalloc(&d.top, t + 8));
   HIP_TRY(dmalloc(&d.counters, 8 + kMaxSpanList));
-  // CG (vectors padded to even length for the 16 B paths)
-  const size_t nv = (size_t)N + 2;
-  HIP_TRY(dmalloc(&d.x, nv));
-  HIP_TRY(dmalloc(&d.r, nv));
-  HIP_TRY(dmalloc(&d.p0, nv));
-  HIP_TRY(dmalloc(&d.p1, nv));
-  HIP_TRY(dmalloc(&d.q, nv));
+  // CG vectors (padded to even length for the 16 B paths) and the row codes.
+  // One hipMalloc per array: a single arena with the arrays at staggered
+  // offsets (0 / 256 B .. 64 KB per array) measured no better (march P+S
+  // 0.104-0.117 ms either way, profiles/r2_4_march_depth.log)
+  {
+    const size_t nv = (size_t)N + 2;
+    HIP_TRY(dmalloc(&d.r, nv));
+    HIP_TRY(dmalloc(&d.p0, nv));
+    HIP_TRY(dmalloc(&d.p1, nv));
+    HIP_TRY(dmalloc(&d.q, nv));
+    HIP_TRY(dmalloc(&d.x, nv));
+    HIP_TRY(dmalloc(&d.code, (size_t)N + 8));
+  }
   h->grid = cg_grid(N);
   int cus = 0;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, h->device) != hipSuccess)
@@ -3230,23 +3335,40 @@ hipError_t dev_canon(perc_ctx* h, int* canon_out) {
   return hipFree(tmp);
 }
 
-// band height and grid of the register-march kernel: the requested height,
-// or the tallest (32 .. 2 rows) that still gives kMarchMinWaves waves
+// band height of the register-march kernel over `nrows` rows: the
+// requested height (perc_set_march_rows, or PERC_MARCH_ROWS for probes);
+// vectors past the Infinity Cache: 16-row bands, i.e. several rounds of
+// resident waves, each over a narrower window of the arrays (L = 8192:
+// 0.423 vs 0.451 ms with 32 rows); else one round of resident waves, the
+// height that gives every wave slot of the chip one strip-band (the PQ
+// kernel with 3 rows prefetched holds 173 VGPRs: 2 waves per SIMD, L = 4096:
+// 64-row bands)
+int march_rows_for(const perc_ctx* h, int nrows) {
+  const Geom& g = h->g;
+  const char* env_rows = getenv("PERC_MARCH_ROWS");
+  if (h->march_rows_req > 0) return h->march_rows_req;
+  if (env_rows && atoi(env_rows) > 0) return atoi(env_rows);
+  if ((size_t)g.m * nrows * sizeof(double) > kLargeVector) return 16;
+  int cus = 0, per_cu = 0;
+  hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, h->device);
+  if (h->march_depth == 2)
+    hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_cg_march<kMarchPQ, false, 2>, 64 * kMarchWaves, 0);
+  else
+    hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_cg_march<kMarchPQ, false, 3>, 64 * kMarchWaves, 0);
+  const long long slots = (long long)std::max(cus, 1) * std::max(per_cu, 1) * kMarchWaves;
+  const long long bands = std::max(1ll, slots / (g.m / kMarchW));
+  return std::max(2, cdiv(nrows, bands));
+}
+
+// band height and grid of the register-march kernel
 void march_geometry(perc_ctx* h) {
   const Geom& g = h->g;
   h->march_grid = 0;
+  // rows prefetched ahead by the P+S march (PERC_MARCH_DEPTH: 2 for probes)
+  h->march_depth = getenv("PERC_MARCH_DEPTH") && atoi(getenv("PERC_MARCH_DEPTH")) == 2 ? 2 : 3;
   if (g.m % kMarchW != 0 || g.n <= 2) return;
   const int spr = g.m / kMarchW, nrows = g.n - 2;
-  if (h->march_rows_req > 0) {
-    h->march_h = h->march_rows_req;
-  } else {
-    // vectors past the Infinity Cache: 16-row bands, i.e. several rounds
-    // of resident waves, each over a narrower window of the arrays (L =
-    // 8192: 0.423 vs 0.451 ms with 32 rows; at L = 4096 32 rows stay best)
-    h->march_h = (size_t)g.m * nrows * sizeof(double) > kLargeVector ? 16 : 32;
-    while (h->march_h > 2 && (long long)spr * cdiv(nrows, h->march_h) < kMarchMinWaves)
-      h->march_h /= 2;
-  }
+  h->march_h = march_rows_for(h, nrows);
   h->march_grid = cdiv(spr * cdiv(nrows, h->march_h), kMarchWaves);
   // workgroup row-march: the widest strip of 2048 / 1024 / 512 columns that
   // divides m, the tallest band (32 .. 2 rows) that gives >= kRmMinGroups
@@ -3635,10 +3757,7 @@ hipError_t dev_solve_slabs(perc_ctx* h, int K, int itol, double tol, int itmax, 
     b.N = b.rows * m;
     b.glo = s > 0 ? -1 : 0;
     b.ghi = s < K - 1 ? b.rows + 1 : b.rows;
-    // march band height as march_geometry picks it for this slab's rows
-    b.march_h = h->march_rows_req > 0 ? h->march_rows_req : ((size_t)b.N * 8 > kLargeVector ? 16 : 32);
-    if (h->march_rows_req <= 0)
-      while (b.march_h > 2 && (long long)spr * cdiv(b.rows, b.march_h) < kMarchMinWaves) b.march_h /= 2;
+    b.march_h = march_rows_for(h, b.rows);  // as march_geometry picks it for these rows
     b.march_grid = cdiv(spr * cdiv(b.rows, b.march_h), kMarchWaves);
     b.b_grid = std::max(1, std::min(2 * cus, cg_grid(b.N)));
     b.init_grid = cg_grid(b.N);
@@ -3722,7 +3841,8 @@ hipError_t dev_solve_slabs(perc_ctx* h, int K, int itol, double tol, int itmax, 
     for (int j = 0; j < chunk; ++j) {
       for (int s = 0; s < K; ++s) {
         A[s].kiter = (int)(launched + j + 1);
-        k_cg_march<kMarchPQ><<<sl[s].march_grid, 64 * kMarchWaves, 0, st>>>(A[s]);
+        if (h->march_depth == 2) k_cg_march<kMarchPQ, false, 2><<<sl[s].march_grid, 64 * kMarchWaves, 0, st>>>(A[s]);
+        else k_cg_march<kMarchPQ, false, 3><<<sl[s].march_grid, 64 * kMarchWaves, 0, st>>>(A[s]);
       }
       SLAB_TRY(dbg_sync(st, "k_cg_march (slabs)"));
       k_slab_combine<0><<<1, 64, 0, st>>>(S, K, d.err_hist, d.err_hist_cap);

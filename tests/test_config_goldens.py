@@ -28,18 +28,23 @@ pytestmark = pytest.mark.gpu
 HERE = os.path.dirname(os.path.abspath(__file__))
 FIXTURES = sorted(glob.glob(os.path.join(HERE, "golden", "configs", "*.json")))
 
-# Bars.  The fixture's tightest tolerance is the converged reference: tol
-# <= 1e-14 -> Gtop and Gbot within 1e-10 relative.  At a looser tolerance
-# the solve itself is accurate only to |G(tol) - G(converged)| (c2 at 1e-8:
+# Bars.  The fixture's tightest tolerance (1e-14) is the converged
+# reference.  There Gtop and Gbot must agree within 1e-10 relative, or
+# within the oracle's own remaining truncation error if that is larger --
+# estimated as a fifth of its change over the last tolerance decade
+# (1e-13 -> 1e-14; the recursive residual falls linearly, so the iterate
+# error falls about tenfold per decade): c2's Gbot still moves 4.8e-9
+# between 1e-13 and 1e-14, its Gtop 5.1e-10.  At a looser tolerance the
+# solve itself is accurate only to |G(tol) - G(converged)| (c2 at 1e-8:
 # 2.1e-7 relative), and over 10^4 iterations the association of the dot
 # products -- the only re-associated operations -- moves the iterates
 # within that error: G within twice the reference's own truncation error
-# there, the iteration count within +-1 at 1e-8 (+-3 at 1e-13, where the
-# recursive residual is near the fp64 floor).  Measured at 1e-8: c2 Gtop
-# 1.2e-7 / Gbot 1.6e-10, c3 1.0e-7 / 1.3e-9; at 1e-13: c2 5.8e-10 /
-# 1.5e-10, c3 8.2e-11 / 1.0e-10.
+# there, the iteration count within +-1 at 1e-8 (+-3 below 1e-10, where the
+# recursive residual is near the fp64 floor).  Measured (r2): at 1e-8 c2
+# Gtop 1.2e-7 / Gbot 1.6e-10, c3 1.0e-7 / 1.3e-9; at 1e-14 c2 7.3e-11 /
+# 1.5e-10, c3 7.9e-11 / 1.0e-10 (4 slabs: 4.9e-11 / 1.5e-10, 8.9e-11 /
+# 1.0e-10).
 CONVERGED = 1e-10
-ONLY_1E13 = 1e-9  # a fixture whose tightest solve is 1e-13 (no 1e-14 yet)
 
 def rel(a, b):
     return abs(a - b) / max(abs(b), 1e-300)
@@ -92,13 +97,16 @@ def test_config_fixture(path):
                      gtop_rel=rel(c["gtop"], ref["gtop"]), gbot_rel=rel(c["gbot"], ref["gbot"]))
             report.append((tight, d))
             print(json.dumps(d))
-    tight = min(doc["solves"], key=float)
+    tols = sorted(doc["solves"], key=float)
+    tight = tols[0]
     conv = doc["solves"][tight]
+    prev = doc["solves"][tols[1]] if len(tols) > 1 else None
     for tkey, d in report:
         ref = doc["solves"][tkey]
         if tkey == tight:
-            bar = CONVERGED if float(tkey) <= 1e-14 else ONLY_1E13
-            assert d["gtop_rel"] < bar and d["gbot_rel"] < bar, d
+            for g in ("gtop", "gbot"):
+                rest = rel(conv[g], prev[g]) / 5 if prev is not None else 0.0
+                assert d[g + "_rel"] < max(CONVERGED, rest), (g, rest, d)
             continue
         assert abs(d["iter"] - d["iter_ref"]) <= (1 if float(tkey) >= 1e-10 else 3), d
         for g in ("gtop", "gbot"):
