@@ -475,6 +475,11 @@ def main():
             return [("res", "spmv", 5, G * 4 * L_ * 8 * 2 + x_bytes(N, L_, full))]
         if f in ("stencil", "stencil_tiled"):
             qf = f == "stencil" and minfo["qfree"]
+            if f == "stencil" and not qf and minfo.get("kernel") in ("wave", "rows"):
+                # the march kernels carry no x: the streaming B applies
+                # x += ak p(k) (reads x and p(k), writes x: 24 B per x row)
+                xb = 24 * N if full else 24 * 2 * L_
+                return [("pm", "spmv", 1, 34 * N), ("resid", "resid", 2, resid_bytes(N, f) + xb)]
             return [("pm" if f == "stencil" else "ps", "spmv", 1, ps_bytes(N, L_, full, qf)),
                     ("resid", "resid", 2, resid_bytes(N, f))]
         return [("spmv", "spmv", 1, spmv_bytes(N, nnz, f)), ("resid", "resid", 2, resid_bytes(N, f)),

@@ -120,6 +120,16 @@ int perc_label(perc_ctx *h, perc_label_info *info, int *canon_out);
 int perc_label_numbers(perc_ctx *h, int *bond_label, int *site_label,
                        int *csize, int cap, int *stats);
 
+/* Cluster sizes of the labeled occupancy on the GPU (bond or site kind):
+   *maxcs = the largest cluster's size and *span_size = the size of the
+   spanning cluster perc_label chose (0 if none), in bonds for PERC_BOND
+   (c(label) of Square/bond_perc.f:296-322) and sites for PERC_SITE
+   (site_perc.f).  These are the maxcs / perccls columns of bond_perc.txt /
+   site_perc.txt: the same numbers as perc_label_numbers' stats[2] and
+   csize[perccln] (clusters only grow, so the running maximum is the final
+   largest size), without the host replay. */
+int perc_cluster_sizes(perc_ctx *h, int *maxcs, int *span_size);
+
 /* Percolation threshold of one order (Square/bond_perc.f:204-366,
    Square/site_perc.f:150-256, Square/bond_cond.f:381 pc): *first = the
    smallest count c such that occupying order[0..c) (bond ids for PERC_BOND,

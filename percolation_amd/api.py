@@ -204,6 +204,13 @@ class Context:
         """Keep every interior voltage up to date during the solve (perc.h)."""
         L.check(L.lib().perc_set_full_voltages(self.h, int(enable)), "perc_set_full_voltages")
 
+    def cluster_sizes(self):
+        """(maxcs, span_size) of the labeled bond / site occupancy on the
+        GPU (perc_cluster_sizes)."""
+        mx, sp = C.c_int(), C.c_int()
+        L.check(L.lib().perc_cluster_sizes(self.h, C.byref(mx), C.byref(sp)), "perc_cluster_sizes")
+        return mx.value, sp.value
+
     def set_slabs(self, nslab=1):
         """Row-slab decomposition of the CG solve (perc_set_slabs)."""
         L.check(L.lib().perc_set_slabs(self.h, int(nslab)), "perc_set_slabs")
@@ -409,13 +416,14 @@ def first_spanning(ctx, order, kind=L.BOND, n=None):
 
 
 def threshold_scan(lattice=0, m=50, n=50, pbc=0, kind=L.BOND, master=58302, numtrials=10,
-                   ctx=None, device=0):
+                   ctx=None, device=0, replay=False):
     """bond_perc / site_perc (Fortran/Square/bond_perc.f, site_perc.f): per
     trial ii, seed tseed(ii) = int(rand(0)*1e6)+1, the reference shuffle,
     then the first occupation count that spans; the record is (tseed,
     fraction = REAL*4 count/N, largest cluster size, spanning cluster size)
-    at that step (the whole order if nothing spans), sizes by the host
-    label replay."""
+    at that step (the whole order if nothing spans), sizes on the GPU
+    (perc_cluster_sizes; replay=True: by the host label replay, which also
+    gives the reference label number perccln)."""
     own = ctx is None
     ctx = ctx or Context(lattice, m, n, pbc, device)
     try:
@@ -426,11 +434,16 @@ def threshold_scan(lattice=0, m=50, n=50, pbc=0, kind=L.BOND, master=58302, numt
             order = shuffled_ids(N, int(seeds[ii]))
             first = first_spanning(ctx, order, kind, N)
             c = first if first else N
-            r = ctx.label_numbers(kind)
-            perccls = int(r["csize"][r["perccln"]]) if first and r["perccln"] else 0
+            if replay:  # reference label numbers too (host replay)
+                r = ctx.label_numbers(kind)
+                maxcs, perccln = r["maxcs"], r["perccln"]
+                perccls = int(r["csize"][perccln]) if first and perccln else 0
+            else:  # the two sizes the record needs, on the GPU
+                maxcs, span = ctx.cluster_sizes()
+                perccls, perccln = (span if first else 0), None
             out.append(dict(tseed=int(seeds[ii]), count=c,
                             f=float(np.float32(np.float32(c) / np.float32(N))),
-                            maxcs=r["maxcs"], perccls=perccls, perccln=r["perccln"]))
+                            maxcs=maxcs, perccls=perccls, perccln=perccln))
         return out
     finally:
         if own:

@@ -497,6 +497,43 @@ __global__ __launch_bounds__(kCcThreads) void k_count_root(int t, const int* par
   block_count_add(cnt, counter);
 }
 
+// cluster sizes c(label) of the reference (bond_perc.f:296-322: bonds of
+// the cluster; site_perc.f: sites): each site adds its occupied forward
+// bonds (bond) or itself (site) to its root's count, one atomic per site
+// that contributes
+__global__ __launch_bounds__(kCcThreads) void k_cluster_sizes(Geom g, int kind,
+                                                              const int* bond_first,
+                                                              const uint8_t* bocc,
+                                                              const uint8_t* member,
+                                                              const int* parent, int* size) {
+  for (int s = blockIdx.x * kCcThreads + threadIdx.x + 1; s <= g.t; s += gridDim.x * kCcThreads) {
+    int c = 0;
+    if (kind == PERC_BOND) {
+      for (int j = bond_first[s]; j < bond_first[s + 1]; ++j) c += bocc[j];
+    } else {
+      c = member[s];
+    }
+    if (c) atomicAdd(&size[parent[s]], c);
+  }
+}
+
+// largest entry of size[1..t] (wave max, workgroup max, one atomicMax per
+// workgroup)
+__global__ __launch_bounds__(kCcThreads) void k_max_size(int t, const int* size, int* out) {
+  __shared__ int s_m[kCcThreads / 64];
+  int v = 0;
+  for (int s = blockIdx.x * kCcThreads + threadIdx.x + 1; s <= t; s += gridDim.x * kCcThreads)
+    v = max(v, size[s]);
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v = max(v, __shfl_xor(v, off, 64));
+  if ((threadIdx.x & 63) == 0) s_m[threadIdx.x >> 6] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int w = 1; w < kCcThreads / 64; ++w) v = max(v, s_m[w]);
+    if (v) atomicMax(out, v);
+  }
+}
+
 __global__ void k_canon(int t, const int* parent, const uint8_t* member, int* canon) {
   const int s = blockIdx.x * blockDim.x + threadIdx.x + 1;
   if (s > t) return;
@@ -1228,7 +1265,10 @@ __global__ __launch_bounds__(kBlock) void k_cg_spmv(CGArgs a) {
   }
 }
 
-template <bool ST>
+// XF: x kept on every row (perc_set_full_voltages / vint): the update
+// x += ak p(k) rides in the batched pair loop (16-B accesses, loads issued
+// with the batch) instead of a separate scalar pass
+template <bool ST, bool XF = false>
 __global__ __launch_bounds__(kBlock) void k_cg_b(CGArgs a) {
   CGScalars* S = a.S;
   if (S->done) return;
@@ -1251,11 +1291,12 @@ __global__ __launch_bounds__(kBlock) void k_cg_b(CGArgs a) {
   double acc[2] = {0.0, 0.0};  // z.r, r.r
   const int qf = min(q1, N / 2);
   constexpr bool nt = ST;
-  if (a.bx) {
+  const double* __restrict__ pkx = a.pb[k & 1];
+  if (a.bx && !XF) {
     // x += ak(k) p(k) on the rows x is kept on (linbcg's update of
     // iteration k, bondc.f:795), before the march P of the next iteration
     // would have applied it: the march kernels then carry no x at all
-    const double* __restrict__ pk = a.pb[k & 1];
+    const double* __restrict__ pk = pkx;
     const int xr = a.xrows == 0 ? N : max(a.xrows, 0);
     const int xh = a.xhi < 0 ? a.xrows : a.xhi;
     const int i0 = 2 * q0, i1 = min(2 * q1, N);
@@ -1271,7 +1312,7 @@ __global__ __launch_bounds__(kBlock) void k_cg_b(CGArgs a) {
   // to r, so a plain loop waits out one memory round trip per pair)
   constexpr int kBU = 4;
   for (int j0 = q0 + threadIdx.x; j0 < qf; j0 += kBlock * kBU) {
-    double2 qv[kBU], rv[kBU], dv[kBU];
+    double2 qv[kBU], rv[kBU], dv[kBU], xv[kBU], pv[kBU];
     unsigned cc[kBU];
 #pragma unroll
     for (int u = 0; u < kBU; ++u) {
@@ -1279,6 +1320,10 @@ __global__ __launch_bounds__(kBlock) void k_cg_b(CGArgs a) {
       if (j < qf) {
         qv[u] = *reinterpret_cast<const double2*>(q + 2 * j);
         rv[u] = *reinterpret_cast<const double2*>(r + 2 * j);
+        if (XF) {
+          xv[u] = *reinterpret_cast<const double2*>(a.x + 2 * j);
+          pv[u] = *reinterpret_cast<const double2*>(pkx + 2 * j);
+        }
         if (ST) cc[u] = *reinterpret_cast<const unsigned*>(a.St.code + 2 * j);
         else dv[u] = *reinterpret_cast<const double2*>(a.A.diag + 2 * j);
       }
@@ -1291,6 +1336,11 @@ __global__ __launch_bounds__(kBlock) void k_cg_b(CGArgs a) {
         rn.x = rv[u].x - ak * qv[u].x;
         rn.y = rv[u].y - ak * qv[u].y;
         st2(r + 2 * j, rn, nt);
+        if (XF) {
+          xv[u].x = xv[u].x + ak * pv[u].x;
+          xv[u].y = xv[u].y + ak * pv[u].y;
+          st2(a.x + 2 * j, xv[u], nt);
+        }
         double z0, z1;
         if (ST) {
           z0 = div_tab(rn.x, s_dt[diag_idx(cc[u] & 0xffffu)]);
@@ -1308,6 +1358,7 @@ __global__ __launch_bounds__(kBlock) void k_cg_b(CGArgs a) {
   }
   if ((N & 1) && q1 > N / 2 && threadIdx.x == 0) {
     const int i = N - 1;
+    if (XF) a.x[i] = a.x[i] + ak * pkx[i];
     const double rn = r[i] - ak * q[i];
     r[i] = rn;
     const double z0 = rn / diag1<ST>(a, i);
@@ -3015,7 +3066,9 @@ void launch_cg_b(perc_ctx* h, const CGArgs& a, int G) {
   } else if (h->march && h->qfree) {
     klaunch(h, k_cg_march<kMarchB>, h->march_grid, 64 * kMarchWaves, h->stream, a);
   } else if (h->stencil) {
-    klaunch(h, k_cg_b<true>, G, kBlock, h->stream, a);
+    // x on every row with the march's x-in-B (fused, row-major): XF
+    if (a.bx && a.xrows == 0 && !a.sm) klaunch(h, k_cg_b<true, true>, G, kBlock, h->stream, a);
+    else klaunch(h, k_cg_b<true>, G, kBlock, h->stream, a);
   } else {
     klaunch(h, k_cg_b<false>, G, kBlock, h->stream, a);
   }
@@ -3252,7 +3305,7 @@ void dev_free_all(perc_ctx* h) {
   void* ptrs[] = {d.bond_first, d.rowptr, d.col, d.val, d.diag, d.rhs, d.code, d.dtab, d.sflag, d.bocc, d.socc,
                   d.order, d.parent, d.member, d.top, d.counters, d.x, d.r,
                   d.p0, d.p1, d.q, d.partials, d.tickets, d.scal, d.err_hist, d.iout,
-                  d.res_xch, d.res_part, d.res_bar, d.bw, d.code_sm};
+                  d.res_xch, d.res_part, d.res_bar, d.bw, d.code_sm, d.csize};
   for (void* p : ptrs)
     if (p) hipFree(p);
   d = DeviceBuffers{};
@@ -3321,6 +3374,27 @@ hipError_t dev_span_sites(perc_ctx* h, int root, int* count) {
       h->g.t, h->d.parent, h->d.member, root, h->d.counters + 2);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipMemcpyAsync(count, h->d.counters + 2, sizeof(int), hipMemcpyDeviceToHost, st));
+  return hipStreamSynchronize(st);
+}
+
+hipError_t dev_cluster_sizes(perc_ctx* h, int kind, int root, int* maxcs, int* rootsize) {
+  DeviceBuffers& d = h->d;
+  hipStream_t st = h->stream;
+  const Geom& g = h->g;
+  if (!d.csize) HIP_TRY(dmalloc(&d.csize, (size_t)g.t + 2));
+  HIP_TRY(hipMemsetAsync(d.csize, 0, sizeof(int) * ((size_t)g.t + 2), st));
+  HIP_TRY(hipMemsetAsync(d.counters + 3, 0, sizeof(int), st));
+  const int G = std::min(cdiv(g.t, kCcThreads), kReduceGrid * 4);
+  k_cluster_sizes<<<G, kCcThreads, 0, st>>>(g, kind, d.bond_first, d.bocc, d.member, d.parent,
+                                            d.csize);
+  HIP_TRY(dbg_sync(st, "k_cluster_sizes"));
+  k_max_size<<<std::min(cdiv(g.t, kCcThreads), kReduceGrid), kCcThreads, 0, st>>>(g.t, d.csize,
+                                                                                  d.counters + 3);
+  HIP_TRY(dbg_sync(st, "k_max_size"));
+  HIP_TRY(hipMemcpyAsync(maxcs, d.counters + 3, sizeof(int), hipMemcpyDeviceToHost, st));
+  *rootsize = 0;
+  if (root > 0 && root <= g.t)
+    HIP_TRY(hipMemcpyAsync(rootsize, d.csize + root, sizeof(int), hipMemcpyDeviceToHost, st));
   return hipStreamSynchronize(st);
 }
 
@@ -3846,7 +3920,10 @@ hipError_t dev_solve_slabs(perc_ctx* h, int K, int itol, double tol, int itmax, 
       }
       SLAB_TRY(dbg_sync(st, "k_cg_march (slabs)"));
       k_slab_combine<0><<<1, 64, 0, st>>>(S, K, d.err_hist, d.err_hist_cap);
-      for (int s = 0; s < K; ++s) k_cg_b<true><<<sl[s].b_grid, kBlock, 0, st>>>(A[s]);
+      for (int s = 0; s < K; ++s) {
+        if (full_x) k_cg_b<true, true><<<sl[s].b_grid, kBlock, 0, st>>>(A[s]);
+        else k_cg_b<true><<<sl[s].b_grid, kBlock, 0, st>>>(A[s]);
+      }
       SLAB_TRY(dbg_sync(st, "k_cg_b (slabs)"));
       k_slab_combine<1><<<1, 64, 0, st>>>(S, K, d.err_hist, d.err_hist_cap);
       SLAB_TRY(halo());

@@ -393,6 +393,18 @@ int perc_label(perc_ctx* h, perc_label_info* info, int* canon_out) {
   return PERC_OK;
 }
 
+int perc_cluster_sizes(perc_ctx* h, int* maxcs, int* span_size) {
+  if (!h || !maxcs || !span_size) return PERC_EINVAL;
+  if (!h->labeled) return PERC_ESTATE;
+  if (h->last.kind != PERC_BOND && h->last.kind != PERC_SITE) {
+    set_error("perc_cluster_sizes: bond or site occupancy only");
+    return PERC_EINVAL;
+  }
+  hipSetDevice(h->device);
+  return hip_status(dev_cluster_sizes(h, h->last.kind, h->span_root, maxcs, span_size),
+                    "perc_cluster_sizes");
+}
+
 static int label_numbers_impl(const Geom& g, const std::vector<int>& bond_first, int kind,
                               const int* sites, int nsites, const int* bonds, int nbond,
                               int* bond_label, int* site_label, int* csize, int cap,

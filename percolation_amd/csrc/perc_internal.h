@@ -87,7 +87,8 @@ struct DeviceBuffers {
   int* parent = nullptr;     // t+1
   uint8_t* member = nullptr; // t+1 (site belongs to some cluster)
   uint8_t* top = nullptr;    // t+1 (spanning-root flags, m+1 used)
-  int* counters = nullptr;   // [0]=nspan [1]=nclusters [2]=span_sites, then list
+  int* counters = nullptr;   // [0]=nspan [1]=nclusters [2]=span_sites [3]=max size, then list
+  int* csize = nullptr;      // t+2 per-root cluster sizes (perc_cluster_sizes)
   // CG
   double* x = nullptr;
   double* r = nullptr;
@@ -189,6 +190,7 @@ hipError_t dev_occupy(perc_ctx* h, int kind, int nsites, const int* site_order, 
 hipError_t dev_label(perc_ctx* h, int* nspan, int* span_list, int* nclusters);
 hipError_t dev_span_sites(perc_ctx* h, int root, int* count);
 hipError_t dev_canon(perc_ctx* h, int* canon_out);
+hipError_t dev_cluster_sizes(perc_ctx* h, int kind, int root, int* maxcs, int* rootsize);
 hipError_t dev_assemble(perc_ctx* h, int rule, double g0, double leak, double Va, int span_root);
 void select_format(perc_ctx* h);  // stencil / fused flags from fmt_req + assembly checks
 void march_geometry(perc_ctx* h); // band height + grid of the register-march kernel

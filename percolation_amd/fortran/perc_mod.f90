@@ -141,6 +141,13 @@ module perc_api
       integer(c_int) :: stats(4)
     end function perc_label_numbers
 
+    integer(c_int) function perc_cluster_sizes(h, maxcs, span_size) &
+        bind(C, name='perc_cluster_sizes')
+      import :: c_int, c_ptr
+      type(c_ptr), value :: h
+      integer(c_int) :: maxcs, span_size
+    end function perc_cluster_sizes
+
     integer(c_int) function perc_conductance(h, rule, cur_rule, Va, g0, leak, itol, tol, &
         itmax, res, vint_out) bind(C, name='perc_conductance')
       import :: c_int, c_ptr, c_double, perc_cond_result

@@ -9,7 +9,8 @@
 ! The reference re-labels after every element and scans for spanning; here
 ! the first spanning count comes from perc_first_spanning (GPU labeling in a
 ! bisection, spanning being monotone in the count) and the cluster sizes at
-! that count from the reference-order label replay.
+! that count from perc_cluster_sizes (GPU; equal to the reference's c(label)
+! of the largest and of the spanning cluster, tests/test_threshold_scan.py).
 !
 ! Parameters: the reference's block (50x50, numtrials 10 for bond_perc /
 ! 1000 for site_perc, master seed 58302), overridable by bond_perc.nml /
@@ -25,8 +26,8 @@ program perc_scan
 #endif
   integer(c_int) :: lattice, m, n, pbc, numtrials, seed, device
   namelist /perc_scan_nml/ lattice, m, n, pbc, numtrials, seed, device
-  integer(c_int) :: kind, nn, ii, first, cnt, stats(4), perccls
-  integer(c_int), allocatable, target :: tseed(:), order(:), csize(:)
+  integer(c_int) :: kind, nn, ii, first, cnt, perccls, maxcs, spansz
+  integer(c_int), allocatable, target :: tseed(:), order(:)
   character(len=16) :: nml, out
   real :: f
   type(c_ptr) :: h
@@ -61,7 +62,7 @@ program perc_scan
   else
     nn = m * n
   end if
-  allocate(tseed(numtrials), order(nn + 1), csize(nn + 2))
+  allocate(tseed(numtrials), order(nn + 1))
   call perc_trial_seeds_scaled(seed, numtrials, 1000000, tseed)
   call perc_check(perc_ctx_create(device, lattice, m, n, pbc, h), 'perc_ctx_create')
   open(unit=10, file=trim(out))
@@ -71,14 +72,14 @@ program perc_scan
                     'perc_first_spanning')
     cnt = first
     if (first == 0) cnt = nn
-    ! cluster sizes at that step (the context is left occupied at cnt)
-    call perc_check(perc_label_numbers(h, c_null_ptr, c_null_ptr, c_loc(csize), nn + 2, stats), &
-                    'perc_label_numbers')
+    ! cluster sizes at that step (the context is left occupied at cnt and
+    ! labeled): largest cluster and spanning cluster, on the GPU
+    call perc_check(perc_cluster_sizes(h, maxcs, spansz), 'perc_cluster_sizes')
     perccls = 0
-    if (first > 0 .and. stats(4) > 0) perccls = csize(stats(4) + 1)
+    if (first > 0) perccls = spansz
     f = real(cnt) / real(nn)
-    write(6, *) tseed(ii), f, stats(3), perccls
-    write(10, 111) tseed(ii), f, stats(3), perccls
+    write(6, *) tseed(ii), f, maxcs, perccls
+    write(10, 111) tseed(ii), f, maxcs, perccls
   end do
   close(10)
   call perc_check(perc_ctx_destroy(h), 'perc_ctx_destroy')

@@ -162,3 +162,34 @@ def test_bs_scan_gpu_intended_equals_replay():
             tb = int(0.6 * nb)
             assert api.first_spanning_mixed(ctx, PL.SITE, so, t, bo, tb) == \
                 api.bs_perc_replay(lat, m, n, pbc, so, t, bo, tb, False)
+
+
+# ---------------------------------------------------------------- GPU cluster sizes
+@pytest.mark.gpu
+@pytest.mark.parametrize("lat,m,n,pbc", [(0, 64, 64, 0), (0, 100, 70, 1), (1, 64, 80, 0),
+                                         (1, 90, 64, 1), (0, 512, 512, 0)])
+@pytest.mark.parametrize("kind", [PL.BOND, PL.SITE])
+def test_cluster_sizes_equal_replay(lat, m, n, pbc, kind):
+    """perc_cluster_sizes (GPU) = the reference's maxcs (running maximum of
+    c(label), bond_perc.f:313-322) and c(perccln) of the lowest-label
+    spanning cluster, by the host replay, at counts below, at and above the
+    threshold."""
+    N = api.nbonds(lat, m, n, pbc) if kind == PL.BOND else m * n
+    order = api.shuffled_ids(N, 4242 + m + n)
+    pcs = (0.3, 0.45, 0.5, 0.55, 0.7, 1.0) if kind == PL.BOND else (0.4, 0.55, 0.6, 0.65, 0.8)
+    if lat == 1:
+        pcs = tuple(p - 0.15 if kind == PL.BOND else p - 0.1 for p in pcs)
+    with api.Context(lat, m, n, pbc) as ctx:
+        for p in pcs:
+            c = int(p * N)
+            if kind == PL.BOND:
+                ctx.occupy(kind, bond_order=order, nbonds_=c)
+            else:
+                ctx.occupy(kind, site_order=order, nsites=c)
+            li = ctx.label()
+            mx, sp = ctx.cluster_sizes()
+            r = replay({"lattice": lat, "m": m, "n": n, "pbc": pbc}, kind, order, c)
+            assert mx == r["maxcs"], (p, mx, r["maxcs"])
+            want = int(r["csize"][r["perccln"]]) if r["perccln"] > 0 else 0
+            assert (li["nspan"] > 0) == (r["perccln"] > 0)
+            assert sp == want, (p, sp, want)

@@ -4,7 +4,8 @@
   bond_perc / site_perc (threshold scans, Square/bond_perc.f:86-369,
     site_perc.f:69-260): per trial the reference shuffle (host), the first
     spanning occupation count by GPU bisection (perc_first_spanning, ~log2 N
-    labelings), the reference label numbers at that count (host replay);
+    labelings), the largest and spanning cluster sizes at that count
+    (perc_cluster_sizes, GPU);
   bond_cond (Square/bond_cond.f:123-498): per trial one labeling +
     conductance solve at each of the ~100 grid points, then the pc scan.
 
@@ -38,7 +39,7 @@ def scan(api, L_mod, lat, L_, kind, trials):
             b = time.perf_counter()
             first = api.first_spanning(ctx, order, kind, N)
             c = time.perf_counter()
-            ctx.label_numbers(kind)
+            ctx.cluster_sizes()  # maxcs, spanning size on the GPU (perc_cluster_sizes)
             d = time.perf_counter()
             t_shuf += b - a
             t_gpu += c - b
@@ -51,7 +52,7 @@ def scan(api, L_mod, lat, L_, kind, trials):
                 ms_per_trial=round(wall * 1e3 / trials, 2),
                 host_shuffle_ms=round(t_shuf * 1e3 / trials, 2),
                 gpu_first_spanning_ms=round(t_gpu * 1e3 / trials, 2),
-                host_label_replay_ms=round(t_rep * 1e3 / trials, 2),
+                gpu_cluster_sizes_ms=round(t_rep * 1e3 / trials, 2),
                 mean_first_fraction=round(float(np.mean(firsts)) / N, 5))
 
 
