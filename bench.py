@@ -283,6 +283,10 @@ def main():
     ap.add_argument("--format", choices=("auto", "stencil", "stencil_tiled", "stencil_split", "csr"),
                     default="auto",
                     help="solver operator format (perc_set_matrix_format)")
+    ap.add_argument("--inline-orders", action="store_true",
+                    help="draw each timed realisation's occupation order inside the timed region "
+                         "(host thread, overlapping the previous realisation's GPU solve) instead "
+                         "of before it")
     ap.add_argument("--slabs", type=int, default=1,
                     help="row slabs of each CG solve on this GPU (perc_set_slabs; SURVEY §8(f) 2)")
     ap.add_argument("--cpu-worker", nargs=6, default=None, help=argparse.SUPPRESS)
@@ -341,10 +345,21 @@ def main():
         return (rng.permutation(n)[:cnt] + 1).astype(np.int32)
 
     t_draw = 0.0
+    inline = args.inline_orders and args.kind == "bond" and args.concurrent <= 1
     for k, ii in enumerate(ensemble.trial_indices(nreal, world, rank, nseeds=len(seeds))):
+        if inline and k >= args.warmup and k != args.warmup:
+            orders.append(None)  # drawn in the timed region (k == warmup: host copy kept below)
+            host_orders.append(None)
+            ii_list.append(ii)
+            continue
         td = time.perf_counter()
         o = draw(nb, tb, int(seeds[ii])) if args.kind != "site" else np.zeros(1, np.int32)
         t_draw += time.perf_counter() - td
+        if inline and k == args.warmup:  # drawn again inside the timed region
+            orders.append(None)
+            host_orders.append(o)
+            ii_list.append(ii)
+            continue
         orders.append(torch.from_numpy(np.ascontiguousarray(o)).to(dev))
         if args.kind != "bond":
             td = time.perf_counter()
@@ -419,7 +434,26 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     timed = list(range(args.warmup, nreal))
-    if K == 1:
+    if inline:
+        # order k + 1 is drawn and uploaded by a host thread while
+        # realisation k solves (libperc calls release the GIL); the first
+        # timed order is drawn inside the timed region too
+        from concurrent.futures import ThreadPoolExecutor
+
+        def prep(k_):
+            torch.cuda.set_device(local)
+            o_ = draw(nb, tb, int(seeds[ii_list[k_]]))
+            return torch.from_numpy(np.ascontiguousarray(o_)).to(dev)
+
+        results = []
+        with ThreadPoolExecutor(1) as tp:
+            fut = tp.submit(prep, timed[0])
+            for j_, k in enumerate(timed):
+                orders[k] = fut.result()
+                if j_ + 1 < len(timed):
+                    fut = tp.submit(prep, timed[j_ + 1])
+                results.append(run(k))
+    elif K == 1:
         results = [run(k) for k in timed]
     else:  # one host thread per context (ctypes drops the GIL in libperc calls)
         from concurrent.futures import ThreadPoolExecutor
@@ -568,6 +602,7 @@ def main():
         "cg_iterations_mean": round(float(stats[4]) / max(nspan, 1), 1),
         "spanning_fraction": round(float(stats[3]) / max(nsolves, 1), 3),
         "host_order_ms_per_realisation": round(t_draw * 1e3 / max(nreal, 1), 1),
+        "orders_in_timed_region": bool(inline),
         "host_order_note": ("occupation orders are drawn on the host before the timed region "
                             "and kept in HBM; an ensemble that draws them inline pays this per "
                             "realisation on one host core unless it overlaps the GPU solve"),

@@ -2808,9 +2808,12 @@ __global__ __launch_bounds__(kResThreads) void k_cg_res(ResArgs a) {
       block_sum<1>(v1, s_red);
       if (t == 0) store_sc1(&part[w], v1[0]);
     }
-    if (!(ok = res_barrier<MT == 1>(a, epoch, s_flag))) break;
     {
       double tot[1];
+      // (wave 0 summing the partials right after its own poll, with the
+      // workgroup barriers in between dropped, measured no faster: L = 1024
+      // 16.6 vs 16.4-16.6 us per iteration, L = 2048 35.8 vs 34.7)
+      if (!(ok = res_barrier<MT == 1>(a, epoch, s_flag))) break;
       res_total<1>(a, part, tot, s_red);
       ak = bknum / tot[0];
     }
@@ -2851,9 +2854,9 @@ __global__ __launch_bounds__(kResThreads) void k_cg_res(ResArgs a) {
       store_sc1(&part[G + w], acc2[0]);
       store_sc1(&part[2 * G + w], acc2[1]);
     }
-    if (!(ok = res_barrier<MT == 1>(a, epoch, s_flag))) break;
     {
       double tot[2];
+      if (!(ok = res_barrier<MT == 1>(a, epoch, s_flag))) break;
       res_total<2>(a, part + G, tot, s_red);
       err = sqrt(tot[1]) / bnrm;
       bk = tot[0] / bknum;
