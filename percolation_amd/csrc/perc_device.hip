@@ -2493,6 +2493,7 @@ struct ResArgs {
   double* xch;       // [2 parity][G][top, bottom][r, p][m]
   double* part;      // [2 parity][3][G]
   unsigned* bar;     // 9 counters, 128 B apart (zeroed before the launch)
+  double* gran;      // [3][G] 16-B granules {partial, tag} (zeroed before the launch)
 };
 
 // single-level (m = 1024: 0.0166 vs 0.0178 ms per iteration)
@@ -2535,9 +2536,9 @@ __device__ __forceinline__ bool res_barrier1(const ResArgs& a, unsigned& epoch, 
 // vs 0.0352 ms per iteration)
 __device__ __forceinline__ bool res_barrier2(const ResArgs& a, unsigned& epoch, int* s_flag) {
   __syncthreads();
+  ++epoch;  // in every thread: res_gather's tags are per lane
   if (threadIdx.x == 0) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    ++epoch;
     const int G = a.G, grp = blockIdx.x & 7, ngrp = G < 8 ? G : 8;
     const unsigned ng = (unsigned)((G - grp + 7) / 8);
     const unsigned old = __hip_atomic_fetch_add(&a.bar[grp * kTicketStride], 1u, __ATOMIC_RELAXED,
@@ -2566,6 +2567,74 @@ __device__ __forceinline__ bool res_barrier2(const ResArgs& a, unsigned& epoch, 
 template <bool POLL8>
 __device__ __forceinline__ bool res_barrier(const ResArgs& a, unsigned& epoch, int* s_flag) {
   return POLL8 ? res_barrier1(a, epoch, s_flag) : res_barrier2(a, epoch, s_flag);
+}
+
+// Reduction by all-gather of tagged granules (no counter): thread 0 of every
+// workgroup publishes each of its NV partials as one 16-B {value, tag}
+// write-through store after the workgroup barrier that drained every wave's
+// stores (its exchange rows included: payload sc1 -> vmcnt(0) -> granule,
+// MI355X_MICROARCH.md hand-off table, granule row); wave 0 of every
+// workgroup sweeps the G granules of each slot (16-B sc1 loads, lane l takes
+// workgroups l, l+64, ...) until every tag equals this reduction's epoch,
+// then sums the values lane-strided + butterfly (the association of
+// res_total, the same on every workgroup).  One slot per reduction kind
+// suffices: no workgroup can publish the next epoch of a kind before every
+// workgroup has left the other kind's reduction, i.e. finished polling this
+// one.  Returns false after a ~1 s timeout (a.S->pad[0] set).
+template <int NV>
+__device__ __forceinline__ bool res_gather(const ResArgs& a, unsigned& epoch, double* gran,
+                                           const double (&v)[NV], double (&tot)[NV],
+                                           double* s_red) {
+  __syncthreads();  // every wave's stores complete (release)
+  ++epoch;
+  const double tag = (double)epoch;
+  const int G = a.G;
+  const __amdgpu_buffer_rsrc_t rg = rsrc(gran, (unsigned)(NV * G * 16));
+  if (threadIdx.x == 0) {
+#pragma unroll
+    for (int j = 0; j < NV; ++j)  // one 16-B write-through (sc1) store per granule: untorn
+      __builtin_amdgcn_raw_buffer_store_b128(
+          __builtin_bit_cast(u32x4, make_double2(v[j], tag)), rg,
+          (int)(((size_t)j * G + blockIdx.x) * 16), 0, 16);
+  }
+  if (threadIdx.x < 64) {
+    const int lane = threadIdx.x;
+    int ok = 1;
+    double acc[NV];
+    for (unsigned spin = 0;; ++spin) {
+      bool all = true;
+#pragma unroll
+      for (int j = 0; j < NV; ++j) {
+        acc[j] = 0.0;
+        for (int i = lane; i < G; i += 64) {
+          // one 16-B sc1 load: value and tag of one granule, untorn
+          const double2 g2 = __builtin_bit_cast(
+              double2, __builtin_amdgcn_raw_buffer_load_b128(rg, (int)(((size_t)j * G + i) * 16), 0, 16));
+          all = all && g2.y == tag;
+          acc[j] = acc[j] + g2.x;
+        }
+      }
+      if (__builtin_amdgcn_readfirstlane(__all(all))) break;
+      if (spin > (1u << 24)) {  // ~1 s: give up, report, leave
+        if (lane == 0) a.S->pad[0] = 1;
+        ok = 0;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+#pragma unroll
+    for (int j = 0; j < NV; ++j) {
+      const double t = wave_sum(acc[j]);
+      if (lane == 0) s_red[24 + j] = t;
+    }
+    if (lane == 0) s_red[30] = ok ? 1.0 : 0.0;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < NV; ++j) tot[j] = s_red[24 + j];
+  const bool ok = s_red[30] != 0.0;
+  __syncthreads();  // s_red reuse by the next block_sum
+  return ok;
 }
 
 // every workgroup sums the G partials of one slot in workgroup order
@@ -2629,7 +2698,7 @@ __device__ __forceinline__ void res_pos(double& acc, unsigned um, unsigned map, 
 // UMC: compile-time superset of the raster positions the forms use (0x5A:
 // the square lattice's four neighbours), so unused positions and their
 // halo columns take no registers
-template <int MT, int HMAX, bool QREG = true, unsigned UMC = 0xFFu>
+template <int MT, int HMAX, bool QREG = true, unsigned UMC = 0xFFu, bool GATHER = false>
 __global__ __launch_bounds__(kResThreads) void k_cg_res(ResArgs a) {
   __shared__ double s_p[kResLdsRows];
   __shared__ double2 s_dt[kDiagTab];
@@ -2806,15 +2875,17 @@ __global__ __launch_bounds__(kResThreads) void k_cg_res(ResArgs a) {
     {
       double v1[1] = {dot};
       block_sum<1>(v1, s_red);
-      if (t == 0) store_sc1(&part[w], v1[0]);
-    }
-    {
       double tot[1];
-      // (wave 0 summing the partials right after its own poll, with the
-      // workgroup barriers in between dropped, measured no faster: L = 1024
-      // 16.6 vs 16.4-16.6 us per iteration, L = 2048 35.8 vs 34.7)
-      if (!(ok = res_barrier<MT == 1>(a, epoch, s_flag))) break;
-      res_total<1>(a, part, tot, s_red);
+      if (GATHER) {
+        if (!(ok = res_gather<1>(a, epoch, a.gran, v1, tot, s_red))) break;
+      } else {
+        if (t == 0) store_sc1(&part[w], v1[0]);
+        // (wave 0 summing the partials right after its own poll, with the
+        // workgroup barriers in between dropped, measured no faster: L =
+        // 1024 16.6 vs 16.4-16.6 us per iteration, L = 2048 35.8 vs 34.7)
+        if (!(ok = res_barrier<MT == 1>(a, epoch, s_flag))) break;
+        res_total<1>(a, part, tot, s_red);
+      }
       ak = bknum / tot[0];
     }
     // 3. r, z, dots, x; the band's first / last rows of r(k+1) and p(k)
@@ -2850,14 +2921,18 @@ __global__ __launch_bounds__(kResThreads) void k_cg_res(ResArgs a) {
         if constexpr (!QREG) __builtin_amdgcn_sched_barrier(0);
       }
     block_sum<2>(acc2, s_red);
-    if (t == 0) {
-      store_sc1(&part[G + w], acc2[0]);
-      store_sc1(&part[2 * G + w], acc2[1]);
-    }
     {
       double tot[2];
-      if (!(ok = res_barrier<MT == 1>(a, epoch, s_flag))) break;
-      res_total<2>(a, part + G, tot, s_red);
+      if (GATHER) {
+        if (!(ok = res_gather<2>(a, epoch, a.gran + 2 * (size_t)G, acc2, tot, s_red))) break;
+      } else {
+        if (t == 0) {
+          store_sc1(&part[G + w], acc2[0]);
+          store_sc1(&part[2 * G + w], acc2[1]);
+        }
+        if (!(ok = res_barrier<MT == 1>(a, epoch, s_flag))) break;
+        res_total<2>(a, part + G, tot, s_red);
+      }
       err = sqrt(tot[1]) / bnrm;
       bk = tot[0] / bknum;
       bknum = tot[0];
@@ -3267,6 +3342,7 @@ hipError_t dev_build_lattice(perc_ctx* h) {
     HIP_TRY(dmalloc(&d.res_xch, (size_t)2 * h->res_G * 2 * 2 * g.m));
     HIP_TRY(dmalloc(&d.res_part, (size_t)2 * 3 * h->res_G));
     HIP_TRY(dmalloc(&d.res_bar, 9 * kTicketStride));
+    HIP_TRY(dmalloc(&d.res_gran, (size_t)2 * 3 * h->res_G));
   }
   HIP_TRY(dmalloc(&d.partials, kRedSlots * red_partials_size(red_grid(h))));
   HIP_TRY(dmalloc(&d.tickets, kRedSlots * red_tickets_size(red_grid(h))));
@@ -3308,7 +3384,7 @@ void dev_free_all(perc_ctx* h) {
   void* ptrs[] = {d.bond_first, d.rowptr, d.col, d.val, d.diag, d.rhs, d.code, d.dtab, d.sflag, d.bocc, d.socc,
                   d.order, d.parent, d.member, d.top, d.counters, d.x, d.r,
                   d.p0, d.p1, d.q, d.partials, d.tickets, d.scal, d.err_hist, d.iout,
-                  d.res_xch, d.res_part, d.res_bar, d.bw, d.code_sm, d.csize};
+                  d.res_xch, d.res_part, d.res_bar, d.bw, d.code_sm, d.csize, d.res_gran};
   for (void* p : ptrs)
     if (p) hipFree(p);
   d = DeviceBuffers{};
@@ -3574,13 +3650,24 @@ hipError_t dev_solve_resident(perc_ctx* h, const CGArgs& ca, int* iter, double* 
   a.xch = d.res_xch;
   a.part = d.res_part;
   a.bar = d.res_bar;
+  a.gran = d.res_gran;
   HIP_TRY(hipMemsetAsync(d.res_bar, 0, 9 * kTicketStride * sizeof(unsigned), st));
+  HIP_TRY(hipMemsetAsync(d.res_gran, 0, (size_t)2 * 3 * h->res_G * sizeof(double), st));
   void* args[] = {&a};
   const void* fn = nullptr;
-  fn = h->res_MT == 1 ? (const void*)k_cg_res<1, 4>
-                      : (h->forms.umask & ~kResSquareMask) == 0
-                            ? (const void*)k_cg_res<2, 8, false, kResSquareMask>
-                            : (const void*)k_cg_res<2, 8, false>;
+  // reductions by tagged-granule all-gather (res_gather; PERC_RES_GATHER=0:
+  // the counter barrier + partial reads, for A/B): L = 1024 15.5 vs 16.6 us
+  // per iteration, L = 2048 33.7 vs 34.65 (profiles/r2_10_resident_gather_ab.log)
+  const bool gat = !(getenv("PERC_RES_GATHER") && atoi(getenv("PERC_RES_GATHER")) == 0);
+  const bool sq = (h->forms.umask & ~kResSquareMask) == 0;
+  if (gat)
+    fn = h->res_MT == 1 ? (const void*)k_cg_res<1, 4, true, 0xFFu, true>
+         : sq ? (const void*)k_cg_res<2, 8, false, kResSquareMask, true>
+              : (const void*)k_cg_res<2, 8, false, 0xFFu, true>;
+  else
+    fn = h->res_MT == 1 ? (const void*)k_cg_res<1, 4>
+         : sq ? (const void*)k_cg_res<2, 8, false, kResSquareMask>
+              : (const void*)k_cg_res<2, 8, false>;
   KernelTiming& T = h->timing;
   if (T.enabled) {
     if (T.ev.size() < 2) T.ev.resize(2, nullptr);

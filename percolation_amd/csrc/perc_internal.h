@@ -105,6 +105,7 @@ struct DeviceBuffers {
   double* res_xch = nullptr;    // resident solve: exchange rows, partials
   double* res_part = nullptr;
   unsigned* res_bar = nullptr;
+  double* res_gran = nullptr;   // resident solve: tagged partial granules
 };
 
 struct ReplayOrder {
