@@ -174,8 +174,9 @@ def kernel_label(key, minfo):
     if key == "pm" and minfo.get("kernel") in ("wave", "rows"):
         name = "k_cg_rm (workgroup row-march" if minfo["kernel"] == "rows" else \
             "k_cg_march (per-wave register march"
-        return "%s %d cols x %d rows%s): fused p = bk p + r/d, x += ak p, q = A p, q.p%s" % (
+        return "%s %d cols x %d rows%s%s): fused p = bk p + r/d, q = A p, q.p%s" % (
             name, minfo["strip_cols"], minfo["band_rows"], ", alternating" if minfo["alt"] else "",
+            ", strip-major" if minfo.get("strips") else "",
             "" if minfo["qfree"] else ", q stored")
     if key == "res":
         return ("k_cg_res (resident persistent solve, %d-row bands: p in LDS, r/q in registers, "
@@ -496,6 +497,9 @@ def main():
         assembled = False
     if "fmt" in seen:  # what the spanning realisations ran (labels + bytes below)
         fmt, minfo = fmt_names[seen["fmt"]], seen["minfo"]
+    mode_bits = args.march_mode if args.march_mode >= 0 else P.MARCH_DEFAULT
+    minfo["strips"] = bool(mode_bits & P._lib.MARCH_STRIPS) and not minfo.get("qfree") and \
+        minfo.get("kernel") == "wave" and N * 8 < (1 << 31) - 64 and args.slabs <= 1
 
     def kernel_set(f, probe=False):
         """(key, stats key, perc_bench_kernel id, bytes) of the CG kernels of

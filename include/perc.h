@@ -278,15 +278,17 @@ int perc_set_march_rows(perc_ctx *h, int rows);
    solve, r, p, q and the row codes are kept strip-major (each 128-column
    strip of the lattice contiguous, rows of a strip 1 KB apart), so every
    wave of the per-wave march walks one contiguous stream; x stays
-   row-major.  Measured at L = 4096: march 0.118 vs 0.111 ms row-major
-   (although the pure access pattern streams 8 % faster strip-major,
-   tools/mix_bench.hip), so it is not in the default. */
+   row-major.  In the default since round 2: with every memory instruction
+   of the march unconditional (no waitcnt drain per step) the strip-major
+   march runs 0.107 vs 0.115 ms row-major at L = 4096 (same box), the
+   solve 0.253 vs 0.238 solves/s.  Used when the vectors stay below 2 GB
+   (L < 16384); larger lattices solve row-major. */
 #define PERC_MARCH_QFREE 1
 #define PERC_MARCH_ALT 2
 #define PERC_MARCH_ROWS 4
 #define PERC_SOLVE_RESIDENT 8
 #define PERC_MARCH_STRIPS 16
-#define PERC_MARCH_DEFAULT (PERC_MARCH_ALT | PERC_SOLVE_RESIDENT)
+#define PERC_MARCH_DEFAULT (PERC_MARCH_ALT | PERC_SOLVE_RESIDENT | PERC_MARCH_STRIPS)
 int perc_set_march_mode(perc_ctx *h, int mode);
 /* Random bond conductances (MATLAB/ConductCalc.m condtype 2, :38-47 and
    :94-97): the bonds of the spanning cluster get G = -g0 * w[id] instead of

@@ -1740,12 +1740,6 @@ struct MGeom {
   bool hok;
 };
 
-// element (row gr, column col) in the solve's layout
-template <bool SM>
-__device__ __forceinline__ int midx(const CGArgs& a, int gr, int col) {
-  return SM ? sm_at(a.T, gr, col) : gr * a.T.m + col;
-}
-
 // Buffer views of the rows one march wave touches, [lo, hi) = its band plus
 // the halo rows, clipped to the loadable rows [glo, ghi): every load and
 // store of a step is issued unconditionally with a byte offset that is out
@@ -1762,13 +1756,25 @@ struct MBuf {
   int lo, hi;
 };
 
-template <int MODE>
+// strip-major solve (SM): whole-array views (vectors < 2 GB there), element
+// offsets through sm_at; row-major: the band's views, offsets from row lo
+template <int MODE, bool SM>
 __device__ __forceinline__ MBuf march_bufs(const CGArgs& a, const MGeom& g, const double* psrc,
                                            double* pnew) {
   const int m = a.T.m;
   MBuf B;
   B.lo = max(g.r0 - 1, a.glo);
   B.hi = max(min(g.rend + 1, a.ghi), B.lo);
+  if constexpr (SM) {
+    const unsigned nall = (unsigned)a.T.nrows * (unsigned)m;
+    B.p = rsrc(psrc, nall * 8u);
+    B.r = rsrc(a.r, nall * 8u);
+    B.c = rsrc(a.St.code, nall * 2u);
+    B.pn = rsrc(pnew, nall * 8u);
+    B.q = rsrc(a.q, MODE == kMarchPQ ? nall * 8u : 0u);
+    B.x = rsrc(a.x, 0u);  // the strip-major solve keeps x in B
+    return B;
+  }
   const long long base = (long long)B.lo * m;
   const unsigned n = (unsigned)(B.hi - B.lo) * (unsigned)m;
   const unsigned nown = (unsigned)max(g.rend - g.r0, 0) * (unsigned)m;
@@ -1781,14 +1787,19 @@ __device__ __forceinline__ MBuf march_bufs(const CGArgs& a, const MGeom& g, cons
   return B;
 }
 
+// element offset (in elements) of (row gr, column col) in a view of MBuf
+template <bool SM>
+__device__ __forceinline__ unsigned melem(const CGArgs& a, const MBuf& B, int gr, int col) {
+  return SM ? (unsigned)sm_at(a.T, gr, col) : (unsigned)((gr - B.lo) * a.T.m + col);
+}
+
 template <int MODE, bool SM>
 __device__ __forceinline__ void march_load(const CGArgs& a, const MGeom& g, const MBuf& B, int gr,
                                            bool first, const double* __restrict__ psrc, MRow& R) {
-  if constexpr (!SM) {
-    const int m = a.T.m;
+  {
     const bool rowok = (unsigned)(gr - B.lo) < (unsigned)(B.hi - B.lo);
-    const unsigned e = (unsigned)((gr - B.lo) * m + g.col);
-    const unsigned eh = (unsigned)((gr - B.lo) * m + g.hcol);
+    const unsigned e = rowok ? melem<SM>(a, B, gr, g.col) : 0u;
+    const unsigned eh = rowok ? melem<SM>(a, B, gr, g.hcol) : 0u;
     const unsigned o8 = rowok ? e * 8u : kOOB;
     const bool rown = MODE != kMarchB || (gr >= g.r0 && gr < g.rend);
     const bool hk = rowok && g.hok;
@@ -1804,25 +1815,6 @@ __device__ __forceinline__ void march_load(const CGArgs& a, const MGeom& g, cons
       R.hr = 0.0;
     }
     R.hp = bld1(B.p, first ? kOOB : h8);
-    return;
-  }
-  R.p = R.r = make_double2(0.0, 0.0);
-  R.c = R.hc = 0u;
-  R.hp = R.hr = 0.0;
-  if (gr >= a.glo && gr < a.ghi) {
-    const int i = midx<SM>(a, gr, g.col);
-    R.c = *reinterpret_cast<const unsigned*>(a.St.code + i);
-    if (MODE != kMarchB || (gr >= g.r0 && gr < g.rend))
-      R.r = *reinterpret_cast<const double2*>(a.r + i);
-    if (!first) R.p = *reinterpret_cast<const double2*>(psrc + i);
-    if (g.hok) {
-      const int hi = midx<SM>(a, gr, g.hcol);
-      if (MODE != kMarchB) {
-        R.hc = a.St.code[hi];
-        R.hr = a.r[hi];
-      }
-      if (!first) R.hp = psrc[hi];
-    }
   }
 }
 
@@ -1866,22 +1858,18 @@ __device__ __forceinline__ void march_step(const CGArgs& a, const MGeom& g, cons
         const double zh = div_tab(R.hr, s_dt[diag_idx(R.hc)]);
         hpn = first ? zh : bk * R.hp + zh;
       }
-      // own row; in a slab also the ghost rows, so the next iteration's
-      // halo p(k) is at hand (bitwise the neighbour slab's own value)
-      if (SM && ((gr >= g.r0 && gr < g.rend) || (a.slab && (gr < 0 || gr >= nrows)))) {
-        const int i = midx<SM>(a, gr, g.col);
-        st2(pnew + i, pn, true);
-      }
     }
   }
-  if constexpr (!SM) {
+  {
     if (MODE != kMarchB) {
       const int m = a.T.m;
+      // own row; in a slab also the ghost rows, so the next iteration's
+      // halo p(k) is at hand (bitwise the neighbour slab's own value)
       const bool own = gr >= g.r0 && gr < g.rend;
       const bool pst = (unsigned)(gr - B.lo) < (unsigned)(B.hi - B.lo) &&
                        (own || (a.slab && (gr < 0 || gr >= nrows)));
-      bst2<kNT>(B.pn, pst ? (unsigned)((gr - B.lo) * m + g.col) * 8u : kOOB, pn);
-      if (MODE == kMarchP) {  // x += ak p(k-1) on the x rows (the P-only march keeps x)
+      bst2<kNT>(B.pn, pst ? melem<SM>(a, B, gr, g.col) * 8u : kOOB, pn);
+      if (MODE == kMarchP && !SM) {  // x += ak p(k-1) on the x rows (the P-only march keeps x)
         const int i = gr * m + g.col;
         const bool xw = own && !first && !a.bx && (a.xrows == 0 || i < a.xrows || i >= N - a.xrows);
         const unsigned ox = xw ? (unsigned)((gr - g.r0) * m + g.col) * 8u : kOOB;
@@ -1949,13 +1937,11 @@ __device__ __forceinline__ void march_step(const CGArgs& a, const MGeom& g, cons
         q1 = march_q_gen<1>(c1w, dM1.x, W.C.e1, s_rpos[f1], s_w, lane, ng0, nleak);
       }
     }
-    const int i = midx<SM>(a, mid, g.col);
     if (MODE == kMarchB) {
       // k_cg_b's per-pair arithmetic
       double2 rn;
       rn.x = W.rM.x - ak * q0;
       rn.y = W.rM.y - ak * q1;
-      if (SM) st2(a.r + i, rn, true);
       mr = rn;
       const double z0 = div_tab(rn.x, dM0), z1 = div_tab(rn.y, dM1);
       acc[0] = acc[0] + z0 * rn.x;
@@ -1963,18 +1949,16 @@ __device__ __forceinline__ void march_step(const CGArgs& a, const MGeom& g, cons
       acc[1] = acc[1] + rn.x * rn.x;
       acc[1] = acc[1] + rn.y * rn.y;
     } else {
-      if (SM && MODE == kMarchPQ) st2(a.q + i, make_double2(q0, q1), true);
       mq = make_double2(q0, q1);
       acc[0] = acc[0] + q0 * W.C.e0;
       acc[0] = acc[0] + q1 * W.C.e1;
     }
   }
-  if constexpr (!SM) {
+  {
     const int m = a.T.m;
-    if (MODE == kMarchPQ)
-      bst2<kNT>(B.q, mown ? (unsigned)((mid - g.r0) * m + g.col) * 8u : kOOB, mq);
-    if (MODE == kMarchB)
-      bst2<kNT>(B.r, mown ? (unsigned)((mid - B.lo) * m + g.col) * 8u : kOOB, mr);
+    const unsigned eq = SM ? (unsigned)sm_at(a.T, mid, g.col) : (unsigned)((mid - g.r0) * m + g.col);
+    if (MODE == kMarchPQ) bst2<kNT>(B.q, mown ? eq * 8u : kOOB, mq);
+    if (MODE == kMarchB) bst2<kNT>(B.r, mown ? melem<SM>(a, B, mid, g.col) * 8u : kOOB, mr);
   }
 }
 
@@ -1997,22 +1981,13 @@ __device__ __forceinline__ void march_walk(const CGArgs& a, const MGeom& g, cons
 #pragma unroll
     for (int u = 0; u < D; ++u) {
       const int j = j0 + u;
-      if constexpr (!SM) {
-        // no branches around memory instructions: a step past the walk
-        // (odd step count) and the prefetch past its end address rows
-        // outside the view (loads return 0, stores are dropped) and finish
-        // no row
-        const MRow R = ring[u];
-        march_load<MODE, SM>(a, g, B, UP ? g.rend - (j + D) : g.r0 - 1 + j + D, first, psrc, ring[u]);
-        march_step<MODE, UP, SM>(a, g, B, R, UP ? g.rend - j : g.r0 - 1 + j, first, bk, ak, pnew, s_dt,
-                                 s_rpos, s_rmap, s_w, W, acc);
-      } else if (j < nsteps) {
-        const MRow R = ring[u];
-        if (j + D < nsteps)
-          march_load<MODE, SM>(a, g, B, UP ? g.rend - (j + D) : g.r0 - 1 + j + D, first, psrc, ring[u]);
-        march_step<MODE, UP, SM>(a, g, B, R, UP ? g.rend - j : g.r0 - 1 + j, first, bk, ak, pnew, s_dt,
-                                 s_rpos, s_rmap, s_w, W, acc);
-      }
+      // no branches around memory instructions: a step past the walk (odd
+      // step count) and the prefetch past its end address rows outside the
+      // view (loads return 0, stores are dropped) and finish no row
+      const MRow R = ring[u];
+      march_load<MODE, SM>(a, g, B, UP ? g.rend - (j + D) : g.r0 - 1 + j + D, first, psrc, ring[u]);
+      march_step<MODE, UP, SM>(a, g, B, R, UP ? g.rend - j : g.r0 - 1 + j, first, bk, ak, pnew, s_dt,
+                               s_rpos, s_rmap, s_w, W, acc);
     }
   }
 }
@@ -2055,7 +2030,7 @@ __global__ __launch_bounds__(64 * kMarchWaves) void k_cg_march(CGArgs a) {
   }
   const bool up = (a.march_alt && (band & 1)) != (MODE == kMarchB);
   const int nsteps = g.rend - g.r0 + 2;
-  const MBuf B = march_bufs<MODE>(a, g, psrc, pnew);
+  const MBuf B = march_bufs<MODE, SM>(a, g, psrc, pnew);
   MRow ring[D];
   if (active) {
 #pragma unroll
@@ -3113,7 +3088,7 @@ void launch_cg_spmv(perc_ctx* h, const CGArgs& a, int G) {
     }
     if (h->march) {
       if (h->qfree) klaunch(h, k_cg_march<kMarchP>, h->march_grid, 64 * kMarchWaves, st, a);
-      else if (a.sm) klaunch(h, k_cg_march<kMarchPQ, true>, h->march_grid, 64 * kMarchWaves, st, a);
+      else if (a.sm) klaunch(h, k_cg_march<kMarchPQ, true, 3>, h->march_grid, 64 * kMarchWaves, st, a);
       else if (h->march_depth == 2) klaunch(h, k_cg_march<kMarchPQ, false, 2>, h->march_grid, 64 * kMarchWaves, st, a);
       else klaunch(h, k_cg_march<kMarchPQ, false, 3>, h->march_grid, 64 * kMarchWaves, st, a);
       return;
@@ -3585,7 +3560,9 @@ void select_format(perc_ctx* h) {
   h->qfree = (h->march || h->rowmarch) && (h->march_mode & PERC_MARCH_QFREE);
   h->march_alt = (h->march || h->rowmarch) && (h->march_mode & PERC_MARCH_ALT);
   // strip-major solve: the per-wave march with the streaming B (x in B)
-  h->strips = h->march && !h->qfree && (h->march_mode & PERC_MARCH_STRIPS);
+  // (whole-array buffer views in the strip-major march: vectors < 2 GB)
+  h->strips = h->march && !h->qfree && (h->march_mode & PERC_MARCH_STRIPS) &&
+              (size_t)h->N * sizeof(double) < ((size_t)1 << 31) - 64;
 }
 
 // strip-major copies of r (into the q buffer: r and q swap roles for the
@@ -3888,7 +3865,8 @@ hipError_t dev_solve_slabs(perc_ctx* h, int K, int itol, double tol, int itmax, 
   DeviceBuffers& d = h->d;
   hipStream_t st = h->stream;
   const int m = h->g.m, nrows = h->g.n - 2;
-  if (!h->march || h->qfree || h->strips || K < 1 || K > nrows) return hipErrorInvalidValue;
+  // (the slabs run the row-major march: PERC_MARCH_STRIPS does not apply)
+  if (!h->march || h->qfree || K < 1 || K > nrows) return hipErrorInvalidValue;
   int cus = 0;
   HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, h->device));
   const int spr = m / kMarchW;
