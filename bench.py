@@ -499,7 +499,7 @@ def main():
         fmt, minfo = fmt_names[seen["fmt"]], seen["minfo"]
     mode_bits = args.march_mode if args.march_mode >= 0 else P.MARCH_DEFAULT
     minfo["strips"] = bool(mode_bits & P._lib.MARCH_STRIPS) and not minfo.get("qfree") and \
-        minfo.get("kernel") == "wave" and N * 8 < (1 << 31) - 64 and args.slabs <= 1
+        minfo.get("kernel") == "wave" and N * 8 <= (256 << 20) and args.slabs <= 1
 
     def kernel_set(f, probe=False):
         """(key, stats key, perc_bench_kernel id, bytes) of the CG kernels of

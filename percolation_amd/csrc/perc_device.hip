@@ -3560,9 +3560,12 @@ void select_format(perc_ctx* h) {
   h->qfree = (h->march || h->rowmarch) && (h->march_mode & PERC_MARCH_QFREE);
   h->march_alt = (h->march || h->rowmarch) && (h->march_mode & PERC_MARCH_ALT);
   // strip-major solve: the per-wave march with the streaming B (x in B)
-  // (whole-array buffer views in the strip-major march: vectors < 2 GB)
+  // strip-major only while a vector fits the Infinity Cache (L <= 4096):
+  // past it (16-row bands, several rounds of waves) the row-major march is
+  // faster (L = 8192: 0.439 vs 0.480 ms, profiles/r2_11_ab_strips.log); the
+  // strip-major march's whole-array buffer views also need < 2 GB
   h->strips = h->march && !h->qfree && (h->march_mode & PERC_MARCH_STRIPS) &&
-              (size_t)h->N * sizeof(double) < ((size_t)1 << 31) - 64;
+              (size_t)h->N * sizeof(double) <= kLargeVector;
 }
 
 // strip-major copies of r (into the q buffer: r and q swap roles for the

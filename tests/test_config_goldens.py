@@ -99,6 +99,11 @@ def test_config_fixture(path):
             print(json.dumps(d))
     tols = sorted(doc["solves"], key=float)
     tight = tols[0]
+    if float(tight) > 1e-13:  # no converged fixture yet (still generating)
+        for tkey, d in report:
+            assert abs(d["iter"] - d["iter_ref"]) <= 1, d
+            assert d["gtop_rel"] < 1e-6 and d["gbot_rel"] < 1e-6, d  # the solver-tolerance scale
+        return
     conv = doc["solves"][tight]
     prev = doc["solves"][tols[1]] if len(tols) > 1 else None
     for tkey, d in report:
