@@ -3088,6 +3088,8 @@ void launch_cg_spmv(perc_ctx* h, const CGArgs& a, int G) {
     }
     if (h->march) {
       if (h->qfree) klaunch(h, k_cg_march<kMarchP>, h->march_grid, 64 * kMarchWaves, st, a);
+      else if (a.sm && h->march_depth == 2) klaunch(h, k_cg_march<kMarchPQ, true, 2>, h->march_grid, 64 * kMarchWaves, st, a);
+      else if (a.sm && h->march_depth == 4) klaunch(h, k_cg_march<kMarchPQ, true, 4>, h->march_grid, 64 * kMarchWaves, st, a);
       else if (a.sm) klaunch(h, k_cg_march<kMarchPQ, true, 3>, h->march_grid, 64 * kMarchWaves, st, a);
       else if (h->march_depth == 2) klaunch(h, k_cg_march<kMarchPQ, false, 2>, h->march_grid, 64 * kMarchWaves, st, a);
       else klaunch(h, k_cg_march<kMarchPQ, false, 3>, h->march_grid, 64 * kMarchWaves, st, a);
@@ -3479,8 +3481,11 @@ int march_rows_for(const perc_ctx* h, int nrows) {
   if ((size_t)g.m * nrows * sizeof(double) > kLargeVector) return 16;
   int cus = 0, per_cu = 0;
   hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, h->device);
+  // (the strip-major kernel of the same depth: within a few VGPRs, same occupancy)
   if (h->march_depth == 2)
     hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_cg_march<kMarchPQ, false, 2>, 64 * kMarchWaves, 0);
+  else if (h->march_depth == 4)
+    hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_cg_march<kMarchPQ, true, 4>, 64 * kMarchWaves, 0);
   else
     hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_cg_march<kMarchPQ, false, 3>, 64 * kMarchWaves, 0);
   const long long slots = (long long)std::max(cus, 1) * std::max(per_cu, 1) * kMarchWaves;
@@ -3493,7 +3498,8 @@ void march_geometry(perc_ctx* h) {
   const Geom& g = h->g;
   h->march_grid = 0;
   // rows prefetched ahead by the P+S march (PERC_MARCH_DEPTH: 2 for probes)
-  h->march_depth = getenv("PERC_MARCH_DEPTH") && atoi(getenv("PERC_MARCH_DEPTH")) == 2 ? 2 : 3;
+  h->march_depth = 3;
+  if (const char* e = getenv("PERC_MARCH_DEPTH")) h->march_depth = std::min(std::max(atoi(e), 2), 4);
   if (g.m % kMarchW != 0 || g.n <= 2) return;
   const int spr = g.m / kMarchW, nrows = g.n - 2;
   h->march_h = march_rows_for(h, nrows);
