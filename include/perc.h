@@ -299,7 +299,9 @@ int perc_set_march_mode(perc_ctx *h, int mode);
 int perc_set_bond_weights(perc_ctx *h, const double *w, long long n);
 /* Solver loop of the assembled system: out5[0] = 0 (no march kernel: LDS
    tiles, split or CSR), 1 (per-wave march k_cg_march), 2 (workgroup
-   row-march k_cg_rm), 3 (resident persistent solve k_cg_res); out5[1] =
+   row-march k_cg_rm), 3 (resident persistent solve k_cg_res), 4 (one-
+   workgroup solve of a small system, k_cg_small: N <= 12288 under
+   PERC_FMT_AUTO with PERC_SOLVE_RESIDENT set); out5[1] =
    q-free B, out5[2] = alternating
    directions, out5[3] = band height, out5[4] = strip width (columns). */
 int perc_march_info(perc_ctx *h, int *out5);

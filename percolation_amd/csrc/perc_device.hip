@@ -2925,6 +2925,152 @@ __global__ __launch_bounds__(kResThreads) void k_cg_res(ResArgs a) {
   }
 }
 
+// ---------------------------------------------------------------------------
+// Small systems (N <= kSmallRows = 8192: lattices up to ~91 x 91, the reference
+// drivers' 10 x 10 .. 50 x 50): the whole linbcg loop in ONE workgroup.
+// Launched kernels spend ~20 us per iteration there on launch gaps and
+// reduction tails for microseconds of work; here an iteration is two
+// workgroup barriers.  Thread t owns rows t, t + 1024, ...: r and the
+// diagonal stay in registers, p(k) in LDS, the CSR operator (NR order:
+// diagonal first, then ascending columns, bondc.f:887-899) is read from
+// global memory (L2-resident at this size).  Per-row arithmetic is the
+// launched kernels' (p = bk p + r/d, q, r -= ak q, x += ak p); the dots are
+// summed per thread in row order, then wave butterflies, then the waves in
+// order.  The prologue (r, bnrm, the first bknum) is k_cg_init's.
+constexpr int kSmallThreads = 1024, kSmallEPT = 8, kSmallRows = kSmallThreads * kSmallEPT;
+
+// ST: the stencil operator (row codes in registers, the forms' offsets in
+// LDS: no global memory access in the loop but the x update); else the CSR
+// operator from global memory
+template <bool ST>
+__global__ __launch_bounds__(kSmallThreads) void k_cg_small(CGArgs a) {
+  __shared__ double s_p[kSmallRows], s_q[kSmallRows];
+  __shared__ uint16_t s_c[ST ? kSmallRows : 1];
+  __shared__ double s_red[40];
+  __shared__ int s_off[kMaxForms * kMaxSlots];
+  if (ST) load_forms(a.St.F, s_off);  // (includes a workgroup barrier)
+  CGScalars* S = a.S;
+  const int N = a.A.N, t = threadIdx.x;
+  const int lane = t & 63, wid = t >> 6;
+  const double ng0 = a.St.ng0, nleak = a.St.nleak;
+  // r, the diagonal and x in registers (loops over j fully unrolled);
+  // p(k), q and the row codes in LDS
+  double rv[kSmallEPT], dv[kSmallEPT], xv[kSmallEPT];
+#pragma unroll
+  for (int j = 0; j < kSmallEPT; ++j) {
+    const int i = t + j * kSmallThreads;
+    rv[j] = i < N ? a.r[i] : 0.0;
+    xv[j] = i < N ? a.x[i] : 0.0;
+    const unsigned c = ST && i < N ? (unsigned)a.St.code[i] : 0u;
+    if (ST && i < N) s_c[i] = (uint16_t)c;
+    dv[j] = i < N ? (ST ? code_diag(c, ng0, nleak) : a.A.diag[i]) : 1.0;
+  }
+  double bknum = S->bknum, bk = 0.0, ak = 0.0, err = S->err;
+  const double bnrm = S->bnrm, tol = S->tol;
+  const int itmax = S->itmax;
+  // workgroup sum: per-wave butterfly, then the waves in order
+  auto wg_sum = [&](double v0, double v1, double* o0, double* o1) {
+    v0 = wave_sum(v0);
+    v1 = wave_sum(v1);
+    if (lane == 0) {
+      s_red[wid] = v0;
+      s_red[16 + wid] = v1;
+    }
+    __syncthreads();
+    double t0 = s_red[0], t1 = s_red[16];
+    for (int w = 1; w < kSmallThreads / 64; ++w) {
+      t0 = t0 + s_red[w];
+      t1 = t1 + s_red[16 + w];
+    }
+    __syncthreads();  // s_red reuse
+    *o0 = t0;
+    *o1 = t1;
+  };
+  int k = 0;
+  while (true) {
+    ++k;
+    // p(k) = bk p(k-1) + z (k = 1: p = z), linbcg :789-797
+#pragma unroll
+    for (int j = 0; j < kSmallEPT; ++j) {
+      const int i = t + j * kSmallThreads;
+      if (i < N) {
+        const double z = rv[j] / dv[j];
+        s_p[i] = k == 1 ? z : bk * s_p[i] + z;
+      }
+    }
+    __syncthreads();
+    // q = A p (dsprsax order) into LDS, and q.p (one row at a time: the
+    // slot arrays stay in registers)
+    double dot = 0.0;
+#pragma unroll 1
+    for (int i = t; i < N; i += kSmallThreads) {
+      double q;
+      {
+        const double pi = s_p[i];
+        if (ST) {
+          const unsigned c = s_c[i];
+          const int f = c >> 11, cnt = (c >> 8) & 7;
+          double xn[kMaxSlots];
+          bool use[kMaxSlots];
+#pragma unroll
+          for (int e = 0; e < kMaxSlots; ++e) {
+            const int col = i + s_off[f * kMaxSlots + e];
+            use[e] = e < cnt && (unsigned)col < (unsigned)N;
+            xn[e] = s_p[use[e] ? col : i];
+          }
+          q = st_combine<kMaxSlots>(c, xn, use, pi, ng0, nleak);
+        } else {
+          q = a.A.diag[i] * pi;
+          for (int e = a.A.rowptr[i]; e < a.A.rowptr[i + 1]; ++e) q = q + a.A.val[e] * s_p[a.A.col[e]];
+        }
+        dot = dot + q * pi;
+      }
+      s_q[i] = q;
+    }
+    double akden, unused;
+    wg_sum(dot, 0.0, &akden, &unused);
+    ak = bknum / akden;
+    // x += ak p, r -= ak q, z = r/d, z.r and r.r (linbcg :801-806, 808-813)
+    double zr = 0.0, rr = 0.0;
+#pragma unroll
+    for (int j = 0; j < kSmallEPT; ++j) {
+      const int i = t + j * kSmallThreads;
+      if (i < N) {
+        xv[j] = xv[j] + ak * s_p[i];
+        const double rn = rv[j] - ak * s_q[i];
+        rv[j] = rn;
+        const double z = rn / dv[j];
+        zr = zr + z * rn;
+        rr = rr + rn * rn;
+      }
+    }
+    double tzr, trr;
+    wg_sum(zr, rr, &tzr, &trr);
+    err = sqrt(trr) / bnrm;
+    bk = tzr / bknum;
+    bknum = tzr;
+    if (t == 0 && k - 1 < a.err_hist_cap) a.err_hist[k - 1] = err;
+    if (!(err > tol) || k >= itmax + 1) break;
+  }
+#pragma unroll
+  for (int j = 0; j < kSmallEPT; ++j) {
+    const int i = t + j * kSmallThreads;
+    if (i < N) {
+      a.r[i] = rv[j];
+      a.x[i] = xv[j];
+    }
+  }
+  if (t == 0) {
+    S->iter = k;
+    S->err = err;
+    S->ak = ak;
+    S->bk = bk;
+    S->bknum = bknum;
+    S->akden = 0.0;
+    S->done = 1;
+  }
+}
+
 // r = b - A x (or r = b when x = 0), then bnrm and the first bknum
 // (linbcg prologue, bondc.f:758-779)
 template <bool ST>
@@ -3566,6 +3712,10 @@ void select_format(perc_ctx* h) {
   h->qfree = (h->march || h->rowmarch) && (h->march_mode & PERC_MARCH_QFREE);
   h->march_alt = (h->march || h->rowmarch) && (h->march_mode & PERC_MARCH_ALT);
   // strip-major solve: the per-wave march with the streaming B (x in B)
+  // one-workgroup solve for small systems, under the default format only
+  // (an explicit format keeps its launched kernels, e.g. for the tests)
+  h->small = h->fmt_req == PERC_FMT_AUTO && h->N > 0 && h->N <= kSmallRows &&
+             (h->march_mode & PERC_SOLVE_RESIDENT) && h->d.rowptr != nullptr;
   // strip-major only while a vector fits the Infinity Cache (L <= 4096):
   // past it (16-row bands, several rounds of waves) the row-major march is
   // faster (L = 8192: 0.439 vs 0.480 ms, profiles/r2_11_ab_strips.log); the
@@ -3716,6 +3866,18 @@ hipError_t dev_solve(perc_ctx* h, int itol, double tol, int itmax, bool x0_zero,
   if (ST) k_cg_init<true><<<G, kBlock, 0, st>>>(a, itol, x0_zero ? 1 : 0);
   else k_cg_init<false><<<G, kBlock, 0, st>>>(a, itol, x0_zero ? 1 : 0);
   HIP_TRY(dbg_sync(st, "k_cg_init"));
+  if (h->small) {  // one workgroup runs the whole loop (k_cg_small)
+    // (x is kept on every row here: the operator is the CSR one and N small)
+    if (ST) k_cg_small<true><<<1, kSmallThreads, 0, st>>>(a);
+    else k_cg_small<false><<<1, kSmallThreads, 0, st>>>(a);
+    HIP_TRY(dbg_sync(st, "k_cg_small"));
+    CGScalars hs{};
+    HIP_TRY(hipMemcpyAsync(&hs, d.scal, sizeof(hs), hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    *iter = hs.iter;
+    *err = hs.err;
+    return hipSuccess;
+  }
   if (h->resident) {
     const hipError_t e = dev_solve_resident(h, a, iter, err);
     // the cooperative launch can be refused when the grid cannot be

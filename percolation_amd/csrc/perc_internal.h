@@ -168,6 +168,7 @@ struct perc_ctx {
   int b_grid = 0;               // streaming B workgroups in the fused formats (dev_build_lattice)
   bool has_weights = false;     // perc_set_bond_weights: G = -g0 w for the spanning bonds
   bool resident = false;        // persistent resident solve (k_cg_res)
+  bool small = false;           // one-workgroup solve of a small system (k_cg_small)
   int res_G = 0, res_H = 0, res_MT = 0, res_HMAX = 0;  // its grid, band height, template
   int rm_w = 0, rm_h = 16;      // their strip width (columns) and band height
   int rm_grid = 0;              // their workgroups
