@@ -1713,10 +1713,10 @@ __device__ __forceinline__ double march_q_map(unsigned c, double d, double xi, u
 }
 
 // Rows prefetched ahead (template D).  The P+S kernel of the solve runs
-// D = 3 (march_geometry: 173 VGPRs, 2 waves per SIMD, one round of 64-row
-// bands at L = 4096): 0.104-0.107 vs 0.114-0.117 ms with D = 2 (136 VGPRs,
-// 3 waves per SIMD, 43-row bands) on the same box, D = 4 no better
-// (profiles/r2_4_march_depth.log).  Before the memory instructions were
+// D = 3 (strip-major: 162 VGPRs, 3 waves per SIMD, one round of 43-row
+// bands at L = 4096): 0.106-0.107 ms vs D = 4 / 5 at 2 waves per SIMD
+// 0.114-0.116 (profiles/r2_12_strips_depth_rows_probe.log,
+// r2_14_march_depth5.log): waves per SIMD, not rows in flight, decide.  Before the memory instructions were
 // made unconditional (MBuf) every step waited for vmcnt(0) and deeper
 // prefetch could not help.  The opt-in variants (q-free P and B, strip-
 // major) keep D = 2.

@@ -743,3 +743,29 @@ def test_full_and_tiny_lattices_vs_oracle(lat, m, n, pbc):
     oc = O.conductance(lat, m, n, pbc, b1, b2, -np.ones(nb), tol=1e-14, itmax=100000)
     assert rel(c["gtop"], oc["gtop"]) < REL and rel(c["gbot"], oc["gbot"]) < REL
     assert abs(c["iter"] - oc["iter"]) <= 1
+
+
+@pytest.mark.parametrize("lat,m,n,pbc,p", [(0, 90, 90, 0, 0.6), (1, 64, 80, 1, 0.42),
+                                           (0, 100, 80, 1, 0.55), (1, 50, 50, 0, 0.4)])
+def test_small_solver_matches_launched(lat, m, n, pbc, p):
+    """The one-workgroup solve (k_cg_small, default format, N <= 8192)
+    against the launched kernels of an explicit format: same per-row
+    arithmetic, dots associated differently -- iterations +-1 and Gtop /
+    Gbot / voltages to 1e-10 at tol 1e-13; and it is the solver that ran."""
+    nb = api.nbonds(lat, m, n, pbc)
+    order = api.shuffled_ids(nb, 999 + m)
+    out = {}
+    for fmt in (PL.FMT_AUTO, PL.FMT_STENCIL_SPLIT, PL.FMT_CSR):
+        with api.Context(lat, m, n, pbc) as ctx:
+            ctx.set_matrix_format(fmt)
+            ctx.occupy(PL.BOND, bond_order=order, nbonds_=int(p * nb))
+            if ctx.label()["nspan"] == 0:
+                pytest.skip("no spanning cluster")
+            out[fmt] = ctx.conductance(tol=1e-13, itmax=100000, vint=True)
+            assert (ctx.march_info()["kernel"] == "small") == (fmt == PL.FMT_AUTO)
+    s = out[PL.FMT_AUTO]
+    for fmt in (PL.FMT_STENCIL_SPLIT, PL.FMT_CSR):
+        c = out[fmt]
+        assert abs(s["iter"] - c["iter"]) <= 1
+        assert rel(s["gtop"], c["gtop"]) < REL and rel(s["gbot"], c["gbot"]) < REL
+        assert np.max(np.abs(s["vint"] - c["vint"])) < 1e-8
