@@ -1992,8 +1992,12 @@ __device__ __forceinline__ void march_walk(const CGArgs& a, const MGeom& g, cons
   }
 }
 
+// (the P+S kernel with D = 2: at most 128 VGPRs, i.e. 4 waves per SIMD)
+template <int MODE, int D>
+constexpr int kMarchWavesPerEU = D == 2 && MODE == kMarchPQ ? 4 : 1;
+
 template <int MODE, bool SM = false, int D = kMarchDepth>
-__global__ __launch_bounds__(64 * kMarchWaves) void k_cg_march(CGArgs a) {
+__global__ __launch_bounds__(64 * kMarchWaves, (kMarchWavesPerEU<MODE, D>)) void k_cg_march(CGArgs a) {
   CGScalars* S = a.S;
   __shared__ double s_red[32];
   __shared__ int s_flag[2];
