@@ -2,8 +2,9 @@
 """Benchmark: conductance solves/s + CG SpMV GB/s on the BASELINE.json metric
 workload (square L=4096 bond percolation at p=0.60, bondc semantics).
 
-One "step" = one realisation through the whole hot path: occupancy from a
-device-resident occupation order, GPU labeling + spanning, Kirchhoff
+One "step" = one realisation through the whole hot path: occupancy drawn
+on the GPU (perc_occupy_random; or from a device-resident order drawn on
+the host, --occupancy uniform), GPU labeling + spanning, Kirchhoff
 assembly, fused Jacobi-PCG to tol 1e-8 (linbcg stopping rule, itmax 1e6),
 terminal currents.  Realisations shard across ranks (ii = step*world+rank,
 seeds tseed(ii) from master 58302, bond_cond.f:65-70); the only collective
@@ -136,20 +137,25 @@ def cpu_worker(spec, cpu_iters):
     iters, nb, tb; the order drawn as main() draws it)."""
     L_, p, seed, iters, nb, tb = (int(spec[0]), float(spec[1]), int(spec[2]), int(spec[3]),
                                   int(spec[4]), int(spec[5]))
-    order = (np.random.default_rng(seed).permutation(nb)[:tb] + 1).astype(np.int32)
+    if os.environ.get("PERC_BENCH_OCCUPANCY") == "device":  # the keys' order (host, libperc)
+        from percolation_amd import api
+        order = np.ascontiguousarray(api.random_order(nb, tb, seed), dtype=np.int32)
+    else:
+        order = (np.random.default_rng(seed).permutation(nb)[:tb] + 1).astype(np.int32)
     print(json.dumps(cpu_baseline(L_, p, order, iters, cpu_iters)), flush=True)
 
 
-def cpu_ensemble(L_, p, seeds, iters, nb, tb, cpu_iters, cores):
+def cpu_ensemble(L_, p, seeds, iters, nb, tb, cpu_iters, cores, occupancy="uniform"):
     """ensemble throughput of the CPU path with all host
     cores, one independent realisation per core (child processes running
     cpu_worker concurrently, so memory-bandwidth contention is included)."""
     import subprocess
     t0 = time.perf_counter()
+    env = dict(os.environ, PERC_BENCH_OCCUPANCY=occupancy)
     procs = [subprocess.Popen([sys.executable, os.path.abspath(__file__), "--cpu-iters",
                                str(cpu_iters), "--cpu-worker", str(L_), str(p), str(int(sd)),
                                str(iters), str(nb), str(tb)],
-                              stdout=subprocess.PIPE, stderr=subprocess.DEVNULL, text=True)
+                              stdout=subprocess.PIPE, stderr=subprocess.DEVNULL, text=True, env=env)
              for sd in seeds[:cores]]
     res = []
     for pr in procs:
@@ -257,7 +263,7 @@ def pmc_traffic(key, fmt, L_):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=4)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--L", type=int, default=4096)
     ap.add_argument("--p", type=float, default=0.60)
@@ -266,7 +272,11 @@ def main():
     ap.add_argument("--itmax", type=int, default=10 ** 6)
     ap.add_argument("--cpu-iters", type=int, default=20)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--occupancy", choices=("uniform", "reference"), default="uniform")
+    ap.add_argument("--occupancy", choices=("device", "uniform", "reference"), default="device",
+                    help="device: drawn on the GPU inside each realisation (perc_occupy_random, "
+                         "counter-based keys from tseed(ii)); uniform: numpy PCG64 permutation "
+                         "drawn on the host before the timed region; reference: the reference's "
+                         "REAL*4 shuffle (biased above 2^22 bonds, H10)")
     ap.add_argument("--force-dist", action="store_true",
                     help="initialise the RCCL process group even at world size 1 (checks the "
                          "multi-GPU path on one GPU)")
@@ -347,7 +357,14 @@ def main():
 
     t_draw = 0.0
     inline = args.inline_orders and args.kind == "bond" and args.concurrent <= 1
+    devocc = args.occupancy == "device"
     for k, ii in enumerate(ensemble.trial_indices(nreal, world, rank, nseeds=len(seeds))):
+        if devocc:  # drawn on the GPU inside the realisation
+            orders.append(None)
+            site_orders.append(None)
+            host_orders.append(None)
+            ii_list.append(ii)
+            continue
         if inline and k >= args.warmup and k != args.warmup:
             orders.append(None)  # drawn in the timed region (k == warmup: host copy kept below)
             host_orders.append(None)
@@ -407,6 +424,23 @@ def main():
         return note_solver(ctx, run_(k, ctx))
 
     def run_(k, ctx):
+        if devocc:  # occupancy drawn on the device (perc_occupy_random), then the path
+            kind = {"bond": P._lib.BOND, "site": P._lib.SITE, "sitebond": P._lib.SITEBOND}[args.kind]
+            rule = {"bond": P._lib.RULE_BOND, "site": P._lib.RULE_SITE,
+                    "sitebond": P._lib.RULE_MIXED}[args.kind]
+            cur = P._lib.CUR_FORTRAN if args.kind == "bond" else P._lib.CUR_MATLAB
+            t_0 = time.perf_counter()
+            ctx.occupy_random(kind, ts if args.kind != "bond" else 0, tb, int(seeds[ii_list[k]]))
+            li = ctx.label()
+            t_1 = time.perf_counter()
+            if li["nspan"] == 0:
+                return dict(gtop=0.0, gbot=0.0, iter=0, nspan=0, t_label_ms=(t_1 - t_0) * 1e3,
+                            t_solve_ms=0.0, t_total_ms=(t_1 - t_0) * 1e3)
+            c = ctx.conductance(rule, cur, tol=args.tol, itmax=args.itmax)
+            t_2 = time.perf_counter()
+            return dict(gtop=c["gtop"], gbot=c["gbot"], iter=c["iter"], nspan=li["nspan"],
+                        t_label_ms=(t_1 - t_0) * 1e3, t_solve_ms=c["t_solve_ms"],
+                        t_total_ms=(t_2 - t_0) * 1e3)
         if args.kind == "bond":
             return ctx.bondc_realisation(None, tb, tol=args.tol, itmax=args.itmax,
                                          device_ptr=orders[k].data_ptr())
@@ -573,10 +607,14 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f64",
-        "data": ("synthetic: %s occupation order of int(p*nb) bonds per realisation, seeds "
+        "data": ("synthetic: %s occupation of int(p*nb) bonds per realisation, seeds "
                  "tseed(ii) from master %d (bond_cond.f:65-70)"
-                 % ("uniform PCG64" if args.occupancy == "uniform"
-                    else "reference REAL*4 gfortran-rand Fisher-Yates", args.master)),
+                 % ({"device": "uniform, drawn on the GPU inside the timed realisation "
+                               "(perc_occupy_random: counter-based keys, radix select)",
+                     "uniform": "uniform PCG64 order drawn on the host before the timed region,"
+                                " resident in HBM",
+                     "reference": "reference REAL*4 gfortran-rand Fisher-Yates order"}
+                    [args.occupancy], args.master)),
         "config": {"workload": (
             "%s L=%d bond percolation p=%.2f, bondc semantics" % (args.lattice, L_, p)
             if args.kind == "bond" else
@@ -606,7 +644,7 @@ def main():
         "cg_iterations_mean": round(float(stats[4]) / max(nspan, 1), 1),
         "spanning_fraction": round(float(stats[3]) / max(nsolves, 1), 3),
         "host_order_ms_per_realisation": round(t_draw * 1e3 / max(nreal, 1), 1),
-        "orders_in_timed_region": bool(inline),
+        "orders_in_timed_region": bool(inline or devocc),
         "host_order_note": ("occupation orders are drawn on the host before the timed region "
                             "and kept in HBM; an ensemble that draws them inline pays this per "
                             "realisation on one host core unless it overlaps the GPU solve"),
@@ -618,6 +656,9 @@ def main():
         "kernel_probe": probe,
         "stream_copy": stream_copy,
     }
+    if rank == 0 and world == 1 and args.kind == "bond" and devocc:
+        out["pcie_inclusive"] = {"note": "occupancy drawn on the device: no host array crosses "
+                                         "PCIe per realisation"}
     if rank == 0 and world == 1 and args.kind == "bond" and host_orders[args.warmup] is not None:
         # the host-array boundary (perc_occupy with a host order) adds one
         # PCIe upload of the order per realisation; timed here outside the
@@ -646,11 +687,14 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.kind == "bond" and lat == 0:
         log("cpu baseline: oracle on a bounded sample ...")
         try:
-            out["cpu_baseline"] = cpu_baseline(L_, p, host_orders[args.warmup],
-                                               results[0]["iter"], args.cpu_iters)
+            ho = host_orders[args.warmup]
+            if devocc:  # the same occupancy, as the keys' order (host)
+                ho = np.ascontiguousarray(api.random_order(nb, tb, int(seeds[ii_list[args.warmup]])),
+                                          dtype=np.int32)
+            out["cpu_baseline"] = cpu_baseline(L_, p, ho, results[0]["iter"], args.cpu_iters)
         except Exception as e:  # keep the GPU line even if the host is short of memory
             out["cpu_baseline"] = {"value": None, "error": repr(e)}
-        if args.cpu_cores >= 0 and args.occupancy == "uniform":
+        if args.cpu_cores >= 0 and args.occupancy in ("uniform", "device"):
             try:
                 aff = len(os.sched_getaffinity(0))
             except AttributeError:
@@ -661,7 +705,7 @@ def main():
             ens_seeds = [int(seeds[(ii_list[args.warmup] + j) % len(seeds)]) for j in range(cores)]
             try:
                 out["cpu_baseline_ensemble"] = cpu_ensemble(L_, p, ens_seeds, iters_mean, nb, tb,
-                                                            args.cpu_iters, cores)
+                                                            args.cpu_iters, cores, args.occupancy)
             except Exception as e:
                 out["cpu_baseline_ensemble"] = {"value": None, "error": repr(e)}
     for c in ctxs:

@@ -106,6 +106,18 @@ typedef struct {
   int perccln;        /* reference label of the chosen component if known     */
 } perc_label_info;
 
+/* Occupation drawn on the device, with no order array (the metric
+   ensemble's inputs without a host draw or an upload): element id (1-based)
+   gets the key (hash32(seed, id) << 32) | id and the nsites / nbonds
+   smallest keys are occupied (a radix select, 8 passes of one key byte) --
+   the first nsites / nbonds of the permutation "ids in ascending key
+   order", a uniform random permutation up to the order of equal 32-bit
+   hashes.  Bonds use the key stream of mix64(seed ^ 0x5DEECE66D).  A host
+   replay (perc_label_numbers, several spanning clusters) regenerates the
+   order on the host; perc_random_order gives it to a caller. */
+int perc_occupy_random(perc_ctx *h, int kind, int nsites, int nbonds, unsigned long long seed);
+int perc_random_order(long long n, int count, unsigned long long seed, int kind, int *order_out);
+
 /* GPU connected components of the occupancy + spanning detection.  When
    more than one component spans, the reference's lowest-label rule is
    resolved by the host replay (hazard H4).  canon_out (optional, host,

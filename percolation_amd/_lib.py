@@ -93,6 +93,8 @@ SIGNATURES = {
     "perc_set_march_rows": (C.c_int, [_VP, C.c_int]),
     "perc_set_slabs": (C.c_int, [_VP, C.c_int]),
     "perc_cluster_sizes": (C.c_int, [_VP, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
+    "perc_occupy_random": (C.c_int, [_VP, C.c_int, C.c_int, C.c_int, C.c_ulonglong]),
+    "perc_random_order": (C.c_int, [C.c_longlong, C.c_int, C.c_ulonglong, C.c_int, _I]),
     "perc_set_march_mode": (C.c_int, [_VP, C.c_int]),
     "perc_march_info": (C.c_int, [_VP, _VP]),
     "perc_set_bond_weights": (C.c_int, [_VP, _VP, C.c_longlong]),

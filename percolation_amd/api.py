@@ -54,6 +54,15 @@ def shuffled_ids(N, seed):
     return order
 
 
+def random_order(n, count, seed, kind=L.BOND):
+    """The order perc_occupy_random's occupancy is the prefix of: the first
+    `count` ids (1-based) in ascending counter-based key order (host)."""
+    out = _i32(max(count, 1))
+    L.check(L.lib().perc_random_order(int(n), int(count), int(seed), int(kind), out),
+            "perc_random_order")
+    return out[:count]
+
+
 def trial_seeds(master, k=1000, scale=10000000):
     """tseed(1..k) = int(rand(0)*scale)+1 after srand(master): scale 1e7 in
     bond_cond.f:65-70, 1e6 in bond_perc.f / site_perc.f:70-74."""
@@ -120,6 +129,12 @@ class Context:
         bo = None if bond_order is None else np.ascontiguousarray(bond_order, dtype=np.int32)
         L.check(L.lib().perc_occupy(self.h, kind, nsites, L.ptr(so), nbonds_, L.ptr(bo)),
                 "perc_occupy")
+
+    def occupy_random(self, kind, nsites=0, nbonds_=0, seed=1):
+        """perc_occupy_random: the nsites / nbonds_ smallest counter-based
+        keys occupied, drawn on the device (no order array)."""
+        L.check(L.lib().perc_occupy_random(self.h, kind, int(nsites), int(nbonds_), int(seed)),
+                "perc_occupy_random")
 
     def occupy_device(self, kind, site_ptr=None, nsites=0, bond_ptr=None, nbonds_=0):
         """perc_occupy_device: order lists already in device memory (int

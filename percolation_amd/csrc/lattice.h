@@ -176,4 +176,21 @@ __host__ __device__ inline int forward_count(const Geom& g, int rn) {
   return c;
 }
 
+// Random occupation without an order array (perc_occupy_random): element id
+// (1-based) gets the key (hash32(seed, id) << 32) | id, unique per id; the
+// `count` elements with the smallest keys are occupied, i.e. the first
+// `count` of the permutation "ids in ascending key order" -- a uniform
+// random permutation up to the order of equal 32-bit hashes (by id).
+// Host and device compute the same keys (perc_random_order gives the order).
+__host__ __device__ inline unsigned long long perc_mix64(unsigned long long x) {
+  x += 0x9E3779B97F4A7C15ull;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+  return x ^ (x >> 31);
+}
+__host__ __device__ inline unsigned long long perc_rand_key(unsigned long long seed, unsigned id) {
+  const unsigned long long h = perc_mix64(perc_mix64(seed) ^ (unsigned long long)id);
+  return (h & 0xFFFFFFFF00000000ull) | (unsigned long long)id;
+}
+
 }  // namespace perc

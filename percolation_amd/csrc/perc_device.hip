@@ -232,6 +232,35 @@ __global__ void k_occupy(const int* order, int count, long long limit, uint8_t* 
   const int id = order[k];
   if (id > 0 && id <= limit) occ[id - 1] = 1;
 }
+// radix select of the `count`-th smallest key (perc_occupy_random): per pass
+// the 256-bin histogram of one key byte among the keys matching the prefix
+// found so far (LDS bins, one global atomic per bin and workgroup)
+__global__ __launch_bounds__(kBlock) void k_select_hist(long long n, unsigned long long seed,
+                                                         unsigned long long prefix,
+                                                         unsigned long long pmask, int shift,
+                                                         unsigned* hist) {
+  __shared__ unsigned s_h[256];
+  s_h[threadIdx.x] = 0;  // kBlock == 256
+  __syncthreads();
+  for (long long i = (long long)blockIdx.x * kBlock + threadIdx.x; i < n;
+       i += (long long)gridDim.x * kBlock) {
+    const unsigned long long key = perc_rand_key(seed, (unsigned)(i + 1));
+    if ((key & pmask) == prefix) atomicAdd(&s_h[(key >> shift) & 255u], 1u);
+  }
+  __syncthreads();
+  if (s_h[threadIdx.x]) atomicAdd(&hist[threadIdx.x], s_h[threadIdx.x]);
+}
+
+// occupy every id whose key is <= T (T = the count-th smallest key);
+// occ[id - 1 + base] (bonds: base 0, 0-based; sites: base 1, socc[id])
+__global__ __launch_bounds__(kBlock) void k_occupy_rand(long long n, unsigned long long seed,
+                                                         unsigned long long T, int base,
+                                                         uint8_t* occ) {
+  const long long i = (long long)blockIdx.x * kBlock + threadIdx.x;
+  if (i >= n) return;
+  occ[i + base] = perc_rand_key(seed, (unsigned)(i + 1)) <= T ? 1 : 0;
+}
+
 __global__ void k_occupy_sites(const int* order, int count, int t, uint8_t* socc) {
   const int k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= count) return;
@@ -3511,7 +3540,8 @@ void dev_free_all(perc_ctx* h) {
   void* ptrs[] = {d.bond_first, d.rowptr, d.col, d.val, d.diag, d.rhs, d.code, d.dtab, d.sflag, d.bocc, d.socc,
                   d.order, d.parent, d.member, d.top, d.counters, d.x, d.r,
                   d.p0, d.p1, d.q, d.partials, d.tickets, d.scal, d.err_hist, d.iout,
-                  d.res_xch, d.res_part, d.res_bar, d.bw, d.code_sm, d.csize, d.res_gran};
+                  d.res_xch, d.res_part, d.res_bar, d.bw, d.code_sm, d.csize, d.res_gran,
+                  d.sel_hist};
   for (void* p : ptrs)
     if (p) hipFree(p);
   d = DeviceBuffers{};
@@ -3543,6 +3573,55 @@ hipError_t dev_occupy(perc_ctx* h, int kind, int nsites, const int* site_order, 
     k_occupy<<<blocks_for(nbonds), kBlock, 0, st>>>(src, nbonds, h->nb, d.bocc);
     HIP_TRY(hipGetLastError());
   }
+  return hipSuccess;
+}
+
+// the count smallest keys of ids 1..n occupied (radix select, 8 passes of
+// one key byte; the histogram goes to the host each pass: 256 counters)
+static hipError_t occupy_rand_one(perc_ctx* h, long long n, long long count,
+                                  unsigned long long seed, int base, uint8_t* occ) {
+  hipStream_t st = h->stream;
+  if (count <= 0) return hipSuccess;  // occ is zeroed by the caller
+  const int G = (int)std::min<long long>(cdiv(n, kBlock), 2048);
+  unsigned long long T = ~0ull;
+  if (count < n) {
+    if (!h->d.sel_hist) HIP_TRY(dmalloc(&h->d.sel_hist, 256));
+    unsigned* d_hist = h->d.sel_hist;
+    unsigned hist[256];
+    unsigned long long prefix = 0, mask = 0;
+    long long need = count;
+    for (int pass = 0; pass < 8; ++pass) {
+      const int shift = 56 - 8 * pass;
+      HIP_TRY(hipMemsetAsync(d_hist, 0, sizeof(hist), st));
+      k_select_hist<<<G, kBlock, 0, st>>>(n, seed, prefix, mask, shift, d_hist);
+      HIP_TRY(dbg_sync(st, "k_select_hist"));
+      HIP_TRY(hipMemcpyAsync(hist, d_hist, sizeof(hist), hipMemcpyDeviceToHost, st));
+      HIP_TRY(hipStreamSynchronize(st));
+      long long cum = 0;
+      int b = 0;
+      for (; b < 255; ++b) {
+        if (cum + hist[b] >= need) break;
+        cum += hist[b];
+      }
+      need -= cum;
+      prefix |= (unsigned long long)b << shift;
+      mask |= 0xFFull << shift;
+    }
+    T = prefix;
+  }
+  k_occupy_rand<<<cdiv(n, kBlock), kBlock, 0, st>>>(n, seed, T, base, occ);
+  return hipGetLastError();
+}
+
+hipError_t dev_occupy_random(perc_ctx* h, int kind, int nsites, int nbonds,
+                             unsigned long long seed) {
+  hipStream_t st = h->stream;
+  DeviceBuffers& d = h->d;
+  HIP_TRY(hipMemsetAsync(d.bocc, 0, (size_t)h->nb + 8, st));
+  HIP_TRY(hipMemsetAsync(d.socc, 0, h->g.t + 8, st));
+  if (kind != PERC_BOND) HIP_TRY(occupy_rand_one(h, h->g.t, nsites, seed, 1, d.socc));
+  if (kind != PERC_SITE)
+    HIP_TRY(occupy_rand_one(h, h->nb, nbonds, perc_mix64(seed ^ 0x5DEECE66Dull), 0, d.bocc));
   return hipSuccess;
 }
 

@@ -282,6 +282,7 @@ static int occupy_impl(perc_ctx* h, int kind, int nsites, const int* site_order,
   L.kind = kind;
   L.sites.clear();
   L.bonds.clear();
+  L.random = false;
   L.d_sites = on_device ? site_order : nullptr;
   L.d_bonds = on_device ? bond_order : nullptr;
   L.n_sites = nsites;
@@ -299,10 +300,61 @@ static int occupy_impl(perc_ctx* h, int kind, int nsites, const int* site_order,
   return PERC_OK;
 }
 
+// the first `count` ids of the permutation "ids 1..n in ascending
+// perc_rand_key(seed, id) order" (the occupancy perc_occupy_random selects)
+static void random_order(long long n, long long count, unsigned long long seed, int* out) {
+  std::vector<unsigned long long> keys((size_t)n);
+  for (long long i = 0; i < n; ++i) keys[(size_t)i] = perc_rand_key(seed, (unsigned)(i + 1));
+  if (count < n) std::nth_element(keys.begin(), keys.begin() + count, keys.end());
+  std::sort(keys.begin(), keys.begin() + count);
+  for (long long i = 0; i < count; ++i) out[i] = (int)(keys[(size_t)i] & 0xFFFFFFFFull);
+}
+
+int perc_random_order(long long n, int count, unsigned long long seed, int kind, int* order_out) {
+  if (n <= 0 || n > 0x7FFFFFFFll || count < 0 || count > n || (count && !order_out) ||
+      (kind != PERC_BOND && kind != PERC_SITE))
+    return PERC_EINVAL;
+  random_order(n, count, kind == PERC_BOND ? perc_mix64(seed ^ 0x5DEECE66Dull) : seed, order_out);
+  return PERC_OK;
+}
+
+int perc_occupy_random(perc_ctx* h, int kind, int nsites, int nbonds, unsigned long long seed) {
+  if (!h || kind < PERC_BOND || kind > PERC_SITEBOND) return PERC_EINVAL;
+  if (kind == PERC_SITE) nbonds = 0;
+  if (kind == PERC_BOND) nsites = 0;
+  if (nbonds < 0 || nbonds > h->nb || nsites < 0 || nsites > h->g.t) return PERC_EINVAL;
+  hipSetDevice(h->device);
+  ReplayOrder& L = h->last;
+  L.kind = kind;
+  L.sites.clear();
+  L.bonds.clear();
+  L.d_sites = L.d_bonds = nullptr;
+  L.n_sites = nsites;
+  L.n_bonds = nbonds;
+  L.host_valid = false;
+  L.random = true;
+  L.seed = seed;
+  hipError_t e = dev_occupy_random(h, kind, nsites, nbonds, seed);
+  if (e != hipSuccess) return hip_status(e, "perc_occupy_random");
+  h->occupied = true;
+  h->labeled = false;
+  h->assembled = false;
+  return PERC_OK;
+}
+
 // host copies of a device-resident occupancy, fetched only for a replay
+// (random occupancies: the order regenerated from the keys on the host)
 static int ensure_host_order(perc_ctx* h) {
   ReplayOrder& L = h->last;
   if (L.host_valid) return PERC_OK;
+  if (L.random) {
+    L.sites.resize(L.n_sites);
+    L.bonds.resize(L.n_bonds);
+    if (L.n_sites) random_order(h->g.t, L.n_sites, L.seed, L.sites.data());
+    if (L.n_bonds) random_order(h->nb, L.n_bonds, perc_mix64(L.seed ^ 0x5DEECE66Dull), L.bonds.data());
+    L.host_valid = true;
+    return PERC_OK;
+  }
   L.sites.resize(L.n_sites);
   L.bonds.resize(L.n_bonds);
   hipError_t e = hipSuccess;

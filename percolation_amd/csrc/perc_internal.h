@@ -89,6 +89,7 @@ struct DeviceBuffers {
   uint8_t* top = nullptr;    // t+1 (spanning-root flags, m+1 used)
   int* counters = nullptr;   // [0]=nspan [1]=nclusters [2]=span_sites [3]=max size, then list
   int* csize = nullptr;      // t+2 per-root cluster sizes (perc_cluster_sizes)
+  unsigned* sel_hist = nullptr;  // 256-bin histogram of perc_occupy_random's select
   // CG
   double* x = nullptr;
   double* r = nullptr;
@@ -118,6 +119,10 @@ struct ReplayOrder {
   const int* d_bonds = nullptr;
   int n_sites = 0, n_bonds = 0;
   bool host_valid = true;
+  // perc_occupy_random: no order array; the host order (ascending keys) is
+  // generated only if a replay needs it
+  bool random = false;
+  unsigned long long seed = 0;
 };
 
 struct KernelTiming {
@@ -190,6 +195,7 @@ void dev_free_all(perc_ctx* h);
 hipError_t dev_occupy(perc_ctx* h, int kind, int nsites, const int* site_order, int nbonds,
                       const int* bond_order, bool device_src);
 hipError_t dev_label(perc_ctx* h, int* nspan, int* span_list, int* nclusters);
+hipError_t dev_occupy_random(perc_ctx* h, int kind, int nsites, int nbonds, unsigned long long seed);
 hipError_t dev_span_sites(perc_ctx* h, int root, int* count);
 hipError_t dev_canon(perc_ctx* h, int* canon_out);
 hipError_t dev_cluster_sizes(perc_ctx* h, int kind, int root, int* maxcs, int* rootsize);

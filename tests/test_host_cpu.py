@@ -255,3 +255,22 @@ def test_degenerate_lattice_is_rejected():
     for m, n in [(2, 3), (3, 2), (1, 1)]:
         with pytest.raises(P.PercError, match="PERC_EINVAL"):
             api.Context(0, m, n, 0)
+
+
+def test_random_order_is_a_keyed_permutation():
+    """perc_random_order (the order perc_occupy_random's occupancy is a
+    prefix of): a permutation of 1..n, every prefix the prefix of the full
+    order, deterministic in the seed, the bond stream distinct from the site
+    stream, and roughly uniform (prefix means)."""
+    import numpy as np
+    from percolation_amd import _lib as PL
+    n = 5000
+    full = api.random_order(n, n, 7)
+    assert sorted(full.tolist()) == list(range(1, n + 1))
+    for c in (0, 1, 17, 2500, n):
+        assert np.array_equal(api.random_order(n, c, 7), full[:c])
+    assert np.array_equal(api.random_order(n, n, 7), full)
+    assert not np.array_equal(api.random_order(n, 100, 8), full[:100])
+    assert not np.array_equal(api.random_order(n, 100, 7, PL.SITE), full[:100])
+    means = [api.random_order(n, 1000, s_).mean() for s_ in range(20)]
+    assert abs(np.mean(means) - (n + 1) / 2) < 0.05 * n

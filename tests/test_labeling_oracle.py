@@ -206,3 +206,37 @@ def test_config5_mixed_8192_partition_vs_oracle(ps, pb):
     ts, tb = int(ps * t), int(pb * nb)
     li = gpu_label(lat, m, n, pbc, PL.SITEBOND, sids=sids, ts=ts, bids=bids, tb=tb)
     check(li, *oracle_mixed(lat, m, n, pbc, sids, ts, bids, tb))
+
+
+# ------------------------------------------------------------ GPU: device-drawn occupancy
+@pytest.mark.gpu
+@pytest.mark.parametrize("lat,m,n,pbc", [(0, 200, 70, 0), (1, 130, 90, 1), (0, 512, 512, 0)])
+@pytest.mark.parametrize("kind", [PL.BOND, PL.SITE, PL.SITEBOND])
+def test_occupy_random_equals_its_host_order(lat, m, n, pbc, kind):
+    """perc_occupy_random (keys + radix select on the GPU) occupies exactly
+    the prefix of perc_random_order (host): same partition as occupying that
+    order explicitly, the same reference label numbers by replay (the host
+    regenerates the order), and against the oracle's replay."""
+    t, nb = m * n, api.nbonds(lat, m, n, pbc)
+    ts, tb = int(0.62 * t), int(0.55 * nb)
+    seed = 1234567 + m
+    so = api.random_order(t, ts, seed, PL.SITE) if kind != PL.BOND else None
+    bo = api.random_order(nb, tb, seed, PL.BOND) if kind != PL.SITE else None
+    with api.Context(lat, m, n, pbc) as ctx:
+        ctx.occupy_random(kind, ts if kind != PL.BOND else 0, tb if kind != PL.SITE else 0, seed)
+        lr = ctx.label(canon=True)
+        nr = ctx.label_numbers(kind)
+        ctx.occupy(kind, site_order=so, nsites=ts if so is not None else 0, bond_order=bo,
+                   nbonds_=tb if bo is not None else 0)
+        le = ctx.label(canon=True)
+        ne = ctx.label_numbers(kind)
+    assert np.array_equal(lr["canon"], le["canon"])
+    assert lr["nspan"] == le["nspan"] and lr["span_root"] == le["span_root"]
+    for key in ("bond_label", "site_label"):
+        if nr[key] is not None:
+            assert np.array_equal(nr[key], ne[key])
+    assert nr["perccln"] == ne["perccln"] and nr["maxcs"] == ne["maxcs"]
+    if kind == PL.BOND:
+        check(lr, *oracle_bond(lat, m, n, pbc, bo, tb))
+    elif kind == PL.SITE:
+        check(lr, *oracle_site(lat, m, n, pbc, so, ts))
