@@ -196,12 +196,12 @@ def kernel_label(key, minfo):
 
 # rocprof kernel names of the CG kernels, per operator format
 ROCPROF_NAMES = {("res", "stencil"): ("k_cg_res",),  # default kernel of each role first
-                 ("pm", "stencil"): ("k_cg_march<0", "k_cg_march<1", "k_cg_rm<0", "k_cg_rm<1"),
+                 ("pm", "stencil"): ("k_cg_march<1", "k_cg_march<0", "k_cg_rm<0", "k_cg_rm<1"),
                  ("ps", "stencil_tiled"): ("k_cg_ps<4>", "k_cg_ps<6>"),
                  ("resid", "stencil_tiled"): ("k_cg_b<true>",),
                  ("spmv", "stencil_split"): ("k_cg_spmv<4>", "k_cg_spmv<6>"),
                  ("resid", "stencil_split"): ("k_cg_b<true>",),
-                 ("resid", "stencil"): ("k_cg_b<true>", "k_cg_rm<2", "k_cg_march<2"),
+                 ("resid", "stencil"): ("k_cg_march<2", "k_cg_b<true>", "k_cg_rm<2"),
                  ("xp", "stencil_split"): ("k_cg_p<true>",),
                  ("spmv", "stencil"): ("k_cg_spmv<4>", "k_cg_spmv<6>"),
                  ("spmv", "csr"): ("k_cg_spmv<0>",),
@@ -214,7 +214,24 @@ def base_name(k):
     return k.split(",")[0].rstrip(">")
 
 
-def pmc_traffic(key, fmt, L_):
+def rocprof_base(key, fmt, minfo):
+    """base name (kernel + first template argument, as base_name gives it) of
+    the CG kernel of role `key` that the solve ran"""
+    if fmt == "stencil" and minfo.get("kernel") in ("wave", "rows") and key in ("pm", "resid"):
+        k = "k_cg_rm" if minfo["kernel"] == "rows" else "k_cg_march"
+        if key == "pm":
+            return "%s<%d" % (k, 1 if minfo.get("qfree") else 0)
+        return "%s<2" % k if minfo.get("qfree") else "k_cg_b<true"
+    names = ROCPROF_NAMES.get((key, fmt), ())
+    return base_name(names[0]) if names else None
+
+
+# reconcile summaries before r2_17 name kernels without template arguments;
+# the kernels they measured
+OLD_RECONCILE = {"k_cg_march": "k_cg_march<0", "k_cg_b": "k_cg_b<true"}
+
+
+def pmc_traffic(base, L_):
     """HBM bytes per launch of a CG kernel from the committed rocprofv3 PMC
     summaries.  Preferred: profiles/*_pmc_reconcile_L<L>.csv
     (tools/pmc_r2.sh + tools/pmc_reconcile.py): one fixed dispatch set of
@@ -234,14 +251,11 @@ def pmc_traffic(key, fmt, L_):
                                             for t in re.split(r"(\d+)", os.path.basename(f))],
                       reverse=True)
 
-    names = ROCPROF_NAMES.get((key, fmt), ())
-    # the reconcile rows name kernels without template arguments: the role's
-    # default kernel (first name) only
-    base = base_name(names[0]).split("<")[0] if names else None
     for f in newest_first("*_pmc_reconcile_L%d.csv" % L_):
         with open(f) as fh:
             for r in csv.DictReader(fh):
-                if r["kernel"] == base and r["read_bytes"] and r["write_bytes"]:
+                if OLD_RECONCILE.get(r["kernel"], r["kernel"]) == base and r["read_bytes"] \
+                        and r["write_bytes"]:
                     return float(r["read_bytes"]) + float(r["write_bytes"]), [os.path.relpath(f, REPO)]
     tot, src = 0.0, []
     for kind, ctr in (("fetch", "FETCH_SIZE"), ("write", "WRITE_SIZE")):
@@ -249,7 +263,7 @@ def pmc_traffic(key, fmt, L_):
         for f in newest_first("*_pmc_%s_L%d.csv" % (kind, L_)):
             with open(f) as fh:
                 for r in csv.DictReader(fh):
-                    if base_name(r["kernel"]) in map(base_name, names) and r["counter"] == ctr:
+                    if base_name(r["kernel"]) == base and r["counter"] == ctr:
                         got = float(r["bytes_per_dispatch"])
             if got is not None:
                 src.append(os.path.relpath(f, REPO))
@@ -531,9 +545,7 @@ def main():
         assembled = False
     if "fmt" in seen:  # what the spanning realisations ran (labels + bytes below)
         fmt, minfo = fmt_names[seen["fmt"]], seen["minfo"]
-    mode_bits = args.march_mode if args.march_mode >= 0 else P.MARCH_DEFAULT
-    minfo["strips"] = bool(mode_bits & P._lib.MARCH_STRIPS) and not minfo.get("qfree") and \
-        minfo.get("kernel") == "wave" and N * 8 <= (256 << 20) and args.slabs <= 1
+    minfo["strips"] = bool(minfo.get("strips")) and args.slabs <= 1
 
     def kernel_set(f, probe=False):
         """(key, stats key, perc_bench_kernel id, bytes) of the CG kernels of
@@ -552,6 +564,10 @@ def main():
                 # x += ak p(k) (reads x and p(k), writes x: 24 B per x row)
                 xb = 24 * N if full else 24 * 2 * L_
                 return [("pm", "spmv", 1, 34 * N), ("resid", "resid", 2, resid_bytes(N, f) + xb)]
+            if qf and minfo.get("strips"):
+                # strip-major q-free march: x += ak p(k) in the march B
+                xb = 24 * N if full else 24 * 2 * L_
+                return [("pm", "spmv", 1, 26 * N), ("resid", "resid", 2, resid_bytes(N, f) + xb)]
             return [("pm" if f == "stencil" else "ps", "spmv", 1, ps_bytes(N, L_, full, qf)),
                     ("resid", "resid", 2, resid_bytes(N, f))]
         return [("spmv", "spmv", 1, spmv_bytes(N, nnz, f)), ("resid", "resid", 2, resid_bytes(N, f)),
@@ -570,7 +586,7 @@ def main():
                      "gbs": round(nbytes / (avg * 1e-3) / 1e9, 1) if avg > 0 else None}
     # the roofline line is the kernel with the most device time
     dom = max(kern, key=lambda k_: kern[k_]["total_ms"])
-    traffic, traffic_src = pmc_traffic(dom, fmt, L_)
+    traffic, traffic_src = pmc_traffic(rocprof_base(dom, fmt, minfo), L_)
     achieved = kern[dom]["gbs"] or 0.0  # 0: no realisation spanned, nothing solved
     iter_ms = sum(v["avg_launch_ms"] for v in kern.values())
     iter_bytes = sum(v["bytes_per_launch"] for v in kern.values())
@@ -645,9 +661,13 @@ def main():
         "spanning_fraction": round(float(stats[3]) / max(nsolves, 1), 3),
         "host_order_ms_per_realisation": round(t_draw * 1e3 / max(nreal, 1), 1),
         "orders_in_timed_region": bool(inline or devocc),
-        "host_order_note": ("occupation orders are drawn on the host before the timed region "
-                            "and kept in HBM; an ensemble that draws them inline pays this per "
-                            "realisation on one host core unless it overlaps the GPU solve"),
+        "host_order_note": (
+            "occupancy drawn on the GPU inside each timed realisation (no host order)" if devocc
+            else "orders drawn on a host thread inside the timed region, overlapping the "
+                 "previous realisation's solve" if inline
+            else "occupation orders are drawn on the host before the timed region and kept in "
+                 "HBM; an ensemble that draws them inline pays this per realisation on one host "
+                 "core unless it overlaps the GPU solve"),
         "gtop_mean": float(stats[1]) / max(nsolves, 1),
         "cg_iteration": {"ms": round(iter_ms, 5), "bytes": iter_bytes,
                          "gbs": round(iter_bytes / (iter_ms * 1e-3) / 1e9, 1) if iter_ms > 0

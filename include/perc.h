@@ -292,15 +292,18 @@ int perc_set_march_rows(perc_ctx *h, int rows);
    wave of the per-wave march walks one contiguous stream; x stays
    row-major.  In the default since round 2: with every memory instruction
    of the march unconditional (no waitcnt drain per step) the strip-major
-   march runs 0.107 vs 0.115 ms row-major at L = 4096 (same box), the
-   solve 0.253 vs 0.238 solves/s.  Used when the vectors stay below 2 GB
-   (L < 16384); larger lattices solve row-major. */
+   march runs 0.107 vs 0.115 ms row-major at L = 4096 (same box).  Used
+   while one vector fits the 256 MB Infinity Cache (L <= 4096); larger
+   lattices solve row-major.  PERC_MARCH_QFREE is in the default since
+   late round 2 (strip-major: 0.164 vs 0.178 ms per iteration at L = 4096;
+   row-major at L = 8192: 0.721 vs 0.737 ms).  Row slabs (perc_set_slabs)
+   always run the row-major q-storing march. */
 #define PERC_MARCH_QFREE 1
 #define PERC_MARCH_ALT 2
 #define PERC_MARCH_ROWS 4
 #define PERC_SOLVE_RESIDENT 8
 #define PERC_MARCH_STRIPS 16
-#define PERC_MARCH_DEFAULT (PERC_MARCH_ALT | PERC_SOLVE_RESIDENT | PERC_MARCH_STRIPS)
+#define PERC_MARCH_DEFAULT (PERC_MARCH_QFREE | PERC_MARCH_ALT | PERC_SOLVE_RESIDENT | PERC_MARCH_STRIPS)
 int perc_set_march_mode(perc_ctx *h, int mode);
 /* Random bond conductances (MATLAB/ConductCalc.m condtype 2, :38-47 and
    :94-97): the bonds of the spanning cluster get G = -g0 * w[id] instead of
@@ -312,9 +315,9 @@ int perc_set_bond_weights(perc_ctx *h, const double *w, long long n);
 /* Solver loop of the assembled system: out5[0] = 0 (no march kernel: LDS
    tiles, split or CSR), 1 (per-wave march k_cg_march), 2 (workgroup
    row-march k_cg_rm), 3 (resident persistent solve k_cg_res), 4 (one-
-   workgroup solve of a small system, k_cg_small: N <= 12288 under
-   PERC_FMT_AUTO with PERC_SOLVE_RESIDENT set); out5[1] =
-   q-free B, out5[2] = alternating
+   workgroup solve of a small system, k_cg_small: N <= 8192 under
+   PERC_FMT_AUTO with PERC_SOLVE_RESIDENT set); out5[1] = bit 0: q-free
+   B, bit 1: strip-major solve layout; out5[2] = alternating
    directions, out5[3] = band height, out5[4] = strip width (columns). */
 int perc_march_info(perc_ctx *h, int *out5);
 

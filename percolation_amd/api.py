@@ -252,7 +252,8 @@ class Context:
         """The solver loop of the assembled system (perc_march_info)."""
         out = np.zeros(5, dtype=np.int32)
         L.check(L.lib().perc_march_info(self.h, out.ctypes.data), "perc_march_info")
-        return dict(kernel=("none", "wave", "rows", "resident", "small")[out[0]], qfree=bool(out[1]),
+        return dict(kernel=("none", "wave", "rows", "resident", "small")[out[0]],
+                    qfree=bool(out[1] & 1), strips=bool(out[1] & 2),
                     alt=bool(out[2]), band_rows=int(out[3]), strip_cols=int(out[4]))
 
     def matrix_format(self):

@@ -2083,6 +2083,21 @@ __global__ __launch_bounds__(64 * kMarchWaves, (kMarchWavesPerEU<MODE, D>)) void
     double* s_w = s_win[threadIdx.x >> 6];
     if (up) march_walk<MODE, D, true, SM>(a, g, B, ring, first, bk, ak, psrc, pnew, s_dt, s_rpos, s_rmap, s_w, acc);
     else march_walk<MODE, D, false, SM>(a, g, B, ring, first, bk, ak, psrc, pnew, s_dt, s_rpos, s_rmap, s_w, acc);
+    if (MODE == kMarchB && SM) {
+      // strip-major q-free solve: x (row-major) += ak p(k) on the band's x
+      // rows, after the walk (loads and stores inside it would put a
+      // vmcnt(0) in every step); k_cg_b's x update of the q-storing solve
+      const int N = a.St.N;
+      for (int gr = g.r0; gr < g.rend; ++gr) {
+        const int i = gr * m + g.col;  // m is a multiple of the strip width
+        if (a.xrows != 0 && i >= a.xrows && i < N - a.xrows) continue;
+        const double2 pv = *reinterpret_cast<const double2*>(psrc + sm_at(a.T, gr, g.col));
+        double2 xv = *reinterpret_cast<const double2*>(a.x + i);
+        xv.x = xv.x + ak * pv.x;
+        xv.y = xv.y + ak * pv.y;
+        *reinterpret_cast<double2*>(a.x + i) = xv;
+      }
+    }
   }
   if (MODE != kMarchB) {
     double v[1] = {acc[0]}, tot[1];
@@ -3266,7 +3281,9 @@ void launch_cg_spmv(perc_ctx* h, const CGArgs& a, int G) {
       return;
     }
     if (h->march) {
-      if (h->qfree) klaunch(h, k_cg_march<kMarchP>, h->march_grid, 64 * kMarchWaves, st, a);
+      if (h->qfree && a.sm && h->march_depth == 2) klaunch(h, k_cg_march<kMarchP, true, 2>, h->march_grid, 64 * kMarchWaves, st, a);
+      else if (h->qfree && a.sm) klaunch(h, k_cg_march<kMarchP, true, 3>, h->march_grid, 64 * kMarchWaves, st, a);
+      else if (h->qfree) klaunch(h, k_cg_march<kMarchP>, h->march_grid, 64 * kMarchWaves, st, a);
       else if (a.sm && h->march_depth == 2) klaunch(h, k_cg_march<kMarchPQ, true, 2>, h->march_grid, 64 * kMarchWaves, st, a);
       else if (a.sm && h->march_depth == 4) klaunch(h, k_cg_march<kMarchPQ, true, 4>, h->march_grid, 64 * kMarchWaves, st, a);
       else if (a.sm) klaunch(h, k_cg_march<kMarchPQ, true, 3>, h->march_grid, 64 * kMarchWaves, st, a);
@@ -3298,7 +3315,9 @@ void launch_cg_b(perc_ctx* h, const CGArgs& a, int G) {
     else if (h->rm_w == 1024) klaunch(h, k_cg_rm<kMarchB, 1024>, g, b, h->stream, a);
     else klaunch(h, k_cg_rm<kMarchB, 512>, g, b, h->stream, a);
   } else if (h->march && h->qfree) {
-    klaunch(h, k_cg_march<kMarchB>, h->march_grid, 64 * kMarchWaves, h->stream, a);
+    if (a.sm && h->march_depth == 2) klaunch(h, k_cg_march<kMarchB, true, 2>, h->march_grid, 64 * kMarchWaves, h->stream, a);
+    else if (a.sm) klaunch(h, k_cg_march<kMarchB, true, 3>, h->march_grid, 64 * kMarchWaves, h->stream, a);
+    else klaunch(h, k_cg_march<kMarchB>, h->march_grid, 64 * kMarchWaves, h->stream, a);
   } else if (h->stencil) {
     // x on every row with the march's x-in-B (fused, row-major): XF
     if (a.bx && a.xrows == 0 && !a.sm) klaunch(h, k_cg_b<true, true>, G, kBlock, h->stream, a);
@@ -3803,7 +3822,7 @@ void select_format(perc_ctx* h) {
   // past it (16-row bands, several rounds of waves) the row-major march is
   // faster (L = 8192: 0.439 vs 0.480 ms, profiles/r2_11_ab_strips.log); the
   // strip-major march's whole-array buffer views also need < 2 GB
-  h->strips = h->march && !h->qfree && (h->march_mode & PERC_MARCH_STRIPS) &&
+  h->strips = h->march && (h->march_mode & PERC_MARCH_STRIPS) &&
               (size_t)h->N * sizeof(double) <= kLargeVector;
 }
 
@@ -3821,6 +3840,7 @@ hipError_t to_strips(perc_ctx* h, CGArgs& a) {
   a.q = d.r;
   a.St.code = d.code_sm;
   a.sm = 1;
+  a.bx = 1;  // x (row-major) is updated in B: k_cg_b, or the q-free march B
   return hipSuccess;
 }
 
@@ -4119,8 +4139,9 @@ hipError_t dev_solve_slabs(perc_ctx* h, int K, int itol, double tol, int itmax, 
   DeviceBuffers& d = h->d;
   hipStream_t st = h->stream;
   const int m = h->g.m, nrows = h->g.n - 2;
-  // (the slabs run the row-major march: PERC_MARCH_STRIPS does not apply)
-  if (!h->march || h->qfree || K < 1 || K > nrows) return hipErrorInvalidValue;
+  // (the slabs run the row-major q-storing march + streaming B:
+  // PERC_MARCH_STRIPS and PERC_MARCH_QFREE do not apply)
+  if (!h->march || K < 1 || K > nrows) return hipErrorInvalidValue;
   int cus = 0;
   HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, h->device));
   const int spr = m / kMarchW;

@@ -543,7 +543,8 @@ def test_large_vector_grids_8192():
 MARCH_MODES = (PL.MARCH_DEFAULT, 0, PL.MARCH_QFREE, PL.MARCH_ALT, PL.MARCH_ROWS,
                PL.MARCH_ROWS | PL.MARCH_QFREE, PL.MARCH_ROWS | PL.MARCH_ALT,
                PL.MARCH_ROWS | PL.MARCH_QFREE | PL.MARCH_ALT, PL.MARCH_STRIPS,
-               PL.MARCH_STRIPS | PL.MARCH_QFREE, PL.MARCH_STRIPS | PL.MARCH_ALT)
+               PL.MARCH_STRIPS | PL.MARCH_QFREE, PL.MARCH_STRIPS | PL.MARCH_ALT,
+               PL.MARCH_STRIPS | PL.MARCH_QFREE | PL.MARCH_ALT)
 
 
 @pytest.mark.parametrize("lat,m,n,pbc,p", [(0, 256, 150, 0, 0.6), (1, 128, 99, 1, 0.42),
@@ -605,6 +606,9 @@ def test_march_modes_one_iteration_bitwise(lat, m, n, pbc, p):
             assert c["iter"] == ref["iter"]
             assert np.max(np.abs(c["vint"] - ref["vint"])) <= 1e-13 * np.max(np.abs(ref["vint"]))
             assert rel(c["err"], ref["err"]) < 1e-12
+            # x on the electrode rows only (the default): bitwise the same there
+            part = ctx.conductance(tol=1e-30, itmax=3)
+            assert part["gtop"] == c["gtop"] and part["gbot"] == c["gbot"], mode
 
 
 def test_table_division_is_ieee_division():

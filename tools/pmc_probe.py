@@ -25,6 +25,7 @@ def main():
     ap.add_argument("--p", type=float, default=0.6)
     ap.add_argument("--reps", type=int, default=64)
     ap.add_argument("--copies", type=int, default=16)
+    ap.add_argument("--march-mode", type=int, default=-1, help="perc_set_march_mode bits; -1: default")
     args = ap.parse_args()
     import torch
     from percolation_amd import api
@@ -34,6 +35,8 @@ def main():
     o = (np.random.default_rng(1234).permutation(nb)[:tb] + 1).astype(np.int32)
     dev_o = torch.from_numpy(o).cuda()
     with api.Context(0, L_, L_, 0) as ctx:
+        if args.march_mode >= 0:
+            ctx.set_march_mode(args.march_mode)
         r = ctx.bondc_realisation(None, tb, tol=1e-8, itmax=20, device_ptr=dev_o.data_ptr())
         it_ms = ctx.bench_kernel(5, args.reps)
         cp_ms = ctx.bench_kernel(4, args.copies)

@@ -1,6 +1,9 @@
 #!/usr/bin/env bash
 # PMC passes over one fixed dispatch set (tools/pmc_probe.py), one counter
 # group per run, then tools/pmc_reconcile.py.  Stops at the first failure.
+# (The default solve runs the q-free strip-major march: k_cg_march<1> P+S,
+# k_cg_march<2> B; MODE=26 in the env probes the q-storing march + k_cg_b.)
+MODE=${MODE:--1}
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
 mkdir -p gpurun_out
 export TMPDIR=/tmp
@@ -13,11 +16,13 @@ for ctrs in "TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum 
   i=$((i + 1))
   echo "== pass $i: $ctrs" >> gpurun_out/pmc_r2.log
   timeout -s KILL 120 rocprofv3 --pmc $ctrs --kernel-include-regex "k_cg_march|k_cg_b|k_copy" \
-    -f csv -d gpurun_out/pmc_r2/p$i -o run -- python3 tools/pmc_probe.py --L $L \
+    -f csv -d gpurun_out/pmc_r2/p$i -o run -- python3 tools/pmc_probe.py --L $L --march-mode $MODE \
     >> gpurun_out/pmc_r2.log 2>&1 || { echo "pass $i failed rc=$?" >> gpurun_out/pmc_r2.log; exit 1; }
 done
 python3 tools/pmc_reconcile.py gpurun_out/pmc_r2_reconcile_L$L.csv gpurun_out/pmc_r2/p* \
-  --last k_cg_march=64 k_cg_b=64 k_copy=16 \
-  --algo k_cg_march=$((18 * (L * L - 2 * L))):$((16 * (L * L - 2 * L))) \
-         k_cg_b=$((18 * (L * L - 2 * L))):$((8 * (L * L - 2 * L) + 32 * L)) \
+  --last "k_cg_march<1=64" "k_cg_march<2=64" "k_cg_march<0=64" "k_cg_b<true=64" k_copy=16 \
+  --algo "k_cg_march<1=$((18 * (L * L - 2 * L))):$((8 * (L * L - 2 * L)))" \
+         "k_cg_march<2=$((18 * (L * L - 2 * L) + 32 * L)):$((8 * (L * L - 2 * L) + 16 * L))" \
+         "k_cg_march<0=$((18 * (L * L - 2 * L))):$((16 * (L * L - 2 * L)))" \
+         "k_cg_b<true=$((18 * (L * L - 2 * L) + 32 * L)):$((8 * (L * L - 2 * L) + 16 * L))" \
          k_copy=536870912:536870912 >> gpurun_out/pmc_r2.log 2>&1

@@ -9,8 +9,9 @@ requests: exact, no FETCH_SIZE halving question), write bytes from
 WRITE_SIZE; the STREAM copy (512 MB read + 512 MB written per dispatch)
 calibrates both.
 
-  python tools/pmc_reconcile.py OUT.csv --last k_cg_march=64 k_cg_b=64 k_copy=16 \
-      --algo k_cg_march=R:W k_cg_b=R:W k_copy=R:W  DIR [DIR ...]
+  python tools/pmc_reconcile.py OUT.csv --last "k_cg_march<1=64" k_copy=16 \
+      --algo "k_cg_march<1=R:W" k_copy=R:W  DIR [DIR ...]
+  (kernels are named with their first template argument)
 """
 import argparse
 import csv
@@ -35,7 +36,8 @@ def load(d):
     rows = list(csv.DictReader(open(path[0])))
     rows.sort(key=lambda r: int(r.get("Dispatch_Id", 0)))
     for r in rows:
-        k = short(r["Kernel_Name"]).split("<")[0]
+        # kernel + first template argument (k_cg_march<1: the q-free P, <2: its B)
+        k = short(r["Kernel_Name"]).split(",")[0].rstrip(">")
         out[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
     return out
 
@@ -61,7 +63,9 @@ def main():
                 nd[k][c] = len(v)
     rows = []
     for k in last:
-        c = ctr.get(k, {})
+        if k not in ctr:  # not launched in this probe (another march mode)
+            continue
+        c = ctr[k]
         rd = None
         if "TCC_EA0_RDREQ_128B_sum" in c:
             rd = (128 * c["TCC_EA0_RDREQ_128B_sum"] + 64 * c.get("TCC_EA0_RDREQ_64B_sum", 0)
