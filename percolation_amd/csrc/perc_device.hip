@@ -2517,7 +2517,12 @@ struct ResArgs {
   double* part;      // [2 parity][3][G]
   unsigned* bar;     // 9 counters, 128 B apart (zeroed before the launch)
   double* gran;      // [3][G] 16-B granules {partial, tag} (zeroed before the launch)
+  unsigned long long* trace;  // phase probe (PERC_RES_TRACE): [3 workgroups][kResTrIt][8]
 };
+
+// phase probe of the resident loop: wall clock (100 MHz) at 6 points of
+// each of the first kResTrIt iterations, in workgroups 0, G/2 and G-1
+constexpr int kResTrIt = 256;
 
 // single-level (m = 1024: 0.0166 vs 0.0178 ms per iteration)
 __device__ __forceinline__ bool res_barrier1(const ResArgs& a, unsigned& epoch, int* s_flag) {
@@ -2713,6 +2718,34 @@ __device__ __forceinline__ void res_pos(double& acc, unsigned um, unsigned map, 
   acc = sj != 15u ? acc + pr : acc;
 }
 
+// the same term for a wave whose elements all share one regular form (slot
+// order = raster order, used positions `mask`, wave-uniform): the slot of
+// position KP is the count js of used positions before it, a scalar, so
+// the term needs no lane-private raster -> slot map and no unused-slot
+// select; the arithmetic (acc + gv v in slot order) is res_pos's
+template <int KP, unsigned UMC>
+__device__ __forceinline__ void res_pos_u(double& acc, unsigned mask, unsigned& js, unsigned cc,
+                                          int lr, int Hw, int m, int c, const double* s_p,
+                                          const ResHalo& hu, const ResHalo& hd, double ng0,
+                                          double nleak) {
+  constexpr int DR = KP < 3 ? -1 : (KP < 5 ? 0 : 1);
+  constexpr int DC = KP < 3 ? KP - 1 : (KP == 3 ? -1 : (KP == 4 ? 1 : KP - 6));
+  if (!(UMC & (1u << KP))) return;
+  if (!(mask & (1u << KP))) return;  // wave-uniform
+  const int col = c + DC;
+  double v;
+  if (DR < 0) {
+    v = lr > 0 ? s_p[(lr > 0 ? lr - 1 : 0) * m + col] : halo_at<DC>(hu);
+  } else if (DR > 0) {
+    v = lr + 1 < Hw ? s_p[(lr + 1 < Hw ? lr + 1 : lr) * m + col] : halo_at<DC>(hd);
+  } else {
+    v = s_p[lr * m + col];
+  }
+  const double gv = ((cc >> js) & 1u) ? ng0 : nleak;
+  acc = acc + gv * v;
+  ++js;
+}
+
 // QREG: q of the own rows kept in registers between the q.p reduction and
 // the r update; else (wider / taller bands: L = 2048 has 16 elements per
 // thread) q is formed again from p(k) in LDS and the halo registers with
@@ -2721,11 +2754,12 @@ __device__ __forceinline__ void res_pos(double& acc, unsigned um, unsigned map, 
 // UMC: compile-time superset of the raster positions the forms use (0x5A:
 // the square lattice's four neighbours), so unused positions and their
 // halo columns take no registers
-template <int MT, int HMAX, bool QREG = true, unsigned UMC = 0xFFu, bool GATHER = false>
-__global__ __launch_bounds__(kResThreads) void k_cg_res(ResArgs a) {
+template <int MT, int HMAX, bool QREG = true, unsigned UMC = 0xFFu, bool GATHER = false,
+          bool TR = false, int NT = kResThreads>
+__global__ __launch_bounds__(NT) void k_cg_res(ResArgs a) {
   __shared__ double s_p[kResLdsRows];
   __shared__ double2 s_dt[kDiagTab];
-  __shared__ unsigned s_rmap[kMaxForms];
+  __shared__ unsigned s_rmap[kMaxForms], s_umask[kMaxForms];
   __shared__ double s_red[32];
   __shared__ int s_flag[2];
   int t = threadIdx.x;  // re-made opaque each iteration when !QREG (below)
@@ -2735,7 +2769,10 @@ __global__ __launch_bounds__(kResThreads) void k_cg_res(ResArgs a) {
   const bool has_up = R0 > 0, has_dn = R0 + Hw < nrows;
   const double ng0 = a.St.ng0, nleak = a.St.nleak;
   CGScalars* S = a.S;
-  if (t < kMaxForms) s_rmap[t] = a.St.F.rmap[t];
+  if (t < kMaxForms) {
+    s_rmap[t] = a.St.F.rmap[t];
+    s_umask[t] = a.St.F.regular[t] ? a.St.F.rmask[t] : 0u;  // (a regular form uses >= 1 position)
+  }
   load_dtab(a.St, s_dt);
   // own state: r and the codes of (row lr, column t + j NT)
   double rv[HMAX][MT], qv[QREG ? HMAX : 1][QREG ? MT : 1];
@@ -2746,7 +2783,7 @@ __global__ __launch_bounds__(kResThreads) void k_cg_res(ResArgs a) {
   for (int lr = 0; lr < HMAX; ++lr)
 #pragma unroll
     for (int j = 0; j < MT; ++j) {
-      const int i = (R0 + lr) * m + t + j * kResThreads;
+      const int i = (R0 + lr) * m + t + j * NT;
       const bool own = lr < Hw;
       rv[lr][j] = own ? a.r0[i] : 0.0;
       const unsigned cj = own ? a.St.code[i] : 0u;
@@ -2758,8 +2795,8 @@ __global__ __launch_bounds__(kResThreads) void k_cg_res(ResArgs a) {
   // (static) and whether the position exists
   // (column c + d - 1 exists unless c + d - 1 is -1 or m; regular forms
   // use no wrapped column)
-  auto hin = [&](int j, int d) { const int cc = t + j * kResThreads + d - 1; return cc >= 0 && cc < m; };
-  auto hcol = [&](int j, int d) { const int cc = t + j * kResThreads + d - 1; return cc < 0 ? 0 : (cc >= m ? m - 1 : cc); };
+  auto hin = [&](int j, int d) { const int cc = t + j * NT + d - 1; return cc >= 0 && cc < m; };
+  auto hcol = [&](int j, int d) { const int cc = t + j * NT + d - 1; return cc < 0 ? 0 : (cc >= m ? m - 1 : cc); };
   unsigned hcu[MT][3], hcd[MT][3];
 #pragma unroll
   for (int j = 0; j < MT; ++j)
@@ -2782,10 +2819,24 @@ __global__ __launch_bounds__(kResThreads) void k_cg_res(ResArgs a) {
   for (int lr = 0; lr < HMAX; ++lr)
 #pragma unroll
     for (int j = 0; j < MT; ++j) {
-      const int c = t + j * kResThreads;
+      const int c = t + j * NT;
       if (lr == 0) store_sc1(&xrow(1, w, 0, 0)[c], rv[lr][j]);
       if (lr == Hw - 1) store_sc1(&xrow(1, w, 1, 0)[c], rv[lr][j]);
     }
+  // x kept on the lattice's first and last interior rows only (xrows = m,
+  // the default): those rows' x live in registers of the two workgroups
+  // that own them for the whole solve (a global load + store per iteration
+  // put ~1-1.5 us of latency on those workgroups, which every other one
+  // then waited for at the next reduction)
+  const bool xreg = QREG && a.xrows == m;  // (not with 16 elements per thread: spills)
+  const bool x0w = xreg && R0 == 0, x1w = xreg && R0 + Hw == nrows && nrows > 1;
+  double xa[MT], xb[MT];
+#pragma unroll
+  for (int j = 0; j < MT; ++j) {
+    const int c = t + j * NT;
+    xa[j] = x0w ? a.x[c] : 0.0;
+    xb[j] = x1w ? a.x[(size_t)(nrows - 1) * m + c] : 0.0;
+  }
   unsigned epoch = 0;
   bool ok = res_barrier<MT == 1>(a, epoch, s_flag);
   double bknum = S->bknum, bk = 0.0, ak = 0.0;
@@ -2794,12 +2845,18 @@ __global__ __launch_bounds__(kResThreads) void k_cg_res(ResArgs a) {
   int k = 0;
   double err = 0.0;
   bool done = !ok;
+  const int tw = w == 0 ? 0 : (w == G / 2 ? 1 : (w == G - 1 ? 2 : -1));
+  auto stamp = [&](int ph) {
+    if (TR && t == 0 && tw >= 0 && k <= kResTrIt)
+      a.trace[((size_t)tw * kResTrIt + k - 1) * 8 + ph] = wall_clock64();
+  };
   while (!done) {
     // 16 elements per thread: keep the compiler from hoisting every
     // element's addresses out of the loop (they would stay live across it
     // and spill); recomputing them is a few integer ops
     if constexpr (!QREG) asm volatile("" : "+v"(t));
     ++k;
+    stamp(0);
     const int par = k & 1;
     double* part = a.part + (size_t)par * 3 * G;
     // 1. halo loads first (their latency overlaps the own rows' p(k))
@@ -2834,7 +2891,7 @@ __global__ __launch_bounds__(kResThreads) void k_cg_res(ResArgs a) {
 #pragma unroll
       for (int j = 0; j < MT; ++j) {
         if (lr < Hw) {
-          const int e = lr * m + t + j * kResThreads;
+          const int e = lr * m + t + j * NT;
           const double z = div_tab(rv[lr][j], s_dt[diag_idx(code_at(lr, j))]);
           s_p[e] = k == 1 ? z : bk * s_p[e] + z;
         }
@@ -2860,15 +2917,33 @@ __global__ __launch_bounds__(kResThreads) void k_cg_res(ResArgs a) {
       hd[j] = ResHalo{d3[0], d3[1], d3[2]};
     }
     __syncthreads();
+    stamp(1);
     // q of own element (lr, j) from p(k) in LDS and the halo rows
     auto qcalc = [&](int lr, int j, double xi) {
-      const int c = t + j * kResThreads;
+      const int c = t + j * NT;
       const unsigned cc = code_at(lr, j);
+      double acc = s_dt[diag_idx(cc)].x * xi;
       // raster positions in order (compile-time row / column offsets):
       // for the regular forms the resident path is limited to, raster
-      // order is slot order; the slot of position kp comes from rmap
-      const unsigned map = s_rmap[cc >> 11];
-      double acc = s_dt[diag_idx(cc)].x * xi;
+      // order is slot order
+      const unsigned f = cc >> 11, ff = __builtin_amdgcn_readfirstlane(f);
+      const unsigned mask = s_umask[ff];  // 0: not a regular form
+      // (the square lattice's 4-element variant only: with 16 elements per
+      // thread, or all eight positions, the second path's registers spill)
+      if (QREG && UMC == kResSquareMask && !__any(f != ff) && mask != 0u) {
+        unsigned js = 0;
+        res_pos_u<0, UMC>(acc, mask, js, cc, lr, Hw, m, c, s_p, hu[j], hd[j], ng0, nleak);
+        res_pos_u<1, UMC>(acc, mask, js, cc, lr, Hw, m, c, s_p, hu[j], hd[j], ng0, nleak);
+        res_pos_u<2, UMC>(acc, mask, js, cc, lr, Hw, m, c, s_p, hu[j], hd[j], ng0, nleak);
+        res_pos_u<3, UMC>(acc, mask, js, cc, lr, Hw, m, c, s_p, hu[j], hd[j], ng0, nleak);
+        res_pos_u<4, UMC>(acc, mask, js, cc, lr, Hw, m, c, s_p, hu[j], hd[j], ng0, nleak);
+        res_pos_u<5, UMC>(acc, mask, js, cc, lr, Hw, m, c, s_p, hu[j], hd[j], ng0, nleak);
+        res_pos_u<6, UMC>(acc, mask, js, cc, lr, Hw, m, c, s_p, hu[j], hd[j], ng0, nleak);
+        res_pos_u<7, UMC>(acc, mask, js, cc, lr, Hw, m, c, s_p, hu[j], hd[j], ng0, nleak);
+        return acc;
+      }
+      // mixed forms (edge columns): the slot of position kp comes from rmap
+      const unsigned map = s_rmap[f];
       const unsigned um = a.St.F.umask;
       res_pos<0, UMC>(acc, um, map, cc, lr, Hw, m, c, s_p, hu[j], hd[j], ng0, nleak);
       res_pos<1, UMC>(acc, um, map, cc, lr, Hw, m, c, s_p, hu[j], hd[j], ng0, nleak);
@@ -2887,7 +2962,7 @@ __global__ __launch_bounds__(kResThreads) void k_cg_res(ResArgs a) {
 #pragma unroll
       for (int j = 0; j < MT; ++j) {
         if (lr < Hw) {
-          const double xi = s_p[lr * m + t + j * kResThreads];
+          const double xi = s_p[lr * m + t + j * NT];
           const double acc = qcalc(lr, j, xi);
           if constexpr (QREG) qv[lr][j] = acc;
           dot = dot + acc * xi;
@@ -2898,9 +2973,11 @@ __global__ __launch_bounds__(kResThreads) void k_cg_res(ResArgs a) {
     {
       double v1[1] = {dot};
       block_sum<1>(v1, s_red);
+      stamp(2);
       double tot[1];
       if (GATHER) {
         if (!(ok = res_gather<1>(a, epoch, a.gran, v1, tot, s_red))) break;
+        stamp(3);
       } else {
         if (t == 0) store_sc1(&part[w], v1[0]);
         // (wave 0 summing the partials right after its own poll, with the
@@ -2920,7 +2997,7 @@ __global__ __launch_bounds__(kResThreads) void k_cg_res(ResArgs a) {
 #pragma unroll
       for (int j = 0; j < MT; ++j) {
         if (lr < Hw) {
-          const int c = t + j * kResThreads;
+          const int c = t + j * NT;
           double qq;
           if constexpr (QREG) qq = qv[lr][j];
           else qq = qcalc(lr, j, s_p[lr * m + c]);
@@ -2931,7 +3008,12 @@ __global__ __launch_bounds__(kResThreads) void k_cg_res(ResArgs a) {
           acc2[1] = acc2[1] + rn * rn;
           const double pk = s_p[lr * m + c];
           const int i = (R0 + lr) * m + c;
-          if (a.xrows == 0 || i < a.xrows || i >= N - a.xrows) a.x[i] = a.x[i] + ak * pk;
+          if (xreg) {
+            if (x0w && lr == 0) xa[j] = xa[j] + ak * pk;
+            if (x1w && lr == Hw - 1) xb[j] = xb[j] + ak * pk;
+          } else if (a.xrows == 0 || i < a.xrows || i >= N - a.xrows) {
+            a.x[i] = a.x[i] + ak * pk;
+          }
           if (lr == 0) {
             store_sc1(&xrow(npar, w, 0, 0)[c], rn);
             store_sc1(&xrow(npar, w, 0, 1)[c], pk);
@@ -2944,10 +3026,12 @@ __global__ __launch_bounds__(kResThreads) void k_cg_res(ResArgs a) {
         if constexpr (!QREG) __builtin_amdgcn_sched_barrier(0);
       }
     block_sum<2>(acc2, s_red);
+    stamp(4);
     {
       double tot[2];
       if (GATHER) {
         if (!(ok = res_gather<2>(a, epoch, a.gran + 2 * (size_t)G, acc2, tot, s_red))) break;
+        stamp(5);
       } else {
         if (t == 0) {
           store_sc1(&part[G + w], acc2[0]);
@@ -2962,6 +3046,12 @@ __global__ __launch_bounds__(kResThreads) void k_cg_res(ResArgs a) {
       if (w == 0 && t == 0 && k - 1 < a.err_hist_cap) a.err_hist[k - 1] = err;
       done = !(err > tol) || k >= itmax + 1;
     }
+  }
+#pragma unroll
+  for (int j = 0; j < MT; ++j) {
+    const int c = t + j * NT;
+    if (x0w) a.x[c] = xa[j];
+    if (x1w) a.x[(size_t)(nrows - 1) * m + c] = xb[j];
   }
   if (w == 0 && t == 0) {
     S->iter = k;
@@ -3869,6 +3959,18 @@ hipError_t dev_assemble(perc_ctx* h, int rule, double g0, double leak, double Va
   return hipSuccess;
 }
 
+// the resident kernel for m = 1024 (MT = 1) / 2048, square-lattice
+// positions only (sq) or all eight; GATHER: all-gather reductions; TR:
+// phase probe
+template <bool GATHER, bool TR>
+const void* res_kernel(int MT, bool sq) {
+  if (MT == 1)
+    return sq ? (const void*)k_cg_res<1, 4, true, kResSquareMask, GATHER, TR>
+              : (const void*)k_cg_res<1, 4, true, 0xFFu, GATHER, TR>;
+  return sq ? (const void*)k_cg_res<2, 8, false, kResSquareMask, GATHER, TR>
+            : (const void*)k_cg_res<2, 8, false, 0xFFu, GATHER, TR>;
+}
+
 // one cooperative launch runs the whole iteration loop (k_cg_res)
 hipError_t dev_solve_resident(perc_ctx* h, const CGArgs& ca, int* iter, double* err) {
   DeviceBuffers& d = h->d;
@@ -3899,14 +4001,18 @@ hipError_t dev_solve_resident(perc_ctx* h, const CGArgs& ca, int* iter, double* 
   // per iteration, L = 2048 33.7 vs 34.65 (profiles/r2_10_resident_gather_ab.log)
   const bool gat = !(getenv("PERC_RES_GATHER") && atoi(getenv("PERC_RES_GATHER")) == 0);
   const bool sq = (h->forms.umask & ~kResSquareMask) == 0;
-  if (gat)
-    fn = h->res_MT == 1 ? (const void*)k_cg_res<1, 4, true, 0xFFu, true>
-         : sq ? (const void*)k_cg_res<2, 8, false, kResSquareMask, true>
-              : (const void*)k_cg_res<2, 8, false, 0xFFu, true>;
-  else
-    fn = h->res_MT == 1 ? (const void*)k_cg_res<1, 4>
-         : sq ? (const void*)k_cg_res<2, 8, false, kResSquareMask>
-              : (const void*)k_cg_res<2, 8, false>;
+  // phase probe (PERC_RES_TRACE=<csv path>): wall-clock stamps of the first
+  // kResTrIt iterations in three workgroups, written as CSV after the solve
+  const char* trpath = getenv("PERC_RES_TRACE");
+  a.trace = nullptr;
+  const size_t trn = (size_t)3 * kResTrIt * 8;
+  const bool tr = trpath && gat;
+  if (tr) {
+    HIP_TRY(dmalloc(&a.trace, trn));
+    HIP_TRY(hipMemsetAsync(a.trace, 0, trn * sizeof(unsigned long long), st));
+  }
+  fn = tr ? res_kernel<true, true>(h->res_MT, sq)
+          : (gat ? res_kernel<true, false>(h->res_MT, sq) : res_kernel<false, false>(h->res_MT, sq));
   KernelTiming& T = h->timing;
   if (T.enabled) {
     if (T.ev.size() < 2) T.ev.resize(2, nullptr);
@@ -3920,6 +4026,22 @@ hipError_t dev_solve_resident(perc_ctx* h, const CGArgs& ca, int* iter, double* 
   CGScalars hs{};
   HIP_TRY(hipMemcpyAsync(&hs, d.scal, sizeof(hs), hipMemcpyDeviceToHost, st));
   HIP_TRY(hipStreamSynchronize(st));
+  if (a.trace) {
+    std::vector<unsigned long long> tr(trn);
+    HIP_TRY(hipMemcpy(tr.data(), a.trace, trn * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+    HIP_TRY(hipFree(a.trace));
+    if (FILE* fo = fopen(trpath, "a")) {
+      fprintf(fo, "# m=%d G=%d H=%d iter=%d (wall clock ticks, 100 MHz)\nwg,k,t0,t1,t2,t3,t4,t5\n",
+              a.m, a.G, a.H, hs.iter);
+      for (int q = 0; q < 3; ++q)
+        for (int it = 0; it < std::min(kResTrIt, hs.iter); ++it) {
+          const unsigned long long* v = &tr[((size_t)q * kResTrIt + it) * 8];
+          fprintf(fo, "%d,%d,%llu,%llu,%llu,%llu,%llu,%llu\n", q == 0 ? 0 : (q == 1 ? a.G / 2 : a.G - 1),
+                  it + 1, v[0], v[1], v[2], v[3], v[4], v[5]);
+        }
+      fclose(fo);
+    }
+  }
   if (hs.pad[0] != 0) {
     fprintf(stderr, "[perc] k_cg_res: grid barrier timed out\n");
     return hipErrorLaunchTimeOut;
