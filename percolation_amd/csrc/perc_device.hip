@@ -3405,7 +3405,7 @@ void launch_cg_b(perc_ctx* h, const CGArgs& a, int G) {
     else if (h->rm_w == 1024) klaunch(h, k_cg_rm<kMarchB, 1024>, g, b, h->stream, a);
     else klaunch(h, k_cg_rm<kMarchB, 512>, g, b, h->stream, a);
   } else if (h->march && h->qfree) {
-    if (a.sm && h->march_depth == 2) klaunch(h, k_cg_march<kMarchB, true, 2>, h->march_grid, 64 * kMarchWaves, h->stream, a);
+    if (a.sm && h->march_bdepth == 2) klaunch(h, k_cg_march<kMarchB, true, 2>, h->march_grid, 64 * kMarchWaves, h->stream, a);
     else if (a.sm) klaunch(h, k_cg_march<kMarchB, true, 3>, h->march_grid, 64 * kMarchWaves, h->stream, a);
     else klaunch(h, k_cg_march<kMarchB>, h->march_grid, 64 * kMarchWaves, h->stream, a);
   } else if (h->stencil) {
@@ -3838,6 +3838,9 @@ void march_geometry(perc_ctx* h) {
   // rows prefetched ahead by the P+S march (PERC_MARCH_DEPTH: 2 for probes)
   h->march_depth = 3;
   if (const char* e = getenv("PERC_MARCH_DEPTH")) h->march_depth = std::min(std::max(atoi(e), 2), 4);
+  // the strip-major q-free march B (PERC_MARCH_BDEPTH, probes)
+  h->march_bdepth = std::min(h->march_depth, 3);
+  if (const char* e = getenv("PERC_MARCH_BDEPTH")) h->march_bdepth = std::min(std::max(atoi(e), 2), 3);
   if (g.m % kMarchW != 0 || g.n <= 2) return;
   const int spr = g.m / kMarchW, nrows = g.n - 2;
   h->march_h = march_rows_for(h, nrows);

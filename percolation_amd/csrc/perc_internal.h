@@ -162,6 +162,7 @@ struct perc_ctx {
   bool march = false;           // fused format runs the register-march kernel
   int march_h = 32;             // its band height (rows per wave)
   int march_depth = 3;          // rows its P+S kernel prefetches ahead
+  int march_bdepth = 3;         // rows the q-free march B prefetches ahead
   int march_grid = 0;           // its workgroups
   int march_grid_max = 0;       // workgroups at band height 1 (reduction buffers)
   int march_rows_req = 0;       // perc_set_march_rows (0: auto)
