@@ -357,6 +357,14 @@ int perc_ensemble_create(int ndev, const int *devices, int lattice, int m, int n
                          perc_ensemble **out);
 int perc_ensemble_destroy(perc_ensemble *e);
 int perc_ensemble_ndev(perc_ensemble *e);
+/* W (1..64) contexts, host threads and streams per device for the trial
+   loops (default 1): trial ii runs on device (ii-1) mod ndev and there on
+   worker ((ii-1) / ndev) mod W; per-trial results are the same, the
+   per-device statistics are summed over the workers in worker order before
+   the all-reduce.  For small lattices, whose trials leave a device mostly
+   idle.  perc_ensemble_workers returns W. */
+int perc_ensemble_set_workers(perc_ensemble *e, int workers);
+int perc_ensemble_workers(perc_ensemble *e);
 /* device dev's own context (e.g. for single-trial calls); NULL if out of range */
 perc_ctx *perc_ensemble_ctx(perc_ensemble *e, int dev);
 /* the trials device `dev` of `ndev` runs, 1-based, ascending (ii_out may be

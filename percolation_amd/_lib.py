@@ -115,6 +115,8 @@ SIGNATURES = {
                                        C.POINTER(C.c_void_p)]),
     "perc_ensemble_destroy": (C.c_int, [_VP]),
     "perc_ensemble_ndev": (C.c_int, [_VP]),
+    "perc_ensemble_set_workers": (C.c_int, [_VP, C.c_int]),
+    "perc_ensemble_workers": (C.c_int, [_VP]),
     "perc_ensemble_ctx": (C.c_void_p, [_VP, C.c_int]),
     "perc_ensemble_trials": (C.c_int, [C.c_int, C.c_int, C.c_int, _VP]),
     "perc_ensemble_allreduce": (C.c_int, [_VP, _D, C.c_int]),

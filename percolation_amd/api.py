@@ -618,7 +618,7 @@ class Ensemble:
     trials striped ii -> device (ii-1) mod ndev, one RCCL all-reduce of the
     per-grid-point statistics (include/perc.h; Square/bond_cond.f:123-498)."""
 
-    def __init__(self, lattice, m, n, pbc=0, ndev=1, devices=None):
+    def __init__(self, lattice, m, n, pbc=0, ndev=1, devices=None, workers=1):
         self.lattice, self.m, self.n, self.pbc = lattice, m, n, pbc
         self.nb = nbonds(lattice, m, n, pbc)
         h = C.c_void_p()
@@ -627,6 +627,14 @@ class Ensemble:
                 "perc_ensemble_create")
         self.h = h
         self.ndev = L.lib().perc_ensemble_ndev(h)
+        self.workers = 1
+        if workers != 1:
+            self.set_workers(workers)
+
+    def set_workers(self, workers):
+        """contexts (host threads, streams) per device (perc_ensemble_set_workers)"""
+        L.check(L.lib().perc_ensemble_set_workers(self.h, workers), "perc_ensemble_set_workers")
+        self.workers = L.lib().perc_ensemble_workers(self.h)
 
     def close(self):
         if self.h:

@@ -26,9 +26,10 @@ using namespace perc;
 
 struct perc_ensemble {
   int ndev = 0;
+  int workers = 1;  // contexts (host threads, streams) per device
   int lattice = 0, m = 0, n = 0, pbc = 0;
   std::vector<int> devices;
-  std::vector<perc_ctx*> ctx;
+  std::vector<perc_ctx*> ctx;  // [d * workers + w]
   std::vector<ncclComm_t> comm;
   std::vector<hipStream_t> stream;
   std::vector<double*> d_buf;  // per device all-reduce buffer
@@ -138,12 +139,13 @@ int perc_ensemble_destroy(perc_ensemble* e) {
   if (!e) return PERC_EINVAL;
   for (size_t d = 0; d < e->comm.size(); ++d)
     if (e->comm[d]) ncclCommDestroy(e->comm[d]);
-  for (int d = 0; d < (int)e->ctx.size(); ++d) {
+  for (int d = 0; d < (int)e->stream.size(); ++d) {
     hipSetDevice(e->devices[d]);
     if (e->d_buf[d]) hipFree(e->d_buf[d]);
     if (e->stream[d]) hipStreamDestroy(e->stream[d]);
-    if (e->ctx[d]) perc_ctx_destroy(e->ctx[d]);
   }
+  for (size_t i = 0; i < e->ctx.size(); ++i)
+    if (e->ctx[i]) perc_ctx_destroy(e->ctx[i]);
   delete e;
   return PERC_OK;
 }
@@ -151,8 +153,40 @@ int perc_ensemble_destroy(perc_ensemble* e) {
 int perc_ensemble_ndev(perc_ensemble* e) { return e ? e->ndev : PERC_EINVAL; }
 
 perc_ctx* perc_ensemble_ctx(perc_ensemble* e, int dev) {
-  return (e && dev >= 0 && dev < e->ndev) ? e->ctx[dev] : nullptr;
+  return (e && dev >= 0 && dev < e->ndev) ? e->ctx[(size_t)dev * e->workers] : nullptr;
 }
+
+// W contexts (host threads, streams) per device: small lattices leave most
+// of a device idle in one trial's chain of labelings and one-workgroup
+// solves, and independent trials fill it (bond_cond L = 64 on one GPU, one
+// context per Python thread: 3.2 / 6.3 / 6.5 / 8.9 trials/s at 1 / 2 / 4 / 8,
+// profiles/r2_24_cond_workers.log)
+int perc_ensemble_set_workers(perc_ensemble* e, int workers) {
+  if (!e || workers < 1 || workers > 64) return PERC_EINVAL;
+  if (workers == e->workers) return PERC_OK;
+  std::vector<perc_ctx*> nctx((size_t)e->ndev * workers, nullptr);
+  int rc = PERC_OK;
+  for (int d = 0; d < e->ndev; ++d)
+    for (int w = 0; w < workers; ++w) {
+      perc_ctx*& c = nctx[(size_t)d * workers + w];
+      if (w < e->workers) {
+        std::swap(c, e->ctx[(size_t)d * e->workers + w]);
+      } else if (!rc) {
+        rc = perc_ctx_create(e->devices[d], e->lattice, e->m, e->n, e->pbc, &c);
+      }
+    }
+  for (perc_ctx* c : e->ctx)  // the contexts beyond the new count
+    if (c) perc_ctx_destroy(c);
+  e->ctx.swap(nctx);
+  e->workers = workers;
+  if (rc) {  // keep a consistent ensemble: back to one worker per device
+    perc_ensemble_set_workers(e, 1);
+    return rc;
+  }
+  return PERC_OK;
+}
+
+int perc_ensemble_workers(perc_ensemble* e) { return e ? e->workers : PERC_EINVAL; }
 
 // stats[d*k .. d*k+k) is device d's vector; on return every slice holds the
 // element-wise sum over the devices (ncclAllReduce, sum, fp64).
@@ -197,25 +231,29 @@ int perc_ensemble_bond_cond(perc_ensemble* e, int ntrials, const int* tseed, int
   if (!e || ntrials < 0 || !tseed || npts < 0 || (npts && !nbarr) || !nrows || !bf_c ||
       !perccln || (npts && (!gbot || !gtop || !iters)))
     return PERC_EINVAL;
-  const int ndev = e->ndev;
+  const int ndev = e->ndev, W = e->workers;
   const int nb = perc_nbonds(e->lattice, e->m, e->n, e->pbc);
+  // per worker, then summed per device in worker order
+  std::vector<double> wacc((size_t)ndev * W * npts * 5, 0.0);
   std::vector<double> acc((size_t)ndev * npts * 5, 0.0);
   std::atomic<int> status{PERC_OK};
-  std::vector<std::string> errs(ndev);
+  std::vector<std::string> errs((size_t)ndev * W);
 
-  auto worker = [&](int d) {
-    perc_ctx* h = e->ctx[d];
+  auto worker = [&](int d, int w) {
+    const size_t dw = (size_t)d * W + w;
+    perc_ctx* h = e->ctx[dw];
     hipSetDevice(e->devices[d]);
     std::vector<int> order(nb + 1);
-    double* a = acc.data() + (size_t)d * npts * 5;
+    double* a = wacc.data() + dw * npts * 5;
     auto check = [&](int rc) {
       if (rc && status.load() == PERC_OK) {
         int expect = PERC_OK;
-        if (status.compare_exchange_strong(expect, rc)) errs[d] = perc_last_error();
+        if (status.compare_exchange_strong(expect, rc)) errs[dw] = perc_last_error();
       }
       return rc == PERC_OK && status.load() == PERC_OK;
     };
-    for (int ii = d + 1; ii <= ntrials; ii += ndev) {  // trial ii on device (ii-1) mod ndev
+    // trial ii on device (ii-1) mod ndev; on the device, worker ((ii-1) / ndev) mod W
+    for (int ii = d + 1 + w * ndev; ii <= ntrials; ii += ndev * W) {
       const int t = ii - 1;
       perc_shuffle_seeded(tseed[t], nb, order.data());  // bond_cond.f:181-193
       int jj = 0, lastbf = -1;
@@ -259,8 +297,13 @@ int perc_ensemble_bond_cond(perc_ensemble* e, int ntrials, const int* tseed, int
   };
 
   std::vector<std::thread> th;
-  for (int d = 0; d < ndev; ++d) th.emplace_back(worker, d);
+  for (int d = 0; d < ndev; ++d)
+    for (int w = 0; w < W; ++w) th.emplace_back(worker, d, w);
   for (auto& x : th) x.join();
+  for (int d = 0; d < ndev; ++d)
+    for (int w = 0; w < W; ++w)
+      for (int k = 0; k < npts * 5; ++k)
+        acc[(size_t)d * npts * 5 + k] += wacc[((size_t)d * W + w) * npts * 5 + k];
   if (status.load() != PERC_OK) {
     for (auto& s : errs)
       if (!s.empty()) set_error("perc_ensemble_bond_cond: " + s);

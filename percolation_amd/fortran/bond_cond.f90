@@ -15,7 +15,7 @@
 !
 ! Parameters: the reference's block (10x10, numtrials 1, master seed 58302),
 ! overridable by bond_cond.nml (&bond_cond_nml lattice, m, n, pbc,
-! numtrials, seed, Va, g0, tol, itmax, device, ndev /).  Output: bondcond.txt as
+! numtrials, seed, Va, g0, tol, itmax, device, ndev, workers /).  Output: bondcond.txt as
 ! the reference writes it (bond_cond.f:107-117, 481-496).
 !
 ! ndev >= 1 shards the trials over devices 0..ndev-1 of the node
@@ -23,17 +23,19 @@
 ! thread each, rows gathered in ii order) and all-reduces the per-grid-point
 ! statistics with RCCL; bondcond.txt is the same file, and the reduced
 ! statistics go to bondcond_stats.txt.  ndev = 0 (default) runs every trial
-! on `device` in this thread.
+! on `device` in this thread.  workers > 1 (with ndev >= 1) runs that many
+! trials at a time on each device (perc_ensemble_set_workers: a context,
+! host thread and stream each) -- small lattices leave a device mostly idle.
 program bond_cond
   use perc_api
   implicit none
 #ifndef PERC_LATTICE
 #define PERC_LATTICE 0
 #endif
-  integer(c_int) :: lattice, m, n, pbc, numtrials, seed, itmax, device, ndev
+  integer(c_int) :: lattice, m, n, pbc, numtrials, seed, itmax, device, ndev, workers
   double precision :: Va, g0, tol
   namelist /bond_cond_nml/ lattice, m, n, pbc, numtrials, seed, Va, g0, tol, itmax, device, &
-                           ndev
+                           ndev, workers
   integer(c_int) :: t, nb, i, ii, jj, bf, lastbf, npts, lo, hi, mid, bfc, perccln, stats(4)
   integer(c_int) :: tseed(1000), nbarr(250)
   double precision :: pbarr(250), pb, pc, Gtop, Gbot
@@ -58,6 +60,7 @@ program bond_cond
   itmax = 2500
   device = 0
   ndev = 0
+  workers = 1
   if (perc_have_file('bond_cond.nml')) then
     open(newunit=u, file='bond_cond.nml', status='old')
     read(u, nml=bond_cond_nml)
@@ -102,6 +105,8 @@ program bond_cond
     allocate(e_stats(250 * 5))
     call perc_check(perc_ensemble_create(ndev, c_null_ptr, lattice, m, n, pbc, ens), &
                     'perc_ensemble_create')
+    if (workers > 1) call perc_check(perc_ensemble_set_workers(ens, workers), &
+                                     'perc_ensemble_set_workers')
     call perc_check(perc_ensemble_bond_cond(ens, numtrials, tseed, 250, nbarr, Va, g0, tol, &
                     itmax, e_nrows, e_gbot, e_gtop, e_iters, e_bfc, e_pl, e_stats), &
                     'perc_ensemble_bond_cond')

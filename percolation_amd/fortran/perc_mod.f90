@@ -171,6 +171,13 @@ module perc_api
       type(c_ptr), value :: e
     end function perc_ensemble_destroy
 
+    integer(c_int) function perc_ensemble_set_workers(e, workers) &
+        bind(C, name='perc_ensemble_set_workers')
+      import :: c_int, c_ptr
+      type(c_ptr), value :: e
+      integer(c_int), value :: workers
+    end function perc_ensemble_set_workers
+
     integer(c_int) function perc_ensemble_bond_cond(e, ntrials, tseed, npts, nbarr, Va, g0, &
         tol, itmax, nrows, gbot, gtop, iters, bf_c, perccln, stats) &
         bind(C, name='perc_ensemble_bond_cond')

@@ -82,20 +82,22 @@ def test_fortran_bond_cond_ndev1_equals_single_context(v, tmp_path):
     if not os.path.exists(exe):
         pytest.skip("Fortran drivers not built")
     out = {}
-    for ndev in (0, 1):
-        d = tmp_path / ("ndev%d" % ndev)
+    for ndev, workers in ((0, 1), (1, 1), (1, 3)):
+        d = tmp_path / ("ndev%d_w%d" % (ndev, workers))
         d.mkdir()
         (d / "bond_cond.nml").write_text(
-            "&bond_cond_nml lattice=%d, m=%d, n=%d, pbc=%d, numtrials=%d, seed=%d, ndev=%d /\n"
-            % (p["lattice"], p["m"], p["n"], p["pbc"], p["numtrials"], p["seed"], ndev))
+            "&bond_cond_nml lattice=%d, m=%d, n=%d, pbc=%d, numtrials=%d, seed=%d, ndev=%d, "
+            "workers=%d /\n"
+            % (p["lattice"], p["m"], p["n"], p["pbc"], p["numtrials"], p["seed"], ndev, workers))
         r = subprocess.run([exe], cwd=d, capture_output=True, text=True, timeout=300)
         assert r.returncode == 0, r.stderr[-2000:]
-        out[ndev] = (d / "bondcond.txt").read_bytes()
-    assert out[1] == out[0]
-    stats = (tmp_path / "ndev1" / "bondcond_stats.txt").read_text().splitlines()
+        out[ndev, workers] = (d / "bondcond.txt").read_bytes()
+    # one device, one or three trials at a time: the serial loop's file
+    assert out[1, 1] == out[0, 1] and out[1, 3] == out[0, 1]
+    stats = (tmp_path / "ndev1_w1" / "bondcond_stats.txt").read_text().splitlines()
     assert stats[0] == "devices: 1" and len(stats) > 1
     want = G.text(v, "bondcond.txt").decode().splitlines()
-    got = out[1].decode().splitlines()
+    got = out[1, 1].decode().splitlines()
     assert len(got) == len(want)
     for a, b in zip(got, want):
         if b.count(",") == 3:
@@ -104,6 +106,25 @@ def test_fortran_bond_cond_ndev1_equals_single_context(v, tmp_path):
             assert all(abs(x - y) <= 2e-9 for x, y in zip(fa[1:], fb[1:])), (a, b)
         else:
             assert a == b
+
+
+def test_ensemble_workers_same_trials():
+    """perc_ensemble_set_workers: W contexts per device run the trials
+    concurrently; every trial's rows are bitwise those of one worker, the
+    statistics the same sums up to their association over the workers."""
+    out = {}
+    for W in (1, 3, 4):
+        with api.Ensemble(0, 24, 24, 0, ndev=1, workers=W) as e:
+            assert e.workers == W
+            out[W] = e.bond_cond(58302, 11)
+    (r1, s1) = out[1]
+    for W in (3, 4):
+        rw, sw = out[W]
+        assert len(rw) == len(r1) == 11
+        for a, b in zip(rw, r1):
+            assert a["rows"] == b["rows"] and a["bf_c"] == b["bf_c"] and a["perccln"] == b["perccln"]
+        assert np.array_equal(sw[:, [0, 3, 4]], s1[:, [0, 3, 4]])
+        assert np.allclose(sw[:, 1:3], s1[:, 1:3], rtol=1e-13, atol=0)
 
 
 def test_torch_nccl_group_world1(tmp_path):
