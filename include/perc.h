@@ -272,6 +272,56 @@ int perc_set_full_voltages(perc_ctx *h, int enable);
    nslab > 1 in another format fails with PERC_EHIP.  Default 1. */
 int perc_set_slabs(perc_ctx *h, int nslab);
 
+/* Distributed row slabs: one process per GPU solves slab s of K of the
+   system assembled by perc_assemble (every process labels and assembles
+   the whole lattice; the solve is split).  The per-slab kernels and the
+   slab-order combine are perc_set_slabs's, so K processes reproduce its
+   K-slab numbers bitwise.  The caller moves data between processes
+   (percolation_amd/dslab.py: torch.distributed, RCCL on the context's
+   stream or gloo through the host), through device buffers it owns:
+     part_out  4 doubles   this slab's partials after a step (send);
+     part_all  4K doubles  every slab's part_out in slab order (receive);
+     edge_lo / edge_hi     m doubles: r of the slab's first / last row
+                           (send to slab s-1 / s+1; NULL at s = 0 / K-1);
+     ghost_lo / ghost_hi   m doubles: slab s-1's last / s+1's first row
+                           (receive).
+   Protocol: perc_dslab_begin (prologue; publishes part_out and the edges)
+   -> all-gather part_out into part_all, exchange edges into ghosts ->
+   step COMBINE_INIT, GHOSTS; then per iteration: PS, all-gather,
+   COMBINE_PS, B, all-gather, COMBINE_B, exchange edges, GHOSTS; poll
+   perc_dslab_status every few iterations (the steps are no-ops once the
+   stop test fired: every process takes the same decision).  perc_dslab_end
+   puts this slab's x rows (the electrode rows unless full_x) into the
+   context's x; perc_x_row / perc_currents then give Gtop / Gbot on the
+   process that holds both electrode rows. */
+typedef struct perc_dslab_bufs {
+  double *part_out, *part_all, *edge_lo, *edge_hi, *ghost_lo, *ghost_hi;
+} perc_dslab_bufs;
+#define PERC_DSLAB_COMBINE_INIT 0
+#define PERC_DSLAB_PS 1
+#define PERC_DSLAB_COMBINE_PS 2
+#define PERC_DSLAB_B 3
+#define PERC_DSLAB_COMBINE_B 4
+#define PERC_DSLAB_GHOSTS 5
+int perc_dslab_begin(perc_ctx *h, int K, int s, int itol, double tol, int itmax, int full_x,
+                     const perc_dslab_bufs *bufs);
+int perc_dslab_step(perc_ctx *h, int op);
+int perc_dslab_status(perc_ctx *h, int *iter, double *err, int *done);
+int perc_dslab_end(perc_ctx *h);
+/* assembly only (perc_conductance's first half): the Kirchhoff system of
+   the lowest spanning cluster; PERC_ESTATE before perc_label, status 1 in
+   *spanning = 0 when nothing spans */
+int perc_assemble(perc_ctx *h, int rule, double g0, double leak, double Va, int *spanning);
+/* copy row `row` of the interior voltages between the context and a device
+   buffer of m doubles (to_ctx = 1: into the context) */
+int perc_x_row(perc_ctx *h, int row, double *dev_buf, int to_ctx);
+/* terminal currents of the context's x (perc_conductance's last step) */
+int perc_currents(perc_ctx *h, int rule, int cur_rule, double Va, double g0, double leak,
+                  perc_cond_result *res);
+/* the HIP stream the context enqueues on (hipStream_t), e.g. for a caller's
+   collectives on the same stream */
+void *perc_stream(perc_ctx *h);
+
 /* Band height (lattice rows per wave) of the register-march kernel; 0 (default)
    picks the tallest of 32, 16, .. 2 rows that still gives >= 4096 waves.
    A tuning / test knob: results are the same up to the association of the

@@ -39,6 +39,14 @@ class CondResult(C.Structure):
                 ("t_solve_ms", C.c_double), ("t_currents_ms", C.c_double)]
 
 
+class DslabBufs(C.Structure):
+    _fields_ = [(k, C.c_void_p) for k in ("part_out", "part_all", "edge_lo", "edge_hi",
+                                          "ghost_lo", "ghost_hi")]
+
+
+DSLAB_COMBINE_INIT, DSLAB_PS, DSLAB_COMBINE_PS, DSLAB_B, DSLAB_COMBINE_B, DSLAB_GHOSTS = range(6)
+
+
 class Realisation(C.Structure):
     _fields_ = [("label", LabelInfo), ("cond", CondResult), ("t_upload_ms", C.c_double),
                 ("t_label_ms", C.c_double), ("t_total_ms", C.c_double)]
@@ -92,6 +100,18 @@ SIGNATURES = {
     "perc_set_full_voltages": (C.c_int, [_VP, C.c_int]),
     "perc_set_march_rows": (C.c_int, [_VP, C.c_int]),
     "perc_set_slabs": (C.c_int, [_VP, C.c_int]),
+    "perc_dslab_begin": (C.c_int, [_VP, C.c_int, C.c_int, C.c_int, C.c_double, C.c_int, C.c_int,
+                                   C.POINTER(DslabBufs)]),
+    "perc_dslab_step": (C.c_int, [_VP, C.c_int]),
+    "perc_dslab_status": (C.c_int, [_VP, C.POINTER(C.c_int), C.POINTER(C.c_double),
+                                    C.POINTER(C.c_int)]),
+    "perc_dslab_end": (C.c_int, [_VP]),
+    "perc_assemble": (C.c_int, [_VP, C.c_int, C.c_double, C.c_double, C.c_double,
+                                C.POINTER(C.c_int)]),
+    "perc_x_row": (C.c_int, [_VP, C.c_int, _VP, C.c_int]),
+    "perc_currents": (C.c_int, [_VP, C.c_int, C.c_int, C.c_double, C.c_double, C.c_double,
+                                C.POINTER(CondResult)]),
+    "perc_stream": (C.c_void_p, [_VP]),
     "perc_cluster_sizes": (C.c_int, [_VP, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
     "perc_occupy_random": (C.c_int, [_VP, C.c_int, C.c_int, C.c_int, C.c_ulonglong]),
     "perc_random_order": (C.c_int, [C.c_longlong, C.c_int, C.c_ulonglong, C.c_int, _I]),

@@ -98,6 +98,7 @@ class Context:
 
     def __init__(self, lattice, m, n, pbc=0, device=0):
         self.lattice, self.m, self.n, self.pbc = lattice, m, n, pbc
+        self.device = device
         self.t = m * n
         self.nb = nbonds(lattice, m, n, pbc)
         self.N = self.t - 2 * m

@@ -4215,14 +4215,18 @@ hipError_t dev_solve(perc_ctx* h, int itol, double tol, int itmax, bool x0_zero,
 // device (buffers private per slab, halo by device copies) so the exchange
 // pattern is tested on one GPU; across GPUs the halo copies become xGMI
 // peer copies and the combines an all-gather of 3 doubles.
+// pall: the K slabs' partials gathered from K processes ([s][4], perc_dslab_*),
+// this process's scalars S[0] only; else the K slabs' own S[s].part
 template <int STAGE>  // 0: q.p; 1: z.r, r.r (B epilogue); 2: the prologue
-__global__ void k_slab_combine(CGScalars* S, int K, double* err_hist, int cap) {
+__global__ void k_slab_combine(CGScalars* S, int K, double* err_hist, int cap,
+                               const double* pall = nullptr) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
   if (STAGE != 2 && S[0].done) return;
   double t0 = 0.0, t1 = 0.0;
+  constexpr int i0 = STAGE == 0 ? 0 : (STAGE == 1 ? 1 : 3), i1 = STAGE == 1 ? 2 : 1;
   for (int s = 0; s < K; ++s) {
-    t0 = t0 + S[s].part[STAGE == 0 ? 0 : (STAGE == 1 ? 1 : 3)];
-    t1 = t1 + S[s].part[STAGE == 1 ? 2 : 1];
+    t0 = t0 + (pall ? pall[4 * s + i0] : S[s].part[i0]);
+    t1 = t1 + (pall ? pall[4 * s + i1] : S[s].part[i1]);
   }
   CGScalars v = S[0];
   if (STAGE == 0) {
@@ -4246,7 +4250,12 @@ __global__ void k_slab_combine(CGScalars* S, int K, double* err_hist, int cap) {
     v.iter = 0;
     v.done = 0;
   }
-  for (int s = 0; s < K; ++s) S[s] = v;
+  for (int s = 0; s < (pall ? 1 : K); ++s) S[s] = v;
+}
+
+// this slab's partials into the all-gather send buffer
+__global__ void k_slab_publish(const CGScalars* S, double* part_out) {
+  if (threadIdx.x < 4) part_out[threadIdx.x] = S->part[threadIdx.x];
 }
 
 namespace {
@@ -4422,6 +4431,216 @@ hipError_t dev_solve_slabs(perc_ctx* h, int K, int itol, double tol, int itmax, 
   cleanup();
 #undef SLAB_TRY
   return hipSuccess;
+}
+
+// ---------------------------------------------------------------------------
+// Distributed row slabs (perc_dslab_*): the slab engine above with one slab
+// per process -- slab s of K lives on this process's device, and the two
+// exchanges a single-process solve does with device copies go through the
+// caller: the all-gather of the slabs' partials ([s][4] doubles, reduced
+// here in slab order by k_slab_combine, so every process takes the same
+// stop decision) and the halo rows of r.  The caller's buffers are device
+// memory (perc_dslab_bufs); every step is enqueued on the context's stream,
+// so a caller whose collectives run on that stream (RCCL) never waits on
+// the host in between.  Per-slab kernels and combine order are those of
+// dev_solve_slabs: K processes give its numbers bitwise.
+struct DSlab {
+  Slab b;
+  CGScalars* S = nullptr;
+  CGScalars* hs = nullptr;  // pinned status copy
+  CGArgs a;
+  perc_dslab_bufs buf{};
+  int K = 1, s = 0;
+  bool full_x = false;
+  long long k = 0;  // P+S launches so far
+};
+
+hipError_t dev_dslab_end(perc_ctx* h, bool to_ctx) {
+  DSlab* D = h->dslab;
+  if (!D) return hipSuccess;
+  hipError_t e = hipSuccess;
+  hipStream_t st = h->stream;
+  if (to_ctx) {  // voltages into the context's x, scalars as a single-slab solve leaves them
+    const int m = h->g.m, nrows = h->g.n - 2;
+    const size_t row = sizeof(double) * m;
+    const Slab& b = D->b;
+    if (D->full_x) {
+      e = hipMemcpyAsync(h->d.x + (size_t)b.r0 * m, b.x, row * b.rows, hipMemcpyDeviceToDevice, st);
+    } else {
+      if (D->s == 0) e = hipMemcpyAsync(h->d.x, b.x, row, hipMemcpyDeviceToDevice, st);
+      if (e == hipSuccess && D->s == D->K - 1)
+        e = hipMemcpyAsync(h->d.x + (size_t)(nrows - 1) * m, b.x + (size_t)(b.rows - 1) * m, row,
+                           hipMemcpyDeviceToDevice, st);
+    }
+    if (e == hipSuccess) e = hipMemcpyAsync(h->d.scal, D->S, sizeof(CGScalars), hipMemcpyDeviceToDevice, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+  }
+  (void)hipStreamSynchronize(st);
+  Slab& b = D->b;
+  for (double* v : {b.r, b.p0, b.p1, b.q, b.x, b.partials}) if (v) (void)hipFree(v);
+  if (b.tickets) (void)hipFree(b.tickets);
+  if (D->S) (void)hipFree(D->S);
+  if (D->hs) (void)hipHostFree(D->hs);
+  delete D;
+  h->dslab = nullptr;
+  return e;
+}
+
+hipError_t dev_dslab_begin(perc_ctx* h, int K, int s, int itol, double tol, int itmax, bool full_x,
+                           const perc_dslab_bufs& bufs) {
+  HIP_TRY(dev_dslab_end(h, false));
+  DeviceBuffers& d = h->d;
+  hipStream_t st = h->stream;
+  const int m = h->g.m, nrows = h->g.n - 2;
+  if (!h->march || K < 1 || K > nrows || s < 0 || s >= K || !bufs.part_out || !bufs.part_all ||
+      (s > 0 && (!bufs.edge_lo || !bufs.ghost_lo)) || (s < K - 1 && (!bufs.edge_hi || !bufs.ghost_hi)))
+    return hipErrorInvalidValue;
+  if (d.err_hist_cap < itmax + 2) {
+    if (d.err_hist) HIP_TRY(hipFree(d.err_hist));
+    d.err_hist_cap = itmax + 2;
+    HIP_TRY(dmalloc(&d.err_hist, d.err_hist_cap));
+  }
+  int cus = 0;
+  HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, h->device));
+  auto* D = new DSlab();
+  h->dslab = D;
+  D->K = K;
+  D->s = s;
+  D->full_x = full_x;
+  D->buf = bufs;
+  Slab& b = D->b;
+  for (int q = 0; q < s; ++q) b.r0 += nrows / K + (q < nrows % K ? 1 : 0);
+  b.rows = nrows / K + (s < nrows % K ? 1 : 0);
+  b.N = b.rows * m;
+  b.glo = s > 0 ? -1 : 0;
+  b.ghi = s < K - 1 ? b.rows + 1 : b.rows;
+  b.march_h = march_rows_for(h, b.rows);
+  b.march_grid = cdiv((m / kMarchW) * cdiv(b.rows, b.march_h), kMarchWaves);
+  b.b_grid = std::max(1, std::min(2 * cus, cg_grid(b.N)));
+  b.init_grid = cg_grid(b.N);
+  b.red = std::max({b.march_grid, b.b_grid, b.init_grid});
+  const size_t gpad = 2 * (size_t)m + 8;
+  HIP_TRY(dmalloc(&b.r, b.N + gpad));
+  HIP_TRY(dmalloc(&b.p0, b.N + gpad));
+  HIP_TRY(dmalloc(&b.p1, b.N + gpad));
+  HIP_TRY(dmalloc(&b.q, (size_t)b.N + 8));
+  HIP_TRY(dmalloc(&b.x, (size_t)b.N + 8));
+  HIP_TRY(dmalloc(&b.partials, kRedSlots * red_partials_size(b.red)));
+  HIP_TRY(dmalloc(&b.tickets, kRedSlots * red_tickets_size(b.red)));
+  HIP_TRY(hipMemsetAsync(b.tickets, 0, kRedSlots * red_tickets_size(b.red) * sizeof(unsigned), st));
+  HIP_TRY(hipMemsetAsync(b.x, 0, ((size_t)b.N + 8) * sizeof(double), st));
+  for (double* v : {b.r, b.p0, b.p1}) HIP_TRY(hipMemsetAsync(v, 0, (b.N + gpad) * sizeof(double), st));
+  HIP_TRY(dmalloc(&D->S, 1));
+  HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&D->hs), sizeof(CGScalars)));
+  CGScalars s0{};
+  s0.tol = tol;
+  s0.itmax = itmax;
+  HIP_TRY(hipMemcpyAsync(D->S, &s0, sizeof(CGScalars), hipMemcpyHostToDevice, st));
+  CGArgs a = make_cg_args(h);
+  a.A.N = b.N;
+  a.St.N = b.N;
+  a.St.code = d.code + (size_t)b.r0 * m;
+  a.T.nrows = b.rows;
+  a.T.bh = b.march_h;
+  a.rhs = d.rhs + (size_t)b.r0 * m;
+  a.r = b.r + m;
+  a.pb[0] = b.p0 + m;
+  a.pb[1] = b.p1 + m;
+  a.p = a.pb[0];
+  a.q = b.q;
+  a.x = b.x;
+  a.fused = 1;
+  a.b_reverse = 1;
+  a.bx = 1;
+  a.glo = b.glo;
+  a.ghi = b.ghi;
+  a.slab = 1;
+  a.xrows = full_x ? 0 : (s == 0 ? m : -1);
+  a.xhi = full_x ? -1 : (s == K - 1 ? m : 0);
+  a.pstride = red_partials_size(b.red);
+  a.tstride = red_tickets_size(b.red);
+  a.partials = b.partials;
+  a.tickets = b.tickets;
+  a.S = D->S;
+  D->a = a;
+  // prologue (x0 = 0: r = b): this slab's bnrm^2 and z.r partials, and its
+  // edge rows of r(1) for the neighbours' ghost rows
+  k_cg_init<true><<<b.init_grid, kBlock, 0, st>>>(a, itol, 1);
+  HIP_TRY(dbg_sync(st, "k_cg_init (dslab)"));
+  return dev_dslab_step(h, -1);
+}
+
+// op: -1 publish partials + edge rows (after the prologue); PERC_DSLAB_* of perc.h
+hipError_t dev_dslab_step(perc_ctx* h, int op) {
+  DSlab* D = h->dslab;
+  if (!D) return hipErrorInvalidValue;
+  hipStream_t st = h->stream;
+  const int m = h->g.m, K = D->K;
+  const Slab& b = D->b;
+  CGArgs& a = D->a;
+  const size_t row = sizeof(double) * m;
+  auto edges_out = [&]() -> hipError_t {
+    if (D->s > 0) HIP_TRY(hipMemcpyAsync(D->buf.edge_lo, b.r + m, row, hipMemcpyDeviceToDevice, st));
+    if (D->s < K - 1)
+      HIP_TRY(hipMemcpyAsync(D->buf.edge_hi, b.r + (size_t)b.rows * m, row, hipMemcpyDeviceToDevice, st));
+    return hipSuccess;
+  };
+  switch (op) {
+    case -1:
+      k_slab_publish<<<1, 64, 0, st>>>(D->S, D->buf.part_out);
+      HIP_TRY(edges_out());
+      break;
+    case PERC_DSLAB_COMBINE_INIT:
+      k_slab_combine<2><<<1, 64, 0, st>>>(D->S, K, h->d.err_hist, h->d.err_hist_cap, D->buf.part_all);
+      break;
+    case PERC_DSLAB_PS:
+      a.kiter = (int)(++D->k);
+      if (h->march_depth == 2) k_cg_march<kMarchPQ, false, 2><<<b.march_grid, 64 * kMarchWaves, 0, st>>>(a);
+      else k_cg_march<kMarchPQ, false, 3><<<b.march_grid, 64 * kMarchWaves, 0, st>>>(a);
+      k_slab_publish<<<1, 64, 0, st>>>(D->S, D->buf.part_out);
+      break;
+    case PERC_DSLAB_COMBINE_PS:
+      k_slab_combine<0><<<1, 64, 0, st>>>(D->S, K, h->d.err_hist, h->d.err_hist_cap, D->buf.part_all);
+      break;
+    case PERC_DSLAB_B:
+      if (D->full_x) k_cg_b<true, true><<<b.b_grid, kBlock, 0, st>>>(a);
+      else k_cg_b<true><<<b.b_grid, kBlock, 0, st>>>(a);
+      k_slab_publish<<<1, 64, 0, st>>>(D->S, D->buf.part_out);
+      HIP_TRY(edges_out());
+      break;
+    case PERC_DSLAB_COMBINE_B:
+      k_slab_combine<1><<<1, 64, 0, st>>>(D->S, K, h->d.err_hist, h->d.err_hist_cap, D->buf.part_all);
+      break;
+    case PERC_DSLAB_GHOSTS:
+      if (D->s > 0) HIP_TRY(hipMemcpyAsync(b.r, D->buf.ghost_lo, row, hipMemcpyDeviceToDevice, st));
+      if (D->s < K - 1)
+        HIP_TRY(hipMemcpyAsync(b.r + (size_t)(b.rows + 1) * m, D->buf.ghost_hi, row,
+                               hipMemcpyDeviceToDevice, st));
+      break;
+    default:
+      return hipErrorInvalidValue;
+  }
+  HIP_TRY(hipGetLastError());
+  return dbg_sync(st, "dslab step");
+}
+
+hipError_t dev_dslab_status(perc_ctx* h, int* iter, double* err, int* done) {
+  DSlab* D = h->dslab;
+  if (!D) return hipErrorInvalidValue;
+  HIP_TRY(hipMemcpyAsync(D->hs, D->S, sizeof(CGScalars), hipMemcpyDeviceToHost, h->stream));
+  HIP_TRY(hipStreamSynchronize(h->stream));
+  *iter = D->hs->iter;
+  *err = D->hs->err;
+  *done = D->hs->done || D->k > (long long)D->hs->itmax + 2;
+  return hipSuccess;
+}
+
+hipError_t dev_x_row(perc_ctx* h, int row, double* buf, bool to_ctx) {
+  const int m = h->g.m;
+  double* xr = h->d.x + (size_t)row * m;
+  HIP_TRY(hipMemcpyAsync(to_ctx ? xr : buf, to_ctx ? buf : xr, sizeof(double) * m,
+                         hipMemcpyDeviceToDevice, h->stream));
+  return hipStreamSynchronize(h->stream);
 }
 
 hipError_t dev_currents(perc_ctx* h, int rule, int cur_rule, double g0, double leak, double Va,

@@ -261,6 +261,7 @@ int perc_ctx_destroy(perc_ctx* h) {
   if (!h) return PERC_EINVAL;
   hipSetDevice(h->device);
   if (h->stream) hipStreamSynchronize(h->stream);
+  if (h->dslab) dev_dslab_end(h, false);
   free_buffers(h);
   for (int i = 0; i < 8; ++i)
     if (h->ev[i]) hipEventDestroy(h->ev[i]);
@@ -676,6 +677,24 @@ int perc_replay_labels(int lattice, int m, int n, int pbc, int kind, int nsites,
                             stats);
 }
 
+// the spanning cluster's Kirchhoff system (perc_conductance / perc_assemble)
+static int assemble_impl(perc_ctx* h, int rule, double g0, double leak, double Va, const char* who) {
+  hipError_t e = dev_assemble(h, rule, g0, leak, Va, h->span_root);
+  if (e != hipSuccess) return hip_status(e, who);
+  if (((h->fmt_req == PERC_FMT_STENCIL || h->fmt_req == PERC_FMT_STENCIL_TILED) && !h->tiled_ok) ||
+      (h->fmt_req == PERC_FMT_STENCIL_SPLIT && !h->stencil_ok)) {
+    set_error(std::string(who) + ": requested stencil operator not available for this system");
+    return PERC_EINVAL;
+  }
+  h->assembled = true;
+  h->rule = rule;
+  return PERC_OK;
+}
+
+// terminal currents of the context's x -> Gtop, Gbot (bondc.f:554-592)
+static int currents_impl(perc_ctx* h, int rule, int cur_rule, double Va, double g0, double leak,
+                         perc_cond_result* res, const char* who);
+
 int perc_conductance(perc_ctx* h, int rule, int cur_rule, double Va, double g0, double leak,
                      int itol, double tol, int itmax, perc_cond_result* res, double* vint_out) {
   if (!h || !res) return PERC_EINVAL;
@@ -693,26 +712,35 @@ int perc_conductance(perc_ctx* h, int rule, int cur_rule, double Va, double g0, 
   }
   hipStream_t st = h->stream;
   hipEventRecord(h->ev[0], st);
-  hipError_t e = dev_assemble(h, rule, g0, leak, Va, h->span_root);
-  if (e != hipSuccess) return hip_status(e, "perc_conductance/assemble");
-  if (((h->fmt_req == PERC_FMT_STENCIL || h->fmt_req == PERC_FMT_STENCIL_TILED) && !h->tiled_ok) ||
-      (h->fmt_req == PERC_FMT_STENCIL_SPLIT && !h->stencil_ok)) {
-    set_error("perc_conductance: requested stencil operator not available for this system");
-    return PERC_EINVAL;
-  }
+  int rc = assemble_impl(h, rule, g0, leak, Va, "perc_conductance/assemble");
+  if (rc) return rc;
   hipEventRecord(h->ev[1], st);
-  h->assembled = true;
-  h->rule = rule;
   int iter = 0;
   double err = 0.0;
-  e = dev_solve(h, itol, tol, itmax, true, h->full_voltages || vint_out != nullptr, &iter, &err);
+  hipError_t e = dev_solve(h, itol, tol, itmax, true, h->full_voltages || vint_out != nullptr, &iter, &err);
   if (e != hipSuccess) return hip_status(e, "perc_conductance/solve");
   hipEventRecord(h->ev[2], st);
+  rc = currents_impl(h, rule, cur_rule, Va, g0, leak, res, "perc_conductance/currents");
+  if (rc) return rc;
+  res->iter = iter;
+  res->err = err;
+  res->t_assemble_ms = event_ms(h, 0, 1);
+  res->t_solve_ms = event_ms(h, 1, 2);
+  res->t_currents_ms = event_ms(h, 2, 3);
+  if (vint_out) {
+    e = hipMemcpy(vint_out, h->d.x, sizeof(double) * h->N, hipMemcpyDeviceToHost);
+    if (e != hipSuccess) return hip_status(e, "perc_conductance/vint");
+  }
+  return PERC_OK;
+}
+
+static int currents_impl(perc_ctx* h, int rule, int cur_rule, double Va, double g0, double leak,
+                         perc_cond_result* res, const char* who) {
   std::vector<double> iout(2 * (size_t)h->g.m);
   const double thresh = cur_rule == PERC_CUR_FORTRAN ? 1.0e-10 : 0.0;
-  e = dev_currents(h, rule, cur_rule, g0, leak, Va, h->span_root, thresh, iout.data());
-  if (e != hipSuccess) return hip_status(e, "perc_conductance/currents");
-  hipEventRecord(h->ev[3], st);
+  hipError_t e = dev_currents(h, rule, cur_rule, g0, leak, Va, h->span_root, thresh, iout.data());
+  if (e != hipSuccess) return hip_status(e, who);
+  hipEventRecord(h->ev[3], h->stream);
   hipEventSynchronize(h->ev[3]);
   const int m = h->g.m;
   double Ibot = 0.0, Itop = 0.0;
@@ -729,17 +757,62 @@ int perc_conductance(perc_ctx* h, int rule, int cur_rule, double Va, double g0, 
   }
   res->gtop = Itop / Va;
   res->gbot = std::fabs(Ibot) / Va;
-  res->iter = iter;
-  res->err = err;
-  res->t_assemble_ms = event_ms(h, 0, 1);
-  res->t_solve_ms = event_ms(h, 1, 2);
-  res->t_currents_ms = event_ms(h, 2, 3);
-  if (vint_out) {
-    e = hipMemcpy(vint_out, h->d.x, sizeof(double) * h->N, hipMemcpyDeviceToHost);
-    if (e != hipSuccess) return hip_status(e, "perc_conductance/vint");
-  }
   return PERC_OK;
 }
+
+int perc_assemble(perc_ctx* h, int rule, double g0, double leak, double Va, int* spanning) {
+  if (!h || !spanning) return PERC_EINVAL;
+  if (!h->labeled) return PERC_ESTATE;
+  if (rule < PERC_RULE_BOND || rule > PERC_RULE_MIXED) return PERC_EINVAL;
+  hipSetDevice(h->device);
+  *spanning = h->span_root != 0;
+  if (!*spanning) return PERC_OK;
+  return assemble_impl(h, rule, g0, leak, Va, "perc_assemble");
+}
+
+int perc_currents(perc_ctx* h, int rule, int cur_rule, double Va, double g0, double leak,
+                  perc_cond_result* res) {
+  if (!h || !res) return PERC_EINVAL;
+  if (!h->assembled) return PERC_ESTATE;
+  hipSetDevice(h->device);
+  std::memset(res, 0, sizeof(*res));
+  return currents_impl(h, rule, cur_rule, Va, g0, leak, res, "perc_currents");
+}
+
+int perc_dslab_begin(perc_ctx* h, int K, int s, int itol, double tol, int itmax, int full_x,
+                     const perc_dslab_bufs* bufs) {
+  if (!h || !bufs || itmax < 0) return PERC_EINVAL;
+  if (!h->assembled) return PERC_ESTATE;
+  if (itol != 1 && itol != 2) return PERC_EITOL;
+  hipSetDevice(h->device);
+  return hip_status(dev_dslab_begin(h, K, s, itol, tol, itmax, full_x != 0, *bufs), "perc_dslab_begin");
+}
+
+int perc_dslab_step(perc_ctx* h, int op) {
+  if (!h || !h->dslab || op < PERC_DSLAB_COMBINE_INIT || op > PERC_DSLAB_GHOSTS) return PERC_EINVAL;
+  hipSetDevice(h->device);
+  return hip_status(dev_dslab_step(h, op), "perc_dslab_step");
+}
+
+int perc_dslab_status(perc_ctx* h, int* iter, double* err, int* done) {
+  if (!h || !h->dslab || !iter || !err || !done) return PERC_EINVAL;
+  hipSetDevice(h->device);
+  return hip_status(dev_dslab_status(h, iter, err, done), "perc_dslab_status");
+}
+
+int perc_dslab_end(perc_ctx* h) {
+  if (!h || !h->dslab) return PERC_EINVAL;
+  hipSetDevice(h->device);
+  return hip_status(dev_dslab_end(h, true), "perc_dslab_end");
+}
+
+int perc_x_row(perc_ctx* h, int row, double* dev_buf, int to_ctx) {
+  if (!h || !dev_buf || row < 0 || row >= h->g.n - 2) return PERC_EINVAL;
+  hipSetDevice(h->device);
+  return hip_status(dev_x_row(h, row, dev_buf, to_ctx != 0), "perc_x_row");
+}
+
+void* perc_stream(perc_ctx* h) { return h ? (void*)h->stream : nullptr; }
 
 int perc_get_system(perc_ctx* h, int* rowptr, int* col, double* val, double* diag, double* rhs,
                     int* n_out, int* nnz_out) {

@@ -134,6 +134,10 @@ struct KernelTiming {
 
 }  // namespace perc
 
+namespace perc {
+struct DSlab;
+}
+
 struct perc_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
@@ -180,6 +184,7 @@ struct perc_ctx {
   int rm_grid = 0;              // their workgroups
   bool full_voltages = false;   // perc_set_full_voltages: keep x on every row
   int nslab = 1;                // perc_set_slabs: row slabs of the CG solve
+  perc::DSlab* dslab = nullptr;  // perc_dslab_*: this process's slab of a distributed solve
   double st_ng0 = 0.0, st_nleak = 0.0;  // its two off-diagonal values
   perc::StencilForms forms{};            // row forms of this lattice
   hipEvent_t ev[8];
@@ -204,6 +209,12 @@ hipError_t dev_assemble(perc_ctx* h, int rule, double g0, double leak, double Va
 void select_format(perc_ctx* h);  // stencil / fused flags from fmt_req + assembly checks
 void march_geometry(perc_ctx* h); // band height + grid of the register-march kernel
 void res_geometry(perc_ctx* h);   // grid + band height of the resident solve
+hipError_t dev_dslab_begin(perc_ctx* h, int K, int s, int itol, double tol, int itmax, bool full_x,
+                           const perc_dslab_bufs& bufs);
+hipError_t dev_dslab_step(perc_ctx* h, int op);
+hipError_t dev_dslab_status(perc_ctx* h, int* iter, double* err, int* done);
+hipError_t dev_dslab_end(perc_ctx* h, bool to_ctx);
+hipError_t dev_x_row(perc_ctx* h, int row, double* buf, bool to_ctx);
 hipError_t dev_solve_slabs(perc_ctx* h, int K, int itol, double tol, int itmax, bool full_x,
                            int* iter, double* err);
 hipError_t dev_solve(perc_ctx* h, int itol, double tol, int itmax, bool x0_zero, bool full_x,

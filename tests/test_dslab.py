@@ -1,0 +1,140 @@
+"""One conductance solve split over processes (percolation_amd/dslab.py,
+perc_dslab_* in include/perc.h; SURVEY.md §8(f) row 2, the linbcg loop of
+Square/bondc.f:780-836).
+
+CPU: the exchange layer at world size 3 over gloo -- the all-gather puts
+every slab's partials in slab order, and the halo swap hands slab s-1's
+last row to slab s's lower ghost and slab s+1's first row to its upper
+ghost.
+
+GPU: K processes on the box's one GPU (gloo through host memory; RCCL
+allows one rank per device) give perc_set_slabs(K)'s numbers in one process
+bitwise -- same slab kernels, same slab-order combine; one process over
+RCCL ("nccl", the multi-GPU transport) agrees with the single-slab solve
+up to the dot association.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from percolation_amd import _lib as PL
+from percolation_amd import api, dslab
+
+
+def free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _exchange_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        m = 5
+        po = torch.arange(4, dtype=torch.float64) + 10 * rank
+        pa = torch.zeros(4 * world, dtype=torch.float64)
+        edges = tuple(torch.full((m,), 100.0 * rank + side, dtype=torch.float64)
+                      if 0 <= rank + (2 * side - 1) < world else None for side in (0, 1))
+        ghosts = tuple(torch.zeros(m, dtype=torch.float64) if e is not None else None for e in edges)
+        ex = dslab._Exchange(None, world, rank, po, pa, edges, ghosts)
+        ex.gather()
+        ex.halo()
+        q.put((rank, pa.tolist(), [None if g is None else g.tolist() for g in ghosts]))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_exchange_gather_and_halo_gloo():
+    world = 3
+    ctx = mp.get_context("spawn")
+    q = ctx.SimpleQueue()
+    mp.spawn(_exchange_worker, args=(world, free_port(), q), nprocs=world, join=True)
+    got = {}
+    while not q.empty():
+        r, pa, gh = q.get()
+        got[r] = (pa, gh)
+    assert sorted(got) == [0, 1, 2]
+    want = [v + 10 * r for r in range(world) for v in range(4)]
+    for r in range(world):
+        pa, (glo, ghi) = got[r]
+        assert pa == want  # slab order on every process
+        # lower ghost = slab r-1's upper edge (side 1), upper ghost = slab r+1's lower edge
+        assert glo == (None if r == 0 else [100.0 * (r - 1) + 1] * 5)
+        assert ghi == (None if r == world - 1 else [100.0 * (r + 1)] * 5)
+
+
+CASES = [(0, 256, 150, 0, 0.6, 1234), (1, 128, 99, 0, 0.42, 77)]
+
+
+def _system(lat, m, n, pbc, p, seed):
+    nb = api.nbonds(lat, m, n, pbc)
+    return api.shuffled_ids(nb, seed), int(p * nb)
+
+
+def _solve_worker(rank, world, port, backend, case, tol, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group(backend, rank=rank, world_size=world)
+    try:
+        lat, m, n, pbc = case[:4]
+        order, tb = _system(*case)
+        with api.Context(lat, m, n, pbc) as ctx:
+            ctx.occupy(PL.BOND, bond_order=order, nbonds_=tb)
+            assert ctx.label()["nspan"] > 0
+            r = dslab.conductance(ctx, tol=tol, itmax=100000, check_every=16)
+        q.put((rank, r))
+    finally:
+        dist.destroy_process_group()
+
+
+def _run(world, backend, case, tol):
+    ctx = mp.get_context("spawn")
+    q = ctx.SimpleQueue()
+    mp.spawn(_solve_worker, args=(world, free_port(), backend, case, tol, q), nprocs=world,
+             join=True)
+    out = {}
+    while not q.empty():
+        r, res = q.get()
+        out[r] = res
+    assert sorted(out) == list(range(world))
+    return out
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", CASES, ids=["sq256x150", "tri128x99"])
+@pytest.mark.parametrize("K", [2, 3])
+def test_processes_equal_slabs_in_one_process(case, K):
+    lat, m, n, pbc = case[:4]
+    order, tb = _system(*case)
+    with api.Context(lat, m, n, pbc) as ctx:
+        ctx.occupy(PL.BOND, bond_order=order, nbonds_=tb)
+        ctx.label()
+        ctx.set_march_mode(PL.MARCH_ALT)  # the slabs run the row-major q-storing march
+        ctx.set_slabs(K)
+        ref = ctx.conductance(tol=1e-12, itmax=100000)
+    out = _run(K, "gloo", case, 1e-12)
+    for r in range(K):  # every process reports the same numbers: perc_set_slabs(K)'s
+        assert out[r]["iter"] == ref["iter"], (r, out[r], ref)
+        assert out[r]["gtop"] == ref["gtop"] and out[r]["gbot"] == ref["gbot"], (r, out[r], ref)
+
+
+@pytest.mark.gpu
+def test_one_process_over_rccl():
+    case = CASES[0]
+    lat, m, n, pbc = case[:4]
+    order, tb = _system(*case)
+    with api.Context(lat, m, n, pbc) as ctx:
+        ctx.occupy(PL.BOND, bond_order=order, nbonds_=tb)
+        ctx.label()
+        ref = ctx.conductance(tol=1e-12, itmax=100000)
+    out = _run(1, "nccl", case, 1e-12)[0]
+    assert abs(out["iter"] - ref["iter"]) <= 2
+    assert abs(out["gtop"] - ref["gtop"]) <= 1e-9 * abs(ref["gtop"])
+    assert abs(out["gbot"] - ref["gbot"]) <= 1e-9 * abs(ref["gbot"])
