@@ -3868,18 +3868,22 @@ void march_geometry(perc_ctx* h) {
 }
 
 // resident solve: m a multiple of 1024 (MT = m / 1024 columns per thread
-// and row), the band height H of ceil(nrows / CUs) rows within the LDS and
-// register budget, one workgroup per CU
+// and row), or m = 128 / 256 / 512 with m threads per workgroup (one column
+// each: mid-size lattices, whose launched kernels are latency-bound), the
+// band height H of ceil(nrows / CUs) rows within the LDS and register
+// budget, one workgroup per CU
 void res_geometry(perc_ctx* h) {
   const Geom& g = h->g;
   h->res_G = 0;
-  if (g.m % kResThreads != 0 || g.n <= 2) return;
+  const bool narrow = g.m == 128 || g.m == 256 || g.m == 512;
+  if ((g.m % kResThreads != 0 && !narrow) || g.n <= 2) return;
   int cus = 0, coop = 0;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, h->device) != hipSuccess ||
       hipDeviceGetAttribute(&coop, hipDeviceAttributeCooperativeLaunch, h->device) != hipSuccess ||
       !coop || cus <= 0)
     return;
-  const int nrows = g.n - 2, MT = g.m / kResThreads;
+  h->res_NT = narrow ? g.m : kResThreads;
+  const int nrows = g.n - 2, MT = narrow ? 1 : g.m / kResThreads;
   const int H = cdiv(nrows, cus);
   // m = 1024: at most 4 rows per CU (r, q, code of 4 elements per thread
   // in registers, 97 VGPRs); m = 2048: at most 8 rows per CU, q formed
@@ -3966,7 +3970,17 @@ hipError_t dev_assemble(perc_ctx* h, int rule, double g0, double leak, double Va
 // positions only (sq) or all eight; GATHER: all-gather reductions; TR:
 // phase probe
 template <bool GATHER, bool TR>
-const void* res_kernel(int MT, bool sq) {
+const void* res_kernel(int MT, bool sq, int NT) {
+  if (GATHER && !TR && NT == 512)
+    return sq ? (const void*)k_cg_res<1, 4, true, kResSquareMask, true, false, 512>
+              : (const void*)k_cg_res<1, 4, true, 0xFFu, true, false, 512>;
+  if (GATHER && !TR && NT == 256)
+    return sq ? (const void*)k_cg_res<1, 4, true, kResSquareMask, true, false, 256>
+              : (const void*)k_cg_res<1, 4, true, 0xFFu, true, false, 256>;
+  if (GATHER && !TR && NT == 128)
+    return sq ? (const void*)k_cg_res<1, 4, true, kResSquareMask, true, false, 128>
+              : (const void*)k_cg_res<1, 4, true, 0xFFu, true, false, 128>;
+  if (NT != kResThreads) return nullptr;
   if (MT == 1)
     return sq ? (const void*)k_cg_res<1, 4, true, kResSquareMask, GATHER, TR>
               : (const void*)k_cg_res<1, 4, true, 0xFFu, GATHER, TR>;
@@ -4014,8 +4028,13 @@ hipError_t dev_solve_resident(perc_ctx* h, const CGArgs& ca, int* iter, double* 
     HIP_TRY(dmalloc(&a.trace, trn));
     HIP_TRY(hipMemsetAsync(a.trace, 0, trn * sizeof(unsigned long long), st));
   }
-  fn = tr ? res_kernel<true, true>(h->res_MT, sq)
-          : (gat ? res_kernel<true, false>(h->res_MT, sq) : res_kernel<false, false>(h->res_MT, sq));
+  const int nt = h->res_NT;
+  fn = tr ? res_kernel<true, true>(h->res_MT, sq, nt)
+          : (gat ? res_kernel<true, false>(h->res_MT, sq, nt) : res_kernel<false, false>(h->res_MT, sq, nt));
+  if (!fn) {  // (narrow widths: the all-gather variant only)
+    if (a.trace) (void)hipFree(a.trace);
+    return hipErrorInvalidConfiguration;  // dev_solve falls back to the launched kernels
+  }
   KernelTiming& T = h->timing;
   if (T.enabled) {
     if (T.ev.size() < 2) T.ev.resize(2, nullptr);
@@ -4023,7 +4042,7 @@ hipError_t dev_solve_resident(perc_ctx* h, const CGArgs& ca, int* iter, double* 
       if (!T.ev[i]) HIP_TRY(hipEventCreate(&T.ev[i]));
     HIP_TRY(hipEventRecord(T.ev[0], st));
   }
-  HIP_TRY(hipLaunchCooperativeKernel(fn, dim3(a.G), dim3(kResThreads), args, 0, st));
+  HIP_TRY(hipLaunchCooperativeKernel(fn, dim3(a.G), dim3(nt), args, 0, st));
   HIP_TRY(dbg_sync(st, "k_cg_res"));
   if (T.enabled) HIP_TRY(hipEventRecord(T.ev[1], st));
   CGScalars hs{};

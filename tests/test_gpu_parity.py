@@ -627,7 +627,10 @@ def test_table_division_is_ieee_division():
                                            # 2048 columns: two per thread, q formed twice
                                            (0, 2048, 2048, 0, 0.6), (0, 2048, 300, 0, 0.55),
                                            (0, 2048, 1500, 0, 0.58),
-                                           (1, 2048, 800, 0, 0.42)])
+                                           (1, 2048, 800, 0, 0.42),
+                                           # m = 128 / 256 / 512: m threads per workgroup
+                                           (0, 256, 256, 0, 0.6), (1, 128, 300, 0, 0.42),
+                                           (0, 512, 400, 0, 0.55), (1, 512, 512, 0, 0.42)])
 def test_resident_solve_matches_march(lat, m, n, pbc, p):
     """The persistent resident solve (one cooperative launch, p in LDS,
     three grid barriers per iteration; bands of 1..4 rows per CU) against
