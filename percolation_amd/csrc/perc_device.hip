@@ -3868,14 +3868,14 @@ void march_geometry(perc_ctx* h) {
 }
 
 // resident solve: m a multiple of 1024 (MT = m / 1024 columns per thread
-// and row), or m = 128 / 256 / 512 with m threads per workgroup (one column
-// each: mid-size lattices, whose launched kernels are latency-bound), the
+// and row), or m < 1024 a multiple of 64 with m threads per workgroup (one
+// column each: mid-size lattices, whose launched kernels are latency-bound), the
 // band height H of ceil(nrows / CUs) rows within the LDS and register
 // budget, one workgroup per CU
 void res_geometry(perc_ctx* h) {
   const Geom& g = h->g;
   h->res_G = 0;
-  const bool narrow = g.m == 128 || g.m == 256 || g.m == 512;
+  const bool narrow = g.m % 64 == 0 && g.m < kResThreads;  // whole waves
   if ((g.m % kResThreads != 0 && !narrow) || g.n <= 2) return;
   int cus = 0, coop = 0;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, h->device) != hipSuccess ||
@@ -3969,18 +3969,16 @@ hipError_t dev_assemble(perc_ctx* h, int rule, double g0, double leak, double Va
 // the resident kernel for m = 1024 (MT = 1) / 2048, square-lattice
 // positions only (sq) or all eight; GATHER: all-gather reductions; TR:
 // phase probe
+// (NT threads per workgroup, m of them for m <= 1024: with one column per
+// thread the template's NT is only the launch bound, so widths up to 512
+// share the 512-bound instantiation -- 125-142 VGPRs, no spills)
 template <bool GATHER, bool TR>
 const void* res_kernel(int MT, bool sq, int NT) {
-  if (GATHER && !TR && NT == 512)
+  if (MT == 1 && NT <= 512) {
+    if (!GATHER || TR) return nullptr;
     return sq ? (const void*)k_cg_res<1, 4, true, kResSquareMask, true, false, 512>
               : (const void*)k_cg_res<1, 4, true, 0xFFu, true, false, 512>;
-  if (GATHER && !TR && NT == 256)
-    return sq ? (const void*)k_cg_res<1, 4, true, kResSquareMask, true, false, 256>
-              : (const void*)k_cg_res<1, 4, true, 0xFFu, true, false, 256>;
-  if (GATHER && !TR && NT == 128)
-    return sq ? (const void*)k_cg_res<1, 4, true, kResSquareMask, true, false, 128>
-              : (const void*)k_cg_res<1, 4, true, 0xFFu, true, false, 128>;
-  if (NT != kResThreads) return nullptr;
+  }
   if (MT == 1)
     return sq ? (const void*)k_cg_res<1, 4, true, kResSquareMask, GATHER, TR>
               : (const void*)k_cg_res<1, 4, true, 0xFFu, GATHER, TR>;
