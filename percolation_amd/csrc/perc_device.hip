@@ -2766,6 +2766,10 @@ __global__ __launch_bounds__(NT) void k_cg_res(ResArgs a) {
   const int w = blockIdx.x;
   const int m = a.m, nrows = a.nrows, N = a.St.N, G = a.G;
   const int R0 = w * a.H, Hw = min(a.H, nrows - R0);  // >= 1 (host sizes G)
+  // one column per thread below m = 1024, the workgroup rounded up to whole
+  // waves: threads past the last column own no element (they join the
+  // barriers and reductions with zeros)
+  const bool tin = MT > 1 || t < m;
   const bool has_up = R0 > 0, has_dn = R0 + Hw < nrows;
   const double ng0 = a.St.ng0, nleak = a.St.nleak;
   CGScalars* S = a.S;
@@ -2784,7 +2788,7 @@ __global__ __launch_bounds__(NT) void k_cg_res(ResArgs a) {
 #pragma unroll
     for (int j = 0; j < MT; ++j) {
       const int i = (R0 + lr) * m + t + j * NT;
-      const bool own = lr < Hw;
+      const bool own = lr < Hw && tin;
       rv[lr][j] = own ? a.r0[i] : 0.0;
       const unsigned cj = own ? a.St.code[i] : 0u;
       if (j & 1) cv[lr][j / 2] |= cj << 16;
@@ -2820,8 +2824,8 @@ __global__ __launch_bounds__(NT) void k_cg_res(ResArgs a) {
 #pragma unroll
     for (int j = 0; j < MT; ++j) {
       const int c = t + j * NT;
-      if (lr == 0) store_sc1(&xrow(1, w, 0, 0)[c], rv[lr][j]);
-      if (lr == Hw - 1) store_sc1(&xrow(1, w, 1, 0)[c], rv[lr][j]);
+      if (tin && lr == 0) store_sc1(&xrow(1, w, 0, 0)[c], rv[lr][j]);
+      if (tin && lr == Hw - 1) store_sc1(&xrow(1, w, 1, 0)[c], rv[lr][j]);
     }
   // x kept on the lattice's first and last interior rows only (xrows = m,
   // the default): those rows' x live in registers of the two workgroups
@@ -2829,7 +2833,7 @@ __global__ __launch_bounds__(NT) void k_cg_res(ResArgs a) {
   // put ~1-1.5 us of latency on those workgroups, which every other one
   // then waited for at the next reduction)
   const bool xreg = QREG && a.xrows == m;  // (not with 16 elements per thread: spills)
-  const bool x0w = xreg && R0 == 0, x1w = xreg && R0 + Hw == nrows && nrows > 1;
+  const bool x0w = xreg && tin && R0 == 0, x1w = xreg && tin && R0 + Hw == nrows && nrows > 1;
   double xa[MT], xb[MT];
 #pragma unroll
   for (int j = 0; j < MT; ++j) {
@@ -2890,7 +2894,7 @@ __global__ __launch_bounds__(NT) void k_cg_res(ResArgs a) {
     for (int lr = 0; lr < HMAX; ++lr)
 #pragma unroll
       for (int j = 0; j < MT; ++j) {
-        if (lr < Hw) {
+        if (lr < Hw && tin) {
           const int e = lr * m + t + j * NT;
           const double z = div_tab(rv[lr][j], s_dt[diag_idx(code_at(lr, j))]);
           s_p[e] = k == 1 ? z : bk * s_p[e] + z;
@@ -2961,7 +2965,7 @@ __global__ __launch_bounds__(NT) void k_cg_res(ResArgs a) {
     for (int lr = 0; lr < HMAX; ++lr)
 #pragma unroll
       for (int j = 0; j < MT; ++j) {
-        if (lr < Hw) {
+        if (lr < Hw && tin) {
           const double xi = s_p[lr * m + t + j * NT];
           const double acc = qcalc(lr, j, xi);
           if constexpr (QREG) qv[lr][j] = acc;
@@ -2996,7 +3000,7 @@ __global__ __launch_bounds__(NT) void k_cg_res(ResArgs a) {
     for (int lr = 0; lr < HMAX; ++lr)
 #pragma unroll
       for (int j = 0; j < MT; ++j) {
-        if (lr < Hw) {
+        if (lr < Hw && tin) {
           const int c = t + j * NT;
           double qq;
           if constexpr (QREG) qq = qv[lr][j];
@@ -3868,21 +3872,22 @@ void march_geometry(perc_ctx* h) {
 }
 
 // resident solve: m a multiple of 1024 (MT = m / 1024 columns per thread
-// and row), or m < 1024 a multiple of 64 with m threads per workgroup (one
-// column each: mid-size lattices, whose launched kernels are latency-bound), the
+// and row), or m < 1024 with m threads per workgroup rounded up to whole
+// waves (one column each: mid-size lattices, whose launched kernels are
+// latency-bound), the
 // band height H of ceil(nrows / CUs) rows within the LDS and register
 // budget, one workgroup per CU
 void res_geometry(perc_ctx* h) {
   const Geom& g = h->g;
   h->res_G = 0;
-  const bool narrow = g.m % 64 == 0 && g.m < kResThreads;  // whole waves
+  const bool narrow = g.m < kResThreads;
   if ((g.m % kResThreads != 0 && !narrow) || g.n <= 2) return;
   int cus = 0, coop = 0;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, h->device) != hipSuccess ||
       hipDeviceGetAttribute(&coop, hipDeviceAttributeCooperativeLaunch, h->device) != hipSuccess ||
       !coop || cus <= 0)
     return;
-  h->res_NT = narrow ? g.m : kResThreads;
+  h->res_NT = narrow ? (g.m + 63) / 64 * 64 : kResThreads;  // whole waves
   const int nrows = g.n - 2, MT = narrow ? 1 : g.m / kResThreads;
   const int H = cdiv(nrows, cus);
   // m = 1024: at most 4 rows per CU (r, q, code of 4 elements per thread

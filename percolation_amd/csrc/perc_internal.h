@@ -180,7 +180,7 @@ struct perc_ctx {
   bool resident = false;        // persistent resident solve (k_cg_res)
   bool small = false;           // one-workgroup solve of a small system (k_cg_small)
   int res_G = 0, res_H = 0, res_MT = 0, res_HMAX = 0;  // its grid, band height, template
-  int res_NT = 1024;            // its threads per workgroup (m for m < 1024)
+  int res_NT = 1024;            // its threads per workgroup (m rounded up to 64 for m < 1024)
   int rm_w = 0, rm_h = 16;      // their strip width (columns) and band height
   int rm_grid = 0;              // their workgroups
   bool full_voltages = false;   // perc_set_full_voltages: keep x on every row

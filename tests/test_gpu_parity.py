@@ -632,7 +632,10 @@ def test_table_division_is_ieee_division():
                                            (0, 256, 256, 0, 0.6), (1, 128, 300, 0, 0.42),
                                            (0, 512, 400, 0, 0.55), (1, 512, 512, 0, 0.42),
                                            (0, 192, 300, 0, 0.6), (1, 640, 500, 0, 0.42),
-                                           (0, 960, 700, 0, 0.55)])
+                                           (0, 960, 700, 0, 0.55),
+                                           # widths that are not whole waves
+                                           (0, 1000, 1000, 0, 0.6), (1, 300, 301, 0, 0.42),
+                                           (0, 100, 150, 0, 0.6)])
 def test_resident_solve_matches_march(lat, m, n, pbc, p):
     """The persistent resident solve (one cooperative launch, p in LDS,
     three grid barriers per iteration; bands of 1..4 rows per CU) against
