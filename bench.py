@@ -196,6 +196,7 @@ def kernel_label(key, minfo):
 
 # rocprof kernel names of the CG kernels, per operator format
 ROCPROF_NAMES = {("res", "stencil"): ("k_cg_res",),  # default kernel of each role first
+                 ("res", "stencil_tiled"): ("k_cg_res",),
                  ("pm", "stencil"): ("k_cg_march<1", "k_cg_march<0", "k_cg_rm<0", "k_cg_rm<1"),
                  ("ps", "stencil_tiled"): ("k_cg_ps<4>", "k_cg_ps<6>"),
                  ("resid", "stencil_tiled"): ("k_cg_b<true>",),
@@ -551,7 +552,7 @@ def main():
         """(key, stats key, perc_bench_kernel id, bytes) of the CG kernels of
         operator format f"""
         full = args.full_voltages
-        if f == "stencil" and minfo.get("kernel") == "resident" and not probe:
+        if f in ("stencil", "stencil_tiled") and minfo.get("kernel") == "resident" and not probe:
             # whole iterations in one persistent launch; per iteration it
             # moves only the exchanged band-edge rows (r, p: 4 rows of m per
             # band, written and read) and the electrode-adjacent x rows
