@@ -10,8 +10,9 @@ labels it (partition fingerprint = the oracle's, bit-exact) and solves the
 spanning cluster's Kirchhoff system at each tolerance the fixture holds.
 Bars: converged (tol 1e-13) Gtop and Gbot within 1e-10
 relative, for the default solve and the 4-slab row decomposition; at the
-reference tolerance 1e-8 the iteration count within +-1 and G within the
-reference's own truncation error there (see CONVERGED below).
+reference tolerance 1e-8 the iteration count within +-1 and G within twice
+the reference's own truncation error there plus the tolerance (see
+CONVERGED below).
 """
 import glob
 import hashlib
@@ -119,5 +120,9 @@ def test_config_fixture(path):
             continue
         assert abs(d["iter"] - d["iter_ref"]) <= (1 if float(tkey) >= 1e-10 else 3), d
         for g in ("gtop", "gbot"):
-            trunc = rel(ref[g], conv[g])  # the reference's own error at this tol
-            assert d[g + "_rel"] <= 2 * trunc + CONVERGED, (g, trunc, d)
+            # the reference's own error at this tol, plus the tolerance itself:
+            # where G has converged ahead of the residual (the metric's Gtop
+            # moves 3.6e-10 from 1e-8 to 1e-13), stopping one iteration
+            # apart still moves it by the last step (1.4e-9 there)
+            trunc = rel(ref[g], conv[g])
+            assert d[g + "_rel"] <= 2 * trunc + max(CONVERGED, float(tkey)), (g, trunc, d)
