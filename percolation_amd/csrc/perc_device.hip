@@ -1822,7 +1822,7 @@ __device__ __forceinline__ unsigned melem(const CGArgs& a, const MBuf& B, int gr
   return SM ? (unsigned)sm_at(a.T, gr, col) : (unsigned)((gr - B.lo) * a.T.m + col);
 }
 
-template <int MODE, bool SM>
+template <int MODE, bool SM, int PAUX = 0>
 __device__ __forceinline__ void march_load(const CGArgs& a, const MGeom& g, const MBuf& B, int gr,
                                            bool first, const double* __restrict__ psrc, MRow& R) {
   {
@@ -1834,8 +1834,11 @@ __device__ __forceinline__ void march_load(const CGArgs& a, const MGeom& g, cons
     const bool hk = rowok && g.hok;
     const unsigned h8 = hk ? eh * 8u : kOOB;
     R.c = __builtin_amdgcn_raw_buffer_load_b32(B.c, (int)(rowok ? e * 2u : kOOB), 0, 0);
-    R.r = bld2(B.r, rown ? o8 : kOOB);
-    R.p = bld2(B.p, first ? kOOB : o8);
+    // PAUX on the loads that read a value for the last time: P's p(k-1)
+    // (dead once p(k) is formed), B's r(k) (overwritten by r(k+1))
+    constexpr int kRAux = MODE == kMarchB ? PAUX : 0, kPAux = MODE == kMarchP ? PAUX : 0;
+    R.r = __builtin_bit_cast(double2, __builtin_amdgcn_raw_buffer_load_b128(B.r, (int)(rown ? o8 : kOOB), 0, kRAux));
+    R.p = __builtin_bit_cast(double2, __builtin_amdgcn_raw_buffer_load_b128(B.p, (int)(first ? kOOB : o8), 0, kPAux));
     if (MODE != kMarchB) {
       R.hc = __builtin_amdgcn_raw_buffer_load_b16(B.c, (int)(hk ? eh * 2u : kOOB), 0, 0);
       R.hr = bld1(B.r, h8);
@@ -1855,7 +1858,7 @@ struct MState {
 
 // one step: row gr enters the window, then the middle row (gr -+ 1) is
 // finished when it is one of the band's own rows
-template <int MODE, bool UP, bool SM>
+template <int MODE, bool UP, bool SM, int SAUX = kNT>
 __device__ __forceinline__ void march_step(const CGArgs& a, const MGeom& g, const MBuf& B,
                                            const MRow& R, int gr,
                                            bool first, double bk, double ak,
@@ -1897,7 +1900,7 @@ __device__ __forceinline__ void march_step(const CGArgs& a, const MGeom& g, cons
       const bool own = gr >= g.r0 && gr < g.rend;
       const bool pst = (unsigned)(gr - B.lo) < (unsigned)(B.hi - B.lo) &&
                        (own || (a.slab && (gr < 0 || gr >= nrows)));
-      bst2<kNT>(B.pn, pst ? melem<SM>(a, B, gr, g.col) * 8u : kOOB, pn);
+      bst2<SAUX>(B.pn, pst ? melem<SM>(a, B, gr, g.col) * 8u : kOOB, pn);
       if (MODE == kMarchP && !SM) {  // x += ak p(k-1) on the x rows (the P-only march keeps x)
         const int i = gr * m + g.col;
         const bool xw = own && !first && !a.bx && (a.xrows == 0 || i < a.xrows || i >= N - a.xrows);
@@ -1987,11 +1990,11 @@ __device__ __forceinline__ void march_step(const CGArgs& a, const MGeom& g, cons
     const int m = a.T.m;
     const unsigned eq = SM ? (unsigned)sm_at(a.T, mid, g.col) : (unsigned)((mid - g.r0) * m + g.col);
     if (MODE == kMarchPQ) bst2<kNT>(B.q, mown ? eq * 8u : kOOB, mq);
-    if (MODE == kMarchB) bst2<kNT>(B.r, mown ? melem<SM>(a, B, mid, g.col) * 8u : kOOB, mr);
+    if (MODE == kMarchB) bst2<SAUX>(B.r, mown ? melem<SM>(a, B, mid, g.col) * 8u : kOOB, mr);
   }
 }
 
-template <int MODE, int D, bool UP, bool SM>
+template <int MODE, int D, bool UP, bool SM, int PAUX = 0, int SAUX = kNT>
 __device__ __forceinline__ void march_walk(const CGArgs& a, const MGeom& g, const MBuf& B,
                                            MRow (&ring)[D],
                                            bool first, double bk, double ak,
@@ -2014,8 +2017,8 @@ __device__ __forceinline__ void march_walk(const CGArgs& a, const MGeom& g, cons
       // step count) and the prefetch past its end address rows outside the
       // view (loads return 0, stores are dropped) and finish no row
       const MRow R = ring[u];
-      march_load<MODE, SM>(a, g, B, UP ? g.rend - (j + D) : g.r0 - 1 + j + D, first, psrc, ring[u]);
-      march_step<MODE, UP, SM>(a, g, B, R, UP ? g.rend - j : g.r0 - 1 + j, first, bk, ak, pnew, s_dt,
+      march_load<MODE, SM, PAUX>(a, g, B, UP ? g.rend - (j + D) : g.r0 - 1 + j + D, first, psrc, ring[u]);
+      march_step<MODE, UP, SM, SAUX>(a, g, B, R, UP ? g.rend - j : g.r0 - 1 + j, first, bk, ak, pnew, s_dt,
                                s_rpos, s_rmap, s_w, W, acc);
     }
   }
@@ -2025,7 +2028,8 @@ __device__ __forceinline__ void march_walk(const CGArgs& a, const MGeom& g, cons
 template <int MODE, int D>
 constexpr int kMarchWavesPerEU = D == 2 && MODE == kMarchPQ ? 4 : 1;
 
-template <int MODE, bool SM = false, int D = kMarchDepth>
+// PAUX: cache policy of the last-use loads (P: p(k-1); B: r(k))
+template <int MODE, bool SM = false, int D = kMarchDepth, int PAUX = 0, int SAUX = kNT>
 __global__ __launch_bounds__(64 * kMarchWaves, (kMarchWavesPerEU<MODE, D>)) void k_cg_march(CGArgs a) {
   CGScalars* S = a.S;
   __shared__ double s_red[32];
@@ -2068,7 +2072,7 @@ __global__ __launch_bounds__(64 * kMarchWaves, (kMarchWavesPerEU<MODE, D>)) void
   if (active) {
 #pragma unroll
     for (int u = 0; u < D; ++u)
-      if (u < nsteps) march_load<MODE, SM>(a, g, B, up ? g.rend - u : g.r0 - 1 + u, first, psrc, ring[u]);
+      if (u < nsteps) march_load<MODE, SM, PAUX>(a, g, B, up ? g.rend - u : g.r0 - 1 + u, first, psrc, ring[u]);
   }
   if (S->done) return;
   if (threadIdx.x < kMaxForms) {
@@ -2081,8 +2085,8 @@ __global__ __launch_bounds__(64 * kMarchWaves, (kMarchWavesPerEU<MODE, D>)) void
   double acc[2] = {0.0, 0.0};
   if (active) {
     double* s_w = s_win[threadIdx.x >> 6];
-    if (up) march_walk<MODE, D, true, SM>(a, g, B, ring, first, bk, ak, psrc, pnew, s_dt, s_rpos, s_rmap, s_w, acc);
-    else march_walk<MODE, D, false, SM>(a, g, B, ring, first, bk, ak, psrc, pnew, s_dt, s_rpos, s_rmap, s_w, acc);
+    if (up) march_walk<MODE, D, true, SM, PAUX, SAUX>(a, g, B, ring, first, bk, ak, psrc, pnew, s_dt, s_rpos, s_rmap, s_w, acc);
+    else march_walk<MODE, D, false, SM, PAUX, SAUX>(a, g, B, ring, first, bk, ak, psrc, pnew, s_dt, s_rpos, s_rmap, s_w, acc);
     if (MODE == kMarchB && SM) {
       // strip-major q-free solve: x (row-major) += ak p(k) on the band's x
       // rows, after the walk (loads and stores inside it would put a
@@ -3376,6 +3380,8 @@ void launch_cg_spmv(perc_ctx* h, const CGArgs& a, int G) {
     }
     if (h->march) {
       if (h->qfree && a.sm && h->march_depth == 2) klaunch(h, k_cg_march<kMarchP, true, 2>, h->march_grid, 64 * kMarchWaves, st, a);
+      else if (h->qfree && a.sm && h->march_paux == 2 && h->march_saux == 0) klaunch(h, k_cg_march<kMarchP, true, 3, 2, 0>, h->march_grid, 64 * kMarchWaves, st, a);
+      else if (h->qfree && a.sm && h->march_paux == 2) klaunch(h, k_cg_march<kMarchP, true, 3, 2>, h->march_grid, 64 * kMarchWaves, st, a);
       else if (h->qfree && a.sm) klaunch(h, k_cg_march<kMarchP, true, 3>, h->march_grid, 64 * kMarchWaves, st, a);
       else if (h->qfree) klaunch(h, k_cg_march<kMarchP>, h->march_grid, 64 * kMarchWaves, st, a);
       else if (a.sm && h->march_depth == 2) klaunch(h, k_cg_march<kMarchPQ, true, 2>, h->march_grid, 64 * kMarchWaves, st, a);
@@ -3410,6 +3416,8 @@ void launch_cg_b(perc_ctx* h, const CGArgs& a, int G) {
     else klaunch(h, k_cg_rm<kMarchB, 512>, g, b, h->stream, a);
   } else if (h->march && h->qfree) {
     if (a.sm && h->march_bdepth == 2) klaunch(h, k_cg_march<kMarchB, true, 2>, h->march_grid, 64 * kMarchWaves, h->stream, a);
+    else if (a.sm && h->march_baux == 2 && h->march_saux == 0) klaunch(h, k_cg_march<kMarchB, true, 3, 2, 0>, h->march_grid, 64 * kMarchWaves, h->stream, a);
+    else if (a.sm && h->march_baux == 2) klaunch(h, k_cg_march<kMarchB, true, 3, 2>, h->march_grid, 64 * kMarchWaves, h->stream, a);
     else if (a.sm) klaunch(h, k_cg_march<kMarchB, true, 3>, h->march_grid, 64 * kMarchWaves, h->stream, a);
     else klaunch(h, k_cg_march<kMarchB>, h->march_grid, 64 * kMarchWaves, h->stream, a);
   } else if (h->stencil) {
@@ -3845,6 +3853,17 @@ void march_geometry(perc_ctx* h) {
   // the strip-major q-free march B (PERC_MARCH_BDEPTH, probes)
   h->march_bdepth = std::min(h->march_depth, 3);
   if (const char* e = getenv("PERC_MARCH_BDEPTH")) h->march_bdepth = std::min(std::max(atoi(e), 2), 3);
+  // nontemporal p(k-1) loads in the q-free P: the value is dead after the
+  // load, and streaming it past the caches leaves the Infinity Cache to
+  // the r and p(k) rows the next kernel re-reads (same-box A/B: P 0.0818
+  // vs 0.0830 ms, B 0.0795 vs 0.0808, profiles/r2_34_ab_load_policy.log);
+  // PERC_MARCH_PAUX = 0 / 16 (sc1) and PERC_MARCH_BAUX (B's r(k) loads) probe
+  h->march_paux = 2;
+  if (const char* e = getenv("PERC_MARCH_PAUX")) h->march_paux = atoi(e);
+  h->march_baux = 2;
+  if (const char* e = getenv("PERC_MARCH_BAUX")) h->march_baux = atoi(e);
+  h->march_saux = kNT;  // (probe: PERC_MARCH_SAUX = 0 plain p(k) / r(k+1) stores)
+  if (const char* e = getenv("PERC_MARCH_SAUX")) h->march_saux = atoi(e);
   if (g.m % kMarchW != 0 || g.n <= 2) return;
   const int spr = g.m / kMarchW, nrows = g.n - 2;
   h->march_h = march_rows_for(h, nrows);

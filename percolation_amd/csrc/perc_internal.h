@@ -167,6 +167,9 @@ struct perc_ctx {
   int march_h = 32;             // its band height (rows per wave)
   int march_depth = 3;          // rows its P+S kernel prefetches ahead
   int march_bdepth = 3;         // rows the q-free march B prefetches ahead
+  int march_paux = 2;           // cache policy of the q-free P's p(k-1) loads (nontemporal)
+  int march_baux = 2;           // and of the q-free B's r(k) loads (nontemporal)
+  int march_saux = 2;           // the q-free march's p(k) / r(k+1) stores (nontemporal; probe)
   int march_grid = 0;           // its workgroups
   int march_grid_max = 0;       // workgroups at band height 1 (reduction buffers)
   int march_rows_req = 0;       // perc_set_march_rows (0: auto)
