@@ -2024,13 +2024,14 @@ __device__ __forceinline__ void march_walk(const CGArgs& a, const MGeom& g, cons
   }
 }
 
-// (the P+S kernel with D = 2: at most 128 VGPRs, i.e. 4 waves per SIMD)
-template <int MODE, int D>
-constexpr int kMarchWavesPerEU = D == 2 && MODE == kMarchPQ ? 4 : 1;
+// (the P+S kernel and the strip-major q-free P / B with D = 2: at most 128
+// VGPRs, i.e. 4 waves per SIMD)
+template <int MODE, int D, bool SM = false>
+constexpr int kMarchWavesPerEU = D == 2 && (MODE == kMarchPQ || SM) ? 4 : 1;
 
 // PAUX: cache policy of the last-use loads (P: p(k-1); B: r(k))
 template <int MODE, bool SM = false, int D = kMarchDepth, int PAUX = 0, int SAUX = kNT>
-__global__ __launch_bounds__(64 * kMarchWaves, (kMarchWavesPerEU<MODE, D>)) void k_cg_march(CGArgs a) {
+__global__ __launch_bounds__(64 * kMarchWaves, (kMarchWavesPerEU<MODE, D, SM>)) void k_cg_march(CGArgs a) {
   CGScalars* S = a.S;
   __shared__ double s_red[32];
   __shared__ int s_flag[2];
@@ -3379,7 +3380,8 @@ void launch_cg_spmv(perc_ctx* h, const CGArgs& a, int G) {
       return;
     }
     if (h->march) {
-      if (h->qfree && a.sm && h->march_depth == 2) klaunch(h, k_cg_march<kMarchP, true, 2>, h->march_grid, 64 * kMarchWaves, st, a);
+      if (h->qfree && a.sm && h->march_depth == 2 && h->march_paux == 2) klaunch(h, k_cg_march<kMarchP, true, 2, 2>, h->march_grid, 64 * kMarchWaves, st, a);
+      else if (h->qfree && a.sm && h->march_depth == 2) klaunch(h, k_cg_march<kMarchP, true, 2>, h->march_grid, 64 * kMarchWaves, st, a);
       else if (h->qfree && a.sm && h->march_paux == 2 && h->march_saux == 0) klaunch(h, k_cg_march<kMarchP, true, 3, 2, 0>, h->march_grid, 64 * kMarchWaves, st, a);
       else if (h->qfree && a.sm && h->march_paux == 2) klaunch(h, k_cg_march<kMarchP, true, 3, 2>, h->march_grid, 64 * kMarchWaves, st, a);
       else if (h->qfree && a.sm) klaunch(h, k_cg_march<kMarchP, true, 3>, h->march_grid, 64 * kMarchWaves, st, a);
@@ -3415,7 +3417,8 @@ void launch_cg_b(perc_ctx* h, const CGArgs& a, int G) {
     else if (h->rm_w == 1024) klaunch(h, k_cg_rm<kMarchB, 1024>, g, b, h->stream, a);
     else klaunch(h, k_cg_rm<kMarchB, 512>, g, b, h->stream, a);
   } else if (h->march && h->qfree) {
-    if (a.sm && h->march_bdepth == 2) klaunch(h, k_cg_march<kMarchB, true, 2>, h->march_grid, 64 * kMarchWaves, h->stream, a);
+    if (a.sm && h->march_bdepth == 2 && h->march_baux == 2) klaunch(h, k_cg_march<kMarchB, true, 2, 2>, h->march_grid, 64 * kMarchWaves, h->stream, a);
+    else if (a.sm && h->march_bdepth == 2) klaunch(h, k_cg_march<kMarchB, true, 2>, h->march_grid, 64 * kMarchWaves, h->stream, a);
     else if (a.sm && h->march_baux == 2 && h->march_saux == 0) klaunch(h, k_cg_march<kMarchB, true, 3, 2, 0>, h->march_grid, 64 * kMarchWaves, h->stream, a);
     else if (a.sm && h->march_baux == 2) klaunch(h, k_cg_march<kMarchB, true, 3, 2>, h->march_grid, 64 * kMarchWaves, h->stream, a);
     else if (a.sm) klaunch(h, k_cg_march<kMarchB, true, 3>, h->march_grid, 64 * kMarchWaves, h->stream, a);

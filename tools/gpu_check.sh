@@ -27,6 +27,8 @@ for step in "$@"; do
     tests) run pytest_gpu 900 python -u -m pytest tests -m gpu -v -rs -x --timeout 300 --timeout-method thread ;;
     testsall) run pytest_gpu 900 python -m pytest tests -m gpu -q -rs ;;
     tests_march) run pytest_march 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread -k "march or division or resident" ;;
+    tests_march2) PERC_MARCH_DEPTH=2 run pytest_march2 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -k "march or slab" ;;
+    ab_depth) run ab_depth 800 bash tools/ab_depth4w.sh ;;
     tests_label) run pytest_label 900 python -u -m pytest tests/test_labeling_oracle.py tests/test_gpu_parity.py tests/test_threshold_scan.py -m gpu -x -v --timeout 300 --timeout-method thread ;;
     probe) run march_probe 600 python tools/march_probe.py ;;
     pmc_sq) run pmc_sq 600 bash tools/pmc_march.sh ;;
