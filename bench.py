@@ -12,6 +12,11 @@ is the RCCL all-reduce of the ensemble statistics.  Weak scaling.
 
   python bench.py [--gpus N --steps K --warmup W --L 4096 --p 0.6]
   torchrun --nproc-per-node N bench.py --gpus N ...
+
+`--gpus N` without a launcher starts the N rank processes itself
+(launch_ranks: RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* as
+torch.distributed.run sets them, before any GPU call in the parent); each
+rank then runs its share of the realisations on its GPU.
 """
 import argparse
 import json
@@ -275,6 +280,70 @@ def pmc_traffic(base, L_):
     return tot, src
 
 
+def launch_ranks(n, argv, stub=False):
+    """`bench.py --gpus N` without a launcher: start N rank processes (one per
+    GPU, RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set as torch.distributed.run
+    sets them) before anything here touches the GPU, wait for them and return
+    the first non-zero exit status.  The ranks inherit stdout, so rank 0's
+    JSON line is the only line printed.  If one rank fails the others are
+    ended (a rank left waiting in a collective would never return)."""
+    import signal
+    import socket
+    import subprocess
+    if not stub:
+        import torch  # device_count() does not initialise the GPU
+        ndev = torch.cuda.device_count()
+        if ndev < n:
+            log("bench.py --gpus %d: only %d visible GPU(s)" % (n, ndev))
+            return 2
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv, env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        for pr in list(live):
+            code = pr.poll()
+            if code is None:
+                continue
+            live.remove(pr)
+            if code != 0 and rc == 0:
+                rc = code if code > 0 else 128 - code
+                log("bench.py: rank %d exited with %d; ending the other ranks"
+                    % (procs.index(pr), code))
+                for o in live:
+                    o.send_signal(signal.SIGTERM)
+                deadline = time.time() + 20
+                for o in live:
+                    try:
+                        o.wait(max(deadline - time.time(), 0.1))
+                    except subprocess.TimeoutExpired:
+                        o.kill()
+        time.sleep(0.2)
+    return rc
+
+
+def launch_stub():
+    """--launch-stub: what a rank of launch_ranks() runs in the CPU test --
+    a gloo group of WORLD_SIZE ranks and one all-reduce, rank 0 printing the
+    JSON line (n_gpus = the world size the launcher set)."""
+    import torch
+    import torch.distributed as dist
+    dist.init_process_group("gloo")
+    world, rank = dist.get_world_size(), dist.get_rank()
+    t = torch.tensor([float(rank + 1)])
+    dist.all_reduce(t)
+    if rank == 0:
+        print(json.dumps({"n_gpus": world, "allreduce_sum": float(t.item()),
+                          "local_ranks": int(os.environ["LOCAL_WORLD_SIZE"])}), flush=True)
+    dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -316,12 +385,23 @@ def main():
     ap.add_argument("--slabs", type=int, default=1,
                     help="row slabs of each CG solve on this GPU (perc_set_slabs; SURVEY §8(f) 2)")
     ap.add_argument("--cpu-worker", nargs=6, default=None, help=argparse.SUPPRESS)
+    ap.add_argument("--launch-stub", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--cpu-cores", type=int, default=0,
                     help="processes of the all-cores CPU ensemble baseline (0: the host CPU "
                          "share, at most 16; -1: skip)")
     args = ap.parse_args()
     if args.cpu_worker:
         return cpu_worker(args.cpu_worker, args.cpu_iters)
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # one process per GPU, started here (the driver may call bench.py
+        # --gpus N directly instead of through torch.distributed.run)
+        return launch_ranks(args.gpus, sys.argv[1:], stub=args.launch_stub)
+    if args.launch_stub:
+        return launch_stub()
+    if args.gpus > 1 and int(os.environ.get("WORLD_SIZE", "1")) != args.gpus:
+        log("bench.py --gpus %d under a launcher with WORLD_SIZE=%s" % (args.gpus,
+                                                                         os.environ["WORLD_SIZE"]))
+        return 2
 
     import torch
     import torch.distributed as dist
@@ -738,4 +818,4 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main() or 0)

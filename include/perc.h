@@ -423,7 +423,9 @@ int perc_ensemble_trials(int ntrials, int ndev, int dev, int *ii_out);
 /* stats holds ndev slices of k doubles (device d's at stats[d*k]); on return
    every slice holds the element-wise sum over the devices (ncclAllReduce). */
 int perc_ensemble_allreduce(perc_ensemble *e, double *stats, int k);
-/* bond_cond over the devices: trial ii shuffles with tseed[ii-1] (REAL*4
+/* bond_cond over the devices: trial ii shuffles with tseed[ii-1] (tseed must
+   hold at least ntrials seeds; the reference's tseed(1000) caps numtrials at
+   1000, bond_cond.f:62-70, callers extend the stream past it) (REAL*4
    Fisher-Yates, bondc.f:162-174), computes the lowest-label conductance at
    grid points nbarr[0..) until a value <= 0, a repeat (hazard H3) or npts;
    outputs, per trial t = ii-1: nrows[t] rows at [t*npts + j] of gbot, gtop,

@@ -1072,6 +1072,127 @@ void or_linbcg(const double *sa, const int *ija, int n, const double *b,
   free(p); free(pp); free(r); free(rr); free(z); free(zz);
 }
 
+/* The same linbcg (itol 2), for fixtures at the BASELINE config sizes:
+   bitwise the literal or_linbcg's iterates on a bitwise-symmetric matrix,
+   several times faster, with snapshots of x at a list of tolerances from one
+   run.  Why it is the same arithmetic (Square/bondc.f:750-838):
+   * for a bitwise-symmetric sa, dsprstx (bondc.f:902-917) forms every b(j)
+     as diagonal first, then the rows i of column j in ascending order --
+     which are row j's columns in ascending order with the same values, i.e.
+     exactly dsprsax's sum.  So rr == r, pp == p, zz == z
+     bit for bit and one copy of each suffices;
+   * every per-element update and every SpMV row is computed as in or_linbcg,
+     only split over threads (no element's operation order changes);
+   * the three dot products stay serial sums in ascending j (the literal
+     association); ||r||^2 and the next iteration's z.r (both over the same
+     r) run as two serial chains side by side.
+   Snapshot c is x at the first iteration with !(err > check_tols[c])
+   (check_tols descending) -- the x a literal run with tol = check_tols[c]
+   returns.  Returns 0, or -1 (nothing computed) if sa is not bitwise
+   symmetric. */
+static int sym_entry(const double *sa, const int *ija, int row, int col,
+                     double *v) {
+  int k;
+  for (k = ija[row - 1]; k <= ija[row] - 1; k++)
+    if (ija[k - 1] == col) { *v = sa[k - 1]; return 1; }
+  return 0;
+}
+int or_linbcg_sym(const double *sa, const int *ija, int n, const double *b,
+                  double *x, int itmax, int nthreads, int ncheck,
+                  const double *check_tols, double *check_x, int *check_iter,
+                  double *check_err, int *iter_o, double *err_o,
+                  double *iter_err) {
+  double *p, *r, *z, *q;
+  double ak, akden, bk, bkden = 1.0, bknum = 0.0, bnrm, err = 0.0, rr2 = 0.0;
+  int j, iter = 0, c = 0, bad = 0;
+  double tol = ncheck > 0 ? check_tols[ncheck - 1] : 0.0;
+  if (nthreads < 1) nthreads = 1;
+#pragma omp parallel for schedule(static) num_threads(nthreads) reduction(|| : bad)
+  for (j = 1; j <= n; j++) {
+    int k;
+    for (k = ija[j - 1]; k <= ija[j] - 1; k++) {
+      double v;
+      if (!sym_entry(sa, ija, ija[k - 1], j, &v) || v != sa[k - 1] ||
+          (v == 0.0 && signbit(v) != signbit(sa[k - 1])))
+        bad = 1;
+    }
+  }
+  if (bad) return -1;
+  p = (double *)calloc((size_t)n, sizeof(double));
+  r = (double *)calloc((size_t)n, sizeof(double));
+  z = (double *)calloc((size_t)n, sizeof(double));
+  q = (double *)calloc((size_t)n, sizeof(double));
+  or_dsprsax(sa, ija, x, r, n); /* once, serial: bondc.f:759 */
+#pragma omp parallel for schedule(static) num_threads(nthreads)
+  for (j = 0; j < n; j++) { r[j] = b[j] - r[j]; z[j] = b[j] / sa[j]; }
+  bnrm = snrm2(n, z); /* itol 2: bondc.f:768-770 */
+#pragma omp parallel for schedule(static) num_threads(nthreads)
+  for (j = 0; j < n; j++) z[j] = r[j] / sa[j];
+  for (j = 0; j < n; j++) bknum = bknum + z[j] * r[j];
+  while (iter <= itmax) {
+    iter++;
+    /* bknum = z.rr was formed at the end of the previous iteration */
+    if (iter == 1) {
+#pragma omp parallel for schedule(static) num_threads(nthreads)
+      for (j = 0; j < n; j++) p[j] = z[j];
+    } else {
+      bk = bknum / bkden;
+#pragma omp parallel for schedule(static) num_threads(nthreads)
+      for (j = 0; j < n; j++) p[j] = bk * p[j] + z[j];
+    }
+    bkden = bknum;
+#pragma omp parallel for schedule(dynamic, 4096) num_threads(nthreads)
+    for (j = 1; j <= n; j++) { /* dsprsax row j, bondc.f:887-899 */
+      int k;
+      double acc = sa[j - 1] * p[j - 1];
+      for (k = ija[j - 1]; k <= ija[j] - 1; k++)
+        acc = acc + sa[k - 1] * p[ija[k - 1] - 1];
+      q[j - 1] = acc;
+    }
+    akden = 0.0;
+    for (j = 0; j < n; j++) akden = akden + q[j] * p[j];
+    ak = bknum / akden;
+#pragma omp parallel for schedule(static) num_threads(nthreads)
+    for (j = 0; j < n; j++) {
+      x[j] = x[j] + ak * p[j];
+      r[j] = r[j] - ak * q[j];
+      z[j] = r[j] / sa[j];
+    }
+    /* ||r||^2 (snrm, bondc.f:867-884) and the next iteration's z.rr: two
+       serial chains over the same r, each in ascending j */
+#pragma omp parallel sections num_threads(nthreads > 1 ? 2 : 1)
+    {
+#pragma omp section
+      {
+        double s = 0.0;
+        int i;
+        for (i = 0; i < n; i++) s = s + r[i] * r[i];
+        rr2 = s;
+      }
+#pragma omp section
+      {
+        double s = 0.0;
+        int i;
+        for (i = 0; i < n; i++) s = s + z[i] * r[i];
+        bknum = s;
+      }
+    }
+    err = sqrt(rr2) / bnrm;
+    if (iter_err) iter_err[iter - 1] = err;
+    while (c < ncheck && !(err > check_tols[c])) {
+      memcpy(check_x + (size_t)c * (size_t)n, x, sizeof(double) * (size_t)n);
+      check_iter[c] = iter;
+      check_err[c] = err;
+      c++;
+    }
+    if (!(err > tol)) break;
+  }
+  *iter_o = iter;
+  *err_o = err;
+  free(p); free(r); free(z); free(q);
+  return 0;
+}
+
 void or_currents(int lattice, int m, int n, int pbc, int nb, const int *b1,
                  const int *b2, const double *gval, const double *diag_full,
                  const double *vint, double Va, double thresh, int cur_rule,

@@ -128,6 +128,15 @@ void or_dsprstx(const double *sa, const int *ija, const double *x, double *b,
 void or_linbcg(const double *sa, const int *ija, int n, const double *b,
                double *x, int itol, double tol, int itmax, int *iter,
                double *err, double *iter_err);
+/* the same iterates (itol 2) on a bitwise-symmetric sa, threaded, with
+   snapshots of x (check_x[c*n..]) at the first iteration where err <=
+   check_tols[c] (descending; the last one stops the run).  -1 if sa is not
+   bitwise symmetric (see perc_oracle.c). */
+int or_linbcg_sym(const double *sa, const int *ija, int n, const double *b,
+                  double *x, int itmax, int nthreads, int ncheck,
+                  const double *check_tols, double *check_x, int *check_iter,
+                  double *check_err, int *iter_o, double *err_o,
+                  double *iter_err);
 /* Terminal currents (bondc.f:554-592): V from Vint; full-G sprsin with
    thresh (1e-10 in Fortran; 0 in MATLAB) restricted to the 2m boundary rows.
    cur_rule 0: Fortran (Ibot, Itop ascending), 1: MATLAB (Itop summed t..t-m+1)*/

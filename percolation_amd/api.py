@@ -659,7 +659,11 @@ class Ensemble:
     def bond_cond(self, master=58302, numtrials=1, Va=1.0, g0=1.0, tol=1e-8, itmax=2500):
         """The bond_cond trial loop over the devices; same records as
         bond_cond_grid, plus the all-reduced statistics (npts, 5)."""
-        seeds = trial_seeds(master, 1000)
+        if numtrials < 0:
+            raise ValueError("numtrials < 0")
+        # tseed(1..1000) as bond_cond.f:65-70, extended with the same stream past 1000
+        # trials (perc_ensemble_bond_cond reads tseed[0..numtrials-1])
+        seeds = trial_seeds(master, max(1000, numtrials))
         nbarr = pb_grid(self.lattice, self.nb)
         npts = len(nbarr)
         nrows, bfc, pl = _i32(numtrials), _i32(numtrials), _i32(numtrials)

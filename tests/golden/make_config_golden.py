@@ -20,7 +20,14 @@ and writes tests/golden/configs/<case>.json: the recipe, the partition
 fingerprint (sha256 of the canonical min-site id per site), Gtop, Gbot,
 iter, err and a decimated err history for both tolerances.
 
+Round 3 (--decades): the same iterates from one threaded run
+(or_linbcg_sym: bitwise the literal linbcg's on a symmetric system, checked
+against every solve the literal runs committed) with x snapshotted at
+1e-8 ... 1e-17, so each fixture carries its own convergence: the change of
+Gtop / Gbot over the last decades shows where the oracle has converged.
+
 Usage: python tests/golden/make_config_golden.py [case ...]   (CPU, minutes to hours)
+       GOLDEN_THREADS=k python tests/golden/make_config_golden.py --decades [case ...]
 """
 import hashlib
 import json
@@ -49,8 +56,17 @@ CASES = {
     "c4_sq2048_bond_p50": dict(lattice=0, L=2048, kind="bond", p=0.50, order="pcg64"),
     # the metric: 4096^2 square bond at 0.6 (bench.py's first realisation)
     "metric_sq4096_bond_p60": dict(lattice=0, L=4096, kind="bond", p=0.60, order="pcg64"),
+    # config 5's rule at a size the oracle solves: 1024^2 square mixed site-then-bond at
+    # ps = pb = 0.85 (spans; config 5's (0.593, 0.5) does not), the reference shuffles with
+    # sitebond.f's own seeds (sseed 143285 sites, bseed 43716 bonds; sitebond.f:129-189),
+    # ConductCalc.m:134-160 mixed rule
+    "c5m_sq1024_mixed_p85": dict(lattice=0, L=1024, kind="mixed", p=0.85, pb=0.85,
+                                 order="ref", sseed=143285, bseed=43716),
 }
 TOLS = (1e-8, 1e-13, 1e-14)
+# --decades: one threaded run of the same iterates (oracle or_linbcg_sym, bitwise the
+# literal linbcg's on these symmetric systems) snapshotting x at every tolerance here
+TOLS_DECADES = (1e-8, 1e-13, 1e-14, 1e-15, 1e-16, 1e-17)
 HIST_EVERY = 256
 
 
@@ -122,6 +138,23 @@ def label_case(rc, seed):
                     perccls=int(csize[perccln]), span_sites=int(np.sum(canon == canon[
                         b1[np.argmax(label == perccln)] - 1])))
         sysin = dict(b1=b1, b2=b2, gval=gval, rhs_rule=0, cur_rule=0, cur_thresh=1e-10)
+    elif rc["kind"] == "mixed":
+        b1, b2, o1, o2 = O.bond_order(lattice, L, L, 0, rc["bseed"])
+        nb = len(b1)
+        so = O.site_order(t, rc["sseed"])
+        ts, tb = int(rc["p"] * t), int(rc["pb"] * nb)
+        s, bl, csize, cln, maxcn, maxcs = O.label_sitebond(lattice, L, L, 0, b1, b2, so, ts, o1,
+                                                           o2, tb, literal=False)
+        perccln = lib.or_span_sites(L, L, s, csize, cln, 2 * L - 1)
+        if perccln <= 0:
+            return None
+        canon = canon_from_sites(s)
+        gval = O.f64(nb)
+        lib.or_bond_values(2, nb, b1, b2, bl, s, perccln, 1.0, 1e-12, gval)
+        info = dict(occupied_sites=ts, occupied_bonds=tb, cln=cln, maxcs=maxcs, perccln=perccln,
+                    perccls=int(csize[perccln]), span_sites=int(np.sum(s == perccln)),
+                    g0_bonds=int(np.sum(gval == -1.0)))
+        sysin = dict(b1=b1, b2=b2, gval=gval, rhs_rule=0, cur_rule=1, cur_thresh=0.0)
     else:
         order = O.site_order(t, seed)
         ts = int(rc["p"] * t)
@@ -144,6 +177,11 @@ def label_case(rc, seed):
 
 def find_seed(rc, kmax=64):
     O = _oracle()
+    if "sseed" in rc:  # fixed seeds (the mixed case)
+        r = label_case(rc, 0)
+        if r is None:
+            raise RuntimeError("no spanning cluster")
+        return 0, 0, r
     seeds = O.i32(kmax)
     O.lib().or_trial_seeds(MASTER, kmax, seeds)
     for ii in range(1, kmax + 1):
@@ -168,6 +206,45 @@ def solve(args):
     return case, tol, ii, seed, info, dict(
         gtop=r["gtop"], gbot=r["gbot"], iter=r["iter"], err=r["err"], seconds=time.time() - t0,
         err_history=hist)
+
+
+def decades(case):
+    """all of TOLS_DECADES from one threaded run; existing solves must match bitwise"""
+    rc = CASES[case]
+    O = _oracle()
+    ii, seed, (info, sysin) = find_seed(rc)
+    L = rc["L"]
+    t0 = time.time()
+    res, errs = O.conductance_decades(rc["lattice"], L, L, 0, sysin["b1"], sysin["b2"],
+                                      sysin["gval"], TOLS_DECADES, rhs_rule=sysin["rhs_rule"],
+                                      cur_rule=sysin["cur_rule"], cur_thresh=sysin["cur_thresh"],
+                                      threads=int(os.environ.get("GOLDEN_THREADS", 2)))
+    secs = time.time() - t0
+    path = os.path.join(OUT, case + ".json")
+    doc = json.load(open(path)) if os.path.exists(path) else {}
+    if doc:
+        assert doc["label"]["canon_sha256"] == info["canon_sha256"], case
+    solves = doc.setdefault("solves", {})
+    for r in res:
+        key = "%g" % r["tol"]
+        hist = [[int(k + 1), float(errs[k])] for k in range(HIST_EVERY - 1, r["iter"], HIST_EVERY)]
+        new = dict(gtop=r["gtop"], gbot=r["gbot"], iter=r["iter"], err=r["err"],
+                   true_res=r["true_res"], err_history=hist)
+        if key in solves:  # made by the literal linbcg: must be bitwise the same
+            old = solves[key]
+            for k in ("gtop", "gbot", "iter", "err", "err_history"):
+                assert old[k] == new[k], (case, key, k, old[k], new[k])
+            new["seconds"] = old.get("seconds")
+        solves[key] = new
+        print("%s tol %g: iter %d Gtop %.17g Gbot %.17g true_res %.3g"
+              % (case, r["tol"], r["iter"], r["gtop"], r["gbot"], r["true_res"]), flush=True)
+    doc.update(case=case, recipe=dict(rc, master=MASTER, ii=ii, tseed=seed),
+               oracle="oracle/perc_oracle.c (literal linbcg / or_linbcg_sym, O(N alpha) replay)",
+               label=dict(doc.get("label", {}), **info))
+    doc["decades_run"] = dict(seconds=secs, tols=list(TOLS_DECADES),
+                              threads=int(os.environ.get("GOLDEN_THREADS", 2)))
+    with open(path, "w") as f:
+        json.dump(doc, f, indent=1)
 
 
 def main(cases):
@@ -195,4 +272,9 @@ def main(cases):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1:] or list(CASES))
+    args = sys.argv[1:]
+    if args and args[0] == "--decades":
+        for c in args[1:] or list(CASES):
+            decades(c)
+    else:
+        main(args or list(CASES))

@@ -60,6 +60,8 @@ def lib():
         "or_dsprsax": (None, [_D, _I, _D, _D, i]),
         "or_dsprstx": (None, [_D, _I, _D, _D, i]),
         "or_linbcg": (None, [_D, _I, i, _D, _D, i, d, i, _IP, C.POINTER(d), C.c_void_p]),
+        "or_linbcg_sym": (i, [_D, _I, i, _D, _D, i, i, i, _D, _D, _I, _D, _IP, C.POINTER(d),
+                              C.c_void_p]),
         "or_currents": (None, [i, i, i, i, i, _I, _I, _D, _D, _D, d, d, i,
                                C.POINTER(d), C.POINTER(d)]),
         "or_bondc": (i, [i, i, i, i, d, i, d, d, i, d, i, C.c_void_p, C.c_void_p,
@@ -185,6 +187,48 @@ def conductance(lattice, m, n, pbc, b1, b2, gval, Va=1.0, itol=2, tol=1e-8,
     return dict(sa=sa[:k], ija=ija[:k], itemp=itemp, diag=diag, vint=vint,
                 iter=it.value, err=err.value, errs=errs[:it.value],
                 gtop=gt.value, gbot=gb.value, nnz=k)
+
+
+def conductance_decades(lattice, m, n, pbc, b1, b2, gval, tols, Va=1.0, itmax=10 ** 7,
+                        rhs_rule=0, cur_rule=0, cur_thresh=1e-10, threads=4):
+    """conductance() at several tolerances from one linbcg run
+    (or_linbcg_sym: the literal iterates, threaded; tols descending).
+    Returns a list of dicts (gtop, gbot, iter, err, true_res) per tolerance
+    and the per-iteration err history.  true_res = ||b - A x||_2 / ||b/d||_2
+    of the snapshot, recomputed in the same NR storage (diagnostic)."""
+    L = lib()
+    t = m * n
+    N = t - 2 * m
+    nb = len(b1)
+    nmax = N + 1 + 2 * nb + 8
+    sa, ija = f64(nmax), i32(nmax)
+    itemp, diag = f64(N), f64(t)
+    k = L.or_assemble(lattice, m, n, pbc, nb, b1, b2, gval, Va, 1e-16, rhs_rule,
+                      nmax, sa, ija, itemp, diag)
+    assert k > 0
+    tols = np.ascontiguousarray(sorted(tols, reverse=True), dtype=np.float64)
+    nc = len(tols)
+    vint = f64(N)
+    cx = f64(nc * N)
+    citer, cerr = i32(nc), f64(nc)
+    it, err = C.c_int(), C.c_double()
+    errs = f64(itmax + 2)
+    rc = L.or_linbcg_sym(sa, ija, N, itemp, vint, itmax, threads, nc, tols, cx, citer, cerr,
+                         C.byref(it), C.byref(err), errs.ctypes.data_as(C.c_void_p))
+    assert rc == 0, "matrix not bitwise symmetric"
+    bn = np.linalg.norm(itemp / sa[:N])
+    out = []
+    for c in range(nc):
+        xs = np.ascontiguousarray(cx[c * N:(c + 1) * N])
+        gt, gb = C.c_double(), C.c_double()
+        L.or_currents(lattice, m, n, pbc, nb, b1, b2, gval, diag, xs, Va, cur_thresh,
+                      cur_rule, C.byref(gt), C.byref(gb))
+        ax = f64(N)
+        L.or_dsprsax(sa, ija, xs, ax, N)
+        out.append(dict(tol=float(tols[c]), gtop=gt.value, gbot=gb.value, iter=int(citer[c]),
+                        err=float(cerr[c]),
+                        true_res=float(np.linalg.norm(itemp - ax) / bn)))
+    return out, errs[:it.value]
 
 
 def bondc(lattice, m, n, pbc, pb, seed, Va=1.0, g0=1.0, itmax=2500, tol=1e-8,

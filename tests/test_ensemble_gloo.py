@@ -8,6 +8,7 @@ cluster's conductance by the literal linbcg (Square/bondc.f:189-595).
 Also the device striping of perc_ensemble (include/perc.h) for 2-8 virtual
 devices: ii -> device (ii-1) mod ndev, every trial exactly once, rows
 gathered in ii order."""
+import json
 import os
 import socket
 
@@ -135,3 +136,34 @@ def test_grid_stats_shape():
     rows = [[dict(gtop=0.1, spanning=True, iter=3), dict(gtop=0.0, spanning=False, iter=0)]]
     acc = ensemble.grid_stats(rows, 3)
     assert acc.shape == (3, ensemble.NSTAT) and acc[0, 0] == 1 and acc[2, 0] == 0
+
+
+def _bench(*args, timeout=120):
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    return subprocess.run([sys.executable, os.path.join(repo, "bench.py")] + list(args),
+                          capture_output=True, text=True, timeout=timeout, env=env)
+
+
+def test_bench_gpus_n_launches_n_ranks():
+    """bench.py --gpus N without torch.distributed.run starts N rank processes
+    itself (bench.launch_ranks); here the ranks run the gloo stub: one group
+    of world size 2, one all-reduce, rank 0's JSON line relayed."""
+    r = _bench("--gpus", "2", "--launch-stub")
+    assert r.returncode == 0, r.stderr
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    out = json.loads(lines[0])
+    assert out == {"n_gpus": 2, "allreduce_sum": 3.0, "local_ranks": 2}
+
+
+def test_bench_gpus_n_more_than_visible_fails_loudly():
+    """--gpus N with fewer visible GPUs (none here) is an error, not a
+    one-GPU run reported as N"""
+    r = _bench("--gpus", "2")
+    assert r.returncode != 0
+    assert "visible GPU" in r.stderr
+    assert not [l for l in r.stdout.splitlines() if l.startswith("{")]
