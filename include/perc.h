@@ -347,12 +347,16 @@ int perc_set_march_rows(perc_ctx *h, int rows);
    lattices solve row-major.  PERC_MARCH_QFREE is in the default since
    late round 2 (strip-major: 0.164 vs 0.178 ms per iteration at L = 4096;
    row-major at L = 8192: 0.721 vs 0.737 ms).  Row slabs (perc_set_slabs)
-   always run the row-major q-storing march. */
+   always run the row-major q-storing march.  PERC_MARCH_DEFER (strip-
+   major q-free march): the dot products of a kernel are summed by every
+   workgroup of the next kernel instead of by a last-arriving workgroup at
+   the end of the kernel (bitwise the same totals, no reduction tail). */
 #define PERC_MARCH_QFREE 1
 #define PERC_MARCH_ALT 2
 #define PERC_MARCH_ROWS 4
 #define PERC_SOLVE_RESIDENT 8
 #define PERC_MARCH_STRIPS 16
+#define PERC_MARCH_DEFER 32
 #define PERC_MARCH_DEFAULT (PERC_MARCH_QFREE | PERC_MARCH_ALT | PERC_SOLVE_RESIDENT | PERC_MARCH_STRIPS)
 int perc_set_march_mode(perc_ctx *h, int mode);
 /* Random bond conductances (MATLAB/ConductCalc.m condtype 2, :38-47 and
@@ -367,7 +371,8 @@ int perc_set_bond_weights(perc_ctx *h, const double *w, long long n);
    row-march k_cg_rm), 3 (resident persistent solve k_cg_res), 4 (one-
    workgroup solve of a small system, k_cg_small: N <= 8192 under
    PERC_FMT_AUTO with PERC_SOLVE_RESIDENT set); out5[1] = bit 0: q-free
-   B, bit 1: strip-major solve layout; out5[2] = alternating
+   B, bit 1: strip-major solve layout, bit 2: deferred reductions
+   (PERC_MARCH_DEFER); out5[2] = alternating
    directions, out5[3] = band height, out5[4] = strip width (columns). */
 int perc_march_info(perc_ctx *h, int *out5);
 

@@ -180,6 +180,46 @@ __device__ bool publish_and_reduce(double (&v)[NV], double* partials, unsigned* 
   return true;
 }
 
+// The same totals as publish_and_reduce, formed by EVERY workgroup of the
+// next kernel from the partials the previous kernel's workgroups stored
+// (deferred reduction, k_cg_march<..., DEFER>): the group sums (wave
+// butterflies of kGroup partials) and the strided block sum of the group
+// sums are publish_and_reduce's, term for term, so the totals are bitwise
+// its totals.  The kernel boundary orders the partial stores before these
+// loads.  s_g holds NV * kDeferGroups doubles.
+constexpr int kDeferGroups = 64;  // nwg <= kDeferGroups * kGroup
+template <int NV>
+__device__ void gather_totals(const double* partials, int nwg, double (&tot)[NV], double* s_g,
+                              double* s_red) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  const int ngroups = red_groups(nwg);
+  for (int grp = wid; grp < ngroups; grp += nw) {
+    const int g0 = grp * kGroup, gn = min(kGroup, nwg - g0);
+#pragma unroll
+    for (int j = 0; j < NV; ++j) {
+      double w = lane < gn ? load_sc1(&partials[(size_t)j * nwg + g0 + lane]) : 0.0;
+      w = wave_sum(w);
+      if (lane == 0) s_g[j * kDeferGroups + grp] = w;
+    }
+  }
+  __syncthreads();
+  double acc[NV];
+#pragma unroll
+  for (int j = 0; j < NV; ++j) acc[j] = 0.0;
+  for (int i = threadIdx.x; i < ngroups; i += blockDim.x) {
+#pragma unroll
+    for (int j = 0; j < NV; ++j) acc[j] = acc[j] + s_g[j * kDeferGroups + i];
+  }
+  block_sum<NV>(acc, s_red);
+  if (threadIdx.x == 0) {
+#pragma unroll
+    for (int j = 0; j < NV; ++j) s_red[16 + j] = acc[j];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < NV; ++j) tot[j] = s_red[16 + j];
+}
+
 // ---------------------------------------------------------------------------
 // Lattice build
 __global__ void k_forward_count(Geom g, int* fc /* t+2 */) {
@@ -2029,11 +2069,22 @@ __device__ __forceinline__ void march_walk(const CGArgs& a, const MGeom& g, cons
 template <int MODE, int D, bool SM = false>
 constexpr int kMarchWavesPerEU = D == 2 && (MODE == kMarchPQ || SM) ? 4 : 1;
 
-// PAUX: cache policy of the last-use loads (P: p(k-1); B: r(k))
-template <int MODE, bool SM = false, int D = kMarchDepth, int PAUX = 0, int SAUX = kNT>
+// PAUX: cache policy of the last-use loads (P: p(k-1); B: r(k)).
+// DEFER (q-free P / B, one round of workgroups): no reduction at the end of
+// the kernel -- each workgroup stores its block partial and exits; every
+// workgroup of the NEXT kernel sums the partials (gather_totals, bitwise
+// publish_and_reduce's totals) while its first rows are in flight.  The
+// scalar epilogues move with them: B(k) forms ak from P(k)'s partials, P(k+1)
+// forms bk, err and the stop decision of iteration k from B(k)'s (workgroup
+// 0 records them in S); bknum of iteration k lives in S->bkn[k & 1] so no
+// kernel overwrites a scalar its own workgroups still read.
+template <int MODE, bool SM = false, int D = kMarchDepth, int PAUX = 0, int SAUX = kNT,
+          bool DEFER = false>
 __global__ __launch_bounds__(64 * kMarchWaves, (kMarchWavesPerEU<MODE, D, SM>)) void k_cg_march(CGArgs a) {
+  static_assert(!DEFER || MODE != kMarchPQ, "deferred reduction: q-free P / B only");
   CGScalars* S = a.S;
   __shared__ double s_red[32];
+  __shared__ double s_g[DEFER ? 2 * kDeferGroups : 1];
   __shared__ int s_flag[2];
   __shared__ unsigned s_rpos[kMaxForms], s_rmap[kMaxForms];
   __shared__ double2 s_dt[kDiagTab];
@@ -2082,7 +2133,49 @@ __global__ __launch_bounds__(64 * kMarchWaves, (kMarchWavesPerEU<MODE, D, SM>)) 
   }
   load_dtab(a.St, s_dt);
   __syncthreads();
-  const double bk = S->bk, ak = S->ak;
+  double bk, ak;
+  if constexpr (DEFER) {
+    const bool rec = lb == 0 && threadIdx.x == 0;  // the workgroup that records the scalars
+    if (MODE == kMarchP) {
+      ak = 0.0;  // (x is updated in B)
+      if (k >= 2) {
+        // B(k-1)'s epilogue (k_cg_b / the march B): bk, err, stop of iteration k-1
+        double tot[2];
+        gather_totals<2>(a.partials + a.pstride, gridDim.x, tot, s_g, s_red);
+        const double bkn_prev = S->bkn[(k - 1) & 1];
+        const int kk = k - 1;
+        const double err = sqrt(tot[1]) / S->bnrm;
+        const bool stop = !(err > S->tol) || kk >= S->itmax + 1;
+        bk = tot[0] / bkn_prev;
+        if (rec) {
+          S->bk = bk;
+          S->bknum = tot[0];
+          S->bkn[k & 1] = tot[0];
+          S->err = err;
+          if (kk - 1 < a.err_hist_cap) a.err_hist[kk - 1] = err;
+          S->iter = kk;
+          if (stop) S->done = 1;
+        }
+        if (stop) return;
+      } else {
+        bk = 0.0;
+        if (rec) S->bkn[1] = S->bknum;  // z.r of the prologue (k_cg_init)
+      }
+    } else {
+      // P(k)'s epilogue: ak = bknum / q.p
+      double tot[1];
+      gather_totals<1>(a.partials, gridDim.x, tot, s_g, s_red);
+      bk = 0.0;
+      ak = S->bkn[k & 1] / tot[0];
+      if (rec) {
+        S->akden = tot[0];
+        S->ak = ak;
+      }
+    }
+  } else {
+    bk = S->bk;
+    ak = S->ak;
+  }
   double acc[2] = {0.0, 0.0};
   if (active) {
     double* s_w = s_win[threadIdx.x >> 6];
@@ -2103,6 +2196,22 @@ __global__ __launch_bounds__(64 * kMarchWaves, (kMarchWavesPerEU<MODE, D, SM>)) 
         *reinterpret_cast<double2*>(a.x + i) = xv;
       }
     }
+  }
+  if constexpr (DEFER) {
+    // the block partial only; the next kernel forms the totals
+    if (MODE != kMarchB) {
+      double v[1] = {acc[0]};
+      block_sum<1>(v, s_red);
+      if (threadIdx.x == 0) store_sc1(&a.partials[lb], v[0]);
+    } else {
+      block_sum<2>(acc, s_red);
+      if (threadIdx.x == 0) {
+        double* pt = a.partials + a.pstride;
+        store_sc1(&pt[lb], acc[0]);
+        store_sc1(&pt[(size_t)gridDim.x + lb], acc[1]);
+      }
+    }
+    return;
   }
   if (MODE != kMarchB) {
     double v[1] = {acc[0]}, tot[1];
@@ -3358,6 +3467,25 @@ void klaunch(perc_ctx* h, K kern, dim3 g, dim3 b, hipStream_t st, const CGArgs& 
   }
 }
 
+// the strip-major q-free march P or B with 3 rows prefetched and
+// nontemporal last-use loads (the default solve): store policy SAUX
+// (nontemporal 2, plain 0, write-through sc1 16, sc1 nt 18) and the
+// deferred reduction
+template <int MODE, int SAUX>
+void launch_march_sm2(perc_ctx* h, hipStream_t st, const CGArgs& a) {
+  if (h->march_defer) klaunch(h, k_cg_march<MODE, true, 3, 2, SAUX, true>, h->march_grid, 64 * kMarchWaves, st, a);
+  else klaunch(h, k_cg_march<MODE, true, 3, 2, SAUX, false>, h->march_grid, 64 * kMarchWaves, st, a);
+}
+template <int MODE>
+void launch_march_sm(perc_ctx* h, hipStream_t st, const CGArgs& a) {
+  switch (h->march_saux) {
+    case 0: launch_march_sm2<MODE, 0>(h, st, a); break;
+    case 16: launch_march_sm2<MODE, 16>(h, st, a); break;
+    case 18: launch_march_sm2<MODE, 18>(h, st, a); break;
+    default: launch_march_sm2<MODE, kNT>(h, st, a); break;
+  }
+}
+
 // S(k), or the fused P(k)+S(k) of the tiled stencil kernel
 void launch_cg_spmv(perc_ctx* h, const CGArgs& a, int G) {
   if (h->fused) {
@@ -3382,8 +3510,7 @@ void launch_cg_spmv(perc_ctx* h, const CGArgs& a, int G) {
     if (h->march) {
       if (h->qfree && a.sm && h->march_depth == 2 && h->march_paux == 2) klaunch(h, k_cg_march<kMarchP, true, 2, 2>, h->march_grid, 64 * kMarchWaves, st, a);
       else if (h->qfree && a.sm && h->march_depth == 2) klaunch(h, k_cg_march<kMarchP, true, 2>, h->march_grid, 64 * kMarchWaves, st, a);
-      else if (h->qfree && a.sm && h->march_paux == 2 && h->march_saux == 0) klaunch(h, k_cg_march<kMarchP, true, 3, 2, 0>, h->march_grid, 64 * kMarchWaves, st, a);
-      else if (h->qfree && a.sm && h->march_paux == 2) klaunch(h, k_cg_march<kMarchP, true, 3, 2>, h->march_grid, 64 * kMarchWaves, st, a);
+      else if (h->qfree && a.sm && h->march_paux == 2) launch_march_sm<kMarchP>(h, st, a);
       else if (h->qfree && a.sm) klaunch(h, k_cg_march<kMarchP, true, 3>, h->march_grid, 64 * kMarchWaves, st, a);
       else if (h->qfree) klaunch(h, k_cg_march<kMarchP>, h->march_grid, 64 * kMarchWaves, st, a);
       else if (a.sm && h->march_depth == 2) klaunch(h, k_cg_march<kMarchPQ, true, 2>, h->march_grid, 64 * kMarchWaves, st, a);
@@ -3419,8 +3546,7 @@ void launch_cg_b(perc_ctx* h, const CGArgs& a, int G) {
   } else if (h->march && h->qfree) {
     if (a.sm && h->march_bdepth == 2 && h->march_baux == 2) klaunch(h, k_cg_march<kMarchB, true, 2, 2>, h->march_grid, 64 * kMarchWaves, h->stream, a);
     else if (a.sm && h->march_bdepth == 2) klaunch(h, k_cg_march<kMarchB, true, 2>, h->march_grid, 64 * kMarchWaves, h->stream, a);
-    else if (a.sm && h->march_baux == 2 && h->march_saux == 0) klaunch(h, k_cg_march<kMarchB, true, 3, 2, 0>, h->march_grid, 64 * kMarchWaves, h->stream, a);
-    else if (a.sm && h->march_baux == 2) klaunch(h, k_cg_march<kMarchB, true, 3, 2>, h->march_grid, 64 * kMarchWaves, h->stream, a);
+    else if (a.sm && h->march_baux == 2) launch_march_sm<kMarchB>(h, h->stream, a);
     else if (a.sm) klaunch(h, k_cg_march<kMarchB, true, 3>, h->march_grid, 64 * kMarchWaves, h->stream, a);
     else klaunch(h, k_cg_march<kMarchB>, h->march_grid, 64 * kMarchWaves, h->stream, a);
   } else if (h->stencil) {
@@ -3865,8 +3991,9 @@ void march_geometry(perc_ctx* h) {
   if (const char* e = getenv("PERC_MARCH_PAUX")) h->march_paux = atoi(e);
   h->march_baux = 2;
   if (const char* e = getenv("PERC_MARCH_BAUX")) h->march_baux = atoi(e);
-  h->march_saux = kNT;  // (probe: PERC_MARCH_SAUX = 0 plain p(k) / r(k+1) stores)
+  h->march_saux = kNT;  // (probe: PERC_MARCH_SAUX = 0 plain, 16 sc1, 18 sc1 nt stores)
   if (const char* e = getenv("PERC_MARCH_SAUX")) h->march_saux = atoi(e);
+
   if (g.m % kMarchW != 0 || g.n <= 2) return;
   const int spr = g.m / kMarchW, nrows = g.n - 2;
   h->march_h = march_rows_for(h, nrows);
@@ -3948,6 +4075,14 @@ void select_format(perc_ctx* h) {
   // strip-major march's whole-array buffer views also need < 2 GB
   h->strips = h->march && (h->march_mode & PERC_MARCH_STRIPS) &&
               (size_t)h->N * sizeof(double) <= kLargeVector;
+  // deferred reductions (the strip-major q-free march with its default
+  // cache policies; every workgroup sums every partial, gather_totals:
+  // one round of workgroups); PERC_MARCH_DEFER=0/1 overrides the mode bit
+  // for A/B probes
+  bool defer = (h->march_mode & PERC_MARCH_DEFER) != 0;
+  if (const char* e = getenv("PERC_MARCH_DEFER")) defer = atoi(e) != 0;
+  h->march_defer = defer && h->qfree && h->strips && h->march_depth == 3 && h->march_paux == 2 &&
+                   h->march_baux == 2 && h->march_grid <= kDeferGroups * kGroup;
 }
 
 // strip-major copies of r (into the q buffer: r and q swap roles for the
@@ -4750,6 +4885,15 @@ hipError_t dev_bench(perc_ctx* h, int which, int reps, double* ms) {
   hs.itmax = 1 << 30;
   hs.iter = 1;
   a.kiter = 2;
+  // the deferred-reduction march takes its scalars (and the stop) from the
+  // previous kernel's partials, which a probe of one kernel alone does not
+  // keep meaningful: probes run the in-kernel reduction
+  struct DeferOff {
+    perc_ctx* h;
+    int was;
+    ~DeferOff() { h->march_defer = was; }
+  } defer_off{h, h->march_defer};
+  h->march_defer = 0;
   // the solve's layout for the CG kernels (the plain SpMV probe stays row-major)
   if (h->strips && (which == 1 || which == 2 || which == 5)) HIP_TRY(to_strips(h, a));
   HIP_TRY(hipMemcpyAsync(d.scal, &hs, sizeof(hs), hipMemcpyHostToDevice, st));

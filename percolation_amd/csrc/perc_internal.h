@@ -60,6 +60,7 @@ struct CGScalars {
   int done;      // set once err <= tol or iter > itmax
   int pad[3];
   double part[4];  // row slabs: this slab's raw partials (q.p, z.r, r.r, ||D^-1 b||^2)
+  double bkn[2];   // deferred-reduction march: bknum of iteration k in bkn[k & 1]
 };
 
 struct DeviceBuffers {
@@ -170,6 +171,7 @@ struct perc_ctx {
   int march_paux = 2;           // cache policy of the q-free P's p(k-1) loads (nontemporal)
   int march_baux = 2;           // and of the q-free B's r(k) loads (nontemporal)
   int march_saux = 2;           // the q-free march's p(k) / r(k+1) stores (nontemporal; probe)
+  int march_defer = 0;          // q-free strip-major march: reductions deferred to the next kernel
   int march_grid = 0;           // its workgroups
   int march_grid_max = 0;       // workgroups at band height 1 (reduction buffers)
   int march_rows_req = 0;       // perc_set_march_rows (0: auto)

@@ -66,7 +66,8 @@ CASES = {
 TOLS = (1e-8, 1e-13, 1e-14)
 # --decades: one threaded run of the same iterates (oracle or_linbcg_sym, bitwise the
 # literal linbcg's on these symmetric systems) snapshotting x at every tolerance here
-TOLS_DECADES = (1e-8, 1e-13, 1e-14, 1e-15, 1e-16, 1e-17)
+TOLS_DECADES = tuple(float(t) for t in os.environ.get(
+    "GOLDEN_TOLS", "1e-8,1e-13,1e-14,1e-15,1e-16,1e-17").split(","))
 HIST_EVERY = 256
 
 
