@@ -94,4 +94,29 @@ build sq_sb_perc              Square/sb_perc.f 's/pscount = 42 /pscount = 4 /' '
 build tri_sb_perc             Triangular/sb_perc.f 's/pscount = 51 /pscount = 4 /' 's/iter = 100/iter = 5/' 's/0.50d+00+(0.01d+00\*(i-1))/0.60d+00+(0.10d+00*(i-1))/'
 build sq_bs_perc              Square/bs_perc.f 's/pbcount = 71 /pbcount = 5 /' 's/iter = 1000/iter = 8/' 's/0.30d+00+(0.01d+00\*(i-1))/0.55d+00+(0.10d+00*(i-1))/'
 build tri_bs_perc             Triangular/bs_perc.f 's/pbcount = 71 /pbcount = 5 /' 's/iter = 1000/iter = 8/' 's/0.30d+00+(0.01d+00\*(i-1))/0.55d+00+(0.10d+00*(i-1))/'
+# Route 1 of INTEGRATION.md (link check, CPU side): the reference program with
+# its embedded Numerical Recipes block (from SUBROUTINE sprsin to the end of
+# the file: Square/bondc.f:723-917, Square/bond_cond.f:623-818) removed,
+# linked against libperc's NR symbols (sprsin_, linbcg_, dsprsax_, ...) and
+# its own COMMON /mat/.  Running it needs a GPU; the compiled reference never
+# travels to the GPU box, so these binaries only prove the relink.
+PERC_LIB=${PERC_LIB:-$HERE/../percolation_amd}
+build_nr() {
+  local name=$1 src=$2
+  shift 2
+  local f="$TMP/$name.f"
+  cp "$REF/Fortran/$src" "$f"
+  for e in "$@"; do sed -i "$e" "$f"; done
+  sed -i '/SUBROUTINE sprsin/,$d' "$f"
+  "$FLANG" -O2 "$f" "$TMP/gfrand.o" -L"$PERC_LIB" -lperc -Wl,-rpath,"$PERC_LIB" \
+    -L"$GF" -lgfortran -Wl,-rpath,"$GF" -o "$OUT/$name"
+}
+if [ -e "$PERC_LIB/libperc.so" ]; then
+  build_nr nr_sq_bondc        Square/bondc.f
+  build_nr nr_sq_bondc_p60    Square/bondc.f 's/pb = 0.50d+00/pb = 0.60d+00/'
+  build_nr nr_sq_bond_cond    Square/bond_cond.f
+  build_nr nr_tri_bondc       Triangular/bondc.f
+else
+  echo "build_ref.sh: $PERC_LIB/libperc.so not built; skipping the Route-1 relink" >&2
+fi
 echo "reference binaries in $OUT"

@@ -100,7 +100,10 @@ int upload(int n, const std::vector<int>& rowptr, const std::vector<int>& col,
            const std::vector<double>& val, const std::vector<double>& diag) {
   if (!g_nr) {
     int ndev = 0;
-    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return PERC_ENODEV;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) {
+      set_error("no HIP device (the NR routines run on the GPU; there is no CPU fallback)");
+      return PERC_ENODEV;
+    }
     g_nr = new perc_ctx();
     g_nr->device = 0;
     hipSetDevice(0);
@@ -124,6 +127,15 @@ int upload(int n, const std::vector<int>& rowptr, const std::vector<int>& col,
   if (e == hipSuccess)
     e = hipMemcpy(g_nr->d.diag, diag.data(), sizeof(double) * n, hipMemcpyHostToDevice);
   return hip_status(e, "nr upload");
+}
+
+// The reference `pause`s with a message where these routines fail
+// (bondc.f:737, 777, 891, 906); a caller that never reads perc_nr_status()
+// still sees the failure on stderr instead of a silent zero result.
+void nr_report(const char* who) {
+  if (g_status == PERC_OK) return;
+  std::fprintf(stderr, "[perc] %s failed (status %d)%s%s\n", who, g_status,
+               perc_last_error()[0] ? ": " : "", perc_last_error());
 }
 
 }  // namespace
@@ -156,6 +168,7 @@ void sprsin_(double* a, int* n_, int* np_, double* thresh_, int* nmax_, double* 
         ++k;
         if (k > nmax) {  // 'nmax too small in sprsin'
           g_status = PERC_ENMAX;
+          nr_report("sprsin_ (nmax too small)");
           return;
         }
         sa[k - 1] = v;
@@ -194,14 +207,18 @@ static void spmv_nr(double* sa, int* ija, double* x, double* b, int n, bool tran
   g_nr->assembled = true;
   g_status = hip_status(dev_spmv(g_nr, x, b), "dsprsax_");
 }
+static void spmv_nr_checked(double* sa, int* ija, double* x, double* b, int n, bool transpose) {
+  spmv_nr(sa, ija, x, b, n, transpose);
+  nr_report(transpose ? "dsprstx_" : "dsprsax_");
+}
 
 // b = A x (bondc.f:887-899)
 void dsprsax_(double* sa, int* ija, double* x, double* b, int* n) {
-  spmv_nr(sa, ija, x, b, *n, false);
+  spmv_nr_checked(sa, ija, x, b, *n, false);
 }
 // b = A' x (bondc.f:902-917)
 void dsprstx_(double* sa, int* ija, double* x, double* b, int* n) {
-  spmv_nr(sa, ija, x, b, *n, true);
+  spmv_nr_checked(sa, ija, x, b, *n, true);
 }
 
 void atimes_(int* n, double* x, double* r, int* itrnsp) {  // bondc.f:841-852
@@ -211,7 +228,7 @@ void atimes_(int* n, double* x, double* r, int* itrnsp) {  // bondc.f:841-852
     g_status = PERC_ESTATE;
     return;
   }
-  spmv_nr(sa, ija, x, r, *n, *itrnsp != 0);
+  spmv_nr_checked(sa, ija, x, r, *n, *itrnsp != 0);
 }
 
 void asolve_(int* n, double* b, double* x, int* itrnsp) {  // bondc.f:855-864
@@ -240,8 +257,15 @@ double snrm_(int* n, double* sx, int* itol) {  // bondc.f:867-884
 // linbcg (bondc.f:750-838) on the device: the reference's BiCG with the
 // Jacobi preconditioner reduces to PCG for the symmetric conductance matrix;
 // rr/pp/zz and dsprstx are then bitwise equal to r/p/z and dsprsax.
+static void linbcg_impl(int* n_, double* b, double* x, int* itol, double* tol, int* itmax,
+                        int* iter, double* err);
 void linbcg_(int* n_, double* b, double* x, int* itol, double* tol, int* itmax, int* iter,
              double* err) {
+  linbcg_impl(n_, b, x, itol, tol, itmax, iter, err);
+  nr_report("linbcg_");
+}
+static void linbcg_impl(int* n_, double* b, double* x, int* itol, double* tol, int* itmax,
+                        int* iter, double* err) {
   std::lock_guard<std::mutex> lk(g_nr_mu);
   const int n = *n_;
   *iter = 0;

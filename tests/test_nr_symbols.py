@@ -162,3 +162,35 @@ def test_nr_symbols_from_fortran(tmp_path):
                         C.byref(gb))
     assert abs(gt.value - md["gtop"]) <= 1e-10 * md["gtop"]
     assert abs(gb.value - md["gbot"]) <= 1e-6 * md["gbot"]
+
+
+def test_route1_relink_of_the_reference_program():
+    """INTEGRATION.md Route 1 as a link check (CPU, this container only:
+    the compiled reference never travels to the GPU box).  oracle/build_ref.sh
+    (build_nr) compiles the reference's own Square/bondc.f with its embedded
+    NR block (SUBROUTINE sprsin to the end, bondc.f:723-917) removed and links
+    it against libperc: the NR symbols must come from libperc, COMMON /mat/
+    from the program.  Without a GPU the program runs its labeling and then
+    linbcg_ fails loudly (the reference `pause`s where NR fails) instead of
+    solving on the CPU."""
+    import shutil
+    import subprocess
+    import tempfile
+    exe = os.path.join(REPO, "oracle", "_ref", "nr_sq_bondc_p60")
+    if not os.path.exists(exe):
+        pytest.skip("reference relink not built (oracle/build_ref.sh; /root/reference absent)")
+    dyn = subprocess.run(["readelf", "-d", exe], capture_output=True, text=True).stdout
+    assert "[libperc.so]" in dyn
+    syms = subprocess.run(["nm", "-D", exe], capture_output=True, text=True).stdout.split("\n")
+    und = {l.split()[-1] for l in syms if l.strip().startswith("U ")}
+    assert {"linbcg_", "sprsin_", "dsprsax_"} <= und
+    assert any(l.split()[-1] == "mat_" and " B " in l for l in syms if l.strip())
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is present: the relinked reference would solve; run it by hand")
+    d = tempfile.mkdtemp()
+    try:
+        r = subprocess.run([exe], cwd=d, capture_output=True, text=True, timeout=120)
+        assert "[perc] linbcg_ failed" in r.stderr and "no HIP device" in r.stderr
+    finally:
+        shutil.rmtree(d)
