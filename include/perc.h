@@ -350,13 +350,18 @@ int perc_set_march_rows(perc_ctx *h, int rows);
    always run the row-major q-storing march.  PERC_MARCH_DEFER (strip-
    major q-free march): the dot products of a kernel are summed by every
    workgroup of the next kernel instead of by a last-arriving workgroup at
-   the end of the kernel (bitwise the same totals, no reduction tail). */
+   the end of the kernel (bitwise the same totals, no reduction tail).
+   PERC_MARCH_SLOTS (strip-major q-free march): one workgroup per CU and
+   round, and the bands sized by the round a wave runs in (the first round
+   on a CU streams fastest), so every wave finishes at about the same time;
+   same per-row arithmetic, dot products over other wave partials. */
 #define PERC_MARCH_QFREE 1
 #define PERC_MARCH_ALT 2
 #define PERC_MARCH_ROWS 4
 #define PERC_SOLVE_RESIDENT 8
 #define PERC_MARCH_STRIPS 16
 #define PERC_MARCH_DEFER 32
+#define PERC_MARCH_SLOTS 64
 #define PERC_MARCH_DEFAULT (PERC_MARCH_QFREE | PERC_MARCH_ALT | PERC_SOLVE_RESIDENT | PERC_MARCH_STRIPS)
 int perc_set_march_mode(perc_ctx *h, int mode);
 /* Random bond conductances (MATLAB/ConductCalc.m condtype 2, :38-47 and

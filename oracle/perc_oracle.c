@@ -1097,11 +1097,24 @@ static int sym_entry(const double *sa, const int *ija, int row, int col,
     if (ija[k - 1] == col) { *v = sa[k - 1]; return 1; }
   return 0;
 }
+/* dot_order 1 (not the reference's): the same solver with its three dot
+   products summed in descending j instead -- one other association, to
+   measure how far the converged Gtop / Gbot of the reference solver itself
+   move when only the order of its sums changes. */
+static double dot_ord(int n, const double *u, const double *v, int desc) {
+  double s = 0.0;
+  int i;
+  if (desc)
+    for (i = n - 1; i >= 0; i--) s = s + u[i] * v[i];
+  else
+    for (i = 0; i < n; i++) s = s + u[i] * v[i];
+  return s;
+}
 int or_linbcg_sym(const double *sa, const int *ija, int n, const double *b,
                   double *x, int itmax, int nthreads, int ncheck,
                   const double *check_tols, double *check_x, int *check_iter,
                   double *check_err, int *iter_o, double *err_o,
-                  double *iter_err) {
+                  double *iter_err, int dot_order) {
   double *p, *r, *z, *q;
   double ak, akden, bk, bkden = 1.0, bknum = 0.0, bnrm, err = 0.0, rr2 = 0.0;
   int j, iter = 0, c = 0, bad = 0;
@@ -1128,7 +1141,7 @@ int or_linbcg_sym(const double *sa, const int *ija, int n, const double *b,
   bnrm = snrm2(n, z); /* itol 2: bondc.f:768-770 */
 #pragma omp parallel for schedule(static) num_threads(nthreads)
   for (j = 0; j < n; j++) z[j] = r[j] / sa[j];
-  for (j = 0; j < n; j++) bknum = bknum + z[j] * r[j];
+  bknum = dot_ord(n, z, r, dot_order);
   while (iter <= itmax) {
     iter++;
     /* bknum = z.rr was formed at the end of the previous iteration */
@@ -1149,8 +1162,7 @@ int or_linbcg_sym(const double *sa, const int *ija, int n, const double *b,
         acc = acc + sa[k - 1] * p[ija[k - 1] - 1];
       q[j - 1] = acc;
     }
-    akden = 0.0;
-    for (j = 0; j < n; j++) akden = akden + q[j] * p[j];
+    akden = dot_ord(n, q, p, dot_order);
     ak = bknum / akden;
 #pragma omp parallel for schedule(static) num_threads(nthreads)
     for (j = 0; j < n; j++) {
@@ -1163,19 +1175,9 @@ int or_linbcg_sym(const double *sa, const int *ija, int n, const double *b,
 #pragma omp parallel sections num_threads(nthreads > 1 ? 2 : 1)
     {
 #pragma omp section
-      {
-        double s = 0.0;
-        int i;
-        for (i = 0; i < n; i++) s = s + r[i] * r[i];
-        rr2 = s;
-      }
+      rr2 = dot_ord(n, r, r, dot_order);
 #pragma omp section
-      {
-        double s = 0.0;
-        int i;
-        for (i = 0; i < n; i++) s = s + z[i] * r[i];
-        bknum = s;
-      }
+      bknum = dot_ord(n, z, r, dot_order);
     }
     err = sqrt(rr2) / bnrm;
     if (iter_err) iter_err[iter - 1] = err;

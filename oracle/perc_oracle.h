@@ -136,7 +136,7 @@ int or_linbcg_sym(const double *sa, const int *ija, int n, const double *b,
                   double *x, int itmax, int nthreads, int ncheck,
                   const double *check_tols, double *check_x, int *check_iter,
                   double *check_err, int *iter_o, double *err_o,
-                  double *iter_err);
+                  double *iter_err, int dot_order);
 /* Terminal currents (bondc.f:554-592): V from Vint; full-G sprsin with
    thresh (1e-10 in Fortran; 0 in MATLAB) restricted to the 2m boundary rows.
    cur_rule 0: Fortran (Ibot, Itop ascending), 1: MATLAB (Itop summed t..t-m+1)*/

@@ -1176,6 +1176,8 @@ struct TileGeom {
   int rm_h;                // band height of the workgroup row-march kernel
 };
 
+constexpr int kMaxSlotRounds = 4;
+
 struct CGArgs {
   CsrView A;
   StencilView St;
@@ -1206,6 +1208,12 @@ struct CGArgs {
   CGScalars* S;
   double* err_hist;
   int err_hist_cap;
+  unsigned long long* mtrace;  // march phase probe (PERC_MARCH_TRACE): 4 words per wave
+  // slot-weighted bands of the strip-major march (PERC_MARCH_SLOTS): wslots
+  // workgroup rounds (the workgroups a CU holds at once); the band a wave
+  // walks is sized by the weight of its round, cumulative in wcum[0..wslots]
+  int wslots;
+  int wcum[kMaxSlotRounds + 1];
 };
 
 // diagonal of rows i, i+1 (i even) from the CSR diag array or the stencil code
@@ -2078,10 +2086,14 @@ constexpr int kMarchWavesPerEU = D == 2 && (MODE == kMarchPQ || SM) ? 4 : 1;
 // forms bk, err and the stop decision of iteration k from B(k)'s (workgroup
 // 0 records them in S); bknum of iteration k lives in S->bkn[k & 1] so no
 // kernel overwrites a scalar its own workgroups still read.
+// TR: phase probe -- lane 0 of every wave stores {kernel entry, walk end,
+// exit, hardware id} wall-clock stamps (100 MHz) into a.mtrace[4 w ..]
 template <int MODE, bool SM = false, int D = kMarchDepth, int PAUX = 0, int SAUX = kNT,
-          bool DEFER = false>
+          bool DEFER = false, bool TR = false>
 __global__ __launch_bounds__(64 * kMarchWaves, (kMarchWavesPerEU<MODE, D, SM>)) void k_cg_march(CGArgs a) {
   static_assert(!DEFER || MODE != kMarchPQ, "deferred reduction: q-free P / B only");
+  const unsigned long long tr_t0 = TR ? wall_clock64() : 0ull;
+  unsigned long long tr_t1 = 0ull;
   CGScalars* S = a.S;
   __shared__ double s_red[32];
   __shared__ double s_g[DEFER ? 2 * kDeferGroups : 1];
@@ -2104,10 +2116,36 @@ __global__ __launch_bounds__(64 * kMarchWaves, (kMarchWavesPerEU<MODE, D, SM>)) 
   // the compiler cannot prove uniform gets a readfirstlane loop per access)
   const int w = __builtin_amdgcn_readfirstlane(lb * kMarchWaves + (threadIdx.x >> 6));
   const int spr = m / kMarchW;
-  const int band = w / spr, strip = w - band * spr;
+  int band, strip;
   MGeom g;
-  g.r0 = band * H;
-  g.rend = min(g.r0 + H, nrows);
+  if (a.wslots > 0) {
+    // slot-weighted bands (PERC_MARCH_SLOTS).  Workgroups are dealt one per
+    // CU per round: blockIdx / CUs is the round -- the CU slot -- a
+    // workgroup runs in (observed on MI355X, speed only: any placement
+    // gives the same rows and results).  The waves of the first round get
+    // memory requests served first and stream fastest (L = 4096, equal
+    // bands: 49 / 56 / 66 us per walk for rounds 0 / 1 / 2,
+    // profiles/r3_2_mtrace_static_summary.txt), so the rows of every cycle
+    // of wslots neighbouring bands are split by per-round weights: all
+    // waves finish together instead of the CU idling while its last round
+    // drains.  Band b = q * wslots + round, so neighbouring bands still
+    // alternate walk directions.
+    const int ns = a.wslots, ncu = gridDim.x / ns;
+    const int sl = blockIdx.x / ncu, i = blockIdx.x - sl * ncu;
+    const int v = __builtin_amdgcn_readfirstlane(i * kMarchWaves + (threadIdx.x >> 6));
+    const int Q = ncu * kMarchWaves / spr;  // cycles per strip
+    const int q = v / spr;
+    strip = v - q * spr;
+    band = q * ns + sl;
+    const int c0 = (int)((long long)q * nrows / Q), hc = (int)((long long)(q + 1) * nrows / Q) - c0;
+    g.r0 = c0 + hc * a.wcum[sl] / a.wcum[ns];
+    g.rend = c0 + hc * a.wcum[sl + 1] / a.wcum[ns];
+  } else {
+    band = w / spr;
+    strip = w - band * spr;
+    g.r0 = band * H;
+    g.rend = min(g.r0 + H, nrows);
+  }
   const bool active = g.r0 < nrows;  // wave-uniform
   const int c0 = strip * kMarchW;
   g.col = c0 + 2 * lane;
@@ -2197,6 +2235,18 @@ __global__ __launch_bounds__(64 * kMarchWaves, (kMarchWavesPerEU<MODE, D, SM>)) 
       }
     }
   }
+  if constexpr (TR) {
+    tr_t1 = wall_clock64();
+    if (lane == 0) {
+      unsigned hw;
+      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+      unsigned xcc;
+      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+      a.mtrace[4 * (size_t)w + 0] = tr_t0;
+      a.mtrace[4 * (size_t)w + 1] = tr_t1;
+      a.mtrace[4 * (size_t)w + 3] = ((unsigned long long)xcc << 32) | hw;
+    }
+  }
   if constexpr (DEFER) {
     // the block partial only; the next kernel forms the totals
     if (MODE != kMarchB) {
@@ -2240,6 +2290,9 @@ __global__ __launch_bounds__(64 * kMarchWaves, (kMarchWavesPerEU<MODE, D, SM>)) 
         if (!(err > S->tol) || kk >= S->itmax + 1) S->done = 1;
       }
     }
+  }
+  if constexpr (TR) {
+    if (lane == 0) a.mtrace[4 * (size_t)w + 2] = wall_clock64();
   }
 }
 
@@ -3451,6 +3504,9 @@ CGArgs make_cg_args(perc_ctx* h) {
   a.S = h->d.scal;
   a.err_hist = h->d.err_hist;
   a.err_hist_cap = h->d.err_hist_cap;
+  a.mtrace = nullptr;
+  a.wslots = 0;
+  for (int i = 0; i <= kMaxSlotRounds; ++i) a.wcum[i] = 0;
   return a;
 }
 
@@ -3469,21 +3525,24 @@ void klaunch(perc_ctx* h, K kern, dim3 g, dim3 b, hipStream_t st, const CGArgs& 
 
 // the strip-major q-free march P or B with 3 rows prefetched and
 // nontemporal last-use loads (the default solve): store policy SAUX
-// (nontemporal 2, plain 0, write-through sc1 16, sc1 nt 18) and the
-// deferred reduction
+// (nontemporal 2, plain 0), the deferred reduction
 template <int MODE, int SAUX>
 void launch_march_sm2(perc_ctx* h, hipStream_t st, const CGArgs& a) {
-  if (h->march_defer) klaunch(h, k_cg_march<MODE, true, 3, 2, SAUX, true>, h->march_grid, 64 * kMarchWaves, st, a);
-  else klaunch(h, k_cg_march<MODE, true, 3, 2, SAUX, false>, h->march_grid, 64 * kMarchWaves, st, a);
+  const int grid = a.wslots > 0 ? h->wm_grid : h->march_grid;
+  if constexpr (SAUX == kNT) {
+    if (a.mtrace && !h->march_defer) {  // phase probe (PERC_MARCH_TRACE)
+      klaunch(h, k_cg_march<MODE, true, 3, 2, SAUX, false, true>, grid, 64 * kMarchWaves, st, a);
+      return;
+    }
+  }
+  if (h->march_defer) klaunch(h, k_cg_march<MODE, true, 3, 2, SAUX, true>, grid, 64 * kMarchWaves, st, a);
+  else klaunch(h, k_cg_march<MODE, true, 3, 2, SAUX, false>, grid, 64 * kMarchWaves, st, a);
 }
 template <int MODE>
 void launch_march_sm(perc_ctx* h, hipStream_t st, const CGArgs& a) {
-  switch (h->march_saux) {
-    case 0: launch_march_sm2<MODE, 0>(h, st, a); break;
-    case 16: launch_march_sm2<MODE, 16>(h, st, a); break;
-    case 18: launch_march_sm2<MODE, 18>(h, st, a); break;
-    default: launch_march_sm2<MODE, kNT>(h, st, a); break;
-  }
+  // (write-through sc1 stores, 16 / 18, measured 2-3 % slower: r3_ab1)
+  if (h->march_saux == 0) launch_march_sm2<MODE, 0>(h, st, a);
+  else launch_march_sm2<MODE, kNT>(h, st, a);
 }
 
 // S(k), or the fused P(k)+S(k) of the tiled stencil kernel
@@ -3991,13 +4050,46 @@ void march_geometry(perc_ctx* h) {
   if (const char* e = getenv("PERC_MARCH_PAUX")) h->march_paux = atoi(e);
   h->march_baux = 2;
   if (const char* e = getenv("PERC_MARCH_BAUX")) h->march_baux = atoi(e);
-  h->march_saux = kNT;  // (probe: PERC_MARCH_SAUX = 0 plain, 16 sc1, 18 sc1 nt stores)
+  h->march_saux = kNT;  // (probe: PERC_MARCH_SAUX = 0 plain stores)
   if (const char* e = getenv("PERC_MARCH_SAUX")) h->march_saux = atoi(e);
+
 
   if (g.m % kMarchW != 0 || g.n <= 2) return;
   const int spr = g.m / kMarchW, nrows = g.n - 2;
   h->march_h = march_rows_for(h, nrows);
   h->march_grid = cdiv(spr * cdiv(nrows, h->march_h), kMarchWaves);
+  // slot-weighted bands (strip-major q-free march): one workgroup per CU
+  // and round, bands cycling over the rounds; weights = the rounds' relative
+  // streaming rates with equal bands (PERC_MARCH_SLOTW="100,88,75" or
+  // "100:88:75", "0": off)
+  h->wm_slots = 0;
+  h->wm_grid = 0;
+  {
+    int cus = 0, per_cu = 0;
+    hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, h->device);
+    hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_cg_march<kMarchP, true, 3, 2>, 64 * kMarchWaves, 0);
+    int wts[kMaxSlotRounds] = {100, 88, 75, 64};
+    int nw = per_cu;
+    if (const char* e = getenv("PERC_MARCH_SLOTW")) {
+      nw = 0;
+      for (const char* c = e; *c && nw < kMaxSlotRounds;) {
+        wts[nw++] = atoi(c);
+        while (*c && *c != ',' && *c != ':') ++c;
+        if (*c) ++c;
+      }
+      if (nw == 1 && wts[0] == 0) nw = 0;  // "0": off
+    }
+    const long long waves = (long long)cus * kMarchWaves;
+    bool ok = cus > 0 && per_cu >= 2 && per_cu <= kMaxSlotRounds && nw == per_cu &&
+              waves % spr == 0 && (waves / spr) * per_cu <= nrows;
+    for (int i = 0; ok && i < per_cu; ++i) ok = wts[i] > 0;
+    if (ok) {
+      h->wm_slots = per_cu;
+      h->wm_grid = cus * per_cu;
+      h->wm_cum[0] = 0;
+      for (int i = 0; i < per_cu; ++i) h->wm_cum[i + 1] = h->wm_cum[i] + wts[i];
+    }
+  }
   // workgroup row-march: the widest strip of 2048 / 1024 / 512 columns that
   // divides m, the tallest band (32 .. 2 rows) that gives >= kRmMinGroups
   // workgroups (two per CU), or the requested height
@@ -4083,6 +4175,10 @@ void select_format(perc_ctx* h) {
   if (const char* e = getenv("PERC_MARCH_DEFER")) defer = atoi(e) != 0;
   h->march_defer = defer && h->qfree && h->strips && h->march_depth == 3 && h->march_paux == 2 &&
                    h->march_baux == 2 && h->march_grid <= kDeferGroups * kGroup;
+  // slot-weighted bands (to_strips applies them); PERC_MARCH_SLOTS=0/1 overrides
+  bool slots = (h->march_mode & PERC_MARCH_SLOTS) != 0;
+  if (const char* e = getenv("PERC_MARCH_SLOTS")) slots = atoi(e) != 0;
+  h->march_slots = slots && h->strips && h->qfree && h->wm_slots > 0;
 }
 
 // strip-major copies of r (into the q buffer: r and q swap roles for the
@@ -4100,6 +4196,11 @@ hipError_t to_strips(perc_ctx* h, CGArgs& a) {
   a.St.code = d.code_sm;
   a.sm = 1;
   a.bx = 1;  // x (row-major) is updated in B: k_cg_b, or the q-free march B
+  if (h->march_slots && h->qfree && !h->march_defer && h->march_depth == 3 && h->march_paux == 2 &&
+      h->march_baux == 2 && h->march_bdepth == 3) {
+    a.wslots = h->wm_slots;
+    for (int i = 0; i <= h->wm_slots; ++i) a.wcum[i] = h->wm_cum[i];
+  }
   return hipSuccess;
 }
 
@@ -4317,11 +4418,24 @@ hipError_t dev_solve(perc_ctx* h, int itol, double tol, int itmax, bool x0_zero,
   int done_iters = 0;
   // kernel timing samples every kTimeEvery-th iteration of a chunk
   constexpr int kTimeEvery = 8;
+  // phase probe (PERC_MARCH_TRACE=<csv>): per-wave stamps of the P and B
+  // launches of iterations PERC_MARCH_TRACE_IT (default 1000) .. +3
+  const char* mtpath = getenv("PERC_MARCH_TRACE");
+  const int mt_it = getenv("PERC_MARCH_TRACE_IT") ? atoi(getenv("PERC_MARCH_TRACE_IT")) : 1000;
+  constexpr int kMtN = 4;  // traced iterations
+  unsigned long long* mtbuf = nullptr;
+  const size_t mtwaves = (size_t)h->march_grid * kMarchWaves;
+  if (mtpath && h->march && a.sm && h->qfree) {
+    HIP_TRY(dmalloc(&mtbuf, (size_t)2 * kMtN * 4 * mtwaves));
+    HIP_TRY(hipMemsetAsync(mtbuf, 0, (size_t)2 * kMtN * 4 * mtwaves * 8, st));
+  }
   while (true) {
     for (int j = 0; j < chunk; ++j) {
       const bool tm = T.enabled && j % kTimeEvery == 0;
       hipEvent_t* ev = tm ? &T.ev[kEv * j] : nullptr;
       a.kiter = (int)(launched + j + 1);
+      const int mti = a.kiter - mt_it;
+      a.mtrace = mtbuf && mti >= 0 && mti < kMtN ? mtbuf + (size_t)2 * mti * 4 * mtwaves : nullptr;
       if (!h->fused) {
         if (tm) h->ev_next[0] = ev[0], h->ev_next[1] = ev[1];
         if (ST) klaunch(h, k_cg_p<true>, G, kBlock, st, a);
@@ -4332,7 +4446,9 @@ hipError_t dev_solve(perc_ctx* h, int itol, double tol, int itmax, bool x0_zero,
       launch_cg_spmv(h, a, G);
       HIP_TRY(dbg_sync(st, "k_cg_spmv"));
       if (tm) h->ev_next[0] = ev[4], h->ev_next[1] = ev[5];
+      if (a.mtrace) a.mtrace += 4 * mtwaves;
       launch_cg_b(h, a, G);
+      a.mtrace = nullptr;
       HIP_TRY(dbg_sync(st, "k_cg_b"));
       h->ev_next[0] = h->ev_next[1] = nullptr;
     }
@@ -4368,6 +4484,24 @@ hipError_t dev_solve(perc_ctx* h, int itol, double tol, int itmax, bool x0_zero,
     k_cg_xfinal<<<G, kBlock, 0, st>>>(a);
     e = dbg_sync(st, "k_cg_xfinal");
     if (e == hipSuccess) e = hipStreamSynchronize(st);
+  }
+  if (mtbuf) {
+    std::vector<unsigned long long> tr((size_t)2 * kMtN * 4 * mtwaves);
+    if (e == hipSuccess) e = hipMemcpy(tr.data(), mtbuf, tr.size() * 8, hipMemcpyDeviceToHost);
+    (void)hipFree(mtbuf);
+    if (FILE* fo = e == hipSuccess ? fopen(mtpath, "a") : nullptr) {
+      fprintf(fo, "# m=%d nrows=%d band_rows=%d grid=%d waves=%zu (wall clock ticks, 100 MHz)\n"
+                  "iter,kernel,wave,t_entry,t_walk_end,t_exit,xcc,hw_id\n",
+              h->g.m, h->g.n - 2, h->march_h, h->march_grid, mtwaves);
+      for (int it = 0; it < kMtN; ++it)
+        for (int kb = 0; kb < 2; ++kb)
+          for (size_t wv = 0; wv < mtwaves; ++wv) {
+            const unsigned long long* v = &tr[((size_t)(2 * it + kb) * mtwaves + wv) * 4];
+            fprintf(fo, "%d,%s,%zu,%llu,%llu,%llu,%llu,%llu\n", mt_it + it, kb ? "B" : "P", wv, v[0],
+                    v[1], v[2], v[3] >> 32, v[3] & 0xffffffffull);
+          }
+      fclose(fo);
+    }
   }
   *iter = hsp->iter;
   *err = hsp->err;

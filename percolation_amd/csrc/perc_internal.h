@@ -172,6 +172,10 @@ struct perc_ctx {
   int march_baux = 2;           // and of the q-free B's r(k) loads (nontemporal)
   int march_saux = 2;           // the q-free march's p(k) / r(k+1) stores (nontemporal; probe)
   int march_defer = 0;          // q-free strip-major march: reductions deferred to the next kernel
+  int march_slots = 0;          // q-free strip-major march: slot-weighted bands
+  int wm_slots = 0;             // slot-weighted bands: workgroup rounds (0: not available)
+  int wm_grid = 0;              // their grid (CUs x rounds)
+  int wm_cum[5] = {0, 0, 0, 0, 0};  // cumulative round weights
   int march_grid = 0;           // its workgroups
   int march_grid_max = 0;       // workgroups at band height 1 (reduction buffers)
   int march_rows_req = 0;       // perc_set_march_rows (0: auto)

@@ -28,6 +28,7 @@ Gtop / Gbot over the last decades shows where the oracle has converged.
 
 Usage: python tests/golden/make_config_golden.py [case ...]   (CPU, minutes to hours)
        GOLDEN_THREADS=k python tests/golden/make_config_golden.py --decades [case ...]
+       GOLDEN_THREADS=k python tests/golden/make_config_golden.py --assoc [case ...]
 """
 import hashlib
 import json
@@ -248,6 +249,37 @@ def decades(case):
         json.dump(doc, f, indent=1)
 
 
+def assoc(case):
+    """--assoc: the same solver with its dot products summed in descending
+    order (or_linbcg_sym dot_order 1), to the fixture's decades: how far the
+    reference solver's own converged Gtop / Gbot move when only the order of
+    its sums changes (the floor under any re-associated solve, the GPU's
+    included).  Stored as doc["assoc_desc"][tol]."""
+    rc = CASES[case]
+    O = _oracle()
+    ii, seed, (info, sysin) = find_seed(rc)
+    L = rc["L"]
+    path = os.path.join(OUT, case + ".json")
+    doc = json.load(open(path))
+    assert doc["label"]["canon_sha256"] == info["canon_sha256"], case
+    tols = sorted((float(t) for t in doc["solves"] if float(t) <= 1e-13), reverse=True)
+    t0 = time.time()
+    res, _ = O.conductance_decades(rc["lattice"], L, L, 0, sysin["b1"], sysin["b2"], sysin["gval"],
+                                   tols, rhs_rule=sysin["rhs_rule"], cur_rule=sysin["cur_rule"],
+                                   cur_thresh=sysin["cur_thresh"],
+                                   threads=int(os.environ.get("GOLDEN_THREADS", 2)), dot_order=1)
+    doc["assoc_desc"] = {"%g" % r["tol"]: dict(gtop=r["gtop"], gbot=r["gbot"], iter=r["iter"],
+                                              err=r["err"]) for r in res}
+    doc["assoc_desc_seconds"] = time.time() - t0
+    for r in res:
+        ref = doc["solves"]["%g" % r["tol"]]
+        print("%s desc tol %g: iter %d (asc %d) Gtop %.3e Gbot %.3e rel to asc" % (
+            case, r["tol"], r["iter"], ref["iter"], abs(r["gtop"] - ref["gtop"]) / ref["gtop"],
+            abs(r["gbot"] - ref["gbot"]) / ref["gbot"]), flush=True)
+    with open(path, "w") as f:
+        json.dump(doc, f, indent=1)
+
+
 def main(cases):
     os.makedirs(OUT, exist_ok=True)
     def done(c, tol):
@@ -277,5 +309,8 @@ if __name__ == "__main__":
     if args and args[0] == "--decades":
         for c in args[1:] or list(CASES):
             decades(c)
+    elif args and args[0] == "--assoc":
+        for c in args[1:] or list(CASES):
+            assoc(c)
     else:
         main(args or list(CASES))

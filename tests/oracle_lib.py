@@ -61,7 +61,7 @@ def lib():
         "or_dsprstx": (None, [_D, _I, _D, _D, i]),
         "or_linbcg": (None, [_D, _I, i, _D, _D, i, d, i, _IP, C.POINTER(d), C.c_void_p]),
         "or_linbcg_sym": (i, [_D, _I, i, _D, _D, i, i, i, _D, _D, _I, _D, _IP, C.POINTER(d),
-                              C.c_void_p]),
+                              C.c_void_p, i]),
         "or_currents": (None, [i, i, i, i, i, _I, _I, _D, _D, _D, d, d, i,
                                C.POINTER(d), C.POINTER(d)]),
         "or_bondc": (i, [i, i, i, i, d, i, d, d, i, d, i, C.c_void_p, C.c_void_p,
@@ -190,12 +190,14 @@ def conductance(lattice, m, n, pbc, b1, b2, gval, Va=1.0, itol=2, tol=1e-8,
 
 
 def conductance_decades(lattice, m, n, pbc, b1, b2, gval, tols, Va=1.0, itmax=10 ** 7,
-                        rhs_rule=0, cur_rule=0, cur_thresh=1e-10, threads=4):
+                        rhs_rule=0, cur_rule=0, cur_thresh=1e-10, threads=4, dot_order=0):
     """conductance() at several tolerances from one linbcg run
     (or_linbcg_sym: the literal iterates, threaded; tols descending).
     Returns a list of dicts (gtop, gbot, iter, err, true_res) per tolerance
     and the per-iteration err history.  true_res = ||b - A x||_2 / ||b/d||_2
-    of the snapshot, recomputed in the same NR storage (diagnostic)."""
+    of the snapshot, recomputed in the same NR storage (diagnostic).
+    dot_order 1: the dot products summed in descending order (not the
+    reference's association; measures the solver's own association spread)."""
     L = lib()
     t = m * n
     N = t - 2 * m
@@ -214,7 +216,7 @@ def conductance_decades(lattice, m, n, pbc, b1, b2, gval, tols, Va=1.0, itmax=10
     it, err = C.c_int(), C.c_double()
     errs = f64(itmax + 2)
     rc = L.or_linbcg_sym(sa, ija, N, itemp, vint, itmax, threads, nc, tols, cx, citer, cerr,
-                         C.byref(it), C.byref(err), errs.ctypes.data_as(C.c_void_p))
+                         C.byref(it), C.byref(err), errs.ctypes.data_as(C.c_void_p), dot_order)
     assert rc == 0, "matrix not bitwise symmetric"
     bn = np.linalg.norm(itemp / sa[:N])
     out = []

@@ -24,6 +24,7 @@ def main():
     ap.add_argument("--ii", type=int, default=1)
     ap.add_argument("--rounds", type=int, default=2)
     ap.add_argument("--tol", type=float, default=1e-8)
+    ap.add_argument("--itmax", type=int, default=60000)
     ap.add_argument("--variants", default="DEFER=0;DEFER=1")
     args = ap.parse_args()
     import percolation_amd as P
@@ -46,7 +47,7 @@ def main():
                 ctx.set_kernel_timing(True)
                 ctx.kernel_stats(reset=True)
                 t0 = time.perf_counter()
-                c = ctx.conductance(tol=args.tol, itmax=10 ** 6)
+                c = ctx.conductance(tol=args.tol, itmax=args.itmax)
                 wall = time.perf_counter() - t0
                 ks = ctx.kernel_stats(reset=True)
             for k_ in v:
