@@ -362,7 +362,8 @@ int perc_set_march_rows(perc_ctx *h, int rows);
 #define PERC_MARCH_STRIPS 16
 #define PERC_MARCH_DEFER 32
 #define PERC_MARCH_SLOTS 64
-#define PERC_MARCH_DEFAULT (PERC_MARCH_QFREE | PERC_MARCH_ALT | PERC_SOLVE_RESIDENT | PERC_MARCH_STRIPS)
+#define PERC_MARCH_DEFAULT \
+  (PERC_MARCH_QFREE | PERC_MARCH_ALT | PERC_SOLVE_RESIDENT | PERC_MARCH_STRIPS | PERC_MARCH_SLOTS)
 int perc_set_march_mode(perc_ctx *h, int mode);
 /* Random bond conductances (MATLAB/ConductCalc.m condtype 2, :38-47 and
    :94-97): the bonds of the spanning cluster get G = -g0 * w[id] instead of
@@ -377,7 +378,9 @@ int perc_set_bond_weights(perc_ctx *h, const double *w, long long n);
    workgroup solve of a small system, k_cg_small: N <= 8192 under
    PERC_FMT_AUTO with PERC_SOLVE_RESIDENT set); out5[1] = bit 0: q-free
    B, bit 1: strip-major solve layout, bit 2: deferred reductions
-   (PERC_MARCH_DEFER); out5[2] = alternating
+   (PERC_MARCH_DEFER), bit 3: slot-weighted bands (PERC_MARCH_SLOTS; past
+   the Infinity Cache the row-major P kernel's one round of bands);
+   out5[2] = alternating
    directions, out5[3] = band height, out5[4] = strip width (columns). */
 int perc_march_info(perc_ctx *h, int *out5);
 

@@ -694,6 +694,11 @@ __device__ __forceinline__ double bond_value(int rule, int id, int s, int c, int
   return in ? (w ? -g0 * w[id] : -g0) : -leak;
 }
 
+// CSR: also the NR-ordered CSR values and the diagonal array (the CSR and
+// split formats, perc_get_system, the probes).  The stencil solvers read
+// only code and rhs, so dev_assemble writes the CSR copy only when a
+// consumer asks for it (ensure_csr): 2 + 8 B per row instead of 50.
+template <bool CSR>
 __global__ void k_assemble(Geom g, int N, const int* bond_first, const uint8_t* bocc,
                            const uint8_t* socc, const int* parent, const int* rowptr,
                            double* val, double* diag, double* rhs, uint16_t* code, int* sflag,
@@ -707,7 +712,7 @@ __global__ void k_assemble(Geom g, int N, const int* bond_first, const uint8_t* 
   int nbr[6];
   const int cnt = sorted_neighbours(g, s, nbr);
   double rowsum = 0.0;  // bondc.f:500-504: ascending-column dense row sum
-  int k = rowptr[i];
+  int k = CSR ? rowptr[i] : 0;
   unsigned bits = 0;
   for (int j = 0; j < cnt; ++j) {
     const int c = nbr[j];
@@ -719,7 +724,7 @@ __global__ void k_assemble(Geom g, int N, const int* bond_first, const uint8_t* 
     const double gv = bond_value(rule, id, s, c, ps, bocc, socc, span_root, g0, leak, w);
     if (gv == -g0) bits |= 1u << j;
     rowsum = rowsum + gv;
-    if (c > m && c <= t - m) val[k++] = gv;
+    if (CSR && c > m && c <= t - m) val[k++] = gv;
   }
   int form = -1;  // the row's form: same count and offsets
   for (int f = 0; f < F.nforms && form < 0; ++f) {
@@ -738,7 +743,7 @@ __global__ void k_assemble(Geom g, int N, const int* bond_first, const uint8_t* 
       atomicOr(sflag, 4);
   }
   code[i] = (uint16_t)(bits | (unsigned)cnt << 8 | (unsigned)form << 11);
-  diag[i] = -rowsum;
+  if (CSR) diag[i] = -rowsum;
   // RHS in bond-list order (bondc.f:490-497)
   double acc = 0.0;
   if (s > t - 2 * m && s <= t - m) {
@@ -1213,7 +1218,7 @@ struct CGArgs {
   // workgroup rounds (the workgroups a CU holds at once); the band a wave
   // walks is sized by the weight of its round, cumulative in wcum[0..wslots]
   int wslots;
-  int wcum[kMaxSlotRounds + 1];
+  int wcum[2][kMaxSlotRounds + 1];  // [0]: the P kernel, [1]: the march B
 };
 
 // diagonal of rows i, i+1 (i even) from the CSR diag array or the stencil code
@@ -2138,8 +2143,9 @@ __global__ __launch_bounds__(64 * kMarchWaves, (kMarchWavesPerEU<MODE, D, SM>)) 
     strip = v - q * spr;
     band = q * ns + sl;
     const int c0 = (int)((long long)q * nrows / Q), hc = (int)((long long)(q + 1) * nrows / Q) - c0;
-    g.r0 = c0 + hc * a.wcum[sl] / a.wcum[ns];
-    g.rend = c0 + hc * a.wcum[sl + 1] / a.wcum[ns];
+    const int* wc = a.wcum[MODE == kMarchB ? 1 : 0];
+    g.r0 = c0 + hc * wc[sl] / wc[ns];
+    g.rend = c0 + hc * wc[sl + 1] / wc[ns];
   } else {
     band = w / spr;
     strip = w - band * spr;
@@ -3464,6 +3470,12 @@ __global__ __launch_bounds__(kBlock) void k_to_strips(TileGeom T, const E* __res
 // a vector larger than this does not stay in the 256 MB Infinity Cache
 // between kernels (L = 8192: 537 MB; L = 4096: 134 MB)
 constexpr size_t kLargeVector = (size_t)256 << 20;
+// probe (PERC_MARCH_LARGE=1): vectors past the Infinity Cache also solve
+// strip-major with one round of bands (else row-major, 16-row bands)
+static bool large_strips() {
+  const char* e = getenv("PERC_MARCH_LARGE");
+  return e && atoi(e) != 0;
+}
 
 // workgroups of the largest reduction (CG kernels or the tiled kernel)
 int red_grid(const perc_ctx* h) { return std::max({h->grid, h->tile_grid, h->march_grid_max}); }
@@ -3506,7 +3518,7 @@ CGArgs make_cg_args(perc_ctx* h) {
   a.err_hist_cap = h->d.err_hist_cap;
   a.mtrace = nullptr;
   a.wslots = 0;
-  for (int i = 0; i <= kMaxSlotRounds; ++i) a.wcum[i] = 0;
+  for (int i = 0; i <= kMaxSlotRounds; ++i) a.wcum[0][i] = a.wcum[1][i] = 0;
   return a;
 }
 
@@ -3571,7 +3583,7 @@ void launch_cg_spmv(perc_ctx* h, const CGArgs& a, int G) {
       else if (h->qfree && a.sm && h->march_depth == 2) klaunch(h, k_cg_march<kMarchP, true, 2>, h->march_grid, 64 * kMarchWaves, st, a);
       else if (h->qfree && a.sm && h->march_paux == 2) launch_march_sm<kMarchP>(h, st, a);
       else if (h->qfree && a.sm) klaunch(h, k_cg_march<kMarchP, true, 3>, h->march_grid, 64 * kMarchWaves, st, a);
-      else if (h->qfree) klaunch(h, k_cg_march<kMarchP>, h->march_grid, 64 * kMarchWaves, st, a);
+      else if (h->qfree) klaunch(h, k_cg_march<kMarchP>, a.wslots > 0 ? h->wm_grid : h->march_grid, 64 * kMarchWaves, st, a);
       else if (a.sm && h->march_depth == 2) klaunch(h, k_cg_march<kMarchPQ, true, 2>, h->march_grid, 64 * kMarchWaves, st, a);
       else if (a.sm && h->march_depth == 4) klaunch(h, k_cg_march<kMarchPQ, true, 4>, h->march_grid, 64 * kMarchWaves, st, a);
       else if (a.sm) klaunch(h, k_cg_march<kMarchPQ, true, 3>, h->march_grid, 64 * kMarchWaves, st, a);
@@ -3607,7 +3619,11 @@ void launch_cg_b(perc_ctx* h, const CGArgs& a, int G) {
     else if (a.sm && h->march_bdepth == 2) klaunch(h, k_cg_march<kMarchB, true, 2>, h->march_grid, 64 * kMarchWaves, h->stream, a);
     else if (a.sm && h->march_baux == 2) launch_march_sm<kMarchB>(h, h->stream, a);
     else if (a.sm) klaunch(h, k_cg_march<kMarchB, true, 3>, h->march_grid, 64 * kMarchWaves, h->stream, a);
-    else klaunch(h, k_cg_march<kMarchB>, h->march_grid, 64 * kMarchWaves, h->stream, a);
+    else {  // row-major B: its own bands (slot-weighted bands are the P kernel's, rm_slots)
+      CGArgs ab = a;
+      ab.wslots = 0;
+      klaunch(h, k_cg_march<kMarchB>, h->march_grid, 64 * kMarchWaves, h->stream, ab);
+    }
   } else if (h->stencil) {
     // x on every row with the march's x-in-B (fused, row-major): XF
     if (a.bx && a.xrows == 0 && !a.sm) klaunch(h, k_cg_b<true, true>, G, kBlock, h->stream, a);
@@ -4016,7 +4032,11 @@ int march_rows_for(const perc_ctx* h, int nrows) {
   const char* env_rows = getenv("PERC_MARCH_ROWS");
   if (h->march_rows_req > 0) return h->march_rows_req;
   if (env_rows && atoi(env_rows) > 0) return atoi(env_rows);
-  if ((size_t)g.m * nrows * sizeof(double) > kLargeVector) return 16;
+  // (vectors past the Infinity Cache: 8-row bands for the row-major march B,
+  // 0.310 vs 0.318 ms at 16 rows at L = 8192; its P runs one round of
+  // slot-mapped bands instead, march_slots_rm)
+  if ((size_t)g.m * nrows * sizeof(double) > kLargeVector && !large_strips())
+    return (h->march_mode & PERC_MARCH_SLOTS) ? 8 : 16;
   int cus = 0, per_cu = 0;
   hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, h->device);
   // (the strip-major kernel of the same depth: within a few VGPRs, same occupancy)
@@ -4060,34 +4080,43 @@ void march_geometry(perc_ctx* h) {
   h->march_grid = cdiv(spr * cdiv(nrows, h->march_h), kMarchWaves);
   // slot-weighted bands (strip-major q-free march): one workgroup per CU
   // and round, bands cycling over the rounds; weights = the rounds' relative
-  // streaming rates with equal bands (PERC_MARCH_SLOTW="100,88,75" or
-  // "100:88:75", "0": off)
+  // streaming rates with equal bands (PERC_MARCH_SLOTW / PERC_MARCH_SLOTWB
+  // for P / B, e.g. "100:75:50", "0": off)
   h->wm_slots = 0;
   h->wm_grid = 0;
   {
     int cus = 0, per_cu = 0;
     hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, h->device);
     hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_cg_march<kMarchP, true, 3, 2>, 64 * kMarchWaves, 0);
-    int wts[kMaxSlotRounds] = {100, 88, 75, 64};
-    int nw = per_cu;
-    if (const char* e = getenv("PERC_MARCH_SLOTW")) {
-      nw = 0;
-      for (const char* c = e; *c && nw < kMaxSlotRounds;) {
-        wts[nw++] = atoi(c);
+    // (per kernel: the P kernel and the march B balance at different weights)
+    // (row-major P past the Infinity Cache, L = 8192: flat weights, i.e.
+    // one round of equal bands: 0.364 ms vs 0.387 at 100:80:60 and 0.403
+    // for the 16-row bands, r3 L = 8192 probes)
+    int wts[3][kMaxSlotRounds] = {{100, 75, 50, 40}, {100, 80, 60, 50}, {100, 100, 100, 100}};
+    int nw[3] = {per_cu, per_cu, per_cu};
+    const char* envs[3] = {"PERC_MARCH_SLOTW", "PERC_MARCH_SLOTWB", "PERC_MARCH_SLOTWRM"};
+    for (int k = 0; k < 3; ++k) {
+      const char* e = getenv(envs[k]);
+      if (!e) continue;
+      nw[k] = 0;
+      for (const char* c = e; *c && nw[k] < kMaxSlotRounds;) {
+        wts[k][nw[k]++] = atoi(c);
         while (*c && *c != ',' && *c != ':') ++c;
         if (*c) ++c;
       }
-      if (nw == 1 && wts[0] == 0) nw = 0;  // "0": off
+      if (nw[k] == 1 && wts[k][0] == 0) nw[k] = 0;  // "0": off
     }
     const long long waves = (long long)cus * kMarchWaves;
-    bool ok = cus > 0 && per_cu >= 2 && per_cu <= kMaxSlotRounds && nw == per_cu &&
-              waves % spr == 0 && (waves / spr) * per_cu <= nrows;
-    for (int i = 0; ok && i < per_cu; ++i) ok = wts[i] > 0;
+    bool ok = cus > 0 && per_cu >= 2 && per_cu <= kMaxSlotRounds && nw[0] == per_cu &&
+              nw[1] == per_cu && nw[2] == per_cu && waves % spr == 0 && (waves / spr) * per_cu <= nrows;
+    for (int i = 0; ok && i < per_cu; ++i) ok = wts[0][i] > 0 && wts[1][i] > 0 && wts[2][i] > 0;
     if (ok) {
       h->wm_slots = per_cu;
       h->wm_grid = cus * per_cu;
-      h->wm_cum[0] = 0;
-      for (int i = 0; i < per_cu; ++i) h->wm_cum[i + 1] = h->wm_cum[i] + wts[i];
+      for (int k = 0; k < 3; ++k) {
+        h->wm_cum[k][0] = 0;
+        for (int i = 0; i < per_cu; ++i) h->wm_cum[k][i + 1] = h->wm_cum[k][i] + wts[k][i];
+      }
     }
   }
   // workgroup row-march: the widest strip of 2048 / 1024 / 512 columns that
@@ -4166,7 +4195,7 @@ void select_format(perc_ctx* h) {
   // faster (L = 8192: 0.439 vs 0.480 ms, profiles/r2_11_ab_strips.log); the
   // strip-major march's whole-array buffer views also need < 2 GB
   h->strips = h->march && (h->march_mode & PERC_MARCH_STRIPS) &&
-              (size_t)h->N * sizeof(double) <= kLargeVector;
+              ((size_t)h->N * sizeof(double) <= kLargeVector || large_strips());
   // deferred reductions (the strip-major q-free march with its default
   // cache policies; every workgroup sums every partial, gather_totals:
   // one round of workgroups); PERC_MARCH_DEFER=0/1 overrides the mode bit
@@ -4179,6 +4208,13 @@ void select_format(perc_ctx* h) {
   bool slots = (h->march_mode & PERC_MARCH_SLOTS) != 0;
   if (const char* e = getenv("PERC_MARCH_SLOTS")) slots = atoi(e) != 0;
   h->march_slots = slots && h->strips && h->qfree && h->wm_slots > 0;
+  // row-major q-free march past the Infinity Cache (L = 8192): P on one round
+  // of bands (the slot mapping with PERC_MARCH_SLOTWRM weights), B on 8-row
+  // bands (march_rows_for): P 0.364 + B 0.310 vs 0.403 + 0.318 ms per
+  // iteration (r3 L = 8192 probes); PERC_MARCH_RMSLOTS=0/1 overrides
+  bool rms = slots && (size_t)h->N * sizeof(double) > kLargeVector;
+  if (const char* e = getenv("PERC_MARCH_RMSLOTS")) rms = atoi(e) != 0;
+  h->march_slots_rm = rms && !h->strips && h->qfree && h->wm_slots > 0;
 }
 
 // strip-major copies of r (into the q buffer: r and q swap roles for the
@@ -4199,20 +4235,50 @@ hipError_t to_strips(perc_ctx* h, CGArgs& a) {
   if (h->march_slots && h->qfree && !h->march_defer && h->march_depth == 3 && h->march_paux == 2 &&
       h->march_baux == 2 && h->march_bdepth == 3) {
     a.wslots = h->wm_slots;
-    for (int i = 0; i <= h->wm_slots; ++i) a.wcum[i] = h->wm_cum[i];
+    for (int i = 0; i <= h->wm_slots; ++i) {
+      a.wcum[0][i] = h->wm_cum[0][i];
+      a.wcum[1][i] = h->wm_cum[1][i];
+    }
   }
   return hipSuccess;
+}
+
+static hipError_t launch_assemble(perc_ctx* h, bool csr) {
+  DeviceBuffers& d = h->d;
+  const AsmParams& p = h->asm_p;
+  hipStream_t st = h->stream;
+  HIP_TRY(hipMemsetAsync(d.sflag, 0, 4 * sizeof(int), st));
+  const double* w = h->has_weights ? d.bw : nullptr;
+  if (csr)
+    k_assemble<true><<<blocks_for(h->N), kBlock, 0, st>>>(h->g, h->N, d.bond_first, d.bocc, d.socc,
+                                                          d.parent, d.rowptr, d.val, d.diag, d.rhs,
+                                                          d.code, d.sflag, h->forms, p.rule, p.g0,
+                                                          p.leak, p.Va, p.span_root, w);
+  else
+    k_assemble<false><<<blocks_for(h->N), kBlock, 0, st>>>(h->g, h->N, d.bond_first, d.bocc, d.socc,
+                                                           d.parent, d.rowptr, d.val, d.diag, d.rhs,
+                                                           d.code, d.sflag, h->forms, p.rule, p.g0,
+                                                           p.leak, p.Va, p.span_root, w);
+  HIP_TRY(dbg_sync(st, "k_assemble"));
+  h->csr_ok = csr;
+  return hipSuccess;
+}
+
+// the CSR copy of the assembled system (values, diagonal), for the
+// consumers that read it; the stencil assembly leaves it unwritten
+hipError_t ensure_csr(perc_ctx* h) {
+  if (h->csr_ok || !h->assembled || !h->asm_p.valid) return hipSuccess;
+  return launch_assemble(h, true);
 }
 
 hipError_t dev_assemble(perc_ctx* h, int rule, double g0, double leak, double Va, int span_root) {
   DeviceBuffers& d = h->d;
   hipStream_t st = h->stream;
-  HIP_TRY(hipMemsetAsync(d.sflag, 0, 4 * sizeof(int), st));
-  k_assemble<<<blocks_for(h->N), kBlock, 0, st>>>(h->g, h->N, d.bond_first, d.bocc, d.socc,
-                                                   d.parent, d.rowptr, d.val, d.diag, d.rhs, d.code,
-                                                   d.sflag, h->forms, rule, g0, leak, Va, span_root,
-                                                   h->has_weights ? d.bw : nullptr);
-  HIP_TRY(dbg_sync(st, "k_assemble"));
+  h->asm_p = AsmParams{true, rule, span_root, g0, leak, Va};
+  // per-bond weights take the CSR operator (two-value stencil codes cannot
+  // hold them): assemble the CSR copy at once; else the stencil rows only,
+  // and the CSR copy after all if a row does not fit a stencil form
+  HIP_TRY(launch_assemble(h, h->has_weights));
   int flag = 0;
   HIP_TRY(hipMemcpyAsync(&flag, d.sflag, sizeof(int), hipMemcpyDeviceToHost, st));
   HIP_TRY(hipStreamSynchronize(st));
@@ -4226,6 +4292,7 @@ hipError_t dev_assemble(perc_ctx* h, int rule, double g0, double leak, double Va
   h->tiled_ok = h->stencil_ok && (flag & 4) == 0 && h->tile_grid > 0 && h->g.m % 2 == 0;
   h->march_ok = h->tiled_ok && h->march_grid > 0;
   select_format(h);
+  if (!h->stencil_ok) HIP_TRY(launch_assemble(h, true));
   return hipSuccess;
 }
 
@@ -4344,6 +4411,7 @@ hipError_t dev_solve(perc_ctx* h, int itol, double tol, int itmax, bool x0_zero,
                      int* iter, double* err) {
   DeviceBuffers& d = h->d;
   hipStream_t st = h->stream;
+  if (!h->stencil) HIP_TRY(ensure_csr(h));
   if (d.err_hist_cap < itmax + 2) {
     if (d.err_hist) HIP_TRY(hipFree(d.err_hist));
     d.err_hist_cap = itmax + 2;
@@ -4399,6 +4467,13 @@ hipError_t dev_solve(perc_ctx* h, int itol, double tol, int itmax, bool x0_zero,
     h->resident = false;
   }
   if (h->strips) HIP_TRY(to_strips(h, a));
+  // row-major q-free march past the Infinity Cache: the P kernel on one
+  // round of slot-weighted bands (probe PERC_MARCH_RMSLOTS=1), B on its
+  // short bands
+  if (!h->strips && h->march && h->qfree && h->march_slots_rm && h->wm_slots > 0) {
+    a.wslots = h->wm_slots;
+    for (int i = 0; i <= h->wm_slots; ++i) a.wcum[0][i] = h->wm_cum[2][i];
+  }
   // iterate in chunks; the device flag makes surplus launches no-ops
   int chunk = 8;
   CGScalars* hsp = nullptr;
@@ -4970,6 +5045,7 @@ hipError_t dev_currents(perc_ctx* h, int rule, int cur_rule, double g0, double l
 }
 
 hipError_t dev_spmv(perc_ctx* h, const double* x, double* y) {
+  if (!h->stencil) HIP_TRY(ensure_csr(h));
   DeviceBuffers& d = h->d;
   hipStream_t st = h->stream;
   const size_t bytes = sizeof(double) * h->N;
@@ -5004,6 +5080,7 @@ hipError_t dev_selftest_division(long long n, unsigned long long seed, unsigned 
 }
 
 hipError_t dev_bench(perc_ctx* h, int which, int reps, double* ms) {
+  HIP_TRY(ensure_csr(h));  // the probes run every format
   DeviceBuffers& d = h->d;
   hipStream_t st = h->stream;
   CGArgs a = make_cg_args(h);

@@ -818,9 +818,9 @@ int perc_get_system(perc_ctx* h, int* rowptr, int* col, double* val, double* dia
                     int* n_out, int* nnz_out) {
   if (!h) return PERC_EINVAL;
   hipSetDevice(h->device);
+  hipError_t e = ensure_csr(h);
   hipStreamSynchronize(h->stream);
   const size_t N = h->N, nnz = h->nnz;
-  hipError_t e = hipSuccess;
   if (rowptr && e == hipSuccess) e = hipMemcpy(rowptr, h->d.rowptr, sizeof(int) * (N + 1), hipMemcpyDeviceToHost);
   if (col && e == hipSuccess) e = hipMemcpy(col, h->d.col, sizeof(int) * nnz, hipMemcpyDeviceToHost);
   if (val && e == hipSuccess) e = hipMemcpy(val, h->d.val, sizeof(double) * nnz, hipMemcpyDeviceToHost);
@@ -887,7 +887,7 @@ int perc_march_info(perc_ctx* h, int* out5) {
   if (!h->assembled) return PERC_ESTATE;
   out5[0] = h->small ? 4 : (h->resident && h->stencil ? 3 : (h->rowmarch ? 2 : (h->march ? 1 : 0)));
   out5[1] = (h->qfree ? 1 : 0) | (h->strips ? 2 : 0) | (h->march_defer ? 4 : 0) |
-            (h->march_slots ? 8 : 0);
+            (h->march_slots || h->march_slots_rm ? 8 : 0);
   out5[2] = h->march_alt ? 1 : 0;
   out5[3] = h->resident ? h->res_H : (h->rowmarch ? h->rm_h : (h->march ? h->march_h : 0));
   out5[4] = h->resident ? h->g.m : (h->rowmarch ? h->rm_w : (h->march ? 128 : 0));

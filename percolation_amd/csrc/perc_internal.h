@@ -63,6 +63,12 @@ struct CGScalars {
   double bkn[2];   // deferred-reduction march: bknum of iteration k in bkn[k & 1]
 };
 
+struct AsmParams {
+  bool valid = false;
+  int rule = 0, span_root = 0;
+  double g0 = 0.0, leak = 0.0, Va = 0.0;
+};
+
 struct DeviceBuffers {
   // lattice (1-based sites): bonds whose smaller end is s are
   // [bond_first[s], bond_first[s+1]) in bond-list order
@@ -153,6 +159,8 @@ struct perc_ctx {
   bool occupied = false;
   bool labeled = false;
   bool assembled = false;
+  bool csr_ok = true;    // the CSR values / diagonal of the assembled system are written
+  perc::AsmParams asm_p; // the assembly's parameters (ensure_csr re-runs it)
   int span_root = 0;
   int perccln = 0;
   int rule = -1;
@@ -173,9 +181,10 @@ struct perc_ctx {
   int march_saux = 2;           // the q-free march's p(k) / r(k+1) stores (nontemporal; probe)
   int march_defer = 0;          // q-free strip-major march: reductions deferred to the next kernel
   int march_slots = 0;          // q-free strip-major march: slot-weighted bands
+  int march_slots_rm = 0;       // q-free row-major march: slot-weighted bands for P
   int wm_slots = 0;             // slot-weighted bands: workgroup rounds (0: not available)
   int wm_grid = 0;              // their grid (CUs x rounds)
-  int wm_cum[5] = {0, 0, 0, 0, 0};  // cumulative round weights
+  int wm_cum[3][5] = {};        // cumulative round weights (P, B, row-major P)
   int march_grid = 0;           // its workgroups
   int march_grid_max = 0;       // workgroups at band height 1 (reduction buffers)
   int march_rows_req = 0;       // perc_set_march_rows (0: auto)
@@ -216,6 +225,7 @@ hipError_t dev_span_sites(perc_ctx* h, int root, int* count);
 hipError_t dev_canon(perc_ctx* h, int* canon_out);
 hipError_t dev_cluster_sizes(perc_ctx* h, int kind, int root, int* maxcs, int* rootsize);
 hipError_t dev_assemble(perc_ctx* h, int rule, double g0, double leak, double Va, int span_root);
+hipError_t ensure_csr(perc_ctx* h);  // the CSR copy of the assembled system, on demand
 void select_format(perc_ctx* h);  // stencil / fused flags from fmt_req + assembly checks
 void march_geometry(perc_ctx* h); // band height + grid of the register-march kernel
 void res_geometry(perc_ctx* h);   // grid + band height of the resident solve

@@ -515,8 +515,9 @@ def test_headline_size_properties():
 
 
 def test_large_vector_grids_8192():
-    """8192^2 (config 5 size; vectors past the Infinity Cache, so 16-row
-    march bands and the short in-order B grid): the fused march solve
+    """8192^2 (config 5 size; vectors past the Infinity Cache: row-major
+    march, the P kernel on one round of slot-mapped bands, the march B on
+    8-row bands, the short in-order B grid): the fused march solve
     against the split kernels (fixed 8192-workgroup grid, another dot
     association): iteration count within 1, Gtop/Gbot to the tolerance,
     current conserved."""
@@ -532,7 +533,8 @@ def test_large_vector_grids_8192():
             out[fmt] = ctx.conductance(tol=1e-8, itmax=10 ** 6)
             assert ctx.matrix_format() == fmt
             if fmt == PL.FMT_STENCIL:
-                assert ctx.march_info()["band_rows"] == 16
+                info = ctx.march_info()
+                assert info["band_rows"] == 8 and info["slots"] and not info["strips"]
     c, t = out[PL.FMT_STENCIL], out[PL.FMT_STENCIL_SPLIT]
     assert c["err"] <= 1e-8 and t["err"] <= 1e-8
     assert abs(c["iter"] - t["iter"]) <= 1
@@ -545,7 +547,8 @@ MARCH_MODES = (PL.MARCH_DEFAULT, 0, PL.MARCH_QFREE, PL.MARCH_ALT, PL.MARCH_ROWS,
                PL.MARCH_ROWS | PL.MARCH_QFREE | PL.MARCH_ALT, PL.MARCH_STRIPS,
                PL.MARCH_STRIPS | PL.MARCH_QFREE, PL.MARCH_STRIPS | PL.MARCH_ALT,
                PL.MARCH_STRIPS | PL.MARCH_QFREE | PL.MARCH_ALT,
-               PL.MARCH_STRIPS | PL.MARCH_QFREE | PL.MARCH_ALT | PL.MARCH_DEFER)
+               PL.MARCH_STRIPS | PL.MARCH_QFREE | PL.MARCH_ALT | PL.MARCH_DEFER,
+               PL.MARCH_STRIPS | PL.MARCH_QFREE | PL.MARCH_ALT | PL.MARCH_SLOTS)
 
 
 @pytest.mark.parametrize("lat,m,n,pbc,p", [(0, 256, 150, 0, 0.6), (1, 128, 99, 1, 0.42),
@@ -640,6 +643,47 @@ def test_deferred_reduction_is_bitwise_the_in_kernel_one(lat, m, n, pbc, p):
             assert a["gtop"] == b["gtop"] and a["gbot"] == b["gbot"], tol
             assert np.array_equal(a["vint"].view(np.uint64), b["vint"].view(np.uint64))
         ctx.set_march_mode(PL.MARCH_DEFAULT)
+
+
+@pytest.mark.parametrize("lat,m,n,pbc,p", [(0, 512, 512, 0, 0.6), (1, 384, 300, 0, 0.42),
+                                           (0, 1024, 1024, 0, 0.55), (0, 256, 160, 1, 0.6),
+                                           (0, 128, 1400, 0, 0.6), (0, 2048, 2048, 0, 0.6)])
+def test_slot_weighted_bands_solve_the_same_system(lat, m, n, pbc, p):
+    """PERC_MARCH_SLOTS (one workgroup per CU and round, bands sized by the
+    round): the rows are a partition of the lattice whatever the weights, so
+    the solve is the static march's up to the dot products' association --
+    iteration count within 2, Gtop / Gbot to the solver tolerance, the
+    voltages -- for the default weights and extreme ones."""
+    import os
+    nb = api.nbonds(lat, m, n, pbc)
+    order = api.shuffled_ids(nb, 1618)
+    base = PL.MARCH_QFREE | PL.MARCH_ALT | PL.MARCH_STRIPS
+    out = []
+    for mode, w in ((base, None), (base | PL.MARCH_SLOTS, None), (base | PL.MARCH_SLOTS, "100:30:5"),
+                    (base | PL.MARCH_SLOTS, "1:1:400")):
+        if w:
+            os.environ["PERC_MARCH_SLOTW"] = os.environ["PERC_MARCH_SLOTWB"] = w
+        try:
+            with api.Context(lat, m, n, pbc) as ctx:  # (weights are read with the lattice)
+                ctx.occupy(PL.BOND, bond_order=order, nbonds_=int(p * nb))
+                if ctx.label()["nspan"] == 0:
+                    pytest.skip("no spanning cluster")
+                ctx.set_march_mode(mode)
+                out.append(ctx.conductance(tol=1e-12, itmax=200000, vint=True))
+                info = ctx.march_info()
+                assert info["kernel"] == "wave"
+                if not mode & PL.MARCH_SLOTS:
+                    assert not info["slots"]
+                elif (m, n) in ((512, 512), (1024, 1024), (2048, 2048)):
+                    assert info["slots"]  # (1 strip x 1400 rows: too few rows per cycle -> static)
+        finally:
+            os.environ.pop("PERC_MARCH_SLOTW", None)
+            os.environ.pop("PERC_MARCH_SLOTWB", None)
+    a = out[0]
+    for b in out[1:]:
+        assert abs(a["iter"] - b["iter"]) <= 2, (a["iter"], b["iter"])
+        assert rel(b["gtop"], a["gtop"]) < REL and rel(b["gbot"], a["gbot"]) < REL
+        assert np.max(np.abs(b["vint"] - a["vint"])) < 1e-6
 
 
 def test_table_division_is_ieee_division():
