@@ -7,12 +7,34 @@ outputs at <= 64^2 by tests/test_oracle_golden.py).
 
 Per fixture: the occupation order is rebuilt from its recipe, the GPU
 labels it (partition fingerprint = the oracle's, bit-exact) and solves the
-spanning cluster's Kirchhoff system at each tolerance the fixture holds.
-Bars: converged (tol 1e-13) Gtop and Gbot within 1e-10
-relative, for the default solve and the 4-slab row decomposition; at the
-reference tolerance 1e-8 the iteration count within +-1 and G within twice
-the reference's own truncation error there plus the tolerance (see
-CONVERGED below).
+spanning cluster's Kirchhoff system.  Each fixture holds the oracle's
+solve at every decade 1e-8 ... 1e-17 or 1e-20 from ONE literal linbcg run
+(round 3: or_linbcg_sym, bitwise the literal iterates), so it shows where
+the reference solver has converged: the converged tolerance is the first
+decade from which Gtop and Gbot move by < 2e-11 relative per decade
+(CONV_STEP) to the end of the fixture.  Bars:
+
+  * converged: Gtop and Gbot within 1e-10 relative of the oracle at that
+    tolerance, for the default solve and the 4-slab row decomposition
+    (SURVEY: "both within 1e-10 rel against the reference solver run at
+    tol=1e-14 with itmax large" -- the fixtures show 1e-14 is not yet
+    converged at the critical configs, so the bar is applied where the
+    oracle itself has stopped moving).  The one widening, stated here and
+    in DESIGN.md §5: where the reference solver ITSELF, re-run with only the
+    order of its dot-product sums reversed (fixture "assoc_desc",
+    make_config_golden.py --assoc), converges to a G more than 5e-11 away
+    from the literal run, that G is not defined to 1e-10 by the reference,
+    and the bar is twice that spread.  This happens for one value: c2's
+    Gtop (critical 1024^2, Gtop = 4.7e-4, the top-row currents are
+    differences Va - V of voltages within ~1e-6 of Va): the reversed-sum
+    oracle lands 1.12e-10 away, and so does the 4-slab GPU solve;
+  * the reference tolerance 1e-8: iteration count within +-1 and G within
+    twice the oracle's own truncation error there plus the tolerance (the
+    solve is only accurate to |G(1e-8) - G(converged)|, and the dot
+    products' association -- the only re-associated operations -- moves
+    the iterates within that error);
+  * 1e-13: iteration count within +-3 (the recursive residual is near the
+    fp64 floor) and the same truncation bar.
 """
 import glob
 import hashlib
@@ -25,35 +47,46 @@ import pytest
 from percolation_amd import _lib as PL
 from percolation_amd import api
 
-pytestmark = pytest.mark.gpu
 HERE = os.path.dirname(os.path.abspath(__file__))
 FIXTURES = sorted(glob.glob(os.path.join(HERE, "golden", "configs", "*.json")))
 
-# Bars.  The fixture's tightest tolerance (1e-14) is the converged
-# reference.  There Gtop and Gbot must agree within 1e-10 relative, or
-# within the oracle's own remaining truncation error if that is larger --
-# estimated as a fifth of its change over the last tolerance decade
-# (1e-13 -> 1e-14; the recursive residual falls linearly, so the iterate
-# error falls about tenfold per decade): c2's Gbot still moves 4.8e-9
-# between 1e-13 and 1e-14, its Gtop 5.1e-10.  At a looser tolerance the
-# solve itself is accurate only to |G(tol) - G(converged)| (c2 at 1e-8:
-# 2.1e-7 relative), and over 10^4 iterations the association of the dot
-# products -- the only re-associated operations -- moves the iterates
-# within that error: G within twice the reference's own truncation error
-# there, the iteration count within +-1 at 1e-8 (+-3 below 1e-10, where the
-# recursive residual is near the fp64 floor).  Measured (r2): at 1e-8 c2
-# Gtop 1.2e-7 / Gbot 1.6e-10, c3 1.0e-7 / 1.3e-9; at 1e-14 c2 7.3e-11 /
-# 1.5e-10, c3 7.9e-11 / 1.0e-10 (4 slabs: 4.9e-11 / 1.5e-10, 8.9e-11 /
-# 1.0e-10).
 CONVERGED = 1e-10
+
+CONV_STEP = 2e-11  # per-decade change below which the oracle has converged
+FLAT = 1e-10
+ASSOC_FLOOR = 5e-11  # association spread of the reference solver above which it sets the bar
+
+
+def converged_bar(doc, conv, g):
+    """FLAT, or twice the reference solver's own association spread at the
+    converged tolerance where that exceeds ASSOC_FLOOR (module docstring)"""
+    alt = doc.get("assoc_desc", {}).get(conv)
+    if alt is None:
+        return FLAT
+    spread = rel(alt[g], doc["solves"][conv][g])
+    return max(FLAT, 2 * spread) if spread > ASSOC_FLOOR else FLAT
+
 
 def rel(a, b):
     return abs(a - b) / max(abs(b), 1e-300)
 
 
+def converged_tol(solves):
+    """the first tolerance from which every further decade moves Gtop and
+    Gbot by < CONV_STEP (None if the fixture never gets there)"""
+    tols = sorted(solves, key=float, reverse=True)  # loose -> tight
+    steps = [max(rel(solves[b]["gtop"], solves[a]["gtop"]), rel(solves[b]["gbot"], solves[a]["gbot"]))
+             for a, b in zip(tols, tols[1:])]
+    for i in range(len(steps)):
+        if all(x < CONV_STEP for x in steps[i:]):
+            return tols[i + 1]
+    return None
+
+
 def occupation(rc):
-    lat, L_, p, seed = rc["lattice"], rc["L"], rc["p"], rc["tseed"]
+    lat, L_, p = rc["lattice"], rc["L"], rc["p"]
     if rc["kind"] == "bond":
+        seed = rc["tseed"]
         nb = api.nbonds(lat, L_, L_, 0)
         tb = int(p * nb)
         if rc["order"] == "ref":
@@ -62,67 +95,74 @@ def occupation(rc):
             ids = (np.random.default_rng(seed).permutation(nb)[:tb] + 1).astype(np.int32)
         return dict(kind=PL.BOND, bond_order=ids, nbonds_=tb), PL.RULE_BOND, PL.CUR_FORTRAN
     t = L_ * L_
+    if rc["kind"] == "mixed":  # sitebond.f: sites (sseed) then bonds (bseed), reference shuffles
+        nb = api.nbonds(lat, L_, L_, 0)
+        return (dict(kind=PL.SITEBOND, site_order=api.shuffled_ids(t, rc["sseed"]),
+                     nsites=int(p * t), bond_order=api.shuffled_ids(nb, rc["bseed"]),
+                     nbonds_=int(rc["pb"] * nb)), PL.RULE_MIXED, PL.CUR_MATLAB)
     ts = int(p * t)
-    return (dict(kind=PL.SITE, site_order=api.shuffled_ids(t, seed), nsites=ts), PL.RULE_SITE,
-            PL.CUR_MATLAB)
+    return (dict(kind=PL.SITE, site_order=api.shuffled_ids(t, rc["tseed"]), nsites=ts),
+            PL.RULE_SITE, PL.CUR_MATLAB)
 
 
+def test_converged_tol_rule():
+    """CPU: the converged-decade rule on synthetic histories, and every
+    committed fixture reaches convergence"""
+    mk = lambda *g: {"1e-%d" % (8 + i): dict(gtop=1.0 + a, gbot=1.0 + b) for i, (a, b) in enumerate(g)}
+    assert converged_tol(mk((0, 0), (1e-9, 0), (1e-9 + 1e-12, 5e-12), (1e-9 + 1e-12, 5e-12))) == "1e-10"
+    assert converged_tol(mk((0, 0), (1e-9, 0), (2e-9, 0))) is None
+    assert converged_tol(mk((0, 0), (0, 0))) == "1e-09"
+    for f in FIXTURES:
+        assert converged_tol(json.load(open(f))["solves"]) is not None, f
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("path", FIXTURES, ids=[os.path.basename(f)[:-5] for f in FIXTURES])
 def test_config_fixture(path):
     doc = json.load(open(path))
     rc = doc["recipe"]
     occ, rule, cur = occupation(rc)
     L_ = rc["L"]
-    report = []
+    solves = doc["solves"]
+    conv = converged_tol(solves)
+    assert conv is not None, "fixture not converged: regenerate it deeper (make_config_golden.py)"
+    runs = [t for t in ("1e-08", "1e-13") if t in solves] + [conv]
+    report = {}
     with api.Context(rc["lattice"], L_, L_, 0) as ctx:
         ctx.occupy(**occ)
         li = ctx.label(canon=True)
         h = hashlib.sha256(np.ascontiguousarray(li["canon"], dtype=np.int32).tobytes()).hexdigest()
         assert h == doc["label"]["canon_sha256"], "partition differs from the oracle's"
         assert li["nspan"] > 0
-        for tkey, ref in sorted(doc["solves"].items()):
+        for tkey in runs:
+            ref = solves[tkey]
             c = ctx.conductance(rule, cur, tol=float(tkey), itmax=10 ** 6)
-            d = dict(tol=tkey, iter=c["iter"], iter_ref=ref["iter"],
-                     gtop_rel=rel(c["gtop"], ref["gtop"]), gbot_rel=rel(c["gbot"], ref["gbot"]))
-            report.append((tkey, d))
+            report[tkey] = d = dict(tol=tkey, iter=c["iter"], iter_ref=ref["iter"],
+                                    gtop_rel=rel(c["gtop"], ref["gtop"]),
+                                    gbot_rel=rel(c["gbot"], ref["gbot"]))
             print(json.dumps(d))
-        tight = min(doc["solves"], key=float)
-        if float(tight) <= 1e-13:
-            # the row-slab solve (perc_set_slabs, 4 slabs) against the same
-            # converged fixture
-            ref = doc["solves"][tight]
-            ctx.set_slabs(4)
-            c = ctx.conductance(rule, cur, tol=float(tight), itmax=10 ** 6)
-            ctx.set_slabs(1)
-            d = dict(tol=tight + " (4 slabs)", iter=c["iter"], iter_ref=ref["iter"],
-                     gtop_rel=rel(c["gtop"], ref["gtop"]), gbot_rel=rel(c["gbot"], ref["gbot"]))
-            report.append((tight, d))
-            print(json.dumps(d))
-    tols = sorted(doc["solves"], key=float)
-    tight = tols[0]
-    if float(tight) > 1e-13:  # no converged fixture yet (still generating)
-        for tkey, d in report:
-            assert abs(d["iter"] - d["iter_ref"]) <= 1, d
-            assert d["gtop_rel"] < 1e-6 and d["gbot_rel"] < 1e-6, d  # the solver-tolerance scale
-        return
-    conv = doc["solves"][tight]
-    # the decade above the tightest tolerance, if the fixture has it
-    prev = doc["solves"][tols[1]] if len(tols) > 1 and float(tols[1]) <= 10.5 * float(tight) else None
-    for tkey, d in report:
-        ref = doc["solves"][tkey]
-        if tkey == tight:
-            for g in ("gtop", "gbot"):
-                # without the next decade (c4 while its 1e-14 solve is still
-                # being generated): the 1e-13 iterate's own truncation, which
-                # c2 / c3 put at <= 5e-9 relative (Gbot), bounds the difference
-                rest = rel(conv[g], prev[g]) / 5 if prev is not None else 5e-9
-                assert d[g + "_rel"] < max(CONVERGED, rest), (g, rest, d)
+        # the row-slab solve (perc_set_slabs, 4 slabs) against the converged fixture
+        ctx.set_slabs(4)
+        c = ctx.conductance(rule, cur, tol=float(conv), itmax=10 ** 6)
+        ctx.set_slabs(1)
+        ref = solves[conv]
+        report["slabs"] = d = dict(tol=conv + " (4 slabs)", iter=c["iter"], iter_ref=ref["iter"],
+                                   gtop_rel=rel(c["gtop"], ref["gtop"]),
+                                   gbot_rel=rel(c["gbot"], ref["gbot"]))
+        print(json.dumps(d))
+    for key in (conv, "slabs"):  # converged: 1e-10 on both conductances (see converged_bar)
+        d = report[key]
+        for g in ("gtop", "gbot"):
+            assert d[g + "_rel"] < converged_bar(doc, conv, g), (g, converged_bar(doc, conv, g), d)
+    for tkey in runs:
+        if tkey == conv:
             continue
+        d, ref, cv = report[tkey], solves[tkey], solves[conv]
         assert abs(d["iter"] - d["iter_ref"]) <= (1 if float(tkey) >= 1e-10 else 3), d
         for g in ("gtop", "gbot"):
-            # the reference's own error at this tol, plus the tolerance itself:
+            # the oracle's own error at this tol, plus the tolerance itself:
             # where G has converged ahead of the residual (the metric's Gtop
             # moves 3.6e-10 from 1e-8 to 1e-13), stopping one iteration
             # apart still moves it by the last step (1.4e-9 there)
-            trunc = rel(ref[g], conv[g])
-            assert d[g + "_rel"] <= 2 * trunc + max(CONVERGED, float(tkey)), (g, trunc, d)
+            trunc = rel(ref[g], cv[g])
+            assert d[g + "_rel"] <= 2 * trunc + max(1e-10, float(tkey)), (g, trunc, d)
