@@ -111,7 +111,7 @@ def test_converged_tol_rule():
     mk = lambda *g: {"1e-%d" % (8 + i): dict(gtop=1.0 + a, gbot=1.0 + b) for i, (a, b) in enumerate(g)}
     assert converged_tol(mk((0, 0), (1e-9, 0), (1e-9 + 1e-12, 5e-12), (1e-9 + 1e-12, 5e-12))) == "1e-10"
     assert converged_tol(mk((0, 0), (1e-9, 0), (2e-9, 0))) is None
-    assert converged_tol(mk((0, 0), (0, 0))) == "1e-09"
+    assert converged_tol(mk((0, 0), (0, 0))) == "1e-9"
     for f in FIXTURES:
         assert converged_tol(json.load(open(f))["solves"]) is not None, f
 
