@@ -354,7 +354,10 @@ int perc_set_march_rows(perc_ctx *h, int rows);
    PERC_MARCH_SLOTS (strip-major q-free march): one workgroup per CU and
    round, and the bands sized by the round a wave runs in (the first round
    on a CU streams fastest), so every wave finishes at about the same time;
-   same per-row arithmetic, dot products over other wave partials. */
+   same per-row arithmetic, dot products over other wave partials.
+   PERC_MARCH_TAG (strip-major q-free march): the end-of-kernel reductions
+   publish tagged {value, tag} granules the readers poll for, instead of
+   draining stores before each ticket; bitwise the same totals. */
 #define PERC_MARCH_QFREE 1
 #define PERC_MARCH_ALT 2
 #define PERC_MARCH_ROWS 4
@@ -362,8 +365,10 @@ int perc_set_march_rows(perc_ctx *h, int rows);
 #define PERC_MARCH_STRIPS 16
 #define PERC_MARCH_DEFER 32
 #define PERC_MARCH_SLOTS 64
-#define PERC_MARCH_DEFAULT \
-  (PERC_MARCH_QFREE | PERC_MARCH_ALT | PERC_SOLVE_RESIDENT | PERC_MARCH_STRIPS | PERC_MARCH_SLOTS)
+#define PERC_MARCH_TAG 128
+#define PERC_MARCH_DEFAULT                                                                      \
+  (PERC_MARCH_QFREE | PERC_MARCH_ALT | PERC_SOLVE_RESIDENT | PERC_MARCH_STRIPS | PERC_MARCH_SLOTS | \
+   PERC_MARCH_TAG)
 int perc_set_march_mode(perc_ctx *h, int mode);
 /* Random bond conductances (MATLAB/ConductCalc.m condtype 2, :38-47 and
    :94-97): the bonds of the spanning cluster get G = -g0 * w[id] instead of

@@ -1219,6 +1219,11 @@ struct CGArgs {
   // walks is sized by the weight of its round, cumulative in wcum[0..wslots]
   int wslots;
   int wcum[2][kMaxSlotRounds + 1];  // [0]: the P kernel, [1]: the march B
+  // tagged-granule reductions of the march (PERC_MARCH_TAG): two slots (P, B)
+  // of granules, the launch's tag, the reader-timeout flag
+  double* mgran;
+  double mtag;
+  int* merr;
 };
 
 // diagonal of rows i, i+1 (i even) from the CSR diag array or the stencil code
@@ -1706,6 +1711,92 @@ __device__ __forceinline__ void bst2(__amdgpu_buffer_rsrc_t r, unsigned off, dou
   __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, (int)off, 0, AUX);
 }
 
+// publish_and_reduce with tagged granules (the march kernels, TAG): every
+// partial travels as one 16-B write-through {value, tag} store (untorn), so
+// the workgroup that publishes it need not drain its stores before taking
+// its ticket -- the reader polls the tags instead.  At the end of a march
+// launch the last workgroup to arrive waited twice for s_waitcnt vmcnt(0)
+// (its last rows' stores, then its group partial's) before the totals could
+// be formed.  Association, and so the totals, are publish_and_reduce's term
+// for term.  tag: unique per launch and solve; a reader that polls for ~0.5 s
+// without seeing it sets *err and uses what it has (the host reports it).
+__device__ __forceinline__ double2 gran_poll(__amdgpu_buffer_rsrc_t rg, int off, double tag, int* err) {
+  double2 g2 = __builtin_bit_cast(double2, __builtin_amdgcn_raw_buffer_load_b128(rg, off, 0, 16));
+  for (unsigned spin = 0; g2.y != tag; ++spin) {
+    if (spin > (1u << 22)) {
+      *err = 1;
+      break;
+    }
+    __builtin_amdgcn_s_sleep(1);
+    g2 = __builtin_bit_cast(double2, __builtin_amdgcn_raw_buffer_load_b128(rg, off, 0, 16));
+  }
+  return g2;
+}
+
+template <int NV>
+__device__ bool publish_and_reduce_tagged(double (&v)[NV], double* gran, unsigned* tickets, int lb,
+                                          int nwg, double tag, int* err, double (&tot)[NV],
+                                          double* s_red, int* s_flag) {
+  block_sum<NV>(v, s_red);
+  const int ngroups = red_groups(nwg);
+  const int grp = lb / kGroup, g0 = grp * kGroup, gn = min(kGroup, nwg - g0);
+  // granules: [j][workgroup] then [j][group]
+  const __amdgpu_buffer_rsrc_t rg = rsrc(gran, (unsigned)(NV * (nwg + ngroups) * 16));
+  const int goff = NV * nwg;
+  if (threadIdx.x == 0) {
+#pragma unroll
+    for (int j = 0; j < NV; ++j)
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, make_double2(v[j], tag)), rg,
+                                             (j * nwg + lb) * 16, 0, 16);
+    const unsigned tk = __hip_atomic_fetch_add(&tickets[grp * kTicketStride], 1u,
+                                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_flag[0] = tk == (unsigned)(gn - 1);
+  }
+  __syncthreads();
+  if (!s_flag[0]) return false;
+  if (threadIdx.x < 64) {  // last of its group: wave 0 sums the group's partials
+    const int lane = threadIdx.x;
+    double w[NV];
+#pragma unroll
+    for (int j = 0; j < NV; ++j) {
+      w[j] = lane < gn ? gran_poll(rg, (j * nwg + g0 + lane) * 16, tag, err).x : 0.0;
+      w[j] = wave_sum(w[j]);
+    }
+    if (lane == 0) {
+#pragma unroll
+      for (int j = 0; j < NV; ++j)
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, make_double2(w[j], tag)), rg,
+                                               (goff + j * ngroups + grp) * 16, 0, 16);
+      __hip_atomic_store(&tickets[grp * kTicketStride], 0u, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+      const unsigned tk = __hip_atomic_fetch_add(&tickets[ngroups * kTicketStride], 1u,
+                                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      s_flag[1] = tk == (unsigned)(ngroups - 1);
+    }
+  }
+  __syncthreads();
+  if (!s_flag[1]) return false;
+  double acc[NV];
+#pragma unroll
+  for (int j = 0; j < NV; ++j) acc[j] = 0.0;
+  for (int i = threadIdx.x; i < ngroups; i += blockDim.x) {
+#pragma unroll
+    for (int j = 0; j < NV; ++j) acc[j] = acc[j] + gran_poll(rg, (goff + j * ngroups + i) * 16, tag, err).x;
+  }
+  __syncthreads();  // s_red reuse
+  block_sum<NV>(acc, s_red);
+  if (threadIdx.x == 0) {
+#pragma unroll
+    for (int j = 0; j < NV; ++j) s_red[16 + j] = acc[j];
+    __hip_atomic_store(&tickets[ngroups * kTicketStride], 0u, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < NV; ++j) tot[j] = s_red[16 + j];
+  return true;
+}
+
 constexpr int kMarchW = 128;     // columns per wave strip
 constexpr int kMarchWaves = 4;   // waves (strips) per workgroup
 
@@ -2093,8 +2184,9 @@ constexpr int kMarchWavesPerEU = D == 2 && (MODE == kMarchPQ || SM) ? 4 : 1;
 // kernel overwrites a scalar its own workgroups still read.
 // TR: phase probe -- lane 0 of every wave stores {kernel entry, walk end,
 // exit, hardware id} wall-clock stamps (100 MHz) into a.mtrace[4 w ..]
+// TAG: the epilogue reductions by tagged granules (publish_and_reduce_tagged)
 template <int MODE, bool SM = false, int D = kMarchDepth, int PAUX = 0, int SAUX = kNT,
-          bool DEFER = false, bool TR = false>
+          bool DEFER = false, bool TR = false, bool TAG = false>
 __global__ __launch_bounds__(64 * kMarchWaves, (kMarchWavesPerEU<MODE, D, SM>)) void k_cg_march(CGArgs a) {
   static_assert(!DEFER || MODE != kMarchPQ, "deferred reduction: q-free P / B only");
   const unsigned long long tr_t0 = TR ? wall_clock64() : 0ull;
@@ -2271,7 +2363,10 @@ __global__ __launch_bounds__(64 * kMarchWaves, (kMarchWavesPerEU<MODE, D, SM>)) 
   }
   if (MODE != kMarchB) {
     double v[1] = {acc[0]}, tot[1];
-    if (publish_and_reduce<1>(v, a.partials, a.tickets, lb, gridDim.x, tot, s_red, s_flag)) {
+    const bool last = TAG ? publish_and_reduce_tagged<1>(v, a.mgran, a.tickets, lb, gridDim.x, a.mtag,
+                                                         a.merr, tot, s_red, s_flag)
+                          : publish_and_reduce<1>(v, a.partials, a.tickets, lb, gridDim.x, tot, s_red, s_flag);
+    if (last) {
       if (threadIdx.x == 0) {
         if (a.slab) {
           S->part[0] = tot[0];
@@ -2283,8 +2378,13 @@ __global__ __launch_bounds__(64 * kMarchWaves, (kMarchWavesPerEU<MODE, D, SM>)) 
     }
   } else {
     double tot[2];
-    if (publish_and_reduce<2>(acc, a.partials + a.pstride, a.tickets + a.tstride, lb, gridDim.x,
-                              tot, s_red, s_flag)) {
+    const bool last =
+        TAG ? publish_and_reduce_tagged<2>(acc, a.mgran + 4 * ((size_t)gridDim.x + red_groups(gridDim.x)),
+                                           a.tickets + a.tstride, lb, gridDim.x, a.mtag, a.merr, tot,
+                                           s_red, s_flag)
+            : publish_and_reduce<2>(acc, a.partials + a.pstride, a.tickets + a.tstride, lb, gridDim.x,
+                                    tot, s_red, s_flag);
+    if (last) {
       if (threadIdx.x == 0) {  // k_cg_b's epilogue
         const int kk = S->iter + 1;
         const double err = sqrt(tot[1]) / S->bnrm;
@@ -3519,6 +3619,9 @@ CGArgs make_cg_args(perc_ctx* h) {
   a.mtrace = nullptr;
   a.wslots = 0;
   for (int i = 0; i <= kMaxSlotRounds; ++i) a.wcum[0][i] = a.wcum[1][i] = 0;
+  a.mgran = nullptr;
+  a.mtag = 0.0;
+  a.merr = nullptr;
   return a;
 }
 
@@ -3544,6 +3647,13 @@ void launch_march_sm2(perc_ctx* h, hipStream_t st, const CGArgs& a) {
   if constexpr (SAUX == kNT) {
     if (a.mtrace && !h->march_defer) {  // phase probe (PERC_MARCH_TRACE)
       klaunch(h, k_cg_march<MODE, true, 3, 2, SAUX, false, true>, grid, 64 * kMarchWaves, st, a);
+      return;
+    }
+  }
+  if constexpr (SAUX == kNT) {
+    if (a.mgran && !h->march_defer) {  // tagged-granule reductions (PERC_MARCH_TAG)
+      if (a.mtrace) klaunch(h, k_cg_march<MODE, true, 3, 2, SAUX, false, true, true>, grid, 64 * kMarchWaves, st, a);
+      else klaunch(h, k_cg_march<MODE, true, 3, 2, SAUX, false, false, true>, grid, 64 * kMarchWaves, st, a);
       return;
     }
   }
@@ -3866,7 +3976,7 @@ void dev_free_all(perc_ctx* h) {
                   d.order, d.parent, d.member, d.top, d.counters, d.x, d.r,
                   d.p0, d.p1, d.q, d.partials, d.tickets, d.scal, d.err_hist, d.iout,
                   d.res_xch, d.res_part, d.res_bar, d.bw, d.code_sm, d.csize, d.res_gran,
-                  d.sel_hist};
+                  d.sel_hist, d.mgran};
   for (void* p : ptrs)
     if (p) hipFree(p);
   d = DeviceBuffers{};
@@ -4215,6 +4325,11 @@ void select_format(perc_ctx* h) {
   bool rms = slots && (size_t)h->N * sizeof(double) > kLargeVector;
   if (const char* e = getenv("PERC_MARCH_RMSLOTS")) rms = atoi(e) != 0;
   h->march_slots_rm = rms && !h->strips && h->qfree && h->wm_slots > 0;
+  // tagged-granule reductions (PERC_MARCH_TAG; PERC_MARCH_TAG=0/1 overrides)
+  bool tag = (h->march_mode & PERC_MARCH_TAG) != 0;
+  if (const char* e = getenv("PERC_MARCH_TAG")) tag = atoi(e) != 0;
+  h->march_tag = tag && h->strips && h->qfree && h->march_depth == 3 && h->march_paux == 2 &&
+                 h->march_baux == 2 && h->march_bdepth == 3;
 }
 
 // strip-major copies of r (into the q buffer: r and q swap roles for the
@@ -4232,7 +4347,7 @@ hipError_t to_strips(perc_ctx* h, CGArgs& a) {
   a.St.code = d.code_sm;
   a.sm = 1;
   a.bx = 1;  // x (row-major) is updated in B: k_cg_b, or the q-free march B
-  if (h->march_slots && h->qfree && !h->march_defer && h->march_depth == 3 && h->march_paux == 2 &&
+  if (h->march_slots && h->qfree && h->march_depth == 3 && h->march_paux == 2 &&
       h->march_baux == 2 && h->march_bdepth == 3) {
     a.wslots = h->wm_slots;
     for (int i = 0; i <= h->wm_slots; ++i) {
@@ -4467,6 +4582,21 @@ hipError_t dev_solve(perc_ctx* h, int itol, double tol, int itmax, bool x0_zero,
     h->resident = false;
   }
   if (h->strips) HIP_TRY(to_strips(h, a));
+  // tagged-granule reductions of the strip-major q-free march
+  if (h->march_tag && a.sm && h->qfree && !h->march_defer) {
+    const int G = red_grid(h);
+    const size_t need = (size_t)8 * ((size_t)G + red_groups(G));
+    if (h->d.mgran_n < need) {
+      if (h->d.mgran) HIP_TRY(hipFree(h->d.mgran));
+      h->d.mgran = nullptr;
+      HIP_TRY(dmalloc(&h->d.mgran, need));
+      HIP_TRY(hipMemsetAsync(h->d.mgran, 0, need * sizeof(double), st));  // tag 0: never a launch's
+      h->d.mgran_n = need;
+    }
+    a.mgran = h->d.mgran;
+    a.merr = &d.scal->pad[1];
+    ++h->solve_epoch;
+  }
   // row-major q-free march past the Infinity Cache: the P kernel on one
   // round of slot-weighted bands (probe PERC_MARCH_RMSLOTS=1), B on its
   // short bands
@@ -4509,6 +4639,8 @@ hipError_t dev_solve(perc_ctx* h, int itol, double tol, int itmax, bool x0_zero,
       const bool tm = T.enabled && j % kTimeEvery == 0;
       hipEvent_t* ev = tm ? &T.ev[kEv * j] : nullptr;
       a.kiter = (int)(launched + j + 1);
+      // (tag: exact in a double while solve_epoch < 2^29)
+      a.mtag = (double)(((unsigned long long)h->solve_epoch << 24) | (unsigned long long)a.kiter);
       const int mti = a.kiter - mt_it;
       a.mtrace = mtbuf && mti >= 0 && mti < kMtN ? mtbuf + (size_t)2 * mti * 4 * mtwaves : nullptr;
       if (!h->fused) {
@@ -4577,6 +4709,10 @@ hipError_t dev_solve(perc_ctx* h, int itol, double tol, int itmax, bool x0_zero,
           }
       fclose(fo);
     }
+  }
+  if (e == hipSuccess && a.mgran && hsp->pad[1] != 0) {
+    fprintf(stderr, "[perc] k_cg_march: reduction granule not seen within the poll limit\n");
+    e = hipErrorLaunchTimeOut;
   }
   *iter = hsp->iter;
   *err = hsp->err;

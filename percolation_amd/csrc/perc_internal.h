@@ -106,6 +106,8 @@ struct DeviceBuffers {
   double* partials = nullptr;   // 4 * grid
   unsigned* tickets = nullptr;  // 8
   CGScalars* scal = nullptr;
+  double* mgran = nullptr;      // march tagged-granule reductions
+  size_t mgran_n = 0;
   double* err_hist = nullptr;   // itmax+2
   int err_hist_cap = 0;
   double* iout = nullptr;       // 2m (boundary-row currents)
@@ -182,6 +184,8 @@ struct perc_ctx {
   int march_defer = 0;          // q-free strip-major march: reductions deferred to the next kernel
   int march_slots = 0;          // q-free strip-major march: slot-weighted bands
   int march_slots_rm = 0;       // q-free row-major march: slot-weighted bands for P
+  int march_tag = 0;            // q-free strip-major march: tagged-granule reductions
+  unsigned solve_epoch = 0;     // tags of the granule reductions
   int wm_slots = 0;             // slot-weighted bands: workgroup rounds (0: not available)
   int wm_grid = 0;              // their grid (CUs x rounds)
   int wm_cum[3][5] = {};        // cumulative round weights (P, B, row-major P)

@@ -548,7 +548,8 @@ MARCH_MODES = (PL.MARCH_DEFAULT, 0, PL.MARCH_QFREE, PL.MARCH_ALT, PL.MARCH_ROWS,
                PL.MARCH_STRIPS | PL.MARCH_QFREE, PL.MARCH_STRIPS | PL.MARCH_ALT,
                PL.MARCH_STRIPS | PL.MARCH_QFREE | PL.MARCH_ALT,
                PL.MARCH_STRIPS | PL.MARCH_QFREE | PL.MARCH_ALT | PL.MARCH_DEFER,
-               PL.MARCH_STRIPS | PL.MARCH_QFREE | PL.MARCH_ALT | PL.MARCH_SLOTS)
+               PL.MARCH_STRIPS | PL.MARCH_QFREE | PL.MARCH_ALT | PL.MARCH_SLOTS,
+               PL.MARCH_STRIPS | PL.MARCH_QFREE | PL.MARCH_ALT | PL.MARCH_TAG)
 
 
 @pytest.mark.parametrize("lat,m,n,pbc,p", [(0, 256, 150, 0, 0.6), (1, 128, 99, 1, 0.42),
@@ -619,10 +620,11 @@ def test_march_modes_one_iteration_bitwise(lat, m, n, pbc, p):
                                            (0, 1024, 1024, 0, 0.55), (0, 256, 160, 1, 0.6)])
 def test_deferred_reduction_is_bitwise_the_in_kernel_one(lat, m, n, pbc, p):
     """PERC_MARCH_DEFER (the strip-major q-free march whose dot products
-    are summed by every workgroup of the next kernel): the same totals term
-    for term as the last-arriving-workgroup reduction, so the whole solve --
-    iteration count, err history, Gtop, Gbot, every voltage -- is bitwise
-    the same, at the reference tolerance and converged."""
+    are summed by every workgroup of the next kernel) and PERC_MARCH_TAG
+    (tagged-granule partials, no store drain before the tickets): the same
+    totals term for term as the last-arriving-workgroup reduction, so the
+    whole solve -- iteration count, err history, Gtop, Gbot, every voltage
+    -- is bitwise the same, at the reference tolerance and converged."""
     nb = api.nbonds(lat, m, n, pbc)
     order = api.shuffled_ids(nb, 2718)
     base = PL.MARCH_QFREE | PL.MARCH_ALT | PL.MARCH_STRIPS  # the march, not the resident solve
@@ -632,16 +634,18 @@ def test_deferred_reduction_is_bitwise_the_in_kernel_one(lat, m, n, pbc, p):
             pytest.skip("no spanning cluster")
         for tol in (1e-8, 1e-13):
             out = []
-            for mode in (base, base | PL.MARCH_DEFER):
+            for mode in (base, base | PL.MARCH_DEFER, base | PL.MARCH_TAG):
                 ctx.set_march_mode(mode)
                 c = ctx.conductance(tol=tol, itmax=10 ** 6, vint=True)
                 info = ctx.march_info()
                 assert info["kernel"] == "wave" and info["defer"] == bool(mode & PL.MARCH_DEFER)
+                assert info["tag"] == bool(mode & PL.MARCH_TAG)
                 out.append(c)
-            a, b = out
-            assert a["iter"] == b["iter"] and a["err"] == b["err"], (tol, a["iter"], b["iter"])
-            assert a["gtop"] == b["gtop"] and a["gbot"] == b["gbot"], tol
-            assert np.array_equal(a["vint"].view(np.uint64), b["vint"].view(np.uint64))
+            a = out[0]
+            for b in out[1:]:
+                assert a["iter"] == b["iter"] and a["err"] == b["err"], (tol, a["iter"], b["iter"])
+                assert a["gtop"] == b["gtop"] and a["gbot"] == b["gbot"], tol
+                assert np.array_equal(a["vint"].view(np.uint64), b["vint"].view(np.uint64))
         ctx.set_march_mode(PL.MARCH_DEFAULT)
 
 
