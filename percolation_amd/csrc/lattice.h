@@ -20,6 +20,7 @@ struct Geom {
   int t;        // m*n
   int scn;      // site coordination number (4 / 6)
   int bcn;      // bond coordination number (6 / 10)
+  unsigned long long mrecip;  // ceil(2^64 / m) for m > 1, else 0 (div_m)
 };
 
 __host__ __device__ inline Geom make_geom(int lattice, int m, int n, int pbc) {
@@ -31,6 +32,7 @@ __host__ __device__ inline Geom make_geom(int lattice, int m, int n, int pbc) {
   g.t = m * n;
   g.scn = lattice == kSquare ? 4 : 6;
   g.bcn = lattice == kSquare ? 6 : 10;
+  g.mrecip = m > 1 ? ~0ull / (unsigned long long)m + 1ull : 0ull;
   return g;
 }
 
@@ -41,21 +43,28 @@ __host__ __device__ inline long long nbonds(const Geom& g) {
   return g.pbc ? m * (3 * n - 2) : 3 * m * n - 2 * m - 2 * n + 1;
 }
 
-__host__ __device__ inline void nearestn_square(const Geom& g, int rn, int* nn) {
+// nearestn of site rn at (row r, column col) = ((rn-1)/m, (rn-1)%m): the
+// reference's branches in the reference's order, each test on rn restated on
+// (r, col) -- rn == 1 <=> r == 0 && col == 0, rn < m <=> r == 0 && col < m-1,
+// rn > t-m <=> r == n-1, (rn-1)%m == 0 <=> col == 0, rn%m == 0 <=> col == m-1,
+// and (rn/m)%2 == r%2 where it is asked (interior columns) -- so the device
+// kernels divide once per site (div_m) instead of at every modulo.
+__host__ __device__ inline void nearestn_square_rc(const Geom& g, int rn, int r, int col, int* nn) {
   const int m = g.m, t = g.t;
+  const bool b0 = r == 0, bT = r == g.n - 1, cL = col == 0, cR = col == m - 1;
   nn[0] = nn[1] = nn[2] = nn[3] = 0;
-  if (rn == 1) { nn[0] = rn + 1; nn[1] = rn + m; if (g.pbc) nn[2] = m; return; }
-  if (rn == m) { nn[0] = rn - 1; nn[1] = rn + m; if (g.pbc) nn[2] = 1; return; }
-  if (rn == t - (m - 1)) { nn[0] = rn - m; nn[1] = rn + 1; if (g.pbc) nn[2] = t; return; }
-  if (rn == t) { nn[0] = rn - m; nn[1] = rn - 1; if (g.pbc) nn[2] = rn - (m - 1); return; }
-  if (rn < m) { nn[0] = rn - 1; nn[1] = rn + 1; nn[2] = rn + m; return; }
-  if (rn > t - m) { nn[0] = rn - m; nn[1] = rn - 1; nn[2] = rn + 1; return; }
-  if ((rn - 1) % m == 0) {
+  if (b0 && cL) { nn[0] = rn + 1; nn[1] = rn + m; if (g.pbc) nn[2] = m; return; }
+  if (b0 && cR) { nn[0] = rn - 1; nn[1] = rn + m; if (g.pbc) nn[2] = 1; return; }
+  if (bT && cL) { nn[0] = rn - m; nn[1] = rn + 1; if (g.pbc) nn[2] = t; return; }
+  if (bT && cR) { nn[0] = rn - m; nn[1] = rn - 1; if (g.pbc) nn[2] = rn - (m - 1); return; }
+  if (b0) { nn[0] = rn - 1; nn[1] = rn + 1; nn[2] = rn + m; return; }
+  if (bT) { nn[0] = rn - m; nn[1] = rn - 1; nn[2] = rn + 1; return; }
+  if (cL) {
     nn[0] = rn - m; nn[1] = rn + 1; nn[2] = rn + m;
     if (g.pbc) nn[3] = rn + (m - 1);
     return;
   }
-  if (rn % m == 0) {
+  if (cR) {
     nn[0] = rn - m; nn[1] = rn - 1; nn[2] = rn + m;
     if (g.pbc) nn[3] = rn - (m - 1);
     return;
@@ -63,54 +72,55 @@ __host__ __device__ inline void nearestn_square(const Geom& g, int rn, int* nn) 
   nn[0] = rn - m; nn[1] = rn - 1; nn[2] = rn + 1; nn[3] = rn + m;
 }
 
-__host__ __device__ inline void nearestn_tri(const Geom& g, int rn, int* nn) {
+__host__ __device__ inline void nearestn_tri_rc(const Geom& g, int rn, int r, int col, int* nn) {
   const int m = g.m, t = g.t;
-  const bool odd_m = (m % 2) == 1;
+  const bool odd_m = (m & 1) == 1, even_rn = (rn & 1) == 0;
+  const bool b0 = r == 0, bT = r == g.n - 1, cL = col == 0, cR = col == m - 1;
   for (int z = 0; z < 6; ++z) nn[z] = 0;
-  if (rn == 1) {
+  if (b0 && cL) {
     nn[0] = rn + 1; nn[1] = rn + m; nn[2] = rn + (m + 1);
     if (g.pbc) { nn[3] = rn + (m - 1); nn[4] = rn + (2 * m - 1); }
     return;
   }
-  if (rn == m) {
+  if (b0 && cR) {
     nn[0] = rn - 1; nn[1] = rn + m;
     if (odd_m) { nn[2] = rn + (m - 1); return; }
     if (g.pbc) nn[2] = 1;
     return;
   }
-  if (rn == t - (m - 1)) {
+  if (bT && cL) {
     nn[0] = rn - m; nn[1] = rn + 1;
     if (g.pbc) nn[2] = t;
     return;
   }
-  if (rn == t) {
+  if (bT && cR) {
     if (odd_m) { nn[0] = rn - m; nn[1] = rn - 1; return; }
     nn[0] = rn - (m + 1); nn[1] = rn - m; nn[2] = rn - 1;
     if (g.pbc) { nn[3] = rn - (2 * m - 1); nn[4] = rn - (m - 1); }
     return;
   }
-  if (rn < m) {  // bottom row
-    if (rn % 2 == 0) {
+  if (b0) {  // bottom row
+    if (even_rn) {
       nn[0] = rn - 1; nn[1] = rn + 1; nn[2] = rn + m;
     } else {
       nn[0] = rn - 1; nn[1] = rn + 1; nn[2] = rn + (m - 1); nn[3] = rn + m; nn[4] = rn + (m + 1);
     }
     return;
   }
-  if (rn > t - m) {  // top row
-    if (rn % 2 == 0) {
+  if (bT) {  // top row
+    if (even_rn) {
       nn[0] = rn - (m + 1); nn[1] = rn - m; nn[2] = rn - (m - 1); nn[3] = rn - 1; nn[4] = rn + 1;
     } else {
       nn[0] = rn - m; nn[1] = rn - 1; nn[2] = rn + 1;
     }
     return;
   }
-  if ((rn - 1) % m == 0) {  // left edge
+  if (cL) {  // left edge
     nn[0] = rn - m; nn[1] = rn + 1; nn[2] = rn + m; nn[3] = rn + (m + 1);
     if (g.pbc) { nn[4] = rn + (m - 1); nn[5] = rn + (2 * m - 1); }
     return;
   }
-  if (rn % m == 0) {  // right edge
+  if (cR) {  // right edge
     if (odd_m) {
       nn[0] = rn - m; nn[1] = rn - 1; nn[2] = rn + (m - 1); nn[3] = rn + m;
       return;
@@ -119,12 +129,8 @@ __host__ __device__ inline void nearestn_tri(const Geom& g, int rn, int* nn) {
     if (g.pbc) { nn[4] = rn - (2 * m - 1); nn[5] = rn - (m - 1); }
     return;
   }
-  bool up;  // "up" form: rn-(m+1), rn-m, rn-(m-1), rn-1, rn+1, rn+m
-  if (odd_m) {
-    up = ((rn / m) % 2 == 0) ? (rn % 2 == 0) : (rn % 2 != 0);
-  } else {
-    up = (rn % 2 == 0);
-  }
+  // "up" form: rn-(m+1), rn-m, rn-(m-1), rn-1, rn+1, rn+m
+  const bool up = odd_m ? (((r & 1) == 0) == even_rn) : even_rn;
   if (up) {
     nn[0] = rn - (m + 1); nn[1] = rn - m; nn[2] = rn - (m - 1);
     nn[3] = rn - 1; nn[4] = rn + 1; nn[5] = rn + m;
@@ -134,9 +140,14 @@ __host__ __device__ inline void nearestn_tri(const Geom& g, int rn, int* nn) {
   }
 }
 
+__host__ __device__ inline void nearestn_rc(const Geom& g, int rn, int r, int col, int* nn) {
+  if (g.lattice == kSquare) nearestn_square_rc(g, rn, r, col, nn);
+  else nearestn_tri_rc(g, rn, r, col, nn);
+}
+
 __host__ __device__ inline void nearestn(const Geom& g, int rn, int* nn) {
-  if (g.lattice == kSquare) nearestn_square(g, rn, nn);
-  else nearestn_tri(g, rn, nn);
+  const int r = (rn - 1) / g.m;
+  nearestn_rc(g, rn, r, rn - 1 - r * g.m, nn);
 }
 
 // Neighbours of rn sorted ascending (the dense-row scan order of G, used for
@@ -166,6 +177,15 @@ __host__ __device__ inline void lattice_delta(const Geom& g, int s, int c, int* 
   else if (d < -1) d += g.m;
   *dr = cr - sr;
   *dc = d;
+}
+
+// bond_first of the square lattice's site (row r, column c), r <= n-2: rows
+// 0..n-2 each hold 2m-1 (+1 with pbc) forward bonds -- 2 per site, +1 at
+// column 0 with pbc (the wrap bond), -1 at column m-1 (no right neighbour).
+// Used where perc_ctx::bf_closed says the built bond_first agrees.
+__host__ __device__ inline int bf_square(const Geom& g, int r, int c) {
+  const int pb = g.pbc ? 1 : 0;
+  return r * (2 * g.m - 1 + pb) + 2 * c + (c > 0 ? pb : 0);
 }
 
 // Number of bonds whose smaller end is rn (bond list, Square/bondc.f:139-154)

@@ -13,6 +13,8 @@
 
 #include <hip/hip_ext.h>
 
+#include <cmath>
+
 namespace perc {
 namespace {
 
@@ -241,6 +243,24 @@ __device__ __forceinline__ int bond_id(const Geom& g, const int* bond_first, int
   return -1;
 }
 
+// x / g.m for 0 <= x < 2^31 by the 64-bit reciprocal of lattice.h (exact:
+// ceil(2^64/m) * m - 2^64 < m, so the error term x*(that)/2^64 < 1/m)
+__device__ __forceinline__ int div_m(const Geom& g, int x) {
+  return g.mrecip ? (int)__umul64hi((unsigned long long)x, g.mrecip) : x;
+}
+
+// bond_id(p, q) from p's neighbour list nnp and fb = bond_first[p]: the rank
+// of q among p's forward neighbours
+__device__ __forceinline__ int fwd_bond_id(const Geom& g, const int* nnp, int fb, int p, int q) {
+  int r = 0;
+  for (int k = 0; k < g.scn; ++k)
+    if (nnp[k] > p) {
+      if (nnp[k] == q) return fb + r;
+      ++r;
+    }
+  return -1;
+}
+
 __global__ void k_row_count(Geom g, int N, int* rc /* N+1 */) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i > N) return;
@@ -272,32 +292,211 @@ __global__ void k_occupy(const int* order, int count, long long limit, uint8_t* 
   const int id = order[k];
   if (id > 0 && id <= limit) occ[id - 1] = 1;
 }
-// radix select of the `count`-th smallest key (perc_occupy_random): per pass
-// the 256-bin histogram of one key byte among the keys matching the prefix
-// found so far (LDS bins, one global atomic per bin and workgroup)
-__global__ __launch_bounds__(kBlock) void k_select_hist(long long n, unsigned long long seed,
-                                                         unsigned long long prefix,
-                                                         unsigned long long pmask, int shift,
-                                                         unsigned* hist) {
-  __shared__ unsigned s_h[256];
-  s_h[threadIdx.x] = 0;  // kBlock == 256
+__device__ __forceinline__ int wave_sum_int(int v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+
+// The `count`-th smallest key T of ids 1..n (perc_occupy_random) without a
+// host round trip.  The 32-bit hashes are uniform, so T's hash lies, with
+// overwhelming probability, in a window [lo, hi) a few binomial standard
+// deviations around count/n * 2^32.  k_select_window counts the keys below
+// the window and gathers the keys inside it (LDS staging, one global
+// reservation per workgroup, at most kSelCap keys); k_select_final (one
+// workgroup) bins the window keys by hash (kSelBins LDS bins), finds the bin
+// holding the (count - below)-th smallest and ranks that bin's few keys.  A
+// crowded bin falls back to an 8-pass radix select of the window keys, T
+// outside the window (or an overflowing window) to the radix select of all n
+// keys -- slow, exact: T is the exact order statistic on every path.
+constexpr int kSelCap = 1 << 17, kSelThreads = 1024, kSelStage = 512, kSelBins = 4096;
+constexpr int kSelBinCap = 1024;
+__global__ __launch_bounds__(kBlock) void k_select_window(long long n, unsigned long long seed,
+                                                          unsigned long long lo,
+                                                          unsigned long long hi,
+                                                          unsigned* cnt,
+                                                          unsigned long long* cand) {
+  __shared__ unsigned long long s_c[kSelStage];
+  __shared__ unsigned s_n, s_base, s_b[kBlock / 64];
+  if (threadIdx.x == 0) s_n = 0;
   __syncthreads();
+  unsigned below = 0;
+  const int lane = threadIdx.x & 63;
   for (long long i = (long long)blockIdx.x * kBlock + threadIdx.x; i < n;
        i += (long long)gridDim.x * kBlock) {
     const unsigned long long key = perc_rand_key(seed, (unsigned)(i + 1));
-    if ((key & pmask) == prefix) atomicAdd(&s_h[(key >> shift) & 255u], 1u);
+    const unsigned long long hsh = key >> 32;
+    below += hsh < lo;
+    if (hsh >= lo && hsh < hi) {
+      const unsigned slot = atomicAdd(&s_n, 1u);
+      if (slot < (unsigned)kSelStage) {
+        s_c[slot] = key;
+      } else {  // a crowded workgroup: straight to the global list
+        const unsigned idx = atomicAdd(&cnt[1], 1u);
+        if (idx < (unsigned)kSelCap) cand[1 + idx] = key;
+      }
+    }
+  }
+  below = (unsigned)wave_sum_int((int)below);
+  if (lane == 0) s_b[threadIdx.x >> 6] = below;
+  __syncthreads();
+  const unsigned nst = min(s_n, (unsigned)kSelStage);
+  if (threadIdx.x == 0) {
+    unsigned tot = 0;
+    for (int w = 0; w < kBlock / 64; ++w) tot += s_b[w];
+    if (tot) atomicAdd(&cnt[0], tot);
+    s_base = nst ? atomicAdd(&cnt[1], nst) : 0u;
   }
   __syncthreads();
-  if (s_h[threadIdx.x]) atomicAdd(&hist[threadIdx.x], s_h[threadIdx.x]);
+  for (unsigned j = threadIdx.x; j < nst; j += kBlock)
+    if (s_base + j < (unsigned)kSelCap) cand[1 + s_base + j] = s_c[j];
+}
+
+__global__ __launch_bounds__(kSelThreads) void k_select_final(long long n,
+                                                              unsigned long long seed,
+                                                              long long count,
+                                                              unsigned long long lo,
+                                                              unsigned long long hi,
+                                                              const unsigned* cnt,
+                                                              unsigned long long* cand) {
+  __shared__ unsigned s_h[kSelBins];
+  __shared__ unsigned long long s_k[kSelBinCap];
+  __shared__ unsigned long long s_sel[2];  // prefix, need
+  __shared__ int s_bin, s_nb;
+  unsigned long long* tr = cand + 1 + kSelCap;  // PERC_SELECT_TRACE stamps
+  if (threadIdx.x == 0) tr[0] = wall_clock64();
+  const long long below = cnt[0], nin = cnt[1];
+  const bool win = count > below && count - below <= nin && nin <= kSelCap;
+  if (win) {
+    // bins of the window's hash range: (hash - lo) >> sh < kSelBins
+    const unsigned long long range = hi - lo;
+    const int bits = range > 1 ? 64 - __clzll((long long)(range - 1)) : 0;
+    const int sh = max(0, bits - 12);
+    for (int j = threadIdx.x; j < kSelBins; j += kSelThreads) s_h[j] = 0;
+    if (threadIdx.x == 0) s_nb = 0;
+    __syncthreads();
+    constexpr int kU = 8;  // loads in flight per thread
+    for (long long i0 = threadIdx.x; i0 < nin; i0 += kSelThreads * kU) {
+      unsigned long long kk[kU];
+#pragma unroll
+      for (int u = 0; u < kU; ++u) kk[u] = i0 + u * kSelThreads < nin ? cand[1 + i0 + u * kSelThreads] : 0;
+#pragma unroll
+      for (int u = 0; u < kU; ++u)
+        if (i0 + u * kSelThreads < nin) atomicAdd(&s_h[((kk[u] >> 32) - lo) >> sh], 1u);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) tr[1] = wall_clock64();
+    {  // the bin of the (count - below)-th window key: a block scan of the
+       // bin counts, kPerT consecutive bins per thread (a serial scan of
+       // 4096 LDS words by one thread costs ~70 us)
+      constexpr int kPerT = kSelBins / kSelThreads;
+      static_assert(kSelBins % kSelThreads == 0, "bins per thread");
+      __shared__ unsigned s_w[kSelThreads / 64];
+      const unsigned need = (unsigned)(count - below);
+      unsigned loc[kPerT], sum = 0;
+#pragma unroll
+      for (int u = 0; u < kPerT; ++u) {
+        loc[u] = s_h[threadIdx.x * kPerT + u];
+        sum += loc[u];
+      }
+      const int ln = threadIdx.x & 63, wv = threadIdx.x >> 6;
+      unsigned inc = sum;
+#pragma unroll
+      for (int off = 1; off < 64; off <<= 1) {
+        const unsigned y = __shfl_up(inc, off, 64);
+        if (ln >= off) inc += y;
+      }
+      if (ln == 63) s_w[wv] = inc;
+      __syncthreads();
+      unsigned before = inc - sum;
+      for (int w2 = 0; w2 < wv; ++w2) before += s_w[w2];
+      if (before < need && before + sum >= need) {  // exactly one thread
+        unsigned cum = before;
+        int u = 0;
+        for (; u < kPerT - 1; ++u) {
+          if (cum + loc[u] >= need) break;
+          cum += loc[u];
+        }
+        s_bin = threadIdx.x * kPerT + u;
+        s_sel[1] = need - cum;
+      }
+    }
+    __syncthreads();
+    const int bin = s_bin;
+    if (s_h[bin] <= (unsigned)kSelBinCap) {
+      constexpr int kU = 8;
+      for (long long i0 = threadIdx.x; i0 < nin; i0 += kSelThreads * kU) {
+        unsigned long long kk[kU];
+#pragma unroll
+        for (int u = 0; u < kU; ++u)
+          kk[u] = i0 + u * kSelThreads < nin ? cand[1 + i0 + u * kSelThreads] : ~0ull;
+#pragma unroll
+        for (int u = 0; u < kU; ++u)
+          if (i0 + u * kSelThreads < nin && (int)(((kk[u] >> 32) - lo) >> sh) == bin)
+            s_k[atomicAdd(&s_nb, 1)] = kk[u];
+      }
+      __syncthreads();
+      if (threadIdx.x == 0) tr[2] = wall_clock64();
+      const int nb = s_nb;
+      const unsigned long long want = s_sel[1] - 1;  // 0-based rank in the bin
+      for (int j = threadIdx.x; j < nb; j += kSelThreads) {
+        const unsigned long long kj = s_k[j];
+        unsigned long long r = 0;
+        for (int u = 0; u < nb; ++u) r += s_k[u] < kj;
+        if (r == want) cand[0] = kj;  // keys are unique (id in the low bits)
+      }
+      if (threadIdx.x == 0) {
+        tr[3] = wall_clock64();
+        tr[4] = (unsigned long long)nin;
+        tr[5] = (unsigned long long)s_h[bin];
+      }
+      return;
+    }
+    __syncthreads();
+  }
+  // radix select, 8 passes of one key byte: of the window keys (a crowded
+  // bin) or of all n keys (T outside the window)
+  const long long nk = win ? nin : n;
+  if (threadIdx.x == 0) {
+    s_sel[0] = 0;
+    s_sel[1] = (unsigned long long)(win ? count - below : count);
+  }
+  unsigned long long mask = 0;
+  for (int pass = 0; pass < 8; ++pass) {
+    const int shift = 56 - 8 * pass;
+    if (threadIdx.x < 256) s_h[threadIdx.x] = 0;
+    __syncthreads();
+    const unsigned long long prefix = s_sel[0];
+    for (long long i = threadIdx.x; i < nk; i += kSelThreads) {
+      const unsigned long long key = win ? cand[1 + i] : perc_rand_key(seed, (unsigned)(i + 1));
+      if ((key & mask) == prefix) atomicAdd(&s_h[(key >> shift) & 255u], 1u);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      unsigned long long need = s_sel[1], cum = 0;
+      int b = 0;
+      for (; b < 255; ++b) {
+        if (cum + s_h[b] >= need) break;
+        cum += s_h[b];
+      }
+      s_sel[1] = need - cum;
+      s_sel[0] = prefix | (unsigned long long)b << shift;
+    }
+    mask |= 0xFFull << shift;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) cand[0] = s_sel[0];
 }
 
 // occupy every id whose key is <= T (T = the count-th smallest key);
 // occ[id - 1 + base] (bonds: base 0, 0-based; sites: base 1, socc[id])
+// (Tp: the threshold in device memory, k_select_final's; null: all n)
 __global__ __launch_bounds__(kBlock) void k_occupy_rand(long long n, unsigned long long seed,
-                                                         unsigned long long T, int base,
+                                                         const unsigned long long* Tp, int base,
                                                          uint8_t* occ) {
   const long long i = (long long)blockIdx.x * kBlock + threadIdx.x;
   if (i >= n) return;
+  const unsigned long long T = Tp ? *Tp : ~0ull;
   occ[i + base] = perc_rand_key(seed, (unsigned)(i + 1)) <= T ? 1 : 0;
 }
 
@@ -367,39 +566,126 @@ __device__ __forceinline__ bool cc_link(int kind, const uint8_t* bocc, const uin
 __global__ __launch_bounds__(kCcThreads) void k_cc_tile(Geom g, int kind, const int* bond_first,
                                                         const uint8_t* bocc,
                                                         const uint8_t* socc, int* parent,
-                                                        uint8_t* member) {
+                                                        uint8_t* member, int bf_closed,
+                                                        unsigned long long* trace) {
+  unsigned long long tr0 = trace ? wall_clock64() : 0ull;
+  static_assert(kCcW % 64 == 0 && kCcThreads % kCcW == 0, "a wave covers 64 columns of a tile row");
+  constexpr int kPer = kCcSites / kCcThreads;
   __shared__ int lp[kCcSites];
   __shared__ uint8_t lm[kCcSites];
+  __shared__ uint8_t lk[kCcSites];
   const int ntx = cdiv(g.m, kCcW);
   const int tx = blockIdx.x % ntx, ty = blockIdx.x / ntx;
   const int c0 = tx * kCcW, r0 = ty * kCcH;
   const int tw = min(kCcW, g.m - c0), th = min(kCcH, g.n - r0);
-  for (int li = threadIdx.x; li < kCcSites; li += kCcThreads) {
-    lp[li] = li;
-    lm[li] = 0;
+  const bool sq = g.lattice == kSquare;
+  // phase 1: each site's forward links (bit r: the r-th forward bond in
+  // nearestn order).  Square lattice, interior column, not the top row: the
+  // forward links are (s, s+1), (s, s+m), bond ids fb, fb+1 (nearestn_square
+  // lists +1 before +m in every such case).  All bond_first loads first,
+  // then all link loads: two memory latencies per thread, not 2 per site.
+  constexpr int kG = 8;  // sites per batch: loads of a batch in flight together
+  static_assert(kPer % kG == 0, "batches");
+  for (int k0 = 0; k0 < kPer; k0 += kG) {
+    int fbv[kG];
+    bool occv[kG];
+#pragma unroll
+    for (int u = 0; u < kG; ++u) {
+      const int li = threadIdx.x + (k0 + u) * kCcThreads, lr = li / kCcW, lc = li % kCcW;
+      const int s = (r0 + lr) * g.m + c0 + lc + 1;
+      const bool in = lr < th && lc < tw;
+      occv[u] = in && (kind == PERC_BOND || socc[s]);
+      const int row = r0 + lr;
+      fbv[u] = !in || s > g.t - 1 ? 0
+               : bf_closed && row <= g.n - 2 ? bf_square(g, row, c0 + lc)
+                                             : bond_first[s];
+    }
+#pragma unroll
+    for (int u = 0; u < kG; ++u) {
+      const int li = threadIdx.x + (k0 + u) * kCcThreads, lr = li / kCcW, lc = li % kCcW;
+      const int row = r0 + lr, col = c0 + lc;
+      const int s = row * g.m + col + 1;
+      unsigned mask = 0;
+      if (occv[u] && s <= g.t - 1) {
+        const int fb = fbv[u];
+        if (sq && col >= 1 && col <= g.m - 2 && row <= g.n - 2) {
+          mask = (unsigned)cc_link(kind, bocc, socc, fb, s, s + 1) |
+                 (unsigned)cc_link(kind, bocc, socc, fb + 1, s, s + g.m) << 1;
+        } else {
+          int nn[6];
+          nearestn_rc(g, s, row, col, nn);
+          int r = 0;
+          for (int kk = 0; kk < g.scn; ++kk) {
+            const int q = nn[kk];
+            if (q <= s) continue;
+            if (cc_link(kind, bocc, socc, fb + r, s, q)) mask |= 1u << r;
+            ++r;
+          }
+        }
+      }
+      lk[li] = (uint8_t)mask;
+      lm[li] = (uint8_t)((kind != PERC_BOND && occv[u]) || (kind == PERC_BOND && mask));
+    }
   }
   __syncthreads();
-  for (int li = threadIdx.x; li < kCcSites; li += kCcThreads) {
-    const int lr = li / kCcW, lc = li % kCcW;
-    if (lr >= th || lc >= tw) continue;
-    const int s = (r0 + lr) * g.m + c0 + lc + 1;
-    if (kind != PERC_BOND) {
-      if (!socc[s]) continue;  // an empty site has no links
-      lm[li] = 1;
+  unsigned long long tr1 = trace ? wall_clock64() : 0ull;
+  // phase 1b: the square lattice's horizontal runs.  Its first forward
+  // neighbour is s+1 whenever col < m-1 (every nearestn_square case), so bit
+  // 0 is the link to the right; a run's sites point at its first site (the
+  // run's minimum: larger -> smaller as every union), the second 64-column
+  // half of a row at the first half's last site when the run crosses.
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int k = 0; k < kPer; ++k) {
+    const int li = threadIdx.x + k * kCcThreads, lc = li % kCcW;
+    int par = li;
+    if (sq) {
+      const bool right = lc + 1 < tw && (lk[li] & 1u);
+      const unsigned long long rb = __ballot(right);
+      const bool left =
+          lc > 0 && lc < tw && (lane > 0 ? (rb >> (lane - 1) & 1ull) : (lk[li - 1] & 1u));
+      const unsigned long long starts = __ballot(!left);
+      const unsigned long long upto = starts & (lane == 63 ? ~0ull : ((2ull << lane) - 1ull));
+      par = upto ? li - lane + (63 - __clzll((long long)upto)) : li - lane - 1;
+      if (left && kind == PERC_BOND) lm[li] = 1;
     }
-    if (s > g.t - 1) continue;
-    int nn[6];
-    nearestn(g, s, nn);
-    const int fb = bond_first[s];
-    int r = 0;
-    for (int k = 0; k < g.scn; ++k) {
-      const int q = nn[k];
-      if (q <= s) continue;
-      const bool link = cc_link(kind, bocc, socc, fb + r, s, q);
-      ++r;
-      if (!link) continue;
-      if (kind == PERC_BOND) lm[li] = 1;
-      const int qr = (q - 1) / g.m - r0, qc = (q - 1) % g.m - c0;
+    lp[li] = par;
+  }
+  __syncthreads();
+  unsigned long long tr2 = trace ? wall_clock64() : 0ull;
+  // phase 2: the other links inside the tile, LDS union-find (crossing
+  // links: k_cc_merge).  (Measured: bottom-up order beats top-down -- finds
+  // 23 vs 28 us per tile, flatten 5 vs 12 us.)
+  for (int li = threadIdx.x; li < kCcSites; li += kCcThreads) {
+    unsigned mask = lk[li];
+    const int lr = li / kCcW, lc = li % kCcW;
+    if (sq && lc + 1 < tw) mask &= ~1u;  // in the run
+    // square interior: the link up from s is redundant when s-1 links up
+    // too and both s-1 -> s and s-1+m -> s+m are run links (a closed
+    // plaquette: the union of s-1 already joined the two runs)
+    if (sq && (mask & 2u) && lc >= 1 && lr + 1 < th && c0 + lc <= g.m - 2 && c0 + lc >= 1) {
+      const unsigned lft = lk[li - 1], lup = lk[li - 1 + kCcW];
+      if ((lft & 3u) == 3u && (lup & 1u) && c0 + lc - 1 >= 1) mask &= ~2u;
+    }
+    if (!mask) continue;
+    const int row = r0 + lr, col = c0 + lc;
+    const int s = row * g.m + col + 1;
+    int qs[6], nq = 0;
+    if (sq && col >= 1 && col <= g.m - 2 && row <= g.n - 2) {
+      qs[0] = s + 1;
+      qs[1] = s + g.m;
+      nq = 2;
+    } else {
+      int nn[6];
+      nearestn_rc(g, s, row, col, nn);
+      for (int kk = 0; kk < g.scn; ++kk)
+        if (nn[kk] > s) qs[nq++] = nn[kk];
+    }
+    for (int r = 0; r < nq; ++r) {
+      if (!(mask >> r & 1u)) continue;
+      const int q = qs[r];
+      const int qrow = div_m(g, q - 1);
+      const int qr = qrow - r0, qc = q - 1 - qrow * g.m - c0;
       if (qr < 0 || qr >= th || qc < 0 || qc >= tw) continue;  // crossing: k_cc_merge
       const int lq = qr * kCcW + qc;
       if (kind == PERC_BOND) lm[lq] = 1;
@@ -417,6 +703,7 @@ __global__ __launch_bounds__(kCcThreads) void k_cc_tile(Geom g, int kind, const 
     }
   }
   __syncthreads();
+  unsigned long long tr3 = trace ? wall_clock64() : 0ull;
   for (int li = threadIdx.x; li < kCcSites; li += kCcThreads) {
     const int lr = li / kCcW, lc = li % kCcW;
     if (lr >= th || lc >= tw) continue;
@@ -429,6 +716,14 @@ __global__ __launch_bounds__(kCcThreads) void k_cc_tile(Geom g, int kind, const 
     parent[s] = (r0 + x / kCcW) * g.m + c0 + x % kCcW + 1;
     member[s] = lm[li];
   }
+  if (trace && threadIdx.x == 0) {
+    unsigned long long* o = trace + 5 * (size_t)blockIdx.x;
+    o[0] = tr0;
+    o[1] = tr1;
+    o[2] = tr2;
+    o[3] = tr3;
+    o[4] = wall_clock64();
+  }
 }
 
 // one workgroup per lattice row: the sites whose forward links may leave
@@ -438,11 +733,22 @@ __global__ __launch_bounds__(kCcThreads) void k_cc_merge(Geom g, int kind, const
                                                          const uint8_t* bocc,
                                                          const uint8_t* socc, int* parent,
                                                          uint8_t* member) {
-  const int row = blockIdx.x;
+  // workgroups 0..n-1: one lattice row each (its first kCcThreads
+  // candidates); then the block-top rows' further candidates, nseg - 1
+  // workgroups of kCcThreads per such row (the unions are spread over the
+  // chip instead of queueing behind one workgroup per block-top row)
+  const int nseg = cdiv(g.m, kCcThreads);
+  int row = blockIdx.x, seg = 0, step = kCcThreads;
+  if (row >= g.n) {
+    const int e = row - g.n;
+    row = (e / (nseg - 1)) * kCcH + kCcH - 1;
+    seg = 1 + e % (nseg - 1);
+  }
   const bool full = row % kCcH == kCcH - 1;
   const int ntx = cdiv(g.m, kCcW);
   const int cnt = full ? g.m : 2 * ntx + 1;
-  for (int j = threadIdx.x; j < cnt; j += kCcThreads) {
+  if (full) step = kCcThreads * nseg;  // segment seg: j = seg*kCcThreads + tid (+ k*step)
+  for (int j = seg * kCcThreads + threadIdx.x; j < cnt; j += step) {
     int c;
     if (full) c = j;
     else if (j == 2 * ntx) c = g.m - 1;
@@ -451,7 +757,7 @@ __global__ __launch_bounds__(kCcThreads) void k_cc_merge(Geom g, int kind, const
     if (s > g.t - 1) continue;
     if (kind != PERC_BOND && !socc[s]) continue;
     int nn[6];
-    nearestn(g, s, nn);
+    nearestn_rc(g, s, row, c, nn);
     const int fb = bond_first[s];
     int r = 0;
     for (int k = 0; k < g.scn; ++k) {
@@ -460,18 +766,12 @@ __global__ __launch_bounds__(kCcThreads) void k_cc_merge(Geom g, int kind, const
       const bool link = cc_link(kind, bocc, socc, fb + r, s, q);
       ++r;
       if (!link) continue;
-      const int qrow = (q - 1) / g.m, qcol = (q - 1) % g.m;
+      const int qrow = div_m(g, q - 1), qcol = q - 1 - qrow * g.m;
       if (qrow / kCcH == row / kCcH && qcol / kCcW == c / kCcW) continue;  // inside: k_cc_tile
       if (kind == PERC_BOND) member[q] = 1;
       unite(parent, s, q);
     }
   }
-}
-
-__device__ __forceinline__ int wave_sum_int(int v) {
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
-  return v;
 }
 
 // sum of v over the workgroup of kCcThreads, then one atomic add
@@ -495,15 +795,29 @@ __device__ __forceinline__ void block_count_add(int v, int* counter) {
 __global__ __launch_bounds__(kCcThreads) void k_cc_compress(int t, int* parent,
                                                             const uint8_t* member,
                                                             int* nclusters) {
+  // four sites per thread and step, their first parent loads issued together
+  constexpr int kU = 4;
   int cnt = 0;
-  for (int s = blockIdx.x * kCcThreads + threadIdx.x + 1; s <= t; s += gridDim.x * kCcThreads) {
-    int x = s, p = parent[x];
-    while (p != x) {
-      x = p;
-      p = parent[x];
+  for (long long b = (long long)blockIdx.x * kCcThreads * kU + threadIdx.x + 1; b <= t;
+       b += (long long)gridDim.x * kCcThreads * kU) {
+    int p0[kU];
+#pragma unroll
+    for (int k = 0; k < kU; ++k) {
+      const long long s = b + k * kCcThreads;
+      p0[k] = s <= t ? parent[s] : 0;
     }
-    parent[s] = x;
-    cnt += x == s && member[s];
+#pragma unroll
+    for (int k = 0; k < kU; ++k) {
+      const long long s = b + k * kCcThreads;
+      if (s > t) continue;
+      int x = (int)s, p = p0[k];
+      while (p != x) {
+        x = p;
+        p = parent[x];
+      }
+      parent[s] = x;
+      cnt += x == s && member[s];
+    }
   }
   block_count_add(cnt, nclusters);
 }
@@ -560,9 +874,21 @@ __global__ __launch_bounds__(1024) void k_span_top(Geom g, const int* parent,
 __global__ __launch_bounds__(kCcThreads) void k_count_root(int t, const int* parent,
                                                            const uint8_t* member, int root,
                                                            int* counter) {
+  constexpr int kU = 4;  // loads in flight per thread
   int cnt = 0;
-  for (int s = blockIdx.x * kCcThreads + threadIdx.x + 1; s <= t; s += gridDim.x * kCcThreads)
-    cnt += member[s] && parent[s] == root;
+  for (long long b = (long long)blockIdx.x * kCcThreads * kU + threadIdx.x + 1; b <= t;
+       b += (long long)gridDim.x * kCcThreads * kU) {
+    int pv[kU];
+    uint8_t mv[kU];
+#pragma unroll
+    for (int k = 0; k < kU; ++k) {
+      const long long s = b + k * kCcThreads;
+      pv[k] = s <= t ? parent[s] : 0;
+      mv[k] = s <= t ? member[s] : 0;
+    }
+#pragma unroll
+    for (int k = 0; k < kU; ++k) cnt += mv[k] && pv[k] == root;
+  }
   block_count_add(cnt, counter);
 }
 
@@ -699,24 +1025,102 @@ __device__ __forceinline__ double bond_value(int rule, int id, int s, int c, int
 // only code and rhs, so dev_assemble writes the CSR copy only when a
 // consumer asks for it (ensure_csr): 2 + 8 B per row instead of 50.
 template <bool CSR>
-__global__ void k_assemble(Geom g, int N, const int* bond_first, const uint8_t* bocc,
-                           const uint8_t* socc, const int* parent, const int* rowptr,
-                           double* val, double* diag, double* rhs, uint16_t* code, int* sflag,
-                           StencilForms F, int rule, double g0, double leak, double Va,
-                           int span_root, const double* w) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i == 0 && w) atomicOr(sflag, 1);  // per-bond values: no two-value stencil code
-  if (i >= N) return;
+__device__ __forceinline__ void assemble_row(
+    const Geom& g, int i, const int* bond_first, const uint8_t* bocc, const uint8_t* socc,
+    const int* parent, const int* rowptr, double* val, double* diag, double* rhs, uint16_t* code,
+    int* sflag, const StencilForms& F, int fast_form, int bf_closed, int rule, double g0,
+    double leak, double Va, int span_root, const double* w) {
   const int m = g.m, t = g.t, s = i + m + 1;
   const int ps = parent[s];
-  int nbr[6];
-  const int cnt = sorted_neighbours(g, s, nbr);
+  const int sr = div_m(g, s - 1), sc = s - 1 - sr * m;
+  if (fast_form >= 0 && sc >= 1 && sc <= m - 2) {
+    // square lattice, interior column (fast_form: the host found the form
+    // {-m, -1, +1, +m} with deltas {(-1,0), (0,-1), (0,1), (1,0)}): the
+    // sorted neighbours are s-m, s-1, s+1, s+m and the bond ids close-form --
+    // s's forward bonds are (s, s+1), (s, s+m) in nearestn order, and s is
+    // the second forward neighbour of s-m, the first of s-1, whatever their
+    // edge or pbc case (nearestn_square: every case lists +1 before +m).
+    // The same values in the same order as the general path below.
+    // Every load is issued before any is used (bond_value's short-circuit
+    // loads would serialise four memory latencies per row).
+    int fb, bl, bd;  // bond_first of s, s-1, s-m
+    if (bf_closed) {
+      fb = bf_square(g, sr, sc);
+      bl = bf_square(g, sr, sc - 1);
+      bd = bf_square(g, sr - 1, sc);
+    } else {
+      fb = bond_first[s];
+      bl = bond_first[s - 1];
+      bd = bond_first[s - m];
+    }
+    const int ids[4] = {bd + 1, bl, fb, fb + 1};
+    const int cs[4] = {s - m, s - 1, s + 1, s + m};
+    unsigned bo[4], so[4] = {1u, 1u, 1u, 1u}, ss = 1u;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) bo[j] = rule == PERC_RULE_SITE ? 1u : bocc[ids[j]];
+    if (rule != PERC_RULE_BOND) {
+      ss = socc[s];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) so[j] = socc[cs[j]];
+    }
+    const bool root = ps == span_root;
+    double gvs[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {  // bond_value
+      const bool in = root && bo[j] != 0u && ss != 0u && so[j] != 0u;
+      gvs[j] = in ? (w ? -g0 * w[ids[j]] : -g0) : -leak;
+    }
+    double rowsum = 0.0;
+    unsigned bits = 0;
+    int k = CSR ? rowptr[i] : 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const double gv = gvs[j];
+      if (gv == -g0) bits |= 1u << j;
+      rowsum = rowsum + gv;
+      if (CSR && cs[j] > m && cs[j] <= t - m) val[k++] = gv;
+    }
+    code[i] = (uint16_t)(bits | 4u << 8 | (unsigned)fast_form << 11);
+    if (CSR) diag[i] = -rowsum;
+    double acc = 0.0;
+    if (s > t - 2 * m) acc = acc - (gvs[3] * Va);  // (s, s+m): bond fb + 1
+    rhs[i] = acc;
+    return;
+  }
+  // one division per neighbour (div_m); nearestn of the row once and of
+  // each smaller neighbour once -- the bond ids of bond_id
+  int nn[6];
+  nearestn_rc(g, s, sr, sc, nn);
+  const int fb = bond_first[s];
+  int nbr[6], cnt = 0;  // sorted_neighbours
+  for (int k = 0; k < g.scn; ++k)
+    if (nn[k] != 0) {
+      const int v = nn[k];
+      int j = cnt;
+      while (j > 0 && nbr[j - 1] > v) { nbr[j] = nbr[j - 1]; --j; }
+      nbr[j] = v;
+      ++cnt;
+    }
   double rowsum = 0.0;  // bondc.f:500-504: ascending-column dense row sum
   int k = CSR ? rowptr[i] : 0;
   unsigned bits = 0;
+  int drs[6], dcs[6];
   for (int j = 0; j < cnt; ++j) {
     const int c = nbr[j];
-    const int id = s < c ? bond_id(g, bond_first, s, c) : bond_id(g, bond_first, c, s);
+    const int cr = div_m(g, c - 1), cc = c - 1 - cr * m;
+    int d = cc - sc;  // lattice_delta
+    if (d > 1) d -= m;
+    else if (d < -1) d += m;
+    drs[j] = cr - sr;
+    dcs[j] = d;
+    int id;
+    if (s < c) {
+      id = fwd_bond_id(g, nn, fb, s, c);
+    } else {
+      int nc[6];
+      nearestn_rc(g, c, cr, cc, nc);
+      id = fwd_bond_id(g, nc, bond_first[c], c, s);
+    }
     if (id < 0) {  // no bond in this slot: the stencil operator cannot be used
       atomicOr(sflag, 1);
       continue;
@@ -737,8 +1141,7 @@ __global__ void k_assemble(Geom g, int N, const int* bond_first, const uint8_t* 
     form = 0;
   }
   for (int j = 0; j < cnt; ++j) {  // the tiled kernel reads slot j at (row, col) + (dr, dc)
-    int dr, dc;
-    lattice_delta(g, s, nbr[j], &dr, &dc);
+    const int dr = drs[j], dc = dcs[j];
     if (dr != F.dr[form][j] || dc != F.dc[form][j] || dr < -1 || dr > 1 || dc < -1 || dc > 1)
       atomicOr(sflag, 4);
   }
@@ -747,9 +1150,6 @@ __global__ void k_assemble(Geom g, int N, const int* bond_first, const uint8_t* 
   // RHS in bond-list order (bondc.f:490-497)
   double acc = 0.0;
   if (s > t - 2 * m && s <= t - m) {
-    int nn[6];
-    nearestn(g, s, nn);
-    const int fb = bond_first[s];
     int r = 0;
     for (int kk = 0; kk < g.scn; ++kk) {
       const int q = nn[kk];
@@ -763,6 +1163,22 @@ __global__ void k_assemble(Geom g, int N, const int* bond_first, const uint8_t* 
     }
   }
   rhs[i] = acc;
+}
+
+// grid-stride over the rows: a fixed grid (kAsmGrid workgroups) amortises
+// each wave's start-up (kernel-argument loads, ~1 us) over many rows
+constexpr int kAsmGrid = 2048;
+template <bool CSR>
+__global__ __launch_bounds__(kBlock) void k_assemble(
+    Geom g, int N, const int* bond_first, const uint8_t* bocc, const uint8_t* socc,
+    const int* parent, const int* rowptr, double* val, double* diag, double* rhs, uint16_t* code,
+    int* sflag, StencilForms F, int fast_form, int bf_closed, int rule, double g0, double leak,
+    double Va, int span_root, const double* w) {
+  const int i0 = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i0 == 0 && w) atomicOr(sflag, 1);  // per-bond values: no two-value stencil code
+  for (int i = i0; i < N; i += gridDim.x * blockDim.x)
+    assemble_row<CSR>(g, i, bond_first, bocc, socc, parent, rowptr, val, diag, rhs, code, sflag, F,
+                      fast_form, bf_closed, rule, g0, leak, Va, span_root, w);
 }
 
 // Terminal currents of the 2m boundary rows (bondc.f:554-592; ConductCalc.m:188)
@@ -3863,6 +4279,13 @@ hipError_t dev_build_lattice(perc_ctx* h) {
   h->h_bond_first.resize(t + 2);
   HIP_TRY(hipMemcpy(h->h_bond_first.data(), d.bond_first, sizeof(int) * (t + 2),
                     hipMemcpyDeviceToHost));
+  h->bf_closed = g.lattice == kSquare && g.n >= 2;
+  for (int r = 0; r + 2 <= g.n && h->bf_closed; ++r)
+    for (int c = 0; c < g.m; ++c)
+      if (h->h_bond_first[(size_t)r * g.m + c + 1] != bf_square(g, r, c)) {
+        h->bf_closed = false;
+        break;
+      }
   // CSR pattern of the interior block
   int* rc = nullptr;
   HIP_TRY(dmalloc(&rc, N + 1));
@@ -3976,7 +4399,7 @@ void dev_free_all(perc_ctx* h) {
                   d.order, d.parent, d.member, d.top, d.counters, d.x, d.r,
                   d.p0, d.p1, d.q, d.partials, d.tickets, d.scal, d.err_hist, d.iout,
                   d.res_xch, d.res_part, d.res_bar, d.bw, d.code_sm, d.csize, d.res_gran,
-                  d.sel_hist, d.mgran};
+                  d.sel_hist, d.sel_cand, d.mgran};
   for (void* p : ptrs)
     if (p) hipFree(p);
   d = DeviceBuffers{};
@@ -4011,40 +4434,43 @@ hipError_t dev_occupy(perc_ctx* h, int kind, int nsites, const int* site_order, 
   return hipSuccess;
 }
 
-// the count smallest keys of ids 1..n occupied (radix select, 8 passes of
-// one key byte; the histogram goes to the host each pass: 256 counters)
+// the count smallest keys of ids 1..n occupied: window count + one-workgroup
+// select (k_select_window / k_select_final), then the occupation pass; no
+// host synchronisation
 static hipError_t occupy_rand_one(perc_ctx* h, long long n, long long count,
                                   unsigned long long seed, int base, uint8_t* occ) {
   hipStream_t st = h->stream;
   if (count <= 0) return hipSuccess;  // occ is zeroed by the caller
-  const int G = (int)std::min<long long>(cdiv(n, kBlock), 2048);
-  unsigned long long T = ~0ull;
+  const unsigned long long* Tp = nullptr;
   if (count < n) {
-    if (!h->d.sel_hist) HIP_TRY(dmalloc(&h->d.sel_hist, 256));
-    unsigned* d_hist = h->d.sel_hist;
-    unsigned hist[256];
-    unsigned long long prefix = 0, mask = 0;
-    long long need = count;
-    for (int pass = 0; pass < 8; ++pass) {
-      const int shift = 56 - 8 * pass;
-      HIP_TRY(hipMemsetAsync(d_hist, 0, sizeof(hist), st));
-      k_select_hist<<<G, kBlock, 0, st>>>(n, seed, prefix, mask, shift, d_hist);
-      HIP_TRY(dbg_sync(st, "k_select_hist"));
-      HIP_TRY(hipMemcpyAsync(hist, d_hist, sizeof(hist), hipMemcpyDeviceToHost, st));
+    if (!h->d.sel_hist) HIP_TRY(dmalloc(&h->d.sel_hist, 2));
+    if (!h->d.sel_cand) HIP_TRY(dmalloc(&h->d.sel_cand, (size_t)kSelCap + 1 + 16));
+    // window: T's hash is count/n * 2^32 give or take the binomial spread
+    // sqrt(n q (1-q)) keys; +-(8 sigma + 256) keys of hash width
+    const double q = (double)count / (double)n;
+    const double wkeys = 8.0 * std::sqrt((double)n * q * (1.0 - q)) + 256.0;
+    const double two32 = 4294967296.0, c = q * two32, w = wkeys / (double)n * two32;
+    unsigned long long lo = c - w <= 0.0 ? 0ull : (unsigned long long)(c - w);
+    unsigned long long hi = c + w >= two32 ? (1ull << 32) : (unsigned long long)(c + w) + 1;
+    const char* full = std::getenv("PERC_SELECT_FULL");  // tests: the exact slow path
+    if (full && full[0] == '1') lo = hi = 0;
+    HIP_TRY(hipMemsetAsync(h->d.sel_hist, 0, 2 * sizeof(unsigned), st));
+    const int G = (int)std::min<long long>(cdiv(n, kBlock), 2048);
+    k_select_window<<<G, kBlock, 0, st>>>(n, seed, lo, hi, h->d.sel_hist, h->d.sel_cand);
+    HIP_TRY(dbg_sync(st, "k_select_window"));
+    k_select_final<<<1, kSelThreads, 0, st>>>(n, seed, count, lo, hi, h->d.sel_hist,
+                                              h->d.sel_cand);
+    HIP_TRY(dbg_sync(st, "k_select_final"));
+    Tp = h->d.sel_cand;
+    if (std::getenv("PERC_SELECT_TRACE")) {
+      unsigned long long tr[6];
+      HIP_TRY(hipMemcpyAsync(tr, h->d.sel_cand + 1 + kSelCap, sizeof(tr), hipMemcpyDeviceToHost, st));
       HIP_TRY(hipStreamSynchronize(st));
-      long long cum = 0;
-      int b = 0;
-      for (; b < 255; ++b) {
-        if (cum + hist[b] >= need) break;
-        cum += hist[b];
-      }
-      need -= cum;
-      prefix |= (unsigned long long)b << shift;
-      mask |= 0xFFull << shift;
+      std::fprintf(stderr, "select trace: hist %llu bin %llu rank %llu ticks; nin %llu bin %llu\n",
+                   tr[1] - tr[0], tr[2] - tr[1], tr[3] - tr[2], tr[4], tr[5]);
     }
-    T = prefix;
   }
-  k_occupy_rand<<<cdiv(n, kBlock), kBlock, 0, st>>>(n, seed, T, base, occ);
+  k_occupy_rand<<<cdiv(n, kBlock), kBlock, 0, st>>>(n, seed, Tp, base, occ);
   return hipGetLastError();
 }
 
@@ -4067,11 +4493,31 @@ hipError_t dev_label(perc_ctx* h, int* nspan, int* span_list, int* nclusters) {
   const int kind = h->last.kind;
   HIP_TRY(hipMemsetAsync(d.counters, 0, sizeof(int) * (8 + kMaxSpanList), st));
   const int tiles = cdiv(g.m, kCcW) * cdiv(g.n, kCcH);
+  unsigned long long* ttr = nullptr;  // PERC_TILE_TRACE: per-workgroup phase stamps
+  static const bool ttrace = std::getenv("PERC_TILE_TRACE") != nullptr;
+  if (ttrace) HIP_TRY(dmalloc(&ttr, (size_t)tiles * 5));
   k_cc_tile<<<tiles, kCcThreads, 0, st>>>(g, kind, d.bond_first, d.bocc, d.socc, d.parent,
-                                          d.member);
+                                          d.member, (int)h->bf_closed, ttr);
+  if (ttrace) {
+    std::vector<unsigned long long> v((size_t)tiles * 5);
+    HIP_TRY(hipMemcpyAsync(v.data(), ttr, v.size() * 8, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    HIP_TRY(hipFree(ttr));
+    unsigned long long lo = ~0ull, hi = 0;
+    double ph[4] = {0, 0, 0, 0};
+    for (int b = 0; b < tiles; ++b) {
+      lo = std::min(lo, v[5 * b]);
+      hi = std::max(hi, v[5 * b + 4]);
+      for (int j = 0; j < 4; ++j) ph[j] += (double)(v[5 * b + j + 1] - v[5 * b + j]);
+    }
+    std::fprintf(stderr, "tile trace: span %llu ticks; per-WG avg phase1 %.1f runs %.1f unions %.1f flatten %.1f\n",
+                 hi - lo, ph[0] / tiles, ph[1] / tiles, ph[2] / tiles, ph[3] / tiles);
+  }
   HIP_TRY(dbg_sync(st, "k_cc_tile"));
-  k_cc_merge<<<g.n, kCcThreads, 0, st>>>(g, kind, d.bond_first, d.bocc, d.socc, d.parent,
-                                         d.member);
+  const int nseg = cdiv(g.m, kCcThreads);
+  const int nfull = g.n / kCcH;  // rows kCcH-1, 2kCcH-1, ... (< n)
+  k_cc_merge<<<g.n + (nseg > 1 ? nfull * (nseg - 1) : 0), kCcThreads, 0, st>>>(
+      g, kind, d.bond_first, d.bocc, d.socc, d.parent, d.member);
   HIP_TRY(dbg_sync(st, "k_cc_merge"));
   k_cc_compress<<<std::min(cdiv(g.t, kCcThreads), kReduceGrid), kCcThreads, 0, st>>>(
       g.t, d.parent, d.member, d.counters + 1);
@@ -4364,16 +4810,32 @@ static hipError_t launch_assemble(perc_ctx* h, bool csr) {
   hipStream_t st = h->stream;
   HIP_TRY(hipMemsetAsync(d.sflag, 0, 4 * sizeof(int), st));
   const double* w = h->has_weights ? d.bw : nullptr;
+  // the square lattice's interior-column form (k_assemble's closed-form path)
+  int fast = -1;
+  const StencilForms& F = h->forms;
+  const int m = h->g.m;
+  const char* gen = std::getenv("PERC_ASM_GENERIC");  // tests: the general path only
+  const bool closed = !(gen && gen[0] == '1');
+  for (int f = 0; f < F.nforms && closed && h->g.lattice == kSquare && m >= 3; ++f) {
+    const int off[4] = {-m, -1, 1, m}, dr[4] = {-1, 0, 0, 1}, dc[4] = {0, -1, 1, 0};
+    bool same = F.cnt[f] == 4;
+    for (int j = 0; j < 4 && same; ++j)
+      same = F.off[f][j] == off[j] && F.dr[f][j] == dr[j] && F.dc[f][j] == dc[j];
+    if (same) {
+      fast = f;
+      break;
+    }
+  }
   if (csr)
-    k_assemble<true><<<blocks_for(h->N), kBlock, 0, st>>>(h->g, h->N, d.bond_first, d.bocc, d.socc,
+    k_assemble<true><<<std::min<int>(cdiv(h->N, kBlock), kAsmGrid), kBlock, 0, st>>>(h->g, h->N, d.bond_first, d.bocc, d.socc,
                                                           d.parent, d.rowptr, d.val, d.diag, d.rhs,
-                                                          d.code, d.sflag, h->forms, p.rule, p.g0,
-                                                          p.leak, p.Va, p.span_root, w);
+                                                          d.code, d.sflag, h->forms, fast, (int)h->bf_closed, p.rule,
+                                                          p.g0, p.leak, p.Va, p.span_root, w);
   else
-    k_assemble<false><<<blocks_for(h->N), kBlock, 0, st>>>(h->g, h->N, d.bond_first, d.bocc, d.socc,
+    k_assemble<false><<<std::min<int>(cdiv(h->N, kBlock), kAsmGrid), kBlock, 0, st>>>(h->g, h->N, d.bond_first, d.bocc, d.socc,
                                                            d.parent, d.rowptr, d.val, d.diag, d.rhs,
-                                                           d.code, d.sflag, h->forms, p.rule, p.g0,
-                                                           p.leak, p.Va, p.span_root, w);
+                                                           d.code, d.sflag, h->forms, fast, (int)h->bf_closed, p.rule,
+                                                           p.g0, p.leak, p.Va, p.span_root, w);
   HIP_TRY(dbg_sync(st, "k_assemble"));
   h->csr_ok = csr;
   return hipSuccess;

@@ -96,7 +96,8 @@ struct DeviceBuffers {
   uint8_t* top = nullptr;    // t+1 (spanning-root flags, m+1 used)
   int* counters = nullptr;   // [0]=nspan [1]=nclusters [2]=span_sites [3]=max size, then list
   int* csize = nullptr;      // t+2 per-root cluster sizes (perc_cluster_sizes)
-  unsigned* sel_hist = nullptr;  // 256-bin histogram of perc_occupy_random's select
+  unsigned* sel_hist = nullptr;  // perc_occupy_random's select: [0] keys below, [1] in window
+  unsigned long long* sel_cand = nullptr;  // [0] the threshold key, then the window's keys
   // CG
   double* x = nullptr;
   double* r = nullptr;
@@ -161,6 +162,7 @@ struct perc_ctx {
   bool occupied = false;
   bool labeled = false;
   bool assembled = false;
+  bool bf_closed = false;  // h_bond_first == bf_square on rows 0..n-2 (square lattice)
   bool csr_ok = true;    // the CSR values / diagonal of the assembled system are written
   perc::AsmParams asm_p; // the assembly's parameters (ensure_csr re-runs it)
   int span_root = 0;

@@ -861,3 +861,30 @@ def test_small_solver_matches_launched(lat, m, n, pbc, p):
         assert abs(s["iter"] - c["iter"]) <= 1
         assert rel(s["gtop"], c["gtop"]) < REL and rel(s["gbot"], c["gbot"]) < REL
         assert np.max(np.abs(s["vint"] - c["vint"])) < 1e-8
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind,rule,m,n,pbc", [(PL.BOND, PL.RULE_BOND, 256, 150, 0),
+                                               (PL.BOND, PL.RULE_BOND, 131, 90, 1),
+                                               (PL.SITEBOND, PL.RULE_MIXED, 200, 64, 0)])
+def test_closed_form_assembly_is_the_general_one(kind, rule, m, n, pbc, monkeypatch):
+    """k_assemble's closed-form path for the square lattice's interior
+    columns writes what its general path (PERC_ASM_GENERIC=1: nearestn +
+    bond_id per neighbour) writes: the same CSR system bitwise and the same
+    solve."""
+    nb, t = api.nbonds(0, m, n, pbc), m * n
+    out = []
+    for generic in ("0", "1"):
+        monkeypatch.setenv("PERC_ASM_GENERIC", generic)
+        with api.Context(0, m, n, pbc) as ctx:
+            ctx.occupy_random(kind, int(0.9 * t) if kind != PL.BOND else 0, int(0.62 * nb), 4242)
+            assert ctx.label()["nspan"] >= 1
+            c = ctx.conductance(rule=rule, itmax=25)
+            sysm = ctx.system()
+        out.append((c, sysm))
+    (c0, s0), (c1, s1) = out
+    for key in ("rowptr", "col"):
+        assert np.array_equal(s0[key], s1[key])
+    for key in ("val", "diag", "rhs"):
+        assert np.array_equal(s0[key].view(np.uint64), s1[key].view(np.uint64)), key
+    assert (c0["gtop"], c0["gbot"], c0["iter"]) == (c1["gtop"], c1["gbot"], c1["iter"])

@@ -274,3 +274,17 @@ def test_random_order_is_a_keyed_permutation():
     assert not np.array_equal(api.random_order(n, 100, 7, PL.SITE), full[:100])
     means = [api.random_order(n, 1000, s_).mean() for s_ in range(20)]
     assert abs(np.mean(means) - (n + 1) / 2) < 0.05 * n
+
+
+@pytest.mark.parametrize("m,n,pbc", [(5, 4, 0), (5, 4, 1), (64, 33, 0), (17, 40, 1), (2, 3, 1)])
+def test_square_bond_first_closed_form(m, n, pbc):
+    """lattice.h bf_square: bond_first of the square lattice's rows 0..n-2 is
+    r*(2m-1+pbc) + 2c + pbc*(c>0) -- the form k_assemble / k_cc_tile use when
+    the context's built bond_first agrees (perc_ctx::bf_closed)."""
+    b1, b2 = api.bond_list(0, m, n, pbc)
+    lo = np.minimum(b1, b2)
+    counts = np.bincount(lo, minlength=m * n + 2)
+    first = np.concatenate([[0], np.cumsum(counts)])  # first[s] = bonds with smaller end < s
+    for r in range(n - 1):
+        for c in range(m):
+            assert first[r * m + c + 1] == r * (2 * m - 1 + pbc) + 2 * c + (pbc if c > 0 else 0)

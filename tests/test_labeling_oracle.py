@@ -240,3 +240,28 @@ def test_occupy_random_equals_its_host_order(lat, m, n, pbc, kind):
         check(lr, *oracle_bond(lat, m, n, pbc, bo, tb))
     elif kind == PL.SITE:
         check(lr, *oracle_site(lat, m, n, pbc, so, ts))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("frac", [0.0, 1e-6, 0.003, 0.5, 0.997, 1.0])
+@pytest.mark.parametrize("full", [False, True])
+def test_occupy_random_select_extremes(frac, full, monkeypatch):
+    """The on-device select (k_select_window + k_select_final) at the count
+    extremes -- 1 element, a handful, almost all, n-1, n -- and with
+    PERC_SELECT_FULL=1 (empty window: the exact all-keys path) occupies
+    exactly the prefix of perc_random_order."""
+    if full:
+        monkeypatch.setenv("PERC_SELECT_FULL", "1")
+    lat, m, n, pbc = 0, 300, 211, 0
+    nb = api.nbonds(lat, m, n, pbc)
+    for tb in sorted({max(1, int(frac * nb)), min(nb, max(1, int(frac * nb)) + 1), nb - 1}
+                     if 0.0 < frac < 1.0 else ({1} if frac == 0.0 else {nb - 1, nb})):
+        seed = 99 + tb
+        bo = api.random_order(nb, tb, seed, PL.BOND)
+        with api.Context(lat, m, n, pbc) as ctx:
+            ctx.occupy_random(PL.BOND, 0, tb, seed)
+            lr = ctx.label(canon=True)
+            ctx.occupy(PL.BOND, bond_order=bo, nbonds_=tb)
+            le = ctx.label(canon=True)
+        assert np.array_equal(lr["canon"], le["canon"]), tb
+        assert lr["nspan"] == le["nspan"] and lr["nclusters"] == le["nclusters"], tb
