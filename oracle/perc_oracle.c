@@ -1101,9 +1101,23 @@ static int sym_entry(const double *sa, const int *ija, int row, int col,
    products summed in descending j instead -- one other association, to
    measure how far the converged Gtop / Gbot of the reference solver itself
    move when only the order of its sums changes. */
+/* dot_order 2: pairwise (tree) summation, halving down to runs of 8 summed
+   serially -- the association family of a GPU reduction (wave and
+   workgroup trees), with far smaller rounding growth than a serial sum */
+static double dot_tree(int n, const double *u, const double *v) {
+  double s = 0.0;
+  int i, h;
+  if (n <= 8) {
+    for (i = 0; i < n; i++) s = s + u[i] * v[i];
+    return s;
+  }
+  h = n / 2;
+  return dot_tree(h, u, v) + dot_tree(n - h, u + h, v + h);
+}
 static double dot_ord(int n, const double *u, const double *v, int desc) {
   double s = 0.0;
   int i;
+  if (desc == 2) return dot_tree(n, u, v);
   if (desc)
     for (i = n - 1; i >= 0; i--) s = s + u[i] * v[i];
   else

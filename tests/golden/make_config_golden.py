@@ -29,6 +29,7 @@ Gtop / Gbot over the last decades shows where the oracle has converged.
 Usage: python tests/golden/make_config_golden.py [case ...]   (CPU, minutes to hours)
        GOLDEN_THREADS=k python tests/golden/make_config_golden.py --decades [case ...]
        GOLDEN_THREADS=k python tests/golden/make_config_golden.py --assoc [case ...]
+       GOLDEN_THREADS=k python tests/golden/make_config_golden.py --assoc-tree [case ...]
 """
 import hashlib
 import json
@@ -249,12 +250,14 @@ def decades(case):
         json.dump(doc, f, indent=1)
 
 
-def assoc(case):
+def assoc(case, order=1):
     """--assoc: the same solver with its dot products summed in descending
     order (or_linbcg_sym dot_order 1), to the fixture's decades: how far the
     reference solver's own converged Gtop / Gbot move when only the order of
     its sums changes (the floor under any re-associated solve, the GPU's
-    included).  Stored as doc["assoc_desc"][tol]."""
+    included).  Stored as doc["assoc_desc"][tol]; --assoc-tree: pairwise
+    (tree) sums, dot_order 2, the association family of a GPU reduction,
+    stored as doc["assoc_tree"][tol]."""
     rc = CASES[case]
     O = _oracle()
     ii, seed, (info, sysin) = find_seed(rc)
@@ -267,14 +270,17 @@ def assoc(case):
     res, _ = O.conductance_decades(rc["lattice"], L, L, 0, sysin["b1"], sysin["b2"], sysin["gval"],
                                    tols, rhs_rule=sysin["rhs_rule"], cur_rule=sysin["cur_rule"],
                                    cur_thresh=sysin["cur_thresh"],
-                                   threads=int(os.environ.get("GOLDEN_THREADS", 2)), dot_order=1)
-    doc["assoc_desc"] = {"%g" % r["tol"]: dict(gtop=r["gtop"], gbot=r["gbot"], iter=r["iter"],
-                                              err=r["err"]) for r in res}
-    doc["assoc_desc_seconds"] = time.time() - t0
+                                   threads=int(os.environ.get("GOLDEN_THREADS", 2)),
+                                   dot_order=order)
+    key = "assoc_desc" if order == 1 else "assoc_tree"
+    doc = json.load(open(path))  # re-read: another --assoc run may have written meanwhile
+    doc[key] = {"%g" % r["tol"]: dict(gtop=r["gtop"], gbot=r["gbot"], iter=r["iter"],
+                                     err=r["err"]) for r in res}
+    doc[key + "_seconds"] = time.time() - t0
     for r in res:
         ref = doc["solves"]["%g" % r["tol"]]
-        print("%s desc tol %g: iter %d (asc %d) Gtop %.3e Gbot %.3e rel to asc" % (
-            case, r["tol"], r["iter"], ref["iter"], abs(r["gtop"] - ref["gtop"]) / ref["gtop"],
+        print("%s %s tol %g: iter %d (asc %d) Gtop %.3e Gbot %.3e rel to asc" % (
+            case, key, r["tol"], r["iter"], ref["iter"], abs(r["gtop"] - ref["gtop"]) / ref["gtop"],
             abs(r["gbot"] - ref["gbot"]) / ref["gbot"]), flush=True)
     with open(path, "w") as f:
         json.dump(doc, f, indent=1)
@@ -309,8 +315,8 @@ if __name__ == "__main__":
     if args and args[0] == "--decades":
         for c in args[1:] or list(CASES):
             decades(c)
-    elif args and args[0] == "--assoc":
+    elif args and args[0] in ("--assoc", "--assoc-tree"):
         for c in args[1:] or list(CASES):
-            assoc(c)
+            assoc(c, 1 if args[0] == "--assoc" else 2)
     else:
         main(args or list(CASES))
