@@ -191,7 +191,8 @@ def kernel_label(key, minfo):
             "" if minfo["qfree"] else ", q stored")
     if key == "res":
         return ("k_cg_res (resident persistent solve, %d-row bands: p in LDS, r/q in registers, "
-                "2 grid-wide reductions per iteration; HBM bytes = exchanged band-edge rows + x)"
+                "2 grid-wide reductions per iteration; bytes = the streaming-equivalent 52 B/row "
+                "+ x, not HBM traffic)"
                 % minfo["band_rows"])
     if key == "resid" and minfo.get("qfree"):
         return ("k_cg_rm" if minfo["kernel"] == "rows" else "k_cg_march") + \
@@ -633,11 +634,13 @@ def main():
         operator format f"""
         full = args.full_voltages
         if f in ("stencil", "stencil_tiled") and minfo.get("kernel") == "resident" and not probe:
-            # whole iterations in one persistent launch; per iteration it
-            # moves only the exchanged band-edge rows (r, p: 4 rows of m per
-            # band, written and read) and the electrode-adjacent x rows
-            G = -(-(L_ - 2) // max(minfo["band_rows"], 1))
-            return [("res", "spmv", 5, G * 4 * L_ * 8 * 2 + x_bytes(N, L_, full))]
+            # whole iterations in one persistent launch, r / q / codes held
+            # on chip: the bytes are the streaming-equivalent 52 B/row (what
+            # the launched march P + B move per iteration, 26N each) plus the
+            # electrode-adjacent x rows -- "how fast against the streaming
+            # solver's traffic"; the floor under it is the measured grid
+            # synchronisation (roofline.sync_floor_ms, perc_bench_kernel 6)
+            return [("res", "spmv", 5, 52 * N + x_bytes(N, L_, full))]
         if f in ("stencil", "stencil_tiled"):
             qf = f == "stencil" and minfo["qfree"]
             if f == "stencil" and not qf and minfo.get("kernel") in ("wave", "rows"):
@@ -687,6 +690,11 @@ def main():
             ms = ctx.bench_kernel(which, 50)
             row[key] = {"ms": round(ms, 5), "gbs": round(nbytes / (ms * 1e-3) / 1e9, 1)}
         probe[fname] = row
+    sync_floor = None
+    if minfo.get("kernel") == "resident" and assembled:
+        # two block sums + two tagged-granule all-gathers per iteration on
+        # the resident grid, nothing else (k_res_sync_probe)
+        sync_floor = round(ctx.bench_kernel(6, 20), 5)
     copy_ms = ctx.bench_kernel(4, 20)
     copy_bytes = 2 * 8 * (64 << 20)  # 512 MB read + 512 MB written (perc_bench_kernel 4)
     stream_copy = {"ms": round(copy_ms, 5), "bytes": copy_bytes,
@@ -734,7 +742,13 @@ def main():
                      "avg_launch_ms": kern[dom]["avg_launch_ms"],
                      "launches": kern[dom]["launches"],
                      **({"note": "%d realisations in flight per GPU: kernel durations overlap"
-                                 % K} if K > 1 else {})},
+                                 % K} if K > 1 else {}),
+                     **({"bytes_model": "streaming-equivalent 52 B/row/iteration (resident "
+                                        "solve: r, q, codes on chip)",
+                         "sync_floor_ms": sync_floor,
+                         "sync_floor_frac": round(sync_floor / kern[dom]["avg_launch_ms"], 3)
+                         if kern[dom]["avg_launch_ms"] else None}
+                        if sync_floor is not None else {})},
         "realisations_per_s": round(value, 5),
         "cg_solves_per_s": round(nspan / tmax, 5),
         "cg_solves": nspan,

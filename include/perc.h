@@ -215,8 +215,11 @@ int perc_spmv_host(perc_ctx *h, const double *x, double *y);
    stream).  which: 0 = SpMV (dsprsax), 1 = CG SpMV + q.p dot, 2 = CG
    residual update (B), 3 = CG x/p update (P), 4 = STREAM copy 512 MB ->
    512 MB (16-B accesses, past the 256 MB Infinity Cache; the achievable-HBM
-   reference), 5 = one whole CG iteration (every kernel of it, in order).
-   Clobbers solver vectors. */
+   reference), 5 = one whole CG iteration (every kernel of it, in order),
+   6 = the resident solve's synchronisation floor: per iteration, the two
+   block sums + grid all-gathers of k_cg_res on dummy values, nothing else
+   (only on a context whose system takes the resident solver; else
+   PERC_EHIP).  Clobbers solver vectors. */
 int perc_bench_kernel(perc_ctx *h, int which, int reps, double *ms);
 /* Self-test of the solver's table division (z = r/d from y = RN(1/d) and
    one Markstein correction, bitwise IEEE division when it holds) on the

@@ -572,10 +572,14 @@ __global__ __launch_bounds__(kCcThreads) void k_cc_tile(Geom g, int kind, const 
   static_assert(kCcW % 64 == 0 && kCcThreads % kCcW == 0, "a wave covers 64 columns of a tile row");
   constexpr int kPer = kCcSites / kCcThreads;
   __shared__ int lp[kCcSites];
-  __shared__ uint8_t lm[kCcSites];
+  // lk: bits 0-5 the forward links, bit 7 membership (one byte per site:
+  // 20 KB of LDS, 8 workgroups per CU).  During phase 2 the link bits are
+  // fixed and bit 7 only ever set, so a plain byte read-or-write is exact.
   __shared__ uint8_t lk[kCcSites];
   const int ntx = cdiv(g.m, kCcW);
-  const int tx = blockIdx.x % ntx, ty = blockIdx.x / ntx;
+  // XCD-contiguous tiles (the edge-column tiles, every ntx-th, would share an XCD)
+  const int tb = xcd_logical_block(blockIdx.x, gridDim.x);
+  const int tx = tb % ntx, ty = tb / ntx;
   const int c0 = tx * kCcW, r0 = ty * kCcH;
   const int tw = min(kCcW, g.m - c0), th = min(kCcH, g.n - r0);
   const bool sq = g.lattice == kSquare;
@@ -584,7 +588,7 @@ __global__ __launch_bounds__(kCcThreads) void k_cc_tile(Geom g, int kind, const 
   // forward links are (s, s+1), (s, s+m), bond ids fb, fb+1 (nearestn_square
   // lists +1 before +m in every such case).  All bond_first loads first,
   // then all link loads: two memory latencies per thread, not 2 per site.
-  constexpr int kG = 8;  // sites per batch: loads of a batch in flight together
+  constexpr int kG = 4;  // sites per batch: loads of a batch in flight together
   static_assert(kPer % kG == 0, "batches");
   for (int k0 = 0; k0 < kPer; k0 += kG) {
     int fbv[kG];
@@ -623,8 +627,8 @@ __global__ __launch_bounds__(kCcThreads) void k_cc_tile(Geom g, int kind, const 
           }
         }
       }
-      lk[li] = (uint8_t)mask;
-      lm[li] = (uint8_t)((kind != PERC_BOND && occv[u]) || (kind == PERC_BOND && mask));
+      const bool mem = (kind != PERC_BOND && occv[u]) || (kind == PERC_BOND && mask);
+      lk[li] = (uint8_t)(mask | (mem ? 0x80u : 0u));
     }
   }
   __syncthreads();
@@ -647,7 +651,7 @@ __global__ __launch_bounds__(kCcThreads) void k_cc_tile(Geom g, int kind, const 
       const unsigned long long starts = __ballot(!left);
       const unsigned long long upto = starts & (lane == 63 ? ~0ull : ((2ull << lane) - 1ull));
       par = upto ? li - lane + (63 - __clzll((long long)upto)) : li - lane - 1;
-      if (left && kind == PERC_BOND) lm[li] = 1;
+      if (left && kind == PERC_BOND) lk[li] |= 0x80u;
     }
     lp[li] = par;
   }
@@ -657,7 +661,7 @@ __global__ __launch_bounds__(kCcThreads) void k_cc_tile(Geom g, int kind, const 
   // links: k_cc_merge).  (Measured: bottom-up order beats top-down -- finds
   // 23 vs 28 us per tile, flatten 5 vs 12 us.)
   for (int li = threadIdx.x; li < kCcSites; li += kCcThreads) {
-    unsigned mask = lk[li];
+    unsigned mask = lk[li] & 0x3Fu;
     const int lr = li / kCcW, lc = li % kCcW;
     if (sq && lc + 1 < tw) mask &= ~1u;  // in the run
     // square interior: the link up from s is redundant when s-1 links up
@@ -688,7 +692,7 @@ __global__ __launch_bounds__(kCcThreads) void k_cc_tile(Geom g, int kind, const 
       const int qr = qrow - r0, qc = q - 1 - qrow * g.m - c0;
       if (qr < 0 || qr >= th || qc < 0 || qc >= tw) continue;  // crossing: k_cc_merge
       const int lq = qr * kCcW + qc;
-      if (kind == PERC_BOND) lm[lq] = 1;
+      if (kind == PERC_BOND) lk[lq] |= 0x80u;
       // LDS union (larger local root -> smaller)
       int a = li, b = lq;
       while (true) {
@@ -714,7 +718,7 @@ __global__ __launch_bounds__(kCcThreads) void k_cc_tile(Geom g, int kind, const 
     }
     const int s = (r0 + lr) * g.m + c0 + lc + 1;
     parent[s] = (r0 + x / kCcW) * g.m + c0 + x % kCcW + 1;
-    member[s] = lm[li];
+    member[s] = lk[li] >> 7;
   }
   if (trace && threadIdx.x == 0) {
     unsigned long long* o = trace + 5 * (size_t)blockIdx.x;
@@ -738,6 +742,7 @@ __global__ __launch_bounds__(kCcThreads) void k_cc_merge(Geom g, int kind, const
   // workgroups of kCcThreads per such row (the unions are spread over the
   // chip instead of queueing behind one workgroup per block-top row)
   const int nseg = cdiv(g.m, kCcThreads);
+  // (an XCD-contiguous row order measured slower here: 226 vs 151 us)
   int row = blockIdx.x, seg = 0, step = kCcThreads;
   if (row >= g.n) {
     const int e = row - g.n;
@@ -1028,36 +1033,59 @@ template <bool CSR>
 __device__ __forceinline__ void assemble_row(
     const Geom& g, int i, const int* bond_first, const uint8_t* bocc, const uint8_t* socc,
     const int* parent, const int* rowptr, double* val, double* diag, double* rhs, uint16_t* code,
-    int* sflag, const StencilForms& F, int fast_form, int bf_closed, int rule, double g0,
+    int* sflag, const StencilForms& F, int fast_form, int fast_l, int fast_r, int bf_closed,
+    int rule, double g0,
     double leak, double Va, int span_root, const double* w) {
   const int m = g.m, t = g.t, s = i + m + 1;
   const int ps = parent[s];
   const int sr = div_m(g, s - 1), sc = s - 1 - sr * m;
-  if (fast_form >= 0 && sc >= 1 && sc <= m - 2) {
-    // square lattice, interior column (fast_form: the host found the form
-    // {-m, -1, +1, +m} with deltas {(-1,0), (0,-1), (0,1), (1,0)}): the
-    // sorted neighbours are s-m, s-1, s+1, s+m and the bond ids close-form --
-    // s's forward bonds are (s, s+1), (s, s+m) in nearestn order, and s is
-    // the second forward neighbour of s-m, the first of s-1, whatever their
-    // edge or pbc case (nearestn_square: every case lists +1 before +m).
-    // The same values in the same order as the general path below.
-    // Every load is issued before any is used (bond_value's short-circuit
-    // loads would serialise four memory latencies per row).
-    int fb, bl, bd;  // bond_first of s, s-1, s-m
+  // Square lattice, closed forms (the host found each form in the table and
+  // checked its deltas): the sorted neighbours and their bond ids follow
+  // from nearestn_square case by case --
+  //   interior column: s-m, s-1, s+1, s+m; ids bf(s-m)+1, bf(s-1), fb, fb+1
+  //     (s is the 2nd forward neighbour of s-m, the 1st of s-1 -- every
+  //     nearestn_square case lists +1 before +m);
+  //   column 0: s-m, s+1, [s+m-1 (pbc)], s+m; ids bf(s-m)+1, fb, [fb+2], fb+1
+  //     (s's forward order is s+1, s+m, s+m-1);
+  //   column m-1: s-m, [s-m+1 (pbc)], s-1, s+m; ids bf(s-m), [bf(s-m+1)+2],
+  //     bf(s-1), fb (s-m's only forward neighbour is s; s is the 3rd of s-m+1).
+  // RHS (top system row): the one forward neighbour above, s+m (the pbc
+  // wrap neighbour s+m-1 of column 0 is in s's own row).  Every load is issued before any
+  // is used (bond_value's short-circuit loads would serialise the latencies).
+  const int kind_c = sc >= 1 && sc <= m - 2 ? 0 : (sc == 0 ? 1 : 2);
+  const int cform = kind_c == 0 ? fast_form : kind_c == 1 ? fast_l : fast_r;
+  if (cform >= 0) {
+    const bool pb = g.pbc != 0;
+    int fb, bl, bd, bw = 0;  // bond_first of s, s-1, s-m, s-m+1
     if (bf_closed) {
       fb = bf_square(g, sr, sc);
-      bl = bf_square(g, sr, sc - 1);
+      bl = sc > 0 ? bf_square(g, sr, sc - 1) : 0;
       bd = bf_square(g, sr - 1, sc);
+      bw = bf_square(g, sr, 0);
     } else {
       fb = bond_first[s];
-      bl = bond_first[s - 1];
+      bl = sc > 0 ? bond_first[s - 1] : 0;
       bd = bond_first[s - m];
+      bw = kind_c == 2 && pb ? bond_first[s - m + 1] : 0;
     }
-    const int ids[4] = {bd + 1, bl, fb, fb + 1};
-    const int cs[4] = {s - m, s - 1, s + 1, s + m};
+    int cs[4], ids[4], cnt;
+    if (kind_c == 0) {
+      cnt = 4;
+      cs[0] = s - m; cs[1] = s - 1; cs[2] = s + 1; cs[3] = s + m;
+      ids[0] = bd + 1; ids[1] = bl; ids[2] = fb; ids[3] = fb + 1;
+    } else if (kind_c == 1) {
+      cnt = pb ? 4 : 3;
+      cs[0] = s - m; cs[1] = s + 1; cs[2] = pb ? s + m - 1 : s + m; cs[3] = s + m;
+      ids[0] = bd + 1; ids[1] = fb; ids[2] = pb ? fb + 2 : fb + 1; ids[3] = fb + 1;
+    } else {
+      cnt = pb ? 4 : 3;
+      cs[0] = s - m; cs[1] = pb ? s - m + 1 : s - 1; cs[2] = pb ? s - 1 : s + m; cs[3] = s + m;
+      ids[0] = bd; ids[1] = pb ? bw + 2 : bl; ids[2] = pb ? bl : fb; ids[3] = fb;
+    }
     unsigned bo[4], so[4] = {1u, 1u, 1u, 1u}, ss = 1u;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) bo[j] = rule == PERC_RULE_SITE ? 1u : bocc[ids[j]];
+    for (int j = 0; j < 4; ++j)
+      bo[j] = rule == PERC_RULE_SITE ? 1u : bocc[ids[j]];
     if (rule != PERC_RULE_BOND) {
       ss = socc[s];
 #pragma unroll
@@ -1075,15 +1103,16 @@ __device__ __forceinline__ void assemble_row(
     int k = CSR ? rowptr[i] : 0;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
+      if (j >= cnt) break;
       const double gv = gvs[j];
       if (gv == -g0) bits |= 1u << j;
       rowsum = rowsum + gv;
       if (CSR && cs[j] > m && cs[j] <= t - m) val[k++] = gv;
     }
-    code[i] = (uint16_t)(bits | 4u << 8 | (unsigned)fast_form << 11);
+    code[i] = (uint16_t)(bits | (unsigned)cnt << 8 | (unsigned)cform << 11);
     if (CSR) diag[i] = -rowsum;
     double acc = 0.0;
-    if (s > t - 2 * m) acc = acc - (gvs[3] * Va);  // (s, s+m): bond fb + 1
+    if (s > t - 2 * m) acc = acc - (gvs[cnt - 1] * Va);  // (s, s+m): the last slot
     rhs[i] = acc;
     return;
   }
@@ -1165,20 +1194,44 @@ __device__ __forceinline__ void assemble_row(
   rhs[i] = acc;
 }
 
-// grid-stride over the rows: a fixed grid (kAsmGrid workgroups) amortises
-// each wave's start-up (kernel-argument loads, ~1 us) over many rows
-constexpr int kAsmGrid = 2048;
+// One row per thread (a grid-stride loop measured 1.65x slower: each
+// iteration's loads wait for the last's, fewer rows in flight).  The
+// StencilForms table (~900 B) is read through a device pointer by the
+// general path only: as a kernel argument every wave would s_load it.
 template <bool CSR>
 __global__ __launch_bounds__(kBlock) void k_assemble(
     Geom g, int N, const int* bond_first, const uint8_t* bocc, const uint8_t* socc,
     const int* parent, const int* rowptr, double* val, double* diag, double* rhs, uint16_t* code,
-    int* sflag, StencilForms F, int fast_form, int bf_closed, int rule, double g0, double leak,
-    double Va, int span_root, const double* w) {
-  const int i0 = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i0 == 0 && w) atomicOr(sflag, 1);  // per-bond values: no two-value stencil code
-  for (int i = i0; i < N; i += gridDim.x * blockDim.x)
-    assemble_row<CSR>(g, i, bond_first, bocc, socc, parent, rowptr, val, diag, rhs, code, sflag, F,
-                      fast_form, bf_closed, rule, g0, leak, Va, span_root, w);
+    int* sflag, const StencilForms* F, int fast_form, int fast_l, int fast_r, int bf_closed,
+    int rule, double g0,
+    double leak, double Va, int span_root, const double* w) {
+  // XCD-contiguous row blocks: in dispatch order the lattice's edge-column
+  // workgroups (general path, ~6x the closed form's work) are every 16th at
+  // m = 4096 -- all on one XCD, the kernel waited on it (+120 us at L = 4096)
+  const int i = xcd_logical_block(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
+  if (i == 0 && w) atomicOr(sflag, 1);  // per-bond values: no two-value stencil code
+  // a workgroup with a general-path row (an edge column, a triangular or
+  // non-closed-form lattice) stages the form table in LDS first: read from
+  // global memory inside the general path's loops it was a chain of
+  // dependent loads, ~100 us of latency per such wave -- the kernel's tail
+  __shared__ StencilForms sF;
+  bool gen = false;
+  if (i < N) {
+    const int s = i + g.m + 1, sr = div_m(g, s - 1), sc = s - 1 - sr * g.m;
+    const int f = sc >= 1 && sc <= g.m - 2 ? fast_form : (sc == 0 ? fast_l : fast_r);
+    gen = f < 0;
+  }
+  if (__syncthreads_or(gen)) {
+    static_assert(sizeof(StencilForms) % 4 == 0, "word copy");
+    const int nw = (int)(sizeof(StencilForms) / 4);
+    const int* src = reinterpret_cast<const int*>(F);
+    int* dst = reinterpret_cast<int*>(&sF);
+    for (int k = threadIdx.x; k < nw; k += blockDim.x) dst[k] = src[k];
+    __syncthreads();
+  }
+  if (i >= N) return;
+  assemble_row<CSR>(g, i, bond_first, bocc, socc, parent, rowptr, val, diag, rhs, code, sflag, sF,
+                    fast_form, fast_l, fast_r, bf_closed, rule, g0, leak, Va, span_root, w);
 }
 
 // Terminal currents of the 2m boundary rows (bondc.f:554-592; ConductCalc.m:188)
@@ -4305,6 +4358,8 @@ hipError_t dev_build_lattice(perc_ctx* h) {
   HIP_TRY(dmalloc(&d.rhs, N + 2));
   HIP_TRY(dmalloc(&d.dtab, kDiagTab));  // double2 entries
   h->forms = stencil_forms(g);
+  HIP_TRY(dmalloc(&d.forms_dev, 1));
+  HIP_TRY(hipMemcpy(d.forms_dev, &h->forms, sizeof(StencilForms), hipMemcpyHostToDevice));
   HIP_TRY(dmalloc(&d.sflag, 4));
   // occupancy + labeling
   HIP_TRY(dmalloc(&d.bocc, (size_t)h->nb + 8));
@@ -4399,7 +4454,7 @@ void dev_free_all(perc_ctx* h) {
                   d.order, d.parent, d.member, d.top, d.counters, d.x, d.r,
                   d.p0, d.p1, d.q, d.partials, d.tickets, d.scal, d.err_hist, d.iout,
                   d.res_xch, d.res_part, d.res_bar, d.bw, d.code_sm, d.csize, d.res_gran,
-                  d.sel_hist, d.sel_cand, d.mgran};
+                  d.sel_hist, d.sel_cand, d.mgran, d.forms_dev};
   for (void* p : ptrs)
     if (p) hipFree(p);
   d = DeviceBuffers{};
@@ -4816,25 +4871,42 @@ static hipError_t launch_assemble(perc_ctx* h, bool csr) {
   const int m = h->g.m;
   const char* gen = std::getenv("PERC_ASM_GENERIC");  // tests: the general path only
   const bool closed = !(gen && gen[0] == '1');
-  for (int f = 0; f < F.nforms && closed && h->g.lattice == kSquare && m >= 3; ++f) {
-    const int off[4] = {-m, -1, 1, m}, dr[4] = {-1, 0, 0, 1}, dc[4] = {0, -1, 1, 0};
-    bool same = F.cnt[f] == 4;
-    for (int j = 0; j < 4 && same; ++j)
-      same = F.off[f][j] == off[j] && F.dr[f][j] == dr[j] && F.dc[f][j] == dc[j];
-    if (same) {
-      fast = f;
-      break;
+  // the closed-form rows' forms (k_assemble): offsets and lattice deltas of
+  // the interior, column-0 and column-(m-1) rows of the square lattice
+  auto find_form = [&](int cnt, const int* off, const int* dr, const int* dc) {
+    for (int f = 0; f < F.nforms; ++f) {
+      bool same = F.cnt[f] == cnt;
+      for (int j = 0; j < cnt && same; ++j)
+        same = F.off[f][j] == off[j] && F.dr[f][j] == dr[j] && F.dc[f][j] == dc[j];
+      if (same) return f;
+    }
+    return -1;
+  };
+  int fl = -1, fr = -1;
+  if (closed && h->g.lattice == kSquare && m >= 4) {
+    const int oi[4] = {-m, -1, 1, m}, ri[4] = {-1, 0, 0, 1}, ci[4] = {0, -1, 1, 0};
+    fast = find_form(4, oi, ri, ci);
+    if (h->g.pbc) {
+      const int ol[4] = {-m, 1, m - 1, m}, rl[4] = {-1, 0, 0, 1}, cl[4] = {0, 1, -1, 0};
+      const int orr[4] = {-m, -(m - 1), -1, m}, rr[4] = {-1, 0, 0, 1}, cr[4] = {0, 1, -1, 0};
+      fl = find_form(4, ol, rl, cl);
+      fr = find_form(4, orr, rr, cr);
+    } else {
+      const int ol[3] = {-m, 1, m}, rl[3] = {-1, 0, 1}, cl[3] = {0, 1, 0};
+      const int orr[3] = {-m, -1, m}, rr[3] = {-1, 0, 1}, cr[3] = {0, -1, 0};
+      fl = find_form(3, ol, rl, cl);
+      fr = find_form(3, orr, rr, cr);
     }
   }
   if (csr)
-    k_assemble<true><<<std::min<int>(cdiv(h->N, kBlock), kAsmGrid), kBlock, 0, st>>>(h->g, h->N, d.bond_first, d.bocc, d.socc,
+    k_assemble<true><<<cdiv(h->N, kBlock), kBlock, 0, st>>>(h->g, h->N, d.bond_first, d.bocc, d.socc,
                                                           d.parent, d.rowptr, d.val, d.diag, d.rhs,
-                                                          d.code, d.sflag, h->forms, fast, (int)h->bf_closed, p.rule,
+                                                          d.code, d.sflag, d.forms_dev, fast, fl, fr, (int)h->bf_closed, p.rule,
                                                           p.g0, p.leak, p.Va, p.span_root, w);
   else
-    k_assemble<false><<<std::min<int>(cdiv(h->N, kBlock), kAsmGrid), kBlock, 0, st>>>(h->g, h->N, d.bond_first, d.bocc, d.socc,
+    k_assemble<false><<<cdiv(h->N, kBlock), kBlock, 0, st>>>(h->g, h->N, d.bond_first, d.bocc, d.socc,
                                                            d.parent, d.rowptr, d.val, d.diag, d.rhs,
-                                                           d.code, d.sflag, h->forms, fast, (int)h->bf_closed, p.rule,
+                                                           d.code, d.sflag, d.forms_dev, fast, fl, fr, (int)h->bf_closed, p.rule,
                                                            p.g0, p.leak, p.Va, p.span_root, w);
   HIP_TRY(dbg_sync(st, "k_assemble"));
   h->csr_ok = csr;
@@ -4871,6 +4943,28 @@ hipError_t dev_assemble(perc_ctx* h, int rule, double g0, double leak, double Va
   select_format(h);
   if (!h->stencil_ok) HIP_TRY(launch_assemble(h, true));
   return hipSuccess;
+}
+
+// The resident solve's synchronisation floor (perc_bench_kernel 6): the
+// same cooperative grid running only what an iteration of k_cg_res does to
+// synchronise -- the two block sums and the two tagged-granule all-gathers
+// (res_gather<1>, res_gather<2>) -- on dummy values, `iters` times.  The
+// time per iteration is what the resident solve cannot go below whatever
+// its memory traffic.
+__global__ __launch_bounds__(1024) void k_res_sync_probe(ResArgs a, int iters) {
+  __shared__ double s_red[32];
+  unsigned epoch = 0;
+  double v1[1] = {(double)blockIdx.x}, tot1[1], acc2[2], tot2[2];
+  for (int k = 0; k < iters; ++k) {
+    double w1[1] = {v1[0] + (double)threadIdx.x};
+    block_sum<1>(w1, s_red);
+    if (!res_gather<1>(a, epoch, a.gran, w1, tot1, s_red)) break;
+    acc2[0] = tot1[0] * 1e-30 + (double)threadIdx.x;
+    acc2[1] = (double)k;
+    block_sum<2>(acc2, s_red);
+    if (!res_gather<2>(a, epoch, a.gran + 2 * (size_t)a.G, acc2, tot2, s_red)) break;
+    v1[0] = tot2[0] * 1e-30;
+  }
 }
 
 // the resident kernel for m = 1024 (MT = 1) / 2048, square-lattice
@@ -5708,6 +5802,7 @@ hipError_t dev_bench(perc_ctx* h, int which, int reps, double* ms) {
   HIP_TRY(hipMemcpyAsync(d.scal, &hs, sizeof(hs), hipMemcpyHostToDevice, st));
   HIP_TRY(hipMemsetAsync(d.tickets, 0, kRedSlots * red_tickets_size(red_grid(h)) * sizeof(unsigned),
                          st));
+  if (which == 6 && h->res_G <= 0) return hipErrorInvalidConfiguration;  // no resident grid
   // STREAM copy: 512 MB -> 512 MB, well past the 256 MB Infinity Cache
   double *cp_src = nullptr, *cp_dst = nullptr;
   const size_t cp_n = (size_t)64 << 20;
@@ -5727,6 +5822,16 @@ hipError_t dev_bench(perc_ctx* h, int which, int reps, double* ms) {
     } else if (which == 3) {
       if (ST) k_cg_p<true><<<G, kBlock, 0, st>>>(a);
       else k_cg_p<false><<<G, kBlock, 0, st>>>(a);
+    } else if (which == 6) {  // resident sync floor: 16 iterations per launch
+      ResArgs ra{};
+      ra.G = h->res_G;
+      ra.gran = d.res_gran;
+      ra.S = d.scal;
+      int iters = 16;
+      void* args[] = {&ra, &iters};
+      (void)hipMemsetAsync(d.res_gran, 0, (size_t)2 * 3 * h->res_G * sizeof(double), st);
+      (void)hipLaunchCooperativeKernel((const void*)k_res_sync_probe, dim3(ra.G),
+                                       dim3(h->res_NT), args, 0, st);
     } else if (which == 5) {  // one whole iteration
       if (!h->fused) {
         if (ST) k_cg_p<true><<<G, kBlock, 0, st>>>(a);
@@ -5748,7 +5853,7 @@ hipError_t dev_bench(perc_ctx* h, int which, int reps, double* ms) {
   HIP_TRY(hipEventSynchronize(h->ev[1]));
   float t = 0.f;
   HIP_TRY(hipEventElapsedTime(&t, h->ev[0], h->ev[1]));
-  *ms = (double)t / reps;
+  *ms = (double)t / reps / (which == 6 ? 16 : 1);
   if (cp_src) HIP_TRY(hipFree(cp_src));
   if (cp_dst) HIP_TRY(hipFree(cp_dst));
   return hipSuccess;

@@ -908,7 +908,7 @@ int perc_selftest_division(long long n, unsigned long long seed, unsigned long l
 }
 
 int perc_bench_kernel(perc_ctx* h, int which, int reps, double* ms) {
-  if (!h || !ms || reps <= 0 || which < 0 || which > 5) return PERC_EINVAL;
+  if (!h || !ms || reps <= 0 || which < 0 || which > 6) return PERC_EINVAL;
   if (!h->assembled && which != 4) return PERC_ESTATE;  // the copy needs no system
   hipSetDevice(h->device);
   // the CG kernels clobber the solver vectors (x, r, p, q), not the system

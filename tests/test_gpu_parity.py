@@ -866,10 +866,12 @@ def test_small_solver_matches_launched(lat, m, n, pbc, p):
 @pytest.mark.gpu
 @pytest.mark.parametrize("kind,rule,m,n,pbc", [(PL.BOND, PL.RULE_BOND, 256, 150, 0),
                                                (PL.BOND, PL.RULE_BOND, 131, 90, 1),
-                                               (PL.SITEBOND, PL.RULE_MIXED, 200, 64, 0)])
+                                               (PL.SITEBOND, PL.RULE_MIXED, 200, 64, 0),
+                                               (PL.SITEBOND, PL.RULE_MIXED, 96, 70, 1),
+                                               (PL.SITE, PL.RULE_SITE, 130, 70, 1)])
 def test_closed_form_assembly_is_the_general_one(kind, rule, m, n, pbc, monkeypatch):
-    """k_assemble's closed-form path for the square lattice's interior
-    columns writes what its general path (PERC_ASM_GENERIC=1: nearestn +
+    """k_assemble's closed-form paths for the square lattice (interior,
+    column 0, column m-1; with and without pbc) write what its general path (PERC_ASM_GENERIC=1: nearestn +
     bond_id per neighbour) writes: the same CSR system bitwise and the same
     solve."""
     nb, t = api.nbonds(0, m, n, pbc), m * n

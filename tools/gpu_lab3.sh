@@ -1,0 +1,6 @@
+set -o pipefail
+mkdir -p gpurun_out/lab1
+export TMPDIR=/tmp
+R=$GRAFT_REPO_ROOT
+timeout -k 10 300 python bench.py --L 1024 --p 0.50 --steps 16 --warmup 1 --no-cpu-baseline > gpurun_out/lab1/c2.json 2> gpurun_out/lab1/c2.log && \
+cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d $R/gpurun_out/lab1/prof -o run -- python3 $R/tools/label_probe.py --L 4096 --reps 8 > $R/gpurun_out/lab1/prof.log 2>&1
