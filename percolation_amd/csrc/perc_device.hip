@@ -5566,9 +5566,8 @@ hipError_t dev_dslab_end(perc_ctx* h, bool to_ctx) {
   return e;
 }
 
-hipError_t dev_dslab_begin(perc_ctx* h, int K, int s, int itol, double tol, int itmax, bool full_x,
-                           const perc_dslab_bufs& bufs) {
-  HIP_TRY(dev_dslab_end(h, false));
+static hipError_t dslab_setup(perc_ctx* h, int K, int s, int itol, double tol, int itmax, bool full_x,
+                              const perc_dslab_bufs& bufs) {
   DeviceBuffers& d = h->d;
   hipStream_t st = h->stream;
   const int m = h->g.m, nrows = h->g.n - 2;
@@ -5648,6 +5647,17 @@ hipError_t dev_dslab_begin(perc_ctx* h, int K, int s, int itol, double tol, int 
   k_cg_init<true><<<b.init_grid, kBlock, 0, st>>>(a, itol, 1);
   HIP_TRY(dbg_sync(st, "k_cg_init (dslab)"));
   return dev_dslab_step(h, -1);
+}
+
+// A setup that fails part-way leaves no half-built slab behind: a later
+// perc_dslab_step then sees no slab and returns PERC_EINVAL instead of
+// launching the march on null vectors.
+hipError_t dev_dslab_begin(perc_ctx* h, int K, int s, int itol, double tol, int itmax, bool full_x,
+                           const perc_dslab_bufs& bufs) {
+  HIP_TRY(dev_dslab_end(h, false));
+  const hipError_t e = dslab_setup(h, K, s, itol, tol, itmax, full_x, bufs);
+  if (e != hipSuccess) (void)dev_dslab_end(h, false);
+  return e;
 }
 
 // op: -1 publish partials + edge rows (after the prologue); PERC_DSLAB_* of perc.h
