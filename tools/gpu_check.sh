@@ -25,7 +25,7 @@ run() {  # run NAME TIMEOUT CMD...
 for step in "$@"; do
   case "$step" in
     tests) run pytest_gpu 900 python -u -m pytest tests -m gpu -v -rs -x --timeout 300 --timeout-method thread ;;
-    testsall) run pytest_gpu 900 python -m pytest tests -m gpu -q -rs ;;
+    testsall) run pytest_gpu 900 python -u -m pytest tests -m gpu -q -rs --timeout 300 --timeout-method thread ;;
     tests_march) run pytest_march 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread -k "march or division or resident" ;;
     tests_march2) PERC_MARCH_DEPTH=2 run pytest_march2 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -k "march or slab" ;;
     ab_depth) run ab_depth 800 bash tools/ab_depth4w.sh ;;
@@ -41,6 +41,11 @@ for step in "$@"; do
     prof) run prof 900 rocprofv3 --kernel-trace --stats -f csv -d gpurun_out/prof -o run -- \
             python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline ;;
     pmc) run pmc 900 bash tools/pmc_r2.sh ;;
+    pmc8192) L=8192 run pmc8192 900 bash tools/pmc_r2.sh ;;
+    label) run label 300 python tools/label_probe.py --L 4096 --reps 8 ;;
+    labelprof) run labelprof 300 rocprofv3 --kernel-trace --stats -f csv -d gpurun_out/labelprof -o run -- \
+            python3 tools/label_probe.py --L 4096 --reps 8 ;;
+    scan) run scan 600 python tools/scan_bench.py --L 256,1024 --trials 8 --cond-L 64,256 --cond-trials 2 ;;
     full_voltages) run bench_fullv 900 python bench.py --full-voltages --steps 1 --warmup 1 --no-cpu-baseline ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
