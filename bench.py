@@ -180,6 +180,47 @@ def cpu_ensemble(L_, p, seeds, iters, nb, tb, cpu_iters, cores, occupancy="unifo
             "wall_seconds": round(time.perf_counter() - t0, 2)}
 
 
+def labeling_probe(ctx, P, L_, nb, tb, seeds):
+    """Occupancy draw, labeling + spanning test and Kirchhoff assembly of
+    the timed realisations again, phase by phase after a synchronize (best
+    of the seeds), outside the timed region.  Algorithmic bytes
+    (Square/bondc.f:194-393 labels, :482-532 assembly; t = L^2 sites, N =
+    interior rows): occupy writes the nb u8 bond flags; labeling reads them
+    and writes the int32 parent and u8 member arrays (nb + 5t); assembly
+    reads flags, parents and members (nb + 5t) and writes the u16 row codes
+    and the f64 right-hand side (10N).  The roofline is 8 TB/s."""
+    import torch
+    t = L_ * L_
+    N = t - 2 * L_
+    ctx.set_matrix_format(P.FMT_AUTO)  # (the kernel probe left the last format set)
+    best = None
+    for sd in seeds:
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        ctx.occupy_random(P._lib.BOND, 0, tb, sd)
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        li = ctx.label()
+        t2 = time.perf_counter()
+        if not li["nspan"]:
+            continue
+        c = ctx.conductance(tol=1e-8, itmax=1)
+        row = ((t1 - t0) * 1e3, (t2 - t1) * 1e3, c["t_assemble_ms"])
+        best = row if best is None else tuple(min(a, b) for a, b in zip(best, row))
+    if best is None:
+        return None
+    phases = {"occupy": (best[0], nb), "label": (best[1], nb + 5 * t),
+              "assemble": (best[2], nb + 5 * t + 10 * N)}
+    out = {k: {"ms": round(ms, 4), "bytes": b, "gbs": round(b / (ms * 1e-3) / 1e9, 1),
+               "frac": round(b / (ms * 1e-3) / 1e9 / PEAK_HBM_GBS, 4)}
+           for k, (ms, b) in phases.items()}
+    tot = sum(v[0] for v in phases.values())
+    out["total_ms"] = round(tot, 4)
+    out["note"] = ("per realisation, best of %d, wall time after a synchronize (label includes "
+                   "the spanning test's host read-back)" % len(seeds))
+    return out
+
+
 def kernel_label(key, minfo):
     """Name + role of a CG kernel, for the march variant that ran."""
     if key == "pm" and minfo.get("kernel") in ("wave", "rows"):
@@ -695,6 +736,9 @@ def main():
         # two block sums + two tagged-granule all-gathers per iteration on
         # the resident grid, nothing else (k_res_sync_probe)
         sync_floor = round(ctx.bench_kernel(6, 20), 5)
+    labeling = None
+    if devocc and args.kind == "bond" and rank == 0:
+        labeling = labeling_probe(ctx, P, L_, nb, tb, [int(seeds[ii_list[k]]) for k in timed][:4])
     copy_ms = ctx.bench_kernel(4, 20)
     copy_bytes = 2 * 8 * (64 << 20)  # 512 MB read + 512 MB written (perc_bench_kernel 4)
     stream_copy = {"ms": round(copy_ms, 5), "bytes": copy_bytes,
@@ -771,6 +815,8 @@ def main():
         "kernel_probe": probe,
         "stream_copy": stream_copy,
     }
+    if labeling is not None:
+        out["labeling"] = labeling
     if rank == 0 and world == 1 and args.kind == "bond" and devocc:
         out["pcie_inclusive"] = {"note": "occupancy drawn on the device: no host array crosses "
                                          "PCIe per realisation"}
