@@ -230,6 +230,11 @@ def kernel_label(key, minfo):
             name, minfo["strip_cols"], minfo["band_rows"], ", alternating" if minfo["alt"] else "",
             ", strip-major" if minfo.get("strips") else "",
             "" if minfo["qfree"] else ", q stored")
+    if key == "pmarch":
+        return ("k_cg_pmarch (persistent per-wave register march, 128 cols x ~%d rows, strip-major, "
+                "slot-weighted bands: the P walk, an all-gather of q.p, the B walk, an all-gather of "
+                "z.r and r.r per iteration in one cooperative launch; bytes = 52 B/row + x rows per "
+                "iteration)" % minfo["band_rows"])
     if key == "res":
         return ("k_cg_res (resident persistent solve, %d-row bands: p in LDS, r/q in registers, "
                 "2 grid-wide reductions per iteration; bytes = the streaming-equivalent 52 B/row "
@@ -243,6 +248,7 @@ def kernel_label(key, minfo):
 
 # rocprof kernel names of the CG kernels, per operator format
 ROCPROF_NAMES = {("res", "stencil"): ("k_cg_res",),  # default kernel of each role first
+                 ("pmarch", "stencil"): ("k_cg_pmarch",),
                  ("res", "stencil_tiled"): ("k_cg_res",),
                  ("pm", "stencil"): ("k_cg_march<1", "k_cg_march<0", "k_cg_rm<0", "k_cg_rm<1"),
                  ("ps", "stencil_tiled"): ("k_cg_ps<4>", "k_cg_ps<6>"),
@@ -674,6 +680,11 @@ def main():
         """(key, stats key, perc_bench_kernel id, bytes) of the CG kernels of
         operator format f"""
         full = args.full_voltages
+        if f == "stencil" and minfo.get("kernel") == "persistent" and not probe:
+            # the whole q-free march loop in one cooperative launch: per
+            # iteration the P walk (26N) and the B walk (26N) plus the x rows,
+            # the same bytes as the two launched kernels
+            return [("pmarch", "spmv", 5, 52 * N + 48 * L_)]
         if f in ("stencil", "stencil_tiled") and minfo.get("kernel") == "resident" and not probe:
             # whole iterations in one persistent launch, r / q / codes held
             # on chip: the bytes are the streaming-equivalent 52 B/row (what

@@ -360,7 +360,13 @@ int perc_set_march_rows(perc_ctx *h, int rows);
    same per-row arithmetic, dot products over other wave partials.
    PERC_MARCH_TAG (strip-major q-free march): the end-of-kernel reductions
    publish tagged {value, tag} granules the readers poll for, instead of
-   draining stores before each ticket; bitwise the same totals. */
+   draining stores before each ticket; bitwise the same totals.
+   PERC_MARCH_PERSIST (strip-major q-free march with slot-weighted bands
+   and tagged granules): the whole iteration loop in one cooperative launch
+   (P walk, all-gather of q.p, B walk over the same bands, all-gather of
+   z.r and r.r), cross-workgroup rows stored write-through; bitwise the
+   same iterates.  Falls back to the launched kernels when the grid cannot
+   be co-resident. */
 #define PERC_MARCH_QFREE 1
 #define PERC_MARCH_ALT 2
 #define PERC_MARCH_ROWS 4
@@ -369,6 +375,7 @@ int perc_set_march_rows(perc_ctx *h, int rows);
 #define PERC_MARCH_DEFER 32
 #define PERC_MARCH_SLOTS 64
 #define PERC_MARCH_TAG 128
+#define PERC_MARCH_PERSIST 256
 #define PERC_MARCH_DEFAULT                                                                      \
   (PERC_MARCH_QFREE | PERC_MARCH_ALT | PERC_SOLVE_RESIDENT | PERC_MARCH_STRIPS | PERC_MARCH_SLOTS | \
    PERC_MARCH_TAG)
@@ -384,7 +391,8 @@ int perc_set_bond_weights(perc_ctx *h, const double *w, long long n);
    tiles, split or CSR), 1 (per-wave march k_cg_march), 2 (workgroup
    row-march k_cg_rm), 3 (resident persistent solve k_cg_res), 4 (one-
    workgroup solve of a small system, k_cg_small: N <= 8192 under
-   PERC_FMT_AUTO with PERC_SOLVE_RESIDENT set); out5[1] = bit 0: q-free
+   PERC_FMT_AUTO with PERC_SOLVE_RESIDENT set), 5 (persistent march
+   k_cg_pmarch, PERC_MARCH_PERSIST); out5[1] = bit 0: q-free
    B, bit 1: strip-major solve layout, bit 2: deferred reductions
    (PERC_MARCH_DEFER), bit 3: slot-weighted bands (PERC_MARCH_SLOTS; past
    the Infinity Cache the row-major P kernel's one round of bands);

@@ -26,6 +26,7 @@ CUR_FORTRAN, CUR_MATLAB = 0, 1
 FMT_AUTO, FMT_CSR, FMT_STENCIL, FMT_STENCIL_SPLIT, FMT_STENCIL_TILED = 0, 1, 2, 3, 4
 MARCH_QFREE, MARCH_ALT, MARCH_ROWS, SOLVE_RESIDENT, MARCH_STRIPS, MARCH_DEFER, MARCH_SLOTS, MARCH_TAG = (
     1, 2, 4, 8, 16, 32, 64, 128)
+MARCH_PERSIST = 256
 MARCH_DEFAULT = MARCH_QFREE | MARCH_ALT | SOLVE_RESIDENT | MARCH_STRIPS | MARCH_SLOTS | MARCH_TAG
 
 

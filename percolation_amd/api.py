@@ -253,7 +253,7 @@ class Context:
         """The solver loop of the assembled system (perc_march_info)."""
         out = np.zeros(5, dtype=np.int32)
         L.check(L.lib().perc_march_info(self.h, out.ctypes.data), "perc_march_info")
-        return dict(kernel=("none", "wave", "rows", "resident", "small")[out[0]],
+        return dict(kernel=("none", "wave", "rows", "resident", "small", "persistent")[out[0]],
                     qfree=bool(out[1] & 1), strips=bool(out[1] & 2), defer=bool(out[1] & 4), slots=bool(out[1] & 8), tag=bool(out[1] & 16),
                     alt=bool(out[2]), band_rows=int(out[3]), strip_cols=int(out[4]))
 

@@ -2435,7 +2435,13 @@ __device__ __forceinline__ unsigned melem(const CGArgs& a, const MBuf& B, int gr
   return SM ? (unsigned)sm_at(a.T, gr, col) : (unsigned)((gr - B.lo) * a.T.m + col);
 }
 
-template <int MODE, bool SM, int PAUX = 0>
+// CAUX != 0 (the persistent march): every p / r load carries that cache
+// policy (sc1: rows other workgroups stored write-through in this launch)
+template <int CAUX>
+__device__ __forceinline__ double bld1x(__amdgpu_buffer_rsrc_t r, unsigned off) {
+  return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, (int)off, 0, CAUX));
+}
+template <int MODE, bool SM, int PAUX = 0, int CAUX = 0>
 __device__ __forceinline__ void march_load(const CGArgs& a, const MGeom& g, const MBuf& B, int gr,
                                            bool first, const double* __restrict__ psrc, MRow& R) {
   {
@@ -2449,17 +2455,18 @@ __device__ __forceinline__ void march_load(const CGArgs& a, const MGeom& g, cons
     R.c = __builtin_amdgcn_raw_buffer_load_b32(B.c, (int)(rowok ? e * 2u : kOOB), 0, 0);
     // PAUX on the loads that read a value for the last time: P's p(k-1)
     // (dead once p(k) is formed), B's r(k) (overwritten by r(k+1))
-    constexpr int kRAux = MODE == kMarchB ? PAUX : 0, kPAux = MODE == kMarchP ? PAUX : 0;
+    constexpr int kRAux = CAUX ? CAUX : (MODE == kMarchB ? PAUX : 0);
+    constexpr int kPAux = CAUX ? CAUX : (MODE == kMarchP ? PAUX : 0);
     R.r = __builtin_bit_cast(double2, __builtin_amdgcn_raw_buffer_load_b128(B.r, (int)(rown ? o8 : kOOB), 0, kRAux));
     R.p = __builtin_bit_cast(double2, __builtin_amdgcn_raw_buffer_load_b128(B.p, (int)(first ? kOOB : o8), 0, kPAux));
     if (MODE != kMarchB) {
       R.hc = __builtin_amdgcn_raw_buffer_load_b16(B.c, (int)(hk ? eh * 2u : kOOB), 0, 0);
-      R.hr = bld1(B.r, h8);
+      R.hr = bld1x<CAUX>(B.r, h8);
     } else {
       R.hc = 0u;
       R.hr = 0.0;
     }
-    R.hp = bld1(B.p, first ? kOOB : h8);
+    R.hp = bld1x<CAUX>(B.p, first ? kOOB : h8);
   }
 }
 
@@ -2607,7 +2614,7 @@ __device__ __forceinline__ void march_step(const CGArgs& a, const MGeom& g, cons
   }
 }
 
-template <int MODE, int D, bool UP, bool SM, int PAUX = 0, int SAUX = kNT>
+template <int MODE, int D, bool UP, bool SM, int PAUX = 0, int SAUX = kNT, int CAUX = 0>
 __device__ __forceinline__ void march_walk(const CGArgs& a, const MGeom& g, const MBuf& B,
                                            MRow (&ring)[D],
                                            bool first, double bk, double ak,
@@ -2630,7 +2637,7 @@ __device__ __forceinline__ void march_walk(const CGArgs& a, const MGeom& g, cons
       // step count) and the prefetch past its end address rows outside the
       // view (loads return 0, stores are dropped) and finish no row
       const MRow R = ring[u];
-      march_load<MODE, SM, PAUX>(a, g, B, UP ? g.rend - (j + D) : g.r0 - 1 + j + D, first, psrc, ring[u]);
+      march_load<MODE, SM, PAUX, CAUX>(a, g, B, UP ? g.rend - (j + D) : g.r0 - 1 + j + D, first, psrc, ring[u]);
       march_step<MODE, UP, SM, SAUX>(a, g, B, R, UP ? g.rend - j : g.r0 - 1 + j, first, bk, ak, pnew, s_dt,
                                s_rpos, s_rmap, s_w, W, acc);
     }
@@ -2869,6 +2876,208 @@ __global__ __launch_bounds__(64 * kMarchWaves, (kMarchWavesPerEU<MODE, D, SM>)) 
   if constexpr (TR) {
     if (lane == 0) a.mtrace[4 * (size_t)w + 2] = wall_clock64();
   }
+}
+
+// ---------------------------------------------------------------------------
+// Persistent march (PERC_MARCH_PERSIST): the whole linbcg loop of the
+// strip-major q-free march in ONE cooperative launch -- per iteration the P
+// walk, an all-gather of q.p, the B walk over the same bands, an all-gather
+// of z.r and r.r.  Against two launches per iteration it drops the
+// per-launch dispatch / end-of-kernel time (~5 us of each 78 us launch
+// outside the waves' lifetime, profiles/r3_4_mtrace_summary_L4096.txt) and
+// the last workgroup's ticket tail.  Cross-workgroup data inside the launch
+// (halo rows and columns of p(k) and r(k+1)) is stored write-through (sc1)
+// and every p / r load is an sc1 load; every wave drains its stores before
+// its workgroup publishes (MI355X_MICROARCH.md, hand-off table row 1).
+// Totals: every workgroup sums the same granules in publish_and_reduce's
+// association (group wave butterflies, then the strided block sum), so the
+// iterates are bitwise the launched march's.
+template <int NV>
+__device__ bool pm_allgather(double (&v)[NV], double* gran, int lb, int nwg, double tag,
+                             double (&tot)[NV], double* s_red, double* s_g, int* s_flag) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's row stores are written through
+  block_sum<NV>(v, s_red);                           // (barrier: every wave has drained)
+  const int ngroups = red_groups(nwg);
+  const int grp = lb / kGroup, g0 = grp * kGroup, gn = min(kGroup, nwg - g0);
+  const __amdgpu_buffer_rsrc_t rg = rsrc(gran, (unsigned)(NV * (nwg + ngroups) * 16));
+  const int goff = NV * nwg;
+  int bad = 0;
+  if (threadIdx.x == 0) {
+#pragma unroll
+    for (int j = 0; j < NV; ++j)
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, make_double2(v[j], tag)), rg,
+                                             (j * nwg + lb) * 16, 0, 16);
+  }
+  if (threadIdx.x < 64) {
+    const int lane = threadIdx.x;
+    if (lb == g0) {  // the group's first workgroup sums the group's granules
+#pragma unroll
+      for (int j = 0; j < NV; ++j) {
+        double w = lane < gn ? gran_poll(rg, (j * nwg + g0 + lane) * 16, tag, &bad).x : 0.0;
+        w = wave_sum(w);
+        if (lane == 0)
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, make_double2(w, tag)), rg,
+                                                 (goff + j * ngroups + grp) * 16, 0, 16);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < NV; ++j) {
+      const double gv = lane < ngroups ? gran_poll(rg, (goff + j * ngroups + lane) * 16, tag, &bad).x : 0.0;
+      if (lane < ngroups) s_g[j * 64 + lane] = gv;
+    }
+    if (bad) s_flag[0] = 1;
+  }
+  __syncthreads();
+  double acc[NV];
+#pragma unroll
+  for (int j = 0; j < NV; ++j) {
+    acc[j] = 0.0;
+    if ((int)threadIdx.x < ngroups) acc[j] = acc[j] + s_g[j * 64 + threadIdx.x];
+  }
+  block_sum<NV>(acc, s_red);
+  if (threadIdx.x == 0) {
+#pragma unroll
+    for (int j = 0; j < NV; ++j) s_red[16 + j] = acc[j];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < NV; ++j) tot[j] = s_red[16 + j];
+  return s_flag[0] == 0;
+}
+
+constexpr int kPmAux = 16;  // sc1: write-through stores, L1-bypassing loads
+
+// the iteration loop of k_cg_pmarch for one walk direction of the P walk
+// (the B walk runs the other way): one direction per instantiation keeps
+// the loop's live state to one walk's (both in one loop: 223 VGPRs)
+template <bool UPP>
+__device__ __forceinline__ void pm_loop(const CGArgs& a, const MGeom& g0, bool active, int nsteps, int lb,
+                                        int nwg, const double2* s_dt, const unsigned* s_rpos,
+                                        const unsigned* s_rmap, double* s_w, double* s_red, double* s_g,
+                                        int* s_flag) {
+  CGScalars* S = a.S;
+  const int m = a.T.m;
+  const double bnrm = S->bnrm, tol = S->tol;
+  const int itmax = S->itmax;
+  double bknum = S->bknum, bk = 0.0;
+  double* const gp = a.mgran;
+  double* const gb = a.mgran + 4 * ((size_t)nwg + red_groups(nwg));
+  const int N = a.St.N;
+  for (int k = 1;; ++k) {
+    const double tag = a.mtag + (double)k;
+    const bool first = k == 1;
+    double* __restrict__ pnew = a.pb[k & 1];
+    // P(k): p(k) = bk p(k-1) + r/d, q = A p(k), q.p
+    double acc[2] = {0.0, 0.0};
+    // (the geometry is made opaque per phase so that nothing derived from it
+    // is hoisted out of the iteration loop and held live across both walks)
+    MGeom g = g0;
+    asm volatile("" : "+v"(g.col), "+v"(g.hcol), "+s"(g.r0), "+s"(g.rend));
+    if (active) {
+      const double* __restrict__ psrc = a.pb[(k - 1) & 1];
+      const MBuf B = march_bufs<kMarchP, true>(a, g, psrc, pnew);
+      MRow ring[3];
+#pragma unroll
+      for (int u = 0; u < 3; ++u)
+        if (u < nsteps) march_load<kMarchP, true, 2, kPmAux>(a, g, B, UPP ? g.rend - u : g.r0 - 1 + u, first, psrc, ring[u]);
+      march_walk<kMarchP, 3, UPP, true, 2, kPmAux, kPmAux>(a, g, B, ring, first, bk, 0.0, psrc, pnew, s_dt, s_rpos, s_rmap, s_w, acc);
+    }
+    double t1[1] = {acc[0]}, qp[1];
+    if (!pm_allgather<1>(t1, gp, lb, nwg, tag, qp, s_red, s_g, s_flag)) break;
+    const double ak = bknum / qp[0];
+    // B(k): q = A p(k) rebuilt, r -= ak q, z = r/d, z.r, r.r; x rows
+    acc[0] = acc[1] = 0.0;
+    g = g0;
+    asm volatile("" : "+v"(g.col), "+v"(g.hcol), "+s"(g.r0), "+s"(g.rend));
+    if (active) {
+      const MBuf B = march_bufs<kMarchB, true>(a, g, pnew, pnew);
+      MRow ring[3];
+#pragma unroll
+      for (int u = 0; u < 3; ++u)
+        if (u < nsteps) march_load<kMarchB, true, 2, kPmAux>(a, g, B, !UPP ? g.rend - u : g.r0 - 1 + u, false, pnew, ring[u]);
+      march_walk<kMarchB, 3, !UPP, true, 2, kPmAux, kPmAux>(a, g, B, ring, false, 0.0, ak, pnew, pnew, s_dt, s_rpos, s_rmap, s_w, acc);
+      for (int gr = g.r0; gr < g.rend; ++gr) {  // x += ak p(k) on the band's x rows (own rows only)
+        const int i = gr * m + g.col;
+        if (a.xrows != 0 && i >= a.xrows && i < N - a.xrows) continue;
+        const double2 pv = __builtin_bit_cast(
+            double2, __builtin_amdgcn_raw_buffer_load_b128(B.p, sm_at(a.T, gr, g.col) * 8, 0, kPmAux));
+        double2 xv = *reinterpret_cast<const double2*>(a.x + i);
+        xv.x = xv.x + ak * pv.x;
+        xv.y = xv.y + ak * pv.y;
+        *reinterpret_cast<double2*>(a.x + i) = xv;
+      }
+    }
+    double zr[2];
+    if (!pm_allgather<2>(acc, gb, lb, nwg, tag, zr, s_red, s_g, s_flag)) break;
+    // k_cg_b's epilogue, in every workgroup (the same values everywhere)
+    const double err = sqrt(zr[1]) / bnrm;
+    bk = zr[0] / bknum;
+    const bool stop = !(err > tol) || k >= itmax + 1;
+    if (lb == 0 && threadIdx.x == 0) {
+      S->akden = qp[0];
+      S->ak = ak;
+      S->bk = bk;
+      S->bknum = zr[0];
+      S->err = err;
+      if (k - 1 < a.err_hist_cap) a.err_hist[k - 1] = err;
+      S->iter = k;
+      if (stop) S->done = 1;
+    }
+    bknum = zr[0];
+    if (stop) break;
+  }
+}
+
+__global__ __launch_bounds__(64 * kMarchWaves, 3) void k_cg_pmarch(CGArgs a) {
+  __shared__ double s_red[32];
+  __shared__ double s_g[2 * 64];
+  __shared__ int s_flag[2];
+  __shared__ unsigned s_rpos[kMaxForms], s_rmap[kMaxForms];
+  __shared__ double2 s_dt[kDiagTab];
+  __shared__ double s_win[kMarchWaves][12 * 64];
+  const int m = a.T.m, nrows = a.T.nrows;
+  const int lb = blockIdx.x, nwg = gridDim.x;
+  const int lane = threadIdx.x & 63;
+  const int spr = m / kMarchW;
+  // slot-weighted bands (k_cg_march's mapping, the P kernel's weights for
+  // both walks: the B walk must own the rows its P walk wrote)
+  const int ns = a.wslots, ncu = nwg / ns;
+  const int sl = blockIdx.x / ncu, ib = blockIdx.x - sl * ncu;
+  const int v = __builtin_amdgcn_readfirstlane(ib * kMarchWaves + (threadIdx.x >> 6));
+  const int Q = ncu * kMarchWaves / spr;
+  const int q = v / spr;
+  const int strip = v - q * spr;
+  const int band = q * ns + sl;
+  MGeom g0;
+  {
+    const int c0 = (int)((long long)q * nrows / Q), hc = (int)((long long)(q + 1) * nrows / Q) - c0;
+    const int* wc = a.wcum[0];
+    g0.r0 = c0 + hc * wc[sl] / wc[ns];
+    g0.rend = c0 + hc * wc[sl + 1] / wc[ns];
+  }
+  const bool active = g0.r0 < g0.rend;
+  const int c0 = strip * kMarchW;
+  g0.col = c0 + 2 * lane;
+  g0.hcol = lane == 0 ? c0 - 1 : c0 + kMarchW;
+  g0.hok = lane == 0 || lane == 63;
+  if (g0.hcol < 0 || g0.hcol >= m) {
+    if (a.T.pbc) g0.hcol += g0.hcol < 0 ? m : -m;
+    else g0.hok = false;
+  }
+  const bool upP = a.march_alt && (band & 1);
+  const int nsteps = g0.rend - g0.r0 + 2;
+  if (threadIdx.x < kMaxForms) {
+    s_rpos[threadIdx.x] = a.St.F.rpos[threadIdx.x];
+    s_rmap[threadIdx.x] = a.St.F.rmap[threadIdx.x];
+  }
+  if (threadIdx.x == 0) s_flag[0] = 0;
+  load_dtab(a.St, s_dt);
+  __syncthreads();
+  double* s_w = s_win[threadIdx.x >> 6];
+  if (upP) pm_loop<true>(a, g0, active, nsteps, lb, nwg, s_dt, s_rpos, s_rmap, s_w, s_red, s_g, s_flag);
+  else pm_loop<false>(a, g0, active, nsteps, lb, nwg, s_dt, s_rpos, s_rmap, s_w, s_red, s_g, s_flag);
+  __syncthreads();
+  if (s_flag[0] && threadIdx.x == 0) *a.merr = 1;
 }
 
 // ---------------------------------------------------------------------------
@@ -4831,6 +5040,12 @@ void select_format(perc_ctx* h) {
   if (const char* e = getenv("PERC_MARCH_TAG")) tag = atoi(e) != 0;
   h->march_tag = tag && h->strips && h->qfree && h->march_depth == 3 && h->march_paux == 2 &&
                  h->march_baux == 2 && h->march_bdepth == 3;
+  // persistent march (PERC_MARCH_PERSIST; PERC_MARCH_PERSIST=0/1 overrides):
+  // needs the slot grid (one workgroup per CU and round, all co-resident)
+  bool persist = (h->march_mode & PERC_MARCH_PERSIST) != 0;
+  if (const char* e = getenv("PERC_MARCH_PERSIST")) persist = atoi(e) != 0;
+  h->march_persist = persist && h->march_tag && h->march_slots && !h->march_defer && h->wm_slots == 3 &&
+                     h->wm_grid <= 64 * kGroup && h->march_rows_req == 0;
 }
 
 // strip-major copies of r (into the q buffer: r and q swap roles for the
@@ -5078,6 +5293,48 @@ hipError_t dev_solve_resident(perc_ctx* h, const CGArgs& ca, int* iter, double* 
   return hipSuccess;
 }
 
+// the persistent march (k_cg_pmarch): one cooperative launch per solve on
+// the slot grid; r and the codes are strip-major already (to_strips)
+hipError_t dev_solve_pmarch(perc_ctx* h, CGArgs a, int* iter, double* err) {
+  DeviceBuffers& d = h->d;
+  hipStream_t st = h->stream;
+  int per_cu = 0, cus = 0;
+  HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, h->device));
+  HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_cg_pmarch, 64 * kMarchWaves, 0));
+  if (per_cu < h->wm_slots || cus * h->wm_slots != h->wm_grid) return hipErrorCooperativeLaunchTooLarge;
+  a.wslots = h->wm_slots;
+  for (int i = 0; i <= h->wm_slots; ++i) a.wcum[0][i] = h->wm_cum[0][i];
+  a.mtag = (double)((unsigned long long)h->solve_epoch << 24);
+  a.kiter = 0;
+  KernelTiming& T = h->timing;
+  if (T.enabled) {
+    if (T.ev.size() < 2) T.ev.resize(2, nullptr);
+    for (int i = 0; i < 2; ++i)
+      if (!T.ev[i]) HIP_TRY(hipEventCreate(&T.ev[i]));
+    HIP_TRY(hipEventRecord(T.ev[0], st));
+  }
+  void* args[] = {&a};
+  HIP_TRY(hipLaunchCooperativeKernel((const void*)k_cg_pmarch, dim3(h->wm_grid), dim3(64 * kMarchWaves), args, 0, st));
+  HIP_TRY(dbg_sync(st, "k_cg_pmarch"));
+  if (T.enabled) HIP_TRY(hipEventRecord(T.ev[1], st));
+  CGScalars hs{};
+  HIP_TRY(hipMemcpyAsync(&hs, d.scal, sizeof(hs), hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipStreamSynchronize(st));
+  if (hs.pad[1] != 0) {
+    fprintf(stderr, "[perc] k_cg_pmarch: reduction granule not seen within the poll limit\n");
+    return hipErrorLaunchTimeOut;
+  }
+  if (T.enabled && hs.iter > 0) {
+    float ms = 0.f;
+    HIP_TRY(hipEventElapsedTime(&ms, T.ev[0], T.ev[1]));
+    T.spmv_ms += ms;  // whole iterations: P and B together
+    T.spmv_n += hs.iter;
+  }
+  *iter = hs.iter;
+  *err = hs.err;
+  return hipSuccess;
+}
+
 hipError_t dev_solve(perc_ctx* h, int itol, double tol, int itmax, bool x0_zero, bool full_x,
                      int* iter, double* err) {
   DeviceBuffers& d = h->d;
@@ -5140,7 +5397,7 @@ hipError_t dev_solve(perc_ctx* h, int itol, double tol, int itmax, bool x0_zero,
   if (h->strips) HIP_TRY(to_strips(h, a));
   // tagged-granule reductions of the strip-major q-free march
   if (h->march_tag && a.sm && h->qfree && !h->march_defer) {
-    const int G = red_grid(h);
+    const int G = std::max(red_grid(h), h->wm_grid);
     const size_t need = (size_t)8 * ((size_t)G + red_groups(G));
     if (h->d.mgran_n < need) {
       if (h->d.mgran) HIP_TRY(hipFree(h->d.mgran));
@@ -5152,6 +5409,13 @@ hipError_t dev_solve(perc_ctx* h, int itol, double tol, int itmax, bool x0_zero,
     a.mgran = h->d.mgran;
     a.merr = &d.scal->pad[1];
     ++h->solve_epoch;
+  }
+  if (h->march_persist && a.sm && a.mgran) {
+    const hipError_t e = dev_solve_pmarch(h, a, iter, err);
+    if (e != hipErrorCooperativeLaunchTooLarge && e != hipErrorInvalidConfiguration) return e;
+    (void)hipGetLastError();
+    fprintf(stderr, "[perc] persistent march not launchable (%s): launched kernels\n", hipGetErrorString(e));
+    h->march_persist = 0;
   }
   // row-major q-free march past the Infinity Cache: the P kernel on one
   // round of slot-weighted bands (probe PERC_MARCH_RMSLOTS=1), B on its

@@ -869,7 +869,8 @@ int perc_set_march_rows(perc_ctx* h, int rows) {
 
 int perc_set_march_mode(perc_ctx* h, int mode) {
   if (!h || mode < 0 || mode > (PERC_MARCH_QFREE | PERC_MARCH_ALT | PERC_MARCH_ROWS | PERC_SOLVE_RESIDENT |
-                                 PERC_MARCH_STRIPS | PERC_MARCH_DEFER | PERC_MARCH_SLOTS | PERC_MARCH_TAG))
+                                 PERC_MARCH_STRIPS | PERC_MARCH_DEFER | PERC_MARCH_SLOTS | PERC_MARCH_TAG |
+                                 PERC_MARCH_PERSIST))
     return PERC_EINVAL;
   h->march_mode = mode;
   if (h->assembled) select_format(h);
@@ -885,7 +886,9 @@ int perc_set_bond_weights(perc_ctx* h, const double* w, long long n) {
 int perc_march_info(perc_ctx* h, int* out5) {
   if (!h || !out5) return PERC_EINVAL;
   if (!h->assembled) return PERC_ESTATE;
-  out5[0] = h->small ? 4 : (h->resident && h->stencil ? 3 : (h->rowmarch ? 2 : (h->march ? 1 : 0)));
+  out5[0] = h->small ? 4
+                     : (h->resident && h->stencil ? 3
+                                                  : (h->rowmarch ? 2 : (h->march_persist ? 5 : (h->march ? 1 : 0))));
   out5[1] = (h->qfree ? 1 : 0) | (h->strips ? 2 : 0) | (h->march_defer ? 4 : 0) |
             (h->march_slots || h->march_slots_rm ? 8 : 0) | (h->march_tag ? 16 : 0);
   out5[2] = h->march_alt ? 1 : 0;

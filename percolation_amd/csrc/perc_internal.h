@@ -188,6 +188,7 @@ struct perc_ctx {
   int march_slots = 0;          // q-free strip-major march: slot-weighted bands
   int march_slots_rm = 0;       // q-free row-major march: slot-weighted bands for P
   int march_tag = 0;            // q-free strip-major march: tagged-granule reductions
+  int march_persist = 0;        // q-free strip-major march: one cooperative launch per solve
   unsigned solve_epoch = 0;     // tags of the granule reductions
   int wm_slots = 0;             // slot-weighted bands: workgroup rounds (0: not available)
   int wm_grid = 0;              // their grid (CUs x rounds)

@@ -890,3 +890,42 @@ def test_closed_form_assembly_is_the_general_one(kind, rule, m, n, pbc, monkeypa
     for key in ("val", "diag", "rhs"):
         assert np.array_equal(s0[key].view(np.uint64), s1[key].view(np.uint64)), key
     assert (c0["gtop"], c0["gbot"], c0["iter"]) == (c1["gtop"], c1["gbot"], c1["iter"])
+
+
+@pytest.mark.parametrize("lat,m,n,pbc,p", [(0, 512, 800, 0, 0.6), (1, 1024, 400, 0, 0.42),
+                                           (0, 2048, 300, 1, 0.55), (0, 1024, 1024, 0, 0.55),
+                                           (1, 4096, 120, 1, 0.42)])
+def test_persistent_march_is_bitwise_the_launched_one(lat, m, n, pbc, p):
+    """PERC_MARCH_PERSIST (the whole q-free march loop in one cooperative
+    launch, cross-workgroup rows stored write-through and loaded sc1): with
+    the launched march on the same bands (the B kernel given the P kernel's
+    slot weights) every iterate is the same, so the iteration count, err,
+    Gtop, Gbot and every voltage are bitwise equal, at the reference
+    tolerance and converged (Square/bondc.f:780-836)."""
+    import os
+    nb = api.nbonds(lat, m, n, pbc)
+    order = api.shuffled_ids(nb, 3141)
+    base = PL.MARCH_QFREE | PL.MARCH_ALT | PL.MARCH_STRIPS | PL.MARCH_SLOTS | PL.MARCH_TAG
+    os.environ["PERC_MARCH_SLOTWB"] = "100:75:50"  # the persistent kernel's bands (P's weights)
+    try:
+        with api.Context(lat, m, n, pbc) as ctx:
+            ctx.occupy(PL.BOND, bond_order=order, nbonds_=int(p * nb))
+            if ctx.label()["nspan"] == 0:
+                pytest.skip("no spanning cluster")
+            for tol in (1e-8, 1e-13):
+                out = []
+                for mode in (base, base | PL.MARCH_PERSIST):
+                    ctx.set_march_mode(mode)
+                    for vint in (True, False):
+                        c = ctx.conductance(tol=tol, itmax=10 ** 6, vint=vint)
+                        info = ctx.march_info()
+                        assert info["kernel"] == ("persistent" if mode & PL.MARCH_PERSIST else "wave"), info
+                        out.append(c)
+                for a, b in ((out[0], out[2]), (out[1], out[3])):
+                    assert a["iter"] == b["iter"] and a["err"] == b["err"], (tol, a["iter"], b["iter"])
+                    assert a["gtop"] == b["gtop"] and a["gbot"] == b["gbot"], tol
+                a, b = out[0], out[2]
+                assert np.array_equal(a["vint"].view(np.uint64), b["vint"].view(np.uint64))
+            ctx.set_march_mode(PL.MARCH_DEFAULT)
+    finally:
+        del os.environ["PERC_MARCH_SLOTWB"]
