@@ -3036,7 +3036,8 @@ __global__ __launch_bounds__(64 * kMarchWaves, 3) void k_cg_pmarch(CGArgs a) {
   __shared__ double2 s_dt[kDiagTab];
   __shared__ double s_win[kMarchWaves][12 * 64];
   const int m = a.T.m, nrows = a.T.nrows;
-  const int lb = blockIdx.x, nwg = gridDim.x;
+  // (the reduction index of k_cg_march: the same groups, the same order)
+  const int lb = xcd_logical_block(blockIdx.x, gridDim.x), nwg = gridDim.x;
   const int lane = threadIdx.x & 63;
   const int spr = m / kMarchW;
   // slot-weighted bands (k_cg_march's mapping, the P kernel's weights for
