@@ -4321,8 +4321,16 @@ void klaunch(perc_ctx* h, K kern, dim3 g, dim3 b, hipStream_t st, const CGArgs& 
 // nontemporal last-use loads (the default solve): store policy SAUX
 // (nontemporal 2, plain 0), the deferred reduction
 template <int MODE, int SAUX>
-void launch_march_sm2(perc_ctx* h, hipStream_t st, const CGArgs& a) {
-  const int grid = a.wslots > 0 ? h->wm_grid : h->march_grid;
+void launch_march_sm2(perc_ctx* h, hipStream_t st, const CGArgs& a0) {
+  // strip-major march B on its own band height (march_hb: several rounds
+  // of short bands instead of the slot bands), probe PERC_MARCH_BROWS
+  CGArgs a = a0;
+  int grid = a.wslots > 0 ? h->wm_grid : h->march_grid;
+  if (MODE == kMarchB && h->march_hb > 0) {
+    a.wslots = 0;
+    a.T.bh = h->march_hb;
+    grid = cdiv((h->g.m / kMarchW) * cdiv(h->g.n - 2, h->march_hb), kMarchWaves);
+  }
   if constexpr (SAUX == kNT) {
     if (a.mtrace && !h->march_defer) {  // phase probe (PERC_MARCH_TRACE)
       klaunch(h, k_cg_march<MODE, true, 3, 2, SAUX, false, true>, grid, 64 * kMarchWaves, st, a);
@@ -4372,7 +4380,13 @@ void launch_cg_spmv(perc_ctx* h, const CGArgs& a, int G) {
       else if (h->qfree && a.sm && h->march_depth == 2) klaunch(h, k_cg_march<kMarchP, true, 2>, h->march_grid, 64 * kMarchWaves, st, a);
       else if (h->qfree && a.sm && h->march_paux == 2) launch_march_sm<kMarchP>(h, st, a);
       else if (h->qfree && a.sm) klaunch(h, k_cg_march<kMarchP, true, 3>, h->march_grid, 64 * kMarchWaves, st, a);
-      else if (h->qfree) klaunch(h, k_cg_march<kMarchP>, a.wslots > 0 ? h->wm_grid : h->march_grid, 64 * kMarchWaves, st, a);
+      else if (h->qfree && a.wslots == 0 && h->march_hp > 0) {
+        // row-major q-free P on its own band height (march_hp), B on march_h
+        CGArgs ap = a;
+        ap.T.bh = h->march_hp;
+        klaunch(h, k_cg_march<kMarchP>, cdiv((h->g.m / kMarchW) * cdiv(h->g.n - 2, h->march_hp), kMarchWaves),
+                64 * kMarchWaves, st, ap);
+      } else if (h->qfree) klaunch(h, k_cg_march<kMarchP>, a.wslots > 0 ? h->wm_grid : h->march_grid, 64 * kMarchWaves, st, a);
       else if (a.sm && h->march_depth == 2) klaunch(h, k_cg_march<kMarchPQ, true, 2>, h->march_grid, 64 * kMarchWaves, st, a);
       else if (a.sm && h->march_depth == 4) klaunch(h, k_cg_march<kMarchPQ, true, 4>, h->march_grid, 64 * kMarchWaves, st, a);
       else if (a.sm) klaunch(h, k_cg_march<kMarchPQ, true, 3>, h->march_grid, 64 * kMarchWaves, st, a);
@@ -5036,6 +5050,14 @@ void select_format(perc_ctx* h) {
   bool rms = slots && (size_t)h->N * sizeof(double) > kLargeVector;
   if (const char* e = getenv("PERC_MARCH_RMSLOTS")) rms = atoi(e) != 0;
   h->march_slots_rm = rms && !h->strips && h->qfree && h->wm_slots > 0;
+  // row-major q-free P band height of its own (probe PERC_MARCH_PROWS; the
+  // reduction buffers cover band height 1, march_grid_max)
+  h->march_hb = 0;
+  if (const char* e = getenv("PERC_MARCH_BROWS"))
+    if (h->strips && h->qfree && h->march_rows_req == 0) h->march_hb = std::max(1, atoi(e));
+  h->march_hp = 0;
+  if (const char* e = getenv("PERC_MARCH_PROWS"))
+    if (!h->strips && h->qfree && !h->march_slots_rm && h->march_rows_req == 0) h->march_hp = std::max(1, atoi(e));
   // tagged-granule reductions (PERC_MARCH_TAG; PERC_MARCH_TAG=0/1 overrides)
   bool tag = (h->march_mode & PERC_MARCH_TAG) != 0;
   if (const char* e = getenv("PERC_MARCH_TAG")) tag = atoi(e) != 0;
@@ -5045,7 +5067,7 @@ void select_format(perc_ctx* h) {
   // needs the slot grid (one workgroup per CU and round, all co-resident)
   bool persist = (h->march_mode & PERC_MARCH_PERSIST) != 0;
   if (const char* e = getenv("PERC_MARCH_PERSIST")) persist = atoi(e) != 0;
-  h->march_persist = persist && h->march_tag && h->march_slots && !h->march_defer && h->wm_slots == 3 &&
+  h->march_persist = persist && h->march_tag && h->march_slots && !h->march_defer && h->wm_slots == 3 && h->march_hb == 0 &&
                      h->wm_grid <= 64 * kGroup && h->march_rows_req == 0;
 }
 

@@ -189,6 +189,8 @@ struct perc_ctx {
   int march_slots_rm = 0;       // q-free row-major march: slot-weighted bands for P
   int march_tag = 0;            // q-free strip-major march: tagged-granule reductions
   int march_persist = 0;        // q-free strip-major march: one cooperative launch per solve
+  int march_hp = 0;             // row-major q-free P: own band height (probe; 0: march_h)
+  int march_hb = 0;             // strip-major q-free B: own band height (probe; 0: P's bands)
   unsigned solve_epoch = 0;     // tags of the granule reductions
   int wm_slots = 0;             // slot-weighted bands: workgroup rounds (0: not available)
   int wm_grid = 0;              // their grid (CUs x rounds)
