@@ -11,7 +11,8 @@ import os
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIBPERC = os.path.join(HERE, "libperc.so")
+# (PERC_LIBPERC: a probe build of the same sources, e.g. another tile shape)
+LIBPERC = os.environ.get("PERC_LIBPERC") or os.path.join(HERE, "libperc.so")
 
 PERC_OK = 0
 ERRORS = {

@@ -527,7 +527,10 @@ __global__ void k_occupy_sites(const int* order, int count, int t, uint8_t* socc
 //
 // Path halving (LDS and global): stale reads only cost retries, parents only
 // ever move to smaller ancestors, and only roots are CASed.
-constexpr int kCcW = 128, kCcH = 32, kCcSites = kCcW * kCcH, kCcThreads = 256;
+#ifndef PERC_CC_H
+#define PERC_CC_H 32  // tile height (probe builds: -DPERC_CC_H=64)
+#endif
+constexpr int kCcW = 128, kCcH = PERC_CC_H, kCcSites = kCcW * kCcH, kCcThreads = 256;
 constexpr int kReduceGrid = 1024;  // fixed grid of the counting passes
 
 __device__ __forceinline__ int find_root(int* parent, int x) {
