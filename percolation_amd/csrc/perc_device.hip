@@ -4503,6 +4503,17 @@ StencilForms stencil_forms(const Geom& g) {
 }
 
 // PERC_SYNC_DEBUG=1: synchronise after each launch and name the failing one
+// Kernel-timing events: no system-scope fence when they are recorded (the
+// hipEventDisableSystemFence contract: elapsed times only, read after a
+// stream synchronize).  With the default fence the launches that carry the
+// start / stop events pay an L2 write-back + invalidate the other launches
+// do not, and read ~1 % above rocprofv3's durations of the same kernels
+// (profiles/r3_8_*).  PERC_EVENT_SYSFENCE=1: the default events (A/B).
+hipError_t timing_event_create(hipEvent_t* ev) {
+  static const bool sysfence = getenv("PERC_EVENT_SYSFENCE") && atoi(getenv("PERC_EVENT_SYSFENCE")) != 0;
+  return sysfence ? hipEventCreate(ev) : hipEventCreateWithFlags(ev, hipEventDisableSystemFence);
+}
+
 hipError_t dbg_sync(hipStream_t st, const char* name) {
   static const bool on = getenv("PERC_SYNC_DEBUG") != nullptr;
   if (!on) return hipGetLastError();
@@ -5279,7 +5290,7 @@ hipError_t dev_solve_resident(perc_ctx* h, const CGArgs& ca, int* iter, double* 
   if (T.enabled) {
     if (T.ev.size() < 2) T.ev.resize(2, nullptr);
     for (int i = 0; i < 2; ++i)
-      if (!T.ev[i]) HIP_TRY(hipEventCreate(&T.ev[i]));
+      if (!T.ev[i]) HIP_TRY(timing_event_create(&T.ev[i]));
     HIP_TRY(hipEventRecord(T.ev[0], st));
   }
   HIP_TRY(hipLaunchCooperativeKernel(fn, dim3(a.G), dim3(nt), args, 0, st));
@@ -5336,7 +5347,7 @@ hipError_t dev_solve_pmarch(perc_ctx* h, CGArgs a, int* iter, double* err) {
   if (T.enabled) {
     if (T.ev.size() < 2) T.ev.resize(2, nullptr);
     for (int i = 0; i < 2; ++i)
-      if (!T.ev[i]) HIP_TRY(hipEventCreate(&T.ev[i]));
+      if (!T.ev[i]) HIP_TRY(timing_event_create(&T.ev[i]));
     HIP_TRY(hipEventRecord(T.ev[0], st));
   }
   void* args[] = {&a};
@@ -5464,7 +5475,7 @@ hipError_t dev_solve(perc_ctx* h, int itol, double tol, int itmax, bool x0_zero,
   if (T.enabled && T.ev.size() < kEv * (size_t)kMaxChunk) {
     const size_t have = T.ev.size();
     T.ev.resize(kEv * (size_t)kMaxChunk);
-    for (size_t i = have; i < T.ev.size(); ++i) HIP_TRY(hipEventCreate(&T.ev[i]));
+    for (size_t i = have; i < T.ev.size(); ++i) HIP_TRY(timing_event_create(&T.ev[i]));
   }
   int done_iters = 0;
   // kernel timing samples every kTimeEvery-th iteration of a chunk
