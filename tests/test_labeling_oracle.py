@@ -265,3 +265,24 @@ def test_occupy_random_select_extremes(frac, full, monkeypatch):
             le = ctx.label(canon=True)
         assert np.array_equal(lr["canon"], le["canon"]), tb
         assert lr["nspan"] == le["nspan"] and lr["nclusters"] == le["nclusters"], tb
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("k", [1, 2])
+def test_bench_realisations_partition_vs_oracle(k):
+    """The realisations bench.py times (L = 4096, bond p = 0.6, occupancy
+    drawn on the GPU by perc_occupy_random with the seed tseed(k + 1) of
+    master 58302, bond_cond.f:62-70): the GPU's partition of exactly that
+    occupancy equals the oracle's replay of the same prefix of
+    perc_random_order (Square/bondc.f:194-393), and so do the spanning
+    verdict and root -- the timed workload itself, not a stand-in order."""
+    lat, m, n, pbc = 0, 4096, 4096, 0
+    nb = api.nbonds(lat, m, n, pbc)
+    tb = int(0.6 * nb)
+    seed = int(api.trial_seeds(58302, 1000)[k])
+    with api.Context(lat, m, n, pbc) as ctx:
+        ctx.occupy_random(PL.BOND, 0, tb, seed)
+        li = ctx.label(canon=True)
+    assert li["nspan"] > 0
+    bo = api.random_order(nb, tb, seed, PL.BOND)
+    check(li, *oracle_bond(lat, m, n, pbc, bo, tb))
