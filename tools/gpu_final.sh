@@ -10,11 +10,3 @@ timeout -k 10 400 python -u -m pytest tests/test_config_goldens.py -m gpu -q -s 
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || exit $?
 timeout -k 10 600 python bench.py > gpurun_out/bench.json 2> gpurun_out/bench.log || exit $?
 cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -f csv -d $R/gpurun_out/prof -o run -- python3 $R/bench.py --steps 2 --warmup 1 --no-cpu-baseline > $R/gpurun_out/prof.log 2>&1 || exit $?
-cd $R
-# labeling probe build with 128 x 64 tiles (tools/libperc_h64.so): parity, then timing
-PERC_LIBPERC=$R/tools/libperc_h64.so timeout -k 10 600 python -u -m pytest tests/test_labeling_oracle.py -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/label_h64_test.log 2>&1 || exit $?
-for v in default h64 default h64; do
-  if [ $v = h64 ]; then export PERC_LIBPERC=$R/tools/libperc_h64.so; else unset PERC_LIBPERC; fi
-  echo "== $v" >> gpurun_out/label_ab.log
-  timeout -k 10 120 python tools/label_probe.py --L 4096 --reps 8 >> gpurun_out/label_ab.log 2>&1 || exit $?
-done
