@@ -1114,10 +1114,26 @@ static double dot_tree(int n, const double *u, const double *v) {
   h = n / 2;
   return dot_tree(h, u, v) + dot_tree(n - h, u + h, v + h);
 }
+/* dot_order 3: 4096 contiguous blocks, each summed serially, then the block
+   sums serially -- the shape of a per-thread / per-workgroup partial sum */
+static double dot_block(int n, const double *u, const double *v) {
+  const int nblk = 4096;
+  double s = 0.0;
+  int b;
+  for (b = 0; b < nblk; b++) {
+    const long long i0 = (long long)n * b / nblk, i1 = (long long)n * (b + 1) / nblk;
+    double t = 0.0;
+    long long i;
+    for (i = i0; i < i1; i++) t = t + u[i] * v[i];
+    s = s + t;
+  }
+  return s;
+}
 static double dot_ord(int n, const double *u, const double *v, int desc) {
   double s = 0.0;
   int i;
   if (desc == 2) return dot_tree(n, u, v);
+  if (desc == 3) return dot_block(n, u, v);
   if (desc)
     for (i = n - 1; i >= 0; i--) s = s + u[i] * v[i];
   else

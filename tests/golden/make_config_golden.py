@@ -71,6 +71,10 @@ TOLS = (1e-8, 1e-13, 1e-14)
 TOLS_DECADES = tuple(float(t) for t in os.environ.get(
     "GOLDEN_TOLS", "1e-8,1e-13,1e-14,1e-15,1e-16,1e-17").split(","))
 HIST_EVERY = 256
+# re-associated reference solvers (or_linbcg_sym dot_order): reversed serial sums,
+# pairwise (tree) sums, serial sums of 4096 contiguous blocks then of the block sums
+ASSOC_KEYS = {1: "assoc_desc", 2: "assoc_tree", 3: "assoc_block"}
+ASSOC_FLAGS = {"--assoc": 1, "--assoc-tree": 2, "--assoc-block": 3}
 
 
 def _oracle():
@@ -265,18 +269,26 @@ def assoc(case, order=1):
     path = os.path.join(OUT, case + ".json")
     doc = json.load(open(path))
     assert doc["label"]["canon_sha256"] == info["canon_sha256"], case
-    tols = sorted((float(t) for t in doc["solves"] if float(t) <= 1e-13), reverse=True)
+    # every decade of the fixture, the reference tolerance 1e-8 included (round 4);
+    # GOLDEN_ASSOC_MIN stops the run early (e.g. 1e-8: only the reference tolerance)
+    tmin = float(os.environ.get("GOLDEN_ASSOC_MIN", "0"))
+    tols = sorted((float(t) for t in doc["solves"] if float(t) >= tmin), reverse=True)
     t0 = time.time()
     res, _ = O.conductance_decades(rc["lattice"], L, L, 0, sysin["b1"], sysin["b2"], sysin["gval"],
                                    tols, rhs_rule=sysin["rhs_rule"], cur_rule=sysin["cur_rule"],
                                    cur_thresh=sysin["cur_thresh"],
                                    threads=int(os.environ.get("GOLDEN_THREADS", 2)),
                                    dot_order=order)
-    key = "assoc_desc" if order == 1 else "assoc_tree"
+    key = ASSOC_KEYS[order]
     doc = json.load(open(path))  # re-read: another --assoc run may have written meanwhile
-    doc[key] = {"%g" % r["tol"]: dict(gtop=r["gtop"], gbot=r["gbot"], iter=r["iter"],
-                                     err=r["err"]) for r in res}
-    doc[key + "_seconds"] = time.time() - t0
+    old = doc.get(key, {})
+    new = {"%g" % r["tol"]: dict(gtop=r["gtop"], gbot=r["gbot"], iter=r["iter"],
+                                 err=r["err"]) for r in res}
+    for k, v in new.items():  # the same run again: bitwise the decades already stored
+        if k in old:
+            assert old[k] == v, (case, key, k, old[k], v)
+    doc[key] = dict(sorted(dict(old, **new).items(), key=lambda kv: -float(kv[0])))
+    doc[key + "_seconds"] = max(time.time() - t0, doc.get(key + "_seconds") or 0.0)
     for r in res:
         ref = doc["solves"]["%g" % r["tol"]]
         print("%s %s tol %g: iter %d (asc %d) Gtop %.3e Gbot %.3e rel to asc" % (
@@ -315,8 +327,8 @@ if __name__ == "__main__":
     if args and args[0] == "--decades":
         for c in args[1:] or list(CASES):
             decades(c)
-    elif args and args[0] in ("--assoc", "--assoc-tree"):
+    elif args and args[0] in ASSOC_FLAGS:
         for c in args[1:] or list(CASES):
-            assoc(c, 1 if args[0] == "--assoc" else 2)
+            assoc(c, ASSOC_FLAGS[args[0]])
     else:
         main(args or list(CASES))
