@@ -83,13 +83,14 @@ KERNELS = {"pm": "march kernel (fused p = bk p + r/d, x += ak p, q = A p, q.p)",
            "xp": "k_cg_p (x += ak p, p = bk p + r/d)"}
 
 
-def cpu_baseline(L_, p, order, gpu_iters, cpu_iters):
+def cpu_baseline(L_, p, order, gpu_iters, cpu_iters, tol=1e-8):
     """The oracle (oracle/perc_oracle.c, a serial C restatement of the
     reference path, bit-exact against it) on one host core, on a bounded
     sample of the same workload: union-find labeling + assembly + `cpu_iters`
     linbcg iterations + currents of the first timed L x L realisation (same
     occupation order); the solve is extrapolated to the GPU's iteration
-    count for that realisation."""
+    count for that realisation.  cpu_iters <= 0: the whole solve to `tol`,
+    measured end to end (no extrapolation)."""
     import ctypes as C
 
     import oracle_lib as O
@@ -119,8 +120,12 @@ def cpu_baseline(L_, p, order, gpu_iters, cpu_iters):
     t2 = time.perf_counter()
     vint = O.f64(N)
     it, err = C.c_int(), C.c_double()
-    Or.or_linbcg(sa, ija, N, itemp, vint, 2, -1.0, cpu_iters - 1, C.byref(it), C.byref(err),
-                 None)
+    if cpu_iters > 0:
+        Or.or_linbcg(sa, ija, N, itemp, vint, 2, -1.0, cpu_iters - 1, C.byref(it), C.byref(err),
+                     None)
+    else:
+        Or.or_linbcg(sa, ija, N, itemp, vint, 2, tol, 10 ** 7, C.byref(it), C.byref(err), None)
+        gpu_iters = it.value
     t3 = time.perf_counter()
     gt, gb = C.c_double(), C.c_double()
     Or.or_currents(lat, m, n, 0, nb, b1, b2, gval, diag, vint, 1.0, 1e-10, 0, C.byref(gt),
@@ -128,12 +133,42 @@ def cpu_baseline(L_, p, order, gpu_iters, cpu_iters):
     t4 = time.perf_counter()
     per_iter = (t3 - t2) / it.value
     total = (t1 - t0) + (t2 - t1) + per_iter * gpu_iters + (t4 - t3)
+    how = ("%d linbcg iterations to tol %g (%.3fs/it), measured whole" % (it.value, tol, per_iter)
+           if cpu_iters <= 0 else "%d linbcg iterations (%.3fs/it, extrapolated to the GPU's %d)"
+           % (it.value, per_iter, gpu_iters))
     return dict(value=1.0 / total, unit="solves/s", cores=1, kind="port",
                 sample=("oracle C restatement (perc_oracle.c) on 1 core: union-find labeling "
-                        "%.2fs + assembly %.2fs + %d linbcg iterations (%.3fs/it, extrapolated "
-                        "to the GPU's %d) + currents %.2fs, one L=%d p=%.2f realisation"
-                        % (t1 - t0, t2 - t1, it.value, per_iter, gpu_iters, t4 - t3, L_, p)),
-                sample_seconds=round(t4 - t0, 2), s_per_solve=round(total, 2))
+                        "%.2fs + assembly %.2fs + %s + currents %.2fs, one L=%d p=%.2f realisation"
+                        % (t1 - t0, t2 - t1, how, t4 - t3, L_, p)),
+                sample_seconds=round(t4 - t0, 2), s_per_solve=round(total, 2),
+                measured_seconds=round(t4 - t0, 2), iterations=it.value,
+                extrapolated=cpu_iters > 0, t_label=t1 - t0, t_assemble=t2 - t1,
+                s_per_iter=per_iter, t_currents=t4 - t3, gtop=gt.value)
+
+
+def cpu_anchor_start(L_, p, seed, iters, occupancy):
+    """Start one 1-core oracle process (cpu_worker) in the background, so the
+    CPU anchor runs on its own host core while the GPU realisations run"""
+    import subprocess
+    lat_nb = (2 * L_ * L_ - 2 * L_)
+    env = dict(os.environ, PERC_BENCH_OCCUPANCY=occupancy, OMP_NUM_THREADS="1")
+    return subprocess.Popen([sys.executable, os.path.abspath(__file__), "--cpu-iters", str(iters),
+                             "--cpu-worker", str(L_), str(p), str(int(seed)), "0", str(lat_nb),
+                             str(int(p * lat_nb))],
+                            stdout=subprocess.PIPE, stderr=subprocess.DEVNULL, text=True, env=env)
+
+
+def cpu_anchor_finish(proc, gpu_iters=None):
+    out, _ = proc.communicate()
+    if proc.returncode != 0 or not out.strip():
+        return {"value": None, "error": "cpu anchor process failed (rc %s)" % proc.returncode}
+    r = json.loads(out.strip().splitlines()[-1])
+    if r.get("extrapolated") and gpu_iters:  # the sample's rate, extrapolated to the GPU's count
+        total = r["t_label"] + r["t_assemble"] + r["s_per_iter"] * gpu_iters + r["t_currents"]
+        r["value"], r["s_per_solve"] = 1.0 / total, round(total, 2)
+        r["sample"] = r["sample"].replace("extrapolated to the GPU's 0", "extrapolated to the GPU's %d"
+                                          % gpu_iters)
+    return r
 
 
 def cpu_worker(spec, cpu_iters):
@@ -223,39 +258,32 @@ def labeling_probe(ctx, P, L_, nb, tb, seeds):
 
 def kernel_label(key, minfo):
     """Name + role of a CG kernel, for the march variant that ran."""
-    if key == "pm" and minfo.get("kernel") in ("wave", "rows"):
-        name = "k_cg_rm (workgroup row-march" if minfo["kernel"] == "rows" else \
-            "k_cg_march (per-wave register march"
-        return "%s %d cols x %d rows%s%s): fused p = bk p + r/d, q = A p, q.p%s" % (
-            name, minfo["strip_cols"], minfo["band_rows"], ", alternating" if minfo["alt"] else "",
-            ", strip-major" if minfo.get("strips") else "",
-            "" if minfo["qfree"] else ", q stored")
-    if key == "pmarch":
-        return ("k_cg_pmarch (persistent per-wave register march, 128 cols x ~%d rows, strip-major, "
-                "slot-weighted bands: the P walk, an all-gather of q.p, the B walk, an all-gather of "
-                "z.r and r.r per iteration in one cooperative launch; bytes = 52 B/row + x rows per "
-                "iteration)" % minfo["band_rows"])
+    if key == "pm" and minfo.get("kernel") == "wave":
+        return "k_cg_march (per-wave register march %d cols x %d rows%s%s%s): fused p = bk p + r/d, " \
+            "q = A p, q.p%s" % (
+                minfo["strip_cols"], minfo["band_rows"], ", alternating" if minfo["alt"] else "",
+                ", strip-major" if minfo.get("strips") else "",
+                ", nibble row codes" if minfo.get("nibble") else "",
+                "" if minfo["qfree"] else ", q stored")
     if key == "res":
         return ("k_cg_res (resident persistent solve, %d-row bands: p in LDS, r/q in registers, "
                 "2 grid-wide reductions per iteration; bytes = the streaming-equivalent 52 B/row "
                 "+ x, not HBM traffic)"
                 % minfo["band_rows"])
     if key == "resid" and minfo.get("qfree"):
-        return ("k_cg_rm" if minfo["kernel"] == "rows" else "k_cg_march") + \
-            " B (march: q = A p(k) rebuilt, r -= ak q, z = r/d, z.r and r.r dots)"
+        return "k_cg_march B (march: q = A p(k) rebuilt, r -= ak q, z = r/d, z.r and r.r dots)"
     return KERNELS[key]
 
 
 # rocprof kernel names of the CG kernels, per operator format
 ROCPROF_NAMES = {("res", "stencil"): ("k_cg_res",),  # default kernel of each role first
-                 ("pmarch", "stencil"): ("k_cg_pmarch",),
                  ("res", "stencil_tiled"): ("k_cg_res",),
-                 ("pm", "stencil"): ("k_cg_march<1", "k_cg_march<0", "k_cg_rm<0", "k_cg_rm<1"),
+                 ("pm", "stencil"): ("k_cg_march<1", "k_cg_march<0"),
                  ("ps", "stencil_tiled"): ("k_cg_ps<4>", "k_cg_ps<6>"),
                  ("resid", "stencil_tiled"): ("k_cg_b<true>",),
                  ("spmv", "stencil_split"): ("k_cg_spmv<4>", "k_cg_spmv<6>"),
                  ("resid", "stencil_split"): ("k_cg_b<true>",),
-                 ("resid", "stencil"): ("k_cg_march<2", "k_cg_b<true>", "k_cg_rm<2"),
+                 ("resid", "stencil"): ("k_cg_march<2", "k_cg_b<true>"),
                  ("xp", "stencil_split"): ("k_cg_p<true>",),
                  ("spmv", "stencil"): ("k_cg_spmv<4>", "k_cg_spmv<6>"),
                  ("spmv", "csr"): ("k_cg_spmv<0>",),
@@ -271,8 +299,8 @@ def base_name(k):
 def rocprof_base(key, fmt, minfo):
     """base name (kernel + first template argument, as base_name gives it) of
     the CG kernel of role `key` that the solve ran"""
-    if fmt == "stencil" and minfo.get("kernel") in ("wave", "rows") and key in ("pm", "resid"):
-        k = "k_cg_rm" if minfo["kernel"] == "rows" else "k_cg_march"
+    if fmt == "stencil" and minfo.get("kernel") == "wave" and key in ("pm", "resid"):
+        k = "k_cg_march"
         if key == "pm":
             return "%s<%d" % (k, 1 if minfo.get("qfree") else 0)
         return "%s<2" % k if minfo.get("qfree") else "k_cg_b<true"
@@ -402,7 +430,11 @@ def main():
     ap.add_argument("--master", type=int, default=58302)
     ap.add_argument("--tol", type=float, default=1e-8)
     ap.add_argument("--itmax", type=int, default=10 ** 6)
-    ap.add_argument("--cpu-iters", type=int, default=20)
+    ap.add_argument("--cpu-iters", type=int, default=500,
+                    help="linbcg iterations of the 1-core CPU sample at L (extrapolated to the "
+                         "GPU's count); the whole L=1024 anchor solve runs beside it")
+    ap.add_argument("--cpu-ensemble-iters", type=int, default=20,
+                    help="linbcg iterations of each all-cores ensemble process")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--occupancy", choices=("device", "uniform", "reference"), default="device",
                     help="device: drawn on the GPU inside each realisation (perc_occupy_random, "
@@ -422,7 +454,7 @@ def main():
                     help="realisations in flight per GPU (one context and stream each); the "
                          "per-kernel roofline timings then overlap")
     ap.add_argument("--march-mode", type=int, default=-1,
-                    help="perc_set_march_mode bits (QFREE 1, ALT 2, ROWS 4); -1: library default")
+                    help="perc_set_march_mode bits (perc.h PERC_MARCH_*); -1: library default")
     ap.add_argument("--format", choices=("auto", "stencil", "stencil_tiled", "stencil_split", "csr"),
                     default="auto",
                     help="solver operator format (perc_set_matrix_format)")
@@ -532,6 +564,15 @@ def main():
     torch.cuda.synchronize()
     log("rank %d: %d orders (nb=%d, tbonds=%d) in %.1fs" % (rank, nreal, nb, tb,
                                                             time.perf_counter() - t0))
+    # the CPU baseline runs on two host cores of its own while the GPU
+    # realisations run: the sample at L (same realisation as the first timed
+    # one) and one whole L = 1024 solve as a measured anchor
+    anchors = {}
+    if (rank == 0 and world == 1 and not args.no_cpu_baseline and args.kind == "bond" and lat == 0
+            and args.occupancy in ("uniform", "device")):
+        anchors["sample"] = cpu_anchor_start(L_, p, int(seeds[ii_list[args.warmup]]), args.cpu_iters,
+                                             args.occupancy)
+        anchors["L1024"] = cpu_anchor_start(1024, p, int(seeds[0]), 0, args.occupancy)
     K = max(1, args.concurrent)
 
     def make_ctx():
@@ -680,11 +721,6 @@ def main():
         """(key, stats key, perc_bench_kernel id, bytes) of the CG kernels of
         operator format f"""
         full = args.full_voltages
-        if f == "stencil" and minfo.get("kernel") == "persistent" and not probe:
-            # the whole q-free march loop in one cooperative launch: per
-            # iteration the P walk (26N) and the B walk (26N) plus the x rows,
-            # the same bytes as the two launched kernels
-            return [("pmarch", "spmv", 5, 52 * N + 48 * L_)]
         if f in ("stencil", "stencil_tiled") and minfo.get("kernel") == "resident" and not probe:
             # whole iterations in one persistent launch, r / q / codes held
             # on chip: the bytes are the streaming-equivalent 52 B/row (what
@@ -695,15 +731,18 @@ def main():
             return [("res", "spmv", 5, 52 * N + x_bytes(N, L_, full))]
         if f in ("stencil", "stencil_tiled"):
             qf = f == "stencil" and minfo["qfree"]
-            if f == "stencil" and not qf and minfo.get("kernel") in ("wave", "rows"):
+            if f == "stencil" and not qf and minfo.get("kernel") == "wave":
                 # the march kernels carry no x: the streaming B applies
                 # x += ak p(k) (reads x and p(k), writes x: 24 B per x row)
                 xb = 24 * N if full else 24 * 2 * L_
                 return [("pm", "spmv", 1, 34 * N), ("resid", "resid", 2, resid_bytes(N, f) + xb)]
             if qf and minfo.get("strips"):
-                # strip-major q-free march: x += ak p(k) in the march B
+                # strip-major q-free march: x += ak p(k) in the march B; per
+                # element each kernel reads p, r and the row code and writes
+                # one vector: 24 B + the code (2 B u16, 0.5 B nibble codes)
                 xb = 24 * N if full else 24 * 2 * L_
-                return [("pm", "spmv", 1, 26 * N), ("resid", "resid", 2, resid_bytes(N, f) + xb)]
+                cb = 0.5 if minfo.get("nibble") else 2.0
+                return [("pm", "spmv", 1, int((24 + cb) * N)), ("resid", "resid", 2, int((24 + cb) * N) + xb)]
             return [("pm" if f == "stencil" else "ps", "spmv", 1, ps_bytes(N, L_, full, qf)),
                     ("resid", "resid", 2, resid_bytes(N, f))]
         return [("spmv", "spmv", 1, spmv_bytes(N, nnz, f)), ("resid", "resid", 2, resid_bytes(N, f)),
@@ -857,13 +896,14 @@ def main():
             "note": "host-order boundary: value with one H2D upload of the occupation "
                     "order per realisation (occupy+label host minus device, best of 3)"}
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.kind == "bond" and lat == 0:
-        log("cpu baseline: oracle on a bounded sample ...")
+        log("cpu baseline: waiting for the oracle processes ...")
         try:
-            ho = host_orders[args.warmup]
-            if devocc:  # the same occupancy, as the keys' order (host)
-                ho = np.ascontiguousarray(api.random_order(nb, tb, int(seeds[ii_list[args.warmup]])),
-                                          dtype=np.int32)
-            out["cpu_baseline"] = cpu_baseline(L_, p, ho, results[0]["iter"], args.cpu_iters)
+            if "sample" in anchors:
+                out["cpu_baseline"] = cpu_anchor_finish(anchors["sample"], results[0]["iter"])
+                out["cpu_baseline"]["anchor_L1024"] = cpu_anchor_finish(anchors["L1024"])
+            else:  # reference-order occupancy: the sample in this process
+                ho = host_orders[args.warmup]
+                out["cpu_baseline"] = cpu_baseline(L_, p, ho, results[0]["iter"], args.cpu_iters)
         except Exception as e:  # keep the GPU line even if the host is short of memory
             out["cpu_baseline"] = {"value": None, "error": repr(e)}
         if args.cpu_cores >= 0 and args.occupancy in ("uniform", "device"):
@@ -877,7 +917,8 @@ def main():
             ens_seeds = [int(seeds[(ii_list[args.warmup] + j) % len(seeds)]) for j in range(cores)]
             try:
                 out["cpu_baseline_ensemble"] = cpu_ensemble(L_, p, ens_seeds, iters_mean, nb, tb,
-                                                            args.cpu_iters, cores, args.occupancy)
+                                                            args.cpu_ensemble_iters, cores,
+                                                            args.occupancy)
             except Exception as e:
                 out["cpu_baseline_ensemble"] = {"value": None, "error": repr(e)}
     for c in ctxs:

@@ -332,54 +332,71 @@ void *perc_stream(perc_ctx *h);
 int perc_set_march_rows(perc_ctx *h, int rows);
 
 /* Register-march loop structure (PERC_FMT_STENCIL with m a multiple of
-   128).  PERC_MARCH_QFREE: the P+S kernel does not store q; the B kernel
-   (r -= ak q, z.r, r.r) marches too and rebuilds q = A p(k) from p(k), so
-   an iteration moves 52 instead of 60 bytes per row.  PERC_MARCH_ALT:
-   neighbouring bands walk in opposite directions, so the halo rows they
-   share are read at the same moment (cache hits).  Per-row arithmetic is
-   unchanged in every mode (bitwise the same values); the dot products are
-   summed in a different association.  The mode is read when the system is
-   assembled; default PERC_MARCH_DEFAULT.  PERC_MARCH_STRIPS: for the
-   solve, r, p, q and the row codes are kept strip-major (each 128-column
-   strip of the lattice contiguous, rows of a strip 1 KB apart), so every
-   wave of the per-wave march walks one contiguous stream; x stays
-   row-major.  In the default since round 2: with every memory instruction
-   of the march unconditional (no waitcnt drain per step) the strip-major
-   march runs 0.107 vs 0.115 ms row-major at L = 4096 (same box).  Used
-   while one vector fits the 256 MB Infinity Cache (L <= 4096); larger
-   lattices solve row-major.  PERC_MARCH_QFREE is in the default since
-   late round 2 (strip-major: 0.164 vs 0.178 ms per iteration at L = 4096;
-   row-major at L = 8192: 0.721 vs 0.737 ms).  Row slabs (perc_set_slabs)
-   always run the row-major q-storing march.  PERC_MARCH_DEFER (strip-
-   major q-free march): the dot products of a kernel are summed by every
-   workgroup of the next kernel instead of by a last-arriving workgroup at
-   the end of the kernel (bitwise the same totals, no reduction tail).
-   PERC_MARCH_SLOTS (strip-major q-free march): one workgroup per CU and
-   round, and the bands sized by the round a wave runs in (the first round
-   on a CU streams fastest), so every wave finishes at about the same time;
-   same per-row arithmetic, dot products over other wave partials.
-   PERC_MARCH_TAG (strip-major q-free march): the end-of-kernel reductions
-   publish tagged {value, tag} granules the readers poll for, instead of
-   draining stores before each ticket; bitwise the same totals.
-   PERC_MARCH_PERSIST (strip-major q-free march with slot-weighted bands
-   and tagged granules): the whole iteration loop in one cooperative launch
-   (P walk, all-gather of q.p, B walk over the same bands, all-gather of
-   z.r and r.r), cross-workgroup rows stored write-through; bitwise the
-   same iterates.  Falls back to the launched kernels when the grid cannot
-   be co-resident. */
+   128).  Per-row arithmetic is the same in every mode (bitwise the same
+   values); only the association of the dot products differs.  The mode is
+   read when the system is assembled; default PERC_MARCH_DEFAULT.
+   PERC_MARCH_QFREE: the P+S kernel does not store q; the B kernel (r -= ak
+   q, z.r, r.r) marches too and rebuilds q = A p(k) from p(k), so an
+   iteration moves 52 instead of 60 bytes per row (strip-major at L = 4096:
+   0.164 vs 0.178 ms per iteration; row-major at L = 8192: 0.721 vs 0.737).
+   PERC_MARCH_ALT: neighbouring bands walk in opposite directions, so the
+   halo rows they share are read at the same moment (cache hits).
+   PERC_SOLVE_RESIDENT: the one-workgroup solve of small systems and the
+   resident cooperative solve where they apply.
+   PERC_MARCH_STRIPS (with QFREE): r, p and the row codes strip-major for the
+   solve (each 128-column strip contiguous), so every wave walks one
+   contiguous stream; x stays row-major.  Used while one vector fits the
+   256 MB Infinity Cache (L <= 4096).
+   PERC_MARCH_SLOTS: one workgroup per CU and round, the bands sized by the
+   round a wave runs in (the first round on a CU streams fastest), so every
+   wave finishes at about the same time (past the Infinity Cache: the
+   row-major P kernel's one round of bands).
+   PERC_MARCH_TAG (strip-major march): the end-of-kernel reductions publish
+   tagged {value, tag} granules the readers poll for, instead of draining
+   stores before each ticket; bitwise the same totals.
+   PERC_MARCH_NIBBLE (strip-major march, square lattice): the row codes as
+   one 4-bit slot mask per site (two sites per byte), count and form from
+   the column -- 0.5 instead of 2 bytes of code per element in each kernel
+   (52N -> 49N bytes per iteration); bitwise the same codes (checked per
+   row when packed).
+   Row slabs (perc_set_slabs) and the literal dot order always run the
+   row-major q-storing march.  (Round 4 removed the variants that lost their
+   A/Bs: workgroup row-march 4, deferred reductions 32, persistent march
+   256; those bits are rejected.) */
 #define PERC_MARCH_QFREE 1
 #define PERC_MARCH_ALT 2
-#define PERC_MARCH_ROWS 4
 #define PERC_SOLVE_RESIDENT 8
 #define PERC_MARCH_STRIPS 16
-#define PERC_MARCH_DEFER 32
 #define PERC_MARCH_SLOTS 64
 #define PERC_MARCH_TAG 128
-#define PERC_MARCH_PERSIST 256
+#define PERC_MARCH_NIBBLE 512
 #define PERC_MARCH_DEFAULT                                                                      \
   (PERC_MARCH_QFREE | PERC_MARCH_ALT | PERC_SOLVE_RESIDENT | PERC_MARCH_STRIPS | PERC_MARCH_SLOTS | \
-   PERC_MARCH_TAG)
+   PERC_MARCH_TAG | PERC_MARCH_NIBBLE)
 int perc_set_march_mode(perc_ctx *h, int mode);
+/* Per-round band weights of the slot-weighted bands (PERC_MARCH_SLOTS):
+   which = 0 the strip-major P kernel, 1 its B kernel, 2 the row-major P past
+   the Infinity Cache; n = 0 restores every default (100:75:50, 100:80:60,
+   flat).  A tuning / test knob: the rows stay a partition of the lattice
+   whatever the weights. */
+int perc_set_band_weights(perc_ctx *h, int which, int n, const int *w);
+
+/* Association of linbcg's three dot products (Square/bondc.f:785-787 bknum,
+   :803-805 akden, :872-875 snrm).  PERC_DOT_FAST (default): deterministic
+   wave / workgroup trees inside the fused kernels.  PERC_DOT_LITERAL: each
+   sum folded term after term in ascending j on one wave of the GPU, exactly
+   as the reference loops do -- with every other operation already the
+   reference's, the iterates, iter, err history and voltages are then
+   bitwise the reference solver's.  One dependent fp64 add per term (~4 ns):
+   a verification mode (single slab; runs the q-storing kernels).  The NR
+   drop-in linbcg_ uses PERC_DOT_LITERAL by default (perc_nr_set_dot_order). */
+#define PERC_DOT_FAST 0
+#define PERC_DOT_LITERAL 1
+int perc_set_dot_order(perc_ctx *h, int order);
+/* err of every iteration of the last solve (linbcg's per-iteration
+   `write (*,*) iter, err`, bondc.f:834): min(cap, iterations) values into
+   out; returns the iteration count (>= 0) or a negative status */
+int perc_err_history(perc_ctx *h, double *out, int cap);
 /* Random bond conductances (MATLAB/ConductCalc.m condtype 2, :38-47 and
    :94-97): the bonds of the spanning cluster get G = -g0 * w[id] instead of
    -g0 (w[id] = the MATLAB rand drawn for that bond; the draw order is the
@@ -388,16 +405,14 @@ int perc_set_march_mode(perc_ctx *h, int mode);
    runs the CSR operator (the stencil code encodes two values only). */
 int perc_set_bond_weights(perc_ctx *h, const double *w, long long n);
 /* Solver loop of the assembled system: out5[0] = 0 (no march kernel: LDS
-   tiles, split or CSR), 1 (per-wave march k_cg_march), 2 (workgroup
-   row-march k_cg_rm), 3 (resident persistent solve k_cg_res), 4 (one-
-   workgroup solve of a small system, k_cg_small: N <= 8192 under
-   PERC_FMT_AUTO with PERC_SOLVE_RESIDENT set), 5 (persistent march
-   k_cg_pmarch, PERC_MARCH_PERSIST); out5[1] = bit 0: q-free
-   B, bit 1: strip-major solve layout, bit 2: deferred reductions
-   (PERC_MARCH_DEFER), bit 3: slot-weighted bands (PERC_MARCH_SLOTS; past
-   the Infinity Cache the row-major P kernel's one round of bands);
-   out5[2] = alternating
-   directions, out5[3] = band height, out5[4] = strip width (columns). */
+   tiles, split or CSR), 1 (per-wave march k_cg_march), 3 (resident
+   persistent solve k_cg_res), 4 (one-workgroup solve of a small system,
+   k_cg_small: N <= 8192 under PERC_FMT_AUTO with PERC_SOLVE_RESIDENT set);
+   out5[1] = bit 0: q-free B, bit 1: strip-major solve layout, bit 3:
+   slot-weighted bands (PERC_MARCH_SLOTS; past the Infinity Cache the
+   row-major P kernel's one round of bands), bit 4: tagged-granule
+   reductions, bit 5: nibble row codes (the last solve); out5[2] = alternating directions, out5[3] = band height,
+   out5[4] = strip width (columns). */
 int perc_march_info(perc_ctx *h, int *out5);
 
 /* format the solver kernels use on the assembled system: PERC_FMT_CSR,
@@ -489,6 +504,10 @@ void linbcg_(int *n, double *b, double *x, int *itol, double *tol, int *itmax,
 void perc_nr_bind(double *sa, int *ija, int nmax);
 int perc_nr_status(void);
 int perc_nr_status_(void);  /* F77 spelling: `integer perc_nr_status` */
+/* association of linbcg_'s dot products (PERC_DOT_LITERAL by default: the
+   NR drop-in reproduces the reference solver bitwise; PERC_DOT_FAST: the
+   wave-tree sums of perc_conductance) */
+int perc_nr_set_dot_order(int order);
 
 #ifdef __cplusplus
 }

@@ -25,10 +25,11 @@ BOND, SITE, SITEBOND, BONDSITE = 0, 1, 2, 3
 RULE_BOND, RULE_SITE, RULE_MIXED = 0, 1, 2
 CUR_FORTRAN, CUR_MATLAB = 0, 1
 FMT_AUTO, FMT_CSR, FMT_STENCIL, FMT_STENCIL_SPLIT, FMT_STENCIL_TILED = 0, 1, 2, 3, 4
-MARCH_QFREE, MARCH_ALT, MARCH_ROWS, SOLVE_RESIDENT, MARCH_STRIPS, MARCH_DEFER, MARCH_SLOTS, MARCH_TAG = (
-    1, 2, 4, 8, 16, 32, 64, 128)
-MARCH_PERSIST = 256
-MARCH_DEFAULT = MARCH_QFREE | MARCH_ALT | SOLVE_RESIDENT | MARCH_STRIPS | MARCH_SLOTS | MARCH_TAG
+MARCH_QFREE, MARCH_ALT, SOLVE_RESIDENT, MARCH_STRIPS, MARCH_SLOTS, MARCH_TAG = 1, 2, 8, 16, 64, 128
+MARCH_NIBBLE = 512
+MARCH_DEFAULT = (MARCH_QFREE | MARCH_ALT | SOLVE_RESIDENT | MARCH_STRIPS | MARCH_SLOTS | MARCH_TAG
+                 | MARCH_NIBBLE)
+DOT_FAST, DOT_LITERAL = 0, 1
 
 
 class LabelInfo(C.Structure):
@@ -119,6 +120,9 @@ SIGNATURES = {
     "perc_occupy_random": (C.c_int, [_VP, C.c_int, C.c_int, C.c_int, C.c_ulonglong]),
     "perc_random_order": (C.c_int, [C.c_longlong, C.c_int, C.c_ulonglong, C.c_int, _I]),
     "perc_set_march_mode": (C.c_int, [_VP, C.c_int]),
+    "perc_set_band_weights": (C.c_int, [_VP, C.c_int, C.c_int, _VP]),
+    "perc_set_dot_order": (C.c_int, [_VP, C.c_int]),
+    "perc_err_history": (C.c_int, [_VP, _VP, C.c_int]),
     "perc_march_info": (C.c_int, [_VP, _VP]),
     "perc_set_bond_weights": (C.c_int, [_VP, _VP, C.c_longlong]),
     "perc_selftest_division": (C.c_int, [C.c_longlong, C.c_ulonglong, _VP]),
@@ -133,6 +137,7 @@ SIGNATURES = {
     "perc_nr_bind": (None, [_VP, _VP, C.c_int]),
     "perc_nr_status": (C.c_int, []),
     "perc_nr_status_": (C.c_int, []),
+    "perc_nr_set_dot_order": (C.c_int, [C.c_int]),
     "perc_shuffle_seeded": (None, [C.c_int, C.c_int, _I]),
     "perc_ensemble_create": (C.c_int, [C.c_int, _VP, C.c_int, C.c_int, C.c_int, C.c_int,
                                        C.POINTER(C.c_void_p)]),

@@ -236,8 +236,36 @@ class Context:
         L.check(L.lib().perc_set_march_rows(self.h, int(rows)), "perc_set_march_rows")
 
     def set_march_mode(self, mode):
-        """PERC_MARCH_QFREE | PERC_MARCH_ALT bits of the register-march loop (perc.h)."""
+        """PERC_MARCH_* bits of the register-march loop (perc.h)."""
         L.check(L.lib().perc_set_march_mode(self.h, int(mode)), "perc_set_march_mode")
+
+    def set_band_weights(self, which=None, weights=None):
+        """Per-round weights of the slot-weighted bands (perc_set_band_weights;
+        which 0: strip-major P, 1: its B, 2: row-major P).  No arguments:
+        the defaults."""
+        if which is None:
+            L.check(L.lib().perc_set_band_weights(self.h, 0, 0, None), "perc_set_band_weights")
+            return
+        w = np.ascontiguousarray(weights, dtype=np.int32)
+        L.check(L.lib().perc_set_band_weights(self.h, int(which), len(w), w.ctypes.data),
+                "perc_set_band_weights")
+
+    def set_dot_order(self, order):
+        """PERC_DOT_FAST / PERC_DOT_LITERAL: the association of linbcg's dot
+        products (perc_set_dot_order; LITERAL reproduces the reference solver
+        bitwise)."""
+        L.check(L.lib().perc_set_dot_order(self.h, int(order)), "perc_set_dot_order")
+
+    def err_history(self):
+        """err of every iteration of the last solve (perc_err_history)."""
+        n = L.lib().perc_err_history(self.h, None, 0)
+        if n < 0:
+            L.check(n, "perc_err_history")
+        out = np.zeros(n, dtype=np.float64)
+        m = L.lib().perc_err_history(self.h, out.ctypes.data, n)
+        if m < 0:
+            L.check(m, "perc_err_history")
+        return out
 
     def set_bond_weights(self, w=None):
         """Per-bond conductance multipliers for the spanning cluster's bonds
@@ -253,8 +281,9 @@ class Context:
         """The solver loop of the assembled system (perc_march_info)."""
         out = np.zeros(5, dtype=np.int32)
         L.check(L.lib().perc_march_info(self.h, out.ctypes.data), "perc_march_info")
-        return dict(kernel=("none", "wave", "rows", "resident", "small", "persistent")[out[0]],
-                    qfree=bool(out[1] & 1), strips=bool(out[1] & 2), defer=bool(out[1] & 4), slots=bool(out[1] & 8), tag=bool(out[1] & 16),
+        return dict(kernel=("none", "wave", "", "resident", "small")[out[0]],
+                    qfree=bool(out[1] & 1), strips=bool(out[1] & 2), slots=bool(out[1] & 8), tag=bool(out[1] & 16),
+                    nibble=bool(out[1] & 32),
                     alt=bool(out[2]), band_rows=int(out[3]), strip_cols=int(out[4]))
 
     def matrix_format(self):

@@ -182,46 +182,6 @@ __device__ bool publish_and_reduce(double (&v)[NV], double* partials, unsigned* 
   return true;
 }
 
-// The same totals as publish_and_reduce, formed by EVERY workgroup of the
-// next kernel from the partials the previous kernel's workgroups stored
-// (deferred reduction, k_cg_march<..., DEFER>): the group sums (wave
-// butterflies of kGroup partials) and the strided block sum of the group
-// sums are publish_and_reduce's, term for term, so the totals are bitwise
-// its totals.  The kernel boundary orders the partial stores before these
-// loads.  s_g holds NV * kDeferGroups doubles.
-constexpr int kDeferGroups = 64;  // nwg <= kDeferGroups * kGroup
-template <int NV>
-__device__ void gather_totals(const double* partials, int nwg, double (&tot)[NV], double* s_g,
-                              double* s_red) {
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
-  const int ngroups = red_groups(nwg);
-  for (int grp = wid; grp < ngroups; grp += nw) {
-    const int g0 = grp * kGroup, gn = min(kGroup, nwg - g0);
-#pragma unroll
-    for (int j = 0; j < NV; ++j) {
-      double w = lane < gn ? load_sc1(&partials[(size_t)j * nwg + g0 + lane]) : 0.0;
-      w = wave_sum(w);
-      if (lane == 0) s_g[j * kDeferGroups + grp] = w;
-    }
-  }
-  __syncthreads();
-  double acc[NV];
-#pragma unroll
-  for (int j = 0; j < NV; ++j) acc[j] = 0.0;
-  for (int i = threadIdx.x; i < ngroups; i += blockDim.x) {
-#pragma unroll
-    for (int j = 0; j < NV; ++j) acc[j] = acc[j] + s_g[j * kDeferGroups + i];
-  }
-  block_sum<NV>(acc, s_red);
-  if (threadIdx.x == 0) {
-#pragma unroll
-    for (int j = 0; j < NV; ++j) s_red[16 + j] = acc[j];
-  }
-  __syncthreads();
-#pragma unroll
-  for (int j = 0; j < NV; ++j) tot[j] = s_red[16 + j];
-}
-
 // ---------------------------------------------------------------------------
 // Lattice build
 __global__ void k_forward_count(Geom g, int* fc /* t+2 */) {
@@ -1650,7 +1610,6 @@ __global__ __launch_bounds__(kBlock) void k_spmv_st(StencilView A, const double*
 struct TileGeom {
   int m, nrows, pbc, tpr;  // tpr: tiles per lattice row
   int bh;                  // band height of the register-march kernel
-  int rm_h;                // band height of the workgroup row-march kernel
 };
 
 constexpr int kMaxSlotRounds = 4;
@@ -1691,10 +1650,17 @@ struct CGArgs {
   // walks is sized by the weight of its round, cumulative in wcum[0..wslots]
   int wslots;
   int wcum[2][kMaxSlotRounds + 1];  // [0]: the P kernel, [1]: the march B
-  // tagged-granule reductions of the march (PERC_MARCH_TAG): two slots (P, B)
-  // of granules, the launch's tag, the reader-timeout flag
+  // tagged-granule reductions of the march (PERC_MARCH_TAG): the P and B
+  // granule regions (each sized for the largest grid), the launch's tag,
+  // the reader-timeout flag
   double* mgran;
+  double* mgran_b;
   double mtag;
+  // nibble row codes of the strip-major square-lattice march (PK): slot bits
+  // of two sites per byte; count / form bits of the interior, first and
+  // last columns
+  const uint8_t* nib;
+  unsigned ncls[3];
   int* merr;
 };
 
@@ -2383,6 +2349,7 @@ constexpr int kMarchPQ = 0, kMarchP = 1, kMarchB = 2;
 struct MGeom {
   int r0, rend, col, hcol;
   bool hok;
+  unsigned cb0, cb1, cbh;  // nibble codes (PK): count / form bits of col, col+1, hcol
 };
 
 // Buffer views of the rows one march wave touches, [lo, hi) = its band plus
@@ -2403,7 +2370,7 @@ struct MBuf {
 
 // strip-major solve (SM): whole-array views (vectors < 2 GB there), element
 // offsets through sm_at; row-major: the band's views, offsets from row lo
-template <int MODE, bool SM>
+template <int MODE, bool SM, bool PK = false>
 __device__ __forceinline__ MBuf march_bufs(const CGArgs& a, const MGeom& g, const double* psrc,
                                            double* pnew) {
   const int m = a.T.m;
@@ -2414,7 +2381,7 @@ __device__ __forceinline__ MBuf march_bufs(const CGArgs& a, const MGeom& g, cons
     const unsigned nall = (unsigned)a.T.nrows * (unsigned)m;
     B.p = rsrc(psrc, nall * 8u);
     B.r = rsrc(a.r, nall * 8u);
-    B.c = rsrc(a.St.code, nall * 2u);
+    B.c = PK ? rsrc(a.nib, nall / 2u) : rsrc(a.St.code, nall * 2u);
     B.pn = rsrc(pnew, nall * 8u);
     B.q = rsrc(a.q, MODE == kMarchPQ ? nall * 8u : 0u);
     B.x = rsrc(a.x, 0u);  // the strip-major solve keeps x in B
@@ -2438,13 +2405,7 @@ __device__ __forceinline__ unsigned melem(const CGArgs& a, const MBuf& B, int gr
   return SM ? (unsigned)sm_at(a.T, gr, col) : (unsigned)((gr - B.lo) * a.T.m + col);
 }
 
-// CAUX != 0 (the persistent march): every p / r load carries that cache
-// policy (sc1: rows other workgroups stored write-through in this launch)
-template <int CAUX>
-__device__ __forceinline__ double bld1x(__amdgpu_buffer_rsrc_t r, unsigned off) {
-  return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, (int)off, 0, CAUX));
-}
-template <int MODE, bool SM, int PAUX = 0, int CAUX = 0>
+template <int MODE, bool SM, int PAUX = 0, bool PK = false>
 __device__ __forceinline__ void march_load(const CGArgs& a, const MGeom& g, const MBuf& B, int gr,
                                            bool first, const double* __restrict__ psrc, MRow& R) {
   {
@@ -2455,21 +2416,33 @@ __device__ __forceinline__ void march_load(const CGArgs& a, const MGeom& g, cons
     const bool rown = MODE != kMarchB || (gr >= g.r0 && gr < g.rend);
     const bool hk = rowok && g.hok;
     const unsigned h8 = hk ? eh * 8u : kOOB;
-    R.c = __builtin_amdgcn_raw_buffer_load_b32(B.c, (int)(rowok ? e * 2u : kOOB), 0, 0);
+    if constexpr (PK) {
+      // the pair's two slot nibbles in one byte (element e even); the count
+      // and form bits come from the columns (g.cb0 / cb1): the u16 codes
+      const unsigned b = __builtin_amdgcn_raw_buffer_load_b8(B.c, (int)(rowok ? e / 2u : kOOB), 0, 0);
+      R.c = ((b & 0xFu) | g.cb0) | (((b >> 4) | g.cb1) << 16);
+    } else {
+      R.c = __builtin_amdgcn_raw_buffer_load_b32(B.c, (int)(rowok ? e * 2u : kOOB), 0, 0);
+    }
     // PAUX on the loads that read a value for the last time: P's p(k-1)
     // (dead once p(k) is formed), B's r(k) (overwritten by r(k+1))
-    constexpr int kRAux = CAUX ? CAUX : (MODE == kMarchB ? PAUX : 0);
-    constexpr int kPAux = CAUX ? CAUX : (MODE == kMarchP ? PAUX : 0);
+    constexpr int kRAux = MODE == kMarchB ? PAUX : 0;
+    constexpr int kPAux = MODE == kMarchP ? PAUX : 0;
     R.r = __builtin_bit_cast(double2, __builtin_amdgcn_raw_buffer_load_b128(B.r, (int)(rown ? o8 : kOOB), 0, kRAux));
     R.p = __builtin_bit_cast(double2, __builtin_amdgcn_raw_buffer_load_b128(B.p, (int)(first ? kOOB : o8), 0, kPAux));
     if (MODE != kMarchB) {
-      R.hc = __builtin_amdgcn_raw_buffer_load_b16(B.c, (int)(hk ? eh * 2u : kOOB), 0, 0);
-      R.hr = bld1x<CAUX>(B.r, h8);
+      if constexpr (PK) {
+        const unsigned b = __builtin_amdgcn_raw_buffer_load_b8(B.c, (int)(hk ? eh / 2u : kOOB), 0, 0);
+        R.hc = ((b >> (4u * (eh & 1u))) & 0xFu) | g.cbh;
+      } else {
+        R.hc = __builtin_amdgcn_raw_buffer_load_b16(B.c, (int)(hk ? eh * 2u : kOOB), 0, 0);
+      }
+      R.hr = bld1(B.r, h8);
     } else {
       R.hc = 0u;
       R.hr = 0.0;
     }
-    R.hp = bld1x<CAUX>(B.p, first ? kOOB : h8);
+    R.hp = bld1(B.p, first ? kOOB : h8);
   }
 }
 
@@ -2481,7 +2454,7 @@ struct MState {
 
 // one step: row gr enters the window, then the middle row (gr -+ 1) is
 // finished when it is one of the band's own rows
-template <int MODE, bool UP, bool SM, int SAUX = kNT>
+template <int MODE, bool UP, bool SM>
 __device__ __forceinline__ void march_step(const CGArgs& a, const MGeom& g, const MBuf& B,
                                            const MRow& R, int gr,
                                            bool first, double bk, double ak,
@@ -2523,7 +2496,7 @@ __device__ __forceinline__ void march_step(const CGArgs& a, const MGeom& g, cons
       const bool own = gr >= g.r0 && gr < g.rend;
       const bool pst = (unsigned)(gr - B.lo) < (unsigned)(B.hi - B.lo) &&
                        (own || (a.slab && (gr < 0 || gr >= nrows)));
-      bst2<SAUX>(B.pn, pst ? melem<SM>(a, B, gr, g.col) * 8u : kOOB, pn);
+      bst2<kNT>(B.pn, pst ? melem<SM>(a, B, gr, g.col) * 8u : kOOB, pn);
       if (MODE == kMarchP && !SM) {  // x += ak p(k-1) on the x rows (the P-only march keeps x)
         const int i = gr * m + g.col;
         const bool xw = own && !first && !a.bx && (a.xrows == 0 || i < a.xrows || i >= N - a.xrows);
@@ -2613,11 +2586,11 @@ __device__ __forceinline__ void march_step(const CGArgs& a, const MGeom& g, cons
     const int m = a.T.m;
     const unsigned eq = SM ? (unsigned)sm_at(a.T, mid, g.col) : (unsigned)((mid - g.r0) * m + g.col);
     if (MODE == kMarchPQ) bst2<kNT>(B.q, mown ? eq * 8u : kOOB, mq);
-    if (MODE == kMarchB) bst2<SAUX>(B.r, mown ? melem<SM>(a, B, mid, g.col) * 8u : kOOB, mr);
+    if (MODE == kMarchB) bst2<kNT>(B.r, mown ? melem<SM>(a, B, mid, g.col) * 8u : kOOB, mr);
   }
 }
 
-template <int MODE, int D, bool UP, bool SM, int PAUX = 0, int SAUX = kNT, int CAUX = 0>
+template <int MODE, int D, bool UP, bool SM, int PAUX = 0, bool PK = false>
 __device__ __forceinline__ void march_walk(const CGArgs& a, const MGeom& g, const MBuf& B,
                                            MRow (&ring)[D],
                                            bool first, double bk, double ak,
@@ -2640,39 +2613,24 @@ __device__ __forceinline__ void march_walk(const CGArgs& a, const MGeom& g, cons
       // step count) and the prefetch past its end address rows outside the
       // view (loads return 0, stores are dropped) and finish no row
       const MRow R = ring[u];
-      march_load<MODE, SM, PAUX, CAUX>(a, g, B, UP ? g.rend - (j + D) : g.r0 - 1 + j + D, first, psrc, ring[u]);
-      march_step<MODE, UP, SM, SAUX>(a, g, B, R, UP ? g.rend - j : g.r0 - 1 + j, first, bk, ak, pnew, s_dt,
+      march_load<MODE, SM, PAUX, PK>(a, g, B, UP ? g.rend - (j + D) : g.r0 - 1 + j + D, first, psrc, ring[u]);
+      march_step<MODE, UP, SM>(a, g, B, R, UP ? g.rend - j : g.r0 - 1 + j, first, bk, ak, pnew, s_dt,
                                s_rpos, s_rmap, s_w, W, acc);
     }
   }
 }
 
-// (the P+S kernel and the strip-major q-free P / B with D = 2: at most 128
-// VGPRs, i.e. 4 waves per SIMD)
-template <int MODE, int D, bool SM = false>
-constexpr int kMarchWavesPerEU = D == 2 && (MODE == kMarchPQ || SM) ? 4 : 1;
-
 // PAUX: cache policy of the last-use loads (P: p(k-1); B: r(k)).
-// DEFER (q-free P / B, one round of workgroups): no reduction at the end of
-// the kernel -- each workgroup stores its block partial and exits; every
-// workgroup of the NEXT kernel sums the partials (gather_totals, bitwise
-// publish_and_reduce's totals) while its first rows are in flight.  The
-// scalar epilogues move with them: B(k) forms ak from P(k)'s partials, P(k+1)
-// forms bk, err and the stop decision of iteration k from B(k)'s (workgroup
-// 0 records them in S); bknum of iteration k lives in S->bkn[k & 1] so no
-// kernel overwrites a scalar its own workgroups still read.
 // TR: phase probe -- lane 0 of every wave stores {kernel entry, walk end,
 // exit, hardware id} wall-clock stamps (100 MHz) into a.mtrace[4 w ..]
 // TAG: the epilogue reductions by tagged granules (publish_and_reduce_tagged)
-template <int MODE, bool SM = false, int D = kMarchDepth, int PAUX = 0, int SAUX = kNT,
-          bool DEFER = false, bool TR = false, bool TAG = false>
-__global__ __launch_bounds__(64 * kMarchWaves, (kMarchWavesPerEU<MODE, D, SM>)) void k_cg_march(CGArgs a) {
-  static_assert(!DEFER || MODE != kMarchPQ, "deferred reduction: q-free P / B only");
+template <int MODE, bool SM = false, int D = kMarchDepth, int PAUX = 0, bool TR = false,
+          bool TAG = false, bool PK = false>
+__global__ __launch_bounds__(64 * kMarchWaves) void k_cg_march(CGArgs a) {
   const unsigned long long tr_t0 = TR ? wall_clock64() : 0ull;
   unsigned long long tr_t1 = 0ull;
   CGScalars* S = a.S;
   __shared__ double s_red[32];
-  __shared__ double s_g[DEFER ? 2 * kDeferGroups : 1];
   __shared__ int s_flag[2];
   __shared__ unsigned s_rpos[kMaxForms], s_rmap[kMaxForms];
   __shared__ double2 s_dt[kDiagTab];
@@ -2734,12 +2692,18 @@ __global__ __launch_bounds__(64 * kMarchWaves, (kMarchWavesPerEU<MODE, D, SM>)) 
   }
   const bool up = (a.march_alt && (band & 1)) != (MODE == kMarchB);
   const int nsteps = g.rend - g.r0 + 2;
-  const MBuf B = march_bufs<MODE, SM>(a, g, psrc, pnew);
+  if constexpr (PK) {  // (nibble codes: the square lattice's three column classes)
+    auto cls = [&](int c) { return c == 0 ? a.ncls[1] : (c == m - 1 ? a.ncls[2] : a.ncls[0]); };
+    g.cb0 = cls(g.col);
+    g.cb1 = cls(g.col + 1);
+    g.cbh = cls(g.hcol);
+  }
+  const MBuf B = march_bufs<MODE, SM, PK>(a, g, psrc, pnew);
   MRow ring[D];
   if (active) {
 #pragma unroll
     for (int u = 0; u < D; ++u)
-      if (u < nsteps) march_load<MODE, SM, PAUX>(a, g, B, up ? g.rend - u : g.r0 - 1 + u, first, psrc, ring[u]);
+      if (u < nsteps) march_load<MODE, SM, PAUX, PK>(a, g, B, up ? g.rend - u : g.r0 - 1 + u, first, psrc, ring[u]);
   }
   if (S->done) return;
   if (threadIdx.x < kMaxForms) {
@@ -2748,54 +2712,12 @@ __global__ __launch_bounds__(64 * kMarchWaves, (kMarchWavesPerEU<MODE, D, SM>)) 
   }
   load_dtab(a.St, s_dt);
   __syncthreads();
-  double bk, ak;
-  if constexpr (DEFER) {
-    const bool rec = lb == 0 && threadIdx.x == 0;  // the workgroup that records the scalars
-    if (MODE == kMarchP) {
-      ak = 0.0;  // (x is updated in B)
-      if (k >= 2) {
-        // B(k-1)'s epilogue (k_cg_b / the march B): bk, err, stop of iteration k-1
-        double tot[2];
-        gather_totals<2>(a.partials + a.pstride, gridDim.x, tot, s_g, s_red);
-        const double bkn_prev = S->bkn[(k - 1) & 1];
-        const int kk = k - 1;
-        const double err = sqrt(tot[1]) / S->bnrm;
-        const bool stop = !(err > S->tol) || kk >= S->itmax + 1;
-        bk = tot[0] / bkn_prev;
-        if (rec) {
-          S->bk = bk;
-          S->bknum = tot[0];
-          S->bkn[k & 1] = tot[0];
-          S->err = err;
-          if (kk - 1 < a.err_hist_cap) a.err_hist[kk - 1] = err;
-          S->iter = kk;
-          if (stop) S->done = 1;
-        }
-        if (stop) return;
-      } else {
-        bk = 0.0;
-        if (rec) S->bkn[1] = S->bknum;  // z.r of the prologue (k_cg_init)
-      }
-    } else {
-      // P(k)'s epilogue: ak = bknum / q.p
-      double tot[1];
-      gather_totals<1>(a.partials, gridDim.x, tot, s_g, s_red);
-      bk = 0.0;
-      ak = S->bkn[k & 1] / tot[0];
-      if (rec) {
-        S->akden = tot[0];
-        S->ak = ak;
-      }
-    }
-  } else {
-    bk = S->bk;
-    ak = S->ak;
-  }
+  const double bk = S->bk, ak = S->ak;
   double acc[2] = {0.0, 0.0};
   if (active) {
     double* s_w = s_win[threadIdx.x >> 6];
-    if (up) march_walk<MODE, D, true, SM, PAUX, SAUX>(a, g, B, ring, first, bk, ak, psrc, pnew, s_dt, s_rpos, s_rmap, s_w, acc);
-    else march_walk<MODE, D, false, SM, PAUX, SAUX>(a, g, B, ring, first, bk, ak, psrc, pnew, s_dt, s_rpos, s_rmap, s_w, acc);
+    if (up) march_walk<MODE, D, true, SM, PAUX, PK>(a, g, B, ring, first, bk, ak, psrc, pnew, s_dt, s_rpos, s_rmap, s_w, acc);
+    else march_walk<MODE, D, false, SM, PAUX, PK>(a, g, B, ring, first, bk, ak, psrc, pnew, s_dt, s_rpos, s_rmap, s_w, acc);
     if (MODE == kMarchB && SM) {
       // strip-major q-free solve: x (row-major) += ak p(k) on the band's x
       // rows, after the walk (loads and stores inside it would put a
@@ -2824,22 +2746,6 @@ __global__ __launch_bounds__(64 * kMarchWaves, (kMarchWavesPerEU<MODE, D, SM>)) 
       a.mtrace[4 * (size_t)w + 3] = ((unsigned long long)xcc << 32) | hw;
     }
   }
-  if constexpr (DEFER) {
-    // the block partial only; the next kernel forms the totals
-    if (MODE != kMarchB) {
-      double v[1] = {acc[0]};
-      block_sum<1>(v, s_red);
-      if (threadIdx.x == 0) store_sc1(&a.partials[lb], v[0]);
-    } else {
-      block_sum<2>(acc, s_red);
-      if (threadIdx.x == 0) {
-        double* pt = a.partials + a.pstride;
-        store_sc1(&pt[lb], acc[0]);
-        store_sc1(&pt[(size_t)gridDim.x + lb], acc[1]);
-      }
-    }
-    return;
-  }
   if (MODE != kMarchB) {
     double v[1] = {acc[0]}, tot[1];
     const bool last = TAG ? publish_and_reduce_tagged<1>(v, a.mgran, a.tickets, lb, gridDim.x, a.mtag,
@@ -2858,8 +2764,7 @@ __global__ __launch_bounds__(64 * kMarchWaves, (kMarchWavesPerEU<MODE, D, SM>)) 
   } else {
     double tot[2];
     const bool last =
-        TAG ? publish_and_reduce_tagged<2>(acc, a.mgran + 4 * ((size_t)gridDim.x + red_groups(gridDim.x)),
-                                           a.tickets + a.tstride, lb, gridDim.x, a.mtag, a.merr, tot,
+        TAG ? publish_and_reduce_tagged<2>(acc, a.mgran_b, a.tickets + a.tstride, lb, gridDim.x, a.mtag, a.merr, tot,
                                            s_red, s_flag)
             : publish_and_reduce<2>(acc, a.partials + a.pstride, a.tickets + a.tstride, lb, gridDim.x,
                                     tot, s_red, s_flag);
@@ -2878,556 +2783,6 @@ __global__ __launch_bounds__(64 * kMarchWaves, (kMarchWavesPerEU<MODE, D, SM>)) 
   }
   if constexpr (TR) {
     if (lane == 0) a.mtrace[4 * (size_t)w + 2] = wall_clock64();
-  }
-}
-
-// ---------------------------------------------------------------------------
-// Persistent march (PERC_MARCH_PERSIST): the whole linbcg loop of the
-// strip-major q-free march in ONE cooperative launch -- per iteration the P
-// walk, an all-gather of q.p, the B walk over the same bands, an all-gather
-// of z.r and r.r.  Against two launches per iteration it drops the
-// per-launch dispatch / end-of-kernel time (~5 us of each 78 us launch
-// outside the waves' lifetime, profiles/r3_4_mtrace_summary_L4096.txt) and
-// the last workgroup's ticket tail.  Cross-workgroup data inside the launch
-// (halo rows and columns of p(k) and r(k+1)) is stored write-through (sc1)
-// and every p / r load is an sc1 load; every wave drains its stores before
-// its workgroup publishes (MI355X_MICROARCH.md, hand-off table row 1).
-// Totals: every workgroup sums the same granules in publish_and_reduce's
-// association (group wave butterflies, then the strided block sum), so the
-// iterates are bitwise the launched march's.
-template <int NV>
-__device__ bool pm_allgather(double (&v)[NV], double* gran, int lb, int nwg, double tag,
-                             double (&tot)[NV], double* s_red, double* s_g, int* s_flag) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's row stores are written through
-  block_sum<NV>(v, s_red);                           // (barrier: every wave has drained)
-  const int ngroups = red_groups(nwg);
-  const int grp = lb / kGroup, g0 = grp * kGroup, gn = min(kGroup, nwg - g0);
-  const __amdgpu_buffer_rsrc_t rg = rsrc(gran, (unsigned)(NV * (nwg + ngroups) * 16));
-  const int goff = NV * nwg;
-  int bad = 0;
-  if (threadIdx.x == 0) {
-#pragma unroll
-    for (int j = 0; j < NV; ++j)
-      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, make_double2(v[j], tag)), rg,
-                                             (j * nwg + lb) * 16, 0, 16);
-  }
-  if (threadIdx.x < 64) {
-    const int lane = threadIdx.x;
-    if (lb == g0) {  // the group's first workgroup sums the group's granules
-#pragma unroll
-      for (int j = 0; j < NV; ++j) {
-        double w = lane < gn ? gran_poll(rg, (j * nwg + g0 + lane) * 16, tag, &bad).x : 0.0;
-        w = wave_sum(w);
-        if (lane == 0)
-          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, make_double2(w, tag)), rg,
-                                                 (goff + j * ngroups + grp) * 16, 0, 16);
-      }
-    }
-#pragma unroll
-    for (int j = 0; j < NV; ++j) {
-      const double gv = lane < ngroups ? gran_poll(rg, (goff + j * ngroups + lane) * 16, tag, &bad).x : 0.0;
-      if (lane < ngroups) s_g[j * 64 + lane] = gv;
-    }
-    if (bad) s_flag[0] = 1;
-  }
-  __syncthreads();
-  double acc[NV];
-#pragma unroll
-  for (int j = 0; j < NV; ++j) {
-    acc[j] = 0.0;
-    if ((int)threadIdx.x < ngroups) acc[j] = acc[j] + s_g[j * 64 + threadIdx.x];
-  }
-  block_sum<NV>(acc, s_red);
-  if (threadIdx.x == 0) {
-#pragma unroll
-    for (int j = 0; j < NV; ++j) s_red[16 + j] = acc[j];
-  }
-  __syncthreads();
-#pragma unroll
-  for (int j = 0; j < NV; ++j) tot[j] = s_red[16 + j];
-  return s_flag[0] == 0;
-}
-
-constexpr int kPmAux = 16;  // sc1: write-through stores, L1-bypassing loads
-
-// the iteration loop of k_cg_pmarch for one walk direction of the P walk
-// (the B walk runs the other way): one direction per instantiation keeps
-// the loop's live state to one walk's (both in one loop: 223 VGPRs)
-template <bool UPP>
-__device__ __forceinline__ void pm_loop(const CGArgs& a, const MGeom& g0, bool active, int nsteps, int lb,
-                                        int nwg, const double2* s_dt, const unsigned* s_rpos,
-                                        const unsigned* s_rmap, double* s_w, double* s_red, double* s_g,
-                                        int* s_flag) {
-  CGScalars* S = a.S;
-  const int m = a.T.m;
-  const double bnrm = S->bnrm, tol = S->tol;
-  const int itmax = S->itmax;
-  double bknum = S->bknum, bk = 0.0;
-  double* const gp = a.mgran;
-  double* const gb = a.mgran + 4 * ((size_t)nwg + red_groups(nwg));
-  const int N = a.St.N;
-  for (int k = 1;; ++k) {
-    const double tag = a.mtag + (double)k;
-    const bool first = k == 1;
-    double* __restrict__ pnew = a.pb[k & 1];
-    // P(k): p(k) = bk p(k-1) + r/d, q = A p(k), q.p
-    double acc[2] = {0.0, 0.0};
-    // (the geometry is made opaque per phase so that nothing derived from it
-    // is hoisted out of the iteration loop and held live across both walks)
-    MGeom g = g0;
-    asm volatile("" : "+v"(g.col), "+v"(g.hcol), "+s"(g.r0), "+s"(g.rend));
-    if (active) {
-      const double* __restrict__ psrc = a.pb[(k - 1) & 1];
-      const MBuf B = march_bufs<kMarchP, true>(a, g, psrc, pnew);
-      MRow ring[3];
-#pragma unroll
-      for (int u = 0; u < 3; ++u)
-        if (u < nsteps) march_load<kMarchP, true, 2, kPmAux>(a, g, B, UPP ? g.rend - u : g.r0 - 1 + u, first, psrc, ring[u]);
-      march_walk<kMarchP, 3, UPP, true, 2, kPmAux, kPmAux>(a, g, B, ring, first, bk, 0.0, psrc, pnew, s_dt, s_rpos, s_rmap, s_w, acc);
-    }
-    double t1[1] = {acc[0]}, qp[1];
-    if (!pm_allgather<1>(t1, gp, lb, nwg, tag, qp, s_red, s_g, s_flag)) break;
-    const double ak = bknum / qp[0];
-    // B(k): q = A p(k) rebuilt, r -= ak q, z = r/d, z.r, r.r; x rows
-    acc[0] = acc[1] = 0.0;
-    g = g0;
-    asm volatile("" : "+v"(g.col), "+v"(g.hcol), "+s"(g.r0), "+s"(g.rend));
-    if (active) {
-      const MBuf B = march_bufs<kMarchB, true>(a, g, pnew, pnew);
-      MRow ring[3];
-#pragma unroll
-      for (int u = 0; u < 3; ++u)
-        if (u < nsteps) march_load<kMarchB, true, 2, kPmAux>(a, g, B, !UPP ? g.rend - u : g.r0 - 1 + u, false, pnew, ring[u]);
-      march_walk<kMarchB, 3, !UPP, true, 2, kPmAux, kPmAux>(a, g, B, ring, false, 0.0, ak, pnew, pnew, s_dt, s_rpos, s_rmap, s_w, acc);
-      for (int gr = g.r0; gr < g.rend; ++gr) {  // x += ak p(k) on the band's x rows (own rows only)
-        const int i = gr * m + g.col;
-        if (a.xrows != 0 && i >= a.xrows && i < N - a.xrows) continue;
-        const double2 pv = __builtin_bit_cast(
-            double2, __builtin_amdgcn_raw_buffer_load_b128(B.p, sm_at(a.T, gr, g.col) * 8, 0, kPmAux));
-        double2 xv = *reinterpret_cast<const double2*>(a.x + i);
-        xv.x = xv.x + ak * pv.x;
-        xv.y = xv.y + ak * pv.y;
-        *reinterpret_cast<double2*>(a.x + i) = xv;
-      }
-    }
-    double zr[2];
-    if (!pm_allgather<2>(acc, gb, lb, nwg, tag, zr, s_red, s_g, s_flag)) break;
-    // k_cg_b's epilogue, in every workgroup (the same values everywhere)
-    const double err = sqrt(zr[1]) / bnrm;
-    bk = zr[0] / bknum;
-    const bool stop = !(err > tol) || k >= itmax + 1;
-    if (lb == 0 && threadIdx.x == 0) {
-      S->akden = qp[0];
-      S->ak = ak;
-      S->bk = bk;
-      S->bknum = zr[0];
-      S->err = err;
-      if (k - 1 < a.err_hist_cap) a.err_hist[k - 1] = err;
-      S->iter = k;
-      if (stop) S->done = 1;
-    }
-    bknum = zr[0];
-    if (stop) break;
-  }
-}
-
-__global__ __launch_bounds__(64 * kMarchWaves, 3) void k_cg_pmarch(CGArgs a) {
-  __shared__ double s_red[32];
-  __shared__ double s_g[2 * 64];
-  __shared__ int s_flag[2];
-  __shared__ unsigned s_rpos[kMaxForms], s_rmap[kMaxForms];
-  __shared__ double2 s_dt[kDiagTab];
-  __shared__ double s_win[kMarchWaves][12 * 64];
-  const int m = a.T.m, nrows = a.T.nrows;
-  // (the reduction index of k_cg_march: the same groups, the same order)
-  const int lb = xcd_logical_block(blockIdx.x, gridDim.x), nwg = gridDim.x;
-  const int lane = threadIdx.x & 63;
-  const int spr = m / kMarchW;
-  // slot-weighted bands (k_cg_march's mapping, the P kernel's weights for
-  // both walks: the B walk must own the rows its P walk wrote)
-  const int ns = a.wslots, ncu = nwg / ns;
-  const int sl = blockIdx.x / ncu, ib = blockIdx.x - sl * ncu;
-  const int v = __builtin_amdgcn_readfirstlane(ib * kMarchWaves + (threadIdx.x >> 6));
-  const int Q = ncu * kMarchWaves / spr;
-  const int q = v / spr;
-  const int strip = v - q * spr;
-  const int band = q * ns + sl;
-  MGeom g0;
-  {
-    const int c0 = (int)((long long)q * nrows / Q), hc = (int)((long long)(q + 1) * nrows / Q) - c0;
-    const int* wc = a.wcum[0];
-    g0.r0 = c0 + hc * wc[sl] / wc[ns];
-    g0.rend = c0 + hc * wc[sl + 1] / wc[ns];
-  }
-  const bool active = g0.r0 < g0.rend;
-  const int c0 = strip * kMarchW;
-  g0.col = c0 + 2 * lane;
-  g0.hcol = lane == 0 ? c0 - 1 : c0 + kMarchW;
-  g0.hok = lane == 0 || lane == 63;
-  if (g0.hcol < 0 || g0.hcol >= m) {
-    if (a.T.pbc) g0.hcol += g0.hcol < 0 ? m : -m;
-    else g0.hok = false;
-  }
-  const bool upP = a.march_alt && (band & 1);
-  const int nsteps = g0.rend - g0.r0 + 2;
-  if (threadIdx.x < kMaxForms) {
-    s_rpos[threadIdx.x] = a.St.F.rpos[threadIdx.x];
-    s_rmap[threadIdx.x] = a.St.F.rmap[threadIdx.x];
-  }
-  if (threadIdx.x == 0) s_flag[0] = 0;
-  load_dtab(a.St, s_dt);
-  __syncthreads();
-  double* s_w = s_win[threadIdx.x >> 6];
-  if (upP) pm_loop<true>(a, g0, active, nsteps, lb, nwg, s_dt, s_rpos, s_rmap, s_w, s_red, s_g, s_flag);
-  else pm_loop<false>(a, g0, active, nsteps, lb, nwg, s_dt, s_rpos, s_rmap, s_w, s_red, s_g, s_flag);
-  __syncthreads();
-  if (s_flag[0] && threadIdx.x == 0) *a.merr = 1;
-}
-
-// ---------------------------------------------------------------------------
-// Workgroup row-march (stencil operator, m a multiple of W).  A workgroup of
-// W/4 threads owns a strip of W columns (thread t: column pairs 2t and
-// 2t + W/2, so each wave instruction moves 1 KB contiguous) and walks an
-// H-row band, one lattice row per step.  Each step forms the row's p(k)
-// into a 4-slot LDS ring (plus the strip's two halo columns), one barrier,
-// then sums q of the previous row from the ring in slot order.  Against
-// the per-wave march (k_cg_march) a step moves a whole 16 KB row segment
-// per stream for the workgroup, which streams ~14 % faster on the pure
-// access pattern (tools/mix_bench.hip: 0.0887 vs 0.1035 ms).  Modes,
-// directions and per-row arithmetic are k_cg_march's.
-constexpr int kRmSlots = 4;
-constexpr int kRmMinGroups = 512;
-
-struct RRow {       // one prefetched row of the thread's two pairs (+ halo)
-  double2 pa, pb, ra, rb;
-  unsigned ca, cb;
-  double hp, hr;
-  unsigned hc;
-};
-
-// Workgroup barrier for LDS traffic only: the workgroup's own ds_writes are
-// complete (lgkmcnt(0)), then s_barrier.  __syncthreads() is a release
-// fence for global memory too, i.e. s_waitcnt vmcnt(0) before the barrier:
-// in the row-march that drained every prefetched row and every store in
-// flight once per step.  The asm's "memory" clobber keeps the compiler from
-// moving memory accesses across it.
-__device__ __forceinline__ void lds_barrier() {
-  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-}
-
-// q of one element from the ring in slot order (every form, wrapped ones too)
-__device__ __forceinline__ double rm_q(unsigned c, double d, double xi, unsigned rpos,
-                                       const double* sU, const double* sC, const double* sD,
-                                       int lc, double ng0, double nleak) {
-  double acc = d * xi;
-  const int cnt = (c >> 8) & 7;
-#pragma unroll
-  for (int j = 0; j < kMaxSlots; ++j) {
-    if (j < cnt) {
-      const int kp = (rpos >> (3 * j)) & 7;
-      const double* row = kp < 3 ? sU : (kp < 5 ? sC : sD);
-      const int dc = kp < 3 ? kp - 1 : (kp == 3 ? -1 : (kp == 4 ? 1 : kp - 6));
-      const double gv = ((c >> j) & 1u) ? ng0 : nleak;
-      acc = acc + gv * row[lc + dc];
-    }
-  }
-  return acc;
-}
-
-// rm_q for a wave whose elements all share one regular form (slot order =
-// raster order, used positions `mask`): wave-uniform branches, fixed offsets
-__device__ __forceinline__ double rm_q_uni(unsigned c, double d, double xi, unsigned mask,
-                                           const double* sU, const double* sC, const double* sD,
-                                           int lc, double ng0, double nleak) {
-  double acc = d * xi;
-  int j = 0;
-#pragma unroll
-  for (int kp = 0; kp < 8; ++kp) {
-    if (mask & (1u << kp)) {
-      const double* row = kp < 3 ? sU : (kp < 5 ? sC : sD);
-      const int dc = kp < 3 ? kp - 1 : (kp == 3 ? -1 : (kp == 4 ? 1 : kp - 6));
-      const double gv = ((c >> j) & 1u) ? ng0 : nleak;
-      acc = acc + gv * row[lc + dc];
-      ++j;
-    }
-  }
-  return acc;
-}
-
-template <int MODE, int W, int D, bool XB>
-__device__ __forceinline__ void rm_walk(const CGArgs& a, RRow (&ring)[D], int t, int r0, int rend,
-                                        bool up, int cA, int hcol, bool hok, bool first,
-                                        double bk, double ak, const double2* s_dt,
-                                        const unsigned* s_rpos, double* s_ring,
-                                        double (&acc)[2]);
-
-template <int MODE, int W, int D = 2>
-__global__ __launch_bounds__(W / 4) void k_cg_rm(CGArgs a) {
-  constexpr int T = W / 4, SL = W + 4;  // slot: [1] left halo, [2 + c], [W + 2] right halo
-  CGScalars* S = a.S;
-  __shared__ __attribute__((aligned(16))) double s_ring[kRmSlots * SL];
-  __shared__ double2 s_dt[kDiagTab];
-  __shared__ unsigned s_rpos[kMaxForms];
-  __shared__ double s_red[32];
-  __shared__ int s_flag[2];
-  const int t = threadIdx.x;
-  const int k = a.kiter;
-  const bool first = MODE != kMarchB && k == 1;
-  const int m = a.T.m, nrows = a.T.nrows, H = a.T.rm_h, N = a.St.N;
-  const int lb = xcd_logical_block(blockIdx.x, gridDim.x);
-  const int spr = m / W;
-  const int band = lb / spr, strip = lb - band * spr;
-  const int r0 = band * H, rend = min(r0 + H, nrows);
-  const bool active = r0 < nrows;  // workgroup-uniform
-  const int cA = strip * W + 2 * t;
-  int hcol = t == 0 ? strip * W - 1 : strip * W + W;
-  bool hok = t == 0 || t == T - 1;
-  if (hcol < 0 || hcol >= m) {
-    if (a.T.pbc) hcol += hcol < 0 ? m : -m;
-    else hok = false;
-  }
-  const bool up = (a.march_alt && (band & 1)) != (MODE == kMarchB);
-  // bands holding an electrode-adjacent row (or every band, with all
-  // voltages kept) also carry x in their ring
-  // (the q-storing mode always runs with the streaming B, which does x)
-  const bool xb = MODE == kMarchP && !a.bx && (a.xrows == 0 || r0 == 0 || rend == nrows);
-  RRow ring[D];
-  if (S->done) return;
-  if (t < kMaxForms) s_rpos[t] = a.St.F.rpos[t];
-  load_dtab(a.St, s_dt);
-  __syncthreads();
-  const double bk = S->bk, ak = S->ak;
-  double acc[2] = {0.0, 0.0};
-  if (active) {
-    if (xb) rm_walk<MODE, W, D, true>(a, ring, t, r0, rend, up, cA, hcol, hok, first, bk, ak, s_dt,
-                                      s_rpos, s_ring, acc);
-    else rm_walk<MODE, W, D, false>(a, ring, t, r0, rend, up, cA, hcol, hok, first, bk, ak, s_dt,
-                                    s_rpos, s_ring, acc);
-  }
-  (void)N;
-  if (MODE != kMarchB) {
-    double v[1] = {acc[0]}, tot[1];
-    if (publish_and_reduce<1>(v, a.partials, a.tickets, lb, gridDim.x, tot, s_red, s_flag)) {
-      if (threadIdx.x == 0) {
-        S->akden = tot[0];
-        S->ak = S->bknum / tot[0];
-      }
-    }
-  } else {
-    double tot[2];
-    if (publish_and_reduce<2>(acc, a.partials + a.pstride, a.tickets + a.tstride, lb, gridDim.x,
-                              tot, s_red, s_flag)) {
-      if (threadIdx.x == 0) {  // k_cg_b's epilogue
-        const int kk = S->iter + 1;
-        const double err = sqrt(tot[1]) / S->bnrm;
-        S->bk = tot[0] / S->bknum;
-        S->bknum = tot[0];
-        S->err = err;
-        if (kk - 1 < a.err_hist_cap) a.err_hist[kk - 1] = err;
-        S->iter = kk;
-        if (!(err > S->tol) || kk >= S->itmax + 1) S->done = 1;
-      }
-    }
-  }
-}
-
-template <int MODE, int W, int D, bool XB>
-__device__ __forceinline__ void rm_walk(const CGArgs& a, RRow (&ring)[D], int t, int r0, int rend,
-                                        bool up, int cA, int hcol, bool hok, bool first,
-                                        double bk, double ak, const double2* s_dt,
-                                        const unsigned* s_rpos, double* s_ring,
-                                        double (&acc)[2]) {
-  constexpr int T = W / 4, SL = W + 4;
-  const int m = a.T.m, nrows = a.T.nrows, N = a.St.N;
-  const int k = a.kiter;
-  const unsigned vbytes = (unsigned)(N + 2) * 8u;
-  const __amdgpu_buffer_rsrc_t rc = rsrc(a.St.code, (unsigned)N * 2u);
-  const __amdgpu_buffer_rsrc_t rr = rsrc(a.r, vbytes);
-  const __amdgpu_buffer_rsrc_t rp = rsrc(a.pb[(MODE == kMarchB ? k : k - 1) & 1], vbytes);
-  const __amdgpu_buffer_rsrc_t rpn = rsrc(a.pb[k & 1], vbytes);
-  const __amdgpu_buffer_rsrc_t rq = rsrc(a.q, vbytes);
-  const __amdgpu_buffer_rsrc_t rx = rsrc(a.x, vbytes);
-  const double ng0 = a.St.ng0, nleak = a.St.nleak;
-  const int nsteps = rend - r0 + 2;  // rows r0-1 .. rend
-  auto rowof = [&](int j) { return up ? rend - j : r0 - 1 + j; };
-  auto xrow = [&](int gr) {  // x kept on this row (XB bands only)
-    const int i = gr * m;
-    return a.xrows == 0 || i < a.xrows || i >= N - a.xrows;
-  };
-  // x of the thread's two pairs rides in the ring's p slots' neighbours:
-  // XB bands load it with the row (hp/hr halo slots are separate)
-  double2 ringx[XB ? D : 1][2];
-  auto load = [&](int j, RRow& R, double2 (&X)[2]) {
-    const int gr = rowof(j);
-    const bool ok = j < nsteps && gr >= 0 && gr < nrows;
-    const unsigned ia = (unsigned)(gr * m + cA), ih = (unsigned)(gr * m + hcol);
-    const unsigned o8a = ok ? ia * 8u : kOOB, o8b = ok ? (ia + W / 2) * 8u : kOOB;
-    R.ca = __builtin_amdgcn_raw_buffer_load_b32(rc, (int)(ok ? ia * 2u : kOOB), 0, 0);
-    R.cb = __builtin_amdgcn_raw_buffer_load_b32(rc, (int)(ok ? (ia + W / 2) * 2u : kOOB), 0, 0);
-    const bool rok = MODE != kMarchB || (gr >= r0 && gr < rend);
-    R.ra = bld2(rr, rok ? o8a : kOOB);
-    R.rb = bld2(rr, rok ? o8b : kOOB);
-    R.pa = bld2(rp, first ? kOOB : o8a);
-    R.pb = bld2(rp, first ? kOOB : o8b);
-    const bool hl = ok && hok;
-    R.hp = bld1(rp, hl && !first ? ih * 8u : kOOB);
-    if (MODE != kMarchB) {
-      R.hr = bld1(rr, hl ? ih * 8u : kOOB);
-      R.hc = __builtin_amdgcn_raw_buffer_load_b16(rc, (int)(hl ? ih * 2u : kOOB), 0, 0);
-    } else {
-      R.hr = 0.0;
-      R.hc = 0u;
-    }
-    if (XB) {
-      const bool xo = ok && !first && gr >= r0 && gr < rend && xrow(gr);
-      X[0] = bld2(rx, xo ? o8a : kOOB);
-      X[1] = bld2(rx, xo ? o8b : kOOB);
-    }
-  };
-#pragma unroll
-  for (int u = 0; u < D; ++u) load(u, ring[u], ringx[XB ? u : 0]);
-  // Step j forms row rowof(j) into slot j & 3 and sums q of the row formed
-  // two steps earlier from the rows of steps j-3 .. j-1, which every wave
-  // finished before the previous barrier: the two halves of a step do not
-  // wait for each other, and one barrier per step keeps the 4-slot ring
-  // safe (slot j & 3 was last read in step j-1).  One extra step sums the
-  // band's last row.
-  unsigned c1a = 0u, c1b = 0u, c2a = 0u, c2b = 0u;  // codes of steps j-1, j-2
-  double2 r1a = make_double2(0.0, 0.0), r1b = r1a, r2a = r1a, r2b = r1a;  // r (B)
-  const int nloop = nsteps + 1;
-  for (int j0 = 0; j0 < nloop; j0 += D) {
-#pragma unroll
-    for (int u = 0; u < D; ++u) {
-      const int j = j0 + u;
-      if (j >= nloop) break;  // workgroup-uniform
-      const RRow R = ring[u];
-      double2 X[2] = {make_double2(0.0, 0.0), make_double2(0.0, 0.0)};
-      if (XB) {
-        X[0] = ringx[XB ? u : 0][0];
-        X[1] = ringx[XB ? u : 0][1];
-      }
-      load(j + D, ring[u], ringx[XB ? u : 0]);
-      const int gr = rowof(j);
-      const bool ok = j < nsteps && gr >= 0 && gr < nrows;
-      const bool own = j < nsteps && gr >= r0 && gr < rend;
-      double* sl = s_ring + (j & 3) * SL;
-      double2 pa, pb;
-      double hpn;
-      if (MODE == kMarchB) {
-        pa = R.pa;
-        pb = R.pb;
-        hpn = R.hp;
-      } else {
-        const double za0 = div_tab(R.ra.x, s_dt[diag_idx(R.ca & 0xffffu)]);
-        const double za1 = div_tab(R.ra.y, s_dt[diag_idx(R.ca >> 16)]);
-        const double zb0 = div_tab(R.rb.x, s_dt[diag_idx(R.cb & 0xffffu)]);
-        const double zb1 = div_tab(R.rb.y, s_dt[diag_idx(R.cb >> 16)]);
-        const double zh = div_tab(R.hr, s_dt[diag_idx(R.hc)]);
-        if (first) {
-          pa = make_double2(za0, za1);
-          pb = make_double2(zb0, zb1);
-          hpn = zh;
-        } else {
-          pa.x = bk * R.pa.x + za0;
-          pa.y = bk * R.pa.y + za1;
-          pb.x = bk * R.pb.x + zb0;
-          pb.y = bk * R.pb.y + zb1;
-          hpn = bk * R.hp + zh;
-        }
-        if (!ok) pa = pb = make_double2(0.0, 0.0);
-        if (!(ok && hok)) hpn = 0.0;
-        const unsigned ia = (unsigned)(gr * m + cA);
-        bst2<kNT>(rpn, own ? ia * 8u : kOOB, pa);
-        bst2<kNT>(rpn, own ? (ia + W / 2) * 8u : kOOB, pb);
-        if (XB) {
-          const bool xo = own && !first && xrow(gr);
-          double2 xa = X[0], xb = X[1];
-          xa.x = xa.x + ak * R.pa.x;
-          xa.y = xa.y + ak * R.pa.y;
-          xb.x = xb.x + ak * R.pb.x;
-          xb.y = xb.y + ak * R.pb.y;
-          bst2<0>(rx, xo ? ia * 8u : kOOB, xa);
-          bst2<0>(rx, xo ? (ia + W / 2) * 8u : kOOB, xb);
-        }
-      }
-      *reinterpret_cast<double2*>(sl + 2 + 2 * t) = pa;
-      *reinterpret_cast<double2*>(sl + 2 + 2 * t + W / 2) = pb;
-      if (t == 0) sl[1] = hpn;
-      if (t == T - 1) sl[W + 2] = hpn;
-      const int mid = up ? rend - j + 2 : r0 - 3 + j;
-      const bool qok = j >= 3 && mid >= r0 && mid < rend;  // workgroup-uniform
-      {
-        const double* s1 = s_ring + ((j - 1) & 3) * SL + 2;  // row formed at step j-1
-        const double* sM = s_ring + ((j - 2) & 3) * SL + 2;  // row mid
-        const double* s3 = s_ring + ((j - 3) & 3) * SL + 2;  // row formed at step j-3
-        const double* sU = up ? s1 : s3;                      // row mid - 1
-        const double* sD = up ? s3 : s1;                      // row mid + 1
-        const unsigned cs[4] = {c2a & 0xffffu, c2a >> 16, c2b & 0xffffu, c2b >> 16};
-        double2 dM[4];  // {d, 1/d}
-#pragma unroll
-        for (int e = 0; e < 4; ++e) dM[e] = s_dt[diag_idx(cs[e])];
-        double qv[4], xv[4];
-        const unsigned ff = __builtin_amdgcn_readfirstlane(cs[0] >> 11);
-        const bool uni = !__any((cs[0] >> 11) != ff || (cs[1] >> 11) != ff ||
-                                (cs[2] >> 11) != ff || (cs[3] >> 11) != ff) &&
-                         a.St.F.regular[ff];
-        if (uni) {
-          const unsigned mask = a.St.F.rmask[ff];
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const int lc = 2 * t + (e & 1) + (e >> 1) * (W / 2);
-            xv[e] = sM[lc];
-            qv[e] = rm_q_uni(cs[e], dM[e].x, xv[e], mask, sU, sM, sD, lc, ng0, nleak);
-          }
-        } else {
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const int lc = 2 * t + (e & 1) + (e >> 1) * (W / 2);
-            xv[e] = sM[lc];
-            qv[e] = rm_q(cs[e], dM[e].x, xv[e], s_rpos[cs[e] >> 11], sU, sM, sD, lc, ng0, nleak);
-          }
-        }
-        const unsigned im = (unsigned)(mid * m + cA);
-        const unsigned oqa = qok ? im * 8u : kOOB, oqb = qok ? (im + W / 2) * 8u : kOOB;
-        if (MODE == kMarchB) {
-          const double rv[4] = {r2a.x, r2a.y, r2b.x, r2b.y};
-          double rn[4];
-#pragma unroll
-          for (int e = 0; e < 4; ++e) rn[e] = rv[e] - ak * qv[e];
-          bst2<kNT>(rr, oqa, make_double2(rn[0], rn[1]));
-          bst2<kNT>(rr, oqb, make_double2(rn[2], rn[3]));
-          if (qok) {
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              const double z = div_tab(rn[e], dM[e]);
-              acc[0] = acc[0] + z * rn[e];
-            }
-#pragma unroll
-            for (int e = 0; e < 4; ++e) acc[1] = acc[1] + rn[e] * rn[e];
-          }
-        } else {
-          if (MODE == kMarchPQ) {
-            bst2<kNT>(rq, oqa, make_double2(qv[0], qv[1]));
-            bst2<kNT>(rq, oqb, make_double2(qv[2], qv[3]));
-          }
-          if (qok) {
-#pragma unroll
-            for (int e = 0; e < 4; ++e) acc[0] = acc[0] + qv[e] * xv[e];
-          }
-        }
-      }
-      c2a = c1a;
-      c2b = c1b;
-      c1a = R.ca;
-      c1b = R.cb;
-      if (MODE == kMarchB) {
-        r2a = r1a;
-        r2b = r1b;
-        r1a = R.ra;
-        r1b = R.rb;
-      }
-      lds_barrier();
-    }
   }
 }
 
@@ -3469,15 +2824,10 @@ struct ResArgs {
   double* err_hist;
   int err_hist_cap;
   double* xch;       // [2 parity][G][top, bottom][r, p][m]
-  double* part;      // [2 parity][3][G]
   unsigned* bar;     // 9 counters, 128 B apart (zeroed before the launch)
   double* gran;      // [3][G] 16-B granules {partial, tag} (zeroed before the launch)
-  unsigned long long* trace;  // phase probe (PERC_RES_TRACE): [3 workgroups][kResTrIt][8]
 };
 
-// phase probe of the resident loop: wall clock (100 MHz) at 6 points of
-// each of the first kResTrIt iterations, in workgroups 0, G/2 and G-1
-constexpr int kResTrIt = 256;
 
 // single-level (m = 1024: 0.0166 vs 0.0178 ms per iteration)
 __device__ __forceinline__ bool res_barrier1(const ResArgs& a, unsigned& epoch, int* s_flag) {
@@ -3620,25 +2970,6 @@ __device__ __forceinline__ bool res_gather(const ResArgs& a, unsigned& epoch, do
   return ok;
 }
 
-// every workgroup sums the G partials of one slot in workgroup order
-template <int NV>
-__device__ __forceinline__ void res_total(const ResArgs& a, const double* part, double (&tot)[NV],
-                                          double* s_red) {
-  if (threadIdx.x < 64) {
-    const int lane = threadIdx.x;
-#pragma unroll
-    for (int v = 0; v < NV; ++v) {
-      double acc = 0.0;
-      for (int i = lane; i < a.G; i += 64) acc = acc + load_sc1(&part[(size_t)v * a.G + i]);
-      acc = wave_sum(acc);
-      if (lane == 0) s_red[24 + v] = acc;
-    }
-  }
-  __syncthreads();
-#pragma unroll
-  for (int v = 0; v < NV; ++v) tot[v] = s_red[24 + v];
-  __syncthreads();
-}
 
 // one raster position KP of an element's q (compile-time row / column
 // offsets: the neighbours' rows next to the band come from named registers,
@@ -3709,8 +3040,7 @@ __device__ __forceinline__ void res_pos_u(double& acc, unsigned mask, unsigned& 
 // UMC: compile-time superset of the raster positions the forms use (0x5A:
 // the square lattice's four neighbours), so unused positions and their
 // halo columns take no registers
-template <int MT, int HMAX, bool QREG = true, unsigned UMC = 0xFFu, bool GATHER = false,
-          bool TR = false, int NT = kResThreads>
+template <int MT, int HMAX, bool QREG = true, unsigned UMC = 0xFFu, int NT = kResThreads>
 __global__ __launch_bounds__(NT) void k_cg_res(ResArgs a) {
   __shared__ double s_p[kResLdsRows];
   __shared__ double2 s_dt[kDiagTab];
@@ -3804,20 +3134,13 @@ __global__ __launch_bounds__(NT) void k_cg_res(ResArgs a) {
   int k = 0;
   double err = 0.0;
   bool done = !ok;
-  const int tw = w == 0 ? 0 : (w == G / 2 ? 1 : (w == G - 1 ? 2 : -1));
-  auto stamp = [&](int ph) {
-    if (TR && t == 0 && tw >= 0 && k <= kResTrIt)
-      a.trace[((size_t)tw * kResTrIt + k - 1) * 8 + ph] = wall_clock64();
-  };
   while (!done) {
     // 16 elements per thread: keep the compiler from hoisting every
     // element's addresses out of the loop (they would stay live across it
     // and spill); recomputing them is a few integer ops
     if constexpr (!QREG) asm volatile("" : "+v"(t));
     ++k;
-    stamp(0);
     const int par = k & 1;
-    double* part = a.part + (size_t)par * 3 * G;
     // 1. halo loads first (their latency overlaps the own rows' p(k))
     // (buffer loads with sc1, out-of-range offsets for absent positions: one
     // per-lane offset register for all of them, no branches)
@@ -3876,7 +3199,6 @@ __global__ __launch_bounds__(NT) void k_cg_res(ResArgs a) {
       hd[j] = ResHalo{d3[0], d3[1], d3[2]};
     }
     __syncthreads();
-    stamp(1);
     // q of own element (lr, j) from p(k) in LDS and the halo rows
     auto qcalc = [&](int lr, int j, double xi) {
       const int c = t + j * NT;
@@ -3932,19 +3254,8 @@ __global__ __launch_bounds__(NT) void k_cg_res(ResArgs a) {
     {
       double v1[1] = {dot};
       block_sum<1>(v1, s_red);
-      stamp(2);
       double tot[1];
-      if (GATHER) {
-        if (!(ok = res_gather<1>(a, epoch, a.gran, v1, tot, s_red))) break;
-        stamp(3);
-      } else {
-        if (t == 0) store_sc1(&part[w], v1[0]);
-        // (wave 0 summing the partials right after its own poll, with the
-        // workgroup barriers in between dropped, measured no faster: L =
-        // 1024 16.6 vs 16.4-16.6 us per iteration, L = 2048 35.8 vs 34.7)
-        if (!(ok = res_barrier<MT == 1>(a, epoch, s_flag))) break;
-        res_total<1>(a, part, tot, s_red);
-      }
+      if (!(ok = res_gather<1>(a, epoch, a.gran, v1, tot, s_red))) break;
       ak = bknum / tot[0];
     }
     // 3. r, z, dots, x; the band's first / last rows of r(k+1) and p(k)
@@ -3985,20 +3296,9 @@ __global__ __launch_bounds__(NT) void k_cg_res(ResArgs a) {
         if constexpr (!QREG) __builtin_amdgcn_sched_barrier(0);
       }
     block_sum<2>(acc2, s_red);
-    stamp(4);
     {
       double tot[2];
-      if (GATHER) {
-        if (!(ok = res_gather<2>(a, epoch, a.gran + 2 * (size_t)G, acc2, tot, s_red))) break;
-        stamp(5);
-      } else {
-        if (t == 0) {
-          store_sc1(&part[G + w], acc2[0]);
-          store_sc1(&part[2 * G + w], acc2[1]);
-        }
-        if (!(ok = res_barrier<MT == 1>(a, epoch, s_flag))) break;
-        res_total<2>(a, part + G, tot, s_red);
-      }
+      if (!(ok = res_gather<2>(a, epoch, a.gran + 2 * (size_t)G, acc2, tot, s_red))) break;
       err = sqrt(tot[1]) / bnrm;
       bk = tot[0] / bknum;
       bknum = tot[0];
@@ -4023,6 +3323,121 @@ __global__ __launch_bounds__(NT) void k_cg_res(ResArgs a) {
 }
 
 // ---------------------------------------------------------------------------
+// The literal dot order (perc_set_dot_order(h, PERC_DOT_LITERAL)).  linbcg
+// sums its three dot products term after term in ascending j -- bknum
+// (bondc.f:785-787), akden (:803-805) and snrm's sum of squares (:872-875,
+// also bnrm :768-770) -- and every other operation of an iteration is
+// already the reference's (per-row bitwise, section notes above), so with
+// the sums folded in that order the iterates, iter, err and the voltages
+// are the reference's bitwise.  One wave: lane l forms term j0 + l (one
+// IEEE product, the reference's), then every lane folds the 64 terms in lane
+// order through v_readlane broadcasts (scalar operands of the adds) while
+// the next chunk's loads are in flight.  A serial fold is one dependent
+// fp64 add per term (~4 ns): a verification mode, not the fast path.
+__device__ __forceinline__ double lane_bcast(double v, int l) {
+  const long long b = __double_as_longlong(v);
+  const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)b, l);
+  const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(b >> 32), l);
+  return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+// fold lanes 0 .. cnt-1 of t[c] into acc[c] in lane order (wave-uniform cnt)
+template <int NC>
+__device__ __forceinline__ void fold_chunk(const double (&t)[NC], int cnt, double (&acc)[NC]) {
+  if (cnt == 64) {
+#pragma unroll
+    for (int l = 0; l < 64; ++l)
+#pragma unroll
+      for (int c = 0; c < NC; ++c) acc[c] = acc[c] + lane_bcast(t[c], l);
+  } else {
+    for (int l = 0; l < cnt; ++l)
+#pragma unroll
+      for (int c = 0; c < NC; ++c) acc[c] = acc[c] + lane_bcast(t[c], l);
+  }
+}
+
+// the prologue's sums (k_cg_init wrote r = b - A x): bnrm^2 = sum (b/d)^2
+// (itol 2; sum b^2 for itol 1) and the first bknum = sum (r/d) r
+template <bool ST>
+__global__ __launch_bounds__(64) void k_fold_init(CGArgs a, int itol) {
+  const int N = a.A.N, lane = threadIdx.x;
+  double acc[2] = {0.0, 0.0};
+  auto load = [&](int j0, double& b, double& r, double& d) {
+    const int j = min(j0 + lane, N - 1);
+    b = a.rhs[j];
+    r = a.r[j];
+    d = diag1<ST>(a, j);
+  };
+  double b, r, d;
+  load(0, b, r, d);
+  for (int j0 = 0; j0 < N; j0 += 64) {
+    const double zb = itol == 1 ? b : b / d, z = r / d;
+    const double t[2] = {zb * zb, z * r};
+    double bn, rn, dn;
+    load(j0 + 64 < N ? j0 + 64 : j0, bn, rn, dn);
+    fold_chunk<2>(t, min(64, N - j0), acc);
+    b = bn, r = rn, d = dn;
+  }
+  if (lane == 0) {
+    a.S->bnrm = sqrt(acc[0]);
+    a.S->bknum = acc[1];
+  }
+}
+
+// after S(k): akden = sum q p(k), ak = bknum / akden; bkden keeps bknum
+// (the B epilogue overwrites bknum with its own sum, k_fold_b replaces it)
+__global__ __launch_bounds__(64) void k_fold_qp(CGArgs a) {
+  CGScalars* S = a.S;
+  if (S->done) return;
+  const int N = a.A.N, lane = threadIdx.x;
+  const int k = S->iter + 1;
+  const double* __restrict__ p = a.fused ? a.pb[k & 1] : a.p;
+  double acc[1] = {0.0};
+  double q = a.q[min(lane, N - 1)], pv = p[min(lane, N - 1)];
+  for (int j0 = 0; j0 < N; j0 += 64) {
+    const double t[1] = {q * pv};
+    const int jn = min(j0 + 64 + lane, N - 1);
+    const double qn = a.q[jn], pn = p[jn];
+    fold_chunk<1>(t, min(64, N - j0), acc);
+    q = qn, pv = pn;
+  }
+  if (lane == 0) {
+    S->akden = acc[0];
+    S->ak = S->bknum / acc[0];
+    S->bkden = S->bknum;
+    S->pad[2] = 1;  // this iteration's B is to be folded
+  }
+}
+
+// after B(k): bknum' = sum (r/d) r, err = sqrt(sum r^2) / bnrm, bk, the
+// stop test -- B's epilogue, on the literal sums
+template <bool ST>
+__global__ __launch_bounds__(64) void k_fold_b(CGArgs a) {
+  CGScalars* S = a.S;
+  if (S->pad[2] == 0) return;  // no iteration ran since the last fold
+  const int N = a.A.N, lane = threadIdx.x;
+  double acc[2] = {0.0, 0.0};
+  double r = a.r[min(lane, N - 1)], d = diag1<ST>(a, min(lane, N - 1));
+  for (int j0 = 0; j0 < N; j0 += 64) {
+    const double z = r / d;
+    const double t[2] = {z * r, r * r};
+    const int jn = min(j0 + 64 + lane, N - 1);
+    const double rn = a.r[jn], dn = diag1<ST>(a, jn);
+    fold_chunk<2>(t, min(64, N - j0), acc);
+    r = rn, d = dn;
+  }
+  if (lane == 0) {
+    const int k = S->iter;
+    const double err = sqrt(acc[1]) / S->bnrm;
+    S->bk = acc[0] / S->bkden;
+    S->bknum = acc[0];
+    S->err = err;
+    if (k - 1 < a.err_hist_cap) a.err_hist[k - 1] = err;
+    S->done = !(err > S->tol) || k >= S->itmax + 1 ? 1 : 0;
+    S->pad[2] = 0;
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Small systems (N <= kSmallRows = 8192: lattices up to ~91 x 91, the reference
 // drivers' 10 x 10 .. 50 x 50): the whole linbcg loop in ONE workgroup.
 // Launched kernels spend ~20 us per iteration there on launch gaps and
@@ -4038,8 +3453,9 @@ constexpr int kSmallThreads = 1024, kSmallEPT = 8, kSmallRows = kSmallThreads * 
 
 // ST: the stencil operator (row codes in registers, the forms' offsets in
 // LDS: no global memory access in the loop but the x update); else the CSR
-// operator from global memory
-template <bool ST>
+// operator from global memory.  LIT: the literal dot order (wave 0 folds
+// the terms in ascending j, fold_chunk)
+template <bool ST, bool LIT>
 __global__ __launch_bounds__(kSmallThreads) void k_cg_small(CGArgs a) {
   __shared__ double s_p[kSmallRows], s_q[kSmallRows];
   __shared__ uint16_t s_c[ST ? kSmallRows : 1];
@@ -4125,7 +3541,23 @@ __global__ __launch_bounds__(kSmallThreads) void k_cg_small(CGArgs a) {
       s_q[i] = q;
     }
     double akden, unused;
-    wg_sum(dot, 0.0, &akden, &unused);
+    if constexpr (LIT) {
+      __syncthreads();  // s_q complete
+      if (wid == 0) {
+        double acc[1] = {0.0};
+        for (int j0 = 0; j0 < N; j0 += 64) {
+          const int j = min(j0 + lane, N - 1);
+          const double tq[1] = {s_q[j] * s_p[j]};  // akden, bondc.f:803-805
+          fold_chunk<1>(tq, min(64, N - j0), acc);
+        }
+        if (lane == 0) s_red[32] = acc[0];
+      }
+      __syncthreads();
+      akden = s_red[32];
+      __syncthreads();
+    } else {
+      wg_sum(dot, 0.0, &akden, &unused);
+    }
     ak = bknum / akden;
     // x += ak p, r -= ak q, z = r/d, z.r and r.r (linbcg :801-806, 808-813)
     double zr = 0.0, rr = 0.0;
@@ -4142,7 +3574,38 @@ __global__ __launch_bounds__(kSmallThreads) void k_cg_small(CGArgs a) {
       }
     }
     double tzr, trr;
-    wg_sum(zr, rr, &tzr, &trr);
+    if constexpr (LIT) {
+      // r(k+1) through LDS (q is dead until the next iteration's)
+#pragma unroll
+      for (int j = 0; j < kSmallEPT; ++j) {
+        const int i = t + j * kSmallThreads;
+        if (i < N) s_q[i] = rv[j];
+      }
+      __syncthreads();
+      if (wid == 0) {
+        double acc[2] = {0.0, 0.0};
+        for (int j0 = 0; j0 < N; j0 += 64) {
+          const int j = min(j0 + lane, N - 1);
+          const double rj = s_q[j];
+          double dj;
+          if constexpr (ST) dj = code_diag(s_c[j], ng0, nleak);
+          else dj = a.A.diag[j];
+          const double zj = rj / dj;
+          const double tz[2] = {zj * rj, rj * rj};  // bknum :785-787, snrm :872-875
+          fold_chunk<2>(tz, min(64, N - j0), acc);
+        }
+        if (lane == 0) {
+          s_red[32] = acc[0];
+          s_red[33] = acc[1];
+        }
+      }
+      __syncthreads();
+      tzr = s_red[32];
+      trr = s_red[33];
+      __syncthreads();
+    } else {
+      wg_sum(zr, rr, &tzr, &trr);
+    }
     err = sqrt(trr) / bnrm;
     bk = tzr / bknum;
     bknum = tzr;
@@ -4249,26 +3712,42 @@ __global__ __launch_bounds__(kBlock) void k_to_strips(TileGeom T, const E* __res
   dst[sm_index(T, (int)i)] = src[i];
 }
 
+// the strip-major nibble codes of the square-lattice march (PK): one byte
+// per column pair, the low / high nibble = the two sites' slot bits; every
+// code must be its nibble plus its column class's count / form bits (cls:
+// interior, first, last column), else *bad is set and the solve keeps the
+// u16 codes
+__global__ __launch_bounds__(kBlock) void k_pack_nib(TileGeom T, const uint16_t* __restrict__ code,
+                                                      uint8_t* __restrict__ nib, unsigned c0, unsigned c1,
+                                                      unsigned c2, int* bad) {
+  const long long j = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= (long long)T.nrows * T.m / 2) return;
+  const int i = (int)(2 * j), gr = i / T.m, col = i - gr * T.m;  // m even: col even
+  auto cls = [&](int c) { return c == 0 ? c1 : (c == T.m - 1 ? c2 : c0); };
+  const unsigned a = code[i], b = code[i + 1];
+  if ((a & ~0xFu) != cls(col) || (b & ~0xFu) != cls(col + 1)) atomicOr(bad, 1);
+  nib[sm_at(T, gr, col) / 2] = (uint8_t)((a & 0xFu) | ((b & 0xFu) << 4));
+}
+
 // a vector larger than this does not stay in the 256 MB Infinity Cache
 // between kernels (L = 8192: 537 MB; L = 4096: 134 MB)
 constexpr size_t kLargeVector = (size_t)256 << 20;
-// probe (PERC_MARCH_LARGE=1): vectors past the Infinity Cache also solve
-// strip-major with one round of bands (else row-major, 16-row bands)
-static bool large_strips() {
-  const char* e = getenv("PERC_MARCH_LARGE");
-  return e && atoi(e) != 0;
-}
 
 // workgroups of the largest reduction (CG kernels or the tiled kernel)
 int red_grid(const perc_ctx* h) { return std::max({h->grid, h->tile_grid, h->march_grid_max}); }
+
+// tags of the granule reductions are (solve_epoch << 24) | iteration: at
+// most this many iterations per solve (else the ticket reduction: a tag
+// that wrapped would match granules of an earlier iteration)
+constexpr int kTagMaxIter = (1 << 24) - 2;
+
 
 
 CGArgs make_cg_args(perc_ctx* h) {
   CGArgs a;
   a.A = CsrView{h->N, h->d.rowptr, h->d.col, h->d.val, h->d.diag};
   a.St = StencilView{h->N, h->d.code, h->st_ng0, h->st_nleak, h->forms, h->d.dtab};
-  a.T = TileGeom{h->g.m, h->g.n - 2, h->g.pbc, (h->g.m + kTileW - 1) / kTileW, h->march_h,
-                 h->rm_h};
+  a.T = TileGeom{h->g.m, h->g.n - 2, h->g.pbc, (h->g.m + kTileW - 1) / kTileW, h->march_h};
   a.pb[0] = h->d.p0;
   a.pb[1] = h->d.p1;
   a.fused = h->fused ? 1 : 0;
@@ -4279,7 +3758,7 @@ CGArgs make_cg_args(perc_ctx* h) {
   a.b_reverse = h->fused ? 1 : 0;
   a.kiter = 1;
   a.march_alt = h->march_alt ? 1 : 0;
-  a.bx = (h->march || h->rowmarch) && !h->qfree ? 1 : 0;
+  a.bx = h->march && !h->qfree ? 1 : 0;
   a.sm = 0;  // dev_solve / dev_bench switch to the strip-major copies
   a.glo = 0;
   a.ghi = h->g.n - 2;
@@ -4301,8 +3780,10 @@ CGArgs make_cg_args(perc_ctx* h) {
   a.mtrace = nullptr;
   a.wslots = 0;
   for (int i = 0; i <= kMaxSlotRounds; ++i) a.wcum[0][i] = a.wcum[1][i] = 0;
-  a.mgran = nullptr;
+  a.mgran = a.mgran_b = nullptr;
   a.mtag = 0.0;
+  a.nib = nullptr;
+  a.ncls[0] = a.ncls[1] = a.ncls[2] = 0u;
   a.merr = nullptr;
   return a;
 }
@@ -4320,41 +3801,25 @@ void klaunch(perc_ctx* h, K kern, dim3 g, dim3 b, hipStream_t st, const CGArgs& 
   }
 }
 
-// the strip-major q-free march P or B with 3 rows prefetched and
-// nontemporal last-use loads (the default solve): store policy SAUX
-// (nontemporal 2, plain 0), the deferred reduction
-template <int MODE, int SAUX>
-void launch_march_sm2(perc_ctx* h, hipStream_t st, const CGArgs& a0) {
-  // strip-major march B on its own band height (march_hb: several rounds
-  // of short bands instead of the slot bands), probe PERC_MARCH_BROWS
-  CGArgs a = a0;
-  int grid = a.wslots > 0 ? h->wm_grid : h->march_grid;
-  if (MODE == kMarchB && h->march_hb > 0) {
-    a.wslots = 0;
-    a.T.bh = h->march_hb;
-    grid = cdiv((h->g.m / kMarchW) * cdiv(h->g.n - 2, h->march_hb), kMarchWaves);
+// the strip-major q-free march P or B (the default solve at L <= 4096): 3
+// rows prefetched, nontemporal last-use loads and stores, tagged-granule
+// reductions (a.mgran) or the ticket reduction, phase probe (a.mtrace)
+template <int MODE, bool PK>
+void launch_march_sm2(perc_ctx* h, hipStream_t st, const CGArgs& a) {
+  const int grid = a.wslots > 0 ? h->wm_grid : h->march_grid;
+  if (a.mgran) {
+    if (a.mtrace) klaunch(h, k_cg_march<MODE, true, 3, kNT, true, true, PK>, grid, 64 * kMarchWaves, st, a);
+    else klaunch(h, k_cg_march<MODE, true, 3, kNT, false, true, PK>, grid, 64 * kMarchWaves, st, a);
+  } else if (a.mtrace) {
+    klaunch(h, k_cg_march<MODE, true, 3, kNT, true, false, PK>, grid, 64 * kMarchWaves, st, a);
+  } else {
+    klaunch(h, k_cg_march<MODE, true, 3, kNT, false, false, PK>, grid, 64 * kMarchWaves, st, a);
   }
-  if constexpr (SAUX == kNT) {
-    if (a.mtrace && !h->march_defer) {  // phase probe (PERC_MARCH_TRACE)
-      klaunch(h, k_cg_march<MODE, true, 3, 2, SAUX, false, true>, grid, 64 * kMarchWaves, st, a);
-      return;
-    }
-  }
-  if constexpr (SAUX == kNT) {
-    if (a.mgran && !h->march_defer) {  // tagged-granule reductions (PERC_MARCH_TAG)
-      if (a.mtrace) klaunch(h, k_cg_march<MODE, true, 3, 2, SAUX, false, true, true>, grid, 64 * kMarchWaves, st, a);
-      else klaunch(h, k_cg_march<MODE, true, 3, 2, SAUX, false, false, true>, grid, 64 * kMarchWaves, st, a);
-      return;
-    }
-  }
-  if (h->march_defer) klaunch(h, k_cg_march<MODE, true, 3, 2, SAUX, true>, grid, 64 * kMarchWaves, st, a);
-  else klaunch(h, k_cg_march<MODE, true, 3, 2, SAUX, false>, grid, 64 * kMarchWaves, st, a);
 }
 template <int MODE>
 void launch_march_sm(perc_ctx* h, hipStream_t st, const CGArgs& a) {
-  // (write-through sc1 stores, 16 / 18, measured 2-3 % slower: r3_ab1)
-  if (h->march_saux == 0) launch_march_sm2<MODE, 0>(h, st, a);
-  else launch_march_sm2<MODE, kNT>(h, st, a);
+  if (a.nib) launch_march_sm2<MODE, true>(h, st, a);
+  else launch_march_sm2<MODE, false>(h, st, a);
 }
 
 // S(k), or the fused P(k)+S(k) of the tiled stencil kernel
@@ -4363,37 +3828,12 @@ void launch_cg_spmv(perc_ctx* h, const CGArgs& a, int G) {
     const int th = h->tile_h;
     const dim3 G2(h->tile_grid), B2(tile_threads(th));
     hipStream_t st = h->stream;
-    if (h->rowmarch) {
-      const dim3 g(h->rm_grid), b(h->rm_w / 4);
-      const bool qf = h->qfree;
-      if (h->rm_w == 2048) {
-        if (qf) klaunch(h, k_cg_rm<kMarchP, 2048>, g, b, st, a);
-        else klaunch(h, k_cg_rm<kMarchPQ, 2048>, g, b, st, a);
-      } else if (h->rm_w == 1024) {
-        if (qf) klaunch(h, k_cg_rm<kMarchP, 1024>, g, b, st, a);
-        else klaunch(h, k_cg_rm<kMarchPQ, 1024>, g, b, st, a);
-      } else {
-        if (qf) klaunch(h, k_cg_rm<kMarchP, 512>, g, b, st, a);
-        else klaunch(h, k_cg_rm<kMarchPQ, 512>, g, b, st, a);
-      }
-      return;
-    }
     if (h->march) {
-      if (h->qfree && a.sm && h->march_depth == 2 && h->march_paux == 2) klaunch(h, k_cg_march<kMarchP, true, 2, 2>, h->march_grid, 64 * kMarchWaves, st, a);
-      else if (h->qfree && a.sm && h->march_depth == 2) klaunch(h, k_cg_march<kMarchP, true, 2>, h->march_grid, 64 * kMarchWaves, st, a);
-      else if (h->qfree && a.sm && h->march_paux == 2) launch_march_sm<kMarchP>(h, st, a);
-      else if (h->qfree && a.sm) klaunch(h, k_cg_march<kMarchP, true, 3>, h->march_grid, 64 * kMarchWaves, st, a);
-      else if (h->qfree && a.wslots == 0 && h->march_hp > 0) {
-        // row-major q-free P on its own band height (march_hp), B on march_h
-        CGArgs ap = a;
-        ap.T.bh = h->march_hp;
-        klaunch(h, k_cg_march<kMarchP>, cdiv((h->g.m / kMarchW) * cdiv(h->g.n - 2, h->march_hp), kMarchWaves),
-                64 * kMarchWaves, st, ap);
-      } else if (h->qfree) klaunch(h, k_cg_march<kMarchP>, a.wslots > 0 ? h->wm_grid : h->march_grid, 64 * kMarchWaves, st, a);
-      else if (a.sm && h->march_depth == 2) klaunch(h, k_cg_march<kMarchPQ, true, 2>, h->march_grid, 64 * kMarchWaves, st, a);
-      else if (a.sm && h->march_depth == 4) klaunch(h, k_cg_march<kMarchPQ, true, 4>, h->march_grid, 64 * kMarchWaves, st, a);
-      else if (a.sm) klaunch(h, k_cg_march<kMarchPQ, true, 3>, h->march_grid, 64 * kMarchWaves, st, a);
-      else if (h->march_depth == 2) klaunch(h, k_cg_march<kMarchPQ, false, 2>, h->march_grid, 64 * kMarchWaves, st, a);
+      if (h->qfree && a.sm) launch_march_sm<kMarchP>(h, st, a);
+      // row-major q-free P (vectors past the Infinity Cache): one round of
+      // slot-weighted bands when a.wslots is set
+      else if (h->qfree) klaunch(h, k_cg_march<kMarchP>, a.wslots > 0 ? h->wm_grid : h->march_grid, 64 * kMarchWaves, st, a);
+      // q-storing P+S (row slabs, the literal dot order, modes without QFREE)
       else klaunch(h, k_cg_march<kMarchPQ, false, 3>, h->march_grid, 64 * kMarchWaves, st, a);
       return;
     }
@@ -4415,16 +3855,8 @@ void launch_cg_spmv(perc_ctx* h, const CGArgs& a, int G) {
 void launch_cg_b(perc_ctx* h, const CGArgs& a, int G) {
   // fused formats: b_grid (set with the lattice, see dev_build_lattice)
   if (h->fused && h->b_grid > 0) G = h->b_grid;
-  if (h->rowmarch && h->qfree) {
-    const dim3 g(h->rm_grid), b(h->rm_w / 4);
-    if (h->rm_w == 2048) klaunch(h, k_cg_rm<kMarchB, 2048>, g, b, h->stream, a);
-    else if (h->rm_w == 1024) klaunch(h, k_cg_rm<kMarchB, 1024>, g, b, h->stream, a);
-    else klaunch(h, k_cg_rm<kMarchB, 512>, g, b, h->stream, a);
-  } else if (h->march && h->qfree) {
-    if (a.sm && h->march_bdepth == 2 && h->march_baux == 2) klaunch(h, k_cg_march<kMarchB, true, 2, 2>, h->march_grid, 64 * kMarchWaves, h->stream, a);
-    else if (a.sm && h->march_bdepth == 2) klaunch(h, k_cg_march<kMarchB, true, 2>, h->march_grid, 64 * kMarchWaves, h->stream, a);
-    else if (a.sm && h->march_baux == 2) launch_march_sm<kMarchB>(h, h->stream, a);
-    else if (a.sm) klaunch(h, k_cg_march<kMarchB, true, 3>, h->march_grid, 64 * kMarchWaves, h->stream, a);
+  if (h->march && h->qfree) {
+    if (a.sm) launch_march_sm<kMarchB>(h, h->stream, a);
     else {  // row-major B: its own bands (slot-weighted bands are the P kernel's, rm_slots)
       CGArgs ab = a;
       ab.wslots = 0;
@@ -4508,10 +3940,9 @@ StencilForms stencil_forms(const Geom& g) {
 // stream synchronize).  With the default fence the launches that carry the
 // start / stop events pay an L2 write-back + invalidate the other launches
 // do not, and read ~1 % above rocprofv3's durations of the same kernels
-// (profiles/r3_8_*).  PERC_EVENT_SYSFENCE=1: the default events (A/B).
+// (profiles/r3_8_*, r3_9_ab_event_fence_L4096.log).
 hipError_t timing_event_create(hipEvent_t* ev) {
-  static const bool sysfence = getenv("PERC_EVENT_SYSFENCE") && atoi(getenv("PERC_EVENT_SYSFENCE")) != 0;
-  return sysfence ? hipEventCreate(ev) : hipEventCreateWithFlags(ev, hipEventDisableSystemFence);
+  return hipEventCreateWithFlags(ev, hipEventDisableSystemFence);
 }
 
 hipError_t dbg_sync(hipStream_t st, const char* name) {
@@ -4536,6 +3967,28 @@ inline int cg_grid(int N) {
 template <typename T>
 hipError_t dmalloc(T** p, size_t n) {
   return hipMalloc(reinterpret_cast<void**>(p), sizeof(T) * (n ? n : 1));
+}
+
+// tagged-granule reductions of the strip-major q-free march (a.sm): a P and
+// a B region, each sized for the largest grid either kernel runs; a new
+// solve epoch, so no granule of an earlier solve carries a valid tag
+hipError_t setup_granules(perc_ctx* h, CGArgs& a, int itmax) {
+  if (!h->march_tag || !a.sm || itmax > kTagMaxIter) return hipSuccess;
+  const int GM = std::max(red_grid(h), h->wm_grid);
+  const size_t region = (size_t)2 * 2 * ((size_t)GM + red_groups(GM));  // NV <= 2, 16-B granules
+  const size_t need = 2 * region;
+  if (h->d.mgran_n < need) {
+    if (h->d.mgran) HIP_TRY(hipFree(h->d.mgran));
+    h->d.mgran = nullptr;
+    HIP_TRY(dmalloc(&h->d.mgran, need));
+    HIP_TRY(hipMemsetAsync(h->d.mgran, 0, need * sizeof(double), h->stream));  // tag 0: never a launch's
+    h->d.mgran_n = need;
+  }
+  a.mgran = h->d.mgran;
+  a.mgran_b = h->d.mgran + region;
+  a.merr = &h->d.scal->pad[1];
+  ++h->solve_epoch;
+  return hipSuccess;
 }
 
 hipError_t exclusive_scan(const int* in, int* out, int n, hipStream_t st) {
@@ -4647,7 +4100,6 @@ hipError_t dev_build_lattice(perc_ctx* h) {
     h->b_grid = std::min(2 * cus, h->grid);
   if (h->res_G > 0) {
     HIP_TRY(dmalloc(&d.res_xch, (size_t)2 * h->res_G * 2 * 2 * g.m));
-    HIP_TRY(dmalloc(&d.res_part, (size_t)2 * 3 * h->res_G));
     HIP_TRY(dmalloc(&d.res_bar, 9 * kTicketStride));
     HIP_TRY(dmalloc(&d.res_gran, (size_t)2 * 3 * h->res_G));
   }
@@ -4691,7 +4143,7 @@ void dev_free_all(perc_ctx* h) {
   void* ptrs[] = {d.bond_first, d.rowptr, d.col, d.val, d.diag, d.rhs, d.code, d.dtab, d.sflag, d.bocc, d.socc,
                   d.order, d.parent, d.member, d.top, d.counters, d.x, d.r,
                   d.p0, d.p1, d.q, d.partials, d.tickets, d.scal, d.err_hist, d.iout,
-                  d.res_xch, d.res_part, d.res_bar, d.bw, d.code_sm, d.csize, d.res_gran,
+                  d.res_xch, d.res_bar, d.bw, d.code_sm, d.csize, d.res_gran, (void*)d.nib_sm,
                   d.sel_hist, d.sel_cand, d.mgran, d.forms_dev};
   for (void* p : ptrs)
     if (p) hipFree(p);
@@ -4869,125 +4321,61 @@ hipError_t dev_canon(perc_ctx* h, int* canon_out) {
 }
 
 // band height of the register-march kernel over `nrows` rows: the
-// requested height (perc_set_march_rows, or PERC_MARCH_ROWS for probes);
-// vectors past the Infinity Cache: 16-row bands, i.e. several rounds of
-// resident waves, each over a narrower window of the arrays (L = 8192:
-// 0.423 vs 0.451 ms with 32 rows); else one round of resident waves, the
-// height that gives every wave slot of the chip one strip-band (the PQ
-// kernel with 3 rows prefetched holds 173 VGPRs: 2 waves per SIMD, L = 4096:
-// 64-row bands)
+// requested height (perc_set_march_rows); vectors past the Infinity Cache:
+// 8-row bands for the row-major march B (0.310 vs 0.318 ms at 16 rows at
+// L = 8192; its P runs one round of slot-mapped bands instead,
+// march_slots_rm; 16 rows without PERC_MARCH_SLOTS); else one round of
+// resident waves, the height that gives every wave slot of the chip one
+// strip-band
 int march_rows_for(const perc_ctx* h, int nrows) {
   const Geom& g = h->g;
-  const char* env_rows = getenv("PERC_MARCH_ROWS");
   if (h->march_rows_req > 0) return h->march_rows_req;
-  if (env_rows && atoi(env_rows) > 0) return atoi(env_rows);
-  // (vectors past the Infinity Cache: 8-row bands for the row-major march B,
-  // 0.310 vs 0.318 ms at 16 rows at L = 8192; its P runs one round of
-  // slot-mapped bands instead, march_slots_rm)
-  if ((size_t)g.m * nrows * sizeof(double) > kLargeVector && !large_strips())
+  if ((size_t)g.m * nrows * sizeof(double) > kLargeVector)
     return (h->march_mode & PERC_MARCH_SLOTS) ? 8 : 16;
   int cus = 0, per_cu = 0;
   hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, h->device);
-  // (the strip-major kernel of the same depth: within a few VGPRs, same occupancy)
-  if (h->march_depth == 2)
-    hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_cg_march<kMarchPQ, false, 2>, 64 * kMarchWaves, 0);
-  else if (h->march_depth == 4)
-    hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_cg_march<kMarchPQ, true, 4>, 64 * kMarchWaves, 0);
-  else
-    hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_cg_march<kMarchPQ, false, 3>, 64 * kMarchWaves, 0);
+  hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_cg_march<kMarchP, true, 3, kNT, false, true>,
+                                               64 * kMarchWaves, 0);
   const long long slots = (long long)std::max(cus, 1) * std::max(per_cu, 1) * kMarchWaves;
   const long long bands = std::max(1ll, slots / (g.m / kMarchW));
   return std::max(2, cdiv(nrows, bands));
 }
 
-// band height and grid of the register-march kernel
+// band height and grid of the register-march kernel; the slot-weighted
+// bands (PERC_MARCH_SLOTS): one workgroup per CU and round, bands cycling
+// over the rounds, weights = the rounds' relative streaming rates with
+// equal bands (kSlotW: P, B of the strip-major march, row-major P past the
+// Infinity Cache; same-box A/Bs, profiles/r3_4_ab_slotw_L4096.log and the
+// r3 L = 8192 probes -- flat weights there, i.e. one round of equal bands:
+// 0.364 ms vs 0.387 at 100:80:60 and 0.403 for the 16-row bands)
+constexpr int kSlotW[3][kMaxSlotRounds] = {{100, 75, 50, 40}, {100, 80, 60, 50}, {100, 100, 100, 100}};
+
 void march_geometry(perc_ctx* h) {
   const Geom& g = h->g;
   h->march_grid = 0;
-  // rows prefetched ahead by the P+S march (PERC_MARCH_DEPTH: 2 for probes)
-  h->march_depth = 3;
-  if (const char* e = getenv("PERC_MARCH_DEPTH")) h->march_depth = std::min(std::max(atoi(e), 2), 4);
-  // the strip-major q-free march B (PERC_MARCH_BDEPTH, probes)
-  h->march_bdepth = std::min(h->march_depth, 3);
-  if (const char* e = getenv("PERC_MARCH_BDEPTH")) h->march_bdepth = std::min(std::max(atoi(e), 2), 3);
-  // nontemporal p(k-1) loads in the q-free P: the value is dead after the
-  // load, and streaming it past the caches leaves the Infinity Cache to
-  // the r and p(k) rows the next kernel re-reads (same-box A/B: P 0.0818
-  // vs 0.0830 ms, B 0.0795 vs 0.0808, profiles/r2_34_ab_load_policy.log);
-  // PERC_MARCH_PAUX = 0 / 16 (sc1) and PERC_MARCH_BAUX (B's r(k) loads) probe
-  h->march_paux = 2;
-  if (const char* e = getenv("PERC_MARCH_PAUX")) h->march_paux = atoi(e);
-  h->march_baux = 2;
-  if (const char* e = getenv("PERC_MARCH_BAUX")) h->march_baux = atoi(e);
-  h->march_saux = kNT;  // (probe: PERC_MARCH_SAUX = 0 plain stores)
-  if (const char* e = getenv("PERC_MARCH_SAUX")) h->march_saux = atoi(e);
-
-
+  h->wm_slots = 0;
+  h->wm_grid = 0;
   if (g.m % kMarchW != 0 || g.n <= 2) return;
   const int spr = g.m / kMarchW, nrows = g.n - 2;
   h->march_h = march_rows_for(h, nrows);
   h->march_grid = cdiv(spr * cdiv(nrows, h->march_h), kMarchWaves);
-  // slot-weighted bands (strip-major q-free march): one workgroup per CU
-  // and round, bands cycling over the rounds; weights = the rounds' relative
-  // streaming rates with equal bands (PERC_MARCH_SLOTW / PERC_MARCH_SLOTWB
-  // for P / B, e.g. "100:75:50", "0": off)
-  h->wm_slots = 0;
-  h->wm_grid = 0;
-  {
-    int cus = 0, per_cu = 0;
-    hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, h->device);
-    hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_cg_march<kMarchP, true, 3, 2>, 64 * kMarchWaves, 0);
-    // (per kernel: the P kernel and the march B balance at different weights)
-    // (row-major P past the Infinity Cache, L = 8192: flat weights, i.e.
-    // one round of equal bands: 0.364 ms vs 0.387 at 100:80:60 and 0.403
-    // for the 16-row bands, r3 L = 8192 probes)
-    int wts[3][kMaxSlotRounds] = {{100, 75, 50, 40}, {100, 80, 60, 50}, {100, 100, 100, 100}};
-    int nw[3] = {per_cu, per_cu, per_cu};
-    const char* envs[3] = {"PERC_MARCH_SLOTW", "PERC_MARCH_SLOTWB", "PERC_MARCH_SLOTWRM"};
+  int cus = 0, per_cu = 0;
+  hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, h->device);
+  hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_cg_march<kMarchP, true, 3, kNT, false, true>,
+                                               64 * kMarchWaves, 0);
+  const long long waves = (long long)cus * kMarchWaves;
+  const int(*wts)[kMaxSlotRounds] = h->slot_w_set ? h->slot_w : kSlotW;
+  bool ok = cus > 0 && per_cu >= 2 && per_cu <= kMaxSlotRounds && waves % spr == 0 &&
+            (waves / spr) * per_cu <= nrows;
+  for (int i = 0; ok && i < per_cu; ++i) ok = wts[0][i] > 0 && wts[1][i] > 0 && wts[2][i] > 0;
+  if (ok) {
+    h->wm_slots = per_cu;
+    h->wm_grid = cus * per_cu;
     for (int k = 0; k < 3; ++k) {
-      const char* e = getenv(envs[k]);
-      if (!e) continue;
-      nw[k] = 0;
-      for (const char* c = e; *c && nw[k] < kMaxSlotRounds;) {
-        wts[k][nw[k]++] = atoi(c);
-        while (*c && *c != ',' && *c != ':') ++c;
-        if (*c) ++c;
-      }
-      if (nw[k] == 1 && wts[k][0] == 0) nw[k] = 0;  // "0": off
-    }
-    const long long waves = (long long)cus * kMarchWaves;
-    bool ok = cus > 0 && per_cu >= 2 && per_cu <= kMaxSlotRounds && nw[0] == per_cu &&
-              nw[1] == per_cu && nw[2] == per_cu && waves % spr == 0 && (waves / spr) * per_cu <= nrows;
-    for (int i = 0; ok && i < per_cu; ++i) ok = wts[0][i] > 0 && wts[1][i] > 0 && wts[2][i] > 0;
-    if (ok) {
-      h->wm_slots = per_cu;
-      h->wm_grid = cus * per_cu;
-      for (int k = 0; k < 3; ++k) {
-        h->wm_cum[k][0] = 0;
-        for (int i = 0; i < per_cu; ++i) h->wm_cum[k][i + 1] = h->wm_cum[k][i] + wts[k][i];
-      }
+      h->wm_cum[k][0] = 0;
+      for (int i = 0; i < per_cu; ++i) h->wm_cum[k][i + 1] = h->wm_cum[k][i] + wts[k][i];
     }
   }
-  // workgroup row-march: the widest strip of 2048 / 1024 / 512 columns that
-  // divides m, the tallest band (32 .. 2 rows) that gives >= kRmMinGroups
-  // workgroups (two per CU), or the requested height
-  h->rm_grid = 0;
-  h->rm_w = g.m % 2048 == 0 ? 2048 : (g.m % 1024 == 0 ? 1024 : (g.m % 512 == 0 ? 512 : 0));
-  if (((long long)h->N + 2) * 8 >= (1ll << 31)) h->rm_w = 0;  // buffer offsets (kOOB)
-  if (h->rm_w == 0) return;
-  const int rspr = g.m / h->rm_w;
-  if (h->march_rows_req > 0) {
-    h->rm_h = h->march_rows_req;
-  } else {
-    h->rm_h = 32;
-    while (h->rm_h > 8 && (long long)rspr * cdiv(nrows, h->rm_h) < kRmMinGroups) h->rm_h /= 2;
-    // below 8-row bands the two halo rows per band cost more than the
-    // row segments gain: the per-wave march is used (L = 1024: 0.0285 vs
-    // 0.0294 ms per iteration)
-    if ((long long)rspr * cdiv(nrows, h->rm_h) < kRmMinGroups) h->rm_w = 0;
-  }
-  if (h->rm_w == 0) return;
-  h->rm_grid = rspr * cdiv(nrows, h->rm_h);
 }
 
 // resident solve: m a multiple of 1024 (MT = m / 1024 columns per thread
@@ -5026,63 +4414,36 @@ void select_format(perc_ctx* h) {
   h->stencil = h->fmt_req != PERC_FMT_CSR && h->stencil_ok;
   h->fused = h->stencil && h->tiled_ok && h->fmt_req != PERC_FMT_STENCIL_SPLIT;
   h->march = h->fused && h->march_ok && h->fmt_req != PERC_FMT_STENCIL_TILED;
-  h->rowmarch = h->fused && h->rm_grid > 0 && h->fmt_req != PERC_FMT_STENCIL_TILED &&
-                (h->march_mode & PERC_MARCH_ROWS);
-  h->march = h->march && !h->rowmarch;
+  const bool literal = h->dot_order == PERC_DOT_LITERAL;
   // (dev_solve only: the march kernels stay selected for the probes)
   h->resident = h->fused && h->res_G > 0 && h->fmt_req != PERC_FMT_STENCIL_TILED &&
-                (h->march_mode & PERC_SOLVE_RESIDENT) && h->march_rows_req == 0;
-  h->qfree = (h->march || h->rowmarch) && (h->march_mode & PERC_MARCH_QFREE);
-  h->march_alt = (h->march || h->rowmarch) && (h->march_mode & PERC_MARCH_ALT);
-  // strip-major solve: the per-wave march with the streaming B (x in B)
+                (h->march_mode & PERC_SOLVE_RESIDENT) && h->march_rows_req == 0 && !literal;
+  // the literal dot order folds q.p from the stored q: the q-storing kernels
+  h->qfree = h->march && (h->march_mode & PERC_MARCH_QFREE) && !literal;
+  h->march_alt = h->march && (h->march_mode & PERC_MARCH_ALT);
   // one-workgroup solve for small systems, under the default format only
   // (an explicit format keeps its launched kernels, e.g. for the tests)
   h->small = h->fmt_req == PERC_FMT_AUTO && h->N > 0 && h->N <= kSmallRows &&
              (h->march_mode & PERC_SOLVE_RESIDENT) && h->d.rowptr != nullptr;
-  // strip-major only while a vector fits the Infinity Cache (L <= 4096):
-  // past it (16-row bands, several rounds of waves) the row-major march is
-  // faster (L = 8192: 0.439 vs 0.480 ms, profiles/r2_11_ab_strips.log); the
-  // strip-major march's whole-array buffer views also need < 2 GB
-  h->strips = h->march && (h->march_mode & PERC_MARCH_STRIPS) &&
-              ((size_t)h->N * sizeof(double) <= kLargeVector || large_strips());
-  // deferred reductions (the strip-major q-free march with its default
-  // cache policies; every workgroup sums every partial, gather_totals:
-  // one round of workgroups); PERC_MARCH_DEFER=0/1 overrides the mode bit
-  // for A/B probes
-  bool defer = (h->march_mode & PERC_MARCH_DEFER) != 0;
-  if (const char* e = getenv("PERC_MARCH_DEFER")) defer = atoi(e) != 0;
-  h->march_defer = defer && h->qfree && h->strips && h->march_depth == 3 && h->march_paux == 2 &&
-                   h->march_baux == 2 && h->march_grid <= kDeferGroups * kGroup;
-  // slot-weighted bands (to_strips applies them); PERC_MARCH_SLOTS=0/1 overrides
-  bool slots = (h->march_mode & PERC_MARCH_SLOTS) != 0;
-  if (const char* e = getenv("PERC_MARCH_SLOTS")) slots = atoi(e) != 0;
-  h->march_slots = slots && h->strips && h->qfree && h->wm_slots > 0;
+  // strip-major q-free march only while a vector fits the Infinity Cache
+  // (L <= 4096): past it (16-row bands, several rounds of waves) the
+  // row-major march is faster (L = 8192: 0.439 vs 0.480 ms,
+  // profiles/r2_11_ab_strips.log); its whole-array buffer views also need
+  // < 2 GB
+  h->strips = h->qfree && (h->march_mode & PERC_MARCH_STRIPS) && (size_t)h->N * sizeof(double) <= kLargeVector;
+  // slot-weighted bands of the strip-major march (to_strips applies them)
+  const bool slots = (h->march_mode & PERC_MARCH_SLOTS) != 0;
+  h->march_slots = slots && h->strips && h->wm_slots > 0;
   // row-major q-free march past the Infinity Cache (L = 8192): P on one round
-  // of bands (the slot mapping with PERC_MARCH_SLOTWRM weights), B on 8-row
-  // bands (march_rows_for): P 0.364 + B 0.310 vs 0.403 + 0.318 ms per
-  // iteration (r3 L = 8192 probes); PERC_MARCH_RMSLOTS=0/1 overrides
-  bool rms = slots && (size_t)h->N * sizeof(double) > kLargeVector;
-  if (const char* e = getenv("PERC_MARCH_RMSLOTS")) rms = atoi(e) != 0;
-  h->march_slots_rm = rms && !h->strips && h->qfree && h->wm_slots > 0;
-  // row-major q-free P band height of its own (probe PERC_MARCH_PROWS; the
-  // reduction buffers cover band height 1, march_grid_max)
-  h->march_hb = 0;
-  if (const char* e = getenv("PERC_MARCH_BROWS"))
-    if (h->strips && h->qfree && h->march_rows_req == 0) h->march_hb = std::max(1, atoi(e));
-  h->march_hp = 0;
-  if (const char* e = getenv("PERC_MARCH_PROWS"))
-    if (!h->strips && h->qfree && !h->march_slots_rm && h->march_rows_req == 0) h->march_hp = std::max(1, atoi(e));
-  // tagged-granule reductions (PERC_MARCH_TAG; PERC_MARCH_TAG=0/1 overrides)
-  bool tag = (h->march_mode & PERC_MARCH_TAG) != 0;
-  if (const char* e = getenv("PERC_MARCH_TAG")) tag = atoi(e) != 0;
-  h->march_tag = tag && h->strips && h->qfree && h->march_depth == 3 && h->march_paux == 2 &&
-                 h->march_baux == 2 && h->march_bdepth == 3;
-  // persistent march (PERC_MARCH_PERSIST; PERC_MARCH_PERSIST=0/1 overrides):
-  // needs the slot grid (one workgroup per CU and round, all co-resident)
-  bool persist = (h->march_mode & PERC_MARCH_PERSIST) != 0;
-  if (const char* e = getenv("PERC_MARCH_PERSIST")) persist = atoi(e) != 0;
-  h->march_persist = persist && h->march_tag && h->march_slots && !h->march_defer && h->wm_slots == 3 && h->march_hb == 0 &&
-                     h->wm_grid <= 64 * kGroup && h->march_rows_req == 0;
+  // of bands (the slot mapping with the third weight set), B on 8-row bands
+  // (march_rows_for): P 0.364 + B 0.310 vs 0.403 + 0.318 ms per iteration
+  // (r3 L = 8192 probes)
+  h->march_slots_rm = slots && h->qfree && !h->strips && (size_t)h->N * sizeof(double) > kLargeVector &&
+                      h->wm_slots > 0;
+  // tagged-granule reductions of the strip-major march (PERC_MARCH_TAG);
+  // their tags are (epoch << 24) | iteration, so solves of >= 2^24 - 2
+  // iterations take the ticket reduction
+  h->march_tag = (h->march_mode & PERC_MARCH_TAG) && h->strips;
 }
 
 // strip-major copies of r (into the q buffer: r and q swap roles for the
@@ -5099,9 +4460,26 @@ hipError_t to_strips(perc_ctx* h, CGArgs& a) {
   a.q = d.r;
   a.St.code = d.code_sm;
   a.sm = 1;
-  a.bx = 1;  // x (row-major) is updated in B: k_cg_b, or the q-free march B
-  if (h->march_slots && h->qfree && h->march_depth == 3 && h->march_paux == 2 &&
-      h->march_baux == 2 && h->march_bdepth == 3) {
+  a.bx = 1;  // x (row-major) is updated in the q-free march B
+  // nibble codes (PERC_MARCH_NIBBLE, square lattice): 0.5 instead of 2
+  // bytes of row code per element in both march kernels
+  h->nib_used = false;
+  if (h->nib_ok && (h->march_mode & PERC_MARCH_NIBBLE)) {
+    if (!d.nib_sm) HIP_TRY(dmalloc(&d.nib_sm, (size_t)h->N / 2 + 16));
+    HIP_TRY(hipMemsetAsync(d.sflag + 3, 0, sizeof(int), st));
+    k_pack_nib<<<blocks_for(n / 2), kBlock, 0, st>>>(a.T, d.code, d.nib_sm, h->ncls[0], h->ncls[1],
+                                                     h->ncls[2], d.sflag + 3);
+    HIP_TRY(dbg_sync(st, "k_pack_nib"));
+    int bad = 0;
+    HIP_TRY(hipMemcpyAsync(&bad, d.sflag + 3, sizeof(int), hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    if (!bad) {
+      a.nib = d.nib_sm;
+      for (int c = 0; c < 3; ++c) a.ncls[c] = h->ncls[c];
+    }
+    h->nib_used = !bad;
+  }
+  if (h->march_slots) {
     a.wslots = h->wm_slots;
     for (int i = 0; i <= h->wm_slots; ++i) {
       a.wcum[0][i] = h->wm_cum[0][i];
@@ -5135,6 +4513,7 @@ static hipError_t launch_assemble(perc_ctx* h, bool csr) {
     return -1;
   };
   int fl = -1, fr = -1;
+  h->nib_ok = false;
   if (closed && h->g.lattice == kSquare && m >= 4) {
     const int oi[4] = {-m, -1, 1, m}, ri[4] = {-1, 0, 0, 1}, ci[4] = {0, -1, 1, 0};
     fast = find_form(4, oi, ri, ci);
@@ -5149,6 +4528,12 @@ static hipError_t launch_assemble(perc_ctx* h, bool csr) {
       fl = find_form(3, ol, rl, cl);
       fr = find_form(3, orr, rr, cr);
     }
+    // the column classes of the nibble codes (k_pack_nib checks every row)
+    const unsigned ce = h->g.pbc ? 4u : 3u;
+    h->ncls[0] = 4u << 8 | (unsigned)fast << 11;
+    h->ncls[1] = ce << 8 | (unsigned)fl << 11;
+    h->ncls[2] = ce << 8 | (unsigned)fr << 11;
+    h->nib_ok = fast >= 0 && fl >= 0 && fr >= 0 && m % 2 == 0;
   }
   if (csr)
     k_assemble<true><<<cdiv(h->N, kBlock), kBlock, 0, st>>>(h->g, h->N, d.bond_first, d.bocc, d.socc,
@@ -5220,23 +4605,19 @@ __global__ __launch_bounds__(1024) void k_res_sync_probe(ResArgs a, int iters) {
 }
 
 // the resident kernel for m = 1024 (MT = 1) / 2048, square-lattice
-// positions only (sq) or all eight; GATHER: all-gather reductions; TR:
-// phase probe
+// positions only (sq) or all eight
 // (NT threads per workgroup, m of them for m <= 1024: with one column per
 // thread the template's NT is only the launch bound, so widths up to 512
 // share the 512-bound instantiation -- 125-142 VGPRs, no spills)
-template <bool GATHER, bool TR>
 const void* res_kernel(int MT, bool sq, int NT) {
-  if (MT == 1 && NT <= 512) {
-    if (!GATHER || TR) return nullptr;
-    return sq ? (const void*)k_cg_res<1, 4, true, kResSquareMask, true, false, 512>
-              : (const void*)k_cg_res<1, 4, true, 0xFFu, true, false, 512>;
-  }
+  if (MT == 1 && NT <= 512)
+    return sq ? (const void*)k_cg_res<1, 4, true, kResSquareMask, 512>
+              : (const void*)k_cg_res<1, 4, true, 0xFFu, 512>;
   if (MT == 1)
-    return sq ? (const void*)k_cg_res<1, 4, true, kResSquareMask, GATHER, TR>
-              : (const void*)k_cg_res<1, 4, true, 0xFFu, GATHER, TR>;
-  return sq ? (const void*)k_cg_res<2, 8, false, kResSquareMask, GATHER, TR>
-            : (const void*)k_cg_res<2, 8, false, 0xFFu, GATHER, TR>;
+    return sq ? (const void*)k_cg_res<1, 4, true, kResSquareMask>
+              : (const void*)k_cg_res<1, 4, true, 0xFFu>;
+  return sq ? (const void*)k_cg_res<2, 8, false, kResSquareMask>
+            : (const void*)k_cg_res<2, 8, false, 0xFFu>;
 }
 
 // one cooperative launch runs the whole iteration loop (k_cg_res)
@@ -5257,35 +4638,16 @@ hipError_t dev_solve_resident(perc_ctx* h, const CGArgs& ca, int* iter, double* 
   a.err_hist = d.err_hist;
   a.err_hist_cap = d.err_hist_cap;
   a.xch = d.res_xch;
-  a.part = d.res_part;
   a.bar = d.res_bar;
   a.gran = d.res_gran;
   HIP_TRY(hipMemsetAsync(d.res_bar, 0, 9 * kTicketStride * sizeof(unsigned), st));
   HIP_TRY(hipMemsetAsync(d.res_gran, 0, (size_t)2 * 3 * h->res_G * sizeof(double), st));
   void* args[] = {&a};
-  const void* fn = nullptr;
-  // reductions by tagged-granule all-gather (res_gather; PERC_RES_GATHER=0:
-  // the counter barrier + partial reads, for A/B): L = 1024 15.5 vs 16.6 us
-  // per iteration, L = 2048 33.7 vs 34.65 (profiles/r2_10_resident_gather_ab.log)
-  const bool gat = !(getenv("PERC_RES_GATHER") && atoi(getenv("PERC_RES_GATHER")) == 0);
+  // reductions by tagged-granule all-gather (res_gather): L = 1024 15.5 vs
+  // 16.6 us per iteration against a counter barrier + partial reads, L =
+  // 2048 33.7 vs 34.65 (profiles/r2_10_resident_gather_ab.log)
   const bool sq = (h->forms.umask & ~kResSquareMask) == 0;
-  // phase probe (PERC_RES_TRACE=<csv path>): wall-clock stamps of the first
-  // kResTrIt iterations in three workgroups, written as CSV after the solve
-  const char* trpath = getenv("PERC_RES_TRACE");
-  a.trace = nullptr;
-  const size_t trn = (size_t)3 * kResTrIt * 8;
-  const bool tr = trpath && gat;
-  if (tr) {
-    HIP_TRY(dmalloc(&a.trace, trn));
-    HIP_TRY(hipMemsetAsync(a.trace, 0, trn * sizeof(unsigned long long), st));
-  }
-  const int nt = h->res_NT;
-  fn = tr ? res_kernel<true, true>(h->res_MT, sq, nt)
-          : (gat ? res_kernel<true, false>(h->res_MT, sq, nt) : res_kernel<false, false>(h->res_MT, sq, nt));
-  if (!fn) {  // (narrow widths: the all-gather variant only)
-    if (a.trace) (void)hipFree(a.trace);
-    return hipErrorInvalidConfiguration;  // dev_solve falls back to the launched kernels
-  }
+  const void* fn = res_kernel(h->res_MT, sq, h->res_NT);
   KernelTiming& T = h->timing;
   if (T.enabled) {
     if (T.ev.size() < 2) T.ev.resize(2, nullptr);
@@ -5293,28 +4655,12 @@ hipError_t dev_solve_resident(perc_ctx* h, const CGArgs& ca, int* iter, double* 
       if (!T.ev[i]) HIP_TRY(timing_event_create(&T.ev[i]));
     HIP_TRY(hipEventRecord(T.ev[0], st));
   }
-  HIP_TRY(hipLaunchCooperativeKernel(fn, dim3(a.G), dim3(nt), args, 0, st));
+  HIP_TRY(hipLaunchCooperativeKernel(fn, dim3(a.G), dim3(h->res_NT), args, 0, st));
   HIP_TRY(dbg_sync(st, "k_cg_res"));
   if (T.enabled) HIP_TRY(hipEventRecord(T.ev[1], st));
   CGScalars hs{};
   HIP_TRY(hipMemcpyAsync(&hs, d.scal, sizeof(hs), hipMemcpyDeviceToHost, st));
   HIP_TRY(hipStreamSynchronize(st));
-  if (a.trace) {
-    std::vector<unsigned long long> tr(trn);
-    HIP_TRY(hipMemcpy(tr.data(), a.trace, trn * sizeof(unsigned long long), hipMemcpyDeviceToHost));
-    HIP_TRY(hipFree(a.trace));
-    if (FILE* fo = fopen(trpath, "a")) {
-      fprintf(fo, "# m=%d G=%d H=%d iter=%d (wall clock ticks, 100 MHz)\nwg,k,t0,t1,t2,t3,t4,t5\n",
-              a.m, a.G, a.H, hs.iter);
-      for (int q = 0; q < 3; ++q)
-        for (int it = 0; it < std::min(kResTrIt, hs.iter); ++it) {
-          const unsigned long long* v = &tr[((size_t)q * kResTrIt + it) * 8];
-          fprintf(fo, "%d,%d,%llu,%llu,%llu,%llu,%llu,%llu\n", q == 0 ? 0 : (q == 1 ? a.G / 2 : a.G - 1),
-                  it + 1, v[0], v[1], v[2], v[3], v[4], v[5]);
-        }
-      fclose(fo);
-    }
-  }
   if (hs.pad[0] != 0) {
     fprintf(stderr, "[perc] k_cg_res: grid barrier timed out\n");
     return hipErrorLaunchTimeOut;
@@ -5330,52 +4676,16 @@ hipError_t dev_solve_resident(perc_ctx* h, const CGArgs& ca, int* iter, double* 
   return hipSuccess;
 }
 
-// the persistent march (k_cg_pmarch): one cooperative launch per solve on
-// the slot grid; r and the codes are strip-major already (to_strips)
-hipError_t dev_solve_pmarch(perc_ctx* h, CGArgs a, int* iter, double* err) {
-  DeviceBuffers& d = h->d;
-  hipStream_t st = h->stream;
-  int per_cu = 0, cus = 0;
-  HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, h->device));
-  HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_cg_pmarch, 64 * kMarchWaves, 0));
-  if (per_cu < h->wm_slots || cus * h->wm_slots != h->wm_grid) return hipErrorCooperativeLaunchTooLarge;
-  a.wslots = h->wm_slots;
-  for (int i = 0; i <= h->wm_slots; ++i) a.wcum[0][i] = h->wm_cum[0][i];
-  a.mtag = (double)((unsigned long long)h->solve_epoch << 24);
-  a.kiter = 0;
-  KernelTiming& T = h->timing;
-  if (T.enabled) {
-    if (T.ev.size() < 2) T.ev.resize(2, nullptr);
-    for (int i = 0; i < 2; ++i)
-      if (!T.ev[i]) HIP_TRY(timing_event_create(&T.ev[i]));
-    HIP_TRY(hipEventRecord(T.ev[0], st));
-  }
-  void* args[] = {&a};
-  HIP_TRY(hipLaunchCooperativeKernel((const void*)k_cg_pmarch, dim3(h->wm_grid), dim3(64 * kMarchWaves), args, 0, st));
-  HIP_TRY(dbg_sync(st, "k_cg_pmarch"));
-  if (T.enabled) HIP_TRY(hipEventRecord(T.ev[1], st));
-  CGScalars hs{};
-  HIP_TRY(hipMemcpyAsync(&hs, d.scal, sizeof(hs), hipMemcpyDeviceToHost, st));
-  HIP_TRY(hipStreamSynchronize(st));
-  if (hs.pad[1] != 0) {
-    fprintf(stderr, "[perc] k_cg_pmarch: reduction granule not seen within the poll limit\n");
-    return hipErrorLaunchTimeOut;
-  }
-  if (T.enabled && hs.iter > 0) {
-    float ms = 0.f;
-    HIP_TRY(hipEventElapsedTime(&ms, T.ev[0], T.ev[1]));
-    T.spmv_ms += ms;  // whole iterations: P and B together
-    T.spmv_n += hs.iter;
-  }
-  *iter = hs.iter;
-  *err = hs.err;
-  return hipSuccess;
-}
 
 hipError_t dev_solve(perc_ctx* h, int itol, double tol, int itmax, bool x0_zero, bool full_x,
                      int* iter, double* err) {
   DeviceBuffers& d = h->d;
   hipStream_t st = h->stream;
+  const bool literal = h->dot_order == PERC_DOT_LITERAL;
+  if (literal && h->nslab > 1) {
+    set_error("the literal dot order sums over the whole system: one slab only");
+    return hipErrorInvalidValue;
+  }
   if (!h->stencil) HIP_TRY(ensure_csr(h));
   if (d.err_hist_cap < itmax + 2) {
     if (d.err_hist) HIP_TRY(hipFree(d.err_hist));
@@ -5407,10 +4717,20 @@ hipError_t dev_solve(perc_ctx* h, int itol, double tol, int itmax, bool x0_zero,
   if (ST) k_cg_init<true><<<G, kBlock, 0, st>>>(a, itol, x0_zero ? 1 : 0);
   else k_cg_init<false><<<G, kBlock, 0, st>>>(a, itol, x0_zero ? 1 : 0);
   HIP_TRY(dbg_sync(st, "k_cg_init"));
+  if (literal) {  // bnrm and the first bknum in ascending j
+    if (ST) k_fold_init<true><<<1, 64, 0, st>>>(a, itol);
+    else k_fold_init<false><<<1, 64, 0, st>>>(a, itol);
+    HIP_TRY(dbg_sync(st, "k_fold_init"));
+  }
   if (h->small) {  // one workgroup runs the whole loop (k_cg_small)
     // (x is kept on every row here: the operator is the CSR one and N small)
-    if (ST) k_cg_small<true><<<1, kSmallThreads, 0, st>>>(a);
-    else k_cg_small<false><<<1, kSmallThreads, 0, st>>>(a);
+    if (ST) {
+      if (literal) k_cg_small<true, true><<<1, kSmallThreads, 0, st>>>(a);
+      else k_cg_small<true, false><<<1, kSmallThreads, 0, st>>>(a);
+    } else {
+      if (literal) k_cg_small<false, true><<<1, kSmallThreads, 0, st>>>(a);
+      else k_cg_small<false, false><<<1, kSmallThreads, 0, st>>>(a);
+    }
     HIP_TRY(dbg_sync(st, "k_cg_small"));
     CGScalars hs{};
     HIP_TRY(hipMemcpyAsync(&hs, d.scal, sizeof(hs), hipMemcpyDeviceToHost, st));
@@ -5432,31 +4752,9 @@ hipError_t dev_solve(perc_ctx* h, int itol, double tol, int itmax, bool x0_zero,
     h->resident = false;
   }
   if (h->strips) HIP_TRY(to_strips(h, a));
-  // tagged-granule reductions of the strip-major q-free march
-  if (h->march_tag && a.sm && h->qfree && !h->march_defer) {
-    const int G = std::max(red_grid(h), h->wm_grid);
-    const size_t need = (size_t)8 * ((size_t)G + red_groups(G));
-    if (h->d.mgran_n < need) {
-      if (h->d.mgran) HIP_TRY(hipFree(h->d.mgran));
-      h->d.mgran = nullptr;
-      HIP_TRY(dmalloc(&h->d.mgran, need));
-      HIP_TRY(hipMemsetAsync(h->d.mgran, 0, need * sizeof(double), st));  // tag 0: never a launch's
-      h->d.mgran_n = need;
-    }
-    a.mgran = h->d.mgran;
-    a.merr = &d.scal->pad[1];
-    ++h->solve_epoch;
-  }
-  if (h->march_persist && a.sm && a.mgran) {
-    const hipError_t e = dev_solve_pmarch(h, a, iter, err);
-    if (e != hipErrorCooperativeLaunchTooLarge && e != hipErrorInvalidConfiguration) return e;
-    (void)hipGetLastError();
-    fprintf(stderr, "[perc] persistent march not launchable (%s): launched kernels\n", hipGetErrorString(e));
-    h->march_persist = 0;
-  }
+  HIP_TRY(setup_granules(h, a, itmax));
   // row-major q-free march past the Infinity Cache: the P kernel on one
-  // round of slot-weighted bands (probe PERC_MARCH_RMSLOTS=1), B on its
-  // short bands
+  // round of slot-weighted bands, B on its short bands
   if (!h->strips && h->march && h->qfree && h->march_slots_rm && h->wm_slots > 0) {
     a.wslots = h->wm_slots;
     for (int i = 0; i <= h->wm_slots; ++i) a.wcum[0][i] = h->wm_cum[2][i];
@@ -5486,7 +4784,7 @@ hipError_t dev_solve(perc_ctx* h, int itol, double tol, int itmax, bool x0_zero,
   const int mt_it = getenv("PERC_MARCH_TRACE_IT") ? atoi(getenv("PERC_MARCH_TRACE_IT")) : 1000;
   constexpr int kMtN = 4;  // traced iterations
   unsigned long long* mtbuf = nullptr;
-  const size_t mtwaves = (size_t)h->march_grid * kMarchWaves;
+  const size_t mtwaves = (size_t)std::max(h->march_grid, h->wm_grid) * kMarchWaves;
   if (mtpath && h->march && a.sm && h->qfree) {
     HIP_TRY(dmalloc(&mtbuf, (size_t)2 * kMtN * 4 * mtwaves));
     HIP_TRY(hipMemsetAsync(mtbuf, 0, (size_t)2 * kMtN * 4 * mtwaves * 8, st));
@@ -5509,12 +4807,21 @@ hipError_t dev_solve(perc_ctx* h, int itol, double tol, int itmax, bool x0_zero,
       if (tm) h->ev_next[0] = ev[2], h->ev_next[1] = ev[3];
       launch_cg_spmv(h, a, G);
       HIP_TRY(dbg_sync(st, "k_cg_spmv"));
+      if (literal) {  // akden in ascending j, then ak
+        k_fold_qp<<<1, 64, 0, st>>>(a);
+        HIP_TRY(dbg_sync(st, "k_fold_qp"));
+      }
       if (tm) h->ev_next[0] = ev[4], h->ev_next[1] = ev[5];
       if (a.mtrace) a.mtrace += 4 * mtwaves;
       launch_cg_b(h, a, G);
       a.mtrace = nullptr;
       HIP_TRY(dbg_sync(st, "k_cg_b"));
       h->ev_next[0] = h->ev_next[1] = nullptr;
+      if (literal) {  // z.r and r.r in ascending j: bk, err, the stop test
+        if (ST) k_fold_b<true><<<1, 64, 0, st>>>(a);
+        else k_fold_b<false><<<1, 64, 0, st>>>(a);
+        HIP_TRY(dbg_sync(st, "k_fold_b"));
+      }
     }
     launched += chunk;
     e = hipGetLastError();
@@ -5773,8 +5080,7 @@ hipError_t dev_solve_slabs(perc_ctx* h, int K, int itol, double tol, int itmax, 
     for (int j = 0; j < chunk; ++j) {
       for (int s = 0; s < K; ++s) {
         A[s].kiter = (int)(launched + j + 1);
-        if (h->march_depth == 2) k_cg_march<kMarchPQ, false, 2><<<sl[s].march_grid, 64 * kMarchWaves, 0, st>>>(A[s]);
-        else k_cg_march<kMarchPQ, false, 3><<<sl[s].march_grid, 64 * kMarchWaves, 0, st>>>(A[s]);
+        k_cg_march<kMarchPQ, false, 3><<<sl[s].march_grid, 64 * kMarchWaves, 0, st>>>(A[s]);
       }
       SLAB_TRY(dbg_sync(st, "k_cg_march (slabs)"));
       k_slab_combine<0><<<1, 64, 0, st>>>(S, K, d.err_hist, d.err_hist_cap);
@@ -5986,8 +5292,7 @@ hipError_t dev_dslab_step(perc_ctx* h, int op) {
       break;
     case PERC_DSLAB_PS:
       a.kiter = (int)(++D->k);
-      if (h->march_depth == 2) k_cg_march<kMarchPQ, false, 2><<<b.march_grid, 64 * kMarchWaves, 0, st>>>(a);
-      else k_cg_march<kMarchPQ, false, 3><<<b.march_grid, 64 * kMarchWaves, 0, st>>>(a);
+      k_cg_march<kMarchPQ, false, 3><<<b.march_grid, 64 * kMarchWaves, 0, st>>>(a);
       k_slab_publish<<<1, 64, 0, st>>>(D->S, D->buf.part_out);
       break;
     case PERC_DSLAB_COMBINE_PS:
@@ -6062,6 +5367,11 @@ hipError_t dev_spmv(perc_ctx* h, const double* x, double* y) {
 
 hipError_t dev_set_bond_weights(perc_ctx* h, const double* w) {
   DeviceBuffers& d = h->d;
+  // the assembled system (its stencil codes, rhs, the CSR copy ensure_csr
+  // would re-assemble from the current weights) no longer matches: assemble
+  // again before the next solve / system read
+  h->assembled = false;
+  h->csr_ok = false;
   if (!w) {
     h->has_weights = false;
     return hipSuccess;
@@ -6099,17 +5409,12 @@ hipError_t dev_bench(perc_ctx* h, int which, int reps, double* ms) {
   hs.itmax = 1 << 30;
   hs.iter = 1;
   a.kiter = 2;
-  // the deferred-reduction march takes its scalars (and the stop) from the
-  // previous kernel's partials, which a probe of one kernel alone does not
-  // keep meaningful: probes run the in-kernel reduction
-  struct DeferOff {
-    perc_ctx* h;
-    int was;
-    ~DeferOff() { h->march_defer = was; }
-  } defer_off{h, h->march_defer};
-  h->march_defer = 0;
-  // the solve's layout for the CG kernels (the plain SpMV probe stays row-major)
-  if (h->strips && (which == 1 || which == 2 || which == 5)) HIP_TRY(to_strips(h, a));
+  // the solve's layout and reductions for the CG kernels (the plain SpMV
+  // probe stays row-major): strip-major copies, tagged granules
+  if (h->strips && (which == 1 || which == 2 || which == 5)) {
+    HIP_TRY(to_strips(h, a));
+    HIP_TRY(setup_granules(h, a, hs.itmax));
+  }
   HIP_TRY(hipMemcpyAsync(d.scal, &hs, sizeof(hs), hipMemcpyHostToDevice, st));
   HIP_TRY(hipMemsetAsync(d.tickets, 0, kRedSlots * red_tickets_size(red_grid(h)) * sizeof(unsigned),
                          st));
@@ -6122,6 +5427,7 @@ hipError_t dev_bench(perc_ctx* h, int which, int reps, double* ms) {
     HIP_TRY(dmalloc(&cp_dst, cp_n));
     HIP_TRY(hipMemsetAsync(cp_src, 0, cp_n * sizeof(double), st));
   }
+  hipError_t lerr = hipSuccess;
   auto launch = [&]() {
     const int G = h->grid;
     if (which == 0) {
@@ -6141,8 +5447,10 @@ hipError_t dev_bench(perc_ctx* h, int which, int reps, double* ms) {
       int iters = 16;
       void* args[] = {&ra, &iters};
       (void)hipMemsetAsync(d.res_gran, 0, (size_t)2 * 3 * h->res_G * sizeof(double), st);
-      (void)hipLaunchCooperativeKernel((const void*)k_res_sync_probe, dim3(ra.G),
-                                       dim3(h->res_NT), args, 0, st);
+      // a refused grid (CUs taken) must not time an empty stream
+      const hipError_t le = hipLaunchCooperativeKernel((const void*)k_res_sync_probe, dim3(ra.G),
+                                                       dim3(h->res_NT), args, 0, st);
+      if (le != hipSuccess && lerr == hipSuccess) lerr = le;
     } else if (which == 5) {  // one whole iteration
       if (!h->fused) {
         if (ST) k_cg_p<true><<<G, kBlock, 0, st>>>(a);
@@ -6157,11 +5465,13 @@ hipError_t dev_bench(perc_ctx* h, int which, int reps, double* ms) {
   // the B kernel advances iter (tol < 0 keeps it running); values are
   // irrelevant for timing
   for (int i = 0; i < 3; ++i) launch();
+  HIP_TRY(lerr);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipEventRecord(h->ev[0], st));
   for (int i = 0; i < reps; ++i) launch();
   HIP_TRY(hipEventRecord(h->ev[1], st));
   HIP_TRY(hipEventSynchronize(h->ev[1]));
+  HIP_TRY(lerr);
   float t = 0.f;
   HIP_TRY(hipEventElapsedTime(&t, h->ev[0], h->ev[1]));
   *ms = (double)t / reps / (which == 6 ? 16 : 1);

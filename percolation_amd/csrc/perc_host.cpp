@@ -868,13 +868,54 @@ int perc_set_march_rows(perc_ctx* h, int rows) {
 }
 
 int perc_set_march_mode(perc_ctx* h, int mode) {
-  if (!h || mode < 0 || mode > (PERC_MARCH_QFREE | PERC_MARCH_ALT | PERC_MARCH_ROWS | PERC_SOLVE_RESIDENT |
-                                 PERC_MARCH_STRIPS | PERC_MARCH_DEFER | PERC_MARCH_SLOTS | PERC_MARCH_TAG |
-                                 PERC_MARCH_PERSIST))
-    return PERC_EINVAL;
+  constexpr int kAll = PERC_MARCH_QFREE | PERC_MARCH_ALT | PERC_SOLVE_RESIDENT | PERC_MARCH_STRIPS |
+                       PERC_MARCH_SLOTS | PERC_MARCH_TAG | PERC_MARCH_NIBBLE;
+  if (!h || (mode & ~kAll) != 0) return PERC_EINVAL;
   h->march_mode = mode;
+  march_geometry(h);  // band heights depend on PERC_MARCH_SLOTS
   if (h->assembled) select_format(h);
   return PERC_OK;
+}
+
+int perc_set_band_weights(perc_ctx* h, int which, int n, const int* w) {
+  if (!h || n < 0 || n > 4 || (n && (!w || which < 0 || which > 2))) return PERC_EINVAL;
+  for (int i = 0; i < n; ++i)
+    if (w[i] <= 0) return PERC_EINVAL;
+  if (n == 0) {
+    h->slot_w_set = false;
+  } else {
+    if (!h->slot_w_set) {  // start from the defaults
+      const int def[3][4] = {{100, 75, 50, 40}, {100, 80, 60, 50}, {100, 100, 100, 100}};
+      std::memcpy(h->slot_w, def, sizeof(def));
+    }
+    for (int i = 0; i < 4; ++i) h->slot_w[which][i] = i < n ? w[i] : h->slot_w[which][i];
+    h->slot_w_set = true;
+  }
+  march_geometry(h);
+  if (h->assembled) select_format(h);
+  return PERC_OK;
+}
+
+int perc_set_dot_order(perc_ctx* h, int order) {
+  if (!h || (order != PERC_DOT_FAST && order != PERC_DOT_LITERAL)) return PERC_EINVAL;
+  h->dot_order = order;
+  if (h->assembled) select_format(h);
+  return PERC_OK;
+}
+
+int perc_err_history(perc_ctx* h, double* out, int cap) {
+  if (!h || cap < 0 || (cap && !out)) return PERC_EINVAL;
+  if (!h->assembled) return PERC_ESTATE;
+  CGScalars hs{};
+  hipSetDevice(h->device);
+  hipError_t e = hipMemcpy(&hs, h->d.scal, sizeof(hs), hipMemcpyDeviceToHost);
+  if (e != hipSuccess) return hip_status(e, "perc_err_history");
+  const int n = std::min(std::min(hs.iter, cap), h->d.err_hist_cap);
+  if (n > 0 && h->d.err_hist) {
+    e = hipMemcpy(out, h->d.err_hist, sizeof(double) * n, hipMemcpyDeviceToHost);
+    if (e != hipSuccess) return hip_status(e, "perc_err_history");
+  }
+  return hs.iter;
 }
 
 int perc_set_bond_weights(perc_ctx* h, const double* w, long long n) {
@@ -886,14 +927,12 @@ int perc_set_bond_weights(perc_ctx* h, const double* w, long long n) {
 int perc_march_info(perc_ctx* h, int* out5) {
   if (!h || !out5) return PERC_EINVAL;
   if (!h->assembled) return PERC_ESTATE;
-  out5[0] = h->small ? 4
-                     : (h->resident && h->stencil ? 3
-                                                  : (h->rowmarch ? 2 : (h->march_persist ? 5 : (h->march ? 1 : 0))));
-  out5[1] = (h->qfree ? 1 : 0) | (h->strips ? 2 : 0) | (h->march_defer ? 4 : 0) |
-            (h->march_slots || h->march_slots_rm ? 8 : 0) | (h->march_tag ? 16 : 0);
+  out5[0] = h->small ? 4 : (h->resident && h->stencil ? 3 : (h->march ? 1 : 0));
+  out5[1] = (h->qfree ? 1 : 0) | (h->strips ? 2 : 0) | (h->march_slots || h->march_slots_rm ? 8 : 0) |
+            (h->march_tag ? 16 : 0) | (h->nib_used && h->strips ? 32 : 0);
   out5[2] = h->march_alt ? 1 : 0;
-  out5[3] = h->resident ? h->res_H : (h->rowmarch ? h->rm_h : (h->march ? h->march_h : 0));
-  out5[4] = h->resident ? h->g.m : (h->rowmarch ? h->rm_w : (h->march ? 128 : 0));
+  out5[3] = h->resident ? h->res_H : (h->march ? h->march_h : 0);
+  out5[4] = h->resident ? h->g.m : (h->march ? 128 : 0);
   return PERC_OK;
 }
 
@@ -902,7 +941,7 @@ int perc_matrix_format(perc_ctx* h) {
   if (!h->assembled) return PERC_ESTATE;
   if (!h->stencil) return PERC_FMT_CSR;
   if (!h->fused) return PERC_FMT_STENCIL_SPLIT;
-  return h->march || h->rowmarch ? PERC_FMT_STENCIL : PERC_FMT_STENCIL_TILED;
+  return h->march ? PERC_FMT_STENCIL : PERC_FMT_STENCIL_TILED;
 }
 
 int perc_selftest_division(long long n, unsigned long long seed, unsigned long long* out3) {

@@ -60,7 +60,6 @@ struct CGScalars {
   int done;      // set once err <= tol or iter > itmax
   int pad[3];
   double part[4];  // row slabs: this slab's raw partials (q.p, z.r, r.r, ||D^-1 b||^2)
-  double bkn[2];   // deferred-reduction march: bknum of iteration k in bkn[k & 1]
 };
 
 struct AsmParams {
@@ -84,6 +83,7 @@ struct DeviceBuffers {
   // if some slot has no bond (1) or a row matches no form (2)
   uint16_t* code = nullptr;  // N (+pad)
   uint16_t* code_sm = nullptr;  // strip-major copy of code (PERC_MARCH_STRIPS solves)
+  uint8_t* nib_sm = nullptr;    // strip-major nibble codes (PERC_MARCH_NIBBLE, square lattice)
   double2* dtab = nullptr;    // 512: the diagonal of every code (see diag_idx)
   int* sflag = nullptr;      // 4
   // occupancy
@@ -114,8 +114,7 @@ struct DeviceBuffers {
   int err_hist_cap = 0;
   double* iout = nullptr;       // 2m (boundary-row currents)
   double* bw = nullptr;         // per-bond conductance multipliers (ConductCalc condtype 2)
-  double* res_xch = nullptr;    // resident solve: exchange rows, partials
-  double* res_part = nullptr;
+  double* res_xch = nullptr;    // resident solve: exchange rows
   unsigned* res_bar = nullptr;
   double* res_gran = nullptr;   // resident solve: tagged partial granules
 };
@@ -179,22 +178,19 @@ struct perc_ctx {
   bool march_ok = false;        // register-march kernel usable (m % 128 == 0, tileable)
   bool march = false;           // fused format runs the register-march kernel
   int march_h = 32;             // its band height (rows per wave)
-  int march_depth = 3;          // rows its P+S kernel prefetches ahead
-  int march_bdepth = 3;         // rows the q-free march B prefetches ahead
-  int march_paux = 2;           // cache policy of the q-free P's p(k-1) loads (nontemporal)
-  int march_baux = 2;           // and of the q-free B's r(k) loads (nontemporal)
-  int march_saux = 2;           // the q-free march's p(k) / r(k+1) stores (nontemporal; probe)
-  int march_defer = 0;          // q-free strip-major march: reductions deferred to the next kernel
   int march_slots = 0;          // q-free strip-major march: slot-weighted bands
   int march_slots_rm = 0;       // q-free row-major march: slot-weighted bands for P
   int march_tag = 0;            // q-free strip-major march: tagged-granule reductions
-  int march_persist = 0;        // q-free strip-major march: one cooperative launch per solve
-  int march_hp = 0;             // row-major q-free P: own band height (probe; 0: march_h)
-  int march_hb = 0;             // strip-major q-free B: own band height (probe; 0: P's bands)
   unsigned solve_epoch = 0;     // tags of the granule reductions
   int wm_slots = 0;             // slot-weighted bands: workgroup rounds (0: not available)
   int wm_grid = 0;              // their grid (CUs x rounds)
   int wm_cum[3][5] = {};        // cumulative round weights (P, B, row-major P)
+  bool slot_w_set = false;      // perc_set_band_weights: weights instead of the defaults
+  int slot_w[3][4] = {};        // per round (P, B, row-major P)
+  int dot_order = PERC_DOT_FAST;  // perc_set_dot_order
+  bool nib_ok = false;          // square-lattice column classes known (nibble codes)
+  bool nib_used = false;        // the last strip-major solve ran the nibble codes
+  unsigned ncls[3] = {};        // their count / form bits: interior, first, last column
   int march_grid = 0;           // its workgroups
   int march_grid_max = 0;       // workgroups at band height 1 (reduction buffers)
   int march_rows_req = 0;       // perc_set_march_rows (0: auto)
@@ -202,15 +198,12 @@ struct perc_ctx {
   bool qfree = false;           // march B rebuilds q (52N / iteration)
   bool march_alt = false;       // alternating walk directions
   bool strips = false;          // march solve in the strip-major layout
-  bool rowmarch = false;        // workgroup row-march kernels (k_cg_rm)
   int b_grid = 0;               // streaming B workgroups in the fused formats (dev_build_lattice)
   bool has_weights = false;     // perc_set_bond_weights: G = -g0 w for the spanning bonds
   bool resident = false;        // persistent resident solve (k_cg_res)
   bool small = false;           // one-workgroup solve of a small system (k_cg_small)
   int res_G = 0, res_H = 0, res_MT = 0, res_HMAX = 0;  // its grid, band height, template
   int res_NT = 1024;            // its threads per workgroup (m rounded up to 64 for m < 1024)
-  int rm_w = 0, rm_h = 16;      // their strip width (columns) and band height
-  int rm_grid = 0;              // their workgroups
   bool full_voltages = false;   // perc_set_full_voltages: keep x on every row
   int nslab = 1;                // perc_set_slabs: row slabs of the CG solve
   perc::DSlab* dslab = nullptr;  // perc_dslab_*: this process's slab of a distributed solve

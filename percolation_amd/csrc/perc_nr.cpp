@@ -36,6 +36,7 @@ int* g_ija = nullptr;
 int g_nmax = kNmaxDefault;
 int g_status = PERC_OK;
 perc_ctx* g_nr = nullptr;  // matrix-only device context
+int g_nr_dot = PERC_DOT_LITERAL;  // perc_nr_set_dot_order
 
 }  // namespace
 
@@ -118,6 +119,7 @@ int upload(int n, const std::vector<int>& rowptr, const std::vector<int>& col,
     if (e != hipSuccess) return hip_status(e, "nr upload");
   }
   g_nr->nnz = (long long)col.size();
+  g_nr->dot_order = g_nr_dot;
   hipError_t e = hipMemcpy(g_nr->d.rowptr, rowptr.data(), sizeof(int) * (n + 1),
                            hipMemcpyHostToDevice);
   if (e == hipSuccess && !col.empty())
@@ -150,6 +152,12 @@ void perc_nr_bind(double* sa, int* ija, int nmax) {
 }
 
 int perc_nr_status(void) { return g_status; }
+int perc_nr_set_dot_order(int order) {
+  if (order != PERC_DOT_FAST && order != PERC_DOT_LITERAL) return PERC_EINVAL;
+  std::lock_guard<std::mutex> lk(g_nr_mu);
+  g_nr_dot = order;
+  return PERC_OK;
+}
 // the same for F77 callers (implicit interface: integer perc_nr_status)
 int perc_nr_status_(void) { return g_status; }
 

@@ -542,19 +542,16 @@ def test_large_vector_grids_8192():
     assert rel(c["gtop"], c["gbot"]) < 1e-5
 
 
-MARCH_MODES = (PL.MARCH_DEFAULT, 0, PL.MARCH_QFREE, PL.MARCH_ALT, PL.MARCH_ROWS,
-               PL.MARCH_ROWS | PL.MARCH_QFREE, PL.MARCH_ROWS | PL.MARCH_ALT,
-               PL.MARCH_ROWS | PL.MARCH_QFREE | PL.MARCH_ALT, PL.MARCH_STRIPS,
-               PL.MARCH_STRIPS | PL.MARCH_QFREE, PL.MARCH_STRIPS | PL.MARCH_ALT,
-               PL.MARCH_STRIPS | PL.MARCH_QFREE | PL.MARCH_ALT,
-               PL.MARCH_STRIPS | PL.MARCH_QFREE | PL.MARCH_ALT | PL.MARCH_DEFER,
+MARCH_MODES = (PL.MARCH_DEFAULT, 0, PL.MARCH_QFREE, PL.MARCH_ALT, PL.MARCH_QFREE | PL.MARCH_ALT,
+               PL.MARCH_STRIPS | PL.MARCH_QFREE, PL.MARCH_STRIPS | PL.MARCH_QFREE | PL.MARCH_ALT,
                PL.MARCH_STRIPS | PL.MARCH_QFREE | PL.MARCH_ALT | PL.MARCH_SLOTS,
-               PL.MARCH_STRIPS | PL.MARCH_QFREE | PL.MARCH_ALT | PL.MARCH_TAG)
+               PL.MARCH_STRIPS | PL.MARCH_QFREE | PL.MARCH_ALT | PL.MARCH_TAG,
+               PL.MARCH_STRIPS | PL.MARCH_QFREE | PL.MARCH_ALT | PL.MARCH_TAG | PL.MARCH_NIBBLE)
 
 
 @pytest.mark.parametrize("lat,m,n,pbc,p", [(0, 256, 150, 0, 0.6), (1, 128, 99, 1, 0.42),
                                            (0, 384, 40, 1, 0.55),
-                                           # workgroup row-march strips of 512 / 1024 / 2048
+                                           # wide lattices, few rows
                                            (0, 1536, 40, 1, 0.55), (1, 1024, 45, 0, 0.42),
                                            (0, 2048, 21, 0, 0.6), (1, 512, 70, 1, 0.42)])
 def test_march_band_heights(lat, m, n, pbc, p):
@@ -618,13 +615,12 @@ def test_march_modes_one_iteration_bitwise(lat, m, n, pbc, p):
 
 @pytest.mark.parametrize("lat,m,n,pbc,p", [(0, 512, 512, 0, 0.6), (1, 384, 300, 0, 0.42),
                                            (0, 1024, 1024, 0, 0.55), (0, 256, 160, 1, 0.6)])
-def test_deferred_reduction_is_bitwise_the_in_kernel_one(lat, m, n, pbc, p):
-    """PERC_MARCH_DEFER (the strip-major q-free march whose dot products
-    are summed by every workgroup of the next kernel) and PERC_MARCH_TAG
-    (tagged-granule partials, no store drain before the tickets): the same
-    totals term for term as the last-arriving-workgroup reduction, so the
-    whole solve -- iteration count, err history, Gtop, Gbot, every voltage
-    -- is bitwise the same, at the reference tolerance and converged."""
+def test_tagged_reduction_is_bitwise_the_ticket_one(lat, m, n, pbc, p):
+    """PERC_MARCH_TAG (tagged-granule partials, no store drain before the
+    tickets): the same totals term for term as the last-arriving-workgroup
+    reduction, so the whole solve -- iteration count, err history, Gtop,
+    Gbot, every voltage -- is bitwise the same, at the reference tolerance
+    and converged."""
     nb = api.nbonds(lat, m, n, pbc)
     order = api.shuffled_ids(nb, 2718)
     base = PL.MARCH_QFREE | PL.MARCH_ALT | PL.MARCH_STRIPS  # the march, not the resident solve
@@ -634,16 +630,17 @@ def test_deferred_reduction_is_bitwise_the_in_kernel_one(lat, m, n, pbc, p):
             pytest.skip("no spanning cluster")
         for tol in (1e-8, 1e-13):
             out = []
-            for mode in (base, base | PL.MARCH_DEFER, base | PL.MARCH_TAG):
+            for mode in (base, base | PL.MARCH_TAG):
                 ctx.set_march_mode(mode)
                 c = ctx.conductance(tol=tol, itmax=10 ** 6, vint=True)
+                c["hist"] = ctx.err_history()
                 info = ctx.march_info()
-                assert info["kernel"] == "wave" and info["defer"] == bool(mode & PL.MARCH_DEFER)
-                assert info["tag"] == bool(mode & PL.MARCH_TAG)
+                assert info["kernel"] == "wave" and info["tag"] == bool(mode & PL.MARCH_TAG)
                 out.append(c)
             a = out[0]
             for b in out[1:]:
                 assert a["iter"] == b["iter"] and a["err"] == b["err"], (tol, a["iter"], b["iter"])
+                assert np.array_equal(a["hist"].view(np.uint64), b["hist"].view(np.uint64))
                 assert a["gtop"] == b["gtop"] and a["gbot"] == b["gbot"], tol
                 assert np.array_equal(a["vint"].view(np.uint64), b["vint"].view(np.uint64))
         ctx.set_march_mode(PL.MARCH_DEFAULT)
@@ -658,36 +655,66 @@ def test_slot_weighted_bands_solve_the_same_system(lat, m, n, pbc, p):
     the solve is the static march's up to the dot products' association --
     iteration count within 2, Gtop / Gbot to the solver tolerance, the
     voltages -- for the default weights and extreme ones."""
-    import os
     nb = api.nbonds(lat, m, n, pbc)
     order = api.shuffled_ids(nb, 1618)
     base = PL.MARCH_QFREE | PL.MARCH_ALT | PL.MARCH_STRIPS
     out = []
-    for mode, w in ((base, None), (base | PL.MARCH_SLOTS, None), (base | PL.MARCH_SLOTS, "100:30:5"),
-                    (base | PL.MARCH_SLOTS, "1:1:400")):
-        if w:
-            os.environ["PERC_MARCH_SLOTW"] = os.environ["PERC_MARCH_SLOTWB"] = w
-        try:
-            with api.Context(lat, m, n, pbc) as ctx:  # (weights are read with the lattice)
-                ctx.occupy(PL.BOND, bond_order=order, nbonds_=int(p * nb))
-                if ctx.label()["nspan"] == 0:
-                    pytest.skip("no spanning cluster")
-                ctx.set_march_mode(mode)
-                out.append(ctx.conductance(tol=1e-12, itmax=200000, vint=True))
-                info = ctx.march_info()
-                assert info["kernel"] == "wave"
-                if not mode & PL.MARCH_SLOTS:
-                    assert not info["slots"]
-                elif (m, n) in ((1024, 1024), (2048, 2048)):
-                    assert info["slots"]  # (fewer rows than one round of bands: static)
-        finally:
-            os.environ.pop("PERC_MARCH_SLOTW", None)
-            os.environ.pop("PERC_MARCH_SLOTWB", None)
+    for mode, w in ((base, None), (base | PL.MARCH_SLOTS, None), (base | PL.MARCH_SLOTS, (100, 30, 5)),
+                    (base | PL.MARCH_SLOTS, (1, 1, 400))):
+        with api.Context(lat, m, n, pbc) as ctx:
+            if w:  # perc_set_band_weights: P and B
+                ctx.set_band_weights(0, w)
+                ctx.set_band_weights(1, w)
+            ctx.occupy(PL.BOND, bond_order=order, nbonds_=int(p * nb))
+            if ctx.label()["nspan"] == 0:
+                pytest.skip("no spanning cluster")
+            ctx.set_march_mode(mode)
+            out.append(ctx.conductance(tol=1e-12, itmax=200000, vint=True))
+            info = ctx.march_info()
+            assert info["kernel"] == "wave"
+            if not mode & PL.MARCH_SLOTS:
+                assert not info["slots"]
+            elif (m, n) in ((1024, 1024), (2048, 2048)):
+                assert info["slots"]  # (fewer rows than one round of bands: static)
     a = out[0]
     for b in out[1:]:
         assert abs(a["iter"] - b["iter"]) <= 2, (a["iter"], b["iter"])
         assert rel(b["gtop"], a["gtop"]) < REL and rel(b["gbot"], a["gbot"]) < REL
         assert np.max(np.abs(b["vint"] - a["vint"])) < 1e-6
+
+
+@pytest.mark.parametrize("lat,m,n,pbc,p", [(0, 512, 512, 0, 0.6), (0, 256, 160, 1, 0.6),
+                                           (0, 1024, 1024, 0, 0.55), (0, 128, 1400, 0, 0.6),
+                                           (0, 384, 200, 1, 0.5)])
+def test_nibble_codes_are_bitwise_the_u16_codes(lat, m, n, pbc, p):
+    """PERC_MARCH_NIBBLE (the strip-major march reads one 4-bit slot mask per
+    site, count and form from the column class): the codes it rebuilds are
+    the u16 codes (k_pack_nib checks every row), so the whole solve --
+    iteration count, err history, Gtop, Gbot, every voltage -- is bitwise
+    the u16-code solve's."""
+    nb = api.nbonds(lat, m, n, pbc)
+    order = api.shuffled_ids(nb, 2207)
+    base = PL.MARCH_DEFAULT & ~PL.SOLVE_RESIDENT  # the march, not the resident solve
+    with api.Context(lat, m, n, pbc) as ctx:
+        ctx.occupy(PL.BOND, bond_order=order, nbonds_=int(p * nb))
+        if ctx.label()["nspan"] == 0:
+            pytest.skip("no spanning cluster")
+        for tol in (1e-8, 1e-13):
+            out = []
+            for mode in (base, base & ~PL.MARCH_NIBBLE):
+                ctx.set_march_mode(mode)
+                c = ctx.conductance(tol=tol, itmax=10 ** 6, vint=True)
+                c["hist"] = ctx.err_history()
+                info = ctx.march_info()
+                assert info["kernel"] == "wave" and info["strips"], info
+                assert info["nibble"] == bool(mode & PL.MARCH_NIBBLE), info
+                out.append(c)
+            a, b = out
+            assert a["iter"] == b["iter"] and a["err"] == b["err"], (tol, a["iter"], b["iter"])
+            assert np.array_equal(a["hist"].view(np.uint64), b["hist"].view(np.uint64))
+            assert a["gtop"] == b["gtop"] and a["gbot"] == b["gbot"], tol
+            assert np.array_equal(a["vint"].view(np.uint64), b["vint"].view(np.uint64))
+        ctx.set_march_mode(PL.MARCH_DEFAULT)
 
 
 def test_table_division_is_ieee_division():
@@ -892,40 +919,3 @@ def test_closed_form_assembly_is_the_general_one(kind, rule, m, n, pbc, monkeypa
     assert (c0["gtop"], c0["gbot"], c0["iter"]) == (c1["gtop"], c1["gbot"], c1["iter"])
 
 
-@pytest.mark.parametrize("lat,m,n,pbc,p", [(0, 512, 800, 0, 0.6), (1, 1024, 400, 0, 0.42),
-                                           (0, 2048, 300, 1, 0.55), (0, 1024, 1024, 0, 0.55),
-                                           (1, 4096, 120, 1, 0.42)])
-def test_persistent_march_is_bitwise_the_launched_one(lat, m, n, pbc, p):
-    """PERC_MARCH_PERSIST (the whole q-free march loop in one cooperative
-    launch, cross-workgroup rows stored write-through and loaded sc1): with
-    the launched march on the same bands (the B kernel given the P kernel's
-    slot weights) every iterate is the same, so the iteration count, err,
-    Gtop, Gbot and every voltage are bitwise equal, at the reference
-    tolerance and converged (Square/bondc.f:780-836)."""
-    import os
-    nb = api.nbonds(lat, m, n, pbc)
-    order = api.shuffled_ids(nb, 3141)
-    base = PL.MARCH_QFREE | PL.MARCH_ALT | PL.MARCH_STRIPS | PL.MARCH_SLOTS | PL.MARCH_TAG
-    os.environ["PERC_MARCH_SLOTWB"] = "100:75:50"  # the persistent kernel's bands (P's weights)
-    try:
-        with api.Context(lat, m, n, pbc) as ctx:
-            ctx.occupy(PL.BOND, bond_order=order, nbonds_=int(p * nb))
-            if ctx.label()["nspan"] == 0:
-                pytest.skip("no spanning cluster")
-            for tol in (1e-8, 1e-13):
-                out = []
-                for mode in (base, base | PL.MARCH_PERSIST):
-                    ctx.set_march_mode(mode)
-                    for vint in (True, False):
-                        c = ctx.conductance(tol=tol, itmax=10 ** 6, vint=vint)
-                        info = ctx.march_info()
-                        assert info["kernel"] == ("persistent" if mode & PL.MARCH_PERSIST else "wave"), info
-                        out.append(c)
-                for a, b in ((out[0], out[2]), (out[1], out[3])):
-                    assert a["iter"] == b["iter"] and a["err"] == b["err"], (tol, a["iter"], b["iter"])
-                    assert a["gtop"] == b["gtop"] and a["gbot"] == b["gbot"], tol
-                a, b = out[0], out[2]
-                assert np.array_equal(a["vint"].view(np.uint64), b["vint"].view(np.uint64))
-            ctx.set_march_mode(PL.MARCH_DEFAULT)
-    finally:
-        del os.environ["PERC_MARCH_SLOTWB"]

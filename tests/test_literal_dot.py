@@ -1,0 +1,128 @@
+"""The literal dot order on the GPU (perc_set_dot_order(h, PERC_DOT_LITERAL)).
+
+linbcg sums its three dot products term after term in ascending j --
+bknum (Square/bondc.f:785-787), akden (:803-805), snrm's sum of squares
+(:872-875, bnrm :768-770).  Every other operation of an iteration is
+already the reference's on the GPU (per-row bitwise: test_gpu_parity.py's
+assembly / SpMV / march-mode tests), so with the sums folded in that order
+the whole solve must be the reference solver's BITWISE: iteration count,
+the per-iteration err history (`write (*,*) iter, err`, :834), every
+interior voltage, Gtop and Gbot.  That pins the remaining difference of the
+default solve to the association of the three sums alone.
+
+Pins: every reference bondc golden (tests/golden/*bondc*, made by the
+compiled reference, square / triangular / pbc / tight tolerance) in every
+solver family that folds (one-workgroup, LDS-tiled, split stencil, CSR),
+and the oracle's literal linbcg (oracle/perc_oracle.c, itself bitwise the
+reference at <= 64^2) at 128^2 .. 256^2 through the register-march kernels.
+"""
+import numpy as np
+import pytest
+
+import golden_io as G
+import oracle_lib as O
+from percolation_amd import _lib as PL
+from percolation_amd import api
+
+pytestmark = pytest.mark.gpu
+
+BONDC = [v for v in G.variants() if G.meta(v)["kind"] == "bondc" and G.meta(v)["perccln"]]
+# PERC_FMT_AUTO runs the one-workgroup solver at these sizes (k_cg_small<LIT>)
+FAMILIES = [PL.FMT_AUTO, PL.FMT_STENCIL_TILED, PL.FMT_STENCIL_SPLIT, PL.FMT_CSR]
+
+
+def bits(a):
+    return np.ascontiguousarray(a, dtype=np.float64).view(np.uint64)
+
+
+@pytest.mark.parametrize("fmt", FAMILIES)
+@pytest.mark.parametrize("v", BONDC)
+def test_literal_solve_is_the_reference_bitwise(v, fmt):
+    md = G.meta(v)
+    p = md["params"]
+    tol, itmax = p.get("tol", 1e-8), p.get("itmax", 2500)
+    with api.Context(p["lattice"], p["m"], p["n"], p["pbc"]) as ctx:
+        ctx.set_dot_order(PL.DOT_LITERAL)
+        ctx.set_matrix_format(fmt)
+        try:
+            r = api.bondc(p["lattice"], p["m"], p["n"], p["pbc"], p["pb"], p["seed"], tol=tol,
+                          itmax=itmax, ctx=ctx)
+        except PL.PercError as e:  # this lattice has no such operator (e.g. odd m, tiles)
+            pytest.skip(str(e))
+        hist = ctx.err_history()
+        c = ctx.conductance(tol=tol, itmax=itmax, vint=True)
+    assert r["perccln"] == md["perccln"]
+    assert r["iter"] == md["iter"], (r["iter"], md["iter"])
+    assert np.array_equal(bits(hist), bits(md["linbcg_err"]))
+    assert r["gtop"] == md["gtop"] and r["gbot"] == md["gbot"], (r["gtop"], r["gbot"])
+    assert (c["gtop"], c["gbot"], c["iter"]) == (r["gtop"], r["gbot"], r["iter"])
+    if "vint" in md:
+        assert np.array_equal(bits(c["vint"]), bits(md["vint"]))
+
+
+@pytest.mark.parametrize("fmt", [PL.FMT_AUTO, PL.FMT_STENCIL, PL.FMT_CSR])
+@pytest.mark.parametrize("lat,m,n,pbc,p,seed", [(0, 128, 128, 0, 0.6, 21), (0, 256, 150, 0, 0.55, 31),
+                                                 (1, 128, 99, 0, 0.4, 22), (0, 256, 256, 1, 0.6, 32)])
+def test_literal_solve_is_the_oracle_linbcg_bitwise(lat, m, n, pbc, p, seed, fmt):
+    """Larger lattices, m a multiple of 128: the q-storing register march
+    (PERC_FMT_STENCIL; PERC_FMT_AUTO takes it too -- the resident solve has
+    no literal fold) and CSR, against the oracle's literal linbcg at the
+    reference tolerance and converged: iter, err history, Gtop, Gbot and
+    every voltage bitwise."""
+    b1, b2 = api.bond_list(lat, m, n, pbc)
+    nb = len(b1)
+    order = api.shuffled_ids(nb, seed)
+    tb = int(p * nb)
+    ref = api.replay_labels(lat, m, n, pbc, PL.BOND, bond_order=order, nbond=tb)
+    assert ref["perccln"] > 0
+    gval = O.f64(nb)
+    O.lib().or_bond_values(0, nb, b1, b2, ref["bond_label"], O.i32(1), ref["perccln"], 1.0, 1e-12,
+                           gval)
+    with api.Context(lat, m, n, pbc) as ctx:
+        ctx.set_dot_order(PL.DOT_LITERAL)
+        ctx.set_matrix_format(fmt)
+        ctx.occupy(PL.BOND, bond_order=order, nbonds_=tb)
+        ctx.label()
+        for tol in (1e-8, 1e-13):
+            oc = O.conductance(lat, m, n, pbc, b1, b2, gval, tol=tol, itmax=100000)
+            c = ctx.conductance(tol=tol, itmax=100000, vint=True)
+            hist = ctx.err_history()
+            info = ctx.march_info()
+            if fmt != PL.FMT_CSR and m % 128 == 0:
+                assert info["kernel"] == "wave" and not info["qfree"], info
+            assert c["iter"] == oc["iter"], (tol, c["iter"], oc["iter"])
+            assert np.array_equal(bits(hist), bits(oc["errs"])), tol
+            assert c["gtop"] == oc["gtop"] and c["gbot"] == oc["gbot"], (tol, c["gtop"], oc["gtop"])
+            assert np.array_equal(bits(c["vint"]), bits(oc["vint"])), tol
+
+
+def test_literal_and_fast_orders_differ_by_association_only():
+    """The same system in both orders at a converged tolerance: the same
+    answer to 1e-10 (only the three sums' association differs), and the
+    fast order comes back when asked for."""
+    lat, m, n, pbc, p, seed = 0, 256, 200, 0, 0.6, 41
+    nb = api.nbonds(lat, m, n, pbc)
+    order = api.shuffled_ids(nb, seed)
+    with api.Context(lat, m, n, pbc) as ctx:
+        ctx.occupy(PL.BOND, bond_order=order, nbonds_=int(p * nb))
+        ctx.label()
+        fast = ctx.conductance(tol=1e-14, itmax=100000)
+        ctx.set_dot_order(PL.DOT_LITERAL)
+        lit = ctx.conductance(tol=1e-14, itmax=100000)
+        ctx.set_dot_order(PL.DOT_FAST)
+        again = ctx.conductance(tol=1e-14, itmax=100000)
+    assert abs(lit["gtop"] - fast["gtop"]) < 1e-10 * fast["gtop"]
+    assert abs(lit["gbot"] - fast["gbot"]) < 1e-10 * fast["gbot"]
+    assert (again["gtop"], again["gbot"], again["iter"]) == (fast["gtop"], fast["gbot"], fast["iter"])
+
+
+def test_literal_order_needs_one_slab():
+    lat, m, n = 0, 256, 64
+    nb = api.nbonds(lat, m, n, 0)
+    with api.Context(lat, m, n, 0) as ctx:
+        ctx.occupy(PL.BOND, bond_order=api.shuffled_ids(nb, 5), nbonds_=int(0.65 * nb))
+        ctx.label()
+        ctx.set_dot_order(PL.DOT_LITERAL)
+        ctx.set_slabs(2)
+        with pytest.raises(PL.PercError):
+            ctx.conductance(tol=1e-8, itmax=10000)

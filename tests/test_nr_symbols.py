@@ -154,14 +154,15 @@ def test_nr_symbols_from_fortran(tmp_path):
     v = np.frombuffer(raw[16:], np.float64)
     assert st == 0
     md = G.meta("sq_bondc_p60")
-    assert abs(int(it) - md["iter"]) <= 1 and err <= 1e-8
-    assert np.max(np.abs(v - np.array(md["vint"]))) < 1e-6
+    # linbcg_ folds its dot products in the reference's order by default
+    # (perc_nr_set_dot_order): the reference's own solve, bitwise
+    assert int(it) == md["iter"] and err == md["linbcg_err"][-1], (it, err)
+    assert np.array_equal(bits(v), bits(np.array(md["vint"])))
     gt, gb = C.c_double(), C.c_double()
     O.lib().or_currents(0, 50, 50, 0, len(big["b1"]), big["b1"], big["b2"], big["gval"],
                         big["diag"], np.ascontiguousarray(v), 1.0, 1e-10, 0, C.byref(gt),
                         C.byref(gb))
-    assert abs(gt.value - md["gtop"]) <= 1e-10 * md["gtop"]
-    assert abs(gb.value - md["gbot"]) <= 1e-6 * md["gbot"]
+    assert gt.value == md["gtop"] and gb.value == md["gbot"], (gt.value, gb.value)
 
 
 def test_route1_relink_of_the_reference_program():
