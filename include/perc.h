@@ -311,6 +311,24 @@ int perc_dslab_begin(perc_ctx *h, int K, int s, int itol, double tol, int itmax,
 int perc_dslab_step(perc_ctx *h, int op);
 int perc_dslab_status(perc_ctx *h, int *iter, double *err, int *done);
 int perc_dslab_end(perc_ctx *h);
+/* The whole split solve from one host process, no caller code inside the
+   loop: K labeled contexts (the same lattice and occupancy, context s on
+   its own device for RCCL) solve row slab s each, one host thread per
+   context issuing its slab's loop onto the context's stream.  xport
+   PERC_XPORT_RCCL: ncclCommInitAll over the contexts' devices, the
+   partials all-gathered and the r halo swapped by ncclAllGather /
+   ncclSend / ncclRecv on the streams (no host round trip inside the loop);
+   PERC_XPORT_HOST: the same exchanges staged through host memory (any
+   devices, several contexts on one GPU included).  The numbers are
+   perc_set_slabs(K)'s in one context bitwise.  Assembles every context
+   (perc_assemble), solves, and returns Gtop / Gbot from slab 0 in *res
+   (status 1: nothing spans).  Replaces the linbcg call of
+   Fortran/Square/bondc.f:545 for a lattice split over GPUs. */
+#define PERC_XPORT_RCCL 0
+#define PERC_XPORT_HOST 1
+int perc_dslab_solve_group(int K, perc_ctx **ctxs, int xport, int rule, int cur_rule, double Va,
+                           double g0, double leak, int itol, double tol, int itmax, int full_x,
+                           perc_cond_result *res);
 /* assembly only (perc_conductance's first half): the Kirchhoff system of
    the lowest spanning cluster; PERC_ESTATE before perc_label, status 1 in
    *spanning = 0 when nothing spans */

@@ -30,6 +30,7 @@ MARCH_NIBBLE = 512
 MARCH_DEFAULT = (MARCH_QFREE | MARCH_ALT | SOLVE_RESIDENT | MARCH_STRIPS | MARCH_SLOTS | MARCH_TAG
                  | MARCH_NIBBLE)
 DOT_FAST, DOT_LITERAL = 0, 1
+XPORT_RCCL, XPORT_HOST = 0, 1
 
 
 class LabelInfo(C.Structure):
@@ -110,6 +111,9 @@ SIGNATURES = {
     "perc_dslab_status": (C.c_int, [_VP, C.POINTER(C.c_int), C.POINTER(C.c_double),
                                     C.POINTER(C.c_int)]),
     "perc_dslab_end": (C.c_int, [_VP]),
+    "perc_dslab_solve_group": (C.c_int, [C.c_int, _VP, C.c_int, C.c_int, C.c_int, C.c_double,
+                                         C.c_double, C.c_double, C.c_int, C.c_double, C.c_int,
+                                         C.c_int, _VP]),
     "perc_assemble": (C.c_int, [_VP, C.c_int, C.c_double, C.c_double, C.c_double,
                                 C.POINTER(C.c_int)]),
     "perc_x_row": (C.c_int, [_VP, C.c_int, _VP, C.c_int]),

@@ -317,6 +317,20 @@ class Context:
 
 
 # ---------------------------------------------------------------- programs
+def dslab_solve_group(ctxs, xport=L.XPORT_RCCL, rule=L.RULE_BOND, cur_rule=L.CUR_FORTRAN, Va=1.0,
+                      g0=1.0, leak=LEAK, itol=2, tol=1e-8, itmax=2500, full_x=False):
+    """One solve split over the labeled contexts `ctxs` (slab s on ctxs[s]),
+    the whole loop inside libperc: perc_dslab_solve_group (RCCL over the
+    contexts' devices, or staged through the host)."""
+    K = len(ctxs)
+    arr = (C.c_void_p * K)(*[c.h for c in ctxs])
+    res = L.CondResult()
+    L.check(L.lib().perc_dslab_solve_group(K, arr, int(xport), rule, cur_rule, Va, g0, leak, itol,
+                                           tol, itmax, int(full_x), C.byref(res)),
+            "perc_dslab_solve_group")
+    return {k: getattr(res, k) for k, _ in L.CondResult._fields_}
+
+
 def bondc(lattice=0, m=50, n=50, pbc=0, pb=0.50, seed=626504, Va=1.0, g0=1.0, tol=1e-8,
           itmax=2500, labels=True, ctx=None, device=0):
     """One bond realisation filled to pb, spanning test, conductance

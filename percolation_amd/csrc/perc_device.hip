@@ -1236,6 +1236,17 @@ __global__ void k_currents(Geom g, const int* bond_first, const uint8_t* bocc,
   iout[idx] = acc;
 }
 
+// Buffer access with a hardware range check: a byte offset at or past the
+// buffer's size makes a load return 0 and drops a store (the march and the
+// pipelined SpMV keep their memory instructions unconditional this way).
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+constexpr unsigned kOOB = 0x80000000u;  // buffers are kept below 2 GB (march_geometry)
+constexpr int kNT = 2;                  // aux bits: nontemporal
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* p, unsigned bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, (int)bytes, 0x00020000);
+}
+
 // ---------------------------------------------------------------------------
 // CSR SpMV, one wave per 64-row tile, entries staged through LDS.
 //   y(i) = d(i)*x(i) + sum_k val(k)*x(col(k))   (dsprsax, bondc.f:887-899)
@@ -1251,6 +1262,7 @@ struct CsrView {
   const int* col;
   const double* val;
   const double* diag;
+  int maxrow;  // most off-diagonals in one row (<= kMaxNnzRow: the pipelined kernel)
 };
 
 constexpr int kMaxNnzRow = 6;
@@ -1338,6 +1350,102 @@ __device__ __forceinline__ void spmv_tiles(const CsrView& A, const double* __res
   }
 }
 
+// LDS hand-off inside one wave without a memory fence: a wave's LDS
+// instructions execute in order, so the compiler barrier alone orders the
+// product stores before the row sums' loads (a release fence would also
+// wait for the prefetched global loads: vmcnt(0))
+__device__ __forceinline__ void wave_lds_order() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_wave_barrier();
+  asm volatile("" ::: "memory");
+}
+
+// The same tiles software-pipelined (every row <= kMaxNnzRow off-diagonals,
+// so a tile's entries fit the LDS stage): while tile t forms its gathers,
+// products and row sums, the (col, val) entries of tile t + stride and the
+// row pointers of tile t + 2 stride are already in flight -- three memory
+// round trips of a tile (row pointers, entries, gathers) overlap instead of
+// following one another.  Every load is unconditional (clamped indices), so
+// the waits count exactly.  Per row the arithmetic is spmv_tile's: y(i) =
+// d(i) x(i), then the products in ascending column order (bitwise dsprsax).
+struct CsrStage {
+  int a, b;  // this lane's row range
+  int c[kMaxNnzRow];
+  double v[kMaxNnzRow];
+};
+__device__ __forceinline__ void csr_rowptr(const CsrView& A, int tile, int& a, int& b) {
+  const int r = min(tile * 64 + (int)(threadIdx.x & 63), A.N - 1);
+  a = A.rowptr[r];
+  b = A.rowptr[r + 1];
+}
+__device__ __forceinline__ void csr_entries(const CsrView& A, int tile, CsrStage& S) {
+  const int lane = threadIdx.x & 63, r0 = tile * 64;
+  const int last = min(63, A.N - 1 - r0);
+  const int e0 = __shfl(S.a, 0, 64);
+  const int jmax = max(__shfl(S.b, last, 64) - e0 - 1, 0);
+  // the columns first: the next tile's gathers wait for them only
+#pragma unroll
+  for (int s = 0; s < kMaxNnzRow; ++s) S.c[s] = A.col[e0 + min(lane + 64 * s, jmax)];
+#pragma unroll
+  for (int s = 0; s < kMaxNnzRow; ++s) S.v[s] = A.val[e0 + min(lane + 64 * s, jmax)];
+}
+template <bool DOT>
+__device__ __forceinline__ void spmv_tiles_pipe(const CsrView& A, const double* __restrict__ x,
+                                                double* __restrict__ y, int tile0, int t1, int stride,
+                                                double* s_prod, double* dot) {
+  const int lane = threadIdx.x & 63;
+  if (tile0 >= t1) return;
+  const __amdgpu_buffer_rsrc_t ry = rsrc(y, (unsigned)A.N * 8u);
+  // two stages that swap roles every tile (unrolled by two: no register
+  // copies of loads in flight, which would wait for them)
+  CsrStage s0, s1;
+  csr_rowptr(A, tile0, s0.a, s0.b);
+  csr_entries(A, tile0, s0);
+  csr_rowptr(A, min(tile0 + stride, t1 - 1), s1.a, s1.b);
+  // tile `tile` from `cur`; the next tile's entries into `nxt` (its row
+  // pointers are there already), the row pointers of the one after into
+  // (an, bn)
+  auto step = [&](int tile, CsrStage& cur, CsrStage& nxt, int& an, int& bn) {
+    // (tile >= t1: the unrolled loop's padding step -- cur holds the last
+    // tile again, every lane invalid, nothing stored)
+    const int r0 = min(tile, t1 - 1) * 64, r = r0 + lane;
+    const bool valid = r < A.N && tile < t1;
+    const int rr = valid ? r : A.N - 1;
+    // this tile's row range, before (an, bn) -- cur's own row pointers when
+    // the stages alternate -- receive the tile after next
+    const int e0 = __shfl(cur.a, 0, 64);
+    const int k0 = cur.a - e0, kn = cur.b - cur.a;
+    double xv[kMaxNnzRow];
+#pragma unroll
+    for (int s = 0; s < kMaxNnzRow; ++s) xv[s] = x[cur.c[s]];
+    const double xi = x[rr], di = A.diag[rr];
+    csr_entries(A, min(tile + stride, t1 - 1), nxt);  // (past the last tile: unused)
+    csr_rowptr(A, min(tile + 2 * stride, t1 - 1), an, bn);
+    // every load of the step is issued before the first product waits for
+    // a gather (the scheduler would otherwise interleave them)
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int s = 0; s < kMaxNnzRow; ++s) s_prod[lane + 64 * s] = cur.v[s] * xv[s];
+    wave_lds_order();
+    // the row's products in order, a fixed unrolled count with selects (no
+    // lane-divergent loop, no branch around the store: exact waits)
+    double acc = di * xi;
+#pragma unroll
+    for (int j = 0; j < kMaxNnzRow; ++j) {
+      const double pj = s_prod[min(k0 + j, 64 * kMaxNnzRow - 1)];
+      acc = j < kn ? acc + pj : acc;
+    }
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, acc), ry,
+                                          valid ? r * 8 : (int)kOOB, 0, 0);
+    if (DOT) *dot = valid ? *dot + acc * xi : *dot;
+    wave_lds_order();  // s_prod reused by the next tile
+  };
+  for (int tile = tile0; tile < t1; tile += 2 * stride) {  // (no exit between the steps)
+    step(tile, s0, s1, s0.a, s0.b);
+    step(tile + stride, s1, s0, s1.a, s1.b);
+  }
+}
+
 // wave tiles [t0, t1) of a logical block, strided over its 4 waves
 __device__ __forceinline__ void block_tiles(int N, int* t0, int* t1) {
   const int ntile = cdiv(N, 64);
@@ -1354,7 +1462,8 @@ __global__ __launch_bounds__(kBlock) void k_spmv(CsrView A, const double* __rest
   int t0, t1;
   block_tiles(A.N, &t0, &t1);
   double dummy = 0.0;
-  spmv_tiles<false>(A, x, y, t0 + wid, t1, kWaves, s_prod[wid], &dummy);
+  if (A.maxrow <= kMaxNnzRow) spmv_tiles_pipe<false>(A, x, y, t0 + wid, t1, kWaves, s_prod[wid], &dummy);
+  else spmv_tiles<false>(A, x, y, t0 + wid, t1, kWaves, s_prod[wid], &dummy);
 }
 
 // ---------------------------------------------------------------------------
@@ -1778,7 +1887,10 @@ __global__ __launch_bounds__(kBlock) void k_cg_spmv(CGArgs a) {
     const int wid = threadIdx.x >> 6;
     int t0, t1;
     block_tiles(a.A.N, &t0, &t1);
-    spmv_tiles<true>(a.A, a.p, a.q, t0 + wid, t1, kWaves, s_prod[SL ? 0 : wid], &dot[0]);
+    if (a.A.maxrow <= kMaxNnzRow)
+      spmv_tiles_pipe<true>(a.A, a.p, a.q, t0 + wid, t1, kWaves, s_prod[SL ? 0 : wid], &dot[0]);
+    else
+      spmv_tiles<true>(a.A, a.p, a.q, t0 + wid, t1, kWaves, s_prod[SL ? 0 : wid], &dot[0]);
   }
   double tot[1];
   if (publish_and_reduce<1>(dot, a.partials, a.tickets, xcd_logical_block(blockIdx.x, gridDim.x),
@@ -2127,13 +2239,6 @@ __global__ __launch_bounds__(tile_threads(TILEH)) void k_cg_ps(CGArgs a) {
 // s_waitcnt bookkeeping stays exact across the loop: with loads and stores
 // under branches it waited for vmcnt(0) -- every prefetched row and every
 // store in flight -- once per step.
-typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
-constexpr unsigned kOOB = 0x80000000u;  // buffers are kept below 2 GB (march_geometry)
-constexpr int kNT = 2;                  // aux bits: nontemporal
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* p, unsigned bytes) {
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, (int)bytes, 0x00020000);
-}
 __device__ __forceinline__ double2 bld2(__amdgpu_buffer_rsrc_t r, unsigned off) {
   return __builtin_bit_cast(double2, __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 0));
 }
@@ -3745,7 +3850,7 @@ constexpr int kTagMaxIter = (1 << 24) - 2;
 
 CGArgs make_cg_args(perc_ctx* h) {
   CGArgs a;
-  a.A = CsrView{h->N, h->d.rowptr, h->d.col, h->d.val, h->d.diag};
+  a.A = CsrView{h->N, h->d.rowptr, h->d.col, h->d.val, h->d.diag, h->csr_maxrow};
   a.St = StencilView{h->N, h->d.code, h->st_ng0, h->st_nleak, h->forms, h->d.dtab};
   a.T = TileGeom{h->g.m, h->g.n - 2, h->g.pbc, (h->g.m + kTileW - 1) / kTileW, h->march_h};
   a.pb[0] = h->d.p0;

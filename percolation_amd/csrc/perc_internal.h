@@ -155,6 +155,7 @@ struct perc_ctx {
   long long nb = 0;
   int N = 0;       // interior rows t-2m
   long long nnz = 0;
+  int csr_maxrow = 6;  // most off-diagonals in one CSR row (lattices: <= 6; NR matrices: measured)
   int grid = 0;    // fixed grid of the CG kernels (reduction order depends on it)
   perc::DeviceBuffers d;
   std::vector<int> h_bond_first;  // host copy, t+2

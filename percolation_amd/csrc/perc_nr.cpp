@@ -11,6 +11,7 @@
 // Where the reference `pause`s, the status is kept for perc_nr_status().
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -119,6 +120,9 @@ int upload(int n, const std::vector<int>& rowptr, const std::vector<int>& col,
     if (e != hipSuccess) return hip_status(e, "nr upload");
   }
   g_nr->nnz = (long long)col.size();
+  int mr = 0;
+  for (int i = 0; i < n; ++i) mr = std::max(mr, rowptr[i + 1] - rowptr[i]);
+  g_nr->csr_maxrow = mr;
   g_nr->dot_order = g_nr_dot;
   hipError_t e = hipMemcpy(g_nr->d.rowptr, rowptr.data(), sizeof(int) * (n + 1),
                            hipMemcpyHostToDevice);

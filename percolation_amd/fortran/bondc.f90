@@ -5,7 +5,11 @@
 ! Parameters: the reference's block (Square/bondc.f:67-92; Triangular:
 ! pb = .35, seed = 62703), overridable by an optional namelist file
 ! bondc.nml (&bondc lattice, m, n, pbc, pb, seed, Va, g0, tol, itmax,
-! device /).  Outputs as the reference: bondorder.txt (i10,",",i10) in
+! device, nslab, xport, dot_order /).  nslab > 1 splits the solve into row
+! slabs over nslab contexts (devices device .. device+nslab-1 with xport 0,
+! RCCL; all on `device` with xport 1, host-staged); dot_order 1 folds
+! linbcg's sums in the reference's order (bitwise its solve).  Outputs as
+! the reference: bondorder.txt (i10,",",i10) in
 ! shuffled order (bondc.f:177-180), bond.txt (b1, b2, label, j, c(j);
 ! bondc.f:600-604) and the run summary on stdout.  The per-bond trace
 ! bondocc.txt is not written (SURVEY.md §8(b): optional).
@@ -15,12 +19,14 @@ program bondc
 #ifndef PERC_LATTICE
 #define PERC_LATTICE 0
 #endif
-  integer(c_int) :: lattice, m, n, pbc, seed, itmax, device
+  integer(c_int) :: lattice, m, n, pbc, seed, itmax, device, nslab, xport, dot_order
   double precision :: pb, Va, g0, tol
-  namelist /bondc_nml/ lattice, m, n, pbc, pb, seed, Va, g0, tol, itmax, device
-  integer(c_int) :: nb, tbonds, i, j, id, rc, stats(4), perccln, perccls
+  namelist /bondc_nml/ lattice, m, n, pbc, pb, seed, Va, g0, tol, itmax, device, nslab, xport, &
+                       dot_order
+  integer(c_int) :: nb, tbonds, i, j, id, rc, stats(4), perccln, perccls, s, dev
   integer(c_int), allocatable, target :: b1(:), b2(:), order(:), label(:), csize(:)
   type(c_ptr) :: h
+  type(c_ptr), allocatable, target :: hs(:)
   type(perc_label_info) :: info
   type(perc_cond_result) :: res
   integer :: u
@@ -42,6 +48,9 @@ program bondc
   tol = 1.00d-08            ! linbcg call, bondc.f:545
   itmax = 2500              ! linbcg call, bondc.f:545
   device = 0
+  nslab = 1
+  xport = PERC_XPORT_RCCL
+  dot_order = PERC_DOT_FAST
   if (perc_have_file('bondc.nml')) then
     open(newunit=u, file='bondc.nml', status='old')
     read(u, nml=bondc_nml)
@@ -91,8 +100,29 @@ program bondc
 
   if (perccln > 0) then
     write(6, *) "Calculating internal node voltages"
-    call perc_check(perc_conductance(h, PERC_RULE_BOND, PERC_CUR_FORTRAN, Va, g0, PERC_LEAK, &
-                                     2, tol, itmax, res, c_null_ptr), 'perc_conductance')
+    if (dot_order /= PERC_DOT_FAST) call perc_check(perc_set_dot_order(h, dot_order), 'perc_set_dot_order')
+    if (nslab > 1) then
+      ! the same occupancy labeled on every slab's context, then one split solve
+      allocate(hs(nslab))
+      hs(1) = h
+      do s = 2, nslab
+        dev = device
+        if (xport == PERC_XPORT_RCCL) dev = device + s - 1
+        call perc_check(perc_ctx_create(dev, lattice, m, n, pbc, hs(s)), 'perc_ctx_create')
+        call perc_check(perc_occupy(hs(s), PERC_BOND, 0, c_null_ptr, tbonds, c_loc(order)), 'perc_occupy')
+        call perc_check(perc_label(hs(s), info, c_null_ptr), 'perc_label')
+      end do
+      call perc_check(perc_dslab_solve_group(nslab, c_loc(hs), xport, PERC_RULE_BOND, PERC_CUR_FORTRAN, &
+                                             Va, g0, PERC_LEAK, 2, tol, itmax, 0, res), &
+                      'perc_dslab_solve_group')
+      do s = 2, nslab
+        call perc_check(perc_ctx_destroy(hs(s)), 'perc_ctx_destroy')
+      end do
+      deallocate(hs)
+    else
+      call perc_check(perc_conductance(h, PERC_RULE_BOND, PERC_CUR_FORTRAN, Va, g0, PERC_LEAK, &
+                                       2, tol, itmax, res, c_null_ptr), 'perc_conductance')
+    end if
     write(6, *) "Calculating currents"
     write(6, *) "--------------------"
     write(6, *) "Conductance:", res%gtop, res%gbot

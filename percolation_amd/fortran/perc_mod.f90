@@ -15,6 +15,10 @@ module perc_api
                                 PERC_BONDSITE = 3
   integer(c_int), parameter :: PERC_RULE_BOND = 0, PERC_RULE_SITE = 1, PERC_RULE_MIXED = 2
   integer(c_int), parameter :: PERC_CUR_FORTRAN = 0, PERC_CUR_MATLAB = 1
+  ! association of linbcg's dot products (perc_set_dot_order)
+  integer(c_int), parameter :: PERC_DOT_FAST = 0, PERC_DOT_LITERAL = 1
+  ! transports of the split solve (perc_dslab_solve_group)
+  integer(c_int), parameter :: PERC_XPORT_RCCL = 0, PERC_XPORT_HOST = 1
   ! off-diagonal value of bonds outside the spanning cluster (bondc.f:487)
   real(c_double), parameter :: PERC_LEAK = 1.0d-12
 
@@ -156,6 +160,24 @@ module perc_api
       real(c_double), value :: Va, g0, leak, tol
       type(perc_cond_result) :: res
     end function perc_conductance
+
+    integer(c_int) function perc_set_dot_order(h, order) bind(C, name='perc_set_dot_order')
+      import :: c_int, c_ptr
+      type(c_ptr), value :: h
+      integer(c_int), value :: order
+    end function perc_set_dot_order
+
+    ! one solve split over K labeled contexts (row slabs, one host thread per
+    ! context, RCCL or host-staged exchange): the linbcg call of bondc.f:545
+    ! over several GPUs
+    integer(c_int) function perc_dslab_solve_group(K, ctxs, xport, rule, cur_rule, Va, g0, leak, &
+        itol, tol, itmax, full_x, res) bind(C, name='perc_dslab_solve_group')
+      import :: c_int, c_ptr, c_double, perc_cond_result
+      integer(c_int), value :: K, xport, rule, cur_rule, itol, itmax, full_x
+      type(c_ptr), value :: ctxs
+      real(c_double), value :: Va, g0, leak, tol
+      type(perc_cond_result) :: res
+    end function perc_dslab_solve_group
 
     ! multi-GPU ensemble: one host thread + context per device, RCCL stats
     integer(c_int) function perc_ensemble_create(ndev, devices, lattice, m, n, pbc, e) &

@@ -138,3 +138,62 @@ def test_one_process_over_rccl():
     assert abs(out["iter"] - ref["iter"]) <= 2
     assert abs(out["gtop"] - ref["gtop"]) <= 1e-9 * abs(ref["gtop"])
     assert abs(out["gbot"] - ref["gbot"]) <= 1e-9 * abs(ref["gbot"])
+
+
+# ------------------------------------------------- the loop inside libperc
+def _group(K, case, xport, tol, ordering=None):
+    """K labeled contexts on the box's one GPU, one solve split over them by
+    perc_dslab_solve_group (one host thread per context)"""
+    lat, m, n, pbc = case[:4]
+    order, tb = _system(*case)
+    ctxs = [api.Context(lat, m, n, pbc) for _ in range(K)]
+    try:
+        for c in ctxs:
+            c.set_march_mode(PL.MARCH_ALT)
+            c.occupy(PL.BOND, bond_order=order, nbonds_=tb)
+            c.label()
+        return api.dslab_solve_group(ctxs, xport=xport, tol=tol, itmax=100000)
+    finally:
+        for c in ctxs:
+            c.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", CASES, ids=["sq256x150", "tri128x99"])
+@pytest.mark.parametrize("K", [2, 3, 4])
+def test_group_solve_equals_slabs_in_one_context(case, K):
+    """perc_dslab_solve_group with the host transport (K contexts, K host
+    threads, one GPU): perc_set_slabs(K)'s numbers bitwise"""
+    lat, m, n, pbc = case[:4]
+    order, tb = _system(*case)
+    with api.Context(lat, m, n, pbc) as ctx:
+        ctx.occupy(PL.BOND, bond_order=order, nbonds_=tb)
+        ctx.label()
+        ctx.set_march_mode(PL.MARCH_ALT)
+        ctx.set_slabs(K)
+        ref = ctx.conductance(tol=1e-12, itmax=100000)
+    got = _group(K, case, PL.XPORT_HOST, 1e-12)
+    assert got["iter"] == ref["iter"] and got["err"] == ref["err"], (got, ref)
+    assert got["gtop"] == ref["gtop"] and got["gbot"] == ref["gbot"], (got, ref)
+
+
+@pytest.mark.gpu
+def test_group_solve_over_rccl_one_device():
+    """the RCCL transport at K = 1 (ncclCommInitAll on the one GPU) and the
+    host transport give the same numbers bitwise (the same slab kernels and
+    combine); against the single-context solve they differ only in the dot
+    association (the slab kernels' grids)"""
+    case = CASES[0]
+    lat, m, n, pbc = case[:4]
+    order, tb = _system(*case)
+    with api.Context(lat, m, n, pbc) as ctx:
+        ctx.set_march_mode(PL.MARCH_ALT)
+        ctx.occupy(PL.BOND, bond_order=order, nbonds_=tb)
+        ctx.label()
+        ref = ctx.conductance(tol=1e-12, itmax=100000)
+    rc = _group(1, case, PL.XPORT_RCCL, 1e-12)
+    ho = _group(1, case, PL.XPORT_HOST, 1e-12)
+    assert (rc["iter"], rc["gtop"], rc["gbot"], rc["err"]) == (ho["iter"], ho["gtop"], ho["gbot"], ho["err"])
+    assert abs(rc["iter"] - ref["iter"]) <= 2
+    assert abs(rc["gtop"] - ref["gtop"]) <= 1e-9 * abs(ref["gtop"])
+    assert abs(rc["gbot"] - ref["gbot"]) <= 1e-9 * abs(ref["gbot"])

@@ -45,7 +45,7 @@ def exe(prog, lattice):
     return path
 
 
-def run_variant(v, tmp_path, expect_ok=True):
+def run_variant(v, tmp_path, expect_ok=True, extra=()):
     md = G.meta(v)
     prog, group, keys = NML[md["kind"]]
     p = md["params"]
@@ -58,6 +58,7 @@ def run_variant(v, tmp_path, expect_ok=True):
         pts = p["points"]
         items += ["pstart=%r" % round(pts[0], 6), "pstep=%r" % round(pts[1] - pts[0], 6),
                   "npoints=%d" % len(pts)]
+    items += list(extra)
     (tmp_path / ("%s.nml" % prog)).write_text("&%s_nml %s /\n" % (group, ", ".join(items)))
     r = subprocess.run([exe(prog, p["lattice"])], cwd=tmp_path, capture_output=True, text=True,
                        timeout=600)
@@ -141,3 +142,41 @@ def test_bond_cond_driver(v, tmp_path):
             assert all(abs(x - y) <= 2e-9 for x, y in zip(fa[1:], fb[1:])), (a, b)
         else:
             assert a == b
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("v", ["sq_bondc_p60", "tri_bondc_p35", "sq_bondc_p60_tight"])
+def test_bondc_driver_literal_dot_order(v, tmp_path):
+    """dot_order = 1 (perc_set_dot_order): the driver's printed conductance
+    and iteration count are the reference solver's exactly"""
+    md, r = run_variant(v, tmp_path, extra=["dot_order=1"])
+    for f in golden_files(v):
+        assert (tmp_path / f).read_bytes() == G.text(v, f), f
+    line = [l for l in r.stdout.splitlines() if "Conductance:" in l][-1]
+    gtop, gbot = (float(x) for x in line.split(":")[1].split())
+    assert gtop == md["gtop"] and gbot == md["gbot"], (gtop, gbot, md["gtop"], md["gbot"])
+    it = [l for l in r.stdout.splitlines() if "linbcg iterations:" in l][-1]
+    assert int(it.split(":")[1].split()[0]) == md["iter"]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("nslab", [2, 3])
+def test_bondc_driver_split_solve(nslab, tmp_path):
+    """nslab > 1 (perc_dslab_solve_group from the Fortran host; xport 1: the
+    contexts share the box's one GPU; the slab kernels need m a multiple of
+    128): bond.txt byte-identical to the one-context run and the
+    conductance the one-context solve's to 1e-10 at tol 1e-13"""
+    prog = exe("bondc", 0)
+    out = {}
+    for k in (1, nslab):
+        d = tmp_path / ("k%d" % k)
+        d.mkdir()
+        (d / "bondc.nml").write_text("&bondc_nml lattice=0, m=256, n=200, pbc=0, pb=0.6, "
+                                     "seed=626504, tol=1e-13, itmax=100000, nslab=%d, xport=1 /\n" % k)
+        r = subprocess.run([prog], cwd=d, capture_output=True, text=True, timeout=600)
+        assert r.returncode == 0, r.stderr[-2000:]
+        line = [l for l in r.stdout.splitlines() if "Conductance:" in l][-1]
+        out[k] = [float(x) for x in line.split(":")[1].split()] + [(d / "bond.txt").read_bytes()]
+    (g1, b1, t1), (gk, bk, tk) = out[1], out[nslab]
+    assert t1 == tk
+    assert abs(gk - g1) <= 1e-10 * abs(g1) and abs(bk - b1) <= 1e-10 * abs(b1), (out[1][:2], out[nslab][:2])

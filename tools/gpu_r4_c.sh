@@ -1,0 +1,18 @@
+#!/bin/bash
+# round 4: literal dot order at config 2 vs the oracle fixture; PMC reconcile
+# of the nibble-code march at L = 4096; read-queue levels at L = 8192
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+timeout -k 10 500 python -u tools/literal_config.py c2_sq1024_bond_p50 1e-08 > gpurun_out/r4_literal_c2.log 2>&1
+rc=$?; cat gpurun_out/r4_literal_c2.log | tail -3; [ $rc -gt 1 ] && exit $rc
+L=4096 CBX2=1 bash tools/pmc_r2.sh || { tail -20 gpurun_out/pmc_r2.log; exit 1; }
+cat gpurun_out/pmc_r2_reconcile_L4096.csv
+for L in 8192; do
+  timeout -s KILL 150 rocprofv3 --pmc TCC_EA0_RDREQ_LEVEL_sum TCC_EA0_WRREQ_LEVEL_sum GRBM_GUI_ACTIVE \
+    --kernel-include-regex "k_cg_march|k_cg_b|k_copy" -f csv -d gpurun_out/pmc_level/L$L -o run -- \
+    python3 tools/pmc_probe.py --L $L --reps 16 --copies 8 >> gpurun_out/pmc_level.log 2>&1 || { tail gpurun_out/pmc_level.log; exit 1; }
+  timeout -s KILL 150 rocprofv3 --pmc TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_sum TCC_HIT_sum TCC_MISS_sum \
+    --kernel-include-regex "k_cg_march|k_cg_b|k_copy" -f csv -d gpurun_out/pmc_level/L${L}_n -o run -- \
+    python3 tools/pmc_probe.py --L $L --reps 16 --copies 8 >> gpurun_out/pmc_level.log 2>&1 || { tail gpurun_out/pmc_level.log; exit 1; }
+done
+tail -4 gpurun_out/pmc_level.log

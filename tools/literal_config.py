@@ -1,0 +1,64 @@
+#!/usr/bin/env python3
+"""The literal dot order at a BASELINE config size against the committed
+oracle fixture (tests/golden/configs/<case>.json, the oracle's literal
+linbcg -- bitwise the reference solver at <= 64^2).
+
+With perc_set_dot_order(PERC_DOT_LITERAL) the GPU folds linbcg's three dot
+products in ascending j (Square/bondc.f:785-787, 803-805, 872-875); every
+other operation is already the reference's, so Gtop, Gbot, iter, err and the
+fixture's decimated err history must match bitwise.  Prints one JSON line
+per tolerance; exit status 1 on any difference.
+
+  python tools/literal_config.py c2_sq1024_bond_p50 1e-08 [1e-13 ...]
+"""
+import json
+import os
+import sys
+import time
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(HERE)
+sys.path.insert(0, REPO)
+sys.path.insert(0, os.path.join(REPO, "tests"))
+
+import numpy as np  # noqa: E402
+
+from percolation_amd import _lib as PL  # noqa: E402
+from percolation_amd import api  # noqa: E402
+from test_config_goldens import occupation  # noqa: E402
+
+
+def main():
+    case, tols = sys.argv[1], sys.argv[2:] or ["1e-08"]
+    doc = json.load(open(os.path.join(REPO, "tests", "golden", "configs", case + ".json")))
+    rc = doc["recipe"]
+    occ, rule, cur = occupation(rc)
+    ok = True
+    with api.Context(rc["lattice"], rc["L"], rc["L"], 0) as ctx:
+        ctx.occupy(**occ)
+        li = ctx.label()
+        assert li["nspan"] > 0
+        ctx.set_dot_order(PL.DOT_LITERAL)
+        for tkey in tols:
+            ref = doc["solves"][tkey]
+            t0 = time.time()
+            c = ctx.conductance(rule, cur, tol=float(tkey), itmax=10 ** 6)
+            secs = time.time() - t0
+            hist = ctx.err_history()
+            want = ref["err_history"]
+            hist_ok = all(hist[k - 1] == e for k, e in want)
+            same = (c["iter"] == ref["iter"] and c["err"] == ref["err"] and c["gtop"] == ref["gtop"]
+                    and c["gbot"] == ref["gbot"] and hist_ok)
+            ok = ok and same
+            print(json.dumps(dict(case=case, tol=tkey, bitwise=same, iter=c["iter"], iter_ref=ref["iter"],
+                                  gtop=repr(c["gtop"]), gtop_ref=repr(ref["gtop"]), gbot=repr(c["gbot"]),
+                                  gbot_ref=repr(ref["gbot"]), err=repr(c["err"]), err_ref=repr(ref["err"]),
+                                  err_history_points=len(want), err_history_bitwise=hist_ok,
+                                  seconds=round(secs, 1),
+                                  ms_per_iteration=round(secs * 1e3 / max(c["iter"], 1), 3))),
+                  flush=True)
+    return 0 if ok else 1
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -8,6 +8,11 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 L=${L:-4096}
+# row-code bytes per element of the strip-major q-free march: 1/2 with the
+# nibble codes (PERC_MARCH_NIBBLE, default since round 4; CBX2 = 2 x that),
+# 2 with the u16 codes (CBX2=4); the row-major march (L = 8192) reads u16
+CBX2=${CBX2:-1}
+N=$((L * L - 2 * L))
 timeout -k 10 300 python -c "import torch; torch.cuda.init()" || exit 1
 i=0
 for ctrs in "TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum TCC_EA0_RDREQ_sum" \
@@ -21,8 +26,8 @@ for ctrs in "TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum 
 done
 python3 tools/pmc_reconcile.py gpurun_out/pmc_r2_reconcile_L$L.csv gpurun_out/pmc_r2/p* \
   --last "k_cg_march<1=64" "k_cg_march<2=64" "k_cg_march<0=64" "k_cg_b<true=64" k_copy=16 \
-  --algo "k_cg_march<1=$((18 * (L * L - 2 * L))):$((8 * (L * L - 2 * L)))" \
-         "k_cg_march<2=$((18 * (L * L - 2 * L) + 32 * L)):$((8 * (L * L - 2 * L) + 16 * L))" \
+  --algo "k_cg_march<1=$((16 * N + CBX2 * N / 2)):$((8 * N))" \
+         "k_cg_march<2=$((16 * N + CBX2 * N / 2 + 32 * L)):$((8 * N + 16 * L))" \
          "k_cg_march<0=$((18 * (L * L - 2 * L))):$((16 * (L * L - 2 * L)))" \
          "k_cg_b<true=$((18 * (L * L - 2 * L) + 32 * L)):$((8 * (L * L - 2 * L) + 16 * L))" \
          k_copy=536870912:536870912 >> gpurun_out/pmc_r2.log 2>&1
