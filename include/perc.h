@@ -219,7 +219,9 @@ int perc_spmv_host(perc_ctx *h, const double *x, double *y);
    6 = the resident solve's synchronisation floor: per iteration, the two
    block sums + grid all-gathers of k_cg_res on dummy values, nothing else
    (only on a context whose system takes the resident solver; else
-   PERC_EHIP).  Clobbers solver vectors. */
+   PERC_EHIP).  (Round 4 dropped the probes that lost their A/Bs: the
+   16-B-entry CSR SpMV and the L = 8192 march geometries / load policies,
+   profiles/r4_3_*.)  Clobbers solver vectors. */
 int perc_bench_kernel(perc_ctx *h, int which, int reps, double *ms);
 /* Self-test of the solver's table division (z = r/d from y = RN(1/d) and
    one Markstein correction, bitwise IEEE division when it holds) on the
@@ -288,7 +290,8 @@ int perc_set_slabs(perc_ctx *h, int nslab);
                            (send to slab s-1 / s+1; NULL at s = 0 / K-1);
      ghost_lo / ghost_hi   m doubles: slab s-1's last / s+1's first row
                            (receive).
-   Protocol: perc_dslab_begin (prologue; publishes part_out and the edges)
+   Protocol: perc_dslab_begin (prologue; publishes part_out and the edges;
+   the PS / B steps' kernels write their partials into part_out themselves)
    -> all-gather part_out into part_all, exchange edges into ghosts ->
    step COMBINE_INIT, GHOSTS; then per iteration: PS, all-gather,
    COMBINE_PS, B, all-gather, COMBINE_B, exchange edges, GHOSTS; poll
@@ -323,12 +326,35 @@ int perc_dslab_end(perc_ctx *h);
    perc_set_slabs(K)'s in one context bitwise.  Assembles every context
    (perc_assemble), solves, and returns Gtop / Gbot from slab 0 in *res
    (status 1: nothing spans).  Replaces the linbcg call of
-   Fortran/Square/bondc.f:545 for a lattice split over GPUs. */
+   Fortran/Square/bondc.f:545 for a lattice split over GPUs.
+   K = 1 runs the one-slab kernel epilogues (no combine, no collective: the
+   same arithmetic) unless xport has PERC_XPORT_EXCHANGE set, which keeps
+   the combines and the (one-rank) collectives -- the exchange machinery's
+   own cost, measured by tools/dslab_bench.py.  RCCL communicators are made
+   once per device list and kept for the process (one group call at a time
+   per device list). */
 #define PERC_XPORT_RCCL 0
 #define PERC_XPORT_HOST 1
+#define PERC_XPORT_EXCHANGE 4
 int perc_dslab_solve_group(int K, perc_ctx **ctxs, int xport, int rule, int cur_rule, double Va,
                            double g0, double leak, int itol, double tol, int itmax, int full_x,
                            perc_cond_result *res);
+/* One process per GPU (torchrun / MPI): rank 0 makes an RCCL unique id
+   (PERC_DSLAB_ID_BYTES bytes), the launcher ships it to every rank, each
+   rank binds its labeled context to slab s of K with perc_dslab_comm_init,
+   then perc_dslab_solve runs the whole loop of perc_dslab_solve_group for
+   its slab (assembly, all-gathers and halos over RCCL on the context's
+   stream, the top electrode row to rank 0, rank 0's Gtop / Gbot broadcast
+   to every rank).  The ranks check that they all found the same spanning
+   state before the loop.  The communicator lives until perc_dslab_comm_free
+   or perc_ctx_destroy.  Same numbers as perc_dslab_solve_group over K
+   contexts. */
+#define PERC_DSLAB_ID_BYTES 128
+int perc_dslab_unique_id(void *id, int nbytes);
+int perc_dslab_comm_init(perc_ctx *h, int K, int s, const void *id, int nbytes);
+int perc_dslab_comm_free(perc_ctx *h);
+int perc_dslab_solve(perc_ctx *h, int rule, int cur_rule, double Va, double g0, double leak,
+                     int itol, double tol, int itmax, int full_x, perc_cond_result *res);
 /* assembly only (perc_conductance's first half): the Kirchhoff system of
    the lowest spanning cluster; PERC_ESTATE before perc_label, status 1 in
    *spanning = 0 when nothing spans */
@@ -377,6 +403,8 @@ int perc_set_march_rows(perc_ctx *h, int rows);
    the column -- 0.5 instead of 2 bytes of code per element in each kernel
    (52N -> 49N bytes per iteration); bitwise the same codes (checked per
    row when packed).
+   PERC_MARCH_BIG_STRIPS: the strip-major march past the Infinity Cache
+   too (L = 8192; not in the default, see DESIGN.md for the A/B).
    Row slabs (perc_set_slabs) and the literal dot order always run the
    row-major q-storing march.  (Round 4 removed the variants that lost their
    A/Bs: workgroup row-march 4, deferred reductions 32, persistent march
@@ -388,6 +416,7 @@ int perc_set_march_rows(perc_ctx *h, int rows);
 #define PERC_MARCH_SLOTS 64
 #define PERC_MARCH_TAG 128
 #define PERC_MARCH_NIBBLE 512
+#define PERC_MARCH_BIG_STRIPS 1024
 #define PERC_MARCH_DEFAULT                                                                      \
   (PERC_MARCH_QFREE | PERC_MARCH_ALT | PERC_SOLVE_RESIDENT | PERC_MARCH_STRIPS | PERC_MARCH_SLOTS | \
    PERC_MARCH_TAG | PERC_MARCH_NIBBLE)

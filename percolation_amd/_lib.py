@@ -27,10 +27,12 @@ CUR_FORTRAN, CUR_MATLAB = 0, 1
 FMT_AUTO, FMT_CSR, FMT_STENCIL, FMT_STENCIL_SPLIT, FMT_STENCIL_TILED = 0, 1, 2, 3, 4
 MARCH_QFREE, MARCH_ALT, SOLVE_RESIDENT, MARCH_STRIPS, MARCH_SLOTS, MARCH_TAG = 1, 2, 8, 16, 64, 128
 MARCH_NIBBLE = 512
+MARCH_BIG_STRIPS = 1024
 MARCH_DEFAULT = (MARCH_QFREE | MARCH_ALT | SOLVE_RESIDENT | MARCH_STRIPS | MARCH_SLOTS | MARCH_TAG
                  | MARCH_NIBBLE)
 DOT_FAST, DOT_LITERAL = 0, 1
-XPORT_RCCL, XPORT_HOST = 0, 1
+XPORT_RCCL, XPORT_HOST, XPORT_EXCHANGE = 0, 1, 4
+DSLAB_ID_BYTES = 128
 
 
 class LabelInfo(C.Structure):
@@ -116,6 +118,11 @@ SIGNATURES = {
                                          C.c_int, _VP]),
     "perc_assemble": (C.c_int, [_VP, C.c_int, C.c_double, C.c_double, C.c_double,
                                 C.POINTER(C.c_int)]),
+    "perc_dslab_unique_id": (C.c_int, [_VP, C.c_int]),
+    "perc_dslab_comm_init": (C.c_int, [_VP, C.c_int, C.c_int, _VP, C.c_int]),
+    "perc_dslab_comm_free": (C.c_int, [_VP]),
+    "perc_dslab_solve": (C.c_int, [_VP, C.c_int, C.c_int, C.c_double, C.c_double, C.c_double,
+                                   C.c_int, C.c_double, C.c_int, C.c_int, C.POINTER(CondResult)]),
     "perc_x_row": (C.c_int, [_VP, C.c_int, _VP, C.c_int]),
     "perc_currents": (C.c_int, [_VP, C.c_int, C.c_int, C.c_double, C.c_double, C.c_double,
                                 C.POINTER(CondResult)]),

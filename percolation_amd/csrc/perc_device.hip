@@ -1742,9 +1742,11 @@ struct CGArgs {
   // row slabs (dev_solve_slabs): rows [glo, ghi) may be loaded (glo = -1 /
   // ghi = nrows + 1 when a ghost row of the neighbouring slab is present);
   // slab != 0: the march, B and init epilogues store their raw dot partials
-  // in S->part and leave the scalars to k_slab_combine
+  // in S->part (and in pub[0..3] when set: the all-gather's send buffer of
+  // perc_dslab_*) and leave the scalars to k_slab_combine
   int glo, ghi;
   int slab;
+  double* pub;
   int xhi;        // x kept on rows i >= N - xhi too (< 0: xhi = xrows); xrows < 0: no low rows
   double* q;
   double* partials;  // kRedSlots slots of pstride doubles
@@ -2009,6 +2011,10 @@ __global__ __launch_bounds__(kBlock) void k_cg_b(CGArgs a) {
     if (threadIdx.x == 0 && a.slab) {
       S->part[1] = tot[0];
       S->part[2] = tot[1];
+      if (a.pub) {
+        a.pub[1] = tot[0];
+        a.pub[2] = tot[1];
+      }
     } else if (threadIdx.x == 0) {
       const double err = sqrt(tot[1]) / S->bnrm;
       S->bk = tot[0] / S->bknum;  // next iteration's bknum/bkden (linbcg :799)
@@ -2860,6 +2866,7 @@ __global__ __launch_bounds__(64 * kMarchWaves) void k_cg_march(CGArgs a) {
       if (threadIdx.x == 0) {
         if (a.slab) {
           S->part[0] = tot[0];
+          if (a.pub) a.pub[0] = tot[0];
         } else {
           S->akden = tot[0];
           S->ak = S->bknum / tot[0];
@@ -3776,6 +3783,10 @@ __global__ __launch_bounds__(kBlock) void k_cg_init(CGArgs a, int itol, int x0_z
     if (threadIdx.x == 0 && a.slab) {
       a.S->part[3] = tot[0];
       a.S->part[1] = tot[1];
+      if (a.pub) {
+        a.pub[3] = tot[0];
+        a.pub[1] = tot[1];
+      }
     } else if (threadIdx.x == 0) {
       a.S->bnrm = sqrt(tot[0]);
       a.S->bknum = tot[1];
@@ -3868,6 +3879,7 @@ CGArgs make_cg_args(perc_ctx* h) {
   a.glo = 0;
   a.ghi = h->g.n - 2;
   a.slab = 0;
+  a.pub = nullptr;
   a.xhi = -1;
   a.xrows = h->full_voltages || h->g.m <= 0 ? 0 : h->g.m;  // see dev_solve
   a.pstride = red_partials_size(red_grid(h));
@@ -3962,10 +3974,12 @@ void launch_cg_b(perc_ctx* h, const CGArgs& a, int G) {
   if (h->fused && h->b_grid > 0) G = h->b_grid;
   if (h->march && h->qfree) {
     if (a.sm) launch_march_sm<kMarchB>(h, h->stream, a);
-    else {  // row-major B: its own bands (slot-weighted bands are the P kernel's, rm_slots)
+    else {  // row-major B: its own bands (slot-weighted bands are the P kernel's,
+            // rm_slots), nontemporal r(k) loads (L = 8192: 0.300 vs 0.331 ms,
+            // profiles/r4_3_l8192_probe.json)
       CGArgs ab = a;
       ab.wslots = 0;
-      klaunch(h, k_cg_march<kMarchB>, h->march_grid, 64 * kMarchWaves, h->stream, ab);
+      klaunch(h, k_cg_march<kMarchB, false, kMarchDepth, kNT>, h->march_grid, 64 * kMarchWaves, h->stream, ab);
     }
   } else if (h->stencil) {
     // x on every row with the march's x-in-B (fused, row-major): XF
@@ -4535,7 +4549,8 @@ void select_format(perc_ctx* h) {
   // row-major march is faster (L = 8192: 0.439 vs 0.480 ms,
   // profiles/r2_11_ab_strips.log); its whole-array buffer views also need
   // < 2 GB
-  h->strips = h->qfree && (h->march_mode & PERC_MARCH_STRIPS) && (size_t)h->N * sizeof(double) <= kLargeVector;
+  h->strips = h->qfree && (h->march_mode & PERC_MARCH_STRIPS) &&
+              ((size_t)h->N * sizeof(double) <= kLargeVector || (h->march_mode & PERC_MARCH_BIG_STRIPS));
   // slot-weighted bands of the strip-major march (to_strips applies them)
   const bool slots = (h->march_mode & PERC_MARCH_SLOTS) != 0;
   h->march_slots = slots && h->strips && h->wm_slots > 0;
@@ -5046,11 +5061,6 @@ __global__ void k_slab_combine(CGScalars* S, int K, double* err_hist, int cap,
   for (int s = 0; s < (pall ? 1 : K); ++s) S[s] = v;
 }
 
-// this slab's partials into the all-gather send buffer
-__global__ void k_slab_publish(const CGScalars* S, double* part_out) {
-  if (threadIdx.x < 4) part_out[threadIdx.x] = S->part[threadIdx.x];
-}
-
 namespace {
 struct Slab {
   int r0 = 0, rows = 0, N = 0, glo = 0, ghi = 0;
@@ -5244,7 +5254,8 @@ struct DSlab {
   perc_dslab_bufs buf{};
   int K = 1, s = 0;
   bool full_x = false;
-  long long k = 0;  // P+S launches so far
+  bool solo = false;  // K = 1 without forced exchange: no combines (dslab_setup)
+  long long k = 0;    // P+S launches so far
 };
 
 hipError_t dev_dslab_end(perc_ctx* h, bool to_ctx) {
@@ -5279,7 +5290,7 @@ hipError_t dev_dslab_end(perc_ctx* h, bool to_ctx) {
 }
 
 static hipError_t dslab_setup(perc_ctx* h, int K, int s, int itol, double tol, int itmax, bool full_x,
-                              const perc_dslab_bufs& bufs) {
+                              const perc_dslab_bufs& bufs, bool force_exchange) {
   DeviceBuffers& d = h->d;
   hipStream_t st = h->stream;
   const int m = h->g.m, nrows = h->g.n - 2;
@@ -5345,7 +5356,12 @@ static hipError_t dslab_setup(perc_ctx* h, int K, int s, int itol, double tol, i
   a.bx = 1;
   a.glo = b.glo;
   a.ghi = b.ghi;
-  a.slab = 1;
+  // one slab and no forced exchange: the kernels' own epilogues take the
+  // scalars (k_slab_combine over one partial is the same arithmetic: 0 + t
+  // = t), so the combines, the publishes and the collectives drop out
+  D->solo = K == 1 && !force_exchange;
+  a.slab = D->solo ? 0 : 1;
+  a.pub = D->solo ? nullptr : bufs.part_out;
   a.xrows = full_x ? 0 : (s == 0 ? m : -1);
   a.xhi = full_x ? -1 : (s == K - 1 ? m : 0);
   a.pstride = red_partials_size(b.red);
@@ -5365,9 +5381,9 @@ static hipError_t dslab_setup(perc_ctx* h, int K, int s, int itol, double tol, i
 // perc_dslab_step then sees no slab and returns PERC_EINVAL instead of
 // launching the march on null vectors.
 hipError_t dev_dslab_begin(perc_ctx* h, int K, int s, int itol, double tol, int itmax, bool full_x,
-                           const perc_dslab_bufs& bufs) {
+                           const perc_dslab_bufs& bufs, bool force_exchange) {
   HIP_TRY(dev_dslab_end(h, false));
-  const hipError_t e = dslab_setup(h, K, s, itol, tol, itmax, full_x, bufs);
+  const hipError_t e = dslab_setup(h, K, s, itol, tol, itmax, full_x, bufs, force_exchange);
   if (e != hipSuccess) (void)dev_dslab_end(h, false);
   return e;
 }
@@ -5388,29 +5404,29 @@ hipError_t dev_dslab_step(perc_ctx* h, int op) {
     return hipSuccess;
   };
   switch (op) {
-    case -1:
-      k_slab_publish<<<1, 64, 0, st>>>(D->S, D->buf.part_out);
+    case -1:  // (k_cg_init's epilogue published bnrm^2 and z.r)
       HIP_TRY(edges_out());
       break;
     case PERC_DSLAB_COMBINE_INIT:
-      k_slab_combine<2><<<1, 64, 0, st>>>(D->S, K, h->d.err_hist, h->d.err_hist_cap, D->buf.part_all);
+      if (!D->solo)
+        k_slab_combine<2><<<1, 64, 0, st>>>(D->S, K, h->d.err_hist, h->d.err_hist_cap, D->buf.part_all);
       break;
-    case PERC_DSLAB_PS:
+    case PERC_DSLAB_PS:  // (the march's epilogue publishes its q.p partial)
       a.kiter = (int)(++D->k);
       k_cg_march<kMarchPQ, false, 3><<<b.march_grid, 64 * kMarchWaves, 0, st>>>(a);
-      k_slab_publish<<<1, 64, 0, st>>>(D->S, D->buf.part_out);
       break;
     case PERC_DSLAB_COMBINE_PS:
-      k_slab_combine<0><<<1, 64, 0, st>>>(D->S, K, h->d.err_hist, h->d.err_hist_cap, D->buf.part_all);
+      if (!D->solo)
+        k_slab_combine<0><<<1, 64, 0, st>>>(D->S, K, h->d.err_hist, h->d.err_hist_cap, D->buf.part_all);
       break;
     case PERC_DSLAB_B:
       if (D->full_x) k_cg_b<true, true><<<b.b_grid, kBlock, 0, st>>>(a);
       else k_cg_b<true><<<b.b_grid, kBlock, 0, st>>>(a);
-      k_slab_publish<<<1, 64, 0, st>>>(D->S, D->buf.part_out);
       HIP_TRY(edges_out());
       break;
     case PERC_DSLAB_COMBINE_B:
-      k_slab_combine<1><<<1, 64, 0, st>>>(D->S, K, h->d.err_hist, h->d.err_hist_cap, D->buf.part_all);
+      if (!D->solo)
+        k_slab_combine<1><<<1, 64, 0, st>>>(D->S, K, h->d.err_hist, h->d.err_hist_cap, D->buf.part_all);
       break;
     case PERC_DSLAB_GHOSTS:
       if (D->s > 0) HIP_TRY(hipMemcpyAsync(b.r, D->buf.ghost_lo, row, hipMemcpyDeviceToDevice, st));
@@ -5519,6 +5535,12 @@ hipError_t dev_bench(perc_ctx* h, int which, int reps, double* ms) {
   if (h->strips && (which == 1 || which == 2 || which == 5)) {
     HIP_TRY(to_strips(h, a));
     HIP_TRY(setup_granules(h, a, hs.itmax));
+  }
+  // row-major q-free march past the Infinity Cache: P on the solve's slot
+  // bands (dev_solve)
+  if (!h->strips && h->march && h->qfree && h->march_slots_rm && h->wm_slots > 0) {
+    a.wslots = h->wm_slots;
+    for (int i = 0; i <= h->wm_slots; ++i) a.wcum[0][i] = h->wm_cum[2][i];
   }
   HIP_TRY(hipMemcpyAsync(d.scal, &hs, sizeof(hs), hipMemcpyHostToDevice, st));
   HIP_TRY(hipMemsetAsync(d.tickets, 0, kRedSlots * red_tickets_size(red_grid(h)) * sizeof(unsigned),

@@ -262,6 +262,7 @@ int perc_ctx_destroy(perc_ctx* h) {
   hipSetDevice(h->device);
   if (h->stream) hipStreamSynchronize(h->stream);
   if (h->dslab) dev_dslab_end(h, false);
+  dslab_comm_release(h);
   free_buffers(h);
   for (int i = 0; i < 8; ++i)
     if (h->ev[i]) hipEventDestroy(h->ev[i]);
@@ -869,7 +870,7 @@ int perc_set_march_rows(perc_ctx* h, int rows) {
 
 int perc_set_march_mode(perc_ctx* h, int mode) {
   constexpr int kAll = PERC_MARCH_QFREE | PERC_MARCH_ALT | PERC_SOLVE_RESIDENT | PERC_MARCH_STRIPS |
-                       PERC_MARCH_SLOTS | PERC_MARCH_TAG | PERC_MARCH_NIBBLE;
+                       PERC_MARCH_SLOTS | PERC_MARCH_TAG | PERC_MARCH_NIBBLE | PERC_MARCH_BIG_STRIPS;
   if (!h || (mode & ~kAll) != 0) return PERC_EINVAL;
   h->march_mode = mode;
   march_geometry(h);  // band heights depend on PERC_MARCH_SLOTS

@@ -233,9 +233,13 @@ hipError_t ensure_csr(perc_ctx* h);  // the CSR copy of the assembled system, on
 void select_format(perc_ctx* h);  // stencil / fused flags from fmt_req + assembly checks
 void march_geometry(perc_ctx* h); // band height + grid of the register-march kernel
 void res_geometry(perc_ctx* h);   // grid + band height of the resident solve
+// force_exchange: run the combines and publishes even at K = 1 (measures
+// the exchange machinery; K = 1 otherwise takes the one-slab epilogues)
 hipError_t dev_dslab_begin(perc_ctx* h, int K, int s, int itol, double tol, int itmax, bool full_x,
-                           const perc_dslab_bufs& bufs);
+                           const perc_dslab_bufs& bufs, bool force_exchange = false);
 hipError_t dev_dslab_step(perc_ctx* h, int op);
+// perc_dslab_comm_init's communicator of the context, if any (perc_dslab.cpp)
+void dslab_comm_release(perc_ctx* h);
 hipError_t dev_dslab_status(perc_ctx* h, int* iter, double* err, int* done);
 hipError_t dev_dslab_end(perc_ctx* h, bool to_ctx);
 hipError_t dev_x_row(perc_ctx* h, int row, double* buf, bool to_ctx);

@@ -18,6 +18,13 @@ Every process labels and assembles the whole lattice (a few ms at the
 sizes that need several GPUs); the solve is what is split.  The per-slab
 kernels and the combine order are those of perc_set_slabs(K) in one
 process, so K processes give its numbers bitwise.
+
+`solve` is the production path: libperc runs the whole loop itself
+(perc_dslab_solve over an RCCL communicator of its own, made once per
+context from rank 0's unique id; the group only carries that id), so no
+Python runs per iteration.  `conductance` keeps the loop in Python over the
+group's own backend -- the gloo test transport for several processes on one
+GPU, which one RCCL communicator cannot hold.
 """
 import ctypes as C
 
@@ -149,3 +156,29 @@ def conductance(ctx, rule=L.RULE_BOND, cur_rule=L.CUR_FORTRAN, Va=1.0, g0=1.0, l
         out = o.cpu()
     return dict(gtop=float(out[0]), gbot=float(out[1]), err=float(out[2]), iter=int(out[3]),
                 status=0)
+
+
+def solve(ctx, rule=L.RULE_BOND, cur_rule=L.CUR_FORTRAN, Va=1.0, g0=1.0, leak=LEAK, itol=2,
+          tol=1e-8, itmax=2500, full_x=False, group=None):
+    """`conductance` with the loop inside libperc (perc_dslab_solve): the
+    group's processes, one GPU each, bind their contexts to slab s of K on
+    the first call (rank 0's RCCL unique id broadcast over the group), then
+    every iteration's all-gathers and halos run on the context's stream
+    with no host round trip.  Returns the perc_conductance fields on every
+    process."""
+    lib = L.lib()
+    K, s = dist.get_world_size(group), dist.get_rank(group)
+    if getattr(ctx, "_dslab_rank", None) != (K, s):
+        uid = C.create_string_buffer(L.DSLAB_ID_BYTES)
+        if s == 0:
+            L.check(lib.perc_dslab_unique_id(uid, L.DSLAB_ID_BYTES), "perc_dslab_unique_id")
+        box = [uid.raw]
+        dist.broadcast_object_list(box, src=dist.get_global_rank(group, 0) if group is not None else 0,
+                                   group=group)
+        uid = C.create_string_buffer(box[0], L.DSLAB_ID_BYTES)
+        L.check(lib.perc_dslab_comm_init(ctx.h, K, s, uid, L.DSLAB_ID_BYTES), "perc_dslab_comm_init")
+        ctx._dslab_rank = (K, s)
+    res = L.CondResult()
+    L.check(lib.perc_dslab_solve(ctx.h, rule, cur_rule, Va, g0, leak, itol, tol, itmax, int(full_x),
+                                 C.byref(res)), "perc_dslab_solve")
+    return {k: getattr(res, k) for k, _ in L.CondResult._fields_}

@@ -64,6 +64,11 @@ CASES = {
     # ConductCalc.m:134-160 mixed rule
     "c5m_sq1024_mixed_p85": dict(lattice=0, L=1024, kind="mixed", p=0.85, pb=0.85,
                                  order="ref", sseed=143285, bseed=43716),
+    # the realisation bench.py times first: 4096^2 square bond at 0.6, occupancy drawn on the
+    # GPU by perc_occupy_random with tseed(ii = 2) (the host restatement perc_random_order
+    # gives the same ids, tests/test_labeling_oracle.py; round 4)
+    "bench_sq4096_bond_p60_dev": dict(lattice=0, L=4096, kind="bond", p=0.60, order="device",
+                                      ii=2),
 }
 TOLS = (1e-8, 1e-13, 1e-14)
 # --decades: one threaded run of the same iterates (oracle or_linbcg_sym, bitwise the
@@ -88,6 +93,12 @@ def bond_pairs(O, lattice, L, recipe_order, seed, p):
     tb = int(p * nb)
     if recipe_order == "ref":
         _, _, o1, o2 = O.bond_order(lattice, L, L, 0, seed)
+    elif recipe_order == "device":  # perc_occupy_random's ids (host restatement)
+        sys.path.insert(0, REPO)
+        from percolation_amd import _lib as PL, api
+        ids = api.random_order(nb, tb, seed, PL.BOND).astype(np.int64) - 1
+        o1, o2 = O.i32(nb + 1), O.i32(nb + 1)
+        o1[:tb], o2[:tb] = b1[ids], b2[ids]
     else:
         ids = np.random.default_rng(seed).permutation(nb)[:tb]
         o1, o2 = O.i32(nb + 1), O.i32(nb + 1)
@@ -191,6 +202,11 @@ def find_seed(rc, kmax=64):
         return 0, 0, r
     seeds = O.i32(kmax)
     O.lib().or_trial_seeds(MASTER, kmax, seeds)
+    if "ii" in rc:  # a fixed realisation (must span)
+        r = label_case(rc, int(seeds[rc["ii"] - 1]))
+        if r is None:
+            raise RuntimeError("realisation %d does not span" % rc["ii"])
+        return rc["ii"], int(seeds[rc["ii"] - 1]), r
     for ii in range(1, kmax + 1):
         r = label_case(rc, int(seeds[ii - 1]))
         if r is not None:

@@ -79,7 +79,7 @@ def _system(lat, m, n, pbc, p, seed):
     return api.shuffled_ids(nb, seed), int(p * nb)
 
 
-def _solve_worker(rank, world, port, backend, case, tol, q):
+def _solve_worker(rank, world, port, backend, case, tol, q, inlib=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group(backend, rank=rank, world_size=world)
     try:
@@ -88,16 +88,23 @@ def _solve_worker(rank, world, port, backend, case, tol, q):
         with api.Context(lat, m, n, pbc) as ctx:
             ctx.occupy(PL.BOND, bond_order=order, nbonds_=tb)
             assert ctx.label()["nspan"] > 0
-            r = dslab.conductance(ctx, tol=tol, itmax=100000, check_every=16)
+            if inlib:  # perc_dslab_solve: the loop inside libperc, own RCCL communicator
+                ctx.set_march_mode(PL.MARCH_ALT)
+                r = dslab.solve(ctx, tol=tol, itmax=100000)
+                r2 = dslab.solve(ctx, tol=tol, itmax=100000)  # communicator reused
+                assert [r2[k] for k in ("iter", "gtop", "gbot", "err")] == \
+                    [r[k] for k in ("iter", "gtop", "gbot", "err")]
+            else:
+                r = dslab.conductance(ctx, tol=tol, itmax=100000, check_every=16)
         q.put((rank, r))
     finally:
         dist.destroy_process_group()
 
 
-def _run(world, backend, case, tol):
+def _run(world, backend, case, tol, inlib=False):
     ctx = mp.get_context("spawn")
     q = ctx.SimpleQueue()
-    mp.spawn(_solve_worker, args=(world, free_port(), backend, case, tol, q), nprocs=world,
+    mp.spawn(_solve_worker, args=(world, free_port(), backend, case, tol, q, inlib), nprocs=world,
              join=True)
     out = {}
     while not q.empty():
@@ -179,10 +186,12 @@ def test_group_solve_equals_slabs_in_one_context(case, K):
 
 @pytest.mark.gpu
 def test_group_solve_over_rccl_one_device():
-    """the RCCL transport at K = 1 (ncclCommInitAll on the one GPU) and the
-    host transport give the same numbers bitwise (the same slab kernels and
-    combine); against the single-context solve they differ only in the dot
-    association (the slab kernels' grids)"""
+    """K = 1: the RCCL transport with the exchange forced (ncclCommInitAll on
+    the one GPU, one-rank all-gathers and the slab-order combines), the host
+    transport with it forced, and the plain K = 1 path (the one-slab kernel
+    epilogues, no combine) give the same numbers bitwise -- the combine over
+    one partial is the same arithmetic; against the single-context solve
+    they differ only in the dot association (the slab kernels' grids)"""
     case = CASES[0]
     lat, m, n, pbc = case[:4]
     order, tb = _system(*case)
@@ -191,9 +200,24 @@ def test_group_solve_over_rccl_one_device():
         ctx.occupy(PL.BOND, bond_order=order, nbonds_=tb)
         ctx.label()
         ref = ctx.conductance(tol=1e-12, itmax=100000)
-    rc = _group(1, case, PL.XPORT_RCCL, 1e-12)
-    ho = _group(1, case, PL.XPORT_HOST, 1e-12)
-    assert (rc["iter"], rc["gtop"], rc["gbot"], rc["err"]) == (ho["iter"], ho["gtop"], ho["gbot"], ho["err"])
+    key = lambda r: (r["iter"], r["gtop"], r["gbot"], r["err"])  # noqa: E731
+    rc = _group(1, case, PL.XPORT_RCCL | PL.XPORT_EXCHANGE, 1e-12)
+    rc2 = _group(1, case, PL.XPORT_RCCL | PL.XPORT_EXCHANGE, 1e-12)  # cached communicator
+    ho = _group(1, case, PL.XPORT_HOST | PL.XPORT_EXCHANGE, 1e-12)
+    solo = _group(1, case, PL.XPORT_RCCL, 1e-12)
+    assert key(rc) == key(ho) == key(solo) == key(rc2), (rc, ho, solo)
     assert abs(rc["iter"] - ref["iter"]) <= 2
     assert abs(rc["gtop"] - ref["gtop"]) <= 1e-9 * abs(ref["gtop"])
     assert abs(rc["gbot"] - ref["gbot"]) <= 1e-9 * abs(ref["gbot"])
+
+
+@pytest.mark.gpu
+def test_per_process_solve_world_one():
+    """perc_dslab_solve (one process per GPU, its own RCCL communicator from
+    rank 0's unique id, the loop inside libperc) at world 1: the group
+    solver's numbers bitwise; the second call reuses the communicator"""
+    case = CASES[0]
+    got = _run(1, "gloo", case, 1e-12, inlib=True)[0]
+    want = _group(1, case, PL.XPORT_RCCL, 1e-12)
+    assert (got["iter"], got["gtop"], got["gbot"], got["err"]) == \
+        (want["iter"], want["gtop"], want["gbot"], want["err"]), (got, want)

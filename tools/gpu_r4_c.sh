@@ -1,18 +1,14 @@
 #!/bin/bash
-# round 4: literal dot order at config 2 vs the oracle fixture; PMC reconcile
-# of the nibble-code march at L = 4096; read-queue levels at L = 8192
+# round 4: CSR SpMV A/B, L=8192 march probes, group split-solve + Fortran driver tests, the
+# split solve's per-iteration exchange cost at K=1, the literal dot order at config 2
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -k 10 500 python -u tools/literal_config.py c2_sq1024_bond_p50 1e-08 > gpurun_out/r4_literal_c2.log 2>&1
-rc=$?; cat gpurun_out/r4_literal_c2.log | tail -3; [ $rc -gt 1 ] && exit $rc
-L=4096 CBX2=1 bash tools/pmc_r2.sh || { tail -20 gpurun_out/pmc_r2.log; exit 1; }
-cat gpurun_out/pmc_r2_reconcile_L4096.csv
-for L in 8192; do
-  timeout -s KILL 150 rocprofv3 --pmc TCC_EA0_RDREQ_LEVEL_sum TCC_EA0_WRREQ_LEVEL_sum GRBM_GUI_ACTIVE \
-    --kernel-include-regex "k_cg_march|k_cg_b|k_copy" -f csv -d gpurun_out/pmc_level/L$L -o run -- \
-    python3 tools/pmc_probe.py --L $L --reps 16 --copies 8 >> gpurun_out/pmc_level.log 2>&1 || { tail gpurun_out/pmc_level.log; exit 1; }
-  timeout -s KILL 150 rocprofv3 --pmc TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_sum TCC_HIT_sum TCC_MISS_sum \
-    --kernel-include-regex "k_cg_march|k_cg_b|k_copy" -f csv -d gpurun_out/pmc_level/L${L}_n -o run -- \
-    python3 tools/pmc_probe.py --L $L --reps 16 --copies 8 >> gpurun_out/pmc_level.log 2>&1 || { tail gpurun_out/pmc_level.log; exit 1; }
-done
-tail -4 gpurun_out/pmc_level.log
+timeout -k 10 120 python -u tools/csr_ab.py --L 4096 > gpurun_out/r4_csr_ab.json 2>&1; tail -2 gpurun_out/r4_csr_ab.json
+timeout -k 10 200 python -u tools/l8192_probe.py --L 8192 --reps 10 > gpurun_out/r4_l8192_probe.json 2>&1; tail -2 gpurun_out/r4_l8192_probe.json
+timeout -k 10 300 python -u -m pytest -x -v --timeout 200 --timeout-method thread tests/test_dslab.py \
+  tests/test_fortran_drivers.py -k "group or literal or split or rccl" > gpurun_out/r4_pytest_c.log 2>&1
+rc=$?; tail -12 gpurun_out/r4_pytest_c.log; [ $rc -ne 0 ] && exit $rc
+timeout -k 10 200 python -u tools/dslab_bench.py --L 4096 --iters 2000 --torch > gpurun_out/r4_dslab_bench.json 2> gpurun_out/r4_dslab_bench.err
+rc=$?; cat gpurun_out/r4_dslab_bench.json; tail -3 gpurun_out/r4_dslab_bench.err; [ $rc -ne 0 ] && exit $rc
+timeout -k 10 420 python -u tools/literal_config.py c2_sq1024_bond_p50 1e-08 > gpurun_out/r4_literal_c2.log 2>&1
+rc=$?; tail -3 gpurun_out/r4_literal_c2.log; exit $rc
