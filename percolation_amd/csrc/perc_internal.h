@@ -20,7 +20,7 @@ constexpr int kMaxSlots = 6;      // neighbour slots per row
 
 // Sorted neighbour offsets (c - s) of each row form of the stencil operator
 // (interior / edge columns, up / down triangles): row i's columns are
-// i + off[f][j] for its form f (perc_device.hip, "Stencil-coded operator").
+// i + off[f][j] for its form f (perc_stencil.h).
 // dr/dc: the slot's neighbour in lattice (row, column) steps, column
 // wrapped for pbc; always in {-1, 0, 1} (the LDS-tiled kernel's halo).
 struct StencilForms {
@@ -217,7 +217,7 @@ struct perc_ctx {
 
 namespace perc {
 
-// device entry points (perc_device.hip)
+// device entry points (perc_label.hip, perc_assemble.hip, perc_solve.hip, perc_slabs.hip)
 hipError_t dev_build_lattice(perc_ctx* h);
 hipError_t dev_alloc_matrix(perc_ctx* h, int N, long long nnz);
 void dev_free_all(perc_ctx* h);
@@ -243,6 +243,10 @@ void dslab_comm_release(perc_ctx* h);
 hipError_t dev_dslab_status(perc_ctx* h, int* iter, double* err, int* done);
 hipError_t dev_dslab_end(perc_ctx* h, bool to_ctx);
 hipError_t dev_x_row(perc_ctx* h, int row, double* buf, bool to_ctx);
+// row forms of the interior system (perc_assemble.hip); band height of the
+// register march over nrows rows (perc_solve.hip)
+StencilForms stencil_forms(const Geom& g);
+int march_rows_for(const perc_ctx* h, int nrows);
 hipError_t dev_solve_slabs(perc_ctx* h, int K, int itol, double tol, int itmax, bool full_x,
                            int* iter, double* err);
 hipError_t dev_solve(perc_ctx* h, int itol, double tol, int itmax, bool x0_zero, bool full_x,

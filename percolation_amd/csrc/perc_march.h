@@ -1,0 +1,691 @@
+// perc_march.h -- the register-march P / B kernels.
+//
+// Device code of libperc, included by perc_solve.hip and perc_slabs.hip (every definition sits in an
+// anonymous namespace: each translation unit keeps its own copy of what it
+// launches).
+#pragma once
+#include "perc_cg.h"
+
+// (each TU launches a subset of these internal-linkage helpers)
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Wunused-function"
+namespace perc {
+namespace {
+
+// ---------------------------------------------------------------------------
+// Register-march fused P(k)+S(k) (stencil operator, m a multiple of 128).
+// A wave owns a strip of 128 columns (a column pair per lane, 16-B
+// accesses) and walks down a band of H rows.  Rows are prefetched D steps
+// ahead into registers; p(k) of the rows above, at and below the current
+// row live in a three-row register window, the column neighbours come from
+// the adjacent lanes (lanes 0 / 63 also form p(k) of the halo column left
+// / right of the strip).  No LDS tile, no barrier between loading and the
+// SpMV: every wave streams like the B kernel.  Per row and element the
+// arithmetic is k_cg_ps's (z = r/d, p = bk p + z, x += ak p, q in slot
+// order), so every value is bitwise the other kernels'; only the q.p
+// association differs (rows summed per lane).
+// Buffer access with a hardware range check: a byte offset at or past the
+// buffer's size makes a load return 0 and drops a store.  The row-march
+// keeps every memory instruction of a step unconditional this way (rows
+// outside the lattice or the band, halo columns of non-halo threads, q of
+// the steps without a finished row, x off the electrode rows), so hipcc's
+// s_waitcnt bookkeeping stays exact across the loop: with loads and stores
+// under branches it waited for vmcnt(0) -- every prefetched row and every
+// store in flight -- once per step.
+__device__ __forceinline__ double2 bld2(__amdgpu_buffer_rsrc_t r, unsigned off) {
+  return __builtin_bit_cast(double2, __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 0));
+}
+__device__ __forceinline__ double bld1(__amdgpu_buffer_rsrc_t r, unsigned off) {
+  return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, (int)off, 0, 0));
+}
+// sc1 (agent-coherent) load: data another workgroup stored with sc1
+__device__ __forceinline__ double bld1s(__amdgpu_buffer_rsrc_t r, unsigned off) {
+  return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, (int)off, 0, 16));
+}
+template <int AUX>
+__device__ __forceinline__ void bst2(__amdgpu_buffer_rsrc_t r, unsigned off, double2 v) {
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, (int)off, 0, AUX);
+}
+
+// publish_and_reduce with tagged granules (the march kernels, TAG): every
+// partial travels as one 16-B write-through {value, tag} store (untorn), so
+// the workgroup that publishes it need not drain its stores before taking
+// its ticket -- the reader polls the tags instead.  At the end of a march
+// launch the last workgroup to arrive waited twice for s_waitcnt vmcnt(0)
+// (its last rows' stores, then its group partial's) before the totals could
+// be formed.  Association, and so the totals, are publish_and_reduce's term
+// for term.  tag: unique per launch and solve; a reader that polls for ~0.5 s
+// without seeing it sets *err and uses what it has (the host reports it).
+__device__ __forceinline__ double2 gran_poll(__amdgpu_buffer_rsrc_t rg, int off, double tag, int* err) {
+  double2 g2 = __builtin_bit_cast(double2, __builtin_amdgcn_raw_buffer_load_b128(rg, off, 0, 16));
+  for (unsigned spin = 0; g2.y != tag; ++spin) {
+    if (spin > (1u << 22)) {
+      *err = 1;
+      break;
+    }
+    __builtin_amdgcn_s_sleep(1);
+    g2 = __builtin_bit_cast(double2, __builtin_amdgcn_raw_buffer_load_b128(rg, off, 0, 16));
+  }
+  return g2;
+}
+
+template <int NV>
+__device__ bool publish_and_reduce_tagged(double (&v)[NV], double* gran, unsigned* tickets, int lb,
+                                          int nwg, double tag, int* err, double (&tot)[NV],
+                                          double* s_red, int* s_flag) {
+  block_sum<NV>(v, s_red);
+  const int ngroups = red_groups(nwg);
+  const int grp = lb / kGroup, g0 = grp * kGroup, gn = min(kGroup, nwg - g0);
+  // granules: [j][workgroup] then [j][group]
+  const __amdgpu_buffer_rsrc_t rg = rsrc(gran, (unsigned)(NV * (nwg + ngroups) * 16));
+  const int goff = NV * nwg;
+  if (threadIdx.x == 0) {
+#pragma unroll
+    for (int j = 0; j < NV; ++j)
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, make_double2(v[j], tag)), rg,
+                                             (j * nwg + lb) * 16, 0, 16);
+    const unsigned tk = __hip_atomic_fetch_add(&tickets[grp * kTicketStride], 1u,
+                                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_flag[0] = tk == (unsigned)(gn - 1);
+  }
+  __syncthreads();
+  if (!s_flag[0]) return false;
+  if (threadIdx.x < 64) {  // last of its group: wave 0 sums the group's partials
+    const int lane = threadIdx.x;
+    double w[NV];
+#pragma unroll
+    for (int j = 0; j < NV; ++j) {
+      w[j] = lane < gn ? gran_poll(rg, (j * nwg + g0 + lane) * 16, tag, err).x : 0.0;
+      w[j] = wave_sum(w[j]);
+    }
+    if (lane == 0) {
+#pragma unroll
+      for (int j = 0; j < NV; ++j)
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, make_double2(w[j], tag)), rg,
+                                               (goff + j * ngroups + grp) * 16, 0, 16);
+      __hip_atomic_store(&tickets[grp * kTicketStride], 0u, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+      const unsigned tk = __hip_atomic_fetch_add(&tickets[ngroups * kTicketStride], 1u,
+                                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      s_flag[1] = tk == (unsigned)(ngroups - 1);
+    }
+  }
+  __syncthreads();
+  if (!s_flag[1]) return false;
+  double acc[NV];
+#pragma unroll
+  for (int j = 0; j < NV; ++j) acc[j] = 0.0;
+  for (int i = threadIdx.x; i < ngroups; i += blockDim.x) {
+#pragma unroll
+    for (int j = 0; j < NV; ++j) acc[j] = acc[j] + gran_poll(rg, (goff + j * ngroups + i) * 16, tag, err).x;
+  }
+  __syncthreads();  // s_red reuse
+  block_sum<NV>(acc, s_red);
+  if (threadIdx.x == 0) {
+#pragma unroll
+    for (int j = 0; j < NV; ++j) s_red[16 + j] = acc[j];
+    __hip_atomic_store(&tickets[ngroups * kTicketStride], 0u, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < NV; ++j) tot[j] = s_red[16 + j];
+  return true;
+}
+
+constexpr int kMarchW = 128;     // columns per wave strip
+constexpr int kMarchWaves = 4;   // waves (strips) per workgroup
+
+struct MRow {       // one prefetched row of the lane's pair (+ halo column)
+  double2 p, r;     // p(k-1), r
+  unsigned c;       // the pair's codes
+  double hp, hr;    // halo column (lanes 0 and 63)
+  unsigned hc;
+};
+struct MWin {       // p(k) at columns col-1, col, col+1, col+2 of one row
+  double l, e0, e1, rr;
+};
+
+// neighbour value at raster position kp (0..7: (-1,-1) (-1,0) (-1,1) (0,-1)
+// (0,1) (1,-1) (1,0) (1,1)) of element E (0: column col, 1: col+1)
+template <int E>
+__device__ __forceinline__ double mwin_at(int kp, const MWin& U, const MWin& C, const MWin& D) {
+  const MWin& W = kp < 3 ? U : (kp < 5 ? C : D);
+  const int dc = kp < 3 ? kp - 1 : (kp == 3 ? -1 : (kp == 4 ? 1 : kp - 6));
+  const int s = E + 1 + dc;  // 0: l, 1: e0, 2: e1, 3: rr
+  return s == 0 ? W.l : (s == 1 ? W.e0 : (s == 2 ? W.e1 : W.rr));
+}
+
+// q of element E: d x + sum over the form's slots (slot order) of g x_nb,
+// when the wave's rows all share one regular form (slot order = raster
+// order) with used-position bits `mask` (wave-uniform: scalar branches)
+template <int E>
+__device__ __forceinline__ double march_q(unsigned c, double d, double xi, unsigned mask,
+                                          const MWin& U, const MWin& C, const MWin& D,
+                                          double ng0, double nleak) {
+  double acc = d * xi;
+  int j = 0;
+#pragma unroll
+  for (int kp = 0; kp < 8; ++kp) {
+    if (mask & (1u << kp)) {
+      const double gv = ((c >> j) & 1u) ? ng0 : nleak;
+      acc = acc + gv * mwin_at<E>(kp, U, C, D);
+      ++j;
+    }
+  }
+  return acc;
+}
+
+// general path (rows whose wave mixes forms, or wrapped-column forms): the
+// lane's 12 window values are in the wave's LDS scratch s_w[v * 64 + lane]
+// (v = row * 4 + {l, e0, e1, rr}); slot j reads value kvi(kp_j) + E
+template <int E>
+__device__ __forceinline__ double march_q_gen(unsigned c, double d, double xi, unsigned pos,
+                                              const double* s_w, int lane, double ng0,
+                                              double nleak) {
+  // raster position -> window value index (row * 4 + 1 + dc), 4 bits each
+  constexpr unsigned kVi = 0xA9864210u;
+  double acc = d * xi;
+  const int cnt = (c >> 8) & 7;
+#pragma unroll
+  for (int j = 0; j < kMaxSlots; ++j) {
+    if (j < cnt) {
+      const int kp = (pos >> (3 * j)) & 7;
+      const int v = ((kVi >> (4 * kp)) & 15u) + E;
+      const double gv = ((c >> j) & 1u) ? ng0 : nleak;
+      acc = acc + gv * s_w[v * 64 + lane];
+    }
+  }
+  return acc;
+}
+
+// q of element E for a wave whose rows are all regular (slot order = raster
+// order) but not one form: lane-private raster -> slot map (rmap), so edge
+// strips (columns 0 and m-1 lack a neighbour) take this register path too.
+// Positions a row lacks read an exact 0 from the window (outside the
+// lattice or the interior system) or are skipped by the select.
+template <int E>
+__device__ __forceinline__ double march_q_map(unsigned c, double d, double xi, unsigned map,
+                                              unsigned umask, const MWin& U, const MWin& C,
+                                              const MWin& D, double ng0, double nleak) {
+  double acc = d * xi;
+#pragma unroll
+  for (int kp = 0; kp < 8; ++kp) {
+    if (umask & (1u << kp)) {
+      const unsigned j = (map >> (4 * kp)) & 15u;
+      const double gv = ((c >> j) & 1u) ? ng0 : nleak;
+      const double pr = gv * mwin_at<E>(kp, U, C, D);
+      acc = j != 15u ? acc + pr : acc;
+    }
+  }
+  return acc;
+}
+
+// Rows prefetched ahead (template D).  The P+S kernel of the solve runs
+// D = 3 (strip-major: 162 VGPRs, 3 waves per SIMD, one round of 43-row
+// bands at L = 4096): 0.106-0.107 ms vs D = 4 / 5 at 2 waves per SIMD
+// 0.114-0.116 (profiles/r2_12_strips_depth_rows_probe.log,
+// r2_14_march_depth5.log): waves per SIMD, not rows in flight, decide.  Before the memory instructions were
+// made unconditional (MBuf) every step waited for vmcnt(0) and deeper
+// prefetch could not help.  The opt-in variants (q-free P and B, strip-
+// major) keep D = 2.
+constexpr int kMarchDepth = 2;
+
+// Register march, three kernels of one loop (MODE):
+//   kMarchPQ: P(k)+S(k), stores q for the streaming B (k_cg_b)
+//   kMarchP:  P(k)+S(k) without the q store
+//   kMarchB:  B(k) rebuilding q = A p(k) from p(k) (+ halo) instead of
+//             reading it: r -= ak q, z = r/d, z.r, r.r, bk, err, stop
+// With kMarchP + kMarchB an iteration moves 52N bytes instead of 60N.
+// Direction: a wave walks its band down (increasing rows) or up.  With
+// a.march_alt, odd bands walk up in P and even bands walk up in B, so the
+// halo rows two neighbouring bands share are read by both waves at the
+// same moment (start or end of the walk: the second read hits L2 / the
+// Infinity Cache), and B starts each band on the rows P wrote last.
+constexpr int kMarchPQ = 0, kMarchP = 1, kMarchB = 2;
+
+struct MGeom {
+  int r0, rend, col, hcol;
+  bool hok;
+  unsigned cb0, cb1, cbh;  // nibble codes (PK): count / form bits of col, col+1, hcol
+};
+
+// Buffer views of the rows one march wave touches, [lo, hi) = its band plus
+// the halo rows, clipped to the loadable rows [glo, ghi): every load and
+// store of a step is issued unconditionally with a byte offset that is out
+// of range (kOOB, or a row outside the view) where the row-major kernel had
+// a branch -- a row outside the lattice, a halo column of a non-halo lane,
+// p(k-1) of the first iteration, q / p of a row the wave does not own.
+// With memory instructions under branches hipcc's waitcnt pass put
+// s_waitcnt vmcnt(0) at the top of every step (every prefetched row and
+// every store drained once per step: ~3.5 read requests in flight per wave,
+// TCC_EA0_RDREQ_LEVEL, profiles/r2_3_*); unconditional, the waits count
+// exactly and the prefetch ring keeps its rows in flight.
+struct MBuf {
+  __amdgpu_buffer_rsrc_t p, r, c, pn, q, x;  // p(k-1), r, codes, p(k): rows [lo, hi); q, x: own rows
+  int lo, hi;
+};
+
+// strip-major solve (SM): whole-array views (vectors < 2 GB there), element
+// offsets through sm_at; row-major: the band's views, offsets from row lo
+template <int MODE, bool SM, bool PK = false>
+__device__ __forceinline__ MBuf march_bufs(const CGArgs& a, const MGeom& g, const double* psrc,
+                                           double* pnew) {
+  const int m = a.T.m;
+  MBuf B;
+  B.lo = max(g.r0 - 1, a.glo);
+  B.hi = max(min(g.rend + 1, a.ghi), B.lo);
+  if constexpr (SM) {
+    const unsigned nall = (unsigned)a.T.nrows * (unsigned)m;
+    B.p = rsrc(psrc, nall * 8u);
+    B.r = rsrc(a.r, nall * 8u);
+    B.c = PK ? rsrc(a.nib, nall / 2u) : rsrc(a.St.code, nall * 2u);
+    B.pn = rsrc(pnew, nall * 8u);
+    B.q = rsrc(a.q, MODE == kMarchPQ ? nall * 8u : 0u);
+    B.x = rsrc(a.x, 0u);  // the strip-major solve keeps x in B
+    return B;
+  }
+  const long long base = (long long)B.lo * m;
+  const unsigned n = (unsigned)(B.hi - B.lo) * (unsigned)m;
+  const unsigned nown = (unsigned)max(g.rend - g.r0, 0) * (unsigned)m;
+  B.p = rsrc(psrc + base, n * 8u);
+  B.r = rsrc(a.r + base, n * 8u);
+  B.c = rsrc(a.St.code + base, n * 2u);
+  B.pn = rsrc(pnew + base, n * 8u);
+  B.q = rsrc(MODE == kMarchPQ ? a.q + (long long)g.r0 * m : a.r, MODE == kMarchPQ ? nown * 8u : 0u);
+  B.x = rsrc(MODE == kMarchP ? a.x + (long long)g.r0 * m : a.r, MODE == kMarchP ? nown * 8u : 0u);
+  return B;
+}
+
+// element offset (in elements) of (row gr, column col) in a view of MBuf
+template <bool SM>
+__device__ __forceinline__ unsigned melem(const CGArgs& a, const MBuf& B, int gr, int col) {
+  return SM ? (unsigned)sm_at(a.T, gr, col) : (unsigned)((gr - B.lo) * a.T.m + col);
+}
+
+template <int MODE, bool SM, int PAUX = 0, bool PK = false>
+__device__ __forceinline__ void march_load(const CGArgs& a, const MGeom& g, const MBuf& B, int gr,
+                                           bool first, const double* __restrict__ psrc, MRow& R) {
+  {
+    const bool rowok = (unsigned)(gr - B.lo) < (unsigned)(B.hi - B.lo);
+    const unsigned e = rowok ? melem<SM>(a, B, gr, g.col) : 0u;
+    const unsigned eh = rowok ? melem<SM>(a, B, gr, g.hcol) : 0u;
+    const unsigned o8 = rowok ? e * 8u : kOOB;
+    const bool rown = MODE != kMarchB || (gr >= g.r0 && gr < g.rend);
+    const bool hk = rowok && g.hok;
+    const unsigned h8 = hk ? eh * 8u : kOOB;
+    if constexpr (PK) {
+      // the pair's two slot nibbles in one byte (element e even); the count
+      // and form bits come from the columns (g.cb0 / cb1): the u16 codes
+      const unsigned b = __builtin_amdgcn_raw_buffer_load_b8(B.c, (int)(rowok ? e / 2u : kOOB), 0, 0);
+      R.c = ((b & 0xFu) | g.cb0) | (((b >> 4) | g.cb1) << 16);
+    } else {
+      R.c = __builtin_amdgcn_raw_buffer_load_b32(B.c, (int)(rowok ? e * 2u : kOOB), 0, 0);
+    }
+    // PAUX on the loads that read a value for the last time: P's p(k-1)
+    // (dead once p(k) is formed), B's r(k) (overwritten by r(k+1))
+    constexpr int kRAux = MODE == kMarchB ? PAUX : 0;
+    constexpr int kPAux = MODE == kMarchP ? PAUX : 0;
+    R.r = __builtin_bit_cast(double2, __builtin_amdgcn_raw_buffer_load_b128(B.r, (int)(rown ? o8 : kOOB), 0, kRAux));
+    R.p = __builtin_bit_cast(double2, __builtin_amdgcn_raw_buffer_load_b128(B.p, (int)(first ? kOOB : o8), 0, kPAux));
+    if (MODE != kMarchB) {
+      if constexpr (PK) {
+        const unsigned b = __builtin_amdgcn_raw_buffer_load_b8(B.c, (int)(hk ? eh / 2u : kOOB), 0, 0);
+        R.hc = ((b >> (4u * (eh & 1u))) & 0xFu) | g.cbh;
+      } else {
+        R.hc = __builtin_amdgcn_raw_buffer_load_b16(B.c, (int)(hk ? eh * 2u : kOOB), 0, 0);
+      }
+      R.hr = bld1(B.r, h8);
+    } else {
+      R.hc = 0u;
+      R.hr = 0.0;
+    }
+    R.hp = bld1(B.p, first ? kOOB : h8);
+  }
+}
+
+struct MState {
+  MWin U, C, Dn;
+  unsigned cN, cM;        // codes of the newest / middle window rows
+  double2 rN, rM;         // r of the newest / middle rows (kMarchB)
+};
+
+// one step: row gr enters the window, then the middle row (gr -+ 1) is
+// finished when it is one of the band's own rows
+template <int MODE, bool UP, bool SM>
+__device__ __forceinline__ void march_step(const CGArgs& a, const MGeom& g, const MBuf& B,
+                                           const MRow& R, int gr,
+                                           bool first, double bk, double ak,
+                                           double* __restrict__ pnew, const double2* s_dt,
+                                           const unsigned* s_rpos, const unsigned* s_rmap,
+                                           double* s_w, MState& W, double (&acc)[2]) {
+  const int lane = threadIdx.x & 63;
+  const int nrows = a.T.nrows, N = a.St.N;
+  const double ng0 = a.St.ng0, nleak = a.St.nleak;
+  double2 pn = make_double2(0.0, 0.0);
+  double hpn = 0.0;
+  double2 d0 = make_double2(1.0, 1.0), d1 = d0;  // {d, 1/d}
+  if (gr >= a.glo && gr < a.ghi) {
+    d0 = s_dt[diag_idx(R.c & 0xffffu)];
+    d1 = s_dt[diag_idx(R.c >> 16)];
+    if (MODE == kMarchB) {
+      pn = R.p;
+      hpn = R.hp;
+    } else {
+      const double z0 = div_tab(R.r.x, d0), z1 = div_tab(R.r.y, d1);
+      if (first) {
+        pn.x = z0;
+        pn.y = z1;
+      } else {
+        pn.x = bk * R.p.x + z0;
+        pn.y = bk * R.p.y + z1;
+      }
+      if (g.hok) {
+        const double zh = div_tab(R.hr, s_dt[diag_idx(R.hc)]);
+        hpn = first ? zh : bk * R.hp + zh;
+      }
+    }
+  }
+  {
+    if (MODE != kMarchB) {
+      const int m = a.T.m;
+      // own row; in a slab also the ghost rows, so the next iteration's
+      // halo p(k) is at hand (bitwise the neighbour slab's own value)
+      const bool own = gr >= g.r0 && gr < g.rend;
+      const bool pst = (unsigned)(gr - B.lo) < (unsigned)(B.hi - B.lo) &&
+                       (own || (a.slab && (gr < 0 || gr >= nrows)));
+      bst2<kNT>(B.pn, pst ? melem<SM>(a, B, gr, g.col) * 8u : kOOB, pn);
+      if (MODE == kMarchP && !SM) {  // x += ak p(k-1) on the x rows (the P-only march keeps x)
+        const int i = gr * m + g.col;
+        const bool xw = own && !first && !a.bx && (a.xrows == 0 || i < a.xrows || i >= N - a.xrows);
+        const unsigned ox = xw ? (unsigned)((gr - g.r0) * m + g.col) * 8u : kOOB;
+        double2 xv = bld2(B.x, ox);
+        xv.x = xv.x + ak * R.p.x;
+        xv.y = xv.y + ak * R.p.y;
+        bst2<0>(B.x, ox, xv);
+      }
+    }
+  }
+  MWin Nw;
+  Nw.e0 = pn.x;
+  Nw.e1 = pn.y;
+  const double up = __shfl_up(pn.y, 1);
+  const double dn = __shfl_down(pn.x, 1);
+  Nw.l = lane == 0 ? hpn : up;
+  Nw.rr = lane == 63 ? hpn : dn;
+  if (UP) {
+    W.Dn = W.C;
+    W.C = W.U;
+    W.U = Nw;
+  } else {
+    W.U = W.C;
+    W.C = W.Dn;
+    W.Dn = Nw;
+  }
+  W.cM = W.cN;
+  W.cN = R.c;
+  if (MODE == kMarchB) {
+    W.rM = W.rN;
+    W.rN = R.r;
+  }
+  const int mid = UP ? gr + 1 : gr - 1;
+  const bool mown = mid >= g.r0 && mid < g.rend;  // wave-uniform
+  double2 mq = make_double2(0.0, 0.0), mr = mq;   // q / r(k+1) of the middle row
+  if (mown) {
+    const unsigned c0w = W.cM & 0xffffu, c1w = W.cM >> 16;
+    const unsigned f0 = c0w >> 11, f1 = c1w >> 11;
+    const double2 dM0 = s_dt[diag_idx(c0w)], dM1 = s_dt[diag_idx(c1w)];
+    const unsigned ff = __builtin_amdgcn_readfirstlane(f0);
+    const bool uni = !__any(f0 != ff || f1 != ff) && a.St.F.regular[ff];
+    double q0, q1;
+    if (uni) {
+      const unsigned mask = a.St.F.rmask[ff];
+      q0 = march_q<0>(c0w, dM0.x, W.C.e0, mask, W.U, W.C, W.Dn, ng0, nleak);
+      q1 = march_q<1>(c1w, dM1.x, W.C.e1, mask, W.U, W.C, W.Dn, ng0, nleak);
+    } else {
+      const unsigned mp0 = s_rmap[f0], mp1 = s_rmap[f1];
+      if (!__any(mp0 == kRmapIrregular || mp1 == kRmapIrregular)) {
+        const unsigned um = a.St.F.umask;
+        q0 = march_q_map<0>(c0w, dM0.x, W.C.e0, mp0, um, W.U, W.C, W.Dn, ng0, nleak);
+        q1 = march_q_map<1>(c1w, dM1.x, W.C.e1, mp1, um, W.U, W.C, W.Dn, ng0, nleak);
+      } else {
+        const MWin* rows[3] = {&W.U, &W.C, &W.Dn};
+#pragma unroll
+        for (int rr = 0; rr < 3; ++rr) {
+          s_w[(4 * rr + 0) * 64 + lane] = rows[rr]->l;
+          s_w[(4 * rr + 1) * 64 + lane] = rows[rr]->e0;
+          s_w[(4 * rr + 2) * 64 + lane] = rows[rr]->e1;
+          s_w[(4 * rr + 3) * 64 + lane] = rows[rr]->rr;
+        }
+        // lane-private slots: no cross-lane hazard, only the wave's own
+        // LDS write -> read order (lgkmcnt, inserted by the compiler)
+        q0 = march_q_gen<0>(c0w, dM0.x, W.C.e0, s_rpos[f0], s_w, lane, ng0, nleak);
+        q1 = march_q_gen<1>(c1w, dM1.x, W.C.e1, s_rpos[f1], s_w, lane, ng0, nleak);
+      }
+    }
+    if (MODE == kMarchB) {
+      // k_cg_b's per-pair arithmetic
+      double2 rn;
+      rn.x = W.rM.x - ak * q0;
+      rn.y = W.rM.y - ak * q1;
+      mr = rn;
+      const double z0 = div_tab(rn.x, dM0), z1 = div_tab(rn.y, dM1);
+      acc[0] = acc[0] + z0 * rn.x;
+      acc[0] = acc[0] + z1 * rn.y;
+      acc[1] = acc[1] + rn.x * rn.x;
+      acc[1] = acc[1] + rn.y * rn.y;
+    } else {
+      mq = make_double2(q0, q1);
+      acc[0] = acc[0] + q0 * W.C.e0;
+      acc[0] = acc[0] + q1 * W.C.e1;
+    }
+  }
+  {
+    const int m = a.T.m;
+    const unsigned eq = SM ? (unsigned)sm_at(a.T, mid, g.col) : (unsigned)((mid - g.r0) * m + g.col);
+    if (MODE == kMarchPQ) bst2<kNT>(B.q, mown ? eq * 8u : kOOB, mq);
+    if (MODE == kMarchB) bst2<kNT>(B.r, mown ? melem<SM>(a, B, mid, g.col) * 8u : kOOB, mr);
+  }
+}
+
+template <int MODE, int D, bool UP, bool SM, int PAUX = 0, bool PK = false>
+__device__ __forceinline__ void march_walk(const CGArgs& a, const MGeom& g, const MBuf& B,
+                                           MRow (&ring)[D],
+                                           bool first, double bk, double ak,
+                                           const double* __restrict__ psrc,
+                                           double* __restrict__ pnew, const double2* s_dt,
+                                           const unsigned* s_rpos, const unsigned* s_rmap,
+                                           double* s_w, double (&acc)[2]) {
+  MState W;
+  W.U = MWin{0.0, 0.0, 0.0, 0.0};
+  W.C = W.U;
+  W.Dn = W.U;
+  W.cN = W.cM = 0u;
+  W.rN = W.rM = make_double2(0.0, 0.0);
+  const int nsteps = g.rend - g.r0 + 2;  // rows r0-1 .. rend
+  for (int j0 = 0; j0 < nsteps; j0 += D) {
+#pragma unroll
+    for (int u = 0; u < D; ++u) {
+      const int j = j0 + u;
+      // no branches around memory instructions: a step past the walk (odd
+      // step count) and the prefetch past its end address rows outside the
+      // view (loads return 0, stores are dropped) and finish no row
+      const MRow R = ring[u];
+      march_load<MODE, SM, PAUX, PK>(a, g, B, UP ? g.rend - (j + D) : g.r0 - 1 + j + D, first, psrc, ring[u]);
+      march_step<MODE, UP, SM>(a, g, B, R, UP ? g.rend - j : g.r0 - 1 + j, first, bk, ak, pnew, s_dt,
+                               s_rpos, s_rmap, s_w, W, acc);
+    }
+  }
+}
+
+// PAUX: cache policy of the last-use loads (P: p(k-1); B: r(k)).
+// TR: phase probe -- lane 0 of every wave stores {kernel entry, walk end,
+// exit, hardware id} wall-clock stamps (100 MHz) into a.mtrace[4 w ..]
+// TAG: the epilogue reductions by tagged granules (publish_and_reduce_tagged)
+template <int MODE, bool SM = false, int D = kMarchDepth, int PAUX = 0, bool TR = false,
+          bool TAG = false, bool PK = false>
+__global__ __launch_bounds__(64 * kMarchWaves) void k_cg_march(CGArgs a) {
+  const unsigned long long tr_t0 = TR ? wall_clock64() : 0ull;
+  unsigned long long tr_t1 = 0ull;
+  CGScalars* S = a.S;
+  __shared__ double s_red[32];
+  __shared__ int s_flag[2];
+  __shared__ unsigned s_rpos[kMaxForms], s_rmap[kMaxForms];
+  __shared__ double2 s_dt[kDiagTab];
+  __shared__ double s_win[kMarchWaves][12 * 64];  // general-path window scratch
+  // the launch's iteration comes from the host (launch j of a solve is
+  // iteration j + 1 until the stop; later launches return below), so the
+  // first rows' loads go out before any device scalar is read
+  const int k = a.kiter;
+  const bool first = MODE != kMarchB && k == 1;
+  // P reads p(k-1) and writes p(k); B reads p(k)
+  const double* __restrict__ psrc = a.pb[(MODE == kMarchB ? k : k - 1) & 1];
+  double* __restrict__ pnew = a.pb[k & 1];
+  const int m = a.T.m, nrows = a.T.nrows, H = a.T.bh;
+  const int lb = xcd_logical_block(blockIdx.x, gridDim.x);
+  const int lane = threadIdx.x & 63;
+  // wave-uniform in SGPRs (the buffer views below must be: a resource
+  // the compiler cannot prove uniform gets a readfirstlane loop per access)
+  const int w = __builtin_amdgcn_readfirstlane(lb * kMarchWaves + (threadIdx.x >> 6));
+  const int spr = m / kMarchW;
+  int band, strip;
+  MGeom g;
+  if (a.wslots > 0) {
+    // slot-weighted bands (PERC_MARCH_SLOTS).  Workgroups are dealt one per
+    // CU per round: blockIdx / CUs is the round -- the CU slot -- a
+    // workgroup runs in (observed on MI355X, speed only: any placement
+    // gives the same rows and results).  The waves of the first round get
+    // memory requests served first and stream fastest (L = 4096, equal
+    // bands: 49 / 56 / 66 us per walk for rounds 0 / 1 / 2,
+    // profiles/r3_2_mtrace_static_summary.txt), so the rows of every cycle
+    // of wslots neighbouring bands are split by per-round weights: all
+    // waves finish together instead of the CU idling while its last round
+    // drains.  Band b = q * wslots + round, so neighbouring bands still
+    // alternate walk directions.
+    const int ns = a.wslots, ncu = gridDim.x / ns;
+    const int sl = blockIdx.x / ncu, i = blockIdx.x - sl * ncu;
+    const int v = __builtin_amdgcn_readfirstlane(i * kMarchWaves + (threadIdx.x >> 6));
+    const int Q = ncu * kMarchWaves / spr;  // cycles per strip
+    const int q = v / spr;
+    strip = v - q * spr;
+    band = q * ns + sl;
+    const int c0 = (int)((long long)q * nrows / Q), hc = (int)((long long)(q + 1) * nrows / Q) - c0;
+    const int* wc = a.wcum[MODE == kMarchB ? 1 : 0];
+    g.r0 = c0 + hc * wc[sl] / wc[ns];
+    g.rend = c0 + hc * wc[sl + 1] / wc[ns];
+  } else {
+    band = w / spr;
+    strip = w - band * spr;
+    g.r0 = band * H;
+    g.rend = min(g.r0 + H, nrows);
+  }
+  const bool active = g.r0 < nrows;  // wave-uniform
+  const int c0 = strip * kMarchW;
+  g.col = c0 + 2 * lane;
+  g.hcol = lane == 0 ? c0 - 1 : c0 + kMarchW;
+  g.hok = lane == 0 || lane == 63;
+  if (g.hcol < 0 || g.hcol >= m) {
+    if (a.T.pbc) g.hcol += g.hcol < 0 ? m : -m;
+    else g.hok = false;
+  }
+  const bool up = (a.march_alt && (band & 1)) != (MODE == kMarchB);
+  const int nsteps = g.rend - g.r0 + 2;
+  if constexpr (PK) {  // (nibble codes: the square lattice's three column classes)
+    auto cls = [&](int c) { return c == 0 ? a.ncls[1] : (c == m - 1 ? a.ncls[2] : a.ncls[0]); };
+    g.cb0 = cls(g.col);
+    g.cb1 = cls(g.col + 1);
+    g.cbh = cls(g.hcol);
+  }
+  const MBuf B = march_bufs<MODE, SM, PK>(a, g, psrc, pnew);
+  MRow ring[D];
+  if (active) {
+#pragma unroll
+    for (int u = 0; u < D; ++u)
+      if (u < nsteps) march_load<MODE, SM, PAUX, PK>(a, g, B, up ? g.rend - u : g.r0 - 1 + u, first, psrc, ring[u]);
+  }
+  if (S->done) return;
+  if (threadIdx.x < kMaxForms) {
+    s_rpos[threadIdx.x] = a.St.F.rpos[threadIdx.x];
+    s_rmap[threadIdx.x] = a.St.F.rmap[threadIdx.x];
+  }
+  load_dtab(a.St, s_dt);
+  __syncthreads();
+  const double bk = S->bk, ak = S->ak;
+  double acc[2] = {0.0, 0.0};
+  if (active) {
+    double* s_w = s_win[threadIdx.x >> 6];
+    if (up) march_walk<MODE, D, true, SM, PAUX, PK>(a, g, B, ring, first, bk, ak, psrc, pnew, s_dt, s_rpos, s_rmap, s_w, acc);
+    else march_walk<MODE, D, false, SM, PAUX, PK>(a, g, B, ring, first, bk, ak, psrc, pnew, s_dt, s_rpos, s_rmap, s_w, acc);
+    if (MODE == kMarchB && SM) {
+      // strip-major q-free solve: x (row-major) += ak p(k) on the band's x
+      // rows, after the walk (loads and stores inside it would put a
+      // vmcnt(0) in every step); k_cg_b's x update of the q-storing solve
+      const int N = a.St.N;
+      for (int gr = g.r0; gr < g.rend; ++gr) {
+        const int i = gr * m + g.col;  // m is a multiple of the strip width
+        if (a.xrows != 0 && i >= a.xrows && i < N - a.xrows) continue;
+        const double2 pv = *reinterpret_cast<const double2*>(psrc + sm_at(a.T, gr, g.col));
+        double2 xv = *reinterpret_cast<const double2*>(a.x + i);
+        xv.x = xv.x + ak * pv.x;
+        xv.y = xv.y + ak * pv.y;
+        *reinterpret_cast<double2*>(a.x + i) = xv;
+      }
+    }
+  }
+  if constexpr (TR) {
+    tr_t1 = wall_clock64();
+    if (lane == 0) {
+      unsigned hw;
+      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+      unsigned xcc;
+      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+      a.mtrace[4 * (size_t)w + 0] = tr_t0;
+      a.mtrace[4 * (size_t)w + 1] = tr_t1;
+      a.mtrace[4 * (size_t)w + 3] = ((unsigned long long)xcc << 32) | hw;
+    }
+  }
+  if (MODE != kMarchB) {
+    double v[1] = {acc[0]}, tot[1];
+    const bool last = TAG ? publish_and_reduce_tagged<1>(v, a.mgran, a.tickets, lb, gridDim.x, a.mtag,
+                                                         a.merr, tot, s_red, s_flag)
+                          : publish_and_reduce<1>(v, a.partials, a.tickets, lb, gridDim.x, tot, s_red, s_flag);
+    if (last) {
+      if (threadIdx.x == 0) {
+        if (a.slab) {
+          S->part[0] = tot[0];
+          if (a.pub) a.pub[0] = tot[0];
+        } else {
+          S->akden = tot[0];
+          S->ak = S->bknum / tot[0];
+        }
+      }
+    }
+  } else {
+    double tot[2];
+    const bool last =
+        TAG ? publish_and_reduce_tagged<2>(acc, a.mgran_b, a.tickets + a.tstride, lb, gridDim.x, a.mtag, a.merr, tot,
+                                           s_red, s_flag)
+            : publish_and_reduce<2>(acc, a.partials + a.pstride, a.tickets + a.tstride, lb, gridDim.x,
+                                    tot, s_red, s_flag);
+    if (last) {
+      if (threadIdx.x == 0) {  // k_cg_b's epilogue
+        const int kk = S->iter + 1;
+        const double err = sqrt(tot[1]) / S->bnrm;
+        S->bk = tot[0] / S->bknum;
+        S->bknum = tot[0];
+        S->err = err;
+        if (kk - 1 < a.err_hist_cap) a.err_hist[kk - 1] = err;
+        S->iter = kk;
+        if (!(err > S->tol) || kk >= S->itmax + 1) S->done = 1;
+      }
+    }
+  }
+  if constexpr (TR) {
+    if (lane == 0) a.mtrace[4 * (size_t)w + 2] = wall_clock64();
+  }
+}
+
+
+}  // namespace
+}  // namespace perc
+#pragma clang diagnostic pop

@@ -1,0 +1,909 @@
+// perc_solve.hip -- the conductance solve of libperc (gfx950): lattice and
+// matrix buffers, the solver-format choice, and the fused Jacobi-PCG that
+// follows linbcg's operation order (Square/bondc.f:750-838): the register
+// march (default), the resident cooperative solve, the one-workgroup solve,
+// the literal dot order; plus the SpMV and roofline probes.  All
+// floating-point elementwise work is written out in the reference's order
+// and compiled with -ffp-contract=off, so every per-row value is bitwise what
+// bondc.f computes; only the global dot products are re-associated
+// (deterministically: fixed grid, fixed tree), unless the literal dot order
+// is asked for.
+#include "perc_march.h"
+#include "perc_resident.h"
+
+namespace perc {
+namespace {
+
+// ---------------------------------------------------------------------------
+// Lattice build
+__global__ void k_forward_count(Geom g, int* fc /* t+2 */) {
+  const long long s = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (s > g.t + 1) return;
+  fc[s] = (s >= 1 && s <= g.t - 1) ? forward_count(g, (int)s) : 0;
+}
+
+__global__ void k_row_count(Geom g, int N, int* rc /* N+1 */) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i > N) return;
+  if (i == N) { rc[N] = 0; return; }
+  const int s = i + g.m + 1;
+  int nbr[6];
+  const int c = sorted_neighbours(g, s, nbr);
+  int cnt = 0;
+  for (int j = 0; j < c; ++j) cnt += (nbr[j] > g.m && nbr[j] <= g.t - g.m);
+  rc[i] = cnt;
+}
+
+__global__ void k_fill_col(Geom g, int N, const int* rowptr, int* col) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= N) return;
+  const int s = i + g.m + 1;
+  int nbr[6];
+  const int c = sorted_neighbours(g, s, nbr);
+  int k = rowptr[i];
+  for (int j = 0; j < c; ++j)
+    if (nbr[j] > g.m && nbr[j] <= g.t - g.m) col[k++] = nbr[j] - g.m - 1;
+}
+
+
+// Kernel-timing events: no system-scope fence when they are recorded (the
+// hipEventDisableSystemFence contract: elapsed times only, read after a
+// stream synchronize).  With the default fence the launches that carry the
+// start / stop events pay an L2 write-back + invalidate the other launches
+// do not, and read ~1 % above rocprofv3's durations of the same kernels
+// (profiles/r3_8_*, r3_9_ab_event_fence_L4096.log).
+hipError_t timing_event_create(hipEvent_t* ev) {
+  return hipEventCreateWithFlags(ev, hipEventDisableSystemFence);
+}
+
+// launch a CG kernel; when kernel timing armed h->ev_next, the launch
+// records them at the kernel's own start and end (hipExtLaunchKernel: the
+// dispatch packet's timestamps, no separate event packets around it)
+template <typename K>
+void klaunch(perc_ctx* h, K kern, dim3 g, dim3 b, hipStream_t st, const CGArgs& a) {
+  if (h->ev_next[0]) {
+    hipExtLaunchKernelGGL(kern, g, b, 0, st, h->ev_next[0], h->ev_next[1], 0, a);
+    h->ev_next[0] = h->ev_next[1] = nullptr;
+  } else {
+    kern<<<g, b, 0, st>>>(a);
+  }
+}
+
+// the strip-major q-free march P or B (the default solve at L <= 4096): 3
+// rows prefetched, nontemporal last-use loads and stores, tagged-granule
+// reductions (a.mgran) or the ticket reduction, phase probe (a.mtrace)
+template <int MODE, bool PK>
+void launch_march_sm2(perc_ctx* h, hipStream_t st, const CGArgs& a) {
+  const int grid = a.wslots > 0 ? h->wm_grid : h->march_grid;
+  if (a.mgran) {
+    if (a.mtrace) klaunch(h, k_cg_march<MODE, true, 3, kNT, true, true, PK>, grid, 64 * kMarchWaves, st, a);
+    else klaunch(h, k_cg_march<MODE, true, 3, kNT, false, true, PK>, grid, 64 * kMarchWaves, st, a);
+  } else if (a.mtrace) {
+    klaunch(h, k_cg_march<MODE, true, 3, kNT, true, false, PK>, grid, 64 * kMarchWaves, st, a);
+  } else {
+    klaunch(h, k_cg_march<MODE, true, 3, kNT, false, false, PK>, grid, 64 * kMarchWaves, st, a);
+  }
+}
+template <int MODE>
+void launch_march_sm(perc_ctx* h, hipStream_t st, const CGArgs& a) {
+  if (a.nib) launch_march_sm2<MODE, true>(h, st, a);
+  else launch_march_sm2<MODE, false>(h, st, a);
+}
+
+// S(k), or the fused P(k)+S(k) of the tiled stencil kernel
+void launch_cg_spmv(perc_ctx* h, const CGArgs& a, int G) {
+  if (h->fused) {
+    const int th = h->tile_h;
+    const dim3 G2(h->tile_grid), B2(tile_threads(th));
+    hipStream_t st = h->stream;
+    if (h->march) {
+      if (h->qfree && a.sm) launch_march_sm<kMarchP>(h, st, a);
+      // row-major q-free P (vectors past the Infinity Cache): one round of
+      // slot-weighted bands when a.wslots is set
+      else if (h->qfree) klaunch(h, k_cg_march<kMarchP>, a.wslots > 0 ? h->wm_grid : h->march_grid, 64 * kMarchWaves, st, a);
+      // q-storing P+S (row slabs, the literal dot order, modes without QFREE)
+      else klaunch(h, k_cg_march<kMarchPQ, false, 3>, h->march_grid, 64 * kMarchWaves, st, a);
+      return;
+    }
+    if (h->g.scn == 4) {
+      if (th == 32) klaunch(h, k_cg_ps<4, true, 32>, G2, B2, st, a);
+      else if (th == 16) klaunch(h, k_cg_ps<4, true, 16>, G2, B2, st, a);
+      else klaunch(h, k_cg_ps<4, true, 8>, G2, B2, st, a);
+    } else {
+      if (th == 32) klaunch(h, k_cg_ps<6, true, 32>, G2, B2, st, a);
+      else if (th == 16) klaunch(h, k_cg_ps<6, true, 16>, G2, B2, st, a);
+      else klaunch(h, k_cg_ps<6, true, 8>, G2, B2, st, a);
+    }
+  } else if (!h->stencil) klaunch(h, k_cg_spmv<0>, G, kBlock, h->stream, a);
+  else if (h->g.scn == 4) klaunch(h, k_cg_spmv<4>, G, kBlock, h->stream, a);
+  else klaunch(h, k_cg_spmv<6>, G, kBlock, h->stream, a);
+}
+
+// B(k) (streaming; the fused format walks its chunks in reverse)
+void launch_cg_b(perc_ctx* h, const CGArgs& a, int G) {
+  // fused formats: b_grid (set with the lattice, see dev_build_lattice)
+  if (h->fused && h->b_grid > 0) G = h->b_grid;
+  if (h->march && h->qfree) {
+    if (a.sm) launch_march_sm<kMarchB>(h, h->stream, a);
+    else {  // row-major B: its own bands (slot-weighted bands are the P kernel's,
+            // rm_slots), nontemporal r(k) loads (L = 8192: 0.300 vs 0.331 ms,
+            // profiles/r4_3_l8192_probe.json)
+      CGArgs ab = a;
+      ab.wslots = 0;
+      klaunch(h, k_cg_march<kMarchB, false, kMarchDepth, kNT>, h->march_grid, 64 * kMarchWaves, h->stream, ab);
+    }
+  } else if (h->stencil) {
+    // x on every row with the march's x-in-B (fused, row-major): XF
+    if (a.bx && a.xrows == 0 && !a.sm) klaunch(h, k_cg_b<true, true>, G, kBlock, h->stream, a);
+    else klaunch(h, k_cg_b<true>, G, kBlock, h->stream, a);
+  } else {
+    klaunch(h, k_cg_b<false>, G, kBlock, h->stream, a);
+  }
+}
+
+void launch_spmv(perc_ctx* h, const CGArgs& a, const double* x, double* y) {
+  if (!h->stencil) k_spmv<<<h->grid, kBlock, 0, h->stream>>>(a.A, x, y);
+  else if (h->g.scn == 4) k_spmv_st<4><<<h->grid, kBlock, 0, h->stream>>>(a.St, x, y);
+  else k_spmv_st<6><<<h->grid, kBlock, 0, h->stream>>>(a.St, x, y);
+}
+
+// tagged-granule reductions of the strip-major q-free march (a.sm): a P and
+// a B region, each sized for the largest grid either kernel runs; a new
+// solve epoch, so no granule of an earlier solve carries a valid tag
+hipError_t setup_granules(perc_ctx* h, CGArgs& a, int itmax) {
+  if (!h->march_tag || !a.sm || itmax > kTagMaxIter) return hipSuccess;
+  const int GM = std::max(red_grid(h), h->wm_grid);
+  const size_t region = (size_t)2 * 2 * ((size_t)GM + red_groups(GM));  // NV <= 2, 16-B granules
+  const size_t need = 2 * region;
+  if (h->d.mgran_n < need) {
+    if (h->d.mgran) HIP_TRY(hipFree(h->d.mgran));
+    h->d.mgran = nullptr;
+    HIP_TRY(dmalloc(&h->d.mgran, need));
+    HIP_TRY(hipMemsetAsync(h->d.mgran, 0, need * sizeof(double), h->stream));  // tag 0: never a launch's
+    h->d.mgran_n = need;
+  }
+  a.mgran = h->d.mgran;
+  a.mgran_b = h->d.mgran + region;
+  a.merr = &h->d.scal->pad[1];
+  ++h->solve_epoch;
+  return hipSuccess;
+}
+
+}  // namespace
+
+// ===========================================================================
+hipError_t dev_build_lattice(perc_ctx* h) {
+  const Geom& g = h->g;
+  const int t = g.t, N = h->N;
+  hipStream_t st = h->stream;
+  DeviceBuffers& d = h->d;
+  // bond_first
+  int* fc = nullptr;
+  HIP_TRY(dmalloc(&fc, t + 2));
+  HIP_TRY(dmalloc(&d.bond_first, t + 2));
+  k_forward_count<<<blocks_for(t + 2), kBlock, 0, st>>>(g, fc);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(exclusive_scan(fc, d.bond_first, t + 2, st));
+  HIP_TRY(hipFree(fc));
+  h->h_bond_first.resize(t + 2);
+  HIP_TRY(hipMemcpy(h->h_bond_first.data(), d.bond_first, sizeof(int) * (t + 2),
+                    hipMemcpyDeviceToHost));
+  h->bf_closed = g.lattice == kSquare && g.n >= 2;
+  for (int r = 0; r + 2 <= g.n && h->bf_closed; ++r)
+    for (int c = 0; c < g.m; ++c)
+      if (h->h_bond_first[(size_t)r * g.m + c + 1] != bf_square(g, r, c)) {
+        h->bf_closed = false;
+        break;
+      }
+  // CSR pattern of the interior block
+  int* rc = nullptr;
+  HIP_TRY(dmalloc(&rc, N + 1));
+  HIP_TRY(dmalloc(&d.rowptr, N + 1));
+  k_row_count<<<blocks_for(N + 1), kBlock, 0, st>>>(g, N, rc);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(exclusive_scan(rc, d.rowptr, N + 1, st));
+  HIP_TRY(hipFree(rc));
+  int nnz = 0;
+  HIP_TRY(hipMemcpy(&nnz, d.rowptr + N, sizeof(int), hipMemcpyDeviceToHost));
+  h->nnz = nnz;
+  HIP_TRY(dmalloc(&d.col, (size_t)nnz + 8));
+  HIP_TRY(dmalloc(&d.val, (size_t)nnz + 8));
+  k_fill_col<<<blocks_for(N), kBlock, 0, st>>>(g, N, d.rowptr, d.col);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(dmalloc(&d.diag, N + 2));
+  HIP_TRY(dmalloc(&d.rhs, N + 2));
+  HIP_TRY(dmalloc(&d.dtab, kDiagTab));  // double2 entries
+  h->forms = stencil_forms(g);
+  HIP_TRY(dmalloc(&d.forms_dev, 1));
+  HIP_TRY(hipMemcpy(d.forms_dev, &h->forms, sizeof(StencilForms), hipMemcpyHostToDevice));
+  HIP_TRY(dmalloc(&d.sflag, 4));
+  // occupancy + labeling
+  HIP_TRY(dmalloc(&d.bocc, (size_t)h->nb + 8));
+  HIP_TRY(dmalloc(&d.socc, t + 8));
+  HIP_TRY(dmalloc(&d.order, (size_t)std::max<long long>(h->nb, t) + 8));
+  HIP_TRY(dmalloc(&d.parent, t + 8));
+  HIP_TRY(dmalloc(&d.member, t + 8));
+  HIP_TRY(dmalloc(&d.top, t + 8));
+  HIP_TRY(dmalloc(&d.counters, 8 + kMaxSpanList));
+  // CG vectors (padded to even length for the 16 B paths) and the row codes.
+  // One hipMalloc per array: a single arena with the arrays at staggered
+  // offsets (0 / 256 B .. 64 KB per array) measured no better (march P+S
+  // 0.104-0.117 ms either way, profiles/r2_4_march_depth.log)
+  {
+    const size_t nv = (size_t)N + 2;
+    HIP_TRY(dmalloc(&d.r, nv));
+    HIP_TRY(dmalloc(&d.p0, nv));
+    HIP_TRY(dmalloc(&d.p1, nv));
+    HIP_TRY(dmalloc(&d.q, nv));
+    HIP_TRY(dmalloc(&d.x, nv));
+    HIP_TRY(dmalloc(&d.code, (size_t)N + 8));
+  }
+  h->grid = cg_grid(N);
+  int cus = 0;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, h->device) != hipSuccess)
+    cus = 0;
+  h->tile_h = kTileHMax;
+  while (h->tile_h > 8 && cdiv(std::max(g.n - 2, 0), h->tile_h) * cdiv(g.m, kTileW) < kMinTiles)
+    h->tile_h /= 2;
+  h->tile_grid = cdiv(std::max(g.n - 2, 0), h->tile_h) * cdiv(g.m, kTileW);
+  // register-march kernel (full 128-column strips): reduction buffers for
+  // its largest grid (band height 1)
+  h->march_grid_max =
+      g.m % kMarchW == 0 && g.n > 2 ? cdiv((g.m / kMarchW) * (g.n - 2), kMarchWaves) : 0;
+  march_geometry(h);
+  res_geometry(h);
+  // grid of the streaming B in the fused formats.  Vectors that fit the
+  // 256 MB Infinity Cache (L <= 4096): two long-lived workgroups per CU
+  // (L = 4096: 0.063 vs 0.069 ms for 8192 short ones; 256 .. 2048 long
+  // ones 0.069-0.079).  Larger vectors: short workgroups of 2 pairs per
+  // thread, dispatched in address order, so the accesses in flight stay
+  // in a narrow window of the arrays (L = 8192: 0.312 ms vs 0.361 with
+  // 512, 0.334 with 16384); the partials buffer bounds the grid
+  if ((size_t)N * sizeof(double) > kLargeVector)
+    h->b_grid = std::min<long long>(cdiv((long long)N, 4ll * kBlock), red_grid(h));
+  else
+    h->b_grid = std::min(2 * cus, h->grid);
+  if (h->res_G > 0) {
+    HIP_TRY(dmalloc(&d.res_xch, (size_t)2 * h->res_G * 2 * 2 * g.m));
+    HIP_TRY(dmalloc(&d.res_bar, 9 * kTicketStride));
+    HIP_TRY(dmalloc(&d.res_gran, (size_t)2 * 3 * h->res_G));
+  }
+  HIP_TRY(dmalloc(&d.partials, kRedSlots * red_partials_size(red_grid(h))));
+  HIP_TRY(dmalloc(&d.tickets, kRedSlots * red_tickets_size(red_grid(h))));
+  HIP_TRY(hipMemset(d.tickets, 0, kRedSlots * red_tickets_size(red_grid(h)) * sizeof(unsigned)));
+  HIP_TRY(dmalloc(&d.scal, 1));
+  HIP_TRY(dmalloc(&d.iout, 2 * (size_t)g.m));
+  HIP_TRY(hipMemset(d.bocc, 0, (size_t)h->nb + 8));
+  HIP_TRY(hipMemset(d.socc, 0, t + 8));
+  return hipStreamSynchronize(st);
+}
+
+hipError_t dev_alloc_matrix(perc_ctx* h, int N, long long nnz) {
+  DeviceBuffers& d = h->d;
+  h->N = N;
+  h->nnz = nnz;
+  HIP_TRY(dmalloc(&d.rowptr, N + 1));
+  HIP_TRY(dmalloc(&d.col, (size_t)nnz + 8));
+  HIP_TRY(dmalloc(&d.val, (size_t)nnz + 8));
+  HIP_TRY(dmalloc(&d.diag, N + 2));
+  HIP_TRY(dmalloc(&d.rhs, N + 2));
+  const size_t nv = (size_t)N + 2;
+  HIP_TRY(dmalloc(&d.x, nv));
+  HIP_TRY(dmalloc(&d.r, nv));
+  HIP_TRY(dmalloc(&d.p0, nv));
+  HIP_TRY(dmalloc(&d.p1, nv));
+  HIP_TRY(dmalloc(&d.q, nv));
+  h->grid = cg_grid(N);
+  h->tile_grid = 0;
+  h->march_grid = h->march_grid_max = 0;
+  HIP_TRY(dmalloc(&d.partials, kRedSlots * red_partials_size(red_grid(h))));
+  HIP_TRY(dmalloc(&d.tickets, kRedSlots * red_tickets_size(red_grid(h))));
+  HIP_TRY(hipMemset(d.tickets, 0, kRedSlots * red_tickets_size(red_grid(h)) * sizeof(unsigned)));
+  HIP_TRY(dmalloc(&d.scal, 1));
+  return hipSuccess;
+}
+
+void dev_free_all(perc_ctx* h) {
+  DeviceBuffers& d = h->d;
+  void* ptrs[] = {d.bond_first, d.rowptr, d.col, d.val, d.diag, d.rhs, d.code, d.dtab, d.sflag, d.bocc, d.socc,
+                  d.order, d.parent, d.member, d.top, d.counters, d.x, d.r,
+                  d.p0, d.p1, d.q, d.partials, d.tickets, d.scal, d.err_hist, d.iout,
+                  d.res_xch, d.res_bar, d.bw, d.code_sm, d.csize, d.res_gran, (void*)d.nib_sm,
+                  d.sel_hist, d.sel_cand, d.mgran, d.forms_dev};
+  for (void* p : ptrs)
+    if (p) hipFree(p);
+  d = DeviceBuffers{};
+  h->N = 0;
+  h->nnz = 0;
+}
+
+// band height of the register-march kernel over `nrows` rows: the
+// requested height (perc_set_march_rows); vectors past the Infinity Cache:
+// 8-row bands for the row-major march B (0.310 vs 0.318 ms at 16 rows at
+// L = 8192; its P runs one round of slot-mapped bands instead,
+// march_slots_rm; 16 rows without PERC_MARCH_SLOTS); else one round of
+// resident waves, the height that gives every wave slot of the chip one
+// strip-band
+int march_rows_for(const perc_ctx* h, int nrows) {
+  const Geom& g = h->g;
+  if (h->march_rows_req > 0) return h->march_rows_req;
+  if ((size_t)g.m * nrows * sizeof(double) > kLargeVector)
+    return (h->march_mode & PERC_MARCH_SLOTS) ? 8 : 16;
+  int cus = 0, per_cu = 0;
+  hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, h->device);
+  hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_cg_march<kMarchP, true, 3, kNT, false, true>,
+                                               64 * kMarchWaves, 0);
+  const long long slots = (long long)std::max(cus, 1) * std::max(per_cu, 1) * kMarchWaves;
+  const long long bands = std::max(1ll, slots / (g.m / kMarchW));
+  return std::max(2, cdiv(nrows, bands));
+}
+
+// band height and grid of the register-march kernel; the slot-weighted
+// bands (PERC_MARCH_SLOTS): one workgroup per CU and round, bands cycling
+// over the rounds, weights = the rounds' relative streaming rates with
+// equal bands (kSlotW: P, B of the strip-major march, row-major P past the
+// Infinity Cache; same-box A/Bs, profiles/r3_4_ab_slotw_L4096.log and the
+// r3 L = 8192 probes -- flat weights there, i.e. one round of equal bands:
+// 0.364 ms vs 0.387 at 100:80:60 and 0.403 for the 16-row bands)
+constexpr int kSlotW[3][kMaxSlotRounds] = {{100, 75, 50, 40}, {100, 80, 60, 50}, {100, 100, 100, 100}};
+
+void march_geometry(perc_ctx* h) {
+  const Geom& g = h->g;
+  h->march_grid = 0;
+  h->wm_slots = 0;
+  h->wm_grid = 0;
+  if (g.m % kMarchW != 0 || g.n <= 2) return;
+  const int spr = g.m / kMarchW, nrows = g.n - 2;
+  h->march_h = march_rows_for(h, nrows);
+  h->march_grid = cdiv(spr * cdiv(nrows, h->march_h), kMarchWaves);
+  int cus = 0, per_cu = 0;
+  hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, h->device);
+  hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_cg_march<kMarchP, true, 3, kNT, false, true>,
+                                               64 * kMarchWaves, 0);
+  const long long waves = (long long)cus * kMarchWaves;
+  const int(*wts)[kMaxSlotRounds] = h->slot_w_set ? h->slot_w : kSlotW;
+  bool ok = cus > 0 && per_cu >= 2 && per_cu <= kMaxSlotRounds && waves % spr == 0 &&
+            (waves / spr) * per_cu <= nrows;
+  for (int i = 0; ok && i < per_cu; ++i) ok = wts[0][i] > 0 && wts[1][i] > 0 && wts[2][i] > 0;
+  if (ok) {
+    h->wm_slots = per_cu;
+    h->wm_grid = cus * per_cu;
+    for (int k = 0; k < 3; ++k) {
+      h->wm_cum[k][0] = 0;
+      for (int i = 0; i < per_cu; ++i) h->wm_cum[k][i + 1] = h->wm_cum[k][i] + wts[k][i];
+    }
+  }
+}
+
+// resident solve: m a multiple of 1024 (MT = m / 1024 columns per thread
+// and row), or m < 1024 with m threads per workgroup rounded up to whole
+// waves (one column each: mid-size lattices, whose launched kernels are
+// latency-bound), the
+// band height H of ceil(nrows / CUs) rows within the LDS and register
+// budget, one workgroup per CU
+void res_geometry(perc_ctx* h) {
+  const Geom& g = h->g;
+  h->res_G = 0;
+  const bool narrow = g.m < kResThreads;
+  if ((g.m % kResThreads != 0 && !narrow) || g.n <= 2) return;
+  int cus = 0, coop = 0;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, h->device) != hipSuccess ||
+      hipDeviceGetAttribute(&coop, hipDeviceAttributeCooperativeLaunch, h->device) != hipSuccess ||
+      !coop || cus <= 0)
+    return;
+  h->res_NT = narrow ? (g.m + 63) / 64 * 64 : kResThreads;  // whole waves
+  const int nrows = g.n - 2, MT = narrow ? 1 : g.m / kResThreads;
+  const int H = cdiv(nrows, cus);
+  // m = 1024: at most 4 rows per CU (r, q, code of 4 elements per thread
+  // in registers, 97 VGPRs); m = 2048: at most 8 rows per CU, q formed
+  // twice instead of kept (16 elements per thread: r and code only)
+  if (!((MT == 1 && H <= 4) || (MT == 2 && H <= 8)) || (long long)H * g.m > kResLdsRows) return;
+  for (int f = 0; f < h->forms.nforms; ++f)
+    if (!h->forms.regular[f]) return;  // wrapped columns (pbc): slot order is not raster order
+  h->res_MT = MT;
+  h->res_H = H;
+  h->res_HMAX = MT == 1 ? 4 : 8;
+  h->res_G = cdiv(nrows, H);
+}
+
+// solver kernels for the requested format and what the assembly allows
+void select_format(perc_ctx* h) {
+  h->stencil = h->fmt_req != PERC_FMT_CSR && h->stencil_ok;
+  h->fused = h->stencil && h->tiled_ok && h->fmt_req != PERC_FMT_STENCIL_SPLIT;
+  h->march = h->fused && h->march_ok && h->fmt_req != PERC_FMT_STENCIL_TILED;
+  const bool literal = h->dot_order == PERC_DOT_LITERAL;
+  // (dev_solve only: the march kernels stay selected for the probes)
+  h->resident = h->fused && h->res_G > 0 && h->fmt_req != PERC_FMT_STENCIL_TILED &&
+                (h->march_mode & PERC_SOLVE_RESIDENT) && h->march_rows_req == 0 && !literal;
+  // the literal dot order folds q.p from the stored q: the q-storing kernels
+  h->qfree = h->march && (h->march_mode & PERC_MARCH_QFREE) && !literal;
+  h->march_alt = h->march && (h->march_mode & PERC_MARCH_ALT);
+  // one-workgroup solve for small systems, under the default format only
+  // (an explicit format keeps its launched kernels, e.g. for the tests)
+  h->small = h->fmt_req == PERC_FMT_AUTO && h->N > 0 && h->N <= kSmallRows &&
+             (h->march_mode & PERC_SOLVE_RESIDENT) && h->d.rowptr != nullptr;
+  // strip-major q-free march only while a vector fits the Infinity Cache
+  // (L <= 4096): past it (16-row bands, several rounds of waves) the
+  // row-major march is faster (L = 8192: 0.439 vs 0.480 ms,
+  // profiles/r2_11_ab_strips.log); its whole-array buffer views also need
+  // < 2 GB
+  h->strips = h->qfree && (h->march_mode & PERC_MARCH_STRIPS) &&
+              ((size_t)h->N * sizeof(double) <= kLargeVector || (h->march_mode & PERC_MARCH_BIG_STRIPS));
+  // slot-weighted bands of the strip-major march (to_strips applies them)
+  const bool slots = (h->march_mode & PERC_MARCH_SLOTS) != 0;
+  h->march_slots = slots && h->strips && h->wm_slots > 0;
+  // row-major q-free march past the Infinity Cache (L = 8192): P on one round
+  // of bands (the slot mapping with the third weight set), B on 8-row bands
+  // (march_rows_for): P 0.364 + B 0.310 vs 0.403 + 0.318 ms per iteration
+  // (r3 L = 8192 probes)
+  h->march_slots_rm = slots && h->qfree && !h->strips && (size_t)h->N * sizeof(double) > kLargeVector &&
+                      h->wm_slots > 0;
+  // tagged-granule reductions of the strip-major march (PERC_MARCH_TAG);
+  // their tags are (epoch << 24) | iteration, so solves of >= 2^24 - 2
+  // iterations take the ticket reduction
+  h->march_tag = (h->march_mode & PERC_MARCH_TAG) && h->strips;
+}
+
+// strip-major copies of r (into the q buffer: r and q swap roles for the
+// solve) and of the row codes; a switches to them
+hipError_t to_strips(perc_ctx* h, CGArgs& a) {
+  DeviceBuffers& d = h->d;
+  hipStream_t st = h->stream;
+  if (!d.code_sm) HIP_TRY(dmalloc(&d.code_sm, (size_t)h->N + 8));
+  const long long n = (long long)a.T.nrows * a.T.m;
+  k_to_strips<uint16_t><<<blocks_for(n), kBlock, 0, st>>>(a.T, d.code, d.code_sm);
+  k_to_strips<double><<<blocks_for(n), kBlock, 0, st>>>(a.T, d.r, d.q);
+  HIP_TRY(dbg_sync(st, "k_to_strips"));
+  a.r = d.q;
+  a.q = d.r;
+  a.St.code = d.code_sm;
+  a.sm = 1;
+  a.bx = 1;  // x (row-major) is updated in the q-free march B
+  // nibble codes (PERC_MARCH_NIBBLE, square lattice): 0.5 instead of 2
+  // bytes of row code per element in both march kernels
+  h->nib_used = false;
+  if (h->nib_ok && (h->march_mode & PERC_MARCH_NIBBLE)) {
+    if (!d.nib_sm) HIP_TRY(dmalloc(&d.nib_sm, (size_t)h->N / 2 + 16));
+    HIP_TRY(hipMemsetAsync(d.sflag + 3, 0, sizeof(int), st));
+    k_pack_nib<<<blocks_for(n / 2), kBlock, 0, st>>>(a.T, d.code, d.nib_sm, h->ncls[0], h->ncls[1],
+                                                     h->ncls[2], d.sflag + 3);
+    HIP_TRY(dbg_sync(st, "k_pack_nib"));
+    int bad = 0;
+    HIP_TRY(hipMemcpyAsync(&bad, d.sflag + 3, sizeof(int), hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    if (!bad) {
+      a.nib = d.nib_sm;
+      for (int c = 0; c < 3; ++c) a.ncls[c] = h->ncls[c];
+    }
+    h->nib_used = !bad;
+  }
+  if (h->march_slots) {
+    a.wslots = h->wm_slots;
+    for (int i = 0; i <= h->wm_slots; ++i) {
+      a.wcum[0][i] = h->wm_cum[0][i];
+      a.wcum[1][i] = h->wm_cum[1][i];
+    }
+  }
+  return hipSuccess;
+}
+
+// The resident solve's synchronisation floor (perc_bench_kernel 6): the
+// same cooperative grid running only what an iteration of k_cg_res does to
+// synchronise -- the two block sums and the two tagged-granule all-gathers
+// (res_gather<1>, res_gather<2>) -- on dummy values, `iters` times.  The
+// time per iteration is what the resident solve cannot go below whatever
+// its memory traffic.
+__global__ __launch_bounds__(1024) void k_res_sync_probe(ResArgs a, int iters) {
+  __shared__ double s_red[32];
+  unsigned epoch = 0;
+  double v1[1] = {(double)blockIdx.x}, tot1[1], acc2[2], tot2[2];
+  for (int k = 0; k < iters; ++k) {
+    double w1[1] = {v1[0] + (double)threadIdx.x};
+    block_sum<1>(w1, s_red);
+    if (!res_gather<1>(a, epoch, a.gran, w1, tot1, s_red)) break;
+    acc2[0] = tot1[0] * 1e-30 + (double)threadIdx.x;
+    acc2[1] = (double)k;
+    block_sum<2>(acc2, s_red);
+    if (!res_gather<2>(a, epoch, a.gran + 2 * (size_t)a.G, acc2, tot2, s_red)) break;
+    v1[0] = tot2[0] * 1e-30;
+  }
+}
+
+// the resident kernel for m = 1024 (MT = 1) / 2048, square-lattice
+// positions only (sq) or all eight
+// (NT threads per workgroup, m of them for m <= 1024: with one column per
+// thread the template's NT is only the launch bound, so widths up to 512
+// share the 512-bound instantiation -- 125-142 VGPRs, no spills)
+const void* res_kernel(int MT, bool sq, int NT) {
+  if (MT == 1 && NT <= 512)
+    return sq ? (const void*)k_cg_res<1, 4, true, kResSquareMask, 512>
+              : (const void*)k_cg_res<1, 4, true, 0xFFu, 512>;
+  if (MT == 1)
+    return sq ? (const void*)k_cg_res<1, 4, true, kResSquareMask>
+              : (const void*)k_cg_res<1, 4, true, 0xFFu>;
+  return sq ? (const void*)k_cg_res<2, 8, false, kResSquareMask>
+            : (const void*)k_cg_res<2, 8, false, 0xFFu>;
+}
+
+// one cooperative launch runs the whole iteration loop (k_cg_res)
+hipError_t dev_solve_resident(perc_ctx* h, const CGArgs& ca, int* iter, double* err) {
+  DeviceBuffers& d = h->d;
+  hipStream_t st = h->stream;
+  ResArgs a;
+  a.St = ca.St;
+  a.m = h->g.m;
+  a.nrows = h->g.n - 2;
+  a.pbc = h->g.pbc;
+  a.G = h->res_G;
+  a.H = h->res_H;
+  a.xrows = ca.xrows;
+  a.r0 = d.r;
+  a.x = d.x;
+  a.S = d.scal;
+  a.err_hist = d.err_hist;
+  a.err_hist_cap = d.err_hist_cap;
+  a.xch = d.res_xch;
+  a.bar = d.res_bar;
+  a.gran = d.res_gran;
+  HIP_TRY(hipMemsetAsync(d.res_bar, 0, 9 * kTicketStride * sizeof(unsigned), st));
+  HIP_TRY(hipMemsetAsync(d.res_gran, 0, (size_t)2 * 3 * h->res_G * sizeof(double), st));
+  void* args[] = {&a};
+  // reductions by tagged-granule all-gather (res_gather): L = 1024 15.5 vs
+  // 16.6 us per iteration against a counter barrier + partial reads, L =
+  // 2048 33.7 vs 34.65 (profiles/r2_10_resident_gather_ab.log)
+  const bool sq = (h->forms.umask & ~kResSquareMask) == 0;
+  const void* fn = res_kernel(h->res_MT, sq, h->res_NT);
+  KernelTiming& T = h->timing;
+  if (T.enabled) {
+    if (T.ev.size() < 2) T.ev.resize(2, nullptr);
+    for (int i = 0; i < 2; ++i)
+      if (!T.ev[i]) HIP_TRY(timing_event_create(&T.ev[i]));
+    HIP_TRY(hipEventRecord(T.ev[0], st));
+  }
+  HIP_TRY(hipLaunchCooperativeKernel(fn, dim3(a.G), dim3(h->res_NT), args, 0, st));
+  HIP_TRY(dbg_sync(st, "k_cg_res"));
+  if (T.enabled) HIP_TRY(hipEventRecord(T.ev[1], st));
+  CGScalars hs{};
+  HIP_TRY(hipMemcpyAsync(&hs, d.scal, sizeof(hs), hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipStreamSynchronize(st));
+  if (hs.pad[0] != 0) {
+    fprintf(stderr, "[perc] k_cg_res: grid barrier timed out\n");
+    return hipErrorLaunchTimeOut;
+  }
+  if (T.enabled && hs.iter > 0) {
+    float ms = 0.f;
+    HIP_TRY(hipEventElapsedTime(&ms, T.ev[0], T.ev[1]));
+    T.spmv_ms += ms;  // whole iterations: P+S and B together
+    T.spmv_n += hs.iter;
+  }
+  *iter = hs.iter;
+  *err = hs.err;
+  return hipSuccess;
+}
+
+
+hipError_t dev_solve(perc_ctx* h, int itol, double tol, int itmax, bool x0_zero, bool full_x,
+                     int* iter, double* err) {
+  DeviceBuffers& d = h->d;
+  hipStream_t st = h->stream;
+  const bool literal = h->dot_order == PERC_DOT_LITERAL;
+  if (literal && h->nslab > 1) {
+    set_error("the literal dot order sums over the whole system: one slab only");
+    return hipErrorInvalidValue;
+  }
+  if (!h->stencil) HIP_TRY(ensure_csr(h));
+  if (d.err_hist_cap < itmax + 2) {
+    if (d.err_hist) HIP_TRY(hipFree(d.err_hist));
+    d.err_hist_cap = itmax + 2;
+    HIP_TRY(dmalloc(&d.err_hist, d.err_hist_cap));
+  }
+  CGScalars hs{};
+  hs.tol = tol;
+  hs.itmax = itmax;
+  hs.bkden = 1.0;
+  HIP_TRY(hipMemcpyAsync(d.scal, &hs, sizeof(hs), hipMemcpyHostToDevice, st));
+  HIP_TRY(hipMemsetAsync(d.tickets, 0, kRedSlots * red_tickets_size(red_grid(h)) * sizeof(unsigned),
+                         st));
+  if (x0_zero) {
+    k_zero<<<blocks_for(h->N + 2), kBlock, 0, st>>>(d.x, h->N + 2);
+  }
+  // row slabs (perc_set_slabs; the prologue starts from x = 0, as linbcg's
+  // callers do)
+  if (h->nslab > 1 && x0_zero) return dev_solve_slabs(h, h->nslab, itol, tol, itmax, full_x, iter, err);
+  CGArgs a = make_cg_args(h);
+  // linbcg never reads x inside the iteration (r is recursive), and the
+  // terminal currents read it only on the interior rows next to the
+  // electrodes (bondc.f:554-592): unless the caller wants every voltage, x
+  // is carried on the first and last lattice rows only -- bitwise the same
+  // values there, 16 B/row/iteration less traffic
+  a.xrows = full_x || h->g.m <= 0 ? 0 : h->g.m;
+  const int G = h->grid;
+  const bool ST = h->stencil;
+  if (ST) k_cg_init<true><<<G, kBlock, 0, st>>>(a, itol, x0_zero ? 1 : 0);
+  else k_cg_init<false><<<G, kBlock, 0, st>>>(a, itol, x0_zero ? 1 : 0);
+  HIP_TRY(dbg_sync(st, "k_cg_init"));
+  if (literal) {  // bnrm and the first bknum in ascending j
+    if (ST) k_fold_init<true><<<1, 64, 0, st>>>(a, itol);
+    else k_fold_init<false><<<1, 64, 0, st>>>(a, itol);
+    HIP_TRY(dbg_sync(st, "k_fold_init"));
+  }
+  if (h->small) {  // one workgroup runs the whole loop (k_cg_small)
+    // (x is kept on every row here: the operator is the CSR one and N small)
+    if (ST) {
+      if (literal) k_cg_small<true, true><<<1, kSmallThreads, 0, st>>>(a);
+      else k_cg_small<true, false><<<1, kSmallThreads, 0, st>>>(a);
+    } else {
+      if (literal) k_cg_small<false, true><<<1, kSmallThreads, 0, st>>>(a);
+      else k_cg_small<false, false><<<1, kSmallThreads, 0, st>>>(a);
+    }
+    HIP_TRY(dbg_sync(st, "k_cg_small"));
+    CGScalars hs{};
+    HIP_TRY(hipMemcpyAsync(&hs, d.scal, sizeof(hs), hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    *iter = hs.iter;
+    *err = hs.err;
+    return hipSuccess;
+  }
+  if (h->resident) {
+    const hipError_t e = dev_solve_resident(h, a, iter, err);
+    // the cooperative launch can be refused when the grid cannot be
+    // co-resident (e.g. CUs taken by another context): nothing ran, r and
+    // the scalars are as k_cg_init left them, so the launched kernels take
+    // over for this solve
+    if (e != hipErrorCooperativeLaunchTooLarge && e != hipErrorInvalidConfiguration) return e;
+    (void)hipGetLastError();
+    fprintf(stderr, "[perc] resident solve not launchable (%s): launched kernels\n",
+            hipGetErrorString(e));
+    h->resident = false;
+  }
+  if (h->strips) HIP_TRY(to_strips(h, a));
+  HIP_TRY(setup_granules(h, a, itmax));
+  // row-major q-free march past the Infinity Cache: the P kernel on one
+  // round of slot-weighted bands, B on its short bands
+  if (!h->strips && h->march && h->qfree && h->march_slots_rm && h->wm_slots > 0) {
+    a.wslots = h->wm_slots;
+    for (int i = 0; i <= h->wm_slots; ++i) a.wcum[0][i] = h->wm_cum[2][i];
+  }
+  // iterate in chunks; the device flag makes surplus launches no-ops
+  int chunk = 8;
+  CGScalars* hsp = nullptr;
+  HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&hsp), sizeof(CGScalars)));
+  hipError_t e = hipSuccess;
+  long long launched = 0;
+  KernelTiming& T = h->timing;
+  const int kMaxChunk = 256;
+  // per timed iteration: start/stop of P, S and B, recorded by the
+  // kernels' own dispatch packets (klaunch)
+  constexpr int kEv = 6;
+  if (T.enabled && T.ev.size() < kEv * (size_t)kMaxChunk) {
+    const size_t have = T.ev.size();
+    T.ev.resize(kEv * (size_t)kMaxChunk);
+    for (size_t i = have; i < T.ev.size(); ++i) HIP_TRY(timing_event_create(&T.ev[i]));
+  }
+  int done_iters = 0;
+  // kernel timing samples every kTimeEvery-th iteration of a chunk
+  constexpr int kTimeEvery = 8;
+  // phase probe (PERC_MARCH_TRACE=<csv>): per-wave stamps of the P and B
+  // launches of iterations PERC_MARCH_TRACE_IT (default 1000) .. +3
+  const char* mtpath = getenv("PERC_MARCH_TRACE");
+  const int mt_it = getenv("PERC_MARCH_TRACE_IT") ? atoi(getenv("PERC_MARCH_TRACE_IT")) : 1000;
+  constexpr int kMtN = 4;  // traced iterations
+  unsigned long long* mtbuf = nullptr;
+  const size_t mtwaves = (size_t)std::max(h->march_grid, h->wm_grid) * kMarchWaves;
+  if (mtpath && h->march && a.sm && h->qfree) {
+    HIP_TRY(dmalloc(&mtbuf, (size_t)2 * kMtN * 4 * mtwaves));
+    HIP_TRY(hipMemsetAsync(mtbuf, 0, (size_t)2 * kMtN * 4 * mtwaves * 8, st));
+  }
+  while (true) {
+    for (int j = 0; j < chunk; ++j) {
+      const bool tm = T.enabled && j % kTimeEvery == 0;
+      hipEvent_t* ev = tm ? &T.ev[kEv * j] : nullptr;
+      a.kiter = (int)(launched + j + 1);
+      // (tag: exact in a double while solve_epoch < 2^29)
+      a.mtag = (double)(((unsigned long long)h->solve_epoch << 24) | (unsigned long long)a.kiter);
+      const int mti = a.kiter - mt_it;
+      a.mtrace = mtbuf && mti >= 0 && mti < kMtN ? mtbuf + (size_t)2 * mti * 4 * mtwaves : nullptr;
+      if (!h->fused) {
+        if (tm) h->ev_next[0] = ev[0], h->ev_next[1] = ev[1];
+        if (ST) klaunch(h, k_cg_p<true>, G, kBlock, st, a);
+        else klaunch(h, k_cg_p<false>, G, kBlock, st, a);
+        HIP_TRY(dbg_sync(st, "k_cg_p"));
+      }
+      if (tm) h->ev_next[0] = ev[2], h->ev_next[1] = ev[3];
+      launch_cg_spmv(h, a, G);
+      HIP_TRY(dbg_sync(st, "k_cg_spmv"));
+      if (literal) {  // akden in ascending j, then ak
+        k_fold_qp<<<1, 64, 0, st>>>(a);
+        HIP_TRY(dbg_sync(st, "k_fold_qp"));
+      }
+      if (tm) h->ev_next[0] = ev[4], h->ev_next[1] = ev[5];
+      if (a.mtrace) a.mtrace += 4 * mtwaves;
+      launch_cg_b(h, a, G);
+      a.mtrace = nullptr;
+      HIP_TRY(dbg_sync(st, "k_cg_b"));
+      h->ev_next[0] = h->ev_next[1] = nullptr;
+      if (literal) {  // z.r and r.r in ascending j: bk, err, the stop test
+        if (ST) k_fold_b<true><<<1, 64, 0, st>>>(a);
+        else k_fold_b<false><<<1, 64, 0, st>>>(a);
+        HIP_TRY(dbg_sync(st, "k_fold_b"));
+      }
+    }
+    launched += chunk;
+    e = hipGetLastError();
+    if (e != hipSuccess) break;
+    e = hipMemcpyAsync(hsp, d.scal, sizeof(CGScalars), hipMemcpyDeviceToHost, st);
+    if (e != hipSuccess) break;
+    e = hipStreamSynchronize(st);
+    if (e != hipSuccess) break;
+    if (T.enabled) {  // launches of this chunk that did work
+      const int real = std::min(chunk, hsp->iter - done_iters);
+      int nt = 0;
+      for (int j = 0; j < real; j += kTimeEvery, ++nt) {
+        float tp = 0.f, ts = 0.f, tb = 0.f;
+        if (!h->fused) hipEventElapsedTime(&tp, T.ev[kEv * j], T.ev[kEv * j + 1]);
+        hipEventElapsedTime(&ts, T.ev[kEv * j + 2], T.ev[kEv * j + 3]);
+        hipEventElapsedTime(&tb, T.ev[kEv * j + 4], T.ev[kEv * j + 5]);
+        T.p_ms += tp;
+        T.spmv_ms += ts;
+        T.update_ms += tb;
+      }
+      T.spmv_n += nt;
+      T.update_n += nt;
+      T.p_n += nt;
+    }
+    done_iters = hsp->iter;
+    if (hsp->done) break;
+    if (launched > (long long)itmax + 2) break;  // cannot happen: device stops at itmax+1
+    chunk = std::min(chunk * 2, kMaxChunk);
+  }
+  if (e == hipSuccess && hsp->iter > 0 && !a.bx) {
+    k_cg_xfinal<<<G, kBlock, 0, st>>>(a);
+    e = dbg_sync(st, "k_cg_xfinal");
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+  }
+  if (mtbuf) {
+    std::vector<unsigned long long> tr((size_t)2 * kMtN * 4 * mtwaves);
+    if (e == hipSuccess) e = hipMemcpy(tr.data(), mtbuf, tr.size() * 8, hipMemcpyDeviceToHost);
+    (void)hipFree(mtbuf);
+    if (FILE* fo = e == hipSuccess ? fopen(mtpath, "a") : nullptr) {
+      fprintf(fo, "# m=%d nrows=%d band_rows=%d grid=%d waves=%zu (wall clock ticks, 100 MHz)\n"
+                  "iter,kernel,wave,t_entry,t_walk_end,t_exit,xcc,hw_id\n",
+              h->g.m, h->g.n - 2, h->march_h, h->march_grid, mtwaves);
+      for (int it = 0; it < kMtN; ++it)
+        for (int kb = 0; kb < 2; ++kb)
+          for (size_t wv = 0; wv < mtwaves; ++wv) {
+            const unsigned long long* v = &tr[((size_t)(2 * it + kb) * mtwaves + wv) * 4];
+            fprintf(fo, "%d,%s,%zu,%llu,%llu,%llu,%llu,%llu\n", mt_it + it, kb ? "B" : "P", wv, v[0],
+                    v[1], v[2], v[3] >> 32, v[3] & 0xffffffffull);
+          }
+      fclose(fo);
+    }
+  }
+  if (e == hipSuccess && a.mgran && hsp->pad[1] != 0) {
+    fprintf(stderr, "[perc] k_cg_march: reduction granule not seen within the poll limit\n");
+    e = hipErrorLaunchTimeOut;
+  }
+  *iter = hsp->iter;
+  *err = hsp->err;
+  hipHostFree(hsp);
+  return e;
+}
+
+hipError_t dev_spmv(perc_ctx* h, const double* x, double* y) {
+  if (!h->stencil) HIP_TRY(ensure_csr(h));
+  DeviceBuffers& d = h->d;
+  hipStream_t st = h->stream;
+  const size_t bytes = sizeof(double) * h->N;
+  HIP_TRY(hipMemcpyAsync(d.p0, x, bytes, hipMemcpyHostToDevice, st));
+  CGArgs a = make_cg_args(h);
+  launch_spmv(h, a, d.p0, d.q);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipMemcpyAsync(y, d.q, bytes, hipMemcpyDeviceToHost, st));
+  return hipStreamSynchronize(st);
+}
+
+hipError_t dev_selftest_division(long long n, unsigned long long seed, unsigned long long* out3) {
+  unsigned long long* d = nullptr;
+  HIP_TRY(dmalloc(&d, 3));
+  HIP_TRY(hipMemset(d, 0, 3 * sizeof(unsigned long long)));
+  k_selftest_div<<<4096, kBlock>>>(n, seed, d);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipMemcpy(out3, d, 3 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+  return hipFree(d);
+}
+
+hipError_t dev_bench(perc_ctx* h, int which, int reps, double* ms) {
+  HIP_TRY(ensure_csr(h));  // the probes run every format
+  DeviceBuffers& d = h->d;
+  hipStream_t st = h->stream;
+  CGArgs a = make_cg_args(h);
+  const bool ST = h->stencil;
+  // scalars for a steady-state iteration (iter = 1 -> general p update)
+  CGScalars hs{};
+  hs.bknum = 1.0;
+  hs.bkden = 2.0;
+  hs.bk = 0.5;
+  hs.ak = 0.5;
+  hs.bnrm = 1.0;
+  hs.tol = -1.0;
+  hs.itmax = 1 << 30;
+  hs.iter = 1;
+  a.kiter = 2;
+  // the solve's layout and reductions for the CG kernels (the plain SpMV
+  // probe stays row-major): strip-major copies, tagged granules
+  if (h->strips && (which == 1 || which == 2 || which == 5)) {
+    HIP_TRY(to_strips(h, a));
+    HIP_TRY(setup_granules(h, a, hs.itmax));
+  }
+  // row-major q-free march past the Infinity Cache: P on the solve's slot
+  // bands (dev_solve)
+  if (!h->strips && h->march && h->qfree && h->march_slots_rm && h->wm_slots > 0) {
+    a.wslots = h->wm_slots;
+    for (int i = 0; i <= h->wm_slots; ++i) a.wcum[0][i] = h->wm_cum[2][i];
+  }
+  HIP_TRY(hipMemcpyAsync(d.scal, &hs, sizeof(hs), hipMemcpyHostToDevice, st));
+  HIP_TRY(hipMemsetAsync(d.tickets, 0, kRedSlots * red_tickets_size(red_grid(h)) * sizeof(unsigned),
+                         st));
+  if (which == 6 && h->res_G <= 0) return hipErrorInvalidConfiguration;  // no resident grid
+  // STREAM copy: 512 MB -> 512 MB, well past the 256 MB Infinity Cache
+  double *cp_src = nullptr, *cp_dst = nullptr;
+  const size_t cp_n = (size_t)64 << 20;
+  if (which == 4) {
+    HIP_TRY(dmalloc(&cp_src, cp_n));
+    HIP_TRY(dmalloc(&cp_dst, cp_n));
+    HIP_TRY(hipMemsetAsync(cp_src, 0, cp_n * sizeof(double), st));
+  }
+  hipError_t lerr = hipSuccess;
+  auto launch = [&]() {
+    const int G = h->grid;
+    if (which == 0) {
+      launch_spmv(h, a, d.p0, d.q);
+    } else if (which == 1) {
+      launch_cg_spmv(h, a, G);
+    } else if (which == 2) {
+      launch_cg_b(h, a, G);
+    } else if (which == 3) {
+      if (ST) k_cg_p<true><<<G, kBlock, 0, st>>>(a);
+      else k_cg_p<false><<<G, kBlock, 0, st>>>(a);
+    } else if (which == 6) {  // resident sync floor: 16 iterations per launch
+      ResArgs ra{};
+      ra.G = h->res_G;
+      ra.gran = d.res_gran;
+      ra.S = d.scal;
+      int iters = 16;
+      void* args[] = {&ra, &iters};
+      (void)hipMemsetAsync(d.res_gran, 0, (size_t)2 * 3 * h->res_G * sizeof(double), st);
+      // a refused grid (CUs taken) must not time an empty stream
+      const hipError_t le = hipLaunchCooperativeKernel((const void*)k_res_sync_probe, dim3(ra.G),
+                                                       dim3(h->res_NT), args, 0, st);
+      if (le != hipSuccess && lerr == hipSuccess) lerr = le;
+    } else if (which == 5) {  // one whole iteration
+      if (!h->fused) {
+        if (ST) k_cg_p<true><<<G, kBlock, 0, st>>>(a);
+        else k_cg_p<false><<<G, kBlock, 0, st>>>(a);
+      }
+      launch_cg_spmv(h, a, G);
+      launch_cg_b(h, a, G);
+    } else {
+      k_copy<<<cdiv(cp_n / 2, kBlock), kBlock, 0, st>>>(cp_src, cp_dst, (int)cp_n);
+    }
+  };
+  // the B kernel advances iter (tol < 0 keeps it running); values are
+  // irrelevant for timing
+  for (int i = 0; i < 3; ++i) launch();
+  HIP_TRY(lerr);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipEventRecord(h->ev[0], st));
+  for (int i = 0; i < reps; ++i) launch();
+  HIP_TRY(hipEventRecord(h->ev[1], st));
+  HIP_TRY(hipEventSynchronize(h->ev[1]));
+  HIP_TRY(lerr);
+  float t = 0.f;
+  HIP_TRY(hipEventElapsedTime(&t, h->ev[0], h->ev[1]));
+  *ms = (double)t / reps / (which == 6 ? 16 : 1);
+  if (cp_src) HIP_TRY(hipFree(cp_src));
+  if (cp_dst) HIP_TRY(hipFree(cp_dst));
+  return hipSuccess;
+}
+
+}  // namespace perc

@@ -1,5 +1,5 @@
 #!/bin/bash
-# round 4: loop-in-libperc solve (group K=1 exchange forms, one process per GPU), its
+# round 4: the GPU suite on libperc split by phase; loop-in-libperc solve (group K=1 exchange forms, one process per GPU), its
 # per-iteration cost at K=1, the L=8192 strip-major A/B, the L=4096 PMC reconcile of the
 # nibble march, the literal dot order at config 2 (tol 1e-8)
 mkdir -p gpurun_out
@@ -14,9 +14,8 @@ step() {  # step NAME TIMEOUT CMD...
   tail -3 "gpurun_out/r4e_$name.out"
   [ "$rc" -eq 0 ] || exit "$rc"
 }
-step pytest_dslab 400 python -u -m pytest -x -v --timeout 200 --timeout-method thread tests/test_dslab.py
+step pytest_gpu 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests/
 step dslab_bench 300 python -u tools/dslab_bench.py --L 4096 --iters 2000 --torch
 step l8192 300 python -u tools/l8192_probe.py --L 8192 --reps 10
 L=4096 CBX2=1 bash tools/pmc_r2.sh || { tail -20 gpurun_out/pmc_r2.log; exit 1; }
 tail -8 gpurun_out/pmc_r2_reconcile_L4096.csv
-step literal_c2 480 python -u tools/literal_config.py c2_sq1024_bond_p50 1e-08
