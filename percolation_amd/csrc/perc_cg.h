@@ -182,7 +182,7 @@ __global__ __launch_bounds__(kBlock) void k_cg_p(CGArgs a) {
 
 // S(k): q = A p and akden = q.p, then ak = bknum/akden.  SL = 0: CSR,
 // SL = 4 / 6: stencil operator with that many slots per row.
-template <int SL>
+template <int SL, int NS = 0>  // NS: CSR slots (SL = 0)
 __global__ __launch_bounds__(kBlock) void k_cg_spmv(CGArgs a) {
   CGScalars* S = a.S;
   if (S->done) return;
@@ -198,10 +198,7 @@ __global__ __launch_bounds__(kBlock) void k_cg_spmv(CGArgs a) {
     const int wid = threadIdx.x >> 6;
     int t0, t1;
     block_tiles(a.A.N, &t0, &t1);
-    if (a.A.maxrow <= kMaxNnzRow)
-      spmv_tiles_pipe<true>(a.A, a.p, a.q, t0 + wid, t1, kWaves, s_prod[SL ? 0 : wid], &dot[0]);
-    else
-      spmv_tiles<true>(a.A, a.p, a.q, t0 + wid, t1, kWaves, s_prod[SL ? 0 : wid], &dot[0]);
+    spmv_tiles_any<true, NS>(a.A, a.p, a.q, t0 + wid, t1, kWaves, s_prod[SL ? 0 : wid], &dot[0]);
   }
   double tot[1];
   if (publish_and_reduce<1>(dot, a.partials, a.tickets, xcd_logical_block(blockIdx.x, gridDim.x),

@@ -133,28 +133,34 @@ __device__ __forceinline__ void wave_lds_order() {
 // following one another.  Every load is unconditional (clamped indices), so
 // the waits count exactly.  Per row the arithmetic is spmv_tile's: y(i) =
 // d(i) x(i), then the products in ascending column order (bitwise dsprsax).
+// NS entry slots per lane and tile: rows of <= NS off-diagonals (4 on the
+// square lattice, 6 on the triangular one; CsrView.maxrow picks), so the
+// square lattice's tiles issue 4 (col, val) loads, gathers and products per
+// lane instead of 6.
+template <int NS>
 struct CsrStage {
   int a, b;  // this lane's row range
-  int c[kMaxNnzRow];
-  double v[kMaxNnzRow];
+  int c[NS];
+  double v[NS];
 };
 __device__ __forceinline__ void csr_rowptr(const CsrView& A, int tile, int& a, int& b) {
   const int r = min(tile * 64 + (int)(threadIdx.x & 63), A.N - 1);
   a = A.rowptr[r];
   b = A.rowptr[r + 1];
 }
-__device__ __forceinline__ void csr_entries(const CsrView& A, int tile, CsrStage& S) {
+template <int NS>
+__device__ __forceinline__ void csr_entries(const CsrView& A, int tile, CsrStage<NS>& S) {
   const int lane = threadIdx.x & 63, r0 = tile * 64;
   const int last = min(63, A.N - 1 - r0);
   const int e0 = __shfl(S.a, 0, 64);
   const int jmax = max(__shfl(S.b, last, 64) - e0 - 1, 0);
   // the columns first: the next tile's gathers wait for them only
 #pragma unroll
-  for (int s = 0; s < kMaxNnzRow; ++s) S.c[s] = A.col[e0 + min(lane + 64 * s, jmax)];
+  for (int s = 0; s < NS; ++s) S.c[s] = A.col[e0 + min(lane + 64 * s, jmax)];
 #pragma unroll
-  for (int s = 0; s < kMaxNnzRow; ++s) S.v[s] = A.val[e0 + min(lane + 64 * s, jmax)];
+  for (int s = 0; s < NS; ++s) S.v[s] = A.val[e0 + min(lane + 64 * s, jmax)];
 }
-template <bool DOT>
+template <bool DOT, int NS>
 __device__ __forceinline__ void spmv_tiles_pipe(const CsrView& A, const double* __restrict__ x,
                                                 double* __restrict__ y, int tile0, int t1, int stride,
                                                 double* s_prod, double* dot) {
@@ -163,14 +169,14 @@ __device__ __forceinline__ void spmv_tiles_pipe(const CsrView& A, const double* 
   const __amdgpu_buffer_rsrc_t ry = rsrc(y, (unsigned)A.N * 8u);
   // two stages that swap roles every tile (unrolled by two: no register
   // copies of loads in flight, which would wait for them)
-  CsrStage s0, s1;
+  CsrStage<NS> s0, s1;
   csr_rowptr(A, tile0, s0.a, s0.b);
   csr_entries(A, tile0, s0);
   csr_rowptr(A, min(tile0 + stride, t1 - 1), s1.a, s1.b);
   // tile `tile` from `cur`; the next tile's entries into `nxt` (its row
   // pointers are there already), the row pointers of the one after into
   // (an, bn)
-  auto step = [&](int tile, CsrStage& cur, CsrStage& nxt, int& an, int& bn) {
+  auto step = [&](int tile, CsrStage<NS>& cur, CsrStage<NS>& nxt, int& an, int& bn) {
     // (tile >= t1: the unrolled loop's padding step -- cur holds the last
     // tile again, every lane invalid, nothing stored)
     const int r0 = min(tile, t1 - 1) * 64, r = r0 + lane;
@@ -180,9 +186,9 @@ __device__ __forceinline__ void spmv_tiles_pipe(const CsrView& A, const double* 
     // the stages alternate -- receive the tile after next
     const int e0 = __shfl(cur.a, 0, 64);
     const int k0 = cur.a - e0, kn = cur.b - cur.a;
-    double xv[kMaxNnzRow];
+    double xv[NS];
 #pragma unroll
-    for (int s = 0; s < kMaxNnzRow; ++s) xv[s] = x[cur.c[s]];
+    for (int s = 0; s < NS; ++s) xv[s] = x[cur.c[s]];
     const double xi = x[rr], di = A.diag[rr];
     csr_entries(A, min(tile + stride, t1 - 1), nxt);  // (past the last tile: unused)
     csr_rowptr(A, min(tile + 2 * stride, t1 - 1), an, bn);
@@ -190,14 +196,14 @@ __device__ __forceinline__ void spmv_tiles_pipe(const CsrView& A, const double* 
     // a gather (the scheduler would otherwise interleave them)
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-    for (int s = 0; s < kMaxNnzRow; ++s) s_prod[lane + 64 * s] = cur.v[s] * xv[s];
+    for (int s = 0; s < NS; ++s) s_prod[lane + 64 * s] = cur.v[s] * xv[s];
     wave_lds_order();
     // the row's products in order, a fixed unrolled count with selects (no
     // lane-divergent loop, no branch around the store: exact waits)
     double acc = di * xi;
 #pragma unroll
-    for (int j = 0; j < kMaxNnzRow; ++j) {
-      const double pj = s_prod[min(k0 + j, 64 * kMaxNnzRow - 1)];
+    for (int j = 0; j < NS; ++j) {
+      const double pj = s_prod[min(k0 + j, 64 * NS - 1)];
       acc = j < kn ? acc + pj : acc;
     }
     __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, acc), ry,
@@ -211,6 +217,18 @@ __device__ __forceinline__ void spmv_tiles_pipe(const CsrView& A, const double* 
   }
 }
 
+// a wave's tiles: the pipelined tiles with NS slots (NS = csr_slots(maxrow),
+// a template parameter of the kernels, so each instantiation allocates the
+// registers of its own slot count), or the general ones (NS = 0)
+template <bool DOT, int NS>
+__device__ __forceinline__ void spmv_tiles_any(const CsrView& A, const double* __restrict__ x,
+                                               double* __restrict__ y, int tile0, int t1, int stride,
+                                               double* s_prod, double* dot) {
+  if constexpr (NS > 0) spmv_tiles_pipe<DOT, NS>(A, x, y, tile0, t1, stride, s_prod, dot);
+  else spmv_tiles<DOT>(A, x, y, tile0, t1, stride, s_prod, dot);
+}
+inline int csr_slots(int maxrow) { return maxrow <= 4 ? 4 : (maxrow <= kMaxNnzRow ? kMaxNnzRow : 0); }
+
 // wave tiles [t0, t1) of a logical block, strided over its 4 waves
 __device__ __forceinline__ void block_tiles(int N, int* t0, int* t1) {
   const int ntile = cdiv(N, 64);
@@ -220,6 +238,7 @@ __device__ __forceinline__ void block_tiles(int N, int* t0, int* t1) {
   *t1 = min(*t0 + chunk, ntile);
 }
 
+template <int NS>
 __global__ __launch_bounds__(kBlock) void k_spmv(CsrView A, const double* __restrict__ x,
                                                  double* __restrict__ y) {
   __shared__ double s_prod[kWaves][64 * kMaxNnzRow];
@@ -227,10 +246,29 @@ __global__ __launch_bounds__(kBlock) void k_spmv(CsrView A, const double* __rest
   int t0, t1;
   block_tiles(A.N, &t0, &t1);
   double dummy = 0.0;
-  if (A.maxrow <= kMaxNnzRow) spmv_tiles_pipe<false>(A, x, y, t0 + wid, t1, kWaves, s_prod[wid], &dummy);
-  else spmv_tiles<false>(A, x, y, t0 + wid, t1, kWaves, s_prod[wid], &dummy);
+  spmv_tiles_any<false, NS>(A, x, y, t0 + wid, t1, kWaves, s_prod[wid], &dummy);
 }
 
+// y = A x on a stream: k_spmv at the rows' slot count, one resident round
+// of workgroups (no reduction, so the grid is free; each wave then walks
+// ~50 tiles at L = 4096 and the pipeline's fill and drain are amortised)
+inline void spmv_launch(perc_ctx* h, const CsrView& A, const double* x, double* y, hipStream_t st) {
+  const int ns = csr_slots(A.maxrow);
+  const void* k = ns == 4 ? (const void*)k_spmv<4> : ns == kMaxNnzRow ? (const void*)k_spmv<kMaxNnzRow>
+                                                                       : (const void*)k_spmv<0>;
+  if (h->spmv_ns != ns || h->spmv_n != A.N) {  // (once per system)
+    int cus = 0, per_cu = 0;
+    hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, h->device);
+    hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, kBlock, 0);
+    h->spmv_grid = std::max(1, std::min(std::max(cus, 1) * std::max(per_cu, 1), cdiv(cdiv(A.N, 64), kWaves)));
+    h->spmv_ns = ns;
+    h->spmv_n = A.N;
+  }
+  const int grid = h->spmv_grid;
+  if (ns == 4) k_spmv<4><<<grid, kBlock, 0, st>>>(A, x, y);
+  else if (ns == kMaxNnzRow) k_spmv<kMaxNnzRow><<<grid, kBlock, 0, st>>>(A, x, y);
+  else k_spmv<0><<<grid, kBlock, 0, st>>>(A, x, y);
+}
 
 }  // namespace
 }  // namespace perc

@@ -114,7 +114,12 @@ void launch_cg_spmv(perc_ctx* h, const CGArgs& a, int G) {
       else if (th == 16) klaunch(h, k_cg_ps<6, true, 16>, G2, B2, st, a);
       else klaunch(h, k_cg_ps<6, true, 8>, G2, B2, st, a);
     }
-  } else if (!h->stencil) klaunch(h, k_cg_spmv<0>, G, kBlock, h->stream, a);
+  } else if (!h->stencil) {
+    const int ns = csr_slots(a.A.maxrow);
+    if (ns == 4) klaunch(h, k_cg_spmv<0, 4>, G, kBlock, h->stream, a);
+    else if (ns == kMaxNnzRow) klaunch(h, k_cg_spmv<0, kMaxNnzRow>, G, kBlock, h->stream, a);
+    else klaunch(h, k_cg_spmv<0, 0>, G, kBlock, h->stream, a);
+  }
   else if (h->g.scn == 4) klaunch(h, k_cg_spmv<4>, G, kBlock, h->stream, a);
   else klaunch(h, k_cg_spmv<6>, G, kBlock, h->stream, a);
 }
@@ -142,7 +147,7 @@ void launch_cg_b(perc_ctx* h, const CGArgs& a, int G) {
 }
 
 void launch_spmv(perc_ctx* h, const CGArgs& a, const double* x, double* y) {
-  if (!h->stencil) k_spmv<<<h->grid, kBlock, 0, h->stream>>>(a.A, x, y);
+  if (!h->stencil) spmv_launch(h, a.A, x, y, h->stream);
   else if (h->g.scn == 4) k_spmv_st<4><<<h->grid, kBlock, 0, h->stream>>>(a.St, x, y);
   else k_spmv_st<6><<<h->grid, kBlock, 0, h->stream>>>(a.St, x, y);
 }

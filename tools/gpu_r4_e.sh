@@ -15,6 +15,7 @@ step() {  # step NAME TIMEOUT CMD...
   [ "$rc" -eq 0 ] || exit "$rc"
 }
 step pytest_gpu 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests/
+step bench 300 python -u bench.py --steps 2 --warmup 1 --no-cpu-baseline
 step dslab_bench 300 python -u tools/dslab_bench.py --L 4096 --iters 2000 --torch
 step l8192 300 python -u tools/l8192_probe.py --L 8192 --reps 10
 L=4096 CBX2=1 bash tools/pmc_r2.sh || { tail -20 gpurun_out/pmc_r2.log; exit 1; }
