@@ -18,7 +18,9 @@ module perc_api
   ! association of linbcg's dot products (perc_set_dot_order)
   integer(c_int), parameter :: PERC_DOT_FAST = 0, PERC_DOT_LITERAL = 1
   ! transports of the split solve (perc_dslab_solve_group)
-  integer(c_int), parameter :: PERC_XPORT_RCCL = 0, PERC_XPORT_HOST = 1
+  integer(c_int), parameter :: PERC_XPORT_RCCL = 0, PERC_XPORT_HOST = 1, PERC_XPORT_EXCHANGE = 4
+  ! bytes of the RCCL unique id of the one-process-per-GPU split solve
+  integer(c_int), parameter :: PERC_DSLAB_ID_BYTES = 128
   ! off-diagonal value of bonds outside the spanning cluster (bondc.f:487)
   real(c_double), parameter :: PERC_LEAK = 1.0d-12
 
@@ -178,6 +180,32 @@ module perc_api
       real(c_double), value :: Va, g0, leak, tol
       type(perc_cond_result) :: res
     end function perc_dslab_solve_group
+
+    ! the same loop with one process per GPU (an MPI program: rank 0 calls
+    ! perc_dslab_unique_id, MPI_Bcast's the PERC_DSLAB_ID_BYTES bytes, every
+    ! rank binds its labeled context to slab s of K, then perc_dslab_solve)
+    integer(c_int) function perc_dslab_unique_id(id, nbytes) bind(C, name='perc_dslab_unique_id')
+      import :: c_int, c_ptr
+      type(c_ptr), value :: id
+      integer(c_int), value :: nbytes
+    end function perc_dslab_unique_id
+    integer(c_int) function perc_dslab_comm_init(h, K, s, id, nbytes) bind(C, name='perc_dslab_comm_init')
+      import :: c_int, c_ptr
+      type(c_ptr), value :: h, id
+      integer(c_int), value :: K, s, nbytes
+    end function perc_dslab_comm_init
+    integer(c_int) function perc_dslab_comm_free(h) bind(C, name='perc_dslab_comm_free')
+      import :: c_int, c_ptr
+      type(c_ptr), value :: h
+    end function perc_dslab_comm_free
+    integer(c_int) function perc_dslab_solve(h, rule, cur_rule, Va, g0, leak, itol, tol, itmax, &
+        full_x, res) bind(C, name='perc_dslab_solve')
+      import :: c_int, c_ptr, c_double, perc_cond_result
+      type(c_ptr), value :: h
+      integer(c_int), value :: rule, cur_rule, itol, itmax, full_x
+      real(c_double), value :: Va, g0, leak, tol
+      type(perc_cond_result) :: res
+    end function perc_dslab_solve
 
     ! multi-GPU ensemble: one host thread + context per device, RCCL stats
     integer(c_int) function perc_ensemble_create(ndev, devices, lattice, m, n, pbc, e) &
