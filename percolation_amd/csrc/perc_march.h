@@ -42,6 +42,14 @@ __device__ __forceinline__ double bld1(__amdgpu_buffer_rsrc_t r, unsigned off) {
 __device__ __forceinline__ double bld1s(__amdgpu_buffer_rsrc_t r, unsigned off) {
   return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, (int)off, 0, 16));
 }
+// cache policy of the march's p / q / r stores: nontemporal (probe builds:
+// -DPERC_MARCH_SAUX=<aux>, e.g. 16 = sc1 write-through, which leaves no
+// dirty line in the XCD's L2 for the end-of-kernel write-back)
+#ifndef PERC_MARCH_SAUX
+#define PERC_MARCH_SAUX 2
+#endif
+constexpr int kStAux = PERC_MARCH_SAUX;
+
 template <int AUX>
 __device__ __forceinline__ void bst2(__amdgpu_buffer_rsrc_t r, unsigned off, double2 v) {
   __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, (int)off, 0, AUX);
@@ -394,7 +402,7 @@ __device__ __forceinline__ void march_step(const CGArgs& a, const MGeom& g, cons
       const bool own = gr >= g.r0 && gr < g.rend;
       const bool pst = (unsigned)(gr - B.lo) < (unsigned)(B.hi - B.lo) &&
                        (own || (a.slab && (gr < 0 || gr >= nrows)));
-      bst2<kNT>(B.pn, pst ? melem<SM>(a, B, gr, g.col) * 8u : kOOB, pn);
+      bst2<kStAux>(B.pn, pst ? melem<SM>(a, B, gr, g.col) * 8u : kOOB, pn);
       if (MODE == kMarchP && !SM) {  // x += ak p(k-1) on the x rows (the P-only march keeps x)
         const int i = gr * m + g.col;
         const bool xw = own && !first && !a.bx && (a.xrows == 0 || i < a.xrows || i >= N - a.xrows);
@@ -483,8 +491,8 @@ __device__ __forceinline__ void march_step(const CGArgs& a, const MGeom& g, cons
   {
     const int m = a.T.m;
     const unsigned eq = SM ? (unsigned)sm_at(a.T, mid, g.col) : (unsigned)((mid - g.r0) * m + g.col);
-    if (MODE == kMarchPQ) bst2<kNT>(B.q, mown ? eq * 8u : kOOB, mq);
-    if (MODE == kMarchB) bst2<kNT>(B.r, mown ? melem<SM>(a, B, mid, g.col) * 8u : kOOB, mr);
+    if (MODE == kMarchPQ) bst2<kStAux>(B.q, mown ? eq * 8u : kOOB, mq);
+    if (MODE == kMarchB) bst2<kStAux>(B.r, mown ? melem<SM>(a, B, mid, g.col) * 8u : kOOB, mr);
   }
 }
 

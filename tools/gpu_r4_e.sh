@@ -18,5 +18,5 @@ step pytest_gpu 900 python -u -m pytest -x -q --timeout 300 --timeout-method thr
 step bench 300 python -u bench.py --steps 2 --warmup 1 --no-cpu-baseline
 step dslab_bench 300 python -u tools/dslab_bench.py --L 4096 --iters 2000 --torch
 step l8192 300 python -u tools/l8192_probe.py --L 8192 --reps 10
-L=4096 CBX2=1 bash tools/pmc_r2.sh || { tail -20 gpurun_out/pmc_r2.log; exit 1; }
-tail -8 gpurun_out/pmc_r2_reconcile_L4096.csv
+step store_ab 300 python -u tools/store_ab.py --L 4096 --libs main,s16,s18,s17
+step label_trace 120 env PERC_TILE_TRACE=1 python -u tools/label_probe.py --L 4096 --reps 4

@@ -1,0 +1,87 @@
+#!/usr/bin/env python3
+"""Same-box A/B of libperc probe builds (percolation_amd/probe/libperc_<tag>.so,
+`make -C percolation_amd/csrc probe TAG=... PFLAGS=...`) against the
+in-tree library: per library, in a child process of its own (PERC_LIBPERC),
+one L x L bond realisation, perc_bench_kernel 1 (P), 2 (B) and 5 (a whole
+iteration), best of 3 x `reps` launches, plus ms per iteration of
+fixed-iteration solves (slope between itmax/2 and itmax, tol 0); the
+libraries alternate for `rounds` rounds and each figure keeps its best.
+
+  python tools/store_ab.py --L 4096 --libs main,s16,s18 [--mode 1559]
+"""
+import argparse
+import json
+import os
+import subprocess
+import sys
+import time
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+
+
+def child(args):
+    from percolation_amd import _lib as PL
+    from percolation_amd import api
+    L_ = args.L
+    nb = api.nbonds(0, L_, L_, 0)
+    out = {}
+    with api.Context(0, L_, L_, 0) as ctx:
+        if args.mode >= 0:
+            ctx.set_march_mode(args.mode)
+        ctx.occupy_random(PL.BOND, 0, int(args.p * nb), 777)
+        assert ctx.label()["nspan"] > 0
+        c = ctx.conductance(tol=1e-8, itmax=args.iters)
+        out["fp"] = [c["iter"], c["gtop"], c["gbot"]]  # same numbers across store policies
+        for w, k in ((1, "P"), (2, "B"), (5, "iteration")):
+            out[k] = min(ctx.bench_kernel(w, args.reps) for _ in range(3))
+        t = {}
+        for n in (args.iters // 2, args.iters):
+            t0 = time.perf_counter()
+            it = ctx.conductance(tol=0.0, itmax=n - 1)["iter"]
+            t[n] = (time.perf_counter() - t0, it)
+        (t1, i1), (t2, i2) = t[args.iters // 2], t[args.iters]
+        out["solve_ms_per_it"] = (t2 - t1) * 1e3 / (i2 - i1)
+    print(json.dumps(out), flush=True)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--L", type=int, default=4096)
+    ap.add_argument("--p", type=float, default=0.6)
+    ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--iters", type=int, default=600)
+    ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--mode", type=int, default=-1)
+    ap.add_argument("--libs", default="main")
+    ap.add_argument("--child", action="store_true")
+    args = ap.parse_args()
+    if args.child:
+        return child(args)
+    libs = args.libs.split(",")
+    best = {}
+    fps = {}
+    for _ in range(args.rounds):
+        for lib in libs:
+            env = dict(os.environ)
+            if lib != "main":
+                env["PERC_LIBPERC"] = os.path.join(REPO, "percolation_amd", "probe", "libperc_%s.so" % lib)
+            cmd = [sys.executable, os.path.abspath(__file__), "--child", "--L", str(args.L), "--p", str(args.p),
+                   "--reps", str(args.reps), "--iters", str(args.iters), "--mode", str(args.mode)]
+            r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600)
+            if r.returncode != 0:
+                sys.stderr.write(r.stderr[-3000:])
+                raise SystemExit("child %s failed rc=%d" % (lib, r.returncode))
+            o = json.loads(r.stdout.strip().splitlines()[-1])
+            fps.setdefault(lib, o.pop("fp"))
+            b = best.setdefault(lib, {})
+            for k, v in o.items():
+                b[k] = min(b.get(k, 9e9), v)
+    out = {lib: {k: round(v, 5) for k, v in b.items()} for lib, b in best.items()}
+    out["fingerprints"] = fps
+    out["L"] = args.L
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()
