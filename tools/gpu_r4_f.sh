@@ -1,0 +1,11 @@
+#!/bin/bash
+# round 4: fresh L=4096 PMC reconcile of the default march (nibble codes), the BASELINE
+# configs (config 5 as stated), the literal dot order at config 2 (tol 1e-8)
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+L=4096 CBX2=1 bash tools/pmc_r2.sh || { tail -20 gpurun_out/pmc_r2.log; exit 1; }
+tail -8 gpurun_out/pmc_r2_reconcile_L4096.csv
+bash tools/configs.sh || { tail -5 gpurun_out/configs.log; exit 1; }
+tail -12 gpurun_out/configs.log
+timeout -k 10 480 python -u tools/literal_config.py c2_sq1024_bond_p50 1e-08 > gpurun_out/r4_literal_c2.log 2>&1
+rc=$?; tail -3 gpurun_out/r4_literal_c2.log; exit $rc

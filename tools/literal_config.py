@@ -14,6 +14,7 @@ per tolerance; exit status 1 on any difference.
 import json
 import os
 import sys
+import threading
 import time
 
 HERE = os.path.dirname(os.path.abspath(__file__))
@@ -30,6 +31,14 @@ from test_config_goldens import occupation  # noqa: E402
 
 def main():
     case, tols = sys.argv[1], sys.argv[2:] or ["1e-08"]
+    # a heartbeat on stderr while a solve runs (minutes in the literal order)
+    t_start = time.time()
+    stop = threading.Event()
+
+    def beat():
+        while not stop.wait(30.0):
+            print("... %.0f s" % (time.time() - t_start), file=sys.stderr, flush=True)
+    threading.Thread(target=beat, daemon=True).start()
     doc = json.load(open(os.path.join(REPO, "tests", "golden", "configs", case + ".json")))
     rc = doc["recipe"]
     occ, rule, cur = occupation(rc)
@@ -57,6 +66,7 @@ def main():
                                   seconds=round(secs, 1),
                                   ms_per_iteration=round(secs * 1e3 / max(c["iter"], 1), 3))),
                   flush=True)
+    stop.set()
     return 0 if ok else 1
 
 
