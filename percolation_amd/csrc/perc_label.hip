@@ -244,7 +244,8 @@ __global__ void k_occupy_sites(const int* order, int count, int t, uint8_t* socc
 //                 coalesced.  No global atomics.
 //  k_cc_merge     only the links that cross a block edge (sites on the top
 //                 row or the edge columns of a block: ~1/32 + 2/128 of them)
-//                 are united in the global array (lock-free CAS, same rule).
+//                 are united in the global array (lock-free CAS, same rule;
+//                 neighbouring lanes with the same pair of parents unite once).
 //  k_cc_compress  parent[s] = final root; cluster count reduced per
 //                 workgroup (one atomic per workgroup of a fixed grid).
 //
@@ -456,13 +457,66 @@ __global__ __launch_bounds__(kCcThreads) void k_cc_tile(Geom g, int kind, const 
   }
 }
 
+#ifndef PERC_CC_MERGE_ROWS
+// The links that cross a block edge, with neighbouring lanes on neighbouring
+// sites of the same edge: part A, the blocks' top rows (every column: the
+// links up into the next block row), one workgroup per kCcThreads columns;
+// part B, the other rows' candidate columns (the block edge columns and the
+// last column), one workgroup per candidate column and kCcThreads rows.
+// Before any union a lane reads the parents of its link's two sites (after
+// k_cc_tile: the block-local roots, or ancestors of them); a lane whose pair
+// equals the previous lane's skips its union -- that lane's union joins the
+// same two sets (by induction down to the first lane of the run).  Along an
+// edge most crossing links join the same two block components, so most
+// unions drop out; the rest start one hop closer to the roots.
+__global__ __launch_bounds__(kCcThreads) void k_cc_merge(Geom g, int kind, const int* bond_first,
+                                                         const uint8_t* bocc,
+                                                         const uint8_t* socc, int* parent,
+                                                         uint8_t* member, int nseg, int nfull) {
+  const int ntx = cdiv(g.m, kCcW), lane = threadIdx.x & 63;
+  int row, c;
+  if ((int)blockIdx.x < nfull * nseg) {  // A: block-top row, columns of segment
+    row = (blockIdx.x / nseg) * kCcH + kCcH - 1;
+    c = (blockIdx.x % nseg) * kCcThreads + threadIdx.x;
+  } else {  // B: candidate column j, rows of block rb (block-top rows are A's)
+    const int e = blockIdx.x - nfull * nseg, nrb = cdiv(g.n, kCcThreads);
+    const int j = e / nrb;
+    row = (e % nrb) * kCcThreads + threadIdx.x;
+    c = j == 2 * ntx ? g.m - 1 : min((j >> 1) * kCcW + (j & 1) * (kCcW - 1), g.m - 1);
+    if (row % kCcH == kCcH - 1) row = g.n;  // (part A's)
+  }
+  const int s = row * g.m + c + 1;
+  bool site = row < g.n && c < g.m && s <= g.t - 1 && (kind == PERC_BOND || socc[s]);
+  int nn[6] = {0, 0, 0, 0, 0, 0}, fb = 0;
+  if (site) {
+    nearestn_rc(g, s, row, c, nn);
+    fb = bond_first[s];
+  }
+  int r = 0;
+  for (int k = 0; k < g.scn; ++k) {  // (uniform trip count: the shuffles below)
+    const int q = nn[k];
+    const bool fwd = site && q > s;
+    bool want = fwd && cc_link(kind, bocc, socc, fb + r, s, q);
+    r += fwd ? 1 : 0;
+    if (want) {
+      const int qrow = div_m(g, q - 1), qcol = q - 1 - qrow * g.m;
+      want = !(qrow / kCcH == row / kCcH && qcol / kCcW == c / kCcW);  // inside: k_cc_tile's
+    }
+    if (want && kind == PERC_BOND) member[q] = 1;
+    const int a = want ? parent[s] : -1, b = want ? parent[q] : -1;
+    const int pa = __shfl_up(a, 1, 64), pb = __shfl_up(b, 1, 64);
+    if (want && !(lane > 0 && pa == a && pb == b)) unite(parent, a, b);
+  }
+}
+#else
+// (probe build: the round-3 mapping, one workgroup per lattice row)
 // one workgroup per lattice row: the sites whose forward links may leave
 // their block (block top row: every column; other rows: the block edge
 // columns and the last column), then only the links that do
 __global__ __launch_bounds__(kCcThreads) void k_cc_merge(Geom g, int kind, const int* bond_first,
                                                          const uint8_t* bocc,
                                                          const uint8_t* socc, int* parent,
-                                                         uint8_t* member) {
+                                                         uint8_t* member, int, int) {
   // workgroups 0..n-1: one lattice row each (its first kCcThreads
   // candidates); then the block-top rows' further candidates, nseg - 1
   // workgroups of kCcThreads per such row (the unions are spread over the
@@ -504,6 +558,8 @@ __global__ __launch_bounds__(kCcThreads) void k_cc_merge(Geom g, int kind, const
     }
   }
 }
+
+#endif
 
 // sum of v over the workgroup of kCcThreads, then one atomic add
 __device__ __forceinline__ void block_count_add(int v, int* counter) {
@@ -777,8 +833,14 @@ hipError_t dev_label(perc_ctx* h, int* nspan, int* span_list, int* nclusters) {
   HIP_TRY(dbg_sync(st, "k_cc_tile"));
   const int nseg = cdiv(g.m, kCcThreads);
   const int nfull = g.n / kCcH;  // rows kCcH-1, 2kCcH-1, ... (< n)
+#ifndef PERC_CC_MERGE_ROWS
+  const int ncand = 2 * cdiv(g.m, kCcW) + 1;
+  k_cc_merge<<<nfull * nseg + ncand * cdiv(g.n, kCcThreads), kCcThreads, 0, st>>>(
+      g, kind, d.bond_first, d.bocc, d.socc, d.parent, d.member, nseg, nfull);
+#else
   k_cc_merge<<<g.n + (nseg > 1 ? nfull * (nseg - 1) : 0), kCcThreads, 0, st>>>(
-      g, kind, d.bond_first, d.bocc, d.socc, d.parent, d.member);
+      g, kind, d.bond_first, d.bocc, d.socc, d.parent, d.member, nseg, nfull);
+#endif
   HIP_TRY(dbg_sync(st, "k_cc_merge"));
   k_cc_compress<<<std::min(cdiv(g.t, kCcThreads), kReduceGrid), kCcThreads, 0, st>>>(
       g.t, d.parent, d.member, d.counters + 1);

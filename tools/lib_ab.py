@@ -2,12 +2,17 @@
 """Same-box A/B of libperc probe builds (percolation_amd/probe/libperc_<tag>.so,
 `make -C percolation_amd/csrc probe TAG=... PFLAGS=...`) against the
 in-tree library: per library, in a child process of its own (PERC_LIBPERC),
-one L x L bond realisation, perc_bench_kernel 1 (P), 2 (B) and 5 (a whole
-iteration), best of 3 x `reps` launches, plus ms per iteration of
-fixed-iteration solves (slope between itmax/2 and itmax, tol 0); the
-libraries alternate for `rounds` rounds and each figure keeps its best.
+the libraries alternating for `rounds` rounds, each figure its best.
 
-  python tools/store_ab.py --L 4096 --libs main,s16,s18 [--mode 1559]
+--what solve: one L x L bond realisation, perc_bench_kernel 1 (P), 2 (B) and
+  5 (a whole iteration), best of 3 x `reps` launches, plus ms per iteration
+  of fixed-iteration solves (slope between itmax/2 and itmax, tol 0);
+--what label: per realisation (device-drawn bond occupancy, `reps`
+  realisations), wall ms of perc_occupy_random, perc_label (labels +
+  spanning test + its read-back) and the partition's cluster count.
+
+  python tools/lib_ab.py --L 4096 --libs main,s16,s18 [--mode 1559]
+  python tools/lib_ab.py --what label --L 4096 --libs main,mrows
 """
 import argparse
 import json
@@ -20,9 +25,35 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
 
 
+def child_label(args):
+    import torch  # (torch.cuda.synchronize: a device-wide wait)
+    from percolation_amd import _lib as PL
+    from percolation_amd import api
+    L_ = args.L
+    nb = api.nbonds(0, L_, L_, 0)
+    occ, lab, fp = [], [], []
+    with api.Context(0, L_, L_, 0) as ctx:
+        for k in range(args.reps + 1):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            ctx.occupy_random(PL.BOND, 0, int(args.p * nb), 1000 + k)
+            torch.cuda.synchronize()
+            t1 = time.perf_counter()
+            li = ctx.label()
+            t2 = time.perf_counter()
+            if k:
+                occ.append((t1 - t0) * 1e3)
+                lab.append((t2 - t1) * 1e3)
+            fp.append([li["nspan"], li["nclusters"]])
+    med = lambda v: sorted(v)[len(v) // 2]  # noqa: E731
+    print(json.dumps(dict(fp=fp, occupy_ms=med(occ), label_ms=med(lab))), flush=True)
+
+
 def child(args):
     from percolation_amd import _lib as PL
     from percolation_amd import api
+    if args.what == "label":
+        return child_label(args)
     L_ = args.L
     nb = api.nbonds(0, L_, L_, 0)
     out = {}
@@ -54,6 +85,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--mode", type=int, default=-1)
     ap.add_argument("--libs", default="main")
+    ap.add_argument("--what", default="solve", choices=("solve", "label"))
     ap.add_argument("--child", action="store_true")
     args = ap.parse_args()
     if args.child:
@@ -67,7 +99,8 @@ def main():
             if lib != "main":
                 env["PERC_LIBPERC"] = os.path.join(REPO, "percolation_amd", "probe", "libperc_%s.so" % lib)
             cmd = [sys.executable, os.path.abspath(__file__), "--child", "--L", str(args.L), "--p", str(args.p),
-                   "--reps", str(args.reps), "--iters", str(args.iters), "--mode", str(args.mode)]
+                   "--reps", str(args.reps), "--iters", str(args.iters), "--mode", str(args.mode),
+                   "--what", args.what]
             r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600)
             if r.returncode != 0:
                 sys.stderr.write(r.stderr[-3000:])
