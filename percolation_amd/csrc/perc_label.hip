@@ -315,7 +315,10 @@ __global__ __launch_bounds__(kCcThreads) void k_cc_tile(Geom g, int kind, const 
   // forward links are (s, s+1), (s, s+m), bond ids fb, fb+1 (nearestn_square
   // lists +1 before +m in every such case).  All bond_first loads first,
   // then all link loads: two memory latencies per thread, not 2 per site.
-  constexpr int kG = 4;  // sites per batch: loads of a batch in flight together
+#ifndef PERC_CC_G
+#define PERC_CC_G 4  // (probe builds: -DPERC_CC_G=8)
+#endif
+  constexpr int kG = PERC_CC_G;  // sites per batch: loads of a batch in flight together
   static_assert(kPer % kG == 0, "batches");
   for (int k0 = 0; k0 < kPer; k0 += kG) {
     int fbv[kG];
