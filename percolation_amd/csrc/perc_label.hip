@@ -256,6 +256,9 @@ __global__ void k_occupy_sites(const int* order, int count, int t, uint8_t* socc
 #endif
 constexpr int kCcW = 128, kCcH = PERC_CC_H, kCcSites = kCcW * kCcH, kCcThreads = 256;
 constexpr int kReduceGrid = 1024;  // fixed grid of the counting passes
+#ifndef PERC_CC_COMPRESS_GRID
+#define PERC_CC_COMPRESS_GRID 1024  // k_cc_compress's grid cap (probe builds: 16384)
+#endif
 
 __device__ __forceinline__ int find_root(int* parent, int x) {
   int p = parent[x];
@@ -845,7 +848,7 @@ hipError_t dev_label(perc_ctx* h, int* nspan, int* span_list, int* nclusters) {
       g, kind, d.bond_first, d.bocc, d.socc, d.parent, d.member, nseg, nfull);
 #endif
   HIP_TRY(dbg_sync(st, "k_cc_merge"));
-  k_cc_compress<<<std::min(cdiv(g.t, kCcThreads), kReduceGrid), kCcThreads, 0, st>>>(
+  k_cc_compress<<<std::min(cdiv(g.t, kCcThreads), PERC_CC_COMPRESS_GRID), kCcThreads, 0, st>>>(
       g.t, d.parent, d.member, d.counters + 1);
   HIP_TRY(dbg_sync(st, "k_cc_compress"));
   k_span_top<<<1, 1024, 0, st>>>(g, d.parent, d.member, d.top, d.counters);

@@ -19,5 +19,5 @@ step bench 300 python -u bench.py --steps 2 --warmup 1 --no-cpu-baseline
 step dslab_bench 300 python -u tools/dslab_bench.py --L 4096 --iters 2000 --torch
 step l8192 300 python -u tools/l8192_probe.py --L 8192 --reps 10
 step store_ab 300 python -u tools/lib_ab.py --L 4096 --libs main,s16,s18,s17
-step label_ab 300 python -u tools/lib_ab.py --what label --L 4096 --reps 6 --libs main,mrows,g8,h16,h64
+step label_ab 300 python -u tools/lib_ab.py --what label --L 4096 --reps 6 --libs main,mrows,g8,h16,h64,cg16k
 step label_trace 120 env PERC_TILE_TRACE=1 python -u tools/label_probe.py --L 4096 --reps 4
