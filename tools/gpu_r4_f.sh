@@ -5,6 +5,13 @@ mkdir -p gpurun_out
 export TMPDIR=/tmp
 L=4096 CBX2=1 bash tools/pmc_r2.sh || { tail -20 gpurun_out/pmc_r2.log; exit 1; }
 tail -8 gpurun_out/pmc_r2_reconcile_L4096.csv
+# read-queue levels of the row-major march at L = 8192 (Little's law: requests in flight)
+timeout -s KILL 150 rocprofv3 --pmc TCC_EA0_RDREQ_LEVEL_sum TCC_EA0_WRREQ_LEVEL_sum GRBM_GUI_ACTIVE \
+  --kernel-include-regex "k_cg_march|k_cg_b|k_copy" -f csv -d gpurun_out/pmc_level/L8192 -o run -- \
+  python3 tools/pmc_probe.py --L 8192 --reps 16 --copies 8 >> gpurun_out/pmc_level.log 2>&1 || { tail gpurun_out/pmc_level.log; exit 1; }
+timeout -s KILL 150 rocprofv3 --pmc TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_sum TCC_HIT_sum TCC_MISS_sum \
+  --kernel-include-regex "k_cg_march|k_cg_b|k_copy" -f csv -d gpurun_out/pmc_level/L8192_n -o run -- \
+  python3 tools/pmc_probe.py --L 8192 --reps 16 --copies 8 >> gpurun_out/pmc_level.log 2>&1 || { tail gpurun_out/pmc_level.log; exit 1; }
 bash tools/configs.sh || { tail -5 gpurun_out/configs.log; exit 1; }
 tail -12 gpurun_out/configs.log
 timeout -k 10 480 python -u tools/literal_config.py c2_sq1024_bond_p50 1e-08 > gpurun_out/r4_literal_c2.log 2>&1
