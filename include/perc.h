@@ -403,12 +403,11 @@ int perc_set_march_rows(perc_ctx *h, int rows);
    the column -- 0.5 instead of 2 bytes of code per element in each kernel
    (52N -> 49N bytes per iteration); bitwise the same codes (checked per
    row when packed).
-   PERC_MARCH_BIG_STRIPS: the strip-major march past the Infinity Cache
-   too (L = 8192; not in the default, see DESIGN.md for the A/B).
    Row slabs (perc_set_slabs) and the literal dot order always run the
    row-major q-storing march.  (Round 4 removed the variants that lost their
    A/Bs: workgroup row-march 4, deferred reductions 32, persistent march
-   256; those bits are rejected.) */
+   256, the strip-major march past the Infinity Cache 1024; those bits are
+   rejected.) */
 #define PERC_MARCH_QFREE 1
 #define PERC_MARCH_ALT 2
 #define PERC_SOLVE_RESIDENT 8
@@ -416,7 +415,6 @@ int perc_set_march_rows(perc_ctx *h, int rows);
 #define PERC_MARCH_SLOTS 64
 #define PERC_MARCH_TAG 128
 #define PERC_MARCH_NIBBLE 512
-#define PERC_MARCH_BIG_STRIPS 1024
 #define PERC_MARCH_DEFAULT                                                                      \
   (PERC_MARCH_QFREE | PERC_MARCH_ALT | PERC_SOLVE_RESIDENT | PERC_MARCH_STRIPS | PERC_MARCH_SLOTS | \
    PERC_MARCH_TAG | PERC_MARCH_NIBBLE)

@@ -27,7 +27,6 @@ CUR_FORTRAN, CUR_MATLAB = 0, 1
 FMT_AUTO, FMT_CSR, FMT_STENCIL, FMT_STENCIL_SPLIT, FMT_STENCIL_TILED = 0, 1, 2, 3, 4
 MARCH_QFREE, MARCH_ALT, SOLVE_RESIDENT, MARCH_STRIPS, MARCH_SLOTS, MARCH_TAG = 1, 2, 8, 16, 64, 128
 MARCH_NIBBLE = 512
-MARCH_BIG_STRIPS = 1024
 MARCH_DEFAULT = (MARCH_QFREE | MARCH_ALT | SOLVE_RESIDENT | MARCH_STRIPS | MARCH_SLOTS | MARCH_TAG
                  | MARCH_NIBBLE)
 DOT_FAST, DOT_LITERAL = 0, 1

@@ -870,7 +870,7 @@ int perc_set_march_rows(perc_ctx* h, int rows) {
 
 int perc_set_march_mode(perc_ctx* h, int mode) {
   constexpr int kAll = PERC_MARCH_QFREE | PERC_MARCH_ALT | PERC_SOLVE_RESIDENT | PERC_MARCH_STRIPS |
-                       PERC_MARCH_SLOTS | PERC_MARCH_TAG | PERC_MARCH_NIBBLE | PERC_MARCH_BIG_STRIPS;
+                       PERC_MARCH_SLOTS | PERC_MARCH_TAG | PERC_MARCH_NIBBLE;
   if (!h || (mode & ~kAll) != 0) return PERC_EINVAL;
   h->march_mode = mode;
   march_geometry(h);  // band heights depend on PERC_MARCH_SLOTS

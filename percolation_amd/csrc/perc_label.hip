@@ -256,9 +256,7 @@ __global__ void k_occupy_sites(const int* order, int count, int t, uint8_t* socc
 #endif
 constexpr int kCcW = 128, kCcH = PERC_CC_H, kCcSites = kCcW * kCcH, kCcThreads = 256;
 constexpr int kReduceGrid = 1024;  // fixed grid of the counting passes
-#ifndef PERC_CC_COMPRESS_GRID
-#define PERC_CC_COMPRESS_GRID 1024  // k_cc_compress's grid cap (probe builds: 16384)
-#endif
+
 
 __device__ __forceinline__ int find_root(int* parent, int x) {
   int p = parent[x];
@@ -318,10 +316,7 @@ __global__ __launch_bounds__(kCcThreads) void k_cc_tile(Geom g, int kind, const 
   // forward links are (s, s+1), (s, s+m), bond ids fb, fb+1 (nearestn_square
   // lists +1 before +m in every such case).  All bond_first loads first,
   // then all link loads: two memory latencies per thread, not 2 per site.
-#ifndef PERC_CC_G
-#define PERC_CC_G 4  // (probe builds: -DPERC_CC_G=8)
-#endif
-  constexpr int kG = PERC_CC_G;  // sites per batch: loads of a batch in flight together
+  constexpr int kG = 4;  // sites per batch: loads of a batch in flight together (8: no faster)
   static_assert(kPer % kG == 0, "batches");
   for (int k0 = 0; k0 < kPer; k0 += kG) {
     int fbv[kG];
@@ -463,7 +458,6 @@ __global__ __launch_bounds__(kCcThreads) void k_cc_tile(Geom g, int kind, const 
   }
 }
 
-#ifndef PERC_CC_MERGE_ROWS
 // The links that cross a block edge, with neighbouring lanes on neighbouring
 // sites of the same edge: part A, the blocks' top rows (every column: the
 // links up into the next block row), one workgroup per kCcThreads columns;
@@ -474,7 +468,9 @@ __global__ __launch_bounds__(kCcThreads) void k_cc_tile(Geom g, int kind, const 
 // equals the previous lane's skips its union -- that lane's union joins the
 // same two sets (by induction down to the first lane of the run).  Along an
 // edge most crossing links join the same two block components, so most
-// unions drop out; the rest start one hop closer to the roots.
+// unions drop out; the rest start one hop closer to the roots.  (Against
+// the round-3 mapping, one workgroup per lattice row: labels 0.435 vs
+// 0.512 ms per realisation at L = 4096, profiles/r4_4_label_ab_L4096.json.)
 __global__ __launch_bounds__(kCcThreads) void k_cc_merge(Geom g, int kind, const int* bond_first,
                                                          const uint8_t* bocc,
                                                          const uint8_t* socc, int* parent,
@@ -514,58 +510,6 @@ __global__ __launch_bounds__(kCcThreads) void k_cc_merge(Geom g, int kind, const
     if (want && !(lane > 0 && pa == a && pb == b)) unite(parent, a, b);
   }
 }
-#else
-// (probe build: the round-3 mapping, one workgroup per lattice row)
-// one workgroup per lattice row: the sites whose forward links may leave
-// their block (block top row: every column; other rows: the block edge
-// columns and the last column), then only the links that do
-__global__ __launch_bounds__(kCcThreads) void k_cc_merge(Geom g, int kind, const int* bond_first,
-                                                         const uint8_t* bocc,
-                                                         const uint8_t* socc, int* parent,
-                                                         uint8_t* member, int, int) {
-  // workgroups 0..n-1: one lattice row each (its first kCcThreads
-  // candidates); then the block-top rows' further candidates, nseg - 1
-  // workgroups of kCcThreads per such row (the unions are spread over the
-  // chip instead of queueing behind one workgroup per block-top row)
-  const int nseg = cdiv(g.m, kCcThreads);
-  // (an XCD-contiguous row order measured slower here: 226 vs 151 us)
-  int row = blockIdx.x, seg = 0, step = kCcThreads;
-  if (row >= g.n) {
-    const int e = row - g.n;
-    row = (e / (nseg - 1)) * kCcH + kCcH - 1;
-    seg = 1 + e % (nseg - 1);
-  }
-  const bool full = row % kCcH == kCcH - 1;
-  const int ntx = cdiv(g.m, kCcW);
-  const int cnt = full ? g.m : 2 * ntx + 1;
-  if (full) step = kCcThreads * nseg;  // segment seg: j = seg*kCcThreads + tid (+ k*step)
-  for (int j = seg * kCcThreads + threadIdx.x; j < cnt; j += step) {
-    int c;
-    if (full) c = j;
-    else if (j == 2 * ntx) c = g.m - 1;
-    else c = min((j >> 1) * kCcW + (j & 1) * (kCcW - 1), g.m - 1);
-    const int s = row * g.m + c + 1;
-    if (s > g.t - 1) continue;
-    if (kind != PERC_BOND && !socc[s]) continue;
-    int nn[6];
-    nearestn_rc(g, s, row, c, nn);
-    const int fb = bond_first[s];
-    int r = 0;
-    for (int k = 0; k < g.scn; ++k) {
-      const int q = nn[k];
-      if (q <= s) continue;
-      const bool link = cc_link(kind, bocc, socc, fb + r, s, q);
-      ++r;
-      if (!link) continue;
-      const int qrow = div_m(g, q - 1), qcol = q - 1 - qrow * g.m;
-      if (qrow / kCcH == row / kCcH && qcol / kCcW == c / kCcW) continue;  // inside: k_cc_tile
-      if (kind == PERC_BOND) member[q] = 1;
-      unite(parent, s, q);
-    }
-  }
-}
-
-#endif
 
 // sum of v over the workgroup of kCcThreads, then one atomic add
 __device__ __forceinline__ void block_count_add(int v, int* counter) {
@@ -839,16 +783,11 @@ hipError_t dev_label(perc_ctx* h, int* nspan, int* span_list, int* nclusters) {
   HIP_TRY(dbg_sync(st, "k_cc_tile"));
   const int nseg = cdiv(g.m, kCcThreads);
   const int nfull = g.n / kCcH;  // rows kCcH-1, 2kCcH-1, ... (< n)
-#ifndef PERC_CC_MERGE_ROWS
   const int ncand = 2 * cdiv(g.m, kCcW) + 1;
   k_cc_merge<<<nfull * nseg + ncand * cdiv(g.n, kCcThreads), kCcThreads, 0, st>>>(
       g, kind, d.bond_first, d.bocc, d.socc, d.parent, d.member, nseg, nfull);
-#else
-  k_cc_merge<<<g.n + (nseg > 1 ? nfull * (nseg - 1) : 0), kCcThreads, 0, st>>>(
-      g, kind, d.bond_first, d.bocc, d.socc, d.parent, d.member, nseg, nfull);
-#endif
   HIP_TRY(dbg_sync(st, "k_cc_merge"));
-  k_cc_compress<<<std::min(cdiv(g.t, kCcThreads), PERC_CC_COMPRESS_GRID), kCcThreads, 0, st>>>(
+  k_cc_compress<<<std::min(cdiv(g.t, kCcThreads), kReduceGrid), kCcThreads, 0, st>>>(
       g.t, d.parent, d.member, d.counters + 1);
   HIP_TRY(dbg_sync(st, "k_cc_compress"));
   k_span_top<<<1, 1024, 0, st>>>(g, d.parent, d.member, d.top, d.counters);

@@ -42,13 +42,11 @@ __device__ __forceinline__ double bld1(__amdgpu_buffer_rsrc_t r, unsigned off) {
 __device__ __forceinline__ double bld1s(__amdgpu_buffer_rsrc_t r, unsigned off) {
   return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, (int)off, 0, 16));
 }
-// cache policy of the march's p / q / r stores: nontemporal (probe builds:
-// -DPERC_MARCH_SAUX=<aux>, e.g. 16 = sc1 write-through, which leaves no
-// dirty line in the XCD's L2 for the end-of-kernel write-back)
-#ifndef PERC_MARCH_SAUX
-#define PERC_MARCH_SAUX 2
-#endif
-constexpr int kStAux = PERC_MARCH_SAUX;
+// the march's p / q / r stores are nontemporal (write-through sc1 stores,
+// which leave no dirty L2 line for the end-of-kernel write-back, measured
+// no faster: solve 0.1441 / 0.1427 (sc0 sc1) vs 0.1422 ms per iteration,
+// profiles/r4_4_store_policy_ab_L4096.json)
+constexpr int kStAux = kNT;
 
 template <int AUX>
 __device__ __forceinline__ void bst2(__amdgpu_buffer_rsrc_t r, unsigned off, double2 v) {

@@ -428,12 +428,11 @@ void select_format(perc_ctx* h) {
   h->small = h->fmt_req == PERC_FMT_AUTO && h->N > 0 && h->N <= kSmallRows &&
              (h->march_mode & PERC_SOLVE_RESIDENT) && h->d.rowptr != nullptr;
   // strip-major q-free march only while a vector fits the Infinity Cache
-  // (L <= 4096): past it (16-row bands, several rounds of waves) the
-  // row-major march is faster (L = 8192: 0.439 vs 0.480 ms,
-  // profiles/r2_11_ab_strips.log); its whole-array buffer views also need
-  // < 2 GB
-  h->strips = h->qfree && (h->march_mode & PERC_MARCH_STRIPS) &&
-              ((size_t)h->N * sizeof(double) <= kLargeVector || (h->march_mode & PERC_MARCH_BIG_STRIPS));
+  // (L <= 4096): past it the row-major march is faster (L = 8192, round 4
+  // with nibble codes and slot bands: 0.652 vs 0.734 ms per iteration,
+  // profiles/r4_4_l8192_strips_ab.json; round 2: 0.439 vs 0.480 ms); its
+  // whole-array buffer views also need < 2 GB
+  h->strips = h->qfree && (h->march_mode & PERC_MARCH_STRIPS) && (size_t)h->N * sizeof(double) <= kLargeVector;
   // slot-weighted bands of the strip-major march (to_strips applies them)
   const bool slots = (h->march_mode & PERC_MARCH_SLOTS) != 0;
   h->march_slots = slots && h->strips && h->wm_slots > 0;

@@ -1,12 +1,11 @@
 #!/usr/bin/env python3
-"""The march past the Infinity Cache (L = 8192): the default row-major q-free
-march (P on one round of slot-mapped bands, B on 8-row bands with
-nontemporal r(k) loads) against the strip-major march with nibble codes and
-slot-weighted bands (PERC_MARCH_BIG_STRIPS), alternating, best of 3 x `reps`
-launches of perc_bench_kernel 1 (P), 2 (B) and 5 (a whole iteration), plus
-ms per iteration of fixed-iteration solves (the slope between itmax/2 and
-itmax, tol 0).  GB/s on each layout's byte model (row-major: 26 B/row for P
-and B; strip-major nibble: 24.5 B/row).
+"""The march past the Infinity Cache (L = 8192): the row-major q-free march
+(P on one round of slot-mapped bands, B on 8-row bands with nontemporal r(k)
+loads), best of 3 x `reps` launches of perc_bench_kernel 1 (P), 2 (B) and 5
+(a whole iteration), plus ms per iteration of fixed-iteration solves (the
+slope between itmax/2 and itmax, tol 0); GB/s on 26 B/row for P and B.
+(Round 4 also ran the strip-major march with nibble codes here: 0.734 vs
+0.652 ms per iteration, profiles/r4_4_l8192_strips_ab.json; removed.)
 
   python tools/l8192_probe.py --L 8192 --reps 10
 """
@@ -31,7 +30,7 @@ def main():
     from percolation_amd import api
     L_ = args.L
     nb = api.nbonds(0, L_, L_, 0)
-    modes = {"rowmajor": PL.MARCH_DEFAULT, "strips": PL.MARCH_DEFAULT | PL.MARCH_BIG_STRIPS}
+    modes = {"rowmajor": PL.MARCH_DEFAULT}
     out = dict(L=L_)
     with api.Context(0, L_, L_, 0) as ctx:
         ctx.occupy_random(PL.BOND, 0, int(args.p * nb), 777)
