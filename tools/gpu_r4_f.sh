@@ -3,8 +3,6 @@
 # configs (config 5 as stated), the literal dot order at config 2 (tol 1e-8)
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -k 10 400 python -u tools/rccl_exit_probe.py > gpurun_out/r4f_rccl_exit.log 2>&1
-rc=$?; tail -2 gpurun_out/r4f_rccl_exit.log; [ $rc -ne 0 ] && exit $rc
 timeout -k 10 300 python -u tools/dslab_bench.py --L 4096 --iters 4000 --reps 3 > gpurun_out/r4f_dslab_bench.json 2> gpurun_out/r4f_dslab_bench.err
 rc=$?; cat gpurun_out/r4f_dslab_bench.json; [ $rc -ne 0 ] && exit $rc
 L=4096 CBX2=1 bash tools/pmc_r2.sh || { tail -20 gpurun_out/pmc_r2.log; exit 1; }
@@ -19,4 +17,7 @@ timeout -s KILL 150 rocprofv3 --pmc TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_sum TCC_HIT_
 bash tools/configs.sh || { tail -5 gpurun_out/configs.log; exit 1; }
 tail -12 gpurun_out/configs.log
 timeout -k 10 480 python -u tools/literal_config.py c2_sq1024_bond_p50 1e-08 > gpurun_out/r4_literal_c2.log 2>&1
-rc=$?; tail -3 gpurun_out/r4_literal_c2.log; exit $rc
+rc=$?; tail -3 gpurun_out/r4_literal_c2.log; [ $rc -ne 0 ] && exit $rc
+# last: which torch "nccl" / libperc combination ends a process abnormally (stops at the first)
+timeout -k 10 400 python -u tools/rccl_exit_probe.py > gpurun_out/r4f_rccl_exit.log 2>&1
+rc=$?; tail -3 gpurun_out/r4f_rccl_exit.log; exit $rc

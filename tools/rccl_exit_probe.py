@@ -2,7 +2,10 @@
 """Which combination of torch.distributed "nccl" (torch's bundled RCCL) and
 libperc (linked against /opt/rocm's RCCL) ends a process abnormally?  Each
 case runs in a child process of its own (world size 1) and reports its exit
-status; a case prints "done" before returning from main.
+status; a case prints "done" before returning from main.  The probe stops
+at the first case that does not exit cleanly and exits 3 (nothing more is
+started on the GPU after an abnormal exit); the cases run from the plainest
+(torch alone) to the most combined.
 
   python tools/rccl_exit_probe.py
 """
@@ -59,8 +62,11 @@ def main():
         out[name] = dict(rc=r.returncode, done="done" in r.stdout,
                          tail=(r.stderr.strip().splitlines() or [""])[-1][-160:])
         print(name, json.dumps(out[name]), flush=True)
+        if r.returncode != 0:
+            break
     print(json.dumps(out), flush=True)
+    return 3 if any(v["rc"] != 0 for v in out.values()) else 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())
