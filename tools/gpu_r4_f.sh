@@ -18,6 +18,11 @@ bash tools/configs.sh || { tail -5 gpurun_out/configs.log; exit 1; }
 tail -12 gpurun_out/configs.log
 timeout -k 10 480 python -u tools/literal_config.py c2_sq1024_bond_p50 1e-08 > gpurun_out/r4_literal_c2.log 2>&1
 rc=$?; tail -3 gpurun_out/r4_literal_c2.log; [ $rc -ne 0 ] && exit $rc
+# the driver's multi-GPU launch shape at one rank (torchrun, "nccl" group, libperc in the process)
+timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 \
+  --master-port 29531 bench.py --gpus 1 --steps 1 --warmup 0 --force-dist --no-cpu-baseline \
+  > gpurun_out/r4f_bench_torchrun1.log 2>&1
+rc=$?; tail -3 gpurun_out/r4f_bench_torchrun1.log; [ $rc -ne 0 ] && exit $rc
 # last: which torch "nccl" / libperc combination ends a process abnormally (stops at the first)
 timeout -k 10 400 python -u tools/rccl_exit_probe.py > gpurun_out/r4f_rccl_exit.log 2>&1
 rc=$?; tail -3 gpurun_out/r4f_rccl_exit.log; exit $rc
