@@ -1,0 +1,350 @@
+// perc_cc.h -- the connected-component labeling kernels of libperc
+// (k_cc_tile, k_cc_merge, k_cc_compress), included by perc_label.hip and by
+// tools/cc_bench.hip (the kernels' stand-alone A/B harness).  Definitions in
+// an anonymous namespace, like the other device headers.
+#pragma once
+#include "perc_common.h"
+
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Wunused-function"
+namespace perc {
+namespace {
+
+__device__ __forceinline__ int wave_sum_int(int v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+
+// ---------------------------------------------------------------------------
+// Connected components (the partition of bondc.f:194-393, site.f:167-289,
+// sitebond.f:190-400).  Roots are always linked larger -> smaller, so the
+// final root of a component is its minimum site id: a canonical,
+// schedule-independent partition.  Three passes:
+//
+//  k_cc_tile      one workgroup per kCcW x kCcH block of sites.  The links
+//                 inside the block are united in an LDS union-find (local
+//                 index order = site order inside a block, so the local root
+//                 is the block-local minimum site); then every site's parent
+//                 (that root's global id) and member flag are written once,
+//                 coalesced.  No global atomics.
+//  k_cc_merge     only the links that cross a block edge (sites on the top
+//                 row or the edge columns of a block: ~1/32 + 2/128 of them)
+//                 are united in the global array (lock-free CAS, same rule;
+//                 neighbouring lanes with the same pair of parents unite once).
+//  k_cc_compress  parent[s] = final root; cluster count reduced per
+//                 workgroup (one atomic per workgroup of a fixed grid).
+//
+// Path halving (LDS and global): stale reads only cost retries, parents only
+// ever move to smaller ancestors, and only roots are CASed.
+#ifndef PERC_CC_H
+#define PERC_CC_H 32  // tile height (probe builds: -DPERC_CC_H=64)
+#endif
+constexpr int kCcW = 128, kCcH = PERC_CC_H, kCcSites = kCcW * kCcH, kCcThreads = 256;
+constexpr int kReduceGrid = 1024;  // fixed grid of the counting passes
+
+
+__device__ __forceinline__ int find_root(int* parent, int x) {
+  int p = parent[x];
+  while (p != x) {
+    const int gp = parent[p];
+    if (gp != p) parent[x] = gp;
+    x = gp;
+    p = parent[x];
+  }
+  return x;
+}
+
+__device__ __forceinline__ void unite(int* parent, int a, int b) {
+  while (true) {
+    a = find_root(parent, a);
+    b = find_root(parent, b);
+    if (a == b) return;
+    if (a < b) { const int tmp = a; a = b; b = tmp; }
+    const int old = atomicCAS(&parent[a], a, b);
+    if (old == a) return;
+    a = old;
+  }
+}
+
+// link predicate of the forward bond id = (s, q), s < q (bondc.f:194-393:
+// occupied bond; site.f: both sites occupied; sitebond.f / the mixed
+// conductance rule: bond and both sites)
+__device__ __forceinline__ bool cc_link(int kind, const uint8_t* bocc, const uint8_t* socc,
+                                        long long id, int s, int q) {
+  if (kind == PERC_BOND) return bocc[id];
+  if (kind == PERC_SITE) return socc[s] && socc[q];
+  return bocc[id] && socc[s] && socc[q];
+}
+
+__global__ __launch_bounds__(kCcThreads) void k_cc_tile(Geom g, int kind, const int* bond_first,
+                                                        const uint8_t* bocc,
+                                                        const uint8_t* socc, int* parent,
+                                                        uint8_t* member, int bf_closed,
+                                                        unsigned long long* trace) {
+  unsigned long long tr0 = trace ? wall_clock64() : 0ull;
+  static_assert(kCcW % 64 == 0 && kCcThreads % kCcW == 0, "a wave covers 64 columns of a tile row");
+  constexpr int kPer = kCcSites / kCcThreads;
+  __shared__ int lp[kCcSites];
+  // lk: bits 0-5 the forward links, bit 7 membership (one byte per site:
+  // 20 KB of LDS, 8 workgroups per CU).  During phase 2 the link bits are
+  // fixed and bit 7 only ever set, so a plain byte read-or-write is exact.
+  __shared__ uint8_t lk[kCcSites];
+  const int ntx = cdiv(g.m, kCcW);
+  // XCD-contiguous tiles (the edge-column tiles, every ntx-th, would share an XCD)
+  const int tb = xcd_logical_block(blockIdx.x, gridDim.x);
+  const int tx = tb % ntx, ty = tb / ntx;
+  const int c0 = tx * kCcW, r0 = ty * kCcH;
+  const int tw = min(kCcW, g.m - c0), th = min(kCcH, g.n - r0);
+  const bool sq = g.lattice == kSquare;
+  // phase 1: each site's forward links (bit r: the r-th forward bond in
+  // nearestn order).  Square lattice, interior column, not the top row: the
+  // forward links are (s, s+1), (s, s+m), bond ids fb, fb+1 (nearestn_square
+  // lists +1 before +m in every such case).  All bond_first loads first,
+  // then all link loads: two memory latencies per thread, not 2 per site.
+  constexpr int kG = 4;  // sites per batch: loads of a batch in flight together (8: no faster)
+  static_assert(kPer % kG == 0, "batches");
+  for (int k0 = 0; k0 < kPer; k0 += kG) {
+    int fbv[kG];
+    bool occv[kG];
+#pragma unroll
+    for (int u = 0; u < kG; ++u) {
+      const int li = threadIdx.x + (k0 + u) * kCcThreads, lr = li / kCcW, lc = li % kCcW;
+      const int s = (r0 + lr) * g.m + c0 + lc + 1;
+      const bool in = lr < th && lc < tw;
+      occv[u] = in && (kind == PERC_BOND || socc[s]);
+      const int row = r0 + lr;
+      fbv[u] = !in || s > g.t - 1 ? 0
+               : bf_closed && row <= g.n - 2 ? bf_square(g, row, c0 + lc)
+                                             : bond_first[s];
+    }
+#pragma unroll
+    for (int u = 0; u < kG; ++u) {
+      const int li = threadIdx.x + (k0 + u) * kCcThreads, lr = li / kCcW, lc = li % kCcW;
+      const int row = r0 + lr, col = c0 + lc;
+      const int s = row * g.m + col + 1;
+      unsigned mask = 0;
+      if (occv[u] && s <= g.t - 1) {
+        const int fb = fbv[u];
+        if (sq && col >= 1 && col <= g.m - 2 && row <= g.n - 2) {
+          mask = (unsigned)cc_link(kind, bocc, socc, fb, s, s + 1) |
+                 (unsigned)cc_link(kind, bocc, socc, fb + 1, s, s + g.m) << 1;
+        } else {
+          int nn[6];
+          nearestn_rc(g, s, row, col, nn);
+          int r = 0;
+          for (int kk = 0; kk < g.scn; ++kk) {
+            const int q = nn[kk];
+            if (q <= s) continue;
+            if (cc_link(kind, bocc, socc, fb + r, s, q)) mask |= 1u << r;
+            ++r;
+          }
+        }
+      }
+      const bool mem = (kind != PERC_BOND && occv[u]) || (kind == PERC_BOND && mask);
+      lk[li] = (uint8_t)(mask | (mem ? 0x80u : 0u));
+    }
+  }
+  __syncthreads();
+  unsigned long long tr1 = trace ? wall_clock64() : 0ull;
+  // phase 1b: the square lattice's horizontal runs.  Its first forward
+  // neighbour is s+1 whenever col < m-1 (every nearestn_square case), so bit
+  // 0 is the link to the right; a run's sites point at its first site (the
+  // run's minimum: larger -> smaller as every union), the second 64-column
+  // half of a row at the first half's last site when the run crosses.
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int k = 0; k < kPer; ++k) {
+    const int li = threadIdx.x + k * kCcThreads, lc = li % kCcW;
+    int par = li;
+    if (sq) {
+      const bool right = lc + 1 < tw && (lk[li] & 1u);
+      const unsigned long long rb = __ballot(right);
+      const bool left =
+          lc > 0 && lc < tw && (lane > 0 ? (rb >> (lane - 1) & 1ull) : (lk[li - 1] & 1u));
+      const unsigned long long starts = __ballot(!left);
+      const unsigned long long upto = starts & (lane == 63 ? ~0ull : ((2ull << lane) - 1ull));
+      par = upto ? li - lane + (63 - __clzll((long long)upto)) : li - lane - 1;
+      if (left && kind == PERC_BOND) lk[li] |= 0x80u;
+    }
+    lp[li] = par;
+  }
+  __syncthreads();
+  unsigned long long tr2 = trace ? wall_clock64() : 0ull;
+  // phase 2: the other links inside the tile, LDS union-find (crossing
+  // links: k_cc_merge).  (Measured: bottom-up order beats top-down -- finds
+  // 23 vs 28 us per tile, flatten 5 vs 12 us.)
+  for (int li = threadIdx.x; li < kCcSites; li += kCcThreads) {
+    unsigned mask = lk[li] & 0x3Fu;
+    const int lr = li / kCcW, lc = li % kCcW;
+    if (sq && lc + 1 < tw) mask &= ~1u;  // in the run
+    // square interior: the link up from s is redundant when s-1 links up
+    // too and both s-1 -> s and s-1+m -> s+m are run links (a closed
+    // plaquette: the union of s-1 already joined the two runs)
+    if (sq && (mask & 2u) && lc >= 1 && lr + 1 < th && c0 + lc <= g.m - 2 && c0 + lc >= 1) {
+      const unsigned lft = lk[li - 1], lup = lk[li - 1 + kCcW];
+      if ((lft & 3u) == 3u && (lup & 1u) && c0 + lc - 1 >= 1) mask &= ~2u;
+    }
+    if (!mask) continue;
+    const int row = r0 + lr, col = c0 + lc;
+    const int s = row * g.m + col + 1;
+    int qs[6], nq = 0;
+    if (sq && col >= 1 && col <= g.m - 2 && row <= g.n - 2) {
+      qs[0] = s + 1;
+      qs[1] = s + g.m;
+      nq = 2;
+    } else {
+      int nn[6];
+      nearestn_rc(g, s, row, col, nn);
+      for (int kk = 0; kk < g.scn; ++kk)
+        if (nn[kk] > s) qs[nq++] = nn[kk];
+    }
+    for (int r = 0; r < nq; ++r) {
+      if (!(mask >> r & 1u)) continue;
+      const int q = qs[r];
+      const int qrow = div_m(g, q - 1);
+      const int qr = qrow - r0, qc = q - 1 - qrow * g.m - c0;
+      if (qr < 0 || qr >= th || qc < 0 || qc >= tw) continue;  // crossing: k_cc_merge
+      const int lq = qr * kCcW + qc;
+      if (kind == PERC_BOND) lk[lq] |= 0x80u;
+      // LDS union (larger local root -> smaller)
+      int a = li, b = lq;
+      while (true) {
+        a = find_root(lp, a);
+        b = find_root(lp, b);
+        if (a == b) break;
+        if (a < b) { const int tmp = a; a = b; b = tmp; }
+        const int old = atomicCAS(&lp[a], a, b);
+        if (old == a) break;
+        a = old;
+      }
+    }
+  }
+  __syncthreads();
+  unsigned long long tr3 = trace ? wall_clock64() : 0ull;
+  for (int li = threadIdx.x; li < kCcSites; li += kCcThreads) {
+    const int lr = li / kCcW, lc = li % kCcW;
+    if (lr >= th || lc >= tw) continue;
+    int x = li, p = lp[x];
+    while (p != x) {
+      x = p;
+      p = lp[x];
+    }
+    const int s = (r0 + lr) * g.m + c0 + lc + 1;
+    parent[s] = (r0 + x / kCcW) * g.m + c0 + x % kCcW + 1;
+    member[s] = lk[li] >> 7;
+  }
+  if (trace && threadIdx.x == 0) {
+    unsigned long long* o = trace + 5 * (size_t)blockIdx.x;
+    o[0] = tr0;
+    o[1] = tr1;
+    o[2] = tr2;
+    o[3] = tr3;
+    o[4] = wall_clock64();
+  }
+}
+
+// The links that cross a block edge, with neighbouring lanes on neighbouring
+// sites of the same edge: part A, the blocks' top rows (every column: the
+// links up into the next block row), one workgroup per kCcThreads columns;
+// part B, the other rows' candidate columns (the block edge columns and the
+// last column), one workgroup per candidate column and kCcThreads rows.
+// Before any union a lane reads the parents of its link's two sites (after
+// k_cc_tile: the block-local roots, or ancestors of them); a lane whose pair
+// equals the previous lane's skips its union -- that lane's union joins the
+// same two sets (by induction down to the first lane of the run).  Along an
+// edge most crossing links join the same two block components, so most
+// unions drop out; the rest start one hop closer to the roots.  (Against
+// the round-3 mapping, one workgroup per lattice row: labels 0.435 vs
+// 0.512 ms per realisation at L = 4096, profiles/r4_4_label_ab_L4096.json.)
+__global__ __launch_bounds__(kCcThreads) void k_cc_merge(Geom g, int kind, const int* bond_first,
+                                                         const uint8_t* bocc,
+                                                         const uint8_t* socc, int* parent,
+                                                         uint8_t* member, int nseg, int nfull) {
+  const int ntx = cdiv(g.m, kCcW), lane = threadIdx.x & 63;
+  int row, c;
+  if ((int)blockIdx.x < nfull * nseg) {  // A: block-top row, columns of segment
+    row = (blockIdx.x / nseg) * kCcH + kCcH - 1;
+    c = (blockIdx.x % nseg) * kCcThreads + threadIdx.x;
+  } else {  // B: candidate column j, rows of block rb (block-top rows are A's)
+    const int e = blockIdx.x - nfull * nseg, nrb = cdiv(g.n, kCcThreads);
+    const int j = e / nrb;
+    row = (e % nrb) * kCcThreads + threadIdx.x;
+    c = j == 2 * ntx ? g.m - 1 : min((j >> 1) * kCcW + (j & 1) * (kCcW - 1), g.m - 1);
+    if (row % kCcH == kCcH - 1) row = g.n;  // (part A's)
+  }
+  const int s = row * g.m + c + 1;
+  bool site = row < g.n && c < g.m && s <= g.t - 1 && (kind == PERC_BOND || socc[s]);
+  int nn[6] = {0, 0, 0, 0, 0, 0}, fb = 0;
+  if (site) {
+    nearestn_rc(g, s, row, c, nn);
+    fb = bond_first[s];
+  }
+  int r = 0;
+  for (int k = 0; k < g.scn; ++k) {  // (uniform trip count: the shuffles below)
+    const int q = nn[k];
+    const bool fwd = site && q > s;
+    bool want = fwd && cc_link(kind, bocc, socc, fb + r, s, q);
+    r += fwd ? 1 : 0;
+    if (want) {
+      const int qrow = div_m(g, q - 1), qcol = q - 1 - qrow * g.m;
+      want = !(qrow / kCcH == row / kCcH && qcol / kCcW == c / kCcW);  // inside: k_cc_tile's
+    }
+    if (want && kind == PERC_BOND) member[q] = 1;
+    const int a = want ? parent[s] : -1, b = want ? parent[q] : -1;
+    const int pa = __shfl_up(a, 1, 64), pb = __shfl_up(b, 1, 64);
+    if (want && !(lane > 0 && pa == a && pb == b)) unite(parent, a, b);
+  }
+}
+
+// sum of v over the workgroup of kCcThreads, then one atomic add
+__device__ __forceinline__ void block_count_add(int v, int* counter) {
+  __shared__ int s_cnt[kCcThreads / 64];
+  v = wave_sum_int(v);
+  if ((threadIdx.x & 63) == 0) s_cnt[threadIdx.x >> 6] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int tot = 0;
+#pragma unroll
+    for (int w = 0; w < kCcThreads / 64; ++w) tot += s_cnt[w];
+    if (tot) atomicAdd(counter, tot);
+  }
+}
+
+// final flattening: a read-only walk, then each thread writes only its own
+// entry (path halving here would let one thread overwrite another's freshly
+// written root with an intermediate ancestor); counts the clusters (member
+// roots)
+__global__ __launch_bounds__(kCcThreads) void k_cc_compress(int t, int* parent,
+                                                            const uint8_t* member,
+                                                            int* nclusters) {
+  // four sites per thread and step, their first parent loads issued together
+  constexpr int kU = 4;
+  int cnt = 0;
+  for (long long b = (long long)blockIdx.x * kCcThreads * kU + threadIdx.x + 1; b <= t;
+       b += (long long)gridDim.x * kCcThreads * kU) {
+    int p0[kU];
+#pragma unroll
+    for (int k = 0; k < kU; ++k) {
+      const long long s = b + k * kCcThreads;
+      p0[k] = s <= t ? parent[s] : 0;
+    }
+#pragma unroll
+    for (int k = 0; k < kU; ++k) {
+      const long long s = b + k * kCcThreads;
+      if (s > t) continue;
+      int x = (int)s, p = p0[k];
+      while (p != x) {
+        x = p;
+        p = parent[x];
+      }
+      parent[s] = x;
+      cnt += x == s && member[s];
+    }
+  }
+  block_count_add(cnt, nclusters);
+}
+
+}  // namespace
+}  // namespace perc
+#pragma clang diagnostic pop
