@@ -7,6 +7,8 @@ timeout -k 10 300 python -u tools/dslab_bench.py --L 4096 --iters 4000 --reps 3 
 rc=$?; cat gpurun_out/r4f_dslab_bench.json; [ $rc -ne 0 ] && exit $rc
 timeout -k 10 120 ./tools/cc_bench 4096 0.6 20 > gpurun_out/r4f_cc_bench.log 2>&1
 rc=$?; cat gpurun_out/r4f_cc_bench.log; [ $rc -ne 0 ] && exit $rc
+timeout -k 10 120 ./tools/spmv_bench 4096 20 > gpurun_out/r4f_spmv_bench.log 2>&1
+rc=$?; cat gpurun_out/r4f_spmv_bench.log; [ $rc -ne 0 ] && exit $rc
 L=4096 CBX2=1 bash tools/pmc_r2.sh || { tail -20 gpurun_out/pmc_r2.log; exit 1; }
 tail -8 gpurun_out/pmc_r2_reconcile_L4096.csv
 # read-queue levels of the row-major march at L = 8192 (Little's law: requests in flight)
