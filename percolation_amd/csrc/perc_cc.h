@@ -257,6 +257,7 @@ __global__ __launch_bounds__(kCcThreads) void k_cc_tile(Geom g, int kind, const 
 // unions drop out; the rest start one hop closer to the roots.  (Against
 // the round-3 mapping, one workgroup per lattice row: labels 0.435 vs
 // 0.512 ms per realisation at L = 4096, profiles/r4_4_label_ab_L4096.json.)
+template <int TH = kCcH>  // block height of the tile kernel that ran before
 __global__ __launch_bounds__(kCcThreads) void k_cc_merge(Geom g, int kind, const int* bond_first,
                                                          const uint8_t* bocc,
                                                          const uint8_t* socc, int* parent,
@@ -264,14 +265,14 @@ __global__ __launch_bounds__(kCcThreads) void k_cc_merge(Geom g, int kind, const
   const int ntx = cdiv(g.m, kCcW), lane = threadIdx.x & 63;
   int row, c;
   if ((int)blockIdx.x < nfull * nseg) {  // A: block-top row, columns of segment
-    row = (blockIdx.x / nseg) * kCcH + kCcH - 1;
+    row = (blockIdx.x / nseg) * TH + TH - 1;
     c = (blockIdx.x % nseg) * kCcThreads + threadIdx.x;
   } else {  // B: candidate column j, rows of block rb (block-top rows are A's)
     const int e = blockIdx.x - nfull * nseg, nrb = cdiv(g.n, kCcThreads);
     const int j = e / nrb;
     row = (e % nrb) * kCcThreads + threadIdx.x;
     c = j == 2 * ntx ? g.m - 1 : min((j >> 1) * kCcW + (j & 1) * (kCcW - 1), g.m - 1);
-    if (row % kCcH == kCcH - 1) row = g.n;  // (part A's)
+    if (row % TH == TH - 1) row = g.n;  // (part A's)
   }
   const int s = row * g.m + c + 1;
   bool site = row < g.n && c < g.m && s <= g.t - 1 && (kind == PERC_BOND || socc[s]);
@@ -288,7 +289,7 @@ __global__ __launch_bounds__(kCcThreads) void k_cc_merge(Geom g, int kind, const
     r += fwd ? 1 : 0;
     if (want) {
       const int qrow = div_m(g, q - 1), qcol = q - 1 - qrow * g.m;
-      want = !(qrow / kCcH == row / kCcH && qcol / kCcW == c / kCcW);  // inside: k_cc_tile's
+      want = !(qrow / TH == row / TH && qcol / kCcW == c / kCcW);  // inside: k_cc_tile's
     }
     if (want && kind == PERC_BOND) member[q] = 1;
     const int a = want ? parent[s] : -1, b = want ? parent[q] : -1;

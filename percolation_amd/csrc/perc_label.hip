@@ -450,7 +450,7 @@ hipError_t dev_label(perc_ctx* h, int* nspan, int* span_list, int* nclusters) {
   const int nseg = cdiv(g.m, kCcThreads);
   const int nfull = g.n / kCcH;  // rows kCcH-1, 2kCcH-1, ... (< n)
   const int ncand = 2 * cdiv(g.m, kCcW) + 1;
-  k_cc_merge<<<nfull * nseg + ncand * cdiv(g.n, kCcThreads), kCcThreads, 0, st>>>(
+  k_cc_merge<kCcH><<<nfull * nseg + ncand * cdiv(g.n, kCcThreads), kCcThreads, 0, st>>>(
       g, kind, d.bond_first, d.bocc, d.socc, d.parent, d.member, nseg, nfull);
   HIP_TRY(dbg_sync(st, "k_cc_merge"));
   k_cc_compress<<<std::min(cdiv(g.t, kCcThreads), kReduceGrid), kCcThreads, 0, st>>>(

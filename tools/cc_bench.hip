@@ -10,6 +10,7 @@
 
 #include <cstdio>
 #include <cstdlib>
+#include <type_traits>
 #include <vector>
 
 using namespace perc;
@@ -231,47 +232,65 @@ int main(int argc, char** argv) {
   auto tile = [&](int* par, uint8_t* mem) {
     k_cc_tile<<<R.tiles, kCcThreads>>>(g, PERC_BOND, R.bf, R.bocc, R.socc, par, mem, 1, nullptr);
   };
-  const int nseg = cdiv(g.m, kCcThreads), nfull = g.n / kCcH, ncand = 2 * cdiv(g.m, kCcW) + 1;
-  auto merge = [&]() {
-    k_cc_merge<<<nfull * nseg + ncand * cdiv(g.n, kCcThreads), kCcThreads>>>(g, PERC_BOND, R.bf, R.bocc, R.socc,
-                                                                             R.parent, R.member, nseg, nfull);
-  };
-  auto compress = [&]() {
-    k_cc_compress<<<std::min(cdiv(g.t, kCcThreads), 1024), kCcThreads>>>(g.t, R.parent, R.member, R.counters);
-  };
-  // production chain, each kernel on the previous one's output (re-run from the tile stage each rep)
+  // the production tile kernel vs a candidate of the same block height, element by element
   tile(R.parent_ref, R.member_ref);
   CK(hipDeviceSynchronize());
   const double t_tile = time_ms([&]() { tile(R.parent, R.member); }, reps);
   same(R, "k_cc_tile (production)");
-  // merge and compress timed one launch at a time on fresh tile output
-  hipEvent_t e0, e1, e2;
-  CK(hipEventCreate(&e0));
-  CK(hipEventCreate(&e1));
-  CK(hipEventCreate(&e2));
-  double t_merge = 0, t_comp = 0;
-  for (int i = 0; i < reps; ++i) {
-    tile(R.parent, R.member);
-    CK(hipEventRecord(e0, 0));
-    merge();
-    CK(hipEventRecord(e1, 0));
-    compress();
-    CK(hipEventRecord(e2, 0));
-    CK(hipEventSynchronize(e2));
-    float a = 0, b = 0;
-    CK(hipEventElapsedTime(&a, e0, e1));
-    CK(hipEventElapsedTime(&b, e1, e2));
-    t_merge += a / reps;
-    t_comp += b / reps;
-  }
-  std::printf("production: tile %.1f us, merge %.1f us, compress %.1f us\n", t_tile * 1e3, t_merge * 1e3,
-              t_comp * 1e3);
-  if (kCcH == 32) {
-    auto tw32 = [&]() { k_cc_tile_w<32><<<R.tiles, 64>>>(g, R.bf, R.bocc, R.parent, R.member, 1); };
-    CK(hipMemset(R.parent, 0, ((size_t)g.t + 2) * 4));
-    tw32();
-    CK(hipDeviceSynchronize());
-    if (same(R, "k_cc_tile_w<32>")) std::printf("  k_cc_tile_w<32>: %.1f us\n", time_ms(tw32, reps) * 1e3);
-  }
+  auto tw32 = [&]() { k_cc_tile_w<kCcH><<<R.tiles, 64>>>(g, R.bf, R.bocc, R.parent, R.member, 1); };
+  CK(hipMemset(R.parent, 0, ((size_t)g.t + 2) * 4));
+  tw32();
+  CK(hipDeviceSynchronize());
+  if (same(R, "k_cc_tile_w (same blocks)"))
+    std::printf("  tile: production %.1f us, k_cc_tile_w %.1f us\n", t_tile * 1e3, time_ms(tw32, reps) * 1e3);
+  // whole chains (tile, merge, compress): the final parents are the partition's
+  // minimum sites whatever the blocks, so chains of other block heights compare too
+  hipEvent_t e[4];
+  for (auto& x : e) CK(hipEventCreate(&x));
+  auto chain = [&](const char* what, auto tilef, auto mergef, bool ref) {
+    double t[3] = {0, 0, 0};
+    for (int i = 0; i < reps; ++i) {
+      CK(hipEventRecord(e[0], 0));
+      tilef();
+      CK(hipEventRecord(e[1], 0));
+      mergef();
+      CK(hipEventRecord(e[2], 0));
+      k_cc_compress<<<std::min(cdiv(g.t, kCcThreads), 1024), kCcThreads>>>(g.t, R.parent, R.member, R.counters);
+      CK(hipEventRecord(e[3], 0));
+      CK(hipEventSynchronize(e[3]));
+      for (int k = 0; k < 3; ++k) {
+        float ms = 0;
+        CK(hipEventElapsedTime(&ms, e[k], e[k + 1]));
+        t[k] += ms * 1e3 / reps;
+      }
+    }
+    if (ref) {
+      CK(hipMemcpy(R.parent_ref, R.parent, ((size_t)g.t + 2) * 4, hipMemcpyDeviceToDevice));
+      CK(hipMemcpy(R.member_ref, R.member, (size_t)g.t + 2, hipMemcpyDeviceToDevice));
+      std::printf("  chain %-24s tile %.1f + merge %.1f + compress %.1f = %.1f us\n", what, t[0], t[1], t[2],
+                  t[0] + t[1] + t[2]);
+    } else if (same(R, what)) {
+      std::printf("  chain %-24s tile %.1f + merge %.1f + compress %.1f = %.1f us\n", what, t[0], t[1], t[2],
+                  t[0] + t[1] + t[2]);
+    }
+  };
+  auto merge_for = [&](auto hconst) {
+    constexpr int H = decltype(hconst)::value;
+    const int nseg = cdiv(g.m, kCcThreads), nfull = g.n / H, ncand = 2 * cdiv(g.m, kCcW) + 1;
+    return [&, nseg, nfull, ncand]() {
+      k_cc_merge<H><<<nfull * nseg + ncand * cdiv(g.n, kCcThreads), kCcThreads>>>(
+          g, PERC_BOND, R.bf, R.bocc, R.socc, R.parent, R.member, nseg, nfull);
+    };
+  };
+  chain("production", [&]() { tile(R.parent, R.member); }, merge_for(std::integral_constant<int, kCcH>{}), true);
+  chain("tile_w<32>", [&]() { k_cc_tile_w<32><<<cdiv(g.m, kCcW) * cdiv(g.n, 32), 64>>>(g, R.bf, R.bocc, R.parent,
+                                                                                       R.member, 1); },
+        merge_for(std::integral_constant<int, 32>{}), false);
+  chain("tile_w<16>", [&]() { k_cc_tile_w<16><<<cdiv(g.m, kCcW) * cdiv(g.n, 16), 64>>>(g, R.bf, R.bocc, R.parent,
+                                                                                       R.member, 1); },
+        merge_for(std::integral_constant<int, 16>{}), false);
+  chain("tile_w<64>", [&]() { k_cc_tile_w<64><<<cdiv(g.m, kCcW) * cdiv(g.n, 64), 64>>>(g, R.bf, R.bocc, R.parent,
+                                                                                       R.member, 1); },
+        merge_for(std::integral_constant<int, 64>{}), false);
   return 0;
 }
