@@ -9,6 +9,11 @@ timeout -k 10 120 ./tools/cc_bench 4096 0.6 20 > gpurun_out/r4f_cc_bench.log 2>&
 rc=$?; cat gpurun_out/r4f_cc_bench.log; [ $rc -ne 0 ] && exit $rc
 timeout -k 10 120 ./tools/spmv_bench 4096 20 > gpurun_out/r4f_spmv_bench.log 2>&1
 rc=$?; cat gpurun_out/r4f_spmv_bench.log; [ $rc -ne 0 ] && exit $rc
+# per-iteration cost over short (300-iteration) and long (10 000-iteration) stretches of one solve
+timeout -k 10 200 python -u tools/lib_ab.py --L 4096 --libs main --iters 600 --rounds 2 > gpurun_out/r4f_slope_short.json 2>&1
+rc=$?; tail -1 gpurun_out/r4f_slope_short.json; [ $rc -ne 0 ] && exit $rc
+timeout -k 10 300 python -u tools/lib_ab.py --L 4096 --libs main --iters 20000 --rounds 1 > gpurun_out/r4f_slope_long.json 2>&1
+rc=$?; tail -1 gpurun_out/r4f_slope_long.json; [ $rc -ne 0 ] && exit $rc
 L=4096 CBX2=1 bash tools/pmc_r2.sh || { tail -20 gpurun_out/pmc_r2.log; exit 1; }
 tail -8 gpurun_out/pmc_r2_reconcile_L4096.csv
 # read-queue levels of the row-major march at L = 8192 (Little's law: requests in flight)
