@@ -25,8 +25,6 @@ timeout -s KILL 150 rocprofv3 --pmc TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_sum TCC_HIT_
   python3 tools/pmc_probe.py --L 8192 --reps 16 --copies 8 >> gpurun_out/pmc_level.log 2>&1 || { tail gpurun_out/pmc_level.log; exit 1; }
 bash tools/configs.sh || { tail -5 gpurun_out/configs.log; exit 1; }
 tail -12 gpurun_out/configs.log
-timeout -k 10 480 python -u tools/literal_config.py c2_sq1024_bond_p50 1e-08 > gpurun_out/r4_literal_c2.log 2>&1
-rc=$?; tail -3 gpurun_out/r4_literal_c2.log; [ $rc -ne 0 ] && exit $rc
 # the driver's multi-GPU launch shape at one rank (torchrun, "nccl" group, libperc in the process)
 timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 \
   --master-port 29531 bench.py --gpus 1 --steps 1 --warmup 0 --force-dist --no-cpu-baseline \
