@@ -90,10 +90,12 @@ bool same(const Run& R, const char* what) {
 // nodes (larger root -> smaller, so a root is its component's minimum site;
 // a lane whose (run, run below) pair equals the column to its left skips
 // its union), the run node written as the provisional parent; a last pass
-// writes every site's root.  Square lattice, no pbc, bond kind.
+// writes every site's root.  Square lattice, no pbc; kind as cc_link (bond:
+// member = any incident occupied bond; site / mixed: the occupied site).
 template <int H>
-__global__ __launch_bounds__(64) void k_cc_tile_w(Geom g, const int* bond_first, const uint8_t* bocc,
-                                                  int* parent, uint8_t* member, int bf_closed) {
+__global__ __launch_bounds__(64) void k_cc_tile_w(Geom g, int kind, const int* bond_first, const uint8_t* bocc,
+                                                  const uint8_t* socc, int* parent, uint8_t* member,
+                                                  int bf_closed) {
   __shared__ int uf[kCcW * H];
   const int ntx = cdiv(g.m, kCcW);
   const int tb = xcd_logical_block(blockIdx.x, gridDim.x);
@@ -101,24 +103,39 @@ __global__ __launch_bounds__(64) void k_cc_tile_w(Geom g, const int* bond_first,
   const int c0 = tx * kCcW, r0 = ty * H;
   const int tw = min(kCcW, g.m - c0), th = min(H, g.n - r0);
   const int lane = threadIdx.x;
-  auto load_row = [&](int r, unsigned (&R)[2], unsigned (&U)[2]) {
+  // R / U: the link right / up of each of the lane's two sites; O: the site occupied (site kinds)
+  auto load_row = [&](int r, unsigned (&R)[2], unsigned (&U)[2], unsigned (&O)[2]) {
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       const int lc = lane + 64 * h, col = c0 + lc, row = r0 + r;
       const bool v = lc < tw && r < th;
       const int s = row * g.m + col + 1;
-      const int fb = !v ? 0 : bf_closed && row <= g.n - 2 ? bf_square(g, row, col) : bond_first[s];
       const bool hr = v && col < g.m - 1, hu = v && row < g.n - 1;
+      if (kind == PERC_SITE) {
+        const unsigned o = v ? socc[s] : 0u;
+        O[h] = o;
+        R[h] = o && hr ? socc[s + 1] : 0u;
+        U[h] = o && hu ? socc[s + g.m] : 0u;
+        continue;
+      }
+      const int fb = !v ? 0 : bf_closed && row <= g.n - 2 ? bf_square(g, row, col) : bond_first[s];
       R[h] = hr ? bocc[fb] : 0u;
       U[h] = hu ? bocc[fb + (col < g.m - 1 ? 1 : 0)] : 0u;
+      O[h] = 1u;
+      if (kind != PERC_BOND) {  // mixed: the bond and both sites
+        const unsigned o = v ? socc[s] : 0u;
+        O[h] = o;
+        R[h] = R[h] && o && socc[s + 1];
+        U[h] = U[h] && o && socc[s + g.m];
+      }
     }
   };
-  unsigned R[2], U[2], Rn[2], Un[2], Up[2] = {0u, 0u};
+  unsigned R[2], U[2], O[2], Rn[2], Un[2], On[2], Up[2] = {0u, 0u};
   int labp[2] = {0, 0};
-  load_row(0, R, U);
+  load_row(0, R, U, O);
   const unsigned long long le = lane == 63 ? ~0ull : ((2ull << lane) - 1ull);
   for (int r = 0; r < th; ++r) {
-    load_row(r + 1, Rn, Un);  // (past th: nothing loaded)
+    load_row(r + 1, Rn, Un, On);  // (past th: nothing loaded)
     // runs: column c has a left link iff c - 1 links right
     const unsigned rl0 = __shfl(R[0], (lane + 63) & 63, 64), rl1 = __shfl(R[1], (lane + 63) & 63, 64);
     const bool left0 = lane > 0 && rl0, left1 = lane > 0 ? rl1 != 0u : rl0 != 0u;  // (lane 0, half 1: column 63)
@@ -165,7 +182,8 @@ __global__ __launch_bounds__(64) void k_cc_tile_w(Geom g, const int* bond_first,
       const int lc = lane + 64 * h, s = (r0 + r) * g.m + c0 + lc + 1;
       const bool lft = h ? left1 : left0;
       parent[s] = node[h];
-      member[s] = (R[h] | U[h] | (lft ? 1u : 0u) | (r > 0 ? Up[h] : 0u)) ? 1 : 0;
+      member[s] = kind == PERC_BOND ? ((R[h] | U[h] | (lft ? 1u : 0u) | (r > 0 ? Up[h] : 0u)) ? 1 : 0)
+                                    : (O[h] ? 1 : 0);
     }
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
@@ -173,6 +191,7 @@ __global__ __launch_bounds__(64) void k_cc_tile_w(Geom g, const int* bond_first,
       Up[h] = U[h];
       R[h] = Rn[h];
       U[h] = Un[h];
+      O[h] = On[h];
     }
   }
   __builtin_amdgcn_wave_barrier();
@@ -237,7 +256,7 @@ int main(int argc, char** argv) {
   CK(hipDeviceSynchronize());
   const double t_tile = time_ms([&]() { tile(R.parent, R.member); }, reps);
   same(R, "k_cc_tile (production)");
-  auto tw32 = [&]() { k_cc_tile_w<kCcH><<<R.tiles, 64>>>(g, R.bf, R.bocc, R.parent, R.member, 1); };
+  auto tw32 = [&]() { k_cc_tile_w<kCcH><<<R.tiles, 64>>>(g, PERC_BOND, R.bf, R.bocc, R.socc, R.parent, R.member, 1); };
   CK(hipMemset(R.parent, 0, ((size_t)g.t + 2) * 4));
   tw32();
   CK(hipDeviceSynchronize());
@@ -283,14 +302,26 @@ int main(int argc, char** argv) {
     };
   };
   chain("production", [&]() { tile(R.parent, R.member); }, merge_for(std::integral_constant<int, kCcH>{}), true);
-  chain("tile_w<32>", [&]() { k_cc_tile_w<32><<<cdiv(g.m, kCcW) * cdiv(g.n, 32), 64>>>(g, R.bf, R.bocc, R.parent,
-                                                                                       R.member, 1); },
+  chain("tile_w<32>", [&]() { k_cc_tile_w<32><<<cdiv(g.m, kCcW) * cdiv(g.n, 32), 64>>>(g, PERC_BOND, R.bf, R.bocc, R.socc,
+                                                                                       R.parent, R.member, 1); },
         merge_for(std::integral_constant<int, 32>{}), false);
-  chain("tile_w<16>", [&]() { k_cc_tile_w<16><<<cdiv(g.m, kCcW) * cdiv(g.n, 16), 64>>>(g, R.bf, R.bocc, R.parent,
-                                                                                       R.member, 1); },
+  chain("tile_w<16>", [&]() { k_cc_tile_w<16><<<cdiv(g.m, kCcW) * cdiv(g.n, 16), 64>>>(g, PERC_BOND, R.bf, R.bocc, R.socc,
+                                                                                       R.parent, R.member, 1); },
         merge_for(std::integral_constant<int, 16>{}), false);
-  chain("tile_w<64>", [&]() { k_cc_tile_w<64><<<cdiv(g.m, kCcW) * cdiv(g.n, 64), 64>>>(g, R.bf, R.bocc, R.parent,
-                                                                                       R.member, 1); },
+  chain("tile_w<64>", [&]() { k_cc_tile_w<64><<<cdiv(g.m, kCcW) * cdiv(g.n, 64), 64>>>(g, PERC_BOND, R.bf, R.bocc, R.socc,
+                                                                                       R.parent, R.member, 1); },
         merge_for(std::integral_constant<int, 64>{}), false);
+  // site and mixed kinds (sites occupied at 0.8 by another hash): the production tile kernel vs the candidate
+  {
+    std::vector<uint8_t> so((size_t)g.t + 2, 0);
+    for (int st = 1; st <= g.t; ++st) so[st] = hash32((unsigned long long)st * 0xD1B54A32D192ED03ull + 777) < 0xCCCCCCCCu;
+    CK(hipMemcpy(R.socc, so.data(), so.size(), hipMemcpyHostToDevice));
+    for (int kind : {PERC_SITE, PERC_SITEBOND}) {
+      k_cc_tile<<<R.tiles, kCcThreads>>>(g, kind, R.bf, R.bocc, R.socc, R.parent_ref, R.member_ref, 1, nullptr);
+      k_cc_tile_w<kCcH><<<R.tiles, 64>>>(g, kind, R.bf, R.bocc, R.socc, R.parent, R.member, 1);
+      CK(hipDeviceSynchronize());
+      same(R, kind == PERC_SITE ? "k_cc_tile_w, site kind" : "k_cc_tile_w, mixed kind");
+    }
+  }
   return 0;
 }
