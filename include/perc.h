@@ -449,6 +449,16 @@ int perc_err_history(perc_ctx *h, double *out, int cap);
    conductances.  n = the lattice's bond count.  With weights the solver
    runs the CSR operator (the stencil code encodes two values only). */
 int perc_set_bond_weights(perc_ctx *h, const double *w, long long n);
+/* ConductCalc.m condtype 2 from C / Fortran (MATLAB/ConductCalc.m:38-47,
+   94-97, 114-118, 136-146): after perc_label, every bond the assembly gives
+   -g0 under `rule` (the spanning cluster's) gets -g0*rand, one
+   rand('twister', seed) draw per such bond in bond-list order; the others
+   keep their value (perc_set_bond_weights with those multipliers; no
+   spanning cluster: fixed conductances).  perc_twister_uniform: n draws of
+   that generator (MT19937 init_genrand(seed), 53-bit genrand_res53
+   doubles).  MATLAB parity itself is unpinned (no MATLAB here). */
+int perc_set_conductcalc_weights(perc_ctx *h, int rule, unsigned int seed);
+int perc_twister_uniform(unsigned int seed, long long n, double *out);
 /* Solver loop of the assembled system: out5[0] = 0 (no march kernel: LDS
    tiles, split or CSR), 1 (per-wave march k_cg_march), 3 (resident
    persistent solve k_cg_res), 4 (one-workgroup solve of a small system,

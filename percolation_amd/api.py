@@ -267,6 +267,14 @@ class Context:
             L.check(m, "perc_err_history")
         return out
 
+    def set_conductcalc_weights(self, rule, seed=1838534):
+        """ConductCalc.m condtype 2 inside libperc (perc_set_conductcalc_weights):
+        the spanning cluster's -g0 bonds of the last labeling get
+        -g0*rand('twister', seed), one draw per bond in bond-list order --
+        conductcalc_weights + set_bond_weights without the host replay."""
+        L.check(L.lib().perc_set_conductcalc_weights(self.h, rule, int(seed) & 0xFFFFFFFF),
+                "perc_set_conductcalc_weights")
+
     def set_bond_weights(self, w=None):
         """Per-bond conductance multipliers for the spanning cluster's bonds
         (ConductCalc.m condtype 2; None: fixed g0).  perc_set_bond_weights."""
@@ -432,6 +440,15 @@ def bondsite(lattice=0, m=10, n=10, pbc=0, ps=0.50, pb=0.50, sseed=143285, bseed
     r["bsbond"] = fmt_i10(b1, b2, r["bond_label"])
     r.update(sorder=sorder, border=border)
     return r
+
+
+def twister_uniform(seed, n):
+    """n draws of rand('twister', seed): MT19937 init_genrand(seed), 53-bit
+    genrand_res53 doubles (perc_twister_uniform, host C)."""
+    out = np.empty(max(int(n), 1))
+    L.check(L.lib().perc_twister_uniform(int(seed) & 0xFFFFFFFF, int(n), out.ctypes.data),
+            "perc_twister_uniform")
+    return out[:n]
 
 
 def conductcalc_weights(rule, b1, b2, bond_label, site_label, perccln, seed=1838534):

@@ -436,6 +436,43 @@ hipError_t dev_currents(perc_ctx* h, int rule, int cur_rule, double g0, double l
   return hipStreamSynchronize(st);
 }
 
+// the bonds the assembly gives -g0 (bond_value's "in"), one byte per bond in
+// bond-list order: ConductCalc.m condtype 2 draws one rand per such bond
+// (perc_set_conductcalc_weights)
+__global__ void k_bond_mask(Geom g, int rule, const int* bond_first, const uint8_t* bocc,
+                            const uint8_t* socc, const int* parent, int span_root, uint8_t* mask) {
+  const int s = blockIdx.x * blockDim.x + threadIdx.x + 1;
+  if (s > g.t - 1) return;
+  const int row = div_m(g, s - 1);
+  int nn[6];
+  nearestn_rc(g, s, row, s - 1 - row * g.m, nn);
+  const int fb = bond_first[s];
+  int r = 0;
+  for (int k = 0; k < g.scn; ++k) {
+    const int q = nn[k];
+    if (q <= s) continue;
+    const int id = fb + r++;
+    bool in;
+    if (rule == PERC_RULE_BOND) in = bocc[id] && parent[s] == span_root;
+    else if (rule == PERC_RULE_SITE) in = socc[s] && socc[q] && parent[s] == span_root;
+    else in = bocc[id] && socc[s] && socc[q] && parent[s] == span_root;
+    mask[id] = in ? 1 : 0;
+  }
+}
+
+hipError_t dev_bond_mask(perc_ctx* h, int rule, uint8_t* mask_host) {
+  DeviceBuffers& d = h->d;
+  uint8_t* dm = nullptr;
+  HIP_TRY(dmalloc(&dm, (size_t)h->nb + 8));
+  k_bond_mask<<<blocks_for(h->g.t), kBlock, 0, h->stream>>>(h->g, rule, d.bond_first, d.bocc, d.socc, d.parent,
+                                                           h->span_root, dm);
+  hipError_t e = hipGetLastError();
+  if (e == hipSuccess) e = hipMemcpyAsync(mask_host, dm, (size_t)h->nb, hipMemcpyDeviceToHost, h->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
+  (void)hipFree(dm);
+  return e;
+}
+
 hipError_t dev_set_bond_weights(perc_ctx* h, const double* w) {
   DeviceBuffers& d = h->d;
   // the assembled system (its stencil codes, rhs, the CSR copy ensure_csr

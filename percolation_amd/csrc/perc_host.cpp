@@ -925,6 +925,61 @@ int perc_set_bond_weights(perc_ctx* h, const double* w, long long n) {
   return hip_status(dev_set_bond_weights(h, w), "perc_set_bond_weights");
 }
 
+// MT19937 (Matsumoto & Nishimura): init_genrand + genrand_int32, and the
+// 53-bit doubles of genrand_res53 -- MATLAB's rand('twister', seed)
+// (ConductCalc.m:38-47), also numpy.random.RandomState(seed).random_sample
+namespace {
+struct Twister {
+  uint32_t mt[624];
+  int mti = 625;
+  explicit Twister(uint32_t seed) {
+    mt[0] = seed;
+    for (mti = 1; mti < 624; ++mti) mt[mti] = 1812433253u * (mt[mti - 1] ^ (mt[mti - 1] >> 30)) + (uint32_t)mti;
+  }
+  uint32_t next() {
+    if (mti >= 624) {
+      for (int k = 0; k < 624; ++k) {
+        const uint32_t y = (mt[k] & 0x80000000u) | (mt[(k + 1) % 624] & 0x7fffffffu);
+        mt[k] = mt[(k + 397) % 624] ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
+      }
+      mti = 0;
+    }
+    uint32_t y = mt[mti++];
+    y ^= y >> 11;
+    y ^= (y << 7) & 0x9d2c5680u;
+    y ^= (y << 15) & 0xefc60000u;
+    y ^= y >> 18;
+    return y;
+  }
+  double res53() {
+    const uint32_t a = next() >> 5, b = next() >> 6;
+    return (a * 67108864.0 + b) * (1.0 / 9007199254740992.0);
+  }
+};
+}  // namespace
+
+int perc_twister_uniform(unsigned int seed, long long n, double* out) {
+  if (n < 0 || (n && !out)) return PERC_EINVAL;
+  Twister t(seed);
+  for (long long k = 0; k < n; ++k) out[k] = t.res53();
+  return PERC_OK;
+}
+
+int perc_set_conductcalc_weights(perc_ctx* h, int rule, unsigned int seed) {
+  if (!h || (rule != PERC_RULE_BOND && rule != PERC_RULE_SITE && rule != PERC_RULE_MIXED)) return PERC_EINVAL;
+  if (!h->labeled) return PERC_ESTATE;
+  hipSetDevice(h->device);
+  if (!h->span_root) return hip_status(dev_set_bond_weights(h, nullptr), "perc_set_conductcalc_weights");
+  std::vector<uint8_t> mask((size_t)h->nb);
+  int rc = hip_status(dev_bond_mask(h, rule, mask.data()), "perc_set_conductcalc_weights");
+  if (rc) return rc;
+  std::vector<double> w((size_t)h->nb, 1.0);
+  Twister t(seed);
+  for (size_t id = 0; id < mask.size(); ++id)
+    if (mask[id]) w[id] = t.res53();  // one rand per -g0 bond, bond-list order (ConductCalc.m:94-97)
+  return hip_status(dev_set_bond_weights(h, w.data()), "perc_set_conductcalc_weights");
+}
+
 int perc_march_info(perc_ctx* h, int* out5) {
   if (!h || !out5) return PERC_EINVAL;
   if (!h->assembled) return PERC_ESTATE;

@@ -257,6 +257,8 @@ hipError_t dev_currents(perc_ctx* h, int rule, int cur_rule, double g0, double l
 hipError_t dev_spmv(perc_ctx* h, const double* x, double* y);
 hipError_t dev_selftest_division(long long n, unsigned long long seed, unsigned long long* out3);
 hipError_t dev_set_bond_weights(perc_ctx* h, const double* w);
+// 1 per bond the assembly gives -g0 under `rule` (spanning cluster h->span_root)
+hipError_t dev_bond_mask(perc_ctx* h, int rule, uint8_t* mask_host);
 hipError_t dev_bench(perc_ctx* h, int which, int reps, double* ms);
 
 // host replay (perc_replay.cpp): reference label numbering

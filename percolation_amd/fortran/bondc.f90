@@ -5,7 +5,9 @@
 ! Parameters: the reference's block (Square/bondc.f:67-92; Triangular:
 ! pb = .35, seed = 62703), overridable by an optional namelist file
 ! bondc.nml (&bondc lattice, m, n, pbc, pb, seed, Va, g0, tol, itmax,
-! device, nslab, xport, dot_order /).  nslab > 1 splits the solve into row
+! device, nslab, xport, dot_order, condtype, cseed /).  condtype 2 gives the
+! spanning cluster's bonds -g0*rand('twister', cseed) (MATLAB/ConductCalc.m
+! condtype 2; 1, the default, fixed g0).  nslab > 1 splits the solve into row
 ! slabs over nslab contexts (devices device .. device+nslab-1 with xport 0,
 ! RCCL; all on `device` with xport 1, host-staged); dot_order 1 folds
 ! linbcg's sums in the reference's order (bitwise its solve).  Outputs as
@@ -19,10 +21,10 @@ program bondc
 #ifndef PERC_LATTICE
 #define PERC_LATTICE 0
 #endif
-  integer(c_int) :: lattice, m, n, pbc, seed, itmax, device, nslab, xport, dot_order
+  integer(c_int) :: lattice, m, n, pbc, seed, itmax, device, nslab, xport, dot_order, condtype, cseed
   double precision :: pb, Va, g0, tol
   namelist /bondc_nml/ lattice, m, n, pbc, pb, seed, Va, g0, tol, itmax, device, nslab, xport, &
-                       dot_order
+                       dot_order, condtype, cseed
   integer(c_int) :: nb, tbonds, i, j, id, rc, stats(4), perccln, perccls, s, dev
   integer(c_int), allocatable, target :: b1(:), b2(:), order(:), label(:), csize(:)
   type(c_ptr) :: h
@@ -51,6 +53,8 @@ program bondc
   nslab = 1
   xport = PERC_XPORT_RCCL
   dot_order = PERC_DOT_FAST
+  condtype = 1
+  cseed = 1838534
   if (perc_have_file('bondc.nml')) then
     open(newunit=u, file='bondc.nml', status='old')
     read(u, nml=bondc_nml)
@@ -101,6 +105,8 @@ program bondc
   if (perccln > 0) then
     write(6, *) "Calculating internal node voltages"
     if (dot_order /= PERC_DOT_FAST) call perc_check(perc_set_dot_order(h, dot_order), 'perc_set_dot_order')
+    if (condtype == 2) call perc_check(perc_set_conductcalc_weights(h, PERC_RULE_BOND, cseed), &
+                                       'perc_set_conductcalc_weights')
     if (nslab > 1) then
       ! the same occupancy labeled on every slab's context, then one split solve
       allocate(hs(nslab))
@@ -111,6 +117,8 @@ program bondc
         call perc_check(perc_ctx_create(dev, lattice, m, n, pbc, hs(s)), 'perc_ctx_create')
         call perc_check(perc_occupy(hs(s), PERC_BOND, 0, c_null_ptr, tbonds, c_loc(order)), 'perc_occupy')
         call perc_check(perc_label(hs(s), info, c_null_ptr), 'perc_label')
+        if (condtype == 2) call perc_check(perc_set_conductcalc_weights(hs(s), PERC_RULE_BOND, cseed), &
+                                           'perc_set_conductcalc_weights')
       end do
       call perc_check(perc_dslab_solve_group(nslab, c_loc(hs), xport, PERC_RULE_BOND, PERC_CUR_FORTRAN, &
                                              Va, g0, PERC_LEAK, 2, tol, itmax, 0, res), &

@@ -181,6 +181,14 @@ module perc_api
       type(perc_cond_result) :: res
     end function perc_dslab_solve_group
 
+    ! ConductCalc.m condtype 2: the spanning cluster's bonds get -g0*rand('twister', seed)
+    integer(c_int) function perc_set_conductcalc_weights(h, rule, seed) &
+        bind(C, name='perc_set_conductcalc_weights')
+      import :: c_int, c_ptr
+      type(c_ptr), value :: h
+      integer(c_int), value :: rule, seed
+    end function perc_set_conductcalc_weights
+
     ! the same loop with one process per GPU (an MPI program: rank 0 calls
     ! perc_dslab_unique_id, MPI_Bcast's the PERC_DSLAB_ID_BYTES bytes, every
     ! rank binds its labeled context to slab s of K, then perc_dslab_solve)

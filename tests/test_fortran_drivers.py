@@ -20,6 +20,8 @@ import subprocess
 import pytest
 
 import golden_io as G
+from percolation_amd import _lib as PL
+from percolation_amd import api
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 BIN = os.path.join(REPO, "percolation_amd", "fortran", "bin")
@@ -180,3 +182,37 @@ def test_bondc_driver_split_solve(nslab, tmp_path):
     (g1, b1, t1), (gk, bk, tk) = out[1], out[nslab]
     assert t1 == tk
     assert abs(gk - g1) <= 1e-10 * abs(g1) and abs(bk - b1) <= 1e-10 * abs(b1), (out[1][:2], out[nslab][:2])
+
+
+@pytest.mark.gpu
+def test_bondc_driver_random_conductances(tmp_path):
+    """condtype = 2 (ConductCalc.m condtype 2 from the Fortran host:
+    perc_set_conductcalc_weights): the driver's conductance equals the
+    Python route's -- the same occupancy, the host replay's labels, the
+    weights from numpy's MT19937 (api.conductcalc_weights), perc_set_bond_
+    weights -- to the printed precision; and differs from the fixed-g0 run"""
+    prog = exe("bondc", 0)
+    m = n = 64
+    got = {}
+    for ct in (1, 2):
+        d = tmp_path / ("c%d" % ct)
+        d.mkdir()
+        (d / "bondc.nml").write_text("&bondc_nml lattice=0, m=%d, n=%d, pbc=0, pb=0.6, seed=626504, "
+                                     "tol=1e-13, itmax=100000, condtype=%d, cseed=1838534 /\n" % (m, n, ct))
+        r = subprocess.run([prog], cwd=d, capture_output=True, text=True, timeout=300)
+        assert r.returncode == 0, r.stderr[-2000:]
+        line = [l for l in r.stdout.splitlines() if "Conductance:" in l][-1]
+        got[ct] = [float(x) for x in line.split(":")[1].split()]
+    nb = api.nbonds(0, m, n, 0)
+    order = api.shuffled_ids(nb, 626504)
+    b1, b2 = api.bond_list(0, m, n, 0)
+    with api.Context(0, m, n, 0) as ctx:
+        ctx.occupy(PL.BOND, bond_order=order, nbonds_=int(0.6 * nb))
+        assert ctx.label()["nspan"] > 0
+        ln = ctx.label_numbers(PL.BOND)
+        ctx.set_bond_weights(api.conductcalc_weights(PL.RULE_BOND, b1, b2, ln["bond_label"], None,
+                                                     ln["perccln"]))
+        c = ctx.conductance(tol=1e-13, itmax=100000)
+    assert abs(got[2][0] - c["gtop"]) <= 1e-12 * abs(c["gtop"]), (got[2], c)
+    assert abs(got[2][1] - c["gbot"]) <= 1e-12 * abs(c["gbot"]), (got[2], c)
+    assert abs(got[2][0] - got[1][0]) > 1e-3 * abs(got[1][0])

@@ -796,6 +796,10 @@ def test_random_conductance_vs_direct_solve(kind, rule, lat, m, n, ps, pb):
         ctx.set_bond_weights(w)
         c = ctx.conductance(rule, PL.CUR_MATLAB, tol=1e-14, itmax=400000)
         assert ctx.matrix_format() == PL.FMT_CSR
+        # the same weights drawn inside libperc (the C / Fortran route): the same solve bitwise
+        ctx.set_conductcalc_weights(rule)
+        c_lib = ctx.conductance(rule, PL.CUR_MATLAB, tol=1e-14, itmax=400000)
+        assert (c_lib["gtop"], c_lib["gbot"], c_lib["iter"]) == (c["gtop"], c["gbot"], c["iter"])
         ctx.set_bond_weights(None)
         c_fixed = ctx.conductance(rule, PL.CUR_MATLAB, tol=1e-14, itmax=400000)
     gval = O.f64(nb)

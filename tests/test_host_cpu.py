@@ -288,3 +288,14 @@ def test_square_bond_first_closed_form(m, n, pbc):
     for r in range(n - 1):
         for c in range(m):
             assert first[r * m + c + 1] == r * (2 * m - 1 + pbc) + 2 * c + (pbc if c > 0 else 0)
+
+
+@pytest.mark.parametrize("seed", [0, 1, 1838534, 2 ** 32 - 1])
+def test_twister_equals_numpy_mt19937(seed):
+    """perc_twister_uniform (the C generator behind perc_set_conductcalc_
+    weights, ConductCalc.m:38-47 rand('twister', seed)) draws numpy's
+    RandomState(seed).random_sample bitwise: MT19937 init_genrand + 53-bit
+    genrand_res53, over several state refills"""
+    got = api.twister_uniform(seed, 3000)
+    want = np.random.RandomState(seed).random_sample(3000)
+    assert np.array_equal(got, want)
