@@ -563,6 +563,11 @@ int perc_nr_status_(void);  /* F77 spelling: `integer perc_nr_status` */
    NR drop-in reproduces the reference solver bitwise; PERC_DOT_FAST: the
    wave-tree sums of perc_conductance) */
 int perc_nr_set_dot_order(int order);
+/* call nearestn(rn) (Square/bondc.f:617-715, Triangular/bondc.f:619-804):
+   the neighbours of site rn into the caller's blank COMMON m, n, t, pbc,
+   nn(10), scn (symbol __BLNK__; scn 4 square, 6 triangular), zeros where a
+   neighbour is missing; perc_nr_status() = PERC_ESTATE without one. */
+void nearestn_(const int *rn);
 
 #ifdef __cplusplus
 }

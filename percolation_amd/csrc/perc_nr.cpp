@@ -44,6 +44,12 @@ int g_nr_dot = PERC_DOT_LITERAL;  // perc_nr_set_dot_order
 extern "C" {
 // COMMON /mat/ of the calling Fortran program (weak: absent in non-Fortran hosts)
 extern MatCommon mat_ __attribute__((weak));
+// the calling program's blank COMMON m, n, t, pbc, nn(10), scn (Square/bondc.f:58,
+// Triangular/bondc.f; flang and gfortran name it __BLNK__)
+struct BlankCommon {
+  int m, n, t, pbc, nn[10], scn;
+};
+extern BlankCommon __BLNK__ __attribute__((weak));
 }
 
 namespace {
@@ -325,4 +331,23 @@ static void linbcg_impl(int* n_, double* b, double* x, int* itol, double* tol, i
   }
 }
 
+}  // extern "C"
+
+extern "C" {
+// call nearestn(rn) (Square/bondc.f:617-715, Triangular/bondc.f:619-804): the
+// neighbours of site rn into the caller's blank COMMON nn(1..scn), zeros
+// where a neighbour is missing, from its m, n, pbc and scn (4: square, 6:
+// triangular).  Sets perc_nr_status to PERC_ESTATE without a blank COMMON.
+void nearestn_(const int* rn) {
+  if (&__BLNK__ == nullptr || (__BLNK__.scn != 4 && __BLNK__.scn != 6)) {
+    g_status = PERC_ESTATE;
+    return;
+  }
+  BlankCommon& c = __BLNK__;
+  const perc::Geom g = perc::make_geom(c.scn == 4 ? perc::kSquare : perc::kTriangular, c.m, c.n, c.pbc);
+  int nn[6] = {0, 0, 0, 0, 0, 0};
+  if (*rn >= 1 && *rn <= g.t) perc::nearestn(g, *rn, nn);
+  for (int z = 0; z < c.scn; ++z) c.nn[z] = nn[z];
+  g_status = PERC_OK;
+}
 }  // extern "C"

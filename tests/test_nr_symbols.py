@@ -17,6 +17,7 @@ import pytest
 
 import golden_io as G
 import oracle_lib as O
+from percolation_amd import api
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 EXE = os.path.join(REPO, "percolation_amd", "fortran", "bin", "nr_caller")
@@ -195,3 +196,26 @@ def test_route1_relink_of_the_reference_program():
         assert "[perc] linbcg_ failed" in r.stderr and "no HIP device" in r.stderr
     finally:
         shutil.rmtree(d)
+
+
+NN_EXE = os.path.join(REPO, "percolation_amd", "fortran", "bin", "nn_caller")
+
+
+@pytest.mark.parametrize("lat,m,n,pbc", [(0, 7, 5, 0), (0, 7, 5, 1), (1, 8, 6, 0), (1, 8, 6, 1)])
+def test_nearestn_symbol_fills_blank_common(lat, m, n, pbc, tmp_path):
+    """CPU: an F77 program with the reference's blank COMMON (m, n, t, pbc,
+    nn(10), scn; Square/bondc.f:58) calls nearestn(i) for every site and
+    gets libperc's nearestn_ answer in nn(1..scn) -- the neighbour lists of
+    perc_nearestn (pinned to the oracle and the reference by
+    test_topology_equals_oracle)"""
+    if not os.path.exists(NN_EXE):
+        pytest.skip("nn_caller not built (make -C percolation_amd/fortran)")
+    scn = 4 if lat == 0 else 6
+    (tmp_path / "nn.in").write_text("%d %d %d %d\n" % (m, n, pbc, scn))
+    r = subprocess.run([NN_EXE], cwd=tmp_path, capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0, r.stderr[-2000:]
+    got = np.fromfile(tmp_path / "nn.bin", dtype=np.int32)
+    assert got[-1] == 0
+    got = got[:-1].reshape(m * n, scn)
+    for s in range(1, m * n + 1):
+        assert list(got[s - 1]) == list(api.nearestn(lat, m, n, pbc, s)), s
