@@ -143,6 +143,7 @@ SIGNATURES = {
     "dsprsax_": (None, [_VP] * 5),
     "dsprstx_": (None, [_VP] * 5),
     "atimes_": (None, [_VP] * 4),
+    "nearestn_": (None, [_VP]),
     "asolve_": (None, [_VP] * 4),
     "snrm_": (C.c_double, [_VP] * 3),
     "linbcg_": (None, [_VP] * 8),
