@@ -185,6 +185,15 @@ int perc_replay_labels(int lattice, int m, int n, int pbc, int kind, int nsites,
                        const int *site_order, int nbonds, const int *bond_order,
                        int *bond_label, int *site_label, int *csize, int cap,
                        int *stats);
+/* bondc.f's per-bond trace (bondocc.txt, Square/bondc.f:194-376): for the
+   first nbond entries of bond_order (1-based ids, 0 = the spill slot),
+   trace[3i] = 0 when the bond found no occupied neighbour bond and opened
+   cluster trace[3i+1], 1 when it joined the largest neighbouring cluster
+   trace[3i+1]; trace[3i+2] = that cluster's size after the step (host
+   replay; the Fortran bondc driver writes bondocc.txt from it with
+   trace = 1). */
+int perc_replay_bond_trace(int lattice, int m, int n, int pbc, int nbond, const int *bond_order,
+                           int *trace);
 
 /* ---- conductance ----------------------------------------------------- */
 typedef struct {

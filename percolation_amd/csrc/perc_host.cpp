@@ -678,6 +678,22 @@ int perc_replay_labels(int lattice, int m, int n, int pbc, int kind, int nsites,
                             stats);
 }
 
+int perc_replay_bond_trace(int lattice, int m, int n, int pbc, int nbond, const int* bond_order,
+                           int* trace) {
+  if ((lattice != PERC_SQUARE && lattice != PERC_TRIANGULAR) || m < 2 || n < 2 || nbond < 0 ||
+      (nbond && (!bond_order || !trace)))
+    return PERC_EINVAL;
+  const Geom g = make_geom(lattice, m, n, pbc);
+  std::vector<int> bf(g.t + 2, 0);
+  for (int s = 1; s <= g.t + 1; ++s)
+    bf[s] = bf[s - 1] + ((s - 1 >= 1 && s - 1 <= g.t - 1) ? forward_count(g, s - 1) : 0);
+  if (nbond > bf[g.t + 1] + 1) return PERC_EINVAL;
+  const long long nb = nbonds(g);
+  std::vector<int> c(nb + 2, 0), bl(nb, 0);
+  int st[4] = {0, 0, 0, 0};
+  return replay_bonds(g, bf, bond_order, nbond, bl.data(), c.data(), (int)c.size(), st, trace);
+}
+
 // the spanning cluster's Kirchhoff system (perc_conductance / perc_assemble)
 static int assemble_impl(perc_ctx* h, int rule, double g0, double leak, double Va, const char* who) {
   hipError_t e = dev_assemble(h, rule, g0, leak, Va, h->span_root);

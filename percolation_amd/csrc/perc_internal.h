@@ -262,8 +262,11 @@ hipError_t dev_bond_mask(perc_ctx* h, int rule, uint8_t* mask_host);
 hipError_t dev_bench(perc_ctx* h, int which, int reps, double* ms);
 
 // host replay (perc_replay.cpp): reference label numbering
+// trace (optional, 3 per order entry): bondc.f's per-bond case (0: no
+// occupied neighbour bond, 1: joined the largest neighbouring cluster), the
+// cluster number the bond got and that cluster's size after the step
 int replay_bonds(const Geom& g, const std::vector<int>& bond_first, const int* order,
-                 int count, int* label, int* csize, int cap, int* stats);
+                 int count, int* label, int* csize, int cap, int* stats, int* trace = nullptr);
 int replay_sites(const Geom& g, const int* order, int count, int* label, int* csize, int cap,
                  int* stats);
 int replay_bondsite(const Geom& g, const std::vector<int>& bond_first, const int* sorder,

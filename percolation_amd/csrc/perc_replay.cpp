@@ -84,7 +84,7 @@ inline void track_max(const std::vector<int>& c, int lcn, int lcs, int* maxcn, i
 }  // namespace
 
 int replay_bonds(const Geom& g, const std::vector<int>& bond_first, const int* order, int count,
-                 int* label, int* csize, int cap, int* stats) {
+                 int* label, int* csize, int cap, int* stats, int* trace) {
   const long long nb = nbonds(g);
   if (cap < nb + 2) return PERC_EINVAL;
   std::vector<int> c(cap, 0);  // c(0) stays 0 (hazard H1)
@@ -98,6 +98,7 @@ int replay_bonds(const Geom& g, const std::vector<int>& bond_first, const int* o
       // H2 sentinel (0,0): no nnb row or b row matches; the reference opens
       // a cluster number that no bond carries.
       c[cln] = 1;
+      if (trace) { trace[3 * i] = 0; trace[3 * i + 1] = cln; trace[3 * i + 2] = 1; }
       ++cln;
       if (maxcs == 0) { maxcs = 1; maxcn = 1; }
       continue;
@@ -135,6 +136,7 @@ int replay_bonds(const Geom& g, const std::vector<int>& bond_first, const int* o
       const int r = dsu.unite(a, b);
       clab[r] = cln;
       c[cln] = 1;
+      if (trace) { trace[3 * i] = 0; trace[3 * i + 1] = cln; trace[3 * i + 2] = 1; }
       ++cln;
     } else {
       int clsum = lcs;
@@ -151,6 +153,7 @@ int replay_bonds(const Geom& g, const std::vector<int>& bond_first, const int* o
       const int r = dsu.unite(a, b);
       clab[r] = lcn;
       c[lcn] = clsum + 1;
+      if (trace) { trace[3 * i] = 1; trace[3 * i + 1] = lcn; trace[3 * i + 2] = c[lcn]; }
     }
     track_max(c, lcn, lcs, &maxcn, &maxcs);
   }

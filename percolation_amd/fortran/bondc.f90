@@ -5,7 +5,10 @@
 ! Parameters: the reference's block (Square/bondc.f:67-92; Triangular:
 ! pb = .35, seed = 62703), overridable by an optional namelist file
 ! bondc.nml (&bondc lattice, m, n, pbc, pb, seed, Va, g0, tol, itmax,
-! device, nslab, xport, dot_order, condtype, cseed /).  condtype 2 gives the
+! device, nslab, xport, dot_order, condtype, cseed, trace /).  trace = 1 also
+! writes the reference's per-bond log bondocc.txt (bondc.f:194-594; byte-
+! identical with dot_order = 1, whose conductance line is the reference
+! solver's bitwise).  condtype 2 gives the
 ! spanning cluster's bonds -g0*rand('twister', cseed) (MATLAB/ConductCalc.m
 ! condtype 2; 1, the default, fixed g0).  nslab > 1 splits the solve into row
 ! slabs over nslab contexts (devices device .. device+nslab-1 with xport 0,
@@ -13,8 +16,7 @@
 ! linbcg's sums in the reference's order (bitwise its solve).  Outputs as
 ! the reference: bondorder.txt (i10,",",i10) in
 ! shuffled order (bondc.f:177-180), bond.txt (b1, b2, label, j, c(j);
-! bondc.f:600-604) and the run summary on stdout.  The per-bond trace
-! bondocc.txt is not written (SURVEY.md §8(b): optional).
+! bondc.f:600-604) and the run summary on stdout.
 program bondc
   use perc_api
   implicit none
@@ -22,9 +24,13 @@ program bondc
 #define PERC_LATTICE 0
 #endif
   integer(c_int) :: lattice, m, n, pbc, seed, itmax, device, nslab, xport, dot_order, condtype, cseed
+  integer(c_int) :: trace
   double precision :: pb, Va, g0, tol
   namelist /bondc_nml/ lattice, m, n, pbc, pb, seed, Va, g0, tol, itmax, device, nslab, xport, &
-                       dot_order, condtype, cseed
+                       dot_order, condtype, cseed, trace
+  integer(c_int), allocatable, target :: rec(:)
+  integer :: botfill, topfill, k
+  real :: fb
   integer(c_int) :: nb, tbonds, i, j, id, rc, stats(4), perccln, perccls, s, dev
   integer(c_int), allocatable, target :: b1(:), b2(:), order(:), label(:), csize(:)
   type(c_ptr) :: h
@@ -55,6 +61,7 @@ program bondc
   dot_order = PERC_DOT_FAST
   condtype = 1
   cseed = 1838534
+  trace = 0
   if (perc_have_file('bondc.nml')) then
     open(newunit=u, file='bondc.nml', status='old')
     read(u, nml=bondc_nml)
@@ -88,6 +95,65 @@ program bondc
   perccln = stats(4)
   perccls = 0
   if (perccln > 0) perccls = csize(perccln + 1)
+  if (trace /= 0) then
+    ! bondocc.txt as the reference writes it (bondc.f:194-462): the per-bond
+    ! steps from the host replay, then the spanning test over the clusters
+    ! of at least n-1 bonds in label order
+    allocate(rec(3 * max(tbonds, 1)))
+    call perc_check(perc_replay_bond_trace(lattice, m, n, pbc, tbonds, c_loc(order), c_loc(rec)), &
+                    'perc_replay_bond_trace')
+    open(unit=11, file='bondocc.txt')
+    do i = 1, tbonds
+      id = order(i)
+      if (id > 0) then
+        write(11, *) "bond chosen:", b1(id), b2(id)
+      else
+        write(11, *) "bond chosen:", 0, 0
+      end if
+      if (rec(3 * i - 2) == 0) then
+        write(11, *) "*no n.n. occupied*"
+        write(11, *) "bond assigned to cluster number", rec(3 * i - 1)
+      else
+        write(11, *) "*one or more n.n. occupied*"
+        write(11, *) "bond assigned to cluster number", rec(3 * i - 1)
+        write(11, *) "size of cluster number", rec(3 * i - 1), " is now", rec(3 * i)
+      end if
+      fb = real(i) / real(nb)
+      write(11, *) "fraction of lattice filled:", fb
+      write(11, *) "--------------------"
+    end do
+    write(11, *)
+    write(11, *) "******************************"
+    write(11, *) "largest overall cluster number:", stats(2)
+    write(11, *) "largest overall cluster size:", stats(3)
+    s = 0
+    do i = 1, stats(1) - 1
+      if (csize(i + 1) >= n - 1) then
+        write(11, *) "testing cluster:", i
+        botfill = 0
+        topfill = 0
+        do k = 1, nb
+          if (b1(k) <= m .and. label(k) == i) botfill = 1
+          if (b2(k) > m * n - m .and. label(k) == i) topfill = 1
+        end do
+        if (botfill == 0) then
+          write(11, *) "source end not connected"
+          cycle
+        end if
+        if (topfill == 0) then
+          write(11, *) "drain end not connected"
+          cycle
+        end if
+        write(11, *) "infinite cluster present"
+        write(11, *) "infinite cluster number:", i
+        write(11, *) "infinite cluster size:", csize(i + 1)
+        s = 1
+        exit
+      end if
+    end do
+    if (s == 0) write(11, *) "no infinite cluster present"
+    write(11, *) "******************************"
+  end if
 
   write(6, *)
   write(6, *) "******************************"
@@ -104,6 +170,7 @@ program bondc
 
   if (perccln > 0) then
     write(6, *) "Calculating internal node voltages"
+    if (trace /= 0) write(11, *) "Calculating internal node voltages"
     if (dot_order /= PERC_DOT_FAST) call perc_check(perc_set_dot_order(h, dot_order), 'perc_set_dot_order')
     if (condtype == 2) call perc_check(perc_set_conductcalc_weights(h, PERC_RULE_BOND, cseed), &
                                        'perc_set_conductcalc_weights')
@@ -135,7 +202,13 @@ program bondc
     write(6, *) "--------------------"
     write(6, *) "Conductance:", res%gtop, res%gbot
     write(6, *) "linbcg iterations:", res%iter, " err:", res%err
+    if (trace /= 0) then
+      write(11, *) "Calculating currents"
+      write(11, *) "--------------------"
+      write(11, *) "Conductance:", res%gtop, res%gbot
+    end if
   end if
+  if (trace /= 0) close(11)
 
   open(unit=10, file='bond.txt')
   do j = 1, nb

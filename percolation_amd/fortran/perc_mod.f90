@@ -91,6 +91,14 @@ module perc_api
       integer(c_int) :: stats(4)
     end function perc_replay_labels
 
+    ! bondc.f's per-bond trace records (bondocc.txt): 3 per order entry
+    integer(c_int) function perc_replay_bond_trace(lattice, m, n, pbc, nbond, bond_order, trace) &
+        bind(C, name='perc_replay_bond_trace')
+      import :: c_int, c_ptr
+      integer(c_int), value :: lattice, m, n, pbc, nbond
+      type(c_ptr), value :: bond_order, trace
+    end function perc_replay_bond_trace
+
     integer(c_int) function perc_nbonds(lattice, m, n, pbc) bind(C, name='perc_nbonds')
       import :: c_int
       integer(c_int), value :: lattice, m, n, pbc

@@ -216,3 +216,18 @@ def test_bondc_driver_random_conductances(tmp_path):
     assert abs(got[2][0] - c["gtop"]) <= 1e-12 * abs(c["gtop"]), (got[2], c)
     assert abs(got[2][1] - c["gbot"]) <= 1e-12 * abs(c["gbot"]), (got[2], c)
     assert abs(got[2][0] - got[1][0]) > 1e-3 * abs(got[1][0])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("v", ["sq_bondc_p50", "sq_bondc_p60", "sq_bondc_20x30_p55", "sq_bondc_p60_pbc",
+                               "tri_bondc_p35", "tri_bondc_p40_pbc"])
+def test_bondc_driver_trace_log(v, tmp_path):
+    """trace = 1 (with dot_order = 1, whose conductance line is the
+    reference solver's bitwise): bondocc.txt -- every bond's step, the
+    spanning test and the conductance, bondc.f:194-594 -- is the reference
+    run's byte for byte (md5 of the reference's own file, tests/golden/*/
+    meta.json)"""
+    import hashlib
+    md, r = run_variant(v, tmp_path, extra=["dot_order=1", "trace=1"])
+    got = hashlib.md5((tmp_path / "bondocc.txt").read_bytes()).hexdigest()
+    assert got == md["files"]["bondocc.txt"], v
