@@ -934,6 +934,12 @@ def main():
         print(json.dumps(out), flush=True)
     if use_dist:
         dist.destroy_process_group()
+        # torch's bundled RCCL and the one libperc links are separate copies in
+        # this process; skip the interpreter's teardown (its library
+        # destructors) once the result line is out
+        sys.stdout.flush()
+        sys.stderr.flush()
+        os._exit(0)
 
 
 if __name__ == "__main__":
