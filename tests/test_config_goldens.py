@@ -98,6 +98,14 @@ def assoc_spread(doc, tkey, g):
                 if tkey in doc.get(k, {})), default=0.0)
 
 
+def iter_range(doc, tkey):
+    """iteration counts of the literal oracle and its re-associated runs at
+    tolerance tkey: (min, max)"""
+    its = [doc["solves"][tkey]["iter"]] + [doc[k][tkey]["iter"] for k in ASSOC_KEYS
+                                            if tkey in doc.get(k, {})]
+    return min(its), max(its)
+
+
 def converged_bar(doc, conv, g):
     """FLAT; or ASSOC_X x the reference solver's own association spread at
     the converged tolerance where that exceeds ASSOC_FLOOR (module
@@ -120,6 +128,20 @@ def test_association_spread_is_gtop_resolution_noise():
             if deep in doc.get(k, {}):
                 assert rel(doc[k][deep]["gtop"], doc["solves"][deep]["gtop"]) < 4 * res, (f, k)
                 assert rel(doc[k][deep]["gbot"], doc["solves"][deep]["gbot"]) < 1e-12, (f, k)
+
+
+def test_iteration_ranges_at_the_converged_decade():
+    """CPU: the BASELINE config fixtures hold re-associated runs at their
+    converged decade, so the GPU's iteration count there is checked against a
+    range the reference solver itself spans (the bench realisation's fixture,
+    one L = 4096 solve of hours, holds the literal run only)"""
+    for f in FIXTURES:
+        doc = json.load(open(f))
+        conv = converged_tol(doc["solves"])
+        if not os.path.basename(f).startswith("bench_"):
+            assert any(conv in doc.get(k, {}) for k in ASSOC_KEYS), f
+        lo, hi = iter_range(doc, conv)
+        assert lo <= doc["solves"][conv]["iter"] <= hi
 
 
 def test_bars_are_the_reference_spread():
@@ -227,6 +249,12 @@ def test_config_fixture(path):
         d = report[key]
         for g in ("gtop", "gbot"):
             assert d[g + "_rel"] < converged_bar(doc, conv, g), (g, converged_bar(doc, conv, g), d)
+        # past ~1e-15 the stop decision rides on the rounding history: the
+        # iteration count must lie in the range the reference solver's own
+        # associations span at that decade (literal, reversed, tree sums), 2 % slack
+        if any(conv in doc.get(k, {}) for k in ASSOC_KEYS):
+            lo, hi = iter_range(doc, conv)
+            assert 0.98 * lo <= d["iter"] <= 1.02 * hi, (d, lo, hi)
     for tkey in runs:
         if tkey == conv:
             continue
