@@ -253,11 +253,51 @@ __global__ __launch_bounds__(kCcThreads) void k_cc_tile(Geom g, int kind, const 
 // its union), the run node written as the provisional parent; a last pass
 // writes every site's root.  Square lattice, no pbc; kind as cc_link (bond:
 // member = any incident occupied bond; site / mixed: the occupied site).
-template <int H>
+// LDS union-find over tile nodes: 32-bit entries, or 16-bit ones (P16: half
+// the LDS, so twice the waves per CU; the root CAS is a 32-bit CAS on the
+// entry's word that leaves the other half as it finds it)
+template <bool P16>
+struct TileUF {
+  int* w;  // P16: kCcW * H / 2 words holding two entries each
+  __device__ int get(int x) const {
+    if (P16) return reinterpret_cast<const volatile unsigned short*>(w)[x];
+    return reinterpret_cast<const volatile int*>(w)[x];
+  }
+  __device__ void set(int x, int v) const {
+    if (P16) reinterpret_cast<volatile unsigned short*>(w)[x] = (unsigned short)v;
+    else reinterpret_cast<volatile int*>(w)[x] = v;
+  }
+  // set x's parent to b if it is still a; returns what it found (a: done)
+  __device__ int cas(int a, int b) const {
+    if (!P16) return atomicCAS(&w[a], a, b);
+    unsigned* word = reinterpret_cast<unsigned*>(w) + (a >> 1);
+    const int sh = (a & 1) * 16;
+    while (true) {
+      const unsigned old = *reinterpret_cast<volatile unsigned*>(word);
+      const int cur = (int)((old >> sh) & 0xffffu);
+      if (cur != a) return cur;
+      const unsigned nw = (old & ~(0xffffu << sh)) | ((unsigned)b << sh);
+      if (atomicCAS(word, old, nw) == old) return a;
+    }
+  }
+  __device__ int find(int x) const {  // path halving
+    int p = get(x);
+    while (p != x) {
+      const int gp = get(p);
+      if (gp != p) set(x, gp);
+      x = gp;
+      p = get(x);
+    }
+    return x;
+  }
+};
+
+template <int H, bool P16 = false>
 __global__ __launch_bounds__(64) void k_cc_tile_w(Geom g, int kind, const int* bond_first, const uint8_t* bocc,
                                                   const uint8_t* socc, int* parent, uint8_t* member,
                                                   int bf_closed) {
-  __shared__ int uf[kCcW * H];
+  __shared__ int uf_mem[P16 ? kCcW * H / 2 : kCcW * H];
+  const TileUF<P16> uf{uf_mem};
   const int ntx = cdiv(g.m, kCcW);
   const int tb = xcd_logical_block(blockIdx.x, gridDim.x);
   const int tx = tb % ntx, ty = tb / ntx;
@@ -306,8 +346,8 @@ __global__ __launch_bounds__(64) void k_cc_tile_w(Geom g, int kind, const int* b
     node[0] = r * kCcW + 63 - __clzll((long long)(lo & le));
     const unsigned long long hm = hi & le;
     node[1] = r * kCcW + (hm ? 64 + 63 - __clzll((long long)hm) : 63 - __clzll((long long)lo));
-    if (v0 && !left0) uf[node[0]] = node[0];
-    if (v1 && !left1) uf[node[1]] = node[1];
+    if (v0 && !left0) uf.set(node[0], node[0]);
+    if (v1 && !left1) uf.set(node[1], node[1]);
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -326,11 +366,11 @@ __global__ __launch_bounds__(64) void k_cc_tile_w(Geom g, int kind, const int* b
       if (!w) continue;
       int a = h ? a1 : a0, b = h ? b1 : b0;
       while (true) {
-        a = find_root(uf, a);
-        b = find_root(uf, b);
+        a = uf.find(a);
+        b = uf.find(b);
         if (a == b) break;
         if (a < b) { const int t = a; a = b; b = t; }
-        const int old = atomicCAS(&uf[a], a, b);
+        const int old = uf.cas(a, b);
         if (old == a) break;
         a = old;
       }
@@ -364,10 +404,10 @@ __global__ __launch_bounds__(64) void k_cc_tile_w(Geom g, int kind, const int* b
       const int lc = lane + 64 * h;
       if (lc >= tw) continue;
       const int s = (r0 + r) * g.m + c0 + lc + 1;
-      int x = parent[s], p = uf[x];
+      int x = parent[s], p = uf.get(x);
       while (p != x) {
         x = p;
-        p = uf[x];
+        p = uf.get(x);
       }
       parent[s] = (r0 + x / kCcW) * g.m + c0 + x % kCcW + 1;
     }

@@ -178,6 +178,12 @@ int main(int argc, char** argv) {
   chain("tile_w<16>", [&]() { k_cc_tile_w<16><<<cdiv(g.m, kCcW) * cdiv(g.n, 16), 64>>>(g, PERC_BOND, R.bf, R.bocc, R.socc,
                                                                                        R.parent, R.member, 1); },
         merge_for(std::integral_constant<int, 16>{}), false);
+  chain("tile_w<32, u16>", [&]() { k_cc_tile_w<32, true><<<cdiv(g.m, kCcW) * cdiv(g.n, 32), 64>>>(
+                                      g, PERC_BOND, R.bf, R.bocc, R.socc, R.parent, R.member, 1); },
+        merge_for(std::integral_constant<int, 32>{}), false);
+  chain("tile_w<16, u16>", [&]() { k_cc_tile_w<16, true><<<cdiv(g.m, kCcW) * cdiv(g.n, 16), 64>>>(
+                                      g, PERC_BOND, R.bf, R.bocc, R.socc, R.parent, R.member, 1); },
+        merge_for(std::integral_constant<int, 16>{}), false);
   chain("tile_w<64>", [&]() { k_cc_tile_w<64><<<cdiv(g.m, kCcW) * cdiv(g.n, 64), 64>>>(g, PERC_BOND, R.bf, R.bocc, R.socc,
                                                                                        R.parent, R.member, 1); },
         merge_for(std::integral_constant<int, 64>{}), false);
