@@ -42,6 +42,7 @@ __device__ __forceinline__ int wave_sum_int(int v) {
 #endif
 constexpr int kCcW = 128, kCcH = PERC_CC_H, kCcSites = kCcW * kCcH, kCcThreads = 256;
 constexpr int kReduceGrid = 1024;  // fixed grid of the counting passes
+constexpr int kCcWaveH = 16;       // block height of k_cc_tile_w (the square lattice without pbc)
 
 
 __device__ __forceinline__ int find_root(int* parent, int x) {

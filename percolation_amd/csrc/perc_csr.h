@@ -238,33 +238,49 @@ __device__ __forceinline__ void block_tiles(int N, int* t0, int* t1) {
   *t1 = min(*t0 + chunk, ntile);
 }
 
+// The plain SpMV (dsprsax, the NR drop-in and the probes): one row per
+// thread -- the row pointers, the row's <= NS (col, val) entries loaded
+// unconditionally (clamped to the row's last entry), all gathers in flight
+// together, then d(i) x(i) + the products in ascending column order (bitwise
+// dsprsax); NS = 0: rows of any length, a loop.  Against the wave tiles
+// above (LDS-staged, pipelined): 0.239 vs 0.278 ms at L = 4096, 5.33 TB/s
+// on §8(d)'s 1.27 GB (profiles/r4_5_spmv_bench_L4096.txt; grid-stride
+// variants 0.262-0.275 ms).
 template <int NS>
 __global__ __launch_bounds__(kBlock) void k_spmv(CsrView A, const double* __restrict__ x,
                                                  double* __restrict__ y) {
-  __shared__ double s_prod[kWaves][64 * kMaxNnzRow];
-  const int wid = threadIdx.x >> 6;
-  int t0, t1;
-  block_tiles(A.N, &t0, &t1);
-  double dummy = 0.0;
-  spmv_tiles_any<false, NS>(A, x, y, t0 + wid, t1, kWaves, s_prod[wid], &dummy);
+  const int i = blockIdx.x * kBlock + threadIdx.x;
+  if (i >= A.N) return;
+  const int a = A.rowptr[i], b = A.rowptr[i + 1];
+  double acc;
+  if constexpr (NS > 0) {
+    int c[NS];
+    double v[NS], xv[NS];
+    const int last = b - 1 < a ? a : b - 1;
+#pragma unroll
+    for (int j = 0; j < NS; ++j) {
+      const int k = min(a + j, last);
+      c[j] = A.col[k];
+      v[j] = A.val[k];
+    }
+    const double xi = x[i], di = A.diag[i];
+#pragma unroll
+    for (int j = 0; j < NS; ++j) xv[j] = x[c[j]];
+    acc = di * xi;
+#pragma unroll
+    for (int j = 0; j < NS; ++j) acc = j < b - a ? acc + v[j] * xv[j] : acc;
+  } else {
+    acc = A.diag[i] * x[i];
+    for (int k = a; k < b; ++k) acc = acc + A.val[k] * x[A.col[k]];
+  }
+  y[i] = acc;
 }
 
-// y = A x on a stream: k_spmv at the rows' slot count, one resident round
-// of workgroups (no reduction, so the grid is free; each wave then walks
-// ~50 tiles at L = 4096 and the pipeline's fill and drain are amortised)
+// y = A x on a stream: k_spmv at the rows' slot count, one row per thread
 inline void spmv_launch(perc_ctx* h, const CsrView& A, const double* x, double* y, hipStream_t st) {
-  const int ns = csr_slots(A.maxrow);
-  const void* k = ns == 4 ? (const void*)k_spmv<4> : ns == kMaxNnzRow ? (const void*)k_spmv<kMaxNnzRow>
-                                                                       : (const void*)k_spmv<0>;
-  if (h->spmv_ns != ns || h->spmv_n != A.N) {  // (once per system)
-    int cus = 0, per_cu = 0;
-    hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, h->device);
-    hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, kBlock, 0);
-    h->spmv_grid = std::max(1, std::min(std::max(cus, 1) * std::max(per_cu, 1), cdiv(cdiv(A.N, 64), kWaves)));
-    h->spmv_ns = ns;
-    h->spmv_n = A.N;
-  }
-  const int grid = h->spmv_grid;
+  (void)h;
+  const int ns = csr_slots(A.maxrow), grid = cdiv(A.N, kBlock);
+  if (A.N <= 0) return;
   if (ns == 4) k_spmv<4><<<grid, kBlock, 0, st>>>(A, x, y);
   else if (ns == kMaxNnzRow) k_spmv<kMaxNnzRow><<<grid, kBlock, 0, st>>>(A, x, y);
   else k_spmv<0><<<grid, kBlock, 0, st>>>(A, x, y);

@@ -157,7 +157,6 @@ struct perc_ctx {
   long long nnz = 0;
   int csr_maxrow = 6;  // most off-diagonals in one CSR row (lattices: <= 6; NR matrices: measured)
   int grid = 0;    // fixed grid of the CG kernels (reduction order depends on it)
-  int spmv_grid = 0, spmv_ns = -1, spmv_n = -1;  // plain CSR SpMV: one resident round (spmv_launch)
   perc::DeviceBuffers d;
   std::vector<int> h_bond_first;  // host copy, t+2
   perc::ReplayOrder last;          // last occupancy (for the host replay)

@@ -419,12 +419,28 @@ hipError_t dev_occupy_random(perc_ctx* h, int kind, int nsites, int nbonds,
   return hipSuccess;
 }
 
+static hipError_t label_finish(perc_ctx* h, int* nspan, int* span_list, int* nclusters);
+
 hipError_t dev_label(perc_ctx* h, int* nspan, int* span_list, int* nclusters) {
   const Geom& g = h->g;
   hipStream_t st = h->stream;
   DeviceBuffers& d = h->d;
   const int kind = h->last.kind;
   HIP_TRY(hipMemsetAsync(d.counters, 0, sizeof(int) * (8 + kMaxSpanList), st));
+  // square lattice without wrap links: one wave per 128 x 16 block walking
+  // its rows (k_cc_tile_w; labels 0.318 vs 0.361 ms of kernels at L = 4096,
+  // profiles/r4_5_cc_bench_L4096.txt); else the LDS union-find blocks
+  if (g.lattice == kSquare && !g.pbc && !std::getenv("PERC_TILE_TRACE")) {
+    constexpr int H = kCcWaveH;
+    k_cc_tile_w<H><<<cdiv(g.m, kCcW) * cdiv(g.n, H), 64, 0, st>>>(g, kind, d.bond_first, d.bocc, d.socc,
+                                                                   d.parent, d.member, (int)h->bf_closed);
+    HIP_TRY(dbg_sync(st, "k_cc_tile_w"));
+    const int nseg = cdiv(g.m, kCcThreads), nfull = g.n / H, ncand = 2 * cdiv(g.m, kCcW) + 1;
+    k_cc_merge<H><<<nfull * nseg + ncand * cdiv(g.n, kCcThreads), kCcThreads, 0, st>>>(
+        g, kind, d.bond_first, d.bocc, d.socc, d.parent, d.member, nseg, nfull);
+    HIP_TRY(dbg_sync(st, "k_cc_merge"));
+    return label_finish(h, nspan, span_list, nclusters);
+  }
   const int tiles = cdiv(g.m, kCcW) * cdiv(g.n, kCcH);
   unsigned long long* ttr = nullptr;  // PERC_TILE_TRACE: per-workgroup phase stamps
   static const bool ttrace = std::getenv("PERC_TILE_TRACE") != nullptr;
@@ -453,6 +469,14 @@ hipError_t dev_label(perc_ctx* h, int* nspan, int* span_list, int* nclusters) {
   k_cc_merge<kCcH><<<nfull * nseg + ncand * cdiv(g.n, kCcThreads), kCcThreads, 0, st>>>(
       g, kind, d.bond_first, d.bocc, d.socc, d.parent, d.member, nseg, nfull);
   HIP_TRY(dbg_sync(st, "k_cc_merge"));
+  return label_finish(h, nspan, span_list, nclusters);
+}
+
+// every parent to its root, cluster count, spanning roots, read-back
+static hipError_t label_finish(perc_ctx* h, int* nspan, int* span_list, int* nclusters) {
+  const Geom& g = h->g;
+  hipStream_t st = h->stream;
+  DeviceBuffers& d = h->d;
   k_cc_compress<<<std::min(cdiv(g.t, kCcThreads), kReduceGrid), kCcThreads, 0, st>>>(
       g.t, d.parent, d.member, d.counters + 1);
   HIP_TRY(dbg_sync(st, "k_cc_compress"));

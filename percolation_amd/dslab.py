@@ -104,6 +104,11 @@ def conductance(ctx, rule=L.RULE_BOND, cur_rule=L.CUR_FORTRAN, Va=1.0, g0=1.0, l
     bufs = L.DslabBufs(ptr(part_out), ptr(part_all), ptr(edges[0]), ptr(edges[1]),
                        ptr(ghosts[0]), ptr(ghosts[1]))
     ex = _Exchange(group, K, s, part_out, part_all, edges, ghosts)
+    # every tensor the loop touches is allocated here, on the current stream:
+    # a block the caching allocator assigned to the context's stream would
+    # outlive that stream (perc_ctx_destroy) in the allocator's pools
+    row = z(m) if K > 1 and s in (0, K - 1) else None
+    out_dev = z(4)
     stream = torch.cuda.ExternalStream(lib.perc_stream(ctx.h), device=dev)
     step = lambda op: L.check(lib.perc_dslab_step(ctx.h, op), "perc_dslab_step")  # noqa: E731
     it, err, done = C.c_int(), C.c_double(), C.c_int()
@@ -135,7 +140,6 @@ def conductance(ctx, rule=L.RULE_BOND, cur_rule=L.CUR_FORTRAN, Va=1.0, g0=1.0, l
         # the bottom one: the currents there
         out = torch.zeros(4, dtype=torch.float64)
         if K > 1 and s in (0, K - 1):
-            row = z(m)
             if s == K - 1:
                 L.check(lib.perc_x_row(ctx.h, nrows - 1, row.data_ptr(), 0), "perc_x_row")
                 dist.send(row if ex.nccl else row.cpu(), ex.ranks[0], group=group)
@@ -151,9 +155,13 @@ def conductance(ctx, rule=L.RULE_BOND, cur_rule=L.CUR_FORTRAN, Va=1.0, g0=1.0, l
                     "perc_currents")
             out[:] = torch.tensor([res.gtop, res.gbot, err.value, float(it.value)],
                                   dtype=torch.float64)
-        o = out.to(dev) if ex.nccl else out
-        dist.broadcast(o, ex.ranks[0], group=group)
-        out = o.cpu()
+        if ex.nccl:
+            out_dev.copy_(out)
+            dist.broadcast(out_dev, ex.ranks[0], group=group)
+            out = out_dev.cpu()
+        else:
+            dist.broadcast(out, ex.ranks[0], group=group)
+        torch.cuda.current_stream().synchronize()
     return dict(gtop=float(out[0]), gbot=float(out[1]), err=float(out[2]), iter=int(out[3]),
                 status=0)
 

@@ -171,7 +171,7 @@ int main(int argc, char** argv) {
   auto prod = [&]() { spmv_launch(&h, A, dx, dy, 0); };
   const double tp = time_ms(prod, reps);
   std::printf("L = %d: N = %d rows, nnz = %lld, %.1f MB per launch\n", L, N, nnz, bytes / 1e6);
-  std::printf("  production k_spmv<4> (grid %d): %.4f ms = %.1f GB/s\n", h.spmv_grid, tp, bytes / tp / 1e6);
+  std::printf("  production k_spmv<4> (one row per thread): %.4f ms = %.1f GB/s\n", tp, bytes / tp / 1e6);
   std::vector<double> y1(N), y2(N);
   CK(hipMemcpy(y1.data(), dy, (size_t)N * 8, hipMemcpyDeviceToHost));
   int cus = 0;
