@@ -30,7 +30,7 @@ program bondc
                        dot_order, condtype, cseed, trace
   integer(c_int), allocatable, target :: rec(:)
   integer :: botfill, topfill, k
-  real :: fb
+  double precision :: fb    ! bondc.f:52 (a double holding a single-precision quotient)
   integer(c_int) :: nb, tbonds, i, j, id, rc, stats(4), perccln, perccls, s, dev
   integer(c_int), allocatable, target :: b1(:), b2(:), order(:), label(:), csize(:)
   type(c_ptr) :: h
@@ -118,7 +118,7 @@ program bondc
         write(11, *) "bond assigned to cluster number", rec(3 * i - 1)
         write(11, *) "size of cluster number", rec(3 * i - 1), " is now", rec(3 * i)
       end if
-      fb = real(i) / real(nb)
+      fb = real(i) / real(nb)   ! bondc.f:371, single-precision division
       write(11, *) "fraction of lattice filled:", fb
       write(11, *) "--------------------"
     end do
