@@ -28,7 +28,7 @@ namespace {
 // buffer's size makes a load return 0 and drops a store.  The row-march
 // keeps every memory instruction of a step unconditional this way (rows
 // outside the lattice or the band, halo columns of non-halo threads, q of
-// the steps without a finished row, x off the electrode rows), so hipcc's
+// the steps without a finished row), so hipcc's
 // s_waitcnt bookkeeping stays exact across the loop: with loads and stores
 // under branches it waited for vmcnt(0) -- every prefetched row and every
 // store in flight -- once per step.
@@ -268,7 +268,7 @@ struct MGeom {
 // TCC_EA0_RDREQ_LEVEL, profiles/r2_3_*); unconditional, the waits count
 // exactly and the prefetch ring keeps its rows in flight.
 struct MBuf {
-  __amdgpu_buffer_rsrc_t p, r, c, pn, q, x;  // p(k-1), r, codes, p(k): rows [lo, hi); q, x: own rows
+  __amdgpu_buffer_rsrc_t p, r, c, pn, q;  // p(k-1), r, codes, p(k): rows [lo, hi); q: own rows
   int lo, hi;
 };
 
@@ -288,7 +288,6 @@ __device__ __forceinline__ MBuf march_bufs(const CGArgs& a, const MGeom& g, cons
     B.c = PK ? rsrc(a.nib, nall / 2u) : rsrc(a.St.code, nall * 2u);
     B.pn = rsrc(pnew, nall * 8u);
     B.q = rsrc(a.q, MODE == kMarchPQ ? nall * 8u : 0u);
-    B.x = rsrc(a.x, 0u);  // the strip-major solve keeps x in B
     return B;
   }
   const long long base = (long long)B.lo * m;
@@ -299,7 +298,6 @@ __device__ __forceinline__ MBuf march_bufs(const CGArgs& a, const MGeom& g, cons
   B.c = rsrc(a.St.code + base, n * 2u);
   B.pn = rsrc(pnew + base, n * 8u);
   B.q = rsrc(MODE == kMarchPQ ? a.q + (long long)g.r0 * m : a.r, MODE == kMarchPQ ? nown * 8u : 0u);
-  B.x = rsrc(MODE == kMarchP ? a.x + (long long)g.r0 * m : a.r, MODE == kMarchP ? nown * 8u : 0u);
   return B;
 }
 
@@ -366,7 +364,7 @@ __device__ __forceinline__ void march_step(const CGArgs& a, const MGeom& g, cons
                                            const unsigned* s_rpos, const unsigned* s_rmap,
                                            double* s_w, MState& W, double (&acc)[2]) {
   const int lane = threadIdx.x & 63;
-  const int nrows = a.T.nrows, N = a.St.N;
+  const int nrows = a.T.nrows;
   const double ng0 = a.St.ng0, nleak = a.St.nleak;
   double2 pn = make_double2(0.0, 0.0);
   double hpn = 0.0;
@@ -392,25 +390,13 @@ __device__ __forceinline__ void march_step(const CGArgs& a, const MGeom& g, cons
       }
     }
   }
-  {
-    if (MODE != kMarchB) {
-      const int m = a.T.m;
-      // own row; in a slab also the ghost rows, so the next iteration's
-      // halo p(k) is at hand (bitwise the neighbour slab's own value)
-      const bool own = gr >= g.r0 && gr < g.rend;
-      const bool pst = (unsigned)(gr - B.lo) < (unsigned)(B.hi - B.lo) &&
-                       (own || (a.slab && (gr < 0 || gr >= nrows)));
-      bst2<kStAux>(B.pn, pst ? melem<SM>(a, B, gr, g.col) * 8u : kOOB, pn);
-      if (MODE == kMarchP && !SM) {  // x += ak p(k-1) on the x rows (the P-only march keeps x)
-        const int i = gr * m + g.col;
-        const bool xw = own && !first && !a.bx && (a.xrows == 0 || i < a.xrows || i >= N - a.xrows);
-        const unsigned ox = xw ? (unsigned)((gr - g.r0) * m + g.col) * 8u : kOOB;
-        double2 xv = bld2(B.x, ox);
-        xv.x = xv.x + ak * R.p.x;
-        xv.y = xv.y + ak * R.p.y;
-        bst2<0>(B.x, ox, xv);
-      }
-    }
+  if (MODE != kMarchB) {
+    // own row; in a slab also the ghost rows, so the next iteration's
+    // halo p(k) is at hand (bitwise the neighbour slab's own value)
+    const bool own = gr >= g.r0 && gr < g.rend;
+    const bool pst = (unsigned)(gr - B.lo) < (unsigned)(B.hi - B.lo) &&
+                     (own || (a.slab && (gr < 0 || gr >= nrows)));
+    bst2<kStAux>(B.pn, pst ? melem<SM>(a, B, gr, g.col) * 8u : kOOB, pn);
   }
   MWin Nw;
   Nw.e0 = pn.x;
@@ -622,6 +608,22 @@ __global__ __launch_bounds__(64 * kMarchWaves) void k_cg_march(CGArgs a) {
     double* s_w = s_win[threadIdx.x >> 6];
     if (up) march_walk<MODE, D, true, SM, PAUX, PK>(a, g, B, ring, first, bk, ak, psrc, pnew, s_dt, s_rpos, s_rmap, s_w, acc);
     else march_walk<MODE, D, false, SM, PAUX, PK>(a, g, B, ring, first, bk, ak, psrc, pnew, s_dt, s_rpos, s_rmap, s_w, acc);
+    if (MODE == kMarchP && !SM && !first && !a.bx) {
+      // row-major q-free solve: x += ak p(k-1) on the band's x rows, after
+      // the walk.  Inside it the x load feeding the x store made every step
+      // wait for vmcnt(0), draining the prefetched rows (L = 8192: 2 684
+      // read requests in flight vs B's 3 229, profiles/r4_5_*level*)
+      const int N = a.St.N;
+      for (int gr = g.r0; gr < g.rend; ++gr) {
+        const int i = gr * m + g.col;
+        if (a.xrows != 0 && i >= a.xrows && i < N - a.xrows) continue;
+        const double2 pv = *reinterpret_cast<const double2*>(psrc + i);
+        double2 xv = *reinterpret_cast<const double2*>(a.x + i);
+        xv.x = xv.x + ak * pv.x;
+        xv.y = xv.y + ak * pv.y;
+        *reinterpret_cast<double2*>(a.x + i) = xv;
+      }
+    }
     if (MODE == kMarchB && SM) {
       // strip-major q-free solve: x (row-major) += ak p(k) on the band's x
       // rows, after the walk (loads and stores inside it would put a

@@ -66,11 +66,17 @@ def main():
         from percolation_amd import dslab
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29533")
+        import faulthandler
+        faulthandler.enable()  # (an abort names the Python line it came from)
         dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
         c = ctx_new()
+        print("torch leg: context ready", file=sys.stderr, flush=True)
         ms = slope(lambda n: dslab.conductance(c, tol=0.0, itmax=n)["iter"])
+        print("torch leg: timed", file=sys.stderr, flush=True)
         c.close()
+        print("torch leg: context closed", file=sys.stderr, flush=True)
         dist.destroy_process_group()
+        print("torch leg: group destroyed", file=sys.stderr, flush=True)
         print(json.dumps({"python_dslab_nccl_ms_per_it": ms}), flush=True)
         return
     # every leg measured once per round, the legs interleaved round after
