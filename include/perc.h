@@ -118,6 +118,10 @@ typedef struct {
 int perc_occupy_random(perc_ctx *h, int kind, int nsites, int nbonds, unsigned long long seed);
 int perc_random_order(long long n, int count, unsigned long long seed, int kind, int *order_out);
 
+/* The occupancy in device memory, copied out (either output may be NULL):
+   site_occ[t] (site ids 1..t), bond_occ[nb] (bond ids 1..nb), 0 / 1 each. */
+int perc_occupancy(perc_ctx *h, unsigned char *site_occ, unsigned char *bond_occ);
+
 /* GPU connected components of the occupancy + spanning detection.  When
    more than one component spans, the reference's lowest-label rule is
    resolved by the host replay (hazard H4).  canon_out (optional, host,

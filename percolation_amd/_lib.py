@@ -131,6 +131,7 @@ SIGNATURES = {
     "perc_stream": (C.c_void_p, [_VP]),
     "perc_cluster_sizes": (C.c_int, [_VP, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
     "perc_occupy_random": (C.c_int, [_VP, C.c_int, C.c_int, C.c_int, C.c_ulonglong]),
+    "perc_occupancy": (C.c_int, [_VP, _VP, _VP]),
     "perc_random_order": (C.c_int, [C.c_longlong, C.c_int, C.c_ulonglong, C.c_int, _I]),
     "perc_set_march_mode": (C.c_int, [_VP, C.c_int]),
     "perc_set_band_weights": (C.c_int, [_VP, C.c_int, C.c_int, _VP]),

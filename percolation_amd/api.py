@@ -137,6 +137,14 @@ class Context:
         L.check(L.lib().perc_occupy_random(self.h, kind, int(nsites), int(nbonds_), int(seed)),
                 "perc_occupy_random")
 
+    def occupancy(self):
+        """perc_occupancy: (site_occ[t], bond_occ[nb]) uint8 arrays of the
+        device occupancy (site / bond ids 1.. at index 0..)."""
+        so = np.zeros(self.t, dtype=np.uint8)
+        bo = np.zeros(self.nb, dtype=np.uint8)
+        L.check(L.lib().perc_occupancy(self.h, so.ctypes.data, bo.ctypes.data), "perc_occupancy")
+        return so, bo
+
     def occupy_device(self, kind, site_ptr=None, nsites=0, bond_ptr=None, nbonds_=0):
         """perc_occupy_device: order lists already in device memory (int
         addresses of device int32 arrays on this context's device)."""

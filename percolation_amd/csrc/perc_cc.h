@@ -415,135 +415,6 @@ __global__ __launch_bounds__(64) void k_cc_tile_w(Geom g, int kind, const int* b
   }
 }
 
-// k_cc_tile_r: k_cc_tile_w with the block held in registers.  Every row's
-// links are loaded up front (all loads of the block in flight together,
-// packed into per-lane bit masks, bit r = row r), the walk keeps each row's
-// run nodes in registers, and every site's root and member flag are written
-// once at the end -- no provisional parent store and no global re-read of
-// it (k_cc_tile_w: one load latency per row in the walk and one per row in
-// the last pass).  Same unions in the same order: bitwise k_cc_tile_w's
-// parents and members.
-template <int H, bool P16 = false>
-__global__ __launch_bounds__(64) void k_cc_tile_r(Geom g, int kind, const int* bond_first, const uint8_t* bocc,
-                                                  const uint8_t* socc, int* parent, uint8_t* member,
-                                                  int bf_closed) {
-  static_assert(H <= 32, "a row per bit of one word");
-  __shared__ int uf_mem[P16 ? kCcW * H / 2 : kCcW * H];
-  const TileUF<P16> uf{uf_mem};
-  const int ntx = cdiv(g.m, kCcW);
-  const int tb = xcd_logical_block(blockIdx.x, gridDim.x);
-  const int tx = tb % ntx, ty = tb / ntx;
-  const int c0 = tx * kCcW, r0 = ty * H;
-  const int tw = min(kCcW, g.m - c0), th = min(H, g.n - r0);
-  const int lane = threadIdx.x;
-  // Rb / Ub: the link right / up of the lane's site in column lane + 64 h;
-  // Ob: the site occupied (site kinds)
-  unsigned Rb[2] = {0u, 0u}, Ub[2] = {0u, 0u}, Ob[2] = {0u, 0u};
-#pragma unroll
-  for (int r = 0; r < H; ++r) {
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int lc = lane + 64 * h, col = c0 + lc, row = r0 + r;
-      const bool v = lc < tw && r < th;
-      const int s = row * g.m + col + 1;
-      const bool hr = v && col < g.m - 1, hu = v && row < g.n - 1;
-      unsigned R, U, O;
-      if (kind == PERC_SITE) {
-        O = v ? socc[s] : 0u;
-        R = O && hr ? socc[s + 1] : 0u;
-        U = O && hu ? socc[s + g.m] : 0u;
-      } else {
-        const int fb = !v ? 0 : bf_closed && row <= g.n - 2 ? bf_square(g, row, col) : bond_first[s];
-        R = hr ? bocc[fb] : 0u;
-        U = hu ? bocc[fb + (col < g.m - 1 ? 1 : 0)] : 0u;
-        O = 1u;
-        if (kind != PERC_BOND) {  // mixed: the bond and both sites
-          O = v ? socc[s] : 0u;
-          R = R && O && socc[s + 1];
-          U = U && O && socc[s + g.m];
-        }
-      }
-      Rb[h] |= (R ? 1u : 0u) << r;
-      Ub[h] |= (U ? 1u : 0u) << r;
-      Ob[h] |= (O ? 1u : 0u) << r;
-    }
-  }
-  unsigned nodes[H];      // row r: run node of column lane | of column lane + 64 << 16
-  unsigned Mb[2] = {0u, 0u};
-  int labp[2] = {0, 0};
-  const unsigned long long le = lane == 63 ? ~0ull : ((2ull << lane) - 1ull);
-  const bool v0 = lane < tw, v1 = lane + 64 < tw;
-#pragma unroll
-  for (int r = 0; r < H; ++r) {
-    nodes[r] = 0u;
-    if (r >= th) continue;  // (uniform)
-    const unsigned R0 = Rb[0] >> r & 1u, R1 = Rb[1] >> r & 1u;
-    const unsigned rl0 = __shfl(R0, (lane + 63) & 63, 64), rl1 = __shfl(R1, (lane + 63) & 63, 64);
-    const bool left0 = lane > 0 && rl0, left1 = lane > 0 ? rl1 != 0u : rl0 != 0u;
-    const unsigned long long lo = __ballot(!left0 || !v0), hi = __ballot(!left1 || !v1);
-    int node[2];
-    node[0] = r * kCcW + 63 - __clzll((long long)(lo & le));
-    const unsigned long long hm = hi & le;
-    node[1] = r * kCcW + (hm ? 64 + 63 - __clzll((long long)hm) : 63 - __clzll((long long)lo));
-    if (v0 && !left0) uf.set(node[0], node[0]);
-    if (v1 && !left1) uf.set(node[1], node[1]);
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    const unsigned Up0 = r > 0 ? Ub[0] >> (r - 1) & 1u : 0u, Up1 = r > 0 ? Ub[1] >> (r - 1) & 1u : 0u;
-    const bool w0 = v0 && Up0, w1 = v1 && Up1;
-    const int a0 = w0 ? node[0] : -1, b0 = w0 ? labp[0] : -1, a1 = w1 ? node[1] : -1, b1 = w1 ? labp[1] : -1;
-    const int pa0 = __shfl(a0, (lane + 63) & 63, 64), pb0 = __shfl(b0, (lane + 63) & 63, 64);
-    const int pa1 = __shfl(a1, (lane + 63) & 63, 64), pb1 = __shfl(b1, (lane + 63) & 63, 64);
-    const bool sk0 = lane > 0 && pa0 == a0 && pb0 == b0;
-    const bool sk1 = lane > 0 ? (pa1 == a1 && pb1 == b1) : (pa0 == a1 && pb0 == b1);
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const bool w = h ? w1 && !sk1 : w0 && !sk0;
-      if (!w) continue;
-      int a = h ? a1 : a0, b = h ? b1 : b0;
-      while (true) {
-        a = uf.find(a);
-        b = uf.find(b);
-        if (a == b) break;
-        if (a < b) { const int t = a; a = b; b = t; }
-        const int old = uf.cas(a, b);
-        if (old == a) break;
-        a = old;
-      }
-    }
-    const unsigned U0 = Ub[0] >> r & 1u, U1 = Ub[1] >> r & 1u;
-    const bool m0 = kind == PERC_BOND ? (R0 | U0 | (left0 ? 1u : 0u) | Up0) != 0u : (Ob[0] >> r & 1u) != 0u;
-    const bool m1 = kind == PERC_BOND ? (R1 | U1 | (left1 ? 1u : 0u) | Up1) != 0u : (Ob[1] >> r & 1u) != 0u;
-    Mb[0] |= (m0 ? 1u : 0u) << r;
-    Mb[1] |= (m1 ? 1u : 0u) << r;
-    nodes[r] = (unsigned)node[0] | (unsigned)node[1] << 16;
-    labp[0] = node[0];
-    labp[1] = node[1];
-  }
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-#pragma unroll
-  for (int r = 0; r < H; ++r) {
-    if (r >= th) continue;
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int lc = lane + 64 * h;
-      if (lc >= tw) continue;
-      const int s = (r0 + r) * g.m + c0 + lc + 1;
-      int x = (int)(nodes[r] >> (16 * h) & 0xffffu), p = uf.get(x);
-      while (p != x) {
-        x = p;
-        p = uf.get(x);
-      }
-      parent[s] = (r0 + x / kCcW) * g.m + c0 + x % kCcW + 1;
-      member[s] = (uint8_t)(Mb[h] >> r & 1u);
-    }
-  }
-}
-
-
 // The links that cross a block edge, with neighbouring lanes on neighbouring
 // sites of the same edge: part A, the blocks' top rows (every column: the
 // links up into the next block row), one workgroup per kCcThreads columns;
@@ -612,46 +483,16 @@ __device__ __forceinline__ void block_count_add(int v, int* counter) {
   }
 }
 
-// final flattening: a read-only walk, then each thread writes only its own
-// entry (path halving here would let one thread overwrite another's freshly
-// written root with an intermediate ancestor); counts the clusters (member
-// roots)
-__global__ __launch_bounds__(kCcThreads) void k_cc_compress(int t, int* parent,
-                                                            const uint8_t* member,
+// final flattening: read-only walks, then each thread writes only its own
+// entries (path halving here would let one thread overwrite another's
+// freshly written root with an intermediate ancestor); counts the clusters
+// (member roots).  A thread's U sites are chased in lockstep: every hop
+// issues their U parent loads together (one chain after another: compress
+// 83.3 vs 55.3 us at L = 4096, profiles/r4_7_cc_bench_L4096.txt).
+constexpr int kCcCompressU = 8;
+template <int U = kCcCompressU>
+__global__ __launch_bounds__(kCcThreads) void k_cc_compress(int t, int* parent, const uint8_t* member,
                                                             int* nclusters) {
-  // four sites per thread and step, their first parent loads issued together
-  constexpr int kU = 4;
-  int cnt = 0;
-  for (long long b = (long long)blockIdx.x * kCcThreads * kU + threadIdx.x + 1; b <= t;
-       b += (long long)gridDim.x * kCcThreads * kU) {
-    int p0[kU];
-#pragma unroll
-    for (int k = 0; k < kU; ++k) {
-      const long long s = b + k * kCcThreads;
-      p0[k] = s <= t ? parent[s] : 0;
-    }
-#pragma unroll
-    for (int k = 0; k < kU; ++k) {
-      const long long s = b + k * kCcThreads;
-      if (s > t) continue;
-      int x = (int)s, p = p0[k];
-      while (p != x) {
-        x = p;
-        p = parent[x];
-      }
-      parent[s] = x;
-      cnt += x == s && member[s];
-    }
-  }
-  block_count_add(cnt, nclusters);
-}
-
-// k_cc_compress with the U chains of a thread chased in lockstep: every hop
-// issues the U parent loads together (k_cc_compress walks its U chains one
-// after another, one load latency per hop each).  Same roots, same writes.
-template <int U>
-__global__ __launch_bounds__(kCcThreads) void k_cc_compress_ls(int t, int* parent, const uint8_t* member,
-                                                               int* nclusters) {
   int cnt = 0;
   for (long long b = (long long)blockIdx.x * kCcThreads * U + threadIdx.x + 1; b <= t;
        b += (long long)gridDim.x * kCcThreads * U) {

@@ -406,6 +406,18 @@ int perc_system_size(perc_ctx* h, long long* out) {
   return PERC_OK;
 }
 
+int perc_occupancy(perc_ctx* h, uint8_t* site_occ, uint8_t* bond_occ) {
+  if (!h) return PERC_EINVAL;
+  if (!h->occupied) return PERC_ESTATE;
+  hipSetDevice(h->device);
+  hipStream_t st = h->stream;
+  hipError_t e = hipSuccess;
+  if (site_occ) e = hipMemcpyAsync(site_occ, h->d.socc + 1, (size_t)h->g.t, hipMemcpyDeviceToHost, st);
+  if (e == hipSuccess && bond_occ) e = hipMemcpyAsync(bond_occ, h->d.bocc, (size_t)h->nb, hipMemcpyDeviceToHost, st);
+  if (e == hipSuccess) e = hipStreamSynchronize(st);
+  return e == hipSuccess ? PERC_OK : hip_status(e, "perc_occupancy");
+}
+
 int perc_label(perc_ctx* h, perc_label_info* info, int* canon_out) {
   if (!h) return PERC_EINVAL;
   if (!h->occupied) return PERC_ESTATE;

@@ -33,7 +33,8 @@ __global__ __launch_bounds__(kBlock) void k_select_window(long long n, unsigned 
                                                           unsigned long long lo,
                                                           unsigned long long hi,
                                                           unsigned* cnt,
-                                                          unsigned long long* cand) {
+                                                          unsigned long long* cand, int base,
+                                                          uint8_t* occ) {
   __shared__ unsigned long long s_c[kSelStage];
   __shared__ unsigned s_n, s_base, s_b[kBlock / 64];
   if (threadIdx.x == 0) s_n = 0;
@@ -45,6 +46,9 @@ __global__ __launch_bounds__(kBlock) void k_select_window(long long n, unsigned 
     const unsigned long long key = perc_rand_key(seed, (unsigned)(i + 1));
     const unsigned long long hsh = key >> 32;
     below += hsh < lo;
+    // every key below the window is occupied, every key above it is not;
+    // the window's keys (0 here) are decided by k_occupy_cand once T is known
+    occ[i + base] = hsh < lo ? 1 : 0;
     if (hsh >= lo && hsh < hi) {
       const unsigned slot = atomicAdd(&s_n, 1u);
       if (slot < (unsigned)kSelStage) {
@@ -75,7 +79,7 @@ __global__ __launch_bounds__(kSelThreads) void k_select_final(long long n,
                                                               long long count,
                                                               unsigned long long lo,
                                                               unsigned long long hi,
-                                                              const unsigned* cnt,
+                                                              unsigned* cnt,
                                                               unsigned long long* cand) {
   __shared__ unsigned s_h[kSelBins];
   __shared__ unsigned long long s_k[kSelBinCap];
@@ -85,6 +89,10 @@ __global__ __launch_bounds__(kSelThreads) void k_select_final(long long n,
   if (threadIdx.x == 0) tr[0] = wall_clock64();
   const long long below = cnt[0], nin = cnt[1];
   const bool win = count > below && count - below <= nin && nin <= kSelCap;
+  // T inside the window and every window key gathered: k_select_window's
+  // occupation stands and k_occupy_cand completes it; else k_occupy_rand
+  // rewrites the whole occupation from T
+  if (threadIdx.x == 0) cnt[2] = win ? 1u : 0u;
   if (win) {
     // bins of the window's hash range: (hash - lo) >> sh < kSelBins
     const unsigned long long range = hi - lo;
@@ -208,14 +216,29 @@ __global__ __launch_bounds__(kSelThreads) void k_select_final(long long n,
 
 // occupy every id whose key is <= T (T = the count-th smallest key);
 // occ[id - 1 + base] (bonds: base 0, 0-based; sites: base 1, socc[id])
-// (Tp: the threshold in device memory, k_select_final's; null: all n)
+// (Tp: the threshold in device memory, k_select_final's; null: all n).
+// valid (k_select_final's cnt[2]): nonzero when k_select_window's
+// occupation stands -- then this pass returns at once (grid-stride, a
+// small grid)
 __global__ __launch_bounds__(kBlock) void k_occupy_rand(long long n, unsigned long long seed,
                                                          const unsigned long long* Tp, int base,
-                                                         uint8_t* occ) {
-  const long long i = (long long)blockIdx.x * kBlock + threadIdx.x;
-  if (i >= n) return;
+                                                         uint8_t* occ, const unsigned* valid) {
+  if (valid && *valid) return;
   const unsigned long long T = Tp ? *Tp : ~0ull;
-  occ[i + base] = perc_rand_key(seed, (unsigned)(i + 1)) <= T ? 1 : 0;
+  for (long long i = (long long)blockIdx.x * kBlock + threadIdx.x; i < n; i += (long long)gridDim.x * kBlock)
+    occ[i + base] = perc_rand_key(seed, (unsigned)(i + 1)) <= T ? 1 : 0;
+}
+
+// the window's keys (cand[1 ..], id in the low 32 bits) at or below T
+__global__ __launch_bounds__(kBlock) void k_occupy_cand(const unsigned* cnt, const unsigned long long* cand,
+                                                         int base, uint8_t* occ) {
+  if (!cnt[2]) return;
+  const unsigned nin = cnt[1];
+  const unsigned long long T = cand[0];
+  for (unsigned j = blockIdx.x * kBlock + threadIdx.x; j < nin; j += gridDim.x * kBlock) {
+    const unsigned long long key = cand[1 + j];
+    if (key <= T) occ[(long long)(key & 0xFFFFFFFFull) - 1 + base] = 1;
+  }
 }
 
 __global__ void k_occupy_sites(const int* order, int count, int t, uint8_t* socc) {
@@ -367,43 +390,48 @@ hipError_t dev_occupy(perc_ctx* h, int kind, int nsites, const int* site_order, 
   return hipSuccess;
 }
 
-// the count smallest keys of ids 1..n occupied: window count + one-workgroup
-// select (k_select_window / k_select_final), then the occupation pass; no
-// host synchronisation
+// the count smallest keys of ids 1..n occupied, occ[base .. base + n):
+// k_select_window (every key hashed once: the keys below the window
+// occupied, the others not, the window's keys gathered), the one-workgroup
+// select of T (k_select_final), then the window's keys at or below T
+// (k_occupy_cand); when T fell outside the window the whole occupation is
+// rewritten from T (k_occupy_rand, otherwise an early return).  No host
+// synchronisation.
 static hipError_t occupy_rand_one(perc_ctx* h, long long n, long long count,
                                   unsigned long long seed, int base, uint8_t* occ) {
   hipStream_t st = h->stream;
-  if (count <= 0) return hipSuccess;  // occ is zeroed by the caller
-  const unsigned long long* Tp = nullptr;
-  if (count < n) {
-    if (!h->d.sel_hist) HIP_TRY(dmalloc(&h->d.sel_hist, 2));
-    if (!h->d.sel_cand) HIP_TRY(dmalloc(&h->d.sel_cand, (size_t)kSelCap + 1 + 16));
-    // window: T's hash is count/n * 2^32 give or take the binomial spread
-    // sqrt(n q (1-q)) keys; +-(8 sigma + 256) keys of hash width
-    const double q = (double)count / (double)n;
-    const double wkeys = 8.0 * std::sqrt((double)n * q * (1.0 - q)) + 256.0;
-    const double two32 = 4294967296.0, c = q * two32, w = wkeys / (double)n * two32;
-    unsigned long long lo = c - w <= 0.0 ? 0ull : (unsigned long long)(c - w);
-    unsigned long long hi = c + w >= two32 ? (1ull << 32) : (unsigned long long)(c + w) + 1;
-    const char* full = std::getenv("PERC_SELECT_FULL");  // tests: the exact slow path
-    if (full && full[0] == '1') lo = hi = 0;
-    HIP_TRY(hipMemsetAsync(h->d.sel_hist, 0, 2 * sizeof(unsigned), st));
-    const int G = (int)std::min<long long>(cdiv(n, kBlock), 2048);
-    k_select_window<<<G, kBlock, 0, st>>>(n, seed, lo, hi, h->d.sel_hist, h->d.sel_cand);
-    HIP_TRY(dbg_sync(st, "k_select_window"));
-    k_select_final<<<1, kSelThreads, 0, st>>>(n, seed, count, lo, hi, h->d.sel_hist,
-                                              h->d.sel_cand);
-    HIP_TRY(dbg_sync(st, "k_select_final"));
-    Tp = h->d.sel_cand;
-    if (std::getenv("PERC_SELECT_TRACE")) {
-      unsigned long long tr[6];
-      HIP_TRY(hipMemcpyAsync(tr, h->d.sel_cand + 1 + kSelCap, sizeof(tr), hipMemcpyDeviceToHost, st));
-      HIP_TRY(hipStreamSynchronize(st));
-      std::fprintf(stderr, "select trace: hist %llu bin %llu rank %llu ticks; nin %llu bin %llu\n",
-                   tr[1] - tr[0], tr[2] - tr[1], tr[3] - tr[2], tr[4], tr[5]);
-    }
+  const int G = (int)std::min<long long>(cdiv(n, kBlock), 2048);
+  if (count <= 0) return hipMemsetAsync(occ + base, 0, (size_t)n, st);
+  if (count >= n) {
+    k_occupy_rand<<<G, kBlock, 0, st>>>(n, seed, nullptr, base, occ, nullptr);
+    return hipGetLastError();
   }
-  k_occupy_rand<<<cdiv(n, kBlock), kBlock, 0, st>>>(n, seed, Tp, base, occ);
+  if (!h->d.sel_hist) HIP_TRY(dmalloc(&h->d.sel_hist, 4));
+  if (!h->d.sel_cand) HIP_TRY(dmalloc(&h->d.sel_cand, (size_t)kSelCap + 1 + 16));
+  // window: T's hash is count/n * 2^32 give or take the binomial spread
+  // sqrt(n q (1-q)) keys; +-(8 sigma + 256) keys of hash width
+  const double q = (double)count / (double)n;
+  const double wkeys = 8.0 * std::sqrt((double)n * q * (1.0 - q)) + 256.0;
+  const double two32 = 4294967296.0, c = q * two32, w = wkeys / (double)n * two32;
+  unsigned long long lo = c - w <= 0.0 ? 0ull : (unsigned long long)(c - w);
+  unsigned long long hi = c + w >= two32 ? (1ull << 32) : (unsigned long long)(c + w) + 1;
+  const char* full = std::getenv("PERC_SELECT_FULL");  // tests: the exact slow path
+  if (full && full[0] == '1') lo = hi = 0;
+  HIP_TRY(hipMemsetAsync(h->d.sel_hist, 0, 4 * sizeof(unsigned), st));
+  k_select_window<<<G, kBlock, 0, st>>>(n, seed, lo, hi, h->d.sel_hist, h->d.sel_cand, base, occ);
+  HIP_TRY(dbg_sync(st, "k_select_window"));
+  k_select_final<<<1, kSelThreads, 0, st>>>(n, seed, count, lo, hi, h->d.sel_hist, h->d.sel_cand);
+  HIP_TRY(dbg_sync(st, "k_select_final"));
+  if (std::getenv("PERC_SELECT_TRACE")) {
+    unsigned long long tr[6];
+    HIP_TRY(hipMemcpyAsync(tr, h->d.sel_cand + 1 + kSelCap, sizeof(tr), hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    std::fprintf(stderr, "select trace: hist %llu bin %llu rank %llu ticks; nin %llu bin %llu\n",
+                 tr[1] - tr[0], tr[2] - tr[1], tr[3] - tr[2], tr[4], tr[5]);
+  }
+  k_occupy_cand<<<cdiv(kSelCap, kBlock), kBlock, 0, st>>>(h->d.sel_hist, h->d.sel_cand, base, occ);
+  HIP_TRY(dbg_sync(st, "k_occupy_cand"));
+  k_occupy_rand<<<G, kBlock, 0, st>>>(n, seed, h->d.sel_cand, base, occ, h->d.sel_hist + 2);
   return hipGetLastError();
 }
 
@@ -411,8 +439,15 @@ hipError_t dev_occupy_random(perc_ctx* h, int kind, int nsites, int nbonds,
                              unsigned long long seed) {
   hipStream_t st = h->stream;
   DeviceBuffers& d = h->d;
-  HIP_TRY(hipMemsetAsync(d.bocc, 0, (size_t)h->nb + 8, st));
-  HIP_TRY(hipMemsetAsync(d.socc, 0, h->g.t + 8, st));
+  // the drawn ranges are written whole (occupy_rand_one); zero the rest
+  if (kind == PERC_SITE) HIP_TRY(hipMemsetAsync(d.bocc, 0, (size_t)h->nb + 8, st));
+  else HIP_TRY(hipMemsetAsync(d.bocc + h->nb, 0, 8, st));
+  if (kind == PERC_BOND) {
+    HIP_TRY(hipMemsetAsync(d.socc, 0, h->g.t + 8, st));
+  } else {
+    HIP_TRY(hipMemsetAsync(d.socc, 0, 1, st));
+    HIP_TRY(hipMemsetAsync(d.socc + h->g.t + 1, 0, 7, st));
+  }
   if (kind != PERC_BOND) HIP_TRY(occupy_rand_one(h, h->g.t, nsites, seed, 1, d.socc));
   if (kind != PERC_SITE)
     HIP_TRY(occupy_rand_one(h, h->nb, nbonds, perc_mix64(seed ^ 0x5DEECE66Dull), 0, d.bocc));
@@ -429,10 +464,12 @@ hipError_t dev_label(perc_ctx* h, int* nspan, int* span_list, int* nclusters) {
   HIP_TRY(hipMemsetAsync(d.counters, 0, sizeof(int) * (8 + kMaxSpanList), st));
   // square lattice without wrap links: one wave per 128 x 16 block walking
   // its rows (k_cc_tile_w; labels 0.318 vs 0.361 ms of kernels at L = 4096,
-  // profiles/r4_5_cc_bench_L4096.txt); else the LDS union-find blocks
+  // profiles/r4_5_cc_bench_L4096.txt), its union-find in 16-bit LDS entries
+  // (twice the resident waves: tile 126.2 vs 155.7 us, r4_7); else the LDS
+  // union-find blocks
   if (g.lattice == kSquare && !g.pbc && !std::getenv("PERC_TILE_TRACE")) {
     constexpr int H = kCcWaveH;
-    k_cc_tile_w<H><<<cdiv(g.m, kCcW) * cdiv(g.n, H), 64, 0, st>>>(g, kind, d.bond_first, d.bocc, d.socc,
+    k_cc_tile_w<H, true><<<cdiv(g.m, kCcW) * cdiv(g.n, H), 64, 0, st>>>(g, kind, d.bond_first, d.bocc, d.socc,
                                                                    d.parent, d.member, (int)h->bf_closed);
     HIP_TRY(dbg_sync(st, "k_cc_tile_w"));
     const int nseg = cdiv(g.m, kCcThreads), nfull = g.n / H, ncand = 2 * cdiv(g.m, kCcW) + 1;
@@ -477,7 +514,7 @@ static hipError_t label_finish(perc_ctx* h, int* nspan, int* span_list, int* ncl
   const Geom& g = h->g;
   hipStream_t st = h->stream;
   DeviceBuffers& d = h->d;
-  k_cc_compress<<<std::min(cdiv(g.t, kCcThreads), kReduceGrid), kCcThreads, 0, st>>>(
+  k_cc_compress<<<std::min(cdiv(g.t, kCcThreads * kCcCompressU), kReduceGrid), kCcThreads, 0, st>>>(
       g.t, d.parent, d.member, d.counters + 1);
   HIP_TRY(dbg_sync(st, "k_cc_compress"));
   k_span_top<<<1, 1024, 0, st>>>(g, d.parent, d.member, d.top, d.counters);

@@ -100,7 +100,24 @@ void launch_cg_spmv(perc_ctx* h, const CGArgs& a, int G) {
       if (h->qfree && a.sm) launch_march_sm<kMarchP>(h, st, a);
       // row-major q-free P (vectors past the Infinity Cache): one round of
       // slot-weighted bands when a.wslots is set
-      else if (h->qfree) klaunch(h, k_cg_march<kMarchP>, a.wslots > 0 ? h->wm_grid : h->march_grid, 64 * kMarchWaves, st, a);
+      else if (h->qfree) {
+#if defined(PERC_PROBE_PROWS) || defined(PERC_PROBE_PNT)
+#ifdef PERC_PROBE_PNT
+        constexpr int kPA = kNT;
+#else
+        constexpr int kPA = 0;
+#endif
+#ifdef PERC_PROBE_PROWS
+        CGArgs ap = a;
+        ap.wslots = 0;
+        klaunch(h, k_cg_march<kMarchP, false, kMarchDepth, kPA>, h->march_grid, 64 * kMarchWaves, st, ap);
+#else
+        klaunch(h, k_cg_march<kMarchP, false, kMarchDepth, kPA>, a.wslots > 0 ? h->wm_grid : h->march_grid, 64 * kMarchWaves, st, a);
+#endif
+#else
+        klaunch(h, k_cg_march<kMarchP>, a.wslots > 0 ? h->wm_grid : h->march_grid, 64 * kMarchWaves, st, a);
+#endif
+      }
       // q-storing P+S (row slabs, the literal dot order, modes without QFREE)
       else klaunch(h, k_cg_march<kMarchPQ, false, 3>, h->march_grid, 64 * kMarchWaves, st, a);
       return;

@@ -224,12 +224,18 @@ def test_occupy_random_equals_its_host_order(lat, m, n, pbc, kind):
     bo = api.random_order(nb, tb, seed, PL.BOND) if kind != PL.SITE else None
     with api.Context(lat, m, n, pbc) as ctx:
         ctx.occupy_random(kind, ts if kind != PL.BOND else 0, tb if kind != PL.SITE else 0, seed)
+        orr = ctx.occupancy()
         lr = ctx.label(canon=True)
         nr = ctx.label_numbers(kind)
         ctx.occupy(kind, site_order=so, nsites=ts if so is not None else 0, bond_order=bo,
                    nbonds_=tb if bo is not None else 0)
+        ore = ctx.occupancy()
         le = ctx.label(canon=True)
         ne = ctx.label_numbers(kind)
+    # the occupancy itself, element by element (sites and bonds)
+    assert np.array_equal(orr[0], ore[0]) and np.array_equal(orr[1], ore[1])
+    assert int(orr[0].sum()) == (ts if kind != PL.BOND else 0)
+    assert int(orr[1].sum()) == (tb if kind != PL.SITE else 0)
     assert np.array_equal(lr["canon"], le["canon"])
     assert lr["nspan"] == le["nspan"] and lr["span_root"] == le["span_root"]
     for key in ("bond_label", "site_label"):
@@ -260,9 +266,12 @@ def test_occupy_random_select_extremes(frac, full, monkeypatch):
         bo = api.random_order(nb, tb, seed, PL.BOND)
         with api.Context(lat, m, n, pbc) as ctx:
             ctx.occupy_random(PL.BOND, 0, tb, seed)
+            orr = ctx.occupancy()[1]
             lr = ctx.label(canon=True)
             ctx.occupy(PL.BOND, bond_order=bo, nbonds_=tb)
+            ore = ctx.occupancy()[1]
             le = ctx.label(canon=True)
+        assert np.array_equal(orr, ore) and int(orr.sum()) == tb, tb
         assert np.array_equal(lr["canon"], le["canon"]), tb
         assert lr["nspan"] == le["nspan"] and lr["nclusters"] == le["nclusters"], tb
 

@@ -137,7 +137,8 @@ int main(int argc, char** argv) {
   hipEvent_t e[4];
   for (auto& x : e) CK(hipEventCreate(&x));
   auto compress0 = [&]() {
-    k_cc_compress<<<std::min(cdiv(g.t, kCcThreads), 1024), kCcThreads>>>(g.t, R.parent, R.member, R.counters);
+    k_cc_compress<<<std::min(cdiv(g.t, kCcThreads * kCcCompressU), kReduceGrid), kCcThreads>>>(
+        g.t, R.parent, R.member, R.counters);
   };
   auto chain_c = [&](const char* what, auto tilef, auto mergef, auto compressf, bool ref) {
     double t[3] = {0, 0, 0};
@@ -191,34 +192,17 @@ int main(int argc, char** argv) {
   chain("tile_w<64>", [&]() { k_cc_tile_w<64><<<cdiv(g.m, kCcW) * cdiv(g.n, 64), 64>>>(g, PERC_BOND, R.bf, R.bocc, R.socc,
                                                                                        R.parent, R.member, 1); },
         merge_for(std::integral_constant<int, 64>{}), false);
-  // the register-resident tile kernel and the lockstep compress
-  chain("tile_r<16>", [&]() { k_cc_tile_r<16><<<cdiv(g.m, kCcW) * cdiv(g.n, 16), 64>>>(g, PERC_BOND, R.bf, R.bocc, R.socc,
-                                                                                       R.parent, R.member, 1); },
-        merge_for(std::integral_constant<int, 16>{}), false);
-  chain("tile_r<32>", [&]() { k_cc_tile_r<32><<<cdiv(g.m, kCcW) * cdiv(g.n, 32), 64>>>(g, PERC_BOND, R.bf, R.bocc, R.socc,
-                                                                                       R.parent, R.member, 1); },
-        merge_for(std::integral_constant<int, 32>{}), false);
-  chain("tile_r<16, u16>", [&]() { k_cc_tile_r<16, true><<<cdiv(g.m, kCcW) * cdiv(g.n, 16), 64>>>(
-                                      g, PERC_BOND, R.bf, R.bocc, R.socc, R.parent, R.member, 1); },
-        merge_for(std::integral_constant<int, 16>{}), false);
-  chain("tile_r<32, u16>", [&]() { k_cc_tile_r<32, true><<<cdiv(g.m, kCcW) * cdiv(g.n, 32), 64>>>(
-                                      g, PERC_BOND, R.bf, R.bocc, R.socc, R.parent, R.member, 1); },
-        merge_for(std::integral_constant<int, 32>{}), false);
-  for (int grid : {1024, 4096, 16384}) {
-    char nm[64];
-    std::snprintf(nm, sizeof nm, "tile_r<16> + compress_ls<4> g%d", grid);
-    chain_c(nm, [&]() { k_cc_tile_r<16><<<cdiv(g.m, kCcW) * cdiv(g.n, 16), 64>>>(g, PERC_BOND, R.bf, R.bocc, R.socc,
-                                                                                 R.parent, R.member, 1); },
-            merge_for(std::integral_constant<int, 16>{}),
-            [&, grid]() { k_cc_compress_ls<4><<<std::min(cdiv(g.t, kCcThreads * 4), grid), kCcThreads>>>(
-                              g.t, R.parent, R.member, R.counters); }, false);
-    std::snprintf(nm, sizeof nm, "tile_r<16> + compress_ls<8> g%d", grid);
-    chain_c(nm, [&]() { k_cc_tile_r<16><<<cdiv(g.m, kCcW) * cdiv(g.n, 16), 64>>>(g, PERC_BOND, R.bf, R.bocc, R.socc,
-                                                                                 R.parent, R.member, 1); },
-            merge_for(std::integral_constant<int, 16>{}),
-            [&, grid]() { k_cc_compress_ls<8><<<std::min(cdiv(g.t, kCcThreads * 8), grid), kCcThreads>>>(
-                              g.t, R.parent, R.member, R.counters); }, false);
-  }
+  // compress: U sites per thread chased in lockstep (production: kCcCompressU), one site per thread
+  chain_c("tile_w<16, u16> + compress<1>", [&]() { k_cc_tile_w<16, true><<<cdiv(g.m, kCcW) * cdiv(g.n, 16), 64>>>(
+                                                      g, PERC_BOND, R.bf, R.bocc, R.socc, R.parent, R.member, 1); },
+          merge_for(std::integral_constant<int, 16>{}),
+          [&]() { k_cc_compress<1><<<std::min(cdiv(g.t, kCcThreads), kReduceGrid), kCcThreads>>>(
+                      g.t, R.parent, R.member, R.counters); }, false);
+  chain_c("tile_w<16, u16> + compress<4>", [&]() { k_cc_tile_w<16, true><<<cdiv(g.m, kCcW) * cdiv(g.n, 16), 64>>>(
+                                                      g, PERC_BOND, R.bf, R.bocc, R.socc, R.parent, R.member, 1); },
+          merge_for(std::integral_constant<int, 16>{}),
+          [&]() { k_cc_compress<4><<<std::min(cdiv(g.t, kCcThreads * 4), kReduceGrid), kCcThreads>>>(
+                      g.t, R.parent, R.member, R.counters); }, false);
   // site and mixed kinds (sites occupied at 0.8 by another hash): the production tile kernel vs the candidate
   {
     std::vector<uint8_t> so((size_t)g.t + 2, 0);
@@ -229,9 +213,9 @@ int main(int argc, char** argv) {
       k_cc_tile_w<kCcH><<<R.tiles, 64>>>(g, kind, R.bf, R.bocc, R.socc, R.parent, R.member, 1);
       CK(hipDeviceSynchronize());
       same(R, kind == PERC_SITE ? "k_cc_tile_w, site kind" : "k_cc_tile_w, mixed kind");
-      k_cc_tile_r<kCcH><<<R.tiles, 64>>>(g, kind, R.bf, R.bocc, R.socc, R.parent, R.member, 1);
+      k_cc_tile_w<kCcH, true><<<R.tiles, 64>>>(g, kind, R.bf, R.bocc, R.socc, R.parent, R.member, 1);
       CK(hipDeviceSynchronize());
-      same(R, kind == PERC_SITE ? "k_cc_tile_r, site kind" : "k_cc_tile_r, mixed kind");
+      same(R, kind == PERC_SITE ? "k_cc_tile_w u16, site kind" : "k_cc_tile_w u16, mixed kind");
     }
   }
   return 0;
