@@ -24,6 +24,10 @@ CASES = {
     "lib_lazy": dict(lib=True, devid=False, destroy=True, perc_rccl=False),
     "lib_devid_nodestroy": dict(lib=True, devid=True, destroy=False, perc_rccl=False),
     "lib_rccl_then_torch": dict(lib=True, devid=True, destroy=True, perc_rccl=True),
+    # a collective on the context's own stream (torch.cuda.ExternalStream), the context closed
+    # before the group is destroyed; then the Python row-slab loop (dslab.conductance) the same way
+    "extstream_allreduce": dict(lib=True, devid=True, destroy=True, perc_rccl=False, ext="allreduce"),
+    "dslab_conductance": dict(lib=True, devid=True, destroy=True, perc_rccl=False, ext="dslab"),
 }
 
 
@@ -47,6 +51,20 @@ def child(name):
     t = torch.ones(4, device="cuda")
     dist.all_reduce(t)
     torch.cuda.synchronize()
+    if c.get("ext"):
+        from percolation_amd import dslab
+        ctx = api.Context(0, 256, 256, 0)
+        ctx.occupy_random(PL.BOND, 0, int(0.6 * api.nbonds(0, 256, 256, 0)), 7)
+        ctx.label()
+        if c["ext"] == "allreduce":
+            st = torch.cuda.ExternalStream(PL.lib().perc_stream(ctx.h), device=torch.device("cuda", 0))
+            with torch.cuda.stream(st):
+                dist.all_reduce(t)
+            torch.cuda.synchronize()
+        else:
+            dslab.conductance(ctx, tol=1e-8, itmax=10000)
+        ctx.close()
+        print("context closed", flush=True)
     if c["destroy"]:
         dist.destroy_process_group()
     print("done", flush=True)
