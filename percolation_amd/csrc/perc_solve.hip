@@ -98,25 +98,14 @@ void launch_cg_spmv(perc_ctx* h, const CGArgs& a, int G) {
     hipStream_t st = h->stream;
     if (h->march) {
       if (h->qfree && a.sm) launch_march_sm<kMarchP>(h, st, a);
-      // row-major q-free P (vectors past the Infinity Cache): one round of
-      // slot-weighted bands when a.wslots is set
       else if (h->qfree) {
-#if defined(PERC_PROBE_PROWS) || defined(PERC_PROBE_PNT)
-#ifdef PERC_PROBE_PNT
-        constexpr int kPA = kNT;
-#else
-        constexpr int kPA = 0;
-#endif
-#ifdef PERC_PROBE_PROWS
+        // row-major q-free P (vectors past the Infinity Cache) on B's bands
+        // (march_grid): with the x update out of the walk, L = 8192 P 0.314 vs
+        // 0.355 ms on one round of slot-weighted bands, 0.628 vs 0.656 ms per
+        // solve iteration (profiles/r4_8_l8192_ab.json)
         CGArgs ap = a;
         ap.wslots = 0;
-        klaunch(h, k_cg_march<kMarchP, false, kMarchDepth, kPA>, h->march_grid, 64 * kMarchWaves, st, ap);
-#else
-        klaunch(h, k_cg_march<kMarchP, false, kMarchDepth, kPA>, a.wslots > 0 ? h->wm_grid : h->march_grid, 64 * kMarchWaves, st, a);
-#endif
-#else
-        klaunch(h, k_cg_march<kMarchP>, a.wslots > 0 ? h->wm_grid : h->march_grid, 64 * kMarchWaves, st, a);
-#endif
+        klaunch(h, k_cg_march<kMarchP>, h->march_grid, 64 * kMarchWaves, st, ap);
       }
       // q-storing P+S (row slabs, the literal dot order, modes without QFREE)
       else klaunch(h, k_cg_march<kMarchPQ, false, 3>, h->march_grid, 64 * kMarchWaves, st, a);
@@ -147,9 +136,8 @@ void launch_cg_b(perc_ctx* h, const CGArgs& a, int G) {
   if (h->fused && h->b_grid > 0) G = h->b_grid;
   if (h->march && h->qfree) {
     if (a.sm) launch_march_sm<kMarchB>(h, h->stream, a);
-    else {  // row-major B: its own bands (slot-weighted bands are the P kernel's,
-            // rm_slots), nontemporal r(k) loads (L = 8192: 0.300 vs 0.331 ms,
-            // profiles/r4_3_l8192_probe.json)
+    else {  // row-major B: 8-row bands (march_grid, P's too), nontemporal r(k)
+            // loads (L = 8192: 0.300 vs 0.331 ms, profiles/r4_3_l8192_probe.json)
       CGArgs ab = a;
       ab.wslots = 0;
       klaunch(h, k_cg_march<kMarchB, false, kMarchDepth, kNT>, h->march_grid, 64 * kMarchWaves, h->stream, ab);
@@ -363,10 +351,9 @@ int march_rows_for(const perc_ctx* h, int nrows) {
 // band height and grid of the register-march kernel; the slot-weighted
 // bands (PERC_MARCH_SLOTS): one workgroup per CU and round, bands cycling
 // over the rounds, weights = the rounds' relative streaming rates with
-// equal bands (kSlotW: P, B of the strip-major march, row-major P past the
-// Infinity Cache; same-box A/Bs, profiles/r3_4_ab_slotw_L4096.log and the
-// r3 L = 8192 probes -- flat weights there, i.e. one round of equal bands:
-// 0.364 ms vs 0.387 at 100:80:60 and 0.403 for the 16-row bands)
+// equal bands (kSlotW: P, B of the strip-major march; same-box A/Bs,
+// profiles/r3_4_ab_slotw_L4096.log.  The third set, row-major P past the
+// Infinity Cache, is unused since round 4: that P runs on B's 8-row bands)
 constexpr int kSlotW[3][kMaxSlotRounds] = {{100, 75, 50, 40}, {100, 80, 60, 50}, {100, 100, 100, 100}};
 
 void march_geometry(perc_ctx* h) {

@@ -3,6 +3,8 @@
 # L = 8192 row-major P band / load-policy A/B, config 5 as stated, then the whole GPU suite
 mkdir -p gpurun_out
 export TMPDIR=/tmp
+timeout -k 10 120 ./tools/cc_bench 4096 0.6 20 > gpurun_out/r4j_cc_bench.log 2>&1
+rc=$?; cat gpurun_out/r4j_cc_bench.log; [ $rc -ne 0 ] && exit $rc
 timeout -k 10 300 python -u tools/lib_ab.py --what label --L 4096 --libs main,xwalk --reps 6 > gpurun_out/r4j_label_ab_L4096.json 2>&1
 rc=$?; tail -2 gpurun_out/r4j_label_ab_L4096.json; [ $rc -ne 0 ] && exit $rc
 timeout -k 10 500 python -u tools/lib_ab.py --L 8192 --libs main,prows,pnt,prowsnt --iters 400 --rounds 2 > gpurun_out/r4j_l8192_ab.json 2>&1
