@@ -293,10 +293,14 @@ struct TileUF {
   }
 };
 
-template <int H, bool P16 = false>
+// NREG: the rows' run nodes and member flags kept in registers (packed,
+// the loop over the rows unrolled) instead of a provisional parent / member
+// store and a re-read of it in the last pass
+template <int H, bool P16 = false, bool NREG = false>
 __global__ __launch_bounds__(64) void k_cc_tile_w(Geom g, int kind, const int* bond_first, const uint8_t* bocc,
                                                   const uint8_t* socc, int* parent, uint8_t* member,
                                                   int bf_closed) {
+  static_assert(!NREG || H <= 32, "member flags: a row per bit of one word");
   __shared__ int uf_mem[P16 ? kCcW * H / 2 : kCcW * H];
   const TileUF<P16> uf{uf_mem};
   const int ntx = cdiv(g.m, kCcW);
@@ -334,9 +338,10 @@ __global__ __launch_bounds__(64) void k_cc_tile_w(Geom g, int kind, const int* b
   };
   unsigned R[2], U[2], O[2], Rn[2], Un[2], On[2], Up[2] = {0u, 0u};
   int labp[2] = {0, 0};
+  unsigned nodes[NREG ? H : 1], Mb[2] = {0u, 0u};
   load_row(0, R, U, O);
   const unsigned long long le = lane == 63 ? ~0ull : ((2ull << lane) - 1ull);
-  for (int r = 0; r < th; ++r) {
+  auto row_step = [&](int r) {
     load_row(r + 1, Rn, Un, On);  // (past th: nothing loaded)
     // runs: column c has a left link iff c - 1 links right
     const unsigned rl0 = __shfl(R[0], (lane + 63) & 63, 64), rl1 = __shfl(R[1], (lane + 63) & 63, 64);
@@ -380,13 +385,19 @@ __global__ __launch_bounds__(64) void k_cc_tile_w(Geom g, int kind, const int* b
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       const bool v = h ? v1 : v0;
+      const bool lft = h ? left1 : left0;
+      const bool mem = kind == PERC_BOND ? (R[h] | U[h] | (lft ? 1u : 0u) | (r > 0 ? Up[h] : 0u)) != 0u
+                                         : O[h] != 0u;
+      if constexpr (NREG) {
+        Mb[h] |= (mem ? 1u : 0u) << r;
+        continue;
+      }
       if (!v) continue;
       const int lc = lane + 64 * h, s = (r0 + r) * g.m + c0 + lc + 1;
-      const bool lft = h ? left1 : left0;
       parent[s] = node[h];
-      member[s] = kind == PERC_BOND ? ((R[h] | U[h] | (lft ? 1u : 0u) | (r > 0 ? Up[h] : 0u)) ? 1 : 0)
-                                    : (O[h] ? 1 : 0);
+      member[s] = mem ? 1 : 0;
     }
+    if constexpr (NREG) nodes[r] = (unsigned)node[0] | (unsigned)node[1] << 16;
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       labp[h] = node[h];
@@ -395,22 +406,47 @@ __global__ __launch_bounds__(64) void k_cc_tile_w(Geom g, int kind, const int* b
       U[h] = Un[h];
       O[h] = On[h];
     }
+  };
+  if constexpr (NREG) {
+#pragma unroll
+    for (int r = 0; r < H; ++r)
+      if (r < th) row_step(r);
+  } else {
+    for (int r = 0; r < th; ++r) row_step(r);
   }
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  for (int r = 0; r < th; ++r) {
+  auto root_of = [&](int x) {
+    int p = uf.get(x);
+    while (p != x) {
+      x = p;
+      p = uf.get(x);
+    }
+    return (r0 + x / kCcW) * g.m + c0 + x % kCcW + 1;
+  };
+  if constexpr (NREG) {
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int lc = lane + 64 * h;
-      if (lc >= tw) continue;
-      const int s = (r0 + r) * g.m + c0 + lc + 1;
-      int x = parent[s], p = uf.get(x);
-      while (p != x) {
-        x = p;
-        p = uf.get(x);
+    for (int r = 0; r < H; ++r) {
+      if (r >= th) continue;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int lc = lane + 64 * h;
+        if (lc >= tw) continue;
+        const int s = (r0 + r) * g.m + c0 + lc + 1;
+        parent[s] = root_of((int)(nodes[r] >> (16 * h) & 0xffffu));
+        member[s] = (uint8_t)(Mb[h] >> r & 1u);
       }
-      parent[s] = (r0 + x / kCcW) * g.m + c0 + x % kCcW + 1;
+    }
+  } else {
+    for (int r = 0; r < th; ++r) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int lc = lane + 64 * h;
+        if (lc >= tw) continue;
+        const int s = (r0 + r) * g.m + c0 + lc + 1;
+        parent[s] = root_of(parent[s]);
+      }
     }
   }
 }

@@ -210,6 +210,32 @@ __global__ __launch_bounds__(kBlock) void k_cg_spmv(CGArgs a) {
   }
 }
 
+// S(k) on CSR with one row per thread (k_spmv's row, bitwise dsprsax): q(i)
+// and q(i) p(i), summed per workgroup, then the grid-wide reduction; grid
+// cdiv(N, kBlock) (perc_ctx::row_grid).  Against the LDS-staged wave tiles
+// of k_cg_spmv<0, NS>: see DESIGN §4 (CSR).
+template <int NS>
+__global__ __launch_bounds__(kBlock) void k_cg_spmv_row(CGArgs a) {
+  CGScalars* S = a.S;
+  if (S->done) return;
+  __shared__ double s_red[32];
+  __shared__ int s_flag[2];
+  const int i = blockIdx.x * kBlock + threadIdx.x;
+  double dot[1] = {0.0};
+  if (i < a.A.N) {
+    const double qi = csr_row<NS>(a.A, a.p, i);
+    a.q[i] = qi;
+    dot[0] = qi * a.p[i];
+  }
+  double tot[1];
+  if (publish_and_reduce<1>(dot, a.partials, a.tickets, blockIdx.x, gridDim.x, tot, s_red, s_flag)) {
+    if (threadIdx.x == 0) {
+      S->akden = tot[0];
+      S->ak = S->bknum / tot[0];
+    }
+  }
+}
+
 // XF: x kept on every row (perc_set_full_voltages / vint): the update
 // x += ak p(k) rides in the batched pair loop (16-B accesses, loads issued
 // with the batch) instead of a separate scalar pass
@@ -948,7 +974,7 @@ __global__ __launch_bounds__(kBlock) void k_pack_nib(TileGeom T, const uint16_t*
 constexpr size_t kLargeVector = (size_t)256 << 20;
 
 // workgroups of the largest reduction (CG kernels or the tiled kernel)
-int red_grid(const perc_ctx* h) { return std::max({h->grid, h->tile_grid, h->march_grid_max}); }
+int red_grid(const perc_ctx* h) { return std::max({h->grid, h->tile_grid, h->march_grid_max, h->row_grid}); }
 
 // tags of the granule reductions are (solve_epoch << 24) | iteration: at
 // most this many iterations per solve (else the ticket reduction: a tag

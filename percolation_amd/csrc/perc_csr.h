@@ -247,10 +247,7 @@ __device__ __forceinline__ void block_tiles(int N, int* t0, int* t1) {
 // on §8(d)'s 1.27 GB (profiles/r4_5_spmv_bench_L4096.txt; grid-stride
 // variants 0.262-0.275 ms).
 template <int NS>
-__global__ __launch_bounds__(kBlock) void k_spmv(CsrView A, const double* __restrict__ x,
-                                                 double* __restrict__ y) {
-  const int i = blockIdx.x * kBlock + threadIdx.x;
-  if (i >= A.N) return;
+__device__ __forceinline__ double csr_row(const CsrView& A, const double* __restrict__ x, int i) {
   const int a = A.rowptr[i], b = A.rowptr[i + 1];
   double acc;
   if constexpr (NS > 0) {
@@ -273,7 +270,15 @@ __global__ __launch_bounds__(kBlock) void k_spmv(CsrView A, const double* __rest
     acc = A.diag[i] * x[i];
     for (int k = a; k < b; ++k) acc = acc + A.val[k] * x[A.col[k]];
   }
-  y[i] = acc;
+  return acc;
+}
+
+template <int NS>
+__global__ __launch_bounds__(kBlock) void k_spmv(CsrView A, const double* __restrict__ x,
+                                                 double* __restrict__ y) {
+  const int i = blockIdx.x * kBlock + threadIdx.x;
+  if (i >= A.N) return;
+  y[i] = csr_row<NS>(A, x, i);
 }
 
 // y = A x on a stream: k_spmv at the rows' slot count, one row per thread

@@ -180,7 +180,6 @@ struct perc_ctx {
   bool march = false;           // fused format runs the register-march kernel
   int march_h = 32;             // its band height (rows per wave)
   int march_slots = 0;          // q-free strip-major march: slot-weighted bands
-  int march_slots_rm = 0;       // q-free row-major march: slot-weighted bands for P
   int march_tag = 0;            // q-free strip-major march: tagged-granule reductions
   unsigned solve_epoch = 0;     // tags of the granule reductions
   int wm_slots = 0;             // slot-weighted bands: workgroup rounds (0: not available)
@@ -194,6 +193,7 @@ struct perc_ctx {
   unsigned ncls[3] = {};        // their count / form bits: interior, first, last column
   int march_grid = 0;           // its workgroups
   int march_grid_max = 0;       // workgroups at band height 1 (reduction buffers)
+  int row_grid = 0;             // one CSR row per thread: cdiv(N, kBlock) (k_cg_spmv_row)
   int march_rows_req = 0;       // perc_set_march_rows (0: auto)
   int march_mode = PERC_MARCH_DEFAULT;  // perc_set_march_mode
   bool qfree = false;           // march B rebuilds q (52N / iteration)

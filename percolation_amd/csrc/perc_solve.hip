@@ -98,15 +98,11 @@ void launch_cg_spmv(perc_ctx* h, const CGArgs& a, int G) {
     hipStream_t st = h->stream;
     if (h->march) {
       if (h->qfree && a.sm) launch_march_sm<kMarchP>(h, st, a);
-      else if (h->qfree) {
-        // row-major q-free P (vectors past the Infinity Cache) on B's bands
-        // (march_grid): with the x update out of the walk, L = 8192 P 0.314 vs
-        // 0.355 ms on one round of slot-weighted bands, 0.628 vs 0.656 ms per
-        // solve iteration (profiles/r4_8_l8192_ab.json)
-        CGArgs ap = a;
-        ap.wslots = 0;
-        klaunch(h, k_cg_march<kMarchP>, h->march_grid, 64 * kMarchWaves, st, ap);
-      }
+      // row-major q-free P (vectors past the Infinity Cache) on B's 8-row
+      // bands (march_grid): with the x update out of the walk, L = 8192 P
+      // 0.314 vs 0.355 ms on one round of slot-weighted bands, 0.628 vs
+      // 0.656 ms per solve iteration (profiles/r4_8_l8192_ab.json)
+      else if (h->qfree) klaunch(h, k_cg_march<kMarchP>, h->march_grid, 64 * kMarchWaves, st, a);
       // q-storing P+S (row slabs, the literal dot order, modes without QFREE)
       else klaunch(h, k_cg_march<kMarchPQ, false, 3>, h->march_grid, 64 * kMarchWaves, st, a);
       return;
@@ -121,10 +117,11 @@ void launch_cg_spmv(perc_ctx* h, const CGArgs& a, int G) {
       else klaunch(h, k_cg_ps<6, true, 8>, G2, B2, st, a);
     }
   } else if (!h->stencil) {
-    const int ns = csr_slots(a.A.maxrow);
-    if (ns == 4) klaunch(h, k_cg_spmv<0, 4>, G, kBlock, h->stream, a);
-    else if (ns == kMaxNnzRow) klaunch(h, k_cg_spmv<0, kMaxNnzRow>, G, kBlock, h->stream, a);
-    else klaunch(h, k_cg_spmv<0, 0>, G, kBlock, h->stream, a);
+    // CSR: one row per thread (k_spmv's row) and the q.p partials
+    const int ns = csr_slots(a.A.maxrow), GR = h->row_grid;
+    if (ns == 4) klaunch(h, k_cg_spmv_row<4>, GR, kBlock, h->stream, a);
+    else if (ns == kMaxNnzRow) klaunch(h, k_cg_spmv_row<kMaxNnzRow>, GR, kBlock, h->stream, a);
+    else klaunch(h, k_cg_spmv_row<0>, GR, kBlock, h->stream, a);
   }
   else if (h->g.scn == 4) klaunch(h, k_cg_spmv<4>, G, kBlock, h->stream, a);
   else klaunch(h, k_cg_spmv<6>, G, kBlock, h->stream, a);
@@ -136,12 +133,9 @@ void launch_cg_b(perc_ctx* h, const CGArgs& a, int G) {
   if (h->fused && h->b_grid > 0) G = h->b_grid;
   if (h->march && h->qfree) {
     if (a.sm) launch_march_sm<kMarchB>(h, h->stream, a);
-    else {  // row-major B: 8-row bands (march_grid, P's too), nontemporal r(k)
-            // loads (L = 8192: 0.300 vs 0.331 ms, profiles/r4_3_l8192_probe.json)
-      CGArgs ab = a;
-      ab.wslots = 0;
-      klaunch(h, k_cg_march<kMarchB, false, kMarchDepth, kNT>, h->march_grid, 64 * kMarchWaves, h->stream, ab);
-    }
+    // row-major B: 8-row bands (march_grid, P's too), nontemporal r(k) loads
+    // (L = 8192: 0.300 vs 0.331 ms, profiles/r4_3_l8192_probe.json)
+    else klaunch(h, k_cg_march<kMarchB, false, kMarchDepth, kNT>, h->march_grid, 64 * kMarchWaves, h->stream, a);
   } else if (h->stencil) {
     // x on every row with the march's x-in-B (fused, row-major): XF
     if (a.bx && a.xrows == 0 && !a.sm) klaunch(h, k_cg_b<true, true>, G, kBlock, h->stream, a);
@@ -249,6 +243,7 @@ hipError_t dev_build_lattice(perc_ctx* h) {
     HIP_TRY(dmalloc(&d.code, (size_t)N + 8));
   }
   h->grid = cg_grid(N);
+  h->row_grid = cdiv(N, kBlock);
   int cus = 0;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, h->device) != hipSuccess)
     cus = 0;
@@ -304,6 +299,7 @@ hipError_t dev_alloc_matrix(perc_ctx* h, int N, long long nnz) {
   HIP_TRY(dmalloc(&d.p1, nv));
   HIP_TRY(dmalloc(&d.q, nv));
   h->grid = cg_grid(N);
+  h->row_grid = cdiv(N, kBlock);
   h->tile_grid = 0;
   h->march_grid = h->march_grid_max = 0;
   HIP_TRY(dmalloc(&d.partials, kRedSlots * red_partials_size(red_grid(h))));
@@ -329,9 +325,8 @@ void dev_free_all(perc_ctx* h) {
 
 // band height of the register-march kernel over `nrows` rows: the
 // requested height (perc_set_march_rows); vectors past the Infinity Cache:
-// 8-row bands for the row-major march B (0.310 vs 0.318 ms at 16 rows at
-// L = 8192; its P runs one round of slot-mapped bands instead,
-// march_slots_rm; 16 rows without PERC_MARCH_SLOTS); else one round of
+// 8-row bands for the row-major march P and B (B 0.310 vs 0.318 ms at 16
+// rows at L = 8192; 16 rows without PERC_MARCH_SLOTS); else one round of
 // resident waves, the height that gives every wave slot of the chip one
 // strip-band
 int march_rows_for(const perc_ctx* h, int nrows) {
@@ -440,12 +435,6 @@ void select_format(perc_ctx* h) {
   // slot-weighted bands of the strip-major march (to_strips applies them)
   const bool slots = (h->march_mode & PERC_MARCH_SLOTS) != 0;
   h->march_slots = slots && h->strips && h->wm_slots > 0;
-  // row-major q-free march past the Infinity Cache (L = 8192): P on one round
-  // of bands (the slot mapping with the third weight set), B on 8-row bands
-  // (march_rows_for): P 0.364 + B 0.310 vs 0.403 + 0.318 ms per iteration
-  // (r3 L = 8192 probes)
-  h->march_slots_rm = slots && h->qfree && !h->strips && (size_t)h->N * sizeof(double) > kLargeVector &&
-                      h->wm_slots > 0;
   // tagged-granule reductions of the strip-major march (PERC_MARCH_TAG);
   // their tags are (epoch << 24) | iteration, so solves of >= 2^24 - 2
   // iterations take the ticket reduction
@@ -666,12 +655,6 @@ hipError_t dev_solve(perc_ctx* h, int itol, double tol, int itmax, bool x0_zero,
   }
   if (h->strips) HIP_TRY(to_strips(h, a));
   HIP_TRY(setup_granules(h, a, itmax));
-  // row-major q-free march past the Infinity Cache: the P kernel on one
-  // round of slot-weighted bands, B on its short bands
-  if (!h->strips && h->march && h->qfree && h->march_slots_rm && h->wm_slots > 0) {
-    a.wslots = h->wm_slots;
-    for (int i = 0; i <= h->wm_slots; ++i) a.wcum[0][i] = h->wm_cum[2][i];
-  }
   // iterate in chunks; the device flag makes surplus launches no-ops
   int chunk = 8;
   CGScalars* hsp = nullptr;
@@ -842,12 +825,6 @@ hipError_t dev_bench(perc_ctx* h, int which, int reps, double* ms) {
   if (h->strips && (which == 1 || which == 2 || which == 5)) {
     HIP_TRY(to_strips(h, a));
     HIP_TRY(setup_granules(h, a, hs.itmax));
-  }
-  // row-major q-free march past the Infinity Cache: P on the solve's slot
-  // bands (dev_solve)
-  if (!h->strips && h->march && h->qfree && h->march_slots_rm && h->wm_slots > 0) {
-    a.wslots = h->wm_slots;
-    for (int i = 0; i <= h->wm_slots; ++i) a.wcum[0][i] = h->wm_cum[2][i];
   }
   HIP_TRY(hipMemcpyAsync(d.scal, &hs, sizeof(hs), hipMemcpyHostToDevice, st));
   HIP_TRY(hipMemsetAsync(d.tickets, 0, kRedSlots * red_tickets_size(red_grid(h)) * sizeof(unsigned),

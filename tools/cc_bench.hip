@@ -192,6 +192,16 @@ int main(int argc, char** argv) {
   chain("tile_w<64>", [&]() { k_cc_tile_w<64><<<cdiv(g.m, kCcW) * cdiv(g.n, 64), 64>>>(g, PERC_BOND, R.bf, R.bocc, R.socc,
                                                                                        R.parent, R.member, 1); },
         merge_for(std::integral_constant<int, 64>{}), false);
+  // run nodes and member flags kept in registers (no provisional store, no re-read)
+  chain("tile_w<16, u16, nreg>", [&]() { k_cc_tile_w<16, true, true><<<cdiv(g.m, kCcW) * cdiv(g.n, 16), 64>>>(
+                                            g, PERC_BOND, R.bf, R.bocc, R.socc, R.parent, R.member, 1); },
+        merge_for(std::integral_constant<int, 16>{}), false);
+  chain("tile_w<16, u32, nreg>", [&]() { k_cc_tile_w<16, false, true><<<cdiv(g.m, kCcW) * cdiv(g.n, 16), 64>>>(
+                                            g, PERC_BOND, R.bf, R.bocc, R.socc, R.parent, R.member, 1); },
+        merge_for(std::integral_constant<int, 16>{}), false);
+  chain("tile_w<32, u16, nreg>", [&]() { k_cc_tile_w<32, true, true><<<cdiv(g.m, kCcW) * cdiv(g.n, 32), 64>>>(
+                                            g, PERC_BOND, R.bf, R.bocc, R.socc, R.parent, R.member, 1); },
+        merge_for(std::integral_constant<int, 32>{}), false);
   // compress: U sites per thread chased in lockstep (production: kCcCompressU), one site per thread
   chain_c("tile_w<16, u16> + compress<1>", [&]() { k_cc_tile_w<16, true><<<cdiv(g.m, kCcW) * cdiv(g.n, 16), 64>>>(
                                                       g, PERC_BOND, R.bf, R.bocc, R.socc, R.parent, R.member, 1); },
@@ -216,6 +226,9 @@ int main(int argc, char** argv) {
       k_cc_tile_w<kCcH, true><<<R.tiles, 64>>>(g, kind, R.bf, R.bocc, R.socc, R.parent, R.member, 1);
       CK(hipDeviceSynchronize());
       same(R, kind == PERC_SITE ? "k_cc_tile_w u16, site kind" : "k_cc_tile_w u16, mixed kind");
+      k_cc_tile_w<kCcH, true, true><<<R.tiles, 64>>>(g, kind, R.bf, R.bocc, R.socc, R.parent, R.member, 1);
+      CK(hipDeviceSynchronize());
+      same(R, kind == PERC_SITE ? "k_cc_tile_w u16 nreg, site" : "k_cc_tile_w u16 nreg, mixed");
     }
   }
   return 0;

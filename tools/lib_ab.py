@@ -7,6 +7,7 @@ the libraries alternating for `rounds` rounds, each figure its best.
 --what solve: one L x L bond realisation, perc_bench_kernel 1 (P), 2 (B) and
   5 (a whole iteration), best of 3 x `reps` launches, plus ms per iteration
   of fixed-iteration solves (slope between itmax/2 and itmax, tol 0);
+  --format csr: the CSR operator (0 plain SpMV, 1 S, 2 B, 3 P, 5 iteration);
 --what label: per realisation (device-drawn bond occupancy, `reps`
   realisations), wall ms of perc_occupy_random, perc_label (labels +
   spanning test + its read-back) and the partition's cluster count.
@@ -62,9 +63,13 @@ def child(args):
             ctx.set_march_mode(args.mode)
         ctx.occupy_random(PL.BOND, 0, int(args.p * nb), 777)
         assert ctx.label()["nspan"] > 0
+        if args.format == "csr":
+            ctx.set_matrix_format(PL.FMT_CSR)
         c = ctx.conductance(tol=1e-8, itmax=args.iters)
         out["fp"] = [c["iter"], c["gtop"], c["gbot"]]  # same numbers across store policies
-        for w, k in ((1, "P"), (2, "B"), (5, "iteration")):
+        kset = ((1, "P"), (2, "B"), (5, "iteration")) if args.format == "default" else \
+            ((0, "spmv_plain"), (1, "S"), (2, "B"), (3, "P"), (5, "iteration"))
+        for w, k in kset:
             out[k] = min(ctx.bench_kernel(w, args.reps) for _ in range(3))
         t = {}
         for n in (args.iters // 2, args.iters):
@@ -86,6 +91,7 @@ def main():
     ap.add_argument("--mode", type=int, default=-1)
     ap.add_argument("--libs", default="main")
     ap.add_argument("--what", default="solve", choices=("solve", "label"))
+    ap.add_argument("--format", default="default", choices=("default", "csr"))
     ap.add_argument("--child", action="store_true")
     args = ap.parse_args()
     if args.child:
@@ -100,7 +106,7 @@ def main():
                 env["PERC_LIBPERC"] = os.path.join(REPO, "percolation_amd", "probe", "libperc_%s.so" % lib)
             cmd = [sys.executable, os.path.abspath(__file__), "--child", "--L", str(args.L), "--p", str(args.p),
                    "--reps", str(args.reps), "--iters", str(args.iters), "--mode", str(args.mode),
-                   "--what", args.what]
+                   "--what", args.what, "--format", args.format]
             r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600)
             if r.returncode != 0:
                 sys.stderr.write(r.stderr[-3000:])
