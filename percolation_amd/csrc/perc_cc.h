@@ -464,7 +464,10 @@ __global__ __launch_bounds__(64) void k_cc_tile_w(Geom g, int kind, const int* b
 // unions drop out; the rest start one hop closer to the roots.  (Against
 // the round-3 mapping, one workgroup per lattice row: labels 0.435 vs
 // 0.512 ms per realisation at L = 4096, profiles/r4_4_label_ab_L4096.json.)
-template <int TH = kCcH>  // block height of the tile kernel that ran before
+// WD: the wave's unions deduplicated over all its lanes, the pairs taken as
+// (min, max) -- one union per distinct pair of parents in the wave, by the
+// pair's first lane (one ballot round per distinct pair)
+template <int TH = kCcH, bool WD = false>  // TH: block height of the tile kernel that ran before
 __global__ __launch_bounds__(kCcThreads) void k_cc_merge(Geom g, int kind, const int* bond_first,
                                                          const uint8_t* bocc,
                                                          const uint8_t* socc, int* parent,
@@ -500,8 +503,22 @@ __global__ __launch_bounds__(kCcThreads) void k_cc_merge(Geom g, int kind, const
     }
     if (want && kind == PERC_BOND) member[q] = 1;
     const int a = want ? parent[s] : -1, b = want ? parent[q] : -1;
-    const int pa = __shfl_up(a, 1, 64), pb = __shfl_up(b, 1, 64);
-    if (want && !(lane > 0 && pa == a && pb == b)) unite(parent, a, b);
+    if constexpr (WD) {
+      const int lo = min(a, b), hi = max(a, b);
+      bool lead = want && lo != hi;
+      unsigned long long act = __ballot(lead);
+      while (act) {
+        const int l = __builtin_ctzll(act);
+        const int la = __shfl(lo, l, 64), lh = __shfl(hi, l, 64);
+        const bool same = lead && lo == la && hi == lh;
+        act &= ~__ballot(same);
+        if (same && lane != l) lead = false;
+      }
+      if (lead) unite(parent, lo, hi);
+    } else {
+      const int pa = __shfl_up(a, 1, 64), pb = __shfl_up(b, 1, 64);
+      if (want && !(lane > 0 && pa == a && pb == b)) unite(parent, a, b);
+    }
   }
 }
 

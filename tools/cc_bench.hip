@@ -192,6 +192,14 @@ int main(int argc, char** argv) {
   chain("tile_w<64>", [&]() { k_cc_tile_w<64><<<cdiv(g.m, kCcW) * cdiv(g.n, 64), 64>>>(g, PERC_BOND, R.bf, R.bocc, R.socc,
                                                                                        R.parent, R.member, 1); },
         merge_for(std::integral_constant<int, 64>{}), false);
+  // the merge's unions deduplicated over the whole wave
+  {
+    const int nseg = cdiv(g.m, kCcThreads), nfull = g.n / 16, ncand = 2 * cdiv(g.m, kCcW) + 1;
+    chain("tile_w<16, u16> + merge wave-dedup", [&]() { k_cc_tile_w<16, true><<<cdiv(g.m, kCcW) * cdiv(g.n, 16), 64>>>(
+                                                        g, PERC_BOND, R.bf, R.bocc, R.socc, R.parent, R.member, 1); },
+          [&, nseg, nfull, ncand]() { k_cc_merge<16, true><<<nfull * nseg + ncand * cdiv(g.n, kCcThreads), kCcThreads>>>(
+                                          g, PERC_BOND, R.bf, R.bocc, R.socc, R.parent, R.member, nseg, nfull); }, false);
+  }
   // run nodes and member flags kept in registers (no provisional store, no re-read)
   chain("tile_w<16, u16, nreg>", [&]() { k_cc_tile_w<16, true, true><<<cdiv(g.m, kCcW) * cdiv(g.n, 16), 64>>>(
                                             g, PERC_BOND, R.bf, R.bocc, R.socc, R.parent, R.member, 1); },
