@@ -293,14 +293,10 @@ struct TileUF {
   }
 };
 
-// NREG: the rows' run nodes and member flags kept in registers (packed,
-// the loop over the rows unrolled) instead of a provisional parent / member
-// store and a re-read of it in the last pass
-template <int H, bool P16 = false, bool NREG = false>
+template <int H, bool P16 = false>
 __global__ __launch_bounds__(64) void k_cc_tile_w(Geom g, int kind, const int* bond_first, const uint8_t* bocc,
                                                   const uint8_t* socc, int* parent, uint8_t* member,
                                                   int bf_closed) {
-  static_assert(!NREG || H <= 32, "member flags: a row per bit of one word");
   __shared__ int uf_mem[P16 ? kCcW * H / 2 : kCcW * H];
   const TileUF<P16> uf{uf_mem};
   const int ntx = cdiv(g.m, kCcW);
@@ -338,7 +334,6 @@ __global__ __launch_bounds__(64) void k_cc_tile_w(Geom g, int kind, const int* b
   };
   unsigned R[2], U[2], O[2], Rn[2], Un[2], On[2], Up[2] = {0u, 0u};
   int labp[2] = {0, 0};
-  unsigned nodes[NREG ? H : 1], Mb[2] = {0u, 0u};
   load_row(0, R, U, O);
   const unsigned long long le = lane == 63 ? ~0ull : ((2ull << lane) - 1ull);
   auto row_step = [&](int r) {
@@ -388,16 +383,11 @@ __global__ __launch_bounds__(64) void k_cc_tile_w(Geom g, int kind, const int* b
       const bool lft = h ? left1 : left0;
       const bool mem = kind == PERC_BOND ? (R[h] | U[h] | (lft ? 1u : 0u) | (r > 0 ? Up[h] : 0u)) != 0u
                                          : O[h] != 0u;
-      if constexpr (NREG) {
-        Mb[h] |= (mem ? 1u : 0u) << r;
-        continue;
-      }
       if (!v) continue;
       const int lc = lane + 64 * h, s = (r0 + r) * g.m + c0 + lc + 1;
       parent[s] = node[h];
       member[s] = mem ? 1 : 0;
     }
-    if constexpr (NREG) nodes[r] = (unsigned)node[0] | (unsigned)node[1] << 16;
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       labp[h] = node[h];
@@ -407,13 +397,7 @@ __global__ __launch_bounds__(64) void k_cc_tile_w(Geom g, int kind, const int* b
       O[h] = On[h];
     }
   };
-  if constexpr (NREG) {
-#pragma unroll
-    for (int r = 0; r < H; ++r)
-      if (r < th) row_step(r);
-  } else {
-    for (int r = 0; r < th; ++r) row_step(r);
-  }
+  for (int r = 0; r < th; ++r) row_step(r);
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -425,28 +409,13 @@ __global__ __launch_bounds__(64) void k_cc_tile_w(Geom g, int kind, const int* b
     }
     return (r0 + x / kCcW) * g.m + c0 + x % kCcW + 1;
   };
-  if constexpr (NREG) {
+  for (int r = 0; r < th; ++r) {
 #pragma unroll
-    for (int r = 0; r < H; ++r) {
-      if (r >= th) continue;
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const int lc = lane + 64 * h;
-        if (lc >= tw) continue;
-        const int s = (r0 + r) * g.m + c0 + lc + 1;
-        parent[s] = root_of((int)(nodes[r] >> (16 * h) & 0xffffu));
-        member[s] = (uint8_t)(Mb[h] >> r & 1u);
-      }
-    }
-  } else {
-    for (int r = 0; r < th; ++r) {
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const int lc = lane + 64 * h;
-        if (lc >= tw) continue;
-        const int s = (r0 + r) * g.m + c0 + lc + 1;
-        parent[s] = root_of(parent[s]);
-      }
+    for (int h = 0; h < 2; ++h) {
+      const int lc = lane + 64 * h;
+      if (lc >= tw) continue;
+      const int s = (r0 + r) * g.m + c0 + lc + 1;
+      parent[s] = root_of(parent[s]);
     }
   }
 }
@@ -466,8 +435,11 @@ __global__ __launch_bounds__(64) void k_cc_tile_w(Geom g, int kind, const int* b
 // 0.512 ms per realisation at L = 4096, profiles/r4_4_label_ab_L4096.json.)
 // WD: the wave's unions deduplicated over all its lanes, the pairs taken as
 // (min, max) -- one union per distinct pair of parents in the wave, by the
-// pair's first lane (one ballot round per distinct pair)
-template <int TH = kCcH, bool WD = false>  // TH: block height of the tile kernel that ran before
+// pair's first lane (one ballot round per distinct pair); else only a lane
+// whose pair equals the previous lane's skips.  Along a block edge most
+// crossing links join the same few block components, so most lanes drop out:
+// merge 47.4 vs 83.6 us at L = 4096 (profiles/r4_11_cc_bench_L4096.txt)
+template <int TH = kCcH, bool WD = true>  // TH: block height of the tile kernel that ran before
 __global__ __launch_bounds__(kCcThreads) void k_cc_merge(Geom g, int kind, const int* bond_first,
                                                          const uint8_t* bocc,
                                                          const uint8_t* socc, int* parent,

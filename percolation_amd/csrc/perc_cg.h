@@ -180,26 +180,18 @@ __global__ __launch_bounds__(kBlock) void k_cg_p(CGArgs a) {
   }
 }
 
-// S(k): q = A p and akden = q.p, then ak = bknum/akden.  SL = 0: CSR,
-// SL = 4 / 6: stencil operator with that many slots per row.
-template <int SL, int NS = 0>  // NS: CSR slots (SL = 0)
+// S(k) on the stencil operator (SL = 4 / 6 slots per row): q = A p and
+// akden = q.p, then ak = bknum/akden
+template <int SL>
 __global__ __launch_bounds__(kBlock) void k_cg_spmv(CGArgs a) {
   CGScalars* S = a.S;
   if (S->done) return;
-  __shared__ double s_prod[SL ? 1 : kWaves][SL ? 1 : 64 * kMaxNnzRow];
   __shared__ int s_off[kMaxForms * kMaxSlots];
   __shared__ double s_red[32];
   __shared__ int s_flag[2];
   double dot[1] = {0.0};
-  if (SL) {
-    load_forms(a.St.F, s_off);
-    st_block<SL ? SL : 4, true>(a.St, s_off, a.p, a.q, &dot[0]);
-  } else {
-    const int wid = threadIdx.x >> 6;
-    int t0, t1;
-    block_tiles(a.A.N, &t0, &t1);
-    spmv_tiles_any<true, NS>(a.A, a.p, a.q, t0 + wid, t1, kWaves, s_prod[SL ? 0 : wid], &dot[0]);
-  }
+  load_forms(a.St.F, s_off);
+  st_block<SL, true>(a.St, s_off, a.p, a.q, &dot[0]);
   double tot[1];
   if (publish_and_reduce<1>(dot, a.partials, a.tickets, xcd_logical_block(blockIdx.x, gridDim.x),
                             gridDim.x, tot, s_red, s_flag)) {
@@ -213,7 +205,7 @@ __global__ __launch_bounds__(kBlock) void k_cg_spmv(CGArgs a) {
 // S(k) on CSR with one row per thread (k_spmv's row, bitwise dsprsax): q(i)
 // and q(i) p(i), summed per workgroup, then the grid-wide reduction; grid
 // cdiv(N, kBlock) (perc_ctx::row_grid).  Against the LDS-staged wave tiles
-// of k_cg_spmv<0, NS>: see DESIGN §4 (CSR).
+// it replaced: 0.294 vs 0.299 ms at L = 4096 (profiles/r4_11_csr_row_ab_L4096.json).
 template <int NS>
 __global__ __launch_bounds__(kBlock) void k_cg_spmv_row(CGArgs a) {
   CGScalars* S = a.S;

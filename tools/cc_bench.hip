@@ -192,24 +192,14 @@ int main(int argc, char** argv) {
   chain("tile_w<64>", [&]() { k_cc_tile_w<64><<<cdiv(g.m, kCcW) * cdiv(g.n, 64), 64>>>(g, PERC_BOND, R.bf, R.bocc, R.socc,
                                                                                        R.parent, R.member, 1); },
         merge_for(std::integral_constant<int, 64>{}), false);
-  // the merge's unions deduplicated over the whole wave
+  // the merge's unions deduplicated only against the previous lane (WD = false)
   {
     const int nseg = cdiv(g.m, kCcThreads), nfull = g.n / 16, ncand = 2 * cdiv(g.m, kCcW) + 1;
-    chain("tile_w<16, u16> + merge wave-dedup", [&]() { k_cc_tile_w<16, true><<<cdiv(g.m, kCcW) * cdiv(g.n, 16), 64>>>(
+    chain("tile_w<16, u16> + merge lane-pair dedup", [&]() { k_cc_tile_w<16, true><<<cdiv(g.m, kCcW) * cdiv(g.n, 16), 64>>>(
                                                         g, PERC_BOND, R.bf, R.bocc, R.socc, R.parent, R.member, 1); },
-          [&, nseg, nfull, ncand]() { k_cc_merge<16, true><<<nfull * nseg + ncand * cdiv(g.n, kCcThreads), kCcThreads>>>(
+          [&, nseg, nfull, ncand]() { k_cc_merge<16, false><<<nfull * nseg + ncand * cdiv(g.n, kCcThreads), kCcThreads>>>(
                                           g, PERC_BOND, R.bf, R.bocc, R.socc, R.parent, R.member, nseg, nfull); }, false);
   }
-  // run nodes and member flags kept in registers (no provisional store, no re-read)
-  chain("tile_w<16, u16, nreg>", [&]() { k_cc_tile_w<16, true, true><<<cdiv(g.m, kCcW) * cdiv(g.n, 16), 64>>>(
-                                            g, PERC_BOND, R.bf, R.bocc, R.socc, R.parent, R.member, 1); },
-        merge_for(std::integral_constant<int, 16>{}), false);
-  chain("tile_w<16, u32, nreg>", [&]() { k_cc_tile_w<16, false, true><<<cdiv(g.m, kCcW) * cdiv(g.n, 16), 64>>>(
-                                            g, PERC_BOND, R.bf, R.bocc, R.socc, R.parent, R.member, 1); },
-        merge_for(std::integral_constant<int, 16>{}), false);
-  chain("tile_w<32, u16, nreg>", [&]() { k_cc_tile_w<32, true, true><<<cdiv(g.m, kCcW) * cdiv(g.n, 32), 64>>>(
-                                            g, PERC_BOND, R.bf, R.bocc, R.socc, R.parent, R.member, 1); },
-        merge_for(std::integral_constant<int, 32>{}), false);
   // compress: U sites per thread chased in lockstep (production: kCcCompressU), one site per thread
   chain_c("tile_w<16, u16> + compress<1>", [&]() { k_cc_tile_w<16, true><<<cdiv(g.m, kCcW) * cdiv(g.n, 16), 64>>>(
                                                       g, PERC_BOND, R.bf, R.bocc, R.socc, R.parent, R.member, 1); },
@@ -234,9 +224,6 @@ int main(int argc, char** argv) {
       k_cc_tile_w<kCcH, true><<<R.tiles, 64>>>(g, kind, R.bf, R.bocc, R.socc, R.parent, R.member, 1);
       CK(hipDeviceSynchronize());
       same(R, kind == PERC_SITE ? "k_cc_tile_w u16, site kind" : "k_cc_tile_w u16, mixed kind");
-      k_cc_tile_w<kCcH, true, true><<<R.tiles, 64>>>(g, kind, R.bf, R.bocc, R.socc, R.parent, R.member, 1);
-      CK(hipDeviceSynchronize());
-      same(R, kind == PERC_SITE ? "k_cc_tile_w u16 nreg, site" : "k_cc_tile_w u16 nreg, mixed");
     }
   }
   return 0;
