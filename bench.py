@@ -314,6 +314,27 @@ def rocprof_base(key, fmt, minfo):
     return base_name(names[0]) if names else None
 
 
+def rocprof_avg(base, L_):
+    """average duration (ms) of kernel `base` in the newest committed
+    rocprofv3 --kernel-trace --stats summary of this lattice size
+    (profiles/*_rocprof_stats_L<L>.csv) and its path: the cross-check of the
+    live event timing, whose brackets include the dispatch gap before each
+    launch.  (None, None) if absent."""
+    import csv
+    import glob
+    files = sorted(glob.glob(os.path.join(REPO, "profiles", "*_rocprof_stats_L%d.csv" % L_)),
+                   key=lambda f: [int(t) if t.isdigit() else t for t in re.split(r"(\d+)", os.path.basename(f))],
+                   reverse=True)
+    for f in files if base else ():
+        with open(f) as fh:
+            for r in csv.DictReader(fh):
+                name = r.get("Name") or ""
+                i = name.find(base)
+                if i >= 0 and name[i + len(base):i + len(base) + 1] in (",", ">"):
+                    return float(r["AverageNs"]) / 1e6, os.path.relpath(f, REPO)
+    return None, None
+
+
 # reconcile summaries before r2_17 name kernels without template arguments;
 # the kernels they measured
 OLD_RECONCILE = {"k_cg_march": "k_cg_march<0", "k_cg_b": "k_cg_b<true"}
@@ -768,6 +789,7 @@ def main():
     # the roofline line is the kernel with the most device time
     dom = max(kern, key=lambda k_: kern[k_]["total_ms"])
     traffic, traffic_src = pmc_traffic(rocprof_base(dom, fmt, minfo), L_)
+    rp_ms, rp_src = rocprof_avg(rocprof_base(dom, fmt, minfo), L_)
     achieved = kern[dom]["gbs"] or 0.0  # 0: no realisation spanned, nothing solved
     iter_ms = sum(v["avg_launch_ms"] for v in kern.values())
     iter_bytes = sum(v["bytes_per_launch"] for v in kern.values())
@@ -838,6 +860,13 @@ def main():
                      "achievable": stream_copy["gbs"],
                      "frac_of_achievable": round(achieved / stream_copy["gbs"], 4),
                      "traffic": traffic, "traffic_source": traffic_src,
+                     "avg_launch_ms_rocprof": rp_ms, "rocprof_source": rp_src,
+                     "timing_note": "avg_launch_ms: every 8th launch timed live by its own "
+                                    "dispatch timestamps (hipExtLaunchKernel events on the "
+                                    "context stream); a timed launch carries the events' "
+                                    "cache write-back, so it reads a few % above the "
+                                    "kernel-trace average of all launches "
+                                    "(avg_launch_ms_rocprof, committed rocprofv3 --stats)",
                      "kernel": kern[dom]["kernel"], "format": fmt,
                      "bytes_per_launch": kern[dom]["bytes_per_launch"],
                      "avg_launch_ms": kern[dom]["avg_launch_ms"],
