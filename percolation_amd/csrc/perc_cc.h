@@ -260,13 +260,18 @@ __global__ __launch_bounds__(kCcThreads) void k_cc_tile(Geom g, int kind, const 
 template <bool P16>
 struct TileUF {
   int* w;  // P16: kCcW * H / 2 words holding two entries each
+  // relaxed wavefront-scope atomic accesses: every access is performed (other
+  // lanes move entries under a find), and none waits for the wave's global
+  // loads in flight (a volatile access waited for vmcnt(0) and lgkmcnt(0))
   __device__ int get(int x) const {
-    if (P16) return reinterpret_cast<const volatile unsigned short*>(w)[x];
-    return reinterpret_cast<const volatile int*>(w)[x];
+    if (P16) return __hip_atomic_load(reinterpret_cast<unsigned short*>(w) + x, __ATOMIC_RELAXED,
+                                      __HIP_MEMORY_SCOPE_WAVEFRONT);
+    return __hip_atomic_load(w + x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
   }
   __device__ void set(int x, int v) const {
-    if (P16) reinterpret_cast<volatile unsigned short*>(w)[x] = (unsigned short)v;
-    else reinterpret_cast<volatile int*>(w)[x] = v;
+    if (P16) __hip_atomic_store(reinterpret_cast<unsigned short*>(w) + x, (unsigned short)v, __ATOMIC_RELAXED,
+                                __HIP_MEMORY_SCOPE_WAVEFRONT);
+    else __hip_atomic_store(w + x, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
   }
   // set x's parent to b if it is still a; returns what it found (a: done)
   __device__ int cas(int a, int b) const {
@@ -274,7 +279,7 @@ struct TileUF {
     unsigned* word = reinterpret_cast<unsigned*>(w) + (a >> 1);
     const int sh = (a & 1) * 16;
     while (true) {
-      const unsigned old = *reinterpret_cast<volatile unsigned*>(word);
+      const unsigned old = __hip_atomic_load(word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
       const int cur = (int)((old >> sh) & 0xffffu);
       if (cur != a) return cur;
       const unsigned nw = (old & ~(0xffffu << sh)) | ((unsigned)b << sh);
@@ -416,6 +421,165 @@ __global__ __launch_bounds__(64) void k_cc_tile_w(Geom g, int kind, const int* b
       if (lc >= tw) continue;
       const int s = (r0 + r) * g.m + c0 + lc + 1;
       parent[s] = root_of(parent[s]);
+    }
+  }
+}
+
+// wave-level LDS order: a wave's LDS instructions execute in program order,
+// so lanes see each other's earlier LDS stores once the compiler keeps the
+// order -- no memory fence (a release fence would also wait for the
+// prefetched global loads, vmcnt(0), every row)
+__device__ __forceinline__ void wave_lds_order() {
+  __builtin_amdgcn_wave_barrier();
+  asm volatile("" ::: "memory");
+}
+
+// forward bond id of site (row, col) of the open square lattice in the
+// reference's bond order (bondc.f:137-154): rows 0..n-2 bf_square, the top
+// row's right links after them (perc_ctx::bf_closed checks both)
+__device__ __forceinline__ int bf_open_square(const Geom& g, int row, int col) {
+  return row <= g.n - 2 ? bf_square(g, row, col) : (g.n - 1) * (2 * g.m - 1) + col;
+}
+
+// k_cc_tile_v: k_cc_tile_w for the open square lattice with a closed-form
+// bond order, the occupancy kind a template parameter: every load of a row
+// unconditional (buffer loads, out-of-range offsets where a link does not
+// exist), issued one row ahead and waited for once; no fences in the walk
+// (wave_lds_order); the run nodes and member flags of the block's rows kept
+// in registers, so the last pass writes every site's root without reading
+// a provisional parent back.  The same unions in the same order as
+// k_cc_tile_w<H, true>: the same parents and members.
+template <int H, int KIND, int D = 4>  // D: rows whose loads are in flight
+__global__ __launch_bounds__(64) void k_cc_tile_v(Geom g, const uint8_t* bocc, const uint8_t* socc, int* parent,
+                                                  uint8_t* member, unsigned nb_bytes) {
+  static_assert(H <= 32, "member flags: a row per bit of one word");
+  __shared__ int uf_mem[kCcW * H / 2];
+  const TileUF<true> uf{uf_mem};
+  const int ntx = cdiv(g.m, kCcW);
+  const int tb = xcd_logical_block(blockIdx.x, gridDim.x);
+  const int tx = tb % ntx, ty = tb / ntx;
+  const int c0 = tx * kCcW, r0 = ty * H;
+  const int tw = min(kCcW, g.m - c0), th = min(H, g.n - r0);
+  const int lane = threadIdx.x;
+  const __amdgpu_buffer_rsrc_t rb = rsrc(bocc, nb_bytes), rs = rsrc(socc, (unsigned)g.t + 8u);
+  auto ld8 = [](__amdgpu_buffer_rsrc_t r, bool ok, unsigned off) {
+    return (unsigned)__builtin_amdgcn_raw_buffer_load_b8(r, (int)(ok ? off : kOOB), 0, 0);
+  };
+  // R / U: the link right / up of the lane's two sites; O: the site occupied
+  auto load_row = [&](int r, unsigned (&R)[2], unsigned (&U)[2], unsigned (&O)[2]) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int lc = lane + 64 * h, col = c0 + lc, row = r0 + r;
+      const bool v = lc < tw && r < th;
+      const int s = row * g.m + col + 1;
+      const bool hr = v && col < g.m - 1, hu = v && row < g.n - 1;
+      if constexpr (KIND == PERC_SITE) {
+        O[h] = ld8(rs, v, (unsigned)s);
+        R[h] = ld8(rs, hr, (unsigned)s + 1u);
+        U[h] = ld8(rs, hu, (unsigned)(s + g.m));
+      } else {
+        const int fb = bf_open_square(g, row, col);
+        R[h] = ld8(rb, hr, (unsigned)fb);
+        U[h] = ld8(rb, hu, (unsigned)fb + (col < g.m - 1 ? 1u : 0u));
+        O[h] = 1u;
+        if constexpr (KIND != PERC_BOND) {
+          O[h] = ld8(rs, v, (unsigned)s);
+          R[h] &= ld8(rs, hr, (unsigned)s + 1u);
+          U[h] &= ld8(rs, hu, (unsigned)(s + g.m));
+        }
+      }
+    }
+  };
+  auto finish = [&](unsigned (&R)[2], unsigned (&U)[2], unsigned (&O)[2]) {
+    if constexpr (KIND != PERC_BOND) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        R[h] = O[h] ? R[h] : 0u;
+        U[h] = O[h] ? U[h] : 0u;
+      }
+    }
+  };
+  unsigned Rq[D][2], Uq[D][2], Oq[D][2], R[2], U[2], O[2], Up[2] = {0u, 0u};
+  int labp[2] = {0, 0};
+  unsigned nodes[H], Mb[2] = {0u, 0u};
+#pragma unroll
+  for (int d = 0; d < D; ++d) load_row(d, Rq[d], Uq[d], Oq[d]);
+  const unsigned long long le = lane == 63 ? ~0ull : ((2ull << lane) - 1ull);
+  const bool v0 = lane < tw, v1 = lane + 64 < tw;
+#pragma unroll
+  for (int r = 0; r < H; ++r) {
+    nodes[r] = 0u;
+    if (r >= th) continue;  // (uniform)
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      R[h] = Rq[r % D][h];
+      U[h] = Uq[r % D][h];
+      O[h] = Oq[r % D][h];
+    }
+    finish(R, U, O);
+    load_row(r + D, Rq[r % D], Uq[r % D], Oq[r % D]);  // (past th: nothing loaded)
+    const unsigned rl0 = __shfl(R[0], (lane + 63) & 63, 64), rl1 = __shfl(R[1], (lane + 63) & 63, 64);
+    const bool left0 = lane > 0 && rl0, left1 = lane > 0 ? rl1 != 0u : rl0 != 0u;
+    const unsigned long long lo = __ballot(!left0 || !v0), hi = __ballot(!left1 || !v1);
+    int node[2];
+    node[0] = r * kCcW + 63 - __clzll((long long)(lo & le));
+    const unsigned long long hm = hi & le;
+    node[1] = r * kCcW + (hm ? 64 + 63 - __clzll((long long)hm) : 63 - __clzll((long long)lo));
+    if (v0 && !left0) uf.set(node[0], node[0]);
+    if (v1 && !left1) uf.set(node[1], node[1]);
+    wave_lds_order();
+    const bool w0 = r > 0 && v0 && Up[0], w1 = r > 0 && v1 && Up[1];
+    const int a0 = w0 ? node[0] : -1, b0 = w0 ? labp[0] : -1, a1 = w1 ? node[1] : -1, b1 = w1 ? labp[1] : -1;
+    const int pa0 = __shfl(a0, (lane + 63) & 63, 64), pb0 = __shfl(b0, (lane + 63) & 63, 64);
+    const int pa1 = __shfl(a1, (lane + 63) & 63, 64), pb1 = __shfl(b1, (lane + 63) & 63, 64);
+    const bool sk0 = lane > 0 && pa0 == a0 && pb0 == b0;
+    const bool sk1 = lane > 0 ? (pa1 == a1 && pb1 == b1) : (pa0 == a1 && pb0 == b1);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const bool w = h ? w1 && !sk1 : w0 && !sk0;
+      if (!w) continue;
+      int a = h ? a1 : a0, b = h ? b1 : b0;
+      while (true) {
+        a = uf.find(a);
+        b = uf.find(b);
+        if (a == b) break;
+        if (a < b) { const int t = a; a = b; b = t; }
+        const int old = uf.cas(a, b);
+        if (old == a) break;
+        a = old;
+      }
+    }
+    wave_lds_order();
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const bool lft = h ? left1 : left0;
+      const bool mem = KIND == PERC_BOND ? (R[h] | U[h] | (lft ? 1u : 0u) | (r > 0 ? Up[h] : 0u)) != 0u
+                                         : O[h] != 0u;
+      Mb[h] |= (mem ? 1u : 0u) << r;
+    }
+    nodes[r] = (unsigned)node[0] | (unsigned)node[1] << 16;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      labp[h] = node[h];
+      Up[h] = U[h];
+    }
+  }
+  wave_lds_order();
+#pragma unroll
+  for (int r = 0; r < H; ++r) {
+    if (r >= th) continue;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int lc = lane + 64 * h;
+      if (lc >= tw) continue;
+      const int s = (r0 + r) * g.m + c0 + lc + 1;
+      int x = (int)(nodes[r] >> (16 * h) & 0xffffu), p = uf.get(x);
+      while (p != x) {
+        x = p;
+        p = uf.get(x);
+      }
+      parent[s] = (r0 + x / kCcW) * g.m + c0 + x % kCcW + 1;
+      member[s] = (uint8_t)(Mb[h] >> r & 1u);
     }
   }
 }

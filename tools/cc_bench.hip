@@ -130,6 +130,11 @@ int main(int argc, char** argv) {
   CK(hipMemset(R.parent, 0, ((size_t)g.t + 2) * 4));
   tw32();
   CK(hipDeviceSynchronize());
+  k_cc_tile_v<kCcH, PERC_BOND><<<R.tiles, 64>>>(g, R.bocc, R.socc, R.parent, R.member, (unsigned)nb + 8u);
+  CK(hipDeviceSynchronize());
+  same(R, "k_cc_tile_v (same blocks)");
+  tw32();
+  CK(hipDeviceSynchronize());
   if (same(R, "k_cc_tile_w (same blocks)"))
     std::printf("  tile: production %.1f us, k_cc_tile_w %.1f us\n", t_tile * 1e3, time_ms(tw32, reps) * 1e3);
   // whole chains (tile, merge, compress): the final parents are the partition's
@@ -200,6 +205,19 @@ int main(int argc, char** argv) {
           [&, nseg, nfull, ncand]() { k_cc_merge<16, false><<<nfull * nseg + ncand * cdiv(g.n, kCcThreads), kCcThreads>>>(
                                           g, PERC_BOND, R.bf, R.bocc, R.socc, R.parent, R.member, nseg, nfull); }, false);
   }
+  // branch-free row loads, no fences, run nodes in registers (k_cc_tile_v)
+  chain("tile_v<16> (bond)", [&]() { k_cc_tile_v<16, PERC_BOND><<<cdiv(g.m, kCcW) * cdiv(g.n, 16), 64>>>(
+                                       g, R.bocc, R.socc, R.parent, R.member, (unsigned)nb + 8u); },
+        merge_for(std::integral_constant<int, 16>{}), false);
+  chain("tile_v<16, D 2> (bond)", [&]() { k_cc_tile_v<16, PERC_BOND, 2><<<cdiv(g.m, kCcW) * cdiv(g.n, 16), 64>>>(
+                                       g, R.bocc, R.socc, R.parent, R.member, (unsigned)nb + 8u); },
+        merge_for(std::integral_constant<int, 16>{}), false);
+  chain("tile_v<16, D 8> (bond)", [&]() { k_cc_tile_v<16, PERC_BOND, 8><<<cdiv(g.m, kCcW) * cdiv(g.n, 16), 64>>>(
+                                       g, R.bocc, R.socc, R.parent, R.member, (unsigned)nb + 8u); },
+        merge_for(std::integral_constant<int, 16>{}), false);
+  chain("tile_v<32> (bond)", [&]() { k_cc_tile_v<32, PERC_BOND><<<cdiv(g.m, kCcW) * cdiv(g.n, 32), 64>>>(
+                                       g, R.bocc, R.socc, R.parent, R.member, (unsigned)nb + 8u); },
+        merge_for(std::integral_constant<int, 32>{}), false);
   // compress: U sites per thread chased in lockstep (production: kCcCompressU), one site per thread
   chain_c("tile_w<16, u16> + compress<1>", [&]() { k_cc_tile_w<16, true><<<cdiv(g.m, kCcW) * cdiv(g.n, 16), 64>>>(
                                                       g, PERC_BOND, R.bf, R.bocc, R.socc, R.parent, R.member, 1); },
@@ -224,6 +242,12 @@ int main(int argc, char** argv) {
       k_cc_tile_w<kCcH, true><<<R.tiles, 64>>>(g, kind, R.bf, R.bocc, R.socc, R.parent, R.member, 1);
       CK(hipDeviceSynchronize());
       same(R, kind == PERC_SITE ? "k_cc_tile_w u16, site kind" : "k_cc_tile_w u16, mixed kind");
+      if (kind == PERC_SITE)
+        k_cc_tile_v<kCcH, PERC_SITE><<<R.tiles, 64>>>(g, R.bocc, R.socc, R.parent, R.member, (unsigned)nb + 8u);
+      else
+        k_cc_tile_v<kCcH, PERC_SITEBOND><<<R.tiles, 64>>>(g, R.bocc, R.socc, R.parent, R.member, (unsigned)nb + 8u);
+      CK(hipDeviceSynchronize());
+      same(R, kind == PERC_SITE ? "k_cc_tile_v, site kind" : "k_cc_tile_v, mixed kind");
     }
   }
   return 0;
