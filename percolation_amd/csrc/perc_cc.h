@@ -42,7 +42,7 @@ __device__ __forceinline__ int wave_sum_int(int v) {
 #endif
 constexpr int kCcW = 128, kCcH = PERC_CC_H, kCcSites = kCcW * kCcH, kCcThreads = 256;
 constexpr int kReduceGrid = 1024;  // fixed grid of the counting passes
-constexpr int kCcWaveH = 16;       // block height of k_cc_tile_w (the square lattice without pbc)
+constexpr int kCcWaveH = 16;       // block height of k_cc_tile_w (the open square lattice)
 
 
 __device__ __forceinline__ int find_root(int* parent, int x) {
@@ -245,15 +245,15 @@ __global__ __launch_bounds__(kCcThreads) void k_cc_tile(Geom g, int kind, const 
   }
 }
 
-// k_cc_tile_w: one wave per tile, rows walked bottom to top.  Lane l owns the
-// tile's columns l and l + 64.  Per row: the row's links (right, up), its
-// horizontal runs by ballots (a run's node = its first site), the vertical
-// links down into the previous row united in an LDS union-find over run
-// nodes (larger root -> smaller, so a root is its component's minimum site;
-// a lane whose (run, run below) pair equals the column to its left skips
-// its union), the run node written as the provisional parent; a last pass
-// writes every site's root.  Square lattice, no pbc; kind as cc_link (bond:
-// member = any incident occupied bond; site / mixed: the occupied site).
+// k_cc_tile_w (below): one wave per 128 x H tile of the open square lattice,
+// rows walked bottom to top.  Lane l owns the tile's columns l and l + 64.
+// Per row: the row's links (right, up), its horizontal runs by ballots (a
+// run's node = its first site), the vertical links down into the previous
+// row united in an LDS union-find over run nodes (larger root -> smaller, so
+// a root is its component's minimum site; a lane whose (run, run below) pair
+// equals the column to its left skips its union); a last pass writes every
+// site's root.  Kind as cc_link (bond: member = any incident occupied bond;
+// site / mixed: the occupied site).
 // LDS union-find over tile nodes: 32-bit entries, or 16-bit ones (P16: half
 // the LDS, so twice the waves per CU; the root CAS is a 32-bit CAS on the
 // entry's word that leaves the other half as it finds it)
@@ -298,133 +298,6 @@ struct TileUF {
   }
 };
 
-template <int H, bool P16 = false>
-__global__ __launch_bounds__(64) void k_cc_tile_w(Geom g, int kind, const int* bond_first, const uint8_t* bocc,
-                                                  const uint8_t* socc, int* parent, uint8_t* member,
-                                                  int bf_closed) {
-  __shared__ int uf_mem[P16 ? kCcW * H / 2 : kCcW * H];
-  const TileUF<P16> uf{uf_mem};
-  const int ntx = cdiv(g.m, kCcW);
-  const int tb = xcd_logical_block(blockIdx.x, gridDim.x);
-  const int tx = tb % ntx, ty = tb / ntx;
-  const int c0 = tx * kCcW, r0 = ty * H;
-  const int tw = min(kCcW, g.m - c0), th = min(H, g.n - r0);
-  const int lane = threadIdx.x;
-  // R / U: the link right / up of each of the lane's two sites; O: the site occupied (site kinds)
-  auto load_row = [&](int r, unsigned (&R)[2], unsigned (&U)[2], unsigned (&O)[2]) {
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int lc = lane + 64 * h, col = c0 + lc, row = r0 + r;
-      const bool v = lc < tw && r < th;
-      const int s = row * g.m + col + 1;
-      const bool hr = v && col < g.m - 1, hu = v && row < g.n - 1;
-      if (kind == PERC_SITE) {
-        const unsigned o = v ? socc[s] : 0u;
-        O[h] = o;
-        R[h] = o && hr ? socc[s + 1] : 0u;
-        U[h] = o && hu ? socc[s + g.m] : 0u;
-        continue;
-      }
-      const int fb = !v ? 0 : bf_closed && row <= g.n - 2 ? bf_square(g, row, col) : bond_first[s];
-      R[h] = hr ? bocc[fb] : 0u;
-      U[h] = hu ? bocc[fb + (col < g.m - 1 ? 1 : 0)] : 0u;
-      O[h] = 1u;
-      if (kind != PERC_BOND) {  // mixed: the bond and both sites
-        const unsigned o = v ? socc[s] : 0u;
-        O[h] = o;
-        R[h] = R[h] && o && socc[s + 1];
-        U[h] = U[h] && o && socc[s + g.m];
-      }
-    }
-  };
-  unsigned R[2], U[2], O[2], Rn[2], Un[2], On[2], Up[2] = {0u, 0u};
-  int labp[2] = {0, 0};
-  load_row(0, R, U, O);
-  const unsigned long long le = lane == 63 ? ~0ull : ((2ull << lane) - 1ull);
-  auto row_step = [&](int r) {
-    load_row(r + 1, Rn, Un, On);  // (past th: nothing loaded)
-    // runs: column c has a left link iff c - 1 links right
-    const unsigned rl0 = __shfl(R[0], (lane + 63) & 63, 64), rl1 = __shfl(R[1], (lane + 63) & 63, 64);
-    const bool left0 = lane > 0 && rl0, left1 = lane > 0 ? rl1 != 0u : rl0 != 0u;  // (lane 0, half 1: column 63)
-    const bool v0 = lane < tw, v1 = lane + 64 < tw;
-    const unsigned long long lo = __ballot(!left0 || !v0), hi = __ballot(!left1 || !v1);
-    int node[2];
-    node[0] = r * kCcW + 63 - __clzll((long long)(lo & le));
-    const unsigned long long hm = hi & le;
-    node[1] = r * kCcW + (hm ? 64 + 63 - __clzll((long long)hm) : 63 - __clzll((long long)lo));
-    if (v0 && !left0) uf.set(node[0], node[0]);
-    if (v1 && !left1) uf.set(node[1], node[1]);
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    // vertical links down into row r - 1 (that row's up links)
-    const bool w0 = r > 0 && v0 && Up[0], w1 = r > 0 && v1 && Up[1];
-    const int a0 = w0 ? node[0] : -1, b0 = w0 ? labp[0] : -1, a1 = w1 ? node[1] : -1, b1 = w1 ? labp[1] : -1;
-    const int pa0 = __shfl(a0, (lane + 63) & 63, 64), pb0 = __shfl(b0, (lane + 63) & 63, 64);
-    const int pa1 = __shfl(a1, (lane + 63) & 63, 64), pb1 = __shfl(b1, (lane + 63) & 63, 64);
-    const bool sk0 = lane > 0 && pa0 == a0 && pb0 == b0;
-    const bool sk1 = lane > 0 ? (pa1 == a1 && pb1 == b1) : (pa0 == a1 && pb0 == b1);
-    // (lane 0, half 1: the column to the left is column 63 = lane 63, half 0: its pa0/pb0 came
-    // from lane 63 through the same shuffle)
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const bool w = h ? w1 && !sk1 : w0 && !sk0;
-      if (!w) continue;
-      int a = h ? a1 : a0, b = h ? b1 : b0;
-      while (true) {
-        a = uf.find(a);
-        b = uf.find(b);
-        if (a == b) break;
-        if (a < b) { const int t = a; a = b; b = t; }
-        const int old = uf.cas(a, b);
-        if (old == a) break;
-        a = old;
-      }
-    }
-    // provisional parents (run nodes) and member flags
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const bool v = h ? v1 : v0;
-      const bool lft = h ? left1 : left0;
-      const bool mem = kind == PERC_BOND ? (R[h] | U[h] | (lft ? 1u : 0u) | (r > 0 ? Up[h] : 0u)) != 0u
-                                         : O[h] != 0u;
-      if (!v) continue;
-      const int lc = lane + 64 * h, s = (r0 + r) * g.m + c0 + lc + 1;
-      parent[s] = node[h];
-      member[s] = mem ? 1 : 0;
-    }
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      labp[h] = node[h];
-      Up[h] = U[h];
-      R[h] = Rn[h];
-      U[h] = Un[h];
-      O[h] = On[h];
-    }
-  };
-  for (int r = 0; r < th; ++r) row_step(r);
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  auto root_of = [&](int x) {
-    int p = uf.get(x);
-    while (p != x) {
-      x = p;
-      p = uf.get(x);
-    }
-    return (r0 + x / kCcW) * g.m + c0 + x % kCcW + 1;
-  };
-  for (int r = 0; r < th; ++r) {
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int lc = lane + 64 * h;
-      if (lc >= tw) continue;
-      const int s = (r0 + r) * g.m + c0 + lc + 1;
-      parent[s] = root_of(parent[s]);
-    }
-  }
-}
-
 // wave-level LDS order: a wave's LDS instructions execute in program order,
 // so lanes see each other's earlier LDS stores once the compiler keeps the
 // order -- no memory fence (a release fence would also wait for the
@@ -441,16 +314,17 @@ __device__ __forceinline__ int bf_open_square(const Geom& g, int row, int col) {
   return row <= g.n - 2 ? bf_square(g, row, col) : (g.n - 1) * (2 * g.m - 1) + col;
 }
 
-// k_cc_tile_v: k_cc_tile_w for the open square lattice with a closed-form
-// bond order, the occupancy kind a template parameter: every load of a row
+// Row loads: the occupancy kind a template parameter, every load of a row
 // unconditional (buffer loads, out-of-range offsets where a link does not
-// exist), issued one row ahead and waited for once; no fences in the walk
-// (wave_lds_order); the run nodes and member flags of the block's rows kept
-// in registers, so the last pass writes every site's root without reading
-// a provisional parent back.  The same unions in the same order as
-// k_cc_tile_w<H, true>: the same parents and members.
-template <int H, int KIND, int D = 4>  // D: rows whose loads are in flight
-__global__ __launch_bounds__(64) void k_cc_tile_v(Geom g, const uint8_t* bocc, const uint8_t* socc, int* parent,
+// exist), D rows in flight (a ring refilled as rows are consumed); no
+// fences in the walk (wave_lds_order); the run nodes and member flags of
+// the block's rows kept in registers, so the last pass writes every site's
+// root without reading a provisional parent back.  Against the round-4
+// version with branchy per-row loads (each waited for at once), volatile
+// LDS entries, fences and provisional parents: tile 91.7 vs 123.8 us at
+// L = 4096 (profiles/r4_13_cc_bench_L4096.txt).
+template <int H, int KIND, int D = 2>  // D: rows whose loads are in flight
+__global__ __launch_bounds__(64) void k_cc_tile_w(Geom g, const uint8_t* bocc, const uint8_t* socc, int* parent,
                                                   uint8_t* member, unsigned nb_bytes) {
   static_assert(H <= 32, "member flags: a row per bit of one word");
   __shared__ int uf_mem[kCcW * H / 2];

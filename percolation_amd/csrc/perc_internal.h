@@ -164,6 +164,7 @@ struct perc_ctx {
   bool labeled = false;
   bool assembled = false;
   bool bf_closed = false;  // h_bond_first == bf_square on rows 0..n-2 (square lattice)
+  bool bf_open_sq = false; // and the open lattice's top row follows (bf_open_square)
   bool csr_ok = true;    // the CSR values / diagonal of the assembled system are written
   perc::AsmParams asm_p; // the assembly's parameters (ensure_csr re-runs it)
   int span_root = 0;

@@ -462,15 +462,17 @@ hipError_t dev_label(perc_ctx* h, int* nspan, int* span_list, int* nclusters) {
   DeviceBuffers& d = h->d;
   const int kind = h->last.kind;
   HIP_TRY(hipMemsetAsync(d.counters, 0, sizeof(int) * (8 + kMaxSpanList), st));
-  // square lattice without wrap links: one wave per 128 x 16 block walking
-  // its rows (k_cc_tile_w; labels 0.318 vs 0.361 ms of kernels at L = 4096,
-  // profiles/r4_5_cc_bench_L4096.txt), its union-find in 16-bit LDS entries
-  // (twice the resident waves: tile 126.2 vs 155.7 us, r4_7); else the LDS
+  // the open square lattice: one wave per 128 x 16 block walking its rows
+  // (k_cc_tile_w; tile 91.7 vs 190.6 us for the 128 x 32 LDS union-find
+  // blocks at L = 4096, profiles/r4_13_cc_bench_L4096.txt); else the LDS
   // union-find blocks
-  if (g.lattice == kSquare && !g.pbc && !std::getenv("PERC_TILE_TRACE")) {
+  if (g.lattice == kSquare && !g.pbc && h->bf_open_sq && !std::getenv("PERC_TILE_TRACE")) {
     constexpr int H = kCcWaveH;
-    k_cc_tile_w<H, true><<<cdiv(g.m, kCcW) * cdiv(g.n, H), 64, 0, st>>>(g, kind, d.bond_first, d.bocc, d.socc,
-                                                                   d.parent, d.member, (int)h->bf_closed);
+    const int G = cdiv(g.m, kCcW) * cdiv(g.n, H);
+    const unsigned nbb = (unsigned)h->nb + 8u;
+    if (kind == PERC_BOND) k_cc_tile_w<H, PERC_BOND><<<G, 64, 0, st>>>(g, d.bocc, d.socc, d.parent, d.member, nbb);
+    else if (kind == PERC_SITE) k_cc_tile_w<H, PERC_SITE><<<G, 64, 0, st>>>(g, d.bocc, d.socc, d.parent, d.member, nbb);
+    else k_cc_tile_w<H, PERC_SITEBOND><<<G, 64, 0, st>>>(g, d.bocc, d.socc, d.parent, d.member, nbb);
     HIP_TRY(dbg_sync(st, "k_cc_tile_w"));
     const int nseg = cdiv(g.m, kCcThreads), nfull = g.n / H, ncand = 2 * cdiv(g.m, kCcW) + 1;
     k_cc_merge<H><<<nfull * nseg + ncand * cdiv(g.n, kCcThreads), kCcThreads, 0, st>>>(

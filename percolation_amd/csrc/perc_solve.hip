@@ -199,6 +199,10 @@ hipError_t dev_build_lattice(perc_ctx* h) {
         h->bf_closed = false;
         break;
       }
+  // the open lattice's top row too (bf_open_square: the labeling wave tiles)
+  h->bf_open_sq = h->bf_closed && !g.pbc;
+  for (int c = 0; c + 1 < g.m && h->bf_open_sq; ++c)
+    if (h->h_bond_first[(size_t)(g.n - 1) * g.m + c + 1] != (g.n - 1) * (2 * g.m - 1) + c) h->bf_open_sq = false;
   // CSR pattern of the interior block
   int* rc = nullptr;
   HIP_TRY(dmalloc(&rc, N + 1));

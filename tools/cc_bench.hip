@@ -1,9 +1,10 @@
 // cc_bench.hip -- stand-alone A/B harness for the labeling kernels of
 // percolation_amd/csrc/perc_cc.h: one L x L square-lattice bond occupancy
-// (p, a fixed hash), the production k_cc_tile / k_cc_merge / k_cc_compress
-// timed with HIP events, and candidate tile kernels defined here checked
-// against the production tile kernel's output (parent and member arrays,
-// element by element) before they are timed.
+// (p, a fixed hash): the LDS union-find tiles (k_cc_tile, the triangular
+// and pbc lattices' labeling), the wave tiles (k_cc_tile_w, the open square
+// lattice's) at several shapes and the merge / compress variants, timed
+// with HIP events phase by phase; every chain's final parents and members
+// checked element by element against the LDS union-find chain's.
 //
 //   make -C tools cc_bench && ./tools/cc_bench 4096 0.6 20
 #include "perc_cc.h"
@@ -126,17 +127,15 @@ int main(int argc, char** argv) {
   CK(hipDeviceSynchronize());
   const double t_tile = time_ms([&]() { tile(R.parent, R.member); }, reps);
   same(R, "k_cc_tile (production)");
-  auto tw32 = [&]() { k_cc_tile_w<kCcH><<<R.tiles, 64>>>(g, PERC_BOND, R.bf, R.bocc, R.socc, R.parent, R.member, 1); };
+  // the wave tiles at the production kernel's block height, element by element
+  auto tw32 = [&]() {
+    k_cc_tile_w<kCcH, PERC_BOND><<<R.tiles, 64>>>(g, R.bocc, R.socc, R.parent, R.member, (unsigned)nb + 8u);
+  };
   CK(hipMemset(R.parent, 0, ((size_t)g.t + 2) * 4));
   tw32();
   CK(hipDeviceSynchronize());
-  k_cc_tile_v<kCcH, PERC_BOND><<<R.tiles, 64>>>(g, R.bocc, R.socc, R.parent, R.member, (unsigned)nb + 8u);
-  CK(hipDeviceSynchronize());
-  same(R, "k_cc_tile_v (same blocks)");
-  tw32();
-  CK(hipDeviceSynchronize());
   if (same(R, "k_cc_tile_w (same blocks)"))
-    std::printf("  tile: production %.1f us, k_cc_tile_w %.1f us\n", t_tile * 1e3, time_ms(tw32, reps) * 1e3);
+    std::printf("  tile: LDS union-find %.1f us, k_cc_tile_w %.1f us\n", t_tile * 1e3, time_ms(tw32, reps) * 1e3);
   // whole chains (tile, merge, compress): the final parents are the partition's
   // minimum sites whatever the blocks, so chains of other block heights compare too
   hipEvent_t e[4];
@@ -181,52 +180,32 @@ int main(int argc, char** argv) {
           g, PERC_BOND, R.bf, R.bocc, R.socc, R.parent, R.member, nseg, nfull);
     };
   };
-  chain("production", [&]() { tile(R.parent, R.member); }, merge_for(std::integral_constant<int, kCcH>{}), true);
-  chain("tile_w<32>", [&]() { k_cc_tile_w<32><<<cdiv(g.m, kCcW) * cdiv(g.n, 32), 64>>>(g, PERC_BOND, R.bf, R.bocc, R.socc,
-                                                                                       R.parent, R.member, 1); },
-        merge_for(std::integral_constant<int, 32>{}), false);
-  chain("tile_w<16>", [&]() { k_cc_tile_w<16><<<cdiv(g.m, kCcW) * cdiv(g.n, 16), 64>>>(g, PERC_BOND, R.bf, R.bocc, R.socc,
-                                                                                       R.parent, R.member, 1); },
-        merge_for(std::integral_constant<int, 16>{}), false);
-  chain("tile_w<32, u16>", [&]() { k_cc_tile_w<32, true><<<cdiv(g.m, kCcW) * cdiv(g.n, 32), 64>>>(
-                                      g, PERC_BOND, R.bf, R.bocc, R.socc, R.parent, R.member, 1); },
-        merge_for(std::integral_constant<int, 32>{}), false);
-  chain("tile_w<16, u16>", [&]() { k_cc_tile_w<16, true><<<cdiv(g.m, kCcW) * cdiv(g.n, 16), 64>>>(
-                                      g, PERC_BOND, R.bf, R.bocc, R.socc, R.parent, R.member, 1); },
-        merge_for(std::integral_constant<int, 16>{}), false);
-  chain("tile_w<64>", [&]() { k_cc_tile_w<64><<<cdiv(g.m, kCcW) * cdiv(g.n, 64), 64>>>(g, PERC_BOND, R.bf, R.bocc, R.socc,
-                                                                                       R.parent, R.member, 1); },
-        merge_for(std::integral_constant<int, 64>{}), false);
+  chain("LDS union-find 128 x 32", [&]() { tile(R.parent, R.member); }, merge_for(std::integral_constant<int, kCcH>{}),
+        true);
+  auto wave = [&](auto hconst, auto dconst) {
+    constexpr int H = decltype(hconst)::value, D = decltype(dconst)::value;
+    return [&]() {
+      k_cc_tile_w<H, PERC_BOND, D><<<cdiv(g.m, kCcW) * cdiv(g.n, H), 64>>>(g, R.bocc, R.socc, R.parent, R.member,
+                                                                          (unsigned)nb + 8u);
+    };
+  };
+  using I16 = std::integral_constant<int, 16>;
+  using I32 = std::integral_constant<int, 32>;
+  chain("wave 128 x 16 (production)", wave(I16{}, std::integral_constant<int, 2>{}), merge_for(I16{}), false);
+  chain("wave 128 x 16, 4 rows in flight", wave(I16{}, std::integral_constant<int, 4>{}), merge_for(I16{}), false);
+  chain("wave 128 x 32", wave(I32{}, std::integral_constant<int, 2>{}), merge_for(I32{}), false);
   // the merge's unions deduplicated only against the previous lane (WD = false)
   {
     const int nseg = cdiv(g.m, kCcThreads), nfull = g.n / 16, ncand = 2 * cdiv(g.m, kCcW) + 1;
-    chain("tile_w<16, u16> + merge lane-pair dedup", [&]() { k_cc_tile_w<16, true><<<cdiv(g.m, kCcW) * cdiv(g.n, 16), 64>>>(
-                                                        g, PERC_BOND, R.bf, R.bocc, R.socc, R.parent, R.member, 1); },
+    chain("wave 16 + merge lane-pair dedup", wave(I16{}, std::integral_constant<int, 2>{}),
           [&, nseg, nfull, ncand]() { k_cc_merge<16, false><<<nfull * nseg + ncand * cdiv(g.n, kCcThreads), kCcThreads>>>(
                                           g, PERC_BOND, R.bf, R.bocc, R.socc, R.parent, R.member, nseg, nfull); }, false);
   }
-  // branch-free row loads, no fences, run nodes in registers (k_cc_tile_v)
-  chain("tile_v<16> (bond)", [&]() { k_cc_tile_v<16, PERC_BOND><<<cdiv(g.m, kCcW) * cdiv(g.n, 16), 64>>>(
-                                       g, R.bocc, R.socc, R.parent, R.member, (unsigned)nb + 8u); },
-        merge_for(std::integral_constant<int, 16>{}), false);
-  chain("tile_v<16, D 2> (bond)", [&]() { k_cc_tile_v<16, PERC_BOND, 2><<<cdiv(g.m, kCcW) * cdiv(g.n, 16), 64>>>(
-                                       g, R.bocc, R.socc, R.parent, R.member, (unsigned)nb + 8u); },
-        merge_for(std::integral_constant<int, 16>{}), false);
-  chain("tile_v<16, D 8> (bond)", [&]() { k_cc_tile_v<16, PERC_BOND, 8><<<cdiv(g.m, kCcW) * cdiv(g.n, 16), 64>>>(
-                                       g, R.bocc, R.socc, R.parent, R.member, (unsigned)nb + 8u); },
-        merge_for(std::integral_constant<int, 16>{}), false);
-  chain("tile_v<32> (bond)", [&]() { k_cc_tile_v<32, PERC_BOND><<<cdiv(g.m, kCcW) * cdiv(g.n, 32), 64>>>(
-                                       g, R.bocc, R.socc, R.parent, R.member, (unsigned)nb + 8u); },
-        merge_for(std::integral_constant<int, 32>{}), false);
   // compress: U sites per thread chased in lockstep (production: kCcCompressU), one site per thread
-  chain_c("tile_w<16, u16> + compress<1>", [&]() { k_cc_tile_w<16, true><<<cdiv(g.m, kCcW) * cdiv(g.n, 16), 64>>>(
-                                                      g, PERC_BOND, R.bf, R.bocc, R.socc, R.parent, R.member, 1); },
-          merge_for(std::integral_constant<int, 16>{}),
+  chain_c("wave 16 + compress<1>", wave(I16{}, std::integral_constant<int, 2>{}), merge_for(I16{}),
           [&]() { k_cc_compress<1><<<std::min(cdiv(g.t, kCcThreads), kReduceGrid), kCcThreads>>>(
                       g.t, R.parent, R.member, R.counters); }, false);
-  chain_c("tile_w<16, u16> + compress<4>", [&]() { k_cc_tile_w<16, true><<<cdiv(g.m, kCcW) * cdiv(g.n, 16), 64>>>(
-                                                      g, PERC_BOND, R.bf, R.bocc, R.socc, R.parent, R.member, 1); },
-          merge_for(std::integral_constant<int, 16>{}),
+  chain_c("wave 16 + compress<4>", wave(I16{}, std::integral_constant<int, 2>{}), merge_for(I16{}),
           [&]() { k_cc_compress<4><<<std::min(cdiv(g.t, kCcThreads * 4), kReduceGrid), kCcThreads>>>(
                       g.t, R.parent, R.member, R.counters); }, false);
   // site and mixed kinds (sites occupied at 0.8 by another hash): the production tile kernel vs the candidate
@@ -236,18 +215,12 @@ int main(int argc, char** argv) {
     CK(hipMemcpy(R.socc, so.data(), so.size(), hipMemcpyHostToDevice));
     for (int kind : {PERC_SITE, PERC_SITEBOND}) {
       k_cc_tile<<<R.tiles, kCcThreads>>>(g, kind, R.bf, R.bocc, R.socc, R.parent_ref, R.member_ref, 1, nullptr);
-      k_cc_tile_w<kCcH><<<R.tiles, 64>>>(g, kind, R.bf, R.bocc, R.socc, R.parent, R.member, 1);
+      if (kind == PERC_SITE)
+        k_cc_tile_w<kCcH, PERC_SITE><<<R.tiles, 64>>>(g, R.bocc, R.socc, R.parent, R.member, (unsigned)nb + 8u);
+      else
+        k_cc_tile_w<kCcH, PERC_SITEBOND><<<R.tiles, 64>>>(g, R.bocc, R.socc, R.parent, R.member, (unsigned)nb + 8u);
       CK(hipDeviceSynchronize());
       same(R, kind == PERC_SITE ? "k_cc_tile_w, site kind" : "k_cc_tile_w, mixed kind");
-      k_cc_tile_w<kCcH, true><<<R.tiles, 64>>>(g, kind, R.bf, R.bocc, R.socc, R.parent, R.member, 1);
-      CK(hipDeviceSynchronize());
-      same(R, kind == PERC_SITE ? "k_cc_tile_w u16, site kind" : "k_cc_tile_w u16, mixed kind");
-      if (kind == PERC_SITE)
-        k_cc_tile_v<kCcH, PERC_SITE><<<R.tiles, 64>>>(g, R.bocc, R.socc, R.parent, R.member, (unsigned)nb + 8u);
-      else
-        k_cc_tile_v<kCcH, PERC_SITEBOND><<<R.tiles, 64>>>(g, R.bocc, R.socc, R.parent, R.member, (unsigned)nb + 8u);
-      CK(hipDeviceSynchronize());
-      same(R, kind == PERC_SITE ? "k_cc_tile_v, site kind" : "k_cc_tile_v, mixed kind");
     }
   }
   return 0;
