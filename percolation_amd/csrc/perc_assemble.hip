@@ -331,6 +331,7 @@ StencilForms stencil_forms(const Geom& g) {
 }
 
 static hipError_t launch_assemble(perc_ctx* h, bool csr) {
+  HIP_TRY(dev_flatten(h));  // (the roots, not their ancestors)
   DeviceBuffers& d = h->d;
   const AsmParams& p = h->asm_p;
   hipStream_t st = h->stream;
@@ -425,6 +426,7 @@ hipError_t dev_assemble(perc_ctx* h, int rule, double g0, double leak, double Va
 
 hipError_t dev_currents(perc_ctx* h, int rule, int cur_rule, double g0, double leak, double Va,
                         int span_root, double thresh, double* iout_host) {
+  HIP_TRY(dev_flatten(h));
   DeviceBuffers& d = h->d;
   hipStream_t st = h->stream;
   const int m = h->g.m;
@@ -461,6 +463,7 @@ __global__ void k_bond_mask(Geom g, int rule, const int* bond_first, const uint8
 }
 
 hipError_t dev_bond_mask(perc_ctx* h, int rule, uint8_t* mask_host) {
+  HIP_TRY(dev_flatten(h));  // (the roots, not their ancestors)
   DeviceBuffers& d = h->d;
   uint8_t* dm = nullptr;
   HIP_TRY(dmalloc(&dm, (size_t)h->nb + 8));

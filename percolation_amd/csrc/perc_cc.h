@@ -602,6 +602,28 @@ __device__ __forceinline__ void block_count_add(int v, int* counter) {
   }
 }
 
+// member roots (parent[s] == s, member[s]): the cluster count, with or
+// without the parents flattened; a thread's U sites loaded together
+__global__ __launch_bounds__(kCcThreads) void k_cc_count_roots(int t, const int* parent, const uint8_t* member,
+                                                               int* nclusters) {
+  constexpr int U = 4;
+  int cnt = 0;
+  for (long long b = (long long)blockIdx.x * kCcThreads * U + threadIdx.x + 1; b <= t;
+       b += (long long)gridDim.x * kCcThreads * U) {
+    int p[U];
+    uint8_t mb[U];
+#pragma unroll
+    for (int k = 0; k < U; ++k) {
+      const long long s = b + k * kCcThreads;
+      p[k] = s <= t ? parent[s] : 0;
+      mb[k] = s <= t ? member[s] : 0;
+    }
+#pragma unroll
+    for (int k = 0; k < U; ++k) cnt += p[k] == (int)(b + k * kCcThreads) && mb[k];
+  }
+  block_count_add(cnt, nclusters);
+}
+
 // final flattening: read-only walks, then each thread writes only its own
 // entries (path halving here would let one thread overwrite another's
 // freshly written root with an intermediate ancestor); counts the clusters

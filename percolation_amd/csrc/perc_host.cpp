@@ -133,7 +133,9 @@ static int resolve_lowest_label(perc_ctx* h, int* span_root, int* perccln) {
   *span_root = 0;
   if (rep_site) {
     int root = 0;
-    hipError_t e = hipMemcpy(&root, h->d.parent + rep_site, sizeof(int), hipMemcpyDeviceToHost);
+    hipError_t e = dev_flatten(h);
+    if (e == hipSuccess) e = hipMemcpyAsync(&root, h->d.parent + rep_site, sizeof(int), hipMemcpyDeviceToHost, h->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
     if (e != hipSuccess) return hip_status(e, "resolve_lowest_label");
     *span_root = root;
   }

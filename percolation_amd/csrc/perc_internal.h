@@ -165,6 +165,7 @@ struct perc_ctx {
   bool assembled = false;
   bool bf_closed = false;  // h_bond_first == bf_square on rows 0..n-2 (square lattice)
   bool bf_open_sq = false; // and the open lattice's top row follows (bf_open_square)
+  bool flat = true;        // parent[] holds final roots (dev_flatten after a labeling)
   bool csr_ok = true;    // the CSR values / diagonal of the assembled system are written
   perc::AsmParams asm_p; // the assembly's parameters (ensure_csr re-runs it)
   int span_root = 0;
@@ -227,6 +228,7 @@ hipError_t dev_occupy(perc_ctx* h, int kind, int nsites, const int* site_order, 
 hipError_t dev_label(perc_ctx* h, int* nspan, int* span_list, int* nclusters);
 hipError_t dev_occupy_random(perc_ctx* h, int kind, int nsites, int nbonds, unsigned long long seed);
 hipError_t dev_span_sites(perc_ctx* h, int root, int* count);
+hipError_t dev_flatten(perc_ctx* h);  // parent[s] = final root (k_cc_compress) once per labeling
 hipError_t dev_canon(perc_ctx* h, int* canon_out);
 hipError_t dev_cluster_sizes(perc_ctx* h, int kind, int root, int* maxcs, int* rootsize);
 hipError_t dev_assemble(perc_ctx* h, int rule, double g0, double leak, double Va, int span_root);

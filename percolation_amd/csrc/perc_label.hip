@@ -268,7 +268,8 @@ __global__ __launch_bounds__(1024) void k_span_top(Geom g, const int* parent,
   for (int c = threadIdx.x; c < m; c += 1024) {
     const int s = g.t - m + 1 + c;
     if (member[s]) {
-      const int root = parent[s];
+      int root = parent[s];  // (parents may not be flattened yet: dev_flatten)
+      for (int up = parent[root]; up != root; up = parent[root]) root = up;
       if (root <= m) flag[root] = 1;
     }
   }
@@ -516,9 +517,15 @@ static hipError_t label_finish(perc_ctx* h, int* nspan, int* span_list, int* ncl
   const Geom& g = h->g;
   hipStream_t st = h->stream;
   DeviceBuffers& d = h->d;
-  k_cc_compress<<<std::min(cdiv(g.t, kCcThreads * kCcCompressU), kReduceGrid), kCcThreads, 0, st>>>(
+  // the clusters are the member roots, countable before the parents are
+  // flattened; k_cc_compress runs when a consumer of the roots needs it
+  // (dev_flatten: assembly, bond masks, span sizes, cluster sizes, canonical
+  // labels) -- a labeling that spans nothing (config 5 as stated, the
+  // threshold scans' probes) does without it
+  h->flat = false;
+  k_cc_count_roots<<<std::min(cdiv(g.t, kCcThreads * 4), kReduceGrid), kCcThreads, 0, st>>>(
       g.t, d.parent, d.member, d.counters + 1);
-  HIP_TRY(dbg_sync(st, "k_cc_compress"));
+  HIP_TRY(dbg_sync(st, "k_cc_count_roots"));
   k_span_top<<<1, 1024, 0, st>>>(g, d.parent, d.member, d.top, d.counters);
   HIP_TRY(dbg_sync(st, "k_span_top"));
   int hc[8 + kMaxSpanList];
@@ -530,7 +537,18 @@ static hipError_t label_finish(perc_ctx* h, int* nspan, int* span_list, int* ncl
   return hipSuccess;
 }
 
+hipError_t dev_flatten(perc_ctx* h) {
+  if (h->flat) return hipSuccess;
+  const Geom& g = h->g;
+  k_cc_compress<<<std::min(cdiv(g.t, kCcThreads * kCcCompressU), kReduceGrid), kCcThreads, 0, h->stream>>>(
+      g.t, h->d.parent, h->d.member, h->d.counters + 6);
+  HIP_TRY(dbg_sync(h->stream, "k_cc_compress"));
+  h->flat = true;
+  return hipSuccess;
+}
+
 hipError_t dev_span_sites(perc_ctx* h, int root, int* count) {
+  HIP_TRY(dev_flatten(h));
   hipStream_t st = h->stream;
   HIP_TRY(hipMemsetAsync(h->d.counters + 2, 0, sizeof(int), st));
   k_count_root<<<std::min(cdiv(h->g.t, kCcThreads), kReduceGrid), kCcThreads, 0, st>>>(
@@ -541,6 +559,7 @@ hipError_t dev_span_sites(perc_ctx* h, int root, int* count) {
 }
 
 hipError_t dev_cluster_sizes(perc_ctx* h, int kind, int root, int* maxcs, int* rootsize) {
+  HIP_TRY(dev_flatten(h));
   DeviceBuffers& d = h->d;
   hipStream_t st = h->stream;
   const Geom& g = h->g;
@@ -562,6 +581,7 @@ hipError_t dev_cluster_sizes(perc_ctx* h, int kind, int root, int* maxcs, int* r
 }
 
 hipError_t dev_canon(perc_ctx* h, int* canon_out) {
+  HIP_TRY(dev_flatten(h));
   hipStream_t st = h->stream;
   int* tmp = nullptr;
   HIP_TRY(dmalloc(&tmp, h->g.t));
