@@ -532,62 +532,6 @@ __global__ __launch_bounds__(kCcThreads) void k_cc_merge(Geom g, int kind, const
   }
 }
 
-// k_cc_merge_w: the merge after k_cc_tile_w<H> on the open square lattice,
-// whose only block-crossing links are the up links of the blocks' top rows
-// (part A: thread i < nA on row (i / m + 1) H - 1, column i % m) and the
-// right links of the blocks' last columns (part B: column 128 k + 127, row
-// j % n, k = j / n).  The kind a template parameter, bond ids in closed form
-// (bf_open_square), the link flags and both parents loaded together
-// (buffer loads, out-of-range offsets past the work), then k_cc_merge's
-// wave-wide deduplication of the unions.
-template <int H, int KIND>
-__global__ __launch_bounds__(kCcThreads) void k_cc_merge_w(Geom g, const uint8_t* bocc, const uint8_t* socc,
-                                                           int* parent, uint8_t* member, unsigned nb_bytes,
-                                                           long long nA, long long nB) {
-  const long long i = (long long)blockIdx.x * kCcThreads + threadIdx.x;
-  const int lane = threadIdx.x & 63, m = g.m;
-  int s = 1, q = 1, id = 0;
-  bool ok = false;
-  if (i < nA) {
-    const int row = (int)(i / m + 1) * H - 1, c = (int)(i % m);
-    s = row * m + c + 1;
-    q = s + m;
-    id = bf_open_square(g, row, c) + (c < m - 1 ? 1 : 0);
-    ok = true;
-  } else if (i < nA + nB) {
-    const long long j = i - nA;
-    const int row = (int)(j % g.n), c = (int)(j / g.n) * kCcW + kCcW - 1;
-    s = row * m + c + 1;
-    q = s + 1;
-    id = bf_open_square(g, row, c);
-    ok = true;
-  }
-  const __amdgpu_buffer_rsrc_t rb = rsrc(bocc, nb_bytes), rs = rsrc(socc, (unsigned)g.t + 8u);
-  const __amdgpu_buffer_rsrc_t rp = rsrc(parent, ((unsigned)g.t + 2u) * 4u);
-  const unsigned lb = KIND != PERC_SITE
-                          ? (unsigned)__builtin_amdgcn_raw_buffer_load_b8(rb, (int)(ok ? (unsigned)id : kOOB), 0, 0)
-                          : 1u;
-  unsigned ls = 1u;
-  if constexpr (KIND != PERC_BOND)
-    ls = (unsigned)__builtin_amdgcn_raw_buffer_load_b8(rs, (int)(ok ? (unsigned)s : kOOB), 0, 0) &
-         (unsigned)__builtin_amdgcn_raw_buffer_load_b8(rs, (int)(ok ? (unsigned)q : kOOB), 0, 0);
-  const int a0 = (int)__builtin_amdgcn_raw_buffer_load_b32(rp, (int)(ok ? (unsigned)s * 4u : kOOB), 0, 0);
-  const int b0 = (int)__builtin_amdgcn_raw_buffer_load_b32(rp, (int)(ok ? (unsigned)q * 4u : kOOB), 0, 0);
-  const bool want = ok && (lb & ls) != 0u;
-  if (want && KIND == PERC_BOND) member[q] = 1;
-  const int lo = want ? min(a0, b0) : -1, hi = want ? max(a0, b0) : -1;
-  bool lead = want && lo != hi;
-  unsigned long long act = __ballot(lead);
-  while (act) {
-    const int l = __builtin_ctzll(act);
-    const int la = __shfl(lo, l, 64), lh = __shfl(hi, l, 64);
-    const bool same = lead && lo == la && hi == lh;
-    act &= ~__ballot(same);
-    if (same && lane != l) lead = false;
-  }
-  if (lead) unite(parent, lo, hi);
-}
-
 // sum of v over the workgroup of kCcThreads, then one atomic add
 __device__ __forceinline__ void block_count_add(int v, int* counter) {
   __shared__ int s_cnt[kCcThreads / 64];

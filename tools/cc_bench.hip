@@ -201,13 +201,6 @@ int main(int argc, char** argv) {
           [&, nseg, nfull, ncand]() { k_cc_merge<16, false><<<nfull * nseg + ncand * cdiv(g.n, kCcThreads), kCcThreads>>>(
                                           g, PERC_BOND, R.bf, R.bocc, R.socc, R.parent, R.member, nseg, nfull); }, false);
   }
-  // the merge of the open square lattice's two crossing link kinds (k_cc_merge_w)
-  {
-    const long long nA = (long long)((g.n - 1) / 16) * g.m, nB = (long long)((g.m - 1) / kCcW) * g.n;
-    chain("wave 16 + merge_w", wave(I16{}, std::integral_constant<int, 2>{}),
-          [&, nA, nB]() { k_cc_merge_w<16, PERC_BOND><<<cdiv(nA + nB, (long long)kCcThreads), kCcThreads>>>(
-                              g, R.bocc, R.socc, R.parent, R.member, (unsigned)nb + 8u, nA, nB); }, false);
-  }
   // compress: U sites per thread chased in lockstep (production: kCcCompressU), one site per thread
   chain_c("wave 16 + compress<1>", wave(I16{}, std::integral_constant<int, 2>{}), merge_for(I16{}),
           [&]() { k_cc_compress<1><<<std::min(cdiv(g.t, kCcThreads), kReduceGrid), kCcThreads>>>(
