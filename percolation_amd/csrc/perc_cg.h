@@ -558,28 +558,39 @@ __global__ __launch_bounds__(tile_threads(TILEH)) void k_cg_ps(CGArgs a) {
 // the sums folded in that order the iterates, iter, err and the voltages
 // are the reference's bitwise.  One wave: lane l forms term j0 + l (one
 // IEEE product, the reference's), then every lane folds the 64 terms in lane
-// order through v_readlane broadcasts (scalar operands of the adds) while
-// the next chunk's loads are in flight.  A serial fold is one dependent
+// order through LDS broadcasts (fold_chunk) while the next chunk's loads
+// are in flight.  A serial fold is one dependent
 // fp64 add per term (~4 ns): a verification mode, not the fast path.
-__device__ __forceinline__ double lane_bcast(double v, int l) {
-  const long long b = __double_as_longlong(v);
-  const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)b, l);
-  const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(b >> 32), l);
-  return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+// fold lanes 0 .. cnt-1 of t[c] into acc[c] in lane order (wave-uniform cnt;
+// one wave).  The terms go through a wave-private LDS row and every lane
+// reads them back as broadcasts, so the serial chain is one fp64 add per
+// term with an LDS operand (the v_readlane pair per term of the round-4
+// first version doubled the VALU work; config 2's literal solve then ran
+// 30.9 ms per iteration).  A wave's LDS instructions execute in order, so
+// a compiler barrier orders the stores before the reads and the reads
+// before the next chunk's stores.
+__device__ __forceinline__ void fold_lds_order() {
+  __builtin_amdgcn_wave_barrier();
+  asm volatile("" ::: "memory");
 }
-// fold lanes 0 .. cnt-1 of t[c] into acc[c] in lane order (wave-uniform cnt)
 template <int NC>
 __device__ __forceinline__ void fold_chunk(const double (&t)[NC], int cnt, double (&acc)[NC]) {
+  __shared__ double s_t[NC][64];
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int c = 0; c < NC; ++c) s_t[c][lane] = t[c];
+  fold_lds_order();
   if (cnt == 64) {
 #pragma unroll
     for (int l = 0; l < 64; ++l)
 #pragma unroll
-      for (int c = 0; c < NC; ++c) acc[c] = acc[c] + lane_bcast(t[c], l);
+      for (int c = 0; c < NC; ++c) acc[c] = acc[c] + s_t[c][l];
   } else {
     for (int l = 0; l < cnt; ++l)
 #pragma unroll
-      for (int c = 0; c < NC; ++c) acc[c] = acc[c] + lane_bcast(t[c], l);
+      for (int c = 0; c < NC; ++c) acc[c] = acc[c] + s_t[c][l];
   }
+  fold_lds_order();
 }
 
 // the prologue's sums (k_cg_init wrote r = b - A x): bnrm^2 = sum (b/d)^2
