@@ -106,6 +106,28 @@ def iter_range(doc, tkey):
     return min(its), max(its)
 
 
+def iter_ok(doc, tkey, it):
+    """the iteration count at a non-converged tolerance: +-1 while the
+    recursive residual still tracks the true one (tol >= 1e-10); below that
+    the stop decision rides on the rounding history (the fixtures' true
+    residual has reached its floor at 1e-13: 0.8-2.8e-12), so the count must
+    lie in the range the reference solver's own associations span (2 %
+    slack, +-3); a fixture without re-associated runs takes the relative
+    spread of the metric fixture (the same lattice class: L = 4096, bond p =
+    0.6) at that tolerance -- its reversed sums stop 9.4 % later at 1e-13"""
+    ref = doc["solves"][tkey]["iter"]
+    if float(tkey) >= 1e-10:
+        return abs(it - ref) <= 1
+    if any(tkey in doc.get(k, {}) for k in ASSOC_KEYS):
+        lo, hi = iter_range(doc, tkey)
+        return 0.98 * lo - 3 <= it <= 1.02 * hi + 3
+    metric = json.load(open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "configs",
+                                         "metric_sq4096_bond_p60.json")))
+    lo, hi = iter_range(metric, tkey)
+    spread = (hi - lo) / metric["solves"][tkey]["iter"]
+    return abs(it - ref) <= max(3, 1.02 * spread * ref)
+
+
 def converged_bar(doc, conv, g):
     """FLAT; or ASSOC_X x the reference solver's own association spread at
     the converged tolerance where that exceeds ASSOC_FLOOR (module
@@ -259,7 +281,7 @@ def test_config_fixture(path):
         if tkey == conv:
             continue
         d, ref, cv = report[tkey], solves[tkey], solves[conv]
-        assert abs(d["iter"] - d["iter_ref"]) <= (1 if float(tkey) >= 1e-10 else 3), d
+        assert iter_ok(doc, tkey, d["iter"]), d
         for g in ("gtop", "gbot"):
             # the oracle's own error at this tol, plus the tolerance itself:
             # where G has converged ahead of the residual (the metric's Gtop
