@@ -962,13 +962,9 @@ def main():
     if rank == 0:
         print(json.dumps(out), flush=True)
     if use_dist:
+        # (normal teardown: libperc binds to torch's HIP / HSA / RCCL copies,
+        # one runtime per process -- percolation_amd/_lib.py _one_runtime)
         dist.destroy_process_group()
-        # torch's bundled RCCL and the one libperc links are separate copies in
-        # this process; skip the interpreter's teardown (its library
-        # destructors) once the result line is out
-        sys.stdout.flush()
-        sys.stderr.flush()
-        os._exit(0)
 
 
 if __name__ == "__main__":

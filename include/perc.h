@@ -445,12 +445,33 @@ int perc_set_band_weights(perc_ctx *h, int which, int n, const int *w);
    sum folded term after term in ascending j on one wave of the GPU, exactly
    as the reference loops do -- with every other operation already the
    reference's, the iterates, iter, err history and voltages are then
-   bitwise the reference solver's.  One dependent fp64 add per term (~4 ns):
-   a verification mode (single slab; runs the q-storing kernels).  The NR
-   drop-in linbcg_ uses PERC_DOT_LITERAL by default (perc_nr_set_dot_order). */
+   bitwise the reference solver's.  One dependent fp64 add per term: a
+   verification mode (single slab).  It runs the production kernels of the
+   fast order -- the q-free strip-major / row-major march (k_cg_march P, B)
+   and the resident solve (k_cg_res), the same code objects -- which store
+   each row's dot terms (the reference's IEEE products) for the folds; other
+   formats fold from their stored q, p, r.  perc_last_solve says what ran.
+   The NR drop-in linbcg_ uses PERC_DOT_LITERAL by default
+   (perc_nr_set_dot_order). */
 #define PERC_DOT_FAST 0
 #define PERC_DOT_LITERAL 1
 int perc_set_dot_order(perc_ctx *h, int order);
+/* What the last solve of the context actually ran: out4[0] = kernel family
+   (0 other launched kernels: LDS tiles, split stencil, CSR; PERC_RAN_MARCH,
+   PERC_RAN_RESIDENT, PERC_RAN_SMALL), out4[1] = PERC_RAN_* flag bits,
+   out4[2] = iterations, out4[3] = 0 (reserved).  PERC_ESTATE before any
+   solve. */
+#define PERC_RAN_MARCH 1
+#define PERC_RAN_SLABS 2      /* row slabs (perc_set_slabs) */
+#define PERC_RAN_RESIDENT 3
+#define PERC_RAN_SMALL 4
+#define PERC_RAN_LITERAL 1    /* literal dot order */
+#define PERC_RAN_LIT_TERMS 2  /* ... folding the terms the solve kernels stored */
+#define PERC_RAN_QFREE 4      /* q-free march (P + B rebuild q) */
+#define PERC_RAN_STRIPS 8     /* strip-major layout */
+#define PERC_RAN_NIBBLE 16    /* 4-bit row codes */
+#define PERC_RAN_TAG 32       /* tagged-granule reductions */
+int perc_last_solve(perc_ctx *h, int *out4);
 /* err of every iteration of the last solve (linbcg's per-iteration
    `write (*,*) iter, err`, bondc.f:834): min(cap, iterations) values into
    out; returns the iteration count (>= 0) or a negative status */

@@ -30,6 +30,9 @@ MARCH_NIBBLE = 512
 MARCH_DEFAULT = (MARCH_QFREE | MARCH_ALT | SOLVE_RESIDENT | MARCH_STRIPS | MARCH_SLOTS | MARCH_TAG
                  | MARCH_NIBBLE)
 DOT_FAST, DOT_LITERAL = 0, 1
+# perc_last_solve: kernel family and flag bits of the last solve
+RAN_OTHER, RAN_MARCH, RAN_SLABS, RAN_RESIDENT, RAN_SMALL = 0, 1, 2, 3, 4
+RAN_LITERAL, RAN_LIT_TERMS, RAN_QFREE, RAN_STRIPS, RAN_NIBBLE, RAN_TAG = 1, 2, 4, 8, 16, 32
 XPORT_RCCL, XPORT_HOST, XPORT_EXCHANGE = 0, 1, 4
 DSLAB_ID_BYTES = 128
 
@@ -138,6 +141,7 @@ SIGNATURES = {
     "perc_set_dot_order": (C.c_int, [_VP, C.c_int]),
     "perc_err_history": (C.c_int, [_VP, _VP, C.c_int]),
     "perc_march_info": (C.c_int, [_VP, _VP]),
+    "perc_last_solve": (C.c_int, [_VP, _VP]),
     "perc_set_bond_weights": (C.c_int, [_VP, _VP, C.c_longlong]),
     "perc_selftest_division": (C.c_int, [C.c_longlong, C.c_ulonglong, _VP]),
     "perc_stats_accumulate": (None, [_D, C.c_int, C.c_double, C.c_int, C.c_int]),
@@ -168,6 +172,27 @@ SIGNATURES = {
 }
 
 
+def _one_runtime():
+    """One HIP / HSA / RCCL runtime per process.  torch ships its own copies
+    (torch/lib/libamdhip64.so, libhsa-runtime64.so, librccl.so, sonames .so.7
+    / .so.1 / .so.1) and names them unversioned in its NEEDED entries; libperc
+    names the sonames.  Loaded after torch, libperc's sonames bind to torch's
+    copies already in the process.  Loaded BEFORE torch, libperc brings
+    /opt/rocm's copies and a later `import torch` loads torch's beside them:
+    two HIP and two HSA runtimes on one device, a torch ExternalStream of a
+    libperc stream names a handle of the other runtime, and interpreter exit
+    aborts with glibc's "double free or corruption (!prev)" (round 4's
+    teardown abort; reproduced without a GPU by tests/test_host_cpu.py).  So
+    torch, where installed, is imported first (PERC_NO_TORCH=1 skips it for a
+    process that will never import torch: /opt/rocm's runtime then)."""
+    if os.environ.get("PERC_NO_TORCH") == "1":
+        return
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
+
+
 def lib():
     """Load libperc.so (raises if it has not been built)."""
     global _lib
@@ -176,6 +201,7 @@ def lib():
     if not os.path.exists(LIBPERC):
         raise PercError("libperc.so not built: run `python -c 'import __graft_entry__ as g; "
                         "g.build()'` or `make -C percolation_amd/csrc` (%s missing)" % LIBPERC)
+    _one_runtime()
     L = C.CDLL(LIBPERC, mode=C.RTLD_GLOBAL)
     probe = bool(os.environ.get("PERC_LIBPERC"))
     for name, (res, args) in SIGNATURES.items():

@@ -302,6 +302,19 @@ class Context:
                     nibble=bool(out[1] & 32),
                     alt=bool(out[2]), band_rows=int(out[3]), strip_cols=int(out[4]))
 
+    def last_solve(self):
+        """What the last solve actually ran (perc_last_solve): the kernel
+        family ('other', 'march', 'slabs', 'resident', 'small'), its flags and
+        the iteration count.  lit_terms: the literal folds summed the terms
+        the solve kernels themselves stored (the production kernels ran)."""
+        out = np.zeros(4, dtype=np.int32)
+        L.check(L.lib().perc_last_solve(self.h, out.ctypes.data), "perc_last_solve")
+        f = int(out[1])
+        return dict(kernel=("other", "march", "slabs", "resident", "small")[out[0]],
+                    literal=bool(f & L.RAN_LITERAL), lit_terms=bool(f & L.RAN_LIT_TERMS),
+                    qfree=bool(f & L.RAN_QFREE), strips=bool(f & L.RAN_STRIPS),
+                    nibble=bool(f & L.RAN_NIBBLE), tag=bool(f & L.RAN_TAG), iter=int(out[2]))
+
     def matrix_format(self):
         rc = L.lib().perc_matrix_format(self.h)
         if rc < 0:

@@ -82,6 +82,13 @@ struct CGArgs {
   const uint8_t* nib;
   unsigned ncls[3];
   int* merr;
+  // literal dot order on the q-free march (PERC_DOT_LITERAL): the march P
+  // stores each row's q.p term and the march B each row's z.r and r.r terms
+  // (the reference's IEEE products) at their row-major index into lit[0..N),
+  // lit[N..2N), lit[2N..3N), and the serial folds sum them in ascending j.
+  // Set (non-null) only for the kernels' LIT instantiation -- the same
+  // source with those stores compiled in; nullptr in the fast order
+  double* lit;
 };
 
 // diagonal of rows i, i+1 (i even) from the CSR diag array or the stencil code
@@ -573,18 +580,35 @@ __device__ __forceinline__ void fold_lds_order() {
   __builtin_amdgcn_wave_barrier();
   asm volatile("" ::: "memory");
 }
-template <int NC>
+// A full chunk is read back in batches of U terms per sum -- U / 2 16-B
+// broadcast reads each, all issued before the batch's adds -- so the serial
+// chain waits for LDS once per batch instead of every few terms: 7.7 vs 13.7
+// ns per term of two sums (tools/fold_bench.hip, profiles/r5_2_fold_bench.json;
+// 16 in the fold kernels, 8 in the resident solve's register-bound literal
+// instantiation)
+template <int NC, int U = 16>
 __device__ __forceinline__ void fold_chunk(const double (&t)[NC], int cnt, double (&acc)[NC]) {
-  __shared__ double s_t[NC][64];
+  __shared__ __attribute__((aligned(16))) double s_t[NC][64];
   const int lane = threadIdx.x & 63;
 #pragma unroll
   for (int c = 0; c < NC; ++c) s_t[c][lane] = t[c];
   fold_lds_order();
   if (cnt == 64) {
 #pragma unroll
-    for (int l = 0; l < 64; ++l)
+    for (int b = 0; b < 32; b += U / 2) {
+      double2 x[NC][U / 2];
 #pragma unroll
-      for (int c = 0; c < NC; ++c) acc[c] = acc[c] + s_t[c][l];
+      for (int i = 0; i < U / 2; ++i)
+#pragma unroll
+        for (int c = 0; c < NC; ++c) x[c][i] = reinterpret_cast<const double2*>(s_t[c])[b + i];
+#pragma unroll
+      for (int i = 0; i < U / 2; ++i)
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+          acc[c] = acc[c] + x[c][i].x;  // terms 2(b+i), 2(b+i)+1 in order
+          acc[c] = acc[c] + x[c][i].y;
+        }
+    }
   } else {
     for (int l = 0; l < cnt; ++l)
 #pragma unroll
@@ -593,28 +617,84 @@ __device__ __forceinline__ void fold_chunk(const double (&t)[NC], int cnt, doubl
   fold_lds_order();
 }
 
+// One wave folds the N terms of NC sums in ascending j.  Lane l loads the
+// raw operands of term c * 64 + l kFoldD chunks ahead into a register ring
+// (Raw: what LD fetches; TERM forms the NC terms from it when the chunk is
+// folded, so no product waits for its loads at the prefetch), and every
+// chunk is folded serially by fold_chunk.  With one chunk in flight (round
+// 4) a chunk's HBM latency (~900 cycles) exceeded the 64 dependent adds it
+// covered; kFoldD = 8 keeps ~512 terms in flight per sum.  Every load is
+// issued unconditionally (index clamped to N - 1; chunks past the end fold
+// 0 terms), so the waits count exactly.
+constexpr int kFoldD = 8;
+template <int NC, int D, typename Raw, int U = 16, typename LD, typename TERM>
+__device__ __forceinline__ void fold_wave(int N, LD ld, TERM term, double (&acc)[NC]) {
+  const int lane = threadIdx.x & 63;
+  const int nch = (N + 63) / 64;
+  Raw ring[D];
+#pragma unroll
+  for (int u = 0; u < D; ++u) ring[u] = ld(min(u * 64 + lane, N - 1));
+  for (int c0 = 0; c0 < nch; c0 += D) {
+#pragma unroll
+    for (int u = 0; u < D; ++u) {
+      const int c = c0 + u;
+      double t[NC];
+      term(ring[u], t);
+      ring[u] = ld(min((c + D) * 64 + lane, N - 1));
+      fold_chunk<NC, U>(t, max(0, min(64, N - c * 64)), acc);
+    }
+  }
+}
+
+struct Raw2 {
+  double a, b;
+};
+// raw operands of a row's diagonal: the CSR diagonal, or the stencil code
+// (the diagonal formed from it at fold time, not at the prefetch)
+struct RawD {
+  double d;
+  unsigned c;
+};
+template <bool ST>
+__device__ __forceinline__ RawD diag_raw(const CGArgs& a, int i) {
+  RawD v;
+  if constexpr (ST) {
+    v.c = a.St.code[i];
+    v.d = 0.0;
+  } else {
+    v.d = a.A.diag[i];
+    v.c = 0u;
+  }
+  return v;
+}
+template <bool ST>
+__device__ __forceinline__ double diag_of(const CGArgs& a, const RawD& v) {
+  return ST ? code_diag(v.c, a.St.ng0, a.St.nleak) : v.d;
+}
+struct RawBRD {
+  double b, r;
+  RawD d;
+};
+struct RawRD {
+  double r;
+  RawD d;
+};
+
 // the prologue's sums (k_cg_init wrote r = b - A x): bnrm^2 = sum (b/d)^2
 // (itol 2; sum b^2 for itol 1) and the first bknum = sum (r/d) r
 template <bool ST>
 __global__ __launch_bounds__(64) void k_fold_init(CGArgs a, int itol) {
   const int N = a.A.N, lane = threadIdx.x;
   double acc[2] = {0.0, 0.0};
-  auto load = [&](int j0, double& b, double& r, double& d) {
-    const int j = min(j0 + lane, N - 1);
-    b = a.rhs[j];
-    r = a.r[j];
-    d = diag1<ST>(a, j);
-  };
-  double b, r, d;
-  load(0, b, r, d);
-  for (int j0 = 0; j0 < N; j0 += 64) {
-    const double zb = itol == 1 ? b : b / d, z = r / d;
-    const double t[2] = {zb * zb, z * r};
-    double bn, rn, dn;
-    load(j0 + 64 < N ? j0 + 64 : j0, bn, rn, dn);
-    fold_chunk<2>(t, min(64, N - j0), acc);
-    b = bn, r = rn, d = dn;
-  }
+  fold_wave<2, kFoldD, RawBRD>(
+      N, [&](int j) { return RawBRD{a.rhs[j], a.r[j], diag_raw<ST>(a, j)}; },
+      [&](const RawBRD& v, double (&t)[2]) {
+        const double d = diag_of<ST>(a, v.d);
+        const double zb = itol == 1 ? v.b : v.b / d, z = v.r / d;
+        t[0] = zb * zb;
+        t[1] = z * v.r;
+      },
+      acc);
   if (lane == 0) {
     a.S->bnrm = sqrt(acc[0]);
     a.S->bknum = acc[1];
@@ -622,7 +702,8 @@ __global__ __launch_bounds__(64) void k_fold_init(CGArgs a, int itol) {
 }
 
 // after S(k): akden = sum q p(k), ak = bknum / akden; bkden keeps bknum
-// (the B epilogue overwrites bknum with its own sum, k_fold_b replaces it)
+// (the B epilogue overwrites bknum with its own sum, k_fold_b replaces it).
+// The q-free march has no q array: it stored the terms (a.lit)
 __global__ __launch_bounds__(64) void k_fold_qp(CGArgs a) {
   CGScalars* S = a.S;
   if (S->done) return;
@@ -630,13 +711,14 @@ __global__ __launch_bounds__(64) void k_fold_qp(CGArgs a) {
   const int k = S->iter + 1;
   const double* __restrict__ p = a.fused ? a.pb[k & 1] : a.p;
   double acc[1] = {0.0};
-  double q = a.q[min(lane, N - 1)], pv = p[min(lane, N - 1)];
-  for (int j0 = 0; j0 < N; j0 += 64) {
-    const double t[1] = {q * pv};
-    const int jn = min(j0 + 64 + lane, N - 1);
-    const double qn = a.q[jn], pn = p[jn];
-    fold_chunk<1>(t, min(64, N - j0), acc);
-    q = qn, pv = pn;
+  if (a.lit) {
+    const double* __restrict__ t0 = a.lit;
+    fold_wave<1, kFoldD, double>(
+        N, [&](int j) { return t0[j]; }, [&](double v, double (&t)[1]) { t[0] = v; }, acc);
+  } else {
+    fold_wave<1, kFoldD, Raw2>(
+        N, [&](int j) { return Raw2{a.q[j], p[j]}; },
+        [&](const Raw2& v, double (&t)[1]) { t[0] = v.a * v.b; }, acc);
   }
   if (lane == 0) {
     S->akden = acc[0];
@@ -647,21 +729,33 @@ __global__ __launch_bounds__(64) void k_fold_qp(CGArgs a) {
 }
 
 // after B(k): bknum' = sum (r/d) r, err = sqrt(sum r^2) / bnrm, bk, the
-// stop test -- B's epilogue, on the literal sums
+// stop test -- B's epilogue, on the literal sums (the q-free march B stored
+// the terms: a.lit + N, a.lit + 2N)
 template <bool ST>
 __global__ __launch_bounds__(64) void k_fold_b(CGArgs a) {
   CGScalars* S = a.S;
   if (S->pad[2] == 0) return;  // no iteration ran since the last fold
   const int N = a.A.N, lane = threadIdx.x;
   double acc[2] = {0.0, 0.0};
-  double r = a.r[min(lane, N - 1)], d = diag1<ST>(a, min(lane, N - 1));
-  for (int j0 = 0; j0 < N; j0 += 64) {
-    const double z = r / d;
-    const double t[2] = {z * r, r * r};
-    const int jn = min(j0 + 64 + lane, N - 1);
-    const double rn = a.r[jn], dn = diag1<ST>(a, jn);
-    fold_chunk<2>(t, min(64, N - j0), acc);
-    r = rn, d = dn;
+  if (a.lit) {
+    const double* __restrict__ t1 = a.lit + N;
+    const double* __restrict__ t2 = a.lit + 2 * (size_t)N;
+    fold_wave<2, kFoldD, Raw2>(
+        N, [&](int j) { return Raw2{t1[j], t2[j]}; },
+        [&](const Raw2& v, double (&t)[2]) {
+          t[0] = v.a;
+          t[1] = v.b;
+        },
+        acc);
+  } else {
+    fold_wave<2, kFoldD, RawRD>(
+        N, [&](int j) { return RawRD{a.r[j], diag_raw<ST>(a, j)}; },
+        [&](const RawRD& v, double (&t)[2]) {
+          const double z = v.r / diag_of<ST>(a, v.d);
+          t[0] = z * v.r;
+          t[1] = v.r * v.r;
+        },
+        acc);
   }
   if (lane == 0) {
     const int k = S->iter;
@@ -1029,6 +1123,7 @@ CGArgs make_cg_args(perc_ctx* h) {
   a.nib = nullptr;
   a.ncls[0] = a.ncls[1] = a.ncls[2] = 0u;
   a.merr = nullptr;
+  a.lit = nullptr;
   return a;
 }
 

@@ -32,7 +32,10 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <atomic>
+#include <chrono>
 #include <condition_variable>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <mutex>
@@ -100,12 +103,47 @@ struct Loop {
   // host transport (every slab in this process): pinned staging per slab
   std::vector<double*> h_part, h_edge;
   Barrier* bar = nullptr;
+  // RCCL, group driver: set by a slab thread that failed; the others abort
+  // their own communicator when they see it (their collectives wait for the
+  // failed slab's data, which never comes)
+  std::atomic<bool> failed{false};
 };
 
 int nccl_check(ncclResult_t r, const char* where) {
   if (r == ncclSuccess) return PERC_OK;
   set_error(std::string(where) + ": " + ncclGetErrorString(r));
   return PERC_EHIP;
+}
+
+// Wait for the slab's stream with RCCL collectives in it, boundedly: a peer
+// that failed never sends what a collective of ours waits for.  Polls the
+// stream; gives up when the group driver's failure flag is set, when the
+// communicator reports an asynchronous error, or after PERC_DSLAB_TIMEOUT_S
+// seconds (default 120) without progress -- then the caller aborts its
+// communicator (its kernels leave) and returns the error.
+int wait_stream(perc_ctx* h, ncclComm_t comm, const Loop* L, const char* where) {
+  static const double limit = getenv("PERC_DSLAB_TIMEOUT_S") ? atof(getenv("PERC_DSLAB_TIMEOUT_S")) : 120.0;
+  const auto t0 = std::chrono::steady_clock::now();
+  for (;;) {
+    const hipError_t e = hipStreamQuery(h->stream);
+    if (e == hipSuccess) return PERC_OK;
+    if (e != hipErrorNotReady) return hip_status(e, where);
+    if (L && L->failed.load()) {
+      set_error(std::string(where) + ": another slab failed");
+      return PERC_EHIP;
+    }
+    if (comm) {
+      ncclResult_t ae = ncclSuccess;
+      if (ncclCommGetAsyncError(comm, &ae) == ncclSuccess && ae != ncclSuccess && ae != ncclInProgress)
+        return nccl_check(ae, where);
+    }
+    const double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    if (s > limit) {
+      set_error(std::string(where) + ": no progress within PERC_DSLAB_TIMEOUT_S (a peer failed?)");
+      return PERC_EHIP;
+    }
+    std::this_thread::sleep_for(std::chrono::microseconds(20));
+  }
 }
 
 #define SLAB_TRY(x)                       \
@@ -193,9 +231,12 @@ int slab_solve(Loop& L, Member& b, int itol, double tol, int itmax, bool full_x)
     SLAB_TRY(halo(L, b));
     SLAB_TRY(step(h, PERC_DSLAB_GHOSTS));
     ++k;
-    // every slab reads the same (bitwise) flag at the same k: all leave together
-    if (k % kCheckEvery == 0 || k > (long long)itmax)
+    // every slab reads the same (bitwise) flag at the same k: all leave
+    // together (over RCCL the wait for it is bounded: wait_stream)
+    if (k % kCheckEvery == 0 || k > (long long)itmax) {
+      if (L.xport == PERC_XPORT_RCCL && !solo(L)) SLAB_TRY(wait_stream(h, b.comm, &L, "dslab status"));
       SLAB_TRY(hip_status(dev_dslab_status(h, &b.iter, &b.err, &done), "dslab status"));
+    }
   }
   return hip_status(dev_dslab_end(h, true), "dslab end");
 }
@@ -274,6 +315,20 @@ void dslab_comm_release(perc_ctx* h) {
 }
 }  // namespace perc
 
+namespace {
+// after a failure inside perc_dslab_solve: abort the context's communicator
+// (its pending kernels leave; a peer's collectives that wait for this rank
+// then end in their own wait_stream) and forget it, so the caller must make
+// a new one with perc_dslab_comm_init
+void dslab_comm_abort(perc_ctx* h) {
+  std::lock_guard<std::mutex> lk(g_rank_mu);
+  auto it = g_rank.find(h);
+  if (it == g_rank.end()) return;
+  if (it->second.comm) (void)ncclCommAbort(it->second.comm);
+  g_rank.erase(it);
+}
+}  // namespace
+
 extern "C" {
 
 int perc_dslab_solve_group(int K, perc_ctx** ctxs, int xport, int rule, int cur_rule, double Va,
@@ -351,9 +406,19 @@ int perc_dslab_solve_group(int K, perc_ctx** ctxs, int xport, int rule, int cur_
     cleanup();
     return rc;
   }
+  // a failing slab aborts the host barrier, or (RCCL) sets L.failed and
+  // aborts its own communicator: the others' waits (wait_stream) see the
+  // flag, abort theirs too (their kernels leave the collectives) and return
   auto body = [&](int s) {
     mem[s].status = slab_solve(L, mem[s], itol, tol, itmax, full_x != 0);
-    if (mem[s].status != PERC_OK && L.bar) L.bar->abort();
+    if (mem[s].status != PERC_OK) {
+      if (L.bar) L.bar->abort();
+      if (mem[s].comm) {
+        L.failed = true;
+        (void)ncclCommAbort(mem[s].comm);
+        mem[s].comm = nullptr;
+      }
+    }
   };
   if (K == 1) {
     body(0);
@@ -363,6 +428,14 @@ int perc_dslab_solve_group(int K, perc_ctx** ctxs, int xport, int rule, int cur_
     for (auto& t : th) t.join();
   }
   for (int s = 0; s < K && rc == PERC_OK; ++s) rc = mem[s].status;
+  if (cs && rc != PERC_OK) {
+    // the set is unusable now: abort what is left of it (every thread has
+    // joined) and let the next call make a new one
+    for (Member& b : mem)
+      if (b.comm) (void)ncclCommAbort(b.comm);
+    for (Member& b : mem) b.comm = nullptr;
+    cs->comm.clear();
+  }
   // the top electrode row's voltages (slab K-1) to slab 0, which holds the
   // bottom one: the terminal currents there (bondc.f:554-592)
   if (rc == PERC_OK && K > 1) {
@@ -432,13 +505,17 @@ int perc_dslab_solve(perc_ctx* h, int rule, int cur_rule, double Va, double g0, 
     }
     rcm = it->second;
   }
-  SLAB_TRY(check_ctx(h, h));
   const int K = rcm.K, s = rcm.s;
-  if (K > h->g.n - 2) return PERC_EINVAL;
   std::memset(res, 0, sizeof(*res));
   hipSetDevice(h->device);
+  // Local preparation; a failure here is NOT returned at once: every rank
+  // must reach the agreement all-reduce below, or the ranks that did would
+  // wait in it forever (the span check existed to prevent exactly
+  // that hang, and an early return bypassed it)
+  int lrc = check_ctx(h, h);
+  if (lrc == PERC_OK && K > h->g.n - 2) lrc = PERC_EINVAL;
   int spans = 0;
-  SLAB_TRY(perc_assemble(h, rule, g0, leak, Va, &spans));
+  if (lrc == PERC_OK) lrc = perc_assemble(h, rule, g0, leak, Va, &spans);
   Loop L;
   L.K = K;
   L.xport = PERC_XPORT_RCCL;
@@ -447,59 +524,87 @@ int perc_dslab_solve(perc_ctx* h, int rule, int cur_rule, double Va, double g0, 
   b.h = h;
   b.s = s;
   b.comm = rcm.comm;
-  int rc = alloc_member(b, K, L.m);
-  // every rank checks that all ranks found the same spanning state before
-  // entering the loop (a rank that left early would hang the others)
+  const std::string lerr = lrc == PERC_OK ? std::string() : std::string(perc_last_error());
+  if (lrc == PERC_OK) lrc = alloc_member(b, K, L.m);
+  // the agreement: {max spans, -min spans, any rank failed}, one all-reduce
   double* flags = nullptr;
-  if (rc == PERC_OK) rc = hip_status(hipMalloc(reinterpret_cast<void**>(&flags), 2 * sizeof(double)), "dslab flags");
-  if (rc == PERC_OK) {
-    double hf[2] = {(double)spans, -(double)spans};  // max(spans), -min(spans)
-    hipError_t e = hipMemcpyAsync(flags, hf, sizeof(hf), hipMemcpyHostToDevice, h->stream);
-    rc = hip_status(e, "dslab flags");
-    if (rc == PERC_OK)
-      rc = nccl_check(ncclAllReduce(flags, flags, 2, ncclDouble, ncclMax, b.comm, h->stream), "dslab span check");
-    if (rc == PERC_OK) e = hipMemcpyAsync(hf, flags, sizeof(hf), hipMemcpyDeviceToHost, h->stream);
-    if (rc == PERC_OK && e == hipSuccess) e = hipStreamSynchronize(h->stream);
-    if (rc == PERC_OK) rc = hip_status(e, "dslab span check");
-    if (rc == PERC_OK && hf[0] != -hf[1]) {
-      set_error("perc_dslab_solve: the ranks are not labeled alike");
-      rc = PERC_EINVAL;
+  const int frc = hip_status(hipMalloc(reinterpret_cast<void**>(&flags), 3 * sizeof(double)), "dslab flags");
+  // after a failure past this point the communicator is aborted: a peer's
+  // pending collective then leaves instead of waiting for this rank
+  auto fail = [&](int rc) {
+    dslab_comm_abort(h);
+    if (flags) (void)hipFree(flags);
+    free_member(b);
+    return rc;
+  };
+  if (frc != PERC_OK) return fail(frc);  // (no buffer to agree with: abort)
+  double hf[3] = {(double)spans, -(double)spans, lrc == PERC_OK ? 0.0 : 1.0};
+  int rc = hip_status(hipMemcpyAsync(flags, hf, sizeof(hf), hipMemcpyHostToDevice, h->stream), "dslab flags");
+  if (rc == PERC_OK)
+    rc = nccl_check(ncclAllReduce(flags, flags, 3, ncclDouble, ncclMax, b.comm, h->stream), "dslab agreement");
+  if (rc == PERC_OK)
+    rc = hip_status(hipMemcpyAsync(hf, flags, sizeof(hf), hipMemcpyDeviceToHost, h->stream), "dslab agreement");
+  if (rc == PERC_OK) rc = wait_stream(h, b.comm, nullptr, "dslab agreement");
+  if (rc != PERC_OK) return fail(rc);
+  if (hf[2] != 0.0) {  // some rank failed: every rank leaves here, together
+    if (lrc != PERC_OK) {
+      if (!lerr.empty()) set_error(lerr);
+    } else {
+      set_error("perc_dslab_solve: another rank failed before the loop");
     }
+    (void)hipFree(flags);
+    free_member(b);
+    return lrc != PERC_OK ? lrc : PERC_EHIP;
   }
-  if (rc == PERC_OK && !spans) {
+  if (hf[0] != -hf[1]) {
+    set_error("perc_dslab_solve: the ranks are not labeled alike");
+    (void)hipFree(flags);
+    free_member(b);
+    return PERC_EINVAL;
+  }
+  if (!spans) {
     res->status = 1;
-  } else if (rc == PERC_OK) {
-    rc = slab_solve(L, b, itol, tol, itmax, full_x != 0);
-    // top electrode row: rank K-1 -> rank 0 (ncclSend / ncclRecv on the stream)
-    const int nrows = h->g.n - 2;
-    if (rc == PERC_OK && K > 1 && (s == 0 || s == K - 1)) {
-      hipError_t e = hipSuccess;
-      if (s == K - 1) e = dev_x_row(h, nrows - 1, b.row, false);
-      rc = hip_status(e, "dslab top row");
-      if (rc == PERC_OK)
-        rc = s == K - 1 ? nccl_check(ncclSend(b.row, L.m, ncclDouble, 0, b.comm, h->stream), "dslab top row")
-                        : nccl_check(ncclRecv(b.row, L.m, ncclDouble, K - 1, b.comm, h->stream), "dslab top row");
-      if (rc == PERC_OK && s == 0) rc = hip_status(dev_x_row(h, nrows - 1, b.row, true), "dslab top row");
-    }
-    // rank 0's Gtop / Gbot to every rank
-    double hv[2] = {0.0, 0.0};
-    if (rc == PERC_OK && s == 0) {
-      rc = perc_currents(h, rule, cur_rule, Va, g0, leak, res);
-      hv[0] = res->gtop;
-      hv[1] = res->gbot;
-    }
-    if (rc == PERC_OK) rc = hip_status(hipMemcpyAsync(flags, hv, sizeof(hv), hipMemcpyHostToDevice, h->stream), "dslab result");
-    if (rc == PERC_OK) rc = nccl_check(ncclBroadcast(flags, flags, 2, ncclDouble, 0, b.comm, h->stream), "dslab result");
-    if (rc == PERC_OK) rc = hip_status(hipMemcpyAsync(hv, flags, sizeof(hv), hipMemcpyDeviceToHost, h->stream), "dslab result");
-    if (rc == PERC_OK) rc = hip_status(hipStreamSynchronize(h->stream), "dslab result");
-    if (rc == PERC_OK) {
-      res->gtop = hv[0];
-      res->gbot = hv[1];
-      res->iter = b.iter;
-      res->err = b.err;
-    }
+    (void)hipFree(flags);
+    free_member(b);
+    return PERC_OK;
   }
-  if (flags) (void)hipFree(flags);
+  rc = slab_solve(L, b, itol, tol, itmax, full_x != 0);
+  if (rc != PERC_OK) return fail(rc);
+  // top electrode row: rank K-1 -> rank 0 (ncclSend / ncclRecv on the stream)
+  const int nrows = h->g.n - 2;
+  if (K > 1 && (s == 0 || s == K - 1)) {
+    if (s == K - 1) rc = hip_status(dev_x_row(h, nrows - 1, b.row, false), "dslab top row");
+    if (rc == PERC_OK)
+      rc = s == K - 1 ? nccl_check(ncclSend(b.row, L.m, ncclDouble, 0, b.comm, h->stream), "dslab top row")
+                      : nccl_check(ncclRecv(b.row, L.m, ncclDouble, K - 1, b.comm, h->stream), "dslab top row");
+    if (rc == PERC_OK && s == 0) rc = wait_stream(h, b.comm, nullptr, "dslab top row");
+    if (rc == PERC_OK && s == 0) rc = hip_status(dev_x_row(h, nrows - 1, b.row, true), "dslab top row");
+    if (rc != PERC_OK) return fail(rc);
+  }
+  // rank 0's Gtop / Gbot and status to every rank: rank 0 always joins the
+  // broadcast, also when its currents failed (status word != 0)
+  double hv[3] = {0.0, 0.0, 0.0};
+  if (s == 0) {
+    const int crc = perc_currents(h, rule, cur_rule, Va, g0, leak, res);
+    hv[0] = res->gtop;
+    hv[1] = res->gbot;
+    hv[2] = (double)crc;  // (PERC_OK = 0; errors are negative)
+  }
+  rc = hip_status(hipMemcpyAsync(flags, hv, sizeof(hv), hipMemcpyHostToDevice, h->stream), "dslab result");
+  if (rc == PERC_OK) rc = nccl_check(ncclBroadcast(flags, flags, 3, ncclDouble, 0, b.comm, h->stream), "dslab result");
+  if (rc == PERC_OK) rc = hip_status(hipMemcpyAsync(hv, flags, sizeof(hv), hipMemcpyDeviceToHost, h->stream), "dslab result");
+  if (rc == PERC_OK) rc = wait_stream(h, b.comm, nullptr, "dslab result");
+  if (rc != PERC_OK) return fail(rc);
+  if (hv[2] != 0.0) {
+    if (s != 0) set_error("perc_dslab_solve: rank 0's terminal currents failed");
+    rc = (int)hv[2];
+  } else {
+    res->gtop = hv[0];
+    res->gbot = hv[1];
+    res->iter = b.iter;
+    res->err = b.err;
+  }
+  (void)hipFree(flags);
   free_member(b);
   return rc;
 }

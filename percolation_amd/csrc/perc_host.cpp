@@ -1022,6 +1022,16 @@ int perc_march_info(perc_ctx* h, int* out5) {
   return PERC_OK;
 }
 
+int perc_last_solve(perc_ctx* h, int* out4) {
+  if (!h || !out4) return PERC_EINVAL;
+  if (h->last_iter < 0) return PERC_ESTATE;
+  out4[0] = h->last_kernel;
+  out4[1] = h->last_flags;
+  out4[2] = h->last_iter;
+  out4[3] = 0;
+  return PERC_OK;
+}
+
 int perc_matrix_format(perc_ctx* h) {
   if (!h) return PERC_EINVAL;
   if (!h->assembled) return PERC_ESTATE;

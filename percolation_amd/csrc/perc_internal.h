@@ -117,6 +117,8 @@ struct DeviceBuffers {
   double* res_xch = nullptr;    // resident solve: exchange rows
   unsigned* res_bar = nullptr;
   double* res_gran = nullptr;   // resident solve: tagged partial granules
+  double* lit = nullptr;        // literal dot order: the q.p, z.r, r.r terms (3 N) of the
+                                // q-free march and the resident solve
 };
 
 struct ReplayOrder {
@@ -207,6 +209,10 @@ struct perc_ctx {
   bool small = false;           // one-workgroup solve of a small system (k_cg_small)
   int res_G = 0, res_H = 0, res_MT = 0, res_HMAX = 0;  // its grid, band height, template
   int res_NT = 1024;            // its threads per workgroup (m rounded up to 64 for m < 1024)
+  // what the last dev_solve ran (perc_last_solve): kernel family (PERC_RAN_*)
+  // and flags (PERC_RAN_* bits: q-free, strip-major, nibble codes, tagged
+  // reductions, literal folds of kernel-stored terms)
+  int last_kernel = 0, last_flags = 0, last_iter = -1;
   bool full_voltages = false;   // perc_set_full_voltages: keep x on every row
   int nslab = 1;                // perc_set_slabs: row slabs of the CG solve
   perc::DSlab* dslab = nullptr;  // perc_dslab_*: this process's slab of a distributed solve

@@ -254,6 +254,11 @@ struct MGeom {
   int r0, rend, col, hcol;
   bool hok;
   unsigned cb0, cb1, cbh;  // nibble codes (PK): count / form bits of col, col+1, hcol
+  // open square lattice with nibble codes (PK): the slot bits of element 0 /
+  // 1 in the INTERIOR form's slot numbering, c' = (c & lo) | ((c & hi) << 1)
+  // -- the identity inside, a gap at the absent neighbour of column 0 (lo 1,
+  // hi 6) and column m-1 (lo 3, hi 4); see march_step
+  unsigned lo0, hi0, lo1, hi1;
 };
 
 // Buffer views of the rows one march wave touches, [lo, hi) = its band plus
@@ -269,6 +274,7 @@ struct MGeom {
 // exactly and the prefetch ring keeps its rows in flight.
 struct MBuf {
   __amdgpu_buffer_rsrc_t p, r, c, pn, q;  // p(k-1), r, codes, p(k): rows [lo, hi); q: own rows
+  __amdgpu_buffer_rsrc_t t;  // literal dot terms (a.lit, row-major; size 0 in the fast order)
   int lo, hi;
 };
 
@@ -281,6 +287,9 @@ __device__ __forceinline__ MBuf march_bufs(const CGArgs& a, const MGeom& g, cons
   MBuf B;
   B.lo = max(g.r0 - 1, a.glo);
   B.hi = max(min(g.rend + 1, a.ghi), B.lo);
+  // (dev_solve sets a.lit only where 3 N doubles stay below 2 GB; only the
+  // LIT instantiation stores through this view)
+  B.t = rsrc(a.lit, a.lit ? (unsigned)a.St.N * 24u : 0u);
   if constexpr (SM) {
     const unsigned nall = (unsigned)a.T.nrows * (unsigned)m;
     B.p = rsrc(psrc, nall * 8u);
@@ -356,7 +365,7 @@ struct MState {
 
 // one step: row gr enters the window, then the middle row (gr -+ 1) is
 // finished when it is one of the band's own rows
-template <int MODE, bool UP, bool SM>
+template <int MODE, bool UP, bool SM, bool LIT = false, bool PK = false>
 __device__ __forceinline__ void march_step(const CGArgs& a, const MGeom& g, const MBuf& B,
                                            const MRow& R, int gr,
                                            bool first, double bk, double ak,
@@ -423,6 +432,9 @@ __device__ __forceinline__ void march_step(const CGArgs& a, const MGeom& g, cons
   const int mid = UP ? gr + 1 : gr - 1;
   const bool mown = mid >= g.r0 && mid < g.rend;  // wave-uniform
   double2 mq = make_double2(0.0, 0.0), mr = mq;   // q / r(k+1) of the middle row
+  // the middle row's dot terms (P: q.p; B: z.r, r.r), summed into acc and
+  // stored for the literal folds
+  double2 t0 = mq, t1 = mq;
   if (mown) {
     const unsigned c0w = W.cM & 0xffffu, c1w = W.cM >> 16;
     const unsigned f0 = c0w >> 11, f1 = c1w >> 11;
@@ -430,7 +442,26 @@ __device__ __forceinline__ void march_step(const CGArgs& a, const MGeom& g, cons
     const unsigned ff = __builtin_amdgcn_readfirstlane(f0);
     const bool uni = !__any(f0 != ff || f1 != ff) && a.St.F.regular[ff];
     double q0, q1;
-    if (uni) {
+    if (PK && !a.T.pbc) {
+      // Open square lattice, nibble codes: every row is interior, column 0
+      // or column m-1 (k_pack_nib checked it), so EVERY wave -- the edge
+      // strips too -- takes the interior form's scalar path.  A row of
+      // column 0 (m-1) lacks its left (right) neighbour: its slot bits are
+      // spread into the interior numbering with a gap there (MGeom lo/hi),
+      // whose term is leak x (+0.0) -- the window holds an exact +0 for the
+      // absent column (hok false: hpn = 0 / an out-of-range load) -- i.e.
+      // -0.0, and acc + (-0.0) == acc for every acc: the row's sum is
+      // bitwise the form's own (the first / last interior rows rely on the
+      // same identity for their electrode neighbours).  Before, one lane's
+      // edge form sent the whole edge-strip wave to march_q_map: edge
+      // strips walked 69.8 vs 65.9 us (P, iteration 20000) and set the
+      // kernel's end (profiles/r5_2_mtrace_summary_it20000_L4096.txt)
+      const unsigned mask = a.St.F.rmask[a.ncls[0] >> 11];
+      const unsigned e0 = (c0w & g.lo0) | ((c0w & g.hi0) << 1);
+      const unsigned e1 = (c1w & g.lo1) | ((c1w & g.hi1) << 1);
+      q0 = march_q<0>(e0, dM0.x, W.C.e0, mask, W.U, W.C, W.Dn, ng0, nleak);
+      q1 = march_q<1>(e1, dM1.x, W.C.e1, mask, W.U, W.C, W.Dn, ng0, nleak);
+    } else if (uni) {
       const unsigned mask = a.St.F.rmask[ff];
       q0 = march_q<0>(c0w, dM0.x, W.C.e0, mask, W.U, W.C, W.Dn, ng0, nleak);
       q1 = march_q<1>(c1w, dM1.x, W.C.e1, mask, W.U, W.C, W.Dn, ng0, nleak);
@@ -462,14 +493,17 @@ __device__ __forceinline__ void march_step(const CGArgs& a, const MGeom& g, cons
       rn.y = W.rM.y - ak * q1;
       mr = rn;
       const double z0 = div_tab(rn.x, dM0), z1 = div_tab(rn.y, dM1);
-      acc[0] = acc[0] + z0 * rn.x;
-      acc[0] = acc[0] + z1 * rn.y;
-      acc[1] = acc[1] + rn.x * rn.x;
-      acc[1] = acc[1] + rn.y * rn.y;
+      t0 = make_double2(z0 * rn.x, z1 * rn.y);  // bknum's terms (bondc.f:785-787)
+      t1 = make_double2(rn.x * rn.x, rn.y * rn.y);  // snrm's (:872-875)
+      acc[0] = acc[0] + t0.x;
+      acc[0] = acc[0] + t0.y;
+      acc[1] = acc[1] + t1.x;
+      acc[1] = acc[1] + t1.y;
     } else {
       mq = make_double2(q0, q1);
-      acc[0] = acc[0] + q0 * W.C.e0;
-      acc[0] = acc[0] + q1 * W.C.e1;
+      t0 = make_double2(q0 * W.C.e0, q1 * W.C.e1);  // akden's terms (:803-805)
+      acc[0] = acc[0] + t0.x;
+      acc[0] = acc[0] + t0.y;
     }
   }
   {
@@ -477,10 +511,22 @@ __device__ __forceinline__ void march_step(const CGArgs& a, const MGeom& g, cons
     const unsigned eq = SM ? (unsigned)sm_at(a.T, mid, g.col) : (unsigned)((mid - g.r0) * m + g.col);
     if (MODE == kMarchPQ) bst2<kStAux>(B.q, mown ? eq * 8u : kOOB, mq);
     if (MODE == kMarchB) bst2<kStAux>(B.r, mown ? melem<SM>(a, B, mid, g.col) * 8u : kOOB, mr);
+    // literal dot terms at the row-major index (the LIT instantiation only:
+    // as a runtime-dropped store in the fast order it cost P ~1.7 us)
+    if constexpr (LIT) {
+      const unsigned to = mown ? (unsigned)(mid * m + g.col) * 8u : kOOB;
+      if (MODE != kMarchB) {
+        bst2<kNT>(B.t, to, t0);
+      } else {
+        const unsigned n8 = (unsigned)a.St.N * 8u;
+        bst2<kNT>(B.t, mown ? to + n8 : kOOB, t0);
+        bst2<kNT>(B.t, mown ? to + 2u * n8 : kOOB, t1);
+      }
+    }
   }
 }
 
-template <int MODE, int D, bool UP, bool SM, int PAUX = 0, bool PK = false>
+template <int MODE, int D, bool UP, bool SM, int PAUX = 0, bool PK = false, bool LIT = false>
 __device__ __forceinline__ void march_walk(const CGArgs& a, const MGeom& g, const MBuf& B,
                                            MRow (&ring)[D],
                                            bool first, double bk, double ak,
@@ -504,7 +550,7 @@ __device__ __forceinline__ void march_walk(const CGArgs& a, const MGeom& g, cons
       // view (loads return 0, stores are dropped) and finish no row
       const MRow R = ring[u];
       march_load<MODE, SM, PAUX, PK>(a, g, B, UP ? g.rend - (j + D) : g.r0 - 1 + j + D, first, psrc, ring[u]);
-      march_step<MODE, UP, SM>(a, g, B, R, UP ? g.rend - j : g.r0 - 1 + j, first, bk, ak, pnew, s_dt,
+      march_step<MODE, UP, SM, LIT, PK>(a, g, B, R, UP ? g.rend - j : g.r0 - 1 + j, first, bk, ak, pnew, s_dt,
                                s_rpos, s_rmap, s_w, W, acc);
     }
   }
@@ -515,7 +561,7 @@ __device__ __forceinline__ void march_walk(const CGArgs& a, const MGeom& g, cons
 // exit, hardware id} wall-clock stamps (100 MHz) into a.mtrace[4 w ..]
 // TAG: the epilogue reductions by tagged granules (publish_and_reduce_tagged)
 template <int MODE, bool SM = false, int D = kMarchDepth, int PAUX = 0, bool TR = false,
-          bool TAG = false, bool PK = false>
+          bool TAG = false, bool PK = false, bool LIT = false>
 __global__ __launch_bounds__(64 * kMarchWaves) void k_cg_march(CGArgs a) {
   const unsigned long long tr_t0 = TR ? wall_clock64() : 0ull;
   unsigned long long tr_t1 = 0ull;
@@ -555,6 +601,10 @@ __global__ __launch_bounds__(64 * kMarchWaves) void k_cg_march(CGArgs a) {
     // drains.  Band b = q * wslots + round, so neighbouring bands still
     // alternate walk directions.
     const int ns = a.wslots, ncu = gridDim.x / ns;
+    // (round 5: the round's workgroups taken in XCD-contiguous order, so a
+    // band's neighbouring strips share an L2 for their halo columns,
+    // measured no faster: P 76.75 vs 77.04 us, solve 0.1533 vs 0.1526 ms
+    // per iteration, profiles/r5_2_ab_L4096.json)
     const int sl = blockIdx.x / ncu, i = blockIdx.x - sl * ncu;
     const int v = __builtin_amdgcn_readfirstlane(i * kMarchWaves + (threadIdx.x >> 6));
     const int Q = ncu * kMarchWaves / spr;  // cycles per strip
@@ -587,6 +637,10 @@ __global__ __launch_bounds__(64 * kMarchWaves) void k_cg_march(CGArgs a) {
     g.cb0 = cls(g.col);
     g.cb1 = cls(g.col + 1);
     g.cbh = cls(g.hcol);
+    g.lo0 = g.col == 0 ? 1u : 0xFu;
+    g.hi0 = g.col == 0 ? 6u : 0u;
+    g.lo1 = g.col + 1 == m - 1 ? 3u : 0xFu;
+    g.hi1 = g.col + 1 == m - 1 ? 4u : 0u;
   }
   const MBuf B = march_bufs<MODE, SM, PK>(a, g, psrc, pnew);
   MRow ring[D];
@@ -606,8 +660,8 @@ __global__ __launch_bounds__(64 * kMarchWaves) void k_cg_march(CGArgs a) {
   double acc[2] = {0.0, 0.0};
   if (active) {
     double* s_w = s_win[threadIdx.x >> 6];
-    if (up) march_walk<MODE, D, true, SM, PAUX, PK>(a, g, B, ring, first, bk, ak, psrc, pnew, s_dt, s_rpos, s_rmap, s_w, acc);
-    else march_walk<MODE, D, false, SM, PAUX, PK>(a, g, B, ring, first, bk, ak, psrc, pnew, s_dt, s_rpos, s_rmap, s_w, acc);
+    if (up) march_walk<MODE, D, true, SM, PAUX, PK, LIT>(a, g, B, ring, first, bk, ak, psrc, pnew, s_dt, s_rpos, s_rmap, s_w, acc);
+    else march_walk<MODE, D, false, SM, PAUX, PK, LIT>(a, g, B, ring, first, bk, ak, psrc, pnew, s_dt, s_rpos, s_rmap, s_w, acc);
     if (MODE == kMarchP && !SM && !first && !a.bx) {
       // row-major q-free solve: x += ak p(k-1) on the band's x rows, after
       // the walk.  Inside it the x load feeding the x store made every step

@@ -51,8 +51,15 @@ struct ResArgs {
   int err_hist_cap;
   double* xch;       // [2 parity][G][top, bottom][r, p][m]
   unsigned* bar;     // 9 counters, 128 B apart (zeroed before the launch)
-  double* gran;      // [3][G] 16-B granules {partial, tag} (zeroed before the launch)
+  double* gran;      // [3][G] 16-B granules {partial, tag}, then kResLitGran result
+                     // granules of the literal folds (zeroed before the launch)
+  // literal dot order (PERC_DOT_LITERAL): the elements' q.p, z.r and r.r terms
+  // at their row-major index in lit[0..N), [N..2N), [2N..3N), folded in
+  // ascending j by workgroup 0 (res_fold); nullptr in the fast order (the
+  // term stores then go to a zero-size buffer view and are dropped)
+  double* lit;
 };
+constexpr int kResLitGran = 4;
 
 
 // single-level (m = 1024: 0.0166 vs 0.0178 ms per iteration)
@@ -196,6 +203,108 @@ __device__ __forceinline__ bool res_gather(const ResArgs& a, unsigned& epoch, do
   return ok;
 }
 
+// The literal dot order inside the resident solve (bondc.f:785-787, 803-805,
+// 872-875).  Every workgroup has stored its elements' terms of sums c0 ..
+// c0+NC-1 write-through (sc1) at lit[c N + i]; behind the workgroup barrier
+// that drains those stores thread 0 publishes an arrival granule {0, tag} in
+// `arr` (the kind's res_gather slot).  Wave 0 of workgroup 0 waits for all
+// G arrivals, folds the N terms of each sum in ascending j (fold_wave, sc1
+// loads: the terms come from every XCD's workgroups within this launch) and
+// publishes the totals as result granules {sum, tag}; wave 0 of every
+// workgroup polls them (s_sleep-paced: a fold takes milliseconds).  The
+// reduction's association is the reference's, so iter, err and every
+// iterate are its linbcg's bitwise.  A verification mode: one serial fold of
+// N terms per reduction.  Returns false after a timeout (a.S->pad[0] set).
+// workgroup 0's part (wave 0): wait for the G arrivals, fold, publish
+template <int NC>
+__device__ __forceinline__ int res_fold_wg0(const ResArgs& a, const double* arr, int c0, double tag) {
+  const int lane = threadIdx.x & 63, G = a.G, N = a.St.N;
+  const __amdgpu_buffer_rsrc_t ra = rsrc(arr, (unsigned)(G * 16));
+  const __amdgpu_buffer_rsrc_t rr = rsrc(a.gran + 6 * (size_t)G, (unsigned)(kResLitGran * 16));
+  int ok = 1;
+  for (unsigned spin = 0;; ++spin) {
+    bool all = true;
+    for (int i = lane; i < G; i += 64) {
+      const double2 g2 = __builtin_bit_cast(double2, __builtin_amdgcn_raw_buffer_load_b128(ra, i * 16, 0, 16));
+      all = all && g2.y == tag;
+    }
+    if (__builtin_amdgcn_readfirstlane(__all(all))) break;
+    if (spin > (1u << 24)) {
+      ok = 0;
+      break;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+  const __amdgpu_buffer_rsrc_t rl = rsrc(a.lit, (unsigned)N * 24u);
+  double acc[NC];
+#pragma unroll
+  for (int c = 0; c < NC; ++c) acc[c] = 0.0;
+  struct RawN {
+    double v[NC];
+  };
+  fold_wave<NC, 4, RawN, 8>(
+      N,
+      [&](int j) {
+        RawN r;
+#pragma unroll
+        for (int c = 0; c < NC; ++c) r.v[c] = bld1s(rl, (unsigned)((c0 + c) * (size_t)N + j) * 8u);
+        return r;
+      },
+      [&](const RawN& r, double (&t)[NC]) {
+#pragma unroll
+        for (int c = 0; c < NC; ++c) t[c] = r.v[c];
+      },
+      acc);
+  if (lane == 0)
+#pragma unroll
+    for (int c = 0; c < NC; ++c)
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, make_double2(acc[c], tag)), rr,
+                                             (c0 + c) * 16, 0, 16);
+  return ok;
+}
+
+template <int NC>
+__device__ __forceinline__ bool res_fold(const ResArgs& a, unsigned& epoch, double* arr, int c0,
+                                         double (&tot)[NC], double* s_red) {
+  __syncthreads();  // every wave's term stores complete (release)
+  ++epoch;
+  const double tag = (double)epoch;
+  const int G = a.G;
+  const __amdgpu_buffer_rsrc_t ra = rsrc(arr, (unsigned)(G * 16));
+  const __amdgpu_buffer_rsrc_t rr = rsrc(a.gran + 6 * (size_t)G, (unsigned)(kResLitGran * 16));
+  if (threadIdx.x == 0)
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, make_double2(0.0, tag)), ra,
+                                           (int)(blockIdx.x * 16), 0, 16);
+  if (threadIdx.x < 64) {
+    const int lane = threadIdx.x;
+    int ok = 1;
+    if (blockIdx.x == 0) ok = res_fold_wg0<NC>(a, arr, c0, tag);
+    double v = 0.0;
+    for (unsigned spin = 0; ok; ++spin) {
+      const double2 g2 = lane < NC ? __builtin_bit_cast(double2, __builtin_amdgcn_raw_buffer_load_b128(
+                                                                     rr, (c0 + lane) * 16, 0, 16))
+                                   : make_double2(0.0, tag);
+      v = g2.x;
+      if (__builtin_amdgcn_readfirstlane(__all(g2.y == tag))) break;
+      if (spin > (1u << 22)) {  // ~4 s at s_sleep 64 (64 x 64 cycles per poll)
+        ok = 0;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(64);
+    }
+    if (lane < NC) s_red[24 + lane] = v;
+    if (lane == 0) {
+      s_red[30] = ok ? 1.0 : 0.0;
+      if (!ok) a.S->pad[0] = 1;
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int c = 0; c < NC; ++c) tot[c] = s_red[24 + c];
+  const bool ok = s_red[30] != 0.0;
+  __syncthreads();  // s_red reuse
+  return ok;
+}
 
 // one raster position KP of an element's q (compile-time row / column
 // offsets: the neighbours' rows next to the band come from named registers,
@@ -266,7 +375,12 @@ __device__ __forceinline__ void res_pos_u(double& acc, unsigned mask, unsigned& 
 // UMC: compile-time superset of the raster positions the forms use (0x5A:
 // the square lattice's four neighbours), so unused positions and their
 // halo columns take no registers
-template <int MT, int HMAX, bool QREG = true, unsigned UMC = 0xFFu, int NT = kResThreads>
+// LIT: the literal dot order (a.lit): the elements' terms are stored and the
+// two all-gathers become res_fold's serial folds; every other line of the
+// loop is the fast instantiation's (a separate instantiation because the
+// fold's registers would otherwise join the fast loop's allocation: 122 ->
+// 256 VGPRs with spills at m = 1024)
+template <int MT, int HMAX, bool QREG = true, unsigned UMC = 0xFFu, int NT = kResThreads, bool LIT = false>
 __global__ __launch_bounds__(NT) void k_cg_res(ResArgs a) {
   __shared__ double s_p[kResLdsRows];
   __shared__ double2 s_dt[kDiagTab];
@@ -325,6 +439,9 @@ __global__ __launch_bounds__(NT) void k_cg_res(ResArgs a) {
       hcd[j][d] = has_dn && hin(j, d) ? a.St.code[(R0 + Hw) * m + hcol(j, d)] : 0u;
     }
   const __amdgpu_buffer_rsrc_t rx = rsrc(a.xch, (unsigned)((size_t)2 * G * 4 * m * 8));
+  // literal dot terms, write-through (sc1): workgroup 0 folds them in this
+  // launch (size 0 in the fast order: the stores are dropped)
+  const __amdgpu_buffer_rsrc_t rl = rsrc(a.lit, LIT ? (unsigned)N * 24u : 0u);
   // exchange rows: [parity][w][top, bottom][r, p][m]
   auto xrow = [&](int par, int ww, int tb, int rp) {
     return a.xch + ((((size_t)par * G + ww) * 2 + tb) * 2 + rp) * m;
@@ -472,16 +589,24 @@ __global__ __launch_bounds__(NT) void k_cg_res(ResArgs a) {
           const double xi = s_p[lr * m + t + j * NT];
           const double acc = qcalc(lr, j, xi);
           if constexpr (QREG) qv[lr][j] = acc;
-          dot = dot + acc * xi;
+          const double tq = acc * xi;  // akden's term (bondc.f:803-805)
+          dot = dot + tq;
+          if constexpr (LIT)
+            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, tq), rl,
+                                                  (int)((unsigned)((R0 + lr) * m + t + j * NT) * 8u), 0, 16);
         }
         // one element at a time (hoisting every element's LDS reads spills)
         __builtin_amdgcn_sched_barrier(0);
       }
     {
-      double v1[1] = {dot};
-      block_sum<1>(v1, s_red);
       double tot[1];
-      if (!(ok = res_gather<1>(a, epoch, a.gran, v1, tot, s_red))) break;
+      if constexpr (LIT) {
+        if (!(ok = res_fold<1>(a, epoch, a.gran, 0, tot, s_red))) break;
+      } else {
+        double v1[1] = {dot};
+        block_sum<1>(v1, s_red);
+        if (!(ok = res_gather<1>(a, epoch, a.gran, v1, tot, s_red))) break;
+      }
       ak = bknum / tot[0];
     }
     // 3. r, z, dots, x; the band's first / last rows of r(k+1) and p(k)
@@ -500,10 +625,17 @@ __global__ __launch_bounds__(NT) void k_cg_res(ResArgs a) {
           const double rn = rv[lr][j] - ak * qq;
           rv[lr][j] = rn;
           const double z = div_tab(rn, s_dt[diag_idx(code_at(lr, j))]);
-          acc2[0] = acc2[0] + z * rn;
-          acc2[1] = acc2[1] + rn * rn;
+          const double tz = z * rn, tr = rn * rn;  // bknum's, snrm's terms
+          acc2[0] = acc2[0] + tz;
+          acc2[1] = acc2[1] + tr;
           const double pk = s_p[lr * m + c];
           const int i = (R0 + lr) * m + c;
+          if constexpr (LIT) {
+            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, tz), rl,
+                                                  (int)((unsigned)(N + i) * 8u), 0, 16);
+            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, tr), rl,
+                                                  (int)((unsigned)(2 * N + i) * 8u), 0, 16);
+          }
           if (xreg) {
             if (x0w && lr == 0) xa[j] = xa[j] + ak * pk;
             if (x1w && lr == Hw - 1) xb[j] = xb[j] + ak * pk;
@@ -521,10 +653,14 @@ __global__ __launch_bounds__(NT) void k_cg_res(ResArgs a) {
         }
         if constexpr (!QREG) __builtin_amdgcn_sched_barrier(0);
       }
-    block_sum<2>(acc2, s_red);
     {
       double tot[2];
-      if (!(ok = res_gather<2>(a, epoch, a.gran + 2 * (size_t)G, acc2, tot, s_red))) break;
+      if constexpr (LIT) {
+        if (!(ok = res_fold<2>(a, epoch, a.gran + 2 * (size_t)G, 1, tot, s_red))) break;
+      } else {
+        block_sum<2>(acc2, s_red);
+        if (!(ok = res_gather<2>(a, epoch, a.gran + 2 * (size_t)G, acc2, tot, s_red))) break;
+      }
       err = sqrt(tot[1]) / bnrm;
       bk = tot[0] / bknum;
       bknum = tot[0];

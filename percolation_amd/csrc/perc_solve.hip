@@ -75,7 +75,10 @@ void klaunch(perc_ctx* h, K kern, dim3 g, dim3 b, hipStream_t st, const CGArgs& 
 template <int MODE, bool PK>
 void launch_march_sm2(perc_ctx* h, hipStream_t st, const CGArgs& a) {
   const int grid = a.wslots > 0 ? h->wm_grid : h->march_grid;
-  if (a.mgran) {
+  if (a.lit) {  // the literal dot order: the LIT instantiation (term stores)
+    if (a.mgran) klaunch(h, k_cg_march<MODE, true, 3, kNT, false, true, PK, true>, grid, 64 * kMarchWaves, st, a);
+    else klaunch(h, k_cg_march<MODE, true, 3, kNT, false, false, PK, true>, grid, 64 * kMarchWaves, st, a);
+  } else if (a.mgran) {
     if (a.mtrace) klaunch(h, k_cg_march<MODE, true, 3, kNT, true, true, PK>, grid, 64 * kMarchWaves, st, a);
     else klaunch(h, k_cg_march<MODE, true, 3, kNT, false, true, PK>, grid, 64 * kMarchWaves, st, a);
   } else if (a.mtrace) {
@@ -102,6 +105,9 @@ void launch_cg_spmv(perc_ctx* h, const CGArgs& a, int G) {
       // bands (march_grid): with the x update out of the walk, L = 8192 P
       // 0.314 vs 0.355 ms on one round of slot-weighted bands, 0.628 vs
       // 0.656 ms per solve iteration (profiles/r4_8_l8192_ab.json)
+      else if (h->qfree && a.lit)
+        klaunch(h, k_cg_march<kMarchP, false, kMarchDepth, 0, false, false, false, true>, h->march_grid,
+                64 * kMarchWaves, st, a);
       else if (h->qfree) klaunch(h, k_cg_march<kMarchP>, h->march_grid, 64 * kMarchWaves, st, a);
       // q-storing P+S (row slabs, the literal dot order, modes without QFREE)
       else klaunch(h, k_cg_march<kMarchPQ, false, 3>, h->march_grid, 64 * kMarchWaves, st, a);
@@ -135,6 +141,9 @@ void launch_cg_b(perc_ctx* h, const CGArgs& a, int G) {
     if (a.sm) launch_march_sm<kMarchB>(h, h->stream, a);
     // row-major B: 8-row bands (march_grid, P's too), nontemporal r(k) loads
     // (L = 8192: 0.300 vs 0.331 ms, profiles/r4_3_l8192_probe.json)
+    else if (a.lit)
+      klaunch(h, k_cg_march<kMarchB, false, kMarchDepth, kNT, false, false, false, true>, h->march_grid,
+              64 * kMarchWaves, h->stream, a);
     else klaunch(h, k_cg_march<kMarchB, false, kMarchDepth, kNT>, h->march_grid, 64 * kMarchWaves, h->stream, a);
   } else if (h->stencil) {
     // x on every row with the march's x-in-B (fused, row-major): XF
@@ -214,6 +223,10 @@ hipError_t dev_build_lattice(perc_ctx* h) {
   int nnz = 0;
   HIP_TRY(hipMemcpy(&nnz, d.rowptr + N, sizeof(int), hipMemcpyDeviceToHost));
   h->nnz = nnz;
+  // a lattice row has at most scn off-diagonals (square 4, triangular 6):
+  // the CSR kernels' entry slots per row (k_spmv<4> / k_cg_spmv_row<4> on
+  // the square lattice; the default 6 loaded two dead slots per row there)
+  h->csr_maxrow = g.scn;
   HIP_TRY(dmalloc(&d.col, (size_t)nnz + 8));
   HIP_TRY(dmalloc(&d.val, (size_t)nnz + 8));
   k_fill_col<<<blocks_for(N), kBlock, 0, st>>>(g, N, d.rowptr, d.col);
@@ -275,7 +288,7 @@ hipError_t dev_build_lattice(perc_ctx* h) {
   if (h->res_G > 0) {
     HIP_TRY(dmalloc(&d.res_xch, (size_t)2 * h->res_G * 2 * 2 * g.m));
     HIP_TRY(dmalloc(&d.res_bar, 9 * kTicketStride));
-    HIP_TRY(dmalloc(&d.res_gran, (size_t)2 * 3 * h->res_G));
+    HIP_TRY(dmalloc(&d.res_gran, (size_t)2 * (3 * h->res_G + kResLitGran)));
   }
   HIP_TRY(dmalloc(&d.partials, kRedSlots * red_partials_size(red_grid(h))));
   HIP_TRY(dmalloc(&d.tickets, kRedSlots * red_tickets_size(red_grid(h))));
@@ -319,7 +332,7 @@ void dev_free_all(perc_ctx* h) {
                   d.order, d.parent, d.member, d.top, d.counters, d.x, d.r,
                   d.p0, d.p1, d.q, d.partials, d.tickets, d.scal, d.err_hist, d.iout,
                   d.res_xch, d.res_bar, d.bw, d.code_sm, d.csize, d.res_gran, (void*)d.nib_sm,
-                  d.sel_hist, d.sel_cand, d.mgran, d.forms_dev};
+                  d.sel_hist, d.sel_cand, d.mgran, d.forms_dev, d.lit};
   for (void* p : ptrs)
     if (p) hipFree(p);
   d = DeviceBuffers{};
@@ -419,12 +432,17 @@ void select_format(perc_ctx* h) {
   h->stencil = h->fmt_req != PERC_FMT_CSR && h->stencil_ok;
   h->fused = h->stencil && h->tiled_ok && h->fmt_req != PERC_FMT_STENCIL_SPLIT;
   h->march = h->fused && h->march_ok && h->fmt_req != PERC_FMT_STENCIL_TILED;
+  // the literal dot order runs the production kernels: the q-free march and
+  // the resident solve store their rows' dot terms (a.lit / ResArgs::lit,
+  // 3 N doubles addressed by 32-bit buffer offsets: < 2 GB), which the
+  // serial folds sum; past that size the q-storing march (the folds then
+  // form the terms from q, p, r)
   const bool literal = h->dot_order == PERC_DOT_LITERAL;
+  const bool lit_ok = !literal || (size_t)h->N * 24 < ((size_t)1 << 31);
   // (dev_solve only: the march kernels stay selected for the probes)
   h->resident = h->fused && h->res_G > 0 && h->fmt_req != PERC_FMT_STENCIL_TILED &&
-                (h->march_mode & PERC_SOLVE_RESIDENT) && h->march_rows_req == 0 && !literal;
-  // the literal dot order folds q.p from the stored q: the q-storing kernels
-  h->qfree = h->march && (h->march_mode & PERC_MARCH_QFREE) && !literal;
+                (h->march_mode & PERC_SOLVE_RESIDENT) && h->march_rows_req == 0 && lit_ok;
+  h->qfree = h->march && (h->march_mode & PERC_MARCH_QFREE) && lit_ok;
   h->march_alt = h->march && (h->march_mode & PERC_MARCH_ALT);
   // one-workgroup solve for small systems, under the default format only
   // (an explicit format keeps its launched kernels, e.g. for the tests)
@@ -515,15 +533,20 @@ __global__ __launch_bounds__(1024) void k_res_sync_probe(ResArgs a, int iters) {
 // (NT threads per workgroup, m of them for m <= 1024: with one column per
 // thread the template's NT is only the launch bound, so widths up to 512
 // share the 512-bound instantiation -- 125-142 VGPRs, no spills)
-const void* res_kernel(int MT, bool sq, int NT) {
+template <bool LIT>
+const void* res_kernel_t(int MT, bool sq, int NT) {
   if (MT == 1 && NT <= 512)
-    return sq ? (const void*)k_cg_res<1, 4, true, kResSquareMask, 512>
-              : (const void*)k_cg_res<1, 4, true, 0xFFu, 512>;
+    return sq ? (const void*)k_cg_res<1, 4, true, kResSquareMask, 512, LIT>
+              : (const void*)k_cg_res<1, 4, true, 0xFFu, 512, LIT>;
   if (MT == 1)
-    return sq ? (const void*)k_cg_res<1, 4, true, kResSquareMask>
-              : (const void*)k_cg_res<1, 4, true, 0xFFu>;
-  return sq ? (const void*)k_cg_res<2, 8, false, kResSquareMask>
-            : (const void*)k_cg_res<2, 8, false, 0xFFu>;
+    return sq ? (const void*)k_cg_res<1, 4, true, kResSquareMask, kResThreads, LIT>
+              : (const void*)k_cg_res<1, 4, true, 0xFFu, kResThreads, LIT>;
+  return sq ? (const void*)k_cg_res<2, 8, false, kResSquareMask, kResThreads, LIT>
+            : (const void*)k_cg_res<2, 8, false, 0xFFu, kResThreads, LIT>;
+}
+// (lit: the literal dot order's instantiation, LIT = true)
+const void* res_kernel(int MT, bool sq, int NT, bool lit) {
+  return lit ? res_kernel_t<true>(MT, sq, NT) : res_kernel_t<false>(MT, sq, NT);
 }
 
 // one cooperative launch runs the whole iteration loop (k_cg_res)
@@ -546,14 +569,15 @@ hipError_t dev_solve_resident(perc_ctx* h, const CGArgs& ca, int* iter, double* 
   a.xch = d.res_xch;
   a.bar = d.res_bar;
   a.gran = d.res_gran;
+  a.lit = ca.lit;
   HIP_TRY(hipMemsetAsync(d.res_bar, 0, 9 * kTicketStride * sizeof(unsigned), st));
-  HIP_TRY(hipMemsetAsync(d.res_gran, 0, (size_t)2 * 3 * h->res_G * sizeof(double), st));
+  HIP_TRY(hipMemsetAsync(d.res_gran, 0, (size_t)2 * (3 * h->res_G + kResLitGran) * sizeof(double), st));
   void* args[] = {&a};
   // reductions by tagged-granule all-gather (res_gather): L = 1024 15.5 vs
   // 16.6 us per iteration against a counter barrier + partial reads, L =
   // 2048 33.7 vs 34.65 (profiles/r2_10_resident_gather_ab.log)
   const bool sq = (h->forms.umask & ~kResSquareMask) == 0;
-  const void* fn = res_kernel(h->res_MT, sq, h->res_NT);
+  const void* fn = res_kernel(h->res_MT, sq, h->res_NT, a.lit != nullptr);
   KernelTiming& T = h->timing;
   if (T.enabled) {
     if (T.ev.size() < 2) T.ev.resize(2, nullptr);
@@ -583,8 +607,23 @@ hipError_t dev_solve_resident(perc_ctx* h, const CGArgs& ca, int* iter, double* 
 }
 
 
+namespace {
+hipError_t dev_solve_impl(perc_ctx* h, int itol, double tol, int itmax, bool x0_zero, bool full_x,
+                          int* iter, double* err);
+}
+
 hipError_t dev_solve(perc_ctx* h, int itol, double tol, int itmax, bool x0_zero, bool full_x,
                      int* iter, double* err) {
+  h->last_kernel = h->last_flags = 0;
+  h->last_iter = -1;
+  const hipError_t e = dev_solve_impl(h, itol, tol, itmax, x0_zero, full_x, iter, err);
+  if (e == hipSuccess) h->last_iter = *iter;
+  return e;
+}
+
+namespace {
+hipError_t dev_solve_impl(perc_ctx* h, int itol, double tol, int itmax, bool x0_zero, bool full_x,
+                          int* iter, double* err) {
   DeviceBuffers& d = h->d;
   hipStream_t st = h->stream;
   const bool literal = h->dot_order == PERC_DOT_LITERAL;
@@ -610,7 +649,10 @@ hipError_t dev_solve(perc_ctx* h, int itol, double tol, int itmax, bool x0_zero,
   }
   // row slabs (perc_set_slabs; the prologue starts from x = 0, as linbcg's
   // callers do)
-  if (h->nslab > 1 && x0_zero) return dev_solve_slabs(h, h->nslab, itol, tol, itmax, full_x, iter, err);
+  if (h->nslab > 1 && x0_zero) {
+    h->last_kernel = PERC_RAN_SLABS;
+    return dev_solve_slabs(h, h->nslab, itol, tol, itmax, full_x, iter, err);
+  }
   CGArgs a = make_cg_args(h);
   // linbcg never reads x inside the iteration (r is recursive), and the
   // terminal currents read it only on the interior rows next to the
@@ -628,6 +670,14 @@ hipError_t dev_solve(perc_ctx* h, int itol, double tol, int itmax, bool x0_zero,
     else k_fold_init<false><<<1, 64, 0, st>>>(a, itol);
     HIP_TRY(dbg_sync(st, "k_fold_init"));
   }
+  // the production kernels in the literal order store their terms (a.lit):
+  // the q-free march and the resident solve
+  if (literal && !h->small && (h->resident || (h->march && h->qfree))) {
+    if (!d.lit) HIP_TRY(dmalloc(&d.lit, (size_t)3 * h->N + 8));
+    a.lit = d.lit;
+  }
+  h->last_kernel = h->small ? PERC_RAN_SMALL : (h->resident ? PERC_RAN_RESIDENT : (h->march ? PERC_RAN_MARCH : 0));
+  h->last_flags = (literal ? PERC_RAN_LITERAL : 0) | (a.lit ? PERC_RAN_LIT_TERMS : 0);
   if (h->small) {  // one workgroup runs the whole loop (k_cg_small)
     // (x is kept on every row here: the operator is the CSR one and N small)
     if (ST) {
@@ -656,9 +706,14 @@ hipError_t dev_solve(perc_ctx* h, int itol, double tol, int itmax, bool x0_zero,
     fprintf(stderr, "[perc] resident solve not launchable (%s): launched kernels\n",
             hipGetErrorString(e));
     h->resident = false;
+    h->last_kernel = h->march ? PERC_RAN_MARCH : 0;
   }
+  if (!(h->march && h->qfree)) a.lit = nullptr;  // (the other kernels store no terms)
   if (h->strips) HIP_TRY(to_strips(h, a));
   HIP_TRY(setup_granules(h, a, itmax));
+  h->last_flags = (literal ? PERC_RAN_LITERAL : 0) | (a.lit ? PERC_RAN_LIT_TERMS : 0) |
+                  (h->march && h->qfree ? PERC_RAN_QFREE : 0) | (a.sm ? PERC_RAN_STRIPS : 0) |
+                  (a.nib ? PERC_RAN_NIBBLE : 0) | (a.mgran ? PERC_RAN_TAG : 0);
   // iterate in chunks; the device flag makes surplus launches no-ops
   int chunk = 8;
   CGScalars* hsp = nullptr;
@@ -783,6 +838,7 @@ hipError_t dev_solve(perc_ctx* h, int itol, double tol, int itmax, bool x0_zero,
   hipHostFree(hsp);
   return e;
 }
+}  // namespace
 
 hipError_t dev_spmv(perc_ctx* h, const double* x, double* y) {
   if (!h->stencil) HIP_TRY(ensure_csr(h));

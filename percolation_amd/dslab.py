@@ -176,7 +176,12 @@ def solve(ctx, rule=L.RULE_BOND, cur_rule=L.CUR_FORTRAN, Va=1.0, g0=1.0, leak=LE
     process."""
     lib = L.lib()
     K, s = dist.get_world_size(group), dist.get_rank(group)
-    if getattr(ctx, "_dslab_rank", None) != (K, s):
+    # the communicator belongs to this group: keyed on its members and its
+    # identity too, so another group of the same size and rank makes (and
+    # perc_dslab_comm_init's release of the old one frees) a new one
+    ranks = tuple(dist.get_process_group_ranks(group)) if group is not None else tuple(range(K))
+    key = (K, s, ranks, id(group) if group is not None else None)
+    if getattr(ctx, "_dslab_rank", None) != key:
         uid = C.create_string_buffer(L.DSLAB_ID_BYTES)
         if s == 0:
             L.check(lib.perc_dslab_unique_id(uid, L.DSLAB_ID_BYTES), "perc_dslab_unique_id")
@@ -185,7 +190,7 @@ def solve(ctx, rule=L.RULE_BOND, cur_rule=L.CUR_FORTRAN, Va=1.0, g0=1.0, leak=LE
                                    group=group)
         uid = C.create_string_buffer(box[0], L.DSLAB_ID_BYTES)
         L.check(lib.perc_dslab_comm_init(ctx.h, K, s, uid, L.DSLAB_ID_BYTES), "perc_dslab_comm_init")
-        ctx._dslab_rank = (K, s)
+        ctx._dslab_rank = key
     res = L.CondResult()
     L.check(lib.perc_dslab_solve(ctx.h, rule, cur_rule, Va, g0, leak, itol, tol, itmax, int(full_x),
                                  C.byref(res)), "perc_dslab_solve")

@@ -12,8 +12,11 @@
 ! spanning cluster's bonds -g0*rand('twister', cseed) (MATLAB/ConductCalc.m
 ! condtype 2; 1, the default, fixed g0).  nslab > 1 splits the solve into row
 ! slabs over nslab contexts (devices device .. device+nslab-1 with xport 0,
-! RCCL; all on `device` with xport 1, host-staged); dot_order 1 folds
-! linbcg's sums in the reference's order (bitwise its solve).  Outputs as
+! RCCL; all on `device` with xport 1, host-staged); the split solve runs the
+! slab march, so it needs m a multiple of 128, fixed conductances (condtype
+! 1: the stencil operator) and the fast dot order -- otherwise the driver
+! warns on stderr and solves on one context (perc_conductance).  dot_order 1
+! folds linbcg's sums in the reference's order (bitwise its solve).  Outputs as
 ! the reference: bondorder.txt (i10,",",i10) in
 ! shuffled order (bondc.f:177-180), bond.txt (b1, b2, label, j, c(j);
 ! bondc.f:600-604) and the run summary on stdout.
@@ -174,6 +177,11 @@ program bondc
     if (dot_order /= PERC_DOT_FAST) call perc_check(perc_set_dot_order(h, dot_order), 'perc_set_dot_order')
     if (condtype == 2) call perc_check(perc_set_conductcalc_weights(h, PERC_RULE_BOND, cseed), &
                                        'perc_set_conductcalc_weights')
+    if (nslab > 1 .and. (mod(m, 128) /= 0 .or. condtype == 2 .or. dot_order /= PERC_DOT_FAST)) then
+      write(0, '(a)') 'bondc: nslab > 1 needs m a multiple of 128, condtype 1 and dot_order 0;' // &
+                      ' solving on one context'
+      nslab = 1
+    end if
     if (nslab > 1) then
       ! the same occupancy labeled on every slab's context, then one split solve
       allocate(hs(nslab))

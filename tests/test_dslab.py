@@ -79,13 +79,13 @@ def _system(lat, m, n, pbc, p, seed):
     return api.shuffled_ids(nb, seed), int(p * nb)
 
 
-def _solve_worker(rank, world, port, backend, case, tol, q, inlib=False):
+def _solve_worker(rank, world, port, backend, case, tol, q, inlib=False, per_device=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group(backend, rank=rank, world_size=world)
     try:
         lat, m, n, pbc = case[:4]
         order, tb = _system(*case)
-        with api.Context(lat, m, n, pbc) as ctx:
+        with api.Context(lat, m, n, pbc, device=rank if per_device else 0) as ctx:
             ctx.occupy(PL.BOND, bond_order=order, nbonds_=tb)
             assert ctx.label()["nspan"] > 0
             if inlib:  # perc_dslab_solve: the loop inside libperc, own RCCL communicator
@@ -101,11 +101,11 @@ def _solve_worker(rank, world, port, backend, case, tol, q, inlib=False):
         dist.destroy_process_group()
 
 
-def _run(world, backend, case, tol, inlib=False):
+def _run(world, backend, case, tol, inlib=False, per_device=False):
     ctx = mp.get_context("spawn")
     q = ctx.SimpleQueue()
-    mp.spawn(_solve_worker, args=(world, free_port(), backend, case, tol, q, inlib), nprocs=world,
-             join=True)
+    mp.spawn(_solve_worker, args=(world, free_port(), backend, case, tol, q, inlib, per_device),
+             nprocs=world, join=True)
     out = {}
     while not q.empty():
         r, res = q.get()
@@ -221,3 +221,102 @@ def test_per_process_solve_world_one():
     want = _group(1, case, PL.XPORT_RCCL, 1e-12)
     assert (got["iter"], got["gtop"], got["gbot"], got["err"]) == \
         (want["iter"], want["gtop"], want["gbot"], want["err"]), (got, want)
+
+
+def _failure_worker(rank, world, port, case, q):
+    """world 1: a rank whose local preparation fails (the literal dot order,
+    which a split solve cannot run) must still reach perc_dslab_solve's
+    agreement all-reduce and return the error through it -- not before it,
+    where peers would wait forever -- and the communicator stays
+    usable for the next call"""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        lat, m, n, pbc = case[:4]
+        order, tb = _system(*case)
+        with api.Context(lat, m, n, pbc) as ctx:
+            ctx.occupy(PL.BOND, bond_order=order, nbonds_=tb)
+            assert ctx.label()["nspan"] > 0
+            ctx.set_march_mode(PL.MARCH_ALT)
+            ctx.set_dot_order(PL.DOT_LITERAL)
+            try:
+                dslab.solve(ctx, tol=1e-10, itmax=100000)
+                failed = None
+            except PL.PercError as e:
+                failed = str(e)
+            ctx.set_dot_order(PL.DOT_FAST)
+            r = dslab.solve(ctx, tol=1e-10, itmax=100000)
+        q.put((rank, failed, r))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_per_process_solve_failure_is_agreed():
+    ctx = mp.get_context("spawn")
+    q = ctx.SimpleQueue()
+    mp.spawn(_failure_worker, args=(1, free_port(), CASES[0], q), nprocs=1, join=True)
+    rank, failed, r = q.get()
+    assert failed is not None and "literal" in failed, failed
+    assert r["iter"] > 0 and r["gtop"] > 0, r
+
+
+# ------------------------------------------------- several GPUs (skipped on one-GPU boxes)
+# The pool's boxes have one GPU: these K = 2 RCCL paths -- the ncclSend /
+# ncclRecv halo swap, the all-gather across devices, the top-row hand-off
+# (group: hipMemcpyPeer; per process: ncclSend / ncclRecv) -- have not run on
+# hardware yet (INTEGRATION.md, "Unverified on hardware").
+two_gpus = pytest.mark.skipif(not torch.cuda.is_available() or torch.cuda.device_count() < 2,
+                              reason="needs 2 GPUs (RCCL allows one rank per device)")
+
+
+@pytest.mark.gpu
+@two_gpus
+def test_group_solve_over_rccl_two_devices():
+    """perc_dslab_solve_group over RCCL with slab s on device s (K = 2):
+    perc_set_slabs(2)'s numbers in one context, bitwise"""
+    case = CASES[0]
+    lat, m, n, pbc = case[:4]
+    order, tb = _system(*case)
+    with api.Context(lat, m, n, pbc) as ctx:
+        ctx.occupy(PL.BOND, bond_order=order, nbonds_=tb)
+        ctx.label()
+        ctx.set_march_mode(PL.MARCH_ALT)
+        ctx.set_slabs(2)
+        ref = ctx.conductance(tol=1e-12, itmax=100000)
+    ctxs = [api.Context(lat, m, n, pbc, device=d) for d in range(2)]
+    try:
+        for c in ctxs:
+            c.set_march_mode(PL.MARCH_ALT)
+            c.occupy(PL.BOND, bond_order=order, nbonds_=tb)
+            c.label()
+        got = api.dslab_solve_group(ctxs, xport=PL.XPORT_RCCL, tol=1e-12, itmax=100000)
+    finally:
+        for c in ctxs:
+            c.close()
+    assert (got["iter"], got["err"], got["gtop"], got["gbot"]) == \
+        (ref["iter"], ref["err"], ref["gtop"], ref["gbot"]), (got, ref)
+
+
+@pytest.mark.gpu
+@two_gpus
+def test_per_process_solve_two_devices():
+    """perc_dslab_solve, one process per GPU (K = 2, RCCL from rank 0's
+    unique id): both ranks report the group solver's numbers bitwise"""
+    case = CASES[0]
+    out = _run(2, "gloo", case, 1e-12, inlib=True, per_device=True)
+    lat, m, n, pbc = case[:4]
+    order, tb = _system(*case)
+    ctxs = [api.Context(lat, m, n, pbc, device=d) for d in range(2)]
+    try:
+        for c in ctxs:
+            c.set_march_mode(PL.MARCH_ALT)
+            c.occupy(PL.BOND, bond_order=order, nbonds_=tb)
+            c.label()
+        want = api.dslab_solve_group(ctxs, xport=PL.XPORT_RCCL, tol=1e-12, itmax=100000)
+    finally:
+        for c in ctxs:
+            c.close()
+    for r in range(2):
+        assert (out[r]["iter"], out[r]["gtop"], out[r]["gbot"]) == \
+            (want["iter"], want["gtop"], want["gbot"]), (r, out[r], want)

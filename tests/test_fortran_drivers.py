@@ -185,6 +185,28 @@ def test_bondc_driver_split_solve(nslab, tmp_path):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("extra", ["", "dot_order=1", "condtype=2"])
+def test_bondc_driver_split_solve_falls_back(extra, tmp_path):
+    """nslab > 1 where the split solve does not apply (the reference's m =
+    50, not a multiple of 128; the literal dot order; condtype 2's CSR
+    operator): a warning on stderr and the one-context solve -- the same
+    output as nslab = 1, not an abort"""
+    prog = exe("bondc", 0)
+    out = {}
+    m = 50 if not extra else 128
+    for k in (1, 2):
+        d = tmp_path / ("k%d" % k)
+        d.mkdir()
+        (d / "bondc.nml").write_text("&bondc_nml lattice=0, m=%d, n=60, pbc=0, pb=0.6, seed=626504, "
+                                     "nslab=%d, xport=1%s /\n" % (m, k, (", " + extra) if extra else ""))
+        r = subprocess.run([prog], cwd=d, capture_output=True, text=True, timeout=600)
+        assert r.returncode == 0, r.stderr[-2000:]
+        assert ("solving on one context" in r.stderr) == (k > 1), r.stderr[-2000:]
+        out[k] = ([l for l in r.stdout.splitlines() if "Conductance:" in l], (d / "bond.txt").read_bytes())
+    assert out[1] == out[2]
+
+
+@pytest.mark.gpu
 def test_bondc_driver_random_conductances(tmp_path):
     """condtype = 2 (ConductCalc.m condtype 2 from the Fortran host:
     perc_set_conductcalc_weights): the driver's conductance equals the

@@ -38,6 +38,43 @@ def test_exports_every_declared_symbol():
     P.lib()  # signatures bind
 
 
+_RUNTIMES_PROBE = """
+import re, sys
+sys.path.insert(0, %r)
+from percolation_amd import _lib as PL
+PL.lib()
+import torch  # after libperc: the order that used to load a second runtime
+maps = open('/proc/self/maps').read()
+print(sorted(set(re.findall(r'(/\\S*(?:libamdhip64|libhsa-runtime64|librccl)\\S*)', maps))))
+"""
+
+
+@pytest.mark.parametrize("no_torch", [False, True])
+def test_one_hip_runtime_per_process(no_torch):
+    """libperc loaded before torch must not leave two HIP / HSA / RCCL
+    runtimes in the process: that was round 4's interpreter-teardown abort
+    (glibc "double free or corruption (!prev)", SIGABRT), reproduced here
+    without a GPU by the PERC_NO_TORCH=1 run (libperc on /opt/rocm's copies,
+    torch then loads its own); _lib.lib() imports torch first, so the
+    default run exits 0 with torch's copies alone"""
+    import subprocess
+    import sys
+    pytest.importorskip("torch")
+    env = dict(os.environ)
+    env.pop("PERC_NO_TORCH", None)
+    if no_torch:
+        env["PERC_NO_TORCH"] = "1"
+    r = subprocess.run([sys.executable, "-c", _RUNTIMES_PROBE % REPO], capture_output=True, text=True,
+                       timeout=300, env=env)
+    libs = eval(r.stdout.strip().splitlines()[-1])
+    hip = [x for x in libs if "libamdhip64" in x]
+    if no_torch:  # the failure this guards against, shown to still exist without the guard
+        assert len(hip) == 2 and r.returncode != 0, (libs, r.returncode, r.stderr[-500:])
+    else:
+        assert len(hip) == 1 and len(libs) == 3, libs
+        assert r.returncode == 0, r.stderr[-2000:]
+
+
 def test_no_device_is_an_error_not_a_fallback():
     try:
         import torch

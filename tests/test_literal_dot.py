@@ -12,9 +12,14 @@ default solve to the association of the three sums alone.
 
 Pins: every reference bondc golden (tests/golden/*bondc*, made by the
 compiled reference, square / triangular / pbc / tight tolerance) in every
-solver family that folds (one-workgroup, LDS-tiled, split stencil, CSR),
-and the oracle's literal linbcg (oracle/perc_oracle.c, itself bitwise the
-reference at <= 64^2) at 128^2 .. 256^2 through the register-march kernels.
+solver family (one-workgroup, the resident solve, LDS-tiled, split stencil,
+CSR), and the oracle's literal linbcg (oracle/perc_oracle.c, itself bitwise
+the reference at <= 64^2) at 128^2 .. 512^2 through the PRODUCTION kernels:
+the resident cooperative solve (k_cg_res, configs 2-4's solver) and the
+q-free strip-major march with nibble codes and tagged reductions (k_cg_march
+P / B, the metric's kernels).  Those kernels store their rows' dot terms and
+the folds sum them (perc_last_solve: lit_terms); the q-storing march is no
+longer part of the literal path.
 """
 import numpy as np
 import pytest
@@ -27,8 +32,11 @@ from percolation_amd import api
 pytestmark = pytest.mark.gpu
 
 BONDC = [v for v in G.variants() if G.meta(v)["kind"] == "bondc" and G.meta(v)["perccln"]]
-# PERC_FMT_AUTO runs the one-workgroup solver at these sizes (k_cg_small<LIT>)
-FAMILIES = [PL.FMT_AUTO, PL.FMT_STENCIL_TILED, PL.FMT_STENCIL_SPLIT, PL.FMT_CSR]
+# PERC_FMT_AUTO runs the one-workgroup solver at these sizes (k_cg_small<LIT>),
+# PERC_FMT_STENCIL the resident solve (k_cg_res<..., LIT>)
+FAMILIES = [PL.FMT_AUTO, PL.FMT_STENCIL, PL.FMT_STENCIL_TILED, PL.FMT_STENCIL_SPLIT, PL.FMT_CSR]
+# the march without the resident solve (PERC_SOLVE_RESIDENT off)
+MARCH_ONLY = PL.MARCH_DEFAULT & ~PL.SOLVE_RESIDENT
 
 
 def bits(a):
@@ -50,7 +58,13 @@ def test_literal_solve_is_the_reference_bitwise(v, fmt):
         except PL.PercError as e:  # this lattice has no such operator (e.g. odd m, tiles)
             pytest.skip(str(e))
         hist = ctx.err_history()
+        ran = ctx.last_solve()
         c = ctx.conductance(tol=tol, itmax=itmax, vint=True)
+    if fmt == PL.FMT_STENCIL and not p["pbc"]:
+        # the production resident kernel, folding its own terms (pbc: wrapped
+        # forms, no resident grid: the LDS-tiled kernel at m = 50)
+        assert ran["kernel"] == "resident" and ran["lit_terms"], ran
+    assert ran["literal"] and ran["iter"] == r["iter"], ran
     assert r["perccln"] == md["perccln"]
     assert r["iter"] == md["iter"], (r["iter"], md["iter"])
     assert np.array_equal(bits(hist), bits(md["linbcg_err"]))
@@ -60,15 +74,21 @@ def test_literal_solve_is_the_reference_bitwise(v, fmt):
         assert np.array_equal(bits(c["vint"]), bits(md["vint"]))
 
 
-@pytest.mark.parametrize("fmt", [PL.FMT_AUTO, PL.FMT_STENCIL, PL.FMT_CSR])
-@pytest.mark.parametrize("lat,m,n,pbc,p,seed", [(0, 128, 128, 0, 0.6, 21), (0, 256, 150, 0, 0.55, 31),
-                                                 (1, 128, 99, 0, 0.4, 22), (0, 256, 256, 1, 0.6, 32)])
-def test_literal_solve_is_the_oracle_linbcg_bitwise(lat, m, n, pbc, p, seed, fmt):
-    """Larger lattices, m a multiple of 128: the q-storing register march
-    (PERC_FMT_STENCIL; PERC_FMT_AUTO takes it too -- the resident solve has
-    no literal fold) and CSR, against the oracle's literal linbcg at the
-    reference tolerance and converged: iter, err history, Gtop, Gbot and
-    every voltage bitwise."""
+SOLVERS = ["resident", "march", "csr"]
+LATTICES = [(0, 128, 128, 0, 0.6, 21), (0, 256, 150, 0, 0.55, 31), (1, 128, 99, 0, 0.4, 22),
+            (0, 256, 256, 1, 0.6, 32), (0, 512, 512, 0, 0.6, 33)]
+
+
+@pytest.mark.parametrize("solver", SOLVERS)
+@pytest.mark.parametrize("lat,m,n,pbc,p,seed", LATTICES)
+def test_literal_solve_is_the_oracle_linbcg_bitwise(lat, m, n, pbc, p, seed, solver):
+    """Larger lattices, m a multiple of 128, against the oracle's literal
+    linbcg at the reference tolerance and at 1e-13: iter, err history, Gtop,
+    Gbot and every voltage bitwise -- through the production kernels: the
+    resident solve (PERC_FMT_AUTO, where the lattice fits it) and the q-free
+    strip-major march (P / B, nibble codes on the square lattice, tagged
+    reductions: the metric's kernels), each storing its own dot terms; and
+    CSR (terms folded from q, p, r)."""
     b1, b2 = api.bond_list(lat, m, n, pbc)
     nb = len(b1)
     order = api.shuffled_ids(nb, seed)
@@ -80,16 +100,29 @@ def test_literal_solve_is_the_oracle_linbcg_bitwise(lat, m, n, pbc, p, seed, fmt
                            gval)
     with api.Context(lat, m, n, pbc) as ctx:
         ctx.set_dot_order(PL.DOT_LITERAL)
-        ctx.set_matrix_format(fmt)
+        if solver == "csr":
+            ctx.set_matrix_format(PL.FMT_CSR)
+        elif solver == "march":
+            ctx.set_march_mode(MARCH_ONLY)
         ctx.occupy(PL.BOND, bond_order=order, nbonds_=tb)
         ctx.label()
         for tol in (1e-8, 1e-13):
             oc = O.conductance(lat, m, n, pbc, b1, b2, gval, tol=tol, itmax=100000)
             c = ctx.conductance(tol=tol, itmax=100000, vint=True)
             hist = ctx.err_history()
-            info = ctx.march_info()
-            if fmt != PL.FMT_CSR and m % 128 == 0:
-                assert info["kernel"] == "wave" and not info["qfree"], info
+            ran = ctx.last_solve()
+            assert ran["literal"] and ran["iter"] == c["iter"], ran
+            if solver == "resident" and not pbc:  # (pbc: wrapped forms, no resident grid)
+                assert ran["kernel"] == "resident" and ran["lit_terms"], ran
+            elif solver != "csr":
+                # the metric's kernels: q-free, strip-major, tagged; nibble
+                # codes on the open square lattice
+                assert ran["kernel"] == "march" and ran["lit_terms"], ran
+                assert ran["qfree"] and ran["strips"] and ran["tag"], ran
+                if lat == 0 and not pbc:
+                    assert ran["nibble"], ran
+            else:
+                assert ran["kernel"] == "other" and not ran["lit_terms"], ran
             assert c["iter"] == oc["iter"], (tol, c["iter"], oc["iter"])
             assert np.array_equal(bits(hist), bits(oc["errs"])), tol
             assert c["gtop"] == oc["gtop"] and c["gbot"] == oc["gbot"], (tol, c["gtop"], oc["gtop"])

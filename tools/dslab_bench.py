@@ -78,10 +78,7 @@ def main():
         dist.destroy_process_group()
         print("torch leg: group destroyed", file=sys.stderr, flush=True)
         print(json.dumps({"python_dslab_nccl_ms_per_it": ms}), flush=True)
-        # (this leg's interpreter teardown aborts with a glibc "double free"
-        # after everything above has run -- profiles/r4_9_rccl_exit_probe.log
-        # has the Python slab loop at 256^2 exiting cleanly; skip the teardown)
-        os._exit(0)
+        return  # (normal teardown: one HIP runtime per process, _lib._one_runtime)
     # every leg measured once per round, the legs interleaved round after
     # round (clock and power state drift between legs otherwise), best of rounds
     legs = [("single_context", None), ("group_k1", PL.XPORT_RCCL),
