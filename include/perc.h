@@ -455,6 +455,13 @@ int perc_set_band_weights(perc_ctx *h, int which, int n, const int *w);
    (perc_nr_set_dot_order). */
 #define PERC_DOT_FAST 0
 #define PERC_DOT_LITERAL 1
+/* PERC_DOT_LITERAL_HOST: the literal order with the three serial sums formed
+   by the host CPU from the terms the q-free march kernels stored (the same
+   IEEE adds in the same ascending-j order, so bitwise PERC_DOT_LITERAL; the
+   CPU's dependent fp64 add is ~4x shorter than a GPU wave's, which makes the
+   config-size verification runs fit one GPU session).  Runs the launched
+   march (not the resident solve); formats without it fold on the GPU. */
+#define PERC_DOT_LITERAL_HOST 2
 int perc_set_dot_order(perc_ctx *h, int order);
 /* What the last solve of the context actually ran: out4[0] = kernel family
    (0 other launched kernels: LDS tiles, split stencil, CSR; PERC_RAN_MARCH,
@@ -471,6 +478,7 @@ int perc_set_dot_order(perc_ctx *h, int order);
 #define PERC_RAN_STRIPS 8     /* strip-major layout */
 #define PERC_RAN_NIBBLE 16    /* 4-bit row codes */
 #define PERC_RAN_TAG 32       /* tagged-granule reductions */
+#define PERC_RAN_HOST_FOLD 64 /* PERC_DOT_LITERAL_HOST: the sums folded by the host */
 int perc_last_solve(perc_ctx *h, int *out4);
 /* err of every iteration of the last solve (linbcg's per-iteration
    `write (*,*) iter, err`, bondc.f:834): min(cap, iterations) values into

@@ -29,10 +29,10 @@ MARCH_QFREE, MARCH_ALT, SOLVE_RESIDENT, MARCH_STRIPS, MARCH_SLOTS, MARCH_TAG = 1
 MARCH_NIBBLE = 512
 MARCH_DEFAULT = (MARCH_QFREE | MARCH_ALT | SOLVE_RESIDENT | MARCH_STRIPS | MARCH_SLOTS | MARCH_TAG
                  | MARCH_NIBBLE)
-DOT_FAST, DOT_LITERAL = 0, 1
+DOT_FAST, DOT_LITERAL, DOT_LITERAL_HOST = 0, 1, 2
 # perc_last_solve: kernel family and flag bits of the last solve
 RAN_OTHER, RAN_MARCH, RAN_SLABS, RAN_RESIDENT, RAN_SMALL = 0, 1, 2, 3, 4
-RAN_LITERAL, RAN_LIT_TERMS, RAN_QFREE, RAN_STRIPS, RAN_NIBBLE, RAN_TAG = 1, 2, 4, 8, 16, 32
+RAN_LITERAL, RAN_LIT_TERMS, RAN_QFREE, RAN_STRIPS, RAN_NIBBLE, RAN_TAG, RAN_HOST_FOLD = 1, 2, 4, 8, 16, 32, 64
 XPORT_RCCL, XPORT_HOST, XPORT_EXCHANGE = 0, 1, 4
 DSLAB_ID_BYTES = 128
 

@@ -313,7 +313,8 @@ class Context:
         return dict(kernel=("other", "march", "slabs", "resident", "small")[out[0]],
                     literal=bool(f & L.RAN_LITERAL), lit_terms=bool(f & L.RAN_LIT_TERMS),
                     qfree=bool(f & L.RAN_QFREE), strips=bool(f & L.RAN_STRIPS),
-                    nibble=bool(f & L.RAN_NIBBLE), tag=bool(f & L.RAN_TAG), iter=int(out[2]))
+                    nibble=bool(f & L.RAN_NIBBLE), tag=bool(f & L.RAN_TAG),
+                    host_fold=bool(f & L.RAN_HOST_FOLD), iter=int(out[2]))
 
     def matrix_format(self):
         rc = L.lib().perc_matrix_format(self.h)

@@ -271,7 +271,7 @@ int check_ctx(perc_ctx* h, const perc_ctx* ref) {
   const Geom& a = ref->g;
   const Geom& g = h->g;
   if (g.m != a.m || g.n != a.n || g.lattice != a.lattice || g.pbc != a.pbc) return PERC_EINVAL;
-  if (h->dot_order == PERC_DOT_LITERAL) {
+  if (h->dot_order != PERC_DOT_FAST) {
     set_error("perc_dslab: the literal dot order needs one slab (perc_conductance)");
     return PERC_EINVAL;
   }

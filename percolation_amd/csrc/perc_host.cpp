@@ -928,7 +928,8 @@ int perc_set_band_weights(perc_ctx* h, int which, int n, const int* w) {
 }
 
 int perc_set_dot_order(perc_ctx* h, int order) {
-  if (!h || (order != PERC_DOT_FAST && order != PERC_DOT_LITERAL)) return PERC_EINVAL;
+  if (!h || (order != PERC_DOT_FAST && order != PERC_DOT_LITERAL && order != PERC_DOT_LITERAL_HOST))
+    return PERC_EINVAL;
   h->dot_order = order;
   if (h->assembled) select_format(h);
   return PERC_OK;

@@ -75,6 +75,33 @@ __device__ __forceinline__ double2 gran_poll(__amdgpu_buffer_rsrc_t rg, int off,
   return g2;
 }
 
+// NV granules polled together: every load is issued before any tag is
+// checked, so the NV values cost one round trip, not NV (the march B's two
+// sums waited for two, at both reduction levels: its tail ran 5.2 us after
+// the last walk against P's 2.9, profiles/r5_3_mtrace_summary_L4096.txt)
+template <int NV>
+__device__ __forceinline__ void gran_poll_n(__amdgpu_buffer_rsrc_t rg, const int (&off)[NV], double tag,
+                                            int* err, double (&out)[NV]) {
+  for (unsigned spin = 0;; ++spin) {
+    double2 g2[NV];
+#pragma unroll
+    for (int j = 0; j < NV; ++j)
+      g2[j] = __builtin_bit_cast(double2, __builtin_amdgcn_raw_buffer_load_b128(rg, off[j], 0, 16));
+    bool ok = true;
+#pragma unroll
+    for (int j = 0; j < NV; ++j) {
+      ok = ok && g2[j].y == tag;
+      out[j] = g2[j].x;
+    }
+    if (ok) return;
+    if (spin > (1u << 22)) {
+      *err = 1;
+      return;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+}
+
 template <int NV>
 __device__ bool publish_and_reduce_tagged(double (&v)[NV], double* gran, unsigned* tickets, int lb,
                                           int nwg, double tag, int* err, double (&tot)[NV],
@@ -99,11 +126,17 @@ __device__ bool publish_and_reduce_tagged(double (&v)[NV], double* gran, unsigne
   if (threadIdx.x < 64) {  // last of its group: wave 0 sums the group's partials
     const int lane = threadIdx.x;
     double w[NV];
+    if (lane < gn) {
+      int off[NV];
 #pragma unroll
-    for (int j = 0; j < NV; ++j) {
-      w[j] = lane < gn ? gran_poll(rg, (j * nwg + g0 + lane) * 16, tag, err).x : 0.0;
-      w[j] = wave_sum(w[j]);
+      for (int j = 0; j < NV; ++j) off[j] = (j * nwg + g0 + lane) * 16;
+      gran_poll_n<NV>(rg, off, tag, err, w);
+    } else {
+#pragma unroll
+      for (int j = 0; j < NV; ++j) w[j] = 0.0;
     }
+#pragma unroll
+    for (int j = 0; j < NV; ++j) w[j] = wave_sum(w[j]);
     if (lane == 0) {
 #pragma unroll
       for (int j = 0; j < NV; ++j)
@@ -122,8 +155,13 @@ __device__ bool publish_and_reduce_tagged(double (&v)[NV], double* gran, unsigne
 #pragma unroll
   for (int j = 0; j < NV; ++j) acc[j] = 0.0;
   for (int i = threadIdx.x; i < ngroups; i += blockDim.x) {
+    int off[NV];
+    double v[NV];
 #pragma unroll
-    for (int j = 0; j < NV; ++j) acc[j] = acc[j] + gran_poll(rg, (goff + j * ngroups + i) * 16, tag, err).x;
+    for (int j = 0; j < NV; ++j) off[j] = (goff + j * ngroups + i) * 16;
+    gran_poll_n<NV>(rg, off, tag, err, v);
+#pragma unroll
+    for (int j = 0; j < NV; ++j) acc[j] = acc[j] + v[j];
   }
   __syncthreads();  // s_red reuse
   block_sum<NV>(acc, s_red);

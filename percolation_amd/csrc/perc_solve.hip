@@ -437,11 +437,14 @@ void select_format(perc_ctx* h) {
   // 3 N doubles addressed by 32-bit buffer offsets: < 2 GB), which the
   // serial folds sum; past that size the q-storing march (the folds then
   // form the terms from q, p, r)
-  const bool literal = h->dot_order == PERC_DOT_LITERAL;
+  const bool literal = h->dot_order != PERC_DOT_FAST;
   const bool lit_ok = !literal || (size_t)h->N * 24 < ((size_t)1 << 31);
-  // (dev_solve only: the march kernels stay selected for the probes)
+  // (dev_solve only: the march kernels stay selected for the probes; the
+  // host-folded literal order runs the launched march, whose kernels the
+  // host can fold between)
   h->resident = h->fused && h->res_G > 0 && h->fmt_req != PERC_FMT_STENCIL_TILED &&
-                (h->march_mode & PERC_SOLVE_RESIDENT) && h->march_rows_req == 0 && lit_ok;
+                (h->march_mode & PERC_SOLVE_RESIDENT) && h->march_rows_req == 0 && lit_ok &&
+                h->dot_order != PERC_DOT_LITERAL_HOST;
   h->qfree = h->march && (h->march_mode & PERC_MARCH_QFREE) && lit_ok;
   h->march_alt = h->march && (h->march_mode & PERC_MARCH_ALT);
   // one-workgroup solve for small systems, under the default format only
@@ -622,11 +625,71 @@ hipError_t dev_solve(perc_ctx* h, int itol, double tol, int itmax, bool x0_zero,
 }
 
 namespace {
+// PERC_DOT_LITERAL_HOST: k_fold_qp's and k_fold_b's sums and epilogues on the
+// host CPU, from the terms the march kernels stored (a.lit): the same IEEE
+// adds in the same ascending-j order (host code is compiled with
+// -ffp-contract=off and no reassociation), the same divisions and sqrt
+// (correctly rounded on both sides), so every scalar is PERC_DOT_LITERAL's
+// bitwise.  One host round trip per fold; the serial chain runs at the
+// CPU's add latency instead of a GPU wave's (~17 cycles per dependent fp64
+// add, tools/fold_bench.hip).
+struct HostFold {
+  double* t = nullptr;  // pinned, 3 N
+  ~HostFold() {
+    if (t) (void)hipHostFree(t);
+  }
+};
+hipError_t host_fold_qp(perc_ctx* h, const CGArgs& a, HostFold& hf) {
+  const int N = h->N;
+  hipStream_t st = h->stream;
+  CGScalars s{};
+  HIP_TRY(hipMemcpyAsync(&s, h->d.scal, sizeof(s), hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipMemcpyAsync(hf.t, a.lit, sizeof(double) * N, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipStreamSynchronize(st));
+  if (s.done) return hipSuccess;
+  const double* __restrict__ t = hf.t;
+  double acc = 0.0;
+  for (int j = 0; j < N; ++j) acc = acc + t[j];  // akden, bondc.f:803-805
+  s.akden = acc;
+  s.ak = s.bknum / acc;
+  s.bkden = s.bknum;
+  s.pad[2] = 1;
+  HIP_TRY(hipMemcpyAsync(h->d.scal, &s, sizeof(s), hipMemcpyHostToDevice, st));
+  return hipStreamSynchronize(st);
+}
+hipError_t host_fold_b(perc_ctx* h, const CGArgs& a, HostFold& hf) {
+  const int N = h->N;
+  hipStream_t st = h->stream;
+  CGScalars s{};
+  HIP_TRY(hipMemcpyAsync(&s, h->d.scal, sizeof(s), hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipMemcpyAsync(hf.t + N, a.lit + N, sizeof(double) * 2 * (size_t)N, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipStreamSynchronize(st));
+  if (s.pad[2] == 0) return hipSuccess;  // no iteration ran since the last fold
+  const double* __restrict__ t1 = hf.t + N;
+  const double* __restrict__ t2 = hf.t + 2 * (size_t)N;
+  double a0 = 0.0, a1 = 0.0;
+  for (int j = 0; j < N; ++j) {  // bknum :785-787, snrm :872-875
+    a0 = a0 + t1[j];
+    a1 = a1 + t2[j];
+  }
+  const int k = s.iter;
+  const double err = std::sqrt(a1) / s.bnrm;
+  s.bk = a0 / s.bkden;
+  s.bknum = a0;
+  s.err = err;
+  if (k - 1 < a.err_hist_cap)
+    HIP_TRY(hipMemcpyAsync(a.err_hist + (k - 1), &err, sizeof(double), hipMemcpyHostToDevice, st));
+  s.done = !(err > s.tol) || k >= s.itmax + 1 ? 1 : 0;
+  s.pad[2] = 0;
+  HIP_TRY(hipMemcpyAsync(h->d.scal, &s, sizeof(s), hipMemcpyHostToDevice, st));
+  return hipStreamSynchronize(st);
+}
+
 hipError_t dev_solve_impl(perc_ctx* h, int itol, double tol, int itmax, bool x0_zero, bool full_x,
                           int* iter, double* err) {
   DeviceBuffers& d = h->d;
   hipStream_t st = h->stream;
-  const bool literal = h->dot_order == PERC_DOT_LITERAL;
+  const bool literal = h->dot_order != PERC_DOT_FAST;
   if (literal && h->nslab > 1) {
     set_error("the literal dot order sums over the whole system: one slab only");
     return hipErrorInvalidValue;
@@ -711,9 +774,13 @@ hipError_t dev_solve_impl(perc_ctx* h, int itol, double tol, int itmax, bool x0_
   if (!(h->march && h->qfree)) a.lit = nullptr;  // (the other kernels store no terms)
   if (h->strips) HIP_TRY(to_strips(h, a));
   HIP_TRY(setup_granules(h, a, itmax));
+  HostFold hf;
+  const bool host_fold = a.lit && h->dot_order == PERC_DOT_LITERAL_HOST;
+  if (host_fold) HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&hf.t), sizeof(double) * 3 * (size_t)h->N));
   h->last_flags = (literal ? PERC_RAN_LITERAL : 0) | (a.lit ? PERC_RAN_LIT_TERMS : 0) |
                   (h->march && h->qfree ? PERC_RAN_QFREE : 0) | (a.sm ? PERC_RAN_STRIPS : 0) |
-                  (a.nib ? PERC_RAN_NIBBLE : 0) | (a.mgran ? PERC_RAN_TAG : 0);
+                  (a.nib ? PERC_RAN_NIBBLE : 0) | (a.mgran ? PERC_RAN_TAG : 0) |
+                  (host_fold ? PERC_RAN_HOST_FOLD : 0);
   // iterate in chunks; the device flag makes surplus launches no-ops
   int chunk = 8;
   CGScalars* hsp = nullptr;
@@ -762,7 +829,9 @@ hipError_t dev_solve_impl(perc_ctx* h, int itol, double tol, int itmax, bool x0_
       if (tm) h->ev_next[0] = ev[2], h->ev_next[1] = ev[3];
       launch_cg_spmv(h, a, G);
       HIP_TRY(dbg_sync(st, "k_cg_spmv"));
-      if (literal) {  // akden in ascending j, then ak
+      if (host_fold) {  // akden in ascending j, then ak (on the host)
+        HIP_TRY(host_fold_qp(h, a, hf));
+      } else if (literal) {  // akden in ascending j, then ak
         k_fold_qp<<<1, 64, 0, st>>>(a);
         HIP_TRY(dbg_sync(st, "k_fold_qp"));
       }
@@ -772,7 +841,9 @@ hipError_t dev_solve_impl(perc_ctx* h, int itol, double tol, int itmax, bool x0_
       a.mtrace = nullptr;
       HIP_TRY(dbg_sync(st, "k_cg_b"));
       h->ev_next[0] = h->ev_next[1] = nullptr;
-      if (literal) {  // z.r and r.r in ascending j: bk, err, the stop test
+      if (host_fold) {  // z.r and r.r in ascending j: bk, err, the stop test (host)
+        HIP_TRY(host_fold_b(h, a, hf));
+      } else if (literal) {  // z.r and r.r in ascending j: bk, err, the stop test
         if (ST) k_fold_b<true><<<1, 64, 0, st>>>(a);
         else k_fold_b<false><<<1, 64, 0, st>>>(a);
         HIP_TRY(dbg_sync(st, "k_fold_b"));

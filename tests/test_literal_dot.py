@@ -129,6 +129,31 @@ def test_literal_solve_is_the_oracle_linbcg_bitwise(lat, m, n, pbc, p, seed, sol
             assert np.array_equal(bits(c["vint"]), bits(oc["vint"])), tol
 
 
+@pytest.mark.parametrize("lat,m,n,pbc,p,seed", [(0, 512, 512, 0, 0.6, 33), (1, 256, 200, 0, 0.42, 7)])
+def test_host_fold_is_the_device_fold_bitwise(lat, m, n, pbc, p, seed):
+    """PERC_DOT_LITERAL_HOST (the serial sums on the host CPU from the terms
+    the march kernels stored) against PERC_DOT_LITERAL with the same march
+    (the sums folded by one GPU wave): the same IEEE adds in the same order,
+    so iter, the err history, Gtop, Gbot and every voltage are identical"""
+    nb = api.nbonds(lat, m, n, pbc)
+    order = api.shuffled_ids(nb, seed)
+    out = {}
+    with api.Context(lat, m, n, pbc) as ctx:
+        ctx.set_march_mode(MARCH_ONLY)
+        ctx.occupy(PL.BOND, bond_order=order, nbonds_=int(p * nb))
+        assert ctx.label()["nspan"] > 0
+        for order_ in (PL.DOT_LITERAL, PL.DOT_LITERAL_HOST):
+            ctx.set_dot_order(order_)
+            c = ctx.conductance(tol=1e-10, itmax=100000, vint=True)
+            out[order_] = (c, ctx.err_history(), ctx.last_solve())
+    (cd, hd, rd), (ch, hh, rh) = out[PL.DOT_LITERAL], out[PL.DOT_LITERAL_HOST]
+    assert rd["lit_terms"] and not rd["host_fold"] and rh["lit_terms"] and rh["host_fold"], (rd, rh)
+    assert rh["kernel"] == "march" and rh["qfree"] and rh["strips"], rh
+    assert (cd["iter"], cd["gtop"], cd["gbot"], cd["err"]) == (ch["iter"], ch["gtop"], ch["gbot"], ch["err"])
+    assert np.array_equal(bits(hd), bits(hh))
+    assert np.array_equal(bits(cd["vint"]), bits(ch["vint"]))
+
+
 def test_literal_and_fast_orders_differ_by_association_only():
     """The same system in both orders at a converged tolerance: the same
     answer to 1e-10 (only the three sums' association differs), and the

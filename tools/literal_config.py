@@ -9,7 +9,9 @@ other operation is already the reference's, so Gtop, Gbot, iter, err and the
 fixture's decimated err history must match bitwise.  The solve runs the
 production kernels, which store their rows' dot terms for the folds:
 --solver resident (k_cg_res, the default solver of configs 2-4) or march (the
-q-free strip-major march P / B of the metric; PERC_SOLVE_RESIDENT off);
+q-free strip-major march P / B of the metric; PERC_SOLVE_RESIDENT off), or
+march_host (the same march, PERC_DOT_LITERAL_HOST: the serial sums formed by
+the host CPU from the kernels' terms -- bitwise the GPU fold, ~4x faster);
 perc_last_solve's record is printed with each result.  Prints one JSON line
 per tolerance; exit status 1 on any difference.
 
@@ -38,7 +40,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("case")
     ap.add_argument("--tol", action="append", default=None)
-    ap.add_argument("--solver", default="resident", choices=("resident", "march"))
+    ap.add_argument("--solver", default="resident", choices=("resident", "march", "march_host"),
+                    help="march_host: the march with PERC_DOT_LITERAL_HOST (sums folded by the host CPU)")
     ap.add_argument("--probe", type=int, default=0,
                     help="run this many iterations (tol 1e-300) and compare the history prefix")
     args = ap.parse_args()
@@ -56,12 +59,12 @@ def main():
     occ, rule, cur = occupation(rc)
     ok = True
     with api.Context(rc["lattice"], rc["L"], rc["L"], 0) as ctx:
-        if args.solver == "march":
+        if args.solver != "resident":
             ctx.set_march_mode(PL.MARCH_DEFAULT & ~PL.SOLVE_RESIDENT)
         ctx.occupy(**occ)
         li = ctx.label()
         assert li["nspan"] > 0
-        ctx.set_dot_order(PL.DOT_LITERAL)
+        ctx.set_dot_order(PL.DOT_LITERAL_HOST if args.solver == "march_host" else PL.DOT_LITERAL)
         if args.probe:
             ref = doc["solves"][tols[0]]
             t0 = time.time()
