@@ -143,7 +143,12 @@ def cpu_baseline(L_, p, order, gpu_iters, cpu_iters, tol=1e-8):
                 sample_seconds=round(t4 - t0, 2), s_per_solve=round(total, 2),
                 measured_seconds=round(t4 - t0, 2), iterations=it.value,
                 extrapolated=cpu_iters > 0, t_label=t1 - t0, t_assemble=t2 - t1,
-                s_per_iter=per_iter, t_currents=t4 - t3, gtop=gt.value)
+                s_per_iter=per_iter, t_currents=t4 - t3,
+                # the sample's currents: only after a whole solve is this the
+                # realisation's conductance (a bounded sample stops at
+                # cpu_iters iterations, far from converged)
+                **({"gtop_converged": gt.value} if cpu_iters <= 0
+                   else {"gtop_unconverged_after_sample": gt.value}))
 
 
 def cpu_anchor_start(L_, p, seed, iters, occupancy):

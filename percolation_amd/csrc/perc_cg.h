@@ -81,6 +81,9 @@ struct CGArgs {
   // last columns
   const uint8_t* nib;
   unsigned ncls[3];
+  // the open square lattice with those three column classes (ncls set):
+  // the march's u16-code kernels take the interior form's scalar path too
+  int sqcls;
   int* merr;
   // literal dot order on the q-free march (PERC_DOT_LITERAL): the march P
   // stores each row's q.p term and the march B each row's z.r and r.r terms
@@ -1121,7 +1124,8 @@ CGArgs make_cg_args(perc_ctx* h) {
   a.mgran = a.mgran_b = nullptr;
   a.mtag = 0.0;
   a.nib = nullptr;
-  a.ncls[0] = a.ncls[1] = a.ncls[2] = 0u;
+  a.sqcls = h->nib_ok && !h->g.pbc ? 1 : 0;
+  for (int c = 0; c < 3; ++c) a.ncls[c] = a.sqcls ? h->ncls[c] : 0u;
   a.merr = nullptr;
   a.lit = nullptr;
   return a;

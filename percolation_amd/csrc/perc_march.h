@@ -480,7 +480,13 @@ __device__ __forceinline__ void march_step(const CGArgs& a, const MGeom& g, cons
     const unsigned ff = __builtin_amdgcn_readfirstlane(f0);
     const bool uni = !__any(f0 != ff || f1 != ff) && a.St.F.regular[ff];
     double q0, q1;
-    if (PK && !a.T.pbc) {
+    // u16 codes (the row-major march past the Infinity Cache): the same
+    // path where the lattice is the open square one (a.sqcls) and every
+    // row of the step carries its column class's count / form bits
+    bool sqp;
+    if constexpr (PK) sqp = !a.T.pbc;
+    else sqp = a.sqcls && !__any((((c0w ^ g.cb0) | (c1w ^ g.cb1)) >> 8) != 0u);
+    if (sqp) {
       // Open square lattice, nibble codes: every row is interior, column 0
       // or column m-1 (k_pack_nib checked it), so EVERY wave -- the edge
       // strips too -- takes the interior form's scalar path.  A row of
@@ -670,7 +676,12 @@ __global__ __launch_bounds__(64 * kMarchWaves) void k_cg_march(CGArgs a) {
   }
   const bool up = (a.march_alt && (band & 1)) != (MODE == kMarchB);
   const int nsteps = g.rend - g.r0 + 2;
-  if constexpr (PK) {  // (nibble codes: the square lattice's three column classes)
+  // (the square lattice's three column classes: nibble codes, and the u16
+  // codes of the open square lattice)
+  g.cb0 = g.cb1 = g.cbh = 0u;
+  g.lo0 = g.lo1 = 0xFu;
+  g.hi0 = g.hi1 = 0u;
+  if (PK || a.sqcls) {
     auto cls = [&](int c) { return c == 0 ? a.ncls[1] : (c == m - 1 ? a.ncls[2] : a.ncls[0]); };
     g.cb0 = cls(g.col);
     g.cb1 = cls(g.col + 1);

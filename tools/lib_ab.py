@@ -61,6 +61,9 @@ def child(args):
     with api.Context(0, L_, L_, 0) as ctx:
         if args.mode >= 0:
             ctx.set_march_mode(args.mode)
+        for part in filter(None, args.wspec.split("/")):  # "which:w0,w1,w2/..."
+            which, ws = part.split(":")
+            ctx.set_band_weights(int(which), [int(x) for x in ws.split(",")])
         ctx.occupy_random(PL.BOND, 0, int(args.p * nb), 777)
         assert ctx.label()["nspan"] > 0
         if args.format == "csr":
@@ -93,27 +96,33 @@ def main():
     ap.add_argument("--what", default="solve", choices=("solve", "label"))
     ap.add_argument("--format", default="default", choices=("default", "csr"))
     ap.add_argument("--child", action="store_true")
+    ap.add_argument("--wspec", default="", help=argparse.SUPPRESS)
+    ap.add_argument("--wsets", default="",
+                    help="band-weight variants of the main library: 'name=which:w,w,w/which:w,w,w;...'")
     args = ap.parse_args()
     if args.child:
         return child(args)
-    libs = args.libs.split(",")
+    libs = [(lib, lib, "") for lib in args.libs.split(",")]
+    for ws in filter(None, args.wsets.split(";")):
+        name, spec = ws.split("=")
+        libs.append((name, "main", spec))
     best = {}
     fps = {}
     for _ in range(args.rounds):
-        for lib in libs:
+        for name, lib, spec in libs:
             env = dict(os.environ)
             if lib != "main":
                 env["PERC_LIBPERC"] = os.path.join(REPO, "percolation_amd", "probe", "libperc_%s.so" % lib)
             cmd = [sys.executable, os.path.abspath(__file__), "--child", "--L", str(args.L), "--p", str(args.p),
                    "--reps", str(args.reps), "--iters", str(args.iters), "--mode", str(args.mode),
-                   "--what", args.what, "--format", args.format]
+                   "--what", args.what, "--format", args.format, "--wspec", spec]
             r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600)
             if r.returncode != 0:
                 sys.stderr.write(r.stderr[-3000:])
-                raise SystemExit("child %s failed rc=%d" % (lib, r.returncode))
+                raise SystemExit("child %s failed rc=%d" % (name, r.returncode))
             o = json.loads(r.stdout.strip().splitlines()[-1])
-            fps.setdefault(lib, o.pop("fp"))
-            b = best.setdefault(lib, {})
+            fps.setdefault(name, o.pop("fp"))
+            b = best.setdefault(name, {})
             for k, v in o.items():
                 b[k] = min(b.get(k, 9e9), v)
     out = {lib: {k: round(v, 5) for k, v in b.items()} for lib, b in best.items()}

@@ -103,6 +103,77 @@ __global__ __launch_bounds__(kBlock) void k_spmv_row2(CsrView A, const double* _
   }
 }
 
+// Candidate 3: one row per thread, the once-read streams (col, val, diag)
+// loaded nontemporal and y stored nontemporal; x (gathered, re-read by the
+// neighbouring rows) and rowptr keep the default policy
+template <int NS>
+__global__ __launch_bounds__(kBlock) void k_spmv_nt(CsrView A, const double* __restrict__ x,
+                                                    double* __restrict__ y) {
+  const int i = blockIdx.x * kBlock + threadIdx.x;
+  if (i >= A.N) return;
+  const int a = A.rowptr[i], b = A.rowptr[i + 1];
+  int c[NS];
+  double v[NS], xv[NS];
+  const int last = b - 1 < a ? a : b - 1;
+#pragma unroll
+  for (int j = 0; j < NS; ++j) {
+    const int k = min(a + j, last);
+    c[j] = __builtin_nontemporal_load(A.col + k);
+    v[j] = __builtin_nontemporal_load(A.val + k);
+  }
+  const double xi = x[i], di = __builtin_nontemporal_load(A.diag + i);
+#pragma unroll
+  for (int j = 0; j < NS; ++j) xv[j] = x[c[j]];
+  double acc = di * xi;
+#pragma unroll
+  for (int j = 0; j < NS; ++j) acc = j < b - a ? acc + v[j] * xv[j] : acc;
+  __builtin_nontemporal_store(acc, y + i);
+}
+
+// Candidate 4: 4 aligned slots per row (ELL: cols int4, vals 2 x double2, a
+// per-row count byte; padding slots never added) -- 16-B loads, no rowptr
+struct Ell {
+  const int4* col;
+  const double2* val;
+  const unsigned char* cnt;
+  const double* diag;
+  int N;
+};
+template <bool NT>
+__global__ __launch_bounds__(kBlock) void k_spmv_ell(Ell E, const double* __restrict__ x, double* __restrict__ y) {
+  const int i = blockIdx.x * kBlock + threadIdx.x;
+  if (i >= E.N) return;
+  int4 c;
+  double2 v0, v1;
+  double di;
+  if (NT) {
+    typedef int iv4 __attribute__((ext_vector_type(4)));
+    typedef double dv2 __attribute__((ext_vector_type(2)));
+    const iv4 cc = __builtin_nontemporal_load(reinterpret_cast<const iv4*>(E.col) + i);
+    const dv2 a0 = __builtin_nontemporal_load(reinterpret_cast<const dv2*>(E.val) + 2 * i);
+    const dv2 a1 = __builtin_nontemporal_load(reinterpret_cast<const dv2*>(E.val) + 2 * i + 1);
+    c = make_int4(cc.x, cc.y, cc.z, cc.w);
+    v0 = make_double2(a0.x, a0.y);
+    v1 = make_double2(a1.x, a1.y);
+    di = __builtin_nontemporal_load(E.diag + i);
+  } else {
+    c = E.col[i];
+    v0 = E.val[2 * i];
+    v1 = E.val[2 * i + 1];
+    di = E.diag[i];
+  }
+  const int n = E.cnt[i];
+  const double xi = x[i];
+  const double x0 = x[c.x], x1 = x[c.y], x2 = x[c.z], x3 = x[c.w];
+  double acc = di * xi;
+  acc = 0 < n ? acc + v0.x * x0 : acc;
+  acc = 1 < n ? acc + v0.y * x1 : acc;
+  acc = 2 < n ? acc + v1.x * x2 : acc;
+  acc = 3 < n ? acc + v1.y * x3 : acc;
+  if (NT) __builtin_nontemporal_store(acc, y + i);
+  else y[i] = acc;
+}
+
 template <typename F>
 double time_ms(F f, int reps) {
   hipEvent_t a, b;
@@ -191,5 +262,32 @@ int main(int argc, char** argv) {
   }
   const int Gf = cdiv(N, kBlock);
   check("row per lane, one row per thread", time_ms([&]() { k_spmv_row<4><<<Gf, kBlock>>>(A, dx, dy2); }, reps));
+  check("one row per thread, nt streams", time_ms([&]() { k_spmv_nt<4><<<Gf, kBlock>>>(A, dx, dy2); }, reps));
+  // the same system in 4 aligned slots per row
+  std::vector<int> ec((size_t)4 * N, 0);
+  std::vector<double> ev((size_t)4 * N, 0.0);
+  std::vector<unsigned char> en(N);
+  for (int i = 0; i < N; ++i) {
+    en[i] = (unsigned char)(rowptr[i + 1] - rowptr[i]);
+    for (int k = rowptr[i]; k < rowptr[i + 1]; ++k) {
+      ec[(size_t)4 * i + (k - rowptr[i])] = col[k];
+      ev[(size_t)4 * i + (k - rowptr[i])] = val[k];
+    }
+    for (int k = rowptr[i + 1] - rowptr[i]; k < 4; ++k) ec[(size_t)4 * i + k] = i;  // (never added)
+  }
+  int* dec;
+  double* dev;
+  unsigned char* den;
+  CK(hipMalloc(&dec, ec.size() * 4));
+  CK(hipMalloc(&dev, ev.size() * 8));
+  CK(hipMalloc(&den, (size_t)N));
+  CK(hipMemcpy(dec, ec.data(), ec.size() * 4, hipMemcpyHostToDevice));
+  CK(hipMemcpy(dev, ev.data(), ev.size() * 8, hipMemcpyHostToDevice));
+  CK(hipMemcpy(den, en.data(), (size_t)N, hipMemcpyHostToDevice));
+  Ell E{reinterpret_cast<const int4*>(dec), reinterpret_cast<const double2*>(dev), den, ddiag, N};
+  check("4-slot rows (ELL), 16-B loads", time_ms([&]() { k_spmv_ell<false><<<Gf, kBlock>>>(E, dx, dy2); }, reps));
+  check("4-slot rows (ELL), nt streams", time_ms([&]() { k_spmv_ell<true><<<Gf, kBlock>>>(E, dx, dy2); }, reps));
+  std::printf("  (ELL moves %.1f MB per launch: 4 slots x 12 B + count 1 B + diag, x, y 24 B per row)\n",
+              (49.0 + 24.0) * N / 1e6);
   return 0;
 }
