@@ -6,7 +6,8 @@
 // with HIP events phase by phase; every chain's final parents and members
 // checked element by element against the LDS union-find chain's.
 //
-//   make -C tools cc_bench && ./tools/cc_bench 4096 0.6 20
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -Iinclude -Ipercolation_amd/csrc \
+//     tools/cc_bench.hip -o tools/cc_bench && ./tools/cc_bench 4096 0.6 20
 #include "perc_cc.h"
 
 #include <cstdio>
@@ -190,10 +191,16 @@ int main(int argc, char** argv) {
     };
   };
   using I16 = std::integral_constant<int, 16>;
-  using I32 = std::integral_constant<int, 32>;
   chain("wave 128 x 16 (production)", wave(I16{}, std::integral_constant<int, 2>{}), merge_for(I16{}), false);
+  chain("wave 16, word loads", [&]() {
+    k_cc_tile_w<16, PERC_BOND, 2, true><<<cdiv(g.m, kCcW) * cdiv(g.n, 16), 64>>>(g, R.bocc, R.socc, R.parent,
+                                                                                 R.member, (unsigned)nb + 8u);
+  }, merge_for(I16{}), false);
+  chain("wave 16, word loads, D 3", [&]() {
+    k_cc_tile_w<16, PERC_BOND, 3, true><<<cdiv(g.m, kCcW) * cdiv(g.n, 16), 64>>>(g, R.bocc, R.socc, R.parent,
+                                                                                 R.member, (unsigned)nb + 8u);
+  }, merge_for(I16{}), false);
   chain("wave 128 x 16, 4 rows in flight", wave(I16{}, std::integral_constant<int, 4>{}), merge_for(I16{}), false);
-  chain("wave 128 x 32", wave(I32{}, std::integral_constant<int, 2>{}), merge_for(I32{}), false);
   // the merge's unions deduplicated only against the previous lane (WD = false)
   {
     const int nseg = cdiv(g.m, kCcThreads), nfull = g.n / 16, ncand = 2 * cdiv(g.m, kCcW) + 1;
@@ -213,6 +220,21 @@ int main(int argc, char** argv) {
     std::vector<uint8_t> so((size_t)g.t + 2, 0);
     for (int st = 1; st <= g.t; ++st) so[st] = hash32((unsigned long long)st * 0xD1B54A32D192ED03ull + 777) < 0xCCCCCCCCu;
     CK(hipMemcpy(R.socc, so.data(), so.size(), hipMemcpyHostToDevice));
+    // the 16-row wave tiles of each kind (byte loads, the production; word
+    // loads), element by element against the 16-row LDS-free reference
+    // below and timed alone
+    const int G16 = cdiv(g.m, kCcW) * cdiv(g.n, 16);
+    auto wk = [&](auto kc, auto wl) {
+      constexpr int K = decltype(kc)::value;
+      constexpr bool W = decltype(wl)::value;
+      return [&, G16]() {
+        k_cc_tile_w<16, K, 2, W><<<G16, 64>>>(g, R.bocc, R.socc, R.parent, R.member, (unsigned)nb + 8u);
+      };
+    };
+    using KS = std::integral_constant<int, PERC_SITE>;
+    using KM = std::integral_constant<int, PERC_SITEBOND>;
+    using WF = std::false_type;
+    using WT = std::true_type;
     for (int kind : {PERC_SITE, PERC_SITEBOND}) {
       k_cc_tile<<<R.tiles, kCcThreads>>>(g, kind, R.bf, R.bocc, R.socc, R.parent_ref, R.member_ref, 1, nullptr);
       if (kind == PERC_SITE)
@@ -221,6 +243,18 @@ int main(int argc, char** argv) {
         k_cc_tile_w<kCcH, PERC_SITEBOND><<<R.tiles, 64>>>(g, R.bocc, R.socc, R.parent, R.member, (unsigned)nb + 8u);
       CK(hipDeviceSynchronize());
       same(R, kind == PERC_SITE ? "k_cc_tile_w, site kind" : "k_cc_tile_w, mixed kind");
+      // 16-row references: the production wave tile of that height
+      if (kind == PERC_SITE) wk(KS{}, WF{})();
+      else wk(KM{}, WF{})();
+      CK(hipDeviceSynchronize());
+      CK(hipMemcpy(R.parent_ref, R.parent, ((size_t)g.t + 2) * 4, hipMemcpyDeviceToDevice));
+      CK(hipMemcpy(R.member_ref, R.member, (size_t)g.t + 2, hipMemcpyDeviceToDevice));
+      const double tb = kind == PERC_SITE ? time_ms(wk(KS{}, WF{}), reps) : time_ms(wk(KM{}, WF{}), reps);
+      CK(hipMemset(R.parent, 0, ((size_t)g.t + 2) * 4));
+      const double tw = kind == PERC_SITE ? time_ms(wk(KS{}, WT{}), reps) : time_ms(wk(KM{}, WT{}), reps);
+      if (same(R, kind == PERC_SITE ? "wave 16 word loads, site" : "wave 16 word loads, mixed"))
+        std::printf("  tile 16 rows, %s kind: byte loads %.1f us, word loads %.1f us\n",
+                    kind == PERC_SITE ? "site" : "mixed", tb * 1e3, tw * 1e3);
     }
   }
   return 0;
