@@ -213,4 +213,41 @@ __host__ __device__ inline unsigned long long perc_rand_key(unsigned long long s
   return (h & 0xFFFFFFFF00000000ull) | (unsigned long long)id;
 }
 
+// perc_rand_key's hash word, hash32(seed, id) = perc_rand_key(seed, id) >> 32,
+// in 32-bit arithmetic with the seed folded in once per draw: id only
+// touches the low word of S ^ id (S = perc_mix64(seed)), so after the
+// golden-ratio add the high word is Shi + Chi + carry -- one of two
+// constants, and so are the terms of the first multiply it feeds; the last
+// multiply needs only its high word.  5 32-bit multiplies per key instead
+// of 6, and no 64-bit shifts (the occupancy draw is bound by this hash).
+struct RandKeyCtx {
+  unsigned slo;         // low word of S
+  unsigned hs0, hs1;    // (high word of S + C + carry) << 2, carry 0 / 1
+  unsigned t0, t1;      // (y's high word) * C1lo, carry 0 / 1
+};
+__host__ __device__ inline RandKeyCtx perc_rand_key_ctx(unsigned long long seed) {
+  const unsigned long long S = perc_mix64(seed);
+  RandKeyCtx k;
+  k.slo = (unsigned)S;
+  const unsigned h0 = (unsigned)(S >> 32) + 0x9E3779B9u, h1 = h0 + 1u;
+  k.hs0 = h0 << 2;
+  k.hs1 = h1 << 2;
+  k.t0 = (h0 ^ (h0 >> 30)) * 0x1CE4E5B9u;
+  k.t1 = (h1 ^ (h1 >> 30)) * 0x1CE4E5B9u;
+  return k;
+}
+__host__ __device__ inline unsigned perc_rand_hash32(const RandKeyCtx& k, unsigned id) {
+  const unsigned x0lo = (k.slo ^ id) + 0x7F4A7C15u;
+  const bool c = x0lo < 0x7F4A7C15u;  // carry into the high word
+  const unsigned ylo = x0lo ^ ((x0lo >> 30) | (c ? k.hs1 : k.hs0));
+  const unsigned long long pz = (unsigned long long)ylo * 0x1CE4E5B9u;
+  const unsigned zlo = (unsigned)pz;
+  const unsigned zhi = (unsigned)(pz >> 32) + ylo * 0xBF58476Du + (c ? k.t1 : k.t0);
+  const unsigned wlo = zlo ^ ((zlo >> 27) | (zhi << 5));
+  const unsigned whi = zhi ^ (zhi >> 27);
+  const unsigned vhi =
+      (unsigned)(((unsigned long long)wlo * 0x133111EBu) >> 32) + wlo * 0x94D049BBu + whi * 0x133111EBu;
+  return vhi ^ (vhi >> 31);
+}
+
 }  // namespace perc

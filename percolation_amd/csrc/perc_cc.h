@@ -56,14 +56,16 @@ __device__ __forceinline__ int find_root(int* parent, int x) {
   return x;
 }
 
-__device__ __forceinline__ void unite(int* parent, int a, int b) {
+// true when this call joined two sets (its CAS hooked a root): the
+// successful hooks of a pass count the components it merged
+__device__ __forceinline__ bool unite(int* parent, int a, int b) {
   while (true) {
     a = find_root(parent, a);
     b = find_root(parent, b);
-    if (a == b) return;
+    if (a == b) return false;
     if (a < b) { const int tmp = a; a = b; b = tmp; }
     const int old = atomicCAS(&parent[a], a, b);
-    if (old == a) return;
+    if (old == a) return true;
     a = old;
   }
 }
@@ -330,9 +332,13 @@ __device__ __forceinline__ int bf_open_square(const Geom& g, int row, int col) {
 // spread to the owning lanes by shuffles -- 1 or 2 memory instructions per
 // row instead of 4 (bond) or 10 (mixed) byte loads.  A site's up link then
 // carries O(row) only; O(row + 1) is applied when the next row is walked.
+// ncl (site and mixed kinds, whose member flag the tile sees whole): the
+// block's member roots written to ncl[block]; the merge's hooks subtract
+// from that count (k_span_top sums both), so no pass over every parent
+// counts the clusters
 template <int H, int KIND, int D = 2, bool WL = false>  // D: rows whose loads are in flight
 __global__ __launch_bounds__(64) void k_cc_tile_w(Geom g, const uint8_t* bocc, const uint8_t* socc, int* parent,
-                                                  uint8_t* member, unsigned nb_bytes) {
+                                                  uint8_t* member, unsigned nb_bytes, int* ncl = nullptr) {
   static_assert(H <= 32, "member flags: a row per bit of one word");
   __shared__ int uf_mem[kCcW * H / 2];
   const TileUF<true> uf{uf_mem};
@@ -514,6 +520,7 @@ __global__ __launch_bounds__(64) void k_cc_tile_w(Geom g, const uint8_t* bocc, c
     }
   }
   wave_lds_order();
+  int nroot = 0;
 #pragma unroll
   for (int r = 0; r < H; ++r) {
     if (r >= th) continue;
@@ -527,9 +534,15 @@ __global__ __launch_bounds__(64) void k_cc_tile_w(Geom g, const uint8_t* bocc, c
         x = p;
         p = uf.get(x);
       }
-      parent[s] = (r0 + x / kCcW) * g.m + c0 + x % kCcW + 1;
+      const int root = (r0 + x / kCcW) * g.m + c0 + x % kCcW + 1;
+      parent[s] = root;
       member[s] = (uint8_t)(Mb[h] >> r & 1u);
+      nroot += root == s && (Mb[h] >> r & 1u);
     }
+  }
+  if (ncl) {  // (uniform)
+    nroot = wave_sum_int(nroot);
+    if (lane == 0) ncl[blockIdx.x] = nroot;
   }
 }
 
@@ -552,11 +565,14 @@ __global__ __launch_bounds__(64) void k_cc_tile_w(Geom g, const uint8_t* bocc, c
 // whose pair equals the previous lane's skips.  Along a block edge most
 // crossing links join the same few block components, so most lanes drop out:
 // merge 47.4 vs 83.6 us at L = 4096 (profiles/r4_11_cc_bench_L4096.txt)
+// nhook (with the tiles' ncl): minus the workgroup's successful hooks,
+// written to nhook[blockIdx.x]
 template <int TH = kCcH, bool WD = true>  // TH: block height of the tile kernel that ran before
 __global__ __launch_bounds__(kCcThreads) void k_cc_merge(Geom g, int kind, const int* bond_first,
                                                          const uint8_t* bocc,
                                                          const uint8_t* socc, int* parent,
-                                                         uint8_t* member, int nseg, int nfull) {
+                                                         uint8_t* member, int nseg, int nfull,
+                                                         int* nhook = nullptr) {
   const int ntx = cdiv(g.m, kCcW), lane = threadIdx.x & 63;
   int row, c;
   if ((int)blockIdx.x < nfull * nseg) {  // A: block-top row, columns of segment
@@ -576,7 +592,7 @@ __global__ __launch_bounds__(kCcThreads) void k_cc_merge(Geom g, int kind, const
     nearestn_rc(g, s, row, c, nn);
     fb = bond_first[s];
   }
-  int r = 0;
+  int r = 0, hooks = 0;
   for (int k = 0; k < g.scn; ++k) {  // (uniform trip count: the shuffles below)
     const int q = nn[k];
     const bool fwd = site && q > s;
@@ -599,10 +615,22 @@ __global__ __launch_bounds__(kCcThreads) void k_cc_merge(Geom g, int kind, const
         act &= ~__ballot(same);
         if (same && lane != l) lead = false;
       }
-      if (lead) unite(parent, lo, hi);
+      if (lead) hooks += unite(parent, lo, hi) ? 1 : 0;
     } else {
       const int pa = __shfl_up(a, 1, 64), pb = __shfl_up(b, 1, 64);
-      if (want && !(lane > 0 && pa == a && pb == b)) unite(parent, a, b);
+      if (want && !(lane > 0 && pa == a && pb == b)) hooks += unite(parent, a, b) ? 1 : 0;
+    }
+  }
+  if (nhook) {  // (uniform)
+    __shared__ int s_h[kCcThreads / 64];
+    hooks = wave_sum_int(hooks);
+    if (lane == 0) s_h[threadIdx.x >> 6] = hooks;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      int tot = 0;
+#pragma unroll
+      for (int w = 0; w < kCcThreads / 64; ++w) tot += s_h[w];
+      nhook[blockIdx.x] = -tot;
     }
   }
 }

@@ -308,7 +308,11 @@ static int occupy_impl(perc_ctx* h, int kind, int nsites, const int* site_order,
 // perc_rand_key(seed, id) order" (the occupancy perc_occupy_random selects)
 static void random_order(long long n, long long count, unsigned long long seed, int* out) {
   std::vector<unsigned long long> keys((size_t)n);
-  for (long long i = 0; i < n; ++i) keys[(size_t)i] = perc_rand_key(seed, (unsigned)(i + 1));
+  const RandKeyCtx kc = perc_rand_key_ctx(seed);  // (the device draw's arithmetic; = perc_rand_key)
+  for (long long i = 0; i < n; ++i) {
+    const unsigned id = (unsigned)(i + 1);
+    keys[(size_t)i] = (unsigned long long)perc_rand_hash32(kc, id) << 32 | id;
+  }
   if (count < n) std::nth_element(keys.begin(), keys.begin() + count, keys.end());
   std::sort(keys.begin(), keys.begin() + count);
   for (long long i = 0; i < count; ++i) out[i] = (int)(keys[(size_t)i] & 0xFFFFFFFFull);

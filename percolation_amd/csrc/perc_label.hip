@@ -29,7 +29,7 @@ __global__ void k_occupy(const int* order, int count, long long limit, uint8_t* 
 // keys -- slow, exact: T is the exact order statistic on every path.
 constexpr int kSelCap = 1 << 17, kSelThreads = 1024, kSelStage = 512, kSelBins = 4096;
 constexpr int kSelBinCap = 1024;
-__global__ __launch_bounds__(kBlock) void k_select_window(long long n, unsigned long long seed,
+__global__ __launch_bounds__(kBlock) void k_select_window(long long n, RandKeyCtx kc,
                                                           unsigned long long lo,
                                                           unsigned long long hi,
                                                           unsigned* cnt,
@@ -43,8 +43,9 @@ __global__ __launch_bounds__(kBlock) void k_select_window(long long n, unsigned 
   const int lane = threadIdx.x & 63;
   for (long long i = (long long)blockIdx.x * kBlock + threadIdx.x; i < n;
        i += (long long)gridDim.x * kBlock) {
-    const unsigned long long key = perc_rand_key(seed, (unsigned)(i + 1));
-    const unsigned long long hsh = key >> 32;
+    const unsigned id = (unsigned)(i + 1);
+    const unsigned long long hsh = perc_rand_hash32(kc, id);  // = perc_rand_key(seed, id) >> 32
+    const unsigned long long key = hsh << 32 | id;
     below += hsh < lo;
     // every key below the window is occupied, every key above it is not;
     // the window's keys (0 here) are decided by k_occupy_cand once T is known
@@ -220,13 +221,15 @@ __global__ __launch_bounds__(kSelThreads) void k_select_final(long long n,
 // valid (k_select_final's cnt[2]): nonzero when k_select_window's
 // occupation stands -- then this pass returns at once (grid-stride, a
 // small grid)
-__global__ __launch_bounds__(kBlock) void k_occupy_rand(long long n, unsigned long long seed,
+__global__ __launch_bounds__(kBlock) void k_occupy_rand(long long n, RandKeyCtx kc,
                                                          const unsigned long long* Tp, int base,
                                                          uint8_t* occ, const unsigned* valid) {
   if (valid && *valid) return;
   const unsigned long long T = Tp ? *Tp : ~0ull;
-  for (long long i = (long long)blockIdx.x * kBlock + threadIdx.x; i < n; i += (long long)gridDim.x * kBlock)
-    occ[i + base] = perc_rand_key(seed, (unsigned)(i + 1)) <= T ? 1 : 0;
+  for (long long i = (long long)blockIdx.x * kBlock + threadIdx.x; i < n; i += (long long)gridDim.x * kBlock) {
+    const unsigned id = (unsigned)(i + 1);
+    occ[i + base] = ((unsigned long long)perc_rand_hash32(kc, id) << 32 | id) <= T ? 1 : 0;
+  }
 }
 
 // the window's keys (cand[1 ..], id in the low 32 bits) at or below T
@@ -256,9 +259,11 @@ __global__ void k_occupy_sites(const int* order, int count, int t, uint8_t* socc
 // workgroup: flag[root] for the top-row members whose root is <= m, then the
 // flagged roots in ascending order (ballot compaction) -> counters[0] =
 // count, counters[8..] = the first kMaxSpanList roots.
+// part (npart > 0): the cluster count as the sum of the wave tiles' member
+// roots and the merge's negated hooks -> counters[1]
 __global__ __launch_bounds__(1024) void k_span_top(Geom g, const int* parent,
                                                    const uint8_t* member, uint8_t* flag,
-                                                   int* counters) {
+                                                   int* counters, const int* part, int npart) {
   __shared__ int s_w[16];
   __shared__ int s_base;
   const int m = g.m;
@@ -294,6 +299,19 @@ __global__ __launch_bounds__(1024) void k_span_top(Geom g, const int* parent,
     __syncthreads();
   }
   if (threadIdx.x == 0) counters[0] = s_base;
+  if (npart > 0) {  // (uniform)
+    int v = 0;
+    for (int i = threadIdx.x; i < npart; i += 1024) v += part[i];
+    v = wave_sum_int(v);
+    __syncthreads();
+    if (lane == 0) s_w[wid] = v;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      int tot = 0;
+      for (int w = 0; w < 16; ++w) tot += s_w[w];
+      counters[1] = tot;
+    }
+  }
 }
 
 // member sites of the component rooted at root (fixed grid, one atomic per
@@ -403,8 +421,9 @@ static hipError_t occupy_rand_one(perc_ctx* h, long long n, long long count,
   hipStream_t st = h->stream;
   const int G = (int)std::min<long long>(cdiv(n, kBlock), 2048);
   if (count <= 0) return hipMemsetAsync(occ + base, 0, (size_t)n, st);
+  const RandKeyCtx kc = perc_rand_key_ctx(seed);
   if (count >= n) {
-    k_occupy_rand<<<G, kBlock, 0, st>>>(n, seed, nullptr, base, occ, nullptr);
+    k_occupy_rand<<<G, kBlock, 0, st>>>(n, kc, nullptr, base, occ, nullptr);
     return hipGetLastError();
   }
   if (!h->d.sel_hist) HIP_TRY(dmalloc(&h->d.sel_hist, 4));
@@ -419,7 +438,7 @@ static hipError_t occupy_rand_one(perc_ctx* h, long long n, long long count,
   const char* full = std::getenv("PERC_SELECT_FULL");  // tests: the exact slow path
   if (full && full[0] == '1') lo = hi = 0;
   HIP_TRY(hipMemsetAsync(h->d.sel_hist, 0, 4 * sizeof(unsigned), st));
-  k_select_window<<<G, kBlock, 0, st>>>(n, seed, lo, hi, h->d.sel_hist, h->d.sel_cand, base, occ);
+  k_select_window<<<G, kBlock, 0, st>>>(n, kc, lo, hi, h->d.sel_hist, h->d.sel_cand, base, occ);
   HIP_TRY(dbg_sync(st, "k_select_window"));
   k_select_final<<<1, kSelThreads, 0, st>>>(n, seed, count, lo, hi, h->d.sel_hist, h->d.sel_cand);
   HIP_TRY(dbg_sync(st, "k_select_final"));
@@ -432,7 +451,7 @@ static hipError_t occupy_rand_one(perc_ctx* h, long long n, long long count,
   }
   k_occupy_cand<<<cdiv(kSelCap, kBlock), kBlock, 0, st>>>(h->d.sel_hist, h->d.sel_cand, base, occ);
   HIP_TRY(dbg_sync(st, "k_occupy_cand"));
-  k_occupy_rand<<<G, kBlock, 0, st>>>(n, seed, h->d.sel_cand, base, occ, h->d.sel_hist + 2);
+  k_occupy_rand<<<G, kBlock, 0, st>>>(n, kc, h->d.sel_cand, base, occ, h->d.sel_hist + 2);
   return hipGetLastError();
 }
 
@@ -455,7 +474,8 @@ hipError_t dev_occupy_random(perc_ctx* h, int kind, int nsites, int nbonds,
   return hipSuccess;
 }
 
-static hipError_t label_finish(perc_ctx* h, int* nspan, int* span_list, int* nclusters);
+static hipError_t label_finish(perc_ctx* h, int* nspan, int* span_list, int* nclusters,
+                                const int* part = nullptr, int npart = 0);
 
 hipError_t dev_label(perc_ctx* h, int* nspan, int* span_list, int* nclusters) {
   const Geom& g = h->g;
@@ -471,15 +491,25 @@ hipError_t dev_label(perc_ctx* h, int* nspan, int* span_list, int* nclusters) {
     constexpr int H = kCcWaveH;
     const int G = cdiv(g.m, kCcW) * cdiv(g.n, H);
     const unsigned nbb = (unsigned)h->nb + 8u;
-    if (kind == PERC_BOND) k_cc_tile_w<H, PERC_BOND><<<G, 64, 0, st>>>(g, d.bocc, d.socc, d.parent, d.member, nbb);
-    else if (kind == PERC_SITE) k_cc_tile_w<H, PERC_SITE><<<G, 64, 0, st>>>(g, d.bocc, d.socc, d.parent, d.member, nbb);
-    else k_cc_tile_w<H, PERC_SITEBOND><<<G, 64, 0, st>>>(g, d.bocc, d.socc, d.parent, d.member, nbb);
-    HIP_TRY(dbg_sync(st, "k_cc_tile_w"));
     const int nseg = cdiv(g.m, kCcThreads), nfull = g.n / H, ncand = 2 * cdiv(g.m, kCcW) + 1;
-    k_cc_merge<H><<<nfull * nseg + ncand * cdiv(g.n, kCcThreads), kCcThreads, 0, st>>>(
-        g, kind, d.bond_first, d.bocc, d.socc, d.parent, d.member, nseg, nfull);
+    const int GM = nfull * nseg + ncand * cdiv(g.n, kCcThreads);
+    // site and mixed kinds: the cluster count from the tiles' member roots and
+    // the merge's hooks (the bond kind's member flags of a block's edge sites
+    // are completed by the merge, so it counts the roots afterwards)
+    int* part = nullptr;
+    if (kind != PERC_BOND) {
+      if (!d.ccpart) HIP_TRY(dmalloc(&d.ccpart, (size_t)G + GM));
+      part = d.ccpart;
+    }
+    if (kind == PERC_BOND) k_cc_tile_w<H, PERC_BOND><<<G, 64, 0, st>>>(g, d.bocc, d.socc, d.parent, d.member, nbb);
+    else if (kind == PERC_SITE)
+      k_cc_tile_w<H, PERC_SITE><<<G, 64, 0, st>>>(g, d.bocc, d.socc, d.parent, d.member, nbb, part);
+    else k_cc_tile_w<H, PERC_SITEBOND><<<G, 64, 0, st>>>(g, d.bocc, d.socc, d.parent, d.member, nbb, part);
+    HIP_TRY(dbg_sync(st, "k_cc_tile_w"));
+    k_cc_merge<H><<<GM, kCcThreads, 0, st>>>(g, kind, d.bond_first, d.bocc, d.socc, d.parent, d.member, nseg, nfull,
+                                             part ? part + G : nullptr);
     HIP_TRY(dbg_sync(st, "k_cc_merge"));
-    return label_finish(h, nspan, span_list, nclusters);
+    return label_finish(h, nspan, span_list, nclusters, part, part ? G + GM : 0);
   }
   const int tiles = cdiv(g.m, kCcW) * cdiv(g.n, kCcH);
   unsigned long long* ttr = nullptr;  // PERC_TILE_TRACE: per-workgroup phase stamps
@@ -513,7 +543,8 @@ hipError_t dev_label(perc_ctx* h, int* nspan, int* span_list, int* nclusters) {
 }
 
 // every parent to its root, cluster count, spanning roots, read-back
-static hipError_t label_finish(perc_ctx* h, int* nspan, int* span_list, int* nclusters) {
+static hipError_t label_finish(perc_ctx* h, int* nspan, int* span_list, int* nclusters, const int* part,
+                               int npart) {
   const Geom& g = h->g;
   hipStream_t st = h->stream;
   DeviceBuffers& d = h->d;
@@ -523,10 +554,12 @@ static hipError_t label_finish(perc_ctx* h, int* nspan, int* span_list, int* ncl
   // labels) -- a labeling that spans nothing (config 5 as stated, the
   // threshold scans' probes) does without it
   h->flat = false;
-  k_cc_count_roots<<<std::min(cdiv(g.t, kCcThreads * 4), kReduceGrid), kCcThreads, 0, st>>>(
-      g.t, d.parent, d.member, d.counters + 1);
-  HIP_TRY(dbg_sync(st, "k_cc_count_roots"));
-  k_span_top<<<1, 1024, 0, st>>>(g, d.parent, d.member, d.top, d.counters);
+  if (npart == 0) {
+    k_cc_count_roots<<<std::min(cdiv(g.t, kCcThreads * 4), kReduceGrid), kCcThreads, 0, st>>>(
+        g.t, d.parent, d.member, d.counters + 1);
+    HIP_TRY(dbg_sync(st, "k_cc_count_roots"));
+  }
+  k_span_top<<<1, 1024, 0, st>>>(g, d.parent, d.member, d.top, d.counters, part, npart);
   HIP_TRY(dbg_sync(st, "k_span_top"));
   int hc[8 + kMaxSpanList];
   HIP_TRY(hipMemcpyAsync(hc, d.counters, sizeof(hc), hipMemcpyDeviceToHost, st));

@@ -332,7 +332,7 @@ void dev_free_all(perc_ctx* h) {
                   d.order, d.parent, d.member, d.top, d.counters, d.x, d.r,
                   d.p0, d.p1, d.q, d.partials, d.tickets, d.scal, d.err_hist, d.iout,
                   d.res_xch, d.res_bar, d.bw, d.code_sm, d.csize, d.res_gran, (void*)d.nib_sm,
-                  d.sel_hist, d.sel_cand, d.mgran, d.forms_dev, d.lit};
+                  d.sel_hist, d.sel_cand, d.mgran, d.forms_dev, d.lit, d.ccpart};
   for (void* p : ptrs)
     if (p) hipFree(p);
   d = DeviceBuffers{};

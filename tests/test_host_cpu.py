@@ -313,6 +313,30 @@ def test_random_order_is_a_keyed_permutation():
     assert abs(np.mean(means) - (n + 1) / 2) < 0.05 * n
 
 
+def test_random_order_keys_are_the_defined_hash():
+    """The occupancy draw's keys, computed in 32-bit arithmetic with the seed
+    folded in once (lattice.h perc_rand_hash32, the device kernels' and the
+    host order's arithmetic), are the documented definition
+    (perc_rand_key: hash32 = high word of splitmix64(splitmix64(seed) ^ id),
+    key = hash32 << 32 | id; the bond stream seeded by
+    splitmix64(seed ^ 0x5DEECE66D)) -- restated here in Python integers."""
+    from percolation_amd import _lib as PL
+    M = (1 << 64) - 1
+
+    def mix64(x):
+        x = (x + 0x9E3779B97F4A7C15) & M
+        x = ((x ^ (x >> 30)) * 0xBF58476D1CE4E5B9) & M
+        x = ((x ^ (x >> 27)) * 0x94D049BB133111EB) & M
+        return x ^ (x >> 31)
+
+    n = 3000
+    for seed in (0, 1, 58302, 0xFFFFFFFF, 0x123456789ABCDEF0, M):
+        for kind, s_ in ((PL.SITE, seed), (PL.BOND, mix64(seed ^ 0x5DEECE66D))):
+            S = mix64(s_)
+            want = sorted(range(1, n + 1), key=lambda i: ((mix64(S ^ i) >> 32) << 32) | i)
+            assert api.random_order(n, n, seed, kind).tolist() == want, (seed, kind)
+
+
 @pytest.mark.parametrize("m,n,pbc", [(5, 4, 0), (5, 4, 1), (64, 33, 0), (17, 40, 1), (2, 3, 1)])
 def test_square_bond_first_closed_form(m, n, pbc):
     """lattice.h bf_square: bond_first of the square lattice's rows 0..n-2 is
