@@ -16,7 +16,7 @@ module perc_api
   integer(c_int), parameter :: PERC_RULE_BOND = 0, PERC_RULE_SITE = 1, PERC_RULE_MIXED = 2
   integer(c_int), parameter :: PERC_CUR_FORTRAN = 0, PERC_CUR_MATLAB = 1
   ! association of linbcg's dot products (perc_set_dot_order)
-  integer(c_int), parameter :: PERC_DOT_FAST = 0, PERC_DOT_LITERAL = 1
+  integer(c_int), parameter :: PERC_DOT_FAST = 0, PERC_DOT_LITERAL = 1, PERC_DOT_LITERAL_HOST = 2
   ! transports of the split solve (perc_dslab_solve_group)
   integer(c_int), parameter :: PERC_XPORT_RCCL = 0, PERC_XPORT_HOST = 1, PERC_XPORT_EXCHANGE = 4
   ! bytes of the RCCL unique id of the one-process-per-GPU split solve
@@ -176,6 +176,13 @@ module perc_api
       type(c_ptr), value :: h
       integer(c_int), value :: order
     end function perc_set_dot_order
+
+    ! what the last solve ran: out4 = (kernel PERC_RAN_*, flags, iterations, 0)
+    integer(c_int) function perc_last_solve(h, out4) bind(C, name='perc_last_solve')
+      import :: c_int, c_ptr
+      type(c_ptr), value :: h
+      integer(c_int), intent(out) :: out4(4)
+    end function perc_last_solve
 
     ! one solve split over K labeled contexts (row slabs, one host thread per
     ! context, RCCL or host-staged exchange): the linbcg call of bondc.f:545

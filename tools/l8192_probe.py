@@ -8,6 +8,7 @@ slope between itmax/2 and itmax, tol 0); GB/s on 26 B/row for P and B.
 0.652 ms per iteration, profiles/r4_4_l8192_strips_ab.json; removed.)
 
   python tools/l8192_probe.py --L 8192 --reps 10
+  python tools/l8192_probe.py --kind sitebond --ps 0.85 --p 0.85   # the config-5 companion
 """
 import argparse
 import json
@@ -25,6 +26,9 @@ def main():
     ap.add_argument("--p", type=float, default=0.6)
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--iters", type=int, default=400)
+    ap.add_argument("--kind", default="bond", choices=("bond", "sitebond"))
+    ap.add_argument("--ps", type=float, default=0.85)
+    ap.add_argument("--seed", type=int, default=777)
     args = ap.parse_args()
     from percolation_amd import _lib as PL
     from percolation_amd import api
@@ -33,7 +37,12 @@ def main():
     modes = {"rowmajor": PL.MARCH_DEFAULT}
     out = dict(L=L_)
     with api.Context(0, L_, L_, 0) as ctx:
-        ctx.occupy_random(PL.BOND, 0, int(args.p * nb), 777)
+        if args.kind == "bond":
+            ctx.occupy_random(PL.BOND, 0, int(args.p * nb), args.seed)
+            rule = (PL.RULE_BOND, PL.CUR_FORTRAN)
+        else:  # ConductCalc's mixed rule (MATLAB/ConductCalc.m:136-165)
+            ctx.occupy_random(PL.SITEBOND, int(args.ps * L_ * L_), int(args.p * nb), args.seed)
+            rule = (PL.RULE_MIXED, PL.CUR_MATLAB)
         assert ctx.label()["nspan"] > 0
         N, _ = ctx.system_size()
         best = {(m, w): 9e9 for m in modes for w in (1, 2, 5)}
@@ -41,7 +50,7 @@ def main():
         for _ in range(3):
             for name, mode in modes.items():
                 ctx.set_march_mode(mode)
-                ctx.conductance(tol=1e-8, itmax=2)
+                ctx.conductance(*rule, tol=1e-8, itmax=2)
                 info[name] = ctx.march_info()
                 for w in (1, 2, 5):
                     best[(name, w)] = min(best[(name, w)], ctx.bench_kernel(w, args.reps))
@@ -57,12 +66,12 @@ def main():
             t = {}
             for n in (args.iters // 2, args.iters):
                 t0 = time.perf_counter()
-                it = ctx.conductance(tol=0.0, itmax=n - 1)["iter"]
+                it = ctx.conductance(*rule, tol=0.0, itmax=n - 1)["iter"]
                 t[n] = (time.perf_counter() - t0, it)
             (t1, i1), (t2, i2) = t[args.iters // 2], t[args.iters]
             rec["solve_ms_per_it"] = round((t2 - t1) * 1e3 / (i2 - i1), 5)
             out[name] = rec
-    out["N"] = N
+    out.update(N=N, kind=args.kind, p=args.p, ps=args.ps if args.kind != "bond" else None)
     print(json.dumps(out), flush=True)
 
 
