@@ -42,10 +42,30 @@ __device__ __forceinline__ int xcd_logical_block(int b, int nwg) {
 // then one agent-scope ticket add; the workgroup drawing the last ticket sums
 // all partials in index order (cdna_hip_programming.md §6 Guideline 16, the
 // counter form with sc1 payload).
+// The wave's 64 values summed through DPP lane moves (VALU, a few cycles
+// each) instead of ds_bpermute shuffles (an LDS round trip per step): pairs
+// and quads by quad permutes, the row of 16 by rotates of 4 and 8, rows 0+1
+// and 2+3 by the row-15 broadcast, the total in lane 63 by the row-31
+// broadcast, read back to every lane.  A fixed association, the same on
+// every wave and run.
+template <int CTRL, int ROWS = 0xf>
+__device__ __forceinline__ double dpp_f64(double v) {
+  const unsigned long long u = __builtin_bit_cast(unsigned long long, v);
+  const unsigned lo = (unsigned)__builtin_amdgcn_update_dpp(0, (int)(unsigned)u, CTRL, ROWS, 0xf, false);
+  const unsigned hi = (unsigned)__builtin_amdgcn_update_dpp(0, (int)(unsigned)(u >> 32), CTRL, ROWS, 0xf, false);
+  return __builtin_bit_cast(double, (unsigned long long)hi << 32 | lo);
+}
 __device__ __forceinline__ double wave_sum(double v) {
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) v = v + __shfl_xor(v, off, 64);
-  return v;
+  v = v + dpp_f64<0xB1>(v);        // quad_perm [1,0,3,2]
+  v = v + dpp_f64<0x4E>(v);        // quad_perm [2,3,0,1]
+  v = v + dpp_f64<0x124>(v);       // row_ror:4
+  v = v + dpp_f64<0x128>(v);       // row_ror:8 (every lane: its row's sum)
+  v = v + dpp_f64<0x142, 0xA>(v);  // row_bcast:15 into rows 1, 3
+  v = v + dpp_f64<0x143, 0xC>(v);  // row_bcast:31 into rows 2, 3 (lane 63: the total)
+  const unsigned long long u = __builtin_bit_cast(unsigned long long, v);
+  const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)u, 63);
+  const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(u >> 32), 63);
+  return __builtin_bit_cast(double, (unsigned long long)hi << 32 | lo);
 }
 
 template <int NV>
