@@ -56,6 +56,11 @@ __device__ __forceinline__ double dpp_f64(double v) {
   return __builtin_bit_cast(double, (unsigned long long)hi << 32 | lo);
 }
 __device__ __forceinline__ double wave_sum(double v) {
+#ifdef PERC_WAVE_SUM_SHFL  // A/B probe builds only: the ds_bpermute butterfly
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v = v + __shfl_xor(v, off, 64);
+  return v;
+#endif
   v = v + dpp_f64<0xB1>(v);        // quad_perm [1,0,3,2]
   v = v + dpp_f64<0x4E>(v);        // quad_perm [2,3,0,1]
   v = v + dpp_f64<0x124>(v);       // row_ror:4

@@ -8,12 +8,14 @@ the libraries alternating for `rounds` rounds, each figure its best.
   5 (a whole iteration), best of 3 x `reps` launches, plus ms per iteration
   of fixed-iteration solves (slope between itmax/2 and itmax, tol 0);
   --format csr: the CSR operator (0 plain SpMV, 1 S, 2 B, 3 P, 5 iteration);
---what label: per realisation (device-drawn bond occupancy, `reps`
-  realisations), wall ms of perc_occupy_random, perc_label (labels +
-  spanning test + its read-back) and the partition's cluster count.
+--what label: per realisation (device-drawn occupancy, `reps`
+  realisations; --kind bond, or sitebond with --ps: config 5's mixed
+  kind), wall ms of perc_occupy_random, perc_label (labels + spanning test
+  + its read-back) and the partition's cluster count.
 
   python tools/lib_ab.py --L 4096 --libs main,s16,s18 [--mode 1559]
   python tools/lib_ab.py --what label --L 4096 --libs main,mrows
+  python tools/lib_ab.py --what label --L 8192 --kind sitebond --ps 0.593 --p 0.5 --libs main,r5f
 """
 import argparse
 import json
@@ -37,7 +39,10 @@ def child_label(args):
         for k in range(args.reps + 1):
             torch.cuda.synchronize()
             t0 = time.perf_counter()
-            ctx.occupy_random(PL.BOND, 0, int(args.p * nb), 1000 + k)
+            if args.kind == "bond":
+                ctx.occupy_random(PL.BOND, 0, int(args.p * nb), 1000 + k)
+            else:
+                ctx.occupy_random(PL.SITEBOND, int(args.ps * L_ * L_), int(args.p * nb), 1000 + k)
             torch.cuda.synchronize()
             t1 = time.perf_counter()
             li = ctx.label()
@@ -94,6 +99,8 @@ def main():
     ap.add_argument("--mode", type=int, default=-1)
     ap.add_argument("--libs", default="main")
     ap.add_argument("--what", default="solve", choices=("solve", "label"))
+    ap.add_argument("--kind", default="bond", choices=("bond", "sitebond"))
+    ap.add_argument("--ps", type=float, default=0.593)
     ap.add_argument("--format", default="default", choices=("default", "csr"))
     ap.add_argument("--child", action="store_true")
     ap.add_argument("--wspec", default="", help=argparse.SUPPRESS)
@@ -115,7 +122,8 @@ def main():
                 env["PERC_LIBPERC"] = os.path.join(REPO, "percolation_amd", "probe", "libperc_%s.so" % lib)
             cmd = [sys.executable, os.path.abspath(__file__), "--child", "--L", str(args.L), "--p", str(args.p),
                    "--reps", str(args.reps), "--iters", str(args.iters), "--mode", str(args.mode),
-                   "--what", args.what, "--format", args.format, "--wspec", spec]
+                   "--what", args.what, "--format", args.format, "--wspec", spec, "--kind", args.kind,
+                   "--ps", str(args.ps)]
             r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600)
             if r.returncode != 0:
                 sys.stderr.write(r.stderr[-3000:])
