@@ -98,7 +98,7 @@ struct DeviceBuffers {
   int* csize = nullptr;      // t+2 per-root cluster sizes (perc_cluster_sizes)
   int* ccpart = nullptr;     // the wave tiles' member roots per block, then minus the merge's hooks per workgroup
   StencilForms* forms_dev = nullptr;  // device copy of perc_ctx::forms (k_assemble)
-  unsigned* sel_hist = nullptr;  // perc_occupy_random's select: [0] keys below, [1] in window, [2] window valid
+  unsigned* sel_hist = nullptr;  // perc_occupy_random's select, per draw: [0] keys below, [1] in window, [2] window valid, [4 ..] bins
   unsigned long long* sel_cand = nullptr;  // [0] the threshold key, then the window's keys
   // CG
   double* x = nullptr;

@@ -29,12 +29,27 @@ __global__ void k_occupy(const int* order, int count, long long limit, uint8_t* 
 // keys -- slow, exact: T is the exact order statistic on every path.
 constexpr int kSelCap = 1 << 17, kSelThreads = 1024, kSelStage = 512, kSelBins = 4096;
 constexpr int kSelBinCap = 1024;
+constexpr int kSelCnt = 4 + kSelBins;  // unsigned words per draw (cnt)
+// bins of the window's hash range: (hash - lo) >> sh < kSelBins
+__host__ __device__ inline int sel_shift(unsigned long long lo, unsigned long long hi) {
+  const unsigned long long range = hi - lo;
+  int bits = 0;
+  while (bits < 64 && range > 1 && (range - 1) >> bits) ++bits;
+  return bits > 12 ? bits - 12 : 0;
+}
+// cnt: [0] keys below the window, [1] keys in it, [2] window valid, [3]
+// unused, [4 ..] kSelBins bin counts of the window keys by hash; pad (the
+// first workgroup): the occupancy array's pad bytes zeroed, npad at padp
 __global__ __launch_bounds__(kBlock) void k_select_window(long long n, RandKeyCtx kc,
                                                           unsigned long long lo,
-                                                          unsigned long long hi,
+                                                          unsigned long long hi, int sh,
                                                           unsigned* cnt,
                                                           unsigned long long* cand, int base,
-                                                          uint8_t* occ) {
+                                                          uint8_t* occ, uint8_t* padp, int npad) {
+  if (blockIdx.x == 0) {  // the pads: occ[0 .. base) and npad bytes at padp
+    if ((int)threadIdx.x < npad) padp[threadIdx.x] = 0;
+    if ((int)threadIdx.x < base) occ[threadIdx.x] = 0;
+  }
   __shared__ unsigned long long s_c[kSelStage];
   __shared__ unsigned s_n, s_base, s_b[kBlock / 64];
   if (threadIdx.x == 0) s_n = 0;
@@ -51,6 +66,7 @@ __global__ __launch_bounds__(kBlock) void k_select_window(long long n, RandKeyCt
     // the window's keys (0 here) are decided by k_occupy_cand once T is known
     occ[i + base] = hsh < lo ? 1 : 0;
     if (hsh >= lo && hsh < hi) {
+      atomicAdd(&cnt[4 + (int)((hsh - lo) >> sh)], 1u);
       const unsigned slot = atomicAdd(&s_n, 1u);
       if (slot < (unsigned)kSelStage) {
         s_c[slot] = key;
@@ -91,26 +107,16 @@ __global__ __launch_bounds__(kSelThreads) void k_select_final(long long n,
   const long long below = cnt[0], nin = cnt[1];
   const bool win = count > below && count - below <= nin && nin <= kSelCap;
   // T inside the window and every window key gathered: k_select_window's
-  // occupation stands and k_occupy_cand completes it; else k_occupy_rand
+  // occupation stands and k_occupy_cand completes it; else k_occupy_cand
   // rewrites the whole occupation from T
   if (threadIdx.x == 0) cnt[2] = win ? 1u : 0u;
   if (win) {
     // bins of the window's hash range: (hash - lo) >> sh < kSelBins
-    const unsigned long long range = hi - lo;
-    const int bits = range > 1 ? 64 - __clzll((long long)(range - 1)) : 0;
-    const int sh = max(0, bits - 12);
-    for (int j = threadIdx.x; j < kSelBins; j += kSelThreads) s_h[j] = 0;
+    const int sh = sel_shift(lo, hi);
+    // the bin counts k_select_window kept (a block-wide LDS histogram of the
+    // window keys here cost ~15 us per draw of conflicting LDS atomics)
+    for (int j = threadIdx.x; j < kSelBins; j += kSelThreads) s_h[j] = cnt[4 + j];
     if (threadIdx.x == 0) s_nb = 0;
-    __syncthreads();
-    constexpr int kU = 8;  // loads in flight per thread
-    for (long long i0 = threadIdx.x; i0 < nin; i0 += kSelThreads * kU) {
-      unsigned long long kk[kU];
-#pragma unroll
-      for (int u = 0; u < kU; ++u) kk[u] = i0 + u * kSelThreads < nin ? cand[1 + i0 + u * kSelThreads] : 0;
-#pragma unroll
-      for (int u = 0; u < kU; ++u)
-        if (i0 + u * kSelThreads < nin) atomicAdd(&s_h[((kk[u] >> 32) - lo) >> sh], 1u);
-    }
     __syncthreads();
     if (threadIdx.x == 0) tr[1] = wall_clock64();
     {  // the bin of the (count - below)-th window key: a block scan of the
@@ -215,29 +221,21 @@ __global__ __launch_bounds__(kSelThreads) void k_select_final(long long n,
   if (threadIdx.x == 0) cand[0] = s_sel[0];
 }
 
-// occupy every id whose key is <= T (T = the count-th smallest key);
-// occ[id - 1 + base] (bonds: base 0, 0-based; sites: base 1, socc[id])
-// (Tp: the threshold in device memory, k_select_final's; null: all n).
-// valid (k_select_final's cnt[2]): nonzero when k_select_window's
-// occupation stands -- then this pass returns at once (grid-stride, a
-// small grid)
-__global__ __launch_bounds__(kBlock) void k_occupy_rand(long long n, RandKeyCtx kc,
-                                                         const unsigned long long* Tp, int base,
-                                                         uint8_t* occ, const unsigned* valid) {
-  if (valid && *valid) return;
-  const unsigned long long T = Tp ? *Tp : ~0ull;
-  for (long long i = (long long)blockIdx.x * kBlock + threadIdx.x; i < n; i += (long long)gridDim.x * kBlock) {
-    const unsigned id = (unsigned)(i + 1);
-    occ[i + base] = ((unsigned long long)perc_rand_hash32(kc, id) << 32 | id) <= T ? 1 : 0;
-  }
-}
-
-// the window's keys (cand[1 ..], id in the low 32 bits) at or below T
+// the window's keys (cand[1 ..], id in the low 32 bits) at or below T; when
+// T fell outside the window (cnt[2] == 0, rare) the whole occupation is
+// rewritten from T instead, grid-stride over all n ids (one launch either
+// way: an empty second launch cost ~5 us per draw)
 __global__ __launch_bounds__(kBlock) void k_occupy_cand(const unsigned* cnt, const unsigned long long* cand,
-                                                         int base, uint8_t* occ) {
-  if (!cnt[2]) return;
-  const unsigned nin = cnt[1];
+                                                         int base, uint8_t* occ, long long n, RandKeyCtx kc) {
   const unsigned long long T = cand[0];
+  if (!cnt[2]) {
+    for (long long i = (long long)blockIdx.x * kBlock + threadIdx.x; i < n; i += (long long)gridDim.x * kBlock) {
+      const unsigned id = (unsigned)(i + 1);
+      occ[i + base] = ((unsigned long long)perc_rand_hash32(kc, id) << 32 | id) <= T ? 1 : 0;
+    }
+    return;
+  }
+  const unsigned nin = cnt[1];
   for (unsigned j = blockIdx.x * kBlock + threadIdx.x; j < nin; j += gridDim.x * kBlock) {
     const unsigned long long key = cand[1 + j];
     if (key <= T) occ[(long long)(key & 0xFFFFFFFFull) - 1 + base] = 1;
@@ -270,13 +268,34 @@ __global__ __launch_bounds__(1024) void k_span_top(Geom g, const int* parent,
   for (int c = threadIdx.x; c <= m; c += 1024) flag[c] = 0;
   if (threadIdx.x == 0) s_base = 0;
   __syncthreads();
-  for (int c = threadIdx.x; c < m; c += 1024) {
-    const int s = g.t - m + 1 + c;
-    if (member[s]) {
-      int root = parent[s];  // (parents may not be flattened yet: dev_flatten)
-      for (int up = parent[root]; up != root; up = parent[root]) root = up;
-      if (root <= m) flag[root] = 1;
+  // the top row's chains (parents may not be flattened yet: dev_flatten),
+  // a thread's U sites chased in lockstep: every hop issues their U parent
+  // loads together (one site after another: 33 us per labeling at m = 8192)
+  constexpr int U = 8;
+  for (int c0 = threadIdx.x; c0 < m; c0 += 1024 * U) {
+    int x[U];
+    bool act[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int c = c0 + 1024 * u, s = g.t - m + 1 + c;
+      act[u] = c < m && member[s];
+      x[u] = act[u] ? parent[s] : 0;
     }
+    while (true) {
+      int y[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) y[u] = act[u] ? parent[x[u]] : x[u];
+      bool more = false;
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        more |= y[u] != x[u];
+        x[u] = y[u];
+      }
+      if (!more) break;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (act[u] && x[u] <= m) flag[x[u]] = 1;
   }
   __syncthreads();
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -301,7 +320,13 @@ __global__ __launch_bounds__(1024) void k_span_top(Geom g, const int* parent,
   if (threadIdx.x == 0) counters[0] = s_base;
   if (npart > 0) {  // (uniform)
     int v = 0;
-    for (int i = threadIdx.x; i < npart; i += 1024) v += part[i];
+    for (int i0 = threadIdx.x; i0 < npart; i0 += 1024 * 8) {
+      int pv[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) pv[u] = i0 + 1024 * u < npart ? part[i0 + 1024 * u] : 0;
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v += pv[u];
+    }
     v = wave_sum_int(v);
     __syncthreads();
     if (lane == 0) s_w[wid] = v;
@@ -413,21 +438,20 @@ hipError_t dev_occupy(perc_ctx* h, int kind, int nsites, const int* site_order, 
 // k_select_window (every key hashed once: the keys below the window
 // occupied, the others not, the window's keys gathered), the one-workgroup
 // select of T (k_select_final), then the window's keys at or below T
-// (k_occupy_cand); when T fell outside the window the whole occupation is
-// rewritten from T (k_occupy_rand, otherwise an early return).  No host
+// (k_occupy_cand); when T fell outside the window k_occupy_cand rewrites the
+// whole occupation from T instead.  No host
 // synchronisation.
 static hipError_t occupy_rand_one(perc_ctx* h, long long n, long long count,
-                                  unsigned long long seed, int base, uint8_t* occ) {
+                                  unsigned long long seed, int base, uint8_t* occ, unsigned* cnt,
+                                  uint8_t* padp, int npad) {
   hipStream_t st = h->stream;
   const int G = (int)std::min<long long>(cdiv(n, kBlock), 2048);
-  if (count <= 0) return hipMemsetAsync(occ + base, 0, (size_t)n, st);
   const RandKeyCtx kc = perc_rand_key_ctx(seed);
-  if (count >= n) {
-    k_occupy_rand<<<G, kBlock, 0, st>>>(n, kc, nullptr, base, occ, nullptr);
-    return hipGetLastError();
+  if (count <= 0 || count >= n) {
+    HIP_TRY(hipMemsetAsync(occ + base, count <= 0 ? 0 : 1, (size_t)n, st));
+    if (base) HIP_TRY(hipMemsetAsync(occ, 0, (size_t)base, st));
+    return npad ? hipMemsetAsync(padp, 0, (size_t)npad, st) : hipSuccess;
   }
-  if (!h->d.sel_hist) HIP_TRY(dmalloc(&h->d.sel_hist, 4));
-  if (!h->d.sel_cand) HIP_TRY(dmalloc(&h->d.sel_cand, (size_t)kSelCap + 1 + 16));
   // window: T's hash is count/n * 2^32 give or take the binomial spread
   // sqrt(n q (1-q)) keys; +-(8 sigma + 256) keys of hash width
   const double q = (double)count / (double)n;
@@ -437,10 +461,10 @@ static hipError_t occupy_rand_one(perc_ctx* h, long long n, long long count,
   unsigned long long hi = c + w >= two32 ? (1ull << 32) : (unsigned long long)(c + w) + 1;
   const char* full = std::getenv("PERC_SELECT_FULL");  // tests: the exact slow path
   if (full && full[0] == '1') lo = hi = 0;
-  HIP_TRY(hipMemsetAsync(h->d.sel_hist, 0, 4 * sizeof(unsigned), st));
-  k_select_window<<<G, kBlock, 0, st>>>(n, kc, lo, hi, h->d.sel_hist, h->d.sel_cand, base, occ);
+  k_select_window<<<G, kBlock, 0, st>>>(n, kc, lo, hi, sel_shift(lo, hi), cnt, h->d.sel_cand, base, occ, padp,
+                                        npad);
   HIP_TRY(dbg_sync(st, "k_select_window"));
-  k_select_final<<<1, kSelThreads, 0, st>>>(n, seed, count, lo, hi, h->d.sel_hist, h->d.sel_cand);
+  k_select_final<<<1, kSelThreads, 0, st>>>(n, seed, count, lo, hi, cnt, h->d.sel_cand);
   HIP_TRY(dbg_sync(st, "k_select_final"));
   if (std::getenv("PERC_SELECT_TRACE")) {
     unsigned long long tr[6];
@@ -449,28 +473,28 @@ static hipError_t occupy_rand_one(perc_ctx* h, long long n, long long count,
     std::fprintf(stderr, "select trace: hist %llu bin %llu rank %llu ticks; nin %llu bin %llu\n",
                  tr[1] - tr[0], tr[2] - tr[1], tr[3] - tr[2], tr[4], tr[5]);
   }
-  k_occupy_cand<<<cdiv(kSelCap, kBlock), kBlock, 0, st>>>(h->d.sel_hist, h->d.sel_cand, base, occ);
-  HIP_TRY(dbg_sync(st, "k_occupy_cand"));
-  k_occupy_rand<<<G, kBlock, 0, st>>>(n, kc, h->d.sel_cand, base, occ, h->d.sel_hist + 2);
-  return hipGetLastError();
+  k_occupy_cand<<<cdiv(kSelCap, kBlock), kBlock, 0, st>>>(cnt, h->d.sel_cand, base, occ, n, kc);
+  return dbg_sync(st, "k_occupy_cand");
 }
 
 hipError_t dev_occupy_random(perc_ctx* h, int kind, int nsites, int nbonds,
                              unsigned long long seed) {
   hipStream_t st = h->stream;
   DeviceBuffers& d = h->d;
-  // the drawn ranges are written whole (occupy_rand_one); zero the rest
+  // one memset: both draws' counters and bin counts; the drawn ranges are
+  // written whole and their pad bytes by the draw (socc[0] and socc[t+1 ..
+  // t+8) with the sites, bocc[nb .. nb+8) with the bonds); an undrawn kind
+  // is zeroed whole
+  if (!d.sel_hist) HIP_TRY(dmalloc(&d.sel_hist, 2 * kSelCnt));
+  if (!d.sel_cand) HIP_TRY(dmalloc(&d.sel_cand, (size_t)kSelCap + 1 + 16));
+  HIP_TRY(hipMemsetAsync(d.sel_hist, 0, sizeof(unsigned) * 2 * kSelCnt, st));
   if (kind == PERC_SITE) HIP_TRY(hipMemsetAsync(d.bocc, 0, (size_t)h->nb + 8, st));
-  else HIP_TRY(hipMemsetAsync(d.bocc + h->nb, 0, 8, st));
-  if (kind == PERC_BOND) {
-    HIP_TRY(hipMemsetAsync(d.socc, 0, h->g.t + 8, st));
-  } else {
-    HIP_TRY(hipMemsetAsync(d.socc, 0, 1, st));
-    HIP_TRY(hipMemsetAsync(d.socc + h->g.t + 1, 0, 7, st));
-  }
-  if (kind != PERC_BOND) HIP_TRY(occupy_rand_one(h, h->g.t, nsites, seed, 1, d.socc));
+  if (kind == PERC_BOND) HIP_TRY(hipMemsetAsync(d.socc, 0, h->g.t + 8, st));
+  if (kind != PERC_BOND)
+    HIP_TRY(occupy_rand_one(h, h->g.t, nsites, seed, 1, d.socc, d.sel_hist, d.socc + h->g.t + 1, 7));
   if (kind != PERC_SITE)
-    HIP_TRY(occupy_rand_one(h, h->nb, nbonds, perc_mix64(seed ^ 0x5DEECE66Dull), 0, d.bocc));
+    HIP_TRY(occupy_rand_one(h, h->nb, nbonds, perc_mix64(seed ^ 0x5DEECE66Dull), 0, d.bocc, d.sel_hist + kSelCnt,
+                            d.bocc + h->nb, 8));
   return hipSuccess;
 }
 
@@ -482,12 +506,15 @@ hipError_t dev_label(perc_ctx* h, int* nspan, int* span_list, int* nclusters) {
   hipStream_t st = h->stream;
   DeviceBuffers& d = h->d;
   const int kind = h->last.kind;
-  HIP_TRY(hipMemsetAsync(d.counters, 0, sizeof(int) * (8 + kMaxSpanList), st));
+  // (the site and mixed kinds on the open square lattice: k_span_top writes
+  // every counter the labeling reads, no memset)
+  const bool wave = g.lattice == kSquare && !g.pbc && h->bf_open_sq && !std::getenv("PERC_TILE_TRACE");
+  if (!wave || kind == PERC_BOND) HIP_TRY(hipMemsetAsync(d.counters, 0, sizeof(int) * (8 + kMaxSpanList), st));
   // the open square lattice: one wave per 128 x 16 block walking its rows
   // (k_cc_tile_w; tile 91.7 vs 190.6 us for the 128 x 32 LDS union-find
   // blocks at L = 4096, profiles/r4_13_cc_bench_L4096.txt); else the LDS
   // union-find blocks
-  if (g.lattice == kSquare && !g.pbc && h->bf_open_sq && !std::getenv("PERC_TILE_TRACE")) {
+  if (wave) {
     constexpr int H = kCcWaveH;
     const int G = cdiv(g.m, kCcW) * cdiv(g.n, H);
     const unsigned nbb = (unsigned)h->nb + 8u;

@@ -179,6 +179,18 @@ __device__ bool publish_and_reduce_tagged(double (&v)[NV], double* gran, unsigne
 
 constexpr int kMarchW = 128;     // columns per wave strip
 constexpr int kMarchWaves = 4;   // waves (strips) per workgroup
+// A/B probe builds only: the column-class path in the row-major march too
+// (PERC_MARCH_RM_SQ), optionally held to 4 waves per SIMD (PERC_MARCH_RM_SQ4)
+#if defined(PERC_MARCH_RM_SQ) || defined(PERC_MARCH_RM_SQ4)
+constexpr bool kMarchRmSq = true;
+#else
+constexpr bool kMarchRmSq = false;
+#endif
+#ifdef PERC_MARCH_RM_SQ4
+#define PERC_MARCH_MINW(SM, MODE) ((SM) || (MODE) == 0 ? 1 : 4)
+#else
+#define PERC_MARCH_MINW(SM, MODE) 1
+#endif
 
 struct MRow {       // one prefetched row of the lane's pair (+ halo column)
   double2 p, r;     // p(k-1), r
@@ -484,8 +496,12 @@ __device__ __forceinline__ void march_step(const CGArgs& a, const MGeom& g, cons
     // path where the lattice is the open square one (a.sqcls) and every
     // row of the step carries its column class's count / form bits
     bool sqp;
+    // (strip-major u16 codes only: in the row-major march past the Infinity
+    // Cache the path's 6 VGPRs cost a wave per SIMD -- 133 vs 127, P 0.394
+    // vs 0.314 ms at L = 8192, profiles/r5_6_l8192_probe_bond.json)
     if constexpr (PK) sqp = !a.T.pbc;
-    else sqp = a.sqcls && !__any((((c0w ^ g.cb0) | (c1w ^ g.cb1)) >> 8) != 0u);
+    else if constexpr (SM || kMarchRmSq) sqp = a.sqcls && !__any((((c0w ^ g.cb0) | (c1w ^ g.cb1)) >> 8) != 0u);
+    else sqp = false;
     if (sqp) {
       // Open square lattice, nibble codes: every row is interior, column 0
       // or column m-1 (k_pack_nib checked it), so EVERY wave -- the edge
@@ -606,7 +622,7 @@ __device__ __forceinline__ void march_walk(const CGArgs& a, const MGeom& g, cons
 // TAG: the epilogue reductions by tagged granules (publish_and_reduce_tagged)
 template <int MODE, bool SM = false, int D = kMarchDepth, int PAUX = 0, bool TR = false,
           bool TAG = false, bool PK = false, bool LIT = false>
-__global__ __launch_bounds__(64 * kMarchWaves) void k_cg_march(CGArgs a) {
+__global__ __launch_bounds__(64 * kMarchWaves, PERC_MARCH_MINW(SM, MODE)) void k_cg_march(CGArgs a) {
   const unsigned long long tr_t0 = TR ? wall_clock64() : 0ull;
   unsigned long long tr_t1 = 0ull;
   CGScalars* S = a.S;

@@ -85,6 +85,10 @@ def check(li, canon, perccln, span_root):
     assert (li["nspan"] > 0) == (perccln > 0), (li["nspan"], perccln)
     if perccln > 0:
         assert li["span_root"] == span_root
+    # the cluster count (a pass over the member roots, or -- the site and
+    # mixed kinds on the open square lattice -- the wave tiles' member roots
+    # minus the merge's hooks) is the partition's
+    assert li["nclusters"] == len(np.unique(canon[canon > 0])), (li["nclusters"], len(np.unique(canon[canon > 0])))
 
 
 # ------------------------------------------------------------ CPU: the oracle's mixed replay

@@ -1,0 +1,21 @@
+#!/bin/bash
+# round 5, call i: the occupancy draw's select with its bins kept by the
+# window pass, one launch for the window's keys (or the rare full rewrite),
+# one memset per draw pair, the top row's chains in lockstep: the labeling
+# tests, then config 5 as stated (kernel trace; 1 / 2 realisations in flight)
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+step() {
+  local name=$1 t=$2; shift 2
+  timeout -k 10 "$t" "$@" > gpurun_out/r5i_$name.log 2>&1
+  local rc=$?
+  echo "$name rc=$rc"
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then tail -30 gpurun_out/r5i_$name.log; exit $rc; fi
+}
+step pytest 600 python -u -m pytest tests/test_labeling_oracle.py tests/test_gpu_parity.py -m gpu -x -q --timeout 300 --timeout-method thread
+tail -3 gpurun_out/r5i_pytest.log
+C5="--L 8192 --kind sitebond --ps 0.593 --p 0.50 --warmup 1 --no-cpu-baseline"
+step c5prof 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/r5i_c5prof -o c5 -- python3 -u bench.py $C5 --steps 16
+step c5k1 200 python -u bench.py $C5 --steps 32
+step c5k2 200 python -u bench.py $C5 --steps 32 --concurrent 2
+for k in 1 2; do tail -1 gpurun_out/r5i_c5k$k.log | cut -c1-160; done

@@ -4,7 +4,8 @@
 in-tree library: per library, in a child process of its own (PERC_LIBPERC),
 the libraries alternating for `rounds` rounds, each figure its best.
 
---what solve: one L x L bond realisation, perc_bench_kernel 1 (P), 2 (B) and
+--what solve: one L x L bond realisation (--kind sitebond --ps: a mixed one,
+  ConductCalc's mixed rule), perc_bench_kernel 1 (P), 2 (B) and
   5 (a whole iteration), best of 3 x `reps` launches, plus ms per iteration
   of fixed-iteration solves (slope between itmax/2 and itmax, tol 0);
   --format csr: the CSR operator (0 plain SpMV, 1 S, 2 B, 3 P, 5 iteration);
@@ -69,11 +70,16 @@ def child(args):
         for part in filter(None, args.wspec.split("/")):  # "which:w0,w1,w2/..."
             which, ws = part.split(":")
             ctx.set_band_weights(int(which), [int(x) for x in ws.split(",")])
-        ctx.occupy_random(PL.BOND, 0, int(args.p * nb), 777)
+        if args.kind == "bond":
+            ctx.occupy_random(PL.BOND, 0, int(args.p * nb), 777)
+            rule = (PL.RULE_BOND, PL.CUR_FORTRAN)
+        else:  # ConductCalc's mixed rule (the config-5 companion's matrix)
+            ctx.occupy_random(PL.SITEBOND, int(args.ps * L_ * L_), int(args.p * nb), 777)
+            rule = (PL.RULE_MIXED, PL.CUR_MATLAB)
         assert ctx.label()["nspan"] > 0
         if args.format == "csr":
             ctx.set_matrix_format(PL.FMT_CSR)
-        c = ctx.conductance(tol=1e-8, itmax=args.iters)
+        c = ctx.conductance(*rule, tol=1e-8, itmax=args.iters)
         out["fp"] = [c["iter"], c["gtop"], c["gbot"]]  # same numbers across store policies
         kset = ((1, "P"), (2, "B"), (5, "iteration")) if args.format == "default" else \
             ((0, "spmv_plain"), (1, "S"), (2, "B"), (3, "P"), (5, "iteration"))
@@ -82,7 +88,7 @@ def child(args):
         t = {}
         for n in (args.iters // 2, args.iters):
             t0 = time.perf_counter()
-            it = ctx.conductance(tol=0.0, itmax=n - 1)["iter"]
+            it = ctx.conductance(*rule, tol=0.0, itmax=n - 1)["iter"]
             t[n] = (time.perf_counter() - t0, it)
         (t1, i1), (t2, i2) = t[args.iters // 2], t[args.iters]
         out["solve_ms_per_it"] = (t2 - t1) * 1e3 / (i2 - i1)
