@@ -330,7 +330,30 @@ StencilForms stencil_forms(const Geom& g) {
   return F;
 }
 
-static hipError_t launch_assemble(perc_ctx* h, bool csr) {
+static // The CSR rows of <= 4 off-diagonals in 4 aligned slots, in the CSR order:
+// columns (padding: the row itself), values (padding: 0, never added), the
+// entry count (perc_csr.h ell_row)
+__global__ __launch_bounds__(kBlock) void k_csr_to_ell(int N, const int* __restrict__ rowptr,
+                                                       const int* __restrict__ col,
+                                                       const double* __restrict__ val, int4* ecol,
+                                                       double2* eval, uint8_t* ecnt) {
+  const int i = blockIdx.x * kBlock + threadIdx.x;
+  if (i >= N) return;
+  const int a = rowptr[i], n = rowptr[i + 1] - a;
+  int c[4];
+  double v[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    c[j] = j < n ? col[a + j] : i;
+    v[j] = j < n ? val[a + j] : 0.0;
+  }
+  ecol[i] = make_int4(c[0], c[1], c[2], c[3]);
+  eval[2 * i] = make_double2(v[0], v[1]);
+  eval[2 * i + 1] = make_double2(v[2], v[3]);
+  ecnt[i] = (uint8_t)n;
+}
+
+hipError_t launch_assemble(perc_ctx* h, bool csr) {
   HIP_TRY(dev_flatten(h));  // (the roots, not their ancestors)
   DeviceBuffers& d = h->d;
   const AsmParams& p = h->asm_p;
@@ -389,6 +412,18 @@ static hipError_t launch_assemble(perc_ctx* h, bool csr) {
                                                            p.g0, p.leak, p.Va, p.span_root, w);
   HIP_TRY(dbg_sync(st, "k_assemble"));
   h->csr_ok = csr;
+  h->ell_ok = false;
+  if (csr && h->csr_maxrow <= 4) {  // the ELL copy the CSR SpMV kernels read (perc_csr.h ell_row)
+    if (!d.ell_col) {
+      HIP_TRY(hipMalloc(&d.ell_col, sizeof(int4) * (size_t)h->N));
+      HIP_TRY(hipMalloc(&d.ell_val, sizeof(double2) * 2 * (size_t)h->N));
+      HIP_TRY(hipMalloc(&d.ell_cnt, (size_t)h->N));
+    }
+    k_csr_to_ell<<<cdiv(h->N, kBlock), kBlock, 0, st>>>(h->N, d.rowptr, d.col, d.val, d.ell_col, d.ell_val,
+                                                       d.ell_cnt);
+    HIP_TRY(dbg_sync(st, "k_csr_to_ell"));
+    h->ell_ok = true;
+  }
   return hipSuccess;
 }
 
@@ -483,6 +518,7 @@ hipError_t dev_set_bond_weights(perc_ctx* h, const double* w) {
   // again before the next solve / system read
   h->assembled = false;
   h->csr_ok = false;
+  h->ell_ok = false;
   if (!w) {
     h->has_weights = false;
     return hipSuccess;

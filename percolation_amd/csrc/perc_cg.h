@@ -216,6 +216,7 @@ __global__ __launch_bounds__(kBlock) void k_cg_spmv(CGArgs a) {
 // and q(i) p(i), summed per workgroup, then the grid-wide reduction; grid
 // cdiv(N, kBlock) (perc_ctx::row_grid).  Against the LDS-staged wave tiles
 // it replaced: 0.294 vs 0.299 ms at L = 4096 (profiles/r4_11_csr_row_ab_L4096.json).
+// NS = -1: the ELL copy's row (ell_row, q stored nontemporal)
 template <int NS>
 __global__ __launch_bounds__(kBlock) void k_cg_spmv_row(CGArgs a) {
   CGScalars* S = a.S;
@@ -225,9 +226,15 @@ __global__ __launch_bounds__(kBlock) void k_cg_spmv_row(CGArgs a) {
   const int i = blockIdx.x * kBlock + threadIdx.x;
   double dot[1] = {0.0};
   if (i < a.A.N) {
-    const double qi = csr_row<NS>(a.A, a.p, i);
-    a.q[i] = qi;
-    dot[0] = qi * a.p[i];
+    if constexpr (NS < 0) {
+      const double qi = ell_row(a.A, a.p, i);
+      __builtin_nontemporal_store(qi, a.q + i);
+      dot[0] = qi * a.p[i];
+    } else {
+      const double qi = csr_row<NS>(a.A, a.p, i);
+      a.q[i] = qi;
+      dot[0] = qi * a.p[i];
+    }
   }
   double tot[1];
   if (publish_and_reduce<1>(dot, a.partials, a.tickets, blockIdx.x, gridDim.x, tot, s_red, s_flag)) {
@@ -1086,6 +1093,11 @@ constexpr int kTagMaxIter = (1 << 24) - 2;
 CGArgs make_cg_args(perc_ctx* h) {
   CGArgs a;
   a.A = CsrView{h->N, h->d.rowptr, h->d.col, h->d.val, h->d.diag, h->csr_maxrow};
+  if (h->ell_ok) {
+    a.A.ecol = h->d.ell_col;
+    a.A.eval = h->d.ell_val;
+    a.A.ecnt = h->d.ell_cnt;
+  }
   a.St = StencilView{h->N, h->d.code, h->st_ng0, h->st_nleak, h->forms, h->d.dtab};
   a.T = TileGeom{h->g.m, h->g.n - 2, h->g.pbc, (h->g.m + kTileW - 1) / kTileW, h->march_h};
   a.pb[0] = h->d.p0;

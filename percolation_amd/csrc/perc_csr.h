@@ -24,6 +24,12 @@ struct CsrView {
   const double* val;
   const double* diag;
   int maxrow;  // most off-diagonals in one row (<= kMaxNnzRow: a fixed slot count)
+  // the same rows in 4 aligned slots (the assembly's ELL copy where every
+  // row has <= 4 off-diagonals; null otherwise): a row's columns one 16-B
+  // word, its values two, its entry count a byte, in the CSR order
+  const int4* ecol = nullptr;
+  const double2* eval = nullptr;
+  const uint8_t* ecnt = nullptr;
 };
 
 constexpr int kMaxNnzRow = 6;
@@ -73,12 +79,45 @@ __global__ __launch_bounds__(kBlock) void k_spmv(CsrView A, const double* __rest
   y[i] = csr_row<NS>(A, x, i);
 }
 
-// y = A x on a stream: k_spmv at the rows' slot count, one row per thread
+// Row i of the ELL copy: no row pointers, one 16-B column load and two 16-B
+// value loads, the once-read streams (columns, values, count, diagonal)
+// nontemporal; the same products added in the same order as csr_row (bitwise
+// dsprsax).  Against the CSR row: 0.188 vs 0.241 ms at L = 4096
+// (tools/spmv_bench.hip, profiles/r5_6_spmv_bench_L4096.txt; the CSR row
+// with nontemporal streams 0.315)
+typedef int perc_iv4 __attribute__((ext_vector_type(4)));
+typedef double perc_dv2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ double ell_row(const CsrView& A, const double* __restrict__ x, int i) {
+  const perc_iv4 c = __builtin_nontemporal_load(reinterpret_cast<const perc_iv4*>(A.ecol) + i);
+  const perc_dv2 v0 = __builtin_nontemporal_load(reinterpret_cast<const perc_dv2*>(A.eval) + 2 * i);
+  const perc_dv2 v1 = __builtin_nontemporal_load(reinterpret_cast<const perc_dv2*>(A.eval) + 2 * i + 1);
+  const double di = __builtin_nontemporal_load(A.diag + i);
+  const int n = __builtin_nontemporal_load(A.ecnt + i);
+  const double xi = x[i];
+  const double x0 = x[c.x], x1 = x[c.y], x2 = x[c.z], x3 = x[c.w];
+  double acc = di * xi;
+  acc = 0 < n ? acc + v0.x * x0 : acc;
+  acc = 1 < n ? acc + v0.y * x1 : acc;
+  acc = 2 < n ? acc + v1.x * x2 : acc;
+  acc = 3 < n ? acc + v1.y * x3 : acc;
+  return acc;
+}
+
+__global__ __launch_bounds__(kBlock) void k_spmv_ell(CsrView A, const double* __restrict__ x,
+                                                     double* __restrict__ y) {
+  const int i = blockIdx.x * kBlock + threadIdx.x;
+  if (i >= A.N) return;
+  __builtin_nontemporal_store(ell_row(A, x, i), y + i);
+}
+
+// y = A x on a stream: the ELL copy where there is one, else k_spmv at the
+// rows' slot count, one row per thread
 inline void spmv_launch(perc_ctx* h, const CsrView& A, const double* x, double* y, hipStream_t st) {
   (void)h;
   const int ns = csr_slots(A.maxrow), grid = cdiv(A.N, kBlock);
   if (A.N <= 0) return;
-  if (ns == 4) k_spmv<4><<<grid, kBlock, 0, st>>>(A, x, y);
+  if (ns == 4 && A.ecol) k_spmv_ell<<<grid, kBlock, 0, st>>>(A, x, y);
+  else if (ns == 4) k_spmv<4><<<grid, kBlock, 0, st>>>(A, x, y);
   else if (ns == kMaxNnzRow) k_spmv<kMaxNnzRow><<<grid, kBlock, 0, st>>>(A, x, y);
   else k_spmv<0><<<grid, kBlock, 0, st>>>(A, x, y);
 }

@@ -96,6 +96,9 @@ struct DeviceBuffers {
   uint8_t* top = nullptr;    // t+1 (spanning-root flags, m+1 used)
   int* counters = nullptr;   // [0]=nspan [1]=nclusters [2]=span_sites [3]=max size, then list
   int* csize = nullptr;      // t+2 per-root cluster sizes (perc_cluster_sizes)
+  int4* ell_col = nullptr;     // N: the CSR rows in 4 aligned slots (rows of <= 4 off-diagonals)
+  double2* ell_val = nullptr;  // 2N
+  uint8_t* ell_cnt = nullptr;  // N
   int* ccpart = nullptr;     // the wave tiles' member roots per block, then minus the merge's hooks per workgroup
   StencilForms* forms_dev = nullptr;  // device copy of perc_ctx::forms (k_assemble)
   unsigned* sel_hist = nullptr;  // perc_occupy_random's select, per draw: [0] keys below, [1] in window, [2] window valid, [4 ..] bins
@@ -170,6 +173,7 @@ struct perc_ctx {
   bool bf_open_sq = false; // and the open lattice's top row follows (bf_open_square)
   bool flat = true;        // parent[] holds final roots (dev_flatten after a labeling)
   bool csr_ok = true;    // the CSR values / diagonal of the assembled system are written
+  bool ell_ok = false;   // ... and their ELL copy (d.ell_*)
   perc::AsmParams asm_p; // the assembly's parameters (ensure_csr re-runs it)
   int span_root = 0;
   int perccln = 0;

@@ -125,7 +125,8 @@ void launch_cg_spmv(perc_ctx* h, const CGArgs& a, int G) {
   } else if (!h->stencil) {
     // CSR: one row per thread (k_spmv's row) and the q.p partials
     const int ns = csr_slots(a.A.maxrow), GR = h->row_grid;
-    if (ns == 4) klaunch(h, k_cg_spmv_row<4>, GR, kBlock, h->stream, a);
+    if (ns == 4 && a.A.ecol) klaunch(h, k_cg_spmv_row<-1>, GR, kBlock, h->stream, a);
+    else if (ns == 4) klaunch(h, k_cg_spmv_row<4>, GR, kBlock, h->stream, a);
     else if (ns == kMaxNnzRow) klaunch(h, k_cg_spmv_row<kMaxNnzRow>, GR, kBlock, h->stream, a);
     else klaunch(h, k_cg_spmv_row<0>, GR, kBlock, h->stream, a);
   }
@@ -332,7 +333,8 @@ void dev_free_all(perc_ctx* h) {
                   d.order, d.parent, d.member, d.top, d.counters, d.x, d.r,
                   d.p0, d.p1, d.q, d.partials, d.tickets, d.scal, d.err_hist, d.iout,
                   d.res_xch, d.res_bar, d.bw, d.code_sm, d.csize, d.res_gran, (void*)d.nib_sm,
-                  d.sel_hist, d.sel_cand, d.mgran, d.forms_dev, d.lit, d.ccpart};
+                  d.sel_hist, d.sel_cand, d.mgran, d.forms_dev, d.lit, d.ccpart, d.ell_col, d.ell_val,
+                  d.ell_cnt};
   for (void* p : ptrs)
     if (p) hipFree(p);
   d = DeviceBuffers{};

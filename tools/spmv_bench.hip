@@ -287,6 +287,11 @@ int main(int argc, char** argv) {
   Ell E{reinterpret_cast<const int4*>(dec), reinterpret_cast<const double2*>(dev), den, ddiag, N};
   check("4-slot rows (ELL), 16-B loads", time_ms([&]() { k_spmv_ell<false><<<Gf, kBlock>>>(E, dx, dy2); }, reps));
   check("4-slot rows (ELL), nt streams", time_ms([&]() { k_spmv_ell<true><<<Gf, kBlock>>>(E, dx, dy2); }, reps));
+  CsrView AE = A;  // the production launcher given the assembly's ELL copy
+  AE.ecol = E.col;
+  AE.eval = E.val;
+  AE.ecnt = den;
+  check("production, ELL copy (spmv_launch)", time_ms([&]() { spmv_launch(&h, AE, dx, dy2, 0); }, reps));
   std::printf("  (ELL moves %.1f MB per launch: 4 slots x 12 B + count 1 B + diag, x, y 24 B per row)\n",
               (49.0 + 24.0) * N / 1e6);
   return 0;
