@@ -325,18 +325,18 @@ __device__ __forceinline__ int bf_open_square(const Geom& g, int row, int col) {
 // version with branchy per-row loads (each waited for at once), volatile
 // LDS entries, fences and provisional parents: tile 91.7 vs 123.8 us at
 // L = 4096 (profiles/r4_13_cc_bench_L4096.txt).
-// WL (word loads): a row's bond flags (2 B per site, the top row 1 B) and
-// site flags (1 B per site) are each loaded as one 8-B word per lane at the
-// 4-B-aligned address below the row's first byte (overlapping words:
-// lane l holds aligned words l and l + 1), realigned with v_alignbyte, and
-// spread to the owning lanes by shuffles -- 1 or 2 memory instructions per
-// row instead of 4 (bond) or 10 (mixed) byte loads.  A site's up link then
-// carries O(row) only; O(row + 1) is applied when the next row is walked.
+// BAL: the left-link and deduplication tests from ballots of the row's
+// right links and vertical unions -- 64-bit scalar masks (a lane's left
+// neighbour in the row is bit lane - 1; lane 0's h = 1 site follows lane
+// 63's h = 0 one) instead of LDS shuffles -- and each lane's (up to two)
+// unions in one loop.  A lane skips its union when its column and the one
+// to its left share their run in this row (a right link) and in the row
+// below, and that column unites too: the same pair of runs.
 // ncl (site and mixed kinds, whose member flag the tile sees whole): the
 // block's member roots written to ncl[block]; the merge's hooks subtract
 // from that count (k_span_top sums both), so no pass over every parent
 // counts the clusters
-template <int H, int KIND, int D = 2, bool WL = false>  // D: rows whose loads are in flight
+template <int H, int KIND, int D = 2, bool BAL = false>  // D: rows whose loads are in flight
 __global__ __launch_bounds__(64) void k_cc_tile_w(Geom g, const uint8_t* bocc, const uint8_t* socc, int* parent,
                                                   uint8_t* member, unsigned nb_bytes, int* ncl = nullptr) {
   static_assert(H <= 32, "member flags: a row per bit of one word");
@@ -386,95 +386,45 @@ __global__ __launch_bounds__(64) void k_cc_tile_w(Geom g, const uint8_t* bocc, c
       }
     }
   };
-  // WL: the words of row r (B: bond flags, S: site flags), and their
-  // decoding into the lane's two sites at consumption
-  auto load_words = [&](int r, unsigned long long& B, unsigned long long& S) {
-    const int row = r0 + r;
-    const bool ok = r < th;
-    if constexpr (KIND != PERC_SITE) {
-      const unsigned b0 = (unsigned)bf_open_square(g, row, c0) & ~3u;
-      B = __builtin_bit_cast(unsigned long long,
-                             __builtin_amdgcn_raw_buffer_load_b64(rb, (int)(ok ? b0 + 4u * lane : kOOB), 0, 0));
-    }
-    if constexpr (KIND != PERC_BOND) {
-      const unsigned s0 = (unsigned)(row * g.m + c0 + 1) & ~3u;
-      S = __builtin_bit_cast(unsigned long long, __builtin_amdgcn_raw_buffer_load_b64(
-                                                     rs, (int)(ok && lane <= 32 ? s0 + 4u * lane : kOOB), 0, 0));
-    }
-  };
-  auto decode = [&](int r, unsigned long long B, unsigned long long S, unsigned (&R)[2], unsigned (&U)[2],
-                    unsigned (&O)[2]) {
-    const int row = r0 + r;
-    unsigned os[2] = {1u, 1u}, osr[2] = {1u, 1u};
-    if constexpr (KIND != PERC_BOND) {
-      const unsigned sh = (unsigned)(row * g.m + c0 + 1) & 3u;
-      const unsigned d = __builtin_amdgcn_alignbyte((unsigned)(S >> 32), (unsigned)S, sh);
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const int c = lane + 64 * h;
-        os[h] = ((unsigned)__shfl((int)d, c >> 2, 64) >> (8 * (c & 3))) & 0xffu;
-        osr[h] = ((unsigned)__shfl((int)d, (c + 1) >> 2, 64) >> (8 * ((c + 1) & 3))) & 0xffu;
-      }
-    }
-    unsigned rb_[2] = {1u, 1u}, ub_[2] = {1u, 1u};
-    if constexpr (KIND != PERC_SITE) {
-      const bool top = row == g.n - 1;  // (uniform) 1 B per site: right links only
-      const unsigned sh = (unsigned)bf_open_square(g, row, c0) & 3u;
-      const unsigned d = __builtin_amdgcn_alignbyte((unsigned)(B >> 32), (unsigned)B, sh);
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const int c = lane + 64 * h, k = top ? c : 2 * c;
-        const unsigned x = (unsigned)__shfl((int)d, k >> 2, 64) >> (8 * (k & 3));
-        rb_[h] = x & 0xffu;
-        ub_[h] = top ? 0u : (x >> 8) & 0xffu;
-        if (c0 + c == g.m - 1) {  // the last column: its up link only
-          ub_[h] = rb_[h];
-          rb_[h] = 0u;
-        }
-      }
-    }
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int lc = lane + 64 * h, col = c0 + lc;
-      const bool v = lc < tw && r < th;
-      const bool hr = v && col < g.m - 1, hu = v && row < g.n - 1;
-      O[h] = v ? os[h] : 0u;
-      R[h] = hr ? rb_[h] & osr[h] : 0u;
-      U[h] = hu ? ub_[h] : 0u;
-    }
-  };
   unsigned Rq[D][2], Uq[D][2], Oq[D][2], R[2], U[2], O[2], Up[2] = {0u, 0u};
-  unsigned long long Bq[D], Sq[D];
   int labp[2] = {0, 0};
   unsigned nodes[H], Mb[2] = {0u, 0u};
 #pragma unroll
-  for (int d = 0; d < D; ++d) {
-    if constexpr (WL) load_words(d, Bq[d], Sq[d]);
-    else load_row(d, Rq[d], Uq[d], Oq[d]);
-  }
+  for (int d = 0; d < D; ++d) load_row(d, Rq[d], Uq[d], Oq[d]);
   const unsigned long long le = lane == 63 ? ~0ull : ((2ull << lane) - 1ull);
   const bool v0 = lane < tw, v1 = lane + 64 < tw;
+  const unsigned long long vm0 = __ballot(v0), vm1 = __ballot(v1);
+  unsigned long long lmp0 = 0, lmp1 = 0;  // BAL: the row below's left-link masks
 #pragma unroll
   for (int r = 0; r < H; ++r) {
     nodes[r] = 0u;
     if (r >= th) continue;  // (uniform)
-    if constexpr (WL) {
-      decode(r, Bq[r % D], Sq[r % D], R, U, O);
-      finish(R, U, O);
-      load_words(r + D, Bq[r % D], Sq[r % D]);  // (past th: nothing loaded)
-    } else {
 #pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        R[h] = Rq[r % D][h];
-        U[h] = Uq[r % D][h];
-        O[h] = Oq[r % D][h];
-      }
-      finish(R, U, O);
-      load_row(r + D, Rq[r % D], Uq[r % D], Oq[r % D]);  // (past th: nothing loaded)
+    for (int h = 0; h < 2; ++h) {
+      R[h] = Rq[r % D][h];
+      U[h] = Uq[r % D][h];
+      O[h] = Oq[r % D][h];
     }
-    const unsigned rl0 = __shfl(R[0], (lane + 63) & 63, 64), rl1 = __shfl(R[1], (lane + 63) & 63, 64);
-    const bool left0 = lane > 0 && rl0, left1 = lane > 0 ? rl1 != 0u : rl0 != 0u;
-    const unsigned long long lo = __ballot(!left0 || !v0), hi = __ballot(!left1 || !v1);
+    finish(R, U, O);
+    load_row(r + D, Rq[r % D], Uq[r % D], Oq[r % D]);  // (past th: nothing loaded)
+    bool left0, left1;
+    unsigned long long lo, hi, lm0 = 0, lm1 = 0;
+    if constexpr (BAL) {
+      // the columns whose left neighbour links to them in this row
+      const unsigned long long rb0 = __ballot(R[0] != 0u), rb1 = __ballot(R[1] != 0u);
+      lm0 = rb0 << 1;
+      lm1 = rb1 << 1 | rb0 >> 63;
+      left0 = (lm0 >> lane) & 1ull;
+      left1 = (lm1 >> lane) & 1ull;
+      lo = ~(lm0 & vm0);
+      hi = ~(lm1 & vm1);
+    } else {
+      const unsigned rl0 = __shfl(R[0], (lane + 63) & 63, 64), rl1 = __shfl(R[1], (lane + 63) & 63, 64);
+      left0 = lane > 0 && rl0;
+      left1 = lane > 0 ? rl1 != 0u : rl0 != 0u;
+      lo = __ballot(!left0 || !v0);
+      hi = __ballot(!left1 || !v1);
+    }
     int node[2];
     node[0] = r * kCcW + 63 - __clzll((long long)(lo & le));
     const unsigned long long hm = hi & le;
@@ -482,26 +432,58 @@ __global__ __launch_bounds__(64) void k_cc_tile_w(Geom g, const uint8_t* bocc, c
     if (v0 && !left0) uf.set(node[0], node[0]);
     if (v1 && !left1) uf.set(node[1], node[1]);
     wave_lds_order();
-    // (WL: the up link of the row below still needs this row's site)
-    const bool w0 = r > 0 && v0 && Up[0] && (!WL || O[0]), w1 = r > 0 && v1 && Up[1] && (!WL || O[1]);
+    const bool w0 = r > 0 && v0 && Up[0], w1 = r > 0 && v1 && Up[1];
     const int a0 = w0 ? node[0] : -1, b0 = w0 ? labp[0] : -1, a1 = w1 ? node[1] : -1, b1 = w1 ? labp[1] : -1;
-    const int pa0 = __shfl(a0, (lane + 63) & 63, 64), pb0 = __shfl(b0, (lane + 63) & 63, 64);
-    const int pa1 = __shfl(a1, (lane + 63) & 63, 64), pb1 = __shfl(b1, (lane + 63) & 63, 64);
-    const bool sk0 = lane > 0 && pa0 == a0 && pb0 == b0;
-    const bool sk1 = lane > 0 ? (pa1 == a1 && pb1 == b1) : (pa0 == a1 && pb0 == b1);
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const bool w = h ? w1 && !sk1 : w0 && !sk0;
-      if (!w) continue;
-      int a = h ? a1 : a0, b = h ? b1 : b0;
-      while (true) {
+    if constexpr (BAL) {
+      const unsigned long long wb0 = __ballot(w0), wb1 = __ballot(w1);
+      const unsigned long long sm0 = lm0 & lmp0 & wb0 << 1, sm1 = lm1 & lmp1 & (wb1 << 1 | wb0 >> 63);
+      bool more = w1 && !((sm1 >> lane) & 1ull);
+      bool act = w0 && !((sm0 >> lane) & 1ull);
+      int a = a0, b = b0;
+      if (!act && more) {
+        a = a1;
+        b = b1;
+        act = true;
+        more = false;
+      }
+      while (act) {  // the lane's unions, one after the other, in one loop
         a = uf.find(a);
         b = uf.find(b);
-        if (a == b) break;
-        if (a < b) { const int t = a; a = b; b = t; }
-        const int old = uf.cas(a, b);
-        if (old == a) break;
-        a = old;
+        bool done = a == b;
+        if (!done) {
+          if (a < b) { const int t = a; a = b; b = t; }
+          const int old = uf.cas(a, b);
+          done = old == a;
+          a = old;
+        }
+        if (done) {
+          act = more;
+          more = false;
+          a = a1;
+          b = b1;
+        }
+      }
+      lmp0 = lm0;
+      lmp1 = lm1;
+    } else {
+      const int pa0 = __shfl(a0, (lane + 63) & 63, 64), pb0 = __shfl(b0, (lane + 63) & 63, 64);
+      const int pa1 = __shfl(a1, (lane + 63) & 63, 64), pb1 = __shfl(b1, (lane + 63) & 63, 64);
+      const bool sk0 = lane > 0 && pa0 == a0 && pb0 == b0;
+      const bool sk1 = lane > 0 ? (pa1 == a1 && pb1 == b1) : (pa0 == a1 && pb0 == b1);
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const bool w = h ? w1 && !sk1 : w0 && !sk0;
+        if (!w) continue;
+        int a = h ? a1 : a0, b = h ? b1 : b0;
+        while (true) {
+          a = uf.find(a);
+          b = uf.find(b);
+          if (a == b) break;
+          if (a < b) { const int t = a; a = b; b = t; }
+          const int old = uf.cas(a, b);
+          if (old == a) break;
+          a = old;
+        }
       }
     }
     wave_lds_order();

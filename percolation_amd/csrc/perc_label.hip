@@ -268,6 +268,15 @@ __global__ __launch_bounds__(1024) void k_span_top(Geom g, const int* parent,
   for (int c = threadIdx.x; c <= m; c += 1024) flag[c] = 0;
   if (threadIdx.x == 0) s_base = 0;
   __syncthreads();
+  // the cluster count's partials (npart > 0) loaded first, in flight
+  // while the chains below are walked: up to kPartU per thread
+  constexpr int kPartU = 64;
+  int pv[kPartU];
+#pragma unroll
+  for (int u = 0; u < kPartU; ++u) {
+    const int i = (int)threadIdx.x + 1024 * u;
+    pv[u] = i < npart ? part[i] : 0;
+  }
   // the top row's chains (parents may not be flattened yet: dev_flatten),
   // a thread's U sites chased in lockstep: every hop issues their U parent
   // loads together (one site after another: 33 us per labeling at m = 8192)
@@ -320,13 +329,9 @@ __global__ __launch_bounds__(1024) void k_span_top(Geom g, const int* parent,
   if (threadIdx.x == 0) counters[0] = s_base;
   if (npart > 0) {  // (uniform)
     int v = 0;
-    for (int i0 = threadIdx.x; i0 < npart; i0 += 1024 * 8) {
-      int pv[8];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) pv[u] = i0 + 1024 * u < npart ? part[i0 + 1024 * u] : 0;
-#pragma unroll
-      for (int u = 0; u < 8; ++u) v += pv[u];
-    }
+    for (int u = 0; u < kPartU; ++u) v += pv[u];
+    for (int i = (int)threadIdx.x + 1024 * kPartU; i < npart; i += 1024) v += part[i];  // (past 64 K partials)
     v = wave_sum_int(v);
     __syncthreads();
     if (lane == 0) s_w[wid] = v;

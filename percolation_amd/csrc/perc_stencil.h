@@ -87,6 +87,10 @@ __device__ __forceinline__ double div_tab_core(double a, double2 dy) {
   return rem == 0.0 ? q : __builtin_fma(rem, dy.y, q);
 }
 __device__ __forceinline__ double div_tab(double a, double2 dy) {
+#ifdef PERC_DIV_G  // A/B probe builds only: the plain guard
+  if (__builtin_expect(fabs(a) < 0x1p-960, 0)) return a / dy.x;
+  return div_tab_core(a, dy);
+#endif
   if (__builtin_expect(fabs(a) < 0x1p-960, 0)) {
     const double rs = div_tab_core(a * 0x1p512, dy) * 0x1p-512;
     return fabs(rs) < 0x1p-1022 && rs != 0.0 ? a / dy.x : rs;

@@ -192,12 +192,8 @@ int main(int argc, char** argv) {
   };
   using I16 = std::integral_constant<int, 16>;
   chain("wave 128 x 16 (production)", wave(I16{}, std::integral_constant<int, 2>{}), merge_for(I16{}), false);
-  chain("wave 16, word loads", [&]() {
+  chain("wave 16, ballots", [&]() {
     k_cc_tile_w<16, PERC_BOND, 2, true><<<cdiv(g.m, kCcW) * cdiv(g.n, 16), 64>>>(g, R.bocc, R.socc, R.parent,
-                                                                                 R.member, (unsigned)nb + 8u);
-  }, merge_for(I16{}), false);
-  chain("wave 16, word loads, D 3", [&]() {
-    k_cc_tile_w<16, PERC_BOND, 3, true><<<cdiv(g.m, kCcW) * cdiv(g.n, 16), 64>>>(g, R.bocc, R.socc, R.parent,
                                                                                  R.member, (unsigned)nb + 8u);
   }, merge_for(I16{}), false);
   chain("wave 128 x 16, 4 rows in flight", wave(I16{}, std::integral_constant<int, 4>{}), merge_for(I16{}), false);
@@ -220,9 +216,8 @@ int main(int argc, char** argv) {
     std::vector<uint8_t> so((size_t)g.t + 2, 0);
     for (int st = 1; st <= g.t; ++st) so[st] = hash32((unsigned long long)st * 0xD1B54A32D192ED03ull + 777) < 0xCCCCCCCCu;
     CK(hipMemcpy(R.socc, so.data(), so.size(), hipMemcpyHostToDevice));
-    // the 16-row wave tiles of each kind (byte loads, the production; word
-    // loads), element by element against the 16-row LDS-free reference
-    // below and timed alone
+    // the 16-row wave tiles of each kind (the production; ballots), element
+    // by element against the production tile and timed alone
     const int G16 = cdiv(g.m, kCcW) * cdiv(g.n, 16);
     auto wk = [&](auto kc, auto wl) {
       constexpr int K = decltype(kc)::value;
@@ -252,8 +247,8 @@ int main(int argc, char** argv) {
       const double tb = kind == PERC_SITE ? time_ms(wk(KS{}, WF{}), reps) : time_ms(wk(KM{}, WF{}), reps);
       CK(hipMemset(R.parent, 0, ((size_t)g.t + 2) * 4));
       const double tw = kind == PERC_SITE ? time_ms(wk(KS{}, WT{}), reps) : time_ms(wk(KM{}, WT{}), reps);
-      if (same(R, kind == PERC_SITE ? "wave 16 word loads, site" : "wave 16 word loads, mixed"))
-        std::printf("  tile 16 rows, %s kind: byte loads %.1f us, word loads %.1f us\n",
+      if (same(R, kind == PERC_SITE ? "wave 16 ballots, site" : "wave 16 ballots, mixed"))
+        std::printf("  tile 16 rows, %s kind: production %.1f us, ballots %.1f us\n",
                     kind == PERC_SITE ? "site" : "mixed", tb * 1e3, tw * 1e3);
     }
   }
