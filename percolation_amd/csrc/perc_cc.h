@@ -617,6 +617,76 @@ __global__ __launch_bounds__(kCcThreads) void k_cc_merge(Geom g, int kind, const
   }
 }
 
+// The open square lattice's merge (after k_cc_tile_w<TH>): only its two
+// crossing link kinds, bond ids in closed form (bf_open_square), no
+// neighbour lists.  Part A, the block-top rows, one workgroup per kCcThreads
+// columns: every column's up link, and a block's last column's right link;
+// part B, the blocks' last columns (c = 128 k + 127 < m - 1) of the other
+// rows: the right link (the generic merge also walked the blocks' first
+// columns, which have no forward crossing link here).  Unions deduplicated
+// over the wave as in k_cc_merge; nhook as there.
+template <int TH, int KIND>
+__global__ __launch_bounds__(kCcThreads) void k_cc_merge_sq(Geom g, const uint8_t* bocc, const uint8_t* socc,
+                                                            int* parent, uint8_t* member, int nseg, int nfull,
+                                                            int* nhook) {
+  const int lane = threadIdx.x & 63;
+  const bool partA = (int)blockIdx.x < nfull * nseg;
+  int row, c;
+  if (partA) {
+    row = (blockIdx.x / nseg) * TH + TH - 1;
+    c = (blockIdx.x % nseg) * kCcThreads + threadIdx.x;
+  } else {
+    const int e = blockIdx.x - nfull * nseg, nrb = cdiv(g.n, kCcThreads);
+    c = (e / nrb) * kCcW + kCcW - 1;
+    row = (e % nrb) * kCcThreads + threadIdx.x;
+    if (row % TH == TH - 1) row = g.n;  // (part A's)
+  }
+  const bool site = row < g.n && c < g.m;
+  const int s = row * g.m + c + 1;
+  const bool so = site && (KIND == PERC_BOND || socc[s]);
+  int hooks = 0;
+  // link 0: up (part A); link 1: right (part B, and part A's block-last columns)
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    if (k == 0 && !partA) continue;  // (uniform)
+    const bool exists = k == 0 ? row < g.n - 1 : (c % kCcW == kCcW - 1 && c < g.m - 1);
+    const int q = k == 0 ? s + g.m : s + 1;
+    bool want = so && exists;
+    if (want) {
+      const int fb = bf_open_square(g, row, c);
+      const int id = k == 0 ? fb + (c < g.m - 1 ? 1 : 0) : fb;
+      if constexpr (KIND == PERC_BOND) want = bocc[id] != 0;
+      else if constexpr (KIND == PERC_SITE) want = socc[q] != 0;
+      else want = bocc[id] != 0 && socc[q] != 0;
+    }
+    if (want && KIND == PERC_BOND) member[q] = 1;
+    const int a = want ? parent[s] : -1, b = want ? parent[q] : -1;
+    const int lo = min(a, b), hi = max(a, b);
+    bool lead = want && lo != hi;
+    unsigned long long act = __ballot(lead);
+    while (act) {
+      const int l = __builtin_ctzll(act);
+      const int la = __shfl(lo, l, 64), lh = __shfl(hi, l, 64);
+      const bool same = lead && lo == la && hi == lh;
+      act &= ~__ballot(same);
+      if (same && lane != l) lead = false;
+    }
+    if (lead) hooks += unite(parent, lo, hi) ? 1 : 0;
+  }
+  if (nhook) {  // (uniform)
+    __shared__ int s_h[kCcThreads / 64];
+    hooks = wave_sum_int(hooks);
+    if (lane == 0) s_h[threadIdx.x >> 6] = hooks;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      int tot = 0;
+#pragma unroll
+      for (int w = 0; w < kCcThreads / 64; ++w) tot += s_h[w];
+      nhook[blockIdx.x] = -tot;
+    }
+  }
+}
+
 // sum of v over the workgroup of kCcThreads, then one atomic add
 __device__ __forceinline__ void block_count_add(int v, int* counter) {
   __shared__ int s_cnt[kCcThreads / 64];

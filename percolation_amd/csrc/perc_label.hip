@@ -534,9 +534,12 @@ hipError_t dev_label(perc_ctx* h, int* nspan, int* span_list, int* nclusters) {
       part = d.ccpart;
     }
     if (kind == PERC_BOND) k_cc_tile_w<H, PERC_BOND><<<G, 64, 0, st>>>(g, d.bocc, d.socc, d.parent, d.member, nbb);
+    // (site and mixed kinds: the ballot-mask walk, 95.6 vs 103.8 us mixed at
+    // L = 4096, 273.7 vs 298.5 at 8192; the bond kind's is 2 % slower with
+    // it, profiles/r5_10_cc_bench_L*.txt)
     else if (kind == PERC_SITE)
-      k_cc_tile_w<H, PERC_SITE><<<G, 64, 0, st>>>(g, d.bocc, d.socc, d.parent, d.member, nbb, part);
-    else k_cc_tile_w<H, PERC_SITEBOND><<<G, 64, 0, st>>>(g, d.bocc, d.socc, d.parent, d.member, nbb, part);
+      k_cc_tile_w<H, PERC_SITE, 2, true><<<G, 64, 0, st>>>(g, d.bocc, d.socc, d.parent, d.member, nbb, part);
+    else k_cc_tile_w<H, PERC_SITEBOND, 2, true><<<G, 64, 0, st>>>(g, d.bocc, d.socc, d.parent, d.member, nbb, part);
     HIP_TRY(dbg_sync(st, "k_cc_tile_w"));
     k_cc_merge<H><<<GM, kCcThreads, 0, st>>>(g, kind, d.bond_first, d.bocc, d.socc, d.parent, d.member, nseg, nfull,
                                              part ? part + G : nullptr);

@@ -517,7 +517,7 @@ __global__ __launch_bounds__(NT) void k_cg_res(ResArgs a) {
       for (int j = 0; j < MT; ++j) {
         if (lr < Hw && tin) {
           const int e = lr * m + t + j * NT;
-          const double z = div_tab_g(rv[lr][j], s_dt[diag_idx(code_at(lr, j))]);
+          const double z = div_tab(rv[lr][j], s_dt[diag_idx(code_at(lr, j))]);
           s_p[e] = k == 1 ? z : bk * s_p[e] + z;
         }
         if constexpr (!QREG) __builtin_amdgcn_sched_barrier(0);
@@ -533,8 +533,8 @@ __global__ __launch_bounds__(NT) void k_cg_res(ResArgs a) {
           u3[d] = d3[d] = 0.0;
           continue;
         }
-        const double zu = div_tab_g(hur[j][d], s_dt[diag_idx(hcu[j][d])]);
-        const double zd = div_tab_g(hdr[j][d], s_dt[diag_idx(hcd[j][d])]);
+        const double zu = div_tab(hur[j][d], s_dt[diag_idx(hcu[j][d])]);
+        const double zd = div_tab(hdr[j][d], s_dt[diag_idx(hcd[j][d])]);
         u3[d] = has_up && hin(j, d) ? (k == 1 ? zu : bk * hup[j][d] + zu) : 0.0;
         d3[d] = has_dn && hin(j, d) ? (k == 1 ? zd : bk * hdp[j][d] + zd) : 0.0;
       }
@@ -624,7 +624,7 @@ __global__ __launch_bounds__(NT) void k_cg_res(ResArgs a) {
           else qq = qcalc(lr, j, s_p[lr * m + c]);
           const double rn = rv[lr][j] - ak * qq;
           rv[lr][j] = rn;
-          const double z = div_tab_g(rn, s_dt[diag_idx(code_at(lr, j))]);
+          const double z = div_tab(rn, s_dt[diag_idx(code_at(lr, j))]);
           const double tz = z * rn, tr = rn * rn;  // bknum's, snrm's terms
           acc2[0] = acc2[0] + tz;
           acc2[1] = acc2[1] + tr;

@@ -70,15 +70,6 @@ __global__ void k_fill_dtab(double2* dtab, double ng0, double nleak) {
 // late in long solves (config 2 at tol 1e-8 left the reference's literal
 // iterates after iteration 3000 without this; a CPU sweep of 2e8 pairs
 // near underflow: 246 975 mismatches unguarded, none guarded).
-// Round 5: the guarded branch no longer runs the IEEE division sequence
-// (~15 fp64 operations, taken by a whole wave when one lane's r is tiny --
-// the mixed lattice's many isolated sites made that frequent late in its
-// solves): a is scaled by 2^512 (exact), divided by the table (its
-// remainder is then far from underflow), and the quotient scaled back by
-// 2^-512 -- exact while the quotient is a normal number, so the result is
-// still the correctly rounded a / d; only a subnormal quotient (|a| below
-// ~2^-1020 d) takes `/`.  Zero numerators (|a| < 2^-960 too) come out as
-// q = a y = +-0, the sign IEEE division gives (d > 0).
 __device__ __forceinline__ double div_tab_core(double a, double2 dy) {
   const double q = a * dy.y;
   const double rem = __builtin_fma(-q, dy.x, a);
@@ -86,21 +77,14 @@ __device__ __forceinline__ double div_tab_core(double a, double2 dy) {
   // q + rem y would turn into +0)
   return rem == 0.0 ? q : __builtin_fma(rem, dy.y, q);
 }
+// Below |a| = 2^-960 the remainder a - q d may leave the normal range, so
+// the IEEE division is taken there (late in long solves the r of isolated,
+// leak-coupled sites decays that far).  A cheaper exact branch for that
+// range -- the numerator scaled by 2^512, divided by the table, scaled back
+// -- was compiled as predicated straight-line code and cost every element:
+// the march P 0.102 vs 0.077 ms, the solve 0.1572 vs 0.1489 ms per
+// iteration at L = 4096 (profiles/r5_10_ab_division_L4096.json); removed.
 __device__ __forceinline__ double div_tab(double a, double2 dy) {
-#ifdef PERC_DIV_G  // A/B probe builds only: the plain guard
-  if (__builtin_expect(fabs(a) < 0x1p-960, 0)) return a / dy.x;
-  return div_tab_core(a, dy);
-#endif
-  if (__builtin_expect(fabs(a) < 0x1p-960, 0)) {
-    const double rs = div_tab_core(a * 0x1p512, dy) * 0x1p-512;
-    return fabs(rs) < 0x1p-1022 && rs != 0.0 ? a / dy.x : rs;
-  }
-  return div_tab_core(a, dy);
-}
-// the same quotient with the plain guard (`/` below 2^-960): the resident
-// solve's register-bound loops keep it (the scaled branch costs them 3
-// VGPRs and 16-24 B of spills at m = 2048)
-__device__ __forceinline__ double div_tab_g(double a, double2 dy) {
   if (__builtin_expect(fabs(a) < 0x1p-960, 0)) return a / dy.x;
   return div_tab_core(a, dy);
 }

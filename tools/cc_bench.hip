@@ -192,6 +192,13 @@ int main(int argc, char** argv) {
   };
   using I16 = std::integral_constant<int, 16>;
   chain("wave 128 x 16 (production)", wave(I16{}, std::integral_constant<int, 2>{}), merge_for(I16{}), false);
+  {
+    const int nseg = cdiv(g.m, kCcThreads), nfull = g.n / 16, ntx = cdiv(g.m, kCcW);
+    const int GMs = nfull * nseg + (ntx - 1) * cdiv(g.n, kCcThreads);
+    chain("wave 16 + square merge", wave(I16{}, std::integral_constant<int, 2>{}), [&, nseg, nfull, GMs]() {
+      k_cc_merge_sq<16, PERC_BOND><<<GMs, kCcThreads>>>(g, R.bocc, R.socc, R.parent, R.member, nseg, nfull, nullptr);
+    }, false);
+  }
   chain("wave 16, ballots", [&]() {
     k_cc_tile_w<16, PERC_BOND, 2, true><<<cdiv(g.m, kCcW) * cdiv(g.n, 16), 64>>>(g, R.bocc, R.socc, R.parent,
                                                                                  R.member, (unsigned)nb + 8u);
@@ -250,6 +257,28 @@ int main(int argc, char** argv) {
       if (same(R, kind == PERC_SITE ? "wave 16 ballots, site" : "wave 16 ballots, mixed"))
         std::printf("  tile 16 rows, %s kind: production %.1f us, ballots %.1f us\n",
                     kind == PERC_SITE ? "site" : "mixed", tb * 1e3, tw * 1e3);
+      // the merges of that kind after the ballot tile: the generic one, then
+      // the square lattice's (k_cc_merge_sq), whole chains compared
+      const int nseg = cdiv(g.m, kCcThreads), nfull = g.n / 16, ntx = cdiv(g.m, kCcW);
+      const int GMg = nfull * nseg + (2 * ntx + 1) * cdiv(g.n, kCcThreads);
+      const int GMs = nfull * nseg + (ntx - 1) * cdiv(g.n, kCcThreads);
+      auto tilek = [&]() {
+        if (kind == PERC_SITE) wk(KS{}, WT{})();
+        else wk(KM{}, WT{})();
+      };
+      auto mgen = [&]() {
+        k_cc_merge<16><<<GMg, kCcThreads>>>(g, kind, R.bf, R.bocc, R.socc, R.parent, R.member, nseg, nfull);
+      };
+      auto msq = [&]() {
+        if (kind == PERC_SITE)
+          k_cc_merge_sq<16, PERC_SITE><<<GMs, kCcThreads>>>(g, R.bocc, R.socc, R.parent, R.member, nseg, nfull,
+                                                             nullptr);
+        else
+          k_cc_merge_sq<16, PERC_SITEBOND><<<GMs, kCcThreads>>>(g, R.bocc, R.socc, R.parent, R.member, nseg,
+                                                                 nfull, nullptr);
+      };
+      chain(kind == PERC_SITE ? "site: generic merge" : "mixed: generic merge", tilek, mgen, true);
+      chain(kind == PERC_SITE ? "site: square merge" : "mixed: square merge", tilek, msq, false);
     }
   }
   return 0;
