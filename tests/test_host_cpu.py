@@ -68,8 +68,10 @@ def test_one_hip_runtime_per_process(no_torch):
                        timeout=300, env=env)
     libs = eval(r.stdout.strip().splitlines()[-1])
     hip = [x for x in libs if "libamdhip64" in x]
-    if no_torch:  # the failure this guards against, shown to still exist without the guard
-        assert len(hip) == 2 and r.returncode != 0, (libs, r.returncode, r.stderr[-500:])
+    if no_torch:  # the condition this guards against, shown to still arise without the guard
+        # (two runtimes; the heap corruption they cause at teardown aborts
+        # the process most of the time, not always)
+        assert len(hip) == 2, (libs, r.returncode, r.stderr[-500:])
     else:
         assert len(hip) == 1 and len(libs) == 3, libs
         assert r.returncode == 0, r.stderr[-2000:]
