@@ -523,8 +523,8 @@ hipError_t dev_label(perc_ctx* h, int* nspan, int* span_list, int* nclusters) {
     constexpr int H = kCcWaveH;
     const int G = cdiv(g.m, kCcW) * cdiv(g.n, H);
     const unsigned nbb = (unsigned)h->nb + 8u;
-    const int nseg = cdiv(g.m, kCcThreads), nfull = g.n / H, ncand = 2 * cdiv(g.m, kCcW) + 1;
-    const int GM = nfull * nseg + ncand * cdiv(g.n, kCcThreads);
+    const int nseg = cdiv(g.m, kCcThreads), nfull = g.n / H;
+    const int GM = nfull * nseg + (cdiv(g.m, kCcW) - 1) * cdiv(g.n, kCcThreads);  // (k_cc_merge_sq's grid)
     // site and mixed kinds: the cluster count from the tiles' member roots and
     // the merge's hooks (the bond kind's member flags of a block's edge sites
     // are completed by the merge, so it counts the roots afterwards)
@@ -541,9 +541,18 @@ hipError_t dev_label(perc_ctx* h, int* nspan, int* span_list, int* nclusters) {
       k_cc_tile_w<H, PERC_SITE, 2, true><<<G, 64, 0, st>>>(g, d.bocc, d.socc, d.parent, d.member, nbb, part);
     else k_cc_tile_w<H, PERC_SITEBOND, 2, true><<<G, 64, 0, st>>>(g, d.bocc, d.socc, d.parent, d.member, nbb, part);
     HIP_TRY(dbg_sync(st, "k_cc_tile_w"));
-    k_cc_merge<H><<<GM, kCcThreads, 0, st>>>(g, kind, d.bond_first, d.bocc, d.socc, d.parent, d.member, nseg, nfull,
-                                             part ? part + G : nullptr);
-    HIP_TRY(dbg_sync(st, "k_cc_merge"));
+    // the square lattice's merge: 107 vs 163 us mixed, 153 vs 191 bond at
+    // L = 8192 (profiles/r5_11_cc_bench_L8192.txt)
+    int* hk = part ? part + G : nullptr;
+    if (GM == 0) {  // one block: nothing crosses a block edge
+    } else if (kind == PERC_BOND)
+      k_cc_merge_sq<H, PERC_BOND><<<GM, kCcThreads, 0, st>>>(g, d.bocc, d.socc, d.parent, d.member, nseg, nfull, hk);
+    else if (kind == PERC_SITE)
+      k_cc_merge_sq<H, PERC_SITE><<<GM, kCcThreads, 0, st>>>(g, d.bocc, d.socc, d.parent, d.member, nseg, nfull, hk);
+    else
+      k_cc_merge_sq<H, PERC_SITEBOND><<<GM, kCcThreads, 0, st>>>(g, d.bocc, d.socc, d.parent, d.member, nseg, nfull,
+                                                                 hk);
+    HIP_TRY(dbg_sync(st, "k_cc_merge_sq"));
     return label_finish(h, nspan, span_list, nclusters, part, part ? G + GM : 0);
   }
   const int tiles = cdiv(g.m, kCcW) * cdiv(g.n, kCcH);
