@@ -254,20 +254,24 @@ __global__ void k_occupy_sites(const int* order, int count, int t, uint8_t* socc
 // bottom row (bond: a bond with b1 <= m; site / mixed: an occupied site
 // there) iff its root is <= m; it reaches the top row (bond: b2 > t-m; site:
 // an occupied site) iff one of the m top-row sites is a member of it.  One
-// workgroup: flag[root] for the top-row members whose root is <= m, then the
-// flagged roots in ascending order (ballot compaction) -> counters[0] =
-// count, counters[8..] = the first kMaxSpanList roots.
+// workgroup: flag[root] for the top-row members whose root is <= m (flags in
+// LDS where m < kSpanLds), then the flagged roots in ascending order -- each
+// thread counts its own run of consecutive flags, one workgroup scan ->
+// counters[0] = count, counters[8..] = the first kMaxSpanList roots.  (The
+// ballot compaction over 1024-flag windows in global memory, three
+// barriers a window, cost ~10 us at m = 8192.)
 // part (npart > 0): the cluster count as the sum of the wave tiles' member
 // roots and the merge's negated hooks -> counters[1]
+constexpr int kSpanLds = 32768;
+template <bool LF>
 __global__ __launch_bounds__(1024) void k_span_top(Geom g, const int* parent,
-                                                   const uint8_t* member, uint8_t* flag,
+                                                   const uint8_t* member, uint8_t* gflag,
                                                    int* counters, const int* part, int npart) {
+  __shared__ uint8_t s_fl[LF ? kSpanLds : 1];
   __shared__ int s_w[16];
-  __shared__ int s_base;
+  uint8_t* flag = LF ? s_fl : gflag;
   const int m = g.m;
   for (int c = threadIdx.x; c <= m; c += 1024) flag[c] = 0;
-  if (threadIdx.x == 0) s_base = 0;
-  __syncthreads();
   // the cluster count's partials (npart > 0) loaded first, in flight
   // while the chains below are walked: up to kPartU per thread
   constexpr int kPartU = 64;
@@ -277,6 +281,7 @@ __global__ __launch_bounds__(1024) void k_span_top(Geom g, const int* parent,
     const int i = (int)threadIdx.x + 1024 * u;
     pv[u] = i < npart ? part[i] : 0;
   }
+  __syncthreads();
   // the top row's chains (parents may not be flattened yet: dev_flatten),
   // a thread's U sites chased in lockstep: every hop issues their U parent
   // loads together (one site after another: 33 us per labeling at m = 8192)
@@ -307,26 +312,27 @@ __global__ __launch_bounds__(1024) void k_span_top(Geom g, const int* parent,
       if (act[u] && x[u] <= m) flag[x[u]] = 1;
   }
   __syncthreads();
+  // thread t's run of flags: roots c0 .. c0 + K - 1 (1-based, <= m)
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  for (int base = 1; base <= m; base += 1024) {
-    const int c = base + threadIdx.x;
-    const bool f = c <= m && flag[c];
-    const unsigned long long b = __ballot(f);
-    if (lane == 0) s_w[wid] = __popcll(b);
-    __syncthreads();
-    int off = s_base;
-    for (int w = 0; w < wid; ++w) off += s_w[w];
-    off += __popcll(b & ((1ull << lane) - 1ull));
-    if (f && off < kMaxSpanList) counters[8 + off] = c;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      int tot = 0;
-      for (int w = 0; w < 16; ++w) tot += s_w[w];
-      s_base += tot;
-    }
-    __syncthreads();
+  const int K = cdiv(m, 1024), c0 = 1 + (int)threadIdx.x * K;
+  int cnt = 0;
+  for (int k = 0; k < K; ++k) cnt += c0 + k <= m && flag[c0 + k];
+  int inc = cnt;  // inclusive scan over the wave, then over the waves
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const int y = __shfl_up(inc, off, 64);
+    if (lane >= off) inc += y;
   }
-  if (threadIdx.x == 0) counters[0] = s_base;
+  if (lane == 63) s_w[wid] = inc;
+  __syncthreads();
+  int off = inc - cnt, tot = 0;
+  for (int w = 0; w < 16; ++w) {
+    off += w < wid ? s_w[w] : 0;
+    tot += s_w[w];
+  }
+  for (int k = 0; k < K && off < kMaxSpanList; ++k)
+    if (c0 + k <= m && flag[c0 + k]) counters[8 + off++] = c0 + k;
+  if (threadIdx.x == 0) counters[0] = tot;
   if (npart > 0) {  // (uniform)
     int v = 0;
 #pragma unroll
@@ -337,9 +343,9 @@ __global__ __launch_bounds__(1024) void k_span_top(Geom g, const int* parent,
     if (lane == 0) s_w[wid] = v;
     __syncthreads();
     if (threadIdx.x == 0) {
-      int tot = 0;
-      for (int w = 0; w < 16; ++w) tot += s_w[w];
-      counters[1] = tot;
+      int t2 = 0;
+      for (int w = 0; w < 16; ++w) t2 += s_w[w];
+      counters[1] = t2;
     }
   }
 }
@@ -603,7 +609,8 @@ static hipError_t label_finish(perc_ctx* h, int* nspan, int* span_list, int* ncl
         g.t, d.parent, d.member, d.counters + 1);
     HIP_TRY(dbg_sync(st, "k_cc_count_roots"));
   }
-  k_span_top<<<1, 1024, 0, st>>>(g, d.parent, d.member, d.top, d.counters, part, npart);
+  if (g.m < kSpanLds) k_span_top<true><<<1, 1024, 0, st>>>(g, d.parent, d.member, d.top, d.counters, part, npart);
+  else k_span_top<false><<<1, 1024, 0, st>>>(g, d.parent, d.member, d.top, d.counters, part, npart);
   HIP_TRY(dbg_sync(st, "k_span_top"));
   int hc[8 + kMaxSpanList];
   HIP_TRY(hipMemcpyAsync(hc, d.counters, sizeof(hc), hipMemcpyDeviceToHost, st));

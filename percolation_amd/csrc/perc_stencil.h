@@ -85,7 +85,9 @@ __device__ __forceinline__ double div_tab_core(double a, double2 dy) {
 // the march P 0.102 vs 0.077 ms, the solve 0.1572 vs 0.1489 ms per
 // iteration at L = 4096 (profiles/r5_10_ab_division_L4096.json); removed.
 __device__ __forceinline__ double div_tab(double a, double2 dy) {
+#ifndef PERC_DIV_NOGUARD  // (A/B probe builds only: the guard's cost, wrong below 2^-960)
   if (__builtin_expect(fabs(a) < 0x1p-960, 0)) return a / dy.x;
+#endif
   return div_tab_core(a, dy);
 }
 

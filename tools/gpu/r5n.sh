@@ -1,5 +1,6 @@
 #!/bin/bash
-# round 5, call n: what the division's tiny-numerator guard costs late in a
+# round 5, call n: the span test with LDS flags and one scan (labeling
+# tests); what the division's tiny-numerator guard costs late in a
 # solve (A/B over 20000-iteration solves against a build without it); the
 # BASELINE configs 2-5 on one GPU
 mkdir -p gpurun_out
@@ -11,6 +12,8 @@ step() {
   echo "$name rc=$rc"
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then tail -30 gpurun_out/r5n_$name.log; exit $rc; fi
 }
+step pytest 400 python -u -m pytest tests/test_labeling_oracle.py -m gpu -x -q --timeout 300 --timeout-method thread
+tail -2 gpurun_out/r5n_pytest.log
 step guard 600 python -u tools/lib_ab.py --L 4096 --libs main,noguard --iters 20000 --reps 10 --rounds 2
 tail -1 gpurun_out/r5n_guard.log
 rm -f gpurun_out/configs.log
