@@ -37,16 +37,44 @@ __host__ __device__ inline int sel_shift(unsigned long long lo, unsigned long lo
   while (bits < 64 && range > 1 && (range - 1) >> bits) ++bits;
   return bits > 12 ? bits - 12 : 0;
 }
-// cnt: [0] keys below the window, [1] keys in it, [2] window valid, [3]
-// unused, [4 ..] kSelBins bin counts of the window keys by hash; pad (the
-// first workgroup): the occupancy array's pad bytes zeroed, npad at padp
-__global__ __launch_bounds__(kBlock) void k_select_window(long long n, RandKeyCtx kc,
-                                                          unsigned long long lo,
-                                                          unsigned long long hi, int sh,
-                                                          unsigned* cnt,
-                                                          unsigned long long* cand, int base,
-                                                          uint8_t* occ, uint8_t* padp, int npad) {
-  if (blockIdx.x == 0) {  // the pads: occ[0 .. base) and npad bytes at padp
+// One draw of perc_occupy_random: n ids, the count smallest keys occupied
+// in occ[base .. base + n); the window [lo, hi) of T's hash; cnt: [0] keys
+// below the window, [1] keys in it, [2] window valid, [3] unused, [4 ..]
+// kSelBins bin counts of the window keys by hash; cand: [0] T, then the
+// window's keys; the pad bytes occ[0 .. base) and npad at padp.  The
+// site and bond draws of a mixed occupation run in one launch of each
+// kernel: draw k owns the workgroups [g0, g0 + gn) (the select: workgroup
+// k), so neither draw's tail or one-workgroup select idles the device alone.
+struct SelDraw {
+  long long n, count;
+  unsigned long long seed, lo, hi;
+  RandKeyCtx kc;
+  int sh, base, npad, g0, gn;
+  unsigned* cnt;
+  unsigned long long* cand;
+  uint8_t* occ;
+  uint8_t* padp;
+};
+struct SelDraws {
+  SelDraw d[2];
+  int nd;
+};
+// the draw of workgroup b (a draw's range starts at its g0)
+__device__ __forceinline__ SelDraw sel_draw(const SelDraws& D, int b) {
+  return D.nd == 2 && b >= D.d[1].g0 ? D.d[1] : D.d[0];
+}
+
+__global__ __launch_bounds__(kBlock) void k_select_window(SelDraws D) {
+  const SelDraw w = sel_draw(D, blockIdx.x);
+  const long long n = w.n;
+  const RandKeyCtx kc = w.kc;
+  const unsigned long long lo = w.lo, hi = w.hi;
+  const int sh = w.sh, base = w.base, npad = w.npad, bid = blockIdx.x - w.g0;
+  unsigned* cnt = w.cnt;
+  unsigned long long* cand = w.cand;
+  uint8_t* occ = w.occ;
+  if (bid == 0) {  // the pads: occ[0 .. base) and npad bytes at padp
+    uint8_t* padp = w.padp;
     if ((int)threadIdx.x < npad) padp[threadIdx.x] = 0;
     if ((int)threadIdx.x < base) occ[threadIdx.x] = 0;
   }
@@ -56,8 +84,7 @@ __global__ __launch_bounds__(kBlock) void k_select_window(long long n, RandKeyCt
   __syncthreads();
   unsigned below = 0;
   const int lane = threadIdx.x & 63;
-  for (long long i = (long long)blockIdx.x * kBlock + threadIdx.x; i < n;
-       i += (long long)gridDim.x * kBlock) {
+  for (long long i = (long long)bid * kBlock + threadIdx.x; i < n; i += (long long)w.gn * kBlock) {
     const unsigned id = (unsigned)(i + 1);
     const unsigned long long hsh = perc_rand_hash32(kc, id);  // = perc_rand_key(seed, id) >> 32
     const unsigned long long key = hsh << 32 | id;
@@ -91,13 +118,12 @@ __global__ __launch_bounds__(kBlock) void k_select_window(long long n, RandKeyCt
     if (s_base + j < (unsigned)kSelCap) cand[1 + s_base + j] = s_c[j];
 }
 
-__global__ __launch_bounds__(kSelThreads) void k_select_final(long long n,
-                                                              unsigned long long seed,
-                                                              long long count,
-                                                              unsigned long long lo,
-                                                              unsigned long long hi,
-                                                              unsigned* cnt,
-                                                              unsigned long long* cand) {
+__global__ __launch_bounds__(kSelThreads) void k_select_final(SelDraws D) {
+  const SelDraw w = blockIdx.x ? D.d[1] : D.d[0];
+  const long long n = w.n, count = w.count;
+  const unsigned long long seed = w.seed, lo = w.lo, hi = w.hi;
+  unsigned* cnt = w.cnt;
+  unsigned long long* cand = w.cand;
   __shared__ unsigned s_h[kSelBins];
   __shared__ unsigned long long s_k[kSelBinCap];
   __shared__ unsigned long long s_sel[2];  // prefix, need
@@ -225,18 +251,24 @@ __global__ __launch_bounds__(kSelThreads) void k_select_final(long long n,
 // T fell outside the window (cnt[2] == 0, rare) the whole occupation is
 // rewritten from T instead, grid-stride over all n ids (one launch either
 // way: an empty second launch cost ~5 us per draw)
-__global__ __launch_bounds__(kBlock) void k_occupy_cand(const unsigned* cnt, const unsigned long long* cand,
-                                                         int base, uint8_t* occ, long long n, RandKeyCtx kc) {
+__global__ __launch_bounds__(kBlock) void k_occupy_cand(SelDraws D) {
+  const SelDraw w = sel_draw(D, blockIdx.x);
+  const unsigned* cnt = w.cnt;
+  const unsigned long long* cand = w.cand;
+  const int base = w.base, bid = blockIdx.x - w.g0;
+  uint8_t* occ = w.occ;
+  const long long n = w.n;
+  const RandKeyCtx kc = w.kc;
   const unsigned long long T = cand[0];
   if (!cnt[2]) {
-    for (long long i = (long long)blockIdx.x * kBlock + threadIdx.x; i < n; i += (long long)gridDim.x * kBlock) {
+    for (long long i = (long long)bid * kBlock + threadIdx.x; i < n; i += (long long)w.gn * kBlock) {
       const unsigned id = (unsigned)(i + 1);
       occ[i + base] = ((unsigned long long)perc_rand_hash32(kc, id) << 32 | id) <= T ? 1 : 0;
     }
     return;
   }
   const unsigned nin = cnt[1];
-  for (unsigned j = blockIdx.x * kBlock + threadIdx.x; j < nin; j += gridDim.x * kBlock) {
+  for (unsigned j = bid * kBlock + threadIdx.x; j < nin; j += w.gn * kBlock) {
     const unsigned long long key = cand[1 + j];
     if (key <= T) occ[(long long)(key & 0xFFFFFFFFull) - 1 + base] = 1;
   }
@@ -450,14 +482,12 @@ hipError_t dev_occupy(perc_ctx* h, int kind, int nsites, const int* site_order, 
 // occupied, the others not, the window's keys gathered), the one-workgroup
 // select of T (k_select_final), then the window's keys at or below T
 // (k_occupy_cand); when T fell outside the window k_occupy_cand rewrites the
-// whole occupation from T instead.  No host
-// synchronisation.
-static hipError_t occupy_rand_one(perc_ctx* h, long long n, long long count,
-                                  unsigned long long seed, int base, uint8_t* occ, unsigned* cnt,
-                                  uint8_t* padp, int npad) {
+// whole occupation from T instead.  No host synchronisation.  A draw with
+// nothing to select (count <= 0 or >= n) is a memset.
+static hipError_t sel_prepare(perc_ctx* h, long long n, long long count, unsigned long long seed, int base,
+                              uint8_t* occ, unsigned* cnt, unsigned long long* cand, uint8_t* padp, int npad,
+                              SelDraws& D) {
   hipStream_t st = h->stream;
-  const int G = (int)std::min<long long>(cdiv(n, kBlock), 2048);
-  const RandKeyCtx kc = perc_rand_key_ctx(seed);
   if (count <= 0 || count >= n) {
     HIP_TRY(hipMemsetAsync(occ + base, count <= 0 ? 0 : 1, (size_t)n, st));
     if (base) HIP_TRY(hipMemsetAsync(occ, 0, (size_t)base, st));
@@ -472,20 +502,21 @@ static hipError_t occupy_rand_one(perc_ctx* h, long long n, long long count,
   unsigned long long hi = c + w >= two32 ? (1ull << 32) : (unsigned long long)(c + w) + 1;
   const char* full = std::getenv("PERC_SELECT_FULL");  // tests: the exact slow path
   if (full && full[0] == '1') lo = hi = 0;
-  k_select_window<<<G, kBlock, 0, st>>>(n, kc, lo, hi, sel_shift(lo, hi), cnt, h->d.sel_cand, base, occ, padp,
-                                        npad);
-  HIP_TRY(dbg_sync(st, "k_select_window"));
-  k_select_final<<<1, kSelThreads, 0, st>>>(n, seed, count, lo, hi, cnt, h->d.sel_cand);
-  HIP_TRY(dbg_sync(st, "k_select_final"));
-  if (std::getenv("PERC_SELECT_TRACE")) {
-    unsigned long long tr[6];
-    HIP_TRY(hipMemcpyAsync(tr, h->d.sel_cand + 1 + kSelCap, sizeof(tr), hipMemcpyDeviceToHost, st));
-    HIP_TRY(hipStreamSynchronize(st));
-    std::fprintf(stderr, "select trace: hist %llu bin %llu rank %llu ticks; nin %llu bin %llu\n",
-                 tr[1] - tr[0], tr[2] - tr[1], tr[3] - tr[2], tr[4], tr[5]);
-  }
-  k_occupy_cand<<<cdiv(kSelCap, kBlock), kBlock, 0, st>>>(cnt, h->d.sel_cand, base, occ, n, kc);
-  return dbg_sync(st, "k_occupy_cand");
+  SelDraw& x = D.d[D.nd++];
+  x.n = n;
+  x.count = count;
+  x.seed = seed;
+  x.lo = lo;
+  x.hi = hi;
+  x.kc = perc_rand_key_ctx(seed);
+  x.sh = sel_shift(lo, hi);
+  x.base = base;
+  x.npad = npad;
+  x.cnt = cnt;
+  x.cand = cand;
+  x.occ = occ;
+  x.padp = padp;
+  return hipSuccess;
 }
 
 hipError_t dev_occupy_random(perc_ctx* h, int kind, int nsites, int nbonds,
@@ -496,17 +527,50 @@ hipError_t dev_occupy_random(perc_ctx* h, int kind, int nsites, int nbonds,
   // written whole and their pad bytes by the draw (socc[0] and socc[t+1 ..
   // t+8) with the sites, bocc[nb .. nb+8) with the bonds); an undrawn kind
   // is zeroed whole
+  constexpr size_t kCand = (size_t)kSelCap + 1 + 16;  // per draw: T, the window keys, trace stamps
   if (!d.sel_hist) HIP_TRY(dmalloc(&d.sel_hist, 2 * kSelCnt));
-  if (!d.sel_cand) HIP_TRY(dmalloc(&d.sel_cand, (size_t)kSelCap + 1 + 16));
+  if (!d.sel_cand) HIP_TRY(dmalloc(&d.sel_cand, 2 * kCand));
   HIP_TRY(hipMemsetAsync(d.sel_hist, 0, sizeof(unsigned) * 2 * kSelCnt, st));
   if (kind == PERC_SITE) HIP_TRY(hipMemsetAsync(d.bocc, 0, (size_t)h->nb + 8, st));
   if (kind == PERC_BOND) HIP_TRY(hipMemsetAsync(d.socc, 0, h->g.t + 8, st));
+  SelDraws D{};
   if (kind != PERC_BOND)
-    HIP_TRY(occupy_rand_one(h, h->g.t, nsites, seed, 1, d.socc, d.sel_hist, d.socc + h->g.t + 1, 7));
+    HIP_TRY(sel_prepare(h, h->g.t, nsites, seed, 1, d.socc, d.sel_hist, d.sel_cand, d.socc + h->g.t + 1, 7, D));
   if (kind != PERC_SITE)
-    HIP_TRY(occupy_rand_one(h, h->nb, nbonds, perc_mix64(seed ^ 0x5DEECE66Dull), 0, d.bocc, d.sel_hist + kSelCnt,
-                            d.bocc + h->nb, 8));
-  return hipSuccess;
+    HIP_TRY(sel_prepare(h, h->nb, nbonds, perc_mix64(seed ^ 0x5DEECE66Dull), 0, d.bocc, d.sel_hist + kSelCnt,
+                        d.sel_cand + kCand, d.bocc + h->nb, 8, D));
+  if (D.nd == 0) return hipSuccess;
+  // the window pass: a draw's share of 2048 workgroups by its size (>= 1);
+  // the window-key pass: kSelCap / kBlock workgroups a draw
+  long long tot = 0;
+  for (int k = 0; k < D.nd; ++k) tot += D.d[k].n;
+  int G = 0;
+  for (int k = 0; k < D.nd; ++k) {
+    const long long share = D.nd == 1 ? 2048 : std::max<long long>(1, 2048 * D.d[k].n / tot);
+    D.d[k].g0 = G;
+    D.d[k].gn = (int)std::min<long long>(cdiv(D.d[k].n, kBlock), share);
+    G += D.d[k].gn;
+  }
+  k_select_window<<<G, kBlock, 0, st>>>(D);
+  HIP_TRY(dbg_sync(st, "k_select_window"));
+  k_select_final<<<D.nd, kSelThreads, 0, st>>>(D);
+  HIP_TRY(dbg_sync(st, "k_select_final"));
+  if (std::getenv("PERC_SELECT_TRACE")) {
+    for (int k = 0; k < D.nd; ++k) {
+      unsigned long long tr[6];
+      HIP_TRY(hipMemcpyAsync(tr, D.d[k].cand + 1 + kSelCap, sizeof(tr), hipMemcpyDeviceToHost, st));
+      HIP_TRY(hipStreamSynchronize(st));
+      std::fprintf(stderr, "select trace (draw %d): hist %llu bin %llu rank %llu ticks; nin %llu bin %llu\n", k,
+                   tr[1] - tr[0], tr[2] - tr[1], tr[3] - tr[2], tr[4], tr[5]);
+    }
+  }
+  const int GC = cdiv(kSelCap, kBlock);
+  for (int k = 0; k < D.nd; ++k) {
+    D.d[k].g0 = k * GC;
+    D.d[k].gn = GC;
+  }
+  k_occupy_cand<<<GC * D.nd, kBlock, 0, st>>>(D);
+  return dbg_sync(st, "k_occupy_cand");
 }
 
 static hipError_t label_finish(perc_ctx* h, int* nspan, int* span_list, int* nclusters,
