@@ -1063,6 +1063,7 @@ __global__ __launch_bounds__(kBlock) void k_to_strips(TileGeom T, const E* __res
 // code must be its nibble plus its column class's count / form bits (cls:
 // interior, first, last column), else *bad is set and the solve keeps the
 // u16 codes
+template <bool SM>  // false: the row-major nibble codes of the march past the Infinity Cache
 __global__ __launch_bounds__(kBlock) void k_pack_nib(TileGeom T, const uint16_t* __restrict__ code,
                                                       uint8_t* __restrict__ nib, unsigned c0, unsigned c1,
                                                       unsigned c2, int* bad) {
@@ -1072,7 +1073,7 @@ __global__ __launch_bounds__(kBlock) void k_pack_nib(TileGeom T, const uint16_t*
   auto cls = [&](int c) { return c == 0 ? c1 : (c == T.m - 1 ? c2 : c0); };
   const unsigned a = code[i], b = code[i + 1];
   if ((a & ~0xFu) != cls(col) || (b & ~0xFu) != cls(col + 1)) atomicOr(bad, 1);
-  nib[sm_at(T, gr, col) / 2] = (uint8_t)((a & 0xFu) | ((b & 0xFu) << 4));
+  nib[(SM ? sm_at(T, gr, col) : (long long)i) / 2] = (uint8_t)((a & 0xFu) | ((b & 0xFu) << 4));
 }
 
 

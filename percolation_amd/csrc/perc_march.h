@@ -186,10 +186,21 @@ constexpr bool kMarchRmSq = true;
 #else
 constexpr bool kMarchRmSq = false;
 #endif
-#ifdef PERC_MARCH_RM_SQ4
-#define PERC_MARCH_MINW(SM, MODE) ((SM) || (MODE) == 0 ? 1 : 4)
+// the row-major march's nibble codes (on unless PERC_MARCH_RM_U16, A/B probe
+// builds only)
+#ifdef PERC_MARCH_RM_U16
+constexpr bool kMarchRmNib = false;
 #else
-#define PERC_MARCH_MINW(SM, MODE) 1
+constexpr bool kMarchRmNib = true;
+#endif
+// waves per SIMD the row-major nibble march is held to (its column-class
+// path would take 132-135 VGPRs: 3 waves; the u16 march has 123-126)
+#if defined(PERC_MARCH_RM_SQ4)
+#define PERC_MARCH_MINW(SM, MODE, PK) ((SM) || (MODE) == 0 ? 1 : 4)
+#elif defined(PERC_MARCH_RM_NOBOUND)  // (A/B probe builds only)
+#define PERC_MARCH_MINW(SM, MODE, PK) 1
+#else
+#define PERC_MARCH_MINW(SM, MODE, PK) (!(SM) && (PK) && (MODE) != 0 ? 4 : 1)
 #endif
 
 struct MRow {       // one prefetched row of the lane's pair (+ halo column)
@@ -354,7 +365,7 @@ __device__ __forceinline__ MBuf march_bufs(const CGArgs& a, const MGeom& g, cons
   const unsigned nown = (unsigned)max(g.rend - g.r0, 0) * (unsigned)m;
   B.p = rsrc(psrc + base, n * 8u);
   B.r = rsrc(a.r + base, n * 8u);
-  B.c = rsrc(a.St.code + base, n * 2u);
+  B.c = PK ? rsrc(a.nib + base / 2, n / 2u) : rsrc(a.St.code + base, n * 2u);
   B.pn = rsrc(pnew + base, n * 8u);
   B.q = rsrc(MODE == kMarchPQ ? a.q + (long long)g.r0 * m : a.r, MODE == kMarchPQ ? nown * 8u : 0u);
   return B;
@@ -622,7 +633,7 @@ __device__ __forceinline__ void march_walk(const CGArgs& a, const MGeom& g, cons
 // TAG: the epilogue reductions by tagged granules (publish_and_reduce_tagged)
 template <int MODE, bool SM = false, int D = kMarchDepth, int PAUX = 0, bool TR = false,
           bool TAG = false, bool PK = false, bool LIT = false>
-__global__ __launch_bounds__(64 * kMarchWaves, PERC_MARCH_MINW(SM, MODE)) void k_cg_march(CGArgs a) {
+__global__ __launch_bounds__(64 * kMarchWaves, PERC_MARCH_MINW(SM, MODE, PK)) void k_cg_march(CGArgs a) {
   const unsigned long long tr_t0 = TR ? wall_clock64() : 0ull;
   unsigned long long tr_t1 = 0ull;
   CGScalars* S = a.S;

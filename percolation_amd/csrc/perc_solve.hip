@@ -105,9 +105,15 @@ void launch_cg_spmv(perc_ctx* h, const CGArgs& a, int G) {
       // bands (march_grid): with the x update out of the walk, L = 8192 P
       // 0.314 vs 0.355 ms on one round of slot-weighted bands, 0.628 vs
       // 0.656 ms per solve iteration (profiles/r4_8_l8192_ab.json)
+      else if (h->qfree && a.lit && a.nib)
+        klaunch(h, k_cg_march<kMarchP, false, kMarchDepth, 0, false, false, true, true>, h->march_grid,
+                64 * kMarchWaves, st, a);
       else if (h->qfree && a.lit)
         klaunch(h, k_cg_march<kMarchP, false, kMarchDepth, 0, false, false, false, true>, h->march_grid,
                 64 * kMarchWaves, st, a);
+      else if (h->qfree && a.nib)
+        klaunch(h, k_cg_march<kMarchP, false, kMarchDepth, 0, false, false, true>, h->march_grid, 64 * kMarchWaves,
+                st, a);
       else if (h->qfree) klaunch(h, k_cg_march<kMarchP>, h->march_grid, 64 * kMarchWaves, st, a);
       // q-storing P+S (row slabs, the literal dot order, modes without QFREE)
       else klaunch(h, k_cg_march<kMarchPQ, false, 3>, h->march_grid, 64 * kMarchWaves, st, a);
@@ -142,9 +148,15 @@ void launch_cg_b(perc_ctx* h, const CGArgs& a, int G) {
     if (a.sm) launch_march_sm<kMarchB>(h, h->stream, a);
     // row-major B: 8-row bands (march_grid, P's too), nontemporal r(k) loads
     // (L = 8192: 0.300 vs 0.331 ms, profiles/r4_3_l8192_probe.json)
+    else if (a.lit && a.nib)
+      klaunch(h, k_cg_march<kMarchB, false, kMarchDepth, kNT, false, false, true, true>, h->march_grid,
+              64 * kMarchWaves, h->stream, a);
     else if (a.lit)
       klaunch(h, k_cg_march<kMarchB, false, kMarchDepth, kNT, false, false, false, true>, h->march_grid,
               64 * kMarchWaves, h->stream, a);
+    else if (a.nib)
+      klaunch(h, k_cg_march<kMarchB, false, kMarchDepth, kNT, false, false, true>, h->march_grid, 64 * kMarchWaves,
+              h->stream, a);
     else klaunch(h, k_cg_march<kMarchB, false, kMarchDepth, kNT>, h->march_grid, 64 * kMarchWaves, h->stream, a);
   } else if (h->stencil) {
     // x on every row with the march's x-in-B (fused, row-major): XF
@@ -159,6 +171,33 @@ void launch_spmv(perc_ctx* h, const CGArgs& a, const double* x, double* y) {
   if (!h->stencil) spmv_launch(h, a.A, x, y, h->stream);
   else if (h->g.scn == 4) k_spmv_st<4><<<h->grid, kBlock, 0, h->stream>>>(a.St, x, y);
   else k_spmv_st<6><<<h->grid, kBlock, 0, h->stream>>>(a.St, x, y);
+}
+
+// the row-major march's nibble codes (vectors past the Infinity Cache,
+// square lattice, PERC_MARCH_NIBBLE): 0.5 instead of 2 bytes of row code
+// per element in P and B (24.5 instead of 26 B per row); a row whose upper
+// code bits are not its column class's keeps the u16 codes
+hipError_t to_nib_rows(perc_ctx* h, CGArgs& a) {
+  DeviceBuffers& d = h->d;
+  hipStream_t st = h->stream;
+  h->nib_used = false;
+  if (!kMarchRmNib || !h->nib_ok || !(h->march_mode & PERC_MARCH_NIBBLE) || !h->march || !h->qfree || a.sm)
+    return hipSuccess;
+  const long long n = (long long)a.T.nrows * a.T.m;
+  if (!d.nib_sm) HIP_TRY(dmalloc(&d.nib_sm, (size_t)h->N / 2 + 16));
+  HIP_TRY(hipMemsetAsync(d.sflag + 3, 0, sizeof(int), st));
+  k_pack_nib<false><<<blocks_for(n / 2), kBlock, 0, st>>>(a.T, d.code, d.nib_sm, h->ncls[0], h->ncls[1],
+                                                          h->ncls[2], d.sflag + 3);
+  HIP_TRY(dbg_sync(st, "k_pack_nib"));
+  int bad = 0;
+  HIP_TRY(hipMemcpyAsync(&bad, d.sflag + 3, sizeof(int), hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipStreamSynchronize(st));
+  if (!bad) {
+    a.nib = d.nib_sm;
+    for (int c = 0; c < 3; ++c) a.ncls[c] = h->ncls[c];
+  }
+  h->nib_used = !bad;
+  return hipSuccess;
 }
 
 // tagged-granule reductions of the strip-major q-free march (a.sm): a P and
@@ -489,8 +528,8 @@ hipError_t to_strips(perc_ctx* h, CGArgs& a) {
   if (h->nib_ok && (h->march_mode & PERC_MARCH_NIBBLE)) {
     if (!d.nib_sm) HIP_TRY(dmalloc(&d.nib_sm, (size_t)h->N / 2 + 16));
     HIP_TRY(hipMemsetAsync(d.sflag + 3, 0, sizeof(int), st));
-    k_pack_nib<<<blocks_for(n / 2), kBlock, 0, st>>>(a.T, d.code, d.nib_sm, h->ncls[0], h->ncls[1],
-                                                     h->ncls[2], d.sflag + 3);
+    k_pack_nib<true><<<blocks_for(n / 2), kBlock, 0, st>>>(a.T, d.code, d.nib_sm, h->ncls[0], h->ncls[1],
+                                                           h->ncls[2], d.sflag + 3);
     HIP_TRY(dbg_sync(st, "k_pack_nib"));
     int bad = 0;
     HIP_TRY(hipMemcpyAsync(&bad, d.sflag + 3, sizeof(int), hipMemcpyDeviceToHost, st));
@@ -775,6 +814,7 @@ hipError_t dev_solve_impl(perc_ctx* h, int itol, double tol, int itmax, bool x0_
   }
   if (!(h->march && h->qfree)) a.lit = nullptr;  // (the other kernels store no terms)
   if (h->strips) HIP_TRY(to_strips(h, a));
+  else HIP_TRY(to_nib_rows(h, a));
   HIP_TRY(setup_granules(h, a, itmax));
   HostFold hf;
   const bool host_fold = a.lit && h->dot_order == PERC_DOT_LITERAL_HOST;
@@ -958,6 +998,8 @@ hipError_t dev_bench(perc_ctx* h, int which, int reps, double* ms) {
   if (h->strips && (which == 1 || which == 2 || which == 5)) {
     HIP_TRY(to_strips(h, a));
     HIP_TRY(setup_granules(h, a, hs.itmax));
+  } else if (which == 1 || which == 2 || which == 5) {
+    HIP_TRY(to_nib_rows(h, a));
   }
   HIP_TRY(hipMemcpyAsync(d.scal, &hs, sizeof(hs), hipMemcpyHostToDevice, st));
   HIP_TRY(hipMemsetAsync(d.tickets, 0, kRedSlots * red_tickets_size(red_grid(h)) * sizeof(unsigned),

@@ -18,3 +18,9 @@ step c5prof 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_o
 step c5k1 200 python -u bench.py $C5 --steps 32
 step c5k2 200 python -u bench.py $C5 --steps 64 --warmup 2 --concurrent 2
 for k in 1 2; do tail -1 gpurun_out/r5o_c5k$k.log | cut -c1-160; done
+# the row-major march with nibble codes (main: held to 4 waves per SIMD;
+# rmnb: 3 waves, no spills) against the u16 codes (rmu16), L = 8192
+step nib8192 480 python -u tools/lib_ab.py --L 8192 --libs main,rmu16,rmnb --rounds 2 --iters 400 --reps 10
+tail -1 gpurun_out/r5o_nib8192.log
+step nib8192m 480 python -u tools/lib_ab.py --L 8192 --kind sitebond --ps 0.85 --p 0.85 --libs main,rmu16,rmnb --rounds 2 --iters 400 --reps 10
+tail -1 gpurun_out/r5o_nib8192m.log
