@@ -1020,7 +1020,7 @@ int perc_march_info(perc_ctx* h, int* out5) {
   if (!h->assembled) return PERC_ESTATE;
   out5[0] = h->small ? 4 : (h->resident && h->stencil ? 3 : (h->march ? 1 : 0));
   out5[1] = (h->qfree ? 1 : 0) | (h->strips ? 2 : 0) | (h->march_slots ? 8 : 0) |
-            (h->march_tag ? 16 : 0) | (h->nib_used && h->strips ? 32 : 0);
+            (h->march_tag ? 16 : 0) | (h->nib_used && out5[0] == 1 ? 32 : 0);
   out5[2] = h->march_alt ? 1 : 0;
   out5[3] = h->resident ? h->res_H : (h->march ? h->march_h : 0);
   out5[4] = h->resident ? h->g.m : (h->march ? 128 : 0);

@@ -683,18 +683,22 @@ def test_slot_weighted_bands_solve_the_same_system(lat, m, n, pbc, p):
         assert np.max(np.abs(b["vint"] - a["vint"])) < 1e-6
 
 
+@pytest.mark.parametrize("strips", [True, False])
 @pytest.mark.parametrize("lat,m,n,pbc,p", [(0, 512, 512, 0, 0.6), (0, 256, 160, 1, 0.6),
                                            (0, 1024, 1024, 0, 0.55), (0, 128, 1400, 0, 0.6),
                                            (0, 384, 200, 1, 0.5)])
-def test_nibble_codes_are_bitwise_the_u16_codes(lat, m, n, pbc, p):
-    """PERC_MARCH_NIBBLE (the strip-major march reads one 4-bit slot mask per
-    site, count and form from the column class): the codes it rebuilds are
-    the u16 codes (k_pack_nib checks every row), so the whole solve --
-    iteration count, err history, Gtop, Gbot, every voltage -- is bitwise
-    the u16-code solve's."""
+def test_nibble_codes_are_bitwise_the_u16_codes(lat, m, n, pbc, p, strips):
+    """PERC_MARCH_NIBBLE (the march reads one 4-bit slot mask per site,
+    count and form from the column class; strip-major, and row-major as past
+    the Infinity Cache -- STRIPS off): the codes it rebuilds are the u16
+    codes (k_pack_nib checks every row), so the whole solve -- iteration
+    count, err history, Gtop, Gbot, every voltage -- is bitwise the u16-code
+    solve's."""
     nb = api.nbonds(lat, m, n, pbc)
     order = api.shuffled_ids(nb, 2207)
     base = PL.MARCH_DEFAULT & ~PL.SOLVE_RESIDENT  # the march, not the resident solve
+    if not strips:
+        base &= ~PL.MARCH_STRIPS
     with api.Context(lat, m, n, pbc) as ctx:
         ctx.occupy(PL.BOND, bond_order=order, nbonds_=int(p * nb))
         if ctx.label()["nspan"] == 0:
@@ -706,7 +710,7 @@ def test_nibble_codes_are_bitwise_the_u16_codes(lat, m, n, pbc, p):
                 c = ctx.conductance(tol=tol, itmax=10 ** 6, vint=True)
                 c["hist"] = ctx.err_history()
                 info = ctx.march_info()
-                assert info["kernel"] == "wave" and info["strips"], info
+                assert info["kernel"] == "wave" and info["strips"] == strips, info
                 assert info["nibble"] == bool(mode & PL.MARCH_NIBBLE), info
                 out.append(c)
             a, b = out
