@@ -12,7 +12,7 @@ step() {
   echo "$name rc=$rc"
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then tail -30 gpurun_out/r5n_$name.log; exit $rc; fi
 }
-step pytest 400 python -u -m pytest tests/test_labeling_oracle.py -m gpu -x -q --timeout 300 --timeout-method thread
+step pytest 600 python -u -m pytest tests/test_labeling_oracle.py tests/test_gpu_parity.py -m gpu -x -q --timeout 300 --timeout-method thread
 tail -2 gpurun_out/r5n_pytest.log
 step guard 600 python -u tools/lib_ab.py --L 4096 --libs main,noguard --iters 20000 --reps 10 --rounds 2
 tail -1 gpurun_out/r5n_guard.log
