@@ -26,6 +26,9 @@ def main():
     ap.add_argument("--reps", type=int, default=64)
     ap.add_argument("--copies", type=int, default=16)
     ap.add_argument("--march-mode", type=int, default=-1, help="perc_set_march_mode bits; -1: default")
+    ap.add_argument("--kind", default="bond", choices=("bond", "sitebond"),
+                    help="sitebond: a mixed occupation (--ps, --p) under ConductCalc's mixed rule")
+    ap.add_argument("--ps", type=float, default=0.85)
     args = ap.parse_args()
     import torch
     from percolation_amd import api
@@ -37,7 +40,13 @@ def main():
     with api.Context(0, L_, L_, 0) as ctx:
         if args.march_mode >= 0:
             ctx.set_march_mode(args.march_mode)
-        r = ctx.bondc_realisation(None, tb, tol=1e-8, itmax=20, device_ptr=dev_o.data_ptr())
+        if args.kind == "bond":
+            r = ctx.bondc_realisation(None, tb, tol=1e-8, itmax=20, device_ptr=dev_o.data_ptr())
+        else:  # the config-5 companion's matrix
+            from percolation_amd import _lib as PL
+            ctx.occupy_random(PL.SITEBOND, int(args.ps * L_ * L_), tb, 1234)
+            r = ctx.label()
+            ctx.conductance(PL.RULE_MIXED, PL.CUR_MATLAB, tol=1e-8, itmax=20)
         it_ms = ctx.bench_kernel(5, args.reps)
         cp_ms = ctx.bench_kernel(4, args.copies)
     # bench_kernel adds 3 untimed warmup launches per call

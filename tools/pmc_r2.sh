@@ -10,8 +10,11 @@ export TMPDIR=/tmp
 L=${L:-4096}
 # row-code bytes per element of the strip-major q-free march: 1/2 with the
 # nibble codes (PERC_MARCH_NIBBLE, default since round 4; CBX2 = 2 x that),
-# 2 with the u16 codes (CBX2=4); the row-major march (L = 8192) reads u16
+# 2 with the u16 codes (CBX2=4); the row-major march (L = 8192) reads the
+# nibble codes too since round 5.  PROBE_ARGS: extra pmc_probe.py arguments
+# (e.g. "--kind sitebond --ps 0.85 --p 0.85": the config-5 companion)
 CBX2=${CBX2:-1}
+PROBE_ARGS=${PROBE_ARGS:-}
 N=$((L * L - 2 * L))
 timeout -k 10 300 python -c "import torch; torch.cuda.init()" || exit 1
 i=0
@@ -20,8 +23,9 @@ for ctrs in "TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum 
             "TCC_EA0_RDREQ_DRAM_sum TCC_EA0_WRREQ_DRAM_sum TCC_EA0_WRREQ_sum"; do
   i=$((i + 1))
   echo "== pass $i: $ctrs" >> gpurun_out/pmc_r2.log
+  rm -rf gpurun_out/pmc_r2/p$i
   timeout -s KILL 120 rocprofv3 --pmc $ctrs --kernel-include-regex "k_cg_march|k_cg_b|k_copy" \
-    -f csv -d gpurun_out/pmc_r2/p$i -o run -- python3 tools/pmc_probe.py --L $L --march-mode $MODE \
+    -f csv -d gpurun_out/pmc_r2/p$i -o run -- python3 tools/pmc_probe.py --L $L --march-mode $MODE $PROBE_ARGS \
     >> gpurun_out/pmc_r2.log 2>&1 || { echo "pass $i failed rc=$?" >> gpurun_out/pmc_r2.log; exit 1; }
 done
 python3 tools/pmc_reconcile.py gpurun_out/pmc_r2_reconcile_L$L.csv gpurun_out/pmc_r2/p* \
