@@ -193,8 +193,9 @@ constexpr bool kMarchRmNib = false;
 #else
 constexpr bool kMarchRmNib = true;
 #endif
-// waves per SIMD the row-major nibble march is held to (its column-class
-// path would take 132-135 VGPRs: 3 waves; the u16 march has 123-126)
+// waves per SIMD the row-major nibble march (B) is held to (its column-class
+// path would take 132-134 VGPRs: 3 waves; 128 without spills when held;
+// the u16 march has 123-126)
 #if defined(PERC_MARCH_RM_SQ4)
 #define PERC_MARCH_MINW(SM, MODE, PK) ((SM) || (MODE) == 0 ? 1 : 4)
 #elif defined(PERC_MARCH_RM_NOBOUND)  // (A/B probe builds only)

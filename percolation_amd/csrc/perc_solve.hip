@@ -105,15 +105,12 @@ void launch_cg_spmv(perc_ctx* h, const CGArgs& a, int G) {
       // bands (march_grid): with the x update out of the walk, L = 8192 P
       // 0.314 vs 0.355 ms on one round of slot-weighted bands, 0.628 vs
       // 0.656 ms per solve iteration (profiles/r4_8_l8192_ab.json)
-      else if (h->qfree && a.lit && a.nib)
-        klaunch(h, k_cg_march<kMarchP, false, kMarchDepth, 0, false, false, true, true>, h->march_grid,
-                64 * kMarchWaves, st, a);
+      // (row-major P keeps the u16 codes: its column-class path for the
+      // nibble codes costs a wave per SIMD or spills -- P 0.389 / 0.363 vs
+      // 0.330 ms at L = 8192; B takes them, profiles/r5_14_ab_rowmajor_nibble_*)
       else if (h->qfree && a.lit)
         klaunch(h, k_cg_march<kMarchP, false, kMarchDepth, 0, false, false, false, true>, h->march_grid,
                 64 * kMarchWaves, st, a);
-      else if (h->qfree && a.nib)
-        klaunch(h, k_cg_march<kMarchP, false, kMarchDepth, 0, false, false, true>, h->march_grid, 64 * kMarchWaves,
-                st, a);
       else if (h->qfree) klaunch(h, k_cg_march<kMarchP>, h->march_grid, 64 * kMarchWaves, st, a);
       // q-storing P+S (row slabs, the literal dot order, modes without QFREE)
       else klaunch(h, k_cg_march<kMarchPQ, false, 3>, h->march_grid, 64 * kMarchWaves, st, a);
@@ -175,8 +172,10 @@ void launch_spmv(perc_ctx* h, const CGArgs& a, const double* x, double* y) {
 
 // the row-major march's nibble codes (vectors past the Infinity Cache,
 // square lattice, PERC_MARCH_NIBBLE): 0.5 instead of 2 bytes of row code
-// per element in P and B (24.5 instead of 26 B per row); a row whose upper
-// code bits are not its column class's keeps the u16 codes
+// per element in B (24.5 + 48m / N instead of 26 B per row: 0.297 vs 0.304
+// ms at L = 8192); a row whose upper code bits are not its column class's
+// keeps the u16 codes
+// (B only: k_cg_march<P> reads the u16 codes in the row-major layout)
 hipError_t to_nib_rows(perc_ctx* h, CGArgs& a) {
   DeviceBuffers& d = h->d;
   hipStream_t st = h->stream;
