@@ -14,6 +14,7 @@ L=${L:-4096}
 # nibble codes too since round 5.  PROBE_ARGS: extra pmc_probe.py arguments
 # (e.g. "--kind sitebond --ps 0.85 --p 0.85": the config-5 companion)
 CBX2=${CBX2:-1}
+CBX2P=${CBX2P:-$CBX2}  # P's (the row-major P keeps the u16 codes: CBX2P=4 at L = 8192)
 PROBE_ARGS=${PROBE_ARGS:-}
 N=$((L * L - 2 * L))
 timeout -k 10 300 python -c "import torch; torch.cuda.init()" || exit 1
@@ -28,9 +29,9 @@ for ctrs in "TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum 
     -f csv -d gpurun_out/pmc_r2/p$i -o run -- python3 tools/pmc_probe.py --L $L --march-mode $MODE $PROBE_ARGS \
     >> gpurun_out/pmc_r2.log 2>&1 || { echo "pass $i failed rc=$?" >> gpurun_out/pmc_r2.log; exit 1; }
 done
-python3 tools/pmc_reconcile.py gpurun_out/pmc_r2_reconcile_L$L.csv gpurun_out/pmc_r2/p* \
+python3 tools/pmc_reconcile.py gpurun_out/pmc_r2_reconcile_L$L${TAG:+_$TAG}.csv gpurun_out/pmc_r2/p* \
   --last "k_cg_march<1=64" "k_cg_march<2=64" "k_cg_march<0=64" "k_cg_b<true=64" k_copy=16 \
-  --algo "k_cg_march<1=$((16 * N + CBX2 * N / 2)):$((8 * N))" \
+  --algo "k_cg_march<1=$((16 * N + CBX2P * N / 2)):$((8 * N))" \
          "k_cg_march<2=$((16 * N + CBX2 * N / 2 + 32 * L)):$((8 * N + 16 * L))" \
          "k_cg_march<0=$((18 * (L * L - 2 * L))):$((16 * (L * L - 2 * L)))" \
          "k_cg_b<true=$((18 * (L * L - 2 * L) + 32 * L)):$((8 * (L * L - 2 * L) + 16 * L))" \
