@@ -345,7 +345,7 @@ def rocprof_avg(base, L_):
 OLD_RECONCILE = {"k_cg_march": "k_cg_march<0", "k_cg_b": "k_cg_b<true"}
 
 
-def pmc_traffic(base, L_):
+def pmc_traffic(base, L_, kind="bond"):
     """HBM bytes per launch of a CG kernel from the committed rocprofv3 PMC
     summaries.  Preferred: profiles/*_pmc_reconcile_L<L>.csv
     (tools/pmc_r2.sh + tools/pmc_reconcile.py): one fixed dispatch set of
@@ -365,7 +365,11 @@ def pmc_traffic(base, L_):
                                             for t in re.split(r"(\d+)", os.path.basename(f))],
                       reverse=True)
 
-    for f in newest_first("*_pmc_reconcile_L%d.csv" % L_):
+    # a mixed occupation's matrix (the config-5 companion) cites its own
+    # reconciliation (*_pmc_reconcile_L<L>_mixed.csv) where there is one
+    pats = (["*_pmc_reconcile_L%d_mixed.csv" % L_] if kind == "sitebond" else []) + \
+        ["*_pmc_reconcile_L%d.csv" % L_]
+    for f in [f for pat in pats for f in newest_first(pat)]:
         with open(f) as fh:
             for r in csv.DictReader(fh):
                 if OLD_RECONCILE.get(r["kernel"], r["kernel"]) == base and r["read_bytes"] \
@@ -793,7 +797,7 @@ def main():
                      "gbs": round(nbytes / (avg * 1e-3) / 1e9, 1) if avg > 0 else None}
     # the roofline line is the kernel with the most device time
     dom = max(kern, key=lambda k_: kern[k_]["total_ms"])
-    traffic, traffic_src = pmc_traffic(rocprof_base(dom, fmt, minfo), L_)
+    traffic, traffic_src = pmc_traffic(rocprof_base(dom, fmt, minfo), L_, args.kind)
     rp_ms, rp_src = rocprof_avg(rocprof_base(dom, fmt, minfo), L_)
     achieved = kern[dom]["gbs"] or 0.0  # 0: no realisation spanned, nothing solved
     iter_ms = sum(v["avg_launch_ms"] for v in kern.values())
