@@ -84,14 +84,13 @@ __device__ __forceinline__ double div_tab_core(double a, double2 dy) {
 // -- was compiled as predicated straight-line code and cost every element:
 // the march P 0.102 vs 0.077 ms, the solve 0.1572 vs 0.1489 ms per
 // iteration at L = 4096 (profiles/r5_10_ab_division_L4096.json); removed.
+// Written branch-free (scaled by selects, `/` only for subnormal quotients)
+// it is exact and no faster over 20000-iteration solves: 0.15415 vs 0.15406
+// ms per iteration (r5_15_ab_division_scaled_it20000_L4096.json); the guard
+// itself costs 1.3 % there (r5_13_ab_division_guard_it20000_L4096.json).
 __device__ __forceinline__ double div_tab(double a, double2 dy) {
 #if defined(PERC_DIV_NOGUARD)  // (A/B probe builds only: the guard's cost, wrong below 2^-960)
   return div_tab_core(a, dy);
-#elif defined(PERC_DIV_SCALED)  // (A/B probe builds only: scaled numerators, branch-free)
-  const bool tiny = fabs(a) < 0x1p-960;
-  const double z = div_tab_core(a * (tiny ? 0x1p512 : 1.0), dy) * (tiny ? 0x1p-512 : 1.0);
-  if (__builtin_expect(tiny && fabs(z) < 0x1p-1022 && z != 0.0, 0)) return a / dy.x;
-  return z;
 #else
   if (__builtin_expect(fabs(a) < 0x1p-960, 0)) return a / dy.x;
   return div_tab_core(a, dy);
