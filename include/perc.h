@@ -198,6 +198,18 @@ int perc_replay_labels(int lattice, int m, int n, int pbc, int kind, int nsites,
    trace = 1). */
 int perc_replay_bond_trace(int lattice, int m, int n, int pbc, int nbond, const int *bond_order,
                            int *trace);
+/* site.f's per-site trace (siteocc.txt, Square/site.f:167-272,
+   Triangular/site.f): for the first nsite entries of site_order (1-based
+   ids), PERC_SITE_TRACE ints each: [0] the site, [1..6] nearestn (scn
+   used), [7] the neighbour with the largest cluster, [8] that cluster's
+   number, [9] its size, [10] k = clusters absorbed, [11 + 2j] the size
+   added and [12 + 2j] the largest cluster's size after (j < k), [21] the
+   cluster the site joined, [22] its size after the step (host replay; the
+   Fortran site driver writes siteocc.txt from it with trace = 1).
+   PERC_EREPLAY for an id outside 1..m*n. */
+#define PERC_SITE_TRACE 24
+int perc_replay_site_trace(int lattice, int m, int n, int pbc, int nsite, const int *site_order,
+                           int *trace);
 
 /* ---- conductance ----------------------------------------------------- */
 typedef struct {

@@ -712,6 +712,24 @@ int perc_replay_bond_trace(int lattice, int m, int n, int pbc, int nbond, const 
   return replay_bonds(g, bf, bond_order, nbond, bl.data(), c.data(), (int)c.size(), st, trace);
 }
 
+int perc_replay_site_trace(int lattice, int m, int n, int pbc, int nsite, const int* site_order,
+                           int* trace) {
+  if ((lattice != PERC_SQUARE && lattice != PERC_TRIANGULAR) || m < 2 || n < 2 || nsite < 0 ||
+      (nsite && (!site_order || !trace)))
+    return PERC_EINVAL;
+  static_assert(PERC_SITE_TRACE == kSiteTrace, "trace record size");
+  const Geom g = make_geom(lattice, m, n, pbc);
+  if (nsite > g.t) return PERC_EINVAL;
+  for (int i = 0; i < nsite; ++i)
+    if (site_order[i] < 1 || site_order[i] > g.t) {
+      set_error("perc_replay_site_trace: site id outside 1..m*n");
+      return PERC_EREPLAY;
+    }
+  std::vector<int> c(g.t + 2, 0), sl(g.t, 0);
+  int st[4] = {0, 0, 0, 0};
+  return replay_sites(g, site_order, nsite, sl.data(), c.data(), (int)c.size(), st, trace);
+}
+
 // the spanning cluster's Kirchhoff system (perc_conductance / perc_assemble)
 static int assemble_impl(perc_ctx* h, int rule, double g0, double leak, double Va, const char* who) {
   hipError_t e = dev_assemble(h, rule, g0, leak, Va, h->span_root);

@@ -280,8 +280,13 @@ hipError_t dev_bench(perc_ctx* h, int which, int reps, double* ms);
 // cluster number the bond got and that cluster's size after the step
 int replay_bonds(const Geom& g, const std::vector<int>& bond_first, const int* order,
                  int count, int* label, int* csize, int cap, int* stats, int* trace = nullptr);
+// trace (optional, kSiteTrace per order entry): site.f's per-site step
+// (siteocc.txt, Square/site.f:167-272): sn, nn(1..6), nnlc, lcn, lcs, the
+// number of absorbed clusters k, k pairs (size added, largest cluster's
+// size after), the cluster the site joined and that cluster's size after
+constexpr int kSiteTrace = 24;
 int replay_sites(const Geom& g, const int* order, int count, int* label, int* csize, int cap,
-                 int* stats);
+                 int* stats, int* trace = nullptr);
 int replay_bondsite(const Geom& g, const std::vector<int>& bond_first, const int* sorder,
                     int nsites, const int* border, int nbond, int* site_label, int* bond_label,
                     int* csize, int cap, int* stats);

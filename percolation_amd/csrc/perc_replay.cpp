@@ -168,7 +168,7 @@ int replay_bonds(const Geom& g, const std::vector<int>& bond_first, const int* o
 }
 
 int replay_sites(const Geom& g, const int* order, int count, int* label, int* csize, int cap,
-                 int* stats) {
+                 int* stats, int* trace) {
   if (cap < g.t + 2) return PERC_EINVAL;
   std::vector<int> c(cap, 0);
   std::vector<int> clab(g.t + 1, 0);
@@ -184,13 +184,26 @@ int replay_sites(const Geom& g, const int* order, int count, int* label, int* cs
       lab[k] = (nn[k] > 0 && occ[nn[k]]) ? clab[dsu.find(nn[k])] : 0;
       siz[k] = c[lab[k]];
     }
-    int lcn = lab[0], lcs = siz[0];
+    int lcn = lab[0], lcs = siz[0], nnlc = nn[0];
     for (int k = 1; k < g.scn; ++k)
-      if (nn[k] != 0 && lab[k] != 0 && siz[k] > lcs) { lcn = lab[k]; lcs = siz[k]; }
+      if (nn[k] != 0 && lab[k] != 0 && siz[k] > lcs) { lcn = lab[k]; lcs = siz[k]; nnlc = nn[k]; }
+    int* tr = trace ? trace + (size_t)kSiteTrace * i : nullptr;
+    if (tr) {
+      std::memset(tr, 0, sizeof(int) * kSiteTrace);
+      tr[0] = sn;
+      for (int k = 0; k < g.scn; ++k) tr[1 + k] = nn[k];
+      tr[7] = nnlc;
+      tr[8] = lcn;
+      tr[9] = lcs;
+    }
     occ[sn] = 1;
     if (lcs == 0) {
       clab[sn] = cln;
       c[cln] = 1;
+      if (tr) {
+        tr[21] = cln;
+        tr[22] = 1;
+      }
       ++cln;
     } else {
       int clsum = lcs;
@@ -202,12 +215,21 @@ int replay_sites(const Geom& g, const int* order, int count, int* label, int* cs
           if (!dup) {
             clsum += siz[k];
             c[lab[k]] = 0;
+            if (tr && tr[10] < 5) {  // "adding c(s(nn(k))) / largest cluster is now clsum"
+              tr[11 + 2 * tr[10]] = siz[k];
+              tr[12 + 2 * tr[10]] = clsum;
+              ++tr[10];
+            }
           }
         }
         dsu.unite(sn, nn[k]);
       }
       clab[dsu.find(sn)] = lcn;
       c[lcn] = clsum + 1;
+      if (tr) {
+        tr[21] = lcn;
+        tr[22] = c[lcn];
+      }
     }
     track_max(c, lcn, lcs, &maxcn, &maxcs);
   }

@@ -13,6 +13,8 @@ module perc_api
   integer(c_int), parameter :: PERC_SQUARE = 0, PERC_TRIANGULAR = 1
   integer(c_int), parameter :: PERC_BOND = 0, PERC_SITE = 1, PERC_SITEBOND = 2, &
                                 PERC_BONDSITE = 3
+  ! ints per site of perc_replay_site_trace (siteocc.txt)
+  integer(c_int), parameter :: PERC_SITE_TRACE = 24
   integer(c_int), parameter :: PERC_RULE_BOND = 0, PERC_RULE_SITE = 1, PERC_RULE_MIXED = 2
   integer(c_int), parameter :: PERC_CUR_FORTRAN = 0, PERC_CUR_MATLAB = 1
   ! association of linbcg's dot products (perc_set_dot_order)
@@ -98,6 +100,14 @@ module perc_api
       integer(c_int), value :: lattice, m, n, pbc, nbond
       type(c_ptr), value :: bond_order, trace
     end function perc_replay_bond_trace
+
+    ! site.f's per-site steps (siteocc.txt): PERC_SITE_TRACE ints per site
+    integer(c_int) function perc_replay_site_trace(lattice, m, n, pbc, nsite, site_order, trace) &
+        bind(C, name='perc_replay_site_trace')
+      import :: c_int, c_ptr
+      integer(c_int), value :: lattice, m, n, pbc, nsite
+      type(c_ptr), value :: site_order, trace
+    end function perc_replay_site_trace
 
     integer(c_int) function perc_nbonds(lattice, m, n, pbc) bind(C, name='perc_nbonds')
       import :: c_int

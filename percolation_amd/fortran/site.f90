@@ -7,9 +7,11 @@
 ! Parameters: the reference's block (Square/site.f:51-131: 50x50, ps = .60,
 ! seed 1080115; Triangular: ps = .548, seed 143285), overridable by an
 ! optional namelist file site.nml (&site_nml lattice, m, n, pbc, ps, seed,
-! conductance, Va, g0, tol, itmax, device /).  Outputs as the reference:
-! bondlist.txt (i10,",",i10), siteorder.txt (list-directed), site.txt
-! (j, s(j), c(j); site.f:353-358).  siteocc.txt (trace) is not written.
+! conductance, Va, g0, tol, itmax, device, trace /).  Outputs as the
+! reference: bondlist.txt (i10,",",i10), siteorder.txt (list-directed),
+! site.txt (j, s(j), c(j); site.f:353-358); trace = 1 also writes the
+! per-site log siteocc.txt (site.f:167-350) from the host replay, before the
+! device is opened.
 program site
   use perc_api
   implicit none
@@ -19,9 +21,10 @@ program site
   integer(c_int) :: lattice, m, n, pbc, seed, itmax, device
   double precision :: ps, Va, g0, tol
   logical :: conductance
-  namelist /site_nml/ lattice, m, n, pbc, ps, seed, conductance, Va, g0, tol, itmax, device
+  integer(c_int) :: trace
+  namelist /site_nml/ lattice, m, n, pbc, ps, seed, conductance, Va, g0, tol, itmax, device, trace
   integer(c_int) :: t, nb, tsites, i, rc, stats(4)
-  integer(c_int), allocatable, target :: b1(:), b2(:), order(:), slabel(:), csize(:)
+  integer(c_int), allocatable, target :: b1(:), b2(:), order(:), slabel(:), csize(:), rec(:)
   type(c_ptr) :: h
   type(perc_label_info) :: info
   type(perc_cond_result) :: res
@@ -44,6 +47,7 @@ program site
   tol = 1.00d-08
   itmax = 100000
   device = 0
+  trace = 0
   if (perc_have_file('site.nml')) then
     open(newunit=u, file='site.nml', status='old')
     read(u, nml=site_nml)
@@ -68,6 +72,7 @@ program site
   close(12)
 
   tsites = ps * t
+  if (trace /= 0) call write_siteocc()
   call perc_check(perc_ctx_create(device, lattice, m, n, pbc, h), 'perc_ctx_create')
   call perc_check(perc_occupy(h, PERC_SITE, tsites, c_loc(order), 0, c_null_ptr), 'perc_occupy')
   call perc_check(perc_label(h, info, c_null_ptr), 'perc_label')
@@ -101,4 +106,74 @@ program site
 
 111 format(i10, ",", i10, ",", i10)
 121 format(i10, ",", i10)
+
+contains
+
+  ! siteocc.txt as the reference writes it (site.f:167-350): each site's
+  ! step from perc_replay_site_trace, then the largest cluster and the
+  ! spanning test over clusters of at least n sites in label order, from the
+  ! host replay's numbering (perc_replay_labels)
+  subroutine write_siteocc()
+    integer(c_int) :: j, k, r, scn, sstats(4), span
+    integer(c_int), allocatable, target :: s(:), c(:)
+    double precision :: f   ! site.f:40 (a double holding a single-precision quotient)
+    scn = 4
+    if (lattice /= PERC_SQUARE) scn = 6
+    allocate(rec(PERC_SITE_TRACE * max(tsites, 1)), s(t), c(t + nb + 2))
+    call perc_check(perc_replay_site_trace(lattice, m, n, pbc, tsites, c_loc(order), c_loc(rec)), &
+                    'perc_replay_site_trace')
+    call perc_check(perc_replay_labels(lattice, m, n, pbc, PERC_SITE, tsites, c_loc(order), 0, &
+                                       c_null_ptr, c_null_ptr, c_loc(s), c_loc(c), t + nb + 2, &
+                                       sstats), 'perc_replay_labels')
+    open(unit=11, file='siteocc.txt')
+    do i = 1, tsites
+      r = PERC_SITE_TRACE * (i - 1)
+      write(11, *) "site chosen:", rec(r + 1)
+      write(11, *) "nearest neighbors:", (rec(r + 1 + j), j = 1, scn)
+      write(11, *) "n.n. with largest cluster:", rec(r + 8)
+      write(11, *) "largest cluster number:", rec(r + 9)
+      write(11, *) "largest neighbor cluster size:", rec(r + 10)
+      if (rec(r + 10) == 0) then
+        write(11, *) "*no n.n. occupied*"
+        write(11, *) "site assigned to cluster number", rec(r + 22)
+      else
+        write(11, *) "*one or more n.n. occupied*"
+        do k = 1, rec(r + 11)
+          write(11, *) "adding", rec(r + 10 + 2 * k), " to largest cluster"
+          write(11, *) "largest cluster is now", rec(r + 11 + 2 * k)
+        end do
+        write(11, *) "site assigned to cluster number", rec(r + 22)
+        write(11, *) "size of cluster number", rec(r + 22), " is now", rec(r + 23)
+      end if
+      f = real(i) / real(t)   ! site.f:267, single-precision division
+      write(11, *) "fraction of lattice filled:", f
+      write(11, *) "--------------------"
+    end do
+    write(11, *)
+    write(11, *) "******************************"
+    write(11, *) "largest overall cluster number:", sstats(2)
+    write(11, *) "largest overall cluster size:", sstats(3)
+    span = 0
+    do i = 1, sstats(1) - 1
+      if (c(i + 1) >= n) then
+        write(11, *) "testing cluster"
+        if (.not. any(s(1:m) == i)) then
+          write(11, *) "source end not connected"
+          cycle
+        end if
+        if (.not. any(s(t - m + 1:t) == i)) then
+          write(11, *) "drain end not connected"
+          cycle
+        end if
+        write(11, *) "infinite cluster present"
+        write(11, *) "infinite cluster number:", i
+        write(11, *) "infinite cluster size:", c(i + 1)
+        span = 1
+        exit
+      end if
+    end do
+    if (span == 0) write(11, *) "no infinite cluster present"
+    write(11, *) "******************************"
+    close(11)
+  end subroutine write_siteocc
 end program site

@@ -25,7 +25,7 @@ from percolation_amd import api
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 BIN = os.path.join(REPO, "percolation_amd", "fortran", "bin")
-TRACES = {"bondocc.txt", "siteocc.txt", "sbdebug.txt", "bsdebug.txt"}  # per-step logs, not produced
+TRACES = {"bondocc.txt", "siteocc.txt", "sbdebug.txt", "bsdebug.txt"}  # per-step logs (trace = 1 only)
 # golden kind -> (program, namelist group, parameters)
 NML = {"bondc": ("bondc", "bondc", ("lattice", "m", "n", "pbc", "pb", "seed", "tol", "itmax")),
        "site": ("site", "site", ("lattice", "m", "n", "pbc", "ps", "seed")),
@@ -253,3 +253,48 @@ def test_bondc_driver_trace_log(v, tmp_path):
     md, r = run_variant(v, tmp_path, extra=["dot_order=1", "trace=1"])
     got = hashlib.md5((tmp_path / "bondocc.txt").read_bytes()).hexdigest()
     assert got == md["files"]["bondocc.txt"], v
+
+
+SITE_TRACE_VARIANTS = [v for v in G.variants() if "siteocc.txt" in G.meta(v).get("files", {})]
+
+
+@pytest.mark.parametrize("v", SITE_TRACE_VARIANTS)
+def test_site_driver_trace_log(v, tmp_path):
+    """trace = 1: siteocc.txt -- every site's nearest neighbours, largest
+    neighbour cluster, absorbed clusters and fraction filled, then the
+    largest cluster and the spanning test, site.f:167-350 -- is the
+    reference run's byte for byte (md5 of the reference's own file).  The
+    driver writes it from the host replay before it opens the device, so
+    this runs with or without a GPU; with one the run must also finish."""
+    import hashlib
+    md, r = run_variant(v, tmp_path, expect_ok=have_gpu(), extra=["trace=1"])
+    got = hashlib.md5((tmp_path / "siteocc.txt").read_bytes()).hexdigest()
+    assert got == md["files"]["siteocc.txt"], v
+    if not have_gpu():
+        assert "status -8" in r.stderr
+
+
+def test_replay_site_trace_records():
+    """perc_replay_site_trace's records against the site replay: each
+    step's joined cluster/size, and the absorbed sizes summing to the
+    step's cluster size (lcs + sum(added) + 1)."""
+    import numpy as np
+    from percolation_amd import _lib as L
+    lib = L.lib()
+    m = n = 17
+    order = np.random.default_rng(3).permutation(m * n).astype(np.int32) + 1
+    k = int(0.7 * m * n)
+    tr = np.zeros(24 * k, np.int32)
+    assert lib.perc_replay_site_trace(0, m, n, 0, k, order.ctypes.data, tr.ctypes.data) == 0
+    tr = tr.reshape(k, 24)
+    assert (tr[:, 0] == order[:k]).all()
+    for row in tr:
+        if row[9] == 0:
+            assert row[22] == 1 and row[10] == 0
+        else:
+            added = row[11:11 + 2 * row[10]:2]
+            assert row[21] == row[8] and row[22] == row[9] + added.sum() + 1
+    bad = order.copy()
+    bad[0] = m * n + 1
+    assert lib.perc_replay_site_trace(0, m, n, 0, k, bad.ctypes.data, np.zeros(24 * k, np.int32)
+                                      .ctypes.data) == -7
