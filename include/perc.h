@@ -210,6 +210,29 @@ int perc_replay_bond_trace(int lattice, int m, int n, int pbc, int nbond, const 
 #define PERC_SITE_TRACE 24
 int perc_replay_site_trace(int lattice, int m, int n, int pbc, int nsite, const int *site_order,
                            int *trace);
+/* The mixed programs' debug logs (sbdebug.txt, Square/sitebond.f:184-465;
+   bsdebug.txt, Square/bondsite.f:178-418): the second phase's steps as an
+   int stream, one record per order entry (host replay, kind PERC_SITEBOND
+   or PERC_BONDSITE, the other arguments as perc_replay_labels).
+   PERC_SITEBOND, per bond of bond_order[0..nbonds):
+     {0, cln}                      both end sites empty: a new cluster
+     {1, a, lcn, size}             only site a occupied, bond joins its cluster
+     {2, b, lcn, size}             only site b occupied
+     {3, a, la, ca, b, lb, cb, size}     both in one cluster
+     {4|5, a, la, ca, b, lb, cb, ns, ns sites, nk, nk bond ids, lcn, size,
+      oldcn}                       different clusters: 4 when a's is larger,
+                                   5 otherwise; the sites and bonds (1-based
+                                   list ids) relabelled oldcn -> lcn in index
+                                   order; cluster oldcn is then empty
+     {6}                           the shuffle's spill slot (0, 0)
+   PERC_BONDSITE, per site of site_order[0..nsites):
+     {0, cln}                      no occupied neighbour bond: a new cluster
+     {1, k, k x (size added, largest cluster after), lcn, size}
+   *len receives the stream length; trace may be NULL to size it, otherwise
+   PERC_EINVAL when cap < *len. */
+int perc_replay_mixed_trace(int lattice, int m, int n, int pbc, int kind, int nsites,
+                            const int *site_order, int nbonds, const int *bond_order, int *trace,
+                            long long cap, long long *len);
 
 /* ---- conductance ----------------------------------------------------- */
 typedef struct {

@@ -129,6 +129,8 @@ SIGNATURES = {
     "perc_twister_uniform": (C.c_int, [C.c_uint, C.c_longlong, _VP]),
     "perc_replay_bond_trace": (C.c_int, [C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, _VP, _VP]),
     "perc_replay_site_trace": (C.c_int, [C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, _VP, _VP]),
+    "perc_replay_mixed_trace": (C.c_int, [C.c_int] * 6 + [_VP, C.c_int, _VP, _VP, C.c_longlong,
+                                                           C.POINTER(C.c_longlong)]),
     "perc_x_row": (C.c_int, [_VP, C.c_int, _VP, C.c_int]),
     "perc_currents": (C.c_int, [_VP, C.c_int, C.c_int, C.c_double, C.c_double, C.c_double,
                                 C.POINTER(CondResult)]),

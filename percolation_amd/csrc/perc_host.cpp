@@ -730,6 +730,34 @@ int perc_replay_site_trace(int lattice, int m, int n, int pbc, int nsite, const 
   return replay_sites(g, site_order, nsite, sl.data(), c.data(), (int)c.size(), st, trace);
 }
 
+int perc_replay_mixed_trace(int lattice, int m, int n, int pbc, int kind, int nsites,
+                            const int* site_order, int nbond, const int* bond_order, int* trace,
+                            long long cap, long long* len) {
+  if ((lattice != PERC_SQUARE && lattice != PERC_TRIANGULAR) || m < 2 || n < 2 || !len ||
+      (kind != PERC_SITEBOND && kind != PERC_BONDSITE) || nsites < 0 || nbond < 0 ||
+      (nsites && !site_order) || (nbond && !bond_order))
+    return PERC_EINVAL;
+  const Geom g = make_geom(lattice, m, n, pbc);
+  std::vector<int> bf(g.t + 2, 0);
+  for (int s = 1; s <= g.t + 1; ++s)
+    bf[s] = bf[s - 1] + ((s - 1 >= 1 && s - 1 <= g.t - 1) ? forward_count(g, s - 1) : 0);
+  if (nsites > g.t + 1 || nbond > bf[g.t + 1] + 1) return PERC_EINVAL;
+  const long long nb = nbonds(g);
+  std::vector<int> c(g.t + nb + 2, 0), sl(g.t, 0), bl(nb, 0), ev;
+  int st[4] = {0, 0, 0, 0};
+  const int rc = kind == PERC_SITEBOND
+                     ? replay_sitebond(g, bf, site_order, nsites, bond_order, nbond, sl.data(),
+                                       bl.data(), c.data(), (int)c.size(), st, &ev)
+                     : replay_bondsite(g, bf, site_order, nsites, bond_order, nbond, sl.data(),
+                                       bl.data(), c.data(), (int)c.size(), st, &ev);
+  if (rc) return rc;
+  *len = (long long)ev.size();
+  if (!trace) return PERC_OK;
+  if (cap < *len) return PERC_EINVAL;
+  std::memcpy(trace, ev.data(), sizeof(int) * ev.size());
+  return PERC_OK;
+}
+
 // the spanning cluster's Kirchhoff system (perc_conductance / perc_assemble)
 static int assemble_impl(perc_ctx* h, int rule, double g0, double leak, double Va, const char* who) {
   hipError_t e = dev_assemble(h, rule, g0, leak, Va, h->span_root);

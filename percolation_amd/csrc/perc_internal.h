@@ -287,12 +287,16 @@ int replay_bonds(const Geom& g, const std::vector<int>& bond_first, const int* o
 constexpr int kSiteTrace = 24;
 int replay_sites(const Geom& g, const int* order, int count, int* label, int* csize, int cap,
                  int* stats, int* trace = nullptr);
+// ev (optional): the debug log's event stream, one record per step of the
+// second phase (sbdebug.txt / bsdebug.txt; record layout in include/perc.h,
+// perc_replay_mixed_trace)
 int replay_bondsite(const Geom& g, const std::vector<int>& bond_first, const int* sorder,
                     int nsites, const int* border, int nbond, int* site_label, int* bond_label,
-                    int* csize, int cap, int* stats);
+                    int* csize, int cap, int* stats, std::vector<int>* ev = nullptr);
 int replay_sitebond(const Geom& g, const std::vector<int>& bond_first, const int* sorder,
                     int nsites, const int* border, int nbonds, int* site_label,
-                    int* bond_label, int* csize, int cap, int* stats);
+                    int* bond_label, int* csize, int cap, int* stats,
+                    std::vector<int>* ev = nullptr);
 
 int replay_bs_scan(const Geom& g, const std::vector<int>& bond_first, const int* sorder,
                    int nsites, const int* border, int nbond, bool c0_overflow);

@@ -242,7 +242,7 @@ int replay_sites(const Geom& g, const int* order, int count, int* label, int* cs
 
 int replay_sitebond(const Geom& g, const std::vector<int>& bond_first, const int* sorder,
                     int nsites, const int* border, int nbond, int* site_label, int* bond_label,
-                    int* csize, int cap, int* stats) {
+                    int* csize, int cap, int* stats, std::vector<int>* ev) {
   const long long nb = nbonds(g);
   if (cap < g.t + nb + 2) return PERC_EINVAL;
   std::vector<int> c(cap, 0);
@@ -250,16 +250,29 @@ int replay_sitebond(const Geom& g, const std::vector<int>& bond_first, const int
   std::vector<uint8_t> socc(g.t + 1, 0);
   std::vector<int> battach(nb, 0);  // >0: site whose cluster the bond follows; <0: own label
   DSU dsu(g.t + 1);
+  // log only: the sites and bonds (1-based list ids) each label holds, for
+  // the relabel lines of a merge (sitebond.f:317-334), printed in index order
+  std::vector<std::vector<int>> msite, mbond;
+  if (ev) {
+    msite.resize(cap);
+    mbond.resize(cap);
+  }
   int cln = 1;
   for (int i = 0; i < nsites; ++i) {  // sitebond.f:187-196
     const int sn = sorder[i];
     if (sn > 0 && sn <= g.t) {
       socc[sn] = 1;
       clab[sn] = cln;
+      if (ev) msite[cln].push_back(sn);
     }
     c[cln] = 1;
     ++cln;
   }
+  auto take = [&](std::vector<int>& v) {  // sorted member list, emptied
+    std::sort(v.begin(), v.end());
+    ev->push_back((int)v.size());
+    ev->insert(ev->end(), v.begin(), v.end());
+  };
   int maxcn = 1, maxcs = 1, lcn = 0;
   for (int i = 0; i < nbond; ++i) {  // sitebond.f:223-400
     const int id = border[i];
@@ -271,30 +284,48 @@ int replay_sitebond(const Geom& g, const std::vector<int>& bond_first, const int
       if (la == 0 && lb == 0) {
         battach[id - 1] = -cln;
         c[cln] = 1;
+        if (ev) ev->insert(ev->end(), {0, cln});
         ++cln;
       } else if (la > 0 && lb == 0) {
         lcn = la;
         battach[id - 1] = a;
         c[la] += 1;
+        if (ev) ev->insert(ev->end(), {1, a, lcn, c[lcn]});
       } else if (la == 0 && lb > 0) {
         lcn = lb;
         battach[id - 1] = b;
         c[lb] += 1;
+        if (ev) ev->insert(ev->end(), {2, b, lcn, c[lcn]});
       } else if (la == lb) {
         lcn = la;
         battach[id - 1] = a;
+        if (ev) ev->insert(ev->end(), {3, a, la, c[la], b, lb, c[lb], c[la] + 1});
         c[la] += 1;
       } else {
         int oldcn;
-        if (c[la] > c[lb]) { lcn = la; oldcn = lb; }
+        const bool a_big = c[la] > c[lb];
+        if (a_big) { lcn = la; oldcn = lb; }
         else { lcn = lb; oldcn = la; }
         const int clsum = c[lcn] + c[oldcn] + 1;
+        if (ev) {
+          ev->insert(ev->end(), {a_big ? 4 : 5, a, la, c[la], b, lb, c[lb]});
+          take(msite[oldcn]);
+          take(mbond[oldcn]);
+          ev->insert(ev->end(), {lcn, clsum, oldcn});
+          msite[lcn].insert(msite[lcn].end(), msite[oldcn].begin(), msite[oldcn].end());
+          mbond[lcn].insert(mbond[lcn].end(), mbond[oldcn].begin(), mbond[oldcn].end());
+          msite[oldcn].clear();
+          mbond[oldcn].clear();
+        }
         const int r = dsu.unite(a, b);
         clab[r] = lcn;
         battach[id - 1] = a;
         c[oldcn] = 0;
         c[lcn] = clsum;
       }
+      if (ev && battach[id - 1] > 0) mbond[lcn].push_back(id);
+    } else if (ev) {
+      ev->push_back(6);  // the spill slot (0, 0): no list row matches
     }
     if (c[lcn] > maxcs) { maxcs = c[lcn]; maxcn = lcn; }  // sitebond.f:387-390
   }
@@ -324,7 +355,7 @@ int replay_sitebond(const Geom& g, const std::vector<int>& bond_first, const int
 // intended one.  Union-find over bonds 0..nb-1 and sites nb+s.
 int replay_bondsite(const Geom& g, const std::vector<int>& bond_first, const int* sorder,
                     int nsites, const int* border, int nbond, int* site_label, int* bond_label,
-                    int* csize, int cap, int* stats) {
+                    int* csize, int cap, int* stats, std::vector<int>* ev) {
   const int nb = (int)nbonds(g), t = g.t;
   if (cap < t + nb + 2) return PERC_EINVAL;
   std::vector<int> c(cap, 0);
@@ -347,6 +378,7 @@ int replay_bondsite(const Geom& g, const std::vector<int>& bond_first, const int
     int lcn = 0;
     if (sn < 1 || sn > t) {  // spill slot: a one-site cluster with no site
       c[cln] = 1;
+      if (ev) ev->insert(ev->end(), {0, cln});
       ++cln;
     } else {
       int nn[6];
@@ -373,10 +405,17 @@ int replay_bondsite(const Geom& g, const std::vector<int>& bond_first, const int
       if (lcs == 0) {  // bondsite.f:264-274
         lab[node] = cln;
         c[cln] = 1;
+        if (ev) ev->insert(ev->end(), {0, cln});
         ++cln;
       } else {         // bondsite.f:278-313
         int clsum = lcs;
         int root = u.find(le);
+        size_t at = 0;
+        if (ev) {  // {1, k, k x (size added, largest cluster after), lcn, size}
+          ev->push_back(1);
+          at = ev->size();
+          ev->push_back(0);
+        }
         for (int k = 0; k < nr; ++k) {
           if (rl[k] == 0 || rl[k] == lcn) continue;
           bool dup = false;
@@ -384,12 +423,17 @@ int replay_bondsite(const Geom& g, const std::vector<int>& bond_first, const int
           if (!dup) {
             clsum += c[rl[k]];
             root = u.unite(root, re[k]);
+            if (ev) {
+              ev->insert(ev->end(), {c[rl[k]], clsum});
+              ++(*ev)[at];
+            }
           }
           c[rl[k]] = 0;
         }
         root = u.unite(root, node);
         lab[root] = lcn;
         c[lcn] = clsum + 1;
+        if (ev) ev->insert(ev->end(), {lcn, c[lcn]});
       }
     }
     if (c[lcn] > maxcs) {  // bondsite.f:316-319

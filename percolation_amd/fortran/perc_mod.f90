@@ -109,6 +109,17 @@ module perc_api
       type(c_ptr), value :: site_order, trace
     end function perc_replay_site_trace
 
+    ! sitebond.f / bondsite.f debug logs (sbdebug.txt / bsdebug.txt): event stream
+    integer(c_int) function perc_replay_mixed_trace(lattice, m, n, pbc, kind, nsites, site_order, &
+                                                    nbonds, bond_order, trace, cap, len) &
+        bind(C, name='perc_replay_mixed_trace')
+      import :: c_int, c_ptr, c_long_long
+      integer(c_int), value :: lattice, m, n, pbc, kind, nsites, nbonds
+      type(c_ptr), value :: site_order, bond_order, trace
+      integer(c_long_long), value :: cap
+      integer(c_long_long) :: len
+    end function perc_replay_mixed_trace
+
     integer(c_int) function perc_nbonds(lattice, m, n, pbc) bind(C, name='perc_nbonds')
       import :: c_int
       integer(c_int), value :: lattice, m, n, pbc
@@ -306,6 +317,47 @@ contains
     call perc_srand(seed)
     call perc_shuffle(nn, order)
   end subroutine perc_shuffled_ids
+
+  ! the trace logs' closing block (site.f:295-350, sitebond.f:408-465,
+  ! bondsite.f:358-418): largest cluster, then clusters 1..cln-1 of at least
+  ! minsize elements in label order tested for a bottom- and a top-row site
+  ! until one spans.  c(i + 1) is cluster i's size, s(1:t) the site labels;
+  ! numbered: the mixed programs print "testing cluster", i
+  subroutine perc_log_spanning(u, stats, c, s, m, t, minsize, numbered)
+    integer, intent(in) :: u
+    integer(c_int), intent(in) :: stats(4), c(:), s(:), m, t, minsize
+    logical, intent(in) :: numbered
+    integer(c_int) :: i
+    logical :: span
+    write(u, *)
+    write(u, *) "******************************"
+    write(u, *) "largest overall cluster number:", stats(2)
+    write(u, *) "largest overall cluster size:", stats(3)
+    span = .false.
+    do i = 1, stats(1) - 1
+      if (c(i + 1) < minsize) cycle
+      if (numbered) then
+        write(u, *) "testing cluster", i
+      else
+        write(u, *) "testing cluster"
+      end if
+      if (.not. any(s(1:m) == i)) then
+        write(u, *) "source end not connected"
+        cycle
+      end if
+      if (.not. any(s(t - m + 1:t) == i)) then
+        write(u, *) "drain end not connected"
+        cycle
+      end if
+      write(u, *) "infinite cluster present"
+      write(u, *) "infinite cluster number:", i
+      write(u, *) "infinite cluster size:", c(i + 1)
+      span = .true.
+      exit
+    end do
+    if (.not. span) write(u, *) "no infinite cluster present"
+    write(u, *) "******************************"
+  end subroutine perc_log_spanning
 
   ! an optional NAMELIST file overrides the reference parameter block
   logical function perc_have_file(name)

@@ -114,7 +114,7 @@ contains
   ! spanning test over clusters of at least n sites in label order, from the
   ! host replay's numbering (perc_replay_labels)
   subroutine write_siteocc()
-    integer(c_int) :: j, k, r, scn, sstats(4), span
+    integer(c_int) :: j, k, r, scn, sstats(4)
     integer(c_int), allocatable, target :: s(:), c(:)
     double precision :: f   ! site.f:40 (a double holding a single-precision quotient)
     scn = 4
@@ -149,31 +149,7 @@ contains
       write(11, *) "fraction of lattice filled:", f
       write(11, *) "--------------------"
     end do
-    write(11, *)
-    write(11, *) "******************************"
-    write(11, *) "largest overall cluster number:", sstats(2)
-    write(11, *) "largest overall cluster size:", sstats(3)
-    span = 0
-    do i = 1, sstats(1) - 1
-      if (c(i + 1) >= n) then
-        write(11, *) "testing cluster"
-        if (.not. any(s(1:m) == i)) then
-          write(11, *) "source end not connected"
-          cycle
-        end if
-        if (.not. any(s(t - m + 1:t) == i)) then
-          write(11, *) "drain end not connected"
-          cycle
-        end if
-        write(11, *) "infinite cluster present"
-        write(11, *) "infinite cluster number:", i
-        write(11, *) "infinite cluster size:", c(i + 1)
-        span = 1
-        exit
-      end if
-    end do
-    if (span == 0) write(11, *) "no infinite cluster present"
-    write(11, *) "******************************"
+    call perc_log_spanning(11, sstats, c, s, m, t, n, .false.)
     close(11)
   end subroutine write_siteocc
 end program site

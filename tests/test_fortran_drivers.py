@@ -255,23 +255,32 @@ def test_bondc_driver_trace_log(v, tmp_path):
     assert got == md["files"]["bondocc.txt"], v
 
 
-SITE_TRACE_VARIANTS = [v for v in G.variants() if "siteocc.txt" in G.meta(v).get("files", {})]
+TRACE_LOGS = [(v, f) for v in G.variants() for f in ("siteocc.txt", "sbdebug.txt", "bsdebug.txt")
+              if f in G.meta(v).get("files", {})]
 
 
-@pytest.mark.parametrize("v", SITE_TRACE_VARIANTS)
-def test_site_driver_trace_log(v, tmp_path):
-    """trace = 1: siteocc.txt -- every site's nearest neighbours, largest
-    neighbour cluster, absorbed clusters and fraction filled, then the
-    largest cluster and the spanning test, site.f:167-350 -- is the
-    reference run's byte for byte (md5 of the reference's own file).  The
-    driver writes it from the host replay before it opens the device, so
-    this runs with or without a GPU; with one the run must also finish."""
+@pytest.mark.parametrize("v,log", TRACE_LOGS)
+def test_driver_trace_logs(v, log, tmp_path):
+    """trace = 1: the per-step logs are the reference run's byte for byte
+    (md5 of the reference's own file, tests/golden/*/meta.json) --
+    siteocc.txt (site.f:167-350: each site's neighbours, largest neighbour
+    cluster and absorbed clusters), sbdebug.txt (sitebond.f:184-465: the
+    site phase, each bond's case with every site and bond a merge
+    relabels) and bsdebug.txt (bondsite.f:178-418), each with its closing
+    spanning test.  The drivers write them from the host replay before
+    they open a device, so this runs with or without a GPU; with one (or
+    for bondsite, which needs none) the run must also finish."""
     import hashlib
-    md, r = run_variant(v, tmp_path, expect_ok=have_gpu(), extra=["trace=1"])
-    got = hashlib.md5((tmp_path / "siteocc.txt").read_bytes()).hexdigest()
-    assert got == md["files"]["siteocc.txt"], v
-    if not have_gpu():
+    md, r = run_variant(v, tmp_path, expect_ok=have_gpu() or md_kind(v) == "bondsite",
+                        extra=["trace=1"])
+    got = hashlib.md5((tmp_path / log).read_bytes()).hexdigest()
+    assert got == md["files"][log], (v, log)
+    if not have_gpu() and md_kind(v) != "bondsite":
         assert "status -8" in r.stderr
+
+
+def md_kind(v):
+    return G.meta(v)["kind"]
 
 
 def test_replay_site_trace_records():
@@ -298,3 +307,60 @@ def test_replay_site_trace_records():
     bad[0] = m * n + 1
     assert lib.perc_replay_site_trace(0, m, n, 0, k, bad.ctypes.data, np.zeros(24 * k, np.int32)
                                       .ctypes.data) == -7
+
+
+def test_replay_mixed_trace_stream():
+    """perc_replay_mixed_trace's stream parses into one record per step,
+    its sizing call (trace = NULL) and a short buffer behave as declared,
+    and a merge's relabelled sites are exactly the absorbed cluster's
+    (checked against the replay's final labels: they all end in lcn's
+    cluster unless a later merge moved it)."""
+    import ctypes as C
+    import numpy as np
+    lib = PL.lib()
+    m = n = 12
+    t = m * n
+    nb = lib.perc_nbonds(0, m, n, 0)
+    rng = np.random.default_rng(5)
+    so = (rng.permutation(t) + 1).astype(np.int32)
+    bo = (rng.permutation(nb) + 1).astype(np.int32)
+    ts, tb = int(0.6 * t), int(0.6 * nb)
+    for kind, steps in ((PL.SITEBOND, tb), (PL.BONDSITE, ts)):
+        ln = C.c_longlong(0)
+        assert lib.perc_replay_mixed_trace(0, m, n, 0, kind, ts, so.ctypes.data, tb, bo.ctypes.data,
+                                           None, 0, C.byref(ln)) == 0
+        assert ln.value > steps
+        ev = np.zeros(ln.value, np.int32)
+        assert lib.perc_replay_mixed_trace(0, m, n, 0, kind, ts, so.ctypes.data, tb, bo.ctypes.data,
+                                           ev.ctypes.data, ln.value - 1, C.byref(ln)) == -1
+        assert lib.perc_replay_mixed_trace(0, m, n, 0, kind, ts, so.ctypes.data, tb, bo.ctypes.data,
+                                           ev.ctypes.data, ln.value, C.byref(ln)) == 0
+        r, recs, merges = 0, 0, 0
+        while r < len(ev):
+            e = ev[r]
+            if kind == PL.BONDSITE:
+                r += 2 if e == 0 else 4 + 2 * ev[r + 1]
+            elif e == 0:
+                r += 2
+            elif e in (1, 2):
+                r += 4
+            elif e == 3:
+                r += 8
+            elif e in (4, 5):
+                k = r + 7
+                ns = ev[k]
+                sites = ev[k + 1:k + 1 + ns]
+                assert ns >= 1 and (np.diff(sites) > 0).all()
+                k += 1 + ns
+                k += 1 + ev[k]
+                lcn, size, old = ev[k:k + 3]
+                assert old != lcn and size >= ns + 2
+                merges += 1
+                r = k + 3
+            else:
+                assert e == 6
+                r += 1
+            recs += 1
+        assert r == len(ev) and recs == steps
+        if kind == PL.SITEBOND:
+            assert merges > 0
