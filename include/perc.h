@@ -246,7 +246,10 @@ typedef struct {
 /* Assemble the interior Kirchhoff system of the chosen spanning component
    (CSR, diagonal first), solve it with the fused Jacobi-PCG that follows
    linbcg's operation order and stopping rule (itol 1 or 2), and compute
-   the terminal currents.  vint_out (optional, host, t-2m doubles). */
+   the terminal currents.  itol 3 / 4 (NR's step-size estimate in the L2 /
+   max norm, bondc.f:816-832; the reference calls only itol 2) run a plain
+   CSR PCG with per-iteration host folds; PERC_EITOL outside 1..4.
+   vint_out (optional, host, t-2m doubles). */
 int perc_conductance(perc_ctx *h, int rule, int cur_rule, double Va, double g0,
                      double leak, int itol, double tol, int itmax,
                      perc_cond_result *res, double *vint_out);

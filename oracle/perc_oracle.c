@@ -1016,17 +1016,28 @@ static double snrm2(int n, const double *sx) {
   return sqrt(s);
 }
 
+static double snrm_itol(int n, const double *sx, int itol) {
+  /* Square/bondc.f:867-884: sum of squares for itol <= 3, else the first
+     largest |sx(i)| */
+  int i, im = 0;
+  if (itol <= 3) return snrm2(n, sx);
+  for (i = 1; i < n; i++)
+    if (fabs(sx[i]) > fabs(sx[im])) im = i;
+  return fabs(sx[im]);
+}
+
 void or_linbcg(const double *sa, const int *ija, int n, const double *b,
                double *x, int itol, double tol, int itmax, int *iter_o,
                double *err_o, double *iter_err) {
-  /* Square/bondc.f:750-838, literal (itol 1 and 2) */
+  /* Square/bondc.f:750-838, literal (itol 1..4) */
   double *p = (double *)calloc((size_t)n, sizeof(double));
   double *pp = (double *)calloc((size_t)n, sizeof(double));
   double *r = (double *)calloc((size_t)n, sizeof(double));
   double *rr = (double *)calloc((size_t)n, sizeof(double));
   double *z = (double *)calloc((size_t)n, sizeof(double));
   double *zz = (double *)calloc((size_t)n, sizeof(double));
-  double ak, akden, bk, bkden = 1.0, bknum, bnrm, err = 0.0;
+  const double EPS = 1.00e-14; /* bondc.f:753 */
+  double ak, akden, bk, bkden = 1.0, bknum, bnrm, err = 0.0, znrm = 1.0, zm1nrm;
   int j, iter = 0;
   or_dsprsax(sa, ija, x, r, n);
   for (j = 0; j < n; j++) { r[j] = b[j] - r[j]; rr[j] = r[j]; }
@@ -1034,11 +1045,16 @@ void or_linbcg(const double *sa, const int *ija, int n, const double *b,
     bnrm = snrm2(n, b);
   } else {
     for (j = 0; j < n; j++) z[j] = b[j] / sa[j];
-    bnrm = snrm2(n, z);
+    bnrm = snrm_itol(n, z, itol);
+    if (itol >= 3) { /* bondc.f:771-775 */
+      for (j = 0; j < n; j++) z[j] = r[j] / sa[j];
+      znrm = snrm_itol(n, z, itol);
+    }
   }
   for (j = 0; j < n; j++) z[j] = r[j] / sa[j];
   while (iter <= itmax) {
     iter++;
+    zm1nrm = znrm;
     for (j = 0; j < n; j++) zz[j] = rr[j] / sa[j];
     bknum = 0.0;
     for (j = 0; j < n; j++) bknum = bknum + z[j] * rr[j];
@@ -1063,7 +1079,28 @@ void or_linbcg(const double *sa, const int *ija, int n, const double *b,
       rr[j] = rr[j] - ak * zz[j];
     }
     for (j = 0; j < n; j++) z[j] = r[j] / sa[j];
-    err = snrm2(n, r) / bnrm;
+    if (itol <= 2) {
+      err = snrm2(n, r) / bnrm;
+    } else { /* bondc.f:816-832: the step-size estimate; the goto 100
+                branches iterate on without the tolerance test */
+      znrm = snrm_itol(n, z, itol);
+      if (iter_err) iter_err[iter - 1] = znrm / bnrm;
+      if (fabs(zm1nrm - znrm) > EPS * znrm) {
+        err = znrm / fabs(zm1nrm - znrm) * (fabs(ak) * snrm_itol(n, p, itol));
+      } else {
+        err = znrm / bnrm;
+        continue;
+      }
+      {
+        const double xnrm = snrm_itol(n, x, itol);
+        if (err <= 0.50 * xnrm) {
+          err = err / xnrm;
+        } else {
+          err = znrm / bnrm;
+          continue;
+        }
+      }
+    }
     if (iter_err) iter_err[iter - 1] = err;
     if (!(err > tol)) break;
   }

@@ -780,8 +780,8 @@ int perc_conductance(perc_ctx* h, int rule, int cur_rule, double Va, double g0, 
                      int itol, double tol, int itmax, perc_cond_result* res, double* vint_out) {
   if (!h || !res) return PERC_EINVAL;
   if (!h->labeled) return PERC_ESTATE;
-  if (itol != 1 && itol != 2) {
-    set_error("perc_conductance: itol 3/4 not implemented on the device path");
+  if (itol < 1 || itol > 4) {
+    set_error("perc_conductance: illegal itol (1..4)");
     return PERC_EITOL;
   }
   if (rule < PERC_RULE_BOND || rule > PERC_RULE_MIXED || itmax < 0) return PERC_EINVAL;

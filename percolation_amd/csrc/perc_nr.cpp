@@ -297,11 +297,6 @@ static void linbcg_impl(int* n_, double* b, double* x, int* itol, double* tol, i
     g_status = PERC_EITOL;
     return;
   }
-  if (*itol > 2) {
-    set_error("linbcg_: itol 3/4 not implemented on the device path");
-    g_status = PERC_EITOL;
-    return;
-  }
   std::vector<int> rowptr, col;
   std::vector<double> val, diag;
   g_status = nr_to_csr(sa, ija, n, rowptr, col, val, diag);

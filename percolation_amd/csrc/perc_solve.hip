@@ -725,6 +725,252 @@ hipError_t host_fold_b(perc_ctx* h, const CGArgs& a, HostFold& hf) {
   return hipStreamSynchronize(st);
 }
 
+// linbcg with itol 3 or 4 (bondc.f:771-775, 816-832): the stopping test is
+// NR's step-size estimate |z| / |z(k-1) - z| * |ak| |p| / |x| in the L2
+// (itol 3) or max (itol 4) norm, so every iteration needs |z|, |p| and |x|
+// besides the two dots.  The reference only calls itol 2 (its drivers) and
+// this mode is for linbcg_'s other callers: plain row-major kernels on the
+// CSR operator, three launches per iteration (p update; q = A p with p.q;
+// x, r update with z.r and the three norms), block partials summed on the
+// host in block order each iteration -- not the march's single-pass design.
+// kX34Grid blocks stride over the rows.
+constexpr int kX34Grid = 1024;
+
+template <bool MAXN>
+__device__ __forceinline__ double x34_norm(double acc, double v) {
+  return MAXN ? fmax(acc, fabs(v)) : acc + v * v;
+}
+// v[0] summed, v[1..K-1] norm-combined, over the block; thread 0 writes
+// out[blockIdx.x * 4 + k]
+template <int K, bool MAXN>
+__device__ __forceinline__ void x34_block(double (&v)[K], double* out) {
+  __shared__ double s[K][kBlock / 64];
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    double x = v[k];
+    for (int o = 32; o > 0; o >>= 1) {
+      const double y = __shfl_xor(x, o);
+      x = (k == 0 || !MAXN) ? x + y : fmax(x, y);
+    }
+    if ((threadIdx.x & 63) == 0) s[k][threadIdx.x >> 6] = x;
+  }
+  __syncthreads();
+  if (threadIdx.x < K) {
+    const int k = threadIdx.x;
+    double x = s[k][0];
+    for (int w = 1; w < kBlock / 64; ++w) x = (k == 0 || !MAXN) ? x + s[k][w] : fmax(x, s[k][w]);
+    out[blockIdx.x * 4 + k] = x;
+  }
+}
+__device__ __forceinline__ double x34_row(const CsrView& A, const double* __restrict__ x, int i) {
+  double ax = A.diag[i] * x[i];
+  for (int j = A.rowptr[i]; j < A.rowptr[i + 1]; ++j) ax = ax + A.val[j] * x[A.col[j]];
+  return ax;
+}
+// r = b - A x; {z.r, |D^-1 b|, |D^-1 r|}
+template <bool MAXN>
+__global__ __launch_bounds__(kBlock) void k_x34_init(CsrView A, const double* __restrict__ b,
+                                                     const double* __restrict__ x,
+                                                     double* __restrict__ r, double* out) {
+  double v[3] = {0.0, 0.0, 0.0};
+  for (int i = blockIdx.x * kBlock + threadIdx.x; i < A.N; i += gridDim.x * kBlock) {
+    const double di = A.diag[i], ri = b[i] - x34_row(A, x, i);
+    r[i] = ri;
+    v[0] = v[0] + (ri / di) * ri;
+    v[1] = x34_norm<MAXN>(v[1], b[i] / di);
+    v[2] = x34_norm<MAXN>(v[2], ri / di);
+  }
+  x34_block<3, MAXN>(v, out);
+}
+// p = z (first) or bk p + z, z = r / d (bondc.f:789-797)
+__global__ __launch_bounds__(kBlock) void k_x34_p(CsrView A, const double* __restrict__ r,
+                                                  double* __restrict__ p, double bk, int first) {
+  for (int i = blockIdx.x * kBlock + threadIdx.x; i < A.N; i += gridDim.x * kBlock) {
+    const double z = r[i] / A.diag[i];
+    p[i] = first ? z : bk * p[i] + z;
+  }
+}
+// q = A p; {p.q} (bondc.f:799-805)
+__global__ __launch_bounds__(kBlock) void k_x34_qp(CsrView A, const double* __restrict__ p,
+                                                   double* __restrict__ q, double* out) {
+  double v[1] = {0.0};
+  for (int i = blockIdx.x * kBlock + threadIdx.x; i < A.N; i += gridDim.x * kBlock) {
+    const double qi = x34_row(A, p, i);
+    q[i] = qi;
+    v[0] = v[0] + qi * p[i];
+  }
+  x34_block<1, false>(v, out);
+}
+// x += ak p, r -= ak q (bondc.f:808-812); {z.r, |z|, |p|, |x|}
+template <bool MAXN>
+__global__ __launch_bounds__(kBlock) void k_x34_upd(CsrView A, double* __restrict__ x,
+                                                    double* __restrict__ r,
+                                                    const double* __restrict__ p,
+                                                    const double* __restrict__ q, double ak,
+                                                    double* out) {
+  double v[4] = {0.0, 0.0, 0.0, 0.0};
+  for (int i = blockIdx.x * kBlock + threadIdx.x; i < A.N; i += gridDim.x * kBlock) {
+    const double xi = x[i] + ak * p[i], ri = r[i] - ak * q[i], z = ri / A.diag[i];
+    x[i] = xi;
+    r[i] = ri;
+    v[0] = v[0] + z * ri;
+    v[1] = x34_norm<MAXN>(v[1], z);
+    v[2] = x34_norm<MAXN>(v[2], p[i]);
+    v[3] = x34_norm<MAXN>(v[3], xi);
+  }
+  x34_block<4, MAXN>(v, out);
+}
+
+struct X34Scratch {
+  double *r = nullptr, *p = nullptr, *q = nullptr, *part = nullptr;
+  ~X34Scratch() {
+    for (double* v : {r, p, q, part})
+      if (v) (void)hipFree(v);
+  }
+};
+
+hipError_t dev_solve_x34(perc_ctx* h, int itol, double tol, int itmax, int* iter, double* err) {
+  HIP_TRY(ensure_csr(h));
+  if (!h->csr_ok) {
+    set_error("linbcg itol 3/4: no CSR copy of the system");
+    return hipErrorInvalidValue;
+  }
+  const int N = h->N;
+  const bool MX = itol == 4;
+  hipStream_t st = h->stream;
+  const CsrView A = make_cg_args(h).A;
+  const int G = std::max(1, std::min(kX34Grid, cdiv(N, kBlock)));
+  X34Scratch w;
+  HIP_TRY(dmalloc(&w.r, (size_t)N));
+  HIP_TRY(dmalloc(&w.p, (size_t)N));
+  HIP_TRY(dmalloc(&w.q, (size_t)N));
+  HIP_TRY(dmalloc(&w.part, (size_t)4 * G));
+  std::vector<double> part(4 * (size_t)G);
+  double sum[4];
+  // the literal dot orders (perc_set_dot_order, linbcg_'s default): the
+  // vectors come to the host and every sum and norm is formed there in
+  // ascending j as bondc.f:785-787, 803-805, 867-884 form them (host code
+  // has no contraction or reassociation; the device's elementwise x, r, p,
+  // q, z are the reference's expressions, so the iterates are its bitwise)
+  const bool lit = h->dot_order != PERC_DOT_FAST;
+  std::vector<double> hd, hv[3];
+  if (lit) {
+    hd.resize(N);
+    for (auto& v : hv) v.resize(N);
+    HIP_TRY(hipMemcpyAsync(hd.data(), A.diag, sizeof(double) * N, hipMemcpyDeviceToHost, st));
+  }
+  auto snrm = [&](const double* v, bool div) {  // snrm of v (or of v / d)
+    if (!MX) {
+      double a = 0.0;
+      for (int j = 0; j < N; ++j) {
+        const double t = div ? v[j] / hd[j] : v[j];
+        a = a + t * t;
+      }
+      return std::sqrt(a);
+    }
+    double a = std::fabs(div ? v[0] / hd[0] : v[0]);
+    for (int j = 1; j < N; ++j) a = std::max(a, std::fabs(div ? v[j] / hd[j] : v[j]));
+    return a;
+  };
+  auto zdot = [&](const double* r) {  // sum z(j) rr(j), z = r / d
+    double a = 0.0;
+    for (int j = 0; j < N; ++j) a = a + (r[j] / hd[j]) * r[j];
+    return a;
+  };
+  auto get = [&](int k, const double* dv) {
+    return hipMemcpyAsync(hv[k].data(), dv, sizeof(double) * N, hipMemcpyDeviceToHost, st);
+  };
+  auto fold = [&](int K) -> hipError_t {  // block partials in block order
+    HIP_TRY(hipMemcpyAsync(part.data(), w.part, sizeof(double) * 4 * G, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    for (int k = 0; k < K; ++k) {
+      double v = part[k];
+      for (int g = 1; g < G; ++g) v = (k == 0 || !MX) ? v + part[4 * g + k] : std::max(v, part[4 * g + k]);
+      sum[k] = (k == 0 || MX) ? v : std::sqrt(v);
+    }
+    return hipSuccess;
+  };
+  h->last_kernel = 0;  // (other launched kernels)
+  if (MX) k_x34_init<true><<<G, kBlock, 0, st>>>(A, h->d.rhs, h->d.x, w.r, w.part);
+  else k_x34_init<false><<<G, kBlock, 0, st>>>(A, h->d.rhs, h->d.x, w.r, w.part);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(fold(3));
+  if (lit) {  // bondc.f:772-775 and the first bknum
+    HIP_TRY(get(0, h->d.rhs));
+    HIP_TRY(get(1, w.r));
+    HIP_TRY(hipStreamSynchronize(st));
+    sum[1] = snrm(hv[0].data(), true);
+    sum[2] = snrm(hv[1].data(), true);
+    sum[0] = zdot(hv[1].data());
+  }
+  constexpr double kEps = 1.00e-14;  // bondc.f:753
+  double bknum = sum[0], bnrm = sum[1], znrm = sum[2], bkden = 1.0, e = 0.0;
+  std::vector<double> hist;
+  int k = 0;
+  while (k <= itmax) {  // bondc.f:780
+    ++k;
+    const double zm1nrm = znrm;
+    k_x34_p<<<G, kBlock, 0, st>>>(A, w.r, w.p, k == 1 ? 0.0 : bknum / bkden, k == 1);
+    bkden = bknum;
+    k_x34_qp<<<G, kBlock, 0, st>>>(A, w.p, w.q, w.part);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(fold(1));
+    if (lit) {
+      HIP_TRY(get(0, w.p));
+      HIP_TRY(get(1, w.q));
+      HIP_TRY(hipStreamSynchronize(st));
+      double a = 0.0;
+      for (int j = 0; j < N; ++j) a = a + hv[1][j] * hv[0][j];
+      sum[0] = a;
+    }
+    const double ak = bknum / sum[0];
+    if (MX) k_x34_upd<true><<<G, kBlock, 0, st>>>(A, h->d.x, w.r, w.p, w.q, ak, w.part);
+    else k_x34_upd<false><<<G, kBlock, 0, st>>>(A, h->d.x, w.r, w.p, w.q, ak, w.part);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(fold(4));
+    if (lit) {  // (hv[0] still holds this iteration's p)
+      HIP_TRY(get(1, w.r));
+      HIP_TRY(get(2, h->d.x));
+      HIP_TRY(hipStreamSynchronize(st));
+      sum[0] = zdot(hv[1].data());
+      sum[1] = snrm(hv[1].data(), true);
+      sum[2] = snrm(hv[0].data(), false);
+      sum[3] = snrm(hv[2].data(), false);
+    }
+    bknum = sum[0];
+    znrm = sum[1];
+    bool test = false;
+    if (std::fabs(zm1nrm - znrm) > kEps * znrm) {
+      e = znrm / std::fabs(zm1nrm - znrm) * (std::fabs(ak) * sum[2]);
+      if (e <= 0.50 * sum[3]) {
+        e = e / sum[3];
+        test = true;
+      } else {
+        e = znrm / bnrm;  // goto 100: no tolerance test this iteration
+      }
+    } else {
+      e = znrm / bnrm;
+    }
+    hist.push_back(e);
+    if (test && !(e > tol)) break;
+  }
+  if (h->d.err_hist && h->d.err_hist_cap > 0 && !hist.empty())
+    HIP_TRY(hipMemcpyAsync(h->d.err_hist, hist.data(),
+                           sizeof(double) * std::min<size_t>(hist.size(), h->d.err_hist_cap),
+                           hipMemcpyHostToDevice, st));
+  CGScalars hs{};  // (perc_err_history reads the count from the scalars)
+  hs.iter = k;
+  hs.err = e;
+  hs.tol = tol;
+  hs.itmax = itmax;
+  hs.done = 1;
+  HIP_TRY(hipMemcpyAsync(h->d.scal, &hs, sizeof(hs), hipMemcpyHostToDevice, st));
+  HIP_TRY(hipStreamSynchronize(st));
+  *iter = k;
+  *err = e;
+  return hipSuccess;
+}
+
 hipError_t dev_solve_impl(perc_ctx* h, int itol, double tol, int itmax, bool x0_zero, bool full_x,
                           int* iter, double* err) {
   DeviceBuffers& d = h->d;
@@ -750,6 +996,7 @@ hipError_t dev_solve_impl(perc_ctx* h, int itol, double tol, int itmax, bool x0_
   if (x0_zero) {
     k_zero<<<blocks_for(h->N + 2), kBlock, 0, st>>>(d.x, h->N + 2);
   }
+  if (itol >= 3) return dev_solve_x34(h, itol, tol, itmax, iter, err);
   // row slabs (perc_set_slabs; the prologue starts from x = 0, as linbcg's
   // callers do)
   if (h->nslab > 1 && x0_zero) {
