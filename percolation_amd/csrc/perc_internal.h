@@ -121,6 +121,8 @@ struct DeviceBuffers {
   double* res_xch = nullptr;    // resident solve: exchange rows
   unsigned* res_bar = nullptr;
   double* res_gran = nullptr;   // resident solve: tagged partial granules
+  unsigned* res_reg = nullptr;  // resident solve: XCD registration counters
+  double* res_xg = nullptr;     // resident solve: XCD-grouped reduction granules
   double* lit = nullptr;        // literal dot order: the q.p, z.r, r.r terms (3 N) of the
                                 // q-free march and the resident solve
 };

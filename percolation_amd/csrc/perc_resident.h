@@ -20,22 +20,22 @@ namespace {
 // holds columns t + j NT, j < MT, of every own row).  Per iteration (the
 // order of linbcg, bondc.f:780-835, every per-row operation as in the other
 // kernels):
-//   1. p = bk p + r/d (z = r/d at k = 1) into LDS; the band's first and last
-//      rows also to a write-through exchange buffer;  grid barrier
-//   2. q = A p from LDS and the neighbours' exchanged rows; q.p;  barrier
-//   3. every workgroup sums the q.p partials in workgroup order (the same
-//      value everywhere): ak; r -= ak q, z = r/d, z.r, r.r, x += ak p on
-//      the rows x is kept on;  barrier;  bk, err, stop test (identical in
-//      every workgroup, so all leave the loop together)
-// Three grid barriers and no launches per iteration: at L = 1024 an
-// iteration of the launched kernels is ~28 us, almost all fixed costs.
-// The grid barrier counts arrivals per XCD group (blocks b, b+8, ..), after
-// each workgroup's write-through stores are complete (s_waitcnt
-// vmcnt(0)); m = 1024 polls the 8 group counters directly, m = 2048 has the
-// last arriver of a group bump one top counter (res_barrier); data crossing workgroups is
-// written and read with sc1 (agent-scope) accesses, as in
-// publish_and_reduce.  A wait that exceeds ~1 s sets an error flag and
-// leaves the kernel instead of hanging the device.
+//   1. p = bk p + r/d (z = r/d at k = 1) into LDS, and p(k) of the
+//      neighbours' rows next to the band from their exchanged r(k-1) and
+//      p(k-1) with the same arithmetic (no barrier);
+//   2. q = A p, q.p;  grid-wide reduction -> ak (the same everywhere);
+//   3. r -= ak q, z = r/d, z.r, r.r, x += ak p on the rows x is kept on; the
+//      band's first and last rows of r(k) and p(k) to the exchange
+//      (write-through, parity-buffered);  grid-wide reduction -> bk, err,
+//      stop test (identical in every workgroup, so all leave together)
+// Two grid-wide reductions and no launches per iteration (an iteration of
+// the launched kernels at L = 1024 is ~28 us, almost all fixed costs).  The
+// reductions: res_allreduce_x (XCD-grouped, the default) or res_gather (flat
+// all-gather).  One grid barrier before the loop (res_barrier) publishes the
+// first exchange rows; data crossing workgroups is written and read with
+// sc1 (agent-scope) accesses, as in publish_and_reduce.  A wait that
+// exceeds ~1 s sets an error flag and leaves the kernel instead of hanging
+// the device.
 constexpr int kResThreads = 1024;
 constexpr int kResLdsRows = 16384;  // own-row p elements per workgroup (128 KB)
 constexpr unsigned kResSquareMask = 0x5Au;  // raster positions (-1,0) (0,-1) (0,1) (1,0)
@@ -58,8 +58,16 @@ struct ResArgs {
   // ascending j by workgroup 0 (res_fold); nullptr in the fast order (the
   // term stores then go to a zero-size buffer view and are dropped)
   double* lit;
+  // XCD-grouped reductions (res_allreduce_x): registration counters (8 per-XCD
+  // + 1 arrival, kTicketStride apart) and the granules: level 1
+  // [kind][j][xcd][kResXcdMax], level 2 [kind][parity][j][xcd] (zeroed
+  // before the launch)
+  unsigned* reg;
+  double* xg;
 };
 constexpr int kResLitGran = 4;
+constexpr int kResXcdMax = 64;  // workgroups per XCD the grouped reductions take
+constexpr size_t kResXgDoubles = 2 * (2 * 2 * 8 * kResXcdMax + 2 * 2 * 2 * 8);
 
 
 // single-level (m = 1024: 0.0166 vs 0.0178 ms per iteration)
@@ -201,6 +209,177 @@ __device__ __forceinline__ bool res_gather(const ResArgs& a, unsigned& epoch, do
   const bool ok = s_red[30] != 0.0;
   __syncthreads();  // s_red reuse by the next block_sum
   return ok;
+}
+
+// XCD-grouped all-reduction (the fast order's two reductions per iteration).
+// At the start of the launch every workgroup reads the XCD it runs on
+// (HW_REG_XCC_ID) and takes a rank there; when the G workgroups sit G/8 on
+// each XCD, a workgroup's LOGICAL id -- the band of rows it owns -- is xcd
+// * G/8 + rank (res_register).  The association of a reduction is then
+// fixed in logical ids whatever the placement: level 1 sums the XCD's G/8
+// partials in rank order, level 2 the 8 XCD totals in XCD order.  Level 1
+// crosses no XCD: the workgroups store their 16-B {value, tag} granules
+// plainly (kept in the XCD's L2) and the XCD's rank-0 workgroup reads them
+// with sc1 loads (past its L1, served by the same L2); it then publishes
+// the XCD total write-through, and wave 0 of every workgroup polls the 8
+// XCD granules (parity-buffered: a fast XCD's next total must not replace
+// one a slow workgroup has yet to read).  The two reductions (1 + 2 values) of an
+// iteration cost 7.9 vs 12.2 us for the flat all-gather at G = 256, 1024
+// threads (tools/sync_bench.hip, profiles/r5_18_sync_bench.log).  Any
+// other placement (G not a multiple of 8, or an XCD holding more or fewer
+// than G/8 workgroups) ends the grouped launch at once and the host runs
+// the flat instantiation (kResPadUneven).
+#if defined(PERC_RES_FLAT)  // (A/B probe builds only: the flat all-gather everywhere)
+constexpr bool kResXcdGather = false;
+#else
+constexpr bool kResXcdGather = true;
+#endif
+// S->pad[1] of a grouped launch (k_cg_res<..., XG = true>) that found the
+// placement uneven: every workgroup left before touching any state, and
+// the host runs the flat instantiation instead
+constexpr int kResPadUneven = 1;
+struct ResXcd {
+  int w;     // logical workgroup id (the band)
+  int xcd, rank, nx;
+  bool ok;   // grouped reductions (else res_gather, w = blockIdx.x)
+};
+__device__ __forceinline__ ResXcd res_register(const ResArgs& a, int* s_flag) {
+  __shared__ int s_x[4];
+  if (threadIdx.x == 0) {
+    const int G = a.G;
+    const int x = (int)(__builtin_amdgcn_s_getreg((3 << 11) | 20) & 7u);  // HW_REG_XCC_ID
+    const unsigned r = __hip_atomic_fetch_add(&a.reg[x * kTicketStride], 1u, __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_fetch_add(&a.reg[8 * kTicketStride], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    int ok = 1;
+    for (unsigned spin = 0; __hip_atomic_load(&a.reg[8 * kTicketStride], __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT) < (unsigned)G;
+         ++spin) {
+      if (spin > (1u << 25)) {  // ~1 s: the grid is not co-resident
+        a.S->pad[0] = 1;
+        ok = 0;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+    bool even = G % 8 == 0 && G / 8 <= kResXcdMax;
+    for (int y = 0; y < 8 && even; ++y)
+      even = __hip_atomic_load(&a.reg[y * kTicketStride], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+             (unsigned)(G / 8);
+    s_x[0] = even ? x * (G / 8) + (int)r : (int)blockIdx.x;
+    s_x[1] = x;
+    s_x[2] = (int)r;
+    s_x[3] = even ? 1 : 0;
+    s_flag[1] = ok;
+  }
+  __syncthreads();
+  ResXcd X;  // (workgroup-uniform: scalar registers, not VGPRs, across the loop)
+  X.w = __builtin_amdgcn_readfirstlane(s_x[0]);
+  X.xcd = __builtin_amdgcn_readfirstlane(s_x[1]);
+  X.rank = __builtin_amdgcn_readfirstlane(s_x[2]);
+  X.nx = a.G / 8;
+  X.ok = __builtin_amdgcn_readfirstlane(s_x[3]) != 0;
+  return X;
+}
+
+// The block sum is part of it: every wave's lane 0 leaves its wave's sums
+// in s_red, and behind the one workgroup barrier wave 0 adds the waves'
+// values (lane-parallel + butterfly) and publishes; a second barrier hands
+// the totals (s_res) to the workgroup.  The waves' stores are drained by the
+// first barrier, before the granule that releases them is issued.
+template <int NV>
+__device__ __forceinline__ bool res_allreduce_x(const ResArgs& a, unsigned& epoch, int kind, const ResXcd& X,
+                                                const double (&v)[NV], double (&tot)[NV], double* s_red,
+                                                double* s_res) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+#pragma unroll
+  for (int j = 0; j < NV; ++j) {
+    const double t = wave_sum(v[j]);
+    if (lane == 0) s_red[wid * NV + j] = t;
+  }
+  __syncthreads();  // every wave's sums in LDS and its stores complete (release)
+  ++epoch;
+  if (threadIdx.x < 64) {
+    const double tag = (double)epoch;
+    const int par = (epoch >> 1) & 1;  // the kinds alternate: a kind's epochs step by 2
+    const __amdgpu_buffer_rsrc_t r1 = rsrc(a.xg, (unsigned)(2 * 2 * 8 * kResXcdMax * 16));
+    const __amdgpu_buffer_rsrc_t r2 = rsrc(a.xg + 2 * 2 * 2 * 8 * kResXcdMax, (unsigned)(2 * 2 * 2 * 8 * 16));
+    auto o1 = [&](int j, int r) { return (((kind * 2 + j) * 8 + X.xcd) * kResXcdMax + r) * 16; };
+    auto o2 = [&](int j, int x) { return (((kind * 2 + par) * 2 + j) * 8 + x) * 16; };
+    double wv[NV];
+#pragma unroll
+    for (int j = 0; j < NV; ++j) wv[j] = wave_sum(lane < nw ? s_red[lane * NV + j] : 0.0);
+    if (lane == 0)
+#pragma unroll
+      for (int j = 0; j < NV; ++j)  // plain 16-B stores: the line stays in this XCD's L2
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, make_double2(wv[j], tag)), r1,
+                                               o1(j, X.rank), 0, 0);
+    int ok = 1;
+    if (X.rank == 0) {  // the XCD's partials in rank order, then its total write-through
+      double acc[NV];
+      for (unsigned spin = 0;; ++spin) {
+        bool all = true;
+#pragma unroll
+        for (int j = 0; j < NV; ++j) {
+          acc[j] = 0.0;
+          if (lane < X.nx) {
+            const double2 g2 = __builtin_bit_cast(
+                double2, __builtin_amdgcn_raw_buffer_load_b128(r1, o1(j, lane), 0, 16));
+            all = all && g2.y == tag;
+            acc[j] = g2.x;
+          }
+        }
+        if (__builtin_amdgcn_readfirstlane(__all(all))) break;
+        if (spin > (1u << 24)) {
+          ok = 0;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+#pragma unroll
+      for (int j = 0; j < NV; ++j) {
+        const double t = wave_sum(acc[j]);
+        if (lane == 0)
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, make_double2(t, tag)), r2,
+                                                 o2(j, X.xcd), 0, 16);
+      }
+    }
+    double acc[NV];
+    for (unsigned spin = 0; ok; ++spin) {  // the 8 XCD totals, lanes 0..7
+      bool all = true;
+#pragma unroll
+      for (int j = 0; j < NV; ++j) {
+        acc[j] = 0.0;
+        if (lane < 8) {
+          const double2 g2 =
+              __builtin_bit_cast(double2, __builtin_amdgcn_raw_buffer_load_b128(r2, o2(j, lane), 0, 16));
+          all = all && g2.y == tag;
+          acc[j] = g2.x;
+        }
+      }
+      if (__builtin_amdgcn_readfirstlane(__all(all))) break;
+      if (spin > (1u << 24)) {
+        ok = 0;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+#pragma unroll
+    for (int j = 0; j < NV; ++j) {
+      const double t = wave_sum(acc[j]);
+      if (lane == 0) s_res[j] = t;
+    }
+    if (lane == 0) {
+      s_res[7] = ok ? 1.0 : 0.0;
+      if (!ok) a.S->pad[0] = 1;
+    }
+  }
+  // (wave 0 has read s_red before this barrier, and every wave reads s_res
+  // before the next reduction's first barrier: neither needs another one)
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < NV; ++j) tot[j] = s_res[j];
+  return s_res[7] != 0.0;
 }
 
 // The literal dot order inside the resident solve (bondc.f:785-787, 803-805,
@@ -380,15 +559,29 @@ __device__ __forceinline__ void res_pos_u(double& acc, unsigned mask, unsigned& 
 // loop is the fast instantiation's (a separate instantiation because the
 // fold's registers would otherwise join the fast loop's allocation: 122 ->
 // 256 VGPRs with spills at m = 1024)
-template <int MT, int HMAX, bool QREG = true, unsigned UMC = 0xFFu, int NT = kResThreads, bool LIT = false>
+// XG: the XCD-grouped reductions (res_register / res_allreduce_x); without
+// it the flat all-gather (res_gather), the literal folds, w = blockIdx.x
+template <int MT, int HMAX, bool QREG = true, unsigned UMC = 0xFFu, int NT = kResThreads, bool LIT = false,
+          bool XG = false>
 __global__ __launch_bounds__(NT) void k_cg_res(ResArgs a) {
   __shared__ double s_p[kResLdsRows];
   __shared__ double2 s_dt[kDiagTab];
   __shared__ unsigned s_rmap[kMaxForms], s_umask[kMaxForms];
   __shared__ double s_red[32];
+  __shared__ double s_res[8];
   __shared__ int s_flag[2];
   int t = threadIdx.x;  // re-made opaque each iteration when !QREG (below)
-  const int w = blockIdx.x;
+  // the band this workgroup owns: its logical id (res_register) with the
+  // grouped reductions, else its block index
+  ResXcd X{(int)blockIdx.x, 0, 0, 0, false};
+  if constexpr (XG) {
+    X = res_register(a, s_flag);
+    if (!X.ok || !s_flag[1]) {  // (uniform: every workgroup read the same counters)
+      if (blockIdx.x == 0 && threadIdx.x == 0 && s_flag[1]) a.S->pad[kResPadUneven] = 1;
+      return;
+    }
+  }
+  const int w = X.w;
   const int m = a.m, nrows = a.nrows, N = a.St.N, G = a.G;
   const int R0 = w * a.H, Hw = min(a.H, nrows - R0);  // >= 1 (host sizes G)
   // one column per thread below m = 1024, the workgroup rounded up to whole
@@ -604,8 +797,13 @@ __global__ __launch_bounds__(NT) void k_cg_res(ResArgs a) {
         if (!(ok = res_fold<1>(a, epoch, a.gran, 0, tot, s_red))) break;
       } else {
         double v1[1] = {dot};
-        block_sum<1>(v1, s_red);
-        if (!(ok = res_gather<1>(a, epoch, a.gran, v1, tot, s_red))) break;
+        if constexpr (XG) {
+          ok = res_allreduce_x<1>(a, epoch, 0, X, v1, tot, s_red, s_res);
+        } else {
+          block_sum<1>(v1, s_red);
+          ok = res_gather<1>(a, epoch, a.gran, v1, tot, s_red);
+        }
+        if (!ok) break;
       }
       ak = bknum / tot[0];
     }
@@ -658,8 +856,13 @@ __global__ __launch_bounds__(NT) void k_cg_res(ResArgs a) {
       if constexpr (LIT) {
         if (!(ok = res_fold<2>(a, epoch, a.gran + 2 * (size_t)G, 1, tot, s_red))) break;
       } else {
-        block_sum<2>(acc2, s_red);
-        if (!(ok = res_gather<2>(a, epoch, a.gran + 2 * (size_t)G, acc2, tot, s_red))) break;
+        if constexpr (XG) {
+          ok = res_allreduce_x<2>(a, epoch, 1, X, acc2, tot, s_red, s_res);
+        } else {
+          block_sum<2>(acc2, s_red);
+          ok = res_gather<2>(a, epoch, a.gran + 2 * (size_t)G, acc2, tot, s_red);
+        }
+        if (!ok) break;
       }
       err = sqrt(tot[1]) / bnrm;
       bk = tot[0] / bknum;

@@ -328,6 +328,8 @@ hipError_t dev_build_lattice(perc_ctx* h) {
     HIP_TRY(dmalloc(&d.res_xch, (size_t)2 * h->res_G * 2 * 2 * g.m));
     HIP_TRY(dmalloc(&d.res_bar, 9 * kTicketStride));
     HIP_TRY(dmalloc(&d.res_gran, (size_t)2 * (3 * h->res_G + kResLitGran)));
+    HIP_TRY(dmalloc(&d.res_reg, 9 * kTicketStride));
+    HIP_TRY(dmalloc(&d.res_xg, kResXgDoubles));
   }
   HIP_TRY(dmalloc(&d.partials, kRedSlots * red_partials_size(red_grid(h))));
   HIP_TRY(dmalloc(&d.tickets, kRedSlots * red_tickets_size(red_grid(h))));
@@ -372,7 +374,7 @@ void dev_free_all(perc_ctx* h) {
                   d.p0, d.p1, d.q, d.partials, d.tickets, d.scal, d.err_hist, d.iout,
                   d.res_xch, d.res_bar, d.bw, d.code_sm, d.csize, d.res_gran, (void*)d.nib_sm,
                   d.sel_hist, d.sel_cand, d.mgran, d.forms_dev, d.lit, d.ccpart, d.ell_col, d.ell_val,
-                  d.ell_cnt};
+                  d.ell_cnt, d.res_reg, d.res_xg};
   for (void* p : ptrs)
     if (p) hipFree(p);
   d = DeviceBuffers{};
@@ -551,22 +553,33 @@ hipError_t to_strips(perc_ctx* h, CGArgs& a) {
 
 // The resident solve's synchronisation floor (perc_bench_kernel 6): the
 // same cooperative grid running only what an iteration of k_cg_res does to
-// synchronise -- the two block sums and the two tagged-granule all-gathers
-// (res_gather<1>, res_gather<2>) -- on dummy values, `iters` times.  The
-// time per iteration is what the resident solve cannot go below whatever
-// its memory traffic.
+// synchronise -- the two block sums and the two grid-wide reductions
+// (res_allreduce_x, or res_gather where the placement falls back) -- on dummy
+// values, `iters` times.  The time per iteration is what the resident solve
+// cannot go below whatever its memory traffic.
 __global__ __launch_bounds__(1024) void k_res_sync_probe(ResArgs a, int iters) {
   __shared__ double s_red[32];
+  __shared__ double s_res[8];
+  __shared__ int s_flag[2];
+  const ResXcd X = res_register(a, s_flag);
   unsigned epoch = 0;
-  double v1[1] = {(double)blockIdx.x}, tot1[1], acc2[2], tot2[2];
-  for (int k = 0; k < iters; ++k) {
+  double v1[1] = {(double)X.w}, tot1[1], acc2[2], tot2[2];
+  for (int k = 0; k < iters && s_flag[1]; ++k) {
     double w1[1] = {v1[0] + (double)threadIdx.x};
-    block_sum<1>(w1, s_red);
-    if (!res_gather<1>(a, epoch, a.gran, w1, tot1, s_red)) break;
+    if (X.ok) {
+      if (!res_allreduce_x<1>(a, epoch, 0, X, w1, tot1, s_red, s_res)) break;
+    } else {
+      block_sum<1>(w1, s_red);
+      if (!res_gather<1>(a, epoch, a.gran, w1, tot1, s_red)) break;
+    }
     acc2[0] = tot1[0] * 1e-30 + (double)threadIdx.x;
     acc2[1] = (double)k;
-    block_sum<2>(acc2, s_red);
-    if (!res_gather<2>(a, epoch, a.gran + 2 * (size_t)a.G, acc2, tot2, s_red)) break;
+    if (X.ok) {
+      if (!res_allreduce_x<2>(a, epoch, 1, X, acc2, tot2, s_red, s_res)) break;
+    } else {
+      block_sum<2>(acc2, s_red);
+      if (!res_gather<2>(a, epoch, a.gran + 2 * (size_t)a.G, acc2, tot2, s_red)) break;
+    }
     v1[0] = tot2[0] * 1e-30;
   }
 }
@@ -576,20 +589,22 @@ __global__ __launch_bounds__(1024) void k_res_sync_probe(ResArgs a, int iters) {
 // (NT threads per workgroup, m of them for m <= 1024: with one column per
 // thread the template's NT is only the launch bound, so widths up to 512
 // share the 512-bound instantiation -- 125-142 VGPRs, no spills)
-template <bool LIT>
+template <bool LIT, bool XG>
 const void* res_kernel_t(int MT, bool sq, int NT) {
   if (MT == 1 && NT <= 512)
-    return sq ? (const void*)k_cg_res<1, 4, true, kResSquareMask, 512, LIT>
-              : (const void*)k_cg_res<1, 4, true, 0xFFu, 512, LIT>;
+    return sq ? (const void*)k_cg_res<1, 4, true, kResSquareMask, 512, LIT, XG>
+              : (const void*)k_cg_res<1, 4, true, 0xFFu, 512, LIT, XG>;
   if (MT == 1)
-    return sq ? (const void*)k_cg_res<1, 4, true, kResSquareMask, kResThreads, LIT>
-              : (const void*)k_cg_res<1, 4, true, 0xFFu, kResThreads, LIT>;
-  return sq ? (const void*)k_cg_res<2, 8, false, kResSquareMask, kResThreads, LIT>
-            : (const void*)k_cg_res<2, 8, false, 0xFFu, kResThreads, LIT>;
+    return sq ? (const void*)k_cg_res<1, 4, true, kResSquareMask, kResThreads, LIT, XG>
+              : (const void*)k_cg_res<1, 4, true, 0xFFu, kResThreads, LIT, XG>;
+  return sq ? (const void*)k_cg_res<2, 8, false, kResSquareMask, kResThreads, LIT, XG>
+            : (const void*)k_cg_res<2, 8, false, 0xFFu, kResThreads, LIT, XG>;
 }
-// (lit: the literal dot order's instantiation, LIT = true)
-const void* res_kernel(int MT, bool sq, int NT, bool lit) {
-  return lit ? res_kernel_t<true>(MT, sq, NT) : res_kernel_t<false>(MT, sq, NT);
+// (lit: the literal dot order's instantiation, LIT = true, whose reductions
+// are serial folds; xg: the fast order's XCD-grouped reductions)
+const void* res_kernel(int MT, bool sq, int NT, bool lit, bool xg) {
+  if (lit) return res_kernel_t<true, false>(MT, sq, NT);
+  return xg && kResXcdGather ? res_kernel_t<false, true>(MT, sq, NT) : res_kernel_t<false, false>(MT, sq, NT);
 }
 
 // one cooperative launch runs the whole iteration loop (k_cg_res)
@@ -613,14 +628,22 @@ hipError_t dev_solve_resident(perc_ctx* h, const CGArgs& ca, int* iter, double* 
   a.bar = d.res_bar;
   a.gran = d.res_gran;
   a.lit = ca.lit;
+  a.reg = d.res_reg;
+  a.xg = d.res_xg;
   HIP_TRY(hipMemsetAsync(d.res_bar, 0, 9 * kTicketStride * sizeof(unsigned), st));
+  HIP_TRY(hipMemsetAsync(d.res_reg, 0, 9 * kTicketStride * sizeof(unsigned), st));
+  HIP_TRY(hipMemsetAsync(d.res_xg, 0, kResXgDoubles * sizeof(double), st));
   HIP_TRY(hipMemsetAsync(d.res_gran, 0, (size_t)2 * (3 * h->res_G + kResLitGran) * sizeof(double), st));
   void* args[] = {&a};
   // reductions by tagged-granule all-gather (res_gather): L = 1024 15.5 vs
   // 16.6 us per iteration against a counter barrier + partial reads, L =
   // 2048 33.7 vs 34.65 (profiles/r2_10_resident_gather_ab.log)
   const bool sq = (h->forms.umask & ~kResSquareMask) == 0;
-  const void* fn = res_kernel(h->res_MT, sq, h->res_NT, a.lit != nullptr);
+  // (PERC_RES_FLAT=1 in the environment: the flat all-gather instantiation,
+  // for tests of that fallback)
+  const char* flat_env = std::getenv("PERC_RES_FLAT");
+  const bool xg = !(flat_env && flat_env[0] == '1');
+  const void* fn = res_kernel(h->res_MT, sq, h->res_NT, a.lit != nullptr, xg);
   KernelTiming& T = h->timing;
   if (T.enabled) {
     if (T.ev.size() < 2) T.ev.resize(2, nullptr);
@@ -634,6 +657,16 @@ hipError_t dev_solve_resident(perc_ctx* h, const CGArgs& ca, int* iter, double* 
   CGScalars hs{};
   HIP_TRY(hipMemcpyAsync(&hs, d.scal, sizeof(hs), hipMemcpyDeviceToHost, st));
   HIP_TRY(hipStreamSynchronize(st));
+  if (hs.pad[kResPadUneven] != 0) {
+    // the grouped launch found the workgroups spread unevenly over the XCDs
+    // and left at once: the flat all-gather instantiation runs the solve
+    fn = res_kernel(h->res_MT, sq, h->res_NT, a.lit != nullptr, false);
+    HIP_TRY(hipLaunchCooperativeKernel(fn, dim3(a.G), dim3(h->res_NT), args, 0, st));
+    HIP_TRY(dbg_sync(st, "k_cg_res"));
+    if (T.enabled) HIP_TRY(hipEventRecord(T.ev[1], st));
+    HIP_TRY(hipMemcpyAsync(&hs, d.scal, sizeof(hs), hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+  }
   if (hs.pad[0] != 0) {
     fprintf(stderr, "[perc] k_cg_res: grid barrier timed out\n");
     return hipErrorLaunchTimeOut;
@@ -1275,10 +1308,14 @@ hipError_t dev_bench(perc_ctx* h, int which, int reps, double* ms) {
       ResArgs ra{};
       ra.G = h->res_G;
       ra.gran = d.res_gran;
+      ra.reg = d.res_reg;
+      ra.xg = d.res_xg;
       ra.S = d.scal;
       int iters = 16;
       void* args[] = {&ra, &iters};
       (void)hipMemsetAsync(d.res_gran, 0, (size_t)2 * 3 * h->res_G * sizeof(double), st);
+      (void)hipMemsetAsync(d.res_reg, 0, 9 * kTicketStride * sizeof(unsigned), st);
+      (void)hipMemsetAsync(d.res_xg, 0, kResXgDoubles * sizeof(double), st);
       // a refused grid (CUs taken) must not time an empty stream
       const hipError_t le = hipLaunchCooperativeKernel((const void*)k_res_sync_probe, dim3(ra.G),
                                                        dim3(h->res_NT), args, 0, st);

@@ -748,9 +748,9 @@ def test_table_division_is_ieee_division():
                                            (0, 100, 150, 0, 0.6)])
 def test_resident_solve_matches_march(lat, m, n, pbc, p):
     """The persistent resident solve (one cooperative launch, p in LDS,
-    three grid barriers per iteration; bands of 1..4 rows per CU) against
-    the launched march kernels: same per-row arithmetic, so the same solve
-    up to the association of the dots."""
+    two grid-wide reductions per iteration; bands of 1..4 rows per CU)
+    against the launched march kernels: same per-row arithmetic, so the
+    same solve up to the association of the dots."""
     nb = api.nbonds(lat, m, n, pbc)
     order = api.shuffled_ids(nb, 2024)
     out = {}
@@ -771,6 +771,37 @@ def test_resident_solve_matches_march(lat, m, n, pbc, p):
     assert abs(cr["iter"] - cm["iter"]) <= 2
     assert rel(cr["gtop"], cm["gtop"]) < REL and rel(cr["gbot"], cm["gbot"]) < REL
     assert np.max(np.abs(cr["vint"] - cm["vint"])) < 1e-6
+
+
+@pytest.mark.parametrize("lat,m,n,p", [(0, 1024, 1024, 0.5), (1, 1024, 1024, 0.42), (0, 2048, 600, 0.55),
+                                       (0, 512, 300, 0.6)])
+def test_resident_grouped_and_flat_reductions(lat, m, n, p, monkeypatch):
+    """The resident solve's two reduction transports (perc_resident.h):
+    the XCD-grouped all-reduction (default; workgroups take their bands by
+    XCD and rank) and the flat all-gather it falls back to when the
+    workgroups sit unevenly on the XCDs (forced here with PERC_RES_FLAT=1):
+    the same solve up to the association of the sums, and each repeatable
+    bitwise (the grouped association is fixed in logical ids, whatever the
+    placement)."""
+    nb = api.nbonds(lat, m, n, 0)
+    order = api.shuffled_ids(nb, 77)
+    out = {}
+    with api.Context(lat, m, n, 0) as ctx:
+        ctx.occupy(PL.BOND, bond_order=order, nbonds_=int(p * nb))
+        if ctx.label()["nspan"] == 0:
+            pytest.skip("no spanning cluster")
+        for flat in ("0", "1"):
+            monkeypatch.setenv("PERC_RES_FLAT", flat)
+            a = ctx.conductance(tol=1e-12, itmax=200000, vint=True)
+            assert ctx.last_solve()["kernel"] == "resident"
+            b = ctx.conductance(tol=1e-12, itmax=200000, vint=True)
+            assert (a["iter"], a["gtop"], a["gbot"]) == (b["iter"], b["gtop"], b["gbot"]), flat
+            assert np.array_equal(a["vint"], b["vint"]), flat
+            out[flat] = a
+    g, f = out["0"], out["1"]
+    assert abs(g["iter"] - f["iter"]) <= 2
+    assert rel(g["gtop"], f["gtop"]) < REL and rel(g["gbot"], f["gbot"]) < REL
+    assert np.max(np.abs(g["vint"] - f["vint"])) < 1e-6
 
 
 @pytest.mark.parametrize("kind,rule,lat,m,n,ps,pb", [(PL.BOND, PL.RULE_BOND, 0, 64, 64, 0, 0.6),
