@@ -279,6 +279,29 @@ int main(int argc, char** argv) {
       };
       chain(kind == PERC_SITE ? "site: generic merge" : "mixed: generic merge", tilek, mgen, true);
       chain(kind == PERC_SITE ? "site: square merge" : "mixed: square merge", tilek, msq, false);
+      // tile height (16 in production) against 8 and 32: the merge's
+      // block-top rows scale as 1/H, the tile's per-row work does not
+      auto by_h = [&](auto hconst, const char* what) {
+        constexpr int HH = decltype(hconst)::value;
+        const int GH = cdiv(g.m, kCcW) * cdiv(g.n, HH), nfh = g.n / HH;
+        const int GMh = nfh * nseg + (ntx - 1) * cdiv(g.n, kCcThreads);
+        chain(what, [&, GH]() {
+          if (kind == PERC_SITE)
+            k_cc_tile_w<HH, PERC_SITE, 2, true><<<GH, 64>>>(g, R.bocc, R.socc, R.parent, R.member, (unsigned)nb + 8u);
+          else
+            k_cc_tile_w<HH, PERC_SITEBOND, 2, true><<<GH, 64>>>(g, R.bocc, R.socc, R.parent, R.member,
+                                                                (unsigned)nb + 8u);
+        }, [&, nfh, GMh]() {
+          if (kind == PERC_SITE)
+            k_cc_merge_sq<HH, PERC_SITE><<<GMh, kCcThreads>>>(g, R.bocc, R.socc, R.parent, R.member, nseg, nfh,
+                                                               nullptr);
+          else
+            k_cc_merge_sq<HH, PERC_SITEBOND><<<GMh, kCcThreads>>>(g, R.bocc, R.socc, R.parent, R.member, nseg,
+                                                                   nfh, nullptr);
+        }, false);
+      };
+      by_h(std::integral_constant<int, 8>{}, kind == PERC_SITE ? "site: 8-row tiles" : "mixed: 8-row tiles");
+      by_h(std::integral_constant<int, 32>{}, kind == PERC_SITE ? "site: 32-row tiles" : "mixed: 32-row tiles");
     }
   }
   return 0;
