@@ -102,10 +102,77 @@ __device__ __forceinline__ void gran_poll_n(__amdgpu_buffer_rsrc_t rg, const int
   }
 }
 
+// Fixed collectors instead of tickets (the default; PERC_MARCH_TICKETS, A/B
+// probe builds only: the ticket form below): a group's LAST logical
+// workgroup (lb = g0 + gn - 1, dispatched late: logical blocks of an XCD are
+// consecutive) sums its group's granules as they arrive and publishes the
+// group's granule; the last group's collector sums the group granules.  The
+// association is the ticket form's term for term (the group's lanes in
+// order + butterfly; the groups thread-strided + block sum), so every value
+// is bitwise the same; what goes is the two agent-scope ticket atomics (and
+// their resets) on the tail's critical path: the collectors only poll.
 template <int NV>
 __device__ bool publish_and_reduce_tagged(double (&v)[NV], double* gran, unsigned* tickets, int lb,
                                           int nwg, double tag, int* err, double (&tot)[NV],
                                           double* s_red, int* s_flag) {
+#if !defined(PERC_MARCH_TICKETS)
+  (void)tickets;
+  (void)s_flag;
+  block_sum<NV>(v, s_red);
+  const int ngroups = red_groups(nwg);
+  const int grp = lb / kGroup, g0 = grp * kGroup, gn = min(kGroup, nwg - g0);
+  const __amdgpu_buffer_rsrc_t rg = rsrc(gran, (unsigned)(NV * (nwg + ngroups) * 16));
+  const int goff = NV * nwg;
+  if (threadIdx.x == 0) {
+#pragma unroll
+    for (int j = 0; j < NV; ++j)
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, make_double2(v[j], tag)), rg,
+                                             (j * nwg + lb) * 16, 0, 16);
+  }
+  if (lb != g0 + gn - 1) return false;  // (uniform) not a collector
+  if (threadIdx.x < 64) {  // the group's collector: wave 0 sums the group's partials
+    const int lane = threadIdx.x;
+    double w[NV];
+    if (lane < gn) {
+      int off[NV];
+#pragma unroll
+      for (int j = 0; j < NV; ++j) off[j] = (j * nwg + g0 + lane) * 16;
+      gran_poll_n<NV>(rg, off, tag, err, w);
+    } else {
+#pragma unroll
+      for (int j = 0; j < NV; ++j) w[j] = 0.0;
+    }
+#pragma unroll
+    for (int j = 0; j < NV; ++j) w[j] = wave_sum(w[j]);
+    if (lane == 0)
+#pragma unroll
+      for (int j = 0; j < NV; ++j)
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, make_double2(w[j], tag)), rg,
+                                               (goff + j * ngroups + grp) * 16, 0, 16);
+  }
+  if (grp != ngroups - 1) return false;  // (uniform)
+  double acc[NV];
+#pragma unroll
+  for (int j = 0; j < NV; ++j) acc[j] = 0.0;
+  for (int i = threadIdx.x; i < ngroups; i += blockDim.x) {
+    int off[NV];
+    double gv[NV];
+#pragma unroll
+    for (int j = 0; j < NV; ++j) off[j] = (goff + j * ngroups + i) * 16;
+    gran_poll_n<NV>(rg, off, tag, err, gv);
+#pragma unroll
+    for (int j = 0; j < NV; ++j) acc[j] = acc[j] + gv[j];
+  }
+  __syncthreads();  // s_red reuse
+  block_sum<NV>(acc, s_red);
+  if (threadIdx.x == 0)
+#pragma unroll
+    for (int j = 0; j < NV; ++j) s_red[16 + j] = acc[j];
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < NV; ++j) tot[j] = s_red[16 + j];
+  return true;
+#else
   block_sum<NV>(v, s_red);
   const int ngroups = red_groups(nwg);
   const int grp = lb / kGroup, g0 = grp * kGroup, gn = min(kGroup, nwg - g0);
@@ -175,6 +242,7 @@ __device__ bool publish_and_reduce_tagged(double (&v)[NV], double* gran, unsigne
 #pragma unroll
   for (int j = 0; j < NV; ++j) tot[j] = s_red[16 + j];
   return true;
+#endif
 }
 
 constexpr int kMarchW = 128;     // columns per wave strip
