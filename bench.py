@@ -489,6 +489,10 @@ def main():
     ap.add_argument("--concurrent", type=int, default=1,
                     help="realisations in flight per GPU (one context and stream each); the "
                          "per-kernel roofline timings then overlap")
+    ap.add_argument("--inflight", type=int, default=2,
+                    help="after the timed region (K = 1, one GPU, bond, launched march): the "
+                         "same realisations again with this many in flight, reported as "
+                         "in_flight (0 / 1: skip); never `value`")
     ap.add_argument("--march-mode", type=int, default=-1,
                     help="perc_set_march_mode bits (perc.h PERC_MARCH_*); -1: library default")
     ap.add_argument("--format", choices=("auto", "stencil", "stencil_tiled", "stencil_split", "csr"),
@@ -827,6 +831,39 @@ def main():
     if devocc and rank == 0:
         labeling = labeling_probe(ctx, P, L_, nb, tb, [int(seeds[ii_list[k]]) for k in timed][:4],
                                   args.kind, ts if args.kind != "bond" else 0)
+    # realisations in flight (one context and stream each): what a throughput
+    # run of the ensemble gets from one GPU -- the march kernels' fixed costs
+    # (ramp, walk-end spread, reduction tail) of one solve are filled by the
+    # other's work.  Reported beside `value` (K = 1), whose per-kernel
+    # roofline it would blur.
+    in_flight = None
+    if (args.inflight > 1 and K == 1 and world == 1 and devocc and args.kind == "bond"
+            and minfo.get("kernel") != "resident" and timed):
+        K2 = args.inflight
+        mode0 = args.march_mode if args.march_mode >= 0 else P.MARCH_DEFAULT
+        pool_ctx = [ctx] + [make_ctx() for _ in range(K2 - 1)]
+        for c in pool_ctx:
+            c.set_march_mode(mode0 & ~P._lib.SOLVE_RESIDENT)
+            c.set_kernel_timing(False)
+        ks2 = (timed * (2 * K2))[:2 * K2]
+        from concurrent.futures import ThreadPoolExecutor
+        lanes2 = [[k for j, k in enumerate(ks2) if j % K2 == ci] for ci in range(K2)]
+        torch.cuda.synchronize()
+        t_if = time.perf_counter()
+        with ThreadPoolExecutor(K2) as pool:
+            futs = [pool.submit(lambda ks_, c_: [run_(k_, c_) for k_ in ks_], lanes2[ci], pool_ctx[ci])
+                    for ci in range(K2)]
+            res2 = [r_ for f in futs for r_ in f.result()]
+        torch.cuda.synchronize()
+        t_if = time.perf_counter() - t_if
+        for c in pool_ctx[1:]:
+            c.close()
+        ctx.set_march_mode(mode0)
+        in_flight = {"k": K2, "realisations": len(ks2), "value": round(len(ks2) / t_if, 5),
+                     "unit": "solves/s", "ms_per_step": round(t_if / len(ks2) * 1e3, 2),
+                     "cg_iterations_mean": round(float(np.mean([r_["iter"] for r_ in res2])), 1),
+                     "note": "the timed realisations again, %d in flight (one context and stream "
+                             "each), after the timed region; not `value`" % K2}
     copy_ms = ctx.bench_kernel(4, 20)
     copy_bytes = 2 * 8 * (64 << 20)  # 512 MB read + 512 MB written (perc_bench_kernel 4)
     stream_copy = {"ms": round(copy_ms, 5), "bytes": copy_bytes,
@@ -912,6 +949,8 @@ def main():
     }
     if labeling is not None:
         out["labeling"] = labeling
+    if in_flight is not None:
+        out["in_flight"] = in_flight
     if rank == 0 and world == 1 and args.kind == "bond" and devocc:
         out["pcie_inclusive"] = {"note": "occupancy drawn on the device: no host array crosses "
                                          "PCIe per realisation"}
