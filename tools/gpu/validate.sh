@@ -16,5 +16,7 @@ step smoke 200 python -u -c "import __graft_entry__ as g; g.smoke(); print('smok
 tail -1 gpurun_out/val_smoke.log
 step bench 400 python -u bench.py
 tail -1 gpurun_out/val_bench.log | cut -c1-400
-step benchprof 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/val_prof -o bench -- python3 -u bench.py --steps 2 --warmup 1 --no-cpu-baseline
+step benchprof 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/val_prof -o bench -- python3 -u bench.py --steps 2 --warmup 1 --no-cpu-baseline --inflight 0
 tail -1 gpurun_out/val_benchprof.log | cut -c1-300
+# (the per-dispatch trace is tens of MB: only the summaries come back)
+rm -f gpurun_out/val_prof/bench_kernel_trace.csv
