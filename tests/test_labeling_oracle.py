@@ -172,6 +172,39 @@ def test_mixed_partition_vs_oracle(geom, ps, pb):
     check(li, *oracle_mixed(lat, m, n, pbc, sids, ts, bids, tb))
 
 
+# ------------------------------------------------------------ GPU: the open square lattice's wave tiles
+# (k_cc_tile_w: 128 x 16 blocks, ballot masks for site / mixed; k_cc_merge_sq)
+# at widths and heights on either side of the block edges, near each kind's
+# threshold and far above it
+SQ_OPEN = [(127, 15), (128, 16), (129, 17), (255, 31), (257, 33), (384, 100), (513, 47), (64, 129),
+           (3, 40), (300, 3), (130, 4)]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("m,n", SQ_OPEN)
+@pytest.mark.parametrize("kind", [PL.BOND, PL.SITE, PL.SITEBOND])
+def test_open_square_block_edges_vs_oracle(m, n, kind):
+    t, nb = m * n, api.nbonds(0, m, n, 0)
+    rng = np.random.default_rng(m * 1000 + n + kind)
+    for p in (rng.uniform(0.45, 0.55), rng.uniform(0.6, 0.75), 0.95):
+        if kind == PL.BOND:
+            ids = _perm_ids(nb, int(rng.integers(1 << 30)))
+            tb = int(p * nb)
+            li = gpu_label(0, m, n, 0, PL.BOND, bids=ids, tb=tb)
+            check(li, *oracle_bond(0, m, n, 0, ids, tb))
+        elif kind == PL.SITE:
+            ids = _perm_ids(t, int(rng.integers(1 << 30)))
+            ts = int((p + 0.1 if p < 0.9 else p) * t)
+            li = gpu_label(0, m, n, 0, PL.SITE, sids=ids, ts=min(ts, t))
+            check(li, *oracle_site(0, m, n, 0, ids, min(ts, t)))
+        else:
+            sids = _perm_ids(t, int(rng.integers(1 << 30)))
+            bids = _perm_ids(nb, int(rng.integers(1 << 30)))
+            ts, tb = int(min(p + 0.15, 1.0) * t), int(min(p + 0.1, 1.0) * nb)
+            li = gpu_label(0, m, n, 0, PL.SITEBOND, sids=sids, ts=ts, bids=bids, tb=tb)
+            check(li, *oracle_mixed(0, m, n, 0, sids, ts, bids, tb))
+
+
 # ------------------------------------------------------------ GPU: BASELINE config sizes
 @pytest.mark.gpu
 def test_metric_bond_4096_partition_vs_oracle():
