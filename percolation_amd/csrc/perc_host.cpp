@@ -269,6 +269,7 @@ int perc_ctx_destroy(perc_ctx* h) {
   for (int i = 0; i < 8; ++i)
     if (h->ev[i]) hipEventDestroy(h->ev[i]);
   for (hipEvent_t e : h->timing.ev) hipEventDestroy(e);
+  if (h->pin) hipHostFree(h->pin);
   if (h->stream) hipStreamDestroy(h->stream);
   delete h;
   return PERC_OK;

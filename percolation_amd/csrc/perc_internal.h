@@ -159,6 +159,9 @@ struct DSlab;
 struct perc_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
+  // pinned host words for the labeling's read-back (a copy into pageable
+  // memory is staged by the runtime)
+  int* pin = nullptr;
   perc::Geom g{};
   long long nb = 0;
   int N = 0;       // interior rows t-2m

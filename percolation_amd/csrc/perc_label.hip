@@ -676,8 +676,16 @@ static hipError_t label_finish(perc_ctx* h, int* nspan, int* span_list, int* ncl
   if (g.m < kSpanLds) k_span_top<true><<<1, 1024, 0, st>>>(g, d.parent, d.member, d.top, d.counters, part, npart);
   else k_span_top<false><<<1, 1024, 0, st>>>(g, d.parent, d.member, d.top, d.counters, part, npart);
   HIP_TRY(dbg_sync(st, "k_span_top"));
-  int hc[8 + kMaxSpanList];
-  HIP_TRY(hipMemcpyAsync(hc, d.counters, sizeof(hc), hipMemcpyDeviceToHost, st));
+  constexpr int kHc = 8 + kMaxSpanList;
+#if defined(PERC_LABEL_PAGEABLE)  // (A/B probe builds only: a stack array)
+  int hcs[kHc];
+  const int* hc = hcs;
+  HIP_TRY(hipMemcpyAsync(hcs, d.counters, sizeof(hcs), hipMemcpyDeviceToHost, st));
+#else
+  if (!h->pin) HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&h->pin), sizeof(int) * kHc));
+  const int* hc = h->pin;
+  HIP_TRY(hipMemcpyAsync(h->pin, d.counters, sizeof(int) * kHc, hipMemcpyDeviceToHost, st));
+#endif
   HIP_TRY(hipStreamSynchronize(st));
   *nspan = hc[0];
   *nclusters = hc[1];
