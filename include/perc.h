@@ -84,6 +84,15 @@ int perc_ctx_create(int device, int lattice, int m, int n, int pbc, perc_ctx **o
 int perc_ctx_destroy(perc_ctx *h);
 /* last HIP error string for diagnostics (never NULL) */
 const char *perc_last_error(void);
+/* One HIP runtime per process: the number of distinct libamdhip64 objects
+   mapped in the process (dl_iterate_phdr), their paths ';'-separated into
+   buf (cap bytes, may be NULL), the copy libperc's own calls bind to
+   (dladdr of hipGetDeviceCount) first.  Two copies -- e.g. /opt/rocm's,
+   loaded with libperc, and a framework's bundled one loaded later -- share
+   one device through two runtimes and corrupt the heap at process exit;
+   perc_ctx_create refuses to run then (PERC_ESTATE, the paths in
+   perc_last_error). */
+int perc_hip_runtimes(char *buf, int cap);
 
 /* ---- occupancy + labeling -------------------------------------------- */
 /* Occupy the first `count` entries of `order` (1-based bond ids for
@@ -517,10 +526,16 @@ int perc_set_dot_order(perc_ctx *h, int order);
 #define PERC_RAN_NIBBLE 16    /* 4-bit row codes */
 #define PERC_RAN_TAG 32       /* tagged-granule reductions */
 #define PERC_RAN_HOST_FOLD 64 /* PERC_DOT_LITERAL_HOST: the sums folded by the host */
+#define PERC_RAN_XCD_GROUPED 128 /* resident solve: XCD-grouped reductions (else the flat all-gather) */
 int perc_last_solve(perc_ctx *h, int *out4);
 /* err of every iteration of the last solve (linbcg's per-iteration
    `write (*,*) iter, err`, bondc.f:834): min(cap, iterations) values into
-   out; returns the iteration count (>= 0) or a negative status */
+   out, entry k - 1 = err of iteration k; returns the iteration count (>= 0)
+   or a negative status.  itol 3 / 4: EVERY iteration has its entry, also
+   those where linbcg takes `goto 100` (bondc.f:822-831) and prints nothing;
+   there the entry is the err linbcg set before the jump, znrm / bnrm -- so
+   the history has more entries than the reference's log, which holds only
+   the tested iterations.  itol 1 / 2: entry for entry the reference's log. */
 int perc_err_history(perc_ctx *h, double *out, int cap);
 /* Random bond conductances (MATLAB/ConductCalc.m condtype 2, :38-47 and
    :94-97): the bonds of the spanning cluster get G = -g0 * w[id] instead of

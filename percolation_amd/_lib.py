@@ -33,6 +33,7 @@ DOT_FAST, DOT_LITERAL, DOT_LITERAL_HOST = 0, 1, 2
 # perc_last_solve: kernel family and flag bits of the last solve
 RAN_OTHER, RAN_MARCH, RAN_SLABS, RAN_RESIDENT, RAN_SMALL = 0, 1, 2, 3, 4
 RAN_LITERAL, RAN_LIT_TERMS, RAN_QFREE, RAN_STRIPS, RAN_NIBBLE, RAN_TAG, RAN_HOST_FOLD = 1, 2, 4, 8, 16, 32, 64
+RAN_XCD_GROUPED = 128
 XPORT_RCCL, XPORT_HOST, XPORT_EXCHANGE = 0, 1, 4
 DSLAB_ID_BYTES = 128
 
@@ -82,6 +83,7 @@ SIGNATURES = {
     "perc_ctx_create": (C.c_int, [C.c_int] * 5 + [C.POINTER(C.c_void_p)]),
     "perc_ctx_destroy": (C.c_int, [_VP]),
     "perc_last_error": (C.c_char_p, []),
+    "perc_hip_runtimes": (C.c_int, [C.c_char_p, C.c_int]),
     "perc_occupy": (C.c_int, [_VP, C.c_int, C.c_int, _VP, C.c_int, _VP]),
     "perc_label": (C.c_int, [_VP, C.POINTER(LabelInfo), _VP]),
     "perc_label_numbers": (C.c_int, [_VP, _VP, _VP, _VP, C.c_int, _VP]),
@@ -196,6 +198,62 @@ def _one_runtime():
         pass
 
 
+def _torch_runtime():
+    """the libamdhip64 torch would load (its bundled copy), found without
+    importing torch; None if torch or its bundled runtime is absent"""
+    import importlib.util
+    try:
+        spec = importlib.util.find_spec("torch")
+    except (ImportError, ValueError):
+        return None
+    if spec is None or not spec.origin:
+        return None
+    p = os.path.join(os.path.dirname(spec.origin), "lib", "libamdhip64.so")
+    return os.path.realpath(p) if os.path.exists(p) else None
+
+
+class _SecondRuntimeGuard:
+    """sys.meta_path entry installed when libperc was loaded on a HIP runtime
+    other than torch's bundled one (PERC_NO_TORCH=1, or torch not importable
+    then): a later `import torch` would map a second runtime into the
+    process, so it raises PercError before torch's libraries load -- the
+    invariant is checked, not left to the import order"""
+
+    def __init__(self, ours, theirs):
+        self.ours, self.theirs = ours, theirs
+
+    def find_spec(self, name, path=None, target=None):
+        if name == "torch":
+            raise PercError("import torch after libperc would load a second HIP runtime (%s beside "
+                            "libperc's %s; two runtimes corrupt the heap at exit): import torch before "
+                            "percolation_amd, or leave PERC_NO_TORCH unset" % (self.theirs, self.ours))
+        return None
+
+
+def runtimes(L=None):
+    """(count, paths) of the libamdhip64 copies mapped in this process
+    (perc_hip_runtimes): the copy libperc binds to first"""
+    L = L or lib()
+    buf = C.create_string_buffer(8192)
+    n = L.perc_hip_runtimes(buf, len(buf))
+    paths = [p for p in buf.value.decode(errors="replace").split(";") if p]
+    return n, paths
+
+
+def _check_one_runtime(L):
+    import sys
+    if not hasattr(L, "perc_hip_runtimes"):
+        return  # (an older probe build)
+    n, paths = runtimes(L)
+    if n > 1:
+        raise PercError("two HIP runtimes in one process: %s -- import torch before percolation_amd"
+                        % "; ".join(paths))
+    if "torch" not in sys.modules and paths:
+        theirs = _torch_runtime()
+        if theirs and theirs != paths[0] and not any(isinstance(f, _SecondRuntimeGuard) for f in sys.meta_path):
+            sys.meta_path.insert(0, _SecondRuntimeGuard(paths[0], theirs))
+
+
 def lib():
     """Load libperc.so (raises if it has not been built)."""
     global _lib
@@ -213,6 +271,7 @@ def lib():
         f = getattr(L, name)
         f.restype = res
         f.argtypes = args
+    _check_one_runtime(L)
     _lib = L
     return L
 

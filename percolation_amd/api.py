@@ -314,7 +314,8 @@ class Context:
                     literal=bool(f & L.RAN_LITERAL), lit_terms=bool(f & L.RAN_LIT_TERMS),
                     qfree=bool(f & L.RAN_QFREE), strips=bool(f & L.RAN_STRIPS),
                     nibble=bool(f & L.RAN_NIBBLE), tag=bool(f & L.RAN_TAG),
-                    host_fold=bool(f & L.RAN_HOST_FOLD), iter=int(out[2]))
+                    host_fold=bool(f & L.RAN_HOST_FOLD), xcd_grouped=bool(f & L.RAN_XCD_GROUPED),
+                    iter=int(out[2]))
 
     def matrix_format(self):
         rc = L.lib().perc_matrix_format(self.h)

@@ -229,6 +229,14 @@ int perc_ctx_create(int device, int lattice, int m, int n, int pbc, perc_ctx** o
     set_error("perc_ctx_create: triangular lattice needs even m (H7)");
     return PERC_EINVAL;
   }
+  {
+    char rt[2048];
+    if (perc_hip_runtimes(rt, (int)sizeof(rt)) > 1) {
+      set_error(std::string("perc_ctx_create: two HIP runtimes in one process (") + rt +
+                "): load libperc after the framework that brings its own (e.g. import torch first)");
+      return PERC_ESTATE;
+    }
+  }
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) {
     set_error("perc_ctx_create: no HIP device");

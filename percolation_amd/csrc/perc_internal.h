@@ -219,6 +219,7 @@ struct perc_ctx {
   bool small = false;           // one-workgroup solve of a small system (k_cg_small)
   int res_G = 0, res_H = 0, res_MT = 0, res_HMAX = 0;  // its grid, band height, template
   int res_NT = 1024;            // its threads per workgroup (m rounded up to 64 for m < 1024)
+  bool res_uneven = false;      // a grouped resident launch found the XCD placement uneven
   // what the last dev_solve ran (perc_last_solve): kernel family (PERC_RAN_*)
   // and flags (PERC_RAN_* bits: q-free, strip-major, nibble codes, tagged
   // reductions, literal folds of kernel-stored terms)

@@ -250,9 +250,14 @@ __device__ __forceinline__ ResXcd res_register(const ResArgs& a, int* s_flag) {
     const int x = (int)(__builtin_amdgcn_s_getreg((3 << 11) | 20) & 7u);  // HW_REG_XCC_ID
     const unsigned r = __hip_atomic_fetch_add(&a.reg[x * kTicketStride], 1u, __ATOMIC_RELAXED,
                                               __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_fetch_add(&a.reg[8 * kTicketStride], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // release / acquire on the arrival counter: a workgroup's per-XCD add is
+    // ordered before its arrival, and the poll that sees all G arrivals
+    // synchronises with every one of them (the RMWs form one release
+    // sequence), so every workgroup reads the same, final per-XCD counts
+    // below and takes the same grouped / flat decision
+    __hip_atomic_fetch_add(&a.reg[8 * kTicketStride], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
     int ok = 1;
-    for (unsigned spin = 0; __hip_atomic_load(&a.reg[8 * kTicketStride], __ATOMIC_RELAXED,
+    for (unsigned spin = 0; __hip_atomic_load(&a.reg[8 * kTicketStride], __ATOMIC_ACQUIRE,
                                                __HIP_MEMORY_SCOPE_AGENT) < (unsigned)G;
          ++spin) {
       if (spin > (1u << 25)) {  // ~1 s: the grid is not co-resident
@@ -576,7 +581,7 @@ __global__ __launch_bounds__(NT) void k_cg_res(ResArgs a) {
   ResXcd X{(int)blockIdx.x, 0, 0, 0, false};
   if constexpr (XG) {
     X = res_register(a, s_flag);
-    if (!X.ok || !s_flag[1]) {  // (uniform: every workgroup read the same counters)
+    if (!X.ok || !s_flag[1]) {  // (uniform: every workgroup read the same final counters)
       if (blockIdx.x == 0 && threadIdx.x == 0 && s_flag[1]) a.S->pad[kResPadUneven] = 1;
       return;
     }

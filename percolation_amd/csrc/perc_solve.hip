@@ -447,6 +447,7 @@ void march_geometry(perc_ctx* h) {
 void res_geometry(perc_ctx* h) {
   const Geom& g = h->g;
   h->res_G = 0;
+  h->res_uneven = false;
   const bool narrow = g.m < kResThreads;
   if ((g.m % kResThreads != 0 && !narrow) || g.n <= 2) return;
   int cus = 0, coop = 0;
@@ -641,8 +642,14 @@ hipError_t dev_solve_resident(perc_ctx* h, const CGArgs& ca, int* iter, double* 
   const bool sq = (h->forms.umask & ~kResSquareMask) == 0;
   // (PERC_RES_FLAT=1 in the environment: the flat all-gather instantiation,
   // for tests of that fallback)
+  // The grouped reductions need G / 8 workgroups on every XCD: a grid that
+  // cannot be placed so (G % 8 != 0, or more than kResXcdMax per XCD) takes
+  // the flat instantiation from the host, and so does a context whose grouped
+  // launch once found the placement uneven (h->res_uneven, reset with the
+  // lattice), instead of paying a cooperative launch that leaves at once
   const char* flat_env = std::getenv("PERC_RES_FLAT");
-  const bool xg = !(flat_env && flat_env[0] == '1');
+  const bool xg = !(flat_env && flat_env[0] == '1') && a.G % 8 == 0 && a.G / 8 <= kResXcdMax &&
+                  !h->res_uneven;
   const void* fn = res_kernel(h->res_MT, sq, h->res_NT, a.lit != nullptr, xg);
   KernelTiming& T = h->timing;
   if (T.enabled) {
@@ -657,9 +664,16 @@ hipError_t dev_solve_resident(perc_ctx* h, const CGArgs& ca, int* iter, double* 
   CGScalars hs{};
   HIP_TRY(hipMemcpyAsync(&hs, d.scal, sizeof(hs), hipMemcpyDeviceToHost, st));
   HIP_TRY(hipStreamSynchronize(st));
+  bool grouped = xg && a.lit == nullptr && kResXcdGather;
   if (hs.pad[kResPadUneven] != 0) {
     // the grouped launch found the workgroups spread unevenly over the XCDs
-    // and left at once: the flat all-gather instantiation runs the solve
+    // and left at once (no state touched): the flat all-gather instantiation
+    // runs the solve.  Its flag words are cleared first -- pad[1] is also the
+    // tagged march's error word -- and the context remembers the placement
+    h->res_uneven = true;
+    grouped = false;
+    HIP_TRY(hipMemsetAsync(d.scal->pad, 0, 2 * sizeof(int), st));
+    HIP_TRY(hipMemsetAsync(d.res_bar, 0, 9 * kTicketStride * sizeof(unsigned), st));
     fn = res_kernel(h->res_MT, sq, h->res_NT, a.lit != nullptr, false);
     HIP_TRY(hipLaunchCooperativeKernel(fn, dim3(a.G), dim3(h->res_NT), args, 0, st));
     HIP_TRY(dbg_sync(st, "k_cg_res"));
@@ -671,6 +685,7 @@ hipError_t dev_solve_resident(perc_ctx* h, const CGArgs& ca, int* iter, double* 
     fprintf(stderr, "[perc] k_cg_res: grid barrier timed out\n");
     return hipErrorLaunchTimeOut;
   }
+  if (grouped) h->last_flags |= PERC_RAN_XCD_GROUPED;
   if (T.enabled && hs.iter > 0) {
     float ms = 0.f;
     HIP_TRY(hipEventElapsedTime(&ms, T.ev[0], T.ev[1]));

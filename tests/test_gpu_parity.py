@@ -782,9 +782,16 @@ def test_resident_grouped_and_flat_reductions(lat, m, n, p, monkeypatch):
     workgroups sit unevenly on the XCDs (forced here with PERC_RES_FLAT=1):
     the same solve up to the association of the sums, and each repeatable
     bitwise (the grouped association is fixed in logical ids, whatever the
-    placement)."""
+    placement).  perc_last_solve reports which transport ran: grouped where
+    the grid can sit G / 8 per XCD (G = 256 at 1022 rows, 200 at 598 rows on
+    256 CUs), flat from the host where it cannot (G = 149 at 298 rows) and
+    under PERC_RES_FLAT."""
     nb = api.nbonds(lat, m, n, 0)
     order = api.shuffled_ids(nb, 77)
+    nrows = n - 2
+    H = -(-nrows // 256)  # rows per workgroup on MI355X's 256 CUs (res_geometry)
+    G = -(-nrows // H)
+    even = G % 8 == 0 and G // 8 <= 64  # kResXcdMax
     out = {}
     with api.Context(lat, m, n, 0) as ctx:
         ctx.occupy(PL.BOND, bond_order=order, nbonds_=int(p * nb))
@@ -793,7 +800,9 @@ def test_resident_grouped_and_flat_reductions(lat, m, n, p, monkeypatch):
         for flat in ("0", "1"):
             monkeypatch.setenv("PERC_RES_FLAT", flat)
             a = ctx.conductance(tol=1e-12, itmax=200000, vint=True)
-            assert ctx.last_solve()["kernel"] == "resident"
+            ran = ctx.last_solve()
+            assert ran["kernel"] == "resident"
+            assert ran["xcd_grouped"] == (flat == "0" and even), (flat, G, ran)
             b = ctx.conductance(tol=1e-12, itmax=200000, vint=True)
             assert (a["iter"], a["gtop"], a["gbot"]) == (b["iter"], b["gtop"], b["gbot"]), flat
             assert np.array_equal(a["vint"], b["vint"]), flat

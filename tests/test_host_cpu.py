@@ -43,7 +43,11 @@ import re, sys
 sys.path.insert(0, %r)
 from percolation_amd import _lib as PL
 PL.lib()
-import torch  # after libperc: the order that used to load a second runtime
+try:
+    import torch  # after libperc: the order that used to load a second runtime
+    print("torch imported", flush=True)
+except PL.PercError as e:
+    print("refused:", e, flush=True)
 maps = open('/proc/self/maps').read()
 print(sorted(set(re.findall(r'(/\\S*(?:libamdhip64|libhsa-runtime64|librccl)\\S*)', maps))))
 """
@@ -53,10 +57,11 @@ print(sorted(set(re.findall(r'(/\\S*(?:libamdhip64|libhsa-runtime64|librccl)\\S*
 def test_one_hip_runtime_per_process(no_torch):
     """libperc loaded before torch must not leave two HIP / HSA / RCCL
     runtimes in the process: that was round 4's interpreter-teardown abort
-    (glibc "double free or corruption (!prev)", SIGABRT), reproduced here
-    without a GPU by the PERC_NO_TORCH=1 run (libperc on /opt/rocm's copies,
-    torch then loads its own); _lib.lib() imports torch first, so the
-    default run exits 0 with torch's copies alone"""
+    (glibc "double free or corruption (!prev)", SIGABRT).  _lib.lib()
+    imports torch first, so the default run has torch's copies alone; with
+    PERC_NO_TORCH=1 libperc binds /opt/rocm's copies, and the later `import
+    torch` is REFUSED with PercError before torch's libraries load (the
+    runtime guard, _lib._SecondRuntimeGuard): still one runtime, exit 0"""
     import subprocess
     import sys
     pytest.importorskip("torch")
@@ -66,15 +71,49 @@ def test_one_hip_runtime_per_process(no_torch):
         env["PERC_NO_TORCH"] = "1"
     r = subprocess.run([sys.executable, "-c", _RUNTIMES_PROBE % REPO], capture_output=True, text=True,
                        timeout=300, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
     libs = eval(r.stdout.strip().splitlines()[-1])
     hip = [x for x in libs if "libamdhip64" in x]
-    if no_torch:  # the condition this guards against, shown to still arise without the guard
-        # (two runtimes; the heap corruption they cause at teardown aborts
-        # the process most of the time, not always)
-        assert len(hip) == 2, (libs, r.returncode, r.stderr[-500:])
+    assert len(hip) == 1, libs
+    if no_torch:
+        assert "refused: import torch after libperc would load a second HIP runtime" in r.stdout, r.stdout
+        assert "/opt/rocm" in hip[0], hip
     else:
-        assert len(hip) == 1 and len(libs) == 3, libs
-        assert r.returncode == 0, r.stderr[-2000:]
+        assert "torch imported" in r.stdout and len(libs) == 3, (r.stdout, libs)
+
+
+_SECOND_RUNTIME_PROBE = """
+import ctypes as C, sys
+sys.path.insert(0, %r)
+from percolation_amd import _lib as PL
+L = PL.lib()                      # PERC_NO_TORCH=1: /opt/rocm's runtime
+C.CDLL(%r, mode=C.RTLD_LOCAL)     # a second copy mapped behind libperc's back
+n, paths = PL.runtimes()
+h = C.c_void_p()
+rc = L.perc_ctx_create(0, 0, 16, 16, 0, C.byref(h))
+print(n, rc, L.perc_last_error().decode(), flush=True)
+"""
+
+
+def test_second_runtime_is_refused_by_the_library():
+    """The C-ABI's own check (perc_hip_runtimes, perc_ctx_create): with a
+    second libamdhip64 mapped in the process -- whatever loaded it -- the
+    context is refused with PERC_ESTATE naming both copies, before any HIP
+    call (a Fortran or C caller gets the same status).  The child's exit
+    status is not checked: two runtimes may corrupt the heap at teardown,
+    which is the condition being refused."""
+    import subprocess
+    import sys
+    torch_rt = PL._torch_runtime()
+    if not torch_rt:
+        pytest.skip("no bundled runtime to map")
+    env = dict(os.environ, PERC_NO_TORCH="1")
+    r = subprocess.run([sys.executable, "-c", _SECOND_RUNTIME_PROBE % (REPO, torch_rt)],
+                       capture_output=True, text=True, timeout=300, env=env)
+    line = [x for x in r.stdout.splitlines() if x[:2] == "2 "]
+    assert line, (r.stdout, r.stderr[-2000:])
+    n, rc, msg = line[0].split(" ", 2)
+    assert int(rc) == -9 and "two HIP runtimes" in msg and torch_rt in msg, line
 
 
 def test_no_device_is_an_error_not_a_fallback():

@@ -61,7 +61,10 @@ def main():
     with api.Context(rc["lattice"], rc["L"], rc["L"], 0) as ctx:
         if args.solver != "resident":
             ctx.set_march_mode(PL.MARCH_DEFAULT & ~PL.SOLVE_RESIDENT)
-        ctx.occupy(**occ)
+        if "device" in occ:  # drawn on the GPU (the bench realisation's fixture)
+            ctx.occupy_random(*occ["device"])
+        else:
+            ctx.occupy(**occ)
         li = ctx.label()
         assert li["nspan"] > 0
         ctx.set_dot_order(PL.DOT_LITERAL_HOST if args.solver == "march_host" else PL.DOT_LITERAL)
