@@ -527,6 +527,7 @@ int perc_set_dot_order(perc_ctx *h, int order);
 #define PERC_RAN_TAG 32       /* tagged-granule reductions */
 #define PERC_RAN_HOST_FOLD 64 /* PERC_DOT_LITERAL_HOST: the sums folded by the host */
 #define PERC_RAN_XCD_GROUPED 128 /* resident solve: XCD-grouped reductions (else the flat all-gather) */
+#define PERC_RAN_DEFERRED 256 /* march: each launch's totals formed by the next launch (no collector tail) */
 int perc_last_solve(perc_ctx *h, int *out4);
 /* err of every iteration of the last solve (linbcg's per-iteration
    `write (*,*) iter, err`, bondc.f:834): min(cap, iterations) values into

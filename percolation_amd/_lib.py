@@ -33,7 +33,7 @@ DOT_FAST, DOT_LITERAL, DOT_LITERAL_HOST = 0, 1, 2
 # perc_last_solve: kernel family and flag bits of the last solve
 RAN_OTHER, RAN_MARCH, RAN_SLABS, RAN_RESIDENT, RAN_SMALL = 0, 1, 2, 3, 4
 RAN_LITERAL, RAN_LIT_TERMS, RAN_QFREE, RAN_STRIPS, RAN_NIBBLE, RAN_TAG, RAN_HOST_FOLD = 1, 2, 4, 8, 16, 32, 64
-RAN_XCD_GROUPED = 128
+RAN_XCD_GROUPED, RAN_DEFERRED = 128, 256
 XPORT_RCCL, XPORT_HOST, XPORT_EXCHANGE = 0, 1, 4
 DSLAB_ID_BYTES = 128
 

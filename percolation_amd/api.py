@@ -315,6 +315,7 @@ class Context:
                     qfree=bool(f & L.RAN_QFREE), strips=bool(f & L.RAN_STRIPS),
                     nibble=bool(f & L.RAN_NIBBLE), tag=bool(f & L.RAN_TAG),
                     host_fold=bool(f & L.RAN_HOST_FOLD), xcd_grouped=bool(f & L.RAN_XCD_GROUPED),
+                    deferred=bool(f & L.RAN_DEFERRED),
                     iter=int(out[2]))
 
     def matrix_format(self):

@@ -332,10 +332,15 @@ __device__ __forceinline__ int bf_open_square(const Geom& g, int row, int col) {
 // unions in one loop.  A lane skips its union when its column and the one
 // to its left share their run in this row (a right link) and in the row
 // below, and that column unites too: the same pair of runs.
-// ncl (site and mixed kinds, whose member flag the tile sees whole): the
-// block's member roots written to ncl[block]; the merge's hooks subtract
-// from that count (k_span_top sums both), so no pass over every parent
-// counts the clusters
+// ncl: the block's member roots written to ncl[block]; the merge's hooks
+// subtract from that count (k_span_top sums both), so no pass over every
+// parent counts the clusters.  The bond kind's member flag of a block-edge
+// site also depends on the links that cross into the block from the left
+// (lane 0's first column: the right link of the site left of it) and from
+// below (the block's first row: the up links of the row below); the tile
+// reads those two link kinds for the flags only (their unions are the
+// merge's), so the bond kind counts this way too and k_cc_count_roots is
+// not run.
 template <int H, int KIND, int D = 2, bool BAL = false>  // D: rows whose loads are in flight
 __global__ __launch_bounds__(64) void k_cc_tile_w(Geom g, const uint8_t* bocc, const uint8_t* socc, int* parent,
                                                   uint8_t* member, unsigned nb_bytes, int* ncl = nullptr) {
@@ -352,8 +357,10 @@ __global__ __launch_bounds__(64) void k_cc_tile_w(Geom g, const uint8_t* bocc, c
   auto ld8 = [](__amdgpu_buffer_rsrc_t r, bool ok, unsigned off) {
     return (unsigned)__builtin_amdgcn_raw_buffer_load_b8(r, (int)(ok ? off : kOOB), 0, 0);
   };
-  // R / U: the link right / up of the lane's two sites; O: the site occupied
-  auto load_row = [&](int r, unsigned (&R)[2], unsigned (&U)[2], unsigned (&O)[2]) {
+  // R / U: the link right / up of the lane's two sites; O: the site occupied;
+  // X (bond kind): the link into lane 0's first-column site from the left
+  // block (member flag only)
+  auto load_row = [&](int r, unsigned (&R)[2], unsigned (&U)[2], unsigned (&O)[2], unsigned& X) {
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       const int lc = lane + 64 * h, col = c0 + lc, row = r0 + r;
@@ -376,6 +383,12 @@ __global__ __launch_bounds__(64) void k_cc_tile_w(Geom g, const uint8_t* bocc, c
         }
       }
     }
+    if constexpr (KIND == PERC_BOND) {
+      const bool hx = lane == 0 && c0 > 0 && r < th;
+      X = ld8(rb, hx, (unsigned)bf_open_square(g, r0 + r, hx ? c0 - 1 : 0));
+    } else {
+      X = 0u;
+    }
   };
   auto finish = [&](unsigned (&R)[2], unsigned (&U)[2], unsigned (&O)[2]) {
     if constexpr (KIND != PERC_BOND) {
@@ -386,11 +399,20 @@ __global__ __launch_bounds__(64) void k_cc_tile_w(Geom g, const uint8_t* bocc, c
       }
     }
   };
-  unsigned Rq[D][2], Uq[D][2], Oq[D][2], R[2], U[2], O[2], Up[2] = {0u, 0u};
+  unsigned Rq[D][2], Uq[D][2], Oq[D][2], Xq[D], R[2], U[2], O[2], X, Up[2] = {0u, 0u};
   int labp[2] = {0, 0};
   unsigned nodes[H], Mb[2] = {0u, 0u};
+  if constexpr (KIND == PERC_BOND) {
+    // the up links of the row below the block: the first row's member flags
 #pragma unroll
-  for (int d = 0; d < D; ++d) load_row(d, Rq[d], Uq[d], Oq[d]);
+    for (int h = 0; h < 2; ++h) {
+      const int lc = lane + 64 * h, col = c0 + lc;
+      const bool hd = r0 > 0 && lc < tw;
+      Up[h] = ld8(rb, hd, (unsigned)(hd ? bf_open_square(g, r0 - 1, col) + (col < g.m - 1 ? 1 : 0) : 0));
+    }
+  }
+#pragma unroll
+  for (int d = 0; d < D; ++d) load_row(d, Rq[d], Uq[d], Oq[d], Xq[d]);
   const unsigned long long le = lane == 63 ? ~0ull : ((2ull << lane) - 1ull);
   const bool v0 = lane < tw, v1 = lane + 64 < tw;
   const unsigned long long vm0 = __ballot(v0), vm1 = __ballot(v1);
@@ -405,8 +427,9 @@ __global__ __launch_bounds__(64) void k_cc_tile_w(Geom g, const uint8_t* bocc, c
       U[h] = Uq[r % D][h];
       O[h] = Oq[r % D][h];
     }
+    X = Xq[r % D];
     finish(R, U, O);
-    load_row(r + D, Rq[r % D], Uq[r % D], Oq[r % D]);  // (past th: nothing loaded)
+    load_row(r + D, Rq[r % D], Uq[r % D], Oq[r % D], Xq[r % D]);  // (past th: nothing loaded)
     bool left0, left1;
     unsigned long long lo, hi, lm0 = 0, lm1 = 0;
     if constexpr (BAL) {
@@ -490,7 +513,9 @@ __global__ __launch_bounds__(64) void k_cc_tile_w(Geom g, const uint8_t* bocc, c
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       const bool lft = h ? left1 : left0;
-      const bool mem = KIND == PERC_BOND ? (R[h] | U[h] | (lft ? 1u : 0u) | (r > 0 ? Up[h] : 0u)) != 0u
+      // (bond kind: Up of the first row = the row below the block's up
+      // links, X = the left block's link into column 0)
+      const bool mem = KIND == PERC_BOND ? (R[h] | U[h] | (lft ? 1u : 0u) | Up[h] | (h == 0 ? X : 0u)) != 0u
                                          : O[h] != 0u;
       Mb[h] |= (mem ? 1u : 0u) << r;
     }
@@ -730,9 +755,12 @@ __global__ __launch_bounds__(kCcThreads) void k_cc_count_roots(int t, const int*
 // issues their U parent loads together (one chain after another: compress
 // 83.3 vs 55.3 us at L = 4096, profiles/r4_7_cc_bench_L4096.txt).
 constexpr int kCcCompressU = 8;
+// With root > 0 the member sites whose root is `root` are counted into
+// *rcount (the spanning cluster's size, formerly a second pass, k_count_root:
+// 30 us at L = 4096, profiles/r5_35_final_rocprof_kernel_stats.csv).
 template <int U = kCcCompressU>
-__global__ __launch_bounds__(kCcThreads) void k_cc_compress(int t, int* parent, const uint8_t* member,
-                                                            int* nclusters) {
+__global__ __launch_bounds__(kCcThreads) void k_cc_compress(int t, int* parent, const uint8_t* member, int root,
+                                                            int* rcount) {
   int cnt = 0;
   for (long long b = (long long)blockIdx.x * kCcThreads * U + threadIdx.x + 1; b <= t;
        b += (long long)gridDim.x * kCcThreads * U) {
@@ -758,10 +786,10 @@ __global__ __launch_bounds__(kCcThreads) void k_cc_compress(int t, int* parent, 
       const long long s = b + k * kCcThreads;
       if (s > t) continue;
       parent[s] = x[k];
-      cnt += x[k] == s && member[s];
+      cnt += x[k] == root && member[s];
     }
   }
-  block_count_add(cnt, nclusters);
+  if (root > 0) block_count_add(cnt, rcount);  // (uniform)
 }
 
 }  // namespace

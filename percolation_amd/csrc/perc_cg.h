@@ -85,6 +85,17 @@ struct CGArgs {
   // the march's u16-code kernels take the interior form's scalar path too
   int sqcls;
   int* merr;
+  // deferred reductions of the strip-major tagged march (k_cg_march DEF):
+  // 1 = a launch only publishes its workgroups' granules and the NEXT launch
+  // forms the totals itself (B: q.p -> ak; P: z.r, r.r -> bk, err, stop;
+  // k_march_epi after each chunk of launches), 2 = the same kernels in
+  // perc_bench_kernel's fixed-iteration probe (no stop, no scalars but bkn),
+  // 0 = collectors at the end of each launch; mnwg = the grid both march
+  // kernels run
+  int mdef;
+  int mnwg;
+  int mdsc1;  // deferred totals read the granules with sc1 loads (else plain, through L2)
+  int rm_pnib;  // the row-major march P reads the nibble codes too (else the u16 codes)
   // literal dot order on the q-free march (PERC_DOT_LITERAL): the march P
   // stores each row's q.p term and the march B each row's z.r and r.r terms
   // (the reference's IEEE products) at their row-major index into lit[0..N),
@@ -1140,6 +1151,10 @@ CGArgs make_cg_args(perc_ctx* h) {
   a.sqcls = h->nib_ok && !h->g.pbc ? 1 : 0;
   for (int c = 0; c < 3; ++c) a.ncls[c] = a.sqcls ? h->ncls[c] : 0u;
   a.merr = nullptr;
+  a.mdef = 0;
+  a.mnwg = 0;
+  a.mdsc1 = 0;
+  a.rm_pnib = 0;
   a.lit = nullptr;
   return a;
 }

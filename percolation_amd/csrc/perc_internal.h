@@ -60,6 +60,10 @@ struct CGScalars {
   int done;      // set once err <= tol or iter > itmax
   int pad[3];
   double part[4];  // row slabs: this slab's raw partials (q.p, z.r, r.r, ||D^-1 b||^2)
+  // deferred march reductions (CGArgs::mdef): bkn[j & 1] = bknum of
+  // iteration j (j >= 1; iteration 0's is bknum above), parity-buffered so
+  // a launch reads the previous value while its writer stores the new one
+  double bkn[2];
 };
 
 struct AsmParams {

@@ -595,15 +595,13 @@ hipError_t dev_label(perc_ctx* h, int* nspan, int* span_list, int* nclusters) {
     const unsigned nbb = (unsigned)h->nb + 8u;
     const int nseg = cdiv(g.m, kCcThreads), nfull = g.n / H;
     const int GM = nfull * nseg + (cdiv(g.m, kCcW) - 1) * cdiv(g.n, kCcThreads);  // (k_cc_merge_sq's grid)
-    // site and mixed kinds: the cluster count from the tiles' member roots and
-    // the merge's hooks (the bond kind's member flags of a block's edge sites
-    // are completed by the merge, so it counts the roots afterwards)
-    int* part = nullptr;
-    if (kind != PERC_BOND) {
-      if (!d.ccpart) HIP_TRY(dmalloc(&d.ccpart, (size_t)G + GM));
-      part = d.ccpart;
-    }
-    if (kind == PERC_BOND) k_cc_tile_w<H, PERC_BOND><<<G, 64, 0, st>>>(g, d.bocc, d.socc, d.parent, d.member, nbb);
+    // the cluster count from the tiles' member roots and the merge's hooks
+    // (every kind: the bond tile reads the links that cross into its edge
+    // sites for their member flags), no pass over the parents
+    if (!d.ccpart) HIP_TRY(dmalloc(&d.ccpart, (size_t)G + GM));
+    int* part = d.ccpart;
+    if (kind == PERC_BOND)
+      k_cc_tile_w<H, PERC_BOND><<<G, 64, 0, st>>>(g, d.bocc, d.socc, d.parent, d.member, nbb, part);
     // (site and mixed kinds: the ballot-mask walk, 95.6 vs 103.8 us mixed at
     // L = 4096, 273.7 vs 298.5 at 8192; the bond kind's is 2 % slower with
     // it, profiles/r5_10_cc_bench_L*.txt)
@@ -613,7 +611,7 @@ hipError_t dev_label(perc_ctx* h, int* nspan, int* span_list, int* nclusters) {
     HIP_TRY(dbg_sync(st, "k_cc_tile_w"));
     // the square lattice's merge: 107 vs 163 us mixed, 153 vs 191 bond at
     // L = 8192 (profiles/r5_11_cc_bench_L8192.txt)
-    int* hk = part ? part + G : nullptr;
+    int* hk = part + G;
     if (GM == 0) {  // one block: nothing crosses a block edge
     } else if (kind == PERC_BOND)
       k_cc_merge_sq<H, PERC_BOND><<<GM, kCcThreads, 0, st>>>(g, d.bocc, d.socc, d.parent, d.member, nseg, nfull, hk);
@@ -623,7 +621,7 @@ hipError_t dev_label(perc_ctx* h, int* nspan, int* span_list, int* nclusters) {
       k_cc_merge_sq<H, PERC_SITEBOND><<<GM, kCcThreads, 0, st>>>(g, d.bocc, d.socc, d.parent, d.member, nseg, nfull,
                                                                  hk);
     HIP_TRY(dbg_sync(st, "k_cc_merge_sq"));
-    return label_finish(h, nspan, span_list, nclusters, part, part ? G + GM : 0);
+    return label_finish(h, nspan, span_list, nclusters, part, G + GM);
   }
   const int tiles = cdiv(g.m, kCcW) * cdiv(g.n, kCcH);
   unsigned long long* ttr = nullptr;  // PERC_TILE_TRACE: per-workgroup phase stamps
@@ -693,22 +691,31 @@ static hipError_t label_finish(perc_ctx* h, int* nspan, int* span_list, int* ncl
   return hipSuccess;
 }
 
-hipError_t dev_flatten(perc_ctx* h) {
-  if (h->flat) return hipSuccess;
+// every parent to its root; with root > 0 the member sites of that root's
+// cluster counted into *count (device) in the same pass
+static hipError_t flatten_count(perc_ctx* h, int root, int* count) {
   const Geom& g = h->g;
   k_cc_compress<<<std::min(cdiv(g.t, kCcThreads * kCcCompressU), kReduceGrid), kCcThreads, 0, h->stream>>>(
-      g.t, h->d.parent, h->d.member, h->d.counters + 6);
+      g.t, h->d.parent, h->d.member, root, count);
   HIP_TRY(dbg_sync(h->stream, "k_cc_compress"));
   h->flat = true;
   return hipSuccess;
 }
 
+hipError_t dev_flatten(perc_ctx* h) {
+  if (h->flat) return hipSuccess;
+  return flatten_count(h, 0, nullptr);
+}
+
 hipError_t dev_span_sites(perc_ctx* h, int root, int* count) {
-  HIP_TRY(dev_flatten(h));
   hipStream_t st = h->stream;
   HIP_TRY(hipMemsetAsync(h->d.counters + 2, 0, sizeof(int), st));
-  k_count_root<<<std::min(cdiv(h->g.t, kCcThreads), kReduceGrid), kCcThreads, 0, st>>>(
-      h->g.t, h->d.parent, h->d.member, root, h->d.counters + 2);
+  if (!h->flat) {  // the spanning cluster's sites counted by the compress pass itself
+    HIP_TRY(flatten_count(h, root, h->d.counters + 2));
+  } else {
+    k_count_root<<<std::min(cdiv(h->g.t, kCcThreads), kReduceGrid), kCcThreads, 0, st>>>(
+        h->g.t, h->d.parent, h->d.member, root, h->d.counters + 2);
+  }
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipMemcpyAsync(count, h->d.counters + 2, sizeof(int), hipMemcpyDeviceToHost, st));
   return hipStreamSynchronize(st);

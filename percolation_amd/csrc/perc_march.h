@@ -245,6 +245,114 @@ __device__ bool publish_and_reduce_tagged(double (&v)[NV], double* gran, unsigne
 #endif
 }
 
+// Deferred reductions (DEF, an opt-in variant of the strip-major tagged
+// march, PERC_MARCH_DEF; measured and not the default, perc_solve.hip
+// setup_granules): a launch ends once its workgroups have published their
+// granules -- no collector waits on the slowest workgroup's granule and no
+// second hop follows (the march trace put the exits 2.9 us (P) and 4.4 us
+// (B) past the last walk, profiles/r5_4_mtrace_summary_L4096.txt; the
+// launch times moved by 1.4 and 2.3 us).  The NEXT launch forms the totals
+// in every workgroup, after its first rows' loads are issued: the group
+// sums by the same lanes-in-order wave_sum the group collectors formed and
+// the group totals by the same thread-strided block_sum the last collector
+// formed, so every total is the collector form's bitwise in every
+// workgroup (tagged = ticket = deferred: test_tagged_reduction_is_bitwise_
+// the_ticket_one).  The granules are complete when a launch starts (the
+// previous one has ended); their tags are checked, not polled.
+// CGArgs::mdef bits: kDefP -- P publishes only, B forms q.p (ak) at its
+// start; kDefB -- B publishes only, the next P (and k_march_epi) forms z.r,
+// r.r (bk, err, stop); kDefBench -- perc_bench_kernel's fixed iteration (no
+// stop, no scalars but bkn)
+constexpr int kDefP = 1, kDefB = 2, kDefBench = 4;
+constexpr int kDefGroups = 12;  // groups of kGroup workgroups a deferred total takes (grid <= 768)
+template <int NV>
+__device__ __forceinline__ void def_totals(const double* gran, int nwg, double tag, int* err,
+                                           double (&tot)[NV], double* s_red, double* s_grp, bool sc1) {
+  const int ngroups = red_groups(nwg);
+  const __amdgpu_buffer_rsrc_t rg = rsrc(gran, (unsigned)(NV * (nwg + ngroups) * 16));
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  constexpr int kPer = kDefGroups / 4;  // groups per wave (4 waves per workgroup)
+  double2 g2[kPer][NV];
+#pragma unroll
+  for (int i = 0; i < kPer; ++i) {  // every load issued before any is used
+    const int g = wid + 4 * i, g0 = g * kGroup, gn = g < ngroups ? min(kGroup, nwg - g0) : 0;
+#pragma unroll
+    for (int j = 0; j < NV; ++j) {
+      const int off = (int)(lane < gn ? (j * nwg + g0 + lane) * 16 : kOOB);
+      // (sc1: past this XCD's L2; plain: the XCD's workgroups share one L2
+      // fill -- the previous launch's write-through granules are in memory
+      // when this launch starts, and a stale line would fail the tag check)
+      g2[i][j] = __builtin_bit_cast(double2, sc1 ? __builtin_amdgcn_raw_buffer_load_b128(rg, off, 0, 16)
+                                                 : __builtin_amdgcn_raw_buffer_load_b128(rg, off, 0, 0));
+    }
+  }
+  bool bad = false;
+#pragma unroll
+  for (int i = 0; i < kPer; ++i) {
+    const int g = wid + 4 * i;
+    if (g < ngroups) {  // (wave-uniform)
+      const int gn = min(kGroup, nwg - g * kGroup);
+#pragma unroll
+      for (int j = 0; j < NV; ++j) {
+        bad = bad || (lane < gn && g2[i][j].y != tag);
+        const double w = wave_sum(lane < gn ? g2[i][j].x : 0.0);  // the group collector's sum
+        if (lane == 0) s_grp[j * kDefGroups + g] = w;
+      }
+    }
+  }
+  if (err && __any(bad) && lane == 0) *err = 1;
+  __syncthreads();
+  double acc[NV];
+#pragma unroll
+  for (int j = 0; j < NV; ++j) {  // the last collector's thread-strided group sums
+    acc[j] = 0.0;
+    if ((int)threadIdx.x < ngroups) acc[j] = acc[j] + s_grp[j * kDefGroups + threadIdx.x];
+  }
+  block_sum<NV>(acc, s_red);
+  if (threadIdx.x == 0)
+#pragma unroll
+    for (int j = 0; j < NV; ++j) s_red[16 + j] = acc[j];
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < NV; ++j) tot[j] = s_red[16 + j];
+  __syncthreads();  // s_red / s_grp reuse
+}
+
+// a workgroup-uniform double held in SGPRs (values read back from LDS land
+// in VGPRs: 2 more for the whole walk -- P's 169 instead of 167, 2 waves
+// per SIMD instead of 3)
+__device__ __forceinline__ double sgpr_double(double v) {
+  const unsigned long long u = __builtin_bit_cast(unsigned long long, v);
+  const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)u), hi = __builtin_amdgcn_readfirstlane((unsigned)(u >> 32));
+  return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
+}
+
+// B(kk)'s epilogue, deferred to the next P (or k_march_epi): the z.r and
+// r.r totals -> bk, err, the stop test (k_cg_b's epilogue; linbcg
+// bondc.f:785-787, 834).  Every workgroup forms the same values; `writer`
+// stores them.  bkn is parity-buffered: the writer stores bknum(kk) while
+// the others read bknum(kk - 1).  Returns the stop decision.
+__device__ __forceinline__ bool march_def_epilogue(const CGArgs& a, int kk, const double (&tb)[2], bool writer,
+                                                   double& bk) {
+  CGScalars* S = a.S;
+  const double old = kk == 1 ? S->bknum : S->bkn[(kk - 1) & 1];
+  const double err = sqrt(tb[1]) / S->bnrm;
+  bk = tb[0] / old;
+  const bool live = !(a.mdef & kDefBench);
+  const bool dn = live && (!(err > S->tol) || kk >= S->itmax + 1);
+  if (writer) {
+    S->bkn[kk & 1] = tb[0];
+    if (live) {
+      S->bk = bk;
+      S->err = err;
+      if (kk - 1 < a.err_hist_cap) a.err_hist[kk - 1] = err;
+      S->iter = kk;
+      if (dn) S->done = 1;
+    }
+  }
+  return dn;
+}
+
 constexpr int kMarchW = 128;     // columns per wave strip
 constexpr int kMarchWaves = 4;   // waves (strips) per workgroup
 // A/B probe builds only: the column-class path in the row-major march too
@@ -446,6 +554,14 @@ __device__ __forceinline__ unsigned melem(const CGArgs& a, const MBuf& B, int gr
   return SM ? (unsigned)sm_at(a.T, gr, col) : (unsigned)((gr - B.lo) * a.T.m + col);
 }
 
+// count / form bits of column c on the open square lattice (interior, first,
+// last column): the row-major nibble march forms them per access instead of
+// holding them in MGeom (7 VGPRs: its P spilled 6 at the 4-wave bound, 128
+// VGPRs; the strip-major march keeps them in registers)
+__device__ __forceinline__ unsigned col_cls(const CGArgs& a, int c) {
+  return c == 0 ? a.ncls[1] : (c == a.T.m - 1 ? a.ncls[2] : a.ncls[0]);
+}
+
 template <int MODE, bool SM, int PAUX = 0, bool PK = false>
 __device__ __forceinline__ void march_load(const CGArgs& a, const MGeom& g, const MBuf& B, int gr,
                                            bool first, const double* __restrict__ psrc, MRow& R) {
@@ -461,7 +577,8 @@ __device__ __forceinline__ void march_load(const CGArgs& a, const MGeom& g, cons
       // the pair's two slot nibbles in one byte (element e even); the count
       // and form bits come from the columns (g.cb0 / cb1): the u16 codes
       const unsigned b = __builtin_amdgcn_raw_buffer_load_b8(B.c, (int)(rowok ? e / 2u : kOOB), 0, 0);
-      R.c = ((b & 0xFu) | g.cb0) | (((b >> 4) | g.cb1) << 16);
+      const unsigned cb0 = SM ? g.cb0 : col_cls(a, g.col), cb1 = SM ? g.cb1 : col_cls(a, g.col + 1);
+      R.c = ((b & 0xFu) | cb0) | (((b >> 4) | cb1) << 16);
     } else {
       R.c = __builtin_amdgcn_raw_buffer_load_b32(B.c, (int)(rowok ? e * 2u : kOOB), 0, 0);
     }
@@ -474,7 +591,7 @@ __device__ __forceinline__ void march_load(const CGArgs& a, const MGeom& g, cons
     if (MODE != kMarchB) {
       if constexpr (PK) {
         const unsigned b = __builtin_amdgcn_raw_buffer_load_b8(B.c, (int)(hk ? eh / 2u : kOOB), 0, 0);
-        R.hc = ((b >> (4u * (eh & 1u))) & 0xFu) | g.cbh;
+        R.hc = ((b >> (4u * (eh & 1u))) & 0xFu) | (SM ? g.cbh : col_cls(a, g.hcol));
       } else {
         R.hc = __builtin_amdgcn_raw_buffer_load_b16(B.c, (int)(hk ? eh * 2u : kOOB), 0, 0);
       }
@@ -579,7 +696,11 @@ __device__ __forceinline__ void march_step(const CGArgs& a, const MGeom& g, cons
     // (strip-major u16 codes only: in the row-major march past the Infinity
     // Cache the path's 6 VGPRs cost a wave per SIMD -- 133 vs 127, P 0.394
     // vs 0.314 ms at L = 8192, profiles/r5_6_l8192_probe_bond.json)
-    if constexpr (PK) sqp = !a.T.pbc;
+    // (the row-major nibble march runs on the open square lattice only --
+    // the host takes the u16 codes with pbc -- so the other paths are not
+    // compiled into it: their registers spilled it at the 4-wave bound)
+    if constexpr (PK && !SM) sqp = true;
+    else if constexpr (PK) sqp = !a.T.pbc;
     else if constexpr (SM || kMarchRmSq) sqp = a.sqcls && !__any((((c0w ^ g.cb0) | (c1w ^ g.cb1)) >> 8) != 0u);
     else sqp = false;
     if (sqp) {
@@ -597,8 +718,14 @@ __device__ __forceinline__ void march_step(const CGArgs& a, const MGeom& g, cons
       // strips walked 69.8 vs 65.9 us (P, iteration 20000) and set the
       // kernel's end (profiles/r5_2_mtrace_summary_it20000_L4096.txt)
       const unsigned mask = a.St.F.rmask[a.ncls[0] >> 11];
-      const unsigned e0 = (c0w & g.lo0) | ((c0w & g.hi0) << 1);
-      const unsigned e1 = (c1w & g.lo1) | ((c1w & g.hi1) << 1);
+      unsigned e0, e1;
+      if constexpr (SM) {
+        e0 = (c0w & g.lo0) | ((c0w & g.hi0) << 1);
+        e1 = (c1w & g.lo1) | ((c1w & g.hi1) << 1);
+      } else {  // (the same spreads, formed from the column)
+        e0 = g.col == 0 ? (c0w & 1u) | ((c0w & 6u) << 1) : c0w & 0xFu;
+        e1 = g.col + 1 == a.T.m - 1 ? (c1w & 3u) | ((c1w & 4u) << 1) : c1w & 0xFu;
+      }
       q0 = march_q<0>(e0, dM0.x, W.C.e0, mask, W.U, W.C, W.Dn, ng0, nleak);
       q1 = march_q<1>(e1, dM1.x, W.C.e1, mask, W.U, W.C, W.Dn, ng0, nleak);
     } else if (uni) {
@@ -700,9 +827,14 @@ __device__ __forceinline__ void march_walk(const CGArgs& a, const MGeom& g, cons
 // TR: phase probe -- lane 0 of every wave stores {kernel entry, walk end,
 // exit, hardware id} wall-clock stamps (100 MHz) into a.mtrace[4 w ..]
 // TAG: the epilogue reductions by tagged granules (publish_and_reduce_tagged)
+// DEF: deferred reductions (with TAG, strip-major, fast order; see def_totals)
 template <int MODE, bool SM = false, int D = kMarchDepth, int PAUX = 0, bool TR = false,
-          bool TAG = false, bool PK = false, bool LIT = false>
-__global__ __launch_bounds__(64 * kMarchWaves, PERC_MARCH_MINW(SM, MODE, PK)) void k_cg_march(CGArgs a) {
+          bool TAG = false, bool PK = false, bool LIT = false, bool DEF = false>
+// (the deferred instantiations are held to 3 waves per SIMD -- 168 VGPRs:
+// the strip-major march's slot-weighted bands assume 3 resident workgroups
+// per CU, and their totals code left P at 169 without the bound)
+__global__ __launch_bounds__(64 * kMarchWaves, DEF ? 3 : PERC_MARCH_MINW(SM, MODE, PK)) void k_cg_march(CGArgs a) {
+  static_assert(!DEF || (TAG && SM && !LIT), "deferred reductions: the tagged strip-major fast march");
   const unsigned long long tr_t0 = TR ? wall_clock64() : 0ull;
   unsigned long long tr_t1 = 0ull;
   CGScalars* S = a.S;
@@ -777,7 +909,7 @@ __global__ __launch_bounds__(64 * kMarchWaves, PERC_MARCH_MINW(SM, MODE, PK)) vo
   g.cb0 = g.cb1 = g.cbh = 0u;
   g.lo0 = g.lo1 = 0xFu;
   g.hi0 = g.hi1 = 0u;
-  if (PK || a.sqcls) {
+  if ((PK || a.sqcls) && (SM || kMarchRmSq)) {
     auto cls = [&](int c) { return c == 0 ? a.ncls[1] : (c == m - 1 ? a.ncls[2] : a.ncls[0]); };
     g.cb0 = cls(g.col);
     g.cb1 = cls(g.col + 1);
@@ -801,7 +933,36 @@ __global__ __launch_bounds__(64 * kMarchWaves, PERC_MARCH_MINW(SM, MODE, PK)) vo
   }
   load_dtab(a.St, s_dt);
   __syncthreads();
-  const double bk = S->bk, ak = S->ak;
+  double bk = S->bk, ak = S->ak;
+  // bknum of this iteration's ak (P's collector epilogue): the scalar, or
+  // with kDefB the total this launch formed from B(k-1)'s granules
+  double bkn_it = S->bknum;
+  if constexpr (DEF) {
+    // the previous launch's totals, formed here (its first rows' loads are
+    // in flight): B takes P(k)'s q.p -> ak (kDefP); P takes B(k-1)'s z.r and
+    // r.r -> bk, err and the stop test (kDefB)
+    __shared__ double s_grp[2 * kDefGroups];
+    const bool live = !(a.mdef & kDefBench);
+    int* derr = live ? a.merr : nullptr;
+    if (MODE == kMarchB) {
+      if (a.mdef & kDefP) {
+        double tp[1];
+        def_totals<1>(a.mgran, gridDim.x, a.mtag, derr, tp, s_red, s_grp, a.mdsc1 != 0);
+        const double bknum = (a.mdef & kDefB) && k > 1 ? S->bkn[(k - 1) & 1] : S->bknum;
+        ak = sgpr_double(bknum / tp[0]);
+        if (lb == 0 && threadIdx.x == 0 && live) {
+          S->akden = tp[0];
+          S->ak = ak;
+        }
+      }
+    } else if (!first && (a.mdef & kDefB)) {
+      double tb[2];
+      def_totals<2>(a.mgran_b, gridDim.x, a.mtag - 1.0, derr, tb, s_red, s_grp, a.mdsc1 != 0);
+      if (march_def_epilogue(a, k - 1, tb, lb == 0 && threadIdx.x == 0, bk)) return;  // (uniform)
+      bk = sgpr_double(bk);
+      bkn_it = sgpr_double(tb[0]);
+    }
+  }
   double acc[2] = {0.0, 0.0};
   if (active) {
     double* s_w = s_win[threadIdx.x >> 6];
@@ -851,7 +1012,26 @@ __global__ __launch_bounds__(64 * kMarchWaves, PERC_MARCH_MINW(SM, MODE, PK)) vo
       a.mtrace[4 * (size_t)w + 3] = ((unsigned long long)xcc << 32) | hw;
     }
   }
-  if (MODE != kMarchB) {
+  bool pub_only = false;
+  if constexpr (DEF) pub_only = (a.mdef & (MODE == kMarchB ? kDefB : kDefP)) != 0;
+  if (pub_only) {
+    // publish only: this launch's workgroup partials, {value, tag} granules
+    // written through; the next launch (or k_march_epi) forms the totals
+    constexpr int NV = MODE == kMarchB ? 2 : 1;
+    double v[NV];
+#pragma unroll
+    for (int j = 0; j < NV; ++j) v[j] = acc[j];
+    block_sum<NV>(v, s_red);
+    if (threadIdx.x == 0) {
+      const int ngroups = red_groups(gridDim.x);
+      double* gran = MODE == kMarchB ? a.mgran_b : a.mgran;
+      const __amdgpu_buffer_rsrc_t rg = rsrc(gran, (unsigned)(NV * ((int)gridDim.x + ngroups) * 16));
+#pragma unroll
+      for (int j = 0; j < NV; ++j)
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, make_double2(v[j], a.mtag)), rg,
+                                               (j * (int)gridDim.x + lb) * 16, 0, 16);
+    }
+  } else if (MODE != kMarchB) {
     double v[1] = {acc[0]}, tot[1];
     const bool last = TAG ? publish_and_reduce_tagged<1>(v, a.mgran, a.tickets, lb, gridDim.x, a.mtag,
                                                          a.merr, tot, s_red, s_flag)
@@ -863,7 +1043,7 @@ __global__ __launch_bounds__(64 * kMarchWaves, PERC_MARCH_MINW(SM, MODE, PK)) vo
           if (a.pub) a.pub[0] = tot[0];
         } else {
           S->akden = tot[0];
-          S->ak = S->bknum / tot[0];
+          S->ak = bkn_it / tot[0];
         }
       }
     }
@@ -892,6 +1072,19 @@ __global__ __launch_bounds__(64 * kMarchWaves, PERC_MARCH_MINW(SM, MODE, PK)) vo
   }
 }
 
+
+// The deferred epilogue of a chunk's last B (DEF): one workgroup of the
+// march's shape forms the z.r and r.r totals as the next P would and stores
+// iter, err, bk, the stop flag -- the host reads them after each chunk.  The
+// next P forms the same values again (every store idempotent).
+__global__ __launch_bounds__(64 * kMarchWaves) void k_march_epi(CGArgs a) {
+  __shared__ double s_red[32];
+  __shared__ double s_grp[2 * kDefGroups];
+  if (a.S->done) return;
+  double tb[2], bk;
+  def_totals<2>(a.mgran_b, a.mnwg, a.mtag, a.merr, tb, s_red, s_grp, true);
+  march_def_epilogue(a, a.kiter, tb, threadIdx.x == 0, bk);
+}
 
 }  // namespace
 }  // namespace perc

@@ -75,7 +75,10 @@ void klaunch(perc_ctx* h, K kern, dim3 g, dim3 b, hipStream_t st, const CGArgs& 
 template <int MODE, bool PK>
 void launch_march_sm2(perc_ctx* h, hipStream_t st, const CGArgs& a) {
   const int grid = a.wslots > 0 ? h->wm_grid : h->march_grid;
-  if (a.lit) {  // the literal dot order: the LIT instantiation (term stores)
+  if (a.mdef) {  // deferred reductions (the default): the next launch forms the totals
+    if (a.mtrace) klaunch(h, k_cg_march<MODE, true, 3, kNT, true, true, PK, false, true>, grid, 64 * kMarchWaves, st, a);
+    else klaunch(h, k_cg_march<MODE, true, 3, kNT, false, true, PK, false, true>, grid, 64 * kMarchWaves, st, a);
+  } else if (a.lit) {  // the literal dot order: the LIT instantiation (term stores)
     if (a.mgran) klaunch(h, k_cg_march<MODE, true, 3, kNT, false, true, PK, true>, grid, 64 * kMarchWaves, st, a);
     else klaunch(h, k_cg_march<MODE, true, 3, kNT, false, false, PK, true>, grid, 64 * kMarchWaves, st, a);
   } else if (a.mgran) {
@@ -105,12 +108,20 @@ void launch_cg_spmv(perc_ctx* h, const CGArgs& a, int G) {
       // bands (march_grid): with the x update out of the walk, L = 8192 P
       // 0.314 vs 0.355 ms on one round of slot-weighted bands, 0.628 vs
       // 0.656 ms per solve iteration (profiles/r4_8_l8192_ab.json)
-      // (row-major P keeps the u16 codes: its column-class path for the
-      // nibble codes costs a wave per SIMD or spills -- P 0.389 / 0.363 vs
-      // 0.330 ms at L = 8192; B takes them, profiles/r5_14_ab_rowmajor_nibble_*)
+      // Row-major P on the nibble codes (round 6): the column classes formed
+      // per access and only the open-square path compiled in, 128 VGPRs
+      // without spills at the 4-wave bound (round 5's nibble P spilled:
+      // 0.389 / 0.363 vs 0.330 ms on the u16 codes, profiles/r5_14_*);
+      // a.rm_pnib off (PERC_MARCH_RM_PU16=1, A/Bs): the u16 codes
+      else if (h->qfree && a.lit && a.nib && a.rm_pnib)
+        klaunch(h, k_cg_march<kMarchP, false, kMarchDepth, 0, false, false, true, true>, h->march_grid,
+                64 * kMarchWaves, st, a);
       else if (h->qfree && a.lit)
         klaunch(h, k_cg_march<kMarchP, false, kMarchDepth, 0, false, false, false, true>, h->march_grid,
                 64 * kMarchWaves, st, a);
+      else if (h->qfree && a.nib && a.rm_pnib)
+        klaunch(h, k_cg_march<kMarchP, false, kMarchDepth, 0, false, false, true>, h->march_grid, 64 * kMarchWaves,
+                st, a);
       else if (h->qfree) klaunch(h, k_cg_march<kMarchP>, h->march_grid, 64 * kMarchWaves, st, a);
       // q-storing P+S (row slabs, the literal dot order, modes without QFREE)
       else klaunch(h, k_cg_march<kMarchPQ, false, 3>, h->march_grid, 64 * kMarchWaves, st, a);
@@ -170,17 +181,20 @@ void launch_spmv(perc_ctx* h, const CGArgs& a, const double* x, double* y) {
   else k_spmv_st<6><<<h->grid, kBlock, 0, h->stream>>>(a.St, x, y);
 }
 
-// the row-major march's nibble codes (vectors past the Infinity Cache,
-// square lattice, PERC_MARCH_NIBBLE): 0.5 instead of 2 bytes of row code
-// per element in B (24.5 + 48m / N instead of 26 B per row: 0.297 vs 0.304
-// ms at L = 8192); a row whose upper code bits are not its column class's
-// keeps the u16 codes
-// (B only: k_cg_march<P> reads the u16 codes in the row-major layout)
+// the row-major march's nibble codes (vectors past the Infinity Cache, the
+// open square lattice, PERC_MARCH_NIBBLE): 0.5 instead of 2 bytes of row
+// code per element in P and B (24.5 + 48m / N instead of 26 B per row; B
+// 0.297 vs 0.304 ms at L = 8192); a row whose upper code bits are not its
+// column class's keeps the u16 codes.  (pbc lattices keep the u16 codes: the
+// row-major nibble kernels compile the open-square path only)
 hipError_t to_nib_rows(perc_ctx* h, CGArgs& a) {
   DeviceBuffers& d = h->d;
   hipStream_t st = h->stream;
   h->nib_used = false;
-  if (!kMarchRmNib || !h->nib_ok || !(h->march_mode & PERC_MARCH_NIBBLE) || !h->march || !h->qfree || a.sm)
+  const char* pu16 = std::getenv("PERC_MARCH_RM_PU16");
+  a.rm_pnib = pu16 && pu16[0] == '1' ? 0 : 1;
+  if (!kMarchRmNib || !h->nib_ok || h->g.pbc || !(h->march_mode & PERC_MARCH_NIBBLE) || !h->march || !h->qfree ||
+      a.sm)
     return hipSuccess;
   const long long n = (long long)a.T.nrows * a.T.m;
   if (!d.nib_sm) HIP_TRY(dmalloc(&d.nib_sm, (size_t)h->N / 2 + 16));
@@ -218,6 +232,22 @@ hipError_t setup_granules(perc_ctx* h, CGArgs& a, int itmax) {
   a.mgran_b = h->d.mgran + region;
   a.merr = &h->d.scal->pad[1];
   ++h->solve_epoch;
+  // deferred reductions (k_cg_march DEF, opt-in: PERC_MARCH_DEF=<kDefP |
+  // kDefB bits>): the fast order's march, one slab, grids of <= kDefGroups
+  // reduction groups.  Measured on the metric (profiles/r6_4_def_ab_*): the
+  // collectors' tails are 1.4 (P) and 2.3 us (B), the totals formed at the
+  // next launch's start cost 1.7 (one sum) and 3.7 us (two): 0.1511 ms per
+  // iteration with the collectors, 0.1515 / 0.1527 / 0.1523 deferred (P's,
+  // B's, both) -- the collectors stay the default
+  const int grid = a.wslots > 0 ? h->wm_grid : h->march_grid;
+  const char* nodef = std::getenv("PERC_MARCH_NODEF");
+  const char* defb = std::getenv("PERC_MARCH_DEF");
+  a.mnwg = grid;
+  a.mdef = !a.lit && !a.slab && red_groups(grid) <= kDefGroups && !(nodef && nodef[0] == '1') && defb
+               ? (std::atoi(defb) & (kDefP | kDefB))
+               : 0;
+  const char* dsc1 = std::getenv("PERC_MARCH_DEF_SC1");  // (A/B: the totals' loads past L2)
+  a.mdsc1 = dsc1 && dsc1[0] == '1' ? 1 : 0;
   return hipSuccess;
 }
 
@@ -406,9 +436,13 @@ int march_rows_for(const perc_ctx* h, int nrows) {
 // bands (PERC_MARCH_SLOTS): one workgroup per CU and round, bands cycling
 // over the rounds, weights = the rounds' relative streaming rates with
 // equal bands (kSlotW: P, B of the strip-major march; same-box A/Bs,
-// profiles/r3_4_ab_slotw_L4096.log.  The third set, row-major P past the
-// Infinity Cache, is unused since round 4: that P runs on B's 8-row bands)
-constexpr int kSlotW[3][kMaxSlotRounds] = {{100, 75, 50, 40}, {100, 80, 60, 50}, {100, 100, 100, 100}};
+// profiles/r3_4_ab_slotw_L4096.log; round 6 re-tuned P's for the nibble-code
+// tagged march, whose third slot walked ~2 us longer than the others
+// (profiles/r5_4_mtrace_summary_L4096.txt): 100:76:48 against 100:75:50, P
+// 73.2 vs 75.0 us, 0.1489 vs 0.1511 ms per iteration, r6_4_def_ab_w*.json,
+// r6_5_weights.json.  The third set, row-major P past the Infinity Cache,
+// is unused since round 4: that P runs on B's 8-row bands)
+constexpr int kSlotW[3][kMaxSlotRounds] = {{100, 76, 48, 40}, {100, 80, 60, 50}, {100, 100, 100, 100}};
 
 void march_geometry(perc_ctx* h) {
   const Geom& g = h->g;
@@ -1116,7 +1150,7 @@ hipError_t dev_solve_impl(perc_ctx* h, int itol, double tol, int itmax, bool x0_
   h->last_flags = (literal ? PERC_RAN_LITERAL : 0) | (a.lit ? PERC_RAN_LIT_TERMS : 0) |
                   (h->march && h->qfree ? PERC_RAN_QFREE : 0) | (a.sm ? PERC_RAN_STRIPS : 0) |
                   (a.nib ? PERC_RAN_NIBBLE : 0) | (a.mgran ? PERC_RAN_TAG : 0) |
-                  (host_fold ? PERC_RAN_HOST_FOLD : 0);
+                  (host_fold ? PERC_RAN_HOST_FOLD : 0) | (a.mdef ? PERC_RAN_DEFERRED : 0);
   // iterate in chunks; the device flag makes surplus launches no-ops
   int chunk = 8;
   CGScalars* hsp = nullptr;
@@ -1184,6 +1218,10 @@ hipError_t dev_solve_impl(perc_ctx* h, int itol, double tol, int itmax, bool x0_
         else k_fold_b<false><<<1, 64, 0, st>>>(a);
         HIP_TRY(dbg_sync(st, "k_fold_b"));
       }
+    }
+    if (a.mdef & kDefB) {  // the chunk's last B: its epilogue, for the host's stop test
+      k_march_epi<<<1, 64 * kMarchWaves, 0, st>>>(a);
+      HIP_TRY(dbg_sync(st, "k_march_epi"));
     }
     launched += chunk;
     e = hipGetLastError();
@@ -1292,6 +1330,7 @@ hipError_t dev_bench(perc_ctx* h, int which, int reps, double* ms) {
   if (h->strips && (which == 1 || which == 2 || which == 5)) {
     HIP_TRY(to_strips(h, a));
     HIP_TRY(setup_granules(h, a, hs.itmax));
+    if (a.mdef) a.mdef |= kDefBench;  // the deferred march at a fixed iteration: no stop, no scalars
   } else if (which == 1 || which == 2 || which == 5) {
     HIP_TRY(to_nib_rows(h, a));
   }

@@ -291,3 +291,33 @@ def test_config_fixture(path):
             trunc = rel(ref[g], cv[g])
             bar = max(2 * trunc + max(1e-10, float(tkey)), ASSOC_X * assoc_spread(doc, tkey, g))
             assert d[g + "_rel"] <= bar, (g, trunc, bar, d)
+
+
+@pytest.mark.gpu
+def test_literal_c5m_fixture_bitwise():
+    """Config 5's rule at a size the oracle solves (c5m: 1024^2 square mixed
+    site-then-bond, ps = pb = 0.85, ConductCalc.m:134-160) in the literal dot
+    order through the PRODUCTION march (q-free, strip-major, nibble codes,
+    tagged reductions; PERC_DOT_LITERAL_HOST: the serial sums of the
+    kernels' own terms formed by the host, bitwise the GPU fold): iter, err,
+    Gtop, Gbot and every committed err-history point are the oracle
+    fixture's bitwise at the reference tolerance 1e-8 (5 193 iterations;
+    Square/bondc.f:750-838).  The GPU record of the same run at the other
+    config sizes: profiles/r5_4_literal_*, r6_1_literal_metric_*."""
+    doc = json.load(open(os.path.join(HERE, "golden", "configs", "c5m_sq1024_mixed_p85.json")))
+    rc = doc["recipe"]
+    occ, rule, cur = occupation(rc)
+    ref = doc["solves"]["1e-08"]
+    with api.Context(rc["lattice"], rc["L"], rc["L"], 0) as ctx:
+        ctx.set_march_mode(PL.MARCH_DEFAULT & ~PL.SOLVE_RESIDENT)
+        ctx.occupy(**occ)
+        assert ctx.label()["nspan"] > 0
+        ctx.set_dot_order(PL.DOT_LITERAL_HOST)
+        c = ctx.conductance(rule, cur, tol=1e-8, itmax=10 ** 6)
+        hist = ctx.err_history()
+        ran = ctx.last_solve()
+    assert ran["kernel"] == "march" and ran["lit_terms"] and ran["host_fold"], ran
+    assert ran["qfree"] and ran["strips"] and ran["nibble"] and ran["tag"], ran
+    assert (c["iter"], c["err"], c["gtop"], c["gbot"]) == (ref["iter"], ref["err"], ref["gtop"], ref["gbot"]), \
+        (c, ref["iter"], ref["gtop"], ref["gbot"])
+    assert all(hist[k - 1] == e for k, e in ref["err_history"])

@@ -143,7 +143,7 @@ int main(int argc, char** argv) {
   for (auto& x : e) CK(hipEventCreate(&x));
   auto compress0 = [&]() {
     k_cc_compress<<<std::min(cdiv(g.t, kCcThreads * kCcCompressU), kReduceGrid), kCcThreads>>>(
-        g.t, R.parent, R.member, R.counters);
+        g.t, R.parent, R.member, 0, R.counters);
   };
   auto chain_c = [&](const char* what, auto tilef, auto mergef, auto compressf, bool ref) {
     double t[3] = {0, 0, 0};
@@ -214,10 +214,10 @@ int main(int argc, char** argv) {
   // compress: U sites per thread chased in lockstep (production: kCcCompressU), one site per thread
   chain_c("wave 16 + compress<1>", wave(I16{}, std::integral_constant<int, 2>{}), merge_for(I16{}),
           [&]() { k_cc_compress<1><<<std::min(cdiv(g.t, kCcThreads), kReduceGrid), kCcThreads>>>(
-                      g.t, R.parent, R.member, R.counters); }, false);
+                      g.t, R.parent, R.member, 0, R.counters); }, false);
   chain_c("wave 16 + compress<4>", wave(I16{}, std::integral_constant<int, 2>{}), merge_for(I16{}),
           [&]() { k_cc_compress<4><<<std::min(cdiv(g.t, kCcThreads * 4), kReduceGrid), kCcThreads>>>(
-                      g.t, R.parent, R.member, R.counters); }, false);
+                      g.t, R.parent, R.member, 0, R.counters); }, false);
   // site and mixed kinds (sites occupied at 0.8 by another hash): the production tile kernel vs the candidate
   {
     std::vector<uint8_t> so((size_t)g.t + 2, 0);
