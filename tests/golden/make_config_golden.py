@@ -28,6 +28,8 @@ Gtop / Gbot over the last decades shows where the oracle has converged.
 
 Usage: python tests/golden/make_config_golden.py [case ...]   (CPU, minutes to hours)
        GOLDEN_THREADS=k python tests/golden/make_config_golden.py --decades [case ...]
+       GOLDEN_TOLS=1e-8,1e-9 GOLDEN_PREFIX=2000 GOLDEN_THREADS=6 \
+           python tests/golden/make_config_golden.py --decades c5c_sq8192_mixed_p85_dev
        GOLDEN_THREADS=k python tests/golden/make_config_golden.py --assoc [case ...]
        GOLDEN_THREADS=k python tests/golden/make_config_golden.py --assoc-tree [case ...]
 """
@@ -44,6 +46,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(os.path.dirname(HERE))
 sys.path.insert(0, os.path.join(REPO, "tests"))
 OUT = os.path.join(HERE, "configs")
+OUT_LARGE = os.path.join(HERE, "large")
 
 MASTER = 58302  # bench.py / Square/bond_cond.f:65-70 master seed
 
@@ -69,7 +72,17 @@ CASES = {
     # gives the same ids, tests/test_labeling_oracle.py; round 4)
     "bench_sq4096_bond_p60_dev": dict(lattice=0, L=4096, kind="bond", p=0.60, order="device",
                                       ii=2),
+    # config 5's near-critical companion at its own size (round 6): 8192^2 square mixed
+    # site-then-bond at ps = pb = 0.85, both occupations drawn on the GPU by
+    # perc_occupy_random(PERC_SITEBOND, seed 777) as tools/l8192_probe.py does (host
+    # restatement perc_random_order), ConductCalc.m:134-160 mixed rule; vectors past the
+    # Infinity Cache, so the production solver is the ROW-MAJOR q-free march.  Kept in
+    # tests/golden/large/ (decades 1e-8, 1e-9 and the complete err history of the first
+    # GOLDEN_PREFIX iterations; not a converged fixture): tests/test_large_fixture.py
+    "c5c_sq8192_mixed_p85_dev": dict(lattice=0, L=8192, kind="mixed", p=0.85, pb=0.85,
+                                     order="device", seed=777),
 }
+LARGE = {"c5c_sq8192_mixed_p85_dev"}  # written to tests/golden/large/
 TOLS = (1e-8, 1e-13, 1e-14)
 # --decades: one threaded run of the same iterates (oracle or_linbcg_sym, bitwise the
 # literal linbcg's on these symmetric systems) snapshotting x at every tolerance here
@@ -157,10 +170,22 @@ def label_case(rc, seed):
                         b1[np.argmax(label == perccln)] - 1])))
         sysin = dict(b1=b1, b2=b2, gval=gval, rhs_rule=0, cur_rule=0, cur_thresh=1e-10)
     elif rc["kind"] == "mixed":
-        b1, b2, o1, o2 = O.bond_order(lattice, L, L, 0, rc["bseed"])
-        nb = len(b1)
-        so = O.site_order(t, rc["sseed"])
-        ts, tb = int(rc["p"] * t), int(rc["pb"] * nb)
+        if rc["order"] == "device":  # perc_occupy_random(PERC_SITEBOND, seed): host restatement
+            sys.path.insert(0, REPO)
+            from percolation_amd import _lib as PL, api
+            b1, b2 = O.bond_list(lattice, L, L, 0)
+            nb = len(b1)
+            ts, tb = int(rc["p"] * t), int(rc["pb"] * nb)
+            so = O.i32(t + 1)
+            so[:ts] = api.random_order(t, ts, rc["seed"], PL.SITE)
+            ids = api.random_order(nb, tb, rc["seed"], PL.BOND).astype(np.int64) - 1
+            o1, o2 = O.i32(nb + 1), O.i32(nb + 1)
+            o1[:tb], o2[:tb] = b1[ids], b2[ids]
+        else:
+            b1, b2, o1, o2 = O.bond_order(lattice, L, L, 0, rc["bseed"])
+            nb = len(b1)
+            so = O.site_order(t, rc["sseed"])
+            ts, tb = int(rc["p"] * t), int(rc["pb"] * nb)
         s, bl, csize, cln, maxcn, maxcs = O.label_sitebond(lattice, L, L, 0, b1, b2, so, ts, o1,
                                                            o2, tb, literal=False)
         perccln = lib.or_span_sites(L, L, s, csize, cln, 2 * L - 1)
@@ -195,7 +220,7 @@ def label_case(rc, seed):
 
 def find_seed(rc, kmax=64):
     O = _oracle()
-    if "sseed" in rc:  # fixed seeds (the mixed case)
+    if "sseed" in rc or "seed" in rc:  # fixed seeds (the mixed cases)
         r = label_case(rc, 0)
         if r is None:
             raise RuntimeError("no spanning cluster")
@@ -243,8 +268,11 @@ def decades(case):
                                       cur_rule=sysin["cur_rule"], cur_thresh=sysin["cur_thresh"],
                                       threads=int(os.environ.get("GOLDEN_THREADS", 2)))
     secs = time.time() - t0
-    path = os.path.join(OUT, case + ".json")
+    path = os.path.join(OUT_LARGE if case in LARGE else OUT, case + ".json")
     doc = json.load(open(path)) if os.path.exists(path) else {}
+    kpre = int(os.environ.get("GOLDEN_PREFIX", "0"))
+    if kpre:  # the complete err history of the first kpre iterations (bitwise prefix tests)
+        doc["err_prefix"] = [float(e) for e in errs[:kpre]]
     if doc:
         assert doc["label"]["canon_sha256"] == info["canon_sha256"], case
     solves = doc.setdefault("solves", {})
@@ -266,6 +294,7 @@ def decades(case):
                label=dict(doc.get("label", {}), **info))
     doc["decades_run"] = dict(seconds=secs, tols=list(TOLS_DECADES),
                               threads=int(os.environ.get("GOLDEN_THREADS", 2)))
+    os.makedirs(os.path.dirname(path), exist_ok=True)
     with open(path, "w") as f:
         json.dump(doc, f, indent=1)
 

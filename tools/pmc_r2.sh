@@ -14,7 +14,7 @@ L=${L:-4096}
 # nibble codes too since round 5.  PROBE_ARGS: extra pmc_probe.py arguments
 # (e.g. "--kind sitebond --ps 0.85 --p 0.85": the config-5 companion)
 CBX2=${CBX2:-1}
-CBX2P=${CBX2P:-$CBX2}  # P's (the row-major P keeps the u16 codes: CBX2P=4 at L = 8192)
+CBX2P=${CBX2P:-$CBX2}  # P's (round 6: the row-major P reads the nibble codes too; CBX2P=4 for PERC_MARCH_RM_PU16=1)
 PROBE_ARGS=${PROBE_ARGS:-}
 N=$((L * L - 2 * L))
 timeout -k 10 300 python -c "import torch; torch.cuda.init()" || exit 1
