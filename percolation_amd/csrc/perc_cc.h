@@ -357,10 +357,8 @@ __global__ __launch_bounds__(64) void k_cc_tile_w(Geom g, const uint8_t* bocc, c
   auto ld8 = [](__amdgpu_buffer_rsrc_t r, bool ok, unsigned off) {
     return (unsigned)__builtin_amdgcn_raw_buffer_load_b8(r, (int)(ok ? off : kOOB), 0, 0);
   };
-  // R / U: the link right / up of the lane's two sites; O: the site occupied;
-  // X (bond kind): the link into lane 0's first-column site from the left
-  // block (member flag only)
-  auto load_row = [&](int r, unsigned (&R)[2], unsigned (&U)[2], unsigned (&O)[2], unsigned& X) {
+  // R / U: the link right / up of the lane's two sites; O: the site occupied
+  auto load_row = [&](int r, unsigned (&R)[2], unsigned (&U)[2], unsigned (&O)[2]) {
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       const int lc = lane + 64 * h, col = c0 + lc, row = r0 + r;
@@ -383,12 +381,6 @@ __global__ __launch_bounds__(64) void k_cc_tile_w(Geom g, const uint8_t* bocc, c
         }
       }
     }
-    if constexpr (KIND == PERC_BOND) {
-      const bool hx = lane == 0 && c0 > 0 && r < th;
-      X = ld8(rb, hx, (unsigned)bf_open_square(g, r0 + r, hx ? c0 - 1 : 0));
-    } else {
-      X = 0u;
-    }
   };
   auto finish = [&](unsigned (&R)[2], unsigned (&U)[2], unsigned (&O)[2]) {
     if constexpr (KIND != PERC_BOND) {
@@ -399,11 +391,17 @@ __global__ __launch_bounds__(64) void k_cc_tile_w(Geom g, const uint8_t* bocc, c
       }
     }
   };
-  unsigned Rq[D][2], Uq[D][2], Oq[D][2], Xq[D], R[2], U[2], O[2], X, Up[2] = {0u, 0u};
+  unsigned Rq[D][2], Uq[D][2], Oq[D][2], R[2], U[2], O[2], Up[2] = {0u, 0u};
   int labp[2] = {0, 0};
   unsigned nodes[H], Mb[2] = {0u, 0u};
+  // bond kind, the links crossing into the block's edge sites (member flags
+  // only): Xl -- lane r holds the left block's link into row r's column 0
+  // (one load for the block, read back per row with a readlane); Up of the
+  // first row -- the row below's up links
+  unsigned Xl = 0u;
   if constexpr (KIND == PERC_BOND) {
-    // the up links of the row below the block: the first row's member flags
+    const bool hx = c0 > 0 && lane < th;
+    Xl = ld8(rb, hx, (unsigned)bf_open_square(g, hx ? r0 + lane : 0, hx ? c0 - 1 : 0));
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       const int lc = lane + 64 * h, col = c0 + lc;
@@ -412,7 +410,7 @@ __global__ __launch_bounds__(64) void k_cc_tile_w(Geom g, const uint8_t* bocc, c
     }
   }
 #pragma unroll
-  for (int d = 0; d < D; ++d) load_row(d, Rq[d], Uq[d], Oq[d], Xq[d]);
+  for (int d = 0; d < D; ++d) load_row(d, Rq[d], Uq[d], Oq[d]);
   const unsigned long long le = lane == 63 ? ~0ull : ((2ull << lane) - 1ull);
   const bool v0 = lane < tw, v1 = lane + 64 < tw;
   const unsigned long long vm0 = __ballot(v0), vm1 = __ballot(v1);
@@ -427,9 +425,9 @@ __global__ __launch_bounds__(64) void k_cc_tile_w(Geom g, const uint8_t* bocc, c
       U[h] = Uq[r % D][h];
       O[h] = Oq[r % D][h];
     }
-    X = Xq[r % D];
     finish(R, U, O);
-    load_row(r + D, Rq[r % D], Uq[r % D], Oq[r % D], Xq[r % D]);  // (past th: nothing loaded)
+    load_row(r + D, Rq[r % D], Uq[r % D], Oq[r % D]);  // (past th: nothing loaded)
+    const unsigned X = KIND == PERC_BOND && lane == 0 ? (unsigned)__builtin_amdgcn_readlane((int)Xl, r) : 0u;
     bool left0, left1;
     unsigned long long lo, hi, lm0 = 0, lm1 = 0;
     if constexpr (BAL) {

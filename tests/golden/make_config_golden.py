@@ -270,11 +270,11 @@ def decades(case):
     secs = time.time() - t0
     path = os.path.join(OUT_LARGE if case in LARGE else OUT, case + ".json")
     doc = json.load(open(path)) if os.path.exists(path) else {}
+    if doc:
+        assert doc["label"]["canon_sha256"] == info["canon_sha256"], case
     kpre = int(os.environ.get("GOLDEN_PREFIX", "0"))
     if kpre:  # the complete err history of the first kpre iterations (bitwise prefix tests)
         doc["err_prefix"] = [float(e) for e in errs[:kpre]]
-    if doc:
-        assert doc["label"]["canon_sha256"] == info["canon_sha256"], case
     solves = doc.setdefault("solves", {})
     for r in res:
         key = "%g" % r["tol"]
