@@ -96,6 +96,10 @@ struct CGArgs {
   int mnwg;
   int mdsc1;  // deferred totals read the granules with sc1 loads (else plain, through L2)
   int rm_pnib;  // the row-major march P reads the nibble codes too (else the u16 codes)
+  // strip-major q-free march, x on the two electrode-side rows only (the
+  // fast order, no deferred totals): B(k + 1) applies iteration k's x +=
+  // ak(k) p(k) to those rows at its start, k_march_xpend the last one
+  int mxin;
   // literal dot order on the q-free march (PERC_DOT_LITERAL): the march P
   // stores each row's q.p term and the march B each row's z.r and r.r terms
   // (the reference's IEEE products) at their row-major index into lit[0..N),
@@ -1155,6 +1159,7 @@ CGArgs make_cg_args(perc_ctx* h) {
   a.mnwg = 0;
   a.mdsc1 = 0;
   a.rm_pnib = 0;
+  a.mxin = 0;
   a.lit = nullptr;
   return a;
 }

@@ -64,6 +64,9 @@ struct CGScalars {
   // iteration j (j >= 1; iteration 0's is bknum above), parity-buffered so
   // a launch reads the previous value while its writer stores the new one
   double bkn[2];
+  // ak of the previous iteration (the march P's collector keeps it when it
+  // forms the new ak): B(k + 1) applies x += ak(k) p(k) at its start (CGArgs::mxin)
+  double akprev;
 };
 
 struct AsmParams {

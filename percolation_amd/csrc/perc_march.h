@@ -926,7 +926,38 @@ __global__ __launch_bounds__(64 * kMarchWaves, DEF ? 3 : PERC_MARCH_MINW(SM, MOD
     for (int u = 0; u < D; ++u)
       if (u < nsteps) march_load<MODE, SM, PAUX, PK>(a, g, B, up ? g.rend - u : g.r0 - 1 + u, first, psrc, ring[u]);
   }
+  // (B, strip-major, fast order, x on the electrode-side rows: iteration
+  // k - 1's x update of those rows, its loads issued behind the ring's)
+  constexpr bool kXin = MODE == kMarchB && SM && !LIT && !DEF;
+  const bool xin = kXin && a.mxin && k > 1 && active;
+  double2 xo[2], po[2];
+  if constexpr (kXin) {
+    const __amdgpu_buffer_rsrc_t rx = rsrc(a.x, (unsigned)a.St.N * 8u);
+    const __amdgpu_buffer_rsrc_t rp = rsrc(a.pb[(k - 1) & 1], (unsigned)a.St.N * 8u);
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const int xr = e ? nrows - 1 : 0;  // the rows next to the electrodes
+      const bool own = xin && xr >= g.r0 && xr < g.rend && (e == 0 || nrows > 1);
+      xo[e] = bld2(rx, own ? (unsigned)(xr * m + g.col) * 8u : kOOB);
+      po[e] = bld2(rp, own ? (unsigned)sm_at(a.T, xr, g.col) * 8u : kOOB);
+    }
+  }
   if (S->done) return;
+  if constexpr (kXin) {
+    // x(k-1) += ak(k-1) p(k-1): the same per-element expression as the
+    // update after the walk it replaces (bitwise the same voltages), whose
+    // reload held the bands of those rows 2.2 us past their walk (B 73.9 vs
+    // 71.7 us without any x update, profiles/r6_10_ab_nobx.json)
+    const double akp = S->akprev;
+    const __amdgpu_buffer_rsrc_t rx = rsrc(a.x, (unsigned)a.St.N * 8u);
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const int xr = e ? nrows - 1 : 0;
+      const bool own = xin && xr >= g.r0 && xr < g.rend && (e == 0 || nrows > 1);
+      bst2<0>(rx, own ? (unsigned)(xr * m + g.col) * 8u : kOOB,
+              make_double2(xo[e].x + akp * po[e].x, xo[e].y + akp * po[e].y));
+    }
+  }
   if (threadIdx.x < kMaxForms) {
     s_rpos[threadIdx.x] = a.St.F.rpos[threadIdx.x];
     s_rmap[threadIdx.x] = a.St.F.rmap[threadIdx.x];
@@ -984,7 +1015,7 @@ __global__ __launch_bounds__(64 * kMarchWaves, DEF ? 3 : PERC_MARCH_MINW(SM, MOD
         *reinterpret_cast<double2*>(a.x + i) = xv;
       }
     }
-    if (MODE == kMarchB && SM) {
+    if (MODE == kMarchB && SM && !(kXin && a.mxin)) {
       // strip-major q-free solve: x (row-major) += ak p(k) on the band's x
       // rows, after the walk (loads and stores inside it would put a
       // vmcnt(0) in every step); k_cg_b's x update of the q-storing solve
@@ -1042,6 +1073,7 @@ __global__ __launch_bounds__(64 * kMarchWaves, DEF ? 3 : PERC_MARCH_MINW(SM, MOD
           S->part[0] = tot[0];
           if (a.pub) a.pub[0] = tot[0];
         } else {
+          S->akprev = S->ak;
           S->akden = tot[0];
           S->ak = bkn_it / tot[0];
         }
@@ -1072,6 +1104,18 @@ __global__ __launch_bounds__(64 * kMarchWaves, DEF ? 3 : PERC_MARCH_MINW(SM, MOD
   }
 }
 
+
+// The last iteration's x update of the electrode-side rows (CGArgs::mxin):
+// x += ak(K) p(K), p(K) strip-major in pb[K & 1]; m threads per row
+__global__ __launch_bounds__(kBlock) void k_march_xpend(CGArgs a) {
+  const CGScalars* S = a.S;
+  const int m = a.T.m, nrows = a.T.nrows, K = S->iter;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (K < 1 || i >= 2 * m || (i >= m && nrows < 2)) return;
+  const int row = i < m ? 0 : nrows - 1, col = i < m ? i : i - m;
+  const double* __restrict__ p = a.pb[K & 1];
+  a.x[row * m + col] = a.x[row * m + col] + S->ak * p[sm_at(a.T, row, col)];
+}
 
 // The deferred epilogue of a chunk's last B (DEF): one workgroup of the
 // march's shape forms the z.r and r.r totals as the next P would and stores

@@ -1144,6 +1144,11 @@ hipError_t dev_solve_impl(perc_ctx* h, int itol, double tol, int itmax, bool x0_
   if (h->strips) HIP_TRY(to_strips(h, a));
   else HIP_TRY(to_nib_rows(h, a));
   HIP_TRY(setup_granules(h, a, itmax));
+  // x on the electrode-side rows, each iteration's update applied by the
+  // next B at its start (k_cg_march, kXin), the last by k_march_xpend
+  // (PERC_MARCH_XAFTER=1: the update after each B's walk, same-box A/Bs)
+  const char* xafter = std::getenv("PERC_MARCH_XAFTER");
+  a.mxin = a.sm && !a.lit && !a.mdef && !a.slab && a.xrows == h->g.m && !(xafter && xafter[0] == '1') ? 1 : 0;
   HostFold hf;
   const bool host_fold = a.lit && h->dot_order == PERC_DOT_LITERAL_HOST;
   if (host_fold) HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&hf.t), sizeof(double) * 3 * (size_t)h->N));
@@ -1256,6 +1261,11 @@ hipError_t dev_solve_impl(perc_ctx* h, int itol, double tol, int itmax, bool x0_
     e = dbg_sync(st, "k_cg_xfinal");
     if (e == hipSuccess) e = hipStreamSynchronize(st);
   }
+  if (e == hipSuccess && hsp->iter > 0 && a.mxin) {  // the last B's x update
+    k_march_xpend<<<cdiv(2 * h->g.m, kBlock), kBlock, 0, st>>>(a);
+    e = dbg_sync(st, "k_march_xpend");
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+  }
   if (mtbuf) {
     std::vector<unsigned long long> tr((size_t)2 * kMtN * 4 * mtwaves);
     if (e == hipSuccess) e = hipMemcpy(tr.data(), mtbuf, tr.size() * 8, hipMemcpyDeviceToHost);
@@ -1331,6 +1341,7 @@ hipError_t dev_bench(perc_ctx* h, int which, int reps, double* ms) {
     HIP_TRY(to_strips(h, a));
     HIP_TRY(setup_granules(h, a, hs.itmax));
     if (a.mdef) a.mdef |= kDefBench;  // the deferred march at a fixed iteration: no stop, no scalars
+    a.mxin = !a.mdef && a.xrows == h->g.m ? 1 : 0;  // (the production B's x path)
   } else if (which == 1 || which == 2 || which == 5) {
     HIP_TRY(to_nib_rows(h, a));
   }
