@@ -100,6 +100,10 @@ struct CGArgs {
   // fast order, no deferred totals): B(k + 1) applies iteration k's x +=
   // ak(k) p(k) to those rows at its start, k_march_xpend the last one
   int mxin;
+  // strip-major march: {p(k), z = r/d} of every strip's first and last
+  // column, per row ([strip][side][row] double2), stored by B for the next
+  // P's halo columns (k_edge_init fills z from r0 for the first P)
+  double* ez;
   // literal dot order on the q-free march (PERC_DOT_LITERAL): the march P
   // stores each row's q.p term and the march B each row's z.r and r.r terms
   // (the reference's IEEE products) at their row-major index into lit[0..N),
@@ -1160,6 +1164,7 @@ CGArgs make_cg_args(perc_ctx* h) {
   a.mdsc1 = 0;
   a.rm_pnib = 0;
   a.mxin = 0;
+  a.ez = nullptr;
   a.lit = nullptr;
   return a;
 }

@@ -91,6 +91,7 @@ struct DeviceBuffers {
   uint16_t* code = nullptr;  // N (+pad)
   uint16_t* code_sm = nullptr;  // strip-major copy of code (PERC_MARCH_STRIPS solves)
   uint8_t* nib_sm = nullptr;    // strip-major nibble codes (PERC_MARCH_NIBBLE, square lattice)
+  double* ez = nullptr;         // strip-major march: edge-column z per strip side and row (CGArgs::ez)
   double2* dtab = nullptr;    // 512: the diagonal of every code (see diag_idx)
   int* sflag = nullptr;      // 4
   // occupancy

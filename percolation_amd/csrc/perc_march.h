@@ -52,6 +52,10 @@ template <int AUX>
 __device__ __forceinline__ void bst2(__amdgpu_buffer_rsrc_t r, unsigned off, double2 v) {
   __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, (int)off, 0, AUX);
 }
+// one double (the edge z stores)
+__device__ __forceinline__ void bst2e(__amdgpu_buffer_rsrc_t r, unsigned off, double v) {
+  __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), r, (int)off, 0, 0);
+}
 
 // publish_and_reduce with tagged granules (the march kernels, TAG): every
 // partial travels as one 16-B write-through {value, tag} store (untorn), so
@@ -491,6 +495,10 @@ constexpr int kMarchPQ = 0, kMarchP = 1, kMarchB = 2;
 struct MGeom {
   int r0, rend, col, hcol;
   bool hok;
+  // strip-major edge {p, z} (CGArgs::ez), pair bases: ezh -- the halo
+  // column's (P's lanes 0 and 63), ezo -- the lane's own edge column (B's
+  // lanes 0 and 63 store there)
+  int ezh, ezo;
   unsigned cb0, cb1, cbh;  // nibble codes (PK): count / form bits of col, col+1, hcol
   // open square lattice with nibble codes (PK): the slot bits of element 0 /
   // 1 in the INTERIOR form's slot numbering, c' = (c & lo) | ((c & hi) << 1)
@@ -513,6 +521,7 @@ struct MGeom {
 struct MBuf {
   __amdgpu_buffer_rsrc_t p, r, c, pn, q;  // p(k-1), r, codes, p(k): rows [lo, hi); q: own rows
   __amdgpu_buffer_rsrc_t t;  // literal dot terms (a.lit, row-major; size 0 in the fast order)
+  __amdgpu_buffer_rsrc_t ez;  // strip-major: the edge z array (CGArgs::ez)
   int lo, hi;
 };
 
@@ -535,8 +544,10 @@ __device__ __forceinline__ MBuf march_bufs(const CGArgs& a, const MGeom& g, cons
     B.c = PK ? rsrc(a.nib, nall / 2u) : rsrc(a.St.code, nall * 2u);
     B.pn = rsrc(pnew, nall * 8u);
     B.q = rsrc(a.q, MODE == kMarchPQ ? nall * 8u : 0u);
+    B.ez = rsrc(a.ez, a.ez ? (unsigned)(2 * (m / kMarchW) * a.T.nrows) * 16u : 0u);
     return B;
   }
+  B.ez = rsrc(nullptr, 0u);
   const long long base = (long long)B.lo * m;
   const unsigned n = (unsigned)(B.hi - B.lo) * (unsigned)m;
   const unsigned nown = (unsigned)max(g.rend - g.r0, 0) * (unsigned)m;
@@ -571,7 +582,11 @@ __device__ __forceinline__ void march_load(const CGArgs& a, const MGeom& g, cons
     const unsigned eh = rowok ? melem<SM>(a, B, gr, g.hcol) : 0u;
     const unsigned o8 = rowok ? e * 8u : kOOB;
     const bool rown = MODE != kMarchB || (gr >= g.r0 && gr < g.rend);
+#if defined(PERC_PROBE_NO_PHALO)  // (A/B probe builds only: P's halo-column loads' cost, wrong values)
+    const bool hk = rowok && g.hok && MODE == kMarchB;
+#else
     const bool hk = rowok && g.hok;
+#endif
     const unsigned h8 = hk ? eh * 8u : kOOB;
     if constexpr (PK) {
       // the pair's two slot nibbles in one byte (element e even); the count
@@ -588,7 +603,16 @@ __device__ __forceinline__ void march_load(const CGArgs& a, const MGeom& g, cons
     constexpr int kPAux = MODE == kMarchP ? PAUX : 0;
     R.r = __builtin_bit_cast(double2, __builtin_amdgcn_raw_buffer_load_b128(B.r, (int)(rown ? o8 : kOOB), 0, kRAux));
     R.p = __builtin_bit_cast(double2, __builtin_amdgcn_raw_buffer_load_b128(B.p, (int)(first ? kOOB : o8), 0, kPAux));
-    if (MODE != kMarchB) {
+    if (MODE != kMarchB && SM) {
+      // strip-major: the halo column's p(k-1) and z = r/d as the last B
+      // stored them (edge {p, z}): one 16-B load instead of its code, r and
+      // p, and no division -- the three halo loads held P 2.5 us (71.4 vs
+      // 73.9 us without them, profiles/r6_13_ab_p.json)
+      const double2 e = bld2(B.ez, hk ? (unsigned)(g.ezh + gr) * 16u : kOOB);
+      R.hc = 0u;
+      R.hr = e.y;  // z
+      R.hp = e.x;  // p(k-1)
+    } else if (MODE != kMarchB) {
       if constexpr (PK) {
         const unsigned b = __builtin_amdgcn_raw_buffer_load_b8(B.c, (int)(hk ? eh / 2u : kOOB), 0, 0);
         R.hc = ((b >> (4u * (eh & 1u))) & 0xFu) | (SM ? g.cbh : col_cls(a, g.hcol));
@@ -600,7 +624,7 @@ __device__ __forceinline__ void march_load(const CGArgs& a, const MGeom& g, cons
       R.hc = 0u;
       R.hr = 0.0;
     }
-    R.hp = bld1(B.p, first ? kOOB : h8);
+    if (MODE == kMarchB || !SM) R.hp = bld1(B.p, first ? kOOB : h8);
   }
 }
 
@@ -641,7 +665,7 @@ __device__ __forceinline__ void march_step(const CGArgs& a, const MGeom& g, cons
         pn.y = bk * R.p.y + z1;
       }
       if (g.hok) {
-        const double zh = div_tab(R.hr, s_dt[diag_idx(R.hc)]);
+        const double zh = SM ? R.hr : div_tab(R.hr, s_dt[diag_idx(R.hc)]);  // (SM: the edge z)
         hpn = first ? zh : bk * R.hp + zh;
       }
     }
@@ -760,6 +784,14 @@ __device__ __forceinline__ void march_step(const CGArgs& a, const MGeom& g, cons
       rn.y = W.rM.y - ak * q1;
       mr = rn;
       const double z0 = div_tab(rn.x, dM0), z1 = div_tab(rn.y, dM1);
+      if constexpr (SM) {  // {p(k), z} of the edge columns: the next P's halo (lanes 0 and 63)
+        const bool ed = mown && (lane == 0 || lane == 63);
+        // (issued by every lane, the others' offsets out of range: under a
+        // divergent branch with two active lanes B took 0.7 us longer,
+        // profiles/r6_16_ab_edgestore.json)
+        bst2<0>(B.ez, ed ? (unsigned)(g.ezo + mid) * 16u : kOOB,
+                lane == 0 ? make_double2(W.C.e0, z0) : make_double2(W.C.e1, z1));
+      }
       t0 = make_double2(z0 * rn.x, z1 * rn.y);  // bknum's terms (bondc.f:785-787)
       t1 = make_double2(rn.x * rn.x, rn.y * rn.y);  // snrm's (:872-875)
       acc[0] = acc[0] + t0.x;
@@ -901,6 +933,11 @@ __global__ __launch_bounds__(64 * kMarchWaves, DEF ? 3 : PERC_MARCH_MINW(SM, MOD
   if (g.hcol < 0 || g.hcol >= m) {
     if (a.T.pbc) g.hcol += g.hcol < 0 ? m : -m;
     else g.hok = false;
+  }
+  {
+    const int hs = g.hcol / kMarchW, hside = g.hcol % kMarchW == kMarchW - 1 ? 1 : 0;
+    g.ezh = (2 * hs + hside) * nrows;
+    g.ezo = (2 * strip + (lane == 63 ? 1 : 0)) * nrows;
   }
   const bool up = (a.march_alt && (band & 1)) != (MODE == kMarchB);
   const int nsteps = g.rend - g.r0 + 2;
@@ -1104,6 +1141,18 @@ __global__ __launch_bounds__(64 * kMarchWaves, DEF ? 3 : PERC_MARCH_MINW(SM, MOD
   }
 }
 
+
+// the edge {p, z} of the first P: z = r0/d of every strip's first and last
+// column (B stores both later), the same division the march forms; p(0) is
+// not read (the first P takes p = z)
+__global__ __launch_bounds__(kBlock) void k_edge_init(CGArgs a) {
+  const int nrows = a.T.nrows, spr = a.T.m / kMarchW;
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= 2 * spr * nrows) return;
+  const int row = e % nrows, ss = e / nrows, strip = ss / 2, side = ss % 2;
+  const int i = sm_at(a.T, row, strip * kMarchW + (side ? kMarchW - 1 : 0));
+  reinterpret_cast<double2*>(a.ez)[e] = make_double2(0.0, div_tab(a.r[i], a.St.dtab[diag_idx(a.St.code[i])]));
+}
 
 // The last iteration's x update of the electrode-side rows (CGArgs::mxin):
 // x += ak(K) p(K), p(K) strip-major in pb[K & 1]; m threads per row

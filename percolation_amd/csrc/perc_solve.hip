@@ -404,7 +404,7 @@ void dev_free_all(perc_ctx* h) {
                   d.p0, d.p1, d.q, d.partials, d.tickets, d.scal, d.err_hist, d.iout,
                   d.res_xch, d.res_bar, d.bw, d.code_sm, d.csize, d.res_gran, (void*)d.nib_sm,
                   d.sel_hist, d.sel_cand, d.mgran, d.forms_dev, d.lit, d.ccpart, d.ell_col, d.ell_val,
-                  d.ell_cnt, d.res_reg, d.res_xg};
+                  d.ell_cnt, d.res_reg, d.res_xg, d.ez};
   for (void* p : ptrs)
     if (p) hipFree(p);
   d = DeviceBuffers{};
@@ -556,6 +556,12 @@ hipError_t to_strips(perc_ctx* h, CGArgs& a) {
   a.r = d.q;
   a.q = d.r;
   a.St.code = d.code_sm;
+  // edge {p, z} (the march P's halo columns), the first P's from r0
+  const long long ne = 2ll * (a.T.m / kMarchW) * a.T.nrows;
+  if (!d.ez) HIP_TRY(dmalloc(&d.ez, 2 * (size_t)ne + 8));  // {p, z} pairs
+  a.ez = d.ez;
+  k_edge_init<<<blocks_for(ne), kBlock, 0, st>>>(a);
+  HIP_TRY(dbg_sync(st, "k_edge_init"));
   a.sm = 1;
   a.bx = 1;  // x (row-major) is updated in the q-free march B
   // nibble codes (PERC_MARCH_NIBBLE, square lattice): 0.5 instead of 2
