@@ -975,7 +975,7 @@ int perc_set_band_weights(perc_ctx* h, int which, int n, const int* w) {
     h->slot_w_set = false;
   } else {
     if (!h->slot_w_set) {  // start from the defaults
-      const int def[3][4] = {{100, 76, 48, 40}, {100, 80, 60, 50}, {100, 100, 100, 100}};  // (kSlotW)
+      const int def[3][4] = {{100, 76, 48, 40}, {100, 78, 55, 50}, {100, 100, 100, 100}};  // (kSlotW)
       std::memcpy(h->slot_w, def, sizeof(def));
     }
     for (int i = 0; i < 4; ++i) h->slot_w[which][i] = i < n ? w[i] : h->slot_w[which][i];

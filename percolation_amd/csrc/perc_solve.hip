@@ -440,9 +440,11 @@ int march_rows_for(const perc_ctx* h, int nrows) {
 // tagged march, whose third slot walked ~2 us longer than the others
 // (profiles/r5_4_mtrace_summary_L4096.txt): 100:76:48 against 100:75:50, P
 // 73.2 vs 75.0 us, 0.1489 vs 0.1511 ms per iteration, r6_4_def_ab_w*.json,
-// r6_5_weights.json.  The third set, row-major P past the Infinity Cache,
-// is unused since round 4: that P runs on B's 8-row bands)
-constexpr int kSlotW[3][kMaxSlotRounds] = {{100, 76, 48, 40}, {100, 80, 60, 50}, {100, 100, 100, 100}};
+// r6_5_weights.json; and B's 100:78:55 against 100:80:60 once B stores the
+// edge {p, z}: B 71.6 vs 72.4 us, r6_17_weights.json, r6_18_weights.json).
+// The third set, row-major P past the Infinity Cache, is unused since round
+// 4: that P runs on B's 8-row bands)
+constexpr int kSlotW[3][kMaxSlotRounds] = {{100, 76, 48, 40}, {100, 78, 55, 50}, {100, 100, 100, 100}};
 
 void march_geometry(perc_ctx* h) {
   const Geom& g = h->g;
