@@ -104,6 +104,7 @@ struct CGArgs {
   // column, per row ([strip][side][row] double2), stored by B for the next
   // P's halo columns (k_edge_init fills z from r0 for the first P)
   double* ez;
+  int mes;  // the strip-major B stages its edge pairs in LDS (every band <= kEdgeRows rows)
   // literal dot order on the q-free march (PERC_DOT_LITERAL): the march P
   // stores each row's q.p term and the march B each row's z.r and r.r terms
   // (the reference's IEEE products) at their row-major index into lit[0..N),
@@ -1165,6 +1166,7 @@ CGArgs make_cg_args(perc_ctx* h) {
   a.rm_pnib = 0;
   a.mxin = 0;
   a.ez = nullptr;
+  a.mes = 0;
   a.lit = nullptr;
   return a;
 }

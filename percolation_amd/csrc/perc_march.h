@@ -358,6 +358,7 @@ __device__ __forceinline__ bool march_def_epilogue(const CGArgs& a, int kk, cons
 }
 
 constexpr int kMarchW = 128;     // columns per wave strip
+constexpr int kEdgeRows = 64;    // band rows whose edge pairs B can stage in LDS (ES)
 constexpr int kMarchWaves = 4;   // waves (strips) per workgroup
 // A/B probe builds only: the column-class path in the row-major march too
 // (PERC_MARCH_RM_SQ), optionally held to 4 waves per SIMD (PERC_MARCH_RM_SQ4)
@@ -548,6 +549,8 @@ __device__ __forceinline__ MBuf march_bufs(const CGArgs& a, const MGeom& g, cons
     return B;
   }
   B.ez = rsrc(nullptr, 0u);
+  // (the row-major nibble march: edge pairs too)
+  if (PK) B.ez = rsrc(a.ez, a.ez ? (unsigned)(2 * (m / kMarchW) * a.T.nrows) * 16u : 0u);
   const long long base = (long long)B.lo * m;
   const unsigned n = (unsigned)(B.hi - B.lo) * (unsigned)m;
   const unsigned nown = (unsigned)max(g.rend - g.r0, 0) * (unsigned)m;
@@ -603,8 +606,8 @@ __device__ __forceinline__ void march_load(const CGArgs& a, const MGeom& g, cons
     constexpr int kPAux = MODE == kMarchP ? PAUX : 0;
     R.r = __builtin_bit_cast(double2, __builtin_amdgcn_raw_buffer_load_b128(B.r, (int)(rown ? o8 : kOOB), 0, kRAux));
     R.p = __builtin_bit_cast(double2, __builtin_amdgcn_raw_buffer_load_b128(B.p, (int)(first ? kOOB : o8), 0, kPAux));
-    if (MODE != kMarchB && SM) {
-      // strip-major: the halo column's p(k-1) and z = r/d as the last B
+    if (MODE != kMarchB && (SM || PK)) {
+      // strip-major, and the row-major nibble march: the halo column's p(k-1) and z = r/d as the last B
       // stored them (edge {p, z}): one 16-B load instead of its code, r and
       // p, and no division -- the three halo loads held P 2.5 us (71.4 vs
       // 73.9 us without them, profiles/r6_13_ab_p.json)
@@ -624,7 +627,7 @@ __device__ __forceinline__ void march_load(const CGArgs& a, const MGeom& g, cons
       R.hc = 0u;
       R.hr = 0.0;
     }
-    if (MODE == kMarchB || !SM) R.hp = bld1(B.p, first ? kOOB : h8);
+    if (MODE == kMarchB || !(SM || PK)) R.hp = bld1(B.p, first ? kOOB : h8);
   }
 }
 
@@ -636,13 +639,14 @@ struct MState {
 
 // one step: row gr enters the window, then the middle row (gr -+ 1) is
 // finished when it is one of the band's own rows
-template <int MODE, bool UP, bool SM, bool LIT = false, bool PK = false>
+template <int MODE, bool UP, bool SM, bool LIT = false, bool PK = false, bool ES = false>
 __device__ __forceinline__ void march_step(const CGArgs& a, const MGeom& g, const MBuf& B,
                                            const MRow& R, int gr,
                                            bool first, double bk, double ak,
                                            double* __restrict__ pnew, const double2* s_dt,
                                            const unsigned* s_rpos, const unsigned* s_rmap,
-                                           double* s_w, MState& W, double (&acc)[2]) {
+                                           double* s_w, MState& W, double (&acc)[2],
+                                           double2* s_ed = nullptr) {
   const int lane = threadIdx.x & 63;
   const int nrows = a.T.nrows;
   const double ng0 = a.St.ng0, nleak = a.St.nleak;
@@ -665,7 +669,7 @@ __device__ __forceinline__ void march_step(const CGArgs& a, const MGeom& g, cons
         pn.y = bk * R.p.y + z1;
       }
       if (g.hok) {
-        const double zh = SM ? R.hr : div_tab(R.hr, s_dt[diag_idx(R.hc)]);  // (SM: the edge z)
+        const double zh = SM || PK ? R.hr : div_tab(R.hr, s_dt[diag_idx(R.hc)]);  // (the edge z)
         hpn = first ? zh : bk * R.hp + zh;
       }
     }
@@ -784,13 +788,20 @@ __device__ __forceinline__ void march_step(const CGArgs& a, const MGeom& g, cons
       rn.y = W.rM.y - ak * q1;
       mr = rn;
       const double z0 = div_tab(rn.x, dM0), z1 = div_tab(rn.y, dM1);
-      if constexpr (SM) {  // {p(k), z} of the edge columns: the next P's halo (lanes 0 and 63)
+      if constexpr (SM || PK) {  // {p(k), z} of the edge columns: the next P's halo (lanes 0 and 63)
         const bool ed = mown && (lane == 0 || lane == 63);
-        // (issued by every lane, the others' offsets out of range: under a
-        // divergent branch with two active lanes B took 0.7 us longer,
-        // profiles/r6_16_ab_edgestore.json)
-        bst2<0>(B.ez, ed ? (unsigned)(g.ezo + mid) * 16u : kOOB,
-                lane == 0 ? make_double2(W.C.e0, z0) : make_double2(W.C.e1, z1));
+        if constexpr (ES) {
+          // staged in the wave's LDS rows (k_cg_march ES): one store per
+          // lane after the walk instead of one store instruction per step
+          if (ed) s_ed[(lane == 63 ? kEdgeRows : 0) + (mid - g.r0)] = lane == 0 ? make_double2(W.C.e0, z0)
+                                                                                : make_double2(W.C.e1, z1);
+        } else {
+          // (issued by every lane, the others' offsets out of range: under a
+          // divergent branch with two active lanes B took 0.7 us longer,
+          // profiles/r6_16_ab_edgestore.json)
+          bst2<0>(B.ez, ed ? (unsigned)(g.ezo + mid) * 16u : kOOB,
+                  lane == 0 ? make_double2(W.C.e0, z0) : make_double2(W.C.e1, z1));
+        }
       }
       t0 = make_double2(z0 * rn.x, z1 * rn.y);  // bknum's terms (bondc.f:785-787)
       t1 = make_double2(rn.x * rn.x, rn.y * rn.y);  // snrm's (:872-875)
@@ -825,14 +836,14 @@ __device__ __forceinline__ void march_step(const CGArgs& a, const MGeom& g, cons
   }
 }
 
-template <int MODE, int D, bool UP, bool SM, int PAUX = 0, bool PK = false, bool LIT = false>
+template <int MODE, int D, bool UP, bool SM, int PAUX = 0, bool PK = false, bool LIT = false, bool ES = false>
 __device__ __forceinline__ void march_walk(const CGArgs& a, const MGeom& g, const MBuf& B,
                                            MRow (&ring)[D],
                                            bool first, double bk, double ak,
                                            const double* __restrict__ psrc,
                                            double* __restrict__ pnew, const double2* s_dt,
                                            const unsigned* s_rpos, const unsigned* s_rmap,
-                                           double* s_w, double (&acc)[2]) {
+                                           double* s_w, double (&acc)[2], double2* s_ed = nullptr) {
   MState W;
   W.U = MWin{0.0, 0.0, 0.0, 0.0};
   W.C = W.U;
@@ -849,8 +860,8 @@ __device__ __forceinline__ void march_walk(const CGArgs& a, const MGeom& g, cons
       // view (loads return 0, stores are dropped) and finish no row
       const MRow R = ring[u];
       march_load<MODE, SM, PAUX, PK>(a, g, B, UP ? g.rend - (j + D) : g.r0 - 1 + j + D, first, psrc, ring[u]);
-      march_step<MODE, UP, SM, LIT, PK>(a, g, B, R, UP ? g.rend - j : g.r0 - 1 + j, first, bk, ak, pnew, s_dt,
-                               s_rpos, s_rmap, s_w, W, acc);
+      march_step<MODE, UP, SM, LIT, PK, ES>(a, g, B, R, UP ? g.rend - j : g.r0 - 1 + j, first, bk, ak, pnew, s_dt,
+                                            s_rpos, s_rmap, s_w, W, acc, s_ed);
     }
   }
 }
@@ -860,13 +871,16 @@ __device__ __forceinline__ void march_walk(const CGArgs& a, const MGeom& g, cons
 // exit, hardware id} wall-clock stamps (100 MHz) into a.mtrace[4 w ..]
 // TAG: the epilogue reductions by tagged granules (publish_and_reduce_tagged)
 // DEF: deferred reductions (with TAG, strip-major, fast order; see def_totals)
+// ES: B's edge pairs staged in LDS and stored after the walk (bands of <=
+// kEdgeRows rows, strip-major; the host picks it, CGArgs::mes)
 template <int MODE, bool SM = false, int D = kMarchDepth, int PAUX = 0, bool TR = false,
-          bool TAG = false, bool PK = false, bool LIT = false, bool DEF = false>
+          bool TAG = false, bool PK = false, bool LIT = false, bool DEF = false, bool ES = false>
 // (the deferred instantiations are held to 3 waves per SIMD -- 168 VGPRs:
 // the strip-major march's slot-weighted bands assume 3 resident workgroups
 // per CU, and their totals code left P at 169 without the bound)
 __global__ __launch_bounds__(64 * kMarchWaves, DEF ? 3 : PERC_MARCH_MINW(SM, MODE, PK)) void k_cg_march(CGArgs a) {
   static_assert(!DEF || (TAG && SM && !LIT), "deferred reductions: the tagged strip-major fast march");
+  static_assert(!ES || (MODE == kMarchB && SM), "staged edge pairs: the strip-major B");
   const unsigned long long tr_t0 = TR ? wall_clock64() : 0ull;
   unsigned long long tr_t1 = 0ull;
   CGScalars* S = a.S;
@@ -1034,8 +1048,27 @@ __global__ __launch_bounds__(64 * kMarchWaves, DEF ? 3 : PERC_MARCH_MINW(SM, MOD
   double acc[2] = {0.0, 0.0};
   if (active) {
     double* s_w = s_win[threadIdx.x >> 6];
-    if (up) march_walk<MODE, D, true, SM, PAUX, PK, LIT>(a, g, B, ring, first, bk, ak, psrc, pnew, s_dt, s_rpos, s_rmap, s_w, acc);
-    else march_walk<MODE, D, false, SM, PAUX, PK, LIT>(a, g, B, ring, first, bk, ak, psrc, pnew, s_dt, s_rpos, s_rmap, s_w, acc);
+    double2* s_ed = nullptr;
+    if constexpr (ES) {
+      __shared__ double2 s_edge[kMarchWaves][2 * kEdgeRows];
+      s_ed = s_edge[threadIdx.x >> 6];
+    }
+    if (up)
+      march_walk<MODE, D, true, SM, PAUX, PK, LIT, ES>(a, g, B, ring, first, bk, ak, psrc, pnew, s_dt, s_rpos,
+                                                       s_rmap, s_w, acc, s_ed);
+    else
+      march_walk<MODE, D, false, SM, PAUX, PK, LIT, ES>(a, g, B, ring, first, bk, ak, psrc, pnew, s_dt, s_rpos,
+                                                        s_rmap, s_w, acc, s_ed);
+    if constexpr (ES) {
+      // the band's staged edge pairs: lane l stores row r0 + l of both sides
+      // (the wave's own LDS writes, in program order: no barrier)
+      __builtin_amdgcn_wave_barrier();
+      asm volatile("" ::: "memory");
+      const int h = g.rend - g.r0, base = 2 * strip * nrows + g.r0;
+#pragma unroll
+      for (int sd = 0; sd < 2; ++sd)
+        bst2<0>(B.ez, lane < h ? (unsigned)(base + sd * nrows + lane) * 16u : kOOB, s_ed[sd * kEdgeRows + lane]);
+    }
     if (MODE == kMarchP && !SM && !first && !a.bx) {
       // row-major q-free solve: x += ak p(k-1) on the band's x rows, after
       // the walk.  Inside it the x load feeding the x store made every step
@@ -1150,7 +1183,8 @@ __global__ __launch_bounds__(kBlock) void k_edge_init(CGArgs a) {
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= 2 * spr * nrows) return;
   const int row = e % nrows, ss = e / nrows, strip = ss / 2, side = ss % 2;
-  const int i = sm_at(a.T, row, strip * kMarchW + (side ? kMarchW - 1 : 0));
+  const int col = strip * kMarchW + (side ? kMarchW - 1 : 0);
+  const int i = a.sm ? sm_at(a.T, row, col) : row * a.T.m + col;  // (r and the u16 codes in the march's layout)
   reinterpret_cast<double2*>(a.ez)[e] = make_double2(0.0, div_tab(a.r[i], a.St.dtab[diag_idx(a.St.code[i])]));
 }
 

@@ -75,7 +75,12 @@ void klaunch(perc_ctx* h, K kern, dim3 g, dim3 b, hipStream_t st, const CGArgs& 
 template <int MODE, bool PK>
 void launch_march_sm2(perc_ctx* h, hipStream_t st, const CGArgs& a) {
   const int grid = a.wslots > 0 ? h->wm_grid : h->march_grid;
-  if (a.mdef) {  // deferred reductions (the default): the next launch forms the totals
+  if (MODE == kMarchB && a.mes && !a.lit && !a.mdef && a.mgran) {  // edge pairs staged in LDS
+    if (a.mtrace) klaunch(h, k_cg_march<MODE, true, 3, kNT, true, true, PK, false, false, MODE == kMarchB>, grid,
+                          64 * kMarchWaves, st, a);
+    else klaunch(h, k_cg_march<MODE, true, 3, kNT, false, true, PK, false, false, MODE == kMarchB>, grid,
+                 64 * kMarchWaves, st, a);
+  } else if (a.mdef) {  // deferred reductions (opt-in): the next launch forms the totals
     if (a.mtrace) klaunch(h, k_cg_march<MODE, true, 3, kNT, true, true, PK, false, true>, grid, 64 * kMarchWaves, st, a);
     else klaunch(h, k_cg_march<MODE, true, 3, kNT, false, true, PK, false, true>, grid, 64 * kMarchWaves, st, a);
   } else if (a.lit) {  // the literal dot order: the LIT instantiation (term stores)
@@ -208,6 +213,14 @@ hipError_t to_nib_rows(perc_ctx* h, CGArgs& a) {
   if (!bad) {
     a.nib = d.nib_sm;
     for (int c = 0; c < 3; ++c) a.ncls[c] = h->ncls[c];
+    // the row-major nibble march's P takes its halo columns from the edge
+    // {p, z} pairs its B stores (as the strip-major march), the first P's
+    // from r0
+    const long long ne = 2ll * (a.T.m / kMarchW) * a.T.nrows;
+    if (!d.ez) HIP_TRY(dmalloc(&d.ez, 2 * (size_t)ne + 8));
+    a.ez = d.ez;
+    k_edge_init<<<blocks_for(ne), kBlock, 0, st>>>(a);
+    HIP_TRY(dbg_sync(st, "k_edge_init"));
   }
   h->nib_used = !bad;
   return hipSuccess;
@@ -558,14 +571,15 @@ hipError_t to_strips(perc_ctx* h, CGArgs& a) {
   a.r = d.q;
   a.q = d.r;
   a.St.code = d.code_sm;
-  // edge {p, z} (the march P's halo columns), the first P's from r0
+  a.sm = 1;
+  a.bx = 1;  // x (row-major) is updated in the q-free march B
+  // edge {p, z} (the march P's halo columns), the first P's from r0 (the
+  // strip-major r and codes: a.sm set)
   const long long ne = 2ll * (a.T.m / kMarchW) * a.T.nrows;
   if (!d.ez) HIP_TRY(dmalloc(&d.ez, 2 * (size_t)ne + 8));  // {p, z} pairs
   a.ez = d.ez;
   k_edge_init<<<blocks_for(ne), kBlock, 0, st>>>(a);
   HIP_TRY(dbg_sync(st, "k_edge_init"));
-  a.sm = 1;
-  a.bx = 1;  // x (row-major) is updated in the q-free march B
   // nibble codes (PERC_MARCH_NIBBLE, square lattice): 0.5 instead of 2
   // bytes of row code per element in both march kernels
   h->nib_used = false;
@@ -590,6 +604,25 @@ hipError_t to_strips(perc_ctx* h, CGArgs& a) {
       a.wcum[0][i] = h->wm_cum[0][i];
       a.wcum[1][i] = h->wm_cum[1][i];
     }
+  }
+  // B stages its edge pairs in LDS where every band of B holds <= kEdgeRows
+  // rows (the bands as k_cg_march forms them; PERC_MARCH_EDGE_STEP=1: the
+  // per-step stores, same-box A/Bs)
+  {
+    const int nrows = a.T.nrows, spr = a.T.m / kMarchW;
+    int hmax = 0;
+    if (a.wslots > 0) {
+      const int ns = a.wslots, ncu = h->wm_grid / ns, Q = ncu * kMarchWaves / spr;
+      const int* wc = a.wcum[1];
+      for (int q = 0; q < Q; ++q) {
+        const int c0 = (int)((long long)q * nrows / Q), hc = (int)((long long)(q + 1) * nrows / Q) - c0;
+        for (int sl = 0; sl < ns; ++sl) hmax = std::max(hmax, hc * wc[sl + 1] / wc[ns] - hc * wc[sl] / wc[ns]);
+      }
+    } else {
+      hmax = a.T.bh;
+    }
+    const char* es = std::getenv("PERC_MARCH_EDGE_STEP");
+    a.mes = hmax <= kEdgeRows && !(es && es[0] == '1') ? 1 : 0;
   }
   return hipSuccess;
 }
