@@ -639,7 +639,7 @@ struct MState {
 
 // one step: row gr enters the window, then the middle row (gr -+ 1) is
 // finished when it is one of the band's own rows
-template <int MODE, bool UP, bool SM, bool LIT = false, bool PK = false, bool ES = false>
+template <int MODE, bool UP, bool SM, bool LIT = false, bool PK = false, int ESR = 0>
 __device__ __forceinline__ void march_step(const CGArgs& a, const MGeom& g, const MBuf& B,
                                            const MRow& R, int gr,
                                            bool first, double bk, double ak,
@@ -790,11 +790,11 @@ __device__ __forceinline__ void march_step(const CGArgs& a, const MGeom& g, cons
       const double z0 = div_tab(rn.x, dM0), z1 = div_tab(rn.y, dM1);
       if constexpr (SM || PK) {  // {p(k), z} of the edge columns: the next P's halo (lanes 0 and 63)
         const bool ed = mown && (lane == 0 || lane == 63);
-        if constexpr (ES) {
-          // staged in the wave's LDS rows (k_cg_march ES): one store per
+        if constexpr (ESR > 0) {
+          // staged in the wave's LDS rows (k_cg_march ESR): one store per
           // lane after the walk instead of one store instruction per step
-          if (ed) s_ed[(lane == 63 ? kEdgeRows : 0) + (mid - g.r0)] = lane == 0 ? make_double2(W.C.e0, z0)
-                                                                                : make_double2(W.C.e1, z1);
+          if (ed) s_ed[(lane == 63 ? ESR : 0) + (mid - g.r0)] = lane == 0 ? make_double2(W.C.e0, z0)
+                                                                          : make_double2(W.C.e1, z1);
         } else {
           // (issued by every lane, the others' offsets out of range: under a
           // divergent branch with two active lanes B took 0.7 us longer,
@@ -836,7 +836,7 @@ __device__ __forceinline__ void march_step(const CGArgs& a, const MGeom& g, cons
   }
 }
 
-template <int MODE, int D, bool UP, bool SM, int PAUX = 0, bool PK = false, bool LIT = false, bool ES = false>
+template <int MODE, int D, bool UP, bool SM, int PAUX = 0, bool PK = false, bool LIT = false, int ESR = 0>
 __device__ __forceinline__ void march_walk(const CGArgs& a, const MGeom& g, const MBuf& B,
                                            MRow (&ring)[D],
                                            bool first, double bk, double ak,
@@ -860,7 +860,7 @@ __device__ __forceinline__ void march_walk(const CGArgs& a, const MGeom& g, cons
       // view (loads return 0, stores are dropped) and finish no row
       const MRow R = ring[u];
       march_load<MODE, SM, PAUX, PK>(a, g, B, UP ? g.rend - (j + D) : g.r0 - 1 + j + D, first, psrc, ring[u]);
-      march_step<MODE, UP, SM, LIT, PK, ES>(a, g, B, R, UP ? g.rend - j : g.r0 - 1 + j, first, bk, ak, pnew, s_dt,
+      march_step<MODE, UP, SM, LIT, PK, ESR>(a, g, B, R, UP ? g.rend - j : g.r0 - 1 + j, first, bk, ak, pnew, s_dt,
                                             s_rpos, s_rmap, s_w, W, acc, s_ed);
     }
   }
@@ -871,16 +871,17 @@ __device__ __forceinline__ void march_walk(const CGArgs& a, const MGeom& g, cons
 // exit, hardware id} wall-clock stamps (100 MHz) into a.mtrace[4 w ..]
 // TAG: the epilogue reductions by tagged granules (publish_and_reduce_tagged)
 // DEF: deferred reductions (with TAG, strip-major, fast order; see def_totals)
-// ES: B's edge pairs staged in LDS and stored after the walk (bands of <=
-// kEdgeRows rows, strip-major; the host picks it, CGArgs::mes)
+// ESR > 0: B's edge pairs staged in LDS (ESR rows per side) and stored
+// after the walk -- bands of <= ESR rows: kEdgeRows strip-major, 16 on the
+// row-major march's 8-row bands (the host picks it, CGArgs::mes)
 template <int MODE, bool SM = false, int D = kMarchDepth, int PAUX = 0, bool TR = false,
-          bool TAG = false, bool PK = false, bool LIT = false, bool DEF = false, bool ES = false>
+          bool TAG = false, bool PK = false, bool LIT = false, bool DEF = false, int ESR = 0>
 // (the deferred instantiations are held to 3 waves per SIMD -- 168 VGPRs:
 // the strip-major march's slot-weighted bands assume 3 resident workgroups
 // per CU, and their totals code left P at 169 without the bound)
 __global__ __launch_bounds__(64 * kMarchWaves, DEF ? 3 : PERC_MARCH_MINW(SM, MODE, PK)) void k_cg_march(CGArgs a) {
   static_assert(!DEF || (TAG && SM && !LIT), "deferred reductions: the tagged strip-major fast march");
-  static_assert(!ES || (MODE == kMarchB && SM), "staged edge pairs: the strip-major B");
+  static_assert(ESR == 0 || (MODE == kMarchB && (SM || PK)), "staged edge pairs: the march B with edge pairs");
   const unsigned long long tr_t0 = TR ? wall_clock64() : 0ull;
   unsigned long long tr_t1 = 0ull;
   CGScalars* S = a.S;
@@ -1049,25 +1050,28 @@ __global__ __launch_bounds__(64 * kMarchWaves, DEF ? 3 : PERC_MARCH_MINW(SM, MOD
   if (active) {
     double* s_w = s_win[threadIdx.x >> 6];
     double2* s_ed = nullptr;
-    if constexpr (ES) {
-      __shared__ double2 s_edge[kMarchWaves][2 * kEdgeRows];
+    if constexpr (ESR > 0) {
+      __shared__ double2 s_edge[kMarchWaves][2 * (ESR > 0 ? ESR : 1)];
       s_ed = s_edge[threadIdx.x >> 6];
     }
     if (up)
-      march_walk<MODE, D, true, SM, PAUX, PK, LIT, ES>(a, g, B, ring, first, bk, ak, psrc, pnew, s_dt, s_rpos,
+      march_walk<MODE, D, true, SM, PAUX, PK, LIT, ESR>(a, g, B, ring, first, bk, ak, psrc, pnew, s_dt, s_rpos,
                                                        s_rmap, s_w, acc, s_ed);
     else
-      march_walk<MODE, D, false, SM, PAUX, PK, LIT, ES>(a, g, B, ring, first, bk, ak, psrc, pnew, s_dt, s_rpos,
+      march_walk<MODE, D, false, SM, PAUX, PK, LIT, ESR>(a, g, B, ring, first, bk, ak, psrc, pnew, s_dt, s_rpos,
                                                         s_rmap, s_w, acc, s_ed);
-    if constexpr (ES) {
-      // the band's staged edge pairs: lane l stores row r0 + l of both sides
-      // (the wave's own LDS writes, in program order: no barrier)
+    if constexpr (ESR > 0) {
+      // the band's staged edge pairs: lane l stores row r0 + l of side
+      // l / ESR (the wave's own LDS writes, in program order: no barrier)
       __builtin_amdgcn_wave_barrier();
       asm volatile("" ::: "memory");
       const int h = g.rend - g.r0, base = 2 * strip * nrows + g.r0;
 #pragma unroll
-      for (int sd = 0; sd < 2; ++sd)
-        bst2<0>(B.ez, lane < h ? (unsigned)(base + sd * nrows + lane) * 16u : kOOB, s_ed[sd * kEdgeRows + lane]);
+      for (int sd = 0; sd < (2 * ESR + 63) / 64; ++sd) {
+        const int e = sd * 64 + lane, side = e / ESR, row = e % ESR;
+        bst2<0>(B.ez, e < 2 * ESR && row < h ? (unsigned)(base + side * nrows + row) * 16u : kOOB,
+                s_ed[e < 2 * ESR ? e : 0]);
+      }
     }
     if (MODE == kMarchP && !SM && !first && !a.bx) {
       // row-major q-free solve: x += ak p(k-1) on the band's x rows, after

@@ -76,9 +76,10 @@ template <int MODE, bool PK>
 void launch_march_sm2(perc_ctx* h, hipStream_t st, const CGArgs& a) {
   const int grid = a.wslots > 0 ? h->wm_grid : h->march_grid;
   if (MODE == kMarchB && a.mes && !a.lit && !a.mdef && a.mgran) {  // edge pairs staged in LDS
-    if (a.mtrace) klaunch(h, k_cg_march<MODE, true, 3, kNT, true, true, PK, false, false, MODE == kMarchB>, grid,
+    constexpr int kESR = MODE == kMarchB ? kEdgeRows : 0;
+    if (a.mtrace) klaunch(h, k_cg_march<MODE, true, 3, kNT, true, true, PK, false, false, kESR>, grid,
                           64 * kMarchWaves, st, a);
-    else klaunch(h, k_cg_march<MODE, true, 3, kNT, false, true, PK, false, false, MODE == kMarchB>, grid,
+    else klaunch(h, k_cg_march<MODE, true, 3, kNT, false, true, PK, false, false, kESR>, grid,
                  64 * kMarchWaves, st, a);
   } else if (a.mdef) {  // deferred reductions (opt-in): the next launch forms the totals
     if (a.mtrace) klaunch(h, k_cg_march<MODE, true, 3, kNT, true, true, PK, false, true>, grid, 64 * kMarchWaves, st, a);
@@ -167,6 +168,9 @@ void launch_cg_b(perc_ctx* h, const CGArgs& a, int G) {
     else if (a.lit)
       klaunch(h, k_cg_march<kMarchB, false, kMarchDepth, kNT, false, false, false, true>, h->march_grid,
               64 * kMarchWaves, h->stream, a);
+    else if (a.nib && a.mes)  // (edge pairs staged in LDS: 16 rows per side)
+      klaunch(h, k_cg_march<kMarchB, false, kMarchDepth, kNT, false, false, true, false, false, 16>, h->march_grid,
+              64 * kMarchWaves, h->stream, a);
     else if (a.nib)
       klaunch(h, k_cg_march<kMarchB, false, kMarchDepth, kNT, false, false, true>, h->march_grid, 64 * kMarchWaves,
               h->stream, a);
@@ -221,6 +225,8 @@ hipError_t to_nib_rows(perc_ctx* h, CGArgs& a) {
     a.ez = d.ez;
     k_edge_init<<<blocks_for(ne), kBlock, 0, st>>>(a);
     HIP_TRY(dbg_sync(st, "k_edge_init"));
+    const char* es = std::getenv("PERC_MARCH_EDGE_STEP");
+    a.mes = a.T.bh <= 16 && !(es && es[0] == '1') ? 1 : 0;  // (B's bands: march_h rows)
   }
   h->nib_used = !bad;
   return hipSuccess;
