@@ -353,6 +353,11 @@ __global__ __launch_bounds__(64) void k_cc_tile_w(Geom g, const uint8_t* bocc, c
   const int c0 = tx * kCcW, r0 = ty * H;
   const int tw = min(kCcW, g.m - c0), th = min(H, g.n - r0);
   const int lane = threadIdx.x;
+  // NBO (site / mixed kinds with BAL): a row's loads are the sites' own
+  // occupancies (and bonds); the occupancy of the site a link leads to is
+  // the right neighbour's (a ballot) or the next row's own load, applied
+  // where the link is used -- 2 / 6 byte loads per lane and row, not 6 / 10
+  constexpr bool NBO = BAL && KIND != PERC_BOND;
   const __amdgpu_buffer_rsrc_t rb = rsrc(bocc, nb_bytes), rs = rsrc(socc, (unsigned)g.t + 8u);
   auto ld8 = [](__amdgpu_buffer_rsrc_t r, bool ok, unsigned off) {
     return (unsigned)__builtin_amdgcn_raw_buffer_load_b8(r, (int)(ok ? off : kOOB), 0, 0);
@@ -367,8 +372,13 @@ __global__ __launch_bounds__(64) void k_cc_tile_w(Geom g, const uint8_t* bocc, c
       const bool hr = v && col < g.m - 1, hu = v && row < g.n - 1;
       if constexpr (KIND == PERC_SITE) {
         O[h] = ld8(rs, v, (unsigned)s);
-        R[h] = ld8(rs, hr, (unsigned)s + 1u);
-        U[h] = ld8(rs, hu, (unsigned)(s + g.m));
+        if constexpr (NBO) {
+          R[h] = hr ? 1u : 0u;
+          U[h] = hu ? 1u : 0u;
+        } else {
+          R[h] = ld8(rs, hr, (unsigned)s + 1u);
+          U[h] = ld8(rs, hu, (unsigned)(s + g.m));
+        }
       } else {
         const int fb = bf_open_square(g, row, col);
         R[h] = ld8(rb, hr, (unsigned)fb);
@@ -376,8 +386,10 @@ __global__ __launch_bounds__(64) void k_cc_tile_w(Geom g, const uint8_t* bocc, c
         O[h] = 1u;
         if constexpr (KIND != PERC_BOND) {
           O[h] = ld8(rs, v, (unsigned)s);
-          R[h] &= ld8(rs, hr, (unsigned)s + 1u);
-          U[h] &= ld8(rs, hu, (unsigned)(s + g.m));
+          if constexpr (!NBO) {
+            R[h] &= ld8(rs, hr, (unsigned)s + 1u);
+            U[h] &= ld8(rs, hu, (unsigned)(s + g.m));
+          }
         }
       }
     }
@@ -435,6 +447,10 @@ __global__ __launch_bounds__(64) void k_cc_tile_w(Geom g, const uint8_t* bocc, c
       const unsigned long long rb0 = __ballot(R[0] != 0u), rb1 = __ballot(R[1] != 0u);
       lm0 = rb0 << 1;
       lm1 = rb1 << 1 | rb0 >> 63;
+      if constexpr (NBO) {  // the linked-to site occupied too
+        lm0 &= __ballot(O[0] != 0u);
+        lm1 &= __ballot(O[1] != 0u);
+      }
       left0 = (lm0 >> lane) & 1ull;
       left1 = (lm1 >> lane) & 1ull;
       lo = ~(lm0 & vm0);
@@ -453,7 +469,7 @@ __global__ __launch_bounds__(64) void k_cc_tile_w(Geom g, const uint8_t* bocc, c
     if (v0 && !left0) uf.set(node[0], node[0]);
     if (v1 && !left1) uf.set(node[1], node[1]);
     wave_lds_order();
-    const bool w0 = r > 0 && v0 && Up[0], w1 = r > 0 && v1 && Up[1];
+    const bool w0 = r > 0 && v0 && Up[0] && (!NBO || O[0]), w1 = r > 0 && v1 && Up[1] && (!NBO || O[1]);
     const int a0 = w0 ? node[0] : -1, b0 = w0 ? labp[0] : -1, a1 = w1 ? node[1] : -1, b1 = w1 ? labp[1] : -1;
     if constexpr (BAL) {
       const unsigned long long wb0 = __ballot(w0), wb1 = __ballot(w1);
