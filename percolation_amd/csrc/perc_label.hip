@@ -29,6 +29,18 @@ __global__ void k_occupy(const int* order, int count, long long limit, uint8_t* 
 // keys -- slow, exact: T is the exact order statistic on every path.
 constexpr int kSelCap = 1 << 17, kSelThreads = 1024, kSelStage = 512, kSelBins = 4096;
 constexpr int kSelBinCap = 1024;
+// occupancy bytes per thread and trip of k_select_window (one store of a
+// kSelV-byte word; PERC_SEL_V: A/B probe builds only)
+#ifdef PERC_SEL_V
+constexpr int kSelV = PERC_SEL_V;
+#else
+constexpr int kSelV = 4;
+#endif
+template <int V> struct SelWord;
+template <> struct SelWord<1> { using T = uint8_t; };
+template <> struct SelWord<2> { using T = unsigned short; };
+template <> struct SelWord<4> { using T = unsigned; };
+template <> struct SelWord<8> { using T = unsigned long long; };
 constexpr int kSelCnt = 4 + kSelBins;  // unsigned words per draw (cnt)
 // bins of the window's hash range: (hash - lo) >> sh < kSelBins
 __host__ __device__ inline int sel_shift(unsigned long long lo, unsigned long long hi) {
@@ -84,24 +96,37 @@ __global__ __launch_bounds__(kBlock) void k_select_window(SelDraws D) {
   __syncthreads();
   unsigned below = 0;
   const int lane = threadIdx.x & 63;
-  for (long long i = (long long)bid * kBlock + threadIdx.x; i < n; i += (long long)w.gn * kBlock) {
-    const unsigned id = (unsigned)(i + 1);
-    const unsigned long long hsh = perc_rand_hash32(kc, id);  // = perc_rand_key(seed, id) >> 32
-    const unsigned long long key = hsh << 32 | id;
-    below += hsh < lo;
-    // every key below the window is occupied, every key above it is not;
-    // the window's keys (0 here) are decided by k_occupy_cand once T is known
-    occ[i + base] = hsh < lo ? 1 : 0;
-    if (hsh >= lo && hsh < hi) {
-      atomicAdd(&cnt[4 + (int)((hsh - lo) >> sh)], 1u);
-      const unsigned slot = atomicAdd(&s_n, 1u);
-      if (slot < (unsigned)kSelStage) {
-        s_c[slot] = key;
-      } else {  // a crowded workgroup: straight to the global list
-        const unsigned idx = atomicAdd(&cnt[1], 1u);
-        if (idx < (unsigned)kSelCap) cand[1 + idx] = key;
+  // a thread's kSelV bytes of one aligned word of occ per trip (one store
+  // instead of kSelV byte stores): byte o is id o - base + 1, the bytes
+  // outside ids 1..n are pads (written 0 here and by the pad stores above)
+  const long long nw = cdiv(n + base, (long long)kSelV);
+  for (long long j = (long long)bid * kBlock + threadIdx.x; j < nw; j += (long long)w.gn * kBlock) {
+    using Word = typename SelWord<kSelV>::T;
+    Word word = 0;
+#pragma unroll
+    for (int k = 0; k < kSelV; ++k) {
+      const long long i = j * kSelV + k - base;
+      const bool v = i >= 0 && i < n;
+      const unsigned id = (unsigned)(i + 1);
+      const unsigned long long hsh = perc_rand_hash32(kc, id);  // = perc_rand_key(seed, id) >> 32
+      const unsigned long long key = hsh << 32 | id;
+      // every key below the window is occupied, every key above it is not;
+      // the window's keys (0 here) are decided by k_occupy_cand once T is known
+      const bool b = v && hsh < lo;
+      below += b;
+      word |= (Word)(b ? 1u : 0u) << (8 * k);
+      if (v && hsh >= lo && hsh < hi) {
+        atomicAdd(&cnt[4 + (int)((hsh - lo) >> sh)], 1u);
+        const unsigned slot = atomicAdd(&s_n, 1u);
+        if (slot < (unsigned)kSelStage) {
+          s_c[slot] = key;
+        } else {  // a crowded workgroup: straight to the global list
+          const unsigned idx = atomicAdd(&cnt[1], 1u);
+          if (idx < (unsigned)kSelCap) cand[1 + idx] = key;
+        }
       }
     }
+    reinterpret_cast<Word*>(occ)[j] = word;
   }
   below = (unsigned)wave_sum_int((int)below);
   if (lane == 0) s_b[threadIdx.x >> 6] = below;

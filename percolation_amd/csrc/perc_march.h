@@ -106,6 +106,93 @@ __device__ __forceinline__ void gran_poll_n(__amdgpu_buffer_rsrc_t rg, const int
   }
 }
 
+constexpr int kDefGroups = 12;  // groups of kGroup workgroups a deferred total takes (grid <= 768)
+
+// One-hop collector (grids of <= kDefGroups groups, the default; the
+// two-level collectors below with PERC_MARCH_GROUPCOL, A/B probe builds
+// only): the last logical workgroup polls every workgroup granule itself --
+// wave w the granules of groups w, w + 4, w + 8, each lane re-polling only
+// the granules it has not yet seen -- and forms the totals by the two-level
+// association: a group's granules summed by one wave_sum over its lanes in
+// order (the group collector's sum), the group sums thread-strided and
+// block-summed (the last collector's).  Every total is the two-level one
+// bitwise; the hop through the group granules (a write-through store and
+// the last collector's poll of it) leaves the tail.
+template <int NV>
+__device__ __forceinline__ void flat_collect(__amdgpu_buffer_rsrc_t rg, int nwg, int ngroups, double tag, int* err,
+                                             double (&tot)[NV], double* s_red) {
+  __shared__ double s_grp[NV * kDefGroups];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  constexpr int kPer = kDefGroups / 4;  // groups per wave (4 waves per workgroup)
+  double val[kPer][NV];
+  bool need[kPer][NV];
+#pragma unroll
+  for (int i = 0; i < kPer; ++i) {
+    const int g = wid + 4 * i, gn = g < ngroups ? min(kGroup, nwg - g * kGroup) : 0;
+#pragma unroll
+    for (int j = 0; j < NV; ++j) {
+      val[i][j] = 0.0;
+      need[i][j] = lane < gn;
+    }
+  }
+  for (unsigned spin = 0;; ++spin) {
+    double2 g2[kPer][NV];
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) {  // every load issued before any tag is checked
+      const int g0 = (wid + 4 * i) * kGroup;
+#pragma unroll
+      for (int j = 0; j < NV; ++j)
+        g2[i][j] = __builtin_bit_cast(
+            double2, __builtin_amdgcn_raw_buffer_load_b128(
+                         rg, need[i][j] ? (j * nwg + g0 + lane) * 16 : (int)kOOB, 0, 16));
+    }
+    bool more = false;
+#pragma unroll
+    for (int i = 0; i < kPer; ++i)
+#pragma unroll
+      for (int j = 0; j < NV; ++j)
+        if (need[i][j]) {
+          if (g2[i][j].y == tag) {
+            val[i][j] = g2[i][j].x;
+            need[i][j] = false;
+          } else {
+            more = true;
+          }
+        }
+    if (!__any(more)) break;
+    if (spin > (1u << 22)) {  // (uniform)
+      if (more) *err = 1;
+      break;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+#pragma unroll
+  for (int i = 0; i < kPer; ++i) {
+    const int g = wid + 4 * i;
+    if (g < ngroups) {  // (wave-uniform)
+#pragma unroll
+      for (int j = 0; j < NV; ++j) {
+        const double w = wave_sum(val[i][j]);  // the group collector's sum
+        if (lane == 0) s_grp[j * kDefGroups + g] = w;
+      }
+    }
+  }
+  __syncthreads();
+  double acc[NV];
+#pragma unroll
+  for (int j = 0; j < NV; ++j) {  // the last collector's thread-strided group sums
+    acc[j] = 0.0;
+    if ((int)threadIdx.x < ngroups) acc[j] = acc[j] + s_grp[j * kDefGroups + threadIdx.x];
+  }
+  block_sum<NV>(acc, s_red);
+  if (threadIdx.x == 0)
+#pragma unroll
+    for (int j = 0; j < NV; ++j) s_red[16 + j] = acc[j];
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < NV; ++j) tot[j] = s_red[16 + j];
+}
+
 // Fixed collectors instead of tickets (the default; PERC_MARCH_TICKETS, A/B
 // probe builds only: the ticket form below): a group's LAST logical
 // workgroup (lb = g0 + gn - 1, dispatched late: logical blocks of an XCD are
@@ -133,6 +220,13 @@ __device__ bool publish_and_reduce_tagged(double (&v)[NV], double* gran, unsigne
       __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, make_double2(v[j], tag)), rg,
                                              (j * nwg + lb) * 16, 0, 16);
   }
+#if !defined(PERC_MARCH_GROUPCOL)
+  if (ngroups <= kDefGroups) {  // (uniform) the one-hop collector
+    if (lb != nwg - 1) return false;
+    flat_collect<NV>(rg, nwg, ngroups, tag, err, tot, s_red);
+    return true;
+  }
+#endif
   if (lb != g0 + gn - 1) return false;  // (uniform) not a collector
   if (threadIdx.x < 64) {  // the group's collector: wave 0 sums the group's partials
     const int lane = threadIdx.x;
@@ -268,7 +362,6 @@ __device__ bool publish_and_reduce_tagged(double (&v)[NV], double* gran, unsigne
 // r.r (bk, err, stop); kDefBench -- perc_bench_kernel's fixed iteration (no
 // stop, no scalars but bkn)
 constexpr int kDefP = 1, kDefB = 2, kDefBench = 4;
-constexpr int kDefGroups = 12;  // groups of kGroup workgroups a deferred total takes (grid <= 768)
 template <int NV>
 __device__ __forceinline__ void def_totals(const double* gran, int nwg, double tag, int* err,
                                            double (&tot)[NV], double* s_red, double* s_grp, bool sc1) {
