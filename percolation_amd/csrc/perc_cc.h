@@ -43,6 +43,17 @@ __device__ __forceinline__ int wave_sum_int(int v) {
 constexpr int kCcW = 128, kCcH = PERC_CC_H, kCcSites = kCcW * kCcH, kCcThreads = 256;
 constexpr int kReduceGrid = 1024;  // fixed grid of the counting passes
 constexpr int kCcWaveH = 16;       // block height of k_cc_tile_w (the open square lattice)
+// rows whose loads the bond kind's k_cc_tile_w keeps in flight: 3 -- tile
+// 92.6 vs 114.8 (D = 2) and 116 us (D = 4) at L = 4096, 292.7 vs 322.6 /
+// 328.5 at 8192 (profiles/r6_31_cc_depth.txt); labels per realisation at
+// L = 4096 0.2467 vs 0.2664 ms (r6_32).  The site and mixed kinds keep D = 2
+// (D = 3 within 1 %: config 5's labels 0.332 vs 0.329 ms).  PERC_CC_TILE_D:
+// A/B probe builds only
+#ifdef PERC_CC_TILE_D
+constexpr int kCcWaveDBond = PERC_CC_TILE_D;
+#else
+constexpr int kCcWaveDBond = 3;
+#endif
 
 
 __device__ __forceinline__ int find_root(int* parent, int x) {

@@ -626,7 +626,7 @@ hipError_t dev_label(perc_ctx* h, int* nspan, int* span_list, int* nclusters) {
     if (!d.ccpart) HIP_TRY(dmalloc(&d.ccpart, (size_t)G + GM));
     int* part = d.ccpart;
     if (kind == PERC_BOND)
-      k_cc_tile_w<H, PERC_BOND><<<G, 64, 0, st>>>(g, d.bocc, d.socc, d.parent, d.member, nbb, part);
+      k_cc_tile_w<H, PERC_BOND, kCcWaveDBond><<<G, 64, 0, st>>>(g, d.bocc, d.socc, d.parent, d.member, nbb, part);
     // (site and mixed kinds: the ballot-mask walk, 95.6 vs 103.8 us mixed at
     // L = 4096, 273.7 vs 298.5 at 8192; the bond kind's is 2 % slower with
     // it, profiles/r5_10_cc_bench_L*.txt)

@@ -304,5 +304,42 @@ int main(int argc, char** argv) {
       by_h(std::integral_constant<int, 32>{}, kind == PERC_SITE ? "site: 32-row tiles" : "mixed: 32-row tiles");
     }
   }
+  // rows in flight (the ring depth D) of the 16-row wave tiles, each kind:
+  // element by element against D = 2 and timed alone (socc as above: sites
+  // 0.8; the bond kind ignores it)
+  {
+    const int G16 = cdiv(g.m, kCcW) * cdiv(g.n, 16);
+    auto tk = [&](auto kc, auto dc) {
+      constexpr int K = decltype(kc)::value, D = decltype(dc)::value;
+      return [&, G16]() {
+        k_cc_tile_w<16, K, D, K != PERC_BOND><<<G16, 64>>>(g, R.bocc, R.socc, R.parent, R.member, (unsigned)nb + 8u);
+      };
+    };
+    auto depth = [&](auto kc, const char* what) {
+      using D2 = std::integral_constant<int, 2>;
+      using D3 = std::integral_constant<int, 3>;
+      using D4 = std::integral_constant<int, 4>;
+      tk(kc, D2{})();
+      CK(hipDeviceSynchronize());
+      CK(hipMemcpy(R.parent_ref, R.parent, ((size_t)g.t + 2) * 4, hipMemcpyDeviceToDevice));
+      CK(hipMemcpy(R.member_ref, R.member, (size_t)g.t + 2, hipMemcpyDeviceToDevice));
+      double t[3];
+      t[0] = time_ms(tk(kc, D2{}), reps);
+      bool ok = true;
+      CK(hipMemset(R.parent, 0, ((size_t)g.t + 2) * 4));
+      t[1] = time_ms(tk(kc, D3{}), reps);
+      ok = same(R, "D 3") && ok;
+      CK(hipMemset(R.parent, 0, ((size_t)g.t + 2) * 4));
+      t[2] = time_ms(tk(kc, D4{}), reps);
+      ok = same(R, "D 4") && ok;
+      // (again, interleaved: D 2, 4)
+      const double t2b = time_ms(tk(kc, D2{}), reps), t4b = time_ms(tk(kc, D4{}), reps);
+      std::printf("  tile depth, %s kind: D 2 %.1f / %.1f us, D 3 %.1f us, D 4 %.1f / %.1f us%s\n", what,
+                  t[0] * 1e3, t2b * 1e3, t[1] * 1e3, t[2] * 1e3, t4b * 1e3, ok ? "" : " (MISMATCH)");
+    };
+    depth(std::integral_constant<int, PERC_BOND>{}, "bond");
+    depth(std::integral_constant<int, PERC_SITE>{}, "site");
+    depth(std::integral_constant<int, PERC_SITEBOND>{}, "mixed");
+  }
   return 0;
 }
