@@ -606,10 +606,14 @@ hipError_t dev_label(perc_ctx* h, int* nspan, int* span_list, int* nclusters) {
   hipStream_t st = h->stream;
   DeviceBuffers& d = h->d;
   const int kind = h->last.kind;
-  // (the site and mixed kinds on the open square lattice: k_span_top writes
-  // every counter the labeling reads, no memset)
+  // (the open square lattice, every kind -- the tiles' partials count the
+  // clusters: k_span_top writes every counter the labeling reads, no memset)
   const bool wave = g.lattice == kSquare && !g.pbc && h->bf_open_sq && !std::getenv("PERC_TILE_TRACE");
+#if defined(PERC_LABEL_COPYBACK)  // (A/B probe builds only: round 6's memset for the bond kind)
   if (!wave || kind == PERC_BOND) HIP_TRY(hipMemsetAsync(d.counters, 0, sizeof(int) * (8 + kMaxSpanList), st));
+#else
+  if (!wave) HIP_TRY(hipMemsetAsync(d.counters, 0, sizeof(int) * (8 + kMaxSpanList), st));
+#endif
   // the open square lattice: one wave per 128 x 16 block walking its rows
   // (k_cc_tile_w; tile 91.7 vs 190.6 us for the 128 x 32 LDS union-find
   // blocks at L = 4096, profiles/r4_13_cc_bench_L4096.txt); else the LDS
@@ -696,18 +700,34 @@ static hipError_t label_finish(perc_ctx* h, int* nspan, int* span_list, int* ncl
         g.t, d.parent, d.member, d.counters + 1);
     HIP_TRY(dbg_sync(st, "k_cc_count_roots"));
   }
-  if (g.m < kSpanLds) k_span_top<true><<<1, 1024, 0, st>>>(g, d.parent, d.member, d.top, d.counters, part, npart);
-  else k_span_top<false><<<1, 1024, 0, st>>>(g, d.parent, d.member, d.top, d.counters, part, npart);
-  HIP_TRY(dbg_sync(st, "k_span_top"));
   constexpr int kHc = 8 + kMaxSpanList;
 #if defined(PERC_LABEL_PAGEABLE)  // (A/B probe builds only: a stack array)
   int hcs[kHc];
   const int* hc = hcs;
+  int* out = d.counters;
+  const bool direct = false;
+#else
+  if (!h->pin) HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&h->pin), sizeof(int) * kHc, hipHostMallocCoherent));
+  const int* hc = h->pin;
+  // with the cluster count from the partials (npart > 0) k_span_top writes
+  // every word the host reads: straight into the pinned words (coherent
+  // host memory, visible once the stream is synchronised) -- no copy after
+  // it.  (k_cc_count_roots' count is in device memory: copied back.)
+#if defined(PERC_LABEL_COPYBACK)  // (A/B probe builds only)
+  const bool direct = false;
+#else
+  const bool direct = npart > 0;
+#endif
+  int* out = d.counters;
+  if (direct) HIP_TRY(hipHostGetDevicePointer(reinterpret_cast<void**>(&out), h->pin, 0));
+#endif
+  if (g.m < kSpanLds) k_span_top<true><<<1, 1024, 0, st>>>(g, d.parent, d.member, d.top, out, part, npart);
+  else k_span_top<false><<<1, 1024, 0, st>>>(g, d.parent, d.member, d.top, out, part, npart);
+  HIP_TRY(dbg_sync(st, "k_span_top"));
+#if defined(PERC_LABEL_PAGEABLE)
   HIP_TRY(hipMemcpyAsync(hcs, d.counters, sizeof(hcs), hipMemcpyDeviceToHost, st));
 #else
-  if (!h->pin) HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&h->pin), sizeof(int) * kHc));
-  const int* hc = h->pin;
-  HIP_TRY(hipMemcpyAsync(h->pin, d.counters, sizeof(int) * kHc, hipMemcpyDeviceToHost, st));
+  if (!direct) HIP_TRY(hipMemcpyAsync(h->pin, d.counters, sizeof(int) * kHc, hipMemcpyDeviceToHost, st));
 #endif
   HIP_TRY(hipStreamSynchronize(st));
   *nspan = hc[0];
