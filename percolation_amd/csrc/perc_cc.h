@@ -49,6 +49,15 @@ constexpr int kCcWaveH = 16;       // block height of k_cc_tile_w (the open squa
 // L = 4096 0.2467 vs 0.2664 ms (r6_32).  The site and mixed kinds keep D = 2
 // (D = 3 within 1 %: config 5's labels 0.332 vs 0.329 ms).  PERC_CC_TILE_D:
 // A/B probe builds only
+// sites per thread of the square lattice's merge (k_cc_merge_squ; 0: one
+// per thread, k_cc_merge_sq -- PERC_MERGE_U, A/B probe builds only): 2 --
+// config 5's labels 0.3188 vs 0.3287 ms (one per thread), L = 4096 bond
+// 0.2395 vs 0.2412; 4: 0.332 / 0.271 (profiles/r6_35_*)
+#ifdef PERC_MERGE_U
+constexpr int kMergeU = PERC_MERGE_U;
+#else
+constexpr int kMergeU = 2;
+#endif
 #ifdef PERC_CC_TILE_D
 constexpr int kCcWaveDBond = PERC_CC_TILE_D;
 #else
@@ -722,6 +731,152 @@ __global__ __launch_bounds__(kCcThreads) void k_cc_merge_sq(Geom g, const uint8_
       if (same && lane != l) lead = false;
     }
     if (lead) hooks += unite(parent, lo, hi) ? 1 : 0;
+  }
+  if (nhook) {  // (uniform)
+    __shared__ int s_h[kCcThreads / 64];
+    hooks = wave_sum_int(hooks);
+    if (lane == 0) s_h[threadIdx.x >> 6] = hooks;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      int tot = 0;
+#pragma unroll
+      for (int w = 0; w < kCcThreads / 64; ++w) tot += s_h[w];
+      nhook[blockIdx.x] = -tot;
+    }
+  }
+}
+
+// k_cc_merge_sq with U sites per thread whose memory round trips overlap:
+// the occupancy bytes of all U sites' links loaded together (buffer loads,
+// out-of-range offsets where a link does not exist), then their parents,
+// then each link deduplicated over the wave as in k_cc_merge_sq, then the
+// thread's remaining unions in lockstep -- every hop of every chain and
+// every CAS of the round issued before any is waited for (a chain's first
+// node then points at the root it found).  A union that
+// loses its CAS retries from the value it found, as in unite(): the
+// partition, the hooks (one per merged pair of components) and, after the
+// compress, every parent are the one-site-per-thread merge's.  Part A:
+// kCcThreads * U columns of a block-top row per workgroup, part B:
+// kCcThreads * U rows of a block-last column.
+template <int TH, int KIND, int U>
+__global__ __launch_bounds__(kCcThreads) void k_cc_merge_squ(Geom g, const uint8_t* bocc, const uint8_t* socc,
+                                                             int* parent, uint8_t* member, unsigned nb_bytes,
+                                                             int nsegu, int nfull, int* nhook) {
+  const int lane = threadIdx.x & 63;
+  const bool partA = (int)blockIdx.x < nfull * nsegu;
+  const __amdgpu_buffer_rsrc_t rb = rsrc(bocc, nb_bytes), rs = rsrc(socc, (unsigned)g.t + 8u);
+  const __amdgpu_buffer_rsrc_t rp = rsrc(parent, ((unsigned)g.t + 2u) * 4u);
+  constexpr int M = 2 * U;  // (u, link kind k): k = 0 up (part A), 1 right
+  int sq[M], pa[M], pb[M];
+  bool want[M];
+  unsigned ob[M], oq[M], os[U];
+  int s[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    int row, c;
+    if (partA) {
+      row = (blockIdx.x / nsegu) * TH + TH - 1;
+      c = (blockIdx.x % nsegu) * kCcThreads * U + u * kCcThreads + threadIdx.x;
+    } else {
+      const int e = blockIdx.x - nfull * nsegu, nrbu = cdiv(g.n, kCcThreads * U);
+      c = (e / nrbu) * kCcW + kCcW - 1;
+      row = (e % nrbu) * kCcThreads * U + u * kCcThreads + threadIdx.x;
+      if (row % TH == TH - 1) row = g.n;  // (part A's)
+    }
+    const bool site = row < g.n && c < g.m;
+    s[u] = row * g.m + c + 1;
+    os[u] = KIND == PERC_BOND ? 1u : (unsigned)__builtin_amdgcn_raw_buffer_load_b8(rs, site ? s[u] : (int)kOOB, 0, 0);
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int j = 2 * u + k;
+      const bool exists = site && (k == 0 ? partA && row < g.n - 1 : (c % kCcW == kCcW - 1 && c < g.m - 1));
+      sq[j] = k == 0 ? s[u] + g.m : s[u] + 1;
+      want[j] = exists;
+      const int fb = exists ? bf_open_square(g, row, c) : 0;
+      const int id = k == 0 ? fb + (c < g.m - 1 ? 1 : 0) : fb;
+      ob[j] = KIND == PERC_SITE ? 1u : (unsigned)__builtin_amdgcn_raw_buffer_load_b8(rb, exists ? id : (int)kOOB, 0, 0);
+      oq[j] = KIND == PERC_BOND ? 1u : (unsigned)__builtin_amdgcn_raw_buffer_load_b8(rs, exists ? sq[j] : (int)kOOB, 0, 0);
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < M; ++j) {
+    want[j] = want[j] && os[j / 2] && ob[j] && oq[j];
+    if (KIND == PERC_BOND && want[j]) member[sq[j]] = 1;
+    pa[j] = (int)__builtin_amdgcn_raw_buffer_load_b32(rp, want[j] ? s[j / 2] * 4 : (int)kOOB, 0, 0);
+    pb[j] = (int)__builtin_amdgcn_raw_buffer_load_b32(rp, want[j] ? sq[j] * 4 : (int)kOOB, 0, 0);
+  }
+  // one union per distinct pair of parents in the wave, by its first lane
+  int A[M], B[M];
+  bool act[M];
+#pragma unroll
+  for (int j = 0; j < M; ++j) {
+    const int lo = min(pa[j], pb[j]), hi = max(pa[j], pb[j]);
+    bool lead = want[j] && lo != hi;
+    if (j % 2 == 0 && !partA) lead = false;  // (no up links in part B)
+    unsigned long long actm = __ballot(lead);
+    while (actm) {
+      const int l = __builtin_ctzll(actm);
+      const int la = __shfl(lo, l, 64), lh = __shfl(hi, l, 64);
+      const bool same = lead && lo == la && hi == lh;
+      actm &= ~__ballot(same);
+      if (same && lane != l) lead = false;
+    }
+    act[j] = lead;
+    A[j] = lo;
+    B[j] = hi;
+  }
+  int hooks = 0;
+  while (true) {
+    int A0[M], B0[M];
+#pragma unroll
+    for (int j = 0; j < M; ++j) {
+      A0[j] = A[j];
+      B0[j] = B[j];
+    }
+    // roots of every active pair: one hop of every chain per round
+    while (true) {
+      int na[M], nb2[M];
+#pragma unroll
+      for (int j = 0; j < M; ++j) {
+        na[j] = act[j] ? parent[A[j]] : A[j];
+        nb2[j] = act[j] ? parent[B[j]] : B[j];
+      }
+      bool more = false;
+#pragma unroll
+      for (int j = 0; j < M; ++j) {
+        more |= na[j] != A[j] || nb2[j] != B[j];
+        A[j] = na[j];
+        B[j] = nb2[j];
+      }
+      if (!more) break;
+    }
+    // the chains' first nodes straight to the roots found (an ancestor: the
+    // same set, a smaller index) -- the next chase from them is one hop
+#pragma unroll
+    for (int j = 0; j < M; ++j) {
+      if (act[j] && A0[j] != A[j]) parent[A0[j]] = A[j];
+      if (act[j] && B0[j] != B[j]) parent[B0[j]] = B[j];
+    }
+    bool any = false;
+#pragma unroll
+    for (int j = 0; j < M; ++j) {
+      if (!act[j]) continue;
+      if (A[j] == B[j]) {
+        act[j] = false;
+        continue;
+      }
+      int a = max(A[j], B[j]), b = min(A[j], B[j]);
+      const int old = atomicCAS(&parent[a], a, b);
+      if (old == a) {
+        ++hooks;
+        act[j] = false;
+      } else {
+        A[j] = old;  // a lost race: again from what the root became
+        B[j] = b;
+        any = true;
+      }
+    }
+    if (!any) break;
   }
   if (nhook) {  // (uniform)
     __shared__ int s_h[kCcThreads / 64];

@@ -623,7 +623,10 @@ hipError_t dev_label(perc_ctx* h, int* nspan, int* span_list, int* nclusters) {
     const int G = cdiv(g.m, kCcW) * cdiv(g.n, H);
     const unsigned nbb = (unsigned)h->nb + 8u;
     const int nseg = cdiv(g.m, kCcThreads), nfull = g.n / H;
-    const int GM = nfull * nseg + (cdiv(g.m, kCcW) - 1) * cdiv(g.n, kCcThreads);  // (k_cc_merge_sq's grid)
+    // (the merge's grid: kMergeU sites per thread)
+    constexpr int MU = kMergeU > 0 ? kMergeU : 1;
+    const int nsegu = cdiv(g.m, kCcThreads * MU);
+    const int GM = nfull * nsegu + (cdiv(g.m, kCcW) - 1) * cdiv(g.n, kCcThreads * MU);
     // the cluster count from the tiles' member roots and the merge's hooks
     // (every kind: the bond tile reads the links that cross into its edge
     // sites for their member flags), no pass over the parents
@@ -642,6 +645,16 @@ hipError_t dev_label(perc_ctx* h, int* nspan, int* span_list, int* nclusters) {
     // L = 8192 (profiles/r5_11_cc_bench_L8192.txt)
     int* hk = part + G;
     if (GM == 0) {  // one block: nothing crosses a block edge
+    } else if constexpr (kMergeU > 0) {
+      if (kind == PERC_BOND)
+        k_cc_merge_squ<H, PERC_BOND, MU><<<GM, kCcThreads, 0, st>>>(g, d.bocc, d.socc, d.parent, d.member, nbb,
+                                                                    nsegu, nfull, hk);
+      else if (kind == PERC_SITE)
+        k_cc_merge_squ<H, PERC_SITE, MU><<<GM, kCcThreads, 0, st>>>(g, d.bocc, d.socc, d.parent, d.member, nbb,
+                                                                    nsegu, nfull, hk);
+      else
+        k_cc_merge_squ<H, PERC_SITEBOND, MU><<<GM, kCcThreads, 0, st>>>(g, d.bocc, d.socc, d.parent, d.member,
+                                                                        nbb, nsegu, nfull, hk);
     } else if (kind == PERC_BOND)
       k_cc_merge_sq<H, PERC_BOND><<<GM, kCcThreads, 0, st>>>(g, d.bocc, d.socc, d.parent, d.member, nseg, nfull, hk);
     else if (kind == PERC_SITE)
