@@ -503,6 +503,9 @@ __global__ __launch_bounds__(64) void k_cc_tile_w(Geom g, const uint8_t* bocc, c
         act = true;
         more = false;
       }
+#if defined(PERC_TILE_PROBE_NOUNION)  // (cost probes only: wrong partitions)
+      act = false;
+#endif
       while (act) {  // the lane's unions, one after the other, in one loop
         a = uf.find(a);
         b = uf.find(b);
@@ -571,6 +574,9 @@ __global__ __launch_bounds__(64) void k_cc_tile_w(Geom g, const uint8_t* bocc, c
       if (lc >= tw) continue;
       const int s = (r0 + r) * g.m + c0 + lc + 1;
       int x = (int)(nodes[r] >> (16 * h) & 0xffffu), p = uf.get(x);
+#if defined(PERC_TILE_PROBE_NOFINAL)  // (cost probes only: wrong partitions)
+      p = x;
+#endif
       while (p != x) {
         x = p;
         p = uf.get(x);
