@@ -978,6 +978,65 @@ __global__ __launch_bounds__(kCcThreads) void k_cc_compress(int t, int* parent, 
   if (root > 0) block_count_add(cnt, rcount);  // (uniform)
 }
 
+// k_cc_compress of a labeling whose spanning roots the host has not read
+// yet (perc_label's one-synchronisation path): dcnt[0] the spanning count
+// and dcnt[8] the first spanning root as k_span_top left them in device
+// memory.  Nothing spans: every workgroup returns (nothing flattened, nothing
+// counted).  Else every parent to its root and the member sites of that
+// root counted; the last workgroup to finish (ticket and count in the
+// 64-bit word at dcnt[4]) writes the total to hout[2] (the pinned read-back
+// words).
+template <int U = kCcCompressU>
+__global__ __launch_bounds__(kCcThreads) void k_cc_compress_spec(int t, int* parent, const uint8_t* member,
+                                                                 int* dcnt, int* hout) {
+  if (dcnt[0] == 0) return;  // (uniform)
+  const int root = dcnt[8];
+  int cnt = 0;
+  for (long long b = (long long)blockIdx.x * kCcThreads * U + threadIdx.x + 1; b <= t;
+       b += (long long)gridDim.x * kCcThreads * U) {
+    int x[U], y[U];
+#pragma unroll
+    for (int k = 0; k < U; ++k) {
+      const long long s = b + k * kCcThreads;
+      x[k] = s <= t ? parent[s] : 0;
+    }
+    while (true) {
+#pragma unroll
+      for (int k = 0; k < U; ++k) y[k] = b + k * kCcThreads <= t ? parent[x[k]] : 0;
+      bool more = false;
+#pragma unroll
+      for (int k = 0; k < U; ++k) {
+        more |= y[k] != x[k];
+        x[k] = y[k];
+      }
+      if (!more) break;
+    }
+#pragma unroll
+    for (int k = 0; k < U; ++k) {
+      const long long s = b + k * kCcThreads;
+      if (s > t) continue;
+      parent[s] = x[k];
+      cnt += x[k] == root && member[s];
+    }
+  }
+  __shared__ int s_cnt[kCcThreads / 64];
+  cnt = wave_sum_int(cnt);
+  if ((threadIdx.x & 63) == 0) s_cnt[threadIdx.x >> 6] = cnt;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int tot = 0;
+#pragma unroll
+    for (int w = 0; w < kCcThreads / 64; ++w) tot += s_cnt[w];
+    // one 64-bit atomic: the ticket in the high word, the count in the low
+    // one -- the last workgroup's old value holds every other's count (no
+    // fences: an acquire / release pair per workgroup cost 7 us at L = 4096)
+    const unsigned long long old = __hip_atomic_fetch_add(reinterpret_cast<unsigned long long*>(&dcnt[4]),
+                                                          (1ull << 32) | (unsigned)tot, __ATOMIC_RELAXED,
+                                                          __HIP_MEMORY_SCOPE_AGENT);
+    if ((old >> 32) == gridDim.x - 1) hout[2] = (int)(unsigned)old + tot;
+  }
+}
+
 }  // namespace
 }  // namespace perc
 #pragma clang diagnostic pop

@@ -438,8 +438,9 @@ int perc_label(perc_ctx* h, perc_label_info* info, int* canon_out) {
   if (!h->occupied) return PERC_ESTATE;
   hipSetDevice(h->device);
   int nspan = 0, nclus = 0, list[kMaxSpanList];
-  hipError_t e = dev_label(h, &nspan, list, &nclus);
+  hipError_t e = dev_label(h, &nspan, list, &nclus, h->span_guess);
   if (e != hipSuccess) return hip_status(e, "perc_label");
+  h->span_guess = nspan > 0;
   perc_label_info li{};
   li.nclusters = nclus;
   li.nspan = nspan;
@@ -458,7 +459,9 @@ int perc_label(perc_ctx* h, perc_label_info* info, int* canon_out) {
   } else {
     li.perccln = 0;
   }
-  if (li.span_root) {
+  if (li.span_root && nspan == 1 && h->span_count >= 0) {
+    li.span_sites = h->span_count;  // (counted with the labeling: its root is list[0])
+  } else if (li.span_root) {
     e = dev_span_sites(h, li.span_root, &li.span_sites);
     if (e != hipSuccess) return hip_status(e, "perc_label");
   }

@@ -185,6 +185,12 @@ struct perc_ctx {
   bool bf_closed = false;  // h_bond_first == bf_square on rows 0..n-2 (square lattice)
   bool bf_open_sq = false; // and the open lattice's top row follows (bf_open_square)
   bool flat = true;        // parent[] holds final roots (dev_flatten after a labeling)
+  // perc_label's spanning-cluster site count formed on the device in the
+  // labeling's own launch sequence (k_cc_compress_spec) when the previous
+  // labeling spanned: span_count >= 0 -- that count for the first spanning
+  // root, read back with the spanning roots (one host synchronisation)
+  bool span_guess = false;
+  int span_count = -1;
   bool csr_ok = true;    // the CSR values / diagonal of the assembled system are written
   bool ell_ok = false;   // ... and their ELL copy (d.ell_*)
   perc::AsmParams asm_p; // the assembly's parameters (ensure_csr re-runs it)
@@ -250,7 +256,7 @@ hipError_t dev_alloc_matrix(perc_ctx* h, int N, long long nnz);
 void dev_free_all(perc_ctx* h);
 hipError_t dev_occupy(perc_ctx* h, int kind, int nsites, const int* site_order, int nbonds,
                       const int* bond_order, bool device_src);
-hipError_t dev_label(perc_ctx* h, int* nspan, int* span_list, int* nclusters);
+hipError_t dev_label(perc_ctx* h, int* nspan, int* span_list, int* nclusters, bool spec_span = false);
 hipError_t dev_occupy_random(perc_ctx* h, int kind, int nsites, int nbonds, unsigned long long seed);
 hipError_t dev_span_sites(perc_ctx* h, int root, int* count);
 hipError_t dev_flatten(perc_ctx* h);  // parent[s] = final root (k_cc_compress) once per labeling

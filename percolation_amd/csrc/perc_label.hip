@@ -323,7 +323,8 @@ constexpr int kSpanLds = 32768;
 template <bool LF>
 __global__ __launch_bounds__(1024) void k_span_top(Geom g, const int* parent,
                                                    const uint8_t* member, uint8_t* gflag,
-                                                   int* counters, const int* part, int npart) {
+                                                   int* counters, const int* part, int npart,
+                                                   int* dcopy = nullptr) {
   __shared__ uint8_t s_fl[LF ? kSpanLds : 1];
   __shared__ int s_w[16];
   uint8_t* flag = LF ? s_fl : gflag;
@@ -388,8 +389,18 @@ __global__ __launch_bounds__(1024) void k_span_top(Geom g, const int* parent,
     tot += s_w[w];
   }
   for (int k = 0; k < K && off < kMaxSpanList; ++k)
-    if (c0 + k <= m && flag[c0 + k]) counters[8 + off++] = c0 + k;
-  if (threadIdx.x == 0) counters[0] = tot;
+    if (c0 + k <= m && flag[c0 + k]) {
+      if (dcopy && off == 0) dcopy[8] = c0 + k;  // (the first spanning root)
+      counters[8 + off++] = c0 + k;
+    }
+  if (threadIdx.x == 0) {
+    counters[0] = tot;
+    if (dcopy) {  // device copies for k_cc_compress_spec: the count; its ticket and sum zeroed
+      dcopy[0] = tot;
+      dcopy[4] = 0;
+      dcopy[5] = 0;
+    }
+  }
   if (npart > 0) {  // (uniform)
     int v = 0;
 #pragma unroll
@@ -599,9 +610,9 @@ hipError_t dev_occupy_random(perc_ctx* h, int kind, int nsites, int nbonds,
 }
 
 static hipError_t label_finish(perc_ctx* h, int* nspan, int* span_list, int* nclusters,
-                                const int* part = nullptr, int npart = 0);
+                                const int* part = nullptr, int npart = 0, bool spec_span = false);
 
-hipError_t dev_label(perc_ctx* h, int* nspan, int* span_list, int* nclusters) {
+hipError_t dev_label(perc_ctx* h, int* nspan, int* span_list, int* nclusters, bool spec_span) {
   const Geom& g = h->g;
   hipStream_t st = h->stream;
   DeviceBuffers& d = h->d;
@@ -663,7 +674,7 @@ hipError_t dev_label(perc_ctx* h, int* nspan, int* span_list, int* nclusters) {
       k_cc_merge_sq<H, PERC_SITEBOND><<<GM, kCcThreads, 0, st>>>(g, d.bocc, d.socc, d.parent, d.member, nseg, nfull,
                                                                  hk);
     HIP_TRY(dbg_sync(st, "k_cc_merge_sq"));
-    return label_finish(h, nspan, span_list, nclusters, part, G + GM);
+    return label_finish(h, nspan, span_list, nclusters, part, G + GM, spec_span);
   }
   const int tiles = cdiv(g.m, kCcW) * cdiv(g.n, kCcH);
   unsigned long long* ttr = nullptr;  // PERC_TILE_TRACE: per-workgroup phase stamps
@@ -698,7 +709,7 @@ hipError_t dev_label(perc_ctx* h, int* nspan, int* span_list, int* nclusters) {
 
 // every parent to its root, cluster count, spanning roots, read-back
 static hipError_t label_finish(perc_ctx* h, int* nspan, int* span_list, int* nclusters, const int* part,
-                               int npart) {
+                               int npart, bool spec_span) {
   const Geom& g = h->g;
   hipStream_t st = h->stream;
   DeviceBuffers& d = h->d;
@@ -708,6 +719,7 @@ static hipError_t label_finish(perc_ctx* h, int* nspan, int* span_list, int* ncl
   // labels) -- a labeling that spans nothing (config 5 as stated, the
   // threshold scans' probes) does without it
   h->flat = false;
+  h->span_count = -1;
   if (npart == 0) {
     k_cc_count_roots<<<std::min(cdiv(g.t, kCcThreads * 4), kReduceGrid), kCcThreads, 0, st>>>(
         g.t, d.parent, d.member, d.counters + 1);
@@ -734,9 +746,24 @@ static hipError_t label_finish(perc_ctx* h, int* nspan, int* span_list, int* ncl
   int* out = d.counters;
   if (direct) HIP_TRY(hipHostGetDevicePointer(reinterpret_cast<void**>(&out), h->pin, 0));
 #endif
-  if (g.m < kSpanLds) k_span_top<true><<<1, 1024, 0, st>>>(g, d.parent, d.member, d.top, out, part, npart);
-  else k_span_top<false><<<1, 1024, 0, st>>>(g, d.parent, d.member, d.top, out, part, npart);
+  // (perc_label, when the previous labeling spanned: the spanning cluster's
+  // flatten and site count enqueued behind the spanning test, read back in
+  // the same synchronisation -- k_cc_compress_spec does nothing if nothing
+  // spans)
+#if defined(PERC_LABEL_NOSPEC)  // (A/B probe builds only: the count after a second synchronisation)
+  const bool spec = false && spec_span;
+#else
+  const bool spec = direct && spec_span;
+#endif
+  int* dcopy = spec ? d.counters : nullptr;
+  if (g.m < kSpanLds) k_span_top<true><<<1, 1024, 0, st>>>(g, d.parent, d.member, d.top, out, part, npart, dcopy);
+  else k_span_top<false><<<1, 1024, 0, st>>>(g, d.parent, d.member, d.top, out, part, npart, dcopy);
   HIP_TRY(dbg_sync(st, "k_span_top"));
+  if (spec) {
+    k_cc_compress_spec<<<std::min(cdiv(g.t, kCcThreads * kCcCompressU), kReduceGrid), kCcThreads, 0, st>>>(
+        g.t, d.parent, d.member, d.counters, out);
+    HIP_TRY(dbg_sync(st, "k_cc_compress_spec"));
+  }
 #if defined(PERC_LABEL_PAGEABLE)
   HIP_TRY(hipMemcpyAsync(hcs, d.counters, sizeof(hcs), hipMemcpyDeviceToHost, st));
 #else
@@ -745,6 +772,10 @@ static hipError_t label_finish(perc_ctx* h, int* nspan, int* span_list, int* ncl
   HIP_TRY(hipStreamSynchronize(st));
   *nspan = hc[0];
   *nclusters = hc[1];
+  if (spec && hc[0] > 0) {
+    h->flat = true;
+    h->span_count = hc[2];
+  }
   for (int i = 0; i < std::min(hc[0], kMaxSpanList); ++i) span_list[i] = hc[8 + i];
   return hipSuccess;
 }

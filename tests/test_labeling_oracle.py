@@ -332,3 +332,31 @@ def test_bench_realisations_partition_vs_oracle(k):
     assert li["nspan"] > 0
     bo = api.random_order(nb, tb, seed, PL.BOND)
     check(li, *oracle_bond(lat, m, n, pbc, bo, tb))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("lat,m,n,pbc", [(0, 512, 512, 0), (0, 1000, 300, 0), (1, 256, 256, 0)])
+@pytest.mark.parametrize("kind", [PL.BOND, PL.SITE, PL.SITEBOND])
+def test_span_sites_with_and_without_the_speculative_count(lat, m, n, pbc, kind):
+    """perc_label's span_sites (the spanning cluster's member sites): the
+    first labeling of a context counts them after reading the spanning roots
+    back; once a labeling has spanned, the next one flattens and counts on the
+    device behind the spanning test (k_cc_compress_spec, one read-back) --
+    both equal to the member sites whose canonical root is span_root, on
+    realisations that span and ones that do not (a dense, a sparse, a dense
+    draw in turn)."""
+    t, nb = m * n, api.nbonds(lat, m, n, pbc)
+    dense, sparse = 0.9, 0.2
+    with api.Context(lat, m, n, pbc) as ctx:
+        for k, f in enumerate((dense, dense, sparse, dense, dense)):
+            ts = int(f * t) if kind != PL.BOND else 0
+            tb = int(f * nb) if kind != PL.SITE else 0
+            ctx.occupy_random(kind, ts, tb, 4242 + k)
+            li = ctx.label()
+            canon = ctx.label(canon=True)["canon"]  # (the same occupancy, labelled again)
+            if li["nspan"] == 0:
+                assert f == sparse
+                continue
+            assert f == dense and li["nspan"] == 1
+            want = int(np.count_nonzero(canon == li["span_root"]))
+            assert li["span_sites"] == want, (k, li["span_sites"], want)
