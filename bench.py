@@ -789,8 +789,9 @@ def main():
                 ("xp", "xp", 3, xp_bytes(N, f, L_, full))]
 
     # per-kernel live timing: HIP events on the context stream around the
-    # launches of every 8th CG iteration of the timed realisations (those
-    # that did work; perc_set_kernel_timing)
+    # launches of every 64th CG iteration of the timed realisations (those
+    # that did work; perc_set_kernel_timing -- a timed launch's event packets
+    # open a dispatch gap of several us, so every 8th cost the solve ~1 %)
     kern = {}
     for key, skey, _, nbytes in kernel_set(fmt):
         n_ = max(ks[skey + "_n"], 1)
@@ -907,7 +908,7 @@ def main():
                      "frac_of_achievable": round(achieved / stream_copy["gbs"], 4),
                      "traffic": traffic, "traffic_source": traffic_src,
                      "avg_launch_ms_rocprof": rp_ms, "rocprof_source": rp_src,
-                     "timing_note": "avg_launch_ms: every 8th launch timed live by its own "
+                     "timing_note": "avg_launch_ms: every 64th launch timed live by its own "
                                     "dispatch timestamps (hipExtLaunchKernel events on the "
                                     "context stream); a timed launch carries the events' "
                                     "cache write-back, so it reads a few % above the "

@@ -289,10 +289,11 @@ int perc_bench_kernel(perc_ctx *h, int which, int reps, double *ms);
    out3[1..2] = bit patterns of the first mismatching a and d. */
 int perc_selftest_division(long long n, unsigned long long seed, unsigned long long *out3);
 
-/* Live kernel timing: when enabled, the CG launches of every 8th
-   iteration inside perc_conductance are bracketed by HIP events on the
-   context stream (events between every launch would cost ~10 % of an
-   L = 4096 iteration); the accumulated device time of the sampled launches
+/* Live kernel timing: when enabled, the CG launches of every 64th
+   iteration (PERC_TIME_EVERY=n: every n-th) inside perc_conductance are
+   bracketed by HIP events on the context stream (a timed launch opens a
+   dispatch gap of several us: every 8th cost ~1 % of an L = 4096 solve,
+   every launch ~10 %); the accumulated device time of the sampled launches
    that did work is returned (ms) with their count.  stats[0..5] = {spmv_ms, spmv_launches, resid_ms (B),
    resid_launches, xp_ms (P), xp_launches}; reset clears the accumulators. */
 int perc_set_kernel_timing(perc_ctx *h, int enable);

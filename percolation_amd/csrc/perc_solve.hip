@@ -1220,8 +1220,15 @@ hipError_t dev_solve_impl(perc_ctx* h, int itol, double tol, int itmax, bool x0_
     for (size_t i = have; i < T.ev.size(); ++i) HIP_TRY(timing_event_create(&T.ev[i]));
   }
   int done_iters = 0;
-  // kernel timing samples every kTimeEvery-th iteration of a chunk
-  constexpr int kTimeEvery = 8;
+  // kernel timing samples every kTimeEvery-th iteration of a chunk: 64 (a
+  // timed launch's event packets open a dispatch gap of several us: every
+  // 8th iteration timed cost ~1 us per iteration on average,
+  // profiles/r6_43_march_gaps.txt; PERC_TIME_EVERY overrides)
+  static const int kTimeEvery = [] {
+    const char* v = std::getenv("PERC_TIME_EVERY");
+    const int n = v ? std::atoi(v) : 0;
+    return n > 0 ? n : 64;
+  }();
   // phase probe (PERC_MARCH_TRACE=<csv>): per-wave stamps of the P and B
   // launches of iterations PERC_MARCH_TRACE_IT (default 1000) .. +3
   const char* mtpath = getenv("PERC_MARCH_TRACE");

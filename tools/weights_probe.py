@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Slot-weighted band weights of the strip-major march (perc_set_band_weights)
 on the metric realisation: per-kernel launch times inside fixed-iteration
-solves (perc_set_kernel_timing: dispatch timestamps of every 8th launch, P
+solves (perc_set_kernel_timing: dispatch timestamps of every 8th launch -- PERC_TIME_EVERY=8, P
 and B alternating as in the bench) and the solve's ms per iteration, for
 each pair of candidate weight sets (P set i with B set i), the pairs
 interleaved round after round so box drift hits them alike; median and best
@@ -36,6 +36,7 @@ def main():
     ap.add_argument("--p-sets", default="100,75,50:100,76,48:100,77,46:100,78,48:100,74,46:100,76,50")
     ap.add_argument("--b-sets", default="100,80,60:100,84,63:100,82,62:100,86,65:100,83,60:100,85,67")
     args = ap.parse_args()
+    os.environ.setdefault("PERC_TIME_EVERY", "8")  # (more samples per short solve than the bench's 64)
     from percolation_amd import _lib as PL
     from percolation_amd import api
     L_ = args.L
