@@ -29,6 +29,22 @@ __global__ void k_occupy(const int* order, int count, long long limit, uint8_t* 
 // keys -- slow, exact: T is the exact order statistic on every path.
 constexpr int kSelCap = 1 << 17, kSelThreads = 1024, kSelStage = 512, kSelBins = 4096;
 constexpr int kSelBinCap = 1024;
+// workgroups per draw of k_select_final: the window keys of T's bin are
+// picked out by kSelParts workgroups (a share each, appended to a list after
+// the window keys), the last one to finish ranks them (one workgroup walked
+// the ~93 K window keys of a 2^27-bond draw in 12 dependent rounds, 14 of its
+// 19 us, PERC_SELECT_TRACE; PERC_SEL_PARTS, A/B probe builds only)
+#ifdef PERC_SEL_PARTS
+constexpr int kSelParts = PERC_SEL_PARTS;
+#else
+constexpr int kSelParts = 16;
+#endif
+// cand[] layout per draw: [0] T, [1 .. kSelCap] the window keys, then 16
+// words (PERC_SELECT_TRACE stamps [0 .. 5], the bin list's count [8] and the
+// parts' ticket [9]), then the bin's keys (kSelBinCap)
+constexpr int kSelAux = 1 + kSelCap;
+constexpr int kSelList = kSelAux + 16;
+constexpr size_t kSelCand = (size_t)kSelList + kSelBinCap;
 // occupancy bytes per thread and trip of k_select_window (one store of a
 // kSelV-byte word; PERC_SEL_V: A/B probe builds only)
 #ifdef PERC_SEL_V
@@ -89,6 +105,7 @@ __global__ __launch_bounds__(kBlock) void k_select_window(SelDraws D) {
     uint8_t* padp = w.padp;
     if ((int)threadIdx.x < npad) padp[threadIdx.x] = 0;
     if ((int)threadIdx.x < base) occ[threadIdx.x] = 0;
+    if (threadIdx.x < 2) cand[kSelAux + 8 + threadIdx.x] = 0;  // k_select_final's list count and ticket
   }
   __shared__ unsigned long long s_c[kSelStage];
   __shared__ unsigned s_n, s_base, s_b[kBlock / 64];
@@ -144,7 +161,8 @@ __global__ __launch_bounds__(kBlock) void k_select_window(SelDraws D) {
 }
 
 __global__ __launch_bounds__(kSelThreads) void k_select_final(SelDraws D) {
-  const SelDraw w = blockIdx.x ? D.d[1] : D.d[0];
+  const int part = blockIdx.x % kSelParts;
+  const SelDraw w = blockIdx.x >= kSelParts ? D.d[1] : D.d[0];
   const long long n = w.n, count = w.count;
   const unsigned long long seed = w.seed, lo = w.lo, hi = w.hi;
   unsigned* cnt = w.cnt;
@@ -153,14 +171,15 @@ __global__ __launch_bounds__(kSelThreads) void k_select_final(SelDraws D) {
   __shared__ unsigned long long s_k[kSelBinCap];
   __shared__ unsigned long long s_sel[2];  // prefix, need
   __shared__ int s_bin, s_nb;
-  unsigned long long* tr = cand + 1 + kSelCap;  // PERC_SELECT_TRACE stamps
-  if (threadIdx.x == 0) tr[0] = wall_clock64();
+  unsigned long long* tr = cand + kSelAux;  // PERC_SELECT_TRACE stamps
+  const bool p0 = part == 0;
+  if (p0 && threadIdx.x == 0) tr[0] = wall_clock64();
   const long long below = cnt[0], nin = cnt[1];
   const bool win = count > below && count - below <= nin && nin <= kSelCap;
   // T inside the window and every window key gathered: k_select_window's
   // occupation stands and k_occupy_cand completes it; else k_occupy_cand
   // rewrites the whole occupation from T
-  if (threadIdx.x == 0) cnt[2] = win ? 1u : 0u;
+  if (p0 && threadIdx.x == 0) cnt[2] = win ? 1u : 0u;
   if (win) {
     // bins of the window's hash range: (hash - lo) >> sh < kSelBins
     const int sh = sel_shift(lo, hi);
@@ -169,7 +188,7 @@ __global__ __launch_bounds__(kSelThreads) void k_select_final(SelDraws D) {
     for (int j = threadIdx.x; j < kSelBins; j += kSelThreads) s_h[j] = cnt[4 + j];
     if (threadIdx.x == 0) s_nb = 0;
     __syncthreads();
-    if (threadIdx.x == 0) tr[1] = wall_clock64();
+    if (p0 && threadIdx.x == 0) tr[1] = wall_clock64();
     {  // the bin of the (count - below)-th window key: a block scan of the
        // bin counts, kPerT consecutive bins per thread (a serial scan of
        // 4096 LDS words by one thread costs ~70 us)
@@ -208,20 +227,38 @@ __global__ __launch_bounds__(kSelThreads) void k_select_final(SelDraws D) {
     __syncthreads();
     const int bin = s_bin;
     if (s_h[bin] <= (unsigned)kSelBinCap) {
+      // this part's share of the window keys: those of T's bin appended to
+      // the bin list (their count is s_h[bin] over all parts)
+      unsigned long long* list = cand + kSelList;
+      unsigned long long* aux = cand + kSelAux;
+      const long long per = (nin + kSelParts - 1) / kSelParts, i0 = part * per, i1 = min(nin, i0 + per);
       constexpr int kU = 8;
-      for (long long i0 = threadIdx.x; i0 < nin; i0 += kSelThreads * kU) {
+      for (long long ib = i0 + threadIdx.x; ib < i1; ib += kSelThreads * kU) {
         unsigned long long kk[kU];
 #pragma unroll
         for (int u = 0; u < kU; ++u)
-          kk[u] = i0 + u * kSelThreads < nin ? cand[1 + i0 + u * kSelThreads] : ~0ull;
+          kk[u] = ib + u * kSelThreads < i1 ? cand[1 + ib + u * kSelThreads] : ~0ull;
 #pragma unroll
         for (int u = 0; u < kU; ++u)
-          if (i0 + u * kSelThreads < nin && (int)(((kk[u] >> 32) - lo) >> sh) == bin)
-            s_k[atomicAdd(&s_nb, 1)] = kk[u];
+          if (ib + u * kSelThreads < i1 && (int)(((kk[u] >> 32) - lo) >> sh) == bin) {
+            const unsigned long long at =
+                __hip_atomic_fetch_add(&aux[8], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(&list[at], kk[u], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          }
       }
       __syncthreads();
+      if (threadIdx.x == 0) {  // the last part to finish ranks the bin's keys
+        const unsigned long long tk =
+            __hip_atomic_fetch_add(&aux[9], 1ull, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+        s_nb = tk == (unsigned long long)(kSelParts - 1) ? 1 : 0;
+      }
+      __syncthreads();
+      if (!s_nb) return;  // (uniform)
+      const int nb = (int)s_h[bin];
+      for (int j = threadIdx.x; j < nb; j += kSelThreads)
+        s_k[j] = __hip_atomic_load(&list[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __syncthreads();
       if (threadIdx.x == 0) tr[2] = wall_clock64();
-      const int nb = s_nb;
       const unsigned long long want = s_sel[1] - 1;  // 0-based rank in the bin
       for (int j = threadIdx.x; j < nb; j += kSelThreads) {
         const unsigned long long kj = s_k[j];
@@ -239,7 +276,9 @@ __global__ __launch_bounds__(kSelThreads) void k_select_final(SelDraws D) {
     __syncthreads();
   }
   // radix select, 8 passes of one key byte: of the window keys (a crowded
-  // bin) or of all n keys (T outside the window)
+  // bin) or of all n keys (T outside the window) -- by the draw's first
+  // part alone
+  if (!p0) return;  // (uniform)
   const long long nk = win ? nin : n;
   if (threadIdx.x == 0) {
     s_sel[0] = 0;
@@ -563,7 +602,7 @@ hipError_t dev_occupy_random(perc_ctx* h, int kind, int nsites, int nbonds,
   // written whole and their pad bytes by the draw (socc[0] and socc[t+1 ..
   // t+8) with the sites, bocc[nb .. nb+8) with the bonds); an undrawn kind
   // is zeroed whole
-  constexpr size_t kCand = (size_t)kSelCap + 1 + 16;  // per draw: T, the window keys, trace stamps
+  constexpr size_t kCand = kSelCand;  // per draw: T, the window keys, stamps / list count / ticket, the bin list
   if (!d.sel_hist) HIP_TRY(dmalloc(&d.sel_hist, 2 * kSelCnt));
   if (!d.sel_cand) HIP_TRY(dmalloc(&d.sel_cand, 2 * kCand));
   HIP_TRY(hipMemsetAsync(d.sel_hist, 0, sizeof(unsigned) * 2 * kSelCnt, st));
@@ -589,7 +628,7 @@ hipError_t dev_occupy_random(perc_ctx* h, int kind, int nsites, int nbonds,
   }
   k_select_window<<<G, kBlock, 0, st>>>(D);
   HIP_TRY(dbg_sync(st, "k_select_window"));
-  k_select_final<<<D.nd, kSelThreads, 0, st>>>(D);
+  k_select_final<<<D.nd * kSelParts, kSelThreads, 0, st>>>(D);
   HIP_TRY(dbg_sync(st, "k_select_final"));
   if (std::getenv("PERC_SELECT_TRACE")) {
     for (int k = 0; k < D.nd; ++k) {
